@@ -1,0 +1,184 @@
+/* nfgpu.h — C-ABI boundary of the MI355X-native NoahGameFrame per-tick entity
+ * update path (heartbeat scan -> property/record mutation -> dirty diff ->
+ * scene-group fan-out).  Plain pointers and sizes only.
+ *
+ * Every entry point names the reference interface it replaces.  Reference
+ * paths are relative to flyish/NoahGameFrame:
+ *   KM  = NFComm/NFKernelPlugin/NFCKernelModule.cpp
+ *   SM  = NFComm/NFKernelPlugin/NFCScheduleModule.cpp
+ *   AOI = NFComm/NFKernelPlugin/NFCSceneAOIModule.cpp
+ *   PR  = NFComm/NFCore/NFCProperty.cpp
+ *   RC  = NFComm/NFCore/NFCRecord.cpp
+ *
+ * Entities are addressed by NFGUID (head, data) exactly like NFIKernelModule.
+ * Outputs address entities by "object index" = creation order in this world
+ * (nfk_create_objects call order), which the host maps back to NFGUID.
+ */
+#ifndef NFGPU_H
+#define NFGPU_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (every call returns one; nothing fails silently) ---- */
+#define NFK_OK 0
+#define NFK_ERR_ARG (-1)       /* bad argument / schema violation */
+#define NFK_ERR_HIP (-2)       /* HIP runtime error (no GPU, OOM, launch failure) */
+#define NFK_ERR_STATE (-3)     /* call out of order (e.g. execute before commit) */
+#define NFK_ERR_CAPACITY (-4)  /* entity / event / message capacity exceeded */
+#define NFK_ERR_TOUCH (-5)     /* > NFK_MAX_TOUCH distinct properties written per entity per tick */
+#define NFK_ERR_DEVICE (-6)    /* device-side error word set (bounded spin expired) */
+#define NFK_ERR_NOTFOUND (-7)  /* GUID not present */
+
+#define NFK_MAX_INT_PROPS 64
+#define NFK_MAX_FLT_PROPS 64
+#define NFK_MAX_CLASSES 16
+#define NFK_MAX_KINDS 32
+#define NFK_MAX_OPS 4
+#define NFK_MAX_RECORDS 8
+#define NFK_MAX_REC_ROWS 64
+#define NFK_MAX_REC_COLS 16
+#define NFK_MAX_TOUCH 8
+
+/* property / record visibility flags, NFIProperty::GetPublic/GetPrivate/GetUpload */
+#define NFK_PUBLIC 1
+#define NFK_PRIVATE 2
+#define NFK_UPLOAD 4
+
+/* Heartbeat effect ops.  A reference game registers arbitrary C++ functors
+ * with NFIScheduleModule::AddSchedule (SM:236); on the device a heartbeat
+ * kind carries a program of these ops, each one a Get + Set through the
+ * reference's change predicates (PR:254 SetInt, PR:295 SetFloat, RC:182
+ * SetInt, RC:243 SetFloat).
+ *   IADD_CLAMP  dst(int) = clamp(dst + A, LO, HI)        A/LO/HI imm or prop
+ *   FLERP       dst(f64) = dst + (prop[a] - dst) * f64(b) (no FMA contraction)
+ *   FAFFINE     dst(f64) = dst * f64(a) + f64(b)
+ *   RIADD_CLAMP record cell(int) = clamp(cell + a, b, c) for every used row
+ *   RFAFFINE    record cell(f64) = cell * f64(a) + f64(b) for every used row
+ * clamp(v, lo, hi): v < lo -> lo; then v > hi -> hi.  Integer adds wrap.
+ * Record ops: dst = (rec << 8) | col. */
+enum {
+    NFK_OP_NOP = 0,
+    NFK_OP_IADD_CLAMP = 1,
+    NFK_OP_FLERP = 2,
+    NFK_OP_FAFFINE = 3,
+    NFK_OP_RIADD_CLAMP = 4,
+    NFK_OP_RFAFFINE = 5
+};
+#define NFK_A_PROP 1
+#define NFK_LO_PROP 2
+#define NFK_HI_PROP 4
+
+typedef struct nfk_op {
+    uint8_t code;
+    uint8_t flags;
+    uint16_t dst;
+    uint32_t pad;
+    int64_t a, b, c;
+} nfk_op; /* 32 bytes */
+
+typedef struct nfk_config {
+    int32_t capacity;     /* max entities resident on this GPU */
+    int32_t n_int;        /* int64 property columns, prop ids [0, n_int) */
+    int32_t n_flt;        /* f64 property columns, prop ids [n_int, n_int+n_flt) */
+    int32_t n_class;      /* classes (NFIClassModule), flags per class */
+    int32_t n_kind;       /* heartbeat kinds; id order MUST equal lexical name order */
+    int32_t n_rec;        /* records */
+    int64_t msg_capacity; /* fan-out messages per tick (0 = 32 x capacity) */
+    void* stream;         /* hipStream_t to launch on, NULL = library-owned stream */
+} nfk_config;
+
+typedef struct nfk_summary {
+    int64_t n_entities;
+    int64_t n_prop_events;  /* coalesced dirty (entity, property) pairs this tick */
+    int64_t n_rec_events;   /* coalesced dirty (entity, record, row, col) cells */
+    int64_t n_fired;        /* heartbeat callbacks fired (NFCScheduleElement::DoHeartBeatEvent) */
+    int64_t n_msgs;         /* fan-out messages (event x recipient) */
+    int64_t alg_bytes_tick; /* algorithmic HBM bytes of the tick kernel this tick */
+    int64_t alg_bytes_rec;  /* ... of the record kernel */
+    int64_t alg_bytes_fan;  /* ... of the fan-out kernel */
+    int32_t device_error;   /* nonzero: device error word */
+    int32_t tick;           /* ticks executed */
+} nfk_summary;
+
+/* Device-resident outputs of the last tick (valid until the next execute). */
+typedef struct nfk_outputs {
+    /* dirty property events, ordered by (scene, group, guid, prop) */
+    const uint32_t* ev_slot; const uint32_t* ev_pid; const uint64_t* ev_old; const uint64_t* ev_new;
+    /* dirty record cells, ordered by (scene, group, guid, rec, row, col); rrc = rec<<16|row<<8|col */
+    const uint32_t* re_slot; const uint32_t* re_rrc; const uint64_t* re_old; const uint64_t* re_new;
+    /* fired heartbeats, ordered by (scene, group, guid, kind) */
+    const uint32_t* fi_slot; const uint32_t* fi_kind; const int32_t* fi_remain;
+    /* fan-out CSR over [prop events ++ record events]: msg_off[n_ev+n_re+1], recipients = slots */
+    const uint32_t* msg_off; const uint32_t* msg_rcpt;
+    /* slot -> object index */
+    const int32_t* slot_obj;
+} nfk_outputs;
+
+/* ---- lifetime: NFCKernelModule ctor/Init/AfterInit (KM:17,51,1490) ---- */
+int nfk_create(const nfk_config* cfg, void** out_world);
+int nfk_destroy(void* world);
+/* human-readable description of the last error on this thread */
+const char* nfk_last_error(void);
+
+/* ---- schema: NFIClassModule property/record definitions (KM:137-189) ---- */
+int nfk_set_prop_flags(void* world, int32_t cls, const uint8_t* flags /* [n_int+n_flt] */);
+int nfk_define_record(void* world, int32_t rec, int32_t rows, int32_t cols,
+                      const uint8_t* col_types /* [cols] 0=int64 1=f64 */,
+                      const uint8_t* flags_per_class /* [n_class] */);
+/* heartbeat kind program; replaces the functor passed to AddSchedule (SM:236) */
+int nfk_define_kind(void* world, int32_t kind, const nfk_op* ops, int32_t n_ops);
+
+/* ---- objects: NFCKernelModule::CreateObject (KM:101) ---- */
+int nfk_create_objects(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
+                       const int32_t* scene, const int32_t* group, const uint8_t* cls,
+                       const uint8_t* is_player);
+/* creation-time property values (CreateObject's config SetProperty, KM:193-208), creation order */
+int nfk_load_prop(void* world, int32_t pid, const uint64_t* bits /* [n_objects] */);
+/* creation-time record contents, cells [n_objects][cols][rows] as bit patterns, used-row masks */
+int nfk_load_record(void* world, int32_t rec, const uint64_t* cells, const uint64_t* used_mask);
+/* build the device layout: slots sorted by (scene, group, guid) (NFCSceneInfo group maps) */
+int nfk_commit(void* world);
+
+/* ---- property mutation: NFIKernelModule::SetPropertyInt/Float (KM:323,336) ----
+ * Queued in call order, applied at the start of the next nfk_execute with the
+ * reference's change predicates.  bits = int64 or f64 bit pattern. */
+int nfk_set_props(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
+                  const int32_t* pid, const uint64_t* bits);
+
+/* ---- heartbeats: NFIScheduleModule (SM:236,255,260,266) ---- */
+int nfk_add_schedules(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
+                      const int32_t* kind, const float* interval_s, const int32_t* count,
+                      const int64_t* now_ms);
+int nfk_remove_schedule(void* world, int64_t guid_head, int64_t guid_data, int32_t kind);
+int nfk_remove_all_schedules(void* world, int64_t guid_head, int64_t guid_data);
+
+/* ---- one server frame: NFCScheduleModule::Execute (SM:45) + NFCKernelModule::Execute (KM:70)
+ * + NFCSceneAOIModule::OnPropertyCommonEvent/GetBroadCastObject fan-out (AOI:227,260,531).
+ * Asynchronous on the world's stream. */
+int nfk_execute(void* world, int64_t now_ms);
+/* synchronise and read the counters of the last tick */
+int nfk_summary_get(void* world, nfk_summary* out);
+int nfk_outputs_get(void* world, nfk_outputs* out);
+
+/* ---- host copies (synchronising) ---- */
+int nfk_read_prop(void* world, int32_t pid, uint64_t* bits /* [n_objects], creation order */);
+int nfk_read_record(void* world, int32_t rec, uint64_t* cells /* [n_objects][cols][rows] */);
+/* schedule table in creation order: arrays [n_kind][n_objects] */
+int nfk_read_schedules(void* world, int64_t* next_ms, int32_t* remain, uint8_t* state);
+int nfk_read_events(void* world, int32_t* ev_obj, int32_t* ev_pid, uint64_t* ev_old, uint64_t* ev_new);
+int nfk_read_rec_events(void* world, int32_t* re_obj, uint32_t* re_rrc, uint64_t* re_old, uint64_t* re_new);
+int nfk_read_fired(void* world, int32_t* fi_obj, int32_t* fi_kind, int32_t* fi_remain);
+int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj);
+
+/* ---- measurement ---- */
+int nfk_set_profiling(void* world, int32_t on);
+/* accumulated device time (ms) and launch count per kernel: 0 tick, 1 record, 2 fanout, 3 aux */
+int nfk_kernel_times(void* world, double* ms /* [4] */, int64_t* launches /* [4] */, int64_t* bytes /* [4] */);
+int nfk_reset_kernel_times(void* world);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

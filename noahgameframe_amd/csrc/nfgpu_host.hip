@@ -1,0 +1,995 @@
+// nfgpu_host.hip — C-ABI implementation (include/nfgpu.h): world lifetime, schema,
+// membership layout, queued SetProperty / schedule calls, frame launch, readback.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "nfgpu_kernels.hip"
+
+using namespace nfgpu;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                          \
+    do {                                                                                   \
+        hipError_t _e = (x);                                                               \
+        if (_e != hipSuccess)                                                              \
+            return fail(NFK_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(_e));     \
+    } while (0)
+
+struct GuidKey {
+    int64_t h, d;
+    bool operator==(const GuidKey& o) const { return h == o.h && d == o.d; }
+};
+struct GuidHash {
+    size_t operator()(const GuidKey& k) const {
+        uint64_t x = (uint64_t)k.h * 0x9E3779B97F4A7C15ull ^ (uint64_t)k.d;
+        x ^= x >> 31;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 29;
+        return (size_t)x;
+    }
+};
+
+template <typename T>
+int dalloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+    if (e != hipSuccess) return fail(NFK_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return NFK_OK;
+}
+
+enum { KT_TICK = 0, KT_REC = 1, KT_FAN = 2, KT_AUX = 3 };
+
+struct PendingTiming {
+    int kind;
+    hipEvent_t a, b;
+    int64_t bytes_before;
+};
+
+struct World {
+    nfk_config cfg{};
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int32_t n_obj = 0;
+    bool committed = false;
+    int n_prop = 0;
+
+    std::vector<int64_t> gh, gd;
+    std::vector<int32_t> scene, group;
+    std::vector<uint8_t> cls, isplayer;
+    std::unordered_map<GuidKey, int32_t, GuidHash> obj_of;
+    std::vector<int32_t> slot_of_obj, obj_of_slot;
+    std::vector<std::vector<uint64_t>> init_props;
+    std::vector<std::vector<uint64_t>> init_rcells, init_rused;
+    std::vector<bool> rec_defined;
+
+    Tables tab{};
+    bool kind_defined[NFK_MAX_KINDS] = {};
+    uint64_t dst_union_mask[2] = {0, 0};  // properties written by any program (bit per pid)
+    int n_dst_union = 0;
+
+    Dev d{};
+    Tables* tab_d = nullptr;
+    Ctrl* ctrl = nullptr;
+    int32_t* slot_obj_d = nullptr;
+    int32_t nseg = 0;
+    size_t g_ev_n = 0, g_fi_n = 0, g_re_n = 0, g_msg_n = 0;
+    std::vector<void*> allocs;
+
+    // queued calls
+    struct XOp { uint32_t slot, pid; uint64_t bits; };
+    std::vector<XOp> xops;
+    struct HOp { int32_t code; uint32_t slot, kind; float interval; int32_t count; int64_t time; };
+    std::vector<HOp> hops;
+
+    // pinned upload arena + device staging
+    void* pin = nullptr;
+    size_t pin_cap = 0;
+    hipEvent_t pin_done = nullptr;
+    bool pin_pending = false;
+    void* stage = nullptr;
+    size_t stage_cap = 0;
+
+    uint32_t epoch = 0;
+    int32_t ticks = 0;
+
+    bool profiling = false;
+    std::vector<PendingTiming> pend;
+    std::vector<hipEvent_t> evpool;
+    double kt_ms[4] = {0, 0, 0, 0};
+    int64_t kt_n[4] = {0, 0, 0, 0};
+    int64_t kt_bytes[4] = {0, 0, 0, 0};
+    uint64_t last_bytes[3] = {0, 0, 0};
+};
+
+int alloc_track(World* w, void** p, size_t bytes) {
+    *p = nullptr;
+    hipError_t e = hipMalloc(p, bytes ? bytes : 16);
+    if (e != hipSuccess) return fail(NFK_ERR_HIP, std::string("hipMalloc ") + std::to_string(bytes) + ": " + hipGetErrorString(e));
+    w->allocs.push_back(*p);
+    return NFK_OK;
+}
+#define ALLOC(ptr, bytes)                                                    \
+    do {                                                                     \
+        void* _p;                                                            \
+        int _r = alloc_track(w, &_p, (size_t)(bytes));                       \
+        if (_r) return _r;                                                   \
+        ptr = reinterpret_cast<decltype(ptr)>(_p);                           \
+    } while (0)
+
+hipEvent_t get_event(World* w) {
+    if (!w->evpool.empty()) {
+        hipEvent_t e = w->evpool.back();
+        w->evpool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int drain_timings(World* w) {
+    for (auto& p : w->pend) {
+        HIPCHK(hipEventSynchronize(p.b));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+        w->kt_ms[p.kind] += ms;
+        w->kt_n[p.kind] += 1;
+        w->evpool.push_back(p.a);
+        w->evpool.push_back(p.b);
+    }
+    w->pend.clear();
+    return NFK_OK;
+}
+
+struct TimeScope {
+    World* w;
+    int kind;
+    hipEvent_t a = nullptr, b = nullptr;
+    TimeScope(World* ww, int k) : w(ww), kind(k) {
+        if (w->profiling) {
+            a = get_event(w);
+            b = get_event(w);
+            if (a) (void)hipEventRecord(a, w->stream);
+        }
+    }
+    ~TimeScope() {
+        if (w->profiling && a && b) {
+            (void)hipEventRecord(b, w->stream);
+            w->pend.push_back({kind, a, b, 0});
+        }
+    }
+};
+
+// reserve a pinned host arena (waits for the previous upload to finish reading it)
+int pin_reserve(World* w, size_t bytes) {
+    if (w->pin_pending) {
+        HIPCHK(hipEventSynchronize(w->pin_done));
+        w->pin_pending = false;
+    }
+    if (bytes > w->pin_cap) {
+        if (w->pin) HIPCHK(hipHostFree(w->pin));
+        size_t cap = std::max(bytes, w->pin_cap * 2);
+        HIPCHK(hipHostMalloc(&w->pin, cap, hipHostMallocDefault));
+        w->pin_cap = cap;
+    }
+    if (bytes > w->stage_cap) {
+        // kernels of earlier frames may still read the old staging buffer
+        HIPCHK(hipStreamSynchronize(w->stream));
+        if (w->stage) HIPCHK(hipFree(w->stage));
+        size_t cap = std::max(bytes, w->stage_cap * 2);
+        HIPCHK(hipMalloc(&w->stage, cap));
+        w->stage_cap = cap;
+    }
+    return NFK_OK;
+}
+
+size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+int lookup(World* w, int64_t h, int64_t d, int32_t* obj) {
+    auto it = w->obj_of.find(GuidKey{h, d});
+    if (it == w->obj_of.end())
+        return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(h) + "-" + std::to_string(d));
+    *obj = it->second;
+    return NFK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nfk_last_error(void) { return g_err.c_str(); }
+
+int nfk_create(const nfk_config* cfg, void** out) {
+    if (!cfg || !out) return fail(NFK_ERR_ARG, "null argument");
+    if (cfg->capacity <= 0 || cfg->n_int < 0 || cfg->n_int > NFK_MAX_INT_PROPS || cfg->n_flt < 0 ||
+        cfg->n_flt > NFK_MAX_FLT_PROPS || cfg->n_class <= 0 || cfg->n_class > NFK_MAX_CLASSES ||
+        cfg->n_kind < 0 || cfg->n_kind > NFK_MAX_KINDS || cfg->n_rec < 0 || cfg->n_rec > NFK_MAX_RECORDS)
+        return fail(NFK_ERR_ARG, "config out of range");
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) return fail(NFK_ERR_HIP, "no HIP device available");
+    World* w = new World();
+    w->cfg = *cfg;
+    w->n_prop = cfg->n_int + cfg->n_flt;
+    if (cfg->stream) {
+        w->stream = (hipStream_t)cfg->stream;
+    } else {
+        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete w;
+            return fail(NFK_ERR_HIP, "hipStreamCreate failed");
+        }
+        w->own_stream = true;
+    }
+    if (hipEventCreateWithFlags(&w->pin_done, hipEventDisableTiming) != hipSuccess) {
+        delete w;
+        return fail(NFK_ERR_HIP, "hipEventCreate failed");
+    }
+    w->init_props.resize(w->n_prop);
+    w->init_rcells.resize(cfg->n_rec);
+    w->init_rused.resize(cfg->n_rec);
+    w->rec_defined.assign(cfg->n_rec, false);
+    *out = w;
+    return NFK_OK;
+}
+
+int nfk_destroy(void* world) {
+    World* w = (World*)world;
+    if (!w) return NFK_OK;
+    (void)hipStreamSynchronize(w->stream);
+    for (void* p : w->allocs) (void)hipFree(p);
+    if (w->pin) (void)hipHostFree(w->pin);
+    if (w->stage) (void)hipFree(w->stage);
+    for (auto& p : w->pend) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto e : w->evpool) (void)hipEventDestroy(e);
+    if (w->pin_done) (void)hipEventDestroy(w->pin_done);
+    if (w->own_stream) (void)hipStreamDestroy(w->stream);
+    delete w;
+    return NFK_OK;
+}
+
+int nfk_set_prop_flags(void* world, int32_t c, const uint8_t* flags) {
+    World* w = (World*)world;
+    if (!w || !flags || c < 0 || c >= w->cfg.n_class) return fail(NFK_ERR_ARG, "bad class");
+    for (int p = 0; p < w->n_prop; p++) w->tab.pflags[c][p] = flags[p];
+    return NFK_OK;
+}
+
+int nfk_define_record(void* world, int32_t rec, int32_t rows, int32_t cols, const uint8_t* col_types,
+                      const uint8_t* flags_per_class) {
+    World* w = (World*)world;
+    if (!w || rec < 0 || rec >= w->cfg.n_rec || rows <= 0 || rows > NFK_MAX_REC_ROWS || cols <= 0 ||
+        cols > NFK_MAX_REC_COLS || !flags_per_class)
+        return fail(NFK_ERR_ARG, "bad record definition");
+    if (w->committed) return fail(NFK_ERR_STATE, "schema is fixed after commit");
+    w->tab.rec_rows[rec] = rows;
+    w->tab.rec_cols[rec] = cols;
+    for (int c = 0; c < w->cfg.n_class; c++) w->tab.rflags[c][rec] = flags_per_class[c];
+    w->rec_defined[rec] = true;
+    (void)col_types;  // cell type is carried by the op (RIADD_CLAMP = int64, RFAFFINE = f64)
+    return NFK_OK;
+}
+
+int nfk_define_kind(void* world, int32_t kind, const nfk_op* ops, int32_t n_ops) {
+    World* w = (World*)world;
+    if (!w || kind < 0 || kind >= w->cfg.n_kind || n_ops < 0 || n_ops > NFK_MAX_OPS || (n_ops && !ops))
+        return fail(NFK_ERR_ARG, "bad kind definition");
+    if (w->committed) return fail(NFK_ERR_STATE, "schema is fixed after commit");
+    for (int i = 0; i < n_ops; i++) {
+        const nfk_op& op = ops[i];
+        const int np = w->n_prop, ni = w->cfg.n_int;
+        auto isint = [&](int64_t p) { return p >= 0 && p < ni; };
+        auto isflt = [&](int64_t p) { return p >= ni && p < np; };
+        switch (op.code) {
+        case NFK_OP_IADD_CLAMP:
+            if (!isint(op.dst) || ((op.flags & NFK_A_PROP) && !isint(op.a)) ||
+                ((op.flags & NFK_LO_PROP) && !isint(op.b)) || ((op.flags & NFK_HI_PROP) && !isint(op.c)))
+                return fail(NFK_ERR_ARG, "IADD_CLAMP operands must be int properties");
+            break;
+        case NFK_OP_FLERP:
+            if (!isflt(op.dst) || !isflt(op.a)) return fail(NFK_ERR_ARG, "FLERP operands must be float properties");
+            break;
+        case NFK_OP_FAFFINE:
+            if (!isflt(op.dst)) return fail(NFK_ERR_ARG, "FAFFINE dst must be a float property");
+            break;
+        case NFK_OP_RIADD_CLAMP:
+        case NFK_OP_RFAFFINE: {
+            int r = op.dst >> 8, col = op.dst & 255;
+            if (r >= w->cfg.n_rec || !w->rec_defined[r] || col >= w->tab.rec_cols[r])
+                return fail(NFK_ERR_ARG, "record op on undefined record/col");
+            break;
+        }
+        case NFK_OP_NOP:
+            break;
+        default:
+            return fail(NFK_ERR_ARG, "unknown op code");
+        }
+        w->tab.ops[kind][i] = op;
+    }
+    w->tab.nops[kind] = n_ops;
+    w->kind_defined[kind] = true;
+    return NFK_OK;
+}
+
+int nfk_create_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* scene,
+                       const int32_t* group, const uint8_t* cls, const uint8_t* isplayer) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !scene || !group || !cls || !isplayer)))
+        return fail(NFK_ERR_ARG, "null argument");
+    if (w->committed) return fail(NFK_ERR_STATE, "objects after commit are not supported yet");
+    if ((int64_t)w->n_obj + n > w->cfg.capacity) return fail(NFK_ERR_CAPACITY, "entity capacity exceeded");
+    for (int32_t i = 0; i < n; i++) {
+        if (cls[i] >= w->cfg.n_class) return fail(NFK_ERR_ARG, "class id out of range");
+        if (group[i] < 0) return fail(NFK_ERR_ARG, "negative group");
+        GuidKey k{gh[i], gd[i]};
+        if (w->obj_of.count(k)) return fail(NFK_ERR_ARG, "The object has Exists");  // KM:131
+    }
+    for (int32_t i = 0; i < n; i++) {
+        w->obj_of[GuidKey{gh[i], gd[i]}] = w->n_obj + i;
+        w->gh.push_back(gh[i]);
+        w->gd.push_back(gd[i]);
+        w->scene.push_back(scene[i]);
+        w->group.push_back(group[i]);
+        w->cls.push_back(cls[i]);
+        w->isplayer.push_back(isplayer[i] ? 1 : 0);
+    }
+    w->n_obj += n;
+    return NFK_OK;
+}
+
+int nfk_load_prop(void* world, int32_t pid, const uint64_t* bits) {
+    World* w = (World*)world;
+    if (!w || pid < 0 || pid >= w->n_prop || !bits) return fail(NFK_ERR_ARG, "bad property");
+    if (w->committed) return fail(NFK_ERR_STATE, "load before commit");
+    w->init_props[pid].assign(bits, bits + w->n_obj);
+    return NFK_OK;
+}
+
+int nfk_load_record(void* world, int32_t rec, const uint64_t* cells, const uint64_t* used) {
+    World* w = (World*)world;
+    if (!w || rec < 0 || rec >= w->cfg.n_rec || !w->rec_defined[rec] || !cells || !used)
+        return fail(NFK_ERR_ARG, "bad record");
+    if (w->committed) return fail(NFK_ERR_STATE, "load before commit");
+    size_t per = (size_t)w->tab.rec_rows[rec] * w->tab.rec_cols[rec];
+    w->init_rcells[rec].assign(cells, cells + per * w->n_obj);
+    w->init_rused[rec].assign(used, used + w->n_obj);
+    return NFK_OK;
+}
+
+int nfk_commit(void* world) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    if (w->committed) return fail(NFK_ERR_STATE, "already committed");
+    const int32_t N = w->n_obj, cap = w->cfg.capacity;
+    const int NI = w->cfg.n_int, NF = w->cfg.n_flt, NK = w->cfg.n_kind, NR = w->cfg.n_rec;
+    for (int r = 0; r < NR; r++)
+        if (!w->rec_defined[r]) return fail(NFK_ERR_ARG, "record " + std::to_string(r) + " not defined");
+
+    // record ops: compiled list sorted by (rec, col); distinct (rec, col) required
+    int nro = 0;
+    for (int k = 0; k < NK; k++)
+        for (int i = 0; i < w->tab.nops[k]; i++) {
+            const nfk_op& op = w->tab.ops[k][i];
+            if (op.code == NFK_OP_RIADD_CLAMP || op.code == NFK_OP_RFAFFINE) {
+                if (nro == NFK_MAX_OPS) return fail(NFK_ERR_ARG, "at most 4 record ops across all kinds");
+                RecOp ro{k, op.dst >> 8, op.dst & 255, op.code, op.a, op.b, op.c};
+                w->tab.recops[nro++] = ro;
+                w->tab.kind_has_recop |= 1u << k;
+            } else if (op.code == NFK_OP_IADD_CLAMP || op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE) {
+                w->dst_union_mask[op.dst >> 6] |= 1ull << (op.dst & 63);
+            }
+        }
+    std::sort(w->tab.recops, w->tab.recops + nro, [](const RecOp& a, const RecOp& b) {
+        return a.rec != b.rec ? a.rec < b.rec : a.col < b.col;
+    });
+    for (int i = 1; i < nro; i++)
+        if (w->tab.recops[i].rec == w->tab.recops[i - 1].rec && w->tab.recops[i].col == w->tab.recops[i - 1].col)
+            return fail(NFK_ERR_ARG, "two record ops on the same (record, col)");
+    w->tab.n_recops = nro;
+    w->n_dst_union = __builtin_popcountll(w->dst_union_mask[0]) + __builtin_popcountll(w->dst_union_mask[1]);
+    if (w->n_dst_union > NFK_MAX_TOUCH)
+        return fail(NFK_ERR_TOUCH, "programs write more than NFK_MAX_TOUCH distinct properties");
+
+    // membership layout: slots sorted by (scene, group, guid) — NFCSceneInfo/NFCSceneGroupInfo
+    // keep std::map<NFGUID> group lists, so GUID order is the fan-out order (AOI:572)
+    w->obj_of_slot.resize(N);
+    for (int32_t i = 0; i < N; i++) w->obj_of_slot[i] = i;
+    std::sort(w->obj_of_slot.begin(), w->obj_of_slot.end(), [w](int32_t a, int32_t b) {
+        if (w->scene[a] != w->scene[b]) return w->scene[a] < w->scene[b];
+        if (w->group[a] != w->group[b]) return w->group[a] < w->group[b];
+        if (w->gh[a] != w->gh[b]) return w->gh[a] < w->gh[b];
+        return w->gd[a] < w->gd[b];
+    });
+    w->slot_of_obj.resize(N);
+    for (int32_t s = 0; s < N; s++) w->slot_of_obj[w->obj_of_slot[s]] = s;
+    std::vector<int32_t> seg_of(N), seg_pl_off, pl_slot;
+    std::vector<uint8_t> cls_s(N), ip_s(N);
+    int32_t nseg = 0;
+    for (int32_t s = 0; s < N; s++) {
+        int32_t o = w->obj_of_slot[s];
+        if (s == 0 || w->scene[o] != w->scene[w->obj_of_slot[s - 1]] || w->group[o] != w->group[w->obj_of_slot[s - 1]]) {
+            seg_pl_off.push_back((int32_t)pl_slot.size());
+            nseg++;
+        }
+        seg_of[s] = nseg - 1;
+        cls_s[s] = w->cls[o];
+        ip_s[s] = w->isplayer[o];
+        if (w->isplayer[o]) pl_slot.push_back(s);
+    }
+    seg_pl_off.push_back((int32_t)pl_slot.size());
+    w->nseg = nseg;
+
+    // device allocation
+    Dev& d = w->d;
+    d.N = N;
+    d.cap = cap;
+    d.n_int = NI;
+    d.n_flt = NF;
+    d.n_kind = NK;
+    d.n_rec = NR;
+    d.has_recops = nro > 0;
+    ALLOC(w->tab_d, sizeof(Tables));
+    ALLOC(w->ctrl, sizeof(Ctrl));
+    ALLOC(d.icol, (size_t)std::max(NI, 1) * cap * 8);
+    ALLOC(d.fcol, (size_t)std::max(NF, 1) * cap * 8);
+    ALLOC(d.s_next, (size_t)std::max(NK, 1) * cap * 8);
+    ALLOC(d.s_start, (size_t)std::max(NK, 1) * cap * 8);
+    ALLOC(d.s_remain, (size_t)std::max(NK, 1) * cap * 4);
+    ALLOC(d.s_all, (size_t)std::max(NK, 1) * cap * 4);
+    ALLOC(d.s_interval, (size_t)std::max(NK, 1) * cap * 4);
+    ALLOC(d.s_state, (size_t)std::max(NK, 1) * cap);
+    ALLOC(d.e_flags, cap);
+    ALLOC(d.ext_head, (size_t)cap * 4);
+    ALLOC(d.fired_mask, (size_t)cap * 4);
+    size_t rec_events_per_ent = 0;
+    for (int i = 0; i < nro; i++) rec_events_per_ent += w->tab.rec_rows[w->tab.recops[i].rec];
+    for (int r = 0; r < NR; r++) {
+        ALLOC(d.rcells[r], (size_t)cap * w->tab.rec_rows[r] * w->tab.rec_cols[r] * 8);
+        ALLOC(d.rused[r], (size_t)cap * 8);
+    }
+    int32_t *seg_of_d, *seg_pl_off_d, *pl_slot_d;
+    uint8_t *cls_d, *ip_d;
+    ALLOC(seg_of_d, (size_t)cap * 4);
+    ALLOC(cls_d, cap);
+    ALLOC(ip_d, cap);
+    ALLOC(seg_pl_off_d, seg_pl_off.size() * 4);
+    ALLOC(pl_slot_d, std::max<size_t>(pl_slot.size(), 1) * 4);
+    ALLOC(w->slot_obj_d, (size_t)cap * 4);
+    d.seg_of = seg_of_d;
+    d.cls = cls_d;
+    d.isplayer = ip_d;
+    d.seg_pl_off = seg_pl_off_d;
+    d.pl_slot = pl_slot_d;
+    d.ev_cap = (int64_t)cap * std::min(NFK_MAX_TOUCH, std::max(w->n_prop, 1));
+    d.fi_cap = (int64_t)cap * std::max(NK, 1);
+    d.re_cap = (int64_t)cap * (int64_t)std::max<size_t>(rec_events_per_ent, 1);
+    d.msg_cap = w->cfg.msg_capacity > 0 ? w->cfg.msg_capacity : (int64_t)cap * 32;
+    if (d.msg_cap > 0xFFFFFFFFll) return fail(NFK_ERR_ARG, "msg_capacity must fit 32-bit offsets");
+    ALLOC(d.ev_slot, d.ev_cap * 4);
+    ALLOC(d.ev_pid, d.ev_cap * 4);
+    ALLOC(d.ev_old, d.ev_cap * 8);
+    ALLOC(d.ev_new, d.ev_cap * 8);
+    ALLOC(d.fi_slot, d.fi_cap * 4);
+    ALLOC(d.fi_kind, d.fi_cap * 4);
+    ALLOC(d.fi_remain, d.fi_cap * 4);
+    ALLOC(d.re_slot, d.re_cap * 4);
+    ALLOC(d.re_rrc, d.re_cap * 4);
+    ALLOC(d.re_old, d.re_cap * 8);
+    ALLOC(d.re_new, d.re_cap * 8);
+    ALLOC(d.msg_off, (d.ev_cap + d.re_cap + 1) * 4);
+    ALLOC(d.msg_rcpt, d.msg_cap * 4);
+    w->g_ev_n = (cap + kTPB - 1) / kTPB;
+    w->g_fi_n = w->g_ev_n;
+    w->g_re_n = (cap + 3) / 4;
+    w->g_msg_n = (d.ev_cap + d.re_cap + kTPB - 1) / kTPB;
+    ALLOC(d.g_ev, w->g_ev_n * 8);
+    ALLOC(d.g_fi, w->g_fi_n * 8);
+    ALLOC(d.g_re, w->g_re_n * 8);
+    ALLOC(d.g_msg, w->g_msg_n * 8);
+    d.tab = w->tab_d;
+    d.ctrl = w->ctrl;
+
+    // uploads (synchronous: commit is control plane)
+    HIPCHK(hipMemcpy(w->tab_d, &w->tab, sizeof(Tables), hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(w->ctrl, 0, sizeof(Ctrl)));
+    std::vector<uint64_t> col(cap, 0);
+    for (int p = 0; p < w->n_prop; p++) {
+        std::fill(col.begin(), col.end(), 0);
+        if (!w->init_props[p].empty())
+            for (int32_t s = 0; s < N; s++) col[s] = w->init_props[p][w->obj_of_slot[s]];
+        void* dst = p < NI ? (void*)(d.icol + (size_t)p * cap) : (void*)(d.fcol + (size_t)(p - NI) * cap);
+        HIPCHK(hipMemcpy(dst, col.data(), (size_t)cap * 8, hipMemcpyHostToDevice));
+    }
+    for (int r = 0; r < NR; r++) {
+        size_t per = (size_t)w->tab.rec_rows[r] * w->tab.rec_cols[r];
+        std::vector<uint64_t> cells(per * cap, 0), used(cap, 0);
+        if (!w->init_rcells[r].empty())
+            for (int32_t s = 0; s < N; s++) {
+                int32_t o = w->obj_of_slot[s];
+                memcpy(&cells[(size_t)s * per], &w->init_rcells[r][(size_t)o * per], per * 8);
+                used[s] = w->init_rused[r][o];
+            }
+        HIPCHK(hipMemcpy(d.rcells[r], cells.data(), cells.size() * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d.rused[r], used.data(), used.size() * 8, hipMemcpyHostToDevice));
+    }
+    HIPCHK(hipMemset(d.s_state, 0, (size_t)std::max(NK, 1) * cap));
+    HIPCHK(hipMemset(d.e_flags, 0, cap));
+    HIPCHK(hipMemset(d.ext_head, 0, (size_t)cap * 4));
+    HIPCHK(hipMemset(d.fired_mask, 0, (size_t)cap * 4));
+    HIPCHK(hipMemset(d.g_ev, 0, w->g_ev_n * 8));
+    HIPCHK(hipMemset(d.g_fi, 0, w->g_fi_n * 8));
+    HIPCHK(hipMemset(d.g_re, 0, w->g_re_n * 8));
+    HIPCHK(hipMemset(d.g_msg, 0, w->g_msg_n * 8));
+    HIPCHK(hipMemcpy(seg_of_d, seg_of.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(cls_d, cls_s.data(), N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ip_d, ip_s.data(), N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(seg_pl_off_d, seg_pl_off.data(), seg_pl_off.size() * 4, hipMemcpyHostToDevice));
+    if (!pl_slot.empty()) HIPCHK(hipMemcpy(pl_slot_d, pl_slot.data(), pl_slot.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(w->slot_obj_d, w->obj_of_slot.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+    // creation-time values are now on the device
+    for (auto& v : w->init_props) std::vector<uint64_t>().swap(v);
+    for (auto& v : w->init_rcells) std::vector<uint64_t>().swap(v);
+    w->committed = true;
+    return NFK_OK;
+}
+
+int nfk_set_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid,
+                  const uint64_t* bits) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !pid || !bits))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    for (int32_t i = 0; i < n; i++) {
+        int32_t obj;
+        int r = lookup(w, gh[i], gd[i], &obj);
+        if (r) return r;  // NFCKernelModule logs "There is no object" and returns false (KM:331)
+        if (pid[i] < 0 || pid[i] >= w->n_prop) return fail(NFK_ERR_ARG, "bad property id");
+    }
+    for (int32_t i = 0; i < n; i++)
+        w->xops.push_back({(uint32_t)w->slot_of_obj[w->obj_of[GuidKey{gh[i], gd[i]}]], (uint32_t)pid[i], bits[i]});
+    return NFK_OK;
+}
+
+int nfk_add_schedules(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* kind,
+                      const float* interval, const int32_t* count, const int64_t* now_ms) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !kind || !interval || !count || !now_ms)))
+        return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    for (int32_t i = 0; i < n; i++) {
+        int32_t obj;
+        int r = lookup(w, gh[i], gd[i], &obj);
+        if (r) return r;
+        if (kind[i] < 0 || kind[i] >= w->cfg.n_kind || !w->kind_defined[kind[i]])
+            return fail(NFK_ERR_ARG, "undefined heartbeat kind");
+    }
+    for (int32_t i = 0; i < n; i++) {
+        int32_t obj = w->obj_of[GuidKey{gh[i], gd[i]}];
+        w->hops.push_back({1, (uint32_t)w->slot_of_obj[obj], (uint32_t)kind[i], interval[i], count[i], now_ms[i]});
+    }
+    return NFK_OK;
+}
+
+int nfk_remove_schedule(void* world, int64_t gh, int64_t gd, int32_t kind) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    int32_t obj;
+    int r = lookup(w, gh, gd, &obj);
+    if (r) return r;
+    if (kind < 0 || kind >= w->cfg.n_kind) return fail(NFK_ERR_ARG, "bad kind");
+    w->hops.push_back({2, (uint32_t)w->slot_of_obj[obj], (uint32_t)kind, 0.f, 0, 0});
+    return NFK_OK;
+}
+
+int nfk_remove_all_schedules(void* world, int64_t gh, int64_t gd) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    int32_t obj;
+    int r = lookup(w, gh, gd, &obj);
+    if (r) return r;
+    w->hops.push_back({3, (uint32_t)w->slot_of_obj[obj], 0u, 0.f, 0, 0});
+    return NFK_OK;
+}
+
+int nfk_execute(void* world, int64_t now_ms) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    Dev d = w->d;
+    d.now = now_ms;
+
+    // ---- host-side preparation of queued calls ----
+    // SetProperty*: stable by slot keeps call order per entity
+    std::stable_sort(w->xops.begin(), w->xops.end(), [](const World::XOp& a, const World::XOp& b) { return a.slot < b.slot; });
+    // touch-capacity check: written props per entity (programs' union + queued sets)
+    for (size_t i = 0; i < w->xops.size();) {
+        size_t j = i;
+        uint64_t m0 = w->dst_union_mask[0], m1 = w->dst_union_mask[1];
+        while (j < w->xops.size() && w->xops[j].slot == w->xops[i].slot) {
+            uint32_t p = w->xops[j].pid;
+            if (p < 64) m0 |= 1ull << p;
+            else m1 |= 1ull << (p - 64);
+            j++;
+        }
+        if (__builtin_popcountll(m0) + __builtin_popcountll(m1) > NFK_MAX_TOUCH) {
+            w->xops.clear();
+            w->hops.clear();
+            return fail(NFK_ERR_TOUCH, "more than NFK_MAX_TOUCH properties written for one entity in one frame");
+        }
+        i = j;
+    }
+    // schedule calls: pre-scan (remove-list key owner, RemoveSchedule(self)) and post-scan (remove, add)
+    std::vector<uint32_t> pre_slot, pre_op;
+    struct Post { uint32_t slot, kind, op; float interval; int32_t count; int64_t time; };
+    std::vector<Post> post;
+    {
+        std::unordered_map<uint64_t, size_t> post_at;   // (slot, kind) -> index in post
+        std::unordered_map<uint32_t, bool> rm_owner;     // slot owns the remove-list key
+        for (const auto& h : w->hops) {
+            if (h.code == 3) {
+                pre_slot.push_back(h.slot);
+                pre_op.push_back(2);
+                continue;
+            }
+            uint64_t key = ((uint64_t)h.slot << 8) | h.kind;
+            if (h.code == 2) {
+                if (rm_owner.count(h.slot)) continue;  // std::map insert: first (self, name) wins
+                rm_owner[h.slot] = true;
+                pre_slot.push_back(h.slot);
+                pre_op.push_back(1);
+                auto it = post_at.find(key);
+                if (it == post_at.end()) {
+                    post_at[key] = post.size();
+                    post.push_back({h.slot, h.kind, 1u | 4u, 0.f, 0, 0});
+                } else {
+                    post[it->second].op |= 1u | 4u;
+                }
+            } else if (h.code == 1) {
+                auto it = post_at.find(key);
+                if (it == post_at.end()) {
+                    post_at[key] = post.size();
+                    post.push_back({h.slot, h.kind, 2u, h.interval, h.count, h.time});
+                } else if (!(post[it->second].op & 2u)) {
+                    Post& p = post[it->second];
+                    p.op |= 2u;
+                    p.interval = h.interval;
+                    p.count = h.count;
+                    p.time = h.time;
+                }
+            }
+        }
+    }
+
+    // ---- uploads through the pinned arena ----
+    const size_t nx = w->xops.size(), npre = pre_slot.size(), npost = post.size();
+    size_t off_xs = 0, off_xp = align16(off_xs + nx * 4), off_xb = align16(off_xp + nx * 4);
+    size_t off_ps = align16(off_xb + nx * 8), off_po = align16(off_ps + npre * 4);
+    size_t off_qs = align16(off_po + npre * 4), off_qk = align16(off_qs + npost * 4);
+    size_t off_qo = align16(off_qk + npost * 4), off_qi = align16(off_qo + npost * 4);
+    size_t off_qc = align16(off_qi + npost * 4), off_qt = align16(off_qc + npost * 4);
+    size_t total = align16(off_qt + npost * 8);
+    if (total > 0 && (nx || npre || npost)) {
+        int r = pin_reserve(w, total);
+        if (r) return r;
+        char* P = (char*)w->pin;
+        for (size_t i = 0; i < nx; i++) {
+            ((uint32_t*)(P + off_xs))[i] = w->xops[i].slot;
+            ((uint32_t*)(P + off_xp))[i] = w->xops[i].pid;
+            ((uint64_t*)(P + off_xb))[i] = w->xops[i].bits;
+        }
+        for (size_t i = 0; i < npre; i++) {
+            ((uint32_t*)(P + off_ps))[i] = pre_slot[i];
+            ((uint32_t*)(P + off_po))[i] = pre_op[i];
+        }
+        for (size_t i = 0; i < npost; i++) {
+            ((uint32_t*)(P + off_qs))[i] = post[i].slot;
+            ((uint32_t*)(P + off_qk))[i] = post[i].kind;
+            ((uint32_t*)(P + off_qo))[i] = post[i].op;
+            ((float*)(P + off_qi))[i] = post[i].interval;
+            ((int32_t*)(P + off_qc))[i] = post[i].count;
+            ((int64_t*)(P + off_qt))[i] = post[i].time;
+        }
+        HIPCHK(hipMemcpyAsync(w->stage, w->pin, total, hipMemcpyHostToDevice, w->stream));
+        HIPCHK(hipEventRecord(w->pin_done, w->stream));
+        w->pin_pending = true;
+    }
+    char* S = (char*)w->stage;
+    d.n_x = (int32_t)nx;
+    d.x_slot = nx ? (const uint32_t*)(S + off_xs) : nullptr;
+    d.x_pid = nx ? (const uint32_t*)(S + off_xp) : nullptr;
+    d.x_bits = nx ? (const uint64_t*)(S + off_xb) : nullptr;
+    w->xops.clear();
+    w->hops.clear();
+
+    // ---- per-frame control: tickets/totals zeroed, fresh look-back tag ----
+    w->epoch++;
+    if (w->epoch > 0xFFFF) {
+        HIPCHK(hipMemsetAsync(d.g_ev, 0, w->g_ev_n * 8, w->stream));
+        HIPCHK(hipMemsetAsync(d.g_fi, 0, w->g_fi_n * 8, w->stream));
+        HIPCHK(hipMemsetAsync(d.g_re, 0, w->g_re_n * 8, w->stream));
+        HIPCHK(hipMemsetAsync(d.g_msg, 0, w->g_msg_n * 8, w->stream));
+        w->epoch = 1;
+    }
+    d.tag = w->epoch;
+    HIPCHK(hipMemsetAsync(w->ctrl, 0, 64, w->stream));
+
+    if (nx || npre) {
+        TimeScope ts(w, KT_AUX);
+        if (nx)
+            hipLaunchKernelGGL(k_ext_scatter, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, w->stream,
+                               d.x_slot, (int32_t)nx, d.ext_head);
+        if (npre)
+            hipLaunchKernelGGL(k_pre_hostops, dim3((unsigned)((npre + 255) / 256)), dim3(256), 0, w->stream,
+                               (const uint32_t*)(S + off_ps), (const uint32_t*)(S + off_po), (int32_t)npre,
+                               d.e_flags, d.s_state, d.n_kind, d.cap);
+        HIPCHK(hipGetLastError());
+    }
+    const unsigned nb_tick = (unsigned)((d.N + kTPB - 1) / kTPB);
+    if (nb_tick) {
+        TimeScope ts(w, KT_TICK);
+        hipLaunchKernelGGL(k_tick, dim3(nb_tick), dim3(kTPB), 0, w->stream, d);
+        HIPCHK(hipGetLastError());
+    }
+    if (d.has_recops && d.N) {
+        TimeScope ts(w, KT_REC);
+        hipLaunchKernelGGL(k_records, dim3((unsigned)((d.N + 3) / 4)), dim3(kTPB), 0, w->stream, d);
+        HIPCHK(hipGetLastError());
+    }
+    if (npost) {
+        TimeScope ts(w, KT_AUX);
+        hipLaunchKernelGGL(k_post_hostops, dim3((unsigned)((npost + 255) / 256)), dim3(256), 0, w->stream,
+                           (const uint32_t*)(S + off_qs), (const uint32_t*)(S + off_qk),
+                           (const uint32_t*)(S + off_qo), (const float*)(S + off_qi),
+                           (const int32_t*)(S + off_qc), (const int64_t*)(S + off_qt), (int32_t)npost, d);
+        HIPCHK(hipGetLastError());
+    }
+    {
+        TimeScope ts(w, KT_FAN);
+        const unsigned long long max_tiles = (d.ev_cap + d.re_cap + kTPB - 1) / kTPB;
+        const unsigned nb = (unsigned)std::min<unsigned long long>(std::max<unsigned long long>(max_tiles, 1), 1024);
+        hipLaunchKernelGGL(k_fanout, dim3(nb), dim3(kTPB), 0, w->stream, d);
+        HIPCHK(hipGetLastError());
+    }
+    w->ticks++;
+    return NFK_OK;
+}
+
+int nfk_summary_get(void* world, nfk_summary* out) {
+    World* w = (World*)world;
+    if (!w || !out) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    HIPCHK(hipStreamSynchronize(w->stream));
+    Ctrl c;
+    HIPCHK(hipMemcpy(&c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+    memset(out, 0, sizeof *out);
+    out->n_entities = w->d.N;
+    out->n_prop_events = (int64_t)c.n_ev;
+    out->n_rec_events = (int64_t)c.n_re;
+    out->n_fired = (int64_t)c.n_fi;
+    out->n_msgs = (int64_t)c.n_msgs;
+    out->alg_bytes_tick = (int64_t)(c.bytes_tick - w->last_bytes[0]);
+    out->alg_bytes_rec = (int64_t)(c.bytes_rec - w->last_bytes[1]);
+    out->alg_bytes_fan = (int64_t)(c.bytes_fan - w->last_bytes[2]);
+    w->last_bytes[0] = c.bytes_tick;
+    w->last_bytes[1] = c.bytes_rec;
+    w->last_bytes[2] = c.bytes_fan;
+    out->device_error = (int32_t)c.err;
+    out->tick = w->ticks;
+    if (c.err & kErrSpin) return fail(NFK_ERR_DEVICE, "device look-back spin limit exceeded");
+    if (c.err & kErrTouch) return fail(NFK_ERR_TOUCH, "device touch list overflow");
+    if (c.err & (kErrEvCap | kErrMsgCap | kErrFiCap | kErrReCap))
+        return fail(NFK_ERR_CAPACITY, "device output capacity exceeded (err=" + std::to_string(c.err) + ")");
+    return NFK_OK;
+}
+
+int nfk_outputs_get(void* world, nfk_outputs* o) {
+    World* w = (World*)world;
+    if (!w || !o) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    const Dev& d = w->d;
+    o->ev_slot = d.ev_slot; o->ev_pid = d.ev_pid; o->ev_old = d.ev_old; o->ev_new = d.ev_new;
+    o->re_slot = d.re_slot; o->re_rrc = d.re_rrc; o->re_old = d.re_old; o->re_new = d.re_new;
+    o->fi_slot = d.fi_slot; o->fi_kind = d.fi_kind; o->fi_remain = d.fi_remain;
+    o->msg_off = d.msg_off; o->msg_rcpt = d.msg_rcpt;
+    o->slot_obj = w->slot_obj_d;
+    return NFK_OK;
+}
+
+static int read_ctrl(World* w, Ctrl* c) {
+    HIPCHK(hipStreamSynchronize(w->stream));
+    HIPCHK(hipMemcpy(c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+    return NFK_OK;
+}
+
+int nfk_read_prop(void* world, int32_t pid, uint64_t* bits) {
+    World* w = (World*)world;
+    if (!w || !bits || pid < 0 || pid >= w->n_prop) return fail(NFK_ERR_ARG, "bad argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    HIPCHK(hipStreamSynchronize(w->stream));
+    const Dev& d = w->d;
+    std::vector<uint64_t> col(d.N);
+    const void* src = pid < d.n_int ? (const void*)(d.icol + (size_t)pid * d.cap)
+                                    : (const void*)(d.fcol + (size_t)(pid - d.n_int) * d.cap);
+    HIPCHK(hipMemcpy(col.data(), src, (size_t)d.N * 8, hipMemcpyDeviceToHost));
+    for (int32_t s = 0; s < d.N; s++) bits[w->obj_of_slot[s]] = col[s];
+    return NFK_OK;
+}
+
+int nfk_read_record(void* world, int32_t rec, uint64_t* cells) {
+    World* w = (World*)world;
+    if (!w || !cells || rec < 0 || rec >= w->cfg.n_rec) return fail(NFK_ERR_ARG, "bad argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    HIPCHK(hipStreamSynchronize(w->stream));
+    const Dev& d = w->d;
+    size_t per = (size_t)w->tab.rec_rows[rec] * w->tab.rec_cols[rec];
+    std::vector<uint64_t> buf(per * d.N);
+    HIPCHK(hipMemcpy(buf.data(), d.rcells[rec], buf.size() * 8, hipMemcpyDeviceToHost));
+    for (int32_t s = 0; s < d.N; s++) memcpy(cells + (size_t)w->obj_of_slot[s] * per, &buf[(size_t)s * per], per * 8);
+    return NFK_OK;
+}
+
+int nfk_read_schedules(void* world, int64_t* next_ms, int32_t* remain, uint8_t* state) {
+    World* w = (World*)world;
+    if (!w || !next_ms || !remain || !state) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    HIPCHK(hipStreamSynchronize(w->stream));
+    const Dev& d = w->d;
+    const int NK = d.n_kind;
+    std::vector<int64_t> nx((size_t)NK * d.cap);
+    std::vector<int32_t> rm((size_t)NK * d.cap);
+    std::vector<uint8_t> st((size_t)NK * d.cap);
+    if (NK) {
+        HIPCHK(hipMemcpy(nx.data(), d.s_next, nx.size() * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(rm.data(), d.s_remain, rm.size() * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(st.data(), d.s_state, st.size(), hipMemcpyDeviceToHost));
+    }
+    for (int k = 0; k < NK; k++)
+        for (int32_t s = 0; s < d.N; s++) {
+            size_t o = (size_t)k * w->n_obj + w->obj_of_slot[s], a = (size_t)k * d.cap + s;
+            state[o] = st[a];
+            next_ms[o] = (st[a] & 1) ? nx[a] : 0;
+            remain[o] = (st[a] & 1) ? rm[a] : 0;
+        }
+    return NFK_OK;
+}
+
+int nfk_read_events(void* world, int32_t* ev_obj, int32_t* ev_pid, uint64_t* ev_old, uint64_t* ev_new) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    Ctrl c;
+    int r = read_ctrl(w, &c);
+    if (r) return r;
+    const Dev& d = w->d;
+    size_t n = std::min<unsigned long long>(c.n_ev, d.ev_cap);
+    std::vector<uint32_t> sl(n);
+    if (n) {
+        HIPCHK(hipMemcpy(sl.data(), d.ev_slot, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(ev_pid, d.ev_pid, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(ev_old, d.ev_old, n * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(ev_new, d.ev_new, n * 8, hipMemcpyDeviceToHost));
+    }
+    for (size_t i = 0; i < n; i++) ev_obj[i] = w->obj_of_slot[sl[i]];
+    return NFK_OK;
+}
+
+int nfk_read_rec_events(void* world, int32_t* re_obj, uint32_t* re_rrc, uint64_t* re_old, uint64_t* re_new) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    Ctrl c;
+    int r = read_ctrl(w, &c);
+    if (r) return r;
+    const Dev& d = w->d;
+    size_t n = std::min<unsigned long long>(c.n_re, d.re_cap);
+    std::vector<uint32_t> sl(n);
+    if (n) {
+        HIPCHK(hipMemcpy(sl.data(), d.re_slot, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(re_rrc, d.re_rrc, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(re_old, d.re_old, n * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(re_new, d.re_new, n * 8, hipMemcpyDeviceToHost));
+    }
+    for (size_t i = 0; i < n; i++) re_obj[i] = w->obj_of_slot[sl[i]];
+    return NFK_OK;
+}
+
+int nfk_read_fired(void* world, int32_t* fi_obj, int32_t* fi_kind, int32_t* fi_remain) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    Ctrl c;
+    int r = read_ctrl(w, &c);
+    if (r) return r;
+    const Dev& d = w->d;
+    size_t n = std::min<unsigned long long>(c.n_fi, d.fi_cap);
+    std::vector<uint32_t> sl(n);
+    if (n) {
+        HIPCHK(hipMemcpy(sl.data(), d.fi_slot, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(fi_kind, d.fi_kind, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(fi_remain, d.fi_remain, n * 4, hipMemcpyDeviceToHost));
+    }
+    for (size_t i = 0; i < n; i++) fi_obj[i] = w->obj_of_slot[sl[i]];
+    return NFK_OK;
+}
+
+int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    Ctrl c;
+    int r = read_ctrl(w, &c);
+    if (r) return r;
+    const Dev& d = w->d;
+    size_t ne = std::min<unsigned long long>(c.n_ev, d.ev_cap) + std::min<unsigned long long>(c.n_re, d.re_cap);
+    size_t nm = std::min<unsigned long long>(c.n_msgs, d.msg_cap);
+    HIPCHK(hipMemcpy(msg_off, d.msg_off, (ne + 1) * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> rc(nm);
+    if (nm) HIPCHK(hipMemcpy(rc.data(), d.msg_rcpt, nm * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nm; i++) msg_rcpt_obj[i] = w->obj_of_slot[rc[i]];
+    return NFK_OK;
+}
+
+int nfk_set_profiling(void* world, int32_t on) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    w->profiling = on != 0;
+    return NFK_OK;
+}
+
+int nfk_kernel_times(void* world, double* ms, int64_t* launches, int64_t* bytes) {
+    World* w = (World*)world;
+    if (!w || !ms || !launches || !bytes) return fail(NFK_ERR_ARG, "null argument");
+    int r = drain_timings(w);
+    if (r) return r;
+    if (w->committed) {
+        Ctrl c;
+        r = read_ctrl(w, &c);
+        if (r) return r;
+        w->kt_bytes[0] = (int64_t)c.bytes_tick;
+        w->kt_bytes[1] = (int64_t)c.bytes_rec;
+        w->kt_bytes[2] = (int64_t)c.bytes_fan;
+    }
+    for (int i = 0; i < 4; i++) {
+        ms[i] = w->kt_ms[i];
+        launches[i] = w->kt_n[i];
+        bytes[i] = w->kt_bytes[i];
+    }
+    return NFK_OK;
+}
+
+int nfk_reset_kernel_times(void* world) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    int r = drain_timings(w);
+    if (r) return r;
+    for (int i = 0; i < 4; i++) {
+        w->kt_ms[i] = 0;
+        w->kt_n[i] = 0;
+    }
+    if (w->committed) {
+        Ctrl c;
+        r = read_ctrl(w, &c);
+        if (r) return r;
+        w->last_bytes[0] = c.bytes_tick;
+        w->last_bytes[1] = c.bytes_rec;
+        w->last_bytes[2] = c.bytes_fan;
+        // byte tallies restart from the current counters
+        HIPCHK(hipMemset((char*)w->ctrl + offsetof(Ctrl, bytes_tick), 0, 32));
+        w->last_bytes[0] = w->last_bytes[1] = w->last_bytes[2] = 0;
+    }
+    return NFK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,551 @@
+// nfgpu_kernels.hip — hand-written gfx950 kernels for one NoahGameFrame server frame.
+//
+//   k_ext_scatter   index queued SetProperty* calls by slot
+//   k_pre_hostops   RemoveSchedule(self[,name]) effects that precede the scan
+//   k_tick          heartbeat scan (NFCScheduleModule::Execute, SM:45-80) + effect programs
+//                   + property change predicates (NFCProperty::SetInt/SetFloat, PR:254/295)
+//                   + dirty diff + ordered compaction of dirty events and fired heartbeats
+//                   (wave ballot/scan + decoupled look-back)
+//   k_records       record-cell effects (NFCRecord::SetInt/SetFloat, RC:182/243) + diff,
+//                   one wave per entity, lane = row
+//   k_post_hostops  remove list then add list (SM:82-117)
+//   k_fanout        GetBroadCastObject recipient lists (AOI:531-593) for every dirty event,
+//                   CSR over the (scene, group, guid)-sorted slots
+//
+// Compiled with -ffp-contract=off: f64 effects round exactly like the reference's C++.
+#include "nfgpu_device.hpp"
+
+namespace nfgpu {
+
+// ---------------------------------------------------------------------------------
+__global__ void k_ext_scatter(const uint32_t* __restrict__ x_slot, int32_t n, uint32_t* __restrict__ ext_head) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (i == 0 || x_slot[i] != x_slot[i - 1]) ext_head[x_slot[i]] = (uint32_t)i + 1;
+}
+
+// op: 1 = RemoveSchedule(self, name) queued (owns the remove-list key), 2 = RemoveSchedule(self)
+__global__ void k_pre_hostops(const uint32_t* __restrict__ slot, const uint32_t* __restrict__ op, int32_t n,
+                              uint8_t* __restrict__ e_flags, uint8_t* __restrict__ s_state, int32_t n_kind,
+                              int32_t cap) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot[i];
+    if (op[i] == 1) e_flags[s] |= 1;
+    if (op[i] == 2)
+        for (int k = 0; k < n_kind; k++) s_state[(size_t)k * cap + s] = 0;
+}
+
+// post-scan host ops, one entry per (slot, kind): bit0 remove, bit1 add (remove first)
+__global__ void k_post_hostops(const uint32_t* __restrict__ slot, const uint32_t* __restrict__ kind,
+                               const uint32_t* __restrict__ op, const float* __restrict__ interval,
+                               const int32_t* __restrict__ count, const int64_t* __restrict__ time, int32_t n,
+                               Dev d) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot[i];
+    const size_t at = (size_t)kind[i] * d.cap + s;
+    if (op[i] & 1) d.s_state[at] = 0;
+    if (op[i] & 4) d.e_flags[s] = 0;
+    if ((op[i] & 2) && !(d.s_state[at] & 1)) {
+        const float f = interval[i];
+        const int32_t c = count[i];
+        d.s_state[at] = 1 | (c < 0 ? 2 : 0);
+        d.s_interval[at] = f;
+        d.s_next[at] = time[i] + (int64_t)(f * 1000.0f);
+        d.s_start[at] = time[i];
+        d.s_remain[at] = c;
+        d.s_all[at] = c;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Per-entity written-property list, kept in registers (all indices compile-time).
+struct Touch {
+    uint32_t pid[NFK_MAX_TOUCH];
+    uint64_t old[NFK_MAX_TOUCH];
+    uint64_t cur[NFK_MAX_TOUCH];
+    int n;
+};
+
+__device__ __forceinline__ bool tget(const Touch& t, uint32_t pid, uint64_t& v) {
+    bool f = false;
+#pragma unroll
+    for (int j = 0; j < NFK_MAX_TOUCH; j++) {
+        const bool m = (j < t.n) && (t.pid[j] == pid);
+        v = m ? t.cur[j] : v;
+        f |= m;
+    }
+    return f;
+}
+
+__device__ __forceinline__ void tput(Touch& t, uint32_t pid, uint64_t oldv, uint64_t newv, bool& ovf) {
+    bool f = false;
+#pragma unroll
+    for (int j = 0; j < NFK_MAX_TOUCH; j++) {
+        const bool m = (j < t.n) && (t.pid[j] == pid);
+        if (m) t.cur[j] = newv;
+        f |= m;
+    }
+    if (f) return;
+    if (t.n >= NFK_MAX_TOUCH) {
+        ovf = true;
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < NFK_MAX_TOUCH; j++)
+        if (j == t.n) {
+            t.pid[j] = pid;
+            t.old[j] = oldv;
+            t.cur[j] = newv;
+        }
+    t.n++;
+}
+
+struct Ent {
+    const Dev& d;
+    int e;
+    Touch t;
+    bool ovf;
+    unsigned bytes;
+    __device__ __forceinline__ Ent(const Dev& dd, int ee) : d(dd), e(ee), ovf(false), bytes(0) { t.n = 0; }
+
+    __device__ __forceinline__ uint64_t getb(uint32_t pid) {
+        uint64_t v = 0;
+        if (tget(t, pid, v)) return v;
+        bytes += 8;
+        if ((int)pid < d.n_int) return (uint64_t)d.icol[(size_t)pid * d.cap + e];
+        return (uint64_t)__double_as_longlong(d.fcol[(size_t)(pid - d.n_int) * d.cap + e]);
+    }
+    __device__ __forceinline__ int64_t geti(uint32_t pid) { return (int64_t)getb(pid); }
+    __device__ __forceinline__ double getf(uint32_t pid) { return __longlong_as_double((long long)getb(pid)); }
+
+    // NFCProperty::SetInt (PR:254): stored (and an event fired) only when the value changes
+    __device__ __forceinline__ void seti(uint32_t pid, int64_t v) {
+        const int64_t cur = geti(pid);
+        if (v == cur) return;
+        tput(t, pid, (uint64_t)cur, (uint64_t)v, ovf);
+    }
+    // NFCProperty::SetFloat (PR:295): IsZeroDouble(v - cur), eps 1e-15 (NFPlatform.h:362)
+    __device__ __forceinline__ void setf(uint32_t pid, double v) {
+        const double cur = getf(pid);
+        if (fabs(v - cur) <= 1e-15) return;
+        tput(t, pid, (uint64_t)__double_as_longlong(cur), (uint64_t)__double_as_longlong(v), ovf);
+    }
+};
+
+__device__ __forceinline__ int64_t opnd(Ent& en, const nfk_op& op, int bit, int64_t x) {
+    return (op.flags & bit) ? en.geti((uint32_t)x) : x;
+}
+
+__device__ __forceinline__ void run_program(Ent& en, const Tables* tab, int k) {
+    const int n = tab->nops[k];
+    for (int i = 0; i < n; i++) {
+        const nfk_op op = tab->ops[k][i];
+        if (op.code == NFK_OP_IADD_CLAMP) {
+            const int64_t cur = en.geti(op.dst);
+            const int64_t a = opnd(en, op, NFK_A_PROP, op.a);
+            const int64_t lo = opnd(en, op, NFK_LO_PROP, op.b);
+            const int64_t hi = opnd(en, op, NFK_HI_PROP, op.c);
+            int64_t v = (int64_t)((uint64_t)cur + (uint64_t)a);
+            v = v < lo ? lo : v;
+            v = v > hi ? hi : v;
+            en.seti(op.dst, v);
+        } else if (op.code == NFK_OP_FLERP) {
+            const double x = en.getf(op.dst);
+            const double tg = en.getf((uint32_t)op.a);
+            const double dd = tg - x;
+            const double m = dd * __longlong_as_double(op.b);
+            en.setf(op.dst, x + m);
+        } else if (op.code == NFK_OP_FAFFINE) {
+            const double x = en.getf(op.dst);
+            const double m = x * __longlong_as_double(op.a);
+            en.setf(op.dst, m + __longlong_as_double(op.b));
+        }
+        // record ops run in k_records
+    }
+}
+
+// Block-wide exclusive scan of a packed pair of 32-bit counts (sums stay < 2^32 per block).
+__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v, unsigned long long* s_w,
+                                                              unsigned long long& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long inc = wave_incl_scan(v);
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    unsigned long long before = 0;
+    total = 0;
+#pragma unroll
+    for (int i = 0; i < kTPB / 64; i++) {
+        const unsigned long long x = s_w[i];
+        before += (i < w) ? x : 0ull;
+        total += x;
+    }
+    return before + inc - v;
+}
+
+__global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
+    __shared__ unsigned s_vb;
+    __shared__ unsigned long long s_w[kTPB / 64];
+    __shared__ unsigned long long s_base[2];
+    __shared__ unsigned s_bytes;
+    if (threadIdx.x == 0) {
+        s_vb = atomicAdd(&d.ctrl->ticket_tick, 1u);
+        s_bytes = 0;
+    }
+    __syncthreads();
+    const unsigned vb = s_vb;
+    const int e = (int)(vb * kTPB + threadIdx.x);
+    const bool live = e < d.N;
+    Ent en(d, live ? e : 0);
+    uint32_t fired = 0;
+    uint32_t xh = 0;
+    if (live) {
+        // 1. SetProperty* calls queued before this frame, in call order
+        xh = d.ext_head[e];
+        en.bytes += 4;
+        if (xh) {
+            for (int i = (int)xh - 1; i < d.n_x && d.x_slot[i] == (uint32_t)e; i++) {
+                const uint32_t pid = d.x_pid[i];
+                const uint64_t b = d.x_bits[i];
+                en.bytes += 16;
+                if ((int)pid < d.n_int) en.seti(pid, (int64_t)b);
+                else en.setf(pid, __longlong_as_double((long long)b));
+            }
+        }
+        // 2. NFCScheduleModule::Execute (SM:45-80) over this object's schedules in name order
+        bool taken = d.e_flags[e] & 1;  // std::map remove-list key already owned
+        en.bytes += 1;
+        for (int k = 0; k < d.n_kind; k++) {
+            const size_t at = (size_t)k * d.cap + e;
+            uint8_t st = d.s_state[at];
+            en.bytes += 1;
+            if (!(st & 1)) continue;
+            const int64_t nx = d.s_next[at];
+            en.bytes += 8;
+            if (!(d.now > nx)) continue;
+            int32_t rem = d.s_remain[at];
+            en.bytes += 4;
+            const bool forever = st & 2;
+            if (!(rem > 0 || forever)) continue;
+            rem -= 1;
+            fired |= 1u << k;
+            run_program(en, d.tab, k);
+            d.s_remain[at] = rem;
+            en.bytes += 4;
+            if (rem <= 0 && !forever) {
+                if (!taken) {
+                    d.s_state[at] = 0;
+                    en.bytes += 1;
+                    taken = true;
+                }
+            } else {
+                const int64_t step = (int64_t)(d.s_interval[at] * 1000.0f);
+                const int32_t done = (int32_t)((uint32_t)d.s_all[at] - (uint32_t)rem);
+                d.s_next[at] = d.s_start[at] + step * (int64_t)done;
+                en.bytes += 4 + 4 + 8 + 8;
+            }
+        }
+    }
+    // 3. dirty diff: written properties whose bits changed since the frame began
+    uint32_t dmask = 0;
+#pragma unroll
+    for (int j = 0; j < NFK_MAX_TOUCH; j++)
+        if (j < en.t.n && en.t.cur[j] != en.t.old[j]) dmask |= 1u << j;
+    const unsigned nd = __builtin_popcount(dmask);
+    const unsigned nf = __builtin_popcount(fired);
+    if (en.ovf) atomicOr(&d.ctrl->err, kErrTouch);
+
+    // 4. ordered compaction: block scan + look-back (events chain on wave 0, fired chain on wave 1)
+    unsigned long long tot;
+    const unsigned long long excl = block_excl_scan(((unsigned long long)nf << 32) | nd, s_w, tot);
+    const int w = threadIdx.x >> 6;
+    if (w == 0) {
+        const unsigned long long b = lookback(d.g_ev, vb, d.tag, tot & 0xFFFFFFFFull, d.ctrl);
+        if ((threadIdx.x & 63) == 0) s_base[0] = b;
+    } else if (w == 1) {
+        const unsigned long long b = lookback(d.g_fi, vb, d.tag, tot >> 32, d.ctrl);
+        if ((threadIdx.x & 63) == 0) s_base[1] = b;
+    }
+    __syncthreads();
+    unsigned long long pev = s_base[0] + (excl & 0xFFFFFFFFull);
+    unsigned long long pfi = s_base[1] + (excl >> 32);
+
+    if (live) {
+        // write back changed columns
+#pragma unroll
+        for (int j = 0; j < NFK_MAX_TOUCH; j++) {
+            if (!((dmask >> j) & 1)) continue;
+            const uint32_t pid = en.t.pid[j];
+            if ((int)pid < d.n_int) d.icol[(size_t)pid * d.cap + e] = (int64_t)en.t.cur[j];
+            else d.fcol[(size_t)(pid - d.n_int) * d.cap + e] = __longlong_as_double((long long)en.t.cur[j]);
+            en.bytes += 8;
+        }
+        // events in property-id order
+        uint32_t left = dmask;
+        for (unsigned q = 0; q < nd; q++) {
+            uint32_t best = 0xFFFFFFFFu;
+            int bj = 0;
+#pragma unroll
+            for (int j = 0; j < NFK_MAX_TOUCH; j++)
+                if (((left >> j) & 1) && en.t.pid[j] < best) {
+                    best = en.t.pid[j];
+                    bj = j;
+                }
+            uint64_t ov = 0, nv = 0;
+#pragma unroll
+            for (int j = 0; j < NFK_MAX_TOUCH; j++)
+                if (j == bj) {
+                    ov = en.t.old[j];
+                    nv = en.t.cur[j];
+                }
+            left &= ~(1u << bj);
+            if ((long long)pev < d.ev_cap) {
+                d.ev_slot[pev] = (uint32_t)e;
+                d.ev_pid[pev] = best;
+                d.ev_old[pev] = ov;
+                d.ev_new[pev] = nv;
+            } else {
+                atomicOr(&d.ctrl->err, kErrEvCap);
+            }
+            pev++;
+            en.bytes += 24;
+        }
+        uint32_t fl = fired;
+        while (fl) {
+            const int k = __builtin_ctz(fl);
+            fl &= fl - 1;
+            if ((long long)pfi < d.fi_cap) {
+                d.fi_slot[pfi] = (uint32_t)e;
+                d.fi_kind[pfi] = (uint32_t)k;
+                d.fi_remain[pfi] = d.s_remain[(size_t)k * d.cap + e];
+            } else {
+                atomicOr(&d.ctrl->err, kErrFiCap);
+            }
+            pfi++;
+            en.bytes += 16;
+        }
+        if (d.has_recops) {
+            d.fired_mask[e] = fired;
+            en.bytes += 4;
+        }
+        if (xh) d.ext_head[e] = 0;
+    }
+    // totals (last virtual block) and algorithmic-byte tally
+    const unsigned wb = (unsigned)wave_sum(en.bytes);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&s_bytes, wb);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(&d.ctrl->bytes_tick, (unsigned long long)s_bytes);
+        if (vb == gridDim.x - 1) {
+            d.ctrl->n_ev = s_base[0] + (tot & 0xFFFFFFFFull);
+            d.ctrl->n_fi = s_base[1] + (tot >> 32);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Record effects: one wave per entity, lane = row.  Cells [cap][cols][rows] so the
+// wave reads one (entity, col) row-vector contiguously.
+__global__ __launch_bounds__(kTPB) void k_records(Dev d) {
+    __shared__ unsigned s_vb;
+    __shared__ unsigned long long s_w[kTPB / 64];
+    __shared__ unsigned long long s_base;
+    __shared__ unsigned s_bytes;
+    if (threadIdx.x == 0) {
+        s_vb = atomicAdd(&d.ctrl->ticket_rec, 1u);
+        s_bytes = 0;
+    }
+    __syncthreads();
+    const unsigned vb = s_vb;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int e = (int)(vb * (kTPB / 64) + w);
+    const Tables* tab = d.tab;
+    const int nro = tab->n_recops;
+    unsigned bytes = 0;
+    uint32_t mask = 0;
+    if (e < d.N) {
+        mask = d.fired_mask[e];
+        if (lane == 0) bytes += 4;
+    }
+    mask &= tab->kind_has_recop;
+    // apply (at most NFK_MAX_OPS record ops, distinct (rec, col), sorted by (rec, col))
+    bool ch[NFK_MAX_OPS];
+    uint64_t ov[NFK_MAX_OPS], nv[NFK_MAX_OPS];
+#pragma unroll
+    for (int j = 0; j < NFK_MAX_OPS; j++) {
+        ch[j] = false;
+        ov[j] = nv[j] = 0;
+        if (j >= nro || !mask) continue;
+        const RecOp ro = tab->recops[j];
+        if (!((mask >> ro.kind) & 1)) continue;
+        const int rows = tab->rec_rows[ro.rec], cols = tab->rec_cols[ro.rec];
+        const uint64_t used = d.rused[ro.rec][e];
+        if (lane == 0) bytes += 8;
+        if (lane >= rows || !((used >> lane) & 1)) continue;
+        uint64_t* cp = d.rcells[ro.rec] + ((size_t)e * cols + ro.col) * rows + lane;
+        const uint64_t cur = *cp;
+        bytes += 8;
+        uint64_t nb;
+        bool changed;
+        if (ro.code == NFK_OP_RIADD_CLAMP) {
+            int64_t v = (int64_t)(cur + (uint64_t)ro.a);
+            v = v < ro.b ? ro.b : v;
+            v = v > ro.c ? ro.c : v;
+            nb = (uint64_t)v;
+            changed = v != (int64_t)cur;  // TData::operator== (NFIDataList.h:98)
+        } else {
+            const double x = __longlong_as_double((long long)cur);
+            const double m = x * __longlong_as_double(ro.a);
+            const double v = m + __longlong_as_double(ro.b);
+            const double df = v - x;
+            changed = !(df < 0.001 && df > -0.001);  // NFIDataList.h:106-113
+            nb = (uint64_t)__double_as_longlong(v);
+        }
+        if (changed) {
+            *cp = nb;
+            bytes += 8;
+            ch[j] = nb != cur;  // coalesced diff: bits must differ
+            ov[j] = cur;
+            nv[j] = nb;
+        }
+    }
+    // per-entity event order: (rec, row, col) -> records outer, lanes (rows), cols inner
+    unsigned cnt = 0;
+#pragma unroll
+    for (int j = 0; j < NFK_MAX_OPS; j++) cnt += ch[j] ? 1 : 0;
+    const unsigned long long wtot = wave_sum(cnt);
+    // block scan over the 4 entities of this block
+    if (lane == 0) s_w[w] = wtot;
+    __syncthreads();
+    unsigned long long before = 0, btot = 0;
+#pragma unroll
+    for (int i = 0; i < kTPB / 64; i++) {
+        before += (i < w) ? s_w[i] : 0ull;
+        btot += s_w[i];
+    }
+    if (w == 0) {
+        const unsigned long long b = lookback(d.g_re, vb, d.tag, btot, d.ctrl);
+        if (lane == 0) s_base = b;
+    }
+    __syncthreads();
+    unsigned long long pos = s_base + before;
+    // emit: for each record (ascending) the wave compacts rows; within a row, cols ascending
+    int j0 = 0;
+    while (j0 < nro) {
+        const int rec = tab->recops[j0].rec;
+        int j1 = j0;
+        while (j1 < nro && tab->recops[j1].rec == rec) j1++;
+        unsigned c = 0;
+#pragma unroll
+        for (int j = 0; j < NFK_MAX_OPS; j++) c += (j >= j0 && j < j1 && ch[j]) ? 1 : 0;
+        const unsigned long long inc = wave_incl_scan(c);
+        unsigned long long p = pos + inc - c;
+#pragma unroll
+        for (int j = 0; j < NFK_MAX_OPS; j++) {
+            if (!(j >= j0 && j < j1 && ch[j])) continue;
+            if ((long long)p < d.re_cap) {
+                d.re_slot[p] = (uint32_t)e;
+                d.re_rrc[p] = ((uint32_t)rec << 16) | ((uint32_t)lane << 8) | (uint32_t)tab->recops[j].col;
+                d.re_old[p] = ov[j];
+                d.re_new[p] = nv[j];
+            } else {
+                atomicOr(&d.ctrl->err, kErrReCap);
+            }
+            p++;
+            bytes += 24;
+        }
+        pos += __shfl(inc, 63, 64);
+        j0 = j1;
+    }
+    const unsigned wb = (unsigned)wave_sum(bytes);
+    if (lane == 0) atomicAdd(&s_bytes, wb);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(&d.ctrl->bytes_rec, (unsigned long long)s_bytes);
+        if (vb == gridDim.x - 1) d.ctrl->n_re = s_base + btot;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Fan-out over the virtual event stream [prop events ++ record events].  Persistent
+// grid, 256-event tiles pulled from a ticket; message offsets by look-back.
+__global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
+    __shared__ unsigned s_tile;
+    __shared__ unsigned long long s_w[kTPB / 64];
+    __shared__ unsigned long long s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long nev = d.ctrl->n_ev < (unsigned long long)d.ev_cap ? d.ctrl->n_ev : d.ev_cap;
+    const unsigned long long nre = d.ctrl->n_re < (unsigned long long)d.re_cap ? d.ctrl->n_re : d.re_cap;
+    const unsigned long long total = nev + nre;
+    const unsigned long long ntiles = (total + kTPB - 1) / kTPB;
+    unsigned bytes = 0;
+    while (true) {
+        if (threadIdx.x == 0) s_tile = atomicAdd(&d.ctrl->ticket_fan, 1u);
+        __syncthreads();
+        const unsigned tile = s_tile;
+        if (tile >= ntiles) break;
+        const unsigned long long i = (unsigned long long)tile * kTPB + threadIdx.x;
+        unsigned cnt = 0;
+        int32_t slot = 0, pb = 0, np = 0;
+        uint8_t fl = 0;
+        if (i < total) {
+            if (i < nev) {
+                slot = (int32_t)d.ev_slot[i];
+                fl = d.tab->pflags[d.cls[slot]][d.ev_pid[i]];
+            } else {
+                slot = (int32_t)d.re_slot[i - nev];
+                fl = d.tab->rflags[d.cls[slot]][d.re_rrc[i - nev] >> 16];
+            }
+            bytes += 4 + 4 + 1;
+            if (fl & NFK_PUBLIC) {
+                const int seg = d.seg_of[slot];
+                pb = d.seg_pl_off[seg];
+                np = d.seg_pl_off[seg + 1] - pb;
+                cnt = (unsigned)(np - (d.isplayer[slot] ? 1 : 0));
+                bytes += 4 + 8 + 1;
+            } else if ((fl & NFK_PRIVATE) && !(fl & NFK_UPLOAD)) {
+                cnt = 1;
+            }
+        }
+        unsigned long long tot;
+        const unsigned long long excl = block_excl_scan(cnt, s_w, tot);
+        if (w == 0) {
+            const unsigned long long b = lookback(d.g_msg, tile, d.tag, tot, d.ctrl);
+            if (lane == 0) s_base = b;
+        }
+        __syncthreads();
+        const unsigned long long off = s_base + excl;
+        if (i < total) {
+            d.msg_off[i] = (uint32_t)off;
+            bytes += 4;
+            if (off + cnt > (unsigned long long)d.msg_cap) {
+                atomicOr(&d.ctrl->err, kErrMsgCap);
+            } else if (fl & NFK_PUBLIC) {
+                unsigned long long p = off;
+                for (int j = 0; j < np; j++) {
+                    const int32_t r = d.pl_slot[pb + j];
+                    if (r == slot) continue;
+                    d.msg_rcpt[p++] = (uint32_t)r;
+                }
+                bytes += 4 * np + 4 * cnt;
+            } else if (cnt) {
+                d.msg_rcpt[off] = (uint32_t)slot;
+                bytes += 4;
+            }
+        }
+        if (tile == ntiles - 1 && threadIdx.x == 0) {
+            d.ctrl->n_msgs = s_base + tot;
+            d.msg_off[total] = (uint32_t)(s_base + tot);
+        }
+        __syncthreads();
+    }
+    const unsigned wb = (unsigned)wave_sum(bytes);
+    if (lane == 0 && wb) atomicAdd(&d.ctrl->bytes_fan, (unsigned long long)wb);
+    if (ntiles == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+        d.ctrl->n_msgs = 0;
+        d.msg_off[0] = 0;
+    }
+}
+
+}  // namespace nfgpu

@@ -1,0 +1,311 @@
+"""Python host mirror of the reference plugin API over the C-ABI (include/nfgpu.h).
+
+`NFKernelModule` keeps the names, argument meaning and failure behaviour of the
+reference's NFIKernelModule / NFIScheduleModule calls on the tick path
+(NFComm/NFPluginModule/NFIKernelModule.h, NFIScheduleModule.h):
+CreateObject, SetPropertyInt/Float, GetPropertyInt/Float, AddSchedule,
+RemoveSchedule, Execute.  The compute runs in libnfgpu.so (hand-written HIP
+for gfx950).  There is no CPU fallback: constructing a module without the
+library or without a GPU raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import workload as wl
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnfgpu.so")
+
+NFK_OK = 0
+_ERRS = {-1: "NFK_ERR_ARG", -2: "NFK_ERR_HIP", -3: "NFK_ERR_STATE", -4: "NFK_ERR_CAPACITY",
+         -5: "NFK_ERR_TOUCH", -6: "NFK_ERR_DEVICE", -7: "NFK_ERR_NOTFOUND"}
+
+
+class NFKError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{_ERRS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("capacity", ctypes.c_int32), ("n_int", ctypes.c_int32), ("n_flt", ctypes.c_int32),
+                ("n_class", ctypes.c_int32), ("n_kind", ctypes.c_int32), ("n_rec", ctypes.c_int32),
+                ("msg_capacity", ctypes.c_int64), ("stream", ctypes.c_void_p)]
+
+
+class Summary(ctypes.Structure):
+    _fields_ = [("n_entities", ctypes.c_int64), ("n_prop_events", ctypes.c_int64),
+                ("n_rec_events", ctypes.c_int64), ("n_fired", ctypes.c_int64), ("n_msgs", ctypes.c_int64),
+                ("alg_bytes_tick", ctypes.c_int64), ("alg_bytes_rec", ctypes.c_int64),
+                ("alg_bytes_fan", ctypes.c_int64), ("device_error", ctypes.c_int32), ("tick", ctypes.c_int32)]
+
+
+class Outputs(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in
+                ["ev_slot", "ev_pid", "ev_old", "ev_new", "re_slot", "re_rrc", "re_old", "re_new",
+                 "fi_slot", "fi_kind", "fi_remain", "msg_off", "msg_rcpt", "slot_obj"]]
+
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libnfgpu.so; raises if it is missing (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(path)
+    P, I32, I64, VP = ctypes.POINTER, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p
+    sig = {
+        "nfk_create": [P(Config), P(VP)], "nfk_destroy": [VP], "nfk_last_error": [],
+        "nfk_set_prop_flags": [VP, I32, VP], "nfk_define_record": [VP, I32, I32, I32, VP, VP],
+        "nfk_define_kind": [VP, I32, VP, I32],
+        "nfk_create_objects": [VP, I32, VP, VP, VP, VP, VP, VP], "nfk_load_prop": [VP, I32, VP],
+        "nfk_load_record": [VP, I32, VP, VP], "nfk_commit": [VP],
+        "nfk_set_props": [VP, I32, VP, VP, VP, VP],
+        "nfk_add_schedules": [VP, I32, VP, VP, VP, VP, VP, VP],
+        "nfk_remove_schedule": [VP, I64, I64, I32], "nfk_remove_all_schedules": [VP, I64, I64],
+        "nfk_execute": [VP, I64], "nfk_summary_get": [VP, P(Summary)], "nfk_outputs_get": [VP, P(Outputs)],
+        "nfk_read_prop": [VP, I32, VP], "nfk_read_record": [VP, I32, VP], "nfk_read_schedules": [VP, VP, VP, VP],
+        "nfk_read_events": [VP, VP, VP, VP, VP], "nfk_read_rec_events": [VP, VP, VP, VP, VP],
+        "nfk_read_fired": [VP, VP, VP, VP], "nfk_read_fanout": [VP, VP, VP],
+        "nfk_set_profiling": [VP, I32], "nfk_kernel_times": [VP, VP, VP, VP], "nfk_reset_kernel_times": [VP],
+    }
+    for name, args in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_char_p if name == "nfk_last_error" else ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+class NFKernelModule:
+    """One GPU-resident world (the entities of one scene shard)."""
+
+    def __init__(self, capacity, n_int=wl.N_INT, n_flt=wl.N_FLT, n_class=2, n_kind=len(wl.KINDS), n_rec=0,
+                 msg_capacity=0, stream=None):
+        self.lib = load_library()
+        cfg = Config(capacity, n_int, n_flt, n_class, n_kind, n_rec, msg_capacity, stream)
+        h = ctypes.c_void_p()
+        self._chk(self.lib.nfk_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.n_int, self.n_flt, self.n_kind, self.n_rec = n_int, n_flt, n_kind, n_rec
+        self.n_obj = 0
+        self.rec_shape = {}
+
+    def _chk(self, rc):
+        if rc != NFK_OK:
+            raise NFKError(rc, self.lib.nfk_last_error().decode())
+        return rc
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.nfk_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- schema (NFIClassModule) ----
+    def set_prop_flags(self, cls, flags):
+        flags = np.ascontiguousarray(flags, np.uint8)
+        self._chk(self.lib.nfk_set_prop_flags(self.h, cls, _p(flags)))
+
+    def define_record(self, rec, rows, cols, col_types, flags_per_class):
+        ct = np.ascontiguousarray(col_types, np.uint8)
+        fl = np.ascontiguousarray(flags_per_class, np.uint8)
+        self._chk(self.lib.nfk_define_record(self.h, rec, rows, cols, _p(ct), _p(fl)))
+        self.rec_shape[rec] = (cols, rows)
+
+    def define_kind(self, kind, ops):
+        ops = np.ascontiguousarray(ops)
+        if ops.dtype != wl.OP_DTYPE:
+            ops = ops.view(wl.OP_DTYPE).reshape(-1)
+        self._chk(self.lib.nfk_define_kind(self.h, kind, _p(ops), len(ops)))
+
+    # ---- objects (NFIKernelModule::CreateObject) ----
+    def create_objects(self, guid_head, guid_data, scene, group, cls, is_player):
+        a = [np.ascontiguousarray(x, t) for x, t in
+             ((guid_head, np.int64), (guid_data, np.int64), (scene, np.int32), (group, np.int32),
+              (cls, np.uint8), (is_player, np.uint8))]
+        self._chk(self.lib.nfk_create_objects(self.h, len(a[0]), *[_p(x) for x in a]))
+        self._keep = getattr(self, "_keep", []) + [a]
+        self.n_obj += len(a[0])
+
+    def load_prop(self, pid, values):
+        v = np.ascontiguousarray(values)
+        bits = v.view(np.uint64) if v.dtype.itemsize == 8 else v.astype(np.int64).view(np.uint64)
+        self._chk(self.lib.nfk_load_prop(self.h, pid, _p(np.ascontiguousarray(bits))))
+
+    def load_record(self, rec, cells, used):
+        c = np.ascontiguousarray(cells, np.uint64)
+        u = np.ascontiguousarray(used, np.uint64)
+        self._chk(self.lib.nfk_load_record(self.h, rec, _p(c), _p(u)))
+
+    def commit(self):
+        self._chk(self.lib.nfk_commit(self.h))
+
+    # ---- NFIKernelModule::SetProperty* (queued, applied at the next Execute) ----
+    def set_props(self, guid_head, guid_data, pid, bits):
+        a = [np.ascontiguousarray(x, t) for x, t in
+             ((guid_head, np.int64), (guid_data, np.int64), (pid, np.int32), (bits, np.uint64))]
+        self._chk(self.lib.nfk_set_props(self.h, len(a[0]), *[_p(x) for x in a]))
+
+    def SetPropertyInt(self, guid, prop, value):
+        pid = wl.PID[prop] if isinstance(prop, str) else prop
+        self.set_props([guid[0]], [guid[1]], [pid], [np.int64(value).view(np.uint64)])
+        return True
+
+    def SetPropertyFloat(self, guid, prop, value):
+        pid = wl.PID[prop] if isinstance(prop, str) else prop
+        self.set_props([guid[0]], [guid[1]], [pid], [np.float64(value).view(np.uint64)])
+        return True
+
+    # ---- NFIScheduleModule ----
+    def add_schedules(self, guid_head, guid_data, kind, interval_s, count, now_ms):
+        a = [np.ascontiguousarray(x, t) for x, t in
+             ((guid_head, np.int64), (guid_data, np.int64), (kind, np.int32), (interval_s, np.float32),
+              (count, np.int32), (now_ms, np.int64))]
+        self._chk(self.lib.nfk_add_schedules(self.h, len(a[0]), *[_p(x) for x in a]))
+
+    def AddSchedule(self, guid, name, interval_s, count, now_ms):
+        kind = wl.KID[name] if isinstance(name, str) else name
+        self.add_schedules([guid[0]], [guid[1]], [kind], [interval_s], [count], [now_ms])
+        return True
+
+    def RemoveSchedule(self, guid, name=None):
+        if name is None:
+            self._chk(self.lib.nfk_remove_all_schedules(self.h, int(guid[0]), int(guid[1])))
+        else:
+            kind = wl.KID[name] if isinstance(name, str) else name
+            self._chk(self.lib.nfk_remove_schedule(self.h, int(guid[0]), int(guid[1]), kind))
+        return True
+
+    # ---- one frame ----
+    def Execute(self, now_ms):
+        self._chk(self.lib.nfk_execute(self.h, int(now_ms)))
+        return True
+
+    def summary(self):
+        s = Summary()
+        self._chk(self.lib.nfk_summary_get(self.h, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in Summary._fields_}
+
+    def outputs(self):
+        o = Outputs()
+        self._chk(self.lib.nfk_outputs_get(self.h, ctypes.byref(o)))
+        return {f: getattr(o, f) for f, _ in Outputs._fields_}
+
+    # ---- readback ----
+    def read_prop(self, pid):
+        out = np.zeros(self.n_obj, np.uint64)
+        self._chk(self.lib.nfk_read_prop(self.h, pid, _p(out)))
+        return out.view(np.int64) if pid < self.n_int else out.view(np.float64)
+
+    def GetPropertyInt(self, guid, prop):
+        raise NotImplementedError("use read_prop for bulk reads")
+
+    def read_record(self, rec):
+        cols, rows = self.rec_shape[rec]
+        out = np.zeros((self.n_obj, cols, rows), np.uint64)
+        self._chk(self.lib.nfk_read_record(self.h, rec, _p(out)))
+        return out
+
+    def read_schedules(self):
+        nx = np.zeros((self.n_kind, self.n_obj), np.int64)
+        rm = np.zeros((self.n_kind, self.n_obj), np.int32)
+        st = np.zeros((self.n_kind, self.n_obj), np.uint8)
+        self._chk(self.lib.nfk_read_schedules(self.h, _p(nx), _p(rm), _p(st)))
+        return nx, rm, st
+
+    def read_tick(self):
+        """All outputs of the last frame, entities as object (creation) indices."""
+        s = self.summary()
+        ne, nr, nf, nm = s["n_prop_events"], s["n_rec_events"], s["n_fired"], s["n_msgs"]
+        ev = [np.zeros(ne, np.int32), np.zeros(ne, np.int32), np.zeros(ne, np.uint64), np.zeros(ne, np.uint64)]
+        self._chk(self.lib.nfk_read_events(self.h, *[_p(x) for x in ev]))
+        re = [np.zeros(nr, np.int32), np.zeros(nr, np.uint32), np.zeros(nr, np.uint64), np.zeros(nr, np.uint64)]
+        self._chk(self.lib.nfk_read_rec_events(self.h, *[_p(x) for x in re]))
+        fi = [np.zeros(nf, np.int32), np.zeros(nf, np.int32), np.zeros(nf, np.int32)]
+        self._chk(self.lib.nfk_read_fired(self.h, *[_p(x) for x in fi]))
+        mo = np.zeros(ne + nr + 1, np.uint32)
+        mr = np.zeros(nm, np.int32)
+        self._chk(self.lib.nfk_read_fanout(self.h, _p(mo), _p(mr)))
+        return dict(ev_obj=ev[0], ev_pid=ev[1], ev_old=ev[2], ev_new=ev[3],
+                    re_obj=re[0], re_rrc=re[1], re_old=re[2], re_new=re[3],
+                    fi_obj=fi[0], fi_kind=fi[1], fi_rem=fi[2], mo_off=mo, mr_obj=mr, summary=s)
+
+    # ---- measurement ----
+    def set_profiling(self, on):
+        self._chk(self.lib.nfk_set_profiling(self.h, 1 if on else 0))
+
+    def kernel_times(self):
+        ms = np.zeros(4, np.float64)
+        n = np.zeros(4, np.int64)
+        b = np.zeros(4, np.int64)
+        self._chk(self.lib.nfk_kernel_times(self.h, _p(ms), _p(n), _p(b)))
+        return ms, n, b
+
+    def reset_kernel_times(self):
+        self._chk(self.lib.nfk_reset_kernel_times(self.h))
+
+
+def world_from_workload(w, capacity=None, msg_capacity=0, stream=None):
+    """Build an NFKernelModule from a workload dict (see workload.make_world): classes,
+    kinds, objects, creation-time values, then the AddSchedule calls made before frame 0."""
+    cfg = w["cfg"]
+    n_obj, n_int, n_flt, n_cls, n_kind, n_rec = (int(x) for x in cfg[:6])
+    m = NFKernelModule(capacity or n_obj, n_int, n_flt, n_cls, n_kind, n_rec, msg_capacity, stream)
+    for c in range(n_cls):
+        m.set_prop_flags(c, w["prop_flags"][c])
+    for r in range(n_rec):
+        m.define_record(r, int(w["rec_rows"][r]), int(w["rec_cols"][r]), w["rec_ctype"][r],
+                        w["rec_flags"][:, r])
+    for k in range(n_kind):
+        m.define_kind(k, w["ops"][k][: int(w["n_ops"][k])])
+    m.create_objects(w["guid_head"], w["guid_data"], w["scene"], w["group"], w["cls"], w["is_player"])
+    for p in range(n_int):
+        m.load_prop(p, w["init_i"][p])
+    for p in range(n_flt):
+        m.load_prop(n_int + p, w["init_f"][p])
+    for r in range(n_rec):
+        m.load_record(r, w[f"rec{r}_cells"], w[f"rec{r}_used"])
+    m.commit()
+    gh, gd = w["guid_head"], w["guid_data"]
+    so = w["s_obj"]
+    m.add_schedules(gh[so], gd[so], w["s_kind"], w["s_interval"], w["s_count"], w["s_time"])
+    return m
+
+
+def run_workload(m, w, tick, collect=True):
+    """Replay the between-frame calls of frame `tick`, then Execute it."""
+    gh, gd = w["guid_head"], w["guid_data"]
+    hsel = np.nonzero(w["h_tick"] == tick)[0]
+    for i in hsel:   # call order preserved
+        o = int(w["h_obj"][i])
+        op = int(w["h_op"][i])
+        g = (int(gh[o]), int(gd[o]))
+        if op == 1:
+            m.add_schedules([g[0]], [g[1]], [w["h_kind"][i]], [w["h_interval"][i]], [w["h_count"][i]],
+                            [w["h_time"][i]])
+        elif op == 2:
+            m.RemoveSchedule(g, int(w["h_kind"][i]))
+        else:
+            m.RemoveSchedule(g)
+    xsel = np.nonzero(w["x_tick"] == tick)[0]
+    if len(xsel):
+        xo = w["x_obj"][xsel]
+        m.set_props(gh[xo], gd[xo], w["x_pid"][xsel], w["x_bits"][xsel])
+    m.Execute(int(w["tick_time"][tick]))
+    return m.read_tick() if collect else None

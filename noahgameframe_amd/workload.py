@@ -1,0 +1,286 @@
+"""Synthetic NoahGameFrame worlds (product-side input generation, no oracle code).
+
+A world mirrors the reference's game-server shape: NPC / Player classes whose
+property flags follow _Out/NFDataCfg/Struct/Class/{IObject,NPC,Player}.xml,
+objects grouped into (scene, group) cells (NFCSceneInfo / NFCSceneGroupInfo),
+heartbeats registered through NFIScheduleModule::AddSchedule with effect
+programs, optional per-player records (item/skill tables with cooldowns),
+SetProperty calls from game logic between frames, and AddSchedule /
+RemoveSchedule calls between frames.
+
+`make_world(...)` returns a dict of numpy arrays in the NFIO layout consumed by
+the GPU path (noahgameframe_amd.kernel), the CPU oracle and the reference
+harness.
+"""
+import struct
+
+import numpy as np
+
+# ---- schema ---------------------------------------------------------------
+INT_PROPS = ["HP", "MAXHP", "HPREGEN", "MP", "MAXMP", "MPREGEN", "SP", "MAXSP",
+             "SPREGEN", "EXP", "Gold", "Level", "ATK_VALUE", "DEF_VALUE", "Camp", "NPCType"]
+FLT_PROPS = ["X", "Y", "Z", "TargetX", "TargetY", "AtkDis"]
+PROPS = INT_PROPS + FLT_PROPS
+PID = {n: i for i, n in enumerate(PROPS)}
+N_INT, N_FLT = len(INT_PROPS), len(FLT_PROPS)
+
+PUBLIC, PRIVATE, UPLOAD = 1, 2, 4
+CLS_NPC, CLS_PLAYER = 0, 1
+
+# heartbeat kinds: id order == lexical order of the schedule names (NFMapEx<std::string, ...>)
+KINDS = ["HPRegen", "MPRegen", "Move", "Patrol", "Poison", "SkillCD"]
+assert KINDS == sorted(KINDS)
+KID = {n: i for i, n in enumerate(KINDS)}
+
+# op codes / flags (include/nfgpu.h)
+OP_IADD_CLAMP, OP_FLERP, OP_FAFFINE, OP_RIADD_CLAMP, OP_RFAFFINE = 1, 2, 3, 4, 5
+A_PROP, LO_PROP, HI_PROP = 1, 2, 4
+MAX_OPS = 4
+MAX_REC_COLS = 16
+I64_MIN, I64_MAX = -(2 ** 63), 2 ** 63 - 1
+
+OP_DTYPE = np.dtype([("code", "u1"), ("flags", "u1"), ("dst", "<u2"), ("pad", "<u4"),
+                     ("a", "<i8"), ("b", "<i8"), ("c", "<i8")])
+assert OP_DTYPE.itemsize == 32
+
+
+def f64bits(x):
+    return struct.unpack("<q", struct.pack("<d", float(x)))[0]
+
+
+def _prop_flags():
+    f = np.zeros((2, len(PROPS)), np.uint8)
+    pubpriv = PUBLIC | PRIVATE
+    for c in (CLS_NPC, CLS_PLAYER):
+        for n in ["HP", "MAXHP", "HPREGEN", "MP", "MAXMP", "MPREGEN", "SP", "MAXSP", "SPREGEN",
+                  "EXP", "Gold", "Level", "ATK_VALUE", "DEF_VALUE", "X", "Y", "Z"]:
+            f[c, PID[n]] = pubpriv
+    f[CLS_NPC, PID["Camp"]] = PRIVATE             # NPC.xml: Camp Public=0 Private=1
+    f[CLS_PLAYER, PID["Camp"]] = pubpriv          # Player.xml: Camp Public=1 Private=1
+    f[CLS_PLAYER, PID["Gold"]] = PRIVATE | UPLOAD  # an Upload property never echoes to its owner
+    # NPCType, TargetX, TargetY, AtkDis: Public=0 Private=0 (no sync)
+    return f
+
+
+def programs(with_records, rec_float_op=True):
+    ops = np.zeros((len(KINDS), MAX_OPS), OP_DTYPE)
+    n_ops = np.zeros(len(KINDS), np.int32)
+
+    def put(kind, lst):
+        for i, o in enumerate(lst):
+            ops[KID[kind], i] = o
+        n_ops[KID[kind]] = len(lst)
+
+    put("HPRegen", [(OP_IADD_CLAMP, A_PROP | HI_PROP, PID["HP"], 0, PID["HPREGEN"], 0, PID["MAXHP"])])
+    put("MPRegen", [(OP_IADD_CLAMP, A_PROP | HI_PROP, PID["MP"], 0, PID["MPREGEN"], 0, PID["MAXMP"])])
+    put("Move", [(OP_FLERP, 0, PID["X"], 0, PID["TargetX"], f64bits(0.125), 0),
+                 (OP_FLERP, 0, PID["Y"], 0, PID["TargetY"], f64bits(0.125), 0)])
+    put("Patrol", [(OP_FAFFINE, 0, PID["TargetX"], 0, f64bits(-1.0), f64bits(0.0), 0),
+                   (OP_FAFFINE, 0, PID["TargetY"], 0, f64bits(-1.0), f64bits(0.0), 0)])
+    put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 1, PID["MAXHP"])])
+    if with_records:
+        # skill table: col 1 = cooldown ms (int), col 2 = charge (f64) decays
+        lst = [(OP_RIADD_CLAMP, 0, (0 << 8) | 1, 0, -100, 0, I64_MAX)]
+        if rec_float_op:
+            lst.append((OP_RFAFFINE, 0, (0 << 8) | 2, 0, f64bits(0.5), f64bits(0.0), 0))
+        put("SkillCD", lst)
+    return ops, n_ops
+
+
+def _names(lst):
+    a = np.zeros((len(lst), 32), np.uint8)
+    for i, s in enumerate(lst):
+        b = s.encode()
+        a[i, :len(b)] = np.frombuffer(b, np.uint8)
+    return a
+
+
+def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4, n_ticks=8,
+               tick_ms=100, seed=1, ext_frac=0.05, host_ops=True, records=False, rec_rows=64,
+               t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True):
+    rng = np.random.default_rng(seed)
+    n_groups = n_scenes * groups_per_scene
+    # ---- objects ----
+    cell = rng.integers(0, n_groups, n_obj)
+    cell[:n_groups] = np.arange(min(n_groups, n_obj))
+    scene = (cell // groups_per_scene + 1).astype(np.int32)
+    group = (cell % groups_per_scene + 1).astype(np.int32)   # group 0 = scene base group
+    ghead = np.where(rng.random(n_obj) < 0.9, guid_heads[0], guid_heads[-1]).astype(np.int64)
+    gdata = rng.choice(np.int64(1) << 40, size=n_obj, replace=False).astype(np.int64) + 1
+    isplayer = np.zeros(n_obj, np.uint8)
+    order = np.lexsort((rng.random(n_obj), cell))
+    first = np.ones(n_obj, bool)
+    first[1:] = cell[order][1:] != cell[order][:-1]
+    idx_in_cell = np.arange(n_obj) - np.maximum.accumulate(np.where(first, np.arange(n_obj), 0))
+    isplayer[order[idx_in_cell < players_per_group]] = 1
+    cls = np.where(isplayer == 1, CLS_PLAYER, CLS_NPC).astype(np.uint8)
+
+    # ---- creation-time properties ----
+    init_i = np.zeros((N_INT, n_obj), np.int64)
+    maxhp = rng.integers(500, 5000, n_obj)
+    init_i[PID["MAXHP"]] = maxhp
+    init_i[PID["HP"]] = rng.integers(1, maxhp + 1)
+    init_i[PID["HPREGEN"]] = rng.integers(1, 50, n_obj)
+    maxmp = rng.integers(100, 1000, n_obj)
+    init_i[PID["MAXMP"]] = maxmp
+    init_i[PID["MP"]] = rng.integers(0, maxmp + 1)
+    init_i[PID["MPREGEN"]] = rng.integers(1, 20, n_obj)
+    init_i[PID["MAXSP"]] = rng.integers(100, 300, n_obj)
+    init_i[PID["SP"]] = rng.integers(0, 100, n_obj)
+    init_i[PID["SPREGEN"]] = rng.integers(1, 5, n_obj)
+    init_i[PID["EXP"]] = rng.integers(0, 10 ** 6, n_obj)
+    init_i[PID["Gold"]] = rng.integers(0, 10 ** 5, n_obj)
+    init_i[PID["Level"]] = rng.integers(1, 60, n_obj)
+    init_i[PID["ATK_VALUE"]] = rng.integers(10, 500, n_obj)
+    init_i[PID["DEF_VALUE"]] = rng.integers(10, 500, n_obj)
+    init_i[PID["Camp"]] = rng.integers(0, 4, n_obj)
+    init_i[PID["NPCType"]] = rng.integers(0, 6, n_obj)
+    init_f = np.zeros((N_FLT, n_obj), np.float64)
+
+    def coord(n):
+        v = rng.uniform(-1000.0, 1000.0, n)
+        return np.where(np.abs(v) < 1.0, v + np.sign(v + 0.5) * 2.0, v)  # no near-zero values
+    fi = {n: i - N_INT for n, i in PID.items() if i >= N_INT}
+    init_f[fi["X"]] = coord(n_obj)
+    init_f[fi["Y"]] = coord(n_obj)
+    init_f[fi["Z"]] = coord(n_obj)
+    init_f[fi["TargetX"]] = coord(n_obj)
+    init_f[fi["TargetY"]] = coord(n_obj)
+    init_f[fi["AtkDis"]] = rng.uniform(1.0, 10.0, n_obj)
+    # a few objects sit exactly on their target: Move produces no change (SetFloat eps path)
+    still = rng.random(n_obj) < 0.02
+    init_f[fi["X"], still] = init_f[fi["TargetX"], still]
+
+    ops, n_ops = programs(records, rec_float_op)
+    n_kind = len(KINDS) if records else len(KINDS) - 1
+
+    # ---- heartbeats registered before the first frame ----
+    spec = [("HPRegen", 1.0, -1), ("MPRegen", 2.0, -1), ("Move", 0.1, -1), ("Patrol", 3.0, -1),
+            ("Poison", 0.5, None)]
+    s_obj, s_kind, s_int, s_cnt, s_time = [], [], [], [], []
+    for name, iv, cnt in spec:
+        take = rng.random(n_obj) < (0.7 if name == "Poison" else 1.0)
+        objs = np.nonzero(take)[0]
+        s_obj.append(objs)
+        s_kind.append(np.full(len(objs), KID[name]))
+        s_int.append(np.full(len(objs), iv, np.float32))
+        s_cnt.append(rng.integers(3, 40, len(objs)) if cnt is None else np.full(len(objs), cnt))
+        s_time.append(t0 - rng.integers(0, int(iv * 1000) + 1, len(objs)))
+    if records:
+        objs = np.nonzero(isplayer)[0]
+        s_obj.append(objs)
+        s_kind.append(np.full(len(objs), KID["SkillCD"]))
+        s_int.append(np.full(len(objs), 0.1, np.float32))
+        s_cnt.append(np.full(len(objs), -1))
+        s_time.append(t0 - rng.integers(0, 101, len(objs)))
+    s_obj = np.concatenate(s_obj).astype(np.int32)
+    perm = rng.permutation(len(s_obj))   # AddSchedule call order is arbitrary
+    s_obj = s_obj[perm]
+    s_kind = np.concatenate(s_kind).astype(np.int32)[perm]
+    s_int = np.concatenate(s_int).astype(np.float32)[perm]
+    s_cnt = np.concatenate(s_cnt).astype(np.int32)[perm]
+    s_time = np.concatenate(s_time).astype(np.int64)[perm]
+
+    tick_time = (t0 + tick_ms * np.arange(1, n_ticks + 1)).astype(np.int64)
+
+    # ---- SetProperty calls between frames (call order matters) ----
+    xt, xo, xp, xb = [], [], [], []
+    ext_props = [PID["HP"], PID["Gold"], PID["EXP"], PID["TargetX"]]
+    for t in range(n_ticks):
+        k = int(ext_frac * n_obj)
+        if k == 0:
+            continue
+        objs = rng.integers(0, n_obj, k)
+        props = rng.choice(ext_props, k)
+        vals = np.zeros(k, np.uint64)
+        for j, p in enumerate(props):
+            o = objs[j]
+            if p == PID["HP"]:
+                v = int(rng.integers(1, maxhp[o] + 1))
+                if rng.random() < 0.1:
+                    v = int(init_i[PID["HP"], o])  # often unchanged -> no event
+                vals[j] = np.uint64(v & (2 ** 64 - 1))
+            elif p in (PID["Gold"], PID["EXP"]):
+                vals[j] = np.uint64(int(rng.integers(0, 10 ** 6)))
+            else:
+                vals[j] = np.uint64(f64bits(coord(1)[0]) & (2 ** 64 - 1))
+        # duplicates: same (object, property) set twice in one frame (coalesced)
+        dup = rng.random(k) < 0.05
+        objs = np.concatenate([objs, objs[dup]])
+        props = np.concatenate([props, props[dup]])
+        vals = np.concatenate([vals, vals[dup][::-1]])
+        xt.append(np.full(len(objs), t))
+        xo.append(objs)
+        xp.append(props)
+        xb.append(vals)
+    cat = lambda lst, dt: np.concatenate(lst).astype(dt) if lst else np.zeros(0, dt)
+    x_tick, x_obj, x_pid, x_bits = cat(xt, np.int32), cat(xo, np.int32), cat(xp, np.int32), cat(xb, np.uint64)
+
+    # ---- AddSchedule / RemoveSchedule calls between frames ----
+    ht, hop, hob, hk, hiv, hc, htm = [], [], [], [], [], [], []
+    if host_ops:
+        for t in range(1, n_ticks):
+            m = max(1, n_obj // 64)
+            for _ in range(m):
+                o = int(rng.integers(0, n_obj))
+                r = rng.random()
+                if r < 0.45:
+                    op, kind = 1, KID["Poison"]
+                elif r < 0.75:
+                    op, kind = 2, int(rng.choice([KID["Patrol"], KID["Poison"], KID["MPRegen"]]))
+                elif r < 0.85:
+                    op, kind = 3, 0
+                else:
+                    op, kind = 1, int(rng.choice([KID["HPRegen"], KID["Patrol"]]))
+                ht.append(t)
+                hop.append(op)
+                hob.append(o)
+                hk.append(kind)
+                hiv.append(0.5 if kind == KID["Poison"] else 1.0)
+                hc.append(int(rng.integers(1, 5)) if kind == KID["Poison"] else -1)
+                htm.append(int(tick_time[t - 1]) + int(rng.integers(0, tick_ms)))
+    h = dict(h_tick=np.array(ht, np.int32), h_op=np.array(hop, np.int32), h_obj=np.array(hob, np.int32),
+             h_kind=np.array(hk, np.int32), h_interval=np.array(hiv, np.float32),
+             h_count=np.array(hc, np.int32), h_time=np.array(htm, np.int64))
+
+    n_rec = 1 if records else 0
+    w = dict(
+        cfg=np.array([n_obj, N_INT, N_FLT, 2, n_kind, n_rec, len(s_obj), n_ticks], np.int64),
+        prop_flags=_prop_flags(), prop_names=_names(PROPS), kind_names=_names(KINDS[:n_kind]),
+        ops=ops[:n_kind].copy(), n_ops=n_ops[:n_kind].copy(),
+        guid_head=ghead, guid_data=gdata, scene=scene, group=group, cls=cls, is_player=isplayer,
+        init_i=init_i, init_f=init_f,
+        s_obj=s_obj, s_kind=s_kind, s_interval=s_int, s_count=s_cnt, s_time=s_time,
+        tick_time=tick_time, x_tick=x_tick, x_obj=x_obj, x_pid=x_pid, x_bits=x_bits, **h)
+    if records:
+        rows, cols = rec_rows, 3
+        w["rec_rows"] = np.array([rows], np.int32)
+        w["rec_cols"] = np.array([cols], np.int32)
+        ct = np.zeros((1, MAX_REC_COLS), np.uint8)
+        ct[0, 2] = 1                                   # col 0 skill id, 1 cooldown ms, 2 charge (f64)
+        w["rec_ctype"] = ct
+        rf = np.zeros((2, 1), np.uint8)
+        rf[CLS_PLAYER, 0] = PRIVATE                    # skill table: private to its owner
+        rf[CLS_NPC, 0] = PUBLIC | PRIVATE
+        w["rec_flags"] = rf
+        cells = np.zeros((n_obj, cols, rows), np.uint64)
+        cells[:, 0, :] = rng.integers(1000, 2000, (n_obj, rows)).astype(np.uint64)
+        cd = rng.integers(0, 3000, (n_obj, rows))
+        cd[rng.random((n_obj, rows)) < 0.3] = 0
+        cells[:, 1, :] = cd.astype(np.uint64)
+        ch = rng.uniform(0.0, 100.0, (n_obj, rows))
+        ch[rng.random((n_obj, rows)) < 0.2] = 0.0005    # below the 0.001 record threshold
+        cells[:, 2, :] = ch.view(np.uint64)
+        used = rng.integers(0, 2 ** 63, n_obj, dtype=np.int64).astype(np.uint64)
+        if rows < 64:
+            used &= np.uint64((1 << rows) - 1)
+        w["rec0_cells"] = cells
+        w["rec0_used"] = used
+    return w
+
+
+def bench_world(n_obj=1 << 20, groups=4096, players_per_group=8, n_ticks=16, seed=2026, **kw):
+    """config[1]: 1M NPCs in one scene, 4096 groups, int/float mutation + diff + fan-out."""
+    return make_world(n_obj=n_obj, n_scenes=1, groups_per_scene=groups,
+                      players_per_group=players_per_group, n_ticks=n_ticks, seed=seed,
+                      ext_frac=kw.pop("ext_frac", 0.0), host_ops=kw.pop("host_ops", False), **kw)

@@ -1,0 +1,585 @@
+/* nf_oracle.c — CPU restatement of NoahGameFrame's per-tick entity update path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This program is the parity checker for the HIP
+ * path (noahgameframe_amd/csrc); only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may run it.  It is pinned against the real
+ * reference code built by oracle/build_ref.sh (oracle/_ref/nf_ref_harness)
+ * through the golden fixtures under tests/golden/.
+ *
+ * What it restates (flyish/NoahGameFrame, file:line):
+ *   set_int        NFComm/NFCore/NFCProperty.cpp:254-293  (exact compare; null == 0)
+ *   set_flt        NFComm/NFCore/NFCProperty.cpp:295-334  (IsZeroDouble(v-cur), eps 1e-15,
+ *                  NFComm/NFPluginModule/NFPlatform.h:362)
+ *   set_rint       NFComm/NFCore/NFCRecord.cpp:182-241    (TData::operator== exact)
+ *   set_rflt       NFComm/NFCore/NFCRecord.cpp:243-303    (TData::operator== |d| < 0.001,
+ *                  NFComm/NFCore/NFIDataList.h:106-113)
+ *   sched_execute  NFComm/NFKernelPlugin/NFCScheduleModule.cpp:45-110 (object schedules:
+ *                  fire test, count, reschedule, std::map remove-list insert quirk,
+ *                  remove-then-add order, add dedup by name)
+ *   add_schedule   NFComm/NFKernelPlugin/NFCScheduleModule.cpp:236-257
+ *   fanout         NFComm/NFKernelPlugin/NFCSceneAOIModule.cpp:227-290 and 531-593
+ *                  (GetBroadCastObject: public -> group players except self in NFGUID
+ *                  order (NFCSceneGroupInfo::mxPlayerList, std::map), private&&!upload
+ *                  -> self)
+ * Dirty diff: per tick, the Set events of one (entity, property) are coalesced
+ * to (first old, last new) and dropped when the bits are unchanged.
+ *
+ * Usage: nf_oracle <workload.nfio> <out.nfio>
+ * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/nfgpu.h"
+#include "nfio.h"
+
+typedef struct {
+    uint8_t present, forever, rm_mark;
+    int64_t next, start;
+    int32_t remain, all;
+    float interval;
+} sched_t;
+
+typedef struct {
+    int32_t obj, pid;
+    uint64_t old_bits, new_bits;
+    int64_t seq;
+} setlog_t;
+
+typedef struct {
+    int32_t obj;
+    uint32_t rrc;
+    uint64_t old_bits, new_bits;
+    int64_t seq;
+} rsetlog_t;
+
+/* ---------------- world ---------------- */
+static int64_t N, NI, NF, NC, NK, NR;
+static int64_t *I;  /* [NI][N] */
+static double *F;   /* [NF][N] */
+static uint8_t *pflags; /* [NC][NI+NF] */
+static int32_t rec_rows[NFK_MAX_RECORDS], rec_cols[NFK_MAX_RECORDS];
+static uint8_t rec_ctype[NFK_MAX_RECORDS][NFK_MAX_REC_COLS];
+static uint8_t *rflags; /* [NC][NR] */
+static uint64_t *rcells[NFK_MAX_RECORDS]; /* [N][cols][rows] */
+static uint64_t *rused[NFK_MAX_RECORDS];  /* [N] */
+static nfk_op ops[NFK_MAX_KINDS][NFK_MAX_OPS];
+static int32_t nops[NFK_MAX_KINDS];
+static int64_t *ghead, *gdata;
+static int32_t *scene, *group;
+static uint8_t *cls, *isplayer;
+static sched_t *S; /* [N][NK] */
+static int32_t *pend_rm_kind; /* [N], -2 = none, -1 = name not a kind */
+static int64_t *orank;         /* canonical (scene, group, guid) rank of each object */
+
+static setlog_t *slog;
+static int64_t nslog, capslog, seq;
+static rsetlog_t *rlog;
+static int64_t nrlog, caprlog;
+
+static int32_t *fired_obj, *fired_kind, *fired_rem;
+static int64_t nfired, capfired;
+
+static void die(const char* m) {
+    fprintf(stderr, "nf_oracle: %s\n", m);
+    exit(2);
+}
+
+static uint64_t dbits(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
+static double bitsd(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
+
+static void log_set(int32_t obj, int32_t pid, uint64_t o, uint64_t n) {
+    if (nslog == capslog) {
+        capslog = capslog ? capslog * 2 : 4096;
+        slog = (setlog_t*)realloc(slog, capslog * sizeof(setlog_t));
+    }
+    setlog_t e = {obj, pid, o, n, seq++};
+    slog[nslog++] = e;
+}
+
+static void log_rset(int32_t obj, uint32_t rrc, uint64_t o, uint64_t n) {
+    if (nrlog == caprlog) {
+        caprlog = caprlog ? caprlog * 2 : 4096;
+        rlog = (rsetlog_t*)realloc(rlog, caprlog * sizeof(rsetlog_t));
+    }
+    rsetlog_t e = {obj, rrc, o, n, seq++};
+    rlog[nrlog++] = e;
+}
+
+/* NFCProperty::SetInt (PR:254): no event when the value is unchanged; a
+ * never-set property reads 0, so "null" behaves as 0. */
+static void set_int(int32_t obj, int32_t pid, int64_t v) {
+    int64_t cur = I[pid * N + obj];
+    if (v == cur) return;
+    I[pid * N + obj] = v;
+    log_set(obj, pid, (uint64_t)cur, (uint64_t)v);
+}
+
+/* NFCProperty::SetFloat (PR:295): IsZeroDouble(v - cur) with eps 1e-15. */
+static void set_flt(int32_t obj, int32_t pid, double v) {
+    double cur = F[(pid - NI) * N + obj];
+    if (fabs(v - cur) <= 1e-15) return;
+    F[(pid - NI) * N + obj] = v;
+    log_set(obj, pid, dbits(cur), dbits(v));
+}
+
+static uint64_t* cell(int r, int32_t obj, int row, int col) {
+    return &rcells[r][((int64_t)obj * rec_cols[r] + col) * rec_rows[r] + row];
+}
+
+/* NFCRecord::SetInt (RC:182) */
+static void set_rint(int r, int32_t obj, int row, int col, int64_t v) {
+    uint64_t* c = cell(r, obj, row, col);
+    int64_t cur = (int64_t)*c;
+    if (v == cur) return;
+    *c = (uint64_t)v;
+    log_rset(obj, ((uint32_t)r << 16) | ((uint32_t)row << 8) | (uint32_t)col, (uint64_t)cur, (uint64_t)v);
+}
+
+/* NFCRecord::SetFloat (RC:243) with TData::operator== (NFIDataList.h:106): |v-cur| < 0.001 is "equal" */
+static void set_rflt(int r, int32_t obj, int row, int col, double v) {
+    uint64_t* c = cell(r, obj, row, col);
+    double cur = bitsd(*c);
+    double d = v - cur;
+    if (d < 0.001 && d > -0.001) return;
+    *c = dbits(v);
+    log_rset(obj, ((uint32_t)r << 16) | ((uint32_t)row << 8) | (uint32_t)col, dbits(cur), dbits(v));
+}
+
+static int64_t iget(int32_t obj, int64_t pid) { return I[pid * N + obj]; }
+static double fget(int32_t obj, int64_t pid) { return F[(pid - NI) * N + obj]; }
+
+static int64_t opnd(int32_t obj, const nfk_op* op, int bit, int64_t x) {
+    return (op->flags & bit) ? iget(obj, x) : x;
+}
+
+/* one heartbeat callback: the kind's program, every op a Get + Set */
+static void run_program(int32_t obj, int kind) {
+    for (int i = 0; i < nops[kind]; i++) {
+        const nfk_op* op = &ops[kind][i];
+        switch (op->code) {
+        case NFK_OP_IADD_CLAMP: {
+            int64_t cur = iget(obj, op->dst);
+            int64_t a = opnd(obj, op, NFK_A_PROP, op->a);
+            int64_t lo = opnd(obj, op, NFK_LO_PROP, op->b);
+            int64_t hi = opnd(obj, op, NFK_HI_PROP, op->c);
+            int64_t v = (int64_t)((uint64_t)cur + (uint64_t)a);
+            if (v < lo) v = lo;
+            if (v > hi) v = hi;
+            set_int(obj, op->dst, v);
+            break;
+        }
+        case NFK_OP_FLERP: {
+            double x = fget(obj, op->dst);
+            double t = fget(obj, op->a);
+            double k = bitsd((uint64_t)op->b);
+            double d = t - x;
+            double m = d * k;
+            set_flt(obj, op->dst, x + m);
+            break;
+        }
+        case NFK_OP_FAFFINE: {
+            double x = fget(obj, op->dst);
+            double m = x * bitsd((uint64_t)op->a);
+            set_flt(obj, op->dst, m + bitsd((uint64_t)op->b));
+            break;
+        }
+        case NFK_OP_RIADD_CLAMP: {
+            int r = op->dst >> 8, col = op->dst & 255;
+            for (int row = 0; row < rec_rows[r]; row++) {
+                if (!((rused[r][obj] >> row) & 1)) continue;
+                int64_t cur = (int64_t)*cell(r, obj, row, col);
+                int64_t v = (int64_t)((uint64_t)cur + (uint64_t)op->a);
+                if (v < op->b) v = op->b;
+                if (v > op->c) v = op->c;
+                set_rint(r, obj, row, col, v);
+            }
+            break;
+        }
+        case NFK_OP_RFAFFINE: {
+            int r = op->dst >> 8, col = op->dst & 255;
+            for (int row = 0; row < rec_rows[r]; row++) {
+                if (!((rused[r][obj] >> row) & 1)) continue;
+                double x = bitsd(*cell(r, obj, row, col));
+                double m = x * bitsd((uint64_t)op->a);
+                set_rflt(r, obj, row, col, m + bitsd((uint64_t)op->b));
+            }
+            break;
+        }
+        default:
+            break;
+        }
+    }
+}
+
+static void log_fired(int32_t obj, int32_t kind, int32_t rem) {
+    if (nfired == capfired) {
+        capfired = capfired ? capfired * 2 : 4096;
+        fired_obj = (int32_t*)realloc(fired_obj, capfired * 4);
+        fired_kind = (int32_t*)realloc(fired_kind, capfired * 4);
+        fired_rem = (int32_t*)realloc(fired_rem, capfired * 4);
+    }
+    fired_obj[nfired] = obj;
+    fired_kind[nfired] = kind;
+    fired_rem[nfired] = rem;
+    nfired++;
+}
+
+/* NFCScheduleModule::Execute (SM:45-110), object part.  Object iteration
+ * order does not change state (callbacks only touch their own object). */
+static void sched_execute(int64_t now) {
+    for (int32_t o = 0; o < N; o++) {
+        /* mObjectRemoveList is std::map<NFGUID, name>: a RemoveSchedule(self, name)
+         * queued before this Execute owns the key, later inserts for self fail. */
+        int taken = pend_rm_kind[o] != -2;
+        for (int k = 0; k < NK; k++) {
+            sched_t* s = &S[(int64_t)o * NK + k];
+            if (!s->present) continue;
+            if (now > s->next) {
+                if (s->remain > 0 || s->forever) {
+                    s->remain--;
+                    log_fired(o, k, s->remain);
+                    run_program(o, k);
+                    if (s->remain <= 0 && !s->forever) {
+                        if (!taken) {
+                            s->rm_mark = 1;
+                            taken = 1;
+                        }
+                    } else {
+                        int64_t step = (int64_t)(s->interval * 1000.0f);
+                        int32_t done = (int32_t)((uint32_t)s->all - (uint32_t)s->remain);
+                        s->next = s->start + step * (int64_t)done;
+                    }
+                }
+            }
+        }
+    }
+}
+
+/* ---------------- canonical ordering ---------------- */
+static int cmp_obj_key(const void* a, const void* b) {
+    int32_t x = *(const int32_t*)a, y = *(const int32_t*)b;
+    if (scene[x] != scene[y]) return scene[x] < scene[y] ? -1 : 1;
+    if (group[x] != group[y]) return group[x] < group[y] ? -1 : 1;
+    if (ghead[x] != ghead[y]) return ghead[x] < ghead[y] ? -1 : 1;
+    if (gdata[x] != gdata[y]) return gdata[x] < gdata[y] ? -1 : 1;
+    return 0;
+}
+
+static int cmp_slog(const void* a, const void* b) {
+    const setlog_t *x = (const setlog_t*)a, *y = (const setlog_t*)b;
+    if (orank[x->obj] != orank[y->obj]) return orank[x->obj] < orank[y->obj] ? -1 : 1;
+    if (x->pid != y->pid) return x->pid < y->pid ? -1 : 1;
+    return x->seq < y->seq ? -1 : (x->seq > y->seq);
+}
+
+static int cmp_rlog(const void* a, const void* b) {
+    const rsetlog_t *x = (const rsetlog_t*)a, *y = (const rsetlog_t*)b;
+    if (orank[x->obj] != orank[y->obj]) return orank[x->obj] < orank[y->obj] ? -1 : 1;
+    if (x->rrc != y->rrc) return x->rrc < y->rrc ? -1 : 1;
+    return x->seq < y->seq ? -1 : (x->seq > y->seq);
+}
+
+typedef struct { int32_t obj, kind, rem; } fired_t;
+static int cmp_fired(const void* a, const void* b) {
+    const fired_t *x = (const fired_t*)a, *y = (const fired_t*)b;
+    if (orank[x->obj] != orank[y->obj]) return orank[x->obj] < orank[y->obj] ? -1 : 1;
+    return x->kind < y->kind ? -1 : (x->kind > y->kind);
+}
+
+/* players of each (scene, group) in NFGUID order: segment table over sorted objects */
+static int32_t* sorted_objs;      /* objects in canonical order */
+static int64_t* seg_begin_of_obj; /* index in sorted_objs where the object's segment begins */
+static int64_t* seg_end_of_obj;
+
+static void put_tick(nfio_writer* w, int t, const char* pfx, const char* nm, uint32_t code,
+                     const void* d, uint64_t n, uint64_t es) {
+    char name[32];
+    snprintf(name, sizeof name, "%s_t%d_%s", pfx, t, nm);
+    nfio_put1(w, name, code, d, n, es);
+}
+
+int main(int argc, char** argv) {
+    if (argc != 3) die("usage: nf_oracle <workload.nfio> <out.nfio>");
+    nfio_file wf;
+    if (nfio_read(argv[1], &wf) != 0) die("cannot read workload");
+#define GET(name) ({ nfio_arr* _a = nfio_get(&wf, name); if (!_a) die("missing " name); _a; })
+    int64_t* cfg = (int64_t*)GET("cfg")->data;
+    N = cfg[0]; NI = cfg[1]; NF = cfg[2]; NC = cfg[3]; NK = cfg[4]; NR = cfg[5];
+    int64_t NS = cfg[6], NT = cfg[7];
+    int64_t NP = NI + NF;
+    pflags = (uint8_t*)GET("prop_flags")->data;
+    if (NR > 0) {
+        int32_t* rr = (int32_t*)GET("rec_rows")->data;
+        int32_t* rcl = (int32_t*)GET("rec_cols")->data;
+        uint8_t* rct = (uint8_t*)GET("rec_ctype")->data;
+        rflags = (uint8_t*)GET("rec_flags")->data;
+        for (int r = 0; r < NR; r++) {
+            rec_rows[r] = rr[r];
+            rec_cols[r] = rcl[r];
+            memcpy(rec_ctype[r], rct + r * NFK_MAX_REC_COLS, NFK_MAX_REC_COLS);
+            char nm[32];
+            snprintf(nm, sizeof nm, "rec%d_cells", r);
+            nfio_arr* a = nfio_get(&wf, nm);
+            if (!a) die("missing rec cells");
+            rcells[r] = (uint64_t*)a->data;
+            snprintf(nm, sizeof nm, "rec%d_used", r);
+            a = nfio_get(&wf, nm);
+            if (!a) die("missing rec used");
+            rused[r] = (uint64_t*)a->data;
+        }
+    }
+    memcpy(ops, GET("ops")->data, NK * NFK_MAX_OPS * sizeof(nfk_op));
+    memcpy(nops, GET("n_ops")->data, NK * 4);
+    ghead = (int64_t*)GET("guid_head")->data;
+    gdata = (int64_t*)GET("guid_data")->data;
+    scene = (int32_t*)GET("scene")->data;
+    group = (int32_t*)GET("group")->data;
+    cls = (uint8_t*)GET("cls")->data;
+    isplayer = (uint8_t*)GET("is_player")->data;
+    I = (int64_t*)GET("init_i")->data;
+    F = (double*)GET("init_f")->data;
+    int32_t* s_obj = (int32_t*)GET("s_obj")->data;
+    int32_t* s_kind = (int32_t*)GET("s_kind")->data;
+    float* s_interval = (float*)GET("s_interval")->data;
+    int32_t* s_count = (int32_t*)GET("s_count")->data;
+    int64_t* s_time = (int64_t*)GET("s_time")->data;
+    int64_t* tick_time = (int64_t*)GET("tick_time")->data;
+    nfio_arr* xa = GET("x_tick");
+    int64_t NX = (int64_t)xa->shape[0];
+    int32_t* x_tick = (int32_t*)xa->data;
+    int32_t* x_obj = (int32_t*)GET("x_obj")->data;
+    int32_t* x_pid = (int32_t*)GET("x_pid")->data;
+    uint64_t* x_bits = (uint64_t*)GET("x_bits")->data;
+    nfio_arr* ha = GET("h_tick");
+    int64_t NH = (int64_t)ha->shape[0];
+    int32_t* h_tick = (int32_t*)ha->data;
+    int32_t* h_op = (int32_t*)GET("h_op")->data;
+    int32_t* h_obj = (int32_t*)GET("h_obj")->data;
+    int32_t* h_kind = (int32_t*)GET("h_kind")->data;
+    float* h_interval = (float*)GET("h_interval")->data;
+    int32_t* h_count = (int32_t*)GET("h_count")->data;
+    int64_t* h_time = (int64_t*)GET("h_time")->data;
+
+    S = (sched_t*)calloc(N * NK, sizeof(sched_t));
+    pend_rm_kind = (int32_t*)malloc(N * 4);
+    for (int64_t o = 0; o < N; o++) pend_rm_kind[o] = -2;
+
+    /* canonical rank */
+    sorted_objs = (int32_t*)malloc(N * 4);
+    for (int32_t o = 0; o < N; o++) sorted_objs[o] = o;
+    qsort(sorted_objs, N, 4, cmp_obj_key);
+    orank = (int64_t*)malloc(N * 8);
+    seg_begin_of_obj = (int64_t*)malloc(N * 8);
+    seg_end_of_obj = (int64_t*)malloc(N * 8);
+    for (int64_t i = 0; i < N; i++) orank[sorted_objs[i]] = i;
+    for (int64_t i = 0; i < N;) {
+        int64_t j = i;
+        while (j < N && scene[sorted_objs[j]] == scene[sorted_objs[i]] && group[sorted_objs[j]] == group[sorted_objs[i]]) j++;
+        for (int64_t k = i; k < j; k++) {
+            seg_begin_of_obj[sorted_objs[k]] = i;
+            seg_end_of_obj[sorted_objs[k]] = j;
+        }
+        i = j;
+    }
+
+    /* pending schedule adds: the initial AddSchedule calls happen before tick 0 */
+    typedef struct { int32_t obj, kind, count; float interval; int64_t time; } addreq_t;
+    addreq_t* adds = (addreq_t*)malloc((NS + NH + 1) * sizeof(addreq_t));
+    int64_t nadds = 0;
+    for (int64_t i = 0; i < NS; i++) {
+        addreq_t a = {s_obj[i], s_kind[i], s_count[i], s_interval[i], s_time[i]};
+        adds[nadds++] = a;
+    }
+
+    nfio_writer w;
+    if (nfio_wopen(&w, argv[2]) != 0) die("cannot open output");
+    int64_t xi = 0, hi = 0;
+
+    for (int t = 0; t < NT; t++) {
+        int64_t now = tick_time[t];
+        nslog = 0;
+        nrlog = 0;
+        nfired = 0;
+        seq = 0;
+        /* host calls made between the previous Execute and this one */
+        while (hi < NH && h_tick[hi] == t) {
+            int32_t o = h_obj[hi];
+            if (h_op[hi] == 1) {
+                addreq_t a = {o, h_kind[hi], h_count[hi], h_interval[hi], h_time[hi]};
+                adds[nadds++] = a;
+            } else if (h_op[hi] == 2) {
+                if (pend_rm_kind[o] == -2) pend_rm_kind[o] = h_kind[hi];
+            } else if (h_op[hi] == 3) {
+                /* RemoveSchedule(self): immediate erase of the object's map (SM:260) */
+                for (int k = 0; k < NK; k++) S[(int64_t)o * NK + k].present = 0;
+            }
+            hi++;
+        }
+        /* SetProperty* calls made before this Execute, in call order */
+        while (xi < NX && x_tick[xi] == t) {
+            int32_t pid = x_pid[xi];
+            if (pid < NI) set_int(x_obj[xi], pid, (int64_t)x_bits[xi]);
+            else set_flt(x_obj[xi], pid, bitsd(x_bits[xi]));
+            xi++;
+        }
+        sched_execute(now);
+        /* remove list (SM:82-96) */
+        for (int64_t o = 0; o < N; o++) {
+            if (pend_rm_kind[o] >= 0) S[o * NK + pend_rm_kind[o]].present = 0;
+            pend_rm_kind[o] = -2;
+            for (int k = 0; k < NK; k++)
+                if (S[o * NK + k].rm_mark) {
+                    S[o * NK + k].rm_mark = 0;
+                    S[o * NK + k].present = 0;
+                }
+        }
+        /* add list (SM:99-117): AddSchedule(SM:236) fields; an existing name wins */
+        for (int64_t i = 0; i < nadds; i++) {
+            sched_t* s = &S[(int64_t)adds[i].obj * NK + adds[i].kind];
+            if (s->present) continue;
+            memset(s, 0, sizeof *s);
+            s->present = 1;
+            s->interval = adds[i].interval;
+            s->next = adds[i].time + (int64_t)(adds[i].interval * 1000.0f);
+            s->start = adds[i].time;
+            s->remain = adds[i].count;
+            s->all = adds[i].count;
+            s->forever = adds[i].count < 0;
+        }
+        nadds = 0;
+
+        /* coalesce property set events */
+        qsort(slog, nslog, sizeof(setlog_t), cmp_slog);
+        int64_t ne = 0;
+        int32_t* ev_obj = (int32_t*)malloc((nslog + 1) * 4);
+        int32_t* ev_pid = (int32_t*)malloc((nslog + 1) * 4);
+        uint64_t* ev_old = (uint64_t*)malloc((nslog + 1) * 8);
+        uint64_t* ev_new = (uint64_t*)malloc((nslog + 1) * 8);
+        for (int64_t i = 0; i < nslog;) {
+            int64_t j = i;
+            while (j < nslog && slog[j].obj == slog[i].obj && slog[j].pid == slog[i].pid) j++;
+            if (slog[i].old_bits != slog[j - 1].new_bits) {
+                ev_obj[ne] = slog[i].obj;
+                ev_pid[ne] = slog[i].pid;
+                ev_old[ne] = slog[i].old_bits;
+                ev_new[ne] = slog[j - 1].new_bits;
+                ne++;
+            }
+            i = j;
+        }
+        qsort(rlog, nrlog, sizeof(rsetlog_t), cmp_rlog);
+        int64_t nre = 0;
+        int32_t* re_obj = (int32_t*)malloc((nrlog + 1) * 4);
+        uint32_t* re_rrc = (uint32_t*)malloc((nrlog + 1) * 4);
+        uint64_t* re_old = (uint64_t*)malloc((nrlog + 1) * 8);
+        uint64_t* re_new = (uint64_t*)malloc((nrlog + 1) * 8);
+        for (int64_t i = 0; i < nrlog;) {
+            int64_t j = i;
+            while (j < nrlog && rlog[j].obj == rlog[i].obj && rlog[j].rrc == rlog[i].rrc) j++;
+            if (rlog[i].old_bits != rlog[j - 1].new_bits) {
+                re_obj[nre] = rlog[i].obj;
+                re_rrc[nre] = rlog[i].rrc;
+                re_old[nre] = rlog[i].old_bits;
+                re_new[nre] = rlog[j - 1].new_bits;
+                nre++;
+            }
+            i = j;
+        }
+        /* fired list */
+        fired_t* fl = (fired_t*)malloc((nfired + 1) * sizeof(fired_t));
+        for (int64_t i = 0; i < nfired; i++) {
+            fl[i].obj = fired_obj[i];
+            fl[i].kind = fired_kind[i];
+            fl[i].rem = fired_rem[i];
+        }
+        qsort(fl, nfired, sizeof(fired_t), cmp_fired);
+        int32_t* fo = (int32_t*)malloc((nfired + 1) * 4);
+        int32_t* fk = (int32_t*)malloc((nfired + 1) * 4);
+        int32_t* fr = (int32_t*)malloc((nfired + 1) * 4);
+        for (int64_t i = 0; i < nfired; i++) {
+            fo[i] = fl[i].obj;
+            fk[i] = fl[i].kind;
+            fr[i] = fl[i].rem;
+        }
+        /* fan-out over [prop events ++ record events] (AOI:531-593) */
+        uint32_t* moff = (uint32_t*)malloc((ne + nre + 1) * 4);
+        int64_t cap = 1024, nm = 0;
+        int32_t* mr = (int32_t*)malloc(cap * 4);
+        for (int64_t e = 0; e < ne + nre; e++) {
+            moff[e] = (uint32_t)nm;
+            int32_t o = e < ne ? ev_obj[e] : re_obj[e - ne];
+            uint8_t fl8 = e < ne ? pflags[cls[o] * NP + ev_pid[e]] : rflags[cls[o] * NR + (re_rrc[e - ne] >> 16)];
+            if (fl8 & NFK_PUBLIC) {
+                for (int64_t k = seg_begin_of_obj[o]; k < seg_end_of_obj[o]; k++) {
+                    int32_t p = sorted_objs[k];
+                    if (!isplayer[p] || p == o) continue;
+                    if (nm == cap) {
+                        cap *= 2;
+                        mr = (int32_t*)realloc(mr, cap * 4);
+                    }
+                    mr[nm++] = p;
+                }
+            } else if ((fl8 & NFK_PRIVATE) && !(fl8 & NFK_UPLOAD)) {
+                if (nm == cap) {
+                    cap *= 2;
+                    mr = (int32_t*)realloc(mr, cap * 4);
+                }
+                mr[nm++] = o;
+            }
+        }
+        moff[ne + nre] = (uint32_t)nm;
+
+        put_tick(&w, t, "ev", "obj", NFIO_I32, ev_obj, ne, 4);
+        put_tick(&w, t, "ev", "pid", NFIO_I32, ev_pid, ne, 4);
+        put_tick(&w, t, "ev", "old", NFIO_U64, ev_old, ne, 8);
+        put_tick(&w, t, "ev", "new", NFIO_U64, ev_new, ne, 8);
+        put_tick(&w, t, "re", "obj", NFIO_I32, re_obj, nre, 4);
+        put_tick(&w, t, "re", "rrc", NFIO_U32, re_rrc, nre, 4);
+        put_tick(&w, t, "re", "old", NFIO_U64, re_old, nre, 8);
+        put_tick(&w, t, "re", "new", NFIO_U64, re_new, nre, 8);
+        put_tick(&w, t, "fi", "obj", NFIO_I32, fo, nfired, 4);
+        put_tick(&w, t, "fi", "kind", NFIO_I32, fk, nfired, 4);
+        put_tick(&w, t, "fi", "rem", NFIO_I32, fr, nfired, 4);
+        put_tick(&w, t, "mo", "off", NFIO_U32, moff, ne + nre + 1, 4);
+        put_tick(&w, t, "mr", "obj", NFIO_I32, mr, nm, 4);
+        free(ev_obj); free(ev_pid); free(ev_old); free(ev_new);
+        free(re_obj); free(re_rrc); free(re_old); free(re_new);
+        free(fl); free(fo); free(fk); free(fr); free(moff); free(mr);
+    }
+
+    /* final state */
+    {
+        uint64_t sh[2] = {(uint64_t)NI, (uint64_t)N};
+        nfio_put(&w, "final_i", NFIO_I64, 2, sh, I, NI * N * 8);
+        uint64_t sf[2] = {(uint64_t)NF, (uint64_t)N};
+        nfio_put(&w, "final_f", NFIO_F64, 2, sf, F, NF * N * 8);
+        for (int r = 0; r < NR; r++) {
+            char nm[32];
+            snprintf(nm, sizeof nm, "final_rec%d", r);
+            uint64_t sr[3] = {(uint64_t)N, (uint64_t)rec_cols[r], (uint64_t)rec_rows[r]};
+            nfio_put(&w, nm, NFIO_U64, 3, sr, rcells[r], N * rec_cols[r] * rec_rows[r] * 8);
+        }
+        int64_t* sn = (int64_t*)malloc(NK * N * 8);
+        int32_t* sr = (int32_t*)malloc(NK * N * 4);
+        uint8_t* sp = (uint8_t*)malloc(NK * N);
+        for (int64_t k = 0; k < NK; k++)
+            for (int64_t o = 0; o < N; o++) {
+                sched_t* s = &S[o * NK + k];
+                sp[k * N + o] = s->present;
+                sn[k * N + o] = s->present ? s->next : 0;
+                sr[k * N + o] = s->present ? s->remain : 0;
+            }
+        uint64_t ss[2] = {(uint64_t)NK, (uint64_t)N};
+        nfio_put(&w, "final_s_next", NFIO_I64, 2, ss, sn, NK * N * 8);
+        nfio_put(&w, "final_s_remain", NFIO_I32, 2, ss, sr, NK * N * 4);
+        nfio_put(&w, "final_s_present", NFIO_U8, 2, ss, sp, NK * N);
+        free(sn); free(sr); free(sp);
+    }
+    nfio_wclose(&w);
+    nfio_free(&wf);
+    return 0;
+}

@@ -1,0 +1,112 @@
+/* NFIO container reader/writer for the CPU checkers (test infrastructure).
+ * Format: see noahgameframe_amd/nfio.py.  Header-only, C99 and C++ compatible. */
+#ifndef NFIO_H
+#define NFIO_H
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+enum { NFIO_I8 = 1, NFIO_U8, NFIO_I16, NFIO_U16, NFIO_I32, NFIO_U32, NFIO_I64, NFIO_U64, NFIO_F32, NFIO_F64 };
+
+typedef struct {
+    char name[25];
+    uint32_t code, ndim;
+    uint64_t shape[4];
+    uint64_t nbytes;
+    void* data;
+} nfio_arr;
+
+typedef struct {
+    int count, cap;
+    nfio_arr* a;
+} nfio_file;
+
+static inline int nfio_read(const char* path, nfio_file* f) {
+    FILE* fp = fopen(path, "rb");
+    if (!fp) return -1;
+    char magic[8];
+    uint32_t count = 0;
+    if (fread(magic, 1, 8, fp) != 8 || memcmp(magic, "NFIO0001", 8) != 0) { fclose(fp); return -2; }
+    if (fread(&count, 4, 1, fp) != 1) { fclose(fp); return -3; }
+    f->count = (int)count;
+    f->cap = (int)count;
+    f->a = (nfio_arr*)calloc(count ? count : 1, sizeof(nfio_arr));
+    for (uint32_t i = 0; i < count; i++) {
+        nfio_arr* a = &f->a[i];
+        char nm[24];
+        if (fread(nm, 1, 24, fp) != 24) { fclose(fp); return -4; }
+        memcpy(a->name, nm, 24);
+        a->name[24] = 0;
+        if (fread(&a->code, 4, 1, fp) != 1 || fread(&a->ndim, 4, 1, fp) != 1 ||
+            fread(a->shape, 8, 4, fp) != 4 || fread(&a->nbytes, 8, 1, fp) != 1) { fclose(fp); return -5; }
+        uint64_t padded = a->nbytes + ((8 - (a->nbytes % 8)) % 8);
+        a->data = malloc(padded ? padded : 8);
+        if (padded && fread(a->data, 1, padded, fp) != padded) { fclose(fp); return -6; }
+    }
+    fclose(fp);
+    return 0;
+}
+
+static inline nfio_arr* nfio_get(nfio_file* f, const char* name) {
+    for (int i = 0; i < f->count; i++)
+        if (strcmp(f->a[i].name, name) == 0) return &f->a[i];
+    return NULL;
+}
+
+static inline void nfio_free(nfio_file* f) {
+    for (int i = 0; i < f->count; i++) free(f->a[i].data);
+    free(f->a);
+    f->a = NULL;
+    f->count = f->cap = 0;
+}
+
+/* writer: arrays are streamed straight to disk */
+typedef struct {
+    FILE* fp;
+    long count_pos;
+    uint32_t count;
+} nfio_writer;
+
+static inline int nfio_wopen(nfio_writer* w, const char* path) {
+    w->fp = fopen(path, "wb");
+    if (!w->fp) return -1;
+    fwrite("NFIO0001", 1, 8, w->fp);
+    w->count_pos = ftell(w->fp);
+    w->count = 0;
+    fwrite(&w->count, 4, 1, w->fp);
+    return 0;
+}
+
+static inline void nfio_put(nfio_writer* w, const char* name, uint32_t code, uint32_t ndim,
+                            const uint64_t* shape, const void* data, uint64_t nbytes) {
+    char nm[24];
+    memset(nm, 0, 24);
+    strncpy(nm, name, 23);
+    uint64_t sh[4] = {1, 1, 1, 1};
+    for (uint32_t i = 0; i < ndim; i++) sh[i] = shape[i];
+    fwrite(nm, 1, 24, w->fp);
+    fwrite(&code, 4, 1, w->fp);
+    fwrite(&ndim, 4, 1, w->fp);
+    fwrite(sh, 8, 4, w->fp);
+    fwrite(&nbytes, 8, 1, w->fp);
+    if (nbytes) fwrite(data, 1, nbytes, w->fp);
+    uint64_t pad = (8 - (nbytes % 8)) % 8;
+    static const char z[8] = {0};
+    if (pad) fwrite(z, 1, pad, w->fp);
+    w->count++;
+}
+
+static inline void nfio_put1(nfio_writer* w, const char* name, uint32_t code, const void* data,
+                             uint64_t n, uint64_t elem) {
+    uint64_t shape[1] = {n};
+    nfio_put(w, name, code, 1, shape, data, n * elem);
+}
+
+static inline void nfio_wclose(nfio_writer* w) {
+    fseek(w->fp, w->count_pos, SEEK_SET);
+    fwrite(&w->count, 4, 1, w->fp);
+    fclose(w->fp);
+    w->fp = NULL;
+}
+#endif

@@ -1,0 +1,41 @@
+"""Regenerate the golden fixtures: synthetic workloads run through the REFERENCE's own
+classes (oracle/_ref/nf_ref_harness, built from /root/reference by oracle/build_ref.sh).
+Each fixture = <name>.workload.nfio (inputs) + <name>.expected.nfio (reference outputs).
+
+    python tests/golden/gen_golden.py
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from noahgameframe_amd import nfio, workload  # noqa: E402
+
+FIXTURES = {
+    # property path: heartbeats, SetProperty calls (incl. duplicates), Add/RemoveSchedule calls
+    "props": dict(n_obj=600, n_scenes=2, groups_per_scene=6, players_per_group=3, n_ticks=10, seed=101,
+                  ext_frac=0.08, host_ops=True),
+    # record path (int cooldown column; see DESIGN.md for the reference's f64 record bug)
+    "records": dict(n_obj=300, n_scenes=1, groups_per_scene=5, players_per_group=4, n_ticks=8, seed=202,
+                    records=True, rec_rows=16, rec_float_op=False, ext_frac=0.05),
+    # one group, every object a player, no between-frame calls
+    "allplayers": dict(n_obj=64, n_scenes=1, groups_per_scene=1, players_per_group=64, n_ticks=12, seed=303,
+                       ext_frac=0.0, host_ops=False),
+}
+
+
+def main():
+    exe = os.path.join(ROOT, "oracle", "_ref", "nf_ref_harness")
+    for name, kw in FIXTURES.items():
+        w = workload.make_world(**kw)
+        wp = os.path.join(HERE, f"{name}.workload.nfio")
+        ep = os.path.join(HERE, f"{name}.expected.nfio")
+        nfio.write(wp, w)
+        subprocess.run([exe, wp, ep], check=True)
+        print(name, os.path.getsize(wp), os.path.getsize(ep))
+
+
+if __name__ == "__main__":
+    main()
