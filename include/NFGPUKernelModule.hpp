@@ -1,0 +1,162 @@
+// NFGPUKernelModule.hpp — C++ host plugin over the nfgpu C-ABI, with the reference's
+// plugin API names for the tick path, so a NoahGameFrame game server swaps it in for
+// NFCKernelModule + NFCScheduleModule + the NFCSceneAOIModule property fan-out.
+//
+// Reference interfaces mirrored (flyish/NoahGameFrame):
+//   NFComm/NFPluginModule/NFIKernelModule.h     CreateScene, CreateObject, SetPropertyInt/Float,
+//                                               GetPropertyInt/Float, RegisterCommonPropertyEvent,
+//                                               Execute (NFCKernelModule.cpp:70)
+//   NFComm/NFPluginModule/NFIScheduleModule.h   AddSchedule(self, name, cb, fTime, nCount),
+//                                               RemoveSchedule(self[, name]), ExistSchedule
+//   NFComm/NFPluginModule/NFISceneAOIModule.h   AddPropertyEventCallBack / AddRecordEventCallBack
+//                                               (the recipient-list events, AOI.cpp:703-727)
+//   NFComm/NFPluginModule/NFIModule.h           Init / AfterInit / Execute / BeforeShut / Shut
+//
+// Differences a plugin author must know:
+//   * A heartbeat's state change is a device effect program (nfk_op list) registered once per
+//     schedule name; the C++ functor passed to AddSchedule still runs, after the device frame,
+//     with the reference's arguments (self, name, fTime, nCount).
+//   * SetProperty* calls are queued and applied at the start of the next Execute, in call order,
+//     through the reference's change predicates; callbacks see coalesced (first old, last new)
+//     events once per frame, in (scene, group, guid, property) order.
+//   * String / Vector properties stay host-side (not on the frame path).
+#pragma once
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "nfgpu.h"
+
+namespace nfgpu {
+
+struct NFGUID {
+    int64_t nData64 = 0;
+    int64_t nHead64 = 0;
+    NFGUID() = default;
+    NFGUID(int64_t head, int64_t data) : nData64(data), nHead64(head) {}
+    bool IsNull() const { return nData64 == 0 && nHead64 == 0; }
+    bool operator==(const NFGUID& o) const { return nData64 == o.nData64 && nHead64 == o.nHead64; }
+    bool operator!=(const NFGUID& o) const { return !(*this == o); }
+    bool operator<(const NFGUID& o) const {  // NFGUID.h:83
+        return nHead64 == o.nHead64 ? nData64 < o.nData64 : nHead64 < o.nHead64;
+    }
+};
+
+enum TDATA_TYPE { TDATA_UNKNOWN, TDATA_INT, TDATA_FLOAT, TDATA_STRING, TDATA_OBJECT };
+
+struct TData {
+    TDATA_TYPE type = TDATA_UNKNOWN;
+    int64_t i = 0;
+    double f = 0.0;
+    TDATA_TYPE GetType() const { return type; }
+    int64_t GetInt() const { return type == TDATA_INT ? i : 0; }
+    double GetFloat() const { return type == TDATA_FLOAT ? f : 0.0; }
+};
+
+struct RECORD_EVENT_DATA {
+    enum RecordOptype { Add = 0, Del, Swap, Create, Update, Cleared, Sort, Cover, UNKNOW };
+    RecordOptype nOpType = Update;
+    int nRow = 0, nCol = 0;
+    std::string strRecordName;
+};
+
+using PROPERTY_EVENT_FUNCTOR = std::function<int(const NFGUID&, const std::string&, const TData&, const TData&)>;
+using RECORD_EVENT_FUNCTOR =
+    std::function<int(const NFGUID&, const RECORD_EVENT_DATA&, const TData&, const TData&)>;
+using OBJECT_SCHEDULE_FUNCTOR = std::function<int(const NFGUID&, const std::string&, const float, const int)>;
+using PROPERTY_SINGLE_EVENT_FUNCTOR = std::function<int(const NFGUID&, const std::string&, const TData&,
+                                                        const TData&, const std::vector<NFGUID>&)>;
+using RECORD_SINGLE_EVENT_FUNCTOR = std::function<int(const NFGUID&, const std::string&, const RECORD_EVENT_DATA&,
+                                                      const TData&, const TData&, const std::vector<NFGUID>&)>;
+
+class NFGPUKernelModule {
+public:
+    struct PropertyDef { std::string name; TDATA_TYPE type; };
+    struct ClassDef {
+        std::string name;
+        std::map<std::string, uint8_t> prop_flags;   // NFK_PUBLIC | NFK_PRIVATE | NFK_UPLOAD
+        std::map<std::string, uint8_t> record_flags;
+    };
+    struct RecordDef { std::string name; int rows; std::vector<TDATA_TYPE> cols; };
+    struct HeartBeatDef { std::string name; std::vector<nfk_op> ops; };
+
+    // ---- schema (what NFIClassModule loads from Struct/Class/*.xml) ----
+    explicit NFGPUKernelModule(int capacity, void* hip_stream = nullptr);
+    ~NFGPUKernelModule();
+    int AddProperty(const std::string& name, TDATA_TYPE type);  // returns property id
+    int AddClass(const std::string& name);
+    void SetPropertyFlags(const std::string& cls, const std::string& prop, bool pub, bool priv, bool upload);
+    int AddRecord(const std::string& name, int rows, const std::vector<TDATA_TYPE>& cols);
+    void SetRecordFlags(const std::string& cls, const std::string& rec, bool pub, bool priv, bool upload);
+    // the device-side effect of a heartbeat name (see nfgpu.h op list)
+    void AddHeartBeatProgram(const std::string& name, const std::vector<nfk_op>& ops);
+    int PropertyId(const std::string& name) const;
+
+    // ---- NFIModule lifecycle ----
+    bool Init();
+    bool AfterInit();  // commits the layout (objects created before AfterInit)
+    bool Execute(int64_t now_ms);
+    bool BeforeShut();
+    bool Shut();
+
+    // ---- NFIKernelModule ----
+    bool CreateScene(int nSceneID);
+    bool CreateObject(const NFGUID& self, int nSceneID, int nGroupID, const std::string& strClassName,
+                      const std::map<std::string, TData>& init = {});
+    bool SetPropertyInt(const NFGUID& self, const std::string& name, int64_t v);
+    bool SetPropertyFloat(const NFGUID& self, const std::string& name, double v);
+    int64_t GetPropertyInt(const NFGUID& self, const std::string& name);
+    double GetPropertyFloat(const NFGUID& self, const std::string& name);
+    bool RegisterCommonPropertyEvent(const PROPERTY_EVENT_FUNCTOR& cb);
+    bool RegisterCommonRecordEvent(const RECORD_EVENT_FUNCTOR& cb);
+
+    // ---- NFIScheduleModule ----
+    bool AddSchedule(const NFGUID& self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb, float fTime,
+                     int nCount, int64_t now_ms);
+    bool RemoveSchedule(const NFGUID& self, const std::string& name);
+    bool RemoveSchedule(const NFGUID& self);
+
+    // ---- NFISceneAOIModule recipient-list events ----
+    bool AddPropertyEventCallBack(const PROPERTY_SINGLE_EVENT_FUNCTOR& cb);
+    bool AddRecordEventCallBack(const RECORD_SINGLE_EVENT_FUNCTOR& cb);
+
+    void* World() const { return world_; }
+    const nfk_summary& LastSummary() const { return summary_; }
+    int ObjectIndex(const NFGUID& g) const;
+
+private:
+    void check(int rc, const char* what) const;
+    void* world_ = nullptr;
+    int capacity_;
+    void* stream_;
+    bool committed_ = false;
+    std::vector<PropertyDef> props_;
+    std::map<std::string, int> prop_id_;
+    std::vector<ClassDef> classes_;
+    std::map<std::string, int> class_id_;
+    std::vector<RecordDef> records_;
+    std::map<std::string, int> record_id_;
+    std::vector<HeartBeatDef> heartbeats_;
+    std::map<std::string, int> hb_id_;
+    std::map<int, bool> scenes_;
+    // objects
+    std::vector<NFGUID> guids_;
+    std::map<NFGUID, int> obj_of_;
+    std::vector<int32_t> scene_, group_;
+    std::vector<uint8_t> cls_, isplayer_;
+    std::vector<std::vector<uint64_t>> init_;
+    // callbacks
+    std::vector<PROPERTY_EVENT_FUNCTOR> common_prop_cb_;
+    std::vector<RECORD_EVENT_FUNCTOR> common_rec_cb_;
+    std::vector<PROPERTY_SINGLE_EVENT_FUNCTOR> aoi_prop_cb_;
+    std::vector<RECORD_SINGLE_EVENT_FUNCTOR> aoi_rec_cb_;
+    std::map<std::pair<int, int>, OBJECT_SCHEDULE_FUNCTOR> sched_cb_;   // (object, kind)
+    std::map<std::pair<int, int>, float> sched_time_;
+    nfk_summary summary_{};
+};
+
+}  // namespace nfgpu

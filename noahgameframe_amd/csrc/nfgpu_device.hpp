@@ -13,14 +13,32 @@ constexpr unsigned kSpinLimit = 1u << 22; // bounded spins (~0.2 s) before the e
 // device error word bits (Ctrl::err)
 constexpr unsigned kErrSpin = 1, kErrEvCap = 2, kErrMsgCap = 4, kErrTouch = 8, kErrFiCap = 16, kErrReCap = 32;
 
-// Per-tick control block.  The first 64 bytes are zeroed by a memset node before
-// every tick (tickets + totals); look-back granules use per-tick tags instead.
+// Control block.  Tickets are reset in-kernel by a later kernel of the same frame (k_fanout
+// resets k_tick's, k_tick resets k_records'/k_fanout's); totals are overwritten by the last
+// virtual block; the error word is sticky until nfk_summary_get clears it.  Look-back
+// granules carry a per-frame tag, so nothing is memset per frame.
 struct alignas(64) Ctrl {
     unsigned ticket_tick, ticket_rec, ticket_fan, err;                  // 16 B
     unsigned long long n_ev, n_fi, n_re, n_msgs;                        // 32 B
-    unsigned long long pad0, pad1;                                      // 16 B  (end of memset region)
-    unsigned long long bytes_tick, bytes_rec, bytes_fan, pad2;          // accumulated across ticks
+    unsigned long long pad0, pad1;                                      // 16 B
+    unsigned long long bytes_tick, bytes_rec, bytes_fan, pad2;          // accumulated across frames
 };
+
+// Schedule table, one 16-byte hot record per (kind, slot) read every frame by the timer scan,
+// and one 16-byte cold record read only when the heartbeat fires (NFCScheduleElement fields).
+struct alignas(16) SchedHot {
+    int64_t next;    // mnNextTriggerTime
+    int32_t remain;  // mnRemainCount
+    uint32_t state;  // bit0 present, bit1 forever (mbForever)
+};
+struct alignas(16) SchedCold {
+    int64_t start;   // mnStartTime
+    int32_t all;     // mnAllCount
+    float interval;  // mfIntervalTime
+};
+
+// timing-only ablations (NFGPU_ABLATE env var); outputs are wrong when set
+constexpr unsigned kAblTickLookback = 1, kAblFanLookback = 2, kAblPrograms = 4;
 
 // record op compiled from the kind programs, sorted by (rec, col)
 struct RecOp {
@@ -51,12 +69,8 @@ struct Dev {
     int64_t* icol;
     double* fcol;
     // schedules [kind][cap]
-    int64_t* s_next;
-    int64_t* s_start;
-    int32_t* s_remain;
-    int32_t* s_all;
-    float* s_interval;
-    uint8_t* s_state;  // bit0 present, bit1 forever
+    SchedHot* s_hot;
+    SchedCold* s_cold;
     uint8_t* e_flags;  // bit0: a RemoveSchedule(self, name) is queued (owns the remove-list key)
     // queued SetProperty* calls, sorted by slot (stable)
     uint32_t* ext_head;  // [cap] 0 = none, else 1 + first op index
@@ -74,6 +88,8 @@ struct Dev {
     const uint8_t* isplayer;
     const int32_t* seg_pl_off;
     const int32_t* pl_slot;
+    const int32_t* pl_rank;  // [cap] rank of a player slot in its group's player list, -1 otherwise
+    uint32_t ablate;
     // outputs
     uint32_t* ev_slot; uint32_t* ev_pid; uint64_t* ev_old; uint64_t* ev_new; int64_t ev_cap;
     uint32_t* fi_slot; uint32_t* fi_kind; int32_t* fi_remain; int64_t fi_cap;

@@ -1,6 +1,7 @@
 // nfgpu_host.hip — C-ABI implementation (include/nfgpu.h): world lifetime, schema,
 // membership layout, queued SetProperty / schedule calls, frame launch, readback.
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -417,7 +418,7 @@ int nfk_commit(void* world) {
     });
     w->slot_of_obj.resize(N);
     for (int32_t s = 0; s < N; s++) w->slot_of_obj[w->obj_of_slot[s]] = s;
-    std::vector<int32_t> seg_of(N), seg_pl_off, pl_slot;
+    std::vector<int32_t> seg_of(N), seg_pl_off, pl_slot, pl_rank(N, -1);
     std::vector<uint8_t> cls_s(N), ip_s(N);
     int32_t nseg = 0;
     for (int32_t s = 0; s < N; s++) {
@@ -429,7 +430,10 @@ int nfk_commit(void* world) {
         seg_of[s] = nseg - 1;
         cls_s[s] = w->cls[o];
         ip_s[s] = w->isplayer[o];
-        if (w->isplayer[o]) pl_slot.push_back(s);
+        if (w->isplayer[o]) {
+            pl_rank[s] = (int32_t)pl_slot.size() - seg_pl_off.back();
+            pl_slot.push_back(s);
+        }
     }
     seg_pl_off.push_back((int32_t)pl_slot.size());
     w->nseg = nseg;
@@ -447,12 +451,8 @@ int nfk_commit(void* world) {
     ALLOC(w->ctrl, sizeof(Ctrl));
     ALLOC(d.icol, (size_t)std::max(NI, 1) * cap * 8);
     ALLOC(d.fcol, (size_t)std::max(NF, 1) * cap * 8);
-    ALLOC(d.s_next, (size_t)std::max(NK, 1) * cap * 8);
-    ALLOC(d.s_start, (size_t)std::max(NK, 1) * cap * 8);
-    ALLOC(d.s_remain, (size_t)std::max(NK, 1) * cap * 4);
-    ALLOC(d.s_all, (size_t)std::max(NK, 1) * cap * 4);
-    ALLOC(d.s_interval, (size_t)std::max(NK, 1) * cap * 4);
-    ALLOC(d.s_state, (size_t)std::max(NK, 1) * cap);
+    ALLOC(d.s_hot, (size_t)std::max(NK, 1) * cap * sizeof(SchedHot));
+    ALLOC(d.s_cold, (size_t)std::max(NK, 1) * cap * sizeof(SchedCold));
     ALLOC(d.e_flags, cap);
     ALLOC(d.ext_head, (size_t)cap * 4);
     ALLOC(d.fired_mask, (size_t)cap * 4);
@@ -462,7 +462,7 @@ int nfk_commit(void* world) {
         ALLOC(d.rcells[r], (size_t)cap * w->tab.rec_rows[r] * w->tab.rec_cols[r] * 8);
         ALLOC(d.rused[r], (size_t)cap * 8);
     }
-    int32_t *seg_of_d, *seg_pl_off_d, *pl_slot_d;
+    int32_t *seg_of_d, *seg_pl_off_d, *pl_slot_d, *pl_rank_d;
     uint8_t *cls_d, *ip_d;
     ALLOC(seg_of_d, (size_t)cap * 4);
     ALLOC(cls_d, cap);
@@ -470,6 +470,12 @@ int nfk_commit(void* world) {
     ALLOC(seg_pl_off_d, seg_pl_off.size() * 4);
     ALLOC(pl_slot_d, std::max<size_t>(pl_slot.size(), 1) * 4);
     ALLOC(w->slot_obj_d, (size_t)cap * 4);
+    ALLOC(pl_rank_d, (size_t)cap * 4);
+    d.pl_rank = pl_rank_d;
+    {
+        const char* ab = getenv("NFGPU_ABLATE");
+        d.ablate = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0u;
+    }
     d.seg_of = seg_of_d;
     d.cls = cls_d;
     d.isplayer = ip_d;
@@ -527,7 +533,9 @@ int nfk_commit(void* world) {
         HIPCHK(hipMemcpy(d.rcells[r], cells.data(), cells.size() * 8, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(d.rused[r], used.data(), used.size() * 8, hipMemcpyHostToDevice));
     }
-    HIPCHK(hipMemset(d.s_state, 0, (size_t)std::max(NK, 1) * cap));
+    HIPCHK(hipMemset(d.s_hot, 0, (size_t)std::max(NK, 1) * cap * sizeof(SchedHot)));
+    HIPCHK(hipMemset(d.s_cold, 0, (size_t)std::max(NK, 1) * cap * sizeof(SchedCold)));
+    HIPCHK(hipMemcpy(pl_rank_d, pl_rank.data(), (size_t)N * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(d.e_flags, 0, cap));
     HIPCHK(hipMemset(d.ext_head, 0, (size_t)cap * 4));
     HIPCHK(hipMemset(d.fired_mask, 0, (size_t)cap * 4));
@@ -727,7 +735,6 @@ int nfk_execute(void* world, int64_t now_ms) {
         w->epoch = 1;
     }
     d.tag = w->epoch;
-    HIPCHK(hipMemsetAsync(w->ctrl, 0, 64, w->stream));
 
     if (nx || npre) {
         TimeScope ts(w, KT_AUX);
@@ -737,7 +744,7 @@ int nfk_execute(void* world, int64_t now_ms) {
         if (npre)
             hipLaunchKernelGGL(k_pre_hostops, dim3((unsigned)((npre + 255) / 256)), dim3(256), 0, w->stream,
                                (const uint32_t*)(S + off_ps), (const uint32_t*)(S + off_po), (int32_t)npre,
-                               d.e_flags, d.s_state, d.n_kind, d.cap);
+                               d.e_flags, d.s_hot, d.n_kind, d.cap);
         HIPCHK(hipGetLastError());
     }
     const unsigned nb_tick = (unsigned)((d.N + kTPB - 1) / kTPB);
@@ -789,8 +796,35 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     w->last_bytes[0] = c.bytes_tick;
     w->last_bytes[1] = c.bytes_rec;
     w->last_bytes[2] = c.bytes_fan;
+    if ((c.err & kErrMsgCap) && !(c.err & ~kErrMsgCap)) {
+        // The fan-out kernel only reads the (complete) event stream and the membership CSR, so
+        // grow the message buffer to the exact total it counted and re-run it for this frame.
+        const int64_t need = (int64_t)c.n_msgs + (int64_t)c.n_msgs / 4 + 1024;
+        if (need > 0xFFFFFFFFll) return fail(NFK_ERR_CAPACITY, "fan-out exceeds 2^32 messages per frame");
+        HIPCHK(hipFree(w->d.msg_rcpt));
+        w->allocs.erase(std::remove(w->allocs.begin(), w->allocs.end(), (void*)w->d.msg_rcpt), w->allocs.end());
+        int r = alloc_track(w, (void**)&w->d.msg_rcpt, (size_t)need * 4);
+        if (r) return r;
+        w->d.msg_cap = need;
+        Ctrl z{};
+        z.n_ev = c.n_ev;
+        z.n_fi = c.n_fi;
+        z.n_re = c.n_re;
+        HIPCHK(hipMemcpy(w->ctrl, &z, 64, hipMemcpyHostToDevice));
+        Dev d = w->d;
+        d.tag = w->epoch;
+        HIPCHK(hipMemsetAsync(d.g_msg, 0, w->g_msg_n * 8, w->stream));
+        const unsigned long long max_tiles = (d.ev_cap + d.re_cap + kTPB - 1) / kTPB;
+        const unsigned nb = (unsigned)std::min<unsigned long long>(std::max<unsigned long long>(max_tiles, 1), 1024);
+        hipLaunchKernelGGL(k_fanout, dim3(nb), dim3(kTPB), 0, w->stream, d);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(w->stream));
+        HIPCHK(hipMemcpy(&c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+        out->n_msgs = (int64_t)c.n_msgs;
+    }
     out->device_error = (int32_t)c.err;
     out->tick = w->ticks;
+    if (c.err) HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
     if (c.err & kErrSpin) return fail(NFK_ERR_DEVICE, "device look-back spin limit exceeded");
     if (c.err & kErrTouch) return fail(NFK_ERR_TOUCH, "device touch list overflow");
     if (c.err & (kErrEvCap | kErrMsgCap | kErrFiCap | kErrReCap))
@@ -851,20 +885,15 @@ int nfk_read_schedules(void* world, int64_t* next_ms, int32_t* remain, uint8_t* 
     HIPCHK(hipStreamSynchronize(w->stream));
     const Dev& d = w->d;
     const int NK = d.n_kind;
-    std::vector<int64_t> nx((size_t)NK * d.cap);
-    std::vector<int32_t> rm((size_t)NK * d.cap);
-    std::vector<uint8_t> st((size_t)NK * d.cap);
-    if (NK) {
-        HIPCHK(hipMemcpy(nx.data(), d.s_next, nx.size() * 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(rm.data(), d.s_remain, rm.size() * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(st.data(), d.s_state, st.size(), hipMemcpyDeviceToHost));
-    }
+    std::vector<SchedHot> hot((size_t)NK * d.cap);
+    if (NK) HIPCHK(hipMemcpy(hot.data(), d.s_hot, hot.size() * sizeof(SchedHot), hipMemcpyDeviceToHost));
     for (int k = 0; k < NK; k++)
         for (int32_t s = 0; s < d.N; s++) {
             size_t o = (size_t)k * w->n_obj + w->obj_of_slot[s], a = (size_t)k * d.cap + s;
-            state[o] = st[a];
-            next_ms[o] = (st[a] & 1) ? nx[a] : 0;
-            remain[o] = (st[a] & 1) ? rm[a] : 0;
+            const SchedHot& h = hot[a];
+            state[o] = (uint8_t)h.state;
+            next_ms[o] = (h.state & 1) ? h.next : 0;
+            remain[o] = (h.state & 1) ? h.remain : 0;
         }
     return NFK_OK;
 }

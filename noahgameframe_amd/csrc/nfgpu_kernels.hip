@@ -1,16 +1,17 @@
 // nfgpu_kernels.hip — hand-written gfx950 kernels for one NoahGameFrame server frame.
 //
 //   k_ext_scatter   index queued SetProperty* calls by slot
-//   k_pre_hostops   RemoveSchedule(self[,name]) effects that precede the scan
-//   k_tick          heartbeat scan (NFCScheduleModule::Execute, SM:45-80) + effect programs
-//                   + property change predicates (NFCProperty::SetInt/SetFloat, PR:254/295)
-//                   + dirty diff + ordered compaction of dirty events and fired heartbeats
-//                   (wave ballot/scan + decoupled look-back)
+//   k_pre_hostops   RemoveSchedule(self[, name]) effects that precede the scan
+//   k_tick          heartbeat timer scan (NFCScheduleModule::Execute, SM:45-80) + effect
+//                   programs + property change predicates (NFCProperty::SetInt/SetFloat,
+//                   PR:254/295) + dirty diff + ordered compaction of dirty events and fired
+//                   heartbeats (wave ballot/scan + decoupled look-back)
 //   k_records       record-cell effects (NFCRecord::SetInt/SetFloat, RC:182/243) + diff,
 //                   one wave per entity, lane = row
 //   k_post_hostops  remove list then add list (SM:82-117)
 //   k_fanout        GetBroadCastObject recipient lists (AOI:531-593) for every dirty event,
-//                   CSR over the (scene, group, guid)-sorted slots
+//                   CSR over the (scene, group, guid)-sorted slots, LDS-staged so message
+//                   stores are coalesced
 //
 // Compiled with -ffp-contract=off: f64 effects round exactly like the reference's C++.
 #include "nfgpu_device.hpp"
@@ -26,17 +27,17 @@ __global__ void k_ext_scatter(const uint32_t* __restrict__ x_slot, int32_t n, ui
 
 // op: 1 = RemoveSchedule(self, name) queued (owns the remove-list key), 2 = RemoveSchedule(self)
 __global__ void k_pre_hostops(const uint32_t* __restrict__ slot, const uint32_t* __restrict__ op, int32_t n,
-                              uint8_t* __restrict__ e_flags, uint8_t* __restrict__ s_state, int32_t n_kind,
+                              uint8_t* __restrict__ e_flags, SchedHot* __restrict__ s_hot, int32_t n_kind,
                               int32_t cap) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = slot[i];
     if (op[i] == 1) e_flags[s] |= 1;
     if (op[i] == 2)
-        for (int k = 0; k < n_kind; k++) s_state[(size_t)k * cap + s] = 0;
+        for (int k = 0; k < n_kind; k++) s_hot[(size_t)k * cap + s].state = 0;
 }
 
-// post-scan host ops, one entry per (slot, kind): bit0 remove, bit1 add (remove first)
+// post-scan host ops, one entry per (slot, kind): bit0 remove, bit1 add (remove first), bit2 clear key
 __global__ void k_post_hostops(const uint32_t* __restrict__ slot, const uint32_t* __restrict__ kind,
                                const uint32_t* __restrict__ op, const float* __restrict__ interval,
                                const int32_t* __restrict__ count, const int64_t* __restrict__ time, int32_t n,
@@ -45,92 +46,91 @@ __global__ void k_post_hostops(const uint32_t* __restrict__ slot, const uint32_t
     if (i >= n) return;
     const uint32_t s = slot[i];
     const size_t at = (size_t)kind[i] * d.cap + s;
-    if (op[i] & 1) d.s_state[at] = 0;
+    SchedHot h = d.s_hot[at];
+    if (op[i] & 1) h.state = 0;
     if (op[i] & 4) d.e_flags[s] = 0;
-    if ((op[i] & 2) && !(d.s_state[at] & 1)) {
+    if ((op[i] & 2) && !(h.state & 1)) {  // AddSchedule (SM:236): an existing name wins
         const float f = interval[i];
         const int32_t c = count[i];
-        d.s_state[at] = 1 | (c < 0 ? 2 : 0);
-        d.s_interval[at] = f;
-        d.s_next[at] = time[i] + (int64_t)(f * 1000.0f);
-        d.s_start[at] = time[i];
-        d.s_remain[at] = c;
-        d.s_all[at] = c;
+        h.state = 1u | (c < 0 ? 2u : 0u);
+        h.next = time[i] + (int64_t)(f * 1000.0f);
+        h.remain = c;
+        SchedCold cold;
+        cold.start = time[i];
+        cold.all = c;
+        cold.interval = f;
+        d.s_cold[at] = cold;
     }
+    d.s_hot[at] = h;
 }
 
 // ---------------------------------------------------------------------------------
 // Per-entity written-property list, kept in registers (all indices compile-time).
-struct Touch {
+struct Ent {
     uint32_t pid[NFK_MAX_TOUCH];
     uint64_t old[NFK_MAX_TOUCH];
     uint64_t cur[NFK_MAX_TOUCH];
     int n;
-};
-
-__device__ __forceinline__ bool tget(const Touch& t, uint32_t pid, uint64_t& v) {
-    bool f = false;
-#pragma unroll
-    for (int j = 0; j < NFK_MAX_TOUCH; j++) {
-        const bool m = (j < t.n) && (t.pid[j] == pid);
-        v = m ? t.cur[j] : v;
-        f |= m;
-    }
-    return f;
-}
-
-__device__ __forceinline__ void tput(Touch& t, uint32_t pid, uint64_t oldv, uint64_t newv, bool& ovf) {
-    bool f = false;
-#pragma unroll
-    for (int j = 0; j < NFK_MAX_TOUCH; j++) {
-        const bool m = (j < t.n) && (t.pid[j] == pid);
-        if (m) t.cur[j] = newv;
-        f |= m;
-    }
-    if (f) return;
-    if (t.n >= NFK_MAX_TOUCH) {
-        ovf = true;
-        return;
-    }
-#pragma unroll
-    for (int j = 0; j < NFK_MAX_TOUCH; j++)
-        if (j == t.n) {
-            t.pid[j] = pid;
-            t.old[j] = oldv;
-            t.cur[j] = newv;
-        }
-    t.n++;
-}
-
-struct Ent {
-    const Dev& d;
-    int e;
-    Touch t;
     bool ovf;
     unsigned bytes;
-    __device__ __forceinline__ Ent(const Dev& dd, int ee) : d(dd), e(ee), ovf(false), bytes(0) { t.n = 0; }
+    const int64_t* icol;
+    const double* fcol;
+    size_t cap;
+    int n_int;
+    int e;
 
-    __device__ __forceinline__ uint64_t getb(uint32_t pid) {
-        uint64_t v = 0;
-        if (tget(t, pid, v)) return v;
-        bytes += 8;
-        if ((int)pid < d.n_int) return (uint64_t)d.icol[(size_t)pid * d.cap + e];
-        return (uint64_t)__double_as_longlong(d.fcol[(size_t)(pid - d.n_int) * d.cap + e]);
+    __device__ __forceinline__ bool tget(uint32_t p, uint64_t& v) const {
+        bool f = false;
+#pragma unroll
+        for (int j = 0; j < NFK_MAX_TOUCH; j++) {
+            const bool m = (j < n) && (pid[j] == p);
+            v = m ? cur[j] : v;
+            f |= m;
+        }
+        return f;
     }
-    __device__ __forceinline__ int64_t geti(uint32_t pid) { return (int64_t)getb(pid); }
-    __device__ __forceinline__ double getf(uint32_t pid) { return __longlong_as_double((long long)getb(pid)); }
-
+    __device__ __forceinline__ void tput(uint32_t p, uint64_t oldv, uint64_t newv) {
+        bool f = false;
+#pragma unroll
+        for (int j = 0; j < NFK_MAX_TOUCH; j++) {
+            const bool m = (j < n) && (pid[j] == p);
+            if (m) cur[j] = newv;
+            f |= m;
+        }
+        if (f) return;
+        if (n >= NFK_MAX_TOUCH) {
+            ovf = true;
+            return;
+        }
+#pragma unroll
+        for (int j = 0; j < NFK_MAX_TOUCH; j++)
+            if (j == n) {
+                pid[j] = p;
+                old[j] = oldv;
+                cur[j] = newv;
+            }
+        n++;
+    }
+    __device__ __forceinline__ uint64_t getb(uint32_t p) {
+        uint64_t v = 0;
+        if (tget(p, v)) return v;
+        bytes += 8;
+        if ((int)p < n_int) return (uint64_t)icol[(size_t)p * cap + e];
+        return (uint64_t)__double_as_longlong(fcol[(size_t)(p - n_int) * cap + e]);
+    }
+    __device__ __forceinline__ int64_t geti(uint32_t p) { return (int64_t)getb(p); }
+    __device__ __forceinline__ double getf(uint32_t p) { return __longlong_as_double((long long)getb(p)); }
     // NFCProperty::SetInt (PR:254): stored (and an event fired) only when the value changes
-    __device__ __forceinline__ void seti(uint32_t pid, int64_t v) {
-        const int64_t cur = geti(pid);
-        if (v == cur) return;
-        tput(t, pid, (uint64_t)cur, (uint64_t)v, ovf);
+    __device__ __forceinline__ void seti(uint32_t p, int64_t v) {
+        const int64_t c = geti(p);
+        if (v == c) return;
+        tput(p, (uint64_t)c, (uint64_t)v);
     }
     // NFCProperty::SetFloat (PR:295): IsZeroDouble(v - cur), eps 1e-15 (NFPlatform.h:362)
-    __device__ __forceinline__ void setf(uint32_t pid, double v) {
-        const double cur = getf(pid);
-        if (fabs(v - cur) <= 1e-15) return;
-        tput(t, pid, (uint64_t)__double_as_longlong(cur), (uint64_t)__double_as_longlong(v), ovf);
+    __device__ __forceinline__ void setf(uint32_t p, double v) {
+        const double c = getf(p);
+        if (fabs(v - c) <= 1e-15) return;
+        tput(p, (uint64_t)__double_as_longlong(c), (uint64_t)__double_as_longlong(v));
     }
 };
 
@@ -138,7 +138,7 @@ __device__ __forceinline__ int64_t opnd(Ent& en, const nfk_op& op, int bit, int6
     return (op.flags & bit) ? en.geti((uint32_t)x) : x;
 }
 
-__device__ __forceinline__ void run_program(Ent& en, const Tables* tab, int k) {
+__device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ tab, int k) {
     const int n = tab->nops[k];
     for (int i = 0; i < n; i++) {
         const nfk_op op = tab->ops[k][i];
@@ -184,6 +184,8 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
     return before + inc - v;
 }
 
+constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
+
 __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
     __shared__ unsigned s_vb;
     __shared__ unsigned long long s_w[kTPB / 64];
@@ -192,12 +194,24 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
     if (threadIdx.x == 0) {
         s_vb = atomicAdd(&d.ctrl->ticket_tick, 1u);
         s_bytes = 0;
+        if (blockIdx.x == 0) {  // last frame's k_records / k_fanout are complete
+            d.ctrl->ticket_rec = 0;
+            d.ctrl->ticket_fan = 0;
+        }
     }
     __syncthreads();
     const unsigned vb = s_vb;
     const int e = (int)(vb * kTPB + threadIdx.x);
     const bool live = e < d.N;
-    Ent en(d, live ? e : 0);
+    Ent en;
+    en.n = 0;
+    en.ovf = false;
+    en.bytes = 0;
+    en.icol = d.icol;
+    en.fcol = d.fcol;
+    en.cap = (size_t)d.cap;
+    en.n_int = d.n_int;
+    en.e = live ? e : 0;
     uint32_t fired = 0;
     uint32_t xh = 0;
     if (live) {
@@ -213,54 +227,66 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
                 else en.setf(pid, __longlong_as_double((long long)b));
             }
         }
-        // 2. NFCScheduleModule::Execute (SM:45-80) over this object's schedules in name order
-        bool taken = d.e_flags[e] & 1;  // std::map remove-list key already owned
+        // 2. NFCScheduleModule::Execute (SM:45-80): this object's schedules in name order.
+        //    The hot records of a chunk of kinds are loaded together (independent 16 B loads).
+        bool taken = d.e_flags[e] & 1;  // std::map remove-list key already owned (SM:72)
         en.bytes += 1;
-        for (int k = 0; k < d.n_kind; k++) {
-            const size_t at = (size_t)k * d.cap + e;
-            uint8_t st = d.s_state[at];
-            en.bytes += 1;
-            if (!(st & 1)) continue;
-            const int64_t nx = d.s_next[at];
-            en.bytes += 8;
-            if (!(d.now > nx)) continue;
-            int32_t rem = d.s_remain[at];
-            en.bytes += 4;
-            const bool forever = st & 2;
-            if (!(rem > 0 || forever)) continue;
-            rem -= 1;
-            fired |= 1u << k;
-            run_program(en, d.tab, k);
-            d.s_remain[at] = rem;
-            en.bytes += 4;
-            if (rem <= 0 && !forever) {
-                if (!taken) {
-                    d.s_state[at] = 0;
-                    en.bytes += 1;
-                    taken = true;
+        for (int k0 = 0; k0 < d.n_kind; k0 += kKindChunk) {
+            SchedHot h[kKindChunk];
+#pragma unroll
+            for (int j = 0; j < kKindChunk; j++)
+                if (k0 + j < d.n_kind) h[j] = d.s_hot[(size_t)(k0 + j) * d.cap + e];
+#pragma unroll
+            for (int j = 0; j < kKindChunk; j++) {
+                const int k = k0 + j;
+                if (k >= d.n_kind) break;
+                en.bytes += 16;
+                if (!(h[j].state & 1) || !(d.now > h[j].next)) continue;
+                const bool forever = h[j].state & 2;
+                if (!(h[j].remain > 0 || forever)) continue;
+                h[j].remain -= 1;
+                fired |= 1u << k;
+                if (h[j].remain <= 0 && !forever) {
+                    if (!taken) {  // insert into the remove list succeeds for the first one only
+                        h[j].state = 0;
+                        taken = true;
+                    }
+                } else {
+                    const SchedCold c = d.s_cold[(size_t)k * d.cap + e];
+                    en.bytes += 16;
+                    const int64_t step = (int64_t)(c.interval * 1000.0f);
+                    const int32_t done = (int32_t)((uint32_t)c.all - (uint32_t)h[j].remain);
+                    h[j].next = c.start + step * (int64_t)done;
                 }
-            } else {
-                const int64_t step = (int64_t)(d.s_interval[at] * 1000.0f);
-                const int32_t done = (int32_t)((uint32_t)d.s_all[at] - (uint32_t)rem);
-                d.s_next[at] = d.s_start[at] + step * (int64_t)done;
-                en.bytes += 4 + 4 + 8 + 8;
+                d.s_hot[(size_t)k * d.cap + e] = h[j];
+                en.bytes += 16;
             }
         }
+        // 3. the fired heartbeats' effect programs, in schedule-name order
+        if (!(d.ablate & kAblPrograms)) {
+            for (int k = 0; k < d.n_kind; k++)
+                if ((fired >> k) & 1) run_program(en, d.tab, k);
+        }
     }
-    // 3. dirty diff: written properties whose bits changed since the frame began
+    // 4. dirty diff: written properties whose bits changed since the frame began
     uint32_t dmask = 0;
 #pragma unroll
     for (int j = 0; j < NFK_MAX_TOUCH; j++)
-        if (j < en.t.n && en.t.cur[j] != en.t.old[j]) dmask |= 1u << j;
+        if (j < en.n && en.cur[j] != en.old[j]) dmask |= 1u << j;
     const unsigned nd = __builtin_popcount(dmask);
     const unsigned nf = __builtin_popcount(fired);
     if (en.ovf) atomicOr(&d.ctrl->err, kErrTouch);
 
-    // 4. ordered compaction: block scan + look-back (events chain on wave 0, fired chain on wave 1)
+    // 5. ordered compaction: block scan + look-back (events chain on wave 0, fired chain on wave 1)
     unsigned long long tot;
     const unsigned long long excl = block_excl_scan(((unsigned long long)nf << 32) | nd, s_w, tot);
     const int w = threadIdx.x >> 6;
-    if (w == 0) {
+    if (d.ablate & kAblTickLookback) {
+        if (threadIdx.x == 0) {
+            s_base[0] = (unsigned long long)vb * kTPB * NFK_MAX_TOUCH;
+            s_base[1] = (unsigned long long)vb * kTPB * d.n_kind;
+        }
+    } else if (w == 0) {
         const unsigned long long b = lookback(d.g_ev, vb, d.tag, tot & 0xFFFFFFFFull, d.ctrl);
         if ((threadIdx.x & 63) == 0) s_base[0] = b;
     } else if (w == 1) {
@@ -276,9 +302,9 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
 #pragma unroll
         for (int j = 0; j < NFK_MAX_TOUCH; j++) {
             if (!((dmask >> j) & 1)) continue;
-            const uint32_t pid = en.t.pid[j];
-            if ((int)pid < d.n_int) d.icol[(size_t)pid * d.cap + e] = (int64_t)en.t.cur[j];
-            else d.fcol[(size_t)(pid - d.n_int) * d.cap + e] = __longlong_as_double((long long)en.t.cur[j]);
+            const uint32_t pid = en.pid[j];
+            if ((int)pid < d.n_int) d.icol[(size_t)pid * d.cap + e] = (int64_t)en.cur[j];
+            else d.fcol[(size_t)(pid - d.n_int) * d.cap + e] = __longlong_as_double((long long)en.cur[j]);
             en.bytes += 8;
         }
         // events in property-id order
@@ -288,16 +314,16 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
             int bj = 0;
 #pragma unroll
             for (int j = 0; j < NFK_MAX_TOUCH; j++)
-                if (((left >> j) & 1) && en.t.pid[j] < best) {
-                    best = en.t.pid[j];
+                if (((left >> j) & 1) && en.pid[j] < best) {
+                    best = en.pid[j];
                     bj = j;
                 }
             uint64_t ov = 0, nv = 0;
 #pragma unroll
             for (int j = 0; j < NFK_MAX_TOUCH; j++)
                 if (j == bj) {
-                    ov = en.t.old[j];
-                    nv = en.t.cur[j];
+                    ov = en.old[j];
+                    nv = en.cur[j];
                 }
             left &= ~(1u << bj);
             if ((long long)pev < d.ev_cap) {
@@ -318,7 +344,7 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
             if ((long long)pfi < d.fi_cap) {
                 d.fi_slot[pfi] = (uint32_t)e;
                 d.fi_kind[pfi] = (uint32_t)k;
-                d.fi_remain[pfi] = d.s_remain[(size_t)k * d.cap + e];
+                d.fi_remain[pfi] = d.s_hot[(size_t)k * d.cap + e].remain;
             } else {
                 atomicOr(&d.ctrl->err, kErrFiCap);
             }
@@ -415,7 +441,6 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
 #pragma unroll
     for (int j = 0; j < NFK_MAX_OPS; j++) cnt += ch[j] ? 1 : 0;
     const unsigned long long wtot = wave_sum(cnt);
-    // block scan over the 4 entities of this block
     if (lane == 0) s_w[w] = wtot;
     __syncthreads();
     unsigned long long before = 0, btot = 0;
@@ -430,7 +455,6 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     }
     __syncthreads();
     unsigned long long pos = s_base + before;
-    // emit: for each record (ascending) the wave compacts rows; within a row, cols ascending
     int j0 = 0;
     while (j0 < nro) {
         const int rec = tab->recops[j0].rec;
@@ -468,13 +492,19 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
 }
 
 // ---------------------------------------------------------------------------------
-// Fan-out over the virtual event stream [prop events ++ record events].  Persistent
-// grid, 256-event tiles pulled from a ticket; message offsets by look-back.
+// Fan-out over the virtual event stream [prop events ++ record events].  Persistent grid,
+// 256-event tiles pulled from a ticket; message offsets by look-back; the tile's recipient
+// lists are expanded cooperatively from an LDS descriptor table so consecutive lanes store
+// consecutive messages.
 __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
     __shared__ unsigned s_tile;
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_off[kTPB];
+    __shared__ int32_t s_src[kTPB];   // public: first player index in pl_slot; private: -1 - slot
+    __shared__ int32_t s_rank[kTPB];  // public: rank of self in the player list to skip, else -1
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (blockIdx.x == 0 && threadIdx.x == 0) d.ctrl->ticket_tick = 0;  // this frame's k_tick is complete
     const unsigned long long nev = d.ctrl->n_ev < (unsigned long long)d.ev_cap ? d.ctrl->n_ev : d.ev_cap;
     const unsigned long long nre = d.ctrl->n_re < (unsigned long long)d.re_cap ? d.ctrl->n_re : d.re_cap;
     const unsigned long long total = nev + nre;
@@ -487,9 +517,10 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
         if (tile >= ntiles) break;
         const unsigned long long i = (unsigned long long)tile * kTPB + threadIdx.x;
         unsigned cnt = 0;
-        int32_t slot = 0, pb = 0, np = 0;
-        uint8_t fl = 0;
+        int32_t src = 0, rank = -1;
         if (i < total) {
+            int32_t slot;
+            uint8_t fl;
             if (i < nev) {
                 slot = (int32_t)d.ev_slot[i];
                 fl = d.tab->pflags[d.cls[slot]][d.ev_pid[i]];
@@ -498,45 +529,63 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
                 fl = d.tab->rflags[d.cls[slot]][d.re_rrc[i - nev] >> 16];
             }
             bytes += 4 + 4 + 1;
-            if (fl & NFK_PUBLIC) {
+            if (fl & NFK_PUBLIC) {  // every player of the group but self, NFGUID order
                 const int seg = d.seg_of[slot];
-                pb = d.seg_pl_off[seg];
-                np = d.seg_pl_off[seg + 1] - pb;
-                cnt = (unsigned)(np - (d.isplayer[slot] ? 1 : 0));
-                bytes += 4 + 8 + 1;
-            } else if ((fl & NFK_PRIVATE) && !(fl & NFK_UPLOAD)) {
+                src = d.seg_pl_off[seg];
+                const int np = d.seg_pl_off[seg + 1] - src;
+                rank = d.isplayer[slot] ? d.pl_rank[slot] : -1;
+                cnt = (unsigned)(np - (rank >= 0 ? 1 : 0));
+                bytes += 4 + 8 + 1 + (rank >= 0 ? 4 : 0);
+            } else if ((fl & NFK_PRIVATE) && !(fl & NFK_UPLOAD)) {  // self only
                 cnt = 1;
+                src = -1 - slot;
             }
         }
         unsigned long long tot;
         const unsigned long long excl = block_excl_scan(cnt, s_w, tot);
-        if (w == 0) {
+        if (d.ablate & kAblFanLookback) {
+            if (threadIdx.x == 0) s_base = (unsigned long long)tile * kTPB * 8;
+        } else if (w == 0) {
             const unsigned long long b = lookback(d.g_msg, tile, d.tag, tot, d.ctrl);
             if (lane == 0) s_base = b;
         }
+        s_off[threadIdx.x] = (uint32_t)excl;
+        s_src[threadIdx.x] = src;
+        s_rank[threadIdx.x] = rank;
         __syncthreads();
-        const unsigned long long off = s_base + excl;
+        const unsigned long long base = s_base;
         if (i < total) {
-            d.msg_off[i] = (uint32_t)off;
+            d.msg_off[i] = (uint32_t)(base + excl);
             bytes += 4;
-            if (off + cnt > (unsigned long long)d.msg_cap) {
-                atomicOr(&d.ctrl->err, kErrMsgCap);
-            } else if (fl & NFK_PUBLIC) {
-                unsigned long long p = off;
-                for (int j = 0; j < np; j++) {
-                    const int32_t r = d.pl_slot[pb + j];
-                    if (r == slot) continue;
-                    d.msg_rcpt[p++] = (uint32_t)r;
+        }
+        if (base + tot > (unsigned long long)d.msg_cap) {
+            if (threadIdx.x == 0) atomicOr(&d.ctrl->err, kErrMsgCap);
+        } else {
+            for (unsigned q = threadIdx.x; q < (unsigned)tot; q += kTPB) {
+                // owner: the last event whose local offset <= q (it has cnt > 0)
+                int lo = 0, hi = kTPB - 1;
+#pragma unroll
+                for (int step = 0; step < 8; step++) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_off[mid] <= q) lo = mid;
+                    else hi = mid - 1;
                 }
-                bytes += 4 * np + 4 * cnt;
-            } else if (cnt) {
-                d.msg_rcpt[off] = (uint32_t)slot;
-                bytes += 4;
+                const int32_t sr = s_src[lo];
+                const uint32_t idx = q - s_off[lo];
+                int32_t r;
+                if (sr < 0) {
+                    r = -1 - sr;
+                } else {
+                    const int32_t rk = s_rank[lo];
+                    r = d.pl_slot[sr + idx + ((rk >= 0 && (int32_t)idx >= rk) ? 1 : 0)];
+                }
+                d.msg_rcpt[base + q] = (uint32_t)r;
             }
+            bytes += 8 * (unsigned)tot / kTPB + ((threadIdx.x < (tot % kTPB)) ? 8 : 0);
         }
         if (tile == ntiles - 1 && threadIdx.x == 0) {
-            d.ctrl->n_msgs = s_base + tot;
-            d.msg_off[total] = (uint32_t)(s_base + tot);
+            d.ctrl->n_msgs = base + tot;
+            d.msg_off[total] = (uint32_t)(base + tot);
         }
         __syncthreads();
     }

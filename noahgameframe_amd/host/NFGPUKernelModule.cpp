@@ -1,0 +1,329 @@
+// NFGPUKernelModule.cpp — host plugin over the C-ABI (see include/NFGPUKernelModule.hpp).
+#include "NFGPUKernelModule.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace nfgpu {
+
+static uint64_t bits_of(double d) { uint64_t u; std::memcpy(&u, &d, 8); return u; }
+static double dbl_of(uint64_t u) { double d; std::memcpy(&d, &u, 8); return d; }
+
+NFGPUKernelModule::NFGPUKernelModule(int capacity, void* hip_stream) : capacity_(capacity), stream_(hip_stream) {}
+
+NFGPUKernelModule::~NFGPUKernelModule() {
+    if (world_) nfk_destroy(world_);
+}
+
+void NFGPUKernelModule::check(int rc, const char* what) const {
+    if (rc != NFK_OK) throw std::runtime_error(std::string(what) + ": " + nfk_last_error());
+}
+
+int NFGPUKernelModule::AddProperty(const std::string& name, TDATA_TYPE type) {
+    if (committed_) throw std::runtime_error("AddProperty after AfterInit");
+    if (type != TDATA_INT && type != TDATA_FLOAT) throw std::runtime_error("frame-path properties are int or float");
+    auto it = prop_id_.find(name);
+    if (it != prop_id_.end()) return it->second;
+    props_.push_back({name, type});
+    prop_id_[name] = (int)props_.size() - 1;
+    return prop_id_[name];
+}
+
+int NFGPUKernelModule::AddClass(const std::string& name) {
+    auto it = class_id_.find(name);
+    if (it != class_id_.end()) return it->second;
+    classes_.push_back({name, {}, {}});
+    class_id_[name] = (int)classes_.size() - 1;
+    return class_id_[name];
+}
+
+void NFGPUKernelModule::SetPropertyFlags(const std::string& cls, const std::string& prop, bool pub, bool priv,
+                                         bool upload) {
+    classes_.at(class_id_.at(cls)).prop_flags[prop] =
+        (pub ? NFK_PUBLIC : 0) | (priv ? NFK_PRIVATE : 0) | (upload ? NFK_UPLOAD : 0);
+}
+
+int NFGPUKernelModule::AddRecord(const std::string& name, int rows, const std::vector<TDATA_TYPE>& cols) {
+    records_.push_back({name, rows, cols});
+    record_id_[name] = (int)records_.size() - 1;
+    return record_id_[name];
+}
+
+void NFGPUKernelModule::SetRecordFlags(const std::string& cls, const std::string& rec, bool pub, bool priv,
+                                       bool upload) {
+    classes_.at(class_id_.at(cls)).record_flags[rec] =
+        (pub ? NFK_PUBLIC : 0) | (priv ? NFK_PRIVATE : 0) | (upload ? NFK_UPLOAD : 0);
+}
+
+void NFGPUKernelModule::AddHeartBeatProgram(const std::string& name, const std::vector<nfk_op>& ops) {
+    if (committed_) throw std::runtime_error("AddHeartBeatProgram after AfterInit");
+    heartbeats_.push_back({name, ops});
+}
+
+// property ids on the device: int properties first, then float ones, each in definition order
+int NFGPUKernelModule::PropertyId(const std::string& name) const {
+    int pid = prop_id_.at(name);
+    int n_int = 0, before_int = 0, before_flt = 0;
+    for (int i = 0; i < (int)props_.size(); i++) {
+        if (props_[i].type == TDATA_INT) {
+            n_int++;
+            if (i < pid) before_int++;
+        } else if (i < pid) {
+            before_flt++;
+        }
+    }
+    return props_[pid].type == TDATA_INT ? before_int : n_int + before_flt;
+}
+
+bool NFGPUKernelModule::Init() { return true; }
+
+bool NFGPUKernelModule::CreateScene(int nSceneID) {
+    if (scenes_.count(nSceneID)) return false;  // NFCKernelModule::CreateScene (KM:981)
+    scenes_[nSceneID] = true;
+    return true;
+}
+
+bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGroupID, const std::string& cls,
+                                     const std::map<std::string, TData>& init) {
+    if (committed_) throw std::runtime_error("objects are created before AfterInit in this round");
+    if (!scenes_.count(nSceneID)) return false;  // "There is no scene" (KM:107)
+    if (obj_of_.count(self)) return false;       // "The object has Exists" (KM:131)
+    auto c = class_id_.find(cls);
+    if (c == class_id_.end()) return false;
+    int o = (int)guids_.size();
+    guids_.push_back(self);
+    obj_of_[self] = o;
+    scene_.push_back(nSceneID);
+    group_.push_back(nGroupID);
+    cls_.push_back((uint8_t)c->second);
+    isplayer_.push_back(cls == "Player");  // NFCKernelModule.cpp:146
+    if (init_.size() < props_.size()) init_.resize(props_.size());
+    for (auto& v : init_) v.push_back(0);
+    for (auto& kv : init) {
+        int p = prop_id_.at(kv.first);
+        init_[p].back() = props_[p].type == TDATA_INT ? (uint64_t)kv.second.GetInt() : bits_of(kv.second.GetFloat());
+    }
+    return true;
+}
+
+bool NFGPUKernelModule::AfterInit() {
+    int n_int = 0, n_flt = 0;
+    for (auto& p : props_) (p.type == TDATA_INT ? n_int : n_flt)++;
+    nfk_config cfg{};
+    cfg.capacity = std::max(capacity_, 1);
+    cfg.n_int = n_int;
+    cfg.n_flt = n_flt;
+    cfg.n_class = (int)classes_.size();
+    cfg.n_kind = (int)heartbeats_.size();
+    cfg.n_rec = (int)records_.size();
+    cfg.stream = stream_;
+    check(nfk_create(&cfg, &world_), "nfk_create");
+    const int np = n_int + n_flt;
+    for (int c = 0; c < (int)classes_.size(); c++) {
+        std::vector<uint8_t> fl(np, 0);
+        for (auto& kv : classes_[c].prop_flags) fl[PropertyId(kv.first)] = kv.second;
+        check(nfk_set_prop_flags(world_, c, fl.data()), "nfk_set_prop_flags");
+    }
+    for (int r = 0; r < (int)records_.size(); r++) {
+        std::vector<uint8_t> ct, fl(classes_.size(), 0);
+        for (auto t : records_[r].cols) ct.push_back(t == TDATA_FLOAT ? 1 : 0);
+        for (int c = 0; c < (int)classes_.size(); c++) {
+            auto it = classes_[c].record_flags.find(records_[r].name);
+            if (it != classes_[c].record_flags.end()) fl[c] = it->second;
+        }
+        check(nfk_define_record(world_, r, records_[r].rows, (int)records_[r].cols.size(), ct.data(), fl.data()),
+              "nfk_define_record");
+    }
+    // schedule names -> kind ids in lexical order (NFMapEx<std::string, NFCScheduleElement> order)
+    std::sort(heartbeats_.begin(), heartbeats_.end(),
+              [](const HeartBeatDef& a, const HeartBeatDef& b) { return a.name < b.name; });
+    for (int k = 0; k < (int)heartbeats_.size(); k++) {
+        hb_id_[heartbeats_[k].name] = k;
+        check(nfk_define_kind(world_, k, heartbeats_[k].ops.data(), (int)heartbeats_[k].ops.size()),
+              "nfk_define_kind");
+    }
+    const int n = (int)guids_.size();
+    std::vector<int64_t> gh(n), gd(n);
+    for (int i = 0; i < n; i++) {
+        gh[i] = guids_[i].nHead64;
+        gd[i] = guids_[i].nData64;
+    }
+    check(nfk_create_objects(world_, n, gh.data(), gd.data(), scene_.data(), group_.data(), cls_.data(),
+                             isplayer_.data()),
+          "nfk_create_objects");
+    for (int p = 0; p < (int)props_.size(); p++)
+        if (p < (int)init_.size() && !init_[p].empty())
+            check(nfk_load_prop(world_, PropertyId(props_[p].name), init_[p].data()), "nfk_load_prop");
+    check(nfk_commit(world_), "nfk_commit");
+    committed_ = true;
+    return true;
+}
+
+int NFGPUKernelModule::ObjectIndex(const NFGUID& g) const {
+    auto it = obj_of_.find(g);
+    return it == obj_of_.end() ? -1 : it->second;
+}
+
+bool NFGPUKernelModule::SetPropertyInt(const NFGUID& self, const std::string& name, int64_t v) {
+    auto it = prop_id_.find(name);
+    if (it == prop_id_.end() || props_[it->second].type != TDATA_INT || ObjectIndex(self) < 0) return false;
+    int32_t pid = PropertyId(name);
+    uint64_t b = (uint64_t)v;
+    return nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) == NFK_OK;
+}
+
+bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& name, double v) {
+    auto it = prop_id_.find(name);
+    if (it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT || ObjectIndex(self) < 0) return false;
+    int32_t pid = PropertyId(name);
+    uint64_t b = bits_of(v);
+    return nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) == NFK_OK;
+}
+
+int64_t NFGPUKernelModule::GetPropertyInt(const NFGUID& self, const std::string& name) {
+    int o = ObjectIndex(self);
+    if (o < 0) return 0;  // NULL_INT (KM:411)
+    std::vector<uint64_t> col(guids_.size());
+    check(nfk_read_prop(world_, PropertyId(name), col.data()), "nfk_read_prop");
+    return (int64_t)col[o];
+}
+
+double NFGPUKernelModule::GetPropertyFloat(const NFGUID& self, const std::string& name) {
+    int o = ObjectIndex(self);
+    if (o < 0) return 0.0;
+    std::vector<uint64_t> col(guids_.size());
+    check(nfk_read_prop(world_, PropertyId(name), col.data()), "nfk_read_prop");
+    return dbl_of(col[o]);
+}
+
+bool NFGPUKernelModule::RegisterCommonPropertyEvent(const PROPERTY_EVENT_FUNCTOR& cb) {
+    common_prop_cb_.push_back(cb);
+    return true;
+}
+bool NFGPUKernelModule::RegisterCommonRecordEvent(const RECORD_EVENT_FUNCTOR& cb) {
+    common_rec_cb_.push_back(cb);
+    return true;
+}
+bool NFGPUKernelModule::AddPropertyEventCallBack(const PROPERTY_SINGLE_EVENT_FUNCTOR& cb) {
+    aoi_prop_cb_.push_back(cb);
+    return true;
+}
+bool NFGPUKernelModule::AddRecordEventCallBack(const RECORD_SINGLE_EVENT_FUNCTOR& cb) {
+    aoi_rec_cb_.push_back(cb);
+    return true;
+}
+
+bool NFGPUKernelModule::AddSchedule(const NFGUID& self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb,
+                                    float fTime, int nCount, int64_t now_ms) {
+    int o = ObjectIndex(self);
+    auto k = hb_id_.find(name);
+    if (o < 0 || k == hb_id_.end()) return false;
+    int32_t kind = k->second;
+    check(nfk_add_schedules(world_, 1, &self.nHead64, &self.nData64, &kind, &fTime, &nCount, &now_ms),
+          "nfk_add_schedules");
+    if (!sched_cb_.count({o, kind})) {  // an existing name keeps its functor (SM:108)
+        sched_cb_[{o, kind}] = cb;
+        sched_time_[{o, kind}] = fTime;
+    }
+    return true;
+}
+
+bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self, const std::string& name) {
+    auto k = hb_id_.find(name);
+    if (ObjectIndex(self) < 0 || k == hb_id_.end()) return false;
+    check(nfk_remove_schedule(world_, self.nHead64, self.nData64, k->second), "nfk_remove_schedule");
+    return true;
+}
+
+bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self) {
+    if (ObjectIndex(self) < 0) return false;
+    check(nfk_remove_all_schedules(world_, self.nHead64, self.nData64), "nfk_remove_all_schedules");
+    return true;
+}
+
+bool NFGPUKernelModule::Execute(int64_t now_ms) {
+    check(nfk_execute(world_, now_ms), "nfk_execute");
+    check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
+    const bool want_events = !common_prop_cb_.empty() || !aoi_prop_cb_.empty() || !common_rec_cb_.empty() ||
+                             !aoi_rec_cb_.empty();
+    // heartbeat functors, (scene, group, guid, name) order, with the reference's arguments
+    if (summary_.n_fired && !sched_cb_.empty()) {
+        std::vector<int32_t> fo(summary_.n_fired), fk(summary_.n_fired), fr(summary_.n_fired);
+        check(nfk_read_fired(world_, fo.data(), fk.data(), fr.data()), "nfk_read_fired");
+        for (int64_t i = 0; i < summary_.n_fired; i++) {
+            auto it = sched_cb_.find({fo[i], fk[i]});
+            if (it != sched_cb_.end())
+                it->second(guids_[fo[i]], heartbeats_[fk[i]].name, sched_time_[{fo[i], fk[i]}], fr[i]);
+        }
+    }
+    if (!want_events) return true;
+    const int64_t ne = summary_.n_prop_events, nr = summary_.n_rec_events;
+    std::vector<int32_t> eo(ne), ep(ne);
+    std::vector<uint64_t> eold(ne), enew(ne);
+    check(nfk_read_events(world_, eo.data(), ep.data(), eold.data(), enew.data()), "nfk_read_events");
+    std::vector<int32_t> ro(nr);
+    std::vector<uint32_t> rrc(nr);
+    std::vector<uint64_t> rold(nr), rnew(nr);
+    check(nfk_read_rec_events(world_, ro.data(), rrc.data(), rold.data(), rnew.data()), "nfk_read_rec_events");
+    std::vector<uint32_t> moff(ne + nr + 1);
+    std::vector<int32_t> mr(summary_.n_msgs);
+    check(nfk_read_fanout(world_, moff.data(), mr.data()), "nfk_read_fanout");
+    // device pid -> definition index (for the name)
+    std::vector<int> def_of(props_.size());
+    for (int p = 0; p < (int)props_.size(); p++) def_of[PropertyId(props_[p].name)] = p;
+    std::vector<NFGUID> rcpt;
+    for (int64_t e = 0; e < ne; e++) {
+        const PropertyDef& pd = props_[def_of[ep[e]]];
+        TData a, b;
+        a.type = b.type = pd.type;
+        if (pd.type == TDATA_INT) {
+            a.i = (int64_t)eold[e];
+            b.i = (int64_t)enew[e];
+        } else {
+            a.f = dbl_of(eold[e]);
+            b.f = dbl_of(enew[e]);
+        }
+        const NFGUID& self = guids_[eo[e]];
+        for (auto& cb : common_prop_cb_) cb(self, pd.name, a, b);
+        if (!aoi_prop_cb_.empty() && moff[e + 1] > moff[e]) {  // AOI.cpp:250: no call for empty lists
+            rcpt.clear();
+            for (uint32_t m = moff[e]; m < moff[e + 1]; m++) rcpt.push_back(guids_[mr[m]]);
+            for (auto& cb : aoi_prop_cb_) cb(self, pd.name, a, b, rcpt);
+        }
+    }
+    for (int64_t e = 0; e < nr; e++) {
+        const int r = rrc[e] >> 16, row = (rrc[e] >> 8) & 0xFF, col = rrc[e] & 0xFF;
+        RECORD_EVENT_DATA ev;
+        ev.nOpType = RECORD_EVENT_DATA::Update;
+        ev.nRow = row;
+        ev.nCol = col;
+        ev.strRecordName = records_[r].name;
+        TData a, b;
+        a.type = b.type = records_[r].cols[col];
+        if (a.type == TDATA_INT) {
+            a.i = (int64_t)rold[e];
+            b.i = (int64_t)rnew[e];
+        } else {
+            a.f = dbl_of(rold[e]);
+            b.f = dbl_of(rnew[e]);
+        }
+        const NFGUID& self = guids_[ro[e]];
+        for (auto& cb : common_rec_cb_) cb(self, ev, a, b);
+        if (!aoi_rec_cb_.empty()) {
+            rcpt.clear();
+            for (uint32_t m = moff[ne + e]; m < moff[ne + e + 1]; m++) rcpt.push_back(guids_[mr[m]]);
+            for (auto& cb : aoi_rec_cb_) cb(self, ev.strRecordName, ev, a, b, rcpt);
+        }
+    }
+    return true;
+}
+
+bool NFGPUKernelModule::BeforeShut() { return true; }
+
+bool NFGPUKernelModule::Shut() {
+    if (world_) nfk_destroy(world_);
+    world_ = nullptr;
+    return true;
+}
+
+}  // namespace nfgpu
