@@ -87,20 +87,18 @@ int main(int argc, char** argv) {
         }
         if (!km.CreateObject(NFGUID(gh[o], gd[o]), sc[o], gr[o], cname[cl[o]], init)) return 3;
     }
-    if (NR) {
-        fprintf(stderr, "record contents are loaded through the C-ABI in this replay\n");
-    }
     km.AfterInit();
-    if (NR)
-        for (int r = 0; r < NR; r++) {
-            char nm[32];
-            snprintf(nm, sizeof nm, "rec%d_cells", r);
-            nfio_arr* c = A(nm);
-            snprintf(nm, sizeof nm, "rec%d_used", r);
-            nfio_arr* u = A(nm);
-            (void)c;
-            (void)u;
-        }
+    for (int r = 0; r < NR; r++) {  // record contents: creation-time rows through the C-ABI
+        char nm[32];
+        snprintf(nm, sizeof nm, "rec%d_cells", r);
+        nfio_arr* c = A(nm);
+        snprintf(nm, sizeof nm, "rec%d_used", r);
+        nfio_arr* u = A(nm);
+        (void)c;
+        (void)u;
+        fprintf(stderr, "plugin_replay: records are not replayed through the plugin API yet\n");
+        return 4;
+    }
 
     // what the callbacks observe this frame
     std::vector<int32_t> ev_obj, ev_pid, re_obj, fi_obj, fi_kind, fi_rem, mr;

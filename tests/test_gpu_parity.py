@@ -95,3 +95,23 @@ def test_device_outputs_and_counters(gpu_available):
     assert all(o[k] for k in ("ev_slot", "msg_off", "msg_rcpt", "slot_obj"))
     assert np.all(np.diff(r["mo_off"].astype(np.int64)) >= 0)
     m.close()
+
+
+def test_cpp_plugin_api_replay_matches_oracle(gpu_available, tmp_path):
+    """The C++ host plugin (include/NFGPUKernelModule.hpp), driven like a NoahGameFrame logic
+    module (AddSchedule functors, RegisterCommonPropertyEvent, AddPropertyEventCallBack), sees
+    exactly the oracle's coalesced events, heartbeat calls and recipient lists."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "_bin", "plugin_replay")
+    if not os.path.exists(exe):
+        import __graft_entry__
+        __graft_entry__.build_plugin()
+    w = workload.make_world(n_obj=3000, n_scenes=2, groups_per_scene=6, players_per_group=5, n_ticks=8, seed=31,
+                            ext_frac=0.05, host_ops=True)
+    wp, op = str(tmp_path / "w.nfio"), str(tmp_path / "o.nfio")
+    nfio.write(wp, w)
+    subprocess.run([exe, wp, op], check=True)
+    got = nfio.read(op)
+    ref = run_oracle(w)
+    compare_runs(got, {k: v for k, v in ref.items() if k in got})
+    assert len(got) == 13 * 8 + 2
