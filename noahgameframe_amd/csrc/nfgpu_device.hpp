@@ -89,6 +89,10 @@ struct Dev {
     const int32_t* seg_pl_off;
     const int32_t* pl_slot;
     const int32_t* pl_rank;  // [cap] rank of a player slot in its group's player list, -1 otherwise
+    // [cap] fan-out descriptor: bits 0-31 first player index of the slot's group in pl_slot,
+    // 32-45 players in the group, 46-59 1 + rank of the slot among them (0 = not a player),
+    // 60-63 class id
+    const uint64_t* fan_desc;
     uint32_t ablate;
     // outputs
     uint32_t* ev_slot; uint32_t* ev_pid; uint64_t* ev_old; uint64_t* ev_new; int64_t ev_cap;

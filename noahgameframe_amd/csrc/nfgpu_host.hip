@@ -437,6 +437,13 @@ int nfk_commit(void* world) {
     }
     seg_pl_off.push_back((int32_t)pl_slot.size());
     w->nseg = nseg;
+    std::vector<uint64_t> fan_desc(N);
+    for (int32_t s = 0; s < N; s++) {
+        const int32_t pb = seg_pl_off[seg_of[s]], np = seg_pl_off[seg_of[s] + 1] - pb;
+        if (np > 0x3FFF) return fail(NFK_ERR_ARG, "more than 16383 players in one scene group");
+        fan_desc[s] = (uint64_t)(uint32_t)pb | ((uint64_t)np << 32) | ((uint64_t)(pl_rank[s] + 1) << 46) |
+                      ((uint64_t)cls_s[s] << 60);
+    }
 
     // device allocation
     Dev& d = w->d;
@@ -472,6 +479,9 @@ int nfk_commit(void* world) {
     ALLOC(w->slot_obj_d, (size_t)cap * 4);
     ALLOC(pl_rank_d, (size_t)cap * 4);
     d.pl_rank = pl_rank_d;
+    uint64_t* fan_desc_d;
+    ALLOC(fan_desc_d, (size_t)cap * 8);
+    d.fan_desc = fan_desc_d;
     {
         const char* ab = getenv("NFGPU_ABLATE");
         d.ablate = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0u;
@@ -536,6 +546,7 @@ int nfk_commit(void* world) {
     HIPCHK(hipMemset(d.s_hot, 0, (size_t)std::max(NK, 1) * cap * sizeof(SchedHot)));
     HIPCHK(hipMemset(d.s_cold, 0, (size_t)std::max(NK, 1) * cap * sizeof(SchedCold)));
     HIPCHK(hipMemcpy(pl_rank_d, pl_rank.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(fan_desc_d, fan_desc.data(), (size_t)N * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(d.e_flags, 0, cap));
     HIPCHK(hipMemset(d.ext_head, 0, (size_t)cap * 4));
     HIPCHK(hipMemset(d.fired_mask, 0, (size_t)cap * 4));
@@ -769,7 +780,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     {
         TimeScope ts(w, KT_FAN);
         const unsigned long long max_tiles = (d.ev_cap + d.re_cap + kTPB - 1) / kTPB;
-        const unsigned nb = (unsigned)std::min<unsigned long long>(std::max<unsigned long long>(max_tiles, 1), 1024);
+        const unsigned nb = (unsigned)std::min<unsigned long long>(std::max<unsigned long long>(max_tiles, 1), 2048);
         hipLaunchKernelGGL(k_fanout, dim3(nb), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
@@ -815,7 +826,7 @@ int nfk_summary_get(void* world, nfk_summary* out) {
         d.tag = w->epoch;
         HIPCHK(hipMemsetAsync(d.g_msg, 0, w->g_msg_n * 8, w->stream));
         const unsigned long long max_tiles = (d.ev_cap + d.re_cap + kTPB - 1) / kTPB;
-        const unsigned nb = (unsigned)std::min<unsigned long long>(std::max<unsigned long long>(max_tiles, 1), 1024);
+        const unsigned nb = (unsigned)std::min<unsigned long long>(std::max<unsigned long long>(max_tiles, 1), 2048);
         hipLaunchKernelGGL(k_fanout, dim3(nb), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(w->stream));

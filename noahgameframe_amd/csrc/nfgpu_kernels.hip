@@ -65,11 +65,12 @@ __global__ void k_post_hostops(const uint32_t* __restrict__ slot, const uint32_t
 }
 
 // ---------------------------------------------------------------------------------
-// Per-entity written-property list, kept in registers (all indices compile-time).
+// Per-entity written-property list: ids and current values in registers (all indices
+// compile-time), frame-start values in LDS (written once per property, read at the diff).
 struct Ent {
     uint32_t pid[NFK_MAX_TOUCH];
-    uint64_t old[NFK_MAX_TOUCH];
     uint64_t cur[NFK_MAX_TOUCH];
+    uint64_t* old;  // LDS, [NFK_MAX_TOUCH][kTPB] with this thread's column
     int n;
     bool ovf;
     unsigned bytes;
@@ -106,9 +107,9 @@ struct Ent {
         for (int j = 0; j < NFK_MAX_TOUCH; j++)
             if (j == n) {
                 pid[j] = p;
-                old[j] = oldv;
                 cur[j] = newv;
             }
+        old[n * kTPB] = oldv;
         n++;
     }
     __device__ __forceinline__ uint64_t getb(uint32_t p) {
@@ -134,33 +135,61 @@ struct Ent {
     }
 };
 
-__device__ __forceinline__ int64_t opnd(Ent& en, const nfk_op& op, int bit, int64_t x) {
-    return (op.flags & bit) ? en.geti((uint32_t)x) : x;
-}
-
+// One heartbeat callback = the kind's program.  Pass 1 issues every operand load of the
+// program at once (independent loads, one memory round trip); pass 2 runs the ops in order,
+// reading a property from the frame's written-property list when an earlier op (or kind, or
+// queued SetProperty) wrote it, else from the prefetched column value.
 __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ tab, int k) {
     const int n = tab->nops[k];
-    for (int i = 0; i < n; i++) {
+    uint64_t pre[NFK_MAX_OPS][4];
+#pragma unroll
+    for (int i = 0; i < NFK_MAX_OPS; i++) {
+        if (i >= n) break;
+        const nfk_op op = tab->ops[k][i];
+        if (op.code != NFK_OP_IADD_CLAMP && op.code != NFK_OP_FLERP && op.code != NFK_OP_FAFFINE) continue;
+        const uint32_t p0 = op.dst;
+        const bool isf = op.code != NFK_OP_IADD_CLAMP;
+        pre[i][0] = isf ? (uint64_t)__double_as_longlong(en.fcol[(size_t)(p0 - en.n_int) * en.cap + en.e])
+                        : (uint64_t)en.icol[(size_t)p0 * en.cap + en.e];
+        en.bytes += 8;
+        if (op.code == NFK_OP_FLERP) {
+            pre[i][1] = (uint64_t)__double_as_longlong(en.fcol[(size_t)(op.a - en.n_int) * en.cap + en.e]);
+            en.bytes += 8;
+        } else if (op.code == NFK_OP_IADD_CLAMP) {
+            if (op.flags & NFK_A_PROP) { pre[i][1] = (uint64_t)en.icol[(size_t)op.a * en.cap + en.e]; en.bytes += 8; }
+            if (op.flags & NFK_LO_PROP) { pre[i][2] = (uint64_t)en.icol[(size_t)op.b * en.cap + en.e]; en.bytes += 8; }
+            if (op.flags & NFK_HI_PROP) { pre[i][3] = (uint64_t)en.icol[(size_t)op.c * en.cap + en.e]; en.bytes += 8; }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NFK_MAX_OPS; i++) {
+        if (i >= n) break;
         const nfk_op op = tab->ops[k][i];
         if (op.code == NFK_OP_IADD_CLAMP) {
-            const int64_t cur = en.geti(op.dst);
-            const int64_t a = opnd(en, op, NFK_A_PROP, op.a);
-            const int64_t lo = opnd(en, op, NFK_LO_PROP, op.b);
-            const int64_t hi = opnd(en, op, NFK_HI_PROP, op.c);
+            uint64_t t;
+            const int64_t cur = en.tget(op.dst, t) ? (int64_t)t : (int64_t)pre[i][0];
+            const int64_t a = (op.flags & NFK_A_PROP) ? (en.tget((uint32_t)op.a, t) ? (int64_t)t : (int64_t)pre[i][1]) : op.a;
+            const int64_t lo = (op.flags & NFK_LO_PROP) ? (en.tget((uint32_t)op.b, t) ? (int64_t)t : (int64_t)pre[i][2]) : op.b;
+            const int64_t hi = (op.flags & NFK_HI_PROP) ? (en.tget((uint32_t)op.c, t) ? (int64_t)t : (int64_t)pre[i][3]) : op.c;
             int64_t v = (int64_t)((uint64_t)cur + (uint64_t)a);
             v = v < lo ? lo : v;
             v = v > hi ? hi : v;
-            en.seti(op.dst, v);
-        } else if (op.code == NFK_OP_FLERP) {
-            const double x = en.getf(op.dst);
-            const double tg = en.getf((uint32_t)op.a);
-            const double dd = tg - x;
-            const double m = dd * __longlong_as_double(op.b);
-            en.setf(op.dst, x + m);
-        } else if (op.code == NFK_OP_FAFFINE) {
-            const double x = en.getf(op.dst);
-            const double m = x * __longlong_as_double(op.a);
-            en.setf(op.dst, m + __longlong_as_double(op.b));
+            if (v != cur) en.tput(op.dst, (uint64_t)cur, (uint64_t)v);  // NFCProperty::SetInt (PR:273)
+        } else if (op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE) {
+            uint64_t t;
+            const double x = __longlong_as_double((long long)(en.tget(op.dst, t) ? t : pre[i][0]));
+            double v;
+            if (op.code == NFK_OP_FLERP) {
+                const double tg = __longlong_as_double((long long)(en.tget((uint32_t)op.a, t) ? t : pre[i][1]));
+                const double dd = tg - x;
+                const double m = dd * __longlong_as_double(op.b);
+                v = x + m;
+            } else {
+                const double m = x * __longlong_as_double(op.a);
+                v = m + __longlong_as_double(op.b);
+            }
+            if (!(fabs(v - x) <= 1e-15))  // NFCProperty::SetFloat (PR:314): IsZeroDouble(v - cur)
+                en.tput(op.dst, (uint64_t)__double_as_longlong(x), (uint64_t)__double_as_longlong(v));
         }
         // record ops run in k_records
     }
@@ -191,6 +220,7 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned long long s_base[2];
     __shared__ unsigned s_bytes;
+    __shared__ uint64_t s_old[NFK_MAX_TOUCH * kTPB];
     if (threadIdx.x == 0) {
         s_vb = atomicAdd(&d.ctrl->ticket_tick, 1u);
         s_bytes = 0;
@@ -205,6 +235,7 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
     const bool live = e < d.N;
     Ent en;
     en.n = 0;
+    en.old = s_old + threadIdx.x;
     en.ovf = false;
     en.bytes = 0;
     en.icol = d.icol;
@@ -272,7 +303,7 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
     uint32_t dmask = 0;
 #pragma unroll
     for (int j = 0; j < NFK_MAX_TOUCH; j++)
-        if (j < en.n && en.cur[j] != en.old[j]) dmask |= 1u << j;
+        if (j < en.n && en.cur[j] != en.old[j * kTPB]) dmask |= 1u << j;
     const unsigned nd = __builtin_popcount(dmask);
     const unsigned nf = __builtin_popcount(fired);
     if (en.ovf) atomicOr(&d.ctrl->err, kErrTouch);
@@ -318,13 +349,11 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
                     best = en.pid[j];
                     bj = j;
                 }
-            uint64_t ov = 0, nv = 0;
+            uint64_t nv = 0;
 #pragma unroll
             for (int j = 0; j < NFK_MAX_TOUCH; j++)
-                if (j == bj) {
-                    ov = en.old[j];
-                    nv = en.cur[j];
-                }
+                if (j == bj) nv = en.cur[j];
+            const uint64_t ov = en.old[bj * kTPB];
             left &= ~(1u << bj);
             if ((long long)pev < d.ev_cap) {
                 d.ev_slot[pev] = (uint32_t)e;
@@ -503,8 +532,14 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
     __shared__ uint32_t s_off[kTPB];
     __shared__ int32_t s_src[kTPB];   // public: first player index in pl_slot; private: -1 - slot
     __shared__ int32_t s_rank[kTPB];  // public: rank of self in the player list to skip, else -1
+    __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
+    __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (blockIdx.x == 0 && threadIdx.x == 0) d.ctrl->ticket_tick = 0;  // this frame's k_tick is complete
+    for (int i = threadIdx.x; i < (int)sizeof(s_pflags) / 4; i += kTPB)
+        ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
+    for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
+        ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
     const unsigned long long nev = d.ctrl->n_ev < (unsigned long long)d.ev_cap ? d.ctrl->n_ev : d.ev_cap;
     const unsigned long long nre = d.ctrl->n_re < (unsigned long long)d.re_cap ? d.ctrl->n_re : d.re_cap;
     const unsigned long long total = nev + nre;
@@ -520,22 +555,24 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
         int32_t src = 0, rank = -1;
         if (i < total) {
             int32_t slot;
-            uint8_t fl;
-            if (i < nev) {
+            uint32_t key;  // property id or record id
+            const bool isprop = i < nev;
+            if (isprop) {
                 slot = (int32_t)d.ev_slot[i];
-                fl = d.tab->pflags[d.cls[slot]][d.ev_pid[i]];
+                key = d.ev_pid[i];
             } else {
                 slot = (int32_t)d.re_slot[i - nev];
-                fl = d.tab->rflags[d.cls[slot]][d.re_rrc[i - nev] >> 16];
+                key = d.re_rrc[i - nev] >> 16;
             }
-            bytes += 4 + 4 + 1;
+            const uint64_t desc = d.fan_desc[slot];
+            bytes += 4 + 4 + 8;
+            const unsigned cls = (unsigned)(desc >> 60);
+            const uint8_t fl = isprop ? s_pflags[cls][key] : s_rflags[cls][key];
             if (fl & NFK_PUBLIC) {  // every player of the group but self, NFGUID order
-                const int seg = d.seg_of[slot];
-                src = d.seg_pl_off[seg];
-                const int np = d.seg_pl_off[seg + 1] - src;
-                rank = d.isplayer[slot] ? d.pl_rank[slot] : -1;
+                src = (int32_t)(uint32_t)desc;
+                const int np = (int)((desc >> 32) & 0x3FFF);
+                rank = (int)((desc >> 46) & 0x3FFF) - 1;
                 cnt = (unsigned)(np - (rank >= 0 ? 1 : 0));
-                bytes += 4 + 8 + 1 + (rank >= 0 ? 4 : 0);
             } else if ((fl & NFK_PRIVATE) && !(fl & NFK_UPLOAD)) {  // self only
                 cnt = 1;
                 src = -1 - slot;
