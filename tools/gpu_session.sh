@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU session: every GPU step has its own time limit; a crash/abort/timeout stops the
 # session (no further GPU work), an ordinary test failure does not.
-# usage: tools/gpu_session.sh <tag> [steps...]   steps: smoke tests bench prof pmc
+# usage: tools/gpu_session.sh <tag> [steps...]
+#   steps: smoke tests bench prof pmc ablate bench3 bench4
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r01}; shift
@@ -20,17 +21,32 @@ run() {  # run <name> <seconds> <cmd...>
     *) echo "fatal rc=$rc in $name, stopping" | tee -a "$OUT/session.log"; exit $rc ;;
   esac
 }
+B="python bench.py --steps 20 --warmup 3 --cpu-baseline off"
 for step in "$@"; do
   case $step in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 900 python -m pytest tests -m gpu -q --maxfail=5 -p no:cacheprovider ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -v --maxfail=5 -p no:cacheprovider \
+             --timeout 300 --timeout-method thread ;;
     bench) run bench 600 python bench.py --steps 50 --warmup 5 ;;
+    bench3) run bench3 600 python bench.py --config 3 --steps 50 --warmup 5 --cpu-baseline off ;;
+    bench4) run bench4 600 python bench.py --config 4 --steps 50 --warmup 5 --cpu-baseline off ;;
+    ablate) run ablate 600 python tools/ablate.py ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
              python bench.py --steps 50 --warmup 5 --cpu-baseline off ;;
-    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-             python bench.py --steps 20 --warmup 3 --cpu-baseline off &&
-           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-             python bench.py --steps 20 --warmup 3 --cpu-baseline off ;;
+    pmc)
+      run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o run -- \
+        tools/_bin/pmc_calib
+      run calib_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib_write" -o run -- \
+        tools/_bin/pmc_calib
+      run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $B
+      run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $B
+      run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+        SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE \
+        --output-format csv -d "$OUT/pmc_sq" -o run -- $B
+      ALG="$OUT/bench.log"; [ -f "$ALG" ] || ALG=""
+      run pmc_summary 60 python tools/pmc_summary.py --calib "$OUT/calib_fetch" "$OUT/calib_write" \
+        --bench "$OUT/pmc_fetch" "$OUT/pmc_write" --sq "$OUT/pmc_sq" ${ALG:+--alg "$ALG"} \
+        --out "$OUT/pmc_traffic.json" ;;
     *) echo "unknown step $step" ;;
   esac
 done
