@@ -47,7 +47,7 @@ extern "C" {
 #define NFK_UPLOAD 4
 
 /* Heartbeat effect ops.  A reference game registers arbitrary C++ functors
- * with NFIScheduleModule::AddSchedule (SM:236); on the device a heartbeat
+ * with NFIScheduleModule::AddSchedule (SM:218); on the device a heartbeat
  * kind carries a program of these ops, each one a Get + Set through the
  * reference's change predicates (PR:254 SetInt, PR:295 SetFloat, RC:182
  * SetInt, RC:243 SetFloat).
@@ -102,18 +102,36 @@ typedef struct nfk_summary {
     int32_t tick;           /* ticks executed */
 } nfk_summary;
 
-/* Device-resident outputs of the last tick (valid until the next execute). */
+/* Device-resident outputs of the last tick (valid until the next execute).
+ *
+ * Outputs are TILE-STAGED: property events and fired heartbeats are grouped by 256-slot tile
+ * (tile t = slots [256t, 256t+256) in (scene, group, guid) order), record events by 64-slot
+ * record tile.  The i-th output of tile t sits at index t * <x>_tile_cap + i, for
+ * i < <x>_base[t+1] - <x>_base[t]; its rank in the global order is <x>_base[t] + i.  Walking
+ * tiles in order and each tile's entries in order gives exactly the reference order:
+ *   property events  (scene, group, guid, prop)
+ *   record events    (scene, group, guid, rec, row, col); rrc = rec<<16 | row<<8 | col
+ *   fired heartbeats (scene, group, guid, kind)
+ * Fan-out (GetBroadCastObject recipients) is a dense CSR over the virtual event stream
+ * [property events ++ record events] in that order: ev_moff / re_moff hold the global index
+ * in msg_rcpt of the event's first recipient; its recipients end where the next event's begin
+ * (n_msgs after the last).  Recipients are slots; slot_obj maps slot -> object index.
+ * nfk_read_* return the same data as dense arrays in object-index terms. */
 typedef struct nfk_outputs {
-    /* dirty property events, ordered by (scene, group, guid, prop) */
+    int32_t n_tiles, tile_slots;     /* property / fired tiles (tile_slots = 256) */
+    int32_t n_rtiles, rtile_slots;   /* record-event tiles (rtile_slots = 64) */
+    int64_t ev_tile_cap, fi_tile_cap, re_tile_cap;
+    const uint32_t* ev_base;   /* [n_tiles + 1]  exclusive scan of per-tile event counts */
+    const uint32_t* fi_base;   /* [n_tiles + 1] */
+    const uint32_t* re_base;   /* [n_rtiles + 1] */
+    const uint32_t* msg_base;  /* [n_tiles + n_rtiles + 1] first message of each tile */
     const uint32_t* ev_slot; const uint32_t* ev_pid; const uint64_t* ev_old; const uint64_t* ev_new;
-    /* dirty record cells, ordered by (scene, group, guid, rec, row, col); rrc = rec<<16|row<<8|col */
+    const uint32_t* ev_moff;
     const uint32_t* re_slot; const uint32_t* re_rrc; const uint64_t* re_old; const uint64_t* re_new;
-    /* fired heartbeats, ordered by (scene, group, guid, kind) */
+    const uint32_t* re_moff;
     const uint32_t* fi_slot; const uint32_t* fi_kind; const int32_t* fi_remain;
-    /* fan-out CSR over [prop events ++ record events]: msg_off[n_ev+n_re+1], recipients = slots */
-    const uint32_t* msg_off; const uint32_t* msg_rcpt;
-    /* slot -> object index */
-    const int32_t* slot_obj;
+    const uint32_t* msg_rcpt; /* dense [n_msgs] */
+    const int32_t* slot_obj;  /* slot -> object index */
 } nfk_outputs;
 
 /* ---- lifetime: NFCKernelModule ctor/Init/AfterInit (KM:17,51,1490) ---- */
@@ -127,7 +145,7 @@ int nfk_set_prop_flags(void* world, int32_t cls, const uint8_t* flags /* [n_int+
 int nfk_define_record(void* world, int32_t rec, int32_t rows, int32_t cols,
                       const uint8_t* col_types /* [cols] 0=int64 1=f64 */,
                       const uint8_t* flags_per_class /* [n_class] */);
-/* heartbeat kind program; replaces the functor passed to AddSchedule (SM:236) */
+/* heartbeat kind program; replaces the functor passed to AddSchedule (SM:218) */
 int nfk_define_kind(void* world, int32_t kind, const nfk_op* ops, int32_t n_ops);
 
 /* ---- objects: NFCKernelModule::CreateObject (KM:101) ---- */
@@ -147,14 +165,14 @@ int nfk_commit(void* world);
 int nfk_set_props(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
                   const int32_t* pid, const uint64_t* bits);
 
-/* ---- heartbeats: NFIScheduleModule (SM:236,255,260,266) ---- */
+/* ---- heartbeats: NFIScheduleModule (SM:218,240,245,251) ---- */
 int nfk_add_schedules(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
                       const int32_t* kind, const float* interval_s, const int32_t* count,
                       const int64_t* now_ms);
 int nfk_remove_schedule(void* world, int64_t guid_head, int64_t guid_data, int32_t kind);
 int nfk_remove_all_schedules(void* world, int64_t guid_head, int64_t guid_data);
 
-/* ---- one server frame: NFCScheduleModule::Execute (SM:45) + NFCKernelModule::Execute (KM:70)
+/* ---- one server frame: NFCScheduleModule::Execute (SM:49) + NFCKernelModule::Execute (KM:70)
  * + NFCSceneAOIModule::OnPropertyCommonEvent/GetBroadCastObject fan-out (AOI:227,260,531).
  * Asynchronous on the world's stream. */
 int nfk_execute(void* world, int64_t now_ms);
@@ -170,12 +188,15 @@ int nfk_read_schedules(void* world, int64_t* next_ms, int32_t* remain, uint8_t* 
 int nfk_read_events(void* world, int32_t* ev_obj, int32_t* ev_pid, uint64_t* ev_old, uint64_t* ev_new);
 int nfk_read_rec_events(void* world, int32_t* re_obj, uint32_t* re_rrc, uint64_t* re_old, uint64_t* re_new);
 int nfk_read_fired(void* world, int32_t* fi_obj, int32_t* fi_kind, int32_t* fi_remain);
+/* dense CSR over [prop events ++ record events]: msg_off[n_ev + n_re + 1], recipients as objects */
 int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj);
 
 /* ---- measurement ---- */
 int nfk_set_profiling(void* world, int32_t on);
-/* accumulated device time (ms) and launch count per kernel: 0 tick, 1 record, 2 fanout, 3 aux */
-int nfk_kernel_times(void* world, double* ms /* [4] */, int64_t* launches /* [4] */, int64_t* bytes /* [4] */);
+/* accumulated device time (ms), launch count and algorithmic bytes per kernel:
+ * 0 k_tick, 1 k_records, 2 k_fanout, 3 aux (queued host calls), 4 k_scan_tiles */
+#define NFK_N_KERNEL_TIMERS 5
+int nfk_kernel_times(void* world, double* ms /* [5] */, int64_t* launches /* [5] */, int64_t* bytes /* [5] */);
 int nfk_reset_kernel_times(void* world);
 
 #ifdef __cplusplus

@@ -7,18 +7,17 @@
 
 namespace nfgpu {
 
-constexpr int kTPB = 256;                 // 4 waves of 64
-constexpr unsigned kSpinLimit = 1u << 22; // bounded spins (~0.2 s) before the error word is set
+constexpr int kTPB = 256;     // 4 waves of 64
+constexpr int kTile = 256;    // slots per property/fired tile (one k_tick workgroup)
+constexpr int kRTile = 64;    // slots per record-event tile (one k_records wave)
 
 // device error word bits (Ctrl::err)
-constexpr unsigned kErrSpin = 1, kErrEvCap = 2, kErrMsgCap = 4, kErrTouch = 8, kErrFiCap = 16, kErrReCap = 32;
+constexpr unsigned kErrMsgCap = 4, kErrTouch = 8;
 
-// Control block.  Tickets are reset in-kernel by a later kernel of the same frame (k_fanout
-// resets k_tick's, k_tick resets k_records'/k_fanout's); totals are overwritten by the last
-// virtual block; the error word is sticky until nfk_summary_get clears it.  Look-back
-// granules carry a per-frame tag, so nothing is memset per frame.
+// Control block: frame totals written by k_scan_tiles, byte tallies accumulated across frames,
+// the error word is sticky until nfk_summary_get clears it.
 struct alignas(64) Ctrl {
-    unsigned ticket_tick, ticket_rec, ticket_fan, err;                  // 16 B
+    unsigned err, pad_u[3];                                             // 16 B
     unsigned long long n_ev, n_fi, n_re, n_msgs;                        // 32 B
     unsigned long long pad0, pad1;                                      // 16 B
     unsigned long long bytes_tick, bytes_rec, bytes_fan, pad2;          // accumulated across frames
@@ -38,7 +37,7 @@ struct alignas(16) SchedCold {
 };
 
 // timing-only ablations (NFGPU_ABLATE env var); outputs are wrong when set
-constexpr unsigned kAblTickLookback = 1, kAblFanLookback = 2, kAblPrograms = 4;
+constexpr unsigned kAblPrograms = 4;
 
 // record op compiled from the kind programs, sorted by (rec, col)
 struct RecOp {
@@ -59,10 +58,10 @@ struct Tables {
 
 // Everything a kernel needs, passed by value.
 struct Dev {
-    int32_t N, cap, n_int, n_flt, n_kind, n_rec;
+    int32_t N, cap, n_int, n_flt, n_kind, n_rec, n_class;
     int64_t now;
-    uint32_t tag;
     int32_t has_recops;
+    int32_t has_pre;     // RemoveSchedule(self, name) calls are queued this frame (e_flags live)
     const Tables* tab;
     Ctrl* ctrl;
     // SoA entity columns, column-major [col][cap]
@@ -83,27 +82,29 @@ struct Dev {
     uint64_t* rcells[NFK_MAX_RECORDS];
     uint64_t* rused[NFK_MAX_RECORDS];
     // membership (slots sorted by (scene, group, guid))
-    const int32_t* seg_of;
-    const uint8_t* cls;
-    const uint8_t* isplayer;
-    const int32_t* seg_pl_off;
     const int32_t* pl_slot;
-    const int32_t* pl_rank;  // [cap] rank of a player slot in its group's player list, -1 otherwise
     // [cap] fan-out descriptor: bits 0-31 first player index of the slot's group in pl_slot,
     // 32-45 players in the group, 46-59 1 + rank of the slot among them (0 = not a player),
     // 60-63 class id
     const uint64_t* fan_desc;
     uint32_t ablate;
-    // outputs
-    uint32_t* ev_slot; uint32_t* ev_pid; uint64_t* ev_old; uint64_t* ev_new; int64_t ev_cap;
-    uint32_t* fi_slot; uint32_t* fi_kind; int32_t* fi_remain; int64_t fi_cap;
-    uint32_t* re_slot; uint32_t* re_rrc; uint64_t* re_old; uint64_t* re_new; int64_t re_cap;
-    uint32_t* msg_off; uint32_t* msg_rcpt; int64_t msg_cap;
-    // look-back granules
-    unsigned long long* g_ev;
-    unsigned long long* g_fi;
-    unsigned long long* g_re;
-    unsigned long long* g_msg;
+    // tiles: property/fired tile t = slots [t*kTile, (t+1)*kTile); record tile r = slots
+    // [r*kRTile, (r+1)*kRTile).  Outputs of a tile sit at [t*tile_cap, t*tile_cap + count).
+    int32_t n_tiles, n_rtiles;
+    int32_t ev_tcap, fi_tcap, re_tcap;
+    uint32_t* t_ev;    // [n_tiles] dirty property events per tile (k_tick)
+    uint32_t* t_fi;    // [n_tiles] fired heartbeats per tile (k_tick)
+    uint32_t* t_re;    // [n_rtiles] dirty record cells per record tile (k_records)
+    uint32_t* t_msg;   // [n_tiles + n_rtiles] fan-out messages per tile (prop tiles, then record tiles)
+    uint32_t* ev_base; // [n_tiles + 1] exclusive scans (k_scan_tiles)
+    uint32_t* fi_base; // [n_tiles + 1]
+    uint32_t* re_base; // [n_rtiles + 1]
+    uint32_t* msg_base;// [n_tiles + n_rtiles + 1]
+    // outputs (tile-staged)
+    uint32_t* ev_slot; uint32_t* ev_pid; uint64_t* ev_old; uint64_t* ev_new; uint32_t* ev_moff;
+    uint32_t* fi_slot; uint32_t* fi_kind; int32_t* fi_remain;
+    uint32_t* re_slot; uint32_t* re_rrc; uint64_t* re_old; uint64_t* re_new; uint32_t* re_moff;
+    uint32_t* msg_rcpt; int64_t msg_cap;
 };
 
 // ---------------- 64-lane primitives ----------------
@@ -133,65 +134,26 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_u64(v, m);
     return v;
 }
-
-// ---------------- decoupled look-back (single-pass ordered compaction) ----------------
-// Granule = {tag:16 | status:2 | value:46}, one 8-byte relaxed agent-scope store (sc1):
-// the data is the flag (MI355X guide, Guideline 16 recipe R2).  Polls are relaxed
-// agent-scope loads; a bounded spin sets the error word instead of hanging.
-constexpr unsigned long long kStAgg = 1, kStInc = 2;
-__device__ __forceinline__ unsigned long long gmk(unsigned tag, unsigned long long st, unsigned long long v) {
-    return ((unsigned long long)(tag & 0xFFFF) << 48) | (st << 46) | (v & ((1ull << 46) - 1));
-}
-__device__ __forceinline__ void gstore(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long gload(unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Called by all 64 lanes of ONE wave.  Publishes `agg` for virtual block `vb`,
-// returns the exclusive prefix of all blocks before it, publishes the inclusive value.
-__device__ __forceinline__ unsigned long long lookback(unsigned long long* gran, unsigned vb, unsigned tag,
-                                                       unsigned long long agg, Ctrl* ctrl) {
+__device__ __forceinline__ unsigned wave_incl_scan_u32(unsigned v) {
     const int lane = threadIdx.x & 63;
-    if (vb == 0) {
-        if (lane == 0) gstore(&gran[0], gmk(tag, kStInc, agg));
-        return 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        unsigned t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
     }
-    if (lane == 0) gstore(&gran[vb], gmk(tag, kStAgg, agg));
-    unsigned long long excl = 0;
-    long long base = (long long)vb - 1;
-    unsigned spins = 0;
-    while (true) {
-        const long long idx = base - lane;
-        bool valid = true, inc = true;
-        unsigned long long v = 0;
-        if (idx >= 0) {
-            const unsigned long long g = gload(&gran[idx]);
-            const unsigned gt = (unsigned)(g >> 48);
-            const unsigned long long st = (g >> 46) & 3;
-            valid = gt == (tag & 0xFFFF) && st != 0;
-            inc = st == kStInc;
-            v = g & ((1ull << 46) - 1);
-        }
-        const unsigned long long incmask = __ballot(valid && inc);
-        const unsigned long long invmask = __ballot(!valid);
-        const int first_inc = incmask ? __builtin_ctzll(incmask) : 64;
-        const unsigned long long need = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1);
-        if (invmask & need) {
-            if (++spins > kSpinLimit) {
-                if (lane == 0) atomicOr(&ctrl->err, kErrSpin);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        excl += wave_sum(lane <= first_inc ? v : 0ull);
-        if (first_inc < 64) break;
-        base -= 64;
+    return v;
+}
+
+// Recipients of one dirty event (NFCSceneAOIModule::GetBroadCastObject, AOI:531-593):
+// public -> every player of the group but self; private && !upload -> self; else none.
+__device__ __forceinline__ unsigned event_msgs(uint64_t desc, uint8_t fl) {
+    if (fl & NFK_PUBLIC) {
+        const unsigned np = (unsigned)((desc >> 32) & 0x3FFF);
+        const unsigned r1 = (unsigned)((desc >> 46) & 0x3FFF);
+        return np - (r1 ? 1u : 0u);
     }
-    if (lane == 0) gstore(&gran[vb], gmk(tag, kStInc, excl + agg));
-    return excl;
+    if ((fl & NFK_PRIVATE) && !(fl & NFK_UPLOAD)) return 1;
+    return 0;
 }
 
 }  // namespace nfgpu

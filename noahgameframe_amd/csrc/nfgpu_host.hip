@@ -51,7 +51,7 @@ int dalloc(T** p, size_t n) {
     return NFK_OK;
 }
 
-enum { KT_TICK = 0, KT_REC = 1, KT_FAN = 2, KT_AUX = 3 };
+enum { KT_TICK = 0, KT_REC = 1, KT_FAN = 2, KT_AUX = 3, KT_SCAN = 4, KT_N = 5 };
 
 struct PendingTiming {
     int kind;
@@ -86,8 +86,10 @@ struct World {
     Ctrl* ctrl = nullptr;
     int32_t* slot_obj_d = nullptr;
     int32_t nseg = 0;
-    size_t g_ev_n = 0, g_fi_n = 0, g_re_n = 0, g_msg_n = 0;
     std::vector<void*> allocs;
+    // dense readback scratch (nfk_read_*), grown on demand
+    void* dense = nullptr;
+    size_t dense_cap = 0;
 
     // queued calls
     struct XOp { uint32_t slot, pid; uint64_t bits; };
@@ -103,15 +105,14 @@ struct World {
     void* stage = nullptr;
     size_t stage_cap = 0;
 
-    uint32_t epoch = 0;
     int32_t ticks = 0;
 
     bool profiling = false;
     std::vector<PendingTiming> pend;
     std::vector<hipEvent_t> evpool;
-    double kt_ms[4] = {0, 0, 0, 0};
-    int64_t kt_n[4] = {0, 0, 0, 0};
-    int64_t kt_bytes[4] = {0, 0, 0, 0};
+    double kt_ms[KT_N] = {};
+    int64_t kt_n[KT_N] = {};
+    int64_t kt_bytes[KT_N] = {};
     uint64_t last_bytes[3] = {0, 0, 0};
 };
 
@@ -207,6 +208,36 @@ int lookup(World* w, int64_t h, int64_t d, int32_t* obj) {
     return NFK_OK;
 }
 
+// dense scratch for readback, at least `bytes`
+int dense_reserve(World* w, size_t bytes) {
+    if (bytes <= w->dense_cap) return NFK_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    if (w->dense) HIPCHK(hipFree(w->dense));
+    w->dense = nullptr;
+    HIPCHK(hipMalloc(&w->dense, bytes));
+    w->dense_cap = bytes;
+    return NFK_OK;
+}
+
+// tile-staged src -> host array in global order (n entries)
+template <typename T>
+int gather_tiles(World* w, const T* src, const uint32_t* base, int n_tiles, int tcap, size_t n, T* host) {
+    if (n == 0 || n_tiles == 0) return NFK_OK;
+    int r = dense_reserve(w, n * sizeof(T));
+    if (r) return r;
+    const unsigned nb = (unsigned)std::min(n_tiles, 4096);
+    hipLaunchKernelGGL(k_compact<T>, dim3(nb), dim3(kTPB), 0, w->stream, src, (T*)w->dense, base, n_tiles, tcap);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(host, w->dense, n * sizeof(T), hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    return NFK_OK;
+}
+#define GATHER(...)                    \
+    do {                               \
+        int _r = gather_tiles(__VA_ARGS__); \
+        if (_r) return _r;             \
+    } while (0)
+
 }  // namespace
 
 extern "C" {
@@ -253,6 +284,7 @@ int nfk_destroy(void* world) {
     for (void* p : w->allocs) (void)hipFree(p);
     if (w->pin) (void)hipHostFree(w->pin);
     if (w->stage) (void)hipFree(w->stage);
+    if (w->dense) (void)hipFree(w->dense);
     for (auto& p : w->pend) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -419,7 +451,7 @@ int nfk_commit(void* world) {
     w->slot_of_obj.resize(N);
     for (int32_t s = 0; s < N; s++) w->slot_of_obj[w->obj_of_slot[s]] = s;
     std::vector<int32_t> seg_of(N), seg_pl_off, pl_slot, pl_rank(N, -1);
-    std::vector<uint8_t> cls_s(N), ip_s(N);
+    std::vector<uint8_t> cls_s(N);
     int32_t nseg = 0;
     for (int32_t s = 0; s < N; s++) {
         int32_t o = w->obj_of_slot[s];
@@ -429,7 +461,6 @@ int nfk_commit(void* world) {
         }
         seg_of[s] = nseg - 1;
         cls_s[s] = w->cls[o];
-        ip_s[s] = w->isplayer[o];
         if (w->isplayer[o]) {
             pl_rank[s] = (int32_t)pl_slot.size() - seg_pl_off.back();
             pl_slot.push_back(s);
@@ -453,6 +484,7 @@ int nfk_commit(void* world) {
     d.n_flt = NF;
     d.n_kind = NK;
     d.n_rec = NR;
+    d.n_class = w->cfg.n_class;
     d.has_recops = nro > 0;
     ALLOC(w->tab_d, sizeof(Tables));
     ALLOC(w->ctrl, sizeof(Ctrl));
@@ -469,16 +501,9 @@ int nfk_commit(void* world) {
         ALLOC(d.rcells[r], (size_t)cap * w->tab.rec_rows[r] * w->tab.rec_cols[r] * 8);
         ALLOC(d.rused[r], (size_t)cap * 8);
     }
-    int32_t *seg_of_d, *seg_pl_off_d, *pl_slot_d, *pl_rank_d;
-    uint8_t *cls_d, *ip_d;
-    ALLOC(seg_of_d, (size_t)cap * 4);
-    ALLOC(cls_d, cap);
-    ALLOC(ip_d, cap);
-    ALLOC(seg_pl_off_d, seg_pl_off.size() * 4);
+    int32_t* pl_slot_d;
     ALLOC(pl_slot_d, std::max<size_t>(pl_slot.size(), 1) * 4);
     ALLOC(w->slot_obj_d, (size_t)cap * 4);
-    ALLOC(pl_rank_d, (size_t)cap * 4);
-    d.pl_rank = pl_rank_d;
     uint64_t* fan_desc_d;
     ALLOC(fan_desc_d, (size_t)cap * 8);
     d.fan_desc = fan_desc_d;
@@ -486,37 +511,39 @@ int nfk_commit(void* world) {
         const char* ab = getenv("NFGPU_ABLATE");
         d.ablate = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0u;
     }
-    d.seg_of = seg_of_d;
-    d.cls = cls_d;
-    d.isplayer = ip_d;
-    d.seg_pl_off = seg_pl_off_d;
     d.pl_slot = pl_slot_d;
-    d.ev_cap = (int64_t)cap * std::min(NFK_MAX_TOUCH, std::max(w->n_prop, 1));
-    d.fi_cap = (int64_t)cap * std::max(NK, 1);
-    d.re_cap = (int64_t)cap * (int64_t)std::max<size_t>(rec_events_per_ent, 1);
+    // tiles (sized for the committed population; objects after commit are not supported)
+    d.n_tiles = (N + kTile - 1) / kTile;
+    d.n_rtiles = (N + kRTile - 1) / kRTile;
+    d.ev_tcap = kTile * std::min(NFK_MAX_TOUCH, std::max(w->n_prop, 1));
+    d.fi_tcap = kTile * std::max(NK, 1);
+    d.re_tcap = (int32_t)(kRTile * std::max<size_t>(rec_events_per_ent, 1));
+    const size_t nt = std::max(d.n_tiles, 1), nrt = std::max(d.n_rtiles, 1);
+    const size_t ev_n = nt * d.ev_tcap, fi_n = nt * d.fi_tcap, re_n = nro ? nrt * d.re_tcap : 1;
+    ALLOC(d.t_ev, nt * 4);
+    ALLOC(d.t_fi, nt * 4);
+    ALLOC(d.t_re, nrt * 4);
+    ALLOC(d.t_msg, (nt + nrt) * 4);
+    ALLOC(d.ev_base, (nt + 1) * 4);
+    ALLOC(d.fi_base, (nt + 1) * 4);
+    ALLOC(d.re_base, (nrt + 1) * 4);
+    ALLOC(d.msg_base, (nt + nrt + 1) * 4);
     d.msg_cap = w->cfg.msg_capacity > 0 ? w->cfg.msg_capacity : (int64_t)cap * 32;
     if (d.msg_cap > 0xFFFFFFFFll) return fail(NFK_ERR_ARG, "msg_capacity must fit 32-bit offsets");
-    ALLOC(d.ev_slot, d.ev_cap * 4);
-    ALLOC(d.ev_pid, d.ev_cap * 4);
-    ALLOC(d.ev_old, d.ev_cap * 8);
-    ALLOC(d.ev_new, d.ev_cap * 8);
-    ALLOC(d.fi_slot, d.fi_cap * 4);
-    ALLOC(d.fi_kind, d.fi_cap * 4);
-    ALLOC(d.fi_remain, d.fi_cap * 4);
-    ALLOC(d.re_slot, d.re_cap * 4);
-    ALLOC(d.re_rrc, d.re_cap * 4);
-    ALLOC(d.re_old, d.re_cap * 8);
-    ALLOC(d.re_new, d.re_cap * 8);
-    ALLOC(d.msg_off, (d.ev_cap + d.re_cap + 1) * 4);
+    ALLOC(d.ev_slot, ev_n * 4);
+    ALLOC(d.ev_pid, ev_n * 4);
+    ALLOC(d.ev_old, ev_n * 8);
+    ALLOC(d.ev_new, ev_n * 8);
+    ALLOC(d.ev_moff, ev_n * 4);
+    ALLOC(d.fi_slot, fi_n * 4);
+    ALLOC(d.fi_kind, fi_n * 4);
+    ALLOC(d.fi_remain, fi_n * 4);
+    ALLOC(d.re_slot, re_n * 4);
+    ALLOC(d.re_rrc, re_n * 4);
+    ALLOC(d.re_old, re_n * 8);
+    ALLOC(d.re_new, re_n * 8);
+    ALLOC(d.re_moff, re_n * 4);
     ALLOC(d.msg_rcpt, d.msg_cap * 4);
-    w->g_ev_n = (cap + kTPB - 1) / kTPB;
-    w->g_fi_n = w->g_ev_n;
-    w->g_re_n = (cap + 3) / 4;
-    w->g_msg_n = (d.ev_cap + d.re_cap + kTPB - 1) / kTPB;
-    ALLOC(d.g_ev, w->g_ev_n * 8);
-    ALLOC(d.g_fi, w->g_fi_n * 8);
-    ALLOC(d.g_re, w->g_re_n * 8);
-    ALLOC(d.g_msg, w->g_msg_n * 8);
     d.tab = w->tab_d;
     d.ctrl = w->ctrl;
 
@@ -545,19 +572,18 @@ int nfk_commit(void* world) {
     }
     HIPCHK(hipMemset(d.s_hot, 0, (size_t)std::max(NK, 1) * cap * sizeof(SchedHot)));
     HIPCHK(hipMemset(d.s_cold, 0, (size_t)std::max(NK, 1) * cap * sizeof(SchedCold)));
-    HIPCHK(hipMemcpy(pl_rank_d, pl_rank.data(), (size_t)N * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(fan_desc_d, fan_desc.data(), (size_t)N * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(d.e_flags, 0, cap));
     HIPCHK(hipMemset(d.ext_head, 0, (size_t)cap * 4));
     HIPCHK(hipMemset(d.fired_mask, 0, (size_t)cap * 4));
-    HIPCHK(hipMemset(d.g_ev, 0, w->g_ev_n * 8));
-    HIPCHK(hipMemset(d.g_fi, 0, w->g_fi_n * 8));
-    HIPCHK(hipMemset(d.g_re, 0, w->g_re_n * 8));
-    HIPCHK(hipMemset(d.g_msg, 0, w->g_msg_n * 8));
-    HIPCHK(hipMemcpy(seg_of_d, seg_of.data(), (size_t)N * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(cls_d, cls_s.data(), N, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(ip_d, ip_s.data(), N, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(seg_pl_off_d, seg_pl_off.data(), seg_pl_off.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(d.t_ev, 0, nt * 4));
+    HIPCHK(hipMemset(d.t_fi, 0, nt * 4));
+    HIPCHK(hipMemset(d.t_re, 0, nrt * 4));
+    HIPCHK(hipMemset(d.t_msg, 0, (nt + nrt) * 4));
+    HIPCHK(hipMemset(d.ev_base, 0, (nt + 1) * 4));
+    HIPCHK(hipMemset(d.fi_base, 0, (nt + 1) * 4));
+    HIPCHK(hipMemset(d.re_base, 0, (nrt + 1) * 4));
+    HIPCHK(hipMemset(d.msg_base, 0, (nt + nrt + 1) * 4));
     if (!pl_slot.empty()) HIPCHK(hipMemcpy(pl_slot_d, pl_slot.data(), pl_slot.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(w->slot_obj_d, w->obj_of_slot.data(), (size_t)N * 4, hipMemcpyHostToDevice));
     // creation-time values are now on the device
@@ -736,17 +762,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     w->xops.clear();
     w->hops.clear();
 
-    // ---- per-frame control: tickets/totals zeroed, fresh look-back tag ----
-    w->epoch++;
-    if (w->epoch > 0xFFFF) {
-        HIPCHK(hipMemsetAsync(d.g_ev, 0, w->g_ev_n * 8, w->stream));
-        HIPCHK(hipMemsetAsync(d.g_fi, 0, w->g_fi_n * 8, w->stream));
-        HIPCHK(hipMemsetAsync(d.g_re, 0, w->g_re_n * 8, w->stream));
-        HIPCHK(hipMemsetAsync(d.g_msg, 0, w->g_msg_n * 8, w->stream));
-        w->epoch = 1;
-    }
-    d.tag = w->epoch;
-
+    d.has_pre = npre > 0;
     if (nx || npre) {
         TimeScope ts(w, KT_AUX);
         if (nx)
@@ -758,15 +774,14 @@ int nfk_execute(void* world, int64_t now_ms) {
                                d.e_flags, d.s_hot, d.n_kind, d.cap);
         HIPCHK(hipGetLastError());
     }
-    const unsigned nb_tick = (unsigned)((d.N + kTPB - 1) / kTPB);
-    if (nb_tick) {
+    if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
-        hipLaunchKernelGGL(k_tick, dim3(nb_tick), dim3(kTPB), 0, w->stream, d);
+        hipLaunchKernelGGL(k_tick, dim3((unsigned)d.n_tiles), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
-    if (d.has_recops && d.N) {
+    if (d.has_recops && d.n_rtiles) {
         TimeScope ts(w, KT_REC);
-        hipLaunchKernelGGL(k_records, dim3((unsigned)((d.N + 3) / 4)), dim3(kTPB), 0, w->stream, d);
+        hipLaunchKernelGGL(k_records, dim3((unsigned)((d.n_rtiles + 3) / 4)), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
     if (npost) {
@@ -778,10 +793,14 @@ int nfk_execute(void* world, int64_t now_ms) {
         HIPCHK(hipGetLastError());
     }
     {
+        TimeScope ts(w, KT_SCAN);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanTPB), 0, w->stream, d);
+        HIPCHK(hipGetLastError());
+    }
+    const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0);
+    if (nfan) {
         TimeScope ts(w, KT_FAN);
-        const unsigned long long max_tiles = (d.ev_cap + d.re_cap + kTPB - 1) / kTPB;
-        const unsigned nb = (unsigned)std::min<unsigned long long>(std::max<unsigned long long>(max_tiles, 1), 2048);
-        hipLaunchKernelGGL(k_fanout, dim3(nb), dim3(kTPB), 0, w->stream, d);
+        hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
     w->ticks++;
@@ -808,8 +827,9 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     w->last_bytes[1] = c.bytes_rec;
     w->last_bytes[2] = c.bytes_fan;
     if ((c.err & kErrMsgCap) && !(c.err & ~kErrMsgCap)) {
-        // The fan-out kernel only reads the (complete) event stream and the membership CSR, so
-        // grow the message buffer to the exact total it counted and re-run it for this frame.
+        // k_fanout wrote nothing (it checks the scanned total first) and only reads the event
+        // tiles and the membership CSR, so grow the message buffer to the exact total and
+        // re-run it for this frame.
         const int64_t need = (int64_t)c.n_msgs + (int64_t)c.n_msgs / 4 + 1024;
         if (need > 0xFFFFFFFFll) return fail(NFK_ERR_CAPACITY, "fan-out exceeds 2^32 messages per frame");
         HIPCHK(hipFree(w->d.msg_rcpt));
@@ -817,17 +837,10 @@ int nfk_summary_get(void* world, nfk_summary* out) {
         int r = alloc_track(w, (void**)&w->d.msg_rcpt, (size_t)need * 4);
         if (r) return r;
         w->d.msg_cap = need;
-        Ctrl z{};
-        z.n_ev = c.n_ev;
-        z.n_fi = c.n_fi;
-        z.n_re = c.n_re;
-        HIPCHK(hipMemcpy(w->ctrl, &z, 64, hipMemcpyHostToDevice));
+        HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
         Dev d = w->d;
-        d.tag = w->epoch;
-        HIPCHK(hipMemsetAsync(d.g_msg, 0, w->g_msg_n * 8, w->stream));
-        const unsigned long long max_tiles = (d.ev_cap + d.re_cap + kTPB - 1) / kTPB;
-        const unsigned nb = (unsigned)std::min<unsigned long long>(std::max<unsigned long long>(max_tiles, 1), 2048);
-        hipLaunchKernelGGL(k_fanout, dim3(nb), dim3(kTPB), 0, w->stream, d);
+        const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0);
+        hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(w->stream));
         HIPCHK(hipMemcpy(&c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
@@ -836,9 +849,8 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     out->device_error = (int32_t)c.err;
     out->tick = w->ticks;
     if (c.err) HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
-    if (c.err & kErrSpin) return fail(NFK_ERR_DEVICE, "device look-back spin limit exceeded");
     if (c.err & kErrTouch) return fail(NFK_ERR_TOUCH, "device touch list overflow");
-    if (c.err & (kErrEvCap | kErrMsgCap | kErrFiCap | kErrReCap))
+    if (c.err & kErrMsgCap)
         return fail(NFK_ERR_CAPACITY, "device output capacity exceeded (err=" + std::to_string(c.err) + ")");
     return NFK_OK;
 }
@@ -848,10 +860,14 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     if (!w || !o) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     const Dev& d = w->d;
-    o->ev_slot = d.ev_slot; o->ev_pid = d.ev_pid; o->ev_old = d.ev_old; o->ev_new = d.ev_new;
-    o->re_slot = d.re_slot; o->re_rrc = d.re_rrc; o->re_old = d.re_old; o->re_new = d.re_new;
+    o->n_tiles = d.n_tiles; o->tile_slots = kTile;
+    o->n_rtiles = d.has_recops ? d.n_rtiles : 0; o->rtile_slots = kRTile;
+    o->ev_tile_cap = d.ev_tcap; o->fi_tile_cap = d.fi_tcap; o->re_tile_cap = d.re_tcap;
+    o->ev_base = d.ev_base; o->fi_base = d.fi_base; o->re_base = d.re_base; o->msg_base = d.msg_base;
+    o->ev_slot = d.ev_slot; o->ev_pid = d.ev_pid; o->ev_old = d.ev_old; o->ev_new = d.ev_new; o->ev_moff = d.ev_moff;
+    o->re_slot = d.re_slot; o->re_rrc = d.re_rrc; o->re_old = d.re_old; o->re_new = d.re_new; o->re_moff = d.re_moff;
     o->fi_slot = d.fi_slot; o->fi_kind = d.fi_kind; o->fi_remain = d.fi_remain;
-    o->msg_off = d.msg_off; o->msg_rcpt = d.msg_rcpt;
+    o->msg_rcpt = d.msg_rcpt;
     o->slot_obj = w->slot_obj_d;
     return NFK_OK;
 }
@@ -912,18 +928,17 @@ int nfk_read_schedules(void* world, int64_t* next_ms, int32_t* remain, uint8_t* 
 int nfk_read_events(void* world, int32_t* ev_obj, int32_t* ev_pid, uint64_t* ev_old, uint64_t* ev_new) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     Ctrl c;
     int r = read_ctrl(w, &c);
     if (r) return r;
     const Dev& d = w->d;
-    size_t n = std::min<unsigned long long>(c.n_ev, d.ev_cap);
+    const size_t n = c.n_ev;
     std::vector<uint32_t> sl(n);
-    if (n) {
-        HIPCHK(hipMemcpy(sl.data(), d.ev_slot, n * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(ev_pid, d.ev_pid, n * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(ev_old, d.ev_old, n * 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(ev_new, d.ev_new, n * 8, hipMemcpyDeviceToHost));
-    }
+    GATHER(w, d.ev_slot, d.ev_base, d.n_tiles, d.ev_tcap, n, sl.data());
+    GATHER(w, d.ev_pid, d.ev_base, d.n_tiles, d.ev_tcap, n, (uint32_t*)ev_pid);
+    GATHER(w, d.ev_old, d.ev_base, d.n_tiles, d.ev_tcap, n, ev_old);
+    GATHER(w, d.ev_new, d.ev_base, d.n_tiles, d.ev_tcap, n, ev_new);
     for (size_t i = 0; i < n; i++) ev_obj[i] = w->obj_of_slot[sl[i]];
     return NFK_OK;
 }
@@ -931,18 +946,17 @@ int nfk_read_events(void* world, int32_t* ev_obj, int32_t* ev_pid, uint64_t* ev_
 int nfk_read_rec_events(void* world, int32_t* re_obj, uint32_t* re_rrc, uint64_t* re_old, uint64_t* re_new) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     Ctrl c;
     int r = read_ctrl(w, &c);
     if (r) return r;
     const Dev& d = w->d;
-    size_t n = std::min<unsigned long long>(c.n_re, d.re_cap);
+    const size_t n = c.n_re;
     std::vector<uint32_t> sl(n);
-    if (n) {
-        HIPCHK(hipMemcpy(sl.data(), d.re_slot, n * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(re_rrc, d.re_rrc, n * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(re_old, d.re_old, n * 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(re_new, d.re_new, n * 8, hipMemcpyDeviceToHost));
-    }
+    GATHER(w, d.re_slot, d.re_base, d.n_rtiles, d.re_tcap, n, sl.data());
+    GATHER(w, d.re_rrc, d.re_base, d.n_rtiles, d.re_tcap, n, re_rrc);
+    GATHER(w, d.re_old, d.re_base, d.n_rtiles, d.re_tcap, n, re_old);
+    GATHER(w, d.re_new, d.re_base, d.n_rtiles, d.re_tcap, n, re_new);
     for (size_t i = 0; i < n; i++) re_obj[i] = w->obj_of_slot[sl[i]];
     return NFK_OK;
 }
@@ -950,17 +964,16 @@ int nfk_read_rec_events(void* world, int32_t* re_obj, uint32_t* re_rrc, uint64_t
 int nfk_read_fired(void* world, int32_t* fi_obj, int32_t* fi_kind, int32_t* fi_remain) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     Ctrl c;
     int r = read_ctrl(w, &c);
     if (r) return r;
     const Dev& d = w->d;
-    size_t n = std::min<unsigned long long>(c.n_fi, d.fi_cap);
+    const size_t n = c.n_fi;
     std::vector<uint32_t> sl(n);
-    if (n) {
-        HIPCHK(hipMemcpy(sl.data(), d.fi_slot, n * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(fi_kind, d.fi_kind, n * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(fi_remain, d.fi_remain, n * 4, hipMemcpyDeviceToHost));
-    }
+    GATHER(w, d.fi_slot, d.fi_base, d.n_tiles, d.fi_tcap, n, sl.data());
+    GATHER(w, d.fi_kind, d.fi_base, d.n_tiles, d.fi_tcap, n, (uint32_t*)fi_kind);
+    GATHER(w, d.fi_remain, d.fi_base, d.n_tiles, d.fi_tcap, n, fi_remain);
     for (size_t i = 0; i < n; i++) fi_obj[i] = w->obj_of_slot[sl[i]];
     return NFK_OK;
 }
@@ -968,13 +981,16 @@ int nfk_read_fired(void* world, int32_t* fi_obj, int32_t* fi_kind, int32_t* fi_r
 int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     Ctrl c;
     int r = read_ctrl(w, &c);
     if (r) return r;
+    if (c.n_msgs > (unsigned long long)w->d.msg_cap) return fail(NFK_ERR_CAPACITY, "call nfk_summary_get first");
     const Dev& d = w->d;
-    size_t ne = std::min<unsigned long long>(c.n_ev, d.ev_cap) + std::min<unsigned long long>(c.n_re, d.re_cap);
-    size_t nm = std::min<unsigned long long>(c.n_msgs, d.msg_cap);
-    HIPCHK(hipMemcpy(msg_off, d.msg_off, (ne + 1) * 4, hipMemcpyDeviceToHost));
+    GATHER(w, d.ev_moff, d.ev_base, d.n_tiles, d.ev_tcap, (size_t)c.n_ev, msg_off);
+    if (d.has_recops) GATHER(w, d.re_moff, d.re_base, d.n_rtiles, d.re_tcap, (size_t)c.n_re, msg_off + c.n_ev);
+    msg_off[c.n_ev + c.n_re] = (uint32_t)c.n_msgs;
+    const size_t nm = c.n_msgs;
     std::vector<uint32_t> rc(nm);
     if (nm) HIPCHK(hipMemcpy(rc.data(), d.msg_rcpt, nm * 4, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < nm; i++) msg_rcpt_obj[i] = w->obj_of_slot[rc[i]];
@@ -1001,7 +1017,7 @@ int nfk_kernel_times(void* world, double* ms, int64_t* launches, int64_t* bytes)
         w->kt_bytes[1] = (int64_t)c.bytes_rec;
         w->kt_bytes[2] = (int64_t)c.bytes_fan;
     }
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < KT_N; i++) {
         ms[i] = w->kt_ms[i];
         launches[i] = w->kt_n[i];
         bytes[i] = w->kt_bytes[i];
@@ -1014,7 +1030,7 @@ int nfk_reset_kernel_times(void* world) {
     if (!w) return fail(NFK_ERR_ARG, "null world");
     int r = drain_timings(w);
     if (r) return r;
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < KT_N; i++) {
         w->kt_ms[i] = 0;
         w->kt_n[i] = 0;
     }

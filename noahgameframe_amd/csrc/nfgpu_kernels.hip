@@ -2,16 +2,19 @@
 //
 //   k_ext_scatter   index queued SetProperty* calls by slot
 //   k_pre_hostops   RemoveSchedule(self[, name]) effects that precede the scan
-//   k_tick          heartbeat timer scan (NFCScheduleModule::Execute, SM:45-80) + effect
+//   k_tick          heartbeat timer scan (NFCScheduleModule::Execute, SM:49-81) + effect
 //                   programs + property change predicates (NFCProperty::SetInt/SetFloat,
-//                   PR:254/295) + dirty diff + ordered compaction of dirty events and fired
-//                   heartbeats (wave ballot/scan + decoupled look-back)
+//                   PR:254/295) + dirty diff; dirty events and fired heartbeats are compacted
+//                   per 256-slot tile (wave ballot/scan + block scan, no inter-block chain) and
+//                   each event's fan-out message count is scanned in the same pass
 //   k_records       record-cell effects (NFCRecord::SetInt/SetFloat, RC:182/243) + diff,
-//                   one wave per entity, lane = row
-//   k_post_hostops  remove list then add list (SM:82-117)
-//   k_fanout        GetBroadCastObject recipient lists (AOI:531-593) for every dirty event,
-//                   CSR over the (scene, group, guid)-sorted slots, LDS-staged so message
-//                   stores are coalesced
+//                   one wave per 64-slot record tile, lane = row
+//   k_post_hostops  remove list then add list (SM:83-119)
+//   k_scan_tiles    exclusive scans of the per-tile counts (events, fired, record events,
+//                   messages) -> tile bases and frame totals
+//   k_fanout        GetBroadCastObject recipient lists (AOI:531-593) for every dirty event:
+//                   one workgroup per tile, LDS owner search so message stores are coalesced
+//   k_compact_*     readback only: tile-staged outputs -> dense arrays
 //
 // Compiled with -ffp-contract=off: f64 effects round exactly like the reference's C++.
 #include "nfgpu_device.hpp"
@@ -49,7 +52,7 @@ __global__ void k_post_hostops(const uint32_t* __restrict__ slot, const uint32_t
     SchedHot h = d.s_hot[at];
     if (op[i] & 1) h.state = 0;
     if (op[i] & 4) d.e_flags[s] = 0;
-    if ((op[i] & 2) && !(h.state & 1)) {  // AddSchedule (SM:236): an existing name wins
+    if ((op[i] & 2) && !(h.state & 1)) {  // AddSchedule (SM:218): an existing name wins
         const float f = interval[i];
         const int32_t c = count[i];
         h.state = 1u | (c < 0 ? 2u : 0u);
@@ -195,7 +198,8 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
     }
 }
 
-// Block-wide exclusive scan of a packed pair of 32-bit counts (sums stay < 2^32 per block).
+
+// Block-wide exclusive scan of a packed 64-bit value (fields must not overflow into each other).
 __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v, unsigned long long* s_w,
                                                               unsigned long long& total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -215,24 +219,22 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
 
 constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
 
+// One thread per slot, one workgroup per 256-slot tile.  Outputs of tile t are written densely
+// at [t * tile_cap, t * tile_cap + count); k_scan_tiles turns the counts into global ranks.
 __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
-    __shared__ unsigned s_vb;
     __shared__ unsigned long long s_w[kTPB / 64];
-    __shared__ unsigned long long s_base[2];
     __shared__ unsigned s_bytes;
     __shared__ uint64_t s_old[NFK_MAX_TOUCH * kTPB];
-    if (threadIdx.x == 0) {
-        s_vb = atomicAdd(&d.ctrl->ticket_tick, 1u);
-        s_bytes = 0;
-        if (blockIdx.x == 0) {  // last frame's k_records / k_fanout are complete
-            d.ctrl->ticket_rec = 0;
-            d.ctrl->ticket_fan = 0;
-        }
-    }
-    __syncthreads();
-    const unsigned vb = s_vb;
-    const int e = (int)(vb * kTPB + threadIdx.x);
+    __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
+    const int tile = blockIdx.x;
+    const int e = tile * kTile + (int)threadIdx.x;
     const bool live = e < d.N;
+    if (threadIdx.x == 0) s_bytes = 0;
+    {
+        const int words = d.n_class * (NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS) / 4;
+        for (int i = threadIdx.x; i < words; i += kTPB)
+            ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
+    }
     Ent en;
     en.n = 0;
     en.old = s_old + threadIdx.x;
@@ -245,23 +247,31 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
     en.e = live ? e : 0;
     uint32_t fired = 0;
     uint32_t xh = 0;
+    uint64_t desc = 0;
     if (live) {
+        desc = d.fan_desc[e];  // independent of everything below: issued first
+        en.bytes += 8;
         // 1. SetProperty* calls queued before this frame, in call order
-        xh = d.ext_head[e];
-        en.bytes += 4;
-        if (xh) {
-            for (int i = (int)xh - 1; i < d.n_x && d.x_slot[i] == (uint32_t)e; i++) {
-                const uint32_t pid = d.x_pid[i];
-                const uint64_t b = d.x_bits[i];
-                en.bytes += 16;
-                if ((int)pid < d.n_int) en.seti(pid, (int64_t)b);
-                else en.setf(pid, __longlong_as_double((long long)b));
+        if (d.n_x) {
+            xh = d.ext_head[e];
+            en.bytes += 4;
+            if (xh) {
+                for (int i = (int)xh - 1; i < d.n_x && d.x_slot[i] == (uint32_t)e; i++) {
+                    const uint32_t pid = d.x_pid[i];
+                    const uint64_t b = d.x_bits[i];
+                    en.bytes += 16;
+                    if ((int)pid < d.n_int) en.seti(pid, (int64_t)b);
+                    else en.setf(pid, __longlong_as_double((long long)b));
+                }
             }
         }
-        // 2. NFCScheduleModule::Execute (SM:45-80): this object's schedules in name order.
+        // 2. NFCScheduleModule::Execute (SM:51-81): this object's schedules in name order.
         //    The hot records of a chunk of kinds are loaded together (independent 16 B loads).
-        bool taken = d.e_flags[e] & 1;  // std::map remove-list key already owned (SM:72)
-        en.bytes += 1;
+        bool taken = false;  // std::map remove-list key already owned (SM:68)
+        if (d.has_pre) {
+            taken = d.e_flags[e] & 1;
+            en.bytes += 1;
+        }
         for (int k0 = 0; k0 < d.n_kind; k0 += kKindChunk) {
             SchedHot h[kKindChunk];
 #pragma unroll
@@ -299,34 +309,30 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
                 if ((fired >> k) & 1) run_program(en, d.tab, k);
         }
     }
-    // 4. dirty diff: written properties whose bits changed since the frame began
+    __syncthreads();  // s_pflags
+    // 4. dirty diff: written properties whose bits changed since the frame began, and the
+    //    fan-out message count of each dirty event
     uint32_t dmask = 0;
+    unsigned nmsg = 0;
+    const unsigned cls = (unsigned)(desc >> 60);
 #pragma unroll
     for (int j = 0; j < NFK_MAX_TOUCH; j++)
-        if (j < en.n && en.cur[j] != en.old[j * kTPB]) dmask |= 1u << j;
+        if (j < en.n && en.cur[j] != en.old[j * kTPB]) {
+            dmask |= 1u << j;
+            nmsg += event_msgs(desc, s_pflags[cls][en.pid[j]]);
+        }
     const unsigned nd = __builtin_popcount(dmask);
     const unsigned nf = __builtin_popcount(fired);
     if (en.ovf) atomicOr(&d.ctrl->err, kErrTouch);
 
-    // 5. ordered compaction: block scan + look-back (events chain on wave 0, fired chain on wave 1)
+    // 5. tile-local compaction: one block scan of (fired:16 | events:16 | messages:32)
     unsigned long long tot;
-    const unsigned long long excl = block_excl_scan(((unsigned long long)nf << 32) | nd, s_w, tot);
-    const int w = threadIdx.x >> 6;
-    if (d.ablate & kAblTickLookback) {
-        if (threadIdx.x == 0) {
-            s_base[0] = (unsigned long long)vb * kTPB * NFK_MAX_TOUCH;
-            s_base[1] = (unsigned long long)vb * kTPB * d.n_kind;
-        }
-    } else if (w == 0) {
-        const unsigned long long b = lookback(d.g_ev, vb, d.tag, tot & 0xFFFFFFFFull, d.ctrl);
-        if ((threadIdx.x & 63) == 0) s_base[0] = b;
-    } else if (w == 1) {
-        const unsigned long long b = lookback(d.g_fi, vb, d.tag, tot >> 32, d.ctrl);
-        if ((threadIdx.x & 63) == 0) s_base[1] = b;
-    }
-    __syncthreads();
-    unsigned long long pev = s_base[0] + (excl & 0xFFFFFFFFull);
-    unsigned long long pfi = s_base[1] + (excl >> 32);
+    const unsigned long long excl =
+        block_excl_scan(((unsigned long long)nf << 48) | ((unsigned long long)nd << 32) | nmsg, s_w, tot);
+    unsigned pev = (unsigned)((excl >> 32) & 0xFFFF);
+    unsigned pfi = (unsigned)(excl >> 48);
+    unsigned pmsg = (unsigned)excl;
+    const size_t ev0 = (size_t)tile * d.ev_tcap, fi0 = (size_t)tile * d.fi_tcap;
 
     if (live) {
         // write back changed columns
@@ -355,30 +361,26 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
                 if (j == bj) nv = en.cur[j];
             const uint64_t ov = en.old[bj * kTPB];
             left &= ~(1u << bj);
-            if ((long long)pev < d.ev_cap) {
-                d.ev_slot[pev] = (uint32_t)e;
-                d.ev_pid[pev] = best;
-                d.ev_old[pev] = ov;
-                d.ev_new[pev] = nv;
-            } else {
-                atomicOr(&d.ctrl->err, kErrEvCap);
-            }
+            const size_t at = ev0 + pev;
+            d.ev_slot[at] = (uint32_t)e;
+            d.ev_pid[at] = best;
+            d.ev_old[at] = ov;
+            d.ev_new[at] = nv;
+            d.ev_moff[at] = pmsg;  // tile-local; k_fanout adds the tile's message base
+            pmsg += event_msgs(desc, s_pflags[cls][best]);
             pev++;
-            en.bytes += 24;
+            en.bytes += 28;
         }
         uint32_t fl = fired;
         while (fl) {
             const int k = __builtin_ctz(fl);
             fl &= fl - 1;
-            if ((long long)pfi < d.fi_cap) {
-                d.fi_slot[pfi] = (uint32_t)e;
-                d.fi_kind[pfi] = (uint32_t)k;
-                d.fi_remain[pfi] = d.s_hot[(size_t)k * d.cap + e].remain;
-            } else {
-                atomicOr(&d.ctrl->err, kErrFiCap);
-            }
+            const size_t at = fi0 + pfi;
+            d.fi_slot[at] = (uint32_t)e;
+            d.fi_kind[at] = (uint32_t)k;
+            d.fi_remain[at] = d.s_hot[(size_t)k * d.cap + e].remain;
             pfi++;
-            en.bytes += 16;
+            en.bytes += 12;
         }
         if (d.has_recops) {
             d.fired_mask[e] = fired;
@@ -386,251 +388,318 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
         }
         if (xh) d.ext_head[e] = 0;
     }
-    // totals (last virtual block) and algorithmic-byte tally
+    // tile counts and algorithmic-byte tally
     const unsigned wb = (unsigned)wave_sum(en.bytes);
     if ((threadIdx.x & 63) == 0) atomicAdd(&s_bytes, wb);
     __syncthreads();
     if (threadIdx.x == 0) {
-        atomicAdd(&d.ctrl->bytes_tick, (unsigned long long)s_bytes);
-        if (vb == gridDim.x - 1) {
-            d.ctrl->n_ev = s_base[0] + (tot & 0xFFFFFFFFull);
-            d.ctrl->n_fi = s_base[1] + (tot >> 32);
-        }
+        d.t_ev[tile] = (unsigned)((tot >> 32) & 0xFFFF);
+        d.t_fi[tile] = (unsigned)(tot >> 48);
+        d.t_msg[tile] = (unsigned)tot;
+        atomicAdd(&d.ctrl->bytes_tick, (unsigned long long)(s_bytes + 12));
     }
 }
 
 // ---------------------------------------------------------------------------------
-// Record effects: one wave per entity, lane = row.  Cells [cap][cols][rows] so the
-// wave reads one (entity, col) row-vector contiguously.
+// Record effects: one wave per 64-slot record tile, lane = row; the wave walks its slots in
+// order, four at a time with every cell load of the group issued before any is consumed.
+// Cells [cap][cols][rows] so a wave reads one (slot, col) row-vector contiguously.
+constexpr int kRecGroup = 4;
+
 __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
-    __shared__ unsigned s_vb;
-    __shared__ unsigned long long s_w[kTPB / 64];
-    __shared__ unsigned long long s_base;
-    __shared__ unsigned s_bytes;
-    if (threadIdx.x == 0) {
-        s_vb = atomicAdd(&d.ctrl->ticket_rec, 1u);
-        s_bytes = 0;
-    }
+    __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
+    for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
+        ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
     __syncthreads();
-    const unsigned vb = s_vb;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int e = (int)(vb * (kTPB / 64) + w);
+    const int rt = blockIdx.x * (kTPB / 64) + w;
+    if (rt >= d.n_rtiles) return;  // wave-uniform; no barrier follows except the final one below
     const Tables* tab = d.tab;
     const int nro = tab->n_recops;
+    const int s0 = rt * kRTile;
     unsigned bytes = 0;
-    uint32_t mask = 0;
-    if (e < d.N) {
-        mask = d.fired_mask[e];
-        if (lane == 0) bytes += 4;
-    }
-    mask &= tab->kind_has_recop;
-    // apply (at most NFK_MAX_OPS record ops, distinct (rec, col), sorted by (rec, col))
-    bool ch[NFK_MAX_OPS];
-    uint64_t ov[NFK_MAX_OPS], nv[NFK_MAX_OPS];
-#pragma unroll
-    for (int j = 0; j < NFK_MAX_OPS; j++) {
-        ch[j] = false;
-        ov[j] = nv[j] = 0;
-        if (j >= nro || !mask) continue;
-        const RecOp ro = tab->recops[j];
-        if (!((mask >> ro.kind) & 1)) continue;
-        const int rows = tab->rec_rows[ro.rec], cols = tab->rec_cols[ro.rec];
-        const uint64_t used = d.rused[ro.rec][e];
-        if (lane == 0) bytes += 8;
-        if (lane >= rows || !((used >> lane) & 1)) continue;
-        uint64_t* cp = d.rcells[ro.rec] + ((size_t)e * cols + ro.col) * rows + lane;
-        const uint64_t cur = *cp;
-        bytes += 8;
-        uint64_t nb;
-        bool changed;
-        if (ro.code == NFK_OP_RIADD_CLAMP) {
-            int64_t v = (int64_t)(cur + (uint64_t)ro.a);
-            v = v < ro.b ? ro.b : v;
-            v = v > ro.c ? ro.c : v;
-            nb = (uint64_t)v;
-            changed = v != (int64_t)cur;  // TData::operator== (NFIDataList.h:98)
-        } else {
-            const double x = __longlong_as_double((long long)cur);
-            const double m = x * __longlong_as_double(ro.a);
-            const double v = m + __longlong_as_double(ro.b);
-            const double df = v - x;
-            changed = !(df < 0.001 && df > -0.001);  // NFIDataList.h:106-113
-            nb = (uint64_t)__double_as_longlong(v);
-        }
-        if (changed) {
-            *cp = nb;
+    // lane j holds slot s0 + j's fired mask and class
+    uint32_t my_mask = 0;
+    uint64_t my_desc = 0;
+    if (s0 + lane < d.N) {
+        my_mask = d.fired_mask[s0 + lane] & tab->kind_has_recop;
+        bytes += 4;
+        if (my_mask) {
+            my_desc = d.fan_desc[s0 + lane];
             bytes += 8;
-            ch[j] = nb != cur;  // coalesced diff: bits must differ
-            ov[j] = cur;
-            nv[j] = nb;
         }
     }
-    // per-entity event order: (rec, row, col) -> records outer, lanes (rows), cols inner
-    unsigned cnt = 0;
+    unsigned long long work = __ballot(my_mask != 0);
+    unsigned pos = 0, pmsg = 0;  // tile-local
+    const size_t re0 = (size_t)rt * d.re_tcap;
+    while (work) {
+        // next group of up to kRecGroup slots with record work, in slot order
+        int js[kRecGroup];
+        uint32_t masks[kRecGroup];
+        uint64_t used[kRecGroup][NFK_MAX_OPS];
+        uint64_t cur[kRecGroup][NFK_MAX_OPS];
 #pragma unroll
-    for (int j = 0; j < NFK_MAX_OPS; j++) cnt += ch[j] ? 1 : 0;
-    const unsigned long long wtot = wave_sum(cnt);
-    if (lane == 0) s_w[w] = wtot;
-    __syncthreads();
-    unsigned long long before = 0, btot = 0;
+        for (int g = 0; g < kRecGroup; g++) {
+            js[g] = work ? __builtin_ctzll(work) : -1;
+            if (work) work &= work - 1;
+            masks[g] = js[g] >= 0 ? (uint32_t)__shfl((int)my_mask, js[g], 64) : 0u;
+        }
 #pragma unroll
-    for (int i = 0; i < kTPB / 64; i++) {
-        before += (i < w) ? s_w[i] : 0ull;
-        btot += s_w[i];
-    }
-    if (w == 0) {
-        const unsigned long long b = lookback(d.g_re, vb, d.tag, btot, d.ctrl);
-        if (lane == 0) s_base = b;
-    }
-    __syncthreads();
-    unsigned long long pos = s_base + before;
-    int j0 = 0;
-    while (j0 < nro) {
-        const int rec = tab->recops[j0].rec;
-        int j1 = j0;
-        while (j1 < nro && tab->recops[j1].rec == rec) j1++;
-        unsigned c = 0;
+        for (int g = 0; g < kRecGroup; g++)
 #pragma unroll
-        for (int j = 0; j < NFK_MAX_OPS; j++) c += (j >= j0 && j < j1 && ch[j]) ? 1 : 0;
-        const unsigned long long inc = wave_incl_scan(c);
-        unsigned long long p = pos + inc - c;
-#pragma unroll
-        for (int j = 0; j < NFK_MAX_OPS; j++) {
-            if (!(j >= j0 && j < j1 && ch[j])) continue;
-            if ((long long)p < d.re_cap) {
-                d.re_slot[p] = (uint32_t)e;
-                d.re_rrc[p] = ((uint32_t)rec << 16) | ((uint32_t)lane << 8) | (uint32_t)tab->recops[j].col;
-                d.re_old[p] = ov[j];
-                d.re_new[p] = nv[j];
-            } else {
-                atomicOr(&d.ctrl->err, kErrReCap);
+            for (int j = 0; j < NFK_MAX_OPS; j++) {
+                used[g][j] = 0;
+                cur[g][j] = 0;
+                if (j >= nro || js[g] < 0) continue;
+                const RecOp ro = tab->recops[j];
+                if (!((masks[g] >> ro.kind) & 1)) continue;
+                const int e = s0 + js[g];
+                used[g][j] = d.rused[ro.rec][e];
+                const int rows = tab->rec_rows[ro.rec], cols = tab->rec_cols[ro.rec];
+                if (lane < rows) cur[g][j] = d.rcells[ro.rec][((size_t)e * cols + ro.col) * rows + lane];
             }
-            p++;
-            bytes += 24;
+#pragma unroll
+        for (int g = 0; g < kRecGroup; g++) {
+            if (js[g] < 0) break;
+            const int e = s0 + js[g];
+            const uint64_t desc = (uint64_t)__shfl((long long)my_desc, js[g], 64);
+            const unsigned cls = (unsigned)(desc >> 60);
+            bool ch[NFK_MAX_OPS];
+            uint64_t nv[NFK_MAX_OPS];
+#pragma unroll
+            for (int j = 0; j < NFK_MAX_OPS; j++) {
+                ch[j] = false;
+                nv[j] = 0;
+                if (j >= nro) continue;
+                const RecOp ro = tab->recops[j];
+                if (!((masks[g] >> ro.kind) & 1)) continue;
+                const int rows = tab->rec_rows[ro.rec], cols = tab->rec_cols[ro.rec];
+                if (lane == 0) bytes += 8;
+                if (lane >= rows || !((used[g][j] >> lane) & 1)) continue;
+                const uint64_t c = cur[g][j];
+                bytes += 8;
+                uint64_t nb;
+                bool changed;
+                if (ro.code == NFK_OP_RIADD_CLAMP) {
+                    int64_t v = (int64_t)(c + (uint64_t)ro.a);
+                    v = v < ro.b ? ro.b : v;
+                    v = v > ro.c ? ro.c : v;
+                    nb = (uint64_t)v;
+                    changed = v != (int64_t)c;  // TData::operator== (NFIDataList.h:98)
+                } else {
+                    const double x = __longlong_as_double((long long)c);
+                    const double m = x * __longlong_as_double(ro.a);
+                    const double v = m + __longlong_as_double(ro.b);
+                    const double df = v - x;
+                    changed = !(df < 0.001 && df > -0.001);  // NFIDataList.h:106-113
+                    nb = (uint64_t)__double_as_longlong(v);
+                }
+                if (changed) {
+                    d.rcells[ro.rec][((size_t)e * cols + ro.col) * rows + lane] = nb;
+                    bytes += 8;
+                    ch[j] = nb != c;  // coalesced diff: bits must differ
+                    nv[j] = nb;
+                }
+            }
+            // per-slot event order: (rec, row, col) -> records outer, lanes (rows), cols inner
+            int j0 = 0;
+            while (j0 < nro) {
+                const int rec = tab->recops[j0].rec;
+                int j1 = j0;
+                while (j1 < nro && tab->recops[j1].rec == rec) j1++;
+                unsigned c = 0;
+#pragma unroll
+                for (int j = 0; j < NFK_MAX_OPS; j++) c += (j >= j0 && j < j1 && ch[j]) ? 1 : 0;
+                const unsigned inc = wave_incl_scan_u32(c);
+                unsigned p = pos + inc - c;
+                const unsigned per = event_msgs(desc, s_rflags[cls][rec]);
+#pragma unroll
+                for (int j = 0; j < NFK_MAX_OPS; j++) {
+                    if (!(j >= j0 && j < j1 && ch[j])) continue;
+                    const size_t at = re0 + p;
+                    d.re_slot[at] = (uint32_t)e;
+                    d.re_rrc[at] = ((uint32_t)rec << 16) | ((uint32_t)lane << 8) | (uint32_t)tab->recops[j].col;
+                    d.re_old[at] = cur[g][j];
+                    d.re_new[at] = nv[j];
+                    d.re_moff[at] = pmsg + per * (p - pos);
+                    p++;
+                    bytes += 28;
+                }
+                const unsigned n = (unsigned)__shfl((int)inc, 63, 64);
+                pos += n;
+                pmsg += per * n;
+                j0 = j1;
+            }
         }
-        pos += __shfl(inc, 63, 64);
-        j0 = j1;
+    }
+    if (lane == 0) {
+        d.t_re[rt] = pos;
+        d.t_msg[d.n_tiles + rt] = pmsg;
     }
     const unsigned wb = (unsigned)wave_sum(bytes);
-    if (lane == 0) atomicAdd(&s_bytes, wb);
-    __syncthreads();
+    if (lane == 0 && wb) atomicAdd(&d.ctrl->bytes_rec, (unsigned long long)wb + 8);
+}
+
+// ---------------------------------------------------------------------------------
+// Exclusive scans of the per-tile counts: one workgroup of 1024 threads, 4 counts per thread
+// per pass.  Writes bases[n+1] (bases[n] = total) and the frame totals.
+constexpr int kScanTPB = 1024;
+
+__device__ unsigned long long scan_counts(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ base, int n,
+                                          unsigned long long* s_w) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    unsigned long long carry = 0;
+    for (int c0 = 0; c0 < n; c0 += kScanTPB * 4) {
+        unsigned v[4];
+        unsigned long long sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = c0 + tid * 4 + q;
+            v[q] = i < n ? cnt[i] : 0u;
+            sum += v[q];
+        }
+        const unsigned long long inc = wave_incl_scan(sum);
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        unsigned long long before = carry, tot = 0;
+        for (int i = 0; i < kScanTPB / 64; i++) {
+            before += (i < w) ? s_w[i] : 0ull;
+            tot += s_w[i];
+        }
+        unsigned long long run = before + inc - sum;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = c0 + tid * 4 + q;
+            if (i < n) base[i] = (uint32_t)run;
+            run += v[q];
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    if (tid == 0) base[n] = (uint32_t)carry;
+    return carry;
+}
+
+__global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
+    __shared__ unsigned long long s_w[kScanTPB / 64];
+    const unsigned long long nev = scan_counts(d.t_ev, d.ev_base, d.n_tiles, s_w);
+    const unsigned long long nfi = scan_counts(d.t_fi, d.fi_base, d.n_tiles, s_w);
+    unsigned long long nre = 0;
+    if (d.has_recops) nre = scan_counts(d.t_re, d.re_base, d.n_rtiles, s_w);
+    const unsigned long long nm =
+        scan_counts(d.t_msg, d.msg_base, d.n_tiles + (d.has_recops ? d.n_rtiles : 0), s_w);
     if (threadIdx.x == 0) {
-        atomicAdd(&d.ctrl->bytes_rec, (unsigned long long)s_bytes);
-        if (vb == gridDim.x - 1) d.ctrl->n_re = s_base + btot;
+        d.ctrl->n_ev = nev;
+        d.ctrl->n_fi = nfi;
+        d.ctrl->n_re = nre;
+        d.ctrl->n_msgs = nm;
+        if (nm > (unsigned long long)d.msg_cap) atomicOr(&d.ctrl->err, kErrMsgCap);
     }
 }
 
 // ---------------------------------------------------------------------------------
-// Fan-out over the virtual event stream [prop events ++ record events].  Persistent grid,
-// 256-event tiles pulled from a ticket; message offsets by look-back; the tile's recipient
-// lists are expanded cooperatively from an LDS descriptor table so consecutive lanes store
-// consecutive messages.
+// Fan-out: one workgroup per tile (property tiles, then record tiles).  The tile's events are
+// taken 256 at a time; each chunk's recipient lists are expanded cooperatively from an LDS
+// descriptor table so consecutive lanes store consecutive messages.  Also rewrites each
+// event's tile-local message offset as a global one.  Does nothing (and sets no output) when
+// the frame's messages exceed msg_cap: the host grows the buffer and re-runs this kernel.
 __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
-    __shared__ unsigned s_tile;
-    __shared__ unsigned long long s_w[kTPB / 64];
-    __shared__ unsigned long long s_base;
     __shared__ uint32_t s_off[kTPB];
     __shared__ int32_t s_src[kTPB];   // public: first player index in pl_slot; private: -1 - slot
     __shared__ int32_t s_rank[kTPB];  // public: rank of self in the player list to skip, else -1
+    __shared__ uint32_t s_first, s_end;
+    __shared__ unsigned s_bytes;
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (blockIdx.x == 0 && threadIdx.x == 0) d.ctrl->ticket_tick = 0;  // this frame's k_tick is complete
-    for (int i = threadIdx.x; i < (int)sizeof(s_pflags) / 4; i += kTPB)
-        ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
-    for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
-        ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
-    const unsigned long long nev = d.ctrl->n_ev < (unsigned long long)d.ev_cap ? d.ctrl->n_ev : d.ev_cap;
-    const unsigned long long nre = d.ctrl->n_re < (unsigned long long)d.re_cap ? d.ctrl->n_re : d.re_cap;
-    const unsigned long long total = nev + nre;
-    const unsigned long long ntiles = (total + kTPB - 1) / kTPB;
-    unsigned bytes = 0;
-    while (true) {
-        if (threadIdx.x == 0) s_tile = atomicAdd(&d.ctrl->ticket_fan, 1u);
-        __syncthreads();
-        const unsigned tile = s_tile;
-        if (tile >= ntiles) break;
-        const unsigned long long i = (unsigned long long)tile * kTPB + threadIdx.x;
-        unsigned cnt = 0;
+    if (d.ctrl->n_msgs > (unsigned long long)d.msg_cap) return;  // uniform: host re-runs
+    const bool rec = (int)blockIdx.x >= d.n_tiles;
+    const int t = rec ? (int)blockIdx.x - d.n_tiles : (int)blockIdx.x;
+    const uint32_t* base = rec ? d.re_base : d.ev_base;
+    const unsigned cnt = base[t + 1] - base[t];
+    if (cnt == 0) return;  // uniform
+    if (threadIdx.x == 0) s_bytes = 0;
+    if (rec) {
+        for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
+            ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
+    } else {
+        const int words = d.n_class * (NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS) / 4;
+        for (int i = threadIdx.x; i < words; i += kTPB)
+            ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
+    }
+    const uint32_t mbase = d.msg_base[blockIdx.x];
+    const size_t off0 = (size_t)t * (rec ? d.re_tcap : d.ev_tcap);
+    const uint32_t* slots = rec ? d.re_slot : d.ev_slot;
+    uint32_t* moff = rec ? d.re_moff : d.ev_moff;
+    unsigned bytes = 12;
+    __syncthreads();
+    for (unsigned c0 = 0; c0 < cnt; c0 += kTPB) {
+        const unsigned i = c0 + threadIdx.x;
+        const bool valid = i < cnt;
+        unsigned n = 0, lm = 0;
         int32_t src = 0, rank = -1;
-        if (i < total) {
-            int32_t slot;
-            uint32_t key;  // property id or record id
-            const bool isprop = i < nev;
-            if (isprop) {
-                slot = (int32_t)d.ev_slot[i];
-                key = d.ev_pid[i];
-            } else {
-                slot = (int32_t)d.re_slot[i - nev];
-                key = d.re_rrc[i - nev] >> 16;
-            }
+        if (valid) {
+            const int32_t slot = (int32_t)slots[off0 + i];
+            const uint32_t key = rec ? (d.re_rrc[off0 + i] >> 16) : d.ev_pid[off0 + i];
+            lm = moff[off0 + i];
             const uint64_t desc = d.fan_desc[slot];
-            bytes += 4 + 4 + 8;
+            bytes += 4 + 4 + 4 + 8 + 4;
             const unsigned cls = (unsigned)(desc >> 60);
-            const uint8_t fl = isprop ? s_pflags[cls][key] : s_rflags[cls][key];
+            const uint8_t fl = rec ? s_rflags[cls][key] : s_pflags[cls][key];
+            n = event_msgs(desc, fl);
             if (fl & NFK_PUBLIC) {  // every player of the group but self, NFGUID order
                 src = (int32_t)(uint32_t)desc;
-                const int np = (int)((desc >> 32) & 0x3FFF);
                 rank = (int)((desc >> 46) & 0x3FFF) - 1;
-                cnt = (unsigned)(np - (rank >= 0 ? 1 : 0));
-            } else if ((fl & NFK_PRIVATE) && !(fl & NFK_UPLOAD)) {  // self only
-                cnt = 1;
+            } else if (n) {  // self only
                 src = -1 - slot;
             }
+            moff[off0 + i] = mbase + lm;
+            if (i == c0) s_first = lm;
+            if (i + 1 == cnt || threadIdx.x == kTPB - 1) s_end = lm + n;
         }
-        unsigned long long tot;
-        const unsigned long long excl = block_excl_scan(cnt, s_w, tot);
-        if (d.ablate & kAblFanLookback) {
-            if (threadIdx.x == 0) s_base = (unsigned long long)tile * kTPB * 8;
-        } else if (w == 0) {
-            const unsigned long long b = lookback(d.g_msg, tile, d.tag, tot, d.ctrl);
-            if (lane == 0) s_base = b;
-        }
-        s_off[threadIdx.x] = (uint32_t)excl;
+        __syncthreads();
+        const uint32_t first = s_first, total = s_end - first;
+        s_off[threadIdx.x] = valid ? lm - first : total;
         s_src[threadIdx.x] = src;
         s_rank[threadIdx.x] = rank;
         __syncthreads();
-        const unsigned long long base = s_base;
-        if (i < total) {
-            d.msg_off[i] = (uint32_t)(base + excl);
-            bytes += 4;
-        }
-        if (base + tot > (unsigned long long)d.msg_cap) {
-            if (threadIdx.x == 0) atomicOr(&d.ctrl->err, kErrMsgCap);
-        } else {
-            for (unsigned q = threadIdx.x; q < (unsigned)tot; q += kTPB) {
-                // owner: the last event whose local offset <= q (it has cnt > 0)
-                int lo = 0, hi = kTPB - 1;
+        uint32_t* out = d.msg_rcpt + mbase + first;
+        for (unsigned q = threadIdx.x; q < total; q += kTPB) {
+            // owner: the last event whose local offset <= q (it has n > 0)
+            int lo = 0, hi = kTPB - 1;
 #pragma unroll
-                for (int step = 0; step < 8; step++) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (s_off[mid] <= q) lo = mid;
-                    else hi = mid - 1;
-                }
-                const int32_t sr = s_src[lo];
-                const uint32_t idx = q - s_off[lo];
-                int32_t r;
-                if (sr < 0) {
-                    r = -1 - sr;
-                } else {
-                    const int32_t rk = s_rank[lo];
-                    r = d.pl_slot[sr + idx + ((rk >= 0 && (int32_t)idx >= rk) ? 1 : 0)];
-                }
-                d.msg_rcpt[base + q] = (uint32_t)r;
+            for (int step = 0; step < 8; step++) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_off[mid] <= q) lo = mid;
+                else hi = mid - 1;
             }
-            bytes += 8 * (unsigned)tot / kTPB + ((threadIdx.x < (tot % kTPB)) ? 8 : 0);
-        }
-        if (tile == ntiles - 1 && threadIdx.x == 0) {
-            d.ctrl->n_msgs = base + tot;
-            d.msg_off[total] = (uint32_t)(base + tot);
+            const int32_t sr = s_src[lo];
+            const uint32_t idx = q - s_off[lo];
+            int32_t r;
+            if (sr < 0) {
+                r = -1 - sr;
+            } else {
+                const int32_t rk = s_rank[lo];
+                r = d.pl_slot[sr + idx + ((rk >= 0 && (int32_t)idx >= rk) ? 1 : 0)];
+            }
+            out[q] = (uint32_t)r;
+            bytes += 4;
         }
         __syncthreads();
     }
     const unsigned wb = (unsigned)wave_sum(bytes);
-    if (lane == 0 && wb) atomicAdd(&d.ctrl->bytes_fan, (unsigned long long)wb);
-    if (ntiles == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
-        d.ctrl->n_msgs = 0;
-        d.msg_off[0] = 0;
+    if ((threadIdx.x & 63) == 0 && wb) atomicAdd(&s_bytes, wb);
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&d.ctrl->bytes_fan, (unsigned long long)s_bytes);
+}
+
+// ---------------------------------------------------------------------------------
+// Readback only (not part of a frame): tile-staged array -> dense array in global order.
+template <typename T>
+__global__ __launch_bounds__(kTPB) void k_compact(const T* __restrict__ src, T* __restrict__ dst,
+                                                  const uint32_t* __restrict__ base, int n_tiles, int tcap) {
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const uint32_t b = base[t], n = base[t + 1] - b;
+        for (uint32_t i = threadIdx.x; i < n; i += kTPB) dst[b + i] = src[(size_t)t * tcap + i];
     }
 }
 

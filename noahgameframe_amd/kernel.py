@@ -43,9 +43,18 @@ class Summary(ctypes.Structure):
 
 
 class Outputs(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in
-                ["ev_slot", "ev_pid", "ev_old", "ev_new", "re_slot", "re_rrc", "re_old", "re_new",
-                 "fi_slot", "fi_kind", "fi_remain", "msg_off", "msg_rcpt", "slot_obj"]]
+    """nfk_outputs: tile-staged device outputs of the last frame (see include/nfgpu.h)."""
+    _fields_ = ([("n_tiles", ctypes.c_int32), ("tile_slots", ctypes.c_int32), ("n_rtiles", ctypes.c_int32),
+                 ("rtile_slots", ctypes.c_int32), ("ev_tile_cap", ctypes.c_int64), ("fi_tile_cap", ctypes.c_int64),
+                 ("re_tile_cap", ctypes.c_int64)] +
+                [(n, ctypes.c_void_p) for n in
+                 ["ev_base", "fi_base", "re_base", "msg_base", "ev_slot", "ev_pid", "ev_old", "ev_new", "ev_moff",
+                  "re_slot", "re_rrc", "re_old", "re_new", "re_moff", "fi_slot", "fi_kind", "fi_remain",
+                  "msg_rcpt", "slot_obj"]])
+
+
+N_KERNEL_TIMERS = 5
+KERNEL_TIMER_NAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles"]
 
 
 _lib = None
@@ -251,9 +260,9 @@ class NFKernelModule:
         self._chk(self.lib.nfk_set_profiling(self.h, 1 if on else 0))
 
     def kernel_times(self):
-        ms = np.zeros(4, np.float64)
-        n = np.zeros(4, np.int64)
-        b = np.zeros(4, np.int64)
+        ms = np.zeros(N_KERNEL_TIMERS, np.float64)
+        n = np.zeros(N_KERNEL_TIMERS, np.int64)
+        b = np.zeros(N_KERNEL_TIMERS, np.int64)
         self._chk(self.lib.nfk_kernel_times(self.h, _p(ms), _p(n), _p(b)))
         return ms, n, b
 

@@ -13,10 +13,10 @@
  *   set_rint       NFComm/NFCore/NFCRecord.cpp:182-241    (TData::operator== exact)
  *   set_rflt       NFComm/NFCore/NFCRecord.cpp:243-303    (TData::operator== |d| < 0.001,
  *                  NFComm/NFCore/NFIDataList.h:106-113)
- *   sched_execute  NFComm/NFKernelPlugin/NFCScheduleModule.cpp:45-110 (object schedules:
+ *   sched_execute  NFComm/NFKernelPlugin/NFCScheduleModule.cpp:49-119 (object schedules:
  *                  fire test, count, reschedule, std::map remove-list insert quirk,
  *                  remove-then-add order, add dedup by name)
- *   add_schedule   NFComm/NFKernelPlugin/NFCScheduleModule.cpp:236-257
+ *   add_schedule   NFComm/NFKernelPlugin/NFCScheduleModule.cpp:218-238
  *   fanout         NFComm/NFKernelPlugin/NFCSceneAOIModule.cpp:227-290 and 531-593
  *                  (GetBroadCastObject: public -> group players except self in NFGUID
  *                  order (NFCSceneGroupInfo::mxPlayerList, std::map), private&&!upload
@@ -228,7 +228,7 @@ static void log_fired(int32_t obj, int32_t kind, int32_t rem) {
     nfired++;
 }
 
-/* NFCScheduleModule::Execute (SM:45-110), object part.  Object iteration
+/* NFCScheduleModule::Execute (SM:49-119), object part.  Object iteration
  * order does not change state (callbacks only touch their own object). */
 static void sched_execute(int64_t now) {
     for (int32_t o = 0; o < N; o++) {
@@ -414,7 +414,7 @@ int main(int argc, char** argv) {
             } else if (h_op[hi] == 2) {
                 if (pend_rm_kind[o] == -2) pend_rm_kind[o] = h_kind[hi];
             } else if (h_op[hi] == 3) {
-                /* RemoveSchedule(self): immediate erase of the object's map (SM:260) */
+                /* RemoveSchedule(self): immediate erase of the object's map (SM:240) */
                 for (int k = 0; k < NK; k++) S[(int64_t)o * NK + k].present = 0;
             }
             hi++;
@@ -427,7 +427,7 @@ int main(int argc, char** argv) {
             xi++;
         }
         sched_execute(now);
-        /* remove list (SM:82-96) */
+        /* remove list (SM:83-98) */
         for (int64_t o = 0; o < N; o++) {
             if (pend_rm_kind[o] >= 0) S[o * NK + pend_rm_kind[o]].present = 0;
             pend_rm_kind[o] = -2;
@@ -437,7 +437,7 @@ int main(int argc, char** argv) {
                     S[o * NK + k].present = 0;
                 }
         }
-        /* add list (SM:99-117): AddSchedule(SM:236) fields; an existing name wins */
+        /* add list (SM:100-119): AddSchedule(SM:218) fields; an existing name wins */
         for (int64_t i = 0; i < nadds; i++) {
             sched_t* s = &S[(int64_t)adds[i].obj * NK + adds[i].kind];
             if (s->present) continue;

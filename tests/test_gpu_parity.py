@@ -92,7 +92,8 @@ def test_device_outputs_and_counters(gpu_available):
     assert s["n_prop_events"] == len(r["ev_obj"]) and s["n_msgs"] == len(r["mr_obj"])
     assert s["alg_bytes_tick"] > 0 and s["alg_bytes_fan"] > 0
     o = m.outputs()
-    assert all(o[k] for k in ("ev_slot", "msg_off", "msg_rcpt", "slot_obj"))
+    assert all(o[k] for k in ("ev_slot", "ev_moff", "ev_base", "msg_base", "msg_rcpt", "slot_obj"))
+    assert o["n_tiles"] == (5000 + 255) // 256 and o["tile_slots"] == 256 and o["ev_tile_cap"] == 256 * 8
     assert np.all(np.diff(r["mo_off"].astype(np.int64)) >= 0)
     m.close()
 

@@ -12,7 +12,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2,4,7")
+    ap.add_argument("--variants", default="0,4")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--entities", type=int, default=1 << 20)
