@@ -28,8 +28,19 @@ struct alignas(64) Ctrl {
 struct alignas(16) SchedHot {
     int64_t next;    // mnNextTriggerTime
     int32_t remain;  // mnRemainCount
-    uint32_t state;  // bit0 present, bit1 forever (mbForever)
+    uint32_t state;  // kSt* bits below; bits 4..31 = step ms (signed 28-bit) when kStStep
 };
+// SchedHot::state.  The reference reschedules with next = start + step * (all - remain)
+// (SM:71-72, step = (int64)(interval * 1000)).  Between two fires (all - remain) grows by one,
+// so next advances by exactly `step` — except at the first fire after AddSchedule (next stays
+// start + step) and once a forever schedule's remain has wrapped past INT32_MIN (the int32
+// difference wraps).  The hot record therefore carries step and a fired-once bit, and only
+// those two cases (or a step that does not fit 28 bits) read the cold record.
+constexpr uint32_t kStPresent = 1, kStForever = 2, kStFired = 4, kStStep = 8;
+__host__ __device__ __forceinline__ int64_t st_step(uint32_t st) { return (int64_t)((int32_t)st >> 4); }
+__host__ __device__ __forceinline__ uint32_t st_pack_step(int64_t step) {
+    return (step >= -(1ll << 27) && step < (1ll << 27)) ? (kStStep | ((uint32_t)step << 4)) : 0u;
+}
 struct alignas(16) SchedCold {
     int64_t start;   // mnStartTime
     int32_t all;     // mnAllCount
@@ -38,6 +49,7 @@ struct alignas(16) SchedCold {
 
 // timing-only ablations (NFGPU_ABLATE env var); outputs are wrong when set
 constexpr unsigned kAblPrograms = 4;
+constexpr unsigned kAblPerKind = 8;  // not an ablation: force the per-kind operand path (outputs stay exact)
 
 // record op compiled from the kind programs, sorted by (rec, col)
 struct RecOp {
@@ -45,8 +57,17 @@ struct RecOp {
     int64_t a, b, c;
 };
 
+// Frame working set U (k_tick).  Slots [0, kMaxW) hold properties that may be written this
+// frame: the program destinations (fixed at commit, property-id order) followed by this frame's
+// queued-SetProperty properties; slots [kMaxW, kMaxU) hold properties programs only read.
+constexpr int kMaxU = 16, kMaxW = 8;
+constexpr uint8_t kNoU = 0xFF;
+static_assert(kMaxW == NFK_MAX_TOUCH, "writable slots = touch capacity");
+
 struct Tables {
     nfk_op ops[NFK_MAX_KINDS][NFK_MAX_OPS];
+    uint32_t umask[NFK_MAX_KINDS];                 // U slots kind k's program reads or writes
+    uint8_t opu[NFK_MAX_KINDS][NFK_MAX_OPS][4];    // U slot of dst, a, b, c (kNoU = immediate)
     int32_t nops[NFK_MAX_KINDS];
     uint8_t pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     uint8_t rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
@@ -88,6 +109,13 @@ struct Dev {
     // 60-63 class id
     const uint64_t* fan_desc;
     uint32_t ablate;
+    // frame working set (k_tick): properties of the U slots, their columns, writable slots in
+    // property-id order, and the slot of each property queued by SetProperty this frame
+    int32_t n_w;
+    int32_t u_pid[kMaxU];
+    uint64_t* u_col[kMaxU];
+    uint8_t u_order[kMaxW];
+    const uint8_t* u_slot;  // [n_prop], only when n_x > 0
     // tiles: property/fired tile t = slots [t*kTile, (t+1)*kTile); record tile r = slots
     // [r*kRTile, (r+1)*kRTile).  Outputs of a tile sit at [t*tile_cap, t*tile_cap + count).
     int32_t n_tiles, n_rtiles;
@@ -143,6 +171,10 @@ __device__ __forceinline__ unsigned wave_incl_scan_u32(unsigned v) {
     }
     return v;
 }
+
+// fan_desc of a slot that holds no entity (slack of a scene group's slot range)
+constexpr uint64_t kDeadDesc = 0xFull << 60;
+__host__ __device__ __forceinline__ bool desc_dead(uint64_t desc) { return (desc >> 60) == 0xF; }
 
 // Recipients of one dirty event (NFCSceneAOIModule::GetBroadCastObject, AOI:531-593):
 // public -> every player of the group but self; private && !upload -> self; else none.

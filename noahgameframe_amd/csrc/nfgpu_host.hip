@@ -79,6 +79,9 @@ struct World {
     Tables tab{};
     bool kind_defined[NFK_MAX_KINDS] = {};
     uint64_t dst_union_mask[2] = {0, 0};  // properties written by any program (bit per pid)
+    // frame working set of k_tick (Dev::u_*): program destinations / read-only operands
+    bool u_ok = false;
+    std::vector<int> u_wp, u_rp;
     int n_dst_union = 0;
 
     Dev d{};
@@ -434,6 +437,63 @@ int nfk_commit(void* world) {
         if (w->tab.recops[i].rec == w->tab.recops[i - 1].rec && w->tab.recops[i].col == w->tab.recops[i - 1].col)
             return fail(NFK_ERR_ARG, "two record ops on the same (record, col)");
     w->tab.n_recops = nro;
+    // frame working set (k_tick): program destinations -> writable slots [0, n_wp) and
+    // read-only operands -> slots [kMaxW, kMaxW + n_rp), each group in property-id order
+    {
+        std::vector<int> W, R;
+        for (int k = 0; k < NK; k++)
+            for (int i = 0; i < w->tab.nops[k]; i++) {
+                const nfk_op& op = w->tab.ops[k][i];
+                if (op.code == NFK_OP_IADD_CLAMP || op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE)
+                    W.push_back(op.dst);
+            }
+        std::sort(W.begin(), W.end());
+        W.erase(std::unique(W.begin(), W.end()), W.end());
+        auto is_w = [&](int64_t p) { return std::binary_search(W.begin(), W.end(), (int)p); };
+        for (int k = 0; k < NK; k++)
+            for (int i = 0; i < w->tab.nops[k]; i++) {
+                const nfk_op& op = w->tab.ops[k][i];
+                if (op.code == NFK_OP_IADD_CLAMP) {
+                    if ((op.flags & NFK_A_PROP) && !is_w(op.a)) R.push_back((int)op.a);
+                    if ((op.flags & NFK_LO_PROP) && !is_w(op.b)) R.push_back((int)op.b);
+                    if ((op.flags & NFK_HI_PROP) && !is_w(op.c)) R.push_back((int)op.c);
+                } else if (op.code == NFK_OP_FLERP && !is_w(op.a)) {
+                    R.push_back((int)op.a);
+                }
+            }
+        std::sort(R.begin(), R.end());
+        R.erase(std::unique(R.begin(), R.end()), R.end());
+        w->u_ok = (int)W.size() <= kMaxW && (int)R.size() <= kMaxU - kMaxW;
+        w->u_wp.assign(W.begin(), W.end());
+        w->u_rp.assign(R.begin(), R.end());
+        auto slot = [&](int64_t p) -> uint8_t {
+            auto it = std::lower_bound(W.begin(), W.end(), (int)p);
+            if (it != W.end() && *it == p) return (uint8_t)(it - W.begin());
+            it = std::lower_bound(R.begin(), R.end(), (int)p);
+            return (uint8_t)(kMaxW + (it - R.begin()));
+        };
+        for (int k = 0; k < NK && w->u_ok; k++) {
+            w->tab.umask[k] = 0;
+            for (int i = 0; i < w->tab.nops[k]; i++) {
+                const nfk_op& op = w->tab.ops[k][i];
+                uint8_t* u = w->tab.opu[k][i];
+                u[0] = u[1] = u[2] = u[3] = kNoU;
+                if (op.code == NFK_OP_IADD_CLAMP) {
+                    u[0] = slot(op.dst);
+                    if (op.flags & NFK_A_PROP) u[1] = slot(op.a);
+                    if (op.flags & NFK_LO_PROP) u[2] = slot(op.b);
+                    if (op.flags & NFK_HI_PROP) u[3] = slot(op.c);
+                } else if (op.code == NFK_OP_FLERP) {
+                    u[0] = slot(op.dst);
+                    u[1] = slot(op.a);
+                } else if (op.code == NFK_OP_FAFFINE) {
+                    u[0] = slot(op.dst);
+                }
+                for (int q = 0; q < 4; q++)
+                    if (u[q] != kNoU) w->tab.umask[k] |= 1u << u[q];
+            }
+        }
+    }
     w->n_dst_union = __builtin_popcountll(w->dst_union_mask[0]) + __builtin_popcountll(w->dst_union_mask[1]);
     if (w->n_dst_union > NFK_MAX_TOUCH)
         return fail(NFK_ERR_TOUCH, "programs write more than NFK_MAX_TOUCH distinct properties");
@@ -721,6 +781,42 @@ int nfk_execute(void* world, int64_t now_ms) {
         }
     }
 
+    // ---- frame working set of k_tick (Dev::u_*): program slots + this frame's SetProperty
+    //      properties; a frame whose set does not fit runs k_tick_touch instead ----
+    bool use_u = w->u_ok && !(d.ablate & kAblPerKind);
+    std::vector<uint8_t> uslot;
+    if (use_u) {
+        int n_w = (int)w->u_wp.size();
+        for (int j = 0; j < kMaxU; j++) d.u_pid[j] = -1;
+        for (int i = 0; i < n_w; i++) d.u_pid[i] = w->u_wp[i];
+        for (size_t i = 0; i < w->u_rp.size(); i++) d.u_pid[kMaxW + i] = w->u_rp[i];
+        if (!w->xops.empty()) {
+            uslot.assign(w->n_prop, 0xFF);
+            for (int i = 0; i < n_w; i++) uslot[w->u_wp[i]] = (uint8_t)i;
+            for (const auto& x : w->xops) {
+                if (uslot[x.pid] != 0xFF) continue;
+                if (std::binary_search(w->u_rp.begin(), w->u_rp.end(), (int)x.pid) || n_w == kMaxW) {
+                    use_u = false;
+                    break;
+                }
+                uslot[x.pid] = (uint8_t)n_w;
+                d.u_pid[n_w++] = (int32_t)x.pid;
+            }
+        }
+        d.n_w = n_w;
+        std::vector<int> ord(n_w);
+        for (int i = 0; i < n_w; i++) ord[i] = i;
+        std::sort(ord.begin(), ord.end(), [&](int a, int b) { return d.u_pid[a] < d.u_pid[b]; });
+        for (int i = 0; i < n_w; i++) d.u_order[i] = (uint8_t)ord[i];
+        for (int j = 0; j < kMaxU; j++) {
+            const int p = d.u_pid[j];
+            d.u_col[j] = p < 0 ? nullptr
+                               : (p < d.n_int ? (uint64_t*)(d.icol + (size_t)p * d.cap)
+                                              : (uint64_t*)(d.fcol + (size_t)(p - d.n_int) * d.cap));
+        }
+    }
+    if (!use_u) uslot.clear();
+
     // ---- uploads through the pinned arena ----
     const size_t nx = w->xops.size(), npre = pre_slot.size(), npost = post.size();
     size_t off_xs = 0, off_xp = align16(off_xs + nx * 4), off_xb = align16(off_xp + nx * 4);
@@ -728,7 +824,8 @@ int nfk_execute(void* world, int64_t now_ms) {
     size_t off_qs = align16(off_po + npre * 4), off_qk = align16(off_qs + npost * 4);
     size_t off_qo = align16(off_qk + npost * 4), off_qi = align16(off_qo + npost * 4);
     size_t off_qc = align16(off_qi + npost * 4), off_qt = align16(off_qc + npost * 4);
-    size_t total = align16(off_qt + npost * 8);
+    size_t off_us = align16(off_qt + npost * 8);
+    size_t total = align16(off_us + uslot.size());
     if (total > 0 && (nx || npre || npost)) {
         int r = pin_reserve(w, total);
         if (r) return r;
@@ -750,6 +847,7 @@ int nfk_execute(void* world, int64_t now_ms) {
             ((int32_t*)(P + off_qc))[i] = post[i].count;
             ((int64_t*)(P + off_qt))[i] = post[i].time;
         }
+        if (!uslot.empty()) memcpy(P + off_us, uslot.data(), uslot.size());
         HIPCHK(hipMemcpyAsync(w->stage, w->pin, total, hipMemcpyHostToDevice, w->stream));
         HIPCHK(hipEventRecord(w->pin_done, w->stream));
         w->pin_pending = true;
@@ -759,6 +857,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     d.x_slot = nx ? (const uint32_t*)(S + off_xs) : nullptr;
     d.x_pid = nx ? (const uint32_t*)(S + off_xp) : nullptr;
     d.x_bits = nx ? (const uint64_t*)(S + off_xb) : nullptr;
+    d.u_slot = uslot.empty() ? nullptr : (const uint8_t*)(S + off_us);
     w->xops.clear();
     w->hops.clear();
 
@@ -776,7 +875,10 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
-        hipLaunchKernelGGL(k_tick, dim3((unsigned)d.n_tiles), dim3(kTPB), 0, w->stream, d);
+        if (use_u)
+            hipLaunchKernelGGL(k_tick, dim3((unsigned)d.n_tiles), dim3(kTPB), 0, w->stream, d);
+        else
+            hipLaunchKernelGGL(k_tick_touch, dim3((unsigned)d.n_tiles), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
     if (d.has_recops && d.n_rtiles) {
@@ -918,7 +1020,7 @@ int nfk_read_schedules(void* world, int64_t* next_ms, int32_t* remain, uint8_t* 
         for (int32_t s = 0; s < d.N; s++) {
             size_t o = (size_t)k * w->n_obj + w->obj_of_slot[s], a = (size_t)k * d.cap + s;
             const SchedHot& h = hot[a];
-            state[o] = (uint8_t)h.state;
+            state[o] = (uint8_t)(h.state & (kStPresent | kStForever));
             next_ms[o] = (h.state & 1) ? h.next : 0;
             remain[o] = (h.state & 1) ? h.remain : 0;
         }

@@ -55,8 +55,9 @@ __global__ void k_post_hostops(const uint32_t* __restrict__ slot, const uint32_t
     if ((op[i] & 2) && !(h.state & 1)) {  // AddSchedule (SM:218): an existing name wins
         const float f = interval[i];
         const int32_t c = count[i];
-        h.state = 1u | (c < 0 ? 2u : 0u);
-        h.next = time[i] + (int64_t)(f * 1000.0f);
+        const int64_t step = (int64_t)(f * 1000.0f);
+        h.state = kStPresent | (c < 0 ? kStForever : 0u) | st_pack_step(step);
+        h.next = time[i] + step;
         h.remain = c;
         SchedCold cold;
         cold.start = time[i];
@@ -198,6 +199,88 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Frame working set (k_tick).  A thread keeps its entity's values of the U slots in registers;
+// program operands are addressed by wave-uniform slot numbers (Tables::opu), so a program runs
+// without searching a written-property list.
+#define NFK_U16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
+static_assert(kMaxU == 16, "NFK_U16 enumerates kMaxU slots");
+
+// j wave-uniform: a scalar branch to one register move
+__device__ __forceinline__ uint64_t uget(const uint64_t (&v)[kMaxU], uint32_t j) {
+    switch (__builtin_amdgcn_readfirstlane(j)) {
+#define NFK_C(i) \
+    case i:      \
+        return v[i];
+        NFK_U16(NFK_C)
+#undef NFK_C
+    }
+    return 0;
+}
+__device__ __forceinline__ void uput(uint64_t (&v)[kMaxU], uint32_t j, uint64_t x) {
+    switch (__builtin_amdgcn_readfirstlane(j)) {
+#define NFK_C(i)  \
+    case i:       \
+        v[i] = x; \
+        break;
+        NFK_U16(NFK_C)
+#undef NFK_C
+    }
+}
+// j per lane (queued SetProperty calls differ between entities): select over the writable slots
+__device__ __forceinline__ uint64_t uget_lane(const uint64_t (&v)[kMaxU], uint32_t j) {
+    uint64_t r = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxW; i++) r = (j == (uint32_t)i) ? v[i] : r;
+    return r;
+}
+__device__ __forceinline__ void uput_lane(uint64_t (&v)[kMaxU], uint32_t j, uint64_t x) {
+#pragma unroll
+    for (int i = 0; i < kMaxW; i++) v[i] = (j == (uint32_t)i) ? x : v[i];
+}
+
+// The fired kinds' programs in schedule-name order on the register working set.  A Set that
+// fails the reference's change predicate leaves the value as it was; wm collects the slots a
+// Set changed at least once.
+__device__ __forceinline__ void run_programs_u(uint64_t (&v)[kMaxU], uint32_t& wm, const Tables* __restrict__ tab,
+                                               uint32_t fired, int n_kind) {
+    for (int k = 0; k < n_kind; k++) {
+        if (!((fired >> k) & 1)) continue;
+        const int n = tab->nops[k];
+        for (int i = 0; i < n; i++) {
+            const nfk_op op = tab->ops[k][i];
+            const uint8_t* u = tab->opu[k][i];
+            if (op.code == NFK_OP_IADD_CLAMP) {
+                const int64_t cur = (int64_t)uget(v, u[0]);
+                const int64_t a = (op.flags & NFK_A_PROP) ? (int64_t)uget(v, u[1]) : op.a;
+                const int64_t lo = (op.flags & NFK_LO_PROP) ? (int64_t)uget(v, u[2]) : op.b;
+                const int64_t hi = (op.flags & NFK_HI_PROP) ? (int64_t)uget(v, u[3]) : op.c;
+                int64_t r = (int64_t)((uint64_t)cur + (uint64_t)a);
+                r = r < lo ? lo : r;
+                r = r > hi ? hi : r;
+                uput(v, u[0], (uint64_t)r);  // NFCProperty::SetInt (PR:273): r == cur changes nothing
+                wm |= (r != cur) ? (1u << u[0]) : 0u;
+            } else if (op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE) {
+                const uint64_t xb = uget(v, u[0]);
+                const double x = __longlong_as_double((long long)xb);
+                double r;
+                if (op.code == NFK_OP_FLERP) {
+                    const double tg = __longlong_as_double((long long)uget(v, u[1]));
+                    const double dd = tg - x;
+                    const double m = dd * __longlong_as_double(op.b);
+                    r = x + m;
+                } else {
+                    const double m = x * __longlong_as_double(op.a);
+                    r = m + __longlong_as_double(op.b);
+                }
+                const bool set = !(fabs(r - x) <= 1e-15);  // NFCProperty::SetFloat (PR:314): IsZeroDouble(v - cur)
+                uput(v, u[0], set ? (uint64_t)__double_as_longlong(r) : xb);
+                wm |= set ? (1u << u[0]) : 0u;
+            }
+            // record ops run in k_records
+        }
+    }
+}
 
 // Block-wide exclusive scan of a packed 64-bit value (fields must not overflow into each other).
 __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v, unsigned long long* s_w,
@@ -219,16 +302,222 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
 
 constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
 
+// NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
+// order).  The hot records of a chunk of kinds are loaded together (independent 16 B loads).
+// Returns the fired-kind mask; rescheduled / removed records are stored back.
+__device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& bytes) {
+    uint32_t fired = 0;
+    bool taken = false;  // std::map remove-list key already owned (SM:68)
+    if (d.has_pre) {
+        taken = d.e_flags[e] & 1;
+        bytes += 1;
+    }
+    for (int k0 = 0; k0 < d.n_kind; k0 += kKindChunk) {
+        SchedHot h[kKindChunk];
+#pragma unroll
+        for (int j = 0; j < kKindChunk; j++)
+            if (k0 + j < d.n_kind) h[j] = d.s_hot[(size_t)(k0 + j) * d.cap + e];
+#pragma unroll
+        for (int j = 0; j < kKindChunk; j++) {
+            const int k = k0 + j;
+            if (k >= d.n_kind) break;
+            bytes += 16;
+            if (!(h[j].state & kStPresent) || !(d.now > h[j].next)) continue;
+            const bool forever = h[j].state & kStForever;
+            if (!(h[j].remain > 0 || forever)) continue;
+            h[j].remain -= 1;
+            fired |= 1u << k;
+            const uint32_t st = h[j].state;
+            if (h[j].remain <= 0 && !forever) {
+                if (!taken) {  // insert into the remove list succeeds for the first one only
+                    h[j].state = 0;
+                    taken = true;
+                }
+            } else {
+                const bool first = !(st & kStFired);
+                if ((st & kStStep) && (first || !forever || h[j].remain < 0)) {
+                    // next = start + step * (all - remain) without the cold record (see kSt*)
+                    if (!first) h[j].next += st_step(st);
+                } else {
+                    const SchedCold c = d.s_cold[(size_t)k * d.cap + e];
+                    bytes += 16;
+                    const int64_t step = (int64_t)(c.interval * 1000.0f);
+                    const int32_t done = (int32_t)((uint32_t)c.all - (uint32_t)h[j].remain);
+                    h[j].next = c.start + step * (int64_t)done;
+                }
+                h[j].state = st | kStFired;
+            }
+            d.s_hot[(size_t)k * d.cap + e] = h[j];
+            bytes += 16;
+        }
+    }
+    return fired;
+}
+
 // One thread per slot, one workgroup per 256-slot tile.  Outputs of tile t are written densely
 // at [t * tile_cap, t * tile_cap + count); k_scan_tiles turns the counts into global ranks.
+// k_tick: one thread per slot, one workgroup per 256-slot tile, on the frame working set
+// (Dev::u_*).  Every value the entity's frame touches is loaded in ONE batch of independent loads
+// into registers; the queued SetProperty calls and the fired kinds' programs run on those
+// registers with wave-uniform slot numbers; the slots a Set changed are diffed against their
+// frame-start values (kept in LDS).  Outputs of tile t are written densely at
+// [t * tile_cap, t * tile_cap + count); k_scan_tiles turns the counts into global ranks.
 __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
+    __shared__ unsigned long long s_w[kTPB / 64];
+    __shared__ unsigned s_bytes;
+    __shared__ uint64_t s_o[kMaxW * kTPB];  // frame-start values of the writable slots
+    __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
+    const int tile = blockIdx.x;
+    const int e = tile * kTile + (int)threadIdx.x;
+    if (threadIdx.x == 0) s_bytes = 0;
+    {
+        const int words = d.n_class * (NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS) / 4;
+        for (int i = threadIdx.x; i < words; i += kTPB)
+            ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
+    }
+    unsigned bytes = 0;
+    uint32_t fired = 0, xh = 0, wm = 0;
+    uint64_t desc = kDeadDesc;
+    uint64_t v[kMaxU];
+#pragma unroll
+    for (int j = 0; j < kMaxU; j++) v[j] = 0;
+    if (e < d.N) {
+        desc = d.fan_desc[e];
+        bytes += 8;
+    }
+    const bool live = !desc_dead(desc);
+    if (live) {
+        uint32_t need = 0;
+        if (d.n_x) {
+            xh = d.ext_head[e];
+            bytes += 4;
+            if (xh)
+                for (int i = (int)xh - 1; i < d.n_x && d.x_slot[i] == (uint32_t)e; i++)
+                    need |= 1u << d.u_slot[d.x_pid[i]];
+        }
+        fired = sched_scan(d, e, bytes);  // NFCScheduleModule::Execute (SM:51-81)
+        if (!(d.ablate & kAblPrograms))
+            for (int k = 0; k < d.n_kind; k++)
+                if ((fired >> k) & 1) need |= d.tab->umask[k];
+        // one batch of independent loads: every value this entity's frame reads or writes
+#pragma unroll
+        for (int j = 0; j < kMaxU; j++)
+            if ((need >> j) & 1) {
+                v[j] = d.u_col[j][e];
+                bytes += 8;
+            }
+#pragma unroll
+        for (int j = 0; j < kMaxW; j++)
+            if ((need >> j) & 1) s_o[j * kTPB + threadIdx.x] = v[j];
+        // SetProperty* calls queued before this frame, in call order (PR:254 / PR:295 predicates)
+        if (xh) {
+            for (int i = (int)xh - 1; i < d.n_x && d.x_slot[i] == (uint32_t)e; i++) {
+                const uint32_t pid = d.x_pid[i];
+                const uint64_t b = d.x_bits[i];
+                bytes += 16;
+                const uint32_t j = d.u_slot[pid];
+                const uint64_t cur = uget_lane(v, j);
+                const bool set = (int)pid < d.n_int
+                                     ? (int64_t)b != (int64_t)cur
+                                     : !(fabs(__longlong_as_double((long long)b) -
+                                              __longlong_as_double((long long)cur)) <= 1e-15);
+                if (set) {
+                    uput_lane(v, j, b);
+                    wm |= 1u << j;
+                }
+            }
+        }
+        // the fired heartbeats' effect programs, in schedule-name order
+        if (!(d.ablate & kAblPrograms) && fired) run_programs_u(v, wm, d.tab, fired, d.n_kind);
+    }
+    __syncthreads();  // s_pflags
+    // dirty diff against the frame-start values, and each dirty event's fan-out message count
+    uint32_t dm = 0;
+    unsigned nmsg = 0;
+    const unsigned cls = (unsigned)(desc >> 60);
+#pragma unroll
+    for (int j = 0; j < kMaxW; j++)
+        if (((wm >> j) & 1) && v[j] != s_o[j * kTPB + threadIdx.x]) {
+            dm |= 1u << j;
+            nmsg += event_msgs(desc, s_pflags[cls][d.u_pid[j]]);
+        }
+    const unsigned nd = __builtin_popcount(dm);
+    const unsigned nf = __builtin_popcount(fired);
+
+    // tile-local compaction: one block scan of (fired:16 | events:16 | messages:32)
+    unsigned long long tot;
+    const unsigned long long excl =
+        block_excl_scan(((unsigned long long)nf << 48) | ((unsigned long long)nd << 32) | nmsg, s_w, tot);
+    unsigned pev = (unsigned)((excl >> 32) & 0xFFFF);
+    unsigned pfi = (unsigned)(excl >> 48);
+    unsigned pmsg = (unsigned)excl;
+    const size_t ev0 = (size_t)tile * d.ev_tcap, fi0 = (size_t)tile * d.fi_tcap;
+
+    if (live) {
+        // write back the changed values; their events in property-id order
+        if (dm) {
+            for (int q = 0; q < d.n_w; q++) {
+                const uint32_t j = d.u_order[q];
+                if (!((dm >> j) & 1)) continue;
+                const uint64_t nv = uget(v, j);
+                const uint32_t pid = (uint32_t)d.u_pid[j];
+                d.u_col[j][e] = nv;
+                const size_t at = ev0 + pev;
+                d.ev_slot[at] = (uint32_t)e;
+                d.ev_pid[at] = pid;
+                d.ev_old[at] = s_o[j * kTPB + threadIdx.x];
+                d.ev_new[at] = nv;
+                d.ev_moff[at] = pmsg;  // tile-local; k_fanout adds the tile's message base
+                pmsg += event_msgs(desc, s_pflags[cls][pid]);
+                pev++;
+                bytes += 8 + 28;
+            }
+        }
+        uint32_t fl = fired;
+        while (fl) {
+            const int k = __builtin_ctz(fl);
+            fl &= fl - 1;
+            const size_t at = fi0 + pfi;
+            d.fi_slot[at] = (uint32_t)e;
+            d.fi_kind[at] = (uint32_t)k;
+            d.fi_remain[at] = d.s_hot[(size_t)k * d.cap + e].remain;
+            pfi++;
+            bytes += 12;
+        }
+        if (d.has_recops) {
+            d.fired_mask[e] = fired;
+            bytes += 4;
+        }
+        if (xh) d.ext_head[e] = 0;
+    }
+    // tile counts and algorithmic-byte tally
+    const unsigned wb = (unsigned)wave_sum(bytes);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&s_bytes, wb);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        d.t_ev[tile] = (unsigned)((tot >> 32) & 0xFFFF);
+        d.t_fi[tile] = (unsigned)(tot >> 48);
+        d.t_msg[tile] = (unsigned)tot;
+        atomicAdd(&d.ctrl->bytes_tick, (unsigned long long)(s_bytes + 12));
+    }
+}
+
+// k_tick_touch: the general path, used when a frame's property working set does not fit the U
+// slots (see k_tick): a per-entity written-property list, one operand round trip per fired kind.
+__global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
     __shared__ uint64_t s_old[NFK_MAX_TOUCH * kTPB];
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     const int tile = blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
-    const bool live = e < d.N;
+    uint64_t desc = kDeadDesc;
+    unsigned dbytes = 0;
+    if (e < d.N) {
+        desc = d.fan_desc[e];
+        dbytes = 8;
+    }
+    const bool live = !desc_dead(desc);
     if (threadIdx.x == 0) s_bytes = 0;
     {
         const int words = d.n_class * (NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS) / 4;
@@ -245,12 +534,10 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
     en.cap = (size_t)d.cap;
     en.n_int = d.n_int;
     en.e = live ? e : 0;
+    en.bytes = dbytes;
     uint32_t fired = 0;
     uint32_t xh = 0;
-    uint64_t desc = 0;
     if (live) {
-        desc = d.fan_desc[e];  // independent of everything below: issued first
-        en.bytes += 8;
         // 1. SetProperty* calls queued before this frame, in call order
         if (d.n_x) {
             xh = d.ext_head[e];
@@ -265,46 +552,10 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
                 }
             }
         }
-        // 2. NFCScheduleModule::Execute (SM:51-81): this object's schedules in name order.
-        //    The hot records of a chunk of kinds are loaded together (independent 16 B loads).
-        bool taken = false;  // std::map remove-list key already owned (SM:68)
-        if (d.has_pre) {
-            taken = d.e_flags[e] & 1;
-            en.bytes += 1;
-        }
-        for (int k0 = 0; k0 < d.n_kind; k0 += kKindChunk) {
-            SchedHot h[kKindChunk];
-#pragma unroll
-            for (int j = 0; j < kKindChunk; j++)
-                if (k0 + j < d.n_kind) h[j] = d.s_hot[(size_t)(k0 + j) * d.cap + e];
-#pragma unroll
-            for (int j = 0; j < kKindChunk; j++) {
-                const int k = k0 + j;
-                if (k >= d.n_kind) break;
-                en.bytes += 16;
-                if (!(h[j].state & 1) || !(d.now > h[j].next)) continue;
-                const bool forever = h[j].state & 2;
-                if (!(h[j].remain > 0 || forever)) continue;
-                h[j].remain -= 1;
-                fired |= 1u << k;
-                if (h[j].remain <= 0 && !forever) {
-                    if (!taken) {  // insert into the remove list succeeds for the first one only
-                        h[j].state = 0;
-                        taken = true;
-                    }
-                } else {
-                    const SchedCold c = d.s_cold[(size_t)k * d.cap + e];
-                    en.bytes += 16;
-                    const int64_t step = (int64_t)(c.interval * 1000.0f);
-                    const int32_t done = (int32_t)((uint32_t)c.all - (uint32_t)h[j].remain);
-                    h[j].next = c.start + step * (int64_t)done;
-                }
-                d.s_hot[(size_t)k * d.cap + e] = h[j];
-                en.bytes += 16;
-            }
-        }
+        // 2. NFCScheduleModule::Execute (SM:51-81)
+        fired = sched_scan(d, e, en.bytes);
         // 3. the fired heartbeats' effect programs, in schedule-name order
-        if (!(d.ablate & kAblPrograms)) {
+        if (!(d.ablate & kAblPrograms) && fired) {
             for (int k = 0; k < d.n_kind; k++)
                 if ((fired >> k) & 1) run_program(en, d.tab, k);
         }
@@ -541,73 +792,108 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
 }
 
 // ---------------------------------------------------------------------------------
-// Exclusive scans of the per-tile counts: one workgroup of 1024 threads, 4 counts per thread
-// per pass.  Writes bases[n+1] (bases[n] = total) and the frame totals.
-constexpr int kScanTPB = 1024;
+// Exclusive scans of the four per-tile count arrays (events, fired, record events, messages) in
+// one workgroup of 1024 threads: every thread loads kScanPer consecutive counts of all four
+// arrays at once (one memory round trip per pass), then four block scans share each barrier.
+// Writes bases[n+1] (bases[n] = total) and the frame totals.
+constexpr int kScanTPB = 1024, kScanPer = 8;
 
-__device__ unsigned long long scan_counts(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ base, int n,
-                                          unsigned long long* s_w) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    unsigned long long carry = 0;
-    for (int c0 = 0; c0 < n; c0 += kScanTPB * 4) {
-        unsigned v[4];
-        unsigned long long sum = 0;
+struct ScanArr {
+    uint32_t v[kScanPer];
+    unsigned long long sum, inc;
+};
+
+__device__ __forceinline__ void scan_load(ScanArr& x, const uint32_t* __restrict__ cnt, int len, int i0) {
+    x.sum = 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int i = c0 + tid * 4 + q;
-            v[q] = i < n ? cnt[i] : 0u;
-            sum += v[q];
-        }
-        const unsigned long long inc = wave_incl_scan(sum);
-        if (lane == 63) s_w[w] = inc;
-        __syncthreads();
-        unsigned long long before = carry, tot = 0;
-        for (int i = 0; i < kScanTPB / 64; i++) {
-            before += (i < w) ? s_w[i] : 0ull;
-            tot += s_w[i];
-        }
-        unsigned long long run = before + inc - sum;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int i = c0 + tid * 4 + q;
-            if (i < n) base[i] = (uint32_t)run;
-            run += v[q];
-        }
-        carry += tot;
-        __syncthreads();
+    for (int q = 0; q < kScanPer; q++) {
+        x.v[q] = (i0 + q < len) ? cnt[i0 + q] : 0u;
+        x.sum += x.v[q];
     }
-    if (tid == 0) base[n] = (uint32_t)carry;
-    return carry;
+}
+
+// block-scan step of one array (s_pre = exclusive prefix of the wave totals); returns the pass total
+__device__ __forceinline__ unsigned long long scan_store(ScanArr& x, const unsigned long long* s_pre,
+                                                         unsigned long long carry, uint32_t* __restrict__ base,
+                                                         int len, int i0) {
+    unsigned long long run = carry + s_pre[threadIdx.x >> 6] + x.inc - x.sum;
+#pragma unroll
+    for (int q = 0; q < kScanPer; q++) {
+        if (i0 + q < len) base[i0 + q] = (uint32_t)run;
+        run += x.v[q];
+    }
+    return s_pre[kScanTPB / 64];
 }
 
 __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
-    __shared__ unsigned long long s_w[kScanTPB / 64];
-    const unsigned long long nev = scan_counts(d.t_ev, d.ev_base, d.n_tiles, s_w);
-    const unsigned long long nfi = scan_counts(d.t_fi, d.fi_base, d.n_tiles, s_w);
-    unsigned long long nre = 0;
-    if (d.has_recops) nre = scan_counts(d.t_re, d.re_base, d.n_rtiles, s_w);
-    const unsigned long long nm =
-        scan_counts(d.t_msg, d.msg_base, d.n_tiles + (d.has_recops ? d.n_rtiles : 0), s_w);
-    if (threadIdx.x == 0) {
-        d.ctrl->n_ev = nev;
-        d.ctrl->n_fi = nfi;
-        d.ctrl->n_re = nre;
-        d.ctrl->n_msgs = nm;
-        if (nm > (unsigned long long)d.msg_cap) atomicOr(&d.ctrl->err, kErrMsgCap);
+    __shared__ unsigned long long s_w[4][kScanTPB / 64 + 1];  // wave totals -> exclusive prefixes, [16] = total
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nrt = d.has_recops ? d.n_rtiles : 0;
+    const int l_ev = d.n_tiles, l_re = nrt, l_msg = d.n_tiles + nrt;
+    unsigned long long c_ev = 0, c_fi = 0, c_re = 0, c_msg = 0;  // carries (uniform)
+    for (int c0 = 0; c0 < l_msg; c0 += kScanTPB * kScanPer) {
+        const int i0 = c0 + tid * kScanPer;
+        ScanArr ev, fi, re, ms;
+        scan_load(ev, d.t_ev, l_ev, i0);
+        scan_load(fi, d.t_fi, l_ev, i0);
+        scan_load(re, d.t_re, l_re, i0);
+        scan_load(ms, d.t_msg, l_msg, i0);
+        ev.inc = wave_incl_scan(ev.sum);
+        fi.inc = wave_incl_scan(fi.sum);
+        re.inc = wave_incl_scan(re.sum);
+        ms.inc = wave_incl_scan(ms.sum);
+        if (lane == 63) {
+            s_w[0][w] = ev.inc;
+            s_w[1][w] = fi.inc;
+            s_w[2][w] = re.inc;
+            s_w[3][w] = ms.inc;
+        }
+        __syncthreads();
+        if (w < 4 && lane < kScanTPB / 64) {  // wave w scans array w's 16 wave totals
+            const unsigned long long x = s_w[w][lane];
+            unsigned long long y = x;
+#pragma unroll
+            for (int dd = 1; dd < kScanTPB / 64; dd <<= 1) {
+                const unsigned long long t = shfl_up_u64(y, dd);
+                if (lane >= dd) y += t;
+            }
+            s_w[w][lane] = y - x;
+            if (lane == kScanTPB / 64 - 1) s_w[w][kScanTPB / 64] = y;
+        }
+        __syncthreads();
+        c_ev += scan_store(ev, s_w[0], c_ev, d.ev_base, l_ev, i0);
+        c_fi += scan_store(fi, s_w[1], c_fi, d.fi_base, l_ev, i0);
+        c_re += scan_store(re, s_w[2], c_re, d.re_base, l_re, i0);
+        c_msg += scan_store(ms, s_w[3], c_msg, d.msg_base, l_msg, i0);
+        __syncthreads();
+    }
+    if (tid == 0) {
+        d.ev_base[l_ev] = (uint32_t)c_ev;
+        d.fi_base[l_ev] = (uint32_t)c_fi;
+        d.re_base[l_re] = (uint32_t)c_re;
+        d.msg_base[l_msg] = (uint32_t)c_msg;
+        d.ctrl->n_ev = c_ev;
+        d.ctrl->n_fi = c_fi;
+        d.ctrl->n_re = c_re;
+        d.ctrl->n_msgs = c_msg;
+        if (c_msg > (unsigned long long)d.msg_cap) atomicOr(&d.ctrl->err, kErrMsgCap);
     }
 }
 
 // ---------------------------------------------------------------------------------
-// Fan-out: one workgroup per tile (property tiles, then record tiles).  The tile's events are
-// taken 256 at a time; each chunk's recipient lists are expanded cooperatively from an LDS
-// descriptor table so consecutive lanes store consecutive messages.  Also rewrites each
-// event's tile-local message offset as a global one.  Does nothing (and sets no output) when
-// the frame's messages exceed msg_cap: the host grows the buffer and re-runs this kernel.
+// Fan-out: GetBroadCastObject recipient lists (AOI:531-593) for every dirty event, one workgroup
+// per tile (property tiles, then record tiles), one thread per event.  Slots are in (scene, group,
+// guid) order, so the players of every group the tile touches form one contiguous run of
+// pl_slot; it is staged in LDS when it fits.  A thread writes its event's recipients as one
+// contiguous run (every player of the group but itself, NFGUID order, or itself); events with
+// more than kFanCoop recipients are expanded by their whole wave, 64 recipients per store.
+// Also rewrites each event's tile-local message offset as a global one.  Does nothing (and sets
+// no output) when the frame's messages exceed msg_cap: the host grows the buffer and re-runs it.
+constexpr int kFanLds = 4096, kFanCoop = 32;
+
 __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
-    __shared__ uint32_t s_off[kTPB];
-    __shared__ int32_t s_src[kTPB];   // public: first player index in pl_slot; private: -1 - slot
-    __shared__ int32_t s_rank[kTPB];  // public: rank of self in the player list to skip, else -1
-    __shared__ uint32_t s_first, s_end;
+    __shared__ int32_t s_pl[kFanLds];
+    __shared__ uint32_t s_pb[2];
     __shared__ unsigned s_bytes;
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
@@ -617,7 +903,16 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
     const uint32_t* base = rec ? d.re_base : d.ev_base;
     const unsigned cnt = base[t + 1] - base[t];
     if (cnt == 0) return;  // uniform
-    if (threadIdx.x == 0) s_bytes = 0;
+    const size_t off0 = (size_t)t * (rec ? d.re_tcap : d.ev_tcap);
+    const uint32_t* slots = rec ? d.re_slot : d.ev_slot;
+    uint32_t* moff = rec ? d.re_moff : d.ev_moff;
+    if (threadIdx.x == 0) {
+        s_bytes = 0;
+        // player run of the groups between the tile's first and last event
+        const uint64_t a = d.fan_desc[slots[off0]], b = d.fan_desc[slots[off0 + cnt - 1]];
+        s_pb[0] = (uint32_t)a;
+        s_pb[1] = (uint32_t)b + (uint32_t)((b >> 32) & 0x3FFF);
+    }
     if (rec) {
         for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
             ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
@@ -626,65 +921,63 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
         for (int i = threadIdx.x; i < words; i += kTPB)
             ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
     }
-    const uint32_t mbase = d.msg_base[blockIdx.x];
-    const size_t off0 = (size_t)t * (rec ? d.re_tcap : d.ev_tcap);
-    const uint32_t* slots = rec ? d.re_slot : d.ev_slot;
-    uint32_t* moff = rec ? d.re_moff : d.ev_moff;
-    unsigned bytes = 12;
     __syncthreads();
+    const uint32_t pb_lo = s_pb[0], npl = s_pb[1] - s_pb[0];
+    const bool staged = npl <= (uint32_t)kFanLds;
+    unsigned bytes = threadIdx.x == 0 ? 12u + 16u : 0u;
+    if (staged) {
+        for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = d.pl_slot[pb_lo + i];
+        bytes += 4 * ((npl + kTPB - 1 - threadIdx.x) / kTPB);
+    }
+    __syncthreads();
+    const uint32_t mbase = d.msg_base[blockIdx.x];
+    const int lane = threadIdx.x & 63;
     for (unsigned c0 = 0; c0 < cnt; c0 += kTPB) {
         const unsigned i = c0 + threadIdx.x;
-        const bool valid = i < cnt;
-        unsigned n = 0, lm = 0;
-        int32_t src = 0, rank = -1;
-        if (valid) {
-            const int32_t slot = (int32_t)slots[off0 + i];
+        uint32_t n = 0, m0 = 0, src = 0, r1 = 0, self = 0;
+        bool pub = false;
+        if (i < cnt) {
+            const uint32_t slot = slots[off0 + i];
             const uint32_t key = rec ? (d.re_rrc[off0 + i] >> 16) : d.ev_pid[off0 + i];
-            lm = moff[off0 + i];
+            const uint32_t lm = moff[off0 + i];
             const uint64_t desc = d.fan_desc[slot];
             bytes += 4 + 4 + 4 + 8 + 4;
             const unsigned cls = (unsigned)(desc >> 60);
             const uint8_t fl = rec ? s_rflags[cls][key] : s_pflags[cls][key];
             n = event_msgs(desc, fl);
-            if (fl & NFK_PUBLIC) {  // every player of the group but self, NFGUID order
-                src = (int32_t)(uint32_t)desc;
-                rank = (int)((desc >> 46) & 0x3FFF) - 1;
-            } else if (n) {  // self only
-                src = -1 - slot;
+            m0 = mbase + lm;
+            moff[off0 + i] = m0;
+            self = slot;
+            pub = fl & NFK_PUBLIC;
+            if (pub) {  // every player of the group but self, NFGUID order
+                src = (uint32_t)desc;
+                r1 = (uint32_t)((desc >> 46) & 0x3FFF);
             }
-            moff[off0 + i] = mbase + lm;
-            if (i == c0) s_first = lm;
-            if (i + 1 == cnt || threadIdx.x == kTPB - 1) s_end = lm + n;
         }
-        __syncthreads();
-        const uint32_t first = s_first, total = s_end - first;
-        s_off[threadIdx.x] = valid ? lm - first : total;
-        s_src[threadIdx.x] = src;
-        s_rank[threadIdx.x] = rank;
-        __syncthreads();
-        uint32_t* out = d.msg_rcpt + mbase + first;
-        for (unsigned q = threadIdx.x; q < total; q += kTPB) {
-            // owner: the last event whose local offset <= q (it has n > 0)
-            int lo = 0, hi = kTPB - 1;
-#pragma unroll
-            for (int step = 0; step < 8; step++) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (s_off[mid] <= q) lo = mid;
-                else hi = mid - 1;
+        uint32_t* out = d.msg_rcpt + m0;
+        if (!pub) {
+            if (n) out[0] = self;
+        } else if (n <= (uint32_t)kFanCoop) {
+            const uint32_t np = n + (r1 ? 1u : 0u);
+            uint32_t m = 0;
+            for (uint32_t q = 0; q < np; q++) {
+                if (q + 1 == r1) continue;
+                out[m++] = staged ? (uint32_t)s_pl[src - pb_lo + q] : (uint32_t)d.pl_slot[src + q];
             }
-            const int32_t sr = s_src[lo];
-            const uint32_t idx = q - s_off[lo];
-            int32_t r;
-            if (sr < 0) {
-                r = -1 - sr;
-            } else {
-                const int32_t rk = s_rank[lo];
-                r = d.pl_slot[sr + idx + ((rk >= 0 && (int32_t)idx >= rk) ? 1 : 0)];
-            }
-            out[q] = (uint32_t)r;
-            bytes += 4;
         }
-        __syncthreads();
+        bytes += 4 * n;
+        // big groups: the wave expands each such event cooperatively
+        unsigned long long big = __ballot(pub && n > (uint32_t)kFanCoop);
+        while (big) {
+            const int L = __builtin_ctzll(big);
+            big &= big - 1;
+            const uint32_t bn = __shfl(n, L, 64), bsrc = __shfl(src, L, 64), br1 = __shfl(r1, L, 64);
+            const uint32_t bm0 = __shfl(m0, L, 64);
+            for (uint32_t q = lane; q < bn; q += 64) {
+                const uint32_t p = q + ((br1 && q + 1 >= br1) ? 1u : 0u);  // skip self
+                d.msg_rcpt[bm0 + q] = staged ? (uint32_t)s_pl[bsrc - pb_lo + p] : (uint32_t)d.pl_slot[bsrc + p];
+            }
+        }
     }
     const unsigned wb = (unsigned)wave_sum(bytes);
     if ((threadIdx.x & 63) == 0 && wb) atomicAdd(&s_bytes, wb);

@@ -97,7 +97,7 @@ def _names(lst):
 
 def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4, n_ticks=8,
                tick_ms=100, seed=1, ext_frac=0.05, host_ops=True, records=False, rec_rows=64,
-               t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True):
+               t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, sched_edges=False):
     rng = np.random.default_rng(seed)
     n_groups = n_scenes * groups_per_scene
     # ---- objects ----
@@ -173,6 +173,23 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
         s_int.append(np.full(len(objs), 0.1, np.float32))
         s_cnt.append(np.full(len(objs), -1))
         s_time.append(t0 - rng.integers(0, 101, len(objs)))
+    if sched_edges:
+        # reschedule edge cases (SM:71-72): steps that do not fit the hot record's 28-bit field,
+        # negative intervals, forever counts whose int32 remain wraps past INT32_MIN within a few
+        # frames, and zero counts (never fire)
+        for i, (name, iv, cnt) in enumerate(spec):
+            m = len(s_obj[i])
+            pick = rng.random(m) < 0.05
+            if name == "Patrol":      # 2e5 s interval, started long ago: fires, then waits
+                s_int[i][pick] = 2.0e5
+                s_time[i][pick] = t0 - int(2.0e8) - rng.integers(0, 300, pick.sum())
+            elif name == "HPRegen":   # forever, remain wraps INT32_MIN -> INT32_MAX
+                s_cnt[i][pick] = -(2 ** 31) + rng.integers(0, 4, pick.sum())
+                s_int[i][pick] = 0.05
+            elif name == "MPRegen":   # negative interval: next moves backwards, fires every frame
+                s_int[i][pick] = -0.05
+            elif name == "Poison":    # count 0: registered, never fires
+                s_cnt[i][pick] = 0
     s_obj = np.concatenate(s_obj).astype(np.int32)
     perm = rng.permutation(len(s_obj))   # AddSchedule call order is arbitrary
     s_obj = s_obj[perm]

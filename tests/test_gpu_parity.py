@@ -29,6 +29,7 @@ CASES = {
     "one_object": dict(n_obj=1, n_scenes=1, groups_per_scene=1, players_per_group=1, ext_frac=1.0),
     "no_players": dict(n_obj=1000, n_scenes=1, groups_per_scene=2, players_per_group=0),
     "big_group": dict(n_obj=3000, n_scenes=1, groups_per_scene=1, players_per_group=300, host_ops=True),
+    "sched_edges": dict(n_obj=6000, n_scenes=2, groups_per_scene=9, players_per_group=3, sched_edges=True),
     "ragged_4097": dict(n_obj=4097, n_scenes=5, groups_per_scene=13, players_per_group=1, ext_frac=0.3),
 }
 

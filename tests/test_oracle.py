@@ -42,6 +42,7 @@ def test_golden_fixtures_are_nontrivial():
     (3, dict(n_obj=500, n_scenes=2, groups_per_scene=9, players_per_group=5, records=True, rec_rows=64,
              rec_float_op=False)),
     (4, dict(n_obj=1, n_scenes=1, groups_per_scene=1, players_per_group=1, ext_frac=1.0)),
+    (5, dict(n_obj=700, n_scenes=2, groups_per_scene=5, players_per_group=3, sched_edges=True)),
 ])
 def test_oracle_matches_reference(seed, kw):
     w = workload.make_world(n_ticks=9, seed=seed, **kw)

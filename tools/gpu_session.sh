@@ -30,7 +30,7 @@ for step in "$@"; do
     bench) run bench 600 python bench.py --steps 50 --warmup 5 ;;
     bench3) run bench3 600 python bench.py --config 3 --steps 50 --warmup 5 --cpu-baseline off ;;
     bench4) run bench4 600 python bench.py --config 4 --steps 50 --warmup 5 --cpu-baseline off ;;
-    ablate) run ablate 600 python tools/ablate.py ;;
+    ablate) run ablate 600 python tools/ablate.py --variants ${ABL:-0,8,4} ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
              python bench.py --steps 50 --warmup 5 --cpu-baseline off ;;
     pmc)
