@@ -33,13 +33,13 @@ extern "C" {
 
 #define NFK_MAX_INT_PROPS 64
 #define NFK_MAX_FLT_PROPS 64
-#define NFK_MAX_CLASSES 16
+#define NFK_MAX_CLASSES 16 /* class id 15 is reserved (marks a free slot on the device) */
 #define NFK_MAX_KINDS 32
 #define NFK_MAX_OPS 4
 #define NFK_MAX_RECORDS 8
 #define NFK_MAX_REC_ROWS 64
 #define NFK_MAX_REC_COLS 16
-#define NFK_MAX_TOUCH 8
+#define NFK_MAX_TOUCH 12
 
 /* property / record visibility flags, NFIProperty::GetPublic/GetPrivate/GetUpload */
 #define NFK_PUBLIC 1
@@ -87,6 +87,9 @@ typedef struct nfk_config {
     int32_t n_rec;        /* records */
     int64_t msg_capacity; /* fan-out messages per tick (0 = 32 x capacity) */
     void* stream;         /* hipStream_t to launch on, NULL = library-owned stream */
+    int32_t slack_per_256; /* free slots kept per 256 members of a scene group for arrivals
+                              (SwitchScene / imports) without a full re-layout:
+                              0 = default 16, < 0 = none */
 } nfk_config;
 
 typedef struct nfk_summary {
@@ -158,6 +161,42 @@ int nfk_load_prop(void* world, int32_t pid, const uint64_t* bits /* [n_objects] 
 int nfk_load_record(void* world, int32_t rec, const uint64_t* cells, const uint64_t* used_mask);
 /* build the device layout: slots sorted by (scene, group, guid) (NFCSceneInfo group maps) */
 int nfk_commit(void* world);
+
+/* ---- runtime membership (after nfk_commit) ----
+ * Queued like every other between-frame call and applied at the start of the next nfk_execute,
+ * before the queued SetProperty calls, so an entity's events of that frame come from its new
+ * scene group.  Slots stay sorted by (scene, group, guid); only the scene groups that changed
+ * are rewritten. */
+/* property ids SwitchScene writes: SceneID, GroupID (int), X, Y, Z (float); -1 = not in schema */
+int nfk_set_scene_props(void* world, int32_t pid_scene, int32_t pid_group, int32_t pid_x, int32_t pid_y,
+                        int32_t pid_z);
+/* NFCKernelModule::SwitchScene (KM:901-951): leave the group, [GroupID = 0, SceneID = scene when
+ * the scene changes], X/Y/Z = (double)x/y/z, GroupID = group, join the new group */
+int nfk_switch_scene(void* world, int64_t guid_head, int64_t guid_data, int32_t scene, int32_t group, float x,
+                     float y, float z);
+/* NFCKernelModule::DestroyObject (KM:273-308): leaves its group, its schedules go with it */
+int nfk_destroy_objects(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data);
+/* objects ever created in this world (creation-order indices of the nfk_read_* arrays) */
+int nfk_object_count(void* world, int32_t* n);
+/* An entity's state as a ROW of 64-bit words: properties (prop id order), per heartbeat kind its
+ * schedule (next, remain|state, start, all|interval), per record its cells [cols][rows] and its
+ * used-row mask.  Rows let a scene shard hand entities to another (SwitchScene across GPUs). */
+int nfk_row_words(void* world, int32_t* words);
+/* source side: write the entities' rows to rows_dev (device memory, [n][row_words]) on the world's
+ * stream, and remove the entities from this world (they must not have other membership calls
+ * queued in this window) */
+int nfk_export_objects(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
+                       uint64_t* rows_dev);
+/* destination side: new entities with the given rows (device memory, copied on the world's
+ * stream before the call returns); also CreateObject after commit (KM:101) */
+int nfk_import_objects(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
+                       const int32_t* scene, const int32_t* group, const uint8_t* cls, const uint8_t* is_player,
+                       const uint64_t* rows_dev);
+/* CreateObject after commit with creation-time property values from host memory
+ * (props [n][n_int + n_flt] bit patterns; no schedules, empty records) */
+int nfk_spawn_objects(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
+                      const int32_t* scene, const int32_t* group, const uint8_t* cls, const uint8_t* is_player,
+                      const uint64_t* props);
 
 /* ---- property mutation: NFIKernelModule::SetPropertyInt/Float (KM:323,336) ----
  * Queued in call order, applied at the start of the next nfk_execute with the

@@ -60,7 +60,7 @@ struct RecOp {
 // Frame working set U (k_tick).  Slots [0, kMaxW) hold properties that may be written this
 // frame: the program destinations (fixed at commit, property-id order) followed by this frame's
 // queued-SetProperty properties; slots [kMaxW, kMaxU) hold properties programs only read.
-constexpr int kMaxU = 16, kMaxW = 8;
+constexpr int kMaxU = 16, kMaxW = 12;
 constexpr uint8_t kNoU = 0xFF;
 static_assert(kMaxW == NFK_MAX_TOUCH, "writable slots = touch capacity");
 

@@ -4,6 +4,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -71,7 +72,31 @@ struct World {
     std::vector<int32_t> scene, group;
     std::vector<uint8_t> cls, isplayer;
     std::unordered_map<GuidKey, int32_t, GuidHash> obj_of;
-    std::vector<int32_t> slot_of_obj, obj_of_slot;
+    std::vector<int32_t> slot_of_obj, obj_of_slot;  // -1: not resident / slack slot
+    std::vector<uint8_t> alive;                       // object exists (not destroyed / exported)
+    std::vector<int64_t> src_row;                     // >= 0: arrives from row src_row of ins_rows
+    std::vector<uint8_t> m_flag;                      // membership changed in this window
+    std::vector<int32_t> touched;                     // objects with m_flag set
+    // scene-group segments in (scene, group) order; slot range [base, base + cap)
+    struct Seg {
+        int32_t scene, group, base, cap;
+        std::vector<int32_t> objs;  // live objects, NFGUID order
+    };
+    std::vector<Seg> segs;
+    std::map<std::pair<int32_t, int32_t>, int32_t> seg_of;
+    int32_t slack = 16;  // slack slots per 256 live (nfk_config::slack_per_256)
+    int32_t pid_scene = -1, pid_group = -1, pid_x = -1, pid_y = -1, pid_z = -1;  // nfk_set_scene_props
+    int32_t row_words = 0;
+    uint64_t* ins_rows = nullptr;  // rows of entities imported this window
+    size_t ins_cap = 0, ins_n = 0;
+    uint64_t* mv_rows = nullptr;   // rows of entities moving inside this shard
+    size_t mv_cap = 0;
+    void* mlist = nullptr;         // device copy of the membership lists
+    size_t mlist_cap = 0;
+    std::vector<char> mhost;       // host staging of the membership lists
+    uint64_t* fan_desc_w = nullptr;
+    int32_t* pl_slot_w = nullptr;
+    int64_t n_relayout_full = 0, n_relayout_seg = 0;
     std::vector<std::vector<uint64_t>> init_props;
     std::vector<std::vector<uint64_t>> init_rcells, init_rused;
     std::vector<bool> rec_defined;
@@ -95,6 +120,8 @@ struct World {
     size_t dense_cap = 0;
 
     // queued calls
+    // queued calls; `slot` holds the object index until nfk_execute resolves it after the
+    // window's membership changes
     struct XOp { uint32_t slot, pid; uint64_t bits; };
     std::vector<XOp> xops;
     struct HOp { int32_t code; uint32_t slot, kind; float interval; int32_t count; int64_t time; };
@@ -241,6 +268,299 @@ int gather_tiles(World* w, const T* src, const uint32_t* base, int n_tiles, int 
         if (_r) return _r;             \
     } while (0)
 
+// ---------------- membership layout ----------------
+// Slots are grouped in scene-group segments in (scene, group) order.  Inside a segment the live
+// entities sit in NFGUID order, followed by slack slots (fan_desc = kDeadDesc) that absorb
+// arrivals without moving other segments.  NFCSceneGroupInfo keeps its member maps as
+// std::map<NFGUID, ...>, so slot order is both the reference's dirty-sync order and
+// GetBroadCastObject's recipient order (AOI:572, KM:1270-1294).
+bool guid_less(const World* w, int32_t a, int32_t b) {
+    return w->gh[a] != w->gh[b] ? w->gh[a] < w->gh[b] : w->gd[a] < w->gd[b];
+}
+
+int32_t seg_slack(int32_t slack, int32_t len) {
+    return slack <= 0 ? 0 : std::max<int32_t>(2, (int32_t)(((int64_t)len * slack + 255) / 256));
+}
+
+// segments of every live object with `slack` slots per 256; returns the slot total
+int64_t plan_segments(World* w, int32_t slack, std::vector<World::Seg>& segs) {
+    std::vector<int32_t> objs;
+    for (int32_t o = 0; o < w->n_obj; o++)
+        if (w->alive[o]) objs.push_back(o);
+    std::sort(objs.begin(), objs.end(), [w](int32_t a, int32_t b) {
+        if (w->scene[a] != w->scene[b]) return w->scene[a] < w->scene[b];
+        if (w->group[a] != w->group[b]) return w->group[a] < w->group[b];
+        return guid_less(w, a, b);
+    });
+    segs.clear();
+    int64_t base = 0;
+    for (size_t i = 0; i < objs.size();) {
+        size_t j = i;
+        const int32_t o = objs[i];
+        while (j < objs.size() && w->scene[objs[j]] == w->scene[o] && w->group[objs[j]] == w->group[o]) j++;
+        World::Seg g;
+        g.scene = w->scene[o];
+        g.group = w->group[o];
+        g.base = (int32_t)std::min<int64_t>(base, INT32_MAX);
+        g.objs.assign(objs.begin() + i, objs.begin() + j);
+        g.cap = (int32_t)g.objs.size() + seg_slack(slack, (int32_t)g.objs.size());
+        base += g.cap;
+        segs.push_back(std::move(g));
+        i = j;
+    }
+    return base;
+}
+
+// per-slot metadata of one segment: slot -> object, fan-out descriptor, and the player run
+// pl_slot[base, base + players) in NFGUID order (NFCSceneGroupInfo::mxPlayerList)
+struct MetaLists {
+    std::vector<int32_t> slot, obj, pl;
+    std::vector<uint64_t> desc;
+};
+
+int seg_meta(World* w, const World::Seg& g, MetaLists& m) {
+    int32_t np = 0;
+    for (int32_t o : g.objs) np += w->isplayer[o] ? 1 : 0;
+    if (np > 0x3FFF) return fail(NFK_ERR_ARG, "more than 16383 players in one scene group");
+    const size_t at = m.slot.size();
+    int32_t rank = 0;
+    for (int32_t i = 0; i < g.cap; i++) {
+        m.slot.push_back(g.base + i);
+        m.pl.push_back(0);
+        if (i < (int32_t)g.objs.size()) {
+            const int32_t o = g.objs[i];
+            const bool pl = w->isplayer[o];
+            m.obj.push_back(o);
+            m.desc.push_back((uint64_t)(uint32_t)g.base | ((uint64_t)np << 32) |
+                             ((uint64_t)(pl ? rank + 1 : 0) << 46) | ((uint64_t)w->cls[o] << 60));
+            if (pl) m.pl[at + rank++] = g.base + i;
+        } else {
+            m.obj.push_back(-1);
+            m.desc.push_back(kDeadDesc);
+        }
+    }
+    return NFK_OK;
+}
+
+void set_tiles(Dev& d, int32_t n_slots) {
+    d.N = n_slots;
+    d.n_tiles = (n_slots + kTile - 1) / kTile;
+    d.n_rtiles = (n_slots + kRTile - 1) / kRTile;
+}
+
+// grow a device buffer (contents dropped; callers only grow between uses)
+int dev_reserve(World* w, void** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap) return NFK_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    if (*p) HIPCHK(hipFree(*p));
+    *p = nullptr;
+    const size_t c = std::max(bytes, *cap + *cap / 2);
+    HIPCHK(hipMalloc(p, c));
+    *cap = c;
+    return NFK_OK;
+}
+
+template <typename T>
+size_t stage_list(World* w, const std::vector<T>& v) {
+    const size_t off = align16(w->mhost.size());
+    w->mhost.resize(off + v.size() * sizeof(T));
+    if (!v.empty()) memcpy(w->mhost.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+}
+
+unsigned grid_for(size_t work) { return (unsigned)std::max<size_t>(1, std::min<size_t>((work + kTPB - 1) / kTPB, 8192)); }
+
+// Apply this window's membership changes (SwitchScene across groups, DestroyObject, exports,
+// imports) before the frame: only the scene-group segments that changed are rewritten (the
+// entities behind the first change shift by one slot each); a new (scene, group) or a segment
+// whose slack ran out rebuilds the whole layout.
+int apply_membership(World* w) {
+    if (w->touched.empty()) return NFK_OK;
+    Dev& d = w->d;
+    const auto cmp = [w](int32_t a, int32_t b) { return guid_less(w, a, b); };
+    bool full = false;
+    std::vector<int32_t> aff;
+    std::vector<char> is_aff(w->segs.size(), 0);
+    auto mark = [&](int32_t g) {
+        if (!is_aff[g]) {
+            is_aff[g] = 1;
+            aff.push_back(g);
+        }
+    };
+    auto seg_at = [&](int32_t slot) {
+        int32_t lo = 0, hi = (int32_t)w->segs.size() - 1;
+        while (lo < hi) {
+            const int32_t mid = (lo + hi + 1) / 2;
+            if (w->segs[mid].base <= slot) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    for (int32_t o : w->touched) {
+        const int32_t s = w->slot_of_obj[o];
+        if (s < 0) continue;
+        const int32_t g = seg_at(s);
+        auto& v = w->segs[g].objs;
+        auto it = std::lower_bound(v.begin(), v.end(), o, cmp);
+        if (it != v.end() && *it == o) v.erase(it);
+        mark(g);
+    }
+    for (int32_t o : w->touched) {
+        if (!w->alive[o]) continue;
+        auto f = w->seg_of.find({w->scene[o], w->group[o]});
+        if (f == w->seg_of.end()) {
+            full = true;
+            continue;
+        }
+        auto& v = w->segs[f->second].objs;
+        v.insert(std::lower_bound(v.begin(), v.end(), o, cmp), o);
+        mark(f->second);
+    }
+    for (int32_t g : aff)
+        if ((int32_t)w->segs[g].objs.size() > w->segs[g].cap) full = true;
+
+    std::vector<int32_t> pack_src, un_dst;
+    std::vector<int64_t> un_src;
+    MetaLists m;
+    std::vector<World::Seg> nsegs;
+    if (full) {
+        int64_t total = plan_segments(w, w->slack, nsegs);
+        if (total > d.cap) total = plan_segments(w, 0, nsegs);
+        if (total > d.cap) return fail(NFK_ERR_CAPACITY, "entity capacity exceeded");
+        for (const auto& g : nsegs) {
+            for (int32_t i = 0; i < g.cap; i++) {
+                const int32_t ns = g.base + i;
+                if (i >= (int32_t)g.objs.size()) {
+                    un_dst.push_back(ns);
+                    un_src.push_back(kZeroRow);
+                    continue;
+                }
+                const int32_t o = g.objs[i];
+                un_dst.push_back(ns);
+                if (w->src_row[o] >= 0) {
+                    un_src.push_back(-1 - w->src_row[o]);
+                } else {
+                    un_src.push_back((int64_t)pack_src.size());
+                    pack_src.push_back(w->slot_of_obj[o]);
+                }
+            }
+            int r = seg_meta(w, g, m);
+            if (r) return r;
+        }
+        w->n_relayout_full++;
+    } else {
+        for (int32_t gi : aff) {
+            const World::Seg& g = w->segs[gi];
+            for (int32_t i = 0; i < g.cap; i++) {
+                const int32_t ns = g.base + i;
+                if (i >= (int32_t)g.objs.size()) {
+                    if (w->obj_of_slot[ns] >= 0) {  // an entity left this slot: clear it
+                        un_dst.push_back(ns);
+                        un_src.push_back(kZeroRow);
+                    }
+                    continue;
+                }
+                const int32_t o = g.objs[i];
+                if (w->src_row[o] >= 0) {
+                    un_dst.push_back(ns);
+                    un_src.push_back(-1 - w->src_row[o]);
+                } else if (w->slot_of_obj[o] != ns) {
+                    un_dst.push_back(ns);
+                    un_src.push_back((int64_t)pack_src.size());
+                    pack_src.push_back(w->slot_of_obj[o]);
+                }
+            }
+            int r = seg_meta(w, g, m);
+            if (r) return r;
+        }
+        w->n_relayout_seg++;
+    }
+
+    // device: pack movers (old slots), then unpack into the new layout, then the metadata
+    const int32_t rw = w->row_words;
+    w->mhost.clear();
+    const size_t o_ps = stage_list(w, pack_src), o_ud = stage_list(w, un_dst), o_us = stage_list(w, un_src);
+    const size_t o_ms = stage_list(w, m.slot), o_mo = stage_list(w, m.obj), o_md = stage_list(w, m.desc);
+    const size_t o_mp = stage_list(w, m.pl);
+    int r = dev_reserve(w, &w->mlist, &w->mlist_cap, w->mhost.size() + 16);
+    if (r) return r;
+    r = dev_reserve(w, (void**)&w->mv_rows, &w->mv_cap, std::max<size_t>(pack_src.size(), 1) * rw * 8);
+    if (r) return r;
+    HIPCHK(hipMemcpyAsync(w->mlist, w->mhost.data(), w->mhost.size(), hipMemcpyHostToDevice, w->stream));
+    char* L = (char*)w->mlist;
+    if (!pack_src.empty())
+        hipLaunchKernelGGL(k_pack, dim3(grid_for(pack_src.size() * rw)), dim3(kTPB), 0, w->stream, d,
+                           (const int32_t*)(L + o_ps), (int32_t)pack_src.size(), rw, w->mv_rows);
+    if (!un_dst.empty())
+        hipLaunchKernelGGL(k_unpack, dim3(grid_for(un_dst.size() * rw)), dim3(kTPB), 0, w->stream, d,
+                           (const int32_t*)(L + o_ud), (const int64_t*)(L + o_us), (int32_t)un_dst.size(), rw,
+                           (const uint64_t*)w->mv_rows, (const uint64_t*)w->ins_rows);
+    if (!m.slot.empty())
+        hipLaunchKernelGGL(k_meta, dim3(grid_for(m.slot.size())), dim3(kTPB), 0, w->stream,
+                           (const int32_t*)(L + o_ms), (const int32_t*)(L + o_mo), (const uint64_t*)(L + o_md),
+                           (const int32_t*)(L + o_mp), (int32_t)m.slot.size(), w->slot_obj_d, w->fan_desc_w,
+                           w->pl_slot_w);
+    HIPCHK(hipGetLastError());
+    // the pageable staging must outlive the copy
+    HIPCHK(hipStreamSynchronize(w->stream));
+
+    // host maps
+    if (full) {
+        w->segs = std::move(nsegs);
+        w->seg_of.clear();
+        for (size_t g = 0; g < w->segs.size(); g++) w->seg_of[{w->segs[g].scene, w->segs[g].group}] = (int32_t)g;
+        std::fill(w->obj_of_slot.begin(), w->obj_of_slot.end(), -1);
+        std::fill(w->slot_of_obj.begin(), w->slot_of_obj.end(), -1);
+        int64_t total = 0;
+        for (const auto& g : w->segs) total = (int64_t)g.base + g.cap;
+        set_tiles(d, (int32_t)total);
+        aff.clear();
+        for (size_t g = 0; g < w->segs.size(); g++) aff.push_back((int32_t)g);
+    }
+    for (int32_t o : w->touched)
+        if (!w->alive[o]) w->slot_of_obj[o] = -1;
+    for (int32_t gi : aff) {
+        const World::Seg& g = w->segs[gi];
+        for (int32_t i = 0; i < g.cap; i++) {
+            const int32_t ns = g.base + i;
+            const int32_t o = i < (int32_t)g.objs.size() ? g.objs[i] : -1;
+            w->obj_of_slot[ns] = o;
+            if (o >= 0) w->slot_of_obj[o] = ns;
+        }
+    }
+    for (int32_t o : w->touched) {
+        w->m_flag[o] = 0;
+        w->src_row[o] = -1;
+    }
+    w->touched.clear();
+    w->ins_n = 0;
+    return NFK_OK;
+}
+
+// a new object index (creation order in this world)
+int32_t add_object(World* w, int64_t gh, int64_t gd, int32_t scene, int32_t group, uint8_t cls, uint8_t pl) {
+    const int32_t o = w->n_obj++;
+    w->obj_of[GuidKey{gh, gd}] = o;
+    w->gh.push_back(gh);
+    w->gd.push_back(gd);
+    w->scene.push_back(scene);
+    w->group.push_back(group);
+    w->cls.push_back(cls);
+    w->isplayer.push_back(pl ? 1 : 0);
+    w->alive.push_back(1);
+    w->src_row.push_back(-1);
+    w->m_flag.push_back(0);
+    w->slot_of_obj.push_back(-1);
+    return o;
+}
+
+void touch(World* w, int32_t o) {
+    if (!w->m_flag[o]) {
+        w->m_flag[o] = 1;
+        w->touched.push_back(o);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -250,7 +570,7 @@ const char* nfk_last_error(void) { return g_err.c_str(); }
 int nfk_create(const nfk_config* cfg, void** out) {
     if (!cfg || !out) return fail(NFK_ERR_ARG, "null argument");
     if (cfg->capacity <= 0 || cfg->n_int < 0 || cfg->n_int > NFK_MAX_INT_PROPS || cfg->n_flt < 0 ||
-        cfg->n_flt > NFK_MAX_FLT_PROPS || cfg->n_class <= 0 || cfg->n_class > NFK_MAX_CLASSES ||
+        cfg->n_flt > NFK_MAX_FLT_PROPS || cfg->n_class <= 0 || cfg->n_class > NFK_MAX_CLASSES - 1 ||
         cfg->n_kind < 0 || cfg->n_kind > NFK_MAX_KINDS || cfg->n_rec < 0 || cfg->n_rec > NFK_MAX_RECORDS)
         return fail(NFK_ERR_ARG, "config out of range");
     int ndev = 0;
@@ -259,6 +579,7 @@ int nfk_create(const nfk_config* cfg, void** out) {
     World* w = new World();
     w->cfg = *cfg;
     w->n_prop = cfg->n_int + cfg->n_flt;
+    w->slack = cfg->slack_per_256 == 0 ? 16 : std::max(cfg->slack_per_256, 0);
     if (cfg->stream) {
         w->stream = (hipStream_t)cfg->stream;
     } else {
@@ -288,6 +609,9 @@ int nfk_destroy(void* world) {
     if (w->pin) (void)hipHostFree(w->pin);
     if (w->stage) (void)hipFree(w->stage);
     if (w->dense) (void)hipFree(w->dense);
+    if (w->ins_rows) (void)hipFree(w->ins_rows);
+    if (w->mv_rows) (void)hipFree(w->mv_rows);
+    if (w->mlist) (void)hipFree(w->mlist);
     for (auto& p : w->pend) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -367,7 +691,7 @@ int nfk_create_objects(void* world, int32_t n, const int64_t* gh, const int64_t*
     World* w = (World*)world;
     if (!w || n < 0 || (n && (!gh || !gd || !scene || !group || !cls || !isplayer)))
         return fail(NFK_ERR_ARG, "null argument");
-    if (w->committed) return fail(NFK_ERR_STATE, "objects after commit are not supported yet");
+    if (w->committed) return fail(NFK_ERR_STATE, "after commit, create objects with nfk_import_objects / nfk_spawn_objects");
     if ((int64_t)w->n_obj + n > w->cfg.capacity) return fail(NFK_ERR_CAPACITY, "entity capacity exceeded");
     for (int32_t i = 0; i < n; i++) {
         if (cls[i] >= w->cfg.n_class) return fail(NFK_ERR_ARG, "class id out of range");
@@ -375,16 +699,7 @@ int nfk_create_objects(void* world, int32_t n, const int64_t* gh, const int64_t*
         GuidKey k{gh[i], gd[i]};
         if (w->obj_of.count(k)) return fail(NFK_ERR_ARG, "The object has Exists");  // KM:131
     }
-    for (int32_t i = 0; i < n; i++) {
-        w->obj_of[GuidKey{gh[i], gd[i]}] = w->n_obj + i;
-        w->gh.push_back(gh[i]);
-        w->gd.push_back(gd[i]);
-        w->scene.push_back(scene[i]);
-        w->group.push_back(group[i]);
-        w->cls.push_back(cls[i]);
-        w->isplayer.push_back(isplayer[i] ? 1 : 0);
-    }
-    w->n_obj += n;
+    for (int32_t i = 0; i < n; i++) add_object(w, gh[i], gd[i], scene[i], group[i], cls[i], isplayer[i]);
     return NFK_OK;
 }
 
@@ -411,7 +726,8 @@ int nfk_commit(void* world) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");
     if (w->committed) return fail(NFK_ERR_STATE, "already committed");
-    const int32_t N = w->n_obj, cap = w->cfg.capacity;
+    const int32_t cfg_cap = w->cfg.capacity;
+    int32_t cap = 0;
     const int NI = w->cfg.n_int, NF = w->cfg.n_flt, NK = w->cfg.n_kind, NR = w->cfg.n_rec;
     for (int r = 0; r < NR; r++)
         if (!w->rec_defined[r]) return fail(NFK_ERR_ARG, "record " + std::to_string(r) + " not defined");
@@ -498,48 +814,33 @@ int nfk_commit(void* world) {
     if (w->n_dst_union > NFK_MAX_TOUCH)
         return fail(NFK_ERR_TOUCH, "programs write more than NFK_MAX_TOUCH distinct properties");
 
-    // membership layout: slots sorted by (scene, group, guid) — NFCSceneInfo/NFCSceneGroupInfo
-    // keep std::map<NFGUID> group lists, so GUID order is the fan-out order (AOI:572)
-    w->obj_of_slot.resize(N);
-    for (int32_t i = 0; i < N; i++) w->obj_of_slot[i] = i;
-    std::sort(w->obj_of_slot.begin(), w->obj_of_slot.end(), [w](int32_t a, int32_t b) {
-        if (w->scene[a] != w->scene[b]) return w->scene[a] < w->scene[b];
-        if (w->group[a] != w->group[b]) return w->group[a] < w->group[b];
-        if (w->gh[a] != w->gh[b]) return w->gh[a] < w->gh[b];
-        return w->gd[a] < w->gd[b];
-    });
-    w->slot_of_obj.resize(N);
-    for (int32_t s = 0; s < N; s++) w->slot_of_obj[w->obj_of_slot[s]] = s;
-    std::vector<int32_t> seg_of(N), seg_pl_off, pl_slot, pl_rank(N, -1);
-    std::vector<uint8_t> cls_s(N);
-    int32_t nseg = 0;
-    for (int32_t s = 0; s < N; s++) {
-        int32_t o = w->obj_of_slot[s];
-        if (s == 0 || w->scene[o] != w->scene[w->obj_of_slot[s - 1]] || w->group[o] != w->group[w->obj_of_slot[s - 1]]) {
-            seg_pl_off.push_back((int32_t)pl_slot.size());
-            nseg++;
-        }
-        seg_of[s] = nseg - 1;
-        cls_s[s] = w->cls[o];
-        if (w->isplayer[o]) {
-            pl_rank[s] = (int32_t)pl_slot.size() - seg_pl_off.back();
-            pl_slot.push_back(s);
-        }
+    // membership layout: scene-group segments, NFGUID order inside (see apply_membership)
+    const int64_t n_slots = plan_segments(w, w->slack, w->segs);
+    for (size_t g = 0; g < w->segs.size(); g++) w->seg_of[{w->segs[g].scene, w->segs[g].group}] = (int32_t)g;
+    MetaLists meta;
+    for (const auto& g : w->segs) {
+        int r = seg_meta(w, g, meta);
+        if (r) return r;
     }
-    seg_pl_off.push_back((int32_t)pl_slot.size());
-    w->nseg = nseg;
-    std::vector<uint64_t> fan_desc(N);
-    for (int32_t s = 0; s < N; s++) {
-        const int32_t pb = seg_pl_off[seg_of[s]], np = seg_pl_off[seg_of[s] + 1] - pb;
-        if (np > 0x3FFF) return fail(NFK_ERR_ARG, "more than 16383 players in one scene group");
-        fan_desc[s] = (uint64_t)(uint32_t)pb | ((uint64_t)np << 32) | ((uint64_t)(pl_rank[s] + 1) << 46) |
-                      ((uint64_t)cls_s[s] << 60);
+    {
+        // slot capacity: the population plus slack, and at least the configured capacity plus slack
+        const int64_t want = std::max<int64_t>(n_slots, (int64_t)cfg_cap + (int64_t)cfg_cap * w->slack / 256);
+        const int64_t c = (want + kTile - 1) / kTile * kTile;
+        if (c > INT32_MAX / 2) return fail(NFK_ERR_CAPACITY, "slot capacity too large");
+        cap = (int32_t)c;
     }
+    w->obj_of_slot.assign(cap, -1);
+    for (size_t i = 0; i < meta.slot.size(); i++) {
+        w->obj_of_slot[meta.slot[i]] = meta.obj[i];
+        if (meta.obj[i] >= 0) w->slot_of_obj[meta.obj[i]] = meta.slot[i];
+    }
+    w->row_words = w->n_prop + 4 * NK;
+    for (int r = 0; r < NR; r++) w->row_words += w->tab.rec_rows[r] * w->tab.rec_cols[r] + 1;
 
     // device allocation
     Dev& d = w->d;
-    d.N = N;
     d.cap = cap;
+    set_tiles(d, (int32_t)n_slots);
     d.n_int = NI;
     d.n_flt = NF;
     d.n_kind = NK;
@@ -561,24 +862,20 @@ int nfk_commit(void* world) {
         ALLOC(d.rcells[r], (size_t)cap * w->tab.rec_rows[r] * w->tab.rec_cols[r] * 8);
         ALLOC(d.rused[r], (size_t)cap * 8);
     }
-    int32_t* pl_slot_d;
-    ALLOC(pl_slot_d, std::max<size_t>(pl_slot.size(), 1) * 4);
+    ALLOC(w->pl_slot_w, (size_t)cap * 4);
     ALLOC(w->slot_obj_d, (size_t)cap * 4);
-    uint64_t* fan_desc_d;
-    ALLOC(fan_desc_d, (size_t)cap * 8);
-    d.fan_desc = fan_desc_d;
+    ALLOC(w->fan_desc_w, (size_t)cap * 8);
+    d.fan_desc = w->fan_desc_w;
     {
         const char* ab = getenv("NFGPU_ABLATE");
         d.ablate = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0u;
     }
-    d.pl_slot = pl_slot_d;
-    // tiles (sized for the committed population; objects after commit are not supported)
-    d.n_tiles = (N + kTile - 1) / kTile;
-    d.n_rtiles = (N + kRTile - 1) / kRTile;
+    d.pl_slot = w->pl_slot_w;
+    // output staging sized for every tile of the slot capacity
     d.ev_tcap = kTile * std::min(NFK_MAX_TOUCH, std::max(w->n_prop, 1));
     d.fi_tcap = kTile * std::max(NK, 1);
     d.re_tcap = (int32_t)(kRTile * std::max<size_t>(rec_events_per_ent, 1));
-    const size_t nt = std::max(d.n_tiles, 1), nrt = std::max(d.n_rtiles, 1);
+    const size_t nt = cap / kTile, nrt = cap / kRTile;
     const size_t ev_n = nt * d.ev_tcap, fi_n = nt * d.fi_tcap, re_n = nro ? nrt * d.re_tcap : 1;
     ALLOC(d.t_ev, nt * 4);
     ALLOC(d.t_fi, nt * 4);
@@ -614,7 +911,8 @@ int nfk_commit(void* world) {
     for (int p = 0; p < w->n_prop; p++) {
         std::fill(col.begin(), col.end(), 0);
         if (!w->init_props[p].empty())
-            for (int32_t s = 0; s < N; s++) col[s] = w->init_props[p][w->obj_of_slot[s]];
+            for (int32_t s = 0; s < d.N; s++)
+                if (w->obj_of_slot[s] >= 0) col[s] = w->init_props[p][w->obj_of_slot[s]];
         void* dst = p < NI ? (void*)(d.icol + (size_t)p * cap) : (void*)(d.fcol + (size_t)(p - NI) * cap);
         HIPCHK(hipMemcpy(dst, col.data(), (size_t)cap * 8, hipMemcpyHostToDevice));
     }
@@ -622,8 +920,9 @@ int nfk_commit(void* world) {
         size_t per = (size_t)w->tab.rec_rows[r] * w->tab.rec_cols[r];
         std::vector<uint64_t> cells(per * cap, 0), used(cap, 0);
         if (!w->init_rcells[r].empty())
-            for (int32_t s = 0; s < N; s++) {
+            for (int32_t s = 0; s < d.N; s++) {
                 int32_t o = w->obj_of_slot[s];
+                if (o < 0) continue;
                 memcpy(&cells[(size_t)s * per], &w->init_rcells[r][(size_t)o * per], per * 8);
                 used[s] = w->init_rused[r][o];
             }
@@ -632,7 +931,18 @@ int nfk_commit(void* world) {
     }
     HIPCHK(hipMemset(d.s_hot, 0, (size_t)std::max(NK, 1) * cap * sizeof(SchedHot)));
     HIPCHK(hipMemset(d.s_cold, 0, (size_t)std::max(NK, 1) * cap * sizeof(SchedCold)));
-    HIPCHK(hipMemcpy(fan_desc_d, fan_desc.data(), (size_t)N * 8, hipMemcpyHostToDevice));
+    {
+        std::vector<uint64_t> fd(cap, kDeadDesc);
+        std::vector<int32_t> pls(cap, 0), so(cap, -1);
+        for (size_t i = 0; i < meta.slot.size(); i++) {
+            fd[meta.slot[i]] = meta.desc[i];
+            pls[meta.slot[i]] = meta.pl[i];
+            so[meta.slot[i]] = meta.obj[i];
+        }
+        HIPCHK(hipMemcpy(w->fan_desc_w, fd.data(), (size_t)cap * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(w->pl_slot_w, pls.data(), (size_t)cap * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(w->slot_obj_d, so.data(), (size_t)cap * 4, hipMemcpyHostToDevice));
+    }
     HIPCHK(hipMemset(d.e_flags, 0, cap));
     HIPCHK(hipMemset(d.ext_head, 0, (size_t)cap * 4));
     HIPCHK(hipMemset(d.fired_mask, 0, (size_t)cap * 4));
@@ -644,8 +954,6 @@ int nfk_commit(void* world) {
     HIPCHK(hipMemset(d.fi_base, 0, (nt + 1) * 4));
     HIPCHK(hipMemset(d.re_base, 0, (nrt + 1) * 4));
     HIPCHK(hipMemset(d.msg_base, 0, (nt + nrt + 1) * 4));
-    if (!pl_slot.empty()) HIPCHK(hipMemcpy(pl_slot_d, pl_slot.data(), pl_slot.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(w->slot_obj_d, w->obj_of_slot.data(), (size_t)N * 4, hipMemcpyHostToDevice));
     // creation-time values are now on the device
     for (auto& v : w->init_props) std::vector<uint64_t>().swap(v);
     for (auto& v : w->init_rcells) std::vector<uint64_t>().swap(v);
@@ -665,7 +973,7 @@ int nfk_set_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
         if (pid[i] < 0 || pid[i] >= w->n_prop) return fail(NFK_ERR_ARG, "bad property id");
     }
     for (int32_t i = 0; i < n; i++)
-        w->xops.push_back({(uint32_t)w->slot_of_obj[w->obj_of[GuidKey{gh[i], gd[i]}]], (uint32_t)pid[i], bits[i]});
+        w->xops.push_back({(uint32_t)w->obj_of[GuidKey{gh[i], gd[i]}], (uint32_t)pid[i], bits[i]});
     return NFK_OK;
 }
 
@@ -684,7 +992,7 @@ int nfk_add_schedules(void* world, int32_t n, const int64_t* gh, const int64_t* 
     }
     for (int32_t i = 0; i < n; i++) {
         int32_t obj = w->obj_of[GuidKey{gh[i], gd[i]}];
-        w->hops.push_back({1, (uint32_t)w->slot_of_obj[obj], (uint32_t)kind[i], interval[i], count[i], now_ms[i]});
+        w->hops.push_back({1, (uint32_t)obj, (uint32_t)kind[i], interval[i], count[i], now_ms[i]});
     }
     return NFK_OK;
 }
@@ -697,7 +1005,7 @@ int nfk_remove_schedule(void* world, int64_t gh, int64_t gd, int32_t kind) {
     int r = lookup(w, gh, gd, &obj);
     if (r) return r;
     if (kind < 0 || kind >= w->cfg.n_kind) return fail(NFK_ERR_ARG, "bad kind");
-    w->hops.push_back({2, (uint32_t)w->slot_of_obj[obj], (uint32_t)kind, 0.f, 0, 0});
+    w->hops.push_back({2, (uint32_t)obj, (uint32_t)kind, 0.f, 0, 0});
     return NFK_OK;
 }
 
@@ -708,14 +1016,208 @@ int nfk_remove_all_schedules(void* world, int64_t gh, int64_t gd) {
     int32_t obj;
     int r = lookup(w, gh, gd, &obj);
     if (r) return r;
-    w->hops.push_back({3, (uint32_t)w->slot_of_obj[obj], 0u, 0.f, 0, 0});
+    w->hops.push_back({3, (uint32_t)obj, 0u, 0.f, 0, 0});
     return NFK_OK;
+}
+
+int nfk_set_scene_props(void* world, int32_t pid_scene, int32_t pid_group, int32_t pid_x, int32_t pid_y,
+                        int32_t pid_z) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    const int NI = w->cfg.n_int;
+    auto ok_i = [&](int32_t p) { return p == -1 || (p >= 0 && p < NI); };
+    auto ok_f = [&](int32_t p) { return p == -1 || (p >= NI && p < w->n_prop); };
+    if (!ok_i(pid_scene) || !ok_i(pid_group) || !ok_f(pid_x) || !ok_f(pid_y) || !ok_f(pid_z))
+        return fail(NFK_ERR_ARG, "SceneID/GroupID must be int properties, X/Y/Z float properties");
+    w->pid_scene = pid_scene;
+    w->pid_group = pid_group;
+    w->pid_x = pid_x;
+    w->pid_y = pid_y;
+    w->pid_z = pid_z;
+    return NFK_OK;
+}
+
+int nfk_switch_scene(void* world, int64_t gh, int64_t gd, int32_t scene, int32_t group, float x, float y, float z) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    int32_t o;
+    int r = lookup(w, gh, gd, &o);
+    if (r) return r;  // "There is no object" (KM:948)
+    if (group < 0) return fail(NFK_ERR_ARG, "negative group");
+    // the property writes of KM:931-942, in call order (queued like SetProperty*)
+    auto put = [&](int32_t pid, uint64_t bits) {
+        if (pid >= 0) w->xops.push_back({(uint32_t)o, (uint32_t)pid, bits});
+    };
+    auto dbits = [](double v) {
+        uint64_t u;
+        memcpy(&u, &v, 8);
+        return u;
+    };
+    if (scene != w->scene[o]) {
+        put(w->pid_group, 0);
+        put(w->pid_scene, (uint64_t)(int64_t)scene);
+    }
+    put(w->pid_x, dbits((double)x));
+    put(w->pid_y, dbits((double)y));
+    put(w->pid_z, dbits((double)z));
+    put(w->pid_group, (uint64_t)(int64_t)group);
+    // RemoveObjectFromGroup + AddObjectToGroup (KM:928, 944): a new slot in the target group
+    if (scene != w->scene[o] || group != w->group[o]) {
+        w->scene[o] = scene;
+        w->group[o] = group;
+        touch(w, o);
+    }
+    return NFK_OK;
+}
+
+int nfk_destroy_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    for (int32_t i = 0; i < n; i++) {
+        int32_t o;
+        int r = lookup(w, gh[i], gd[i], &o);
+        if (r) return r;
+    }
+    for (int32_t i = 0; i < n; i++) {
+        const int32_t o = w->obj_of[GuidKey{gh[i], gd[i]}];
+        w->obj_of.erase(GuidKey{gh[i], gd[i]});
+        w->alive[o] = 0;
+        touch(w, o);
+    }
+    return NFK_OK;
+}
+
+int nfk_object_count(void* world, int32_t* n) {
+    World* w = (World*)world;
+    if (!w || !n) return fail(NFK_ERR_ARG, "null argument");
+    *n = w->n_obj;
+    return NFK_OK;
+}
+
+int nfk_row_words(void* world, int32_t* words) {
+    World* w = (World*)world;
+    if (!w || !words) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    *words = w->row_words;
+    return NFK_OK;
+}
+
+int nfk_export_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd, uint64_t* rows_dev) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !rows_dev))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    if (n == 0) return NFK_OK;
+    std::vector<int32_t> src(n), objs(n);
+    for (int32_t i = 0; i < n; i++) {
+        int r = lookup(w, gh[i], gd[i], &objs[i]);
+        if (r) return r;
+        if (w->m_flag[objs[i]] || w->slot_of_obj[objs[i]] < 0)
+            return fail(NFK_ERR_STATE, "export of an object whose membership already changed in this window");
+        src[i] = w->slot_of_obj[objs[i]];
+    }
+    w->mhost.clear();
+    const size_t o_src = stage_list(w, src);
+    int r = dev_reserve(w, &w->mlist, &w->mlist_cap, w->mhost.size() + 16);
+    if (r) return r;
+    HIPCHK(hipMemcpyAsync(w->mlist, w->mhost.data(), w->mhost.size(), hipMemcpyHostToDevice, w->stream));
+    hipLaunchKernelGGL(k_pack, dim3(grid_for((size_t)n * w->row_words)), dim3(kTPB), 0, w->stream, w->d,
+                       (const int32_t*)((char*)w->mlist + o_src), n, w->row_words, rows_dev);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(w->stream));  // the pageable staging must outlive the copy
+    for (int32_t i = 0; i < n; i++) {
+        w->obj_of.erase(GuidKey{gh[i], gd[i]});
+        w->alive[objs[i]] = 0;
+        touch(w, objs[i]);
+    }
+    return NFK_OK;
+}
+
+static int import_common(World* w, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* scene,
+                         const int32_t* group, const uint8_t* cls, const uint8_t* isplayer, const void* rows,
+                         hipMemcpyKind kind) {
+    if (n < 0 || (n && (!gh || !gd || !scene || !group || !cls || !isplayer || !rows)))
+        return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first (before it, use nfk_create_objects)");
+    if (n == 0) return NFK_OK;
+    for (int32_t i = 0; i < n; i++) {
+        if (cls[i] >= w->cfg.n_class) return fail(NFK_ERR_ARG, "class id out of range");
+        if (group[i] < 0) return fail(NFK_ERR_ARG, "negative group");
+        if (w->obj_of.count(GuidKey{gh[i], gd[i]})) return fail(NFK_ERR_ARG, "The object has Exists");  // KM:131
+        for (int32_t j = 0; j < i; j++)
+            if (gh[j] == gh[i] && gd[j] == gd[i]) return fail(NFK_ERR_ARG, "The object has Exists");
+    }
+    const size_t rb = (size_t)w->row_words * 8;
+    if (w->ins_n + n > w->ins_cap) {
+        // grow, keeping this window's earlier rows
+        const size_t c = std::max(w->ins_n + n, w->ins_cap * 2);
+        uint64_t* p = nullptr;
+        HIPCHK(hipMalloc((void**)&p, c * rb));
+        if (w->ins_n) HIPCHK(hipMemcpyAsync(p, w->ins_rows, w->ins_n * rb, hipMemcpyDeviceToDevice, w->stream));
+        HIPCHK(hipStreamSynchronize(w->stream));
+        if (w->ins_rows) HIPCHK(hipFree(w->ins_rows));
+        w->ins_rows = p;
+        w->ins_cap = c;
+    }
+    HIPCHK(hipMemcpyAsync(w->ins_rows + w->ins_n * w->row_words, rows, (size_t)n * rb, kind, w->stream));
+    if (kind == hipMemcpyHostToDevice) HIPCHK(hipStreamSynchronize(w->stream));
+    for (int32_t i = 0; i < n; i++) {
+        const int32_t o = add_object(w, gh[i], gd[i], scene[i], group[i], cls[i], isplayer[i]);
+        w->src_row[o] = (int64_t)(w->ins_n + i);
+        touch(w, o);
+    }
+    w->ins_n += n;
+    return NFK_OK;
+}
+
+int nfk_import_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* scene,
+                       const int32_t* group, const uint8_t* cls, const uint8_t* isplayer, const uint64_t* rows_dev) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    return import_common(w, n, gh, gd, scene, group, cls, isplayer, rows_dev, hipMemcpyDeviceToDevice);
+}
+
+int nfk_spawn_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* scene,
+                      const int32_t* group, const uint8_t* cls, const uint8_t* isplayer, const uint64_t* props) {
+    World* w = (World*)world;
+    if (!w || (n > 0 && !props)) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first (before it, use nfk_create_objects)");
+    std::vector<uint64_t> rows((size_t)std::max(n, 0) * w->row_words, 0);
+    for (int32_t i = 0; i < n; i++)
+        memcpy(&rows[(size_t)i * w->row_words], props + (size_t)i * w->n_prop, (size_t)w->n_prop * 8);
+    return import_common(w, n, gh, gd, scene, group, cls, isplayer, rows.data(), hipMemcpyHostToDevice);
 }
 
 int nfk_execute(void* world, int64_t now_ms) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    // ---- membership changes of this window, then queued calls: object -> slot ----
+    {
+        int r = apply_membership(w);
+        if (r) {
+            w->xops.clear();
+            w->hops.clear();
+            return r;
+        }
+        size_t k = 0;
+        for (size_t i = 0; i < w->xops.size(); i++) {
+            const int32_t sl = w->slot_of_obj[w->xops[i].slot];
+            if (sl < 0) continue;  // destroyed / exported: "There is no object"
+            w->xops[k] = w->xops[i];
+            w->xops[k++].slot = (uint32_t)sl;
+        }
+        w->xops.resize(k);
+        k = 0;
+        for (size_t i = 0; i < w->hops.size(); i++) {
+            const int32_t sl = w->slot_of_obj[w->hops[i].slot];
+            if (sl < 0) continue;
+            w->hops[k] = w->hops[i];
+            w->hops[k++].slot = (uint32_t)sl;
+        }
+        w->hops.resize(k);
+    }
     Dev d = w->d;
     d.now = now_ms;
 
@@ -917,7 +1419,11 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     Ctrl c;
     HIPCHK(hipMemcpy(&c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
     memset(out, 0, sizeof *out);
-    out->n_entities = w->d.N;
+    {
+        int64_t live = 0;
+        for (const auto& g : w->segs) live += (int64_t)g.objs.size();
+        out->n_entities = live;
+    }
     out->n_prop_events = (int64_t)c.n_ev;
     out->n_rec_events = (int64_t)c.n_re;
     out->n_fired = (int64_t)c.n_fi;
@@ -990,7 +1496,9 @@ int nfk_read_prop(void* world, int32_t pid, uint64_t* bits) {
     const void* src = pid < d.n_int ? (const void*)(d.icol + (size_t)pid * d.cap)
                                     : (const void*)(d.fcol + (size_t)(pid - d.n_int) * d.cap);
     HIPCHK(hipMemcpy(col.data(), src, (size_t)d.N * 8, hipMemcpyDeviceToHost));
-    for (int32_t s = 0; s < d.N; s++) bits[w->obj_of_slot[s]] = col[s];
+    memset(bits, 0, (size_t)w->n_obj * 8);  // objects no longer in this world read 0
+    for (int32_t s = 0; s < d.N; s++)
+        if (w->obj_of_slot[s] >= 0) bits[w->obj_of_slot[s]] = col[s];
     return NFK_OK;
 }
 
@@ -1003,7 +1511,9 @@ int nfk_read_record(void* world, int32_t rec, uint64_t* cells) {
     size_t per = (size_t)w->tab.rec_rows[rec] * w->tab.rec_cols[rec];
     std::vector<uint64_t> buf(per * d.N);
     HIPCHK(hipMemcpy(buf.data(), d.rcells[rec], buf.size() * 8, hipMemcpyDeviceToHost));
-    for (int32_t s = 0; s < d.N; s++) memcpy(cells + (size_t)w->obj_of_slot[s] * per, &buf[(size_t)s * per], per * 8);
+    memset(cells, 0, (size_t)w->n_obj * per * 8);
+    for (int32_t s = 0; s < d.N; s++)
+        if (w->obj_of_slot[s] >= 0) memcpy(cells + (size_t)w->obj_of_slot[s] * per, &buf[(size_t)s * per], per * 8);
     return NFK_OK;
 }
 
@@ -1016,8 +1526,12 @@ int nfk_read_schedules(void* world, int64_t* next_ms, int32_t* remain, uint8_t* 
     const int NK = d.n_kind;
     std::vector<SchedHot> hot((size_t)NK * d.cap);
     if (NK) HIPCHK(hipMemcpy(hot.data(), d.s_hot, hot.size() * sizeof(SchedHot), hipMemcpyDeviceToHost));
+    memset(state, 0, (size_t)NK * w->n_obj);
+    memset(next_ms, 0, (size_t)NK * w->n_obj * 8);
+    memset(remain, 0, (size_t)NK * w->n_obj * 4);
     for (int k = 0; k < NK; k++)
         for (int32_t s = 0; s < d.N; s++) {
+            if (w->obj_of_slot[s] < 0) continue;
             size_t o = (size_t)k * w->n_obj + w->obj_of_slot[s], a = (size_t)k * d.cap + s;
             const SchedHot& h = hot[a];
             state[o] = (uint8_t)(h.state & (kStPresent | kStForever));

@@ -484,11 +484,11 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
             pfi++;
             bytes += 12;
         }
-        if (d.has_recops) {
-            d.fired_mask[e] = fired;
-            bytes += 4;
-        }
         if (xh) d.ext_head[e] = 0;
+    }
+    if (d.has_recops && e < d.N) {  // slack slots too: a slot's previous occupant left a mask
+        d.fired_mask[e] = fired;
+        bytes += 4;
     }
     // tile counts and algorithmic-byte tally
     const unsigned wb = (unsigned)wave_sum(bytes);
@@ -633,11 +633,11 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
             pfi++;
             en.bytes += 12;
         }
-        if (d.has_recops) {
-            d.fired_mask[e] = fired;
-            en.bytes += 4;
-        }
         if (xh) d.ext_head[e] = 0;
+    }
+    if (d.has_recops && e < d.N) {  // slack slots too: a slot's previous occupant left a mask
+        d.fired_mask[e] = fired;
+        en.bytes += 4;
     }
     // tile counts and algorithmic-byte tally
     const unsigned wb = (unsigned)wave_sum(en.bytes);
@@ -983,6 +983,68 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
     if ((threadIdx.x & 63) == 0 && wb) atomicAdd(&s_bytes, wb);
     __syncthreads();
     if (threadIdx.x == 0) atomicAdd(&d.ctrl->bytes_fan, (unsigned long long)s_bytes);
+}
+
+// ---------------------------------------------------------------------------------
+// Membership changes (SwitchScene / DestroyObject / cross-shard migration): an entity's state
+// travels as a ROW of 64-bit words — its properties, its schedule records (hot 2 words + cold 2
+// words per kind) and its record cells + used mask per record.  k_pack gathers rows from slots,
+// k_unpack scatters rows (or zeros: a slack slot) into slots, k_meta rewrites the per-slot
+// membership metadata of the scene-group segments that changed.  Thread t handles word
+// t / n of row t % n, so a wave reads one column across consecutive slots.
+__device__ __forceinline__ uint64_t* row_word(const Dev& d, int32_t s, int w) {
+    if (w < d.n_int) return (uint64_t*)(d.icol + (size_t)w * d.cap + s);
+    w -= d.n_int;
+    if (w < d.n_flt) return (uint64_t*)(d.fcol + (size_t)w * d.cap + s);
+    w -= d.n_flt;
+    if (w < 4 * d.n_kind) {
+        const int k = w >> 2, q = w & 3;
+        return q < 2 ? (uint64_t*)&d.s_hot[(size_t)k * d.cap + s] + q
+                     : (uint64_t*)&d.s_cold[(size_t)k * d.cap + s] + (q - 2);
+    }
+    w -= 4 * d.n_kind;
+    for (int r = 0; r < d.n_rec; r++) {
+        const int per = d.tab->rec_rows[r] * d.tab->rec_cols[r];
+        if (w < per) return d.rcells[r] + (size_t)s * per + w;
+        if (w == per) return d.rused[r] + s;
+        w -= per + 1;
+    }
+    return nullptr;  // unreachable for w < row words
+}
+
+__global__ __launch_bounds__(kTPB) void k_pack(Dev d, const int32_t* __restrict__ src, int32_t n, int32_t rw,
+                                               uint64_t* __restrict__ rows) {
+    const size_t total = (size_t)n * rw;
+    for (size_t t = (size_t)blockIdx.x * kTPB + threadIdx.x; t < total; t += (size_t)gridDim.x * kTPB) {
+        const int32_t i = (int32_t)(t % (size_t)n), w = (int32_t)(t / (size_t)n);
+        rows[(size_t)i * rw + w] = *row_word(d, src[i], w);
+    }
+}
+
+// src[i] >= 0: row src[i] of mv; kZeroRow: zeros (a slack slot); else row -1 - src[i] of ins
+constexpr int64_t kZeroRow = INT64_MIN;
+__global__ __launch_bounds__(kTPB) void k_unpack(Dev d, const int32_t* __restrict__ dst,
+                                                 const int64_t* __restrict__ src, int32_t n, int32_t rw,
+                                                 const uint64_t* __restrict__ mv, const uint64_t* __restrict__ ins) {
+    const size_t total = (size_t)n * rw;
+    for (size_t t = (size_t)blockIdx.x * kTPB + threadIdx.x; t < total; t += (size_t)gridDim.x * kTPB) {
+        const int32_t i = (int32_t)(t % (size_t)n), w = (int32_t)(t / (size_t)n);
+        const int64_t r = src[i];
+        const uint64_t x = r == kZeroRow ? 0ull : (r >= 0 ? mv[(size_t)r * rw + w] : ins[(size_t)(-1 - r) * rw + w]);
+        *row_word(d, dst[i], w) = x;
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void k_meta(const int32_t* __restrict__ slot, const int32_t* __restrict__ obj,
+                                               const uint64_t* __restrict__ desc, const int32_t* __restrict__ pl,
+                                               int32_t n, int32_t* __restrict__ slot_obj,
+                                               uint64_t* __restrict__ fan_desc, int32_t* __restrict__ pl_slot) {
+    const int32_t i = blockIdx.x * kTPB + threadIdx.x;
+    if (i >= n) return;
+    const int32_t s = slot[i];
+    slot_obj[s] = obj[i];
+    fan_desc[s] = desc[i];
+    pl_slot[s] = pl[i];
 }
 
 // ---------------------------------------------------------------------------------

@@ -32,7 +32,7 @@ class NFKError(RuntimeError):
 class Config(ctypes.Structure):
     _fields_ = [("capacity", ctypes.c_int32), ("n_int", ctypes.c_int32), ("n_flt", ctypes.c_int32),
                 ("n_class", ctypes.c_int32), ("n_kind", ctypes.c_int32), ("n_rec", ctypes.c_int32),
-                ("msg_capacity", ctypes.c_int64), ("stream", ctypes.c_void_p)]
+                ("msg_capacity", ctypes.c_int64), ("stream", ctypes.c_void_p), ("slack_per_256", ctypes.c_int32)]
 
 
 class Summary(ctypes.Structure):
@@ -83,6 +83,12 @@ def load_library(path=LIB_PATH):
         "nfk_read_events": [VP, VP, VP, VP, VP], "nfk_read_rec_events": [VP, VP, VP, VP, VP],
         "nfk_read_fired": [VP, VP, VP, VP], "nfk_read_fanout": [VP, VP, VP],
         "nfk_set_profiling": [VP, I32], "nfk_kernel_times": [VP, VP, VP, VP], "nfk_reset_kernel_times": [VP],
+        "nfk_set_scene_props": [VP, I32, I32, I32, I32, I32],
+        "nfk_switch_scene": [VP, I64, I64, I32, I32, ctypes.c_float, ctypes.c_float, ctypes.c_float],
+        "nfk_destroy_objects": [VP, I32, VP, VP], "nfk_object_count": [VP, VP], "nfk_row_words": [VP, VP],
+        "nfk_export_objects": [VP, I32, VP, VP, VP],
+        "nfk_import_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
+        "nfk_spawn_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -100,9 +106,9 @@ class NFKernelModule:
     """One GPU-resident world (the entities of one scene shard)."""
 
     def __init__(self, capacity, n_int=wl.N_INT, n_flt=wl.N_FLT, n_class=2, n_kind=len(wl.KINDS), n_rec=0,
-                 msg_capacity=0, stream=None):
+                 msg_capacity=0, stream=None, slack_per_256=0):
         self.lib = load_library()
-        cfg = Config(capacity, n_int, n_flt, n_class, n_kind, n_rec, msg_capacity, stream)
+        cfg = Config(capacity, n_int, n_flt, n_class, n_kind, n_rec, msg_capacity, stream, slack_per_256)
         h = ctypes.c_void_p()
         self._chk(self.lib.nfk_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -201,6 +207,54 @@ class NFKernelModule:
             self._chk(self.lib.nfk_remove_schedule(self.h, int(guid[0]), int(guid[1]), kind))
         return True
 
+    # ---- runtime membership (NFCKernelModule::SwitchScene / DestroyObject / CreateObject) ----
+    def set_scene_props(self, pid_scene, pid_group, pid_x, pid_y, pid_z):
+        self._chk(self.lib.nfk_set_scene_props(self.h, pid_scene, pid_group, pid_x, pid_y, pid_z))
+
+    def SwitchScene(self, guid, scene, group, x, y, z):
+        self._chk(self.lib.nfk_switch_scene(self.h, int(guid[0]), int(guid[1]), int(scene), int(group),
+                                            float(x), float(y), float(z)))
+        return True
+
+    def destroy_objects(self, guid_head, guid_data):
+        a = [np.ascontiguousarray(x, np.int64) for x in (guid_head, guid_data)]
+        self._chk(self.lib.nfk_destroy_objects(self.h, len(a[0]), _p(a[0]), _p(a[1])))
+
+    def DestroyObject(self, guid):
+        self.destroy_objects([guid[0]], [guid[1]])
+        return True
+
+    def object_count(self):
+        n = ctypes.c_int32()
+        self._chk(self.lib.nfk_object_count(self.h, ctypes.byref(n)))
+        return n.value
+
+    def row_words(self):
+        n = ctypes.c_int32()
+        self._chk(self.lib.nfk_row_words(self.h, ctypes.byref(n)))
+        return n.value
+
+    def export_objects(self, guid_head, guid_data, rows_dev_ptr):
+        """Pack the entities' state rows into device memory at rows_dev_ptr ([n][row_words] u64)
+        on the world's stream and remove them from this world."""
+        a = [np.ascontiguousarray(x, np.int64) for x in (guid_head, guid_data)]
+        self._chk(self.lib.nfk_export_objects(self.h, len(a[0]), _p(a[0]), _p(a[1]), ctypes.c_void_p(rows_dev_ptr)))
+
+    def import_objects(self, guid_head, guid_data, scene, group, cls, is_player, rows_dev_ptr):
+        a = [np.ascontiguousarray(x, t) for x, t in
+             ((guid_head, np.int64), (guid_data, np.int64), (scene, np.int32), (group, np.int32),
+              (cls, np.uint8), (is_player, np.uint8))]
+        self._chk(self.lib.nfk_import_objects(self.h, len(a[0]), *[_p(x) for x in a], ctypes.c_void_p(rows_dev_ptr)))
+        self.n_obj = self.object_count()
+
+    def spawn_objects(self, guid_head, guid_data, scene, group, cls, is_player, props):
+        a = [np.ascontiguousarray(x, t) for x, t in
+             ((guid_head, np.int64), (guid_data, np.int64), (scene, np.int32), (group, np.int32),
+              (cls, np.uint8), (is_player, np.uint8))]
+        pr = np.ascontiguousarray(props, np.uint64)
+        self._chk(self.lib.nfk_spawn_objects(self.h, len(a[0]), *[_p(x) for x in a], _p(pr)))
+        self.n_obj = self.object_count()
+
     # ---- one frame ----
     def Execute(self, now_ms):
         self._chk(self.lib.nfk_execute(self.h, int(now_ms)))
@@ -270,12 +324,16 @@ class NFKernelModule:
         self._chk(self.lib.nfk_reset_kernel_times(self.h))
 
 
-def world_from_workload(w, capacity=None, msg_capacity=0, stream=None):
+def world_from_workload(w, capacity=None, msg_capacity=0, stream=None, slack_per_256=0):
     """Build an NFKernelModule from a workload dict (see workload.make_world): classes,
     kinds, objects, creation-time values, then the AddSchedule calls made before frame 0."""
     cfg = w["cfg"]
     n_obj, n_int, n_flt, n_cls, n_kind, n_rec = (int(x) for x in cfg[:6])
-    m = NFKernelModule(capacity or n_obj, n_int, n_flt, n_cls, n_kind, n_rec, msg_capacity, stream)
+    m = NFKernelModule(capacity or n_obj, n_int, n_flt, n_cls, n_kind, n_rec, msg_capacity, stream, slack_per_256)
+    if "scene_props" in w:
+        m.set_scene_props(*(int(x) for x in w["scene_props"]))
+    m.cur_scene = np.array(w["scene"], np.int32)   # membership as SwitchScene calls change it
+    m.cur_group = np.array(w["group"], np.int32)
     for c in range(n_cls):
         m.set_prop_flags(c, w["prop_flags"][c])
     for r in range(n_rec):
@@ -298,8 +356,17 @@ def world_from_workload(w, capacity=None, msg_capacity=0, stream=None):
 
 
 def run_workload(m, w, tick, collect=True):
-    """Replay the between-frame calls of frame `tick`, then Execute it."""
+    """Replay the between-frame calls of frame `tick` (SwitchScene first, then schedule calls,
+    then SetProperty calls, as the oracle does), then Execute it."""
     gh, gd = w["guid_head"], w["guid_data"]
+    if "sw_tick" in w:
+        for i in np.nonzero(w["sw_tick"] == tick)[0]:
+            o = int(w["sw_obj"][i])
+            sc, gr = int(w["sw_scene"][i]), int(w["sw_group"][i])
+            if sc < 0:   # the object's own cell
+                sc, gr = int(m.cur_scene[o]), int(m.cur_group[o])
+            m.SwitchScene((int(gh[o]), int(gd[o])), sc, gr, w["sw_x"][i], w["sw_y"][i], w["sw_z"][i])
+            m.cur_scene[o], m.cur_group[o] = sc, gr
     hsel = np.nonzero(w["h_tick"] == tick)[0]
     for i in hsel:   # call order preserved
         o = int(w["h_obj"][i])

@@ -18,7 +18,8 @@ import numpy as np
 
 # ---- schema ---------------------------------------------------------------
 INT_PROPS = ["HP", "MAXHP", "HPREGEN", "MP", "MAXMP", "MPREGEN", "SP", "MAXSP",
-             "SPREGEN", "EXP", "Gold", "Level", "ATK_VALUE", "DEF_VALUE", "Camp", "NPCType"]
+             "SPREGEN", "EXP", "Gold", "Level", "ATK_VALUE", "DEF_VALUE", "Camp", "NPCType",
+             "SceneID", "GroupID"]
 FLT_PROPS = ["X", "Y", "Z", "TargetX", "TargetY", "AtkDis"]
 PROPS = INT_PROPS + FLT_PROPS
 PID = {n: i for i, n in enumerate(PROPS)}
@@ -58,6 +59,10 @@ def _prop_flags():
     f[CLS_NPC, PID["Camp"]] = PRIVATE             # NPC.xml: Camp Public=0 Private=1
     f[CLS_PLAYER, PID["Camp"]] = pubpriv          # Player.xml: Camp Public=1 Private=1
     f[CLS_PLAYER, PID["Gold"]] = PRIVATE | UPLOAD  # an Upload property never echoes to its owner
+    # IObject.xml: SceneID / GroupID Public=0 Private=1
+    for c in (CLS_NPC, CLS_PLAYER):
+        f[c, PID["SceneID"]] = PRIVATE
+        f[c, PID["GroupID"]] = PRIVATE
     # NPCType, TargetX, TargetY, AtkDis: Public=0 Private=0 (no sync)
     return f
 
@@ -97,7 +102,8 @@ def _names(lst):
 
 def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4, n_ticks=8,
                tick_ms=100, seed=1, ext_frac=0.05, host_ops=True, records=False, rec_rows=64,
-               t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, sched_edges=False):
+               t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, sched_edges=False,
+               switch_frac=0.0, switch_new_groups=False):
     rng = np.random.default_rng(seed)
     n_groups = n_scenes * groups_per_scene
     # ---- objects ----
@@ -135,6 +141,8 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
     init_i[PID["DEF_VALUE"]] = rng.integers(10, 500, n_obj)
     init_i[PID["Camp"]] = rng.integers(0, 4, n_obj)
     init_i[PID["NPCType"]] = rng.integers(0, 6, n_obj)
+    init_i[PID["SceneID"]] = scene   # CreateObject sets SceneID / GroupID (KM:248-249)
+    init_i[PID["GroupID"]] = group
     init_f = np.zeros((N_FLT, n_obj), np.float64)
 
     def coord(n):
@@ -260,6 +268,34 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
              h_kind=np.array(hk, np.int32), h_interval=np.array(hiv, np.float32),
              h_count=np.array(hc, np.int32), h_time=np.array(htm, np.int64))
 
+    # ---- SwitchScene calls between frames (KM:901): at most one per object per frame, made
+    #      before the frame's other calls; targets are other cells of any scene, sometimes the
+    #      object's own cell, and (switch_new_groups) groups that do not exist yet ----
+    st, so, ss, sg, sx, sy, sz = [], [], [], [], [], [], []
+    if switch_frac > 0:
+        for t in range(1, n_ticks):
+            k = max(1, int(switch_frac * n_obj))
+            objs = rng.choice(n_obj, size=min(k, n_obj), replace=False)
+            for o in objs:
+                r = rng.random()
+                if r < 0.1:
+                    tc, tg = None, None          # own cell: property writes only
+                elif switch_new_groups and r < 0.2:
+                    tc = int(rng.integers(0, n_groups))
+                    tg = groups_per_scene + 1 + int(rng.integers(0, 3))
+                else:
+                    tc, tg = int(rng.integers(0, n_groups)), None
+                st.append(t)
+                so.append(o)
+                ss.append(-1 if tc is None else tc // groups_per_scene + 1)
+                sg.append(-1 if tc is None else (tg if tg is not None else tc % groups_per_scene + 1))
+                sx.append(np.float32(rng.uniform(-500, 500)))
+                sy.append(np.float32(rng.uniform(-500, 500)))
+                sz.append(np.float32(rng.uniform(0, 50)))
+    sw = dict(sw_tick=np.array(st, np.int32), sw_obj=np.array(so, np.int32), sw_scene=np.array(ss, np.int32),
+              sw_group=np.array(sg, np.int32), sw_x=np.array(sx, np.float32), sw_y=np.array(sy, np.float32),
+              sw_z=np.array(sz, np.float32))
+
     n_rec = 1 if records else 0
     w = dict(
         cfg=np.array([n_obj, N_INT, N_FLT, 2, n_kind, n_rec, len(s_obj), n_ticks], np.int64),
@@ -268,7 +304,8 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
         guid_head=ghead, guid_data=gdata, scene=scene, group=group, cls=cls, is_player=isplayer,
         init_i=init_i, init_f=init_f,
         s_obj=s_obj, s_kind=s_kind, s_interval=s_int, s_count=s_cnt, s_time=s_time,
-        tick_time=tick_time, x_tick=x_tick, x_obj=x_obj, x_pid=x_pid, x_bits=x_bits, **h)
+        tick_time=tick_time, x_tick=x_tick, x_obj=x_obj, x_pid=x_pid, x_bits=x_bits, **h, **sw,
+        scene_props=np.array([PID["SceneID"], PID["GroupID"], PID["X"], PID["Y"], PID["Z"]], np.int32))
     if records:
         rows, cols = rec_rows, 3
         w["rec_rows"] = np.array([rows], np.int32)

@@ -17,6 +17,8 @@
  *                  fire test, count, reschedule, std::map remove-list insert quirk,
  *                  remove-then-add order, add dedup by name)
  *   add_schedule   NFComm/NFKernelPlugin/NFCScheduleModule.cpp:218-238
+ *   switch_scene   NFComm/NFKernelPlugin/NFCKernelModule.cpp:901-951 (group leave/join, the
+ *                  SceneID/GroupID/X/Y/Z writes in call order)
  *   fanout         NFComm/NFKernelPlugin/NFCSceneAOIModule.cpp:227-290 and 531-593
  *                  (GetBroadCastObject: public -> group players except self in NFGUID
  *                  order (NFCSceneGroupInfo::mxPlayerList, std::map), private&&!upload
@@ -295,6 +297,22 @@ static int32_t* sorted_objs;      /* objects in canonical order */
 static int64_t* seg_begin_of_obj; /* index in sorted_objs where the object's segment begins */
 static int64_t* seg_end_of_obj;
 
+/* canonical (scene, group, guid) order and each object's segment; rebuilt after SwitchScene */
+static void build_order(void) {
+    for (int32_t o = 0; o < N; o++) sorted_objs[o] = o;
+    qsort(sorted_objs, N, 4, cmp_obj_key);
+    for (int64_t i = 0; i < N; i++) orank[sorted_objs[i]] = i;
+    for (int64_t i = 0; i < N;) {
+        int64_t j = i;
+        while (j < N && scene[sorted_objs[j]] == scene[sorted_objs[i]] && group[sorted_objs[j]] == group[sorted_objs[i]]) j++;
+        for (int64_t k = i; k < j; k++) {
+            seg_begin_of_obj[sorted_objs[k]] = i;
+            seg_end_of_obj[sorted_objs[k]] = j;
+        }
+        i = j;
+    }
+}
+
 static void put_tick(nfio_writer* w, int t, const char* pfx, const char* nm, uint32_t code,
                      const void* d, uint64_t n, uint64_t es) {
     char name[32];
@@ -370,21 +388,32 @@ int main(int argc, char** argv) {
 
     /* canonical rank */
     sorted_objs = (int32_t*)malloc(N * 4);
-    for (int32_t o = 0; o < N; o++) sorted_objs[o] = o;
-    qsort(sorted_objs, N, 4, cmp_obj_key);
     orank = (int64_t*)malloc(N * 8);
     seg_begin_of_obj = (int64_t*)malloc(N * 8);
     seg_end_of_obj = (int64_t*)malloc(N * 8);
-    for (int64_t i = 0; i < N; i++) orank[sorted_objs[i]] = i;
-    for (int64_t i = 0; i < N;) {
-        int64_t j = i;
-        while (j < N && scene[sorted_objs[j]] == scene[sorted_objs[i]] && group[sorted_objs[j]] == group[sorted_objs[i]]) j++;
-        for (int64_t k = i; k < j; k++) {
-            seg_begin_of_obj[sorted_objs[k]] = i;
-            seg_end_of_obj[sorted_objs[k]] = j;
-        }
-        i = j;
+    build_order();
+
+    /* SwitchScene calls (optional in a workload) and the property ids they write */
+    int32_t pid_scene = -1, pid_group = -1, pid_x = -1, pid_y = -1, pid_z = -1;
+    nfio_arr* spa = nfio_get(&wf, "scene_props");
+    if (spa) {
+        int32_t* sp = (int32_t*)spa->data;
+        pid_scene = sp[0]; pid_group = sp[1]; pid_x = sp[2]; pid_y = sp[3]; pid_z = sp[4];
     }
+    nfio_arr* swa = nfio_get(&wf, "sw_tick");
+    int64_t NSW = swa ? (int64_t)swa->shape[0] : 0;
+    int32_t *sw_tick = NULL, *sw_obj = NULL, *sw_scene = NULL, *sw_group = NULL;
+    float *sw_x = NULL, *sw_y = NULL, *sw_z = NULL;
+    if (NSW) {
+        sw_tick = (int32_t*)swa->data;
+        sw_obj = (int32_t*)GET("sw_obj")->data;
+        sw_scene = (int32_t*)GET("sw_scene")->data;
+        sw_group = (int32_t*)GET("sw_group")->data;
+        sw_x = (float*)GET("sw_x")->data;
+        sw_y = (float*)GET("sw_y")->data;
+        sw_z = (float*)GET("sw_z")->data;
+    }
+    int64_t swi = 0;
 
     /* pending schedule adds: the initial AddSchedule calls happen before tick 0 */
     typedef struct { int32_t obj, kind, count; float interval; int64_t time; } addreq_t;
@@ -405,6 +434,30 @@ int main(int argc, char** argv) {
         nrlog = 0;
         nfired = 0;
         seq = 0;
+        /* NFCKernelModule::SwitchScene (KM:901-951), made first in the window: leave the group,
+         * [GroupID = 0, SceneID = target when the scene changes], X/Y/Z = (double)float,
+         * GroupID = target, join the target group.  sw_scene < 0: the object's own cell. */
+        int relayout = 0;
+        while (swi < NSW && sw_tick[swi] == t) {
+            int32_t o = sw_obj[swi];
+            int32_t ns = sw_scene[swi] < 0 ? scene[o] : sw_scene[swi];
+            int32_t ng = sw_scene[swi] < 0 ? group[o] : sw_group[swi];
+            if (ns != scene[o]) {
+                if (pid_group >= 0) set_int(o, pid_group, 0);
+                if (pid_scene >= 0) set_int(o, pid_scene, ns);
+            }
+            if (pid_x >= 0) set_flt(o, pid_x, (double)sw_x[swi]);
+            if (pid_y >= 0) set_flt(o, pid_y, (double)sw_y[swi]);
+            if (pid_z >= 0) set_flt(o, pid_z, (double)sw_z[swi]);
+            if (pid_group >= 0) set_int(o, pid_group, ng);
+            if (ns != scene[o] || ng != group[o]) {
+                scene[o] = ns;
+                group[o] = ng;
+                relayout = 1;
+            }
+            swi++;
+        }
+        if (relayout) build_order();
         /* host calls made between the previous Execute and this one */
         while (hi < NH && h_tick[hi] == t) {
             int32_t o = h_obj[hi];

@@ -14,6 +14,8 @@
 //   GetBroadCastObject / OnPropertyCommonEvent recipient lists
 //                                          NFCSceneAOIModule.cpp:227-258, 531-593,
 //                                          NFCKernelModule.cpp:1270-1294
+//   SwitchScene                            NFCKernelModule.cpp:901-951 (over the reference's
+//                                          NFCSceneInfo group maps and property manager)
 // NFCScheduleModule reads wall time through NFGetTime() (NFPlatform.h:367,
 // std::chrono::system_clock); this harness supplies a virtual CLOCK_REALTIME
 // by defining clock_gettime, so the real scheduler runs deterministically.
@@ -96,18 +98,23 @@ struct World {
 };
 static World W;
 
-// --- GetBroadCastObject (NFCSceneAOIModule.cpp:531-593) for an (object, flags) pair ---
+// --- GetBroadCastObject (NFCSceneAOIModule.cpp:531-593) for an (object, flags) pair: public ->
+// GetGroupObjectList(scene, group, "Player", self) (NFCKernelModule.cpp:1270-1294): the group's
+// player map then its other map, objects of class Player except self ---
 static void broadcast_list(int32_t o, uint8_t fl, NFIDataList& out) {
     if (fl & NFK_PUBLIC) {
         auto si = W.scenes[W.scene[o]];
         auto gi = si->GetElement(W.group[o]);
         if (!gi) return;
-        NFGUID ident;
-        gi->mxPlayerList.First(ident);
-        while (!ident.IsNull()) {
-            if (ident != W.id[o]) out.Add(ident);
-            ident = NFGUID();
-            gi->mxPlayerList.Next(ident);
+        for (int which = 0; which < 2; which++) {
+            auto& lst = which == 0 ? gi->mxPlayerList : gi->mxOtherList;
+            NFGUID ident;
+            lst.First(ident);
+            while (!ident.IsNull()) {
+                if (ident != W.id[o] && W.isplayer[W.obj_of[ident]]) out.Add(ident);
+                ident = NFGUID();
+                lst.Next(ident);
+            }
         }
     } else if ((fl & NFK_PRIVATE) && !(fl & NFK_UPLOAD)) {
         out.Add(W.id[o]);
@@ -422,16 +429,40 @@ int main(int argc, char** argv) {
     int32_t* h_count = (int32_t*)GET(wf, "h_count")->data;
     int64_t* h_time = (int64_t*)GET(wf, "h_time")->data;
 
-    // canonical rank (scene, group, guid)
+    // canonical rank (scene, group, guid); recomputed after SwitchScene
     std::vector<int32_t> sorted(W.N);
-    for (int64_t i = 0; i < W.N; i++) sorted[i] = (int32_t)i;
-    std::sort(sorted.begin(), sorted.end(), [](int32_t a, int32_t b) {
-        if (W.scene[a] != W.scene[b]) return W.scene[a] < W.scene[b];
-        if (W.group[a] != W.group[b]) return W.group[a] < W.group[b];
-        return W.id[a] < W.id[b];
-    });
     std::vector<int64_t> orank(W.N);
-    for (int64_t i = 0; i < W.N; i++) orank[sorted[i]] = i;
+    auto build_order = [&]() {
+        for (int64_t i = 0; i < W.N; i++) sorted[i] = (int32_t)i;
+        std::sort(sorted.begin(), sorted.end(), [](int32_t a, int32_t b) {
+            if (W.scene[a] != W.scene[b]) return W.scene[a] < W.scene[b];
+            if (W.group[a] != W.group[b]) return W.group[a] < W.group[b];
+            return W.id[a] < W.id[b];
+        });
+        for (int64_t i = 0; i < W.N; i++) orank[sorted[i]] = i;
+    };
+    build_order();
+
+    // SwitchScene calls (optional) and the property ids they write
+    int32_t pid_scene = -1, pid_group = -1, pid_x = -1, pid_y = -1, pid_z = -1;
+    if (nfio_arr* spa = nfio_get(&wf, "scene_props")) {
+        int32_t* sp = (int32_t*)spa->data;
+        pid_scene = sp[0]; pid_group = sp[1]; pid_x = sp[2]; pid_y = sp[3]; pid_z = sp[4];
+    }
+    nfio_arr* swa = nfio_get(&wf, "sw_tick");
+    const int64_t NSW = swa ? (int64_t)swa->shape[0] : 0;
+    int32_t *sw_tick = nullptr, *sw_obj = nullptr, *sw_scene = nullptr, *sw_group = nullptr;
+    float *sw_x = nullptr, *sw_y = nullptr, *sw_z = nullptr;
+    if (NSW) {
+        sw_tick = (int32_t*)swa->data;
+        sw_obj = (int32_t*)GET(wf, "sw_obj")->data;
+        sw_scene = (int32_t*)GET(wf, "sw_scene")->data;
+        sw_group = (int32_t*)GET(wf, "sw_group")->data;
+        sw_x = (float*)GET(wf, "sw_x")->data;
+        sw_y = (float*)GET(wf, "sw_y")->data;
+        sw_z = (float*)GET(wf, "sw_z")->data;
+    }
+    int64_t swi = 0;
 
     nfio_writer w;
     if (!bench && nfio_wopen(&w, argv[2]) != 0) { fprintf(stderr, "cannot open output\n"); return 2; }
@@ -443,6 +474,34 @@ int main(int argc, char** argv) {
         W.rlog.clear();
         W.fired.clear();
         W.seq = 0;
+        // NFCKernelModule::SwitchScene (KM:901-951), restated over the reference's NFCSceneInfo
+        // group maps and property manager; made first in the window.  The target group is
+        // created on demand (NFCKernelModule::RequestGroupScene).
+        bool relayout = false;
+        while (swi < NSW && sw_tick[swi] == t) {
+            const int32_t o = sw_obj[swi];
+            const NFGUID self = W.id[o];
+            const int ns = sw_scene[swi] < 0 ? W.scene[o] : sw_scene[swi];
+            const int ng = sw_scene[swi] < 0 ? W.group[o] : sw_group[swi];
+            auto& nsi = W.scenes[ns];
+            if (!nsi) nsi = NF_SHARE_PTR<NFCSceneInfo>(new NFCSceneInfo(ns));
+            if (!nsi->GetElement(ng)) nsi->AddElement(ng, NF_SHARE_PTR<NFCSceneGroupInfo>(new NFCSceneGroupInfo(ns, ng)));
+            W.scenes[W.scene[o]]->RemoveObjectFromGroup(W.group[o], self, true);
+            if (ns != W.scene[o]) {
+                if (pid_group >= 0) SetInt(self, pid_group, 0);
+                if (pid_scene >= 0) SetInt(self, pid_scene, ns);
+            }
+            if (pid_x >= 0) SetFloat(self, pid_x, (double)sw_x[swi]);
+            if (pid_y >= 0) SetFloat(self, pid_y, (double)sw_y[swi]);
+            if (pid_z >= 0) SetFloat(self, pid_z, (double)sw_z[swi]);
+            if (pid_group >= 0) SetInt(self, pid_group, ng);
+            nsi->AddObjectToGroup(ng, self, true);
+            relayout |= ns != W.scene[o] || ng != W.group[o];
+            W.scene[o] = ns;
+            W.group[o] = ng;
+            swi++;
+        }
+        if (relayout) build_order();
         while (hi < NH && h_tick[hi] == t) {
             NFGUID self = W.id[h_obj[hi]];
             if (h_op[hi] == 1) {

@@ -2,7 +2,7 @@
 classes (oracle/_ref/nf_ref_harness, built from /root/reference by oracle/build_ref.sh).
 Each fixture = <name>.workload.nfio (inputs) + <name>.expected.nfio (reference outputs).
 
-    python tests/golden/gen_golden.py
+    python tests/golden/gen_golden.py [name ...]
 """
 import os
 import subprocess
@@ -23,12 +23,17 @@ FIXTURES = {
     # one group, every object a player, no between-frame calls
     "allplayers": dict(n_obj=64, n_scenes=1, groups_per_scene=1, players_per_group=64, n_ticks=12, seed=303,
                        ext_frac=0.0, host_ops=False),
+    # SwitchScene between frames (KM:901-951): group/scene changes, own-cell switches, new groups
+    "switch": dict(n_obj=400, n_scenes=3, groups_per_scene=4, players_per_group=3, n_ticks=8, seed=404,
+                   ext_frac=0.05, switch_frac=0.05, switch_new_groups=True),
 }
 
 
-def main():
+def main(names=None):
     exe = os.path.join(ROOT, "oracle", "_ref", "nf_ref_harness")
     for name, kw in FIXTURES.items():
+        if names and name not in names:
+            continue
         w = workload.make_world(**kw)
         wp = os.path.join(HERE, f"{name}.workload.nfio")
         ep = os.path.join(HERE, f"{name}.expected.nfio")
@@ -38,4 +43,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

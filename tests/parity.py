@@ -35,11 +35,11 @@ def run_ref(w):
     return _run_cli(REF, w)
 
 
-def run_gpu(w, msg_capacity=0):
+def run_gpu(w, msg_capacity=0, slack_per_256=0):
     """Replay the workload through libnfgpu.so; returns arrays named like the oracle's."""
     from noahgameframe_amd import kernel
 
-    m = kernel.world_from_workload(w, msg_capacity=msg_capacity)
+    m = kernel.world_from_workload(w, msg_capacity=msg_capacity, slack_per_256=slack_per_256)
     out = {}
     n_ticks = int(w["cfg"][7])
     for t in range(n_ticks):

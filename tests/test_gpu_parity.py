@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
-@pytest.mark.parametrize("name", ["props", "records", "allplayers"])
+@pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch"])
 def test_gpu_matches_reference_golden(gpu_available, name):
     w = nfio.read(os.path.join(GOLDEN, f"{name}.workload.nfio"))
     expected = nfio.read(os.path.join(GOLDEN, f"{name}.expected.nfio"))
@@ -29,6 +29,8 @@ CASES = {
     "one_object": dict(n_obj=1, n_scenes=1, groups_per_scene=1, players_per_group=1, ext_frac=1.0),
     "no_players": dict(n_obj=1000, n_scenes=1, groups_per_scene=2, players_per_group=0),
     "big_group": dict(n_obj=3000, n_scenes=1, groups_per_scene=1, players_per_group=300, host_ops=True),
+    "switch_scene": dict(n_obj=6000, n_scenes=3, groups_per_scene=6, players_per_group=4, switch_frac=0.02,
+                         switch_new_groups=True, ext_frac=0.05),
     "sched_edges": dict(n_obj=6000, n_scenes=2, groups_per_scene=9, players_per_group=3, sched_edges=True),
     "ragged_4097": dict(n_obj=4097, n_scenes=5, groups_per_scene=13, players_per_group=1, ext_frac=0.3),
 }
@@ -38,6 +40,15 @@ CASES = {
 def test_gpu_matches_oracle(gpu_available, case):
     w = workload.make_world(n_ticks=10, seed=sum(map(ord, case)), **CASES[case])
     compare_runs(run_gpu(w), run_oracle(w))
+
+
+@pytest.mark.parametrize("slack", [-1, 1, 64])
+def test_switch_scene_layouts(gpu_available, slack):
+    """SwitchScene with no slack (every change rebuilds the layout), tiny slack (segments overflow
+    and rebuild) and ample slack (only the changed scene groups are rewritten)."""
+    w = workload.make_world(n_obj=3000, n_scenes=2, groups_per_scene=5, players_per_group=3, n_ticks=8,
+                            seed=31 + slack, switch_frac=0.03, switch_new_groups=True, records=True, rec_rows=8)
+    compare_runs(run_gpu(w, slack_per_256=slack), run_oracle(w))
 
 
 def test_gpu_full_size_config1(gpu_available):
@@ -61,7 +72,8 @@ def _module(n=300):
 def test_touch_limit_fails_loudly(gpu_available):
     m, w = _module()
     g = (int(w["guid_head"][0]), int(w["guid_data"][0]))
-    for p in ("Level", "ATK_VALUE", "DEF_VALUE"):
+    # programs write 6 properties; 7 more distinct ones for one entity exceed NFK_MAX_TOUCH = 12
+    for p in ("Level", "ATK_VALUE", "DEF_VALUE", "SP", "MAXSP", "SPREGEN", "Camp"):
         m.SetPropertyInt(g, p, 12345)
     with pytest.raises(kernel.NFKError) as e:
         m.Execute(int(w["tick_time"][0]))
@@ -94,7 +106,9 @@ def test_device_outputs_and_counters(gpu_available):
     assert s["alg_bytes_tick"] > 0 and s["alg_bytes_fan"] > 0
     o = m.outputs()
     assert all(o[k] for k in ("ev_slot", "ev_moff", "ev_base", "msg_base", "msg_rcpt", "slot_obj"))
-    assert o["n_tiles"] == (5000 + 255) // 256 and o["tile_slots"] == 256 and o["ev_tile_cap"] == 256 * 8
+    # slots = members + per-group slack (nfk_config.slack_per_256, default 16 per 256)
+    assert s["n_entities"] == 5000 and 5000 <= o["n_tiles"] * 256 <= 5000 * 1.1 + 256 * 2
+    assert o["tile_slots"] == 256 and o["ev_tile_cap"] == 256 * 12
     assert np.all(np.diff(r["mo_off"].astype(np.int64)) >= 0)
     m.close()
 

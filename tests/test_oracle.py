@@ -43,6 +43,8 @@ def test_golden_fixtures_are_nontrivial():
              rec_float_op=False)),
     (4, dict(n_obj=1, n_scenes=1, groups_per_scene=1, players_per_group=1, ext_frac=1.0)),
     (5, dict(n_obj=700, n_scenes=2, groups_per_scene=5, players_per_group=3, sched_edges=True)),
+    (6, dict(n_obj=800, n_scenes=3, groups_per_scene=4, players_per_group=3, switch_frac=0.05,
+             switch_new_groups=True)),
 ])
 def test_oracle_matches_reference(seed, kw):
     w = workload.make_world(n_ticks=9, seed=seed, **kw)
