@@ -215,6 +215,8 @@ int nfk_remove_all_schedules(void* world, int64_t guid_head, int64_t guid_data);
  * + NFCSceneAOIModule::OnPropertyCommonEvent/GetBroadCastObject fan-out (AOI:227,260,531).
  * Asynchronous on the world's stream. */
 int nfk_execute(void* world, int64_t now_ms);
+/* wait for everything queued on the world's stream */
+int nfk_sync(void* world);
 /* synchronise and read the counters of the last tick */
 int nfk_summary_get(void* world, nfk_summary* out);
 int nfk_outputs_get(void* world, nfk_outputs* out);

@@ -1411,6 +1411,13 @@ int nfk_execute(void* world, int64_t now_ms) {
     return NFK_OK;
 }
 
+int nfk_sync(void* world) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    HIPCHK(hipStreamSynchronize(w->stream));
+    return NFK_OK;
+}
+
 int nfk_summary_get(void* world, nfk_summary* out) {
     World* w = (World*)world;
     if (!w || !out) return fail(NFK_ERR_ARG, "null argument");

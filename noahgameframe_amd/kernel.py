@@ -88,7 +88,7 @@ def load_library(path=LIB_PATH):
         "nfk_destroy_objects": [VP, I32, VP, VP], "nfk_object_count": [VP, VP], "nfk_row_words": [VP, VP],
         "nfk_export_objects": [VP, I32, VP, VP, VP],
         "nfk_import_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
-        "nfk_spawn_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
+        "nfk_spawn_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP], "nfk_sync": [VP],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -112,6 +112,7 @@ class NFKernelModule:
         h = ctypes.c_void_p()
         self._chk(self.lib.nfk_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
+        self.stream = stream
         self.n_int, self.n_flt, self.n_kind, self.n_rec = n_int, n_flt, n_kind, n_rec
         self.n_obj = 0
         self.rec_shape = {}
@@ -259,6 +260,9 @@ class NFKernelModule:
     def Execute(self, now_ms):
         self._chk(self.lib.nfk_execute(self.h, int(now_ms)))
         return True
+
+    def synchronize(self):
+        self._chk(self.lib.nfk_sync(self.h))
 
     def summary(self):
         s = Summary()

@@ -1,0 +1,260 @@
+"""Scene shards across GPUs.
+
+One process per GPU owns a range of scenes and runs its own world (libnfgpu.so) on its own
+device; frames need no collective because a scene group never spans two shards.  The only
+exchange on the path is a SwitchScene (NFCKernelModule::SwitchScene, KM:901-951) whose target
+scene belongs to another shard: the entity's state row leaves the source world
+(`nfk_export_objects`), travels GPU-to-GPU with one `all_to_all_single` per frame over the
+process group (RCCL over xGMI with the "nccl" backend), and enters the owner's world
+(`nfk_import_objects`), after which the owner queues the SwitchScene property writes
+(GroupID = 0, SceneID, X, Y, Z, GroupID; KM:930-942).  The events of that frame therefore come
+from the entity's new scene group, exactly as on a single world.
+
+Tickets (which entity goes where) are control-plane metadata: they are exchanged with
+`all_gather_object` over a CPU (gloo) group, or, when every rank already knows the frame's
+global migration plan, derived locally (`migrate(..., plan=...)`) so the frame has no host
+round trip at all.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class Ticket:
+    """One cross-shard SwitchScene: the entity, its class, the target cell and position."""
+    guid_head: int
+    guid_data: int
+    cls: int
+    is_player: int
+    scene: int
+    group: int
+    x: float
+    y: float
+    z: float
+    src: int = -1   # source rank
+    dst: int = -1   # destination rank
+
+
+def scene_ranges(scenes, world_size):
+    """Contiguous scene ranges, one per rank: returns owner(scene) -> rank."""
+    scenes = sorted(set(int(s) for s in scenes))
+    per = -(-len(scenes) // world_size)
+    table = {s: min(i // per, world_size - 1) for i, s in enumerate(scenes)}
+
+    def owner(scene):
+        scene = int(scene)
+        if scene in table:
+            return table[scene]
+        # a scene created later: by position among the known ones
+        return table[max([s for s in scenes if s <= scene], default=scenes[0])]
+    return owner
+
+
+class SceneShard:
+    """This rank's scene range.  `m` is the rank's NFKernelModule (kernel.py)."""
+
+    def __init__(self, m, rank, world_size, owner, scene_props, group=None, meta_group=None, device=None):
+        import torch
+        self.torch = torch
+        self.m, self.rank, self.ws, self.owner = m, rank, world_size, owner
+        self.pid_scene, self.pid_group, self.pid_x, self.pid_y, self.pid_z = (int(p) for p in scene_props)
+        self.pg, self.meta_pg = group, meta_group
+        self.device = device if device is not None else torch.device("cpu")
+        self.rw = m.row_words()
+        self.migrated_out = 0
+        self.migrated_in = 0
+
+    # ---- the SwitchScene call as game logic makes it ----
+    def switch_scene(self, guid, cls, is_player, scene, group, x, y, z, out):
+        """Local target: SwitchScene on this world.  Remote target: a ticket appended to `out`
+        for the next `migrate` (the entity leaves at the start of the frame)."""
+        dst = self.owner(scene)
+        if dst == self.rank:
+            self.m.SwitchScene(guid, scene, group, x, y, z)
+            return None
+        t = Ticket(int(guid[0]), int(guid[1]), int(cls), int(is_player), int(scene), int(group), float(x), float(y),
+                   float(z), self.rank, dst)
+        out.append(t)
+        return t
+
+    def _exchange_tickets(self, out):
+        import torch.distributed as dist
+        allt = [None] * self.ws
+        dist.all_gather_object(allt, out, group=self.meta_pg)
+        return [t for lst in allt for t in lst]
+
+    def migrate(self, out, plan=None):
+        """Collective (every rank calls it once per frame, possibly with nothing to send).
+        `out`: this rank's outgoing tickets.  `plan`: optionally the frame's global ticket list in
+        (source rank, call) order, known to every rank; otherwise tickets are all-gathered over
+        the meta group.  Returns the tickets this rank received."""
+        torch = self.torch
+        tickets = plan if plan is not None else self._exchange_tickets(out)
+        send = [t for t in tickets if t.src == self.rank]
+        recv = [t for t in tickets if t.dst == self.rank]
+        send.sort(key=lambda t: t.dst)   # stable: call order within a destination
+        recv.sort(key=lambda t: t.src)
+        scount = [0] * self.ws
+        rcount = [0] * self.ws
+        for t in send:
+            scount[t.dst] += 1
+        for t in recv:
+            rcount[t.src] += 1
+        if not tickets:   # the same decision on every rank: the collective below is skipped by all
+            return []
+        rw = self.rw
+        sbuf = torch.empty((len(send), rw), dtype=torch.int64, device=self.device)
+        if send:
+            self.m.export_objects([t.guid_head for t in send], [t.guid_data for t in send], sbuf.data_ptr())
+        if self.device.type == "cuda" and self.m.stream != torch.cuda.current_stream(self.device).cuda_stream:
+            self.m.synchronize()   # the rows were packed on the world's own stream
+        rbuf = torch.empty((len(recv), rw), dtype=torch.int64, device=self.device)
+        self._all_to_all(rbuf, sbuf, [c * rw for c in rcount], [c * rw for c in scount])
+        if recv:
+            self.m.import_objects([t.guid_head for t in recv], [t.guid_data for t in recv],
+                                  [t.scene for t in recv], [t.group for t in recv], [t.cls for t in recv],
+                                  [t.is_player for t in recv], rbuf.data_ptr())
+            # the SwitchScene property writes (KM:930-942); the scene always changes here
+            gh, gd, pid, bits = [], [], [], []
+            for t in recv:
+                for p, b in ((self.pid_group, 0), (self.pid_scene, t.scene),
+                             (self.pid_x, _f64(t.x)), (self.pid_y, _f64(t.y)), (self.pid_z, _f64(t.z)),
+                             (self.pid_group, t.group)):
+                    if p >= 0:
+                        gh.append(t.guid_head)
+                        gd.append(t.guid_data)
+                        pid.append(p)
+                        bits.append(np.int64(b).view(np.uint64) if not isinstance(b, np.uint64) else b)
+            self.m.set_props(gh, gd, pid, np.array(bits, np.uint64))
+        self.migrated_out += len(send)
+        self.migrated_in += len(recv)
+        return recv
+
+    def _all_to_all(self, rbuf, sbuf, rsplit, ssplit):
+        torch = self.torch
+        import torch.distributed as dist
+        if self.ws == 1:
+            return
+        if self.device.type == "cuda" and dist.get_backend(self.pg) == "gloo":
+            # gloo moves host tensors: stage the rows through host memory
+            torch.cuda.current_stream(self.device).synchronize()
+            hs, hr = sbuf.cpu(), torch.empty(rbuf.shape, dtype=rbuf.dtype)
+            dist.all_to_all_single(hr.view(-1), hs.view(-1), rsplit, ssplit, group=self.pg)
+            rbuf.copy_(hr)
+        else:
+            dist.all_to_all_single(rbuf.view(-1), sbuf.view(-1), rsplit, ssplit, group=self.pg)
+
+
+def _f64(x):
+    return np.float64(np.float32(x)).view(np.uint64)
+
+
+
+def subset_world(w, objs):
+    """The workload restricted to the objects `objs` (global indices, ascending): objects,
+    creation-time values, records and the AddSchedule calls made before frame 0.  Between-frame
+    calls stay global; ShardedReplay routes them to the rank that owns the object."""
+    idx = np.asarray(objs, np.int64)
+    local = np.full(len(w["guid_head"]), -1, np.int64)
+    local[idx] = np.arange(len(idx))
+    sub = dict(w)
+    sub["cfg"] = w["cfg"].copy()
+    sub["cfg"][0] = len(idx)
+    for k in ("guid_head", "guid_data", "scene", "group", "cls", "is_player"):
+        sub[k] = w[k][idx]
+    sub["init_i"] = w["init_i"][:, idx]
+    sub["init_f"] = w["init_f"][:, idx]
+    for r in range(int(w["cfg"][5])):
+        sub[f"rec{r}_cells"] = w[f"rec{r}_cells"][idx]
+        sub[f"rec{r}_used"] = w[f"rec{r}_used"][idx]
+    sel = local[w["s_obj"]] >= 0
+    sub["s_obj"] = local[w["s_obj"][sel]].astype(np.int32)
+    for k in ("s_kind", "s_interval", "s_count", "s_time"):
+        sub[k] = w[k][sel]
+    sub["cfg"][6] = int(sel.sum())
+    return sub
+
+
+class ShardedReplay:
+    """Replays a global workload (workload.make_world) on this rank's scene range: SwitchScene
+    calls to foreign scenes migrate, the other between-frame calls go to the rank that owns the
+    object at that moment, and every frame's outputs are reported with global object indices
+    so they can be compared with a single-world run."""
+
+    def __init__(self, w, rank, world_size, group=None, meta_group=None, device=None, stream=None, slack_per_256=0):
+        from . import kernel
+        self.w, self.rank, self.ws = w, rank, world_size
+        self.owner = scene_ranges(np.unique(w["scene"]), world_size)
+        n = len(w["guid_head"])
+        mine = [o for o in range(n) if self.owner(w["scene"][o]) == rank]
+        self.m = kernel.world_from_workload(subset_world(w, mine), capacity=max(64, 2 * n // world_size),
+                                            stream=stream, slack_per_256=slack_per_256)
+        self.shard = SceneShard(self.m, rank, world_size, self.owner, w["scene_props"], group, meta_group, device)
+        self.glob = list(mine)                       # local object index -> global
+        self.local_of = {g: i for i, g in enumerate(mine)}
+        self.gidx = {(int(w["guid_head"][o]), int(w["guid_data"][o])): o for o in range(n)}
+        self.cur_scene = np.array(w["scene"], np.int32)
+        self.cur_group = np.array(w["group"], np.int32)
+
+    def _guid(self, o):
+        return int(self.w["guid_head"][o]), int(self.w["guid_data"][o])
+
+    def frame(self, t, collect=True):
+        w = self.w
+        out = []
+        if "sw_tick" in w:
+            for i in np.nonzero(w["sw_tick"] == t)[0]:
+                o = int(w["sw_obj"][i])
+                if o not in self.local_of:
+                    continue
+                sc, gr = int(w["sw_scene"][i]), int(w["sw_group"][i])
+                if sc < 0:
+                    sc, gr = int(self.cur_scene[o]), int(self.cur_group[o])
+                self.shard.switch_scene(self._guid(o), w["cls"][o], w["is_player"][o], sc, gr, w["sw_x"][i],
+                                        w["sw_y"][i], w["sw_z"][i], out)
+                self.cur_scene[o], self.cur_group[o] = sc, gr
+        recv = self.shard.migrate(out)
+        for tk in out:
+            del self.local_of[self.gidx[(tk.guid_head, tk.guid_data)]]
+        for tk in recv:
+            o = self.gidx[(tk.guid_head, tk.guid_data)]
+            self.local_of[o] = len(self.glob)
+            self.glob.append(o)
+            self.cur_scene[o], self.cur_group[o] = tk.scene, tk.group
+        gh, gd = w["guid_head"], w["guid_data"]
+        for i in np.nonzero(w["h_tick"] == t)[0]:
+            o = int(w["h_obj"][i])
+            if o not in self.local_of:
+                continue
+            g = self._guid(o)
+            op = int(w["h_op"][i])
+            if op == 1:
+                self.m.add_schedules([g[0]], [g[1]], [w["h_kind"][i]], [w["h_interval"][i]], [w["h_count"][i]],
+                                     [w["h_time"][i]])
+            elif op == 2:
+                self.m.RemoveSchedule(g, int(w["h_kind"][i]))
+            else:
+                self.m.RemoveSchedule(g)
+        xs = [i for i in np.nonzero(w["x_tick"] == t)[0] if int(w["x_obj"][i]) in self.local_of]
+        if xs:
+            xo = w["x_obj"][xs]
+            self.m.set_props(gh[xo], gd[xo], w["x_pid"][xs], w["x_bits"][xs])
+        self.m.Execute(int(w["tick_time"][t]))
+        if not collect:
+            return None
+        r = self.m.read_tick()
+        g = np.asarray(self.glob, np.int64)
+        for k in ("ev_obj", "re_obj", "fi_obj", "mr_obj"):
+            r[k] = g[r[k]].astype(np.int32) if len(r[k]) else r[k]
+        return r
+
+    def final_state(self):
+        """Final properties / records / schedules of the objects this rank owns: {global: ...}."""
+        n_int = int(self.w["cfg"][1])
+        n_flt = int(self.w["cfg"][2])
+        props = np.stack([self.m.read_prop(p).view(np.uint64) for p in range(n_int + n_flt)])
+        nx, rm, st = self.m.read_schedules()
+        recs = [self.m.read_record(r) for r in range(int(self.w["cfg"][5]))]
+        own = sorted(self.local_of.items())
+        return {o: (props[:, li], nx[:, li], rm[:, li], st[:, li] & 1, [x[li] for x in recs]) for o, li in own}

@@ -1,0 +1,40 @@
+"""One rank of a sharded replay (test infrastructure; launched by tests/test_shard.py with
+torch.distributed.run).  usage: shard_worker.py <workload.nfio> <out_dir> [gpu|stub]"""
+import os
+import pickle
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+    from noahgameframe_amd import nfio
+    from noahgameframe_amd.shard import ShardedReplay
+
+    wp, out = sys.argv[1], sys.argv[2]
+    dist.init_process_group("gloo")
+    rank, ws = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    w = nfio.read(wp)
+    rep = ShardedReplay(w, rank, ws, group=dist.group.WORLD, meta_group=dist.group.WORLD,
+                        device=torch.device("cuda", 0), slack_per_256=int(os.environ.get("NFK_SLACK", "0")))
+    frames = []
+    for t in range(int(w["cfg"][7])):
+        r = rep.frame(t)
+        frames.append({k: r[k] for k in ("ev_obj", "ev_pid", "ev_old", "ev_new", "re_obj", "re_rrc", "re_old",
+                                         "re_new", "fi_obj", "fi_kind", "fi_rem", "mo_off", "mr_obj")})
+    res = {"frames": frames, "final": rep.final_state(), "out": rep.shard.migrated_out, "in": rep.shard.migrated_in}
+    with open(os.path.join(out, f"rank{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)
+    rep.m.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
