@@ -39,9 +39,15 @@ def parse():
     p.add_argument("--players-per-group", type=int, default=8)
     p.add_argument("--tick-ms", type=int, default=100)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    p.add_argument("--cpu-sample", type=int, default=65536, help="entities in the CPU baseline sample")
+    p.add_argument("--cpu-sample", type=int, default=32768, help="entities in the CPU baseline sample")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--migrate", type=int, default=256,
+                   help="N>1: entities per rank per frame that SwitchScene into the next rank's scene "
+                        "(state rows over RCCL all_to_all; BASELINE config[2])")
+    p.add_argument("--slack", type=int, default=None, help="free slots per 256 scene-group members")
+    p.add_argument("--backend", default="nccl", help="process group backend (nccl = RCCL; gloo only to rehearse "
+                                                     "several ranks on one GPU)")
     return p.parse_args()
 
 
@@ -60,17 +66,58 @@ def cpu_baseline(args, w_full):
         wp = os.path.join(d, "w.nfio")
         nfio.write(wp, w)
         # calibrate: a short run, then a run sized to ~cpu_seconds of frame work
-        r = json.loads(subprocess.run([exe, "--bench", wp, "20"], check=True, capture_output=True,
+        r = json.loads(subprocess.run([exe, "--bench", wp, "4"], check=True, capture_output=True,
                                       text=True).stdout)
         per_tick = r["seconds"] / max(r["ticks"], 1)
-        t = int(min(ticks, max(20, args.cpu_seconds / max(per_tick, 1e-6))))
+        t = int(min(ticks, max(4, args.cpu_seconds / max(per_tick, 1e-6))))
         r = json.loads(subprocess.run([exe, "--bench", wp, str(t)], check=True, capture_output=True,
                                       text=True).stdout)
     return {"value": r["entity_ticks_per_s"], "unit": "entity-ticks/s", "cores": 1, "kind": "reference",
             "sample": f"{n} entities ({groups} groups x {n // groups}, {args.players_per_group} players/group), "
                       f"{r['ticks']} frames of the same heartbeat workload through the reference's "
                       f"NFCPropertyManager/NFCProperty + NFCScheduleModule + per-Set GetBroadCastObject "
-                      f"lists, single thread, {r['seconds']:.1f} s"}
+                      f"lists (GetGroupObjectList over the group's player and other maps, KM:1270), "
+                      f"single thread, {r['seconds']:.1f} s"}
+
+
+class Migration:
+    """BASELINE config[2]: every frame each rank's game logic sends `per_frame` of its entities
+    into the next rank's scene (SwitchScene across shards, same group id, new position).  The
+    frame's tickets are decided and all-gathered over a gloo group while the previous frame runs on
+    the GPU; at the frame start the state rows travel GPU-to-GPU with one RCCL all_to_all."""
+
+    def __init__(self, m, w, rank, world, per_frame, dev):
+        import numpy as np
+        import torch.distributed as dist
+        from collections import deque
+        from noahgameframe_amd.shard import SceneShard
+        self.np, self.dist = np, dist
+        self.meta = dist.new_group(backend="gloo")
+        own = lambda scene: int(scene) - 1
+        self.shard = SceneShard(m, rank, world, own, w["scene_props"], group=dist.group.WORLD,
+                                meta_group=self.meta, device=dev)
+        self.rank, self.world, self.per_frame = rank, world, per_frame
+        # entities this rank owns: (guid head, guid data, group, cls, is_player), oldest first
+        self.owned = deque(zip(w["guid_head"].tolist(), w["guid_data"].tolist(), w["group"].tolist(),
+                               w["cls"].tolist(), w["is_player"].tolist()))
+        self.rng = np.random.default_rng(77 + rank)
+        self.plan = None
+        self.after_frame()
+
+    def before_frame(self):
+        recv = self.shard.migrate([], plan=self.plan)
+        for t in recv:
+            self.owned.append((t.guid_head, t.guid_data, t.group, t.cls, t.is_player))
+
+    def after_frame(self):
+        from noahgameframe_amd.shard import Ticket
+        dst = (self.rank + 1) % self.world
+        out = []
+        for _ in range(min(self.per_frame, len(self.owned))):
+            gh, gd, gr, cl, pl = self.owned.popleft()
+            x, y = self.rng.uniform(-500, 500, 2)
+            out.append(Ticket(gh, gd, cl, pl, dst + 1, gr, float(x), float(y), 0.0, self.rank, dst))
+        self.plan = self.shard._exchange_tickets(out)
 
 
 def main():
@@ -82,8 +129,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -94,18 +145,29 @@ def main():
 
     from noahgameframe_amd import kernel, workload
 
-    # this rank's scene shard: 1M entities in scene rank+1
+    # this rank's scene shard: 1M entities in scene rank+1 (GUID heads differ per rank)
     w = workload.bench_world(n_obj=args.entities, groups=args.groups, players_per_group=args.players_per_group,
-                             n_ticks=1, tick_ms=args.tick_ms, seed=2026 + rank)
+                             n_ticks=1, tick_ms=args.tick_ms, seed=2026 + rank, guid_heads=(7 + 16 * rank, 9 + 16 * rank))
     w["scene"][:] = rank + 1
+    w["init_i"][workload.PID["SceneID"]] = rank + 1
     stream = torch.cuda.current_stream()
-    m = kernel.world_from_workload(w, stream=stream.cuda_stream)
+    migrating = world > 1 and args.migrate > 0
+    # config[1] has no membership changes: no slack slots; config[2] keeps 32 per 256 for arrivals
+    slack = args.slack if args.slack is not None else (32 if migrating else -1)
+    m = kernel.world_from_workload(w, stream=stream.cuda_stream, slack_per_256=slack)
     t0 = int(w["tick_time"][0])
     tick = 0
+    mig = None
+    if migrating:
+        mig = Migration(m, w, rank, world, args.migrate, dev)
 
     def frame():
         nonlocal tick
+        if mig:
+            mig.before_frame()
         m.Execute(t0 + tick * args.tick_ms)
+        if mig:
+            mig.after_frame()   # next frame's tickets, exchanged while this frame runs on the GPU
         tick += 1
 
     for _ in range(args.warmup):
@@ -124,7 +186,7 @@ def main():
     m.set_profiling(False)
     s = m.summary()
     ms, nl, byts = m.kernel_times()
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
@@ -152,12 +214,16 @@ def main():
         "metric": METRIC, "value": value, "unit": "entity-ticks/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int64/f64", "data": "synthetic",
-        "config": {"workload": "BASELINE config[1]: 1M NPC/Player entities per GPU in one scene, "
+        "config": {"workload": (f"BASELINE config[2]: {world} scene shards (scene r+1 on GPU r), "
+                                f"{args.migrate} SwitchScene migrations per rank per frame into the next "
+                                "shard (state rows over RCCL all_to_all); per GPU: " if migrating else
+                                "BASELINE config[1]: ") + "1M NPC/Player entities per GPU in one scene, "
                                f"{args.groups} groups x {args.entities // args.groups}, "
                                f"{args.players_per_group} players/group, heartbeats HPRegen 1s/MPRegen 2s/"
                                f"Move 0.1s/Patrol 3s/Poison 0.5s, {args.tick_ms} ms frames",
                    "entities_per_gpu": args.entities, "groups": args.groups,
-                   "players_per_group": args.players_per_group, "parallelism": f"scene-shard x{world}"},
+                   "players_per_group": args.players_per_group, "parallelism": f"scene-shard x{world}",
+                   "migrations_per_rank_per_frame": args.migrate if migrating else 0},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
         "kernels": kern,
