@@ -27,6 +27,12 @@ sys.path.insert(0, ROOT)
 METRIC = "entity-ticks/sec (update+dirty-diff+fanout) at 1M entities/GPU, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 KNAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles"]
+CONFIG_NAMES = {
+    3: "BASELINE config[3]: 256 scenes x 64 groups, 2M entities per GPU, 32 players per group "
+       "(scene-group sync-list fan-out dominated), heartbeats as config[1], 100 ms frames",
+    4: "BASELINE config[4]: 500k players per GPU, 64-row skill record each (int cooldown + f64 charge "
+       "columns updated by a 100 ms SkillCD heartbeat), groups of 16 players, 100 ms frames",
+}
 
 
 def parse():
@@ -46,6 +52,10 @@ def parse():
                    help="N>1: entities per rank per frame that SwitchScene into the next rank's scene "
                         "(state rows over RCCL all_to_all; BASELINE config[2])")
     p.add_argument("--slack", type=int, default=None, help="free slots per 256 scene-group members")
+    p.add_argument("--config", type=int, default=1, choices=[1, 3, 4],
+                   help="BASELINE config: 1 = 1M entities/GPU (the metric's configuration; with --gpus > 1 "
+                        "it becomes config[2]: scene shards + migration), 3 = 256 scenes x 64 groups, 2M "
+                        "entities, 32 players/group (fan-out dominated), 4 = 500k players x 64-row records")
     p.add_argument("--backend", default="nccl", help="process group backend (nccl = RCCL; gloo only to rehearse "
                                                      "several ranks on one GPU)")
     return p.parse_args()
@@ -146,12 +156,26 @@ def main():
     from noahgameframe_amd import kernel, workload
 
     # this rank's scene shard: 1M entities in scene rank+1 (GUID heads differ per rank)
-    w = workload.bench_world(n_obj=args.entities, groups=args.groups, players_per_group=args.players_per_group,
-                             n_ticks=1, tick_ms=args.tick_ms, seed=2026 + rank, guid_heads=(7 + 16 * rank, 9 + 16 * rank))
-    w["scene"][:] = rank + 1
-    w["init_i"][workload.PID["SceneID"]] = rank + 1
+    if args.config == 3:
+        w = workload.fanout_world(n_ticks=1, tick_ms=args.tick_ms, seed=2027 + rank,
+                                  guid_heads=(7 + 16 * rank, 9 + 16 * rank))
+        w["scene"] += 256 * rank
+    elif args.config == 4:
+        w = workload.record_world(n_ticks=1, tick_ms=args.tick_ms, seed=2028 + rank,
+                                  guid_heads=(7 + 16 * rank, 9 + 16 * rank))
+        w["scene"][:] = rank + 1
+    else:
+        w = workload.bench_world(n_obj=args.entities, groups=args.groups, players_per_group=args.players_per_group,
+                                 n_ticks=1, tick_ms=args.tick_ms, seed=2026 + rank,
+                                 guid_heads=(7 + 16 * rank, 9 + 16 * rank))
+        w["scene"][:] = rank + 1
+    w["init_i"][workload.PID["SceneID"]] = w["scene"]
+    args.entities = len(w["guid_head"])
+    cells = np.unique(w["scene"].astype(np.int64) * (1 << 32) + w["group"], return_counts=True)[1]
+    args.groups = len(cells)
+    args.players_per_group = int(w["is_player"].sum()) // max(len(cells), 1)
     stream = torch.cuda.current_stream()
-    migrating = world > 1 and args.migrate > 0
+    migrating = world > 1 and args.migrate > 0 and args.config == 1
     # config[1] has no membership changes: no slack slots; config[2] keeps 32 per 256 for arrivals
     slack = args.slack if args.slack is not None else (32 if migrating else -1)
     m = kernel.world_from_workload(w, stream=stream.cuda_stream, slack_per_256=slack)
@@ -214,7 +238,8 @@ def main():
         "metric": METRIC, "value": value, "unit": "entity-ticks/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int64/f64", "data": "synthetic",
-        "config": {"workload": (f"BASELINE config[2]: {world} scene shards (scene r+1 on GPU r), "
+        "config": {"workload": CONFIG_NAMES[args.config] if args.config != 1 else (
+                               f"BASELINE config[2]: {world} scene shards (scene r+1 on GPU r), "
                                 f"{args.migrate} SwitchScene migrations per rank per frame into the next "
                                 "shard (state rows over RCCL all_to_all); per GPU: " if migrating else
                                 "BASELINE config[1]: ") + "1M NPC/Player entities per GPU in one scene, "
@@ -232,7 +257,7 @@ def main():
                       "frame_GBps_alg": total_alg / (elapsed / args.steps) / 1e9},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto" and args.config == 1:
         out["cpu_baseline"] = cpu_baseline(args, w)
     if rank == 0:
         print(json.dumps(out), flush=True)

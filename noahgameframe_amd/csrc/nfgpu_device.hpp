@@ -50,6 +50,8 @@ struct alignas(16) SchedCold {
 // timing-only ablations (NFGPU_ABLATE env var); outputs are wrong when set
 constexpr unsigned kAblPrograms = 4;
 constexpr unsigned kAblPerKind = 8;  // not an ablation: force the per-kind operand path (outputs stay exact)
+constexpr unsigned kAblWaves6 = 16, kAblWaves8 = 32;  // k_tick register budgets (outputs stay exact)
+constexpr unsigned kAblFanExpand = 64, kAblFanCopy = 128, kAblNoTally = 256;  // timing only: k_fanout without expansion / copy-out
 
 // record op compiled from the kind programs, sorted by (rec, col)
 struct RecOp {
@@ -63,6 +65,15 @@ struct RecOp {
 constexpr int kMaxU = 16, kMaxW = 12;
 constexpr uint8_t kNoU = 0xFF;
 static_assert(kMaxW == NFK_MAX_TOUCH, "writable slots = touch capacity");
+
+// record op as k_records sees it (Dev::rops, kernel-argument space, so every field is a scalar):
+// cells/used of its record, its shape, and the [gfirst, glast] span of ops on the same record
+struct RecOpX {
+    uint64_t* cells;
+    uint64_t* used;
+    int64_t a, b, c;
+    int32_t kind, rec, col, code, rows, cols, gfirst, glast;
+};
 
 struct Tables {
     nfk_op ops[NFK_MAX_KINDS][NFK_MAX_OPS];
@@ -109,6 +120,12 @@ struct Dev {
     // 60-63 class id
     const uint64_t* fan_desc;
     uint32_t ablate;
+    RecOpX rops[NFK_MAX_OPS];  // record ops sorted by (rec, col)
+    int32_t n_rops;
+    uint32_t rop_kinds;        // kinds with record ops
+    // algorithmic-byte tallies: [3 kernels][kTallyN][8] (one 64-byte line per counter), spread
+    // over kTallyN addresses so that workgroups do not serialise on one atomic
+    unsigned long long* tally;
     // frame working set (k_tick): properties of the U slots, their columns, writable slots in
     // property-id order, and the slot of each property queued by SetProperty this frame
     int32_t n_w;
@@ -134,6 +151,11 @@ struct Dev {
     uint32_t* re_slot; uint32_t* re_rrc; uint64_t* re_old; uint64_t* re_new; uint32_t* re_moff;
     uint32_t* msg_rcpt; int64_t msg_cap;
 };
+
+constexpr int kTallyN = 64, kTallyTick = 0, kTallyRec = 1, kTallyFan = 2;
+__device__ __forceinline__ void tally_add(const Dev& d, int k, unsigned long long v) {
+    atomicAdd(&d.tally[((size_t)k * kTallyN + (blockIdx.x % kTallyN)) * 8], v);
+}
 
 // ---------------- 64-lane primitives ----------------
 __device__ __forceinline__ unsigned long long shfl_up_u64(unsigned long long v, int d) {

@@ -238,6 +238,17 @@ int lookup(World* w, int64_t h, int64_t d, int32_t* obj) {
     return NFK_OK;
 }
 
+// accumulated algorithmic-byte tallies of k_tick, k_records, k_fanout
+int read_tallies(World* w, uint64_t out[3]) {
+    std::vector<unsigned long long> t((size_t)3 * kTallyN * 8);
+    HIPCHK(hipMemcpy(t.data(), w->d.tally, t.size() * 8, hipMemcpyDeviceToHost));
+    for (int k = 0; k < 3; k++) {
+        out[k] = 0;
+        for (int i = 0; i < kTallyN; i++) out[k] += t[((size_t)k * kTallyN + i) * 8];
+    }
+    return NFK_OK;
+}
+
 // dense scratch for readback, at least `bytes`
 int dense_reserve(World* w, size_t bytes) {
     if (bytes <= w->dense_cap) return NFK_OK;
@@ -848,6 +859,7 @@ int nfk_commit(void* world) {
     d.n_class = w->cfg.n_class;
     d.has_recops = nro > 0;
     ALLOC(w->tab_d, sizeof(Tables));
+    ALLOC(d.tally, (size_t)3 * kTallyN * 8 * 8);
     ALLOC(w->ctrl, sizeof(Ctrl));
     ALLOC(d.icol, (size_t)std::max(NI, 1) * cap * 8);
     ALLOC(d.fcol, (size_t)std::max(NF, 1) * cap * 8);
@@ -903,10 +915,34 @@ int nfk_commit(void* world) {
     ALLOC(d.msg_rcpt, d.msg_cap * 4);
     d.tab = w->tab_d;
     d.ctrl = w->ctrl;
+    // record ops with their record's arrays and op span (k_records reads them as scalars)
+    d.n_rops = nro;
+    d.rop_kinds = w->tab.kind_has_recop;
+    for (int i = 0; i < nro; i++) {
+        const RecOp& ro = w->tab.recops[i];
+        RecOpX& x = d.rops[i];
+        x.cells = d.rcells[ro.rec];
+        x.used = d.rused[ro.rec];
+        x.a = ro.a;
+        x.b = ro.b;
+        x.c = ro.c;
+        x.kind = ro.kind;
+        x.rec = ro.rec;
+        x.col = ro.col;
+        x.code = ro.code;
+        x.rows = w->tab.rec_rows[ro.rec];
+        x.cols = w->tab.rec_cols[ro.rec];
+        int f = i, l = i;
+        while (f > 0 && w->tab.recops[f - 1].rec == ro.rec) f--;
+        while (l + 1 < nro && w->tab.recops[l + 1].rec == ro.rec) l++;
+        x.gfirst = f;
+        x.glast = l;
+    }
 
     // uploads (synchronous: commit is control plane)
     HIPCHK(hipMemcpy(w->tab_d, &w->tab, sizeof(Tables), hipMemcpyHostToDevice));
     HIPCHK(hipMemset(w->ctrl, 0, sizeof(Ctrl)));
+    HIPCHK(hipMemset(d.tally, 0, (size_t)3 * kTallyN * 8 * 8));
     std::vector<uint64_t> col(cap, 0);
     for (int p = 0; p < w->n_prop; p++) {
         std::fill(col.begin(), col.end(), 0);
@@ -1377,8 +1413,13 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
-        if (use_u)
-            hipLaunchKernelGGL(k_tick, dim3((unsigned)d.n_tiles), dim3(kTPB), 0, w->stream, d);
+        const size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8;
+        if (use_u && (d.ablate & kAblWaves6))
+            hipLaunchKernelGGL(k_tick<6>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
+        else if (use_u && (d.ablate & kAblWaves8))
+            hipLaunchKernelGGL(k_tick<8>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
+        else if (use_u)
+            hipLaunchKernelGGL(k_tick<5>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
         else
             hipLaunchKernelGGL(k_tick_touch, dim3((unsigned)d.n_tiles), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
@@ -1398,7 +1439,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     {
         TimeScope ts(w, KT_SCAN);
-        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanTPB), 0, w->stream, d);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(4), dim3(kScanTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
     const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0);
@@ -1435,12 +1476,15 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     out->n_rec_events = (int64_t)c.n_re;
     out->n_fired = (int64_t)c.n_fi;
     out->n_msgs = (int64_t)c.n_msgs;
-    out->alg_bytes_tick = (int64_t)(c.bytes_tick - w->last_bytes[0]);
-    out->alg_bytes_rec = (int64_t)(c.bytes_rec - w->last_bytes[1]);
-    out->alg_bytes_fan = (int64_t)(c.bytes_fan - w->last_bytes[2]);
-    w->last_bytes[0] = c.bytes_tick;
-    w->last_bytes[1] = c.bytes_rec;
-    w->last_bytes[2] = c.bytes_fan;
+    {
+        uint64_t tb[3];
+        int r = read_tallies(w, tb);
+        if (r) return r;
+        out->alg_bytes_tick = (int64_t)(tb[0] - w->last_bytes[0]);
+        out->alg_bytes_rec = (int64_t)(tb[1] - w->last_bytes[1]);
+        out->alg_bytes_fan = (int64_t)(tb[2] - w->last_bytes[2]);
+        for (int k = 0; k < 3; k++) w->last_bytes[k] = tb[k];
+    }
     if ((c.err & kErrMsgCap) && !(c.err & ~kErrMsgCap)) {
         // k_fanout wrote nothing (it checks the scanned total first) and only reads the event
         // tiles and the membership CSR, so grow the message buffer to the exact total and
@@ -1636,9 +1680,10 @@ int nfk_kernel_times(void* world, double* ms, int64_t* launches, int64_t* bytes)
         Ctrl c;
         r = read_ctrl(w, &c);
         if (r) return r;
-        w->kt_bytes[0] = (int64_t)c.bytes_tick;
-        w->kt_bytes[1] = (int64_t)c.bytes_rec;
-        w->kt_bytes[2] = (int64_t)c.bytes_fan;
+        uint64_t tb[3];
+        r = read_tallies(w, tb);
+        if (r) return r;
+        for (int k = 0; k < 3; k++) w->kt_bytes[k] = (int64_t)tb[k];
     }
     for (int i = 0; i < KT_N; i++) {
         ms[i] = w->kt_ms[i];
@@ -1661,11 +1706,8 @@ int nfk_reset_kernel_times(void* world) {
         Ctrl c;
         r = read_ctrl(w, &c);
         if (r) return r;
-        w->last_bytes[0] = c.bytes_tick;
-        w->last_bytes[1] = c.bytes_rec;
-        w->last_bytes[2] = c.bytes_fan;
-        // byte tallies restart from the current counters
-        HIPCHK(hipMemset((char*)w->ctrl + offsetof(Ctrl, bytes_tick), 0, 32));
+        // byte tallies restart from zero
+        HIPCHK(hipMemset(w->d.tally, 0, (size_t)3 * kTallyN * 8 * 8));
         w->last_bytes[0] = w->last_bytes[1] = w->last_bytes[2] = 0;
     }
     return NFK_OK;

@@ -362,10 +362,13 @@ __device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& by
 // registers with wave-uniform slot numbers; the slots a Set changed are diffed against their
 // frame-start values (kept in LDS).  Outputs of tile t are written densely at
 // [t * tile_cap, t * tile_cap + count); k_scan_tiles turns the counts into global ranks.
-__global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
+// kWPE: waves per SIMD the register allocation aims at (5 fits without spilling).  The LDS image
+// of the frame-start values is dynamic: n_w writable slots x kTPB.
+template <int kWPE>
+__global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8))) void k_tick(Dev d) {
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
-    __shared__ uint64_t s_o[kMaxW * kTPB];  // frame-start values of the writable slots
+    extern __shared__ uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     const int tile = blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
@@ -498,7 +501,7 @@ __global__ __launch_bounds__(kTPB) void k_tick(Dev d) {
         d.t_ev[tile] = (unsigned)((tot >> 32) & 0xFFFF);
         d.t_fi[tile] = (unsigned)(tot >> 48);
         d.t_msg[tile] = (unsigned)tot;
-        atomicAdd(&d.ctrl->bytes_tick, (unsigned long long)(s_bytes + 12));
+        tally_add(d, kTallyTick, (unsigned long long)(s_bytes + 12));
     }
 }
 
@@ -647,7 +650,7 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
         d.t_ev[tile] = (unsigned)((tot >> 32) & 0xFFFF);
         d.t_fi[tile] = (unsigned)(tot >> 48);
         d.t_msg[tile] = (unsigned)tot;
-        atomicAdd(&d.ctrl->bytes_tick, (unsigned long long)(s_bytes + 12));
+        tally_add(d, kTallyTick, (unsigned long long)(s_bytes + 12));
     }
 }
 
@@ -664,16 +667,15 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int rt = blockIdx.x * (kTPB / 64) + w;
-    if (rt >= d.n_rtiles) return;  // wave-uniform; no barrier follows except the final one below
-    const Tables* tab = d.tab;
-    const int nro = tab->n_recops;
+    if (rt >= d.n_rtiles) return;  // wave-uniform; no barrier follows
+    const int nro = d.n_rops;
     const int s0 = rt * kRTile;
     unsigned bytes = 0;
-    // lane j holds slot s0 + j's fired mask and class
+    // lane j holds slot s0 + j's fired mask and fan-out descriptor
     uint32_t my_mask = 0;
     uint64_t my_desc = 0;
     if (s0 + lane < d.N) {
-        my_mask = d.fired_mask[s0 + lane] & tab->kind_has_recop;
+        my_mask = d.fired_mask[s0 + lane] & d.rop_kinds;
         bytes += 4;
         if (my_mask) {
             my_desc = d.fan_desc[s0 + lane];
@@ -684,7 +686,8 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     unsigned pos = 0, pmsg = 0;  // tile-local
     const size_t re0 = (size_t)rt * d.re_tcap;
     while (work) {
-        // next group of up to kRecGroup slots with record work, in slot order
+        // next group of up to kRecGroup slots with record work, in slot order; every cell load of
+        // the group is issued before any is consumed
         int js[kRecGroup];
         uint32_t masks[kRecGroup];
         uint64_t used[kRecGroup][NFK_MAX_OPS];
@@ -701,13 +704,12 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             for (int j = 0; j < NFK_MAX_OPS; j++) {
                 used[g][j] = 0;
                 cur[g][j] = 0;
-                if (j >= nro || js[g] < 0) continue;
-                const RecOp ro = tab->recops[j];
-                if (!((masks[g] >> ro.kind) & 1)) continue;
-                const int e = s0 + js[g];
-                used[g][j] = d.rused[ro.rec][e];
-                const int rows = tab->rec_rows[ro.rec], cols = tab->rec_cols[ro.rec];
-                if (lane < rows) cur[g][j] = d.rcells[ro.rec][((size_t)e * cols + ro.col) * rows + lane];
+                if (j < nro && js[g] >= 0 && ((masks[g] >> d.rops[j].kind) & 1)) {
+                    const int e = s0 + js[g];
+                    used[g][j] = d.rops[j].used[e];
+                    if (lane < d.rops[j].rows)
+                        cur[g][j] = d.rops[j].cells[((size_t)e * d.rops[j].cols + d.rops[j].col) * d.rops[j].rows + lane];
+                }
             }
 #pragma unroll
         for (int g = 0; g < kRecGroup; g++) {
@@ -721,12 +723,10 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             for (int j = 0; j < NFK_MAX_OPS; j++) {
                 ch[j] = false;
                 nv[j] = 0;
-                if (j >= nro) continue;
-                const RecOp ro = tab->recops[j];
-                if (!((masks[g] >> ro.kind) & 1)) continue;
-                const int rows = tab->rec_rows[ro.rec], cols = tab->rec_cols[ro.rec];
+                if (j >= nro || !((masks[g] >> d.rops[j].kind) & 1)) continue;
+                const RecOpX& ro = d.rops[j];
                 if (lane == 0) bytes += 8;
-                if (lane >= rows || !((used[g][j] >> lane) & 1)) continue;
+                if (lane >= ro.rows || !((used[g][j] >> lane) & 1)) continue;
                 const uint64_t c = cur[g][j];
                 bytes += 8;
                 uint64_t nb;
@@ -746,40 +746,39 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     nb = (uint64_t)__double_as_longlong(v);
                 }
                 if (changed) {
-                    d.rcells[ro.rec][((size_t)e * cols + ro.col) * rows + lane] = nb;
+                    ro.cells[((size_t)e * ro.cols + ro.col) * ro.rows + lane] = nb;
                     bytes += 8;
                     ch[j] = nb != c;  // coalesced diff: bits must differ
                     nv[j] = nb;
                 }
             }
-            // per-slot event order: (rec, row, col) -> records outer, lanes (rows), cols inner
-            int j0 = 0;
-            while (j0 < nro) {
-                const int rec = tab->recops[j0].rec;
-                int j1 = j0;
-                while (j1 < nro && tab->recops[j1].rec == rec) j1++;
+            // per-slot event order (rec, row, col): records outer, lanes (rows), cols inner
+#pragma unroll
+            for (int j0 = 0; j0 < NFK_MAX_OPS; j0++) {
+                if (j0 >= nro || d.rops[j0].gfirst != j0) continue;  // j0 opens a record's op span
+                const int j1 = d.rops[j0].glast;
                 unsigned c = 0;
 #pragma unroll
-                for (int j = 0; j < NFK_MAX_OPS; j++) c += (j >= j0 && j < j1 && ch[j]) ? 1 : 0;
+                for (int j = 0; j < NFK_MAX_OPS; j++) c += (j >= j0 && j <= j1 && ch[j]) ? 1 : 0;
                 const unsigned inc = wave_incl_scan_u32(c);
+                const unsigned n = (unsigned)__shfl((int)inc, 63, 64);
+                if (n == 0) continue;  // wave-uniform
                 unsigned p = pos + inc - c;
-                const unsigned per = event_msgs(desc, s_rflags[cls][rec]);
+                const unsigned per = event_msgs(desc, s_rflags[cls][d.rops[j0].rec]);
 #pragma unroll
                 for (int j = 0; j < NFK_MAX_OPS; j++) {
-                    if (!(j >= j0 && j < j1 && ch[j])) continue;
+                    if (!(j >= j0 && j <= j1 && ch[j])) continue;
                     const size_t at = re0 + p;
                     d.re_slot[at] = (uint32_t)e;
-                    d.re_rrc[at] = ((uint32_t)rec << 16) | ((uint32_t)lane << 8) | (uint32_t)tab->recops[j].col;
+                    d.re_rrc[at] = ((uint32_t)d.rops[j].rec << 16) | ((uint32_t)lane << 8) | (uint32_t)d.rops[j].col;
                     d.re_old[at] = cur[g][j];
                     d.re_new[at] = nv[j];
                     d.re_moff[at] = pmsg + per * (p - pos);
                     p++;
                     bytes += 28;
                 }
-                const unsigned n = (unsigned)__shfl((int)inc, 63, 64);
                 pos += n;
                 pmsg += per * n;
-                j0 = j1;
             }
         }
     }
@@ -788,7 +787,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
         d.t_msg[d.n_tiles + rt] = pmsg;
     }
     const unsigned wb = (unsigned)wave_sum(bytes);
-    if (lane == 0 && wb) atomicAdd(&d.ctrl->bytes_rec, (unsigned long long)wb + 8);
+    if (lane == 0 && wb) tally_add(d, kTallyRec, (unsigned long long)wb + 8);
 }
 
 // ---------------------------------------------------------------------------------
@@ -825,58 +824,47 @@ __device__ __forceinline__ unsigned long long scan_store(ScanArr& x, const unsig
     return s_pre[kScanTPB / 64];
 }
 
+// One workgroup per count array (blockIdx.x: 0 events, 1 fired, 2 record events, 3 messages).
 __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
-    __shared__ unsigned long long s_w[4][kScanTPB / 64 + 1];  // wave totals -> exclusive prefixes, [16] = total
+    __shared__ unsigned long long s_w[kScanTPB / 64 + 1];  // wave totals -> exclusive prefixes, [16] = total
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nrt = d.has_recops ? d.n_rtiles : 0;
-    const int l_ev = d.n_tiles, l_re = nrt, l_msg = d.n_tiles + nrt;
-    unsigned long long c_ev = 0, c_fi = 0, c_re = 0, c_msg = 0;  // carries (uniform)
-    for (int c0 = 0; c0 < l_msg; c0 += kScanTPB * kScanPer) {
+    const int a = blockIdx.x;
+    const uint32_t* cnt = a == 0 ? d.t_ev : a == 1 ? d.t_fi : a == 2 ? d.t_re : d.t_msg;
+    uint32_t* base = a == 0 ? d.ev_base : a == 1 ? d.fi_base : a == 2 ? d.re_base : d.msg_base;
+    const int len = a < 2 ? d.n_tiles : a == 2 ? nrt : d.n_tiles + nrt;
+    unsigned long long carry = 0;
+    for (int c0 = 0; c0 < len; c0 += kScanTPB * kScanPer) {
         const int i0 = c0 + tid * kScanPer;
-        ScanArr ev, fi, re, ms;
-        scan_load(ev, d.t_ev, l_ev, i0);
-        scan_load(fi, d.t_fi, l_ev, i0);
-        scan_load(re, d.t_re, l_re, i0);
-        scan_load(ms, d.t_msg, l_msg, i0);
-        ev.inc = wave_incl_scan(ev.sum);
-        fi.inc = wave_incl_scan(fi.sum);
-        re.inc = wave_incl_scan(re.sum);
-        ms.inc = wave_incl_scan(ms.sum);
-        if (lane == 63) {
-            s_w[0][w] = ev.inc;
-            s_w[1][w] = fi.inc;
-            s_w[2][w] = re.inc;
-            s_w[3][w] = ms.inc;
-        }
+        ScanArr x;
+        scan_load(x, cnt, len, i0);
+        x.inc = wave_incl_scan(x.sum);
+        if (lane == 63) s_w[w] = x.inc;
         __syncthreads();
-        if (w < 4 && lane < kScanTPB / 64) {  // wave w scans array w's 16 wave totals
-            const unsigned long long x = s_w[w][lane];
-            unsigned long long y = x;
+        if (w == 0 && lane < kScanTPB / 64) {
+            const unsigned long long v = s_w[lane];
+            unsigned long long y = v;
 #pragma unroll
             for (int dd = 1; dd < kScanTPB / 64; dd <<= 1) {
                 const unsigned long long t = shfl_up_u64(y, dd);
                 if (lane >= dd) y += t;
             }
-            s_w[w][lane] = y - x;
-            if (lane == kScanTPB / 64 - 1) s_w[w][kScanTPB / 64] = y;
+            s_w[lane] = y - v;
+            if (lane == kScanTPB / 64 - 1) s_w[kScanTPB / 64] = y;
         }
         __syncthreads();
-        c_ev += scan_store(ev, s_w[0], c_ev, d.ev_base, l_ev, i0);
-        c_fi += scan_store(fi, s_w[1], c_fi, d.fi_base, l_ev, i0);
-        c_re += scan_store(re, s_w[2], c_re, d.re_base, l_re, i0);
-        c_msg += scan_store(ms, s_w[3], c_msg, d.msg_base, l_msg, i0);
+        carry += scan_store(x, s_w, carry, base, len, i0);
         __syncthreads();
     }
     if (tid == 0) {
-        d.ev_base[l_ev] = (uint32_t)c_ev;
-        d.fi_base[l_ev] = (uint32_t)c_fi;
-        d.re_base[l_re] = (uint32_t)c_re;
-        d.msg_base[l_msg] = (uint32_t)c_msg;
-        d.ctrl->n_ev = c_ev;
-        d.ctrl->n_fi = c_fi;
-        d.ctrl->n_re = c_re;
-        d.ctrl->n_msgs = c_msg;
-        if (c_msg > (unsigned long long)d.msg_cap) atomicOr(&d.ctrl->err, kErrMsgCap);
+        base[len] = (uint32_t)carry;
+        if (a == 0) d.ctrl->n_ev = carry;
+        if (a == 1) d.ctrl->n_fi = carry;
+        if (a == 2) d.ctrl->n_re = carry;
+        if (a == 3) {
+            d.ctrl->n_msgs = carry;
+            if (carry > (unsigned long long)d.msg_cap) atomicOr(&d.ctrl->err, kErrMsgCap);
+        }
     }
 }
 
@@ -889,11 +877,12 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
 // more than kFanCoop recipients are expanded by their whole wave, 64 recipients per store.
 // Also rewrites each event's tile-local message offset as a global one.  Does nothing (and sets
 // no output) when the frame's messages exceed msg_cap: the host grows the buffer and re-runs it.
-constexpr int kFanLds = 4096, kFanCoop = 32;
+constexpr int kFanLds = 2048, kFanCoop = 12, kFanPer = 4, kFanMsgLds = 6144;
 
 __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
     __shared__ int32_t s_pl[kFanLds];
-    __shared__ uint32_t s_pb[2];
+    __shared__ uint32_t s_msg[kFanMsgLds];  // a pass's recipient runs, stored to HBM coalesced
+    __shared__ uint32_t s_pb[2], s_m[2];
     __shared__ unsigned s_bytes;
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
@@ -901,18 +890,29 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
     const bool rec = (int)blockIdx.x >= d.n_tiles;
     const int t = rec ? (int)blockIdx.x - d.n_tiles : (int)blockIdx.x;
     const uint32_t* base = rec ? d.re_base : d.ev_base;
-    const unsigned cnt = base[t + 1] - base[t];
-    if (cnt == 0) return;  // uniform
-    const size_t off0 = (size_t)t * (rec ? d.re_tcap : d.ev_tcap);
+    const unsigned tcap = (unsigned)(rec ? d.re_tcap : d.ev_tcap);
+    const size_t off0 = (size_t)t * tcap;
     const uint32_t* slots = rec ? d.re_slot : d.ev_slot;
     uint32_t* moff = rec ? d.re_moff : d.ev_moff;
-    if (threadIdx.x == 0) {
-        s_bytes = 0;
-        // player run of the groups between the tile's first and last event
-        const uint64_t a = d.fan_desc[slots[off0]], b = d.fan_desc[slots[off0 + cnt - 1]];
-        s_pb[0] = (uint32_t)a;
-        s_pb[1] = (uint32_t)b + (uint32_t)((b >> 32) & 0x3FFF);
+    // one round trip: the tile's counts, its message range and (speculatively, inside the tile's
+    // staging capacity) the first pass's events
+    const uint32_t b0 = base[t], b1 = base[t + 1];
+    const uint32_t mbase = d.msg_base[blockIdx.x], mend = d.msg_base[blockIdx.x + 1];
+    uint32_t slot[kFanPer], key[kFanPer], lm[kFanPer];
+    uint64_t desc[kFanPer];
+#pragma unroll
+    for (int q = 0; q < kFanPer; q++) {
+        const unsigned i = q * kTPB + threadIdx.x;
+        slot[q] = key[q] = lm[q] = 0;
+        if (i < tcap) {
+            slot[q] = slots[off0 + i];
+            key[q] = rec ? (d.re_rrc[off0 + i] >> 16) : d.ev_pid[off0 + i];
+            lm[q] = moff[off0 + i];
+        }
     }
+    const unsigned cnt = b1 - b0;
+    if (cnt == 0) return;  // uniform
+    if (threadIdx.x == 0) s_bytes = 0;
     if (rec) {
         for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
             ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
@@ -921,68 +921,103 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
         for (int i = threadIdx.x; i < words; i += kTPB)
             ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
     }
-    __syncthreads();
-    const uint32_t pb_lo = s_pb[0], npl = s_pb[1] - s_pb[0];
-    const bool staged = npl <= (uint32_t)kFanLds;
-    unsigned bytes = threadIdx.x == 0 ? 12u + 16u : 0u;
-    if (staged) {
-        for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = d.pl_slot[pb_lo + i];
-        bytes += 4 * ((npl + kTPB - 1 - threadIdx.x) / kTPB);
-    }
-    __syncthreads();
-    const uint32_t mbase = d.msg_base[blockIdx.x];
+    unsigned bytes = threadIdx.x == 0 ? 16u : 0u;
     const int lane = threadIdx.x & 63;
-    for (unsigned c0 = 0; c0 < cnt; c0 += kTPB) {
-        const unsigned i = c0 + threadIdx.x;
-        uint32_t n = 0, m0 = 0, src = 0, r1 = 0, self = 0;
-        bool pub = false;
-        if (i < cnt) {
-            const uint32_t slot = slots[off0 + i];
-            const uint32_t key = rec ? (d.re_rrc[off0 + i] >> 16) : d.ev_pid[off0 + i];
-            const uint32_t lm = moff[off0 + i];
-            const uint64_t desc = d.fan_desc[slot];
-            bytes += 4 + 4 + 4 + 8 + 4;
-            const unsigned cls = (unsigned)(desc >> 60);
-            const uint8_t fl = rec ? s_rflags[cls][key] : s_pflags[cls][key];
-            n = event_msgs(desc, fl);
-            m0 = mbase + lm;
-            moff[off0 + i] = m0;
-            self = slot;
-            pub = fl & NFK_PUBLIC;
-            if (pub) {  // every player of the group but self, NFGUID order
-                src = (uint32_t)desc;
-                r1 = (uint32_t)((desc >> 46) & 0x3FFF);
+    for (unsigned c0 = 0; c0 < cnt; c0 += kTPB * kFanPer) {
+        const unsigned c_end = min(cnt, c0 + kTPB * kFanPer);
+        if (c0) {
+#pragma unroll
+            for (int q = 0; q < kFanPer; q++) {
+                const unsigned i = c0 + q * kTPB + threadIdx.x;
+                if (i < cnt) {
+                    slot[q] = slots[off0 + i];
+                    key[q] = rec ? (d.re_rrc[off0 + i] >> 16) : d.ev_pid[off0 + i];
+                    lm[q] = moff[off0 + i];
+                }
             }
         }
-        uint32_t* out = d.msg_rcpt + m0;
-        if (!pub) {
-            if (n) out[0] = self;
-        } else if (n <= (uint32_t)kFanCoop) {
-            const uint32_t np = n + (r1 ? 1u : 0u);
-            uint32_t m = 0;
-            for (uint32_t q = 0; q < np; q++) {
-                if (q + 1 == r1) continue;
-                out[m++] = staged ? (uint32_t)s_pl[src - pb_lo + q] : (uint32_t)d.pl_slot[src + q];
+        // second round trip: the events' fan-out descriptors
+#pragma unroll
+        for (int q = 0; q < kFanPer; q++)
+            desc[q] = (c0 + q * kTPB + threadIdx.x < c_end) ? d.fan_desc[slot[q]] : kDeadDesc;
+        // the pass's message range and the player run of the groups it touches
+#pragma unroll
+        for (int q = 0; q < kFanPer; q++) {
+            const unsigned i = c0 + q * kTPB + threadIdx.x;
+            if (i == c0) {
+                s_m[0] = lm[q];
+                s_pb[0] = (uint32_t)desc[q];
+            }
+            if (i == c_end - 1) s_pb[1] = (uint32_t)desc[q] + (uint32_t)((desc[q] >> 32) & 0x3FFF);
+        }
+        if (threadIdx.x == 0) s_m[1] = c_end < cnt ? moff[off0 + c_end] : mend - mbase;
+        __syncthreads();
+        const uint32_t p0 = s_m[0], pn = s_m[1] - s_m[0];
+        const bool lds_out = pn <= (uint32_t)kFanMsgLds;
+        const uint32_t pb_lo = s_pb[0], npl = s_pb[1] - s_pb[0];
+        const bool staged = npl <= (uint32_t)kFanLds;
+        if (staged) {  // third round trip: the players, NFGUID order (pl_slot is in slot order)
+            for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = d.pl_slot[pb_lo + i];
+            bytes += 4 * ((npl + kTPB - 1 - threadIdx.x) / kTPB);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kFanPer; q++) {
+            const unsigned i = c0 + q * kTPB + threadIdx.x;
+            uint32_t n = 0, m0 = 0, src = 0, r1 = 0;
+            bool pub = false;
+            if (i < c_end) {
+                const unsigned cls = (unsigned)(desc[q] >> 60);
+                const uint8_t fl = rec ? s_rflags[cls][key[q]] : s_pflags[cls][key[q]];
+                bytes += 4 + 4 + 4 + 8 + 4;
+                n = event_msgs(desc[q], fl);
+                m0 = mbase + lm[q];
+                moff[off0 + i] = m0;
+                pub = fl & NFK_PUBLIC;
+                if (pub) {  // every player of the group but self, NFGUID order
+                    src = (uint32_t)desc[q];
+                    r1 = (uint32_t)((desc[q] >> 46) & 0x3FFF);
+                }
+            }
+            uint32_t* out = lds_out ? s_msg + (lm[q] - p0) : d.msg_rcpt + m0;
+            if (d.ablate & kAblFanExpand) {
+                n = 0;
+                pub = false;
+            }
+            if (!pub) {
+                if (n) out[0] = slot[q];
+            } else if (n <= (uint32_t)kFanCoop) {
+                const uint32_t np = n + (r1 ? 1u : 0u);
+                uint32_t m = 0;
+                for (uint32_t p = 0; p < np; p++) {
+                    if (p + 1 == r1) continue;
+                    out[m++] = staged ? (uint32_t)s_pl[src - pb_lo + p] : (uint32_t)d.pl_slot[src + p];
+                }
+            }
+            bytes += 4 * n;
+            // big groups: the wave expands each such event cooperatively
+            unsigned long long big = __ballot(pub && n > (uint32_t)kFanCoop);
+            while (big) {
+                const int L = __builtin_ctzll(big);
+                big &= big - 1;
+                const uint32_t bn = __shfl(n, L, 64), bsrc = __shfl(src, L, 64), br1 = __shfl(r1, L, 64);
+                const uint32_t bm0 = __shfl(m0, L, 64);
+                uint32_t* bout = lds_out ? s_msg + (bm0 - mbase - p0) : d.msg_rcpt + bm0;
+                for (uint32_t p = lane; p < bn; p += 64) {
+                    const uint32_t pp = p + ((br1 && p + 1 >= br1) ? 1u : 0u);  // skip self
+                    bout[p] = staged ? (uint32_t)s_pl[bsrc - pb_lo + pp] : (uint32_t)d.pl_slot[bsrc + pp];
+                }
             }
         }
-        bytes += 4 * n;
-        // big groups: the wave expands each such event cooperatively
-        unsigned long long big = __ballot(pub && n > (uint32_t)kFanCoop);
-        while (big) {
-            const int L = __builtin_ctzll(big);
-            big &= big - 1;
-            const uint32_t bn = __shfl(n, L, 64), bsrc = __shfl(src, L, 64), br1 = __shfl(r1, L, 64);
-            const uint32_t bm0 = __shfl(m0, L, 64);
-            for (uint32_t q = lane; q < bn; q += 64) {
-                const uint32_t p = q + ((br1 && q + 1 >= br1) ? 1u : 0u);  // skip self
-                d.msg_rcpt[bm0 + q] = staged ? (uint32_t)s_pl[bsrc - pb_lo + p] : (uint32_t)d.pl_slot[bsrc + p];
-            }
-        }
+        __syncthreads();
+        if (lds_out && !(d.ablate & kAblFanCopy))
+            for (uint32_t i = threadIdx.x; i < pn; i += kTPB) d.msg_rcpt[mbase + p0 + i] = s_msg[i];
+        __syncthreads();
     }
     const unsigned wb = (unsigned)wave_sum(bytes);
     if ((threadIdx.x & 63) == 0 && wb) atomicAdd(&s_bytes, wb);
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(&d.ctrl->bytes_fan, (unsigned long long)s_bytes);
+    if (threadIdx.x == 0) tally_add(d, kTallyFan, (unsigned long long)s_bytes);
 }
 
 // ---------------------------------------------------------------------------------

@@ -338,3 +338,20 @@ def bench_world(n_obj=1 << 20, groups=4096, players_per_group=8, n_ticks=16, see
     return make_world(n_obj=n_obj, n_scenes=1, groups_per_scene=groups,
                       players_per_group=players_per_group, n_ticks=n_ticks, seed=seed,
                       ext_frac=kw.pop("ext_frac", 0.0), host_ops=kw.pop("host_ops", False), **kw)
+
+
+def fanout_world(n_ticks=4, seed=2027, n_obj=1 << 21, scenes=256, groups=64, players_per_group=32, **kw):
+    """config[3]: 256 scenes x 64 groups, 2M entities; 32 players per group, so every public dirty
+    property fans out to 31 recipients (scene-group sync-list dominated)."""
+    return make_world(n_obj=n_obj, n_scenes=scenes, groups_per_scene=groups, players_per_group=players_per_group,
+                      n_ticks=n_ticks, seed=seed, ext_frac=kw.pop("ext_frac", 0.0),
+                      host_ops=kw.pop("host_ops", False), **kw)
+
+
+def record_world(n_ticks=4, seed=2028, n_obj=500_000, groups=31_250, rec_rows=64, **kw):
+    """config[4]: 500k players, each with a 64-row skill record whose cooldown (int) and charge
+    (f64) columns a 100 ms SkillCD heartbeat updates every frame; groups of 16 players."""
+    per = n_obj // groups
+    return make_world(n_obj=n_obj, n_scenes=1, groups_per_scene=groups, players_per_group=per, n_ticks=n_ticks,
+                      seed=seed, records=True, rec_rows=rec_rows, ext_frac=kw.pop("ext_frac", 0.0),
+                      host_ops=kw.pop("host_ops", False), **kw)

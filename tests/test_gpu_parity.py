@@ -57,6 +57,18 @@ def test_gpu_full_size_config1(gpu_available):
     compare_runs(run_gpu(w), run_oracle(w))
 
 
+def test_gpu_full_size_config3_fanout(gpu_available):
+    """BASELINE config[3] size: 256 scenes x 64 groups, 2M entities, 32 players per group."""
+    w = workload.fanout_world(n_ticks=3)
+    compare_runs(run_gpu(w), run_oracle(w))
+
+
+def test_gpu_full_size_config4_records(gpu_available):
+    """BASELINE config[4] size: 500k players x 64-row records, cooldown heartbeat every frame."""
+    w = workload.record_world(n_ticks=3)
+    compare_runs(run_gpu(w), run_oracle(w))
+
+
 def test_repeat_frames_are_deterministic(gpu_available):
     w = workload.make_world(n_obj=20000, n_scenes=2, groups_per_scene=50, players_per_group=8, n_ticks=5, seed=77,
                             records=True, rec_rows=32)
