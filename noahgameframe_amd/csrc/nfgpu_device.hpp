@@ -51,7 +51,8 @@ struct alignas(16) SchedCold {
 constexpr unsigned kAblPrograms = 4;
 constexpr unsigned kAblPerKind = 8;  // not an ablation: force the per-kind operand path (outputs stay exact)
 constexpr unsigned kAblWaves6 = 16, kAblWaves8 = 32;  // k_tick register budgets (outputs stay exact)
-constexpr unsigned kAblFanExpand = 64, kAblFanCopy = 128, kAblNoTally = 256;  // timing only: k_fanout without expansion / copy-out
+constexpr unsigned kAblFanExpand = 64, kAblFanCopy = 128;  // timing only: k_fanout without expansion / copy-out
+constexpr unsigned kAblNoRun = 512, kAblNoLoads = 1024, kAblNoEmit = 2048;  // timing only (k_tick)
 
 // record op compiled from the kind programs, sorted by (rec, col)
 struct RecOp {
@@ -75,8 +76,24 @@ struct RecOpX {
     int32_t kind, rec, col, code, rows, cols, gfirst, glast;
 };
 
+constexpr int kMaxProps = NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS;
+
+// a kind-program op in scalar-loadable form (32/64-bit fields only: gfx950 has no byte-sized
+// scalar loads): code | flags << 8 | dst << 16, and the U slots of dst/a/b/c one per byte
+struct OpX {
+    uint32_t cfd;
+    uint32_t slots;
+    int64_t a, b, c;
+};
+
 struct Tables {
     nfk_op ops[NFK_MAX_KINDS][NFK_MAX_OPS];
+    OpX opx[NFK_MAX_KINDS][NFK_MAX_OPS];
+    // property storage: property p of slot e is the 64-bit word pmem[p_off[p] + e * p_str[p]].
+    // Properties that one heartbeat program touches together share a column group stored
+    // interleaved ([cap][group size]), so a sparse heartbeat reads one line per entity.
+    int64_t p_off[kMaxProps];
+    int32_t p_str[kMaxProps];
     uint32_t umask[NFK_MAX_KINDS];                 // U slots kind k's program reads or writes
     uint8_t opu[NFK_MAX_KINDS][NFK_MAX_OPS][4];    // U slot of dst, a, b, c (kNoU = immediate)
     int32_t nops[NFK_MAX_KINDS];
@@ -96,9 +113,8 @@ struct Dev {
     int32_t has_pre;     // RemoveSchedule(self, name) calls are queued this frame (e_flags live)
     const Tables* tab;
     Ctrl* ctrl;
-    // SoA entity columns, column-major [col][cap]
-    int64_t* icol;
-    double* fcol;
+    // property words (see Tables::p_off / p_str)
+    uint64_t* pmem;
     // schedules [kind][cap]
     SchedHot* s_hot;
     SchedCold* s_cold;
@@ -130,8 +146,9 @@ struct Dev {
     // property-id order, and the slot of each property queued by SetProperty this frame
     int32_t n_w;
     int32_t u_pid[kMaxU];
-    uint64_t* u_col[kMaxU];
-    uint8_t u_order[kMaxW];
+    uint64_t* u_col[kMaxU];   // property of slot e at u_col[j][e * u_str[j]]
+    int32_t u_str[kMaxU];
+    int32_t u_order[kMaxW];
     const uint8_t* u_slot;  // [n_prop], only when n_x > 0
     // tiles: property/fired tile t = slots [t*kTile, (t+1)*kTile); record tile r = slots
     // [r*kRTile, (r+1)*kRTile).  Outputs of a tile sit at [t*tile_cap, t*tile_cap + count).
@@ -192,6 +209,15 @@ __device__ __forceinline__ unsigned wave_incl_scan_u32(unsigned v) {
         if (lane >= d) v += t;
     }
     return v;
+}
+
+// Tables through the constant address space: wave-uniform reads become scalar loads (s_load)
+// instead of vector loads, so a kind program's op fields cost no vector memory round trip
+typedef const __attribute__((address_space(4))) Tables CTables;
+__device__ __forceinline__ CTables* ctab(const Tables* t) { return (CTables*)t; }
+
+__device__ __forceinline__ uint64_t* prop_ptr(const Dev& d, uint32_t p, int e) {
+    return d.pmem + d.tab->p_off[p] + (size_t)e * d.tab->p_str[p];
 }
 
 // fan_desc of a slot that holds no entity (slack of a scene group's slot range)

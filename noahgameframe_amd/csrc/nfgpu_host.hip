@@ -4,6 +4,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <string>
 #include <unordered_map>
@@ -818,12 +819,63 @@ int nfk_commit(void* world) {
                 }
                 for (int q = 0; q < 4; q++)
                     if (u[q] != kNoU) w->tab.umask[k] |= 1u << u[q];
+                OpX& x = w->tab.opx[k][i];
+                x.cfd = (uint32_t)op.code | ((uint32_t)op.flags << 8) | ((uint32_t)op.dst << 16);
+                x.slots = (uint32_t)u[0] | ((uint32_t)u[1] << 8) | ((uint32_t)u[2] << 16) | ((uint32_t)u[3] << 24);
+                x.a = op.a;
+                x.b = op.b;
+                x.c = op.c;
             }
         }
     }
     w->n_dst_union = __builtin_popcountll(w->dst_union_mask[0]) + __builtin_popcountll(w->dst_union_mask[1]);
     if (w->n_dst_union > NFK_MAX_TOUCH)
         return fail(NFK_ERR_TOUCH, "programs write more than NFK_MAX_TOUCH distinct properties");
+
+    // property column groups (Tables::p_off / p_str): the properties one heartbeat program
+    // touches are stored interleaved, at most kGroupMax per group, so that a heartbeat firing for
+    // a few entities of a line reads and writes one line per entity instead of one per property
+    std::vector<std::vector<int>> pgroups;
+    {
+        const int NP = w->n_prop;
+        constexpr int kGroupMax = 8;
+        std::vector<int> par(NP), sz(NP, 1);
+        for (int p = 0; p < NP; p++) par[p] = p;
+        std::function<int(int)> find = [&](int x) { return par[x] == x ? x : par[x] = find(par[x]); };
+        for (int k = 0; k < NK; k++) {
+            std::vector<int> ps;
+            for (int i = 0; i < w->tab.nops[k]; i++) {
+                const nfk_op& op = w->tab.ops[k][i];
+                if (op.code == NFK_OP_IADD_CLAMP) {
+                    ps.push_back(op.dst);
+                    if (op.flags & NFK_A_PROP) ps.push_back((int)op.a);
+                    if (op.flags & NFK_LO_PROP) ps.push_back((int)op.b);
+                    if (op.flags & NFK_HI_PROP) ps.push_back((int)op.c);
+                } else if (op.code == NFK_OP_FLERP) {
+                    ps.push_back(op.dst);
+                    ps.push_back((int)op.a);
+                } else if (op.code == NFK_OP_FAFFINE) {
+                    ps.push_back(op.dst);
+                }
+            }
+            for (size_t i = 1; i < ps.size(); i++) {
+                const int a = find(ps[0]), b = find(ps[i]);
+                if (a != b && sz[a] + sz[b] <= kGroupMax) {
+                    par[b] = a;
+                    sz[a] += sz[b];
+                }
+            }
+        }
+        std::vector<int> gi(NP, -1);
+        for (int p = 0; p < NP; p++) {
+            const int r = find(p);
+            if (gi[r] < 0) {
+                gi[r] = (int)pgroups.size();
+                pgroups.emplace_back();
+            }
+            pgroups[gi[r]].push_back(p);
+        }
+    }
 
     // membership layout: scene-group segments, NFGUID order inside (see apply_membership)
     const int64_t n_slots = plan_segments(w, w->slack, w->segs);
@@ -861,8 +913,17 @@ int nfk_commit(void* world) {
     ALLOC(w->tab_d, sizeof(Tables));
     ALLOC(d.tally, (size_t)3 * kTallyN * 8 * 8);
     ALLOC(w->ctrl, sizeof(Ctrl));
-    ALLOC(d.icol, (size_t)std::max(NI, 1) * cap * 8);
-    ALLOC(d.fcol, (size_t)std::max(NF, 1) * cap * 8);
+    ALLOC(d.pmem, (size_t)std::max(w->n_prop, 1) * cap * 8);
+    {
+        int64_t off = 0;
+        for (const auto& g : pgroups) {
+            for (size_t i = 0; i < g.size(); i++) {
+                w->tab.p_off[g[i]] = off + (int64_t)i;
+                w->tab.p_str[g[i]] = (int32_t)g.size();
+            }
+            off += (int64_t)g.size() * cap;
+        }
+    }
     ALLOC(d.s_hot, (size_t)std::max(NK, 1) * cap * sizeof(SchedHot));
     ALLOC(d.s_cold, (size_t)std::max(NK, 1) * cap * sizeof(SchedCold));
     ALLOC(d.e_flags, cap);
@@ -943,14 +1004,14 @@ int nfk_commit(void* world) {
     HIPCHK(hipMemcpy(w->tab_d, &w->tab, sizeof(Tables), hipMemcpyHostToDevice));
     HIPCHK(hipMemset(w->ctrl, 0, sizeof(Ctrl)));
     HIPCHK(hipMemset(d.tally, 0, (size_t)3 * kTallyN * 8 * 8));
-    std::vector<uint64_t> col(cap, 0);
-    for (int p = 0; p < w->n_prop; p++) {
-        std::fill(col.begin(), col.end(), 0);
-        if (!w->init_props[p].empty())
-            for (int32_t s = 0; s < d.N; s++)
-                if (w->obj_of_slot[s] >= 0) col[s] = w->init_props[p][w->obj_of_slot[s]];
-        void* dst = p < NI ? (void*)(d.icol + (size_t)p * cap) : (void*)(d.fcol + (size_t)(p - NI) * cap);
-        HIPCHK(hipMemcpy(dst, col.data(), (size_t)cap * 8, hipMemcpyHostToDevice));
+    for (const auto& g : pgroups) {
+        const size_t gs = g.size();
+        std::vector<uint64_t> blk((size_t)cap * gs, 0);
+        for (size_t i = 0; i < gs; i++)
+            if (!w->init_props[g[i]].empty())
+                for (int32_t s = 0; s < d.N; s++)
+                    if (w->obj_of_slot[s] >= 0) blk[(size_t)s * gs + i] = w->init_props[g[i]][w->obj_of_slot[s]];
+        HIPCHK(hipMemcpy(d.pmem + w->tab.p_off[g[0]], blk.data(), blk.size() * 8, hipMemcpyHostToDevice));
     }
     for (int r = 0; r < NR; r++) {
         size_t per = (size_t)w->tab.rec_rows[r] * w->tab.rec_cols[r];
@@ -1345,12 +1406,11 @@ int nfk_execute(void* world, int64_t now_ms) {
         std::vector<int> ord(n_w);
         for (int i = 0; i < n_w; i++) ord[i] = i;
         std::sort(ord.begin(), ord.end(), [&](int a, int b) { return d.u_pid[a] < d.u_pid[b]; });
-        for (int i = 0; i < n_w; i++) d.u_order[i] = (uint8_t)ord[i];
+        for (int i = 0; i < n_w; i++) d.u_order[i] = ord[i];
         for (int j = 0; j < kMaxU; j++) {
             const int p = d.u_pid[j];
-            d.u_col[j] = p < 0 ? nullptr
-                               : (p < d.n_int ? (uint64_t*)(d.icol + (size_t)p * d.cap)
-                                              : (uint64_t*)(d.fcol + (size_t)(p - d.n_int) * d.cap));
+            d.u_col[j] = p < 0 ? nullptr : d.pmem + w->tab.p_off[p];
+            d.u_str[j] = p < 0 ? 0 : w->tab.p_str[p];
         }
     }
     if (!use_u) uslot.clear();
@@ -1413,7 +1473,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
-        const size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8;
+        const size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;
         if (use_u && (d.ablate & kAblWaves6))
             hipLaunchKernelGGL(k_tick<6>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
         else if (use_u && (d.ablate & kAblWaves8))
@@ -1443,7 +1503,7 @@ int nfk_execute(void* world, int64_t now_ms) {
         HIPCHK(hipGetLastError());
     }
     const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0);
-    if (nfan) {
+    if (nfan && !(d.ablate & kAblNoEmit)) {  // (timing ablation: events were not written)
         TimeScope ts(w, KT_FAN);
         hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
@@ -1543,10 +1603,10 @@ int nfk_read_prop(void* world, int32_t pid, uint64_t* bits) {
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     HIPCHK(hipStreamSynchronize(w->stream));
     const Dev& d = w->d;
-    std::vector<uint64_t> col(d.N);
-    const void* src = pid < d.n_int ? (const void*)(d.icol + (size_t)pid * d.cap)
-                                    : (const void*)(d.fcol + (size_t)(pid - d.n_int) * d.cap);
-    HIPCHK(hipMemcpy(col.data(), src, (size_t)d.N * 8, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> col(std::max(d.N, 1));
+    if (d.N)
+        HIPCHK(hipMemcpy2D(col.data(), 8, d.pmem + w->tab.p_off[pid], (size_t)w->tab.p_str[pid] * 8, 8, (size_t)d.N,
+                           hipMemcpyDeviceToHost));
     memset(bits, 0, (size_t)w->n_obj * 8);  // objects no longer in this world read 0
     for (int32_t s = 0; s < d.N; s++)
         if (w->obj_of_slot[s] >= 0) bits[w->obj_of_slot[s]] = col[s];

@@ -78,8 +78,7 @@ struct Ent {
     int n;
     bool ovf;
     unsigned bytes;
-    const int64_t* icol;
-    const double* fcol;
+    const Dev* dv;
     size_t cap;
     int n_int;
     int e;
@@ -120,8 +119,7 @@ struct Ent {
         uint64_t v = 0;
         if (tget(p, v)) return v;
         bytes += 8;
-        if ((int)p < n_int) return (uint64_t)icol[(size_t)p * cap + e];
-        return (uint64_t)__double_as_longlong(fcol[(size_t)(p - n_int) * cap + e]);
+        return *prop_ptr(*dv, p, e);
     }
     __device__ __forceinline__ int64_t geti(uint32_t p) { return (int64_t)getb(p); }
     __device__ __forceinline__ double getf(uint32_t p) { return __longlong_as_double((long long)getb(p)); }
@@ -153,16 +151,16 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
         if (op.code != NFK_OP_IADD_CLAMP && op.code != NFK_OP_FLERP && op.code != NFK_OP_FAFFINE) continue;
         const uint32_t p0 = op.dst;
         const bool isf = op.code != NFK_OP_IADD_CLAMP;
-        pre[i][0] = isf ? (uint64_t)__double_as_longlong(en.fcol[(size_t)(p0 - en.n_int) * en.cap + en.e])
-                        : (uint64_t)en.icol[(size_t)p0 * en.cap + en.e];
+        (void)isf;
+        pre[i][0] = *prop_ptr(*en.dv, p0, en.e);
         en.bytes += 8;
         if (op.code == NFK_OP_FLERP) {
-            pre[i][1] = (uint64_t)__double_as_longlong(en.fcol[(size_t)(op.a - en.n_int) * en.cap + en.e]);
+            pre[i][1] = *prop_ptr(*en.dv, (uint32_t)op.a, en.e);
             en.bytes += 8;
         } else if (op.code == NFK_OP_IADD_CLAMP) {
-            if (op.flags & NFK_A_PROP) { pre[i][1] = (uint64_t)en.icol[(size_t)op.a * en.cap + en.e]; en.bytes += 8; }
-            if (op.flags & NFK_LO_PROP) { pre[i][2] = (uint64_t)en.icol[(size_t)op.b * en.cap + en.e]; en.bytes += 8; }
-            if (op.flags & NFK_HI_PROP) { pre[i][3] = (uint64_t)en.icol[(size_t)op.c * en.cap + en.e]; en.bytes += 8; }
+            if (op.flags & NFK_A_PROP) { pre[i][1] = *prop_ptr(*en.dv, (uint32_t)op.a, en.e); en.bytes += 8; }
+            if (op.flags & NFK_LO_PROP) { pre[i][2] = *prop_ptr(*en.dv, (uint32_t)op.b, en.e); en.bytes += 8; }
+            if (op.flags & NFK_HI_PROP) { pre[i][3] = *prop_ptr(*en.dv, (uint32_t)op.c, en.e); en.bytes += 8; }
         }
     }
 #pragma unroll
@@ -242,40 +240,42 @@ __device__ __forceinline__ void uput_lane(uint64_t (&v)[kMaxU], uint32_t j, uint
 // The fired kinds' programs in schedule-name order on the register working set.  A Set that
 // fails the reference's change predicate leaves the value as it was; wm collects the slots a
 // Set changed at least once.
-__device__ __forceinline__ void run_programs_u(uint64_t (&v)[kMaxU], uint32_t& wm, const Tables* __restrict__ tab,
+__device__ __forceinline__ void run_programs_u(uint64_t (&v)[kMaxU], uint32_t& wm, const Tables* __restrict__ tab_,
                                                uint32_t fired, int n_kind) {
+    CTables* tab = ctab(tab_);
     for (int k = 0; k < n_kind; k++) {
         if (!((fired >> k) & 1)) continue;
         const int n = tab->nops[k];
         for (int i = 0; i < n; i++) {
-            const nfk_op op = tab->ops[k][i];
-            const uint8_t* u = tab->opu[k][i];
-            if (op.code == NFK_OP_IADD_CLAMP) {
-                const int64_t cur = (int64_t)uget(v, u[0]);
-                const int64_t a = (op.flags & NFK_A_PROP) ? (int64_t)uget(v, u[1]) : op.a;
-                const int64_t lo = (op.flags & NFK_LO_PROP) ? (int64_t)uget(v, u[2]) : op.b;
-                const int64_t hi = (op.flags & NFK_HI_PROP) ? (int64_t)uget(v, u[3]) : op.c;
+            const uint32_t cfd = tab->opx[k][i].cfd, sl = tab->opx[k][i].slots;
+            const uint32_t code = cfd & 0xFF, flags = (cfd >> 8) & 0xFF;
+            const uint32_t u0 = sl & 0xFF, u1 = (sl >> 8) & 0xFF, u2 = (sl >> 16) & 0xFF, u3 = sl >> 24;
+            if (code == NFK_OP_IADD_CLAMP) {
+                const int64_t cur = (int64_t)uget(v, u0);
+                const int64_t a = (flags & NFK_A_PROP) ? (int64_t)uget(v, u1) : tab->opx[k][i].a;
+                const int64_t lo = (flags & NFK_LO_PROP) ? (int64_t)uget(v, u2) : tab->opx[k][i].b;
+                const int64_t hi = (flags & NFK_HI_PROP) ? (int64_t)uget(v, u3) : tab->opx[k][i].c;
                 int64_t r = (int64_t)((uint64_t)cur + (uint64_t)a);
                 r = r < lo ? lo : r;
                 r = r > hi ? hi : r;
-                uput(v, u[0], (uint64_t)r);  // NFCProperty::SetInt (PR:273): r == cur changes nothing
-                wm |= (r != cur) ? (1u << u[0]) : 0u;
-            } else if (op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE) {
-                const uint64_t xb = uget(v, u[0]);
+                uput(v, u0, (uint64_t)r);  // NFCProperty::SetInt (PR:273): r == cur changes nothing
+                wm |= (r != cur) ? (1u << u0) : 0u;
+            } else if (code == NFK_OP_FLERP || code == NFK_OP_FAFFINE) {
+                const uint64_t xb = uget(v, u0);
                 const double x = __longlong_as_double((long long)xb);
                 double r;
-                if (op.code == NFK_OP_FLERP) {
-                    const double tg = __longlong_as_double((long long)uget(v, u[1]));
+                if (code == NFK_OP_FLERP) {
+                    const double tg = __longlong_as_double((long long)uget(v, u1));
                     const double dd = tg - x;
-                    const double m = dd * __longlong_as_double(op.b);
+                    const double m = dd * __longlong_as_double(tab->opx[k][i].b);
                     r = x + m;
                 } else {
-                    const double m = x * __longlong_as_double(op.a);
-                    r = m + __longlong_as_double(op.b);
+                    const double m = x * __longlong_as_double(tab->opx[k][i].a);
+                    r = m + __longlong_as_double(tab->opx[k][i].b);
                 }
                 const bool set = !(fabs(r - x) <= 1e-15);  // NFCProperty::SetFloat (PR:314): IsZeroDouble(v - cur)
-                uput(v, u[0], set ? (uint64_t)__double_as_longlong(r) : xb);
-                wm |= set ? (1u << u[0]) : 0u;
+                uput(v, u0, set ? (uint64_t)__double_as_longlong(r) : xb);
+                wm |= set ? (1u << u0) : 0u;
             }
             // record ops run in k_records
         }
@@ -305,7 +305,7 @@ constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
 // NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
 // order).  The hot records of a chunk of kinds are loaded together (independent 16 B loads).
 // Returns the fired-kind mask; rescheduled / removed records are stored back.
-__device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& bytes) {
+__device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& bytes, int32_t* s_rem = nullptr) {
     uint32_t fired = 0;
     bool taken = false;  // std::map remove-list key already owned (SM:68)
     if (d.has_pre) {
@@ -348,6 +348,7 @@ __device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& by
                 h[j].state = st | kStFired;
             }
             d.s_hot[(size_t)k * d.cap + e] = h[j];
+            if (s_rem) s_rem[k * kTPB + threadIdx.x] = h[j].remain;  // for the fired list
             bytes += 16;
         }
     }
@@ -378,6 +379,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         for (int i = threadIdx.x; i < words; i += kTPB)
             ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
     }
+    int32_t* s_rem = (int32_t*)(s_o + (size_t)d.n_w * kTPB);  // [n_kind][kTPB] remain after a fire
     unsigned bytes = 0;
     uint32_t fired = 0, xh = 0, wm = 0;
     uint64_t desc = kDeadDesc;
@@ -385,8 +387,11 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
 #pragma unroll
     for (int j = 0; j < kMaxU; j++) v[j] = 0;
     if (e < d.N) {
+        // descriptor and schedule records in one round trip: a slack slot has no schedules, so
+        // the scan needs no liveness test
         desc = d.fan_desc[e];
         bytes += 8;
+        fired = sched_scan(d, e, bytes, s_rem);  // NFCScheduleModule::Execute (SM:51-81)
     }
     const bool live = !desc_dead(desc);
     if (live) {
@@ -398,15 +403,14 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                 for (int i = (int)xh - 1; i < d.n_x && d.x_slot[i] == (uint32_t)e; i++)
                     need |= 1u << d.u_slot[d.x_pid[i]];
         }
-        fired = sched_scan(d, e, bytes);  // NFCScheduleModule::Execute (SM:51-81)
         if (!(d.ablate & kAblPrograms))
             for (int k = 0; k < d.n_kind; k++)
-                if ((fired >> k) & 1) need |= d.tab->umask[k];
+                if ((fired >> k) & 1) need |= ctab(d.tab)->umask[k];
         // one batch of independent loads: every value this entity's frame reads or writes
 #pragma unroll
         for (int j = 0; j < kMaxU; j++)
-            if ((need >> j) & 1) {
-                v[j] = d.u_col[j][e];
+            if (((need >> j) & 1) && !(d.ablate & kAblNoLoads)) {
+                v[j] = d.u_col[j][(size_t)e * d.u_str[j]];
                 bytes += 8;
             }
 #pragma unroll
@@ -431,7 +435,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             }
         }
         // the fired heartbeats' effect programs, in schedule-name order
-        if (!(d.ablate & kAblPrograms) && fired) run_programs_u(v, wm, d.tab, fired, d.n_kind);
+        if (!(d.ablate & (kAblPrograms | kAblNoRun)) && fired) run_programs_u(v, wm, d.tab, fired, d.n_kind);
     }
     __syncthreads();  // s_pflags
     // dirty diff against the frame-start values, and each dirty event's fan-out message count
@@ -458,13 +462,13 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
 
     if (live) {
         // write back the changed values; their events in property-id order
-        if (dm) {
+        if (dm && !(d.ablate & kAblNoEmit)) {
             for (int q = 0; q < d.n_w; q++) {
                 const uint32_t j = d.u_order[q];
                 if (!((dm >> j) & 1)) continue;
                 const uint64_t nv = uget(v, j);
                 const uint32_t pid = (uint32_t)d.u_pid[j];
-                d.u_col[j][e] = nv;
+                d.u_col[j][(size_t)e * d.u_str[j]] = nv;
                 const size_t at = ev0 + pev;
                 d.ev_slot[at] = (uint32_t)e;
                 d.ev_pid[at] = pid;
@@ -483,7 +487,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             const size_t at = fi0 + pfi;
             d.fi_slot[at] = (uint32_t)e;
             d.fi_kind[at] = (uint32_t)k;
-            d.fi_remain[at] = d.s_hot[(size_t)k * d.cap + e].remain;
+            d.fi_remain[at] = s_rem[k * kTPB + threadIdx.x];
             pfi++;
             bytes += 12;
         }
@@ -532,8 +536,7 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
     en.old = s_old + threadIdx.x;
     en.ovf = false;
     en.bytes = 0;
-    en.icol = d.icol;
-    en.fcol = d.fcol;
+    en.dv = &d;
     en.cap = (size_t)d.cap;
     en.n_int = d.n_int;
     en.e = live ? e : 0;
@@ -594,8 +597,7 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
         for (int j = 0; j < NFK_MAX_TOUCH; j++) {
             if (!((dmask >> j) & 1)) continue;
             const uint32_t pid = en.pid[j];
-            if ((int)pid < d.n_int) d.icol[(size_t)pid * d.cap + e] = (int64_t)en.cur[j];
-            else d.fcol[(size_t)(pid - d.n_int) * d.cap + e] = __longlong_as_double((long long)en.cur[j]);
+            *prop_ptr(d, pid, e) = en.cur[j];
             en.bytes += 8;
         }
         // events in property-id order
@@ -1028,10 +1030,8 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
 // membership metadata of the scene-group segments that changed.  Thread t handles word
 // t / n of row t % n, so a wave reads one column across consecutive slots.
 __device__ __forceinline__ uint64_t* row_word(const Dev& d, int32_t s, int w) {
-    if (w < d.n_int) return (uint64_t*)(d.icol + (size_t)w * d.cap + s);
-    w -= d.n_int;
-    if (w < d.n_flt) return (uint64_t*)(d.fcol + (size_t)w * d.cap + s);
-    w -= d.n_flt;
+    if (w < d.n_int + d.n_flt) return prop_ptr(d, (uint32_t)w, s);
+    w -= d.n_int + d.n_flt;
     if (w < 4 * d.n_kind) {
         const int k = w >> 2, q = w & 3;
         return q < 2 ? (uint64_t*)&d.s_hot[(size_t)k * d.cap + s] + q
