@@ -197,8 +197,7 @@ def main():
     for _ in range(args.warmup):
         frame()
     s = m.summary()  # also surfaces any device error from warmup
-    m.reset_kernel_times()
-    m.set_profiling(True)
+    # the timed region runs without kernel instrumentation ...
     barrier()
     torch.cuda.synchronize()
     ts = time.perf_counter()
@@ -207,8 +206,14 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - ts
-    m.set_profiling(False)
     s = m.summary()
+    # ... then the same number of frames again with HIP events around every kernel, for the
+    # per-kernel durations and algorithmic bytes of the roofline
+    m.reset_kernel_times()
+    m.set_profiling(True)
+    for _ in range(args.steps):
+        frame()
+    m.set_profiling(False)
     ms, nl, byts = m.kernel_times()
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
