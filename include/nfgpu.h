@@ -232,6 +232,14 @@ int nfk_read_fired(void* world, int32_t* fi_obj, int32_t* fi_kind, int32_t* fi_r
 /* dense CSR over [prop events ++ record events]: msg_off[n_ev + n_re + 1], recipients as objects */
 int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj);
 
+/* ---- leaderboards: NFIRankRedisModule::GetRange (NFCRankRedisModule.cpp:109, a Redis
+ * ZREVRANGE 0..k-1 WITH SCORES) with the property as the rank value (SetRankValue takes a double):
+ * the k entities of this world with the highest score, ties by NFGUID::ToString() descending
+ * (Redis orders equal scores by member, reversed).  Across scene shards, every rank's top k is
+ * gathered and merged with the same order (noahgameframe_amd/shard.py rank_top_global). */
+int nfk_rank_top(void* world, int32_t pid, int32_t k, int32_t* n_out, int64_t* guid_head, int64_t* guid_data,
+                 double* score);
+
 /* ---- measurement ---- */
 int nfk_set_profiling(void* world, int32_t on);
 /* accumulated device time (ms), launch count and algorithmic bytes per kernel:

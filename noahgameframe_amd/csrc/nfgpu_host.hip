@@ -1724,6 +1724,85 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
     return NFK_OK;
 }
 
+int nfk_rank_top(void* world, int32_t pid, int32_t k, int32_t* n_out, int64_t* guid_head, int64_t* guid_data,
+                 double* score) {
+    World* w = (World*)world;
+    if (!w || !n_out || (k > 0 && (!guid_head || !guid_data || !score))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    if (pid < 0 || pid >= w->n_prop || k < 0) return fail(NFK_ERR_ARG, "bad property / k");
+    *n_out = 0;
+    const Dev& d = w->d;
+    if (k == 0 || d.N == 0) return NFK_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    unsigned* hist = nullptr;
+    HIPCHK(hipMalloc((void**)&hist, 257 * 4));
+    const unsigned grid = std::min<unsigned>((d.N + kTPB - 1) / kTPB, 2048);
+    // radix select of the k-th largest key, 8 bits at a time
+    uint64_t prefix = 0, pmask = 0;
+    uint64_t above = 0;  // entities with a key above the current prefix range
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        hipError_t e1 = hipMemsetAsync(hist, 0, 256 * 4, w->stream);
+        hipLaunchKernelGGL(k_rank_hist, dim3(grid), dim3(kTPB), 0, w->stream, d, pid, prefix, pmask, shift, hist);
+        unsigned h[256];
+        hipError_t e2 = hipMemcpyAsync(h, hist, sizeof h, hipMemcpyDeviceToHost, w->stream);
+        hipError_t e3 = hipStreamSynchronize(w->stream);
+        if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+            (void)hipFree(hist);
+            return fail(NFK_ERR_HIP, "rank histogram failed");
+        }
+        int dg = 255;
+        for (; dg > 0; dg--) {
+            if (above + h[dg] >= (uint64_t)k) break;
+            above += h[dg];
+        }
+        prefix |= (uint64_t)dg << shift;
+        pmask |= 0xFFull << shift;
+    }
+    // everything at or above the k-th key: fewer than k above it plus all its ties
+    const uint64_t thr = prefix;
+    unsigned cnt = 0;
+    std::vector<int64_t> cand;  // (slot, raw property word) pairs
+    for (int attempt = 0; attempt < 2; attempt++) {
+        const unsigned cap = attempt == 0 ? (unsigned)std::min<int64_t>(4 * (int64_t)k + 1024, d.N) : cnt;
+        int64_t* out = nullptr;
+        HIPCHK(hipMalloc((void**)&out, (size_t)std::max(cap, 1u) * 16));
+        HIPCHK(hipMemsetAsync(hist + 256, 0, 4, w->stream));
+        hipLaunchKernelGGL(k_rank_collect, dim3(grid), dim3(kTPB), 0, w->stream, d, pid, thr, hist + 256, out, cap);
+        HIPCHK(hipMemcpyAsync(&cnt, hist + 256, 4, hipMemcpyDeviceToHost, w->stream));
+        HIPCHK(hipStreamSynchronize(w->stream));
+        if (cnt <= cap) {
+            cand.resize((size_t)cnt * 2);
+            if (cnt) HIPCHK(hipMemcpy(cand.data(), out, (size_t)cnt * 16, hipMemcpyDeviceToHost));
+            (void)hipFree(out);
+            break;
+        }
+        (void)hipFree(out);
+    }
+    (void)hipFree(hist);
+    // ZREVRANGE order: score desc, member (NFGUID::ToString, NFGUID.h:93) desc
+    struct C { double s; int32_t o; std::string m; };
+    std::vector<C> cs;
+    cs.reserve(cand.size() / 2);
+    for (size_t i = 0; i < cand.size(); i += 2) {
+        const int32_t sl = (int32_t)cand[i];
+        const uint64_t raw = (uint64_t)cand[i + 1];
+        double sc;
+        if (pid < d.n_int) sc = (double)(int64_t)raw;
+        else memcpy(&sc, &raw, 8);
+        const int32_t o = w->obj_of_slot[sl];
+        cs.push_back({sc, o, std::to_string(w->gh[o]) + "-" + std::to_string(w->gd[o])});
+    }
+    std::sort(cs.begin(), cs.end(), [](const C& a, const C& b) { return a.s != b.s ? a.s > b.s : a.m > b.m; });
+    const int32_t n = (int32_t)std::min<size_t>(cs.size(), (size_t)k);
+    for (int32_t i = 0; i < n; i++) {
+        guid_head[i] = w->gh[cs[i].o];
+        guid_data[i] = w->gd[cs[i].o];
+        score[i] = cs[i].s;
+    }
+    *n_out = n;
+    return NFK_OK;
+}
+
 int nfk_set_profiling(void* world, int32_t on) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");

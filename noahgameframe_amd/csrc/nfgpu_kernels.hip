@@ -1083,6 +1083,47 @@ __global__ __launch_bounds__(kTPB) void k_meta(const int32_t* __restrict__ slot,
 }
 
 // ---------------------------------------------------------------------------------
+// Leaderboards (NFIRankRedisModule::GetRange, a Redis ZREVRANGE over a property's score): the
+// score is the property as a double (SetRankValue takes a double); keys are the scores' bits
+// mapped to an unsigned order.  A radix select finds the score of the k-th entity (8-bit digits,
+// most significant first), then every entity at or above it is collected; the host orders that
+// small set by (score desc, NFGUID string desc) and keeps k.
+__device__ __forceinline__ uint64_t rank_key(const Dev& d, int32_t pid, int e) {
+    const uint64_t raw = *prop_ptr(d, (uint32_t)pid, e);
+    const double sc = pid < d.n_int ? (double)(int64_t)raw : __longlong_as_double((long long)raw);
+    const uint64_t b = (uint64_t)__double_as_longlong(sc == 0.0 ? 0.0 : sc);  // -0 == +0
+    return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+
+__global__ __launch_bounds__(kTPB) void k_rank_hist(Dev d, int32_t pid, uint64_t prefix, uint64_t pmask, int shift,
+                                                    unsigned* __restrict__ hist) {
+    __shared__ unsigned s_h[256];
+    s_h[threadIdx.x] = 0;
+    __syncthreads();
+    for (int e = blockIdx.x * kTPB + threadIdx.x; e < d.N; e += gridDim.x * kTPB) {
+        if (desc_dead(d.fan_desc[e])) continue;
+        const uint64_t k = rank_key(d, pid, e);
+        if ((k & pmask) == prefix) atomicAdd(&s_h[(k >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    if (s_h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], s_h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kTPB) void k_rank_collect(Dev d, int32_t pid, uint64_t thr, unsigned* __restrict__ n,
+                                                       int64_t* __restrict__ out, unsigned cap) {
+    for (int e = blockIdx.x * kTPB + threadIdx.x; e < d.N; e += gridDim.x * kTPB) {
+        if (desc_dead(d.fan_desc[e])) continue;
+        if (rank_key(d, pid, e) >= thr) {
+            const unsigned i = atomicAdd(n, 1u);
+            if (i < cap) {
+                out[2 * (size_t)i] = e;  // (slot, raw property word)
+                out[2 * (size_t)i + 1] = (int64_t)*prop_ptr(d, (uint32_t)pid, e);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // Readback only (not part of a frame): tile-staged array -> dense array in global order.
 template <typename T>
 __global__ __launch_bounds__(kTPB) void k_compact(const T* __restrict__ src, T* __restrict__ dst,

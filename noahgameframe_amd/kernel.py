@@ -89,6 +89,7 @@ def load_library(path=LIB_PATH):
         "nfk_export_objects": [VP, I32, VP, VP, VP],
         "nfk_import_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
         "nfk_spawn_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP], "nfk_sync": [VP],
+        "nfk_rank_top": [VP, I32, I32, VP, VP, VP, VP],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -255,6 +256,18 @@ class NFKernelModule:
         pr = np.ascontiguousarray(props, np.uint64)
         self._chk(self.lib.nfk_spawn_objects(self.h, len(a[0]), *[_p(x) for x in a], _p(pr)))
         self.n_obj = self.object_count()
+
+    # ---- leaderboards (NFIRankRedisModule::GetRange) ----
+    def rank_top(self, prop, k):
+        """The k entities with the highest score (the property as a double), ties by
+        NFGUID::ToString() descending: (guid_head, guid_data, score) arrays."""
+        pid = wl.PID[prop] if isinstance(prop, str) else int(prop)
+        gh = np.zeros(max(k, 1), np.int64)
+        gd = np.zeros(max(k, 1), np.int64)
+        sc = np.zeros(max(k, 1), np.float64)
+        n = ctypes.c_int32()
+        self._chk(self.lib.nfk_rank_top(self.h, pid, int(k), ctypes.byref(n), _p(gh), _p(gd), _p(sc)))
+        return gh[:n.value], gd[:n.value], sc[:n.value]
 
     # ---- one frame ----
     def Execute(self, now_ms):

@@ -258,3 +258,42 @@ class ShardedReplay:
         recs = [self.m.read_record(r) for r in range(int(self.w["cfg"][5]))]
         own = sorted(self.local_of.items())
         return {o: (props[:, li], nx[:, li], rm[:, li], st[:, li] & 1, [x[li] for x in recs]) for o, li in own}
+
+
+def zrevrange_order(gh, gd, score):
+    """Indices ordering entries like Redis ZREVRANGE over members NFGUID::ToString()
+    ("head-data", NFGUID.h:93): score descending, equal scores by member descending."""
+    items = sorted(range(len(score)), key=lambda i: (float(score[i]), f"{int(gh[i])}-{int(gd[i])}"), reverse=True)
+    return np.asarray(items, np.int64)
+
+
+def rank_top_global(m, prop, k, group=None, device=None):
+    """Global leaderboard across scene shards (NFIRankRedisModule::GetRange over every shard's
+    entities): each rank's exact top k (nfk_rank_top) is all-gathered over the process group
+    (RCCL with device tensors under "nccl") and merged in ZREVRANGE order."""
+    import torch
+    import torch.distributed as dist
+    gh, gd, sc = m.rank_top(prop, k)
+    ws = dist.get_world_size(group) if dist.is_initialized() else 1
+    if ws == 1:
+        return gh, gd, sc
+    dev = device if device is not None and dist.get_backend(group) == "nccl" else torch.device("cpu")
+    buf = torch.zeros((k + 1, 3), dtype=torch.int64)
+    buf[0, 0] = len(gh)
+    if len(gh):
+        buf[1:1 + len(gh), 0] = torch.from_numpy(gh)
+        buf[1:1 + len(gh), 1] = torch.from_numpy(gd)
+        buf[1:1 + len(gh), 2] = torch.from_numpy(sc.view(np.int64))
+    buf = buf.to(dev)
+    parts = [torch.empty_like(buf) for _ in range(ws)]
+    dist.all_gather(parts, buf, group=group)
+    H, D, S = [], [], []
+    for p in parts:
+        p = p.cpu().numpy()
+        n = int(p[0, 0])
+        H.append(p[1:1 + n, 0])
+        D.append(p[1:1 + n, 1])
+        S.append(p[1:1 + n, 2].view(np.float64))
+    H, D, S = np.concatenate(H), np.concatenate(D), np.concatenate(S)
+    o = zrevrange_order(H, D, S)[:k]
+    return H[o], D[o], S[o]

@@ -28,7 +28,10 @@ def main():
         r = rep.frame(t)
         frames.append({k: r[k] for k in ("ev_obj", "ev_pid", "ev_old", "ev_new", "re_obj", "re_rrc", "re_old",
                                          "re_new", "fi_obj", "fi_kind", "fi_rem", "mo_off", "mr_obj")})
-    res = {"frames": frames, "final": rep.final_state(), "out": rep.shard.migrated_out, "in": rep.shard.migrated_in}
+    from noahgameframe_amd.shard import rank_top_global
+    ranks = {p: rank_top_global(rep.m, p, k) for p, k in (("Level", 50), ("Gold", 20), ("X", 30))}
+    res = {"frames": frames, "final": rep.final_state(), "out": rep.shard.migrated_out, "in": rep.shard.migrated_in,
+           "ranks": ranks}
     with open(os.path.join(out, f"rank{rank}.pkl"), "wb") as f:
         pickle.dump(res, f)
     rep.m.close()

@@ -143,3 +143,22 @@ def test_cpp_plugin_api_replay_matches_oracle(gpu_available, tmp_path):
     ref = run_oracle(w)
     compare_runs(got, {k: v for k, v in ref.items() if k in got})
     assert len(got) == 13 * 8 + 2
+
+
+@pytest.mark.parametrize("prop,k", [("Level", 100), ("Gold", 1), ("HP", 1000), ("X", 64), ("Camp", 10)])
+def test_rank_top_matches_zrevrange(gpu_available, prop, k):
+    """nfk_rank_top = Redis ZREVRANGE 0..k-1 over the property (NFCRankRedisModule.cpp:109): score
+    desc, equal scores by NFGUID::ToString() desc — heavy ties (Level, Camp) included."""
+    from noahgameframe_amd.shard import zrevrange_order
+    w = workload.make_world(n_obj=30000, n_scenes=2, groups_per_scene=20, players_per_group=5, n_ticks=3, seed=91,
+                            switch_frac=0.01)
+    m = kernel.world_from_workload(w, slack_per_256=32)
+    for t in range(3):
+        kernel.run_workload(m, w, t, collect=False)
+    pid = workload.PID[prop]
+    vals = m.read_prop(pid).astype(np.float64)
+    gh, gd, sc = m.rank_top(prop, k)
+    o = zrevrange_order(w["guid_head"], w["guid_data"], vals)[:k]
+    assert list(zip(gh.tolist(), gd.tolist())) == list(zip(w["guid_head"][o].tolist(), w["guid_data"][o].tolist()))
+    np.testing.assert_array_equal(sc, vals[o])
+    m.close()
