@@ -3,7 +3,8 @@
 // NFCKernelModule + NFCScheduleModule + the NFCSceneAOIModule property fan-out.
 //
 // Reference interfaces mirrored (flyish/NoahGameFrame):
-//   NFComm/NFPluginModule/NFIKernelModule.h     CreateScene, CreateObject, SetPropertyInt/Float,
+//   NFComm/NFPluginModule/NFIKernelModule.h     CreateScene, CreateObject (before or after AfterInit),
+//                                               DestroyObject, SwitchScene, SetPropertyInt/Float,
 //                                               GetPropertyInt/Float, RegisterCommonPropertyEvent,
 //                                               Execute (NFCKernelModule.cpp:70)
 //   NFComm/NFPluginModule/NFIScheduleModule.h   AddSchedule(self, name, cb, fTime, nCount),
@@ -11,6 +12,7 @@
 //   NFComm/NFPluginModule/NFISceneAOIModule.h   AddPropertyEventCallBack / AddRecordEventCallBack
 //                                               (the recipient-list events, AOI.cpp:703-727)
 //   NFComm/NFPluginModule/NFIModule.h           Init / AfterInit / Execute / BeforeShut / Shut
+//   NFComm/NFPluginModule/NFIRankRedisModule.h  GetRange (leaderboard over a property)
 //
 // Differences a plugin author must know:
 //   * A heartbeat's state change is a device effect program (nfk_op list) registered once per
@@ -111,6 +113,10 @@ public:
     bool SetPropertyFloat(const NFGUID& self, const std::string& name, double v);
     int64_t GetPropertyInt(const NFGUID& self, const std::string& name);
     double GetPropertyFloat(const NFGUID& self, const std::string& name);
+    // NFCKernelModule::SwitchScene (KM:901-951); writes SceneID/GroupID/X/Y/Z when the schema has them
+    bool SwitchScene(const NFGUID& self, int nTargetSceneID, int nTargetGroupID, float fX, float fY, float fZ);
+    // NFCKernelModule::DestroyObject (KM:273-308): leaves its group, its schedules go with it
+    bool DestroyObject(const NFGUID& self);
     bool RegisterCommonPropertyEvent(const PROPERTY_EVENT_FUNCTOR& cb);
     bool RegisterCommonRecordEvent(const RECORD_EVENT_FUNCTOR& cb);
 
@@ -119,6 +125,9 @@ public:
                      int nCount, int64_t now_ms);
     bool RemoveSchedule(const NFGUID& self, const std::string& name);
     bool RemoveSchedule(const NFGUID& self);
+
+    // ---- NFIRankRedisModule::GetRange(type, 0, k - 1, memberScoreVec) over a property ----
+    bool GetRange(const std::string& prop, int k, std::vector<std::pair<std::string, double>>& memberScoreVec);
 
     // ---- NFISceneAOIModule recipient-list events ----
     bool AddPropertyEventCallBack(const PROPERTY_SINGLE_EVENT_FUNCTOR& cb);

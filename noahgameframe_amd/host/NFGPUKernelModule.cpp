@@ -85,8 +85,34 @@ bool NFGPUKernelModule::CreateScene(int nSceneID) {
 
 bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGroupID, const std::string& cls,
                                      const std::map<std::string, TData>& init) {
-    if (committed_) throw std::runtime_error("objects are created before AfterInit in this round");
     if (!scenes_.count(nSceneID)) return false;  // "There is no scene" (KM:107)
+    if (committed_) {
+        // after AfterInit: the entity enters at the start of the next frame (nfk_spawn_objects)
+        if (obj_of_.count(self)) return false;  // "The object has Exists" (KM:131)
+        auto c = class_id_.find(cls);
+        if (c == class_id_.end()) return false;
+        std::vector<uint64_t> row(props_.size(), 0);
+        for (auto& kv : init) {
+            int p = prop_id_.at(kv.first);
+            row[PropertyId(kv.first)] =
+                props_[p].type == TDATA_INT ? (uint64_t)kv.second.GetInt() : bits_of(kv.second.GetFloat());
+        }
+        for (const char* nm : {"SceneID", "GroupID"}) {  // CreateObject sets them (KM:248-249)
+            auto it = prop_id_.find(nm);
+            if (it != prop_id_.end() && props_[it->second].type == TDATA_INT)
+                row[PropertyId(nm)] = (uint64_t)(int64_t)(nm[0] == 'S' ? nSceneID : nGroupID);
+        }
+        const uint8_t cl = (uint8_t)c->second, pl = cls == "Player";
+        check(nfk_spawn_objects(world_, 1, &self.nHead64, &self.nData64, &nSceneID, &nGroupID, &cl, &pl, row.data()),
+              "nfk_spawn_objects");
+        obj_of_[self] = (int)guids_.size();
+        guids_.push_back(self);
+        scene_.push_back(nSceneID);
+        group_.push_back(nGroupID);
+        cls_.push_back(cl);
+        isplayer_.push_back(pl);
+        return true;
+    }
     if (obj_of_.count(self)) return false;       // "The object has Exists" (KM:131)
     auto c = class_id_.find(cls);
     if (c == class_id_.end()) return false;
@@ -155,7 +181,51 @@ bool NFGPUKernelModule::AfterInit() {
         if (p < (int)init_.size() && !init_[p].empty())
             check(nfk_load_prop(world_, PropertyId(props_[p].name), init_[p].data()), "nfk_load_prop");
     check(nfk_commit(world_), "nfk_commit");
+    {
+        auto pid_of = [&](const char* nm, TDATA_TYPE t) {
+            auto it = prop_id_.find(nm);
+            return (it != prop_id_.end() && props_[it->second].type == t) ? PropertyId(nm) : -1;
+        };
+        check(nfk_set_scene_props(world_, pid_of("SceneID", TDATA_INT), pid_of("GroupID", TDATA_INT),
+                                  pid_of("X", TDATA_FLOAT), pid_of("Y", TDATA_FLOAT), pid_of("Z", TDATA_FLOAT)),
+              "nfk_set_scene_props");
+    }
     committed_ = true;
+    return true;
+}
+
+bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int nTargetGroupID, float fX, float fY,
+                                    float fZ) {
+    if (!committed_ || ObjectIndex(self) < 0) return false;  // "There is no object" (KM:948)
+    if (!scenes_.count(nTargetSceneID)) return false;       // "no this container" (KM:917)
+    check(nfk_switch_scene(world_, self.nHead64, self.nData64, nTargetSceneID, nTargetGroupID, fX, fY, fZ),
+          "nfk_switch_scene");
+    const int o = ObjectIndex(self);
+    scene_[o] = nTargetSceneID;
+    group_[o] = nTargetGroupID;
+    return true;
+}
+
+bool NFGPUKernelModule::DestroyObject(const NFGUID& self) {
+    const int o = ObjectIndex(self);
+    if (!committed_ || o < 0) return false;
+    check(nfk_destroy_objects(world_, 1, &self.nHead64, &self.nData64), "nfk_destroy_objects");
+    obj_of_.erase(self);  // its object index stays reserved; later calls find no object
+    for (auto it = sched_cb_.begin(); it != sched_cb_.end();)
+        it = it->first.first == o ? sched_cb_.erase(it) : std::next(it);
+    return true;
+}
+
+bool NFGPUKernelModule::GetRange(const std::string& prop, int k,
+                                 std::vector<std::pair<std::string, double>>& memberScoreVec) {
+    memberScoreVec.clear();
+    if (!committed_ || !prop_id_.count(prop) || k <= 0) return false;
+    std::vector<int64_t> gh(k), gd(k);
+    std::vector<double> sc(k);
+    int32_t n = 0;
+    check(nfk_rank_top(world_, PropertyId(prop), k, &n, gh.data(), gd.data(), sc.data()), "nfk_rank_top");
+    for (int i = 0; i < n; i++)  // member = NFGUID::ToString() (NFGUID.h:93)
+        memberScoreVec.emplace_back(std::to_string(gh[i]) + "-" + std::to_string(gd[i]), sc[i]);
     return true;
 }
 

@@ -172,13 +172,31 @@ int main(int argc, char** argv) {
     int32_t* h_cnt = (int32_t*)A("h_count")->data;
     int64_t* h_time = (int64_t*)A("h_time")->data;
 
+    // SwitchScene calls (optional in the workload); scene -1 = the object's own cell
+    nfio_arr* swa = nfio_get(&wf, "sw_tick");
+    const int64_t NW = swa ? (int64_t)swa->shape[0] : 0;
+    int32_t* sw_tick = NW ? (int32_t*)swa->data : nullptr;
+    int32_t* sw_obj = NW ? (int32_t*)A("sw_obj")->data : nullptr;
+    int32_t* sw_scene = NW ? (int32_t*)A("sw_scene")->data : nullptr;
+    int32_t* sw_group = NW ? (int32_t*)A("sw_group")->data : nullptr;
+    float* sw_x = NW ? (float*)A("sw_x")->data : nullptr;
+    float* sw_y = NW ? (float*)A("sw_y")->data : nullptr;
+    float* sw_z = NW ? (float*)A("sw_z")->data : nullptr;
+    std::vector<int32_t> cur_sc(sc, sc + N), cur_gr(gr, gr + N);
+
     nfio_writer w;
     if (nfio_wopen(&w, argv[2])) return 2;
-    int64_t xi = 0, hi = 0;
+    int64_t xi = 0, hi = 0, wi = 0;
     for (int t = 0; t < NT; t++) {
         ev_obj.clear(); ev_pid.clear(); ev_old.clear(); ev_new.clear();
         re_obj.clear(); re_rrc.clear(); re_old.clear(); re_new.clear();
         fi_obj.clear(); fi_kind.clear(); fi_rem.clear(); mr.clear(); moff.clear();
+        for (; wi < NW && sw_tick[wi] == t; wi++) {
+            const int o = sw_obj[wi];
+            if (sw_scene[wi] >= 0) { cur_sc[o] = sw_scene[wi]; cur_gr[o] = sw_group[wi]; }
+            km.CreateScene(cur_sc[o]);  // false when it exists
+            if (!km.SwitchScene(NFGUID(gh[o], gd[o]), cur_sc[o], cur_gr[o], sw_x[wi], sw_y[wi], sw_z[wi])) return 5;
+        }
         for (; hi < NH && h_tick[hi] == t; hi++) {
             NFGUID g(gh[h_obj[hi]], gd[h_obj[hi]]);
             if (h_op[hi] == 1) km.AddSchedule(g, kname[h_kind[hi]], hb, h_int[hi], h_cnt[hi], h_time[hi]);
@@ -215,6 +233,27 @@ int main(int argc, char** argv) {
         nfk_read_prop(km.World(), km.PropertyId(pname[p]), (uint64_t*)&fi[(size_t)p * N]);
     for (int p = 0; p < NF; p++)
         nfk_read_prop(km.World(), km.PropertyId(pname[NI + p]), (uint64_t*)&fff[(size_t)p * N]);
+    // leaderboard over the first int and first float property: NFIRankRedisModule::GetRange
+    for (int p : {0, (int)NI}) {
+        std::vector<std::pair<std::string, double>> top;
+        if (!km.GetRange(pname[p], 100, top)) return 6;
+        std::vector<int64_t> th, td;
+        std::vector<double> ts;
+        for (auto& m : top) {
+            long long a = 0, b = 0;
+            if (sscanf(m.first.c_str(), "%lld-%lld", &a, &b) != 2) return 7;
+            th.push_back(a);
+            td.push_back(b);
+            ts.push_back(m.second);
+        }
+        char nm[32];
+        snprintf(nm, sizeof nm, "rank_p%d_head", p);
+        nfio_put1(&w, nm, NFIO_I64, th.data(), th.size(), 8);
+        snprintf(nm, sizeof nm, "rank_p%d_data", p);
+        nfio_put1(&w, nm, NFIO_I64, td.data(), td.size(), 8);
+        snprintf(nm, sizeof nm, "rank_p%d_score", p);
+        nfio_put1(&w, nm, NFIO_F64, ts.data(), ts.size(), 8);
+    }
     uint64_t sh[2] = {(uint64_t)NI, (uint64_t)N};
     nfio_put(&w, "final_i", NFIO_I64, 2, sh, fi.data(), fi.size() * 8);
     uint64_t sf[2] = {(uint64_t)NF, (uint64_t)N};

@@ -134,15 +134,25 @@ def test_cpp_plugin_api_replay_matches_oracle(gpu_available, tmp_path):
     if not os.path.exists(exe):
         import __graft_entry__
         __graft_entry__.build_plugin()
+    from noahgameframe_amd.shard import zrevrange_order
     w = workload.make_world(n_obj=3000, n_scenes=2, groups_per_scene=6, players_per_group=5, n_ticks=8, seed=31,
-                            ext_frac=0.05, host_ops=True)
+                            ext_frac=0.05, host_ops=True, switch_frac=0.01, switch_new_groups=True)
+    assert len(w["sw_tick"]) > 0
     wp, op = str(tmp_path / "w.nfio"), str(tmp_path / "o.nfio")
     nfio.write(wp, w)
     subprocess.run([exe, wp, op], check=True)
     got = nfio.read(op)
     ref = run_oracle(w)
-    compare_runs(got, {k: v for k, v in ref.items() if k in got})
-    assert len(got) == 13 * 8 + 2
+    compare_runs({k: v for k, v in got.items() if not k.startswith("rank_")},
+                 {k: v for k, v in ref.items() if k in got})
+    assert len(got) == 13 * 8 + 2 + 6
+    # GetRange (NFIRankRedisModule, ZREVRANGE 0..99) over the final oracle state
+    n_int = w["cfg"][1]
+    for p, final in ((0, ref["final_i"][0].astype(np.float64)), (n_int, ref["final_f"][0])):
+        order = zrevrange_order(w["guid_head"], w["guid_data"], final)[:100]
+        np.testing.assert_array_equal(got[f"rank_p{p}_head"], w["guid_head"][order])
+        np.testing.assert_array_equal(got[f"rank_p{p}_data"], w["guid_data"][order])
+        np.testing.assert_array_equal(got[f"rank_p{p}_score"], final[order])
 
 
 @pytest.mark.parametrize("prop,k", [("Level", 100), ("Gold", 1), ("HP", 1000), ("X", 64), ("Camp", 10)])
