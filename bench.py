@@ -229,11 +229,12 @@ def main():
     dom = max((k for k in kern if kern[k]["alg_bytes_per_launch"]), key=lambda k: kern[k]["avg_us"])
     d = kern[dom]
     achieved = d["alg_bytes_per_launch"] / (d["avg_us"] * 1e-6) / 1e9
-    traffic = None
+    traffic, traffic_src = None, None
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
             traffic = pm.get(dom, {}).get("hbm_bytes_per_launch")
+            traffic_src = pm.get("source")
         except Exception:
             traffic = None
     total_alg = sum(v["alg_bytes_per_launch"] or 0 for v in kern.values())
@@ -255,7 +256,8 @@ def main():
                    "players_per_group": args.players_per_group, "parallelism": f"scene-shard x{world}",
                    "migrations_per_rank_per_frame": args.migrate if migrating else 0},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src},
         "kernels": kern,
         "per_frame": {"prop_events": s["n_prop_events"], "rec_events": s["n_rec_events"], "fired": s["n_fired"],
                       "msgs": s["n_msgs"], "alg_bytes_all_kernels": total_alg,
