@@ -115,10 +115,13 @@ typedef struct nfk_summary {
  *   property events  (scene, group, guid, prop)
  *   record events    (scene, group, guid, rec, row, col); rrc = rec<<16 | row<<8 | col
  *   fired heartbeats (scene, group, guid, kind)
- * Fan-out (GetBroadCastObject recipients) is a dense CSR over the virtual event stream
- * [property events ++ record events] in that order: ev_moff / re_moff hold the global index
- * in msg_rcpt of the event's first recipient; its recipients end where the next event's begin
- * (n_msgs after the last).  Recipients are slots; slot_obj maps slot -> object index.
+ * Fan-out (GetBroadCastObject recipients): the messages of tile t (property tiles, then record
+ * tiles) are one run of msg_cnt[t] recipients at msg_rcpt[msg_base[t]], in event order; tiles
+ * take their runs from one atomic cursor, so runs are placed in completion order.  ev_moff /
+ * re_moff hold the index in msg_rcpt of the event's first recipient; its recipients end where
+ * the next event of its tile begins (msg_base[t] + msg_cnt[t] after the tile's last).
+ * Recipients are slots; slot_obj maps slot -> object index.  nfk_read_fanout returns the dense
+ * CSR over [property events ++ record events].
  * nfk_read_* return the same data as dense arrays in object-index terms. */
 typedef struct nfk_outputs {
     int32_t n_tiles, tile_slots;     /* property / fired tiles (tile_slots = 256) */
@@ -127,13 +130,14 @@ typedef struct nfk_outputs {
     const uint32_t* ev_base;   /* [n_tiles + 1]  exclusive scan of per-tile event counts */
     const uint32_t* fi_base;   /* [n_tiles + 1] */
     const uint32_t* re_base;   /* [n_rtiles + 1] */
-    const uint32_t* msg_base;  /* [n_tiles + n_rtiles + 1] first message of each tile */
+    const uint32_t* msg_base;  /* [n_tiles + n_rtiles] first message of each tile */
+    const uint32_t* msg_cnt;   /* [n_tiles + n_rtiles] messages of each tile */
     const uint32_t* ev_slot; const uint32_t* ev_pid; const uint64_t* ev_old; const uint64_t* ev_new;
     const uint32_t* ev_moff;
     const uint32_t* re_slot; const uint32_t* re_rrc; const uint64_t* re_old; const uint64_t* re_new;
     const uint32_t* re_moff;
     const uint32_t* fi_slot; const uint32_t* fi_kind; const int32_t* fi_remain;
-    const uint32_t* msg_rcpt; /* dense [n_msgs] */
+    const uint32_t* msg_rcpt; /* [n_msgs], one run per tile */
     const int32_t* slot_obj;  /* slot -> object index */
 } nfk_outputs;
 

@@ -137,6 +137,7 @@ struct World {
     size_t stage_cap = 0;
 
     int32_t ticks = 0;
+    int32_t last_par = 0;  // Ctrl::msg_cur parity of the last launched frame
 
     bool profiling = false;
     std::vector<PendingTiming> pend;
@@ -958,6 +959,7 @@ int nfk_commit(void* world) {
     ALLOC(d.fi_base, (nt + 1) * 4);
     ALLOC(d.re_base, (nrt + 1) * 4);
     ALLOC(d.msg_base, (nt + nrt + 1) * 4);
+    ALLOC(d.t_defer, (nt + nrt) * 4);
     d.msg_cap = w->cfg.msg_capacity > 0 ? w->cfg.msg_capacity : (int64_t)cap * 32;
     if (d.msg_cap > 0xFFFFFFFFll) return fail(NFK_ERR_ARG, "msg_capacity must fit 32-bit offsets");
     ALLOC(d.ev_slot, ev_n * 4);
@@ -1051,6 +1053,7 @@ int nfk_commit(void* world) {
     HIPCHK(hipMemset(d.fi_base, 0, (nt + 1) * 4));
     HIPCHK(hipMemset(d.re_base, 0, (nrt + 1) * 4));
     HIPCHK(hipMemset(d.msg_base, 0, (nt + nrt + 1) * 4));
+    HIPCHK(hipMemset(d.t_defer, 0, (nt + nrt) * 4));
     // creation-time values are now on the device
     for (auto& v : w->init_props) std::vector<uint64_t>().swap(v);
     for (auto& v : w->init_rcells) std::vector<uint64_t>().swap(v);
@@ -1471,15 +1474,21 @@ int nfk_execute(void* world, int64_t now_ms) {
                                d.e_flags, d.s_hot, d.n_kind, d.cap);
         HIPCHK(hipGetLastError());
     }
+    d.par = w->ticks & 1;
+    w->last_par = d.par;
+    // k_tick writes its tiles' fan-out itself (its LDS image doubles as the message window)
+    d.fuse_fan = use_u && !(d.ablate & (kAblNoFuse | kAblNoEmit));
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
-        const size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;
-        if (use_u && (d.ablate & kAblWaves6))
-            hipLaunchKernelGGL(k_tick<6>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
+        size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;
+        if (d.fuse_fan) lds = std::max(lds, (size_t)kFanWinBytes);
+        d.lds_words = (int32_t)(lds / 4);
+        if (use_u && (d.ablate & kAblWaves5))
+            hipLaunchKernelGGL(k_tick<5>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
         else if (use_u && (d.ablate & kAblWaves8))
             hipLaunchKernelGGL(k_tick<8>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
-        else if (use_u)
-            hipLaunchKernelGGL(k_tick<5>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
+        else if (use_u)  // 80 VGPRs, no spills: 6 waves per SIMD
+            hipLaunchKernelGGL(k_tick<6>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
         else
             hipLaunchKernelGGL(k_tick_touch, dim3((unsigned)d.n_tiles), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
@@ -1499,13 +1508,15 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     {
         TimeScope ts(w, KT_SCAN);
-        hipLaunchKernelGGL(k_scan_tiles, dim3(4), dim3(kScanTPB), 0, w->stream, d);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(3), dim3(kScanTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
-    const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0);
-    if (nfan && !(d.ablate & kAblNoEmit)) {  // (timing ablation: events were not written)
+    // the tiles k_tick did not fan out: record tiles, and property tiles after k_tick_touch
+    const int fan0 = d.fuse_fan ? d.n_tiles : 0;
+    const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0) - fan0;
+    if (nfan > 0 && !(d.ablate & kAblNoEmit)) {  // (timing ablation: events were not written)
         TimeScope ts(w, KT_FAN);
-        hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d);
+        hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, (int32_t)fan0, 0);
         HIPCHK(hipGetLastError());
     }
     w->ticks++;
@@ -1535,7 +1546,7 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     out->n_prop_events = (int64_t)c.n_ev;
     out->n_rec_events = (int64_t)c.n_re;
     out->n_fired = (int64_t)c.n_fi;
-    out->n_msgs = (int64_t)c.n_msgs;
+    out->n_msgs = (int64_t)c.msg_cur[w->last_par];
     {
         uint64_t tb[3];
         int r = read_tallies(w, tb);
@@ -1546,24 +1557,28 @@ int nfk_summary_get(void* world, nfk_summary* out) {
         for (int k = 0; k < 3; k++) w->last_bytes[k] = tb[k];
     }
     if ((c.err & kErrMsgCap) && !(c.err & ~kErrMsgCap)) {
-        // k_fanout wrote nothing (it checks the scanned total first) and only reads the event
-        // tiles and the membership CSR, so grow the message buffer to the exact total and
-        // re-run it for this frame.
-        const int64_t need = (int64_t)c.n_msgs + (int64_t)c.n_msgs / 4 + 1024;
+        // The tiles whose message range ran past msg_cap wrote no messages and are marked in
+        // t_defer; their ranges are reserved (the cursor holds the frame's exact total).  Grow
+        // the buffer, keeping what the other tiles wrote, and fan the deferred tiles out.
+        const int64_t total = (int64_t)c.msg_cur[w->last_par];
+        const int64_t need = total + total / 4 + 1024;
         if (need > 0xFFFFFFFFll) return fail(NFK_ERR_CAPACITY, "fan-out exceeds 2^32 messages per frame");
+        uint32_t* grown = nullptr;
+        int r = alloc_track(w, (void**)&grown, (size_t)need * 4);
+        if (r) return r;
+        HIPCHK(hipMemcpy(grown, w->d.msg_rcpt, (size_t)w->d.msg_cap * 4, hipMemcpyDeviceToDevice));
         HIPCHK(hipFree(w->d.msg_rcpt));
         w->allocs.erase(std::remove(w->allocs.begin(), w->allocs.end(), (void*)w->d.msg_rcpt), w->allocs.end());
-        int r = alloc_track(w, (void**)&w->d.msg_rcpt, (size_t)need * 4);
-        if (r) return r;
+        w->d.msg_rcpt = grown;
         w->d.msg_cap = need;
         HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
         Dev d = w->d;
+        d.par = w->last_par;
         const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0);
-        hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d);
+        hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, 0, 1);
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(w->stream));
         HIPCHK(hipMemcpy(&c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
-        out->n_msgs = (int64_t)c.n_msgs;
     }
     out->device_error = (int32_t)c.err;
     out->tick = w->ticks;
@@ -1583,6 +1598,7 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     o->n_rtiles = d.has_recops ? d.n_rtiles : 0; o->rtile_slots = kRTile;
     o->ev_tile_cap = d.ev_tcap; o->fi_tile_cap = d.fi_tcap; o->re_tile_cap = d.re_tcap;
     o->ev_base = d.ev_base; o->fi_base = d.fi_base; o->re_base = d.re_base; o->msg_base = d.msg_base;
+    o->msg_cnt = d.t_msg;
     o->ev_slot = d.ev_slot; o->ev_pid = d.ev_pid; o->ev_old = d.ev_old; o->ev_new = d.ev_new; o->ev_moff = d.ev_moff;
     o->re_slot = d.re_slot; o->re_rrc = d.re_rrc; o->re_old = d.re_old; o->re_new = d.re_new; o->re_moff = d.re_moff;
     o->fi_slot = d.fi_slot; o->fi_kind = d.fi_kind; o->fi_remain = d.fi_remain;
@@ -1712,15 +1728,40 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
     Ctrl c;
     int r = read_ctrl(w, &c);
     if (r) return r;
-    if (c.n_msgs > (unsigned long long)w->d.msg_cap) return fail(NFK_ERR_CAPACITY, "call nfk_summary_get first");
+    if (c.err & kErrMsgCap) return fail(NFK_ERR_CAPACITY, "call nfk_summary_get first");
     const Dev& d = w->d;
+    const size_t nm = c.msg_cur[w->last_par];
+    // each tile's messages are one run at msg_base[tile]; the dense CSR walks tiles in order
+    const int ntt = d.n_tiles + (d.has_recops ? d.n_rtiles : 0);
+    std::vector<uint32_t> mb(ntt), mc(ntt), eb(d.n_tiles + 1), rb(d.n_rtiles + 1);
+    std::vector<uint64_t> db(ntt);
+    if (ntt) {
+        HIPCHK(hipMemcpy(mb.data(), d.msg_base, (size_t)ntt * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(mc.data(), d.t_msg, (size_t)ntt * 4, hipMemcpyDeviceToHost));
+    }
+    HIPCHK(hipMemcpy(eb.data(), d.ev_base, eb.size() * 4, hipMemcpyDeviceToHost));
+    if (d.has_recops) HIPCHK(hipMemcpy(rb.data(), d.re_base, rb.size() * 4, hipMemcpyDeviceToHost));
+    uint64_t acc = 0;
+    for (int t = 0; t < ntt; t++) {
+        db[t] = acc;
+        acc += mc[t];
+    }
+    if (acc != nm) return fail(NFK_ERR_STATE, "message cursor and tile counts disagree");
     GATHER(w, d.ev_moff, d.ev_base, d.n_tiles, d.ev_tcap, (size_t)c.n_ev, msg_off);
     if (d.has_recops) GATHER(w, d.re_moff, d.re_base, d.n_rtiles, d.re_tcap, (size_t)c.n_re, msg_off + c.n_ev);
-    msg_off[c.n_ev + c.n_re] = (uint32_t)c.n_msgs;
-    const size_t nm = c.n_msgs;
+    for (int t = 0; t < d.n_tiles; t++)
+        for (uint32_t i = eb[t]; i < eb[t + 1]; i++) msg_off[i] = (uint32_t)(msg_off[i] - mb[t] + db[t]);
+    if (d.has_recops)
+        for (int t = 0; t < d.n_rtiles; t++)
+            for (uint32_t i = rb[t]; i < rb[t + 1]; i++) {
+                const int tg = d.n_tiles + t;
+                msg_off[c.n_ev + i] = (uint32_t)(msg_off[c.n_ev + i] - mb[tg] + db[tg]);
+            }
+    msg_off[c.n_ev + c.n_re] = (uint32_t)nm;
     std::vector<uint32_t> rc(nm);
     if (nm) HIPCHK(hipMemcpy(rc.data(), d.msg_rcpt, nm * 4, hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < nm; i++) msg_rcpt_obj[i] = w->obj_of_slot[rc[i]];
+    for (int t = 0; t < ntt; t++)
+        for (uint32_t i = 0; i < mc[t]; i++) msg_rcpt_obj[db[t] + i] = w->obj_of_slot[rc[(size_t)mb[t] + i]];
     return NFK_OK;
 }
 

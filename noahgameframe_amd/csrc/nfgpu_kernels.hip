@@ -301,6 +301,8 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
 }
 
 constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
+constexpr int kFanCoopT = 12;
+constexpr int kFanWinBytes = 24576;  // k_tick's dynamic LDS floor when it fans out (6 workgroups per CU)  // k_tick's fan-out: events with more recipients are expanded by the wave
 
 // NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
 // order).  The hot records of a chunk of kinds are loaded together (independent 16 B loads).
@@ -369,11 +371,18 @@ template <int kWPE>
 __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8))) void k_tick(Dev d) {
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
+    __shared__ unsigned s_fan[2];  // the tile's first message, deferred
+    __shared__ uint32_t s_pb[2];   // pl_slot run of the groups with dirty events: [lo, hi)
     extern __shared__ uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     const int tile = blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
-    if (threadIdx.x == 0) s_bytes = 0;
+    const bool fuse = d.fuse_fan && !(d.ablate & (kAblNoFuse | kAblNoEmit));
+    if (threadIdx.x == 0) {
+        s_bytes = 0;
+        s_pb[0] = 0xFFFFFFFFu;
+        s_pb[1] = 0;
+    }
     {
         const int words = d.n_class * (NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS) / 4;
         for (int i = threadIdx.x; i < words; i += kTPB)
@@ -450,6 +459,19 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         }
     const unsigned nd = __builtin_popcount(dm);
     const unsigned nf = __builtin_popcount(fired);
+    if (fuse) {  // the pl_slot run of the groups whose members have messages (they are contiguous)
+        const uint32_t np = (uint32_t)((desc >> 32) & 0x3FFF);
+        uint32_t lo = nmsg ? (uint32_t)desc : 0xFFFFFFFFu, hi = nmsg ? (uint32_t)desc + np : 0u;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, m, 64));
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, m, 64));
+        }
+        if ((threadIdx.x & 63) == 0 && hi) {
+            atomicMin(&s_pb[0], lo);
+            atomicMax(&s_pb[1], hi);
+        }
+    }
 
     // tile-local compaction: one block scan of (fired:16 | events:16 | messages:32)
     unsigned long long tot;
@@ -458,7 +480,17 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     unsigned pev = (unsigned)((excl >> 32) & 0xFFFF);
     unsigned pfi = (unsigned)(excl >> 48);
     unsigned pmsg = (unsigned)excl;
+    const unsigned pev0 = pev, pmsg0 = pmsg, tmsg = (unsigned)tot;
     const size_t ev0 = (size_t)tile * d.ev_tcap, fi0 = (size_t)tile * d.fi_tcap;
+    if (fuse && threadIdx.x == 0) {  // the tile's message range: one atomic per tile
+        const unsigned long long mb = tmsg ? atomicAdd(&d.ctrl->msg_cur[d.par], (unsigned long long)tmsg) : 0ull;
+        const bool defer = mb + tmsg > (unsigned long long)d.msg_cap;
+        s_fan[0] = (unsigned)mb;
+        s_fan[1] = defer;
+        d.msg_base[tile] = (uint32_t)mb;
+        d.t_defer[tile] = defer;
+        if (defer) atomicOr(&d.ctrl->err, kErrMsgCap);
+    }
 
     if (live) {
         // write back the changed values; their events in property-id order
@@ -474,10 +506,10 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                 d.ev_pid[at] = pid;
                 d.ev_old[at] = s_o[j * kTPB + threadIdx.x];
                 d.ev_new[at] = nv;
-                d.ev_moff[at] = pmsg;  // tile-local; k_fanout adds the tile's message base
+                if (!fuse) d.ev_moff[at] = pmsg;  // tile-local; k_fanout adds the tile's message base
                 pmsg += event_msgs(desc, s_pflags[cls][pid]);
                 pev++;
-                bytes += 8 + 28;
+                bytes += 8 + 24;
             }
         }
         uint32_t fl = fired;
@@ -497,6 +529,88 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         d.fired_mask[e] = fired;
         bytes += 4;
     }
+    if (!fuse && !(d.ablate & kAblNoEmit)) bytes += 4 * nd;  // ev_moff
+    // fan-out of the tile's events (GetBroadCastObject, AOI:531-593), see k_fanout
+    if (fuse) {
+        __syncthreads();  // s_fan / s_pb; every read of s_o and s_rem is done: the region is reused
+        const unsigned mb = s_fan[0];
+        const bool defer = s_fan[1];
+        // ev_moff: global (tile-local when deferred: k_fanout converts it when it writes the tile)
+        {
+            unsigned m = pmsg0, at = pev0;
+            if (dm)
+                for (int q = 0; q < d.n_w; q++) {
+                    const uint32_t j = d.u_order[q];
+                    if (!((dm >> j) & 1)) continue;
+                    d.ev_moff[ev0 + at] = defer ? m : mb + m;
+                    m += event_msgs(desc, s_pflags[cls][d.u_pid[j]]);
+                    at++;
+                    bytes += 4;
+                }
+        }
+        if (!defer && tmsg) {
+            uint32_t* s_reg = (uint32_t*)s_o;
+            const unsigned R = (unsigned)d.lds_words;
+            const uint32_t pb_lo = s_pb[0], npl = s_pb[1] > s_pb[0] ? s_pb[1] - s_pb[0] : 0u;
+            const bool staged = npl <= R / 2;
+            const unsigned W = staged ? R - npl : R;  // message window entries
+            uint32_t* s_pl = s_reg + W;
+            if (staged) {
+                for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = (uint32_t)d.pl_slot[pb_lo + i];
+                bytes += 4 * ((npl + kTPB - 1 - threadIdx.x) / kTPB);
+            }
+            bytes += 4 * nmsg;
+            __syncthreads();
+            const int lane = threadIdx.x & 63;
+            for (unsigned w0 = 0; w0 < tmsg; w0 += W) {  // uniform
+                const unsigned w1 = min(tmsg, w0 + W);
+                unsigned m = pmsg0;
+                for (int q = 0; q < d.n_w; q++) {  // uniform: the wave expands big groups together
+                    const uint32_t j = d.u_order[q];
+                    const bool has = (dm >> j) & 1;
+                    uint32_t n = 0, src = 0, r1 = 0;
+                    bool pub = false;
+                    if (has) {
+                        const uint8_t fl = s_pflags[cls][d.u_pid[j]];
+                        n = event_msgs(desc, fl);
+                        pub = fl & NFK_PUBLIC;
+                        src = (uint32_t)desc;
+                        r1 = (uint32_t)((desc >> 46) & 0x3FFF);
+                    }
+                    const bool hit = n && m < w1 && m + n > w0;
+                    if (hit && !pub) {
+                        s_reg[m - w0] = (uint32_t)e;  // private: itself
+                    } else if (hit && n <= (uint32_t)kFanCoopT) {  // every player of the group but self
+                        const uint32_t np = n + (r1 ? 1u : 0u);
+                        uint32_t k = m;
+                        for (uint32_t p = 0; p < np; p++) {
+                            if (p + 1 == r1) continue;
+                            if (k >= w0 && k < w1)
+                                s_reg[k - w0] = staged ? s_pl[src - pb_lo + p] : (uint32_t)d.pl_slot[src + p];
+                            k++;
+                        }
+                    }
+                    unsigned long long big = __ballot(hit && pub && n > (uint32_t)kFanCoopT);
+                    while (big) {
+                        const int L = __builtin_ctzll(big);
+                        big &= big - 1;
+                        const uint32_t bn = __shfl(n, L, 64), bsrc = __shfl(src, L, 64), br1 = __shfl(r1, L, 64);
+                        const uint32_t bm = __shfl(m, L, 64);
+                        for (uint32_t p = lane; p < bn; p += 64) {
+                            const uint32_t k = bm + p;
+                            if (k < w0 || k >= w1) continue;
+                            const uint32_t pp = p + ((br1 && p + 1 >= br1) ? 1u : 0u);  // skip self
+                            s_reg[k - w0] = staged ? s_pl[bsrc - pb_lo + pp] : (uint32_t)d.pl_slot[bsrc + pp];
+                        }
+                    }
+                    m += n;
+                }
+                __syncthreads();
+                for (uint32_t i = threadIdx.x; i < w1 - w0; i += kTPB) d.msg_rcpt[mb + w0 + i] = s_reg[i];
+                if (w1 < tmsg) __syncthreads();
+            }
+        }
+    }
     // tile counts and algorithmic-byte tally
     const unsigned wb = (unsigned)wave_sum(bytes);
     if ((threadIdx.x & 63) == 0) atomicAdd(&s_bytes, wb);
@@ -505,7 +619,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         d.t_ev[tile] = (unsigned)((tot >> 32) & 0xFFFF);
         d.t_fi[tile] = (unsigned)(tot >> 48);
         d.t_msg[tile] = (unsigned)tot;
-        tally_add(d, kTallyTick, (unsigned long long)(s_bytes + 12));
+        tally_add(d, kTallyTick, (unsigned long long)(s_bytes + 12 + (fuse ? 16 : 0)));
     }
 }
 
@@ -826,15 +940,16 @@ __device__ __forceinline__ unsigned long long scan_store(ScanArr& x, const unsig
     return s_pre[kScanTPB / 64];
 }
 
-// One workgroup per count array (blockIdx.x: 0 events, 1 fired, 2 record events, 3 messages).
+// One workgroup per count array (blockIdx.x: 0 events, 1 fired, 2 record events).  Messages
+// need no scan: every tile takes its range from Ctrl::msg_cur (k_tick / k_fanout).
 __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
     __shared__ unsigned long long s_w[kScanTPB / 64 + 1];  // wave totals -> exclusive prefixes, [16] = total
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nrt = d.has_recops ? d.n_rtiles : 0;
     const int a = blockIdx.x;
-    const uint32_t* cnt = a == 0 ? d.t_ev : a == 1 ? d.t_fi : a == 2 ? d.t_re : d.t_msg;
-    uint32_t* base = a == 0 ? d.ev_base : a == 1 ? d.fi_base : a == 2 ? d.re_base : d.msg_base;
-    const int len = a < 2 ? d.n_tiles : a == 2 ? nrt : d.n_tiles + nrt;
+    const uint32_t* cnt = a == 0 ? d.t_ev : a == 1 ? d.t_fi : d.t_re;
+    uint32_t* base = a == 0 ? d.ev_base : a == 1 ? d.fi_base : d.re_base;
+    const int len = a < 2 ? d.n_tiles : nrt;
     unsigned long long carry = 0;
     for (int c0 = 0; c0 < len; c0 += kScanTPB * kScanPer) {
         const int i0 = c0 + tid * kScanPer;
@@ -860,37 +975,41 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
     }
     if (tid == 0) {
         base[len] = (uint32_t)carry;
-        if (a == 0) d.ctrl->n_ev = carry;
+        if (a == 0) {
+            d.ctrl->n_ev = carry;
+            d.ctrl->msg_cur[d.par ^ 1] = 0;  // the next frame's cursor (this frame's is in use)
+        }
         if (a == 1) d.ctrl->n_fi = carry;
         if (a == 2) d.ctrl->n_re = carry;
-        if (a == 3) {
-            d.ctrl->n_msgs = carry;
-            if (carry > (unsigned long long)d.msg_cap) atomicOr(&d.ctrl->err, kErrMsgCap);
-        }
     }
 }
 
 // ---------------------------------------------------------------------------------
 // Fan-out: GetBroadCastObject recipient lists (AOI:531-593) for every dirty event, one workgroup
-// per tile (property tiles, then record tiles), one thread per event.  Slots are in (scene, group,
+// per tile (property tiles, then record tiles; blockIdx.x + blk0 is the tile), one thread per
+// event.  k_tick writes its own tiles' fan-out, so this runs for the record tiles, for property
+// tiles after k_tick_touch, and (only_deferred) for the tiles whose message range did not fit
+// msg_cap, after the host has grown the buffer.  A tile takes its range from Ctrl::msg_cur with
+// one atomic, so each tile's messages are one contiguous run at msg_base[tile].  Slots are in (scene, group,
 // guid) order, so the players of every group the tile touches form one contiguous run of
 // pl_slot; it is staged in LDS when it fits.  A thread writes its event's recipients as one
 // contiguous run (every player of the group but itself, NFGUID order, or itself); events with
 // more than kFanCoop recipients are expanded by their whole wave, 64 recipients per store.
-// Also rewrites each event's tile-local message offset as a global one.  Does nothing (and sets
-// no output) when the frame's messages exceed msg_cap: the host grows the buffer and re-runs it.
-constexpr int kFanLds = 2048, kFanCoop = 12, kFanPer = 4, kFanMsgLds = 6144;
+// Also rewrites each event's tile-local message offset as a global one.  A tile whose range does
+// not fit msg_cap writes nothing and is marked deferred: the host grows the buffer and re-runs it.
+constexpr int kFanLds = 2048, kFanCoop = kFanCoopT, kFanPer = 4, kFanMsgLds = 6144;
 
-__global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
+__global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0, int32_t only_deferred) {
     __shared__ int32_t s_pl[kFanLds];
     __shared__ uint32_t s_msg[kFanMsgLds];  // a pass's recipient runs, stored to HBM coalesced
     __shared__ uint32_t s_pb[2], s_m[2];
     __shared__ unsigned s_bytes;
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
-    if (d.ctrl->n_msgs > (unsigned long long)d.msg_cap) return;  // uniform: host re-runs
-    const bool rec = (int)blockIdx.x >= d.n_tiles;
-    const int t = rec ? (int)blockIdx.x - d.n_tiles : (int)blockIdx.x;
+    const int tg = (int)blockIdx.x + blk0;  // tile: property tiles, then record tiles
+    if (only_deferred && !d.t_defer[tg]) return;  // uniform
+    const bool rec = tg >= d.n_tiles;
+    const int t = rec ? tg - d.n_tiles : tg;
     const uint32_t* base = rec ? d.re_base : d.ev_base;
     const unsigned tcap = (unsigned)(rec ? d.re_tcap : d.ev_tcap);
     const size_t off0 = (size_t)t * tcap;
@@ -899,7 +1018,7 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
     // one round trip: the tile's counts, its message range and (speculatively, inside the tile's
     // staging capacity) the first pass's events
     const uint32_t b0 = base[t], b1 = base[t + 1];
-    const uint32_t mbase = d.msg_base[blockIdx.x], mend = d.msg_base[blockIdx.x + 1];
+    const uint32_t tmsg = d.t_msg[tg];
     uint32_t slot[kFanPer], key[kFanPer], lm[kFanPer];
     uint64_t desc[kFanPer];
 #pragma unroll
@@ -913,7 +1032,24 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
         }
     }
     const unsigned cnt = b1 - b0;
-    if (cnt == 0) return;  // uniform
+    if (threadIdx.x == 0) {  // the tile's message range (kept from the first attempt when deferred)
+        unsigned long long mb;
+        if (only_deferred) {
+            mb = d.msg_base[tg];
+        } else {
+            mb = tmsg ? atomicAdd(&d.ctrl->msg_cur[d.par], (unsigned long long)tmsg) : 0ull;
+            d.msg_base[tg] = (uint32_t)mb;
+        }
+        const bool defer = mb + tmsg > (unsigned long long)d.msg_cap;
+        d.t_defer[tg] = defer;
+        if (defer) atomicOr(&d.ctrl->err, kErrMsgCap);
+        s_pb[0] = (uint32_t)mb;
+        s_pb[1] = defer;
+    }
+    __syncthreads();
+    const uint32_t mbase = s_pb[0];
+    if (cnt == 0 || s_pb[1]) return;  // uniform
+    __syncthreads();  // s_pb is reused below
     if (threadIdx.x == 0) s_bytes = 0;
     if (rec) {
         for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
@@ -952,7 +1088,7 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d) {
             }
             if (i == c_end - 1) s_pb[1] = (uint32_t)desc[q] + (uint32_t)((desc[q] >> 32) & 0x3FFF);
         }
-        if (threadIdx.x == 0) s_m[1] = c_end < cnt ? moff[off0 + c_end] : mend - mbase;
+        if (threadIdx.x == 0) s_m[1] = c_end < cnt ? moff[off0 + c_end] : tmsg;
         __syncthreads();
         const uint32_t p0 = s_m[0], pn = s_m[1] - s_m[0];
         const bool lds_out = pn <= (uint32_t)kFanMsgLds;

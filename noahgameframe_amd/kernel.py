@@ -48,7 +48,7 @@ class Outputs(ctypes.Structure):
                  ("rtile_slots", ctypes.c_int32), ("ev_tile_cap", ctypes.c_int64), ("fi_tile_cap", ctypes.c_int64),
                  ("re_tile_cap", ctypes.c_int64)] +
                 [(n, ctypes.c_void_p) for n in
-                 ["ev_base", "fi_base", "re_base", "msg_base", "ev_slot", "ev_pid", "ev_old", "ev_new", "ev_moff",
+                 ["ev_base", "fi_base", "re_base", "msg_base", "msg_cnt", "ev_slot", "ev_pid", "ev_old", "ev_new", "ev_moff",
                   "re_slot", "re_rrc", "re_old", "re_new", "re_moff", "fi_slot", "fi_kind", "fi_remain",
                   "msg_rcpt", "slot_obj"]])
 
