@@ -138,6 +138,7 @@ struct World {
 
     int32_t ticks = 0;
     int32_t last_par = 0;  // Ctrl::msg_cur parity of the last launched frame
+    int32_t max_np = 0;    // most players in one scene group (an upper bound between full re-layouts)
 
     bool profiling = false;
     std::vector<PendingTiming> pend;
@@ -335,6 +336,7 @@ int seg_meta(World* w, const World::Seg& g, MetaLists& m) {
     int32_t np = 0;
     for (int32_t o : g.objs) np += w->isplayer[o] ? 1 : 0;
     if (np > 0x3FFF) return fail(NFK_ERR_ARG, "more than 16383 players in one scene group");
+    w->max_np = std::max(w->max_np, np);
     const size_t at = m.slot.size();
     int32_t rank = 0;
     for (int32_t i = 0; i < g.cap; i++) {
@@ -439,6 +441,7 @@ int apply_membership(World* w) {
     if (full) {
         int64_t total = plan_segments(w, w->slack, nsegs);
         if (total > d.cap) total = plan_segments(w, 0, nsegs);
+        w->max_np = 0;  // recomputed by seg_meta over every segment below
         if (total > d.cap) return fail(NFK_ERR_CAPACITY, "entity capacity exceeded");
         for (const auto& g : nsegs) {
             for (int32_t i = 0; i < g.cap; i++) {
@@ -882,6 +885,7 @@ int nfk_commit(void* world) {
     const int64_t n_slots = plan_segments(w, w->slack, w->segs);
     for (size_t g = 0; g < w->segs.size(); g++) w->seg_of[{w->segs[g].scene, w->segs[g].group}] = (int32_t)g;
     MetaLists meta;
+    w->max_np = 0;
     for (const auto& g : w->segs) {
         int r = seg_meta(w, g, meta);
         if (r) return r;
@@ -1476,8 +1480,11 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     d.par = w->ticks & 1;
     w->last_par = d.par;
-    // k_tick writes its tiles' fan-out itself (its LDS image doubles as the message window)
-    d.fuse_fan = use_u && !(d.ablate & (kAblNoFuse | kAblNoEmit));
+    // k_tick writes its tiles' fan-out itself (its LDS image doubles as the message window) when
+    // every event's recipient run is short enough for one thread; big groups go to k_fanout,
+    // whose workgroups spread the runs over more waves
+    d.fuse_fan = use_u && !(d.ablate & (kAblNoFuse | kAblNoEmit)) &&
+                 (w->max_np <= kFanCoopT + 1 || (d.ablate & kAblForceFuse));
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
         size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;

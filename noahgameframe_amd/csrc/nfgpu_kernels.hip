@@ -301,8 +301,22 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
 }
 
 constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
-constexpr int kFanCoopT = 12;
-constexpr int kFanWinBytes = 24576;  // k_tick's dynamic LDS floor when it fans out (6 workgroups per CU)  // k_tick's fan-out: events with more recipients are expanded by the wave
+
+// The message range of tile tg (property tiles, then record tiles): one atomic on the frame's
+// cursor by the kernel that counted the tile's messages.  A range that runs past msg_cap is
+// reserved all the same (the cursor ends at the frame's exact total) and the tile is marked
+// deferred: nothing is written there until the host has grown the buffer (k_fanout re-run).
+// Returns the range start; bit 63 set = deferred.
+__device__ __forceinline__ unsigned long long alloc_msgs(const Dev& d, int tg, unsigned tmsg) {
+    const unsigned long long mb = tmsg ? atomicAdd(&d.ctrl->msg_cur[d.par], (unsigned long long)tmsg) : 0ull;
+    const bool defer = mb + tmsg > (unsigned long long)d.msg_cap;
+    d.msg_base[tg] = (uint32_t)mb;
+    d.t_defer[tg] = defer;
+    if (defer) atomicOr(&d.ctrl->err, kErrMsgCap);
+    return mb | ((unsigned long long)defer << 63);
+}
+constexpr int kFanCoopT = 16;  // k_tick's fan-out: events with more recipients are expanded by the wave
+constexpr int kFanWinBytes = 24576;  // k_tick's dynamic LDS floor when it fans out (6 workgroups per CU)
 
 // NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
 // order).  The hot records of a chunk of kinds are loaded together (independent 16 B loads).
@@ -482,14 +496,10 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     unsigned pmsg = (unsigned)excl;
     const unsigned pev0 = pev, pmsg0 = pmsg, tmsg = (unsigned)tot;
     const size_t ev0 = (size_t)tile * d.ev_tcap, fi0 = (size_t)tile * d.fi_tcap;
-    if (fuse && threadIdx.x == 0) {  // the tile's message range: one atomic per tile
-        const unsigned long long mb = tmsg ? atomicAdd(&d.ctrl->msg_cur[d.par], (unsigned long long)tmsg) : 0ull;
-        const bool defer = mb + tmsg > (unsigned long long)d.msg_cap;
+    if (threadIdx.x == 0) {  // the tile's message range (read back only by the fused fan-out)
+        const unsigned long long mb = alloc_msgs(d, tile, tmsg);
         s_fan[0] = (unsigned)mb;
-        s_fan[1] = defer;
-        d.msg_base[tile] = (uint32_t)mb;
-        d.t_defer[tile] = defer;
-        if (defer) atomicOr(&d.ctrl->err, kErrMsgCap);
+        s_fan[1] = (unsigned)(mb >> 63);
     }
 
     if (live) {
@@ -549,18 +559,21 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                 }
         }
         if (!defer && tmsg) {
-            uint32_t* s_reg = (uint32_t*)s_o;
+            // messages are staged in an LDS window and stored coalesced (kAblFanDirect: stored
+            // straight from the per-thread runs, for timing comparisons)
+            const bool direct = d.ablate & kAblFanDirect;
+            uint32_t* s_reg = direct ? d.msg_rcpt + mb : (uint32_t*)s_o;
             const unsigned R = (unsigned)d.lds_words;
             const uint32_t pb_lo = s_pb[0], npl = s_pb[1] > s_pb[0] ? s_pb[1] - s_pb[0] : 0u;
-            const bool staged = npl <= R / 2;
-            const unsigned W = staged ? R - npl : R;  // message window entries
-            uint32_t* s_pl = s_reg + W;
+            const bool staged = !direct && npl <= R / 2;
+            const unsigned W = direct ? tmsg : staged ? R - npl : R;  // message window entries
+            uint32_t* s_pl = (uint32_t*)s_o + W;
             if (staged) {
                 for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = (uint32_t)d.pl_slot[pb_lo + i];
                 bytes += 4 * ((npl + kTPB - 1 - threadIdx.x) / kTPB);
             }
             bytes += 4 * nmsg;
-            __syncthreads();
+            if (staged) __syncthreads();
             const int lane = threadIdx.x & 63;
             for (unsigned w0 = 0; w0 < tmsg; w0 += W) {  // uniform
                 const unsigned w1 = min(tmsg, w0 + W);
@@ -605,9 +618,11 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     }
                     m += n;
                 }
-                __syncthreads();
-                for (uint32_t i = threadIdx.x; i < w1 - w0; i += kTPB) d.msg_rcpt[mb + w0 + i] = s_reg[i];
-                if (w1 < tmsg) __syncthreads();
+                if (!direct) {
+                    __syncthreads();
+                    for (uint32_t i = threadIdx.x; i < w1 - w0; i += kTPB) d.msg_rcpt[mb + w0 + i] = s_reg[i];
+                    if (w1 < tmsg) __syncthreads();
+                }
             }
         }
     }
@@ -766,6 +781,7 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
         d.t_ev[tile] = (unsigned)((tot >> 32) & 0xFFFF);
         d.t_fi[tile] = (unsigned)(tot >> 48);
         d.t_msg[tile] = (unsigned)tot;
+        alloc_msgs(d, tile, (unsigned)tot);
         tally_add(d, kTallyTick, (unsigned long long)(s_bytes + 12));
     }
 }
@@ -901,6 +917,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     if (lane == 0) {
         d.t_re[rt] = pos;
         d.t_msg[d.n_tiles + rt] = pmsg;
+        alloc_msgs(d, d.n_tiles + rt, pmsg);
     }
     const unsigned wb = (unsigned)wave_sum(bytes);
     if (lane == 0 && wb) tally_add(d, kTallyRec, (unsigned long long)wb + 8);
@@ -989,9 +1006,9 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
 // per tile (property tiles, then record tiles; blockIdx.x + blk0 is the tile), one thread per
 // event.  k_tick writes its own tiles' fan-out, so this runs for the record tiles, for property
 // tiles after k_tick_touch, and (only_deferred) for the tiles whose message range did not fit
-// msg_cap, after the host has grown the buffer.  A tile takes its range from Ctrl::msg_cur with
-// one atomic, so each tile's messages are one contiguous run at msg_base[tile].  Slots are in (scene, group,
-// guid) order, so the players of every group the tile touches form one contiguous run of
+// msg_cap, after the host has grown the buffer.  The kernel that counted a tile's messages took
+// its range (alloc_msgs), so each tile's messages are one contiguous run at msg_base[tile].
+// Slots are in (scene, group, guid) order, so the players of every group the tile touches form one contiguous run of
 // pl_slot; it is staged in LDS when it fits.  A thread writes its event's recipients as one
 // contiguous run (every player of the group but itself, NFGUID order, or itself); events with
 // more than kFanCoop recipients are expanded by their whole wave, 64 recipients per store.
@@ -1008,6 +1025,10 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0, int32_t on
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
     const int tg = (int)blockIdx.x + blk0;  // tile: property tiles, then record tiles
     if (only_deferred && !d.t_defer[tg]) return;  // uniform
+    if (only_deferred) {
+        __syncthreads();  // every thread has read the flag
+        if (threadIdx.x == 0) d.t_defer[tg] = 0;
+    }
     const bool rec = tg >= d.n_tiles;
     const int t = rec ? tg - d.n_tiles : tg;
     const uint32_t* base = rec ? d.re_base : d.ev_base;
@@ -1018,7 +1039,7 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0, int32_t on
     // one round trip: the tile's counts, its message range and (speculatively, inside the tile's
     // staging capacity) the first pass's events
     const uint32_t b0 = base[t], b1 = base[t + 1];
-    const uint32_t tmsg = d.t_msg[tg];
+    const uint32_t tmsg = d.t_msg[tg], mbase = d.msg_base[tg], defer = d.t_defer[tg];
     uint32_t slot[kFanPer], key[kFanPer], lm[kFanPer];
     uint64_t desc[kFanPer];
 #pragma unroll
@@ -1032,24 +1053,7 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0, int32_t on
         }
     }
     const unsigned cnt = b1 - b0;
-    if (threadIdx.x == 0) {  // the tile's message range (kept from the first attempt when deferred)
-        unsigned long long mb;
-        if (only_deferred) {
-            mb = d.msg_base[tg];
-        } else {
-            mb = tmsg ? atomicAdd(&d.ctrl->msg_cur[d.par], (unsigned long long)tmsg) : 0ull;
-            d.msg_base[tg] = (uint32_t)mb;
-        }
-        const bool defer = mb + tmsg > (unsigned long long)d.msg_cap;
-        d.t_defer[tg] = defer;
-        if (defer) atomicOr(&d.ctrl->err, kErrMsgCap);
-        s_pb[0] = (uint32_t)mb;
-        s_pb[1] = defer;
-    }
-    __syncthreads();
-    const uint32_t mbase = s_pb[0];
-    if (cnt == 0 || s_pb[1]) return;  // uniform
-    __syncthreads();  // s_pb is reused below
+    if (cnt == 0 || (defer && !only_deferred)) return;  // uniform (a deferred tile waits for the re-run)
     if (threadIdx.x == 0) s_bytes = 0;
     if (rec) {
         for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)

@@ -108,6 +108,20 @@ def test_message_buffer_grows_and_stays_exact(gpu_available):
     compare_runs(run_gpu(w, msg_capacity=1000), run_oracle(w))
 
 
+@pytest.mark.parametrize("variant", [0, 4096, 16384 | 32768, 32768],
+                         ids=["default", "k_fanout", "fused-direct", "fused-always"])
+@pytest.mark.parametrize("cap", [0, 3000], ids=["cap-default", "cap-tiny"])
+def test_fanout_paths_agree(gpu_available, monkeypatch, variant, cap):
+    """Every fan-out path gives the oracle's recipient lists: k_tick's fused tail (LDS window or
+    direct stores), the separate k_fanout, and tiles deferred past msg_capacity and re-run after
+    the buffer grows — with groups small enough for the fused path and one big group."""
+    monkeypatch.setenv("NFGPU_ABLATE", str(variant))
+    for ppg in (8, 40):
+        w = workload.make_world(n_obj=6000, n_scenes=2, groups_per_scene=4, players_per_group=ppg, n_ticks=4,
+                                seed=300 + ppg, ext_frac=0.05)
+        compare_runs(run_gpu(w, msg_capacity=cap), run_oracle(w))
+
+
 def test_device_outputs_and_counters(gpu_available):
     w = workload.make_world(n_obj=5000, n_scenes=1, groups_per_scene=10, players_per_group=4, n_ticks=3, seed=8)
     m = kernel.world_from_workload(w)
@@ -115,7 +129,8 @@ def test_device_outputs_and_counters(gpu_available):
         r = kernel.run_workload(m, w, t)
     s = r["summary"]
     assert s["n_prop_events"] == len(r["ev_obj"]) and s["n_msgs"] == len(r["mr_obj"])
-    assert s["alg_bytes_tick"] > 0 and s["alg_bytes_fan"] > 0
+    # fan-out bytes are tallied by the kernel that writes them (k_tick when it fans out itself)
+    assert s["alg_bytes_tick"] > 0 and s["alg_bytes_fan"] >= 0
     o = m.outputs()
     assert all(o[k] for k in ("ev_slot", "ev_moff", "ev_base", "msg_base", "msg_rcpt", "slot_obj"))
     # slots = members + per-group slack (nfk_config.slack_per_256, default 16 per 256)
