@@ -116,10 +116,12 @@ typedef struct nfk_summary {
  *   record events    (scene, group, guid, rec, row, col); rrc = rec<<16 | row<<8 | col
  *   fired heartbeats (scene, group, guid, kind)
  * Fan-out (GetBroadCastObject recipients): the messages of tile t (property tiles, then record
- * tiles) are one run of msg_cnt[t] recipients at msg_rcpt[msg_base[t]], in event order; tiles
- * take their runs from one atomic cursor, so runs are placed in completion order.  ev_moff /
- * re_moff hold the index in msg_rcpt of the event's first recipient; its recipients end where
- * the next event of its tile begins (msg_base[t] + msg_cnt[t] after the tile's last).
+ * tiles) are one run of msg_cnt[t] recipients at msg_rcpt[msg_base[t]], in event order.  Runs
+ * follow each other in tile order; when the frame's k_tick fanned out its own tiles, property
+ * tile runs start at a fixed stride (msg_base[t] = t x an upper bound of a tile's messages) and
+ * the record tiles' runs follow densely.  ev_moff / re_moff hold the index in msg_rcpt of the
+ * event's first recipient; its recipients end where the next event of its tile begins
+ * (msg_base[t] + msg_cnt[t] after the tile's last).
  * Recipients are slots; slot_obj maps slot -> object index.  nfk_read_fanout returns the dense
  * CSR over [property events ++ record events].
  * nfk_read_* return the same data as dense arrays in object-index terms. */
@@ -130,14 +132,14 @@ typedef struct nfk_outputs {
     const uint32_t* ev_base;   /* [n_tiles + 1]  exclusive scan of per-tile event counts */
     const uint32_t* fi_base;   /* [n_tiles + 1] */
     const uint32_t* re_base;   /* [n_rtiles + 1] */
-    const uint32_t* msg_base;  /* [n_tiles + n_rtiles] first message of each tile */
+    const uint32_t* msg_base;  /* [n_tiles + n_rtiles + 1] first message of each tile */
     const uint32_t* msg_cnt;   /* [n_tiles + n_rtiles] messages of each tile */
     const uint32_t* ev_slot; const uint32_t* ev_pid; const uint64_t* ev_old; const uint64_t* ev_new;
     const uint32_t* ev_moff;
     const uint32_t* re_slot; const uint32_t* re_rrc; const uint64_t* re_old; const uint64_t* re_new;
     const uint32_t* re_moff;
     const uint32_t* fi_slot; const uint32_t* fi_kind; const int32_t* fi_remain;
-    const uint32_t* msg_rcpt; /* [n_msgs], one run per tile */
+    const uint32_t* msg_rcpt; /* one run per tile (see above) */
     const int32_t* slot_obj;  /* slot -> object index */
 } nfk_outputs;
 

@@ -15,13 +15,12 @@ constexpr int kRTile = 64;    // slots per record-event tile (one k_records wave
 constexpr unsigned kErrMsgCap = 4, kErrTouch = 8;
 
 // Control block: frame totals written by k_scan_tiles, byte tallies accumulated across frames,
-// the error word is sticky until nfk_summary_get clears it.  msg_cur[par] is the frame's message
-// cursor: every tile takes its message range from it with one atomicAdd (so its final value is
-// the frame's message count); k_scan_tiles clears the other parity's cursor for the next frame.
+// the error word is sticky until nfk_summary_get clears it.  msg_extent = end of the last tile's
+// message run (= n_msgs unless k_tick's fan-out placed property tiles at a fixed stride).
 struct alignas(64) Ctrl {
     unsigned err, pad_u[3];                                             // 16 B
     unsigned long long n_ev, n_fi, n_re, n_msgs;                        // 32 B
-    unsigned long long msg_cur[2];                                      // 16 B
+    unsigned long long msg_extent, n_msgs_ptiles;                       // 16 B
     unsigned long long bytes_tick, bytes_rec, bytes_fan, pad2;          // accumulated across frames
 };
 
@@ -167,10 +166,11 @@ struct Dev {
     uint32_t* ev_base; // [n_tiles + 1] exclusive scans (k_scan_tiles)
     uint32_t* fi_base; // [n_tiles + 1]
     uint32_t* re_base; // [n_rtiles + 1]
-    uint32_t* msg_base;// [n_tiles + n_rtiles] first message of each tile (taken from Ctrl::msg_cur)
-    uint32_t* t_defer; // [n_tiles + n_rtiles] 1: the tile's range did not fit msg_cap, not yet written
-    int32_t par;       // frame parity: Ctrl::msg_cur[par] is this frame's cursor
-    int32_t fuse_fan;  // k_tick writes its tile's fan-out itself
+    uint32_t* msg_base;// [n_tiles + n_rtiles + 1] first message of each tile (k_scan_tiles)
+    // msg_tcap > 0: k_tick writes its tile's fan-out itself, property tile t's messages at
+    // t * msg_tcap (an upper bound of one tile's messages this frame); record tiles follow densely
+    uint32_t msg_tcap;
+    int32_t fuse_fan;
     int32_t lds_words; // k_tick's dynamic LDS in 4-byte words (message window + staged players)
     // outputs (tile-staged)
     uint32_t* ev_slot; uint32_t* ev_pid; uint64_t* ev_old; uint64_t* ev_new; uint32_t* ev_moff;

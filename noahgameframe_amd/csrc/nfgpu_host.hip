@@ -137,7 +137,8 @@ struct World {
     size_t stage_cap = 0;
 
     int32_t ticks = 0;
-    int32_t last_par = 0;  // Ctrl::msg_cur parity of the last launched frame
+    uint32_t last_tcap = 0;  // Dev::msg_tcap of the last launched frame
+    int64_t last_rec_msgs = 0;  // record-tile messages of the last summarised frame (capacity hint)
     int32_t max_np = 0;    // most players in one scene group (an upper bound between full re-layouts)
 
     bool profiling = false;
@@ -963,7 +964,6 @@ int nfk_commit(void* world) {
     ALLOC(d.fi_base, (nt + 1) * 4);
     ALLOC(d.re_base, (nrt + 1) * 4);
     ALLOC(d.msg_base, (nt + nrt + 1) * 4);
-    ALLOC(d.t_defer, (nt + nrt) * 4);
     d.msg_cap = w->cfg.msg_capacity > 0 ? w->cfg.msg_capacity : (int64_t)cap * 32;
     if (d.msg_cap > 0xFFFFFFFFll) return fail(NFK_ERR_ARG, "msg_capacity must fit 32-bit offsets");
     ALLOC(d.ev_slot, ev_n * 4);
@@ -1057,7 +1057,6 @@ int nfk_commit(void* world) {
     HIPCHK(hipMemset(d.fi_base, 0, (nt + 1) * 4));
     HIPCHK(hipMemset(d.re_base, 0, (nrt + 1) * 4));
     HIPCHK(hipMemset(d.msg_base, 0, (nt + nrt + 1) * 4));
-    HIPCHK(hipMemset(d.t_defer, 0, (nt + nrt) * 4));
     // creation-time values are now on the device
     for (auto& v : w->init_props) std::vector<uint64_t>().swap(v);
     for (auto& v : w->init_rcells) std::vector<uint64_t>().swap(v);
@@ -1478,13 +1477,33 @@ int nfk_execute(void* world, int64_t now_ms) {
                                d.e_flags, d.s_hot, d.n_kind, d.cap);
         HIPCHK(hipGetLastError());
     }
-    d.par = w->ticks & 1;
-    w->last_par = d.par;
     // k_tick writes its tiles' fan-out itself (its LDS image doubles as the message window) when
-    // every event's recipient run is short enough for one thread; big groups go to k_fanout,
-    // whose workgroups spread the runs over more waves
-    d.fuse_fan = use_u && !(d.ablate & (kAblNoFuse | kAblNoEmit)) &&
-                 (w->max_np <= kFanCoopT + 1 || (d.ablate & kAblForceFuse));
+    // every event's recipient run is short enough for one thread (big groups go to k_fanout, whose
+    // workgroups spread the runs over more waves).  Property tile t's messages then sit at
+    // t * msg_tcap, msg_tcap = writable properties x slots x most recipients of one event: no
+    // tile waits for another tile's count.
+    d.msg_tcap = 0;
+    if (use_u && d.n_tiles && !(d.ablate & (kAblNoFuse | kAblNoEmit)) &&
+        (w->max_np <= kFanCoopT + 1 || (d.ablate & kAblForceFuse))) {
+        const int64_t tcap = (int64_t)std::max(d.n_w, 1) * kTile * std::max(w->max_np, 1);
+        const int64_t need = tcap * d.n_tiles + w->last_rec_msgs + w->last_rec_msgs / 4 + 1024;
+        if (tcap * d.n_tiles <= kMsgStrideLimit) {
+            if (need > w->d.msg_cap) {  // grow before the frame (the previous frame's messages are dropped)
+                HIPCHK(hipStreamSynchronize(w->stream));
+                HIPCHK(hipFree(w->d.msg_rcpt));
+                w->allocs.erase(std::remove(w->allocs.begin(), w->allocs.end(), (void*)w->d.msg_rcpt),
+                                w->allocs.end());
+                int r = alloc_track(w, (void**)&w->d.msg_rcpt, (size_t)need * 4);
+                if (r) return r;
+                w->d.msg_cap = need;
+                d.msg_rcpt = w->d.msg_rcpt;
+                d.msg_cap = need;
+            }
+            d.msg_tcap = (uint32_t)tcap;
+        }
+    }
+    d.fuse_fan = d.msg_tcap != 0;
+    w->last_tcap = d.msg_tcap;
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
         size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;
@@ -1515,7 +1534,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     {
         TimeScope ts(w, KT_SCAN);
-        hipLaunchKernelGGL(k_scan_tiles, dim3(3), dim3(kScanTPB), 0, w->stream, d);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(5), dim3(kScanTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
     // the tiles k_tick did not fan out: record tiles, and property tiles after k_tick_touch
@@ -1523,7 +1542,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0) - fan0;
     if (nfan > 0 && !(d.ablate & kAblNoEmit)) {  // (timing ablation: events were not written)
         TimeScope ts(w, KT_FAN);
-        hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, (int32_t)fan0, 0);
+        hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, (int32_t)fan0);
         HIPCHK(hipGetLastError());
     }
     w->ticks++;
@@ -1535,6 +1554,12 @@ int nfk_sync(void* world) {
     if (!w) return fail(NFK_ERR_ARG, "null world");
     HIPCHK(hipStreamSynchronize(w->stream));
     return NFK_OK;
+}
+
+// messages of the last frame: the runs are dense unless k_tick placed property tiles at a stride
+static int64_t frame_msgs(const World* w, const Ctrl& c) {
+    if (!w->last_tcap) return (int64_t)c.msg_extent;
+    return (int64_t)c.n_msgs_ptiles + (int64_t)c.msg_extent - (int64_t)w->last_tcap * w->d.n_tiles;
 }
 
 int nfk_summary_get(void* world, nfk_summary* out) {
@@ -1553,7 +1578,7 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     out->n_prop_events = (int64_t)c.n_ev;
     out->n_rec_events = (int64_t)c.n_re;
     out->n_fired = (int64_t)c.n_fi;
-    out->n_msgs = (int64_t)c.msg_cur[w->last_par];
+    out->n_msgs = frame_msgs(w, c);
     {
         uint64_t tb[3];
         int r = read_tallies(w, tb);
@@ -1564,29 +1589,31 @@ int nfk_summary_get(void* world, nfk_summary* out) {
         for (int k = 0; k < 3; k++) w->last_bytes[k] = tb[k];
     }
     if ((c.err & kErrMsgCap) && !(c.err & ~kErrMsgCap)) {
-        // The tiles whose message range ran past msg_cap wrote no messages and are marked in
-        // t_defer; their ranges are reserved (the cursor holds the frame's exact total).  Grow
-        // the buffer, keeping what the other tiles wrote, and fan the deferred tiles out.
-        const int64_t total = (int64_t)c.msg_cur[w->last_par];
-        const int64_t need = total + total / 4 + 1024;
+        // k_fanout wrote nothing (it checks the scanned extent first) and only reads the event
+        // tiles and the membership CSR, so grow the message buffer (keeping what k_tick's own
+        // fan-out wrote) and re-run it for this frame.
+        const int64_t extent = (int64_t)c.msg_extent;
+        const int64_t need = extent + extent / 4 + 1024;
         if (need > 0xFFFFFFFFll) return fail(NFK_ERR_CAPACITY, "fan-out exceeds 2^32 messages per frame");
         uint32_t* grown = nullptr;
         int r = alloc_track(w, (void**)&grown, (size_t)need * 4);
         if (r) return r;
-        HIPCHK(hipMemcpy(grown, w->d.msg_rcpt, (size_t)w->d.msg_cap * 4, hipMemcpyDeviceToDevice));
+        if (w->last_tcap)
+            HIPCHK(hipMemcpy(grown, w->d.msg_rcpt, (size_t)w->last_tcap * w->d.n_tiles * 4, hipMemcpyDeviceToDevice));
         HIPCHK(hipFree(w->d.msg_rcpt));
         w->allocs.erase(std::remove(w->allocs.begin(), w->allocs.end(), (void*)w->d.msg_rcpt), w->allocs.end());
         w->d.msg_rcpt = grown;
         w->d.msg_cap = need;
         HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
         Dev d = w->d;
-        d.par = w->last_par;
-        const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0);
-        hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, 0, 1);
+        const int fan0 = w->last_tcap ? d.n_tiles : 0;
+        const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0) - fan0;
+        if (nfan > 0) hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, (int32_t)fan0);
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(w->stream));
         HIPCHK(hipMemcpy(&c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
     }
+    w->last_rec_msgs = frame_msgs(w, c) - (int64_t)c.n_msgs_ptiles;
     out->device_error = (int32_t)c.err;
     out->tick = w->ticks;
     if (c.err) HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
@@ -1735,9 +1762,9 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
     Ctrl c;
     int r = read_ctrl(w, &c);
     if (r) return r;
-    if (c.err & kErrMsgCap) return fail(NFK_ERR_CAPACITY, "call nfk_summary_get first");
+    if (c.msg_extent > (unsigned long long)w->d.msg_cap) return fail(NFK_ERR_CAPACITY, "call nfk_summary_get first");
     const Dev& d = w->d;
-    const size_t nm = c.msg_cur[w->last_par];
+    const size_t nm = (size_t)frame_msgs(w, c);
     // each tile's messages are one run at msg_base[tile]; the dense CSR walks tiles in order
     const int ntt = d.n_tiles + (d.has_recops ? d.n_rtiles : 0);
     std::vector<uint32_t> mb(ntt), mc(ntt), eb(d.n_tiles + 1), rb(d.n_rtiles + 1);

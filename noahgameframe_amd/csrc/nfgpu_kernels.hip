@@ -302,21 +302,9 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
 
 constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
 
-// The message range of tile tg (property tiles, then record tiles): one atomic on the frame's
-// cursor by the kernel that counted the tile's messages.  A range that runs past msg_cap is
-// reserved all the same (the cursor ends at the frame's exact total) and the tile is marked
-// deferred: nothing is written there until the host has grown the buffer (k_fanout re-run).
-// Returns the range start; bit 63 set = deferred.
-__device__ __forceinline__ unsigned long long alloc_msgs(const Dev& d, int tg, unsigned tmsg) {
-    const unsigned long long mb = tmsg ? atomicAdd(&d.ctrl->msg_cur[d.par], (unsigned long long)tmsg) : 0ull;
-    const bool defer = mb + tmsg > (unsigned long long)d.msg_cap;
-    d.msg_base[tg] = (uint32_t)mb;
-    d.t_defer[tg] = defer;
-    if (defer) atomicOr(&d.ctrl->err, kErrMsgCap);
-    return mb | ((unsigned long long)defer << 63);
-}
 constexpr int kFanCoopT = 16;  // k_tick's fan-out: events with more recipients are expanded by the wave
 constexpr int kFanWinBytes = 24576;  // k_tick's dynamic LDS floor when it fans out (6 workgroups per CU)
+constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: at most 4 GiB reserved
 
 // NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
 // order).  The hot records of a chunk of kinds are loaded together (independent 16 B loads).
@@ -385,13 +373,12 @@ template <int kWPE>
 __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8))) void k_tick(Dev d) {
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
-    __shared__ unsigned s_fan[2];  // the tile's first message, deferred
     __shared__ uint32_t s_pb[2];   // pl_slot run of the groups with dirty events: [lo, hi)
     extern __shared__ uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     const int tile = blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
-    const bool fuse = d.fuse_fan && !(d.ablate & (kAblNoFuse | kAblNoEmit));
+    const bool fuse = d.msg_tcap != 0;  // this tile's fan-out is written here, at tile * msg_tcap
     if (threadIdx.x == 0) {
         s_bytes = 0;
         s_pb[0] = 0xFFFFFFFFu;
@@ -496,11 +483,6 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     unsigned pmsg = (unsigned)excl;
     const unsigned pev0 = pev, pmsg0 = pmsg, tmsg = (unsigned)tot;
     const size_t ev0 = (size_t)tile * d.ev_tcap, fi0 = (size_t)tile * d.fi_tcap;
-    if (threadIdx.x == 0) {  // the tile's message range (read back only by the fused fan-out)
-        const unsigned long long mb = alloc_msgs(d, tile, tmsg);
-        s_fan[0] = (unsigned)mb;
-        s_fan[1] = (unsigned)(mb >> 63);
-    }
 
     if (live) {
         // write back the changed values; their events in property-id order
@@ -542,23 +524,21 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     if (!fuse && !(d.ablate & kAblNoEmit)) bytes += 4 * nd;  // ev_moff
     // fan-out of the tile's events (GetBroadCastObject, AOI:531-593), see k_fanout
     if (fuse) {
-        __syncthreads();  // s_fan / s_pb; every read of s_o and s_rem is done: the region is reused
-        const unsigned mb = s_fan[0];
-        const bool defer = s_fan[1];
-        // ev_moff: global (tile-local when deferred: k_fanout converts it when it writes the tile)
+        __syncthreads();  // s_pb; every read of s_o and s_rem is done: the region is reused
+        const unsigned mb = (unsigned)tile * d.msg_tcap;
         {
             unsigned m = pmsg0, at = pev0;
             if (dm)
                 for (int q = 0; q < d.n_w; q++) {
                     const uint32_t j = d.u_order[q];
                     if (!((dm >> j) & 1)) continue;
-                    d.ev_moff[ev0 + at] = defer ? m : mb + m;
+                    d.ev_moff[ev0 + at] = mb + m;
                     m += event_msgs(desc, s_pflags[cls][d.u_pid[j]]);
                     at++;
                     bytes += 4;
                 }
         }
-        if (!defer && tmsg) {
+        if (tmsg) {
             // messages are staged in an LDS window and stored coalesced (kAblFanDirect: stored
             // straight from the per-thread runs, for timing comparisons)
             const bool direct = d.ablate & kAblFanDirect;
@@ -781,7 +761,6 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
         d.t_ev[tile] = (unsigned)((tot >> 32) & 0xFFFF);
         d.t_fi[tile] = (unsigned)(tot >> 48);
         d.t_msg[tile] = (unsigned)tot;
-        alloc_msgs(d, tile, (unsigned)tot);
         tally_add(d, kTallyTick, (unsigned long long)(s_bytes + 12));
     }
 }
@@ -917,7 +896,6 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     if (lane == 0) {
         d.t_re[rt] = pos;
         d.t_msg[d.n_tiles + rt] = pmsg;
-        alloc_msgs(d, d.n_tiles + rt, pmsg);
     }
     const unsigned wb = (unsigned)wave_sum(bytes);
     if (lane == 0 && wb) tally_add(d, kTallyRec, (unsigned long long)wb + 8);
@@ -957,21 +935,45 @@ __device__ __forceinline__ unsigned long long scan_store(ScanArr& x, const unsig
     return s_pre[kScanTPB / 64];
 }
 
-// One workgroup per count array (blockIdx.x: 0 events, 1 fired, 2 record events).  Messages
-// need no scan: every tile takes its range from Ctrl::msg_cur (k_tick / k_fanout).
+// One workgroup per count array (blockIdx.x: 0 events, 1 fired, 2 record events, 3 message runs,
+// 4 the property tiles' messages when k_tick fanned them out at a fixed stride).
 __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
     __shared__ unsigned long long s_w[kScanTPB / 64 + 1];  // wave totals -> exclusive prefixes, [16] = total
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nrt = d.has_recops ? d.n_rtiles : 0;
     const int a = blockIdx.x;
-    const uint32_t* cnt = a == 0 ? d.t_ev : a == 1 ? d.t_fi : d.t_re;
-    uint32_t* base = a == 0 ? d.ev_base : a == 1 ? d.fi_base : d.re_base;
-    const int len = a < 2 ? d.n_tiles : nrt;
+    if (a == 4) {  // sum of the property tiles' message counts
+        unsigned long long v = 0;
+        if (d.msg_tcap)
+            for (int i = tid; i < d.n_tiles; i += kScanTPB) v += d.t_msg[i];
+        v = wave_sum(v);
+        if (lane == 0) s_w[w] = v;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long t = 0;
+            for (int i = 0; i < kScanTPB / 64; i++) t += s_w[i];
+            d.ctrl->n_msgs_ptiles = t;
+        }
+        return;
+    }
+    const uint32_t* cnt = a == 0 ? d.t_ev : a == 1 ? d.t_fi : a == 2 ? d.t_re : d.t_msg;
+    uint32_t* base = a == 0 ? d.ev_base : a == 1 ? d.fi_base : a == 2 ? d.re_base : d.msg_base;
+    const int len = a < 2 ? d.n_tiles : a == 2 ? nrt : d.n_tiles + nrt;
+    // message runs: property tiles fanned out by k_tick take msg_tcap each
+    const int fixed = (a == 3 && d.msg_tcap) ? d.n_tiles : 0;
     unsigned long long carry = 0;
     for (int c0 = 0; c0 < len; c0 += kScanTPB * kScanPer) {
         const int i0 = c0 + tid * kScanPer;
         ScanArr x;
         scan_load(x, cnt, len, i0);
+        if (fixed) {
+            x.sum = 0;
+#pragma unroll
+            for (int q = 0; q < kScanPer; q++) {
+                if (i0 + q < fixed) x.v[q] = d.msg_tcap;
+                x.sum += x.v[q];
+            }
+        }
         x.inc = wave_incl_scan(x.sum);
         if (lane == 63) s_w[w] = x.inc;
         __syncthreads();
@@ -992,43 +994,38 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
     }
     if (tid == 0) {
         base[len] = (uint32_t)carry;
-        if (a == 0) {
-            d.ctrl->n_ev = carry;
-            d.ctrl->msg_cur[d.par ^ 1] = 0;  // the next frame's cursor (this frame's is in use)
-        }
+        if (a == 0) d.ctrl->n_ev = carry;
         if (a == 1) d.ctrl->n_fi = carry;
         if (a == 2) d.ctrl->n_re = carry;
+        if (a == 3) {
+            d.ctrl->msg_extent = carry;
+            if (carry > (unsigned long long)d.msg_cap) atomicOr(&d.ctrl->err, kErrMsgCap);
+        }
     }
 }
 
 // ---------------------------------------------------------------------------------
 // Fan-out: GetBroadCastObject recipient lists (AOI:531-593) for every dirty event, one workgroup
 // per tile (property tiles, then record tiles; blockIdx.x + blk0 is the tile), one thread per
-// event.  k_tick writes its own tiles' fan-out, so this runs for the record tiles, for property
-// tiles after k_tick_touch, and (only_deferred) for the tiles whose message range did not fit
-// msg_cap, after the host has grown the buffer.  The kernel that counted a tile's messages took
-// its range (alloc_msgs), so each tile's messages are one contiguous run at msg_base[tile].
+// event.  When k_tick writes its own tiles' fan-out this runs for the record tiles only.  Each
+// tile's messages are one contiguous run at msg_base[tile] (k_scan_tiles).
 // Slots are in (scene, group, guid) order, so the players of every group the tile touches form one contiguous run of
 // pl_slot; it is staged in LDS when it fits.  A thread writes its event's recipients as one
 // contiguous run (every player of the group but itself, NFGUID order, or itself); events with
 // more than kFanCoop recipients are expanded by their whole wave, 64 recipients per store.
-// Also rewrites each event's tile-local message offset as a global one.  A tile whose range does
-// not fit msg_cap writes nothing and is marked deferred: the host grows the buffer and re-runs it.
+// Also rewrites each event's tile-local message offset as a global one.  Does nothing (and sets
+// no output) when the frame's message runs exceed msg_cap: the host grows the buffer and re-runs it.
 constexpr int kFanLds = 2048, kFanCoop = kFanCoopT, kFanPer = 4, kFanMsgLds = 6144;
 
-__global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0, int32_t only_deferred) {
+__global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
     __shared__ int32_t s_pl[kFanLds];
     __shared__ uint32_t s_msg[kFanMsgLds];  // a pass's recipient runs, stored to HBM coalesced
     __shared__ uint32_t s_pb[2], s_m[2];
     __shared__ unsigned s_bytes;
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
+    if (d.ctrl->msg_extent > (unsigned long long)d.msg_cap) return;  // uniform: host re-runs
     const int tg = (int)blockIdx.x + blk0;  // tile: property tiles, then record tiles
-    if (only_deferred && !d.t_defer[tg]) return;  // uniform
-    if (only_deferred) {
-        __syncthreads();  // every thread has read the flag
-        if (threadIdx.x == 0) d.t_defer[tg] = 0;
-    }
     const bool rec = tg >= d.n_tiles;
     const int t = rec ? tg - d.n_tiles : tg;
     const uint32_t* base = rec ? d.re_base : d.ev_base;
@@ -1039,7 +1036,7 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0, int32_t on
     // one round trip: the tile's counts, its message range and (speculatively, inside the tile's
     // staging capacity) the first pass's events
     const uint32_t b0 = base[t], b1 = base[t + 1];
-    const uint32_t tmsg = d.t_msg[tg], mbase = d.msg_base[tg], defer = d.t_defer[tg];
+    const uint32_t tmsg = d.t_msg[tg], mbase = d.msg_base[tg];
     uint32_t slot[kFanPer], key[kFanPer], lm[kFanPer];
     uint64_t desc[kFanPer];
 #pragma unroll
@@ -1053,7 +1050,7 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0, int32_t on
         }
     }
     const unsigned cnt = b1 - b0;
-    if (cnt == 0 || (defer && !only_deferred)) return;  // uniform (a deferred tile waits for the re-run)
+    if (cnt == 0) return;  // uniform
     if (threadIdx.x == 0) s_bytes = 0;
     if (rec) {
         for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
