@@ -12,7 +12,7 @@ constexpr int kTile = 256;    // slots per property/fired tile (one k_tick workg
 constexpr int kRTile = 64;    // slots per record-event tile (one k_records wave)
 
 // device error word bits (Ctrl::err)
-constexpr unsigned kErrMsgCap = 4, kErrTouch = 8;
+constexpr unsigned kErrMsgCap = 4, kErrTouch = 8, kErrFanBound = 16;
 
 // Control block: frame totals written by k_scan_tiles, byte tallies accumulated across frames,
 // the error word is sticky until nfk_summary_get clears it.  msg_extent = end of the last tile's

@@ -1618,6 +1618,7 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     out->tick = w->ticks;
     if (c.err) HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
     if (c.err & kErrTouch) return fail(NFK_ERR_TOUCH, "device touch list overflow");
+    if (c.err & kErrFanBound) return fail(NFK_ERR_STATE, "a tile's fan-out exceeded its bound");
     if (c.err & kErrMsgCap)
         return fail(NFK_ERR_CAPACITY, "device output capacity exceeded (err=" + std::to_string(c.err) + ")");
     return NFK_OK;
@@ -1792,8 +1793,10 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
                 msg_off[c.n_ev + i] = (uint32_t)(msg_off[c.n_ev + i] - mb[tg] + db[tg]);
             }
     msg_off[c.n_ev + c.n_re] = (uint32_t)nm;
-    std::vector<uint32_t> rc(nm);
-    if (nm) HIPCHK(hipMemcpy(rc.data(), d.msg_rcpt, nm * 4, hipMemcpyDeviceToHost));
+    // the runs cover [0, extent) with gaps when property tiles sit at a stride
+    const size_t ext = (size_t)c.msg_extent;
+    std::vector<uint32_t> rc(ext);
+    if (ext) HIPCHK(hipMemcpy(rc.data(), d.msg_rcpt, ext * 4, hipMemcpyDeviceToHost));
     for (int t = 0; t < ntt; t++)
         for (uint32_t i = 0; i < mc[t]; i++) msg_rcpt_obj[db[t] + i] = w->obj_of_slot[rc[(size_t)mb[t] + i]];
     return NFK_OK;

@@ -538,7 +538,9 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     bytes += 4;
                 }
         }
-        if (tmsg) {
+        if (tmsg > d.msg_tcap) {  // cannot happen (host bound); never write past the tile's run
+            if (threadIdx.x == 0) atomicOr(&d.ctrl->err, kErrFanBound);
+        } else if (tmsg) {
             // messages are staged in an LDS window and stored coalesced (kAblFanDirect: stored
             // straight from the per-thread runs, for timing comparisons)
             const bool direct = d.ablate & kAblFanDirect;
