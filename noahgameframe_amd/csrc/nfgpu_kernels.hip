@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
     __shared__ uint32_t s_pb[2];   // pl_slot run of the groups with dirty events: [lo, hi)
-    extern __shared__ uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
+    extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     const int tile = blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
@@ -548,7 +548,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             const unsigned R = (unsigned)d.lds_words;
             const uint32_t pb_lo = s_pb[0], npl = s_pb[1] > s_pb[0] ? s_pb[1] - s_pb[0] : 0u;
             const bool staged = !direct && npl <= R / 2;
-            const unsigned W = direct ? tmsg : staged ? R - npl : R;  // message window entries
+            const unsigned W = direct ? tmsg : staged ? (R - npl) & ~3u : R;  // window entries (16 B multiple)
             uint32_t* s_pl = (uint32_t*)s_o + W;
             if (staged) {
                 for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = (uint32_t)d.pl_slot[pb_lo + i];
@@ -602,7 +602,12 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                 }
                 if (!direct) {
                     __syncthreads();
-                    for (uint32_t i = threadIdx.x; i < w1 - w0; i += kTPB) d.msg_rcpt[mb + w0 + i] = s_reg[i];
+                    // mb and w0 are multiples of 4 (msg_tcap and W are): 16-byte stores
+                    const uint32_t n = w1 - w0, n4 = n >> 2;
+                    uint4* dst4 = (uint4*)(d.msg_rcpt + mb + w0);
+                    const uint4* src4 = (const uint4*)s_reg;
+                    for (uint32_t i = threadIdx.x; i < n4; i += kTPB) dst4[i] = src4[i];
+                    if (threadIdx.x < (n & 3u)) d.msg_rcpt[mb + w0 + 4 * n4 + threadIdx.x] = s_reg[4 * n4 + threadIdx.x];
                     if (w1 < tmsg) __syncthreads();
                 }
             }
