@@ -53,7 +53,6 @@ constexpr unsigned kAblPrograms = 4;
 constexpr unsigned kAblPerKind = 8;  // not an ablation: force the per-kind operand path (outputs stay exact)
 constexpr unsigned kAblWaves6 = 16, kAblWaves8 = 32;  // k_tick register budgets (outputs stay exact)
 constexpr unsigned kAblWaves5 = 8192;                  // (6 is the default)
-constexpr unsigned kAblFanDirect = 16384;  // k_tick's fan-out without the LDS message window (outputs stay exact)
 constexpr unsigned kAblForceFuse = 32768;  // k_tick fans out whatever the group sizes (outputs stay exact)
 constexpr unsigned kAblFanExpand = 64, kAblFanCopy = 128;  // timing only: k_fanout without expansion / copy-out
 constexpr unsigned kAblNoRun = 512, kAblNoLoads = 1024, kAblNoEmit = 2048;  // timing only (k_tick)

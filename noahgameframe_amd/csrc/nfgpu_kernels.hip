@@ -522,11 +522,18 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         bytes += 4;
     }
     if (!fuse && !(d.ablate & kAblNoEmit)) bytes += 4 * nd;  // ev_moff
-    // fan-out of the tile's events (GetBroadCastObject, AOI:531-593), see k_fanout
+    // Fan-out of the tile's events (GetBroadCastObject, AOI:531-593; see k_fanout), at the tile's
+    // fixed-stride run mb.  The LDS region of the frame-start image is reused: a chunk of the
+    // tile's events as (first message, first player | slot, count | rank | public) triples, the
+    // groups' player run, and a message window.  Every thread takes whole events of the chunk, so
+    // the lanes stay busy whichever entities the events belong to; the window is stored coalesced.
     if (fuse) {
         __syncthreads();  // s_pb; every read of s_o and s_rem is done: the region is reused
         const unsigned mb = (unsigned)tile * d.msg_tcap;
-        {
+        const unsigned tev = (unsigned)((tot >> 32) & 0xFFFF);
+        const bool fan = tmsg && tmsg <= d.msg_tcap;
+        if (tmsg > d.msg_tcap && threadIdx.x == 0) atomicOr(&d.ctrl->err, kErrFanBound);  // (host bound)
+        if (!fan) {  // ev_moff only
             unsigned m = pmsg0, at = pev0;
             if (dm)
                 for (int q = 0; q < d.n_w; q++) {
@@ -537,79 +544,78 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     at++;
                     bytes += 4;
                 }
-        }
-        if (tmsg > d.msg_tcap) {  // cannot happen (host bound); never write past the tile's run
-            if (threadIdx.x == 0) atomicOr(&d.ctrl->err, kErrFanBound);
-        } else if (tmsg) {
-            // messages are staged in an LDS window and stored coalesced (kAblFanDirect: stored
-            // straight from the per-thread runs, for timing comparisons)
-            const bool direct = d.ablate & kAblFanDirect;
-            uint32_t* s_reg = direct ? d.msg_rcpt + mb : (uint32_t*)s_o;
+        } else {
             const unsigned R = (unsigned)d.lds_words;
             const uint32_t pb_lo = s_pb[0], npl = s_pb[1] > s_pb[0] ? s_pb[1] - s_pb[0] : 0u;
-            const bool staged = !direct && npl <= R / 2;
-            const unsigned W = direct ? tmsg : staged ? (R - npl) & ~3u : R;  // window entries (16 B multiple)
-            uint32_t* s_pl = (uint32_t*)s_o + W;
+            const bool staged = npl <= R / 4;
+            const unsigned ecap = min((tev + 3u) & ~3u, (R / 6u) & ~3u);  // events per chunk
+            const unsigned W = (R - 3u * ecap - (staged ? npl : 0u)) & ~3u;  // window entries
+            uint32_t* s_ev = (uint32_t*)s_o;
+            uint32_t* s_win = s_ev + 3u * ecap;
+            uint32_t* s_pl = s_win + W;
             if (staged) {
                 for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = (uint32_t)d.pl_slot[pb_lo + i];
                 bytes += 4 * ((npl + kTPB - 1 - threadIdx.x) / kTPB);
             }
             bytes += 4 * nmsg;
-            if (staged) __syncthreads();
-            const int lane = threadIdx.x & 63;
-            for (unsigned w0 = 0; w0 < tmsg; w0 += W) {  // uniform
-                const unsigned w1 = min(tmsg, w0 + W);
-                unsigned m = pmsg0;
-                for (int q = 0; q < d.n_w; q++) {  // uniform: the wave expands big groups together
-                    const uint32_t j = d.u_order[q];
-                    const bool has = (dm >> j) & 1;
-                    uint32_t n = 0, src = 0, r1 = 0;
-                    bool pub = false;
-                    if (has) {
+            for (unsigned c0 = 0; c0 < tev; c0 += ecap) {  // uniform
+                const unsigned c1 = min(tev, c0 + ecap);
+                if (dm && pev0 < c1 && pev0 + nd > c0) {  // this thread's events of the chunk
+                    unsigned m = pmsg0, at = pev0;
+                    for (int q = 0; q < d.n_w; q++) {
+                        const uint32_t j = d.u_order[q];
+                        if (!((dm >> j) & 1)) continue;
                         const uint8_t fl = s_pflags[cls][d.u_pid[j]];
-                        n = event_msgs(desc, fl);
-                        pub = fl & NFK_PUBLIC;
-                        src = (uint32_t)desc;
-                        r1 = (uint32_t)((desc >> 46) & 0x3FFF);
+                        const uint32_t n = event_msgs(desc, fl);
+                        if (at >= c0 && at < c1) {
+                            const bool pub = fl & NFK_PUBLIC;
+                            uint32_t* x = s_ev + 3u * (at - c0);
+                            x[0] = m;
+                            x[1] = pub ? (uint32_t)desc : (uint32_t)e;
+                            x[2] = n | ((uint32_t)((desc >> 46) & 0x3FFF) << 14) | (pub ? 0x80000000u : 0u);
+                            d.ev_moff[ev0 + at] = mb + m;
+                            bytes += 4;
+                        }
+                        m += n;
+                        at++;
                     }
-                    const bool hit = n && m < w1 && m + n > w0;
-                    if (hit && !pub) {
-                        s_reg[m - w0] = (uint32_t)e;  // private: itself
-                    } else if (hit && n <= (uint32_t)kFanCoopT) {  // every player of the group but self
-                        const uint32_t np = n + (r1 ? 1u : 0u);
-                        uint32_t k = m;
+                }
+                __syncthreads();
+                const unsigned last = 3u * (c1 - c0 - 1u);
+                const unsigned m_lo = s_ev[0], m_hi = s_ev[last] + (s_ev[last + 2] & 0x3FFFu);
+                for (unsigned w0 = m_lo; w0 < m_hi; w0 += W) {  // uniform
+                    const unsigned w1 = min(m_hi, w0 + W);
+                    for (unsigned i = threadIdx.x; i < c1 - c0; i += kTPB) {
+                        const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
+                        const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
+                        if (n == 0 || ms >= w1 || ms + n <= w0) continue;
+                        if (!(b >> 31)) {  // private & !upload: the entity itself
+                            s_win[ms - w0] = a;
+                            continue;
+                        }
+                        const uint32_t np = n + (r1 ? 1u : 0u);  // every player of the group but self
+                        uint32_t k = ms;
                         for (uint32_t p = 0; p < np; p++) {
                             if (p + 1 == r1) continue;
                             if (k >= w0 && k < w1)
-                                s_reg[k - w0] = staged ? s_pl[src - pb_lo + p] : (uint32_t)d.pl_slot[src + p];
+                                s_win[k - w0] = staged ? s_pl[a - pb_lo + p] : (uint32_t)d.pl_slot[a + p];
                             k++;
                         }
                     }
-                    unsigned long long big = __ballot(hit && pub && n > (uint32_t)kFanCoopT);
-                    while (big) {
-                        const int L = __builtin_ctzll(big);
-                        big &= big - 1;
-                        const uint32_t bn = __shfl(n, L, 64), bsrc = __shfl(src, L, 64), br1 = __shfl(r1, L, 64);
-                        const uint32_t bm = __shfl(m, L, 64);
-                        for (uint32_t p = lane; p < bn; p += 64) {
-                            const uint32_t k = bm + p;
-                            if (k < w0 || k >= w1) continue;
-                            const uint32_t pp = p + ((br1 && p + 1 >= br1) ? 1u : 0u);  // skip self
-                            s_reg[k - w0] = staged ? s_pl[bsrc - pb_lo + pp] : (uint32_t)d.pl_slot[bsrc + pp];
-                        }
-                    }
-                    m += n;
-                }
-                if (!direct) {
                     __syncthreads();
-                    // mb and w0 are multiples of 4 (msg_tcap and W are): 16-byte stores
-                    const uint32_t n = w1 - w0, n4 = n >> 2;
-                    uint4* dst4 = (uint4*)(d.msg_rcpt + mb + w0);
-                    const uint4* src4 = (const uint4*)s_reg;
-                    for (uint32_t i = threadIdx.x; i < n4; i += kTPB) dst4[i] = src4[i];
-                    if (threadIdx.x < (n & 3u)) d.msg_rcpt[mb + w0 + 4 * n4 + threadIdx.x] = s_reg[4 * n4 + threadIdx.x];
-                    if (w1 < tmsg) __syncthreads();
+                    const uint32_t n = w1 - w0;
+                    if ((w0 & 3u) == 0) {  // mb is a multiple of 4 (msg_tcap is): 16-byte stores
+                        const uint32_t n4 = n >> 2;
+                        uint4* dst4 = (uint4*)(d.msg_rcpt + mb + w0);
+                        const uint4* src4 = (const uint4*)s_win;
+                        for (uint32_t i = threadIdx.x; i < n4; i += kTPB) dst4[i] = src4[i];
+                        if (threadIdx.x < (n & 3u)) d.msg_rcpt[mb + w0 + 4 * n4 + threadIdx.x] = s_win[4 * n4 + threadIdx.x];
+                    } else {
+                        for (uint32_t i = threadIdx.x; i < n; i += kTPB) d.msg_rcpt[mb + w0 + i] = s_win[i];
+                    }
+                    __syncthreads();
                 }
+                if (c1 < tev) __syncthreads();  // s_ev[0] / s_ev[last] are read before the next chunk
             }
         }
     }
