@@ -54,7 +54,6 @@ constexpr unsigned kAblPerKind = 8;  // not an ablation: force the per-kind oper
 constexpr unsigned kAblWaves6 = 16, kAblWaves8 = 32;  // k_tick register budgets (outputs stay exact)
 constexpr unsigned kAblWaves5 = 8192;                  // (6 is the default)
 constexpr unsigned kAblForceFuse = 32768;  // k_tick fans out whatever the group sizes (outputs stay exact)
-constexpr unsigned kAblNoSpec = 65536;     // no speculative operand loads in k_tick (outputs stay exact)
 constexpr unsigned kAblFanExpand = 64, kAblFanCopy = 128;  // timing only: k_fanout without expansion / copy-out
 constexpr unsigned kAblNoRun = 512, kAblNoLoads = 1024, kAblNoEmit = 2048;  // timing only (k_tick)
 constexpr unsigned kAblNoFuse = 4096;  // fan-out in k_fanout instead of k_tick's tail (outputs stay exact)
@@ -171,7 +170,6 @@ struct Dev {
     // t * msg_tcap (an upper bound of one tile's messages this frame); record tiles follow densely
     uint32_t msg_tcap;
     int32_t fuse_fan;
-    uint32_t spec_mask;  // U slots k_tick loads beside the schedule records (before it knows what fires)
     int32_t lds_words; // k_tick's dynamic LDS in 4-byte words (message window + staged players)
     // outputs (tile-staged)
     uint32_t* ev_slot; uint32_t* ev_pid; uint64_t* ev_old; uint64_t* ev_new; uint32_t* ev_moff;

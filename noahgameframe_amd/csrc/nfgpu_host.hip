@@ -1503,11 +1503,6 @@ int nfk_execute(void* world, int64_t now_ms) {
         }
     }
     d.fuse_fan = d.msg_tcap != 0;
-    // operands of every kind program loaded with the schedule records: one dependent round trip
-    // less per tile for a few more bytes (a kind's operands share its column group's lines)
-    d.spec_mask = 0;
-    if (use_u && !(d.ablate & (kAblNoSpec | kAblPrograms | kAblNoLoads)))
-        for (int k = 0; k < d.n_kind; k++) d.spec_mask |= w->tab.umask[k];
     w->last_tcap = d.msg_tcap;
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);

@@ -401,11 +401,6 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         // the scan needs no liveness test
         desc = d.fan_desc[e];
         bytes += 8;
-        // speculative: the programs' operands in the same round trip as the schedules (the kinds
-        // that fire are not known yet; a kind's operands share its column group's lines)
-#pragma unroll
-        for (int j = 0; j < kMaxU; j++)
-            if ((d.spec_mask >> j) & 1) v[j] = d.u_col[j][(size_t)e * d.u_str[j]];
         fired = sched_scan(d, e, bytes, s_rem);  // NFCScheduleModule::Execute (SM:51-81)
     }
     const bool live = !desc_dead(desc);
@@ -425,8 +420,8 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
 #pragma unroll
         for (int j = 0; j < kMaxU; j++)
             if (((need >> j) & 1) && !(d.ablate & kAblNoLoads)) {
-                if (!((d.spec_mask >> j) & 1)) v[j] = d.u_col[j][(size_t)e * d.u_str[j]];
-                bytes += 8;  // algorithmic: values the frame needs, whoever loaded them
+                v[j] = d.u_col[j][(size_t)e * d.u_str[j]];
+                bytes += 8;
             }
 #pragma unroll
         for (int j = 0; j < kMaxW; j++)
