@@ -98,8 +98,8 @@ struct Tables {
     // interleaved ([cap][group size]), so a sparse heartbeat reads one line per entity.
     int64_t p_off[kMaxProps];
     int32_t p_str[kMaxProps];
-    uint32_t umask[NFK_MAX_KINDS];                 // U slots kind k's program reads or writes
-    uint8_t opu[NFK_MAX_KINDS][NFK_MAX_OPS][4];    // U slot of dst, a, b, c (kNoU = immediate)
+    uint32_t umask[NFK_MAX_KINDS];                 // kind k's U slots: writable bits | read-only indices << 16
+    uint8_t opu[NFK_MAX_KINDS][NFK_MAX_OPS][4];    // U slot of dst, a, b, c (0x80 | r: read-only r; kNoU = immediate)
     int32_t nops[NFK_MAX_KINDS];
     uint8_t pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     uint8_t rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
@@ -148,7 +148,7 @@ struct Dev {
     unsigned long long* tally;
     // frame working set (k_tick): properties of the U slots, their columns, writable slots in
     // property-id order, and the slot of each property queued by SetProperty this frame
-    int32_t n_w;
+    int32_t n_w, n_u;         // writable slots [0, n_w), read-only slots [n_w, n_u)
     int32_t u_pid[kMaxU];
     uint64_t* u_col[kMaxU];   // property of slot e at u_col[j][e * u_str[j]]
     int32_t u_str[kMaxU];

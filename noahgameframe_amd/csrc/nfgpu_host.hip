@@ -771,7 +771,9 @@ int nfk_commit(void* world) {
             return fail(NFK_ERR_ARG, "two record ops on the same (record, col)");
     w->tab.n_recops = nro;
     // frame working set (k_tick): program destinations -> writable slots [0, n_wp) and
-    // read-only operands -> slots [kMaxW, kMaxW + n_rp), each group in property-id order
+    // read-only operands -> slots [n_w, n_w + n_rp) of the frame (n_w >= n_wp also counts the
+    // frame's SetProperty properties), each group in property-id order; tables name read-only
+    // operand r as 0x80 | r
     {
         std::vector<int> W, R;
         for (int k = 0; k < NK; k++)
@@ -796,14 +798,14 @@ int nfk_commit(void* world) {
             }
         std::sort(R.begin(), R.end());
         R.erase(std::unique(R.begin(), R.end()), R.end());
-        w->u_ok = (int)W.size() <= kMaxW && (int)R.size() <= kMaxU - kMaxW;
+        w->u_ok = (int)W.size() <= kMaxW && (int)(W.size() + R.size()) <= kMaxU;
         w->u_wp.assign(W.begin(), W.end());
         w->u_rp.assign(R.begin(), R.end());
         auto slot = [&](int64_t p) -> uint8_t {
             auto it = std::lower_bound(W.begin(), W.end(), (int)p);
             if (it != W.end() && *it == p) return (uint8_t)(it - W.begin());
             it = std::lower_bound(R.begin(), R.end(), (int)p);
-            return (uint8_t)(kMaxW + (it - R.begin()));
+            return (uint8_t)(0x80 | (it - R.begin()));
         };
         for (int k = 0; k < NK && w->u_ok; k++) {
             w->tab.umask[k] = 0;
@@ -822,8 +824,8 @@ int nfk_commit(void* world) {
                 } else if (op.code == NFK_OP_FAFFINE) {
                     u[0] = slot(op.dst);
                 }
-                for (int q = 0; q < 4; q++)
-                    if (u[q] != kNoU) w->tab.umask[k] |= 1u << u[q];
+                for (int q = 0; q < 4; q++)  // writable bits | read-only bits << 16
+                    if (u[q] != kNoU) w->tab.umask[k] |= (u[q] & 0x80) ? 1u << (16 + (u[q] & 0x7F)) : 1u << u[q];
                 OpX& x = w->tab.opx[k][i];
                 x.cfd = (uint32_t)op.code | ((uint32_t)op.flags << 8) | ((uint32_t)op.dst << 16);
                 x.slots = (uint32_t)u[0] | ((uint32_t)u[1] << 8) | ((uint32_t)u[2] << 16) | ((uint32_t)u[3] << 24);
@@ -1394,13 +1396,14 @@ int nfk_execute(void* world, int64_t now_ms) {
         int n_w = (int)w->u_wp.size();
         for (int j = 0; j < kMaxU; j++) d.u_pid[j] = -1;
         for (int i = 0; i < n_w; i++) d.u_pid[i] = w->u_wp[i];
-        for (size_t i = 0; i < w->u_rp.size(); i++) d.u_pid[kMaxW + i] = w->u_rp[i];
+        const int n_r = (int)w->u_rp.size();
         if (!w->xops.empty()) {
             uslot.assign(w->n_prop, 0xFF);
             for (int i = 0; i < n_w; i++) uslot[w->u_wp[i]] = (uint8_t)i;
             for (const auto& x : w->xops) {
                 if (uslot[x.pid] != 0xFF) continue;
-                if (std::binary_search(w->u_rp.begin(), w->u_rp.end(), (int)x.pid) || n_w == kMaxW) {
+                if (std::binary_search(w->u_rp.begin(), w->u_rp.end(), (int)x.pid) || n_w == kMaxW ||
+                    n_w + n_r == kMaxU) {
                     use_u = false;
                     break;
                 }
@@ -1409,6 +1412,8 @@ int nfk_execute(void* world, int64_t now_ms) {
             }
         }
         d.n_w = n_w;
+        for (int i = 0; i < n_r; i++) d.u_pid[n_w + i] = w->u_rp[i];
+        d.n_u = n_w + n_r;
         std::vector<int> ord(n_w);
         for (int i = 0; i < n_w; i++) ord[i] = i;
         std::sort(ord.begin(), ord.end(), [&](int a, int b) { return d.u_pid[a] < d.u_pid[b]; });
@@ -1507,14 +1512,22 @@ int nfk_execute(void* world, int64_t now_ms) {
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
         size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;
-        if (d.fuse_fan) lds = std::max(lds, (size_t)kFanWinBytes);
+        // the fan-out window takes what LDS the variant's occupancy leaves (waves per SIMD =
+        // workgroups per CU; about 2.3 KB of static LDS per workgroup)
+        const int waves = !use_u ? 6 : (d.n_u <= 8 && !(d.ablate & kAblWaves6)) ? kWavesU8
+                                   : (d.n_u <= 12 && !(d.ablate & kAblWaves6)) ? kWavesU12 : 6;
+        const size_t budget = (size_t)(163840 / (waves > 7 ? 8 : waves) - 2560) & ~(size_t)1023;
+        if (d.fuse_fan) lds = std::max(lds, std::min((size_t)kFanWinBytes, budget));
         d.lds_words = (int32_t)(lds / 4);
-        if (use_u && (d.ablate & kAblWaves5))
-            hipLaunchKernelGGL(k_tick<5>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
-        else if (use_u && (d.ablate & kAblWaves8))
-            hipLaunchKernelGGL(k_tick<8>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
-        else if (use_u)  // 80 VGPRs, no spills: 6 waves per SIMD
-            hipLaunchKernelGGL(k_tick<6>, dim3((unsigned)d.n_tiles), dim3(kTPB), lds, w->stream, d);
+        // the variant whose register slots hold the frame's working set (no spills at 6 or more
+        // waves per SIMD)
+        const dim3 g((unsigned)d.n_tiles), b(kTPB);
+        if (use_u && d.n_u <= 8 && !(d.ablate & kAblWaves6))
+            hipLaunchKernelGGL((k_tick<kWavesU8, 8>), g, b, lds, w->stream, d);
+        else if (use_u && d.n_u <= 12 && !(d.ablate & kAblWaves6))
+            hipLaunchKernelGGL((k_tick<kWavesU12, 12>), g, b, lds, w->stream, d);
+        else if (use_u)
+            hipLaunchKernelGGL((k_tick<6, 16>), g, b, lds, w->stream, d);
         else
             hipLaunchKernelGGL(k_tick_touch, dim3((unsigned)d.n_tiles), dim3(kTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());

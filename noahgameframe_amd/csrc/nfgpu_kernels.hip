@@ -204,44 +204,55 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
 #define NFK_U16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 static_assert(kMaxU == 16, "NFK_U16 enumerates kMaxU slots");
 
+// A frame's U slots: the writable ones [0, n_w), then the read-only ones [n_w, n_w + n_r).  The
+// kind tables name a read-only operand by its index r as 0x80 | r, so one table serves every
+// frame; kU (template) = the register slots a k_tick variant keeps (n_w + n_r <= kU).
+__device__ __forceinline__ uint32_t uslot(uint32_t raw, uint32_t n_w) {
+    return (raw & 0x80u) ? n_w + (raw & 0x7Fu) : raw;
+}
 // j wave-uniform: a scalar branch to one register move
-__device__ __forceinline__ uint64_t uget(const uint64_t (&v)[kMaxU], uint32_t j) {
+template <int kU>
+__device__ __forceinline__ uint64_t uget(const uint64_t (&v)[kU], uint32_t j) {
     switch (__builtin_amdgcn_readfirstlane(j)) {
 #define NFK_C(i) \
     case i:      \
-        return v[i];
+        return v[(i) < kU ? (i) : 0];
         NFK_U16(NFK_C)
 #undef NFK_C
     }
     return 0;
 }
-__device__ __forceinline__ void uput(uint64_t (&v)[kMaxU], uint32_t j, uint64_t x) {
+template <int kU>
+__device__ __forceinline__ void uput(uint64_t (&v)[kU], uint32_t j, uint64_t x) {
     switch (__builtin_amdgcn_readfirstlane(j)) {
-#define NFK_C(i)  \
-    case i:       \
-        v[i] = x; \
+#define NFK_C(i)                   \
+    case i:                        \
+        v[(i) < kU ? (i) : 0] = x; \
         break;
         NFK_U16(NFK_C)
 #undef NFK_C
     }
 }
 // j per lane (queued SetProperty calls differ between entities): select over the writable slots
-__device__ __forceinline__ uint64_t uget_lane(const uint64_t (&v)[kMaxU], uint32_t j) {
+template <int kU>
+__device__ __forceinline__ uint64_t uget_lane(const uint64_t (&v)[kU], uint32_t j) {
     uint64_t r = 0;
 #pragma unroll
-    for (int i = 0; i < kMaxW; i++) r = (j == (uint32_t)i) ? v[i] : r;
+    for (int i = 0; i < (kU < kMaxW ? kU : kMaxW); i++) r = (j == (uint32_t)i) ? v[i] : r;
     return r;
 }
-__device__ __forceinline__ void uput_lane(uint64_t (&v)[kMaxU], uint32_t j, uint64_t x) {
+template <int kU>
+__device__ __forceinline__ void uput_lane(uint64_t (&v)[kU], uint32_t j, uint64_t x) {
 #pragma unroll
-    for (int i = 0; i < kMaxW; i++) v[i] = (j == (uint32_t)i) ? x : v[i];
+    for (int i = 0; i < (kU < kMaxW ? kU : kMaxW); i++) v[i] = (j == (uint32_t)i) ? x : v[i];
 }
 
 // The fired kinds' programs in schedule-name order on the register working set.  A Set that
 // fails the reference's change predicate leaves the value as it was; wm collects the slots a
 // Set changed at least once.
-__device__ __forceinline__ void run_programs_u(uint64_t (&v)[kMaxU], uint32_t& wm, const Tables* __restrict__ tab_,
-                                               uint32_t fired, int n_kind) {
+template <int kU>
+__device__ __forceinline__ void run_programs_u(uint64_t (&v)[kU], uint32_t& wm, const Tables* __restrict__ tab_,
+                                               uint32_t fired, int n_kind, uint32_t n_w) {
     CTables* tab = ctab(tab_);
     for (int k = 0; k < n_kind; k++) {
         if (!((fired >> k) & 1)) continue;
@@ -249,7 +260,8 @@ __device__ __forceinline__ void run_programs_u(uint64_t (&v)[kMaxU], uint32_t& w
         for (int i = 0; i < n; i++) {
             const uint32_t cfd = tab->opx[k][i].cfd, sl = tab->opx[k][i].slots;
             const uint32_t code = cfd & 0xFF, flags = (cfd >> 8) & 0xFF;
-            const uint32_t u0 = sl & 0xFF, u1 = (sl >> 8) & 0xFF, u2 = (sl >> 16) & 0xFF, u3 = sl >> 24;
+            const uint32_t u0 = uslot(sl & 0xFF, n_w), u1 = uslot((sl >> 8) & 0xFF, n_w);
+            const uint32_t u2 = uslot((sl >> 16) & 0xFF, n_w), u3 = uslot(sl >> 24, n_w);
             if (code == NFK_OP_IADD_CLAMP) {
                 const int64_t cur = (int64_t)uget(v, u0);
                 const int64_t a = (flags & NFK_A_PROP) ? (int64_t)uget(v, u1) : tab->opx[k][i].a;
@@ -302,6 +314,8 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
 
 constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
 
+// k_tick register budgets (waves per SIMD) by the frame's U slot count
+constexpr int kWavesU8 = 8, kWavesU12 = 7;
 constexpr int kFanCoopT = 16;  // k_tick's fan-out: events with more recipients are expanded by the wave
 constexpr int kFanWinBytes = 24576;  // k_tick's dynamic LDS floor when it fans out (6 workgroups per CU)
 constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: at most 4 GiB reserved
@@ -369,8 +383,9 @@ __device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& by
 // [t * tile_cap, t * tile_cap + count); k_scan_tiles turns the counts into global ranks.
 // kWPE: waves per SIMD the register allocation aims at (5 fits without spilling).  The LDS image
 // of the frame-start values is dynamic: n_w writable slots x kTPB.
-template <int kWPE>
+template <int kWPE, int kU>
 __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8))) void k_tick(Dev d) {
+    constexpr int kW = kU < kMaxW ? kU : kMaxW;  // writable register slots
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
     __shared__ uint32_t s_pb[2];   // pl_slot run of the groups with dirty events: [lo, hi)
@@ -393,9 +408,9 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     unsigned bytes = 0;
     uint32_t fired = 0, xh = 0, wm = 0;
     uint64_t desc = kDeadDesc;
-    uint64_t v[kMaxU];
+    uint64_t v[kU];
 #pragma unroll
-    for (int j = 0; j < kMaxU; j++) v[j] = 0;
+    for (int j = 0; j < kU; j++) v[j] = 0;
     if (e < d.N) {
         // descriptor and schedule records in one round trip: a slack slot has no schedules, so
         // the scan needs no liveness test
@@ -415,17 +430,20 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         }
         if (!(d.ablate & kAblPrograms))
             for (int k = 0; k < d.n_kind; k++)
-                if ((fired >> k) & 1) need |= ctab(d.tab)->umask[k];
+                if ((fired >> k) & 1) {
+                    const uint32_t um = ctab(d.tab)->umask[k];  // writable bits | read-only bits << 16
+                    need |= (um & 0xFFFFu) | ((um >> 16) << d.n_w);
+                }
         // one batch of independent loads: every value this entity's frame reads or writes
 #pragma unroll
-        for (int j = 0; j < kMaxU; j++)
+        for (int j = 0; j < kU; j++)
             if (((need >> j) & 1) && !(d.ablate & kAblNoLoads)) {
                 v[j] = d.u_col[j][(size_t)e * d.u_str[j]];
                 bytes += 8;
             }
 #pragma unroll
-        for (int j = 0; j < kMaxW; j++)
-            if ((need >> j) & 1) s_o[j * kTPB + threadIdx.x] = v[j];
+        for (int j = 0; j < kW; j++)
+            if (j < d.n_w && ((need >> j) & 1)) s_o[j * kTPB + threadIdx.x] = v[j];
         // SetProperty* calls queued before this frame, in call order (PR:254 / PR:295 predicates)
         if (xh) {
             for (int i = (int)xh - 1; i < d.n_x && d.x_slot[i] == (uint32_t)e; i++) {
@@ -445,7 +463,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             }
         }
         // the fired heartbeats' effect programs, in schedule-name order
-        if (!(d.ablate & (kAblPrograms | kAblNoRun)) && fired) run_programs_u(v, wm, d.tab, fired, d.n_kind);
+        if (!(d.ablate & (kAblPrograms | kAblNoRun)) && fired) run_programs_u(v, wm, d.tab, fired, d.n_kind, d.n_w);
     }
     __syncthreads();  // s_pflags
     // dirty diff against the frame-start values, and each dirty event's fan-out message count
@@ -453,7 +471,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     unsigned nmsg = 0;
     const unsigned cls = (unsigned)(desc >> 60);
 #pragma unroll
-    for (int j = 0; j < kMaxW; j++)
+    for (int j = 0; j < kW; j++)
         if (((wm >> j) & 1) && v[j] != s_o[j * kTPB + threadIdx.x]) {
             dm |= 1u << j;
             nmsg += event_msgs(desc, s_pflags[cls][d.u_pid[j]]);
