@@ -1037,21 +1037,25 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
 
 // ---------------------------------------------------------------------------------
 // Fan-out: GetBroadCastObject recipient lists (AOI:531-593) for every dirty event, one workgroup
-// per tile (property tiles, then record tiles; blockIdx.x + blk0 is the tile), one thread per
-// event.  When k_tick writes its own tiles' fan-out this runs for the record tiles only.  Each
-// tile's messages are one contiguous run at msg_base[tile] (k_scan_tiles).
-// Slots are in (scene, group, guid) order, so the players of every group the tile touches form one contiguous run of
-// pl_slot; it is staged in LDS when it fits.  A thread writes its event's recipients as one
-// contiguous run (every player of the group but itself, NFGUID order, or itself); events with
-// more than kFanCoop recipients are expanded by their whole wave, 64 recipients per store.
-// Also rewrites each event's tile-local message offset as a global one.  Does nothing (and sets
-// no output) when the frame's message runs exceed msg_cap: the host grows the buffer and re-runs it.
-constexpr int kFanLds = 2048, kFanCoop = kFanCoopT, kFanPer = 4, kFanMsgLds = 6144;
+// per tile (property tiles, then record tiles; blockIdx.x + blk0 is the tile).  When k_tick
+// writes its own tiles' fan-out this runs for the record tiles only.  Each tile's messages are
+// one contiguous run at msg_base[tile] (k_scan_tiles).  A pass takes up to kTPB * kFanPer
+// events: their (first message, first player | slot, count | rank | public) triples go to LDS,
+// and each event is then expanded by a group of L lanes (L = the pass's largest recipient count
+// rounded up to a power of two, at most 64), so a group of 32 players fills half a wave per event
+// and a 2-player group an eighth.  Slots are in (scene, group, guid) order, so the players of
+// every group the pass touches form one contiguous run of pl_slot, staged in LDS when it fits;
+// messages are staged in LDS and stored coalesced when the pass's run fits, else stored by the
+// lane groups directly (each group's stores are contiguous).  Also rewrites each event's
+// tile-local message offset as a global one.  Does nothing (and sets no output) when the frame's
+// message runs exceed msg_cap: the host grows the buffer and re-runs it.
+constexpr int kFanLds = 2048, kFanPer = 4, kFanMsgLds = 4096;
 
 __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
-    __shared__ int32_t s_pl[kFanLds];
-    __shared__ uint32_t s_msg[kFanMsgLds];  // a pass's recipient runs, stored to HBM coalesced
-    __shared__ uint32_t s_pb[2], s_m[2];
+    __shared__ uint32_t s_pl[kFanLds];
+    __shared__ __align__(16) uint32_t s_msg[kFanMsgLds];  // a pass's messages, stored to HBM coalesced
+    __shared__ uint32_t s_ev[3 * kTPB * kFanPer];       // a pass's event triples
+    __shared__ uint32_t s_pb[3], s_m[2];                // player run [lo, hi), largest count
     __shared__ unsigned s_bytes;
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
@@ -1069,7 +1073,6 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
     const uint32_t b0 = base[t], b1 = base[t + 1];
     const uint32_t tmsg = d.t_msg[tg], mbase = d.msg_base[tg];
     uint32_t slot[kFanPer], key[kFanPer], lm[kFanPer];
-    uint64_t desc[kFanPer];
 #pragma unroll
     for (int q = 0; q < kFanPer; q++) {
         const unsigned i = q * kTPB + threadIdx.x;
@@ -1106,82 +1109,90 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
                 }
             }
         }
-        // second round trip: the events' fan-out descriptors
-#pragma unroll
-        for (int q = 0; q < kFanPer; q++)
-            desc[q] = (c0 + q * kTPB + threadIdx.x < c_end) ? d.fan_desc[slot[q]] : kDeadDesc;
-        // the pass's message range and the player run of the groups it touches
+        if (threadIdx.x == 0) {
+            s_pb[0] = 0xFFFFFFFFu;
+            s_pb[1] = 0;
+            s_pb[2] = 1;
+        }
+        __syncthreads();  // s_pflags / s_rflags; s_pb reset; the previous pass is done with s_ev
+        // second round trip: the events' fan-out descriptors -> LDS triples, global offsets
+        uint32_t lo = 0xFFFFFFFFu, hi = 0, nmax = 0;
 #pragma unroll
         for (int q = 0; q < kFanPer; q++) {
             const unsigned i = c0 + q * kTPB + threadIdx.x;
-            if (i == c0) {
-                s_m[0] = lm[q];
-                s_pb[0] = (uint32_t)desc[q];
+            if (i < c_end) {
+                const uint64_t desc = d.fan_desc[slot[q]];
+                const unsigned cls = (unsigned)(desc >> 60);
+                const uint8_t fl = rec ? s_rflags[cls][key[q]] : s_pflags[cls][key[q]];
+                const uint32_t n = event_msgs(desc, fl);
+                const bool pub = fl & NFK_PUBLIC;
+                const uint32_t src = (uint32_t)desc, np = (uint32_t)((desc >> 32) & 0x3FFF);
+                uint32_t* x = s_ev + 3 * (i - c0);
+                x[0] = lm[q];
+                x[1] = pub ? src : slot[q];
+                x[2] = n | ((uint32_t)((desc >> 46) & 0x3FFF) << 14) | (pub ? 0x80000000u : 0u);
+                moff[off0 + i] = mbase + lm[q];
+                bytes += 4 + 4 + 4 + 8 + 4 + 4 * n;
+                nmax = max(nmax, n);
+                if (pub && n) {
+                    lo = min(lo, src);
+                    hi = max(hi, src + np);
+                }
             }
-            if (i == c_end - 1) s_pb[1] = (uint32_t)desc[q] + (uint32_t)((desc[q] >> 32) & 0x3FFF);
+            if (i == c0) s_m[0] = lm[q];
         }
         if (threadIdx.x == 0) s_m[1] = c_end < cnt ? moff[off0 + c_end] : tmsg;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, m, 64));
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, m, 64));
+            nmax = max(nmax, (uint32_t)__shfl_xor((int)nmax, m, 64));
+        }
+        if (lane == 0) {
+            if (hi) {
+                atomicMin(&s_pb[0], lo);
+                atomicMax(&s_pb[1], hi);
+            }
+            atomicMax(&s_pb[2], nmax);
+        }
         __syncthreads();
         const uint32_t p0 = s_m[0], pn = s_m[1] - s_m[0];
         const bool lds_out = pn <= (uint32_t)kFanMsgLds;
-        const uint32_t pb_lo = s_pb[0], npl = s_pb[1] - s_pb[0];
+        const uint32_t pb_lo = s_pb[0], npl = s_pb[1] > s_pb[0] ? s_pb[1] - s_pb[0] : 0u;
         const bool staged = npl <= (uint32_t)kFanLds;
+        const uint32_t nm = s_pb[2];
+        const uint32_t L = nm <= 1 ? 1u : nm >= 64 ? 64u : 1u << (32 - __builtin_clz(nm - 1));
         if (staged) {  // third round trip: the players, NFGUID order (pl_slot is in slot order)
-            for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = d.pl_slot[pb_lo + i];
+            for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = (uint32_t)d.pl_slot[pb_lo + i];
             bytes += 4 * ((npl + kTPB - 1 - threadIdx.x) / kTPB);
+            __syncthreads();
         }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < kFanPer; q++) {
-            const unsigned i = c0 + q * kTPB + threadIdx.x;
-            uint32_t n = 0, m0 = 0, src = 0, r1 = 0;
-            bool pub = false;
-            if (i < c_end) {
-                const unsigned cls = (unsigned)(desc[q] >> 60);
-                const uint8_t fl = rec ? s_rflags[cls][key[q]] : s_pflags[cls][key[q]];
-                bytes += 4 + 4 + 4 + 8 + 4;
-                n = event_msgs(desc[q], fl);
-                m0 = mbase + lm[q];
-                moff[off0 + i] = m0;
-                pub = fl & NFK_PUBLIC;
-                if (pub) {  // every player of the group but self, NFGUID order
-                    src = (uint32_t)desc[q];
-                    r1 = (uint32_t)((desc[q] >> 46) & 0x3FFF);
-                }
+        // expansion: lane group g = threadIdx.x / L takes events g, g + kTPB / L, ...
+        uint32_t* out = lds_out ? s_msg : d.msg_rcpt + mbase + p0;
+        const uint32_t sub = threadIdx.x & (L - 1);
+        for (uint32_t i = threadIdx.x / L; i < c_end - c0; i += kTPB / L) {
+            const uint32_t ms = s_ev[3 * i] - p0, a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
+            const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
+            if (!(b >> 31)) {  // private & !upload: the entity itself (n is 0 or 1)
+                if (sub < n) out[ms] = a;
+                continue;
             }
-            uint32_t* out = lds_out ? s_msg + (lm[q] - p0) : d.msg_rcpt + m0;
-            if (d.ablate & kAblFanExpand) {
-                n = 0;
-                pub = false;
-            }
-            if (!pub) {
-                if (n) out[0] = slot[q];
-            } else if (n <= (uint32_t)kFanCoop) {
-                const uint32_t np = n + (r1 ? 1u : 0u);
-                uint32_t m = 0;
-                for (uint32_t p = 0; p < np; p++) {
-                    if (p + 1 == r1) continue;
-                    out[m++] = staged ? (uint32_t)s_pl[src - pb_lo + p] : (uint32_t)d.pl_slot[src + p];
-                }
-            }
-            bytes += 4 * n;
-            // big groups: the wave expands each such event cooperatively
-            unsigned long long big = __ballot(pub && n > (uint32_t)kFanCoop);
-            while (big) {
-                const int L = __builtin_ctzll(big);
-                big &= big - 1;
-                const uint32_t bn = __shfl(n, L, 64), bsrc = __shfl(src, L, 64), br1 = __shfl(r1, L, 64);
-                const uint32_t bm0 = __shfl(m0, L, 64);
-                uint32_t* bout = lds_out ? s_msg + (bm0 - mbase - p0) : d.msg_rcpt + bm0;
-                for (uint32_t p = lane; p < bn; p += 64) {
-                    const uint32_t pp = p + ((br1 && p + 1 >= br1) ? 1u : 0u);  // skip self
-                    bout[p] = staged ? (uint32_t)s_pl[bsrc - pb_lo + pp] : (uint32_t)d.pl_slot[bsrc + pp];
-                }
+            for (uint32_t p = sub; p < n; p += L) {  // every player of the group but self
+                const uint32_t pp = p + ((r1 && p + 1 >= r1) ? 1u : 0u);
+                out[ms + p] = staged ? s_pl[a - pb_lo + pp] : (uint32_t)d.pl_slot[a + pp];
             }
         }
-        __syncthreads();
-        if (lds_out && !(d.ablate & kAblFanCopy))
-            for (uint32_t i = threadIdx.x; i < pn; i += kTPB) d.msg_rcpt[mbase + p0 + i] = s_msg[i];
+        if (lds_out) {
+            __syncthreads();
+            uint32_t* dst = d.msg_rcpt + mbase + p0;
+            if (((mbase + p0) & 3u) == 0) {
+                const uint32_t n4 = pn >> 2;
+                for (uint32_t i = threadIdx.x; i < n4; i += kTPB) ((uint4*)dst)[i] = ((const uint4*)s_msg)[i];
+                if (threadIdx.x < (pn & 3u)) dst[4 * n4 + threadIdx.x] = s_msg[4 * n4 + threadIdx.x];
+            } else {
+                for (uint32_t i = threadIdx.x; i < pn; i += kTPB) dst[i] = s_msg[i];
+            }
+        }
         __syncthreads();
     }
     const unsigned wb = (unsigned)wave_sum(bytes);
