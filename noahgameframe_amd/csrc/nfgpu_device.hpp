@@ -53,7 +53,6 @@ constexpr unsigned kAblPrograms = 4;
 constexpr unsigned kAblPerKind = 8;  // not an ablation: force the per-kind operand path (outputs stay exact)
 constexpr unsigned kAblWaves6 = 16, kAblWaves8 = 32;  // k_tick register budgets (outputs stay exact)
 constexpr unsigned kAblWaves5 = 8192;                  // (6 is the default)
-constexpr unsigned kAblForceFuse = 32768;  // k_tick fans out whatever the group sizes (outputs stay exact)
 constexpr unsigned kAblNoRun = 512, kAblNoLoads = 1024, kAblNoEmit = 2048;  // timing only (k_tick)
 constexpr unsigned kAblNoFuse = 4096;  // fan-out in k_fanout instead of k_tick's tail (outputs stay exact)
 

@@ -1482,14 +1482,12 @@ int nfk_execute(void* world, int64_t now_ms) {
                                d.e_flags, d.s_hot, d.n_kind, d.cap);
         HIPCHK(hipGetLastError());
     }
-    // k_tick writes its tiles' fan-out itself (its LDS image doubles as the message window) when
-    // every event's recipient run is short enough for one thread (big groups go to k_fanout, whose
-    // workgroups spread the runs over more waves).  Property tile t's messages then sit at
-    // t * msg_tcap, msg_tcap = writable properties x slots x most recipients of one event: no
-    // tile waits for another tile's count.
+    // k_tick writes its tiles' fan-out itself (its LDS image is reused for the events): property
+    // tile t's messages sit at t * msg_tcap, msg_tcap = writable properties x slots x most
+    // recipients of one event, so no tile waits for another tile's count.  Worlds whose bound
+    // would reserve more than kMsgStrideLimit run k_fanout after k_scan_tiles instead.
     d.msg_tcap = 0;
-    if (use_u && d.n_tiles && !(d.ablate & (kAblNoFuse | kAblNoEmit)) &&
-        (w->max_np <= kFanCoopT + 1 || (d.ablate & kAblForceFuse))) {
+    if (use_u && d.n_tiles && !(d.ablate & (kAblNoFuse | kAblNoEmit))) {
         const int64_t tcap = (int64_t)std::max(d.n_w, 1) * kTile * std::max(w->max_np, 1);
         const int64_t need = tcap * d.n_tiles + w->last_rec_msgs + w->last_rec_msgs / 4 + 1024;
         if (tcap * d.n_tiles <= kMsgStrideLimit) {
@@ -1512,18 +1510,14 @@ int nfk_execute(void* world, int64_t now_ms) {
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
         size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;
-        // the fan-out window takes what LDS the variant's occupancy leaves (waves per SIMD =
-        // workgroups per CU; about 2.3 KB of static LDS per workgroup)
-        const int waves = !use_u ? 6 : (d.n_u <= 8 && !(d.ablate & kAblWaves6)) ? kWavesU8
-                                   : (d.n_u <= 12 && !(d.ablate & kAblWaves6)) ? kWavesU12 : 6;
-        const size_t budget = (size_t)(163840 / (waves > 7 ? 8 : waves) - 2560) & ~(size_t)1023;
-        if (d.fuse_fan) lds = std::max(lds, std::min((size_t)kFanWinBytes, budget));
         d.lds_words = (int32_t)(lds / 4);
         // the variant whose register slots hold the frame's working set (no spills at 6 or more
         // waves per SIMD)
         const dim3 g((unsigned)d.n_tiles), b(kTPB);
         if (use_u && d.n_u <= 8 && !(d.ablate & kAblWaves6))
             hipLaunchKernelGGL((k_tick<kWavesU8, 8>), g, b, lds, w->stream, d);
+        else if (use_u && d.n_u <= 12 && (d.ablate & kAblWaves8))  // (8 waves, a few spills)
+            hipLaunchKernelGGL((k_tick<8, 12>), g, b, lds, w->stream, d);
         else if (use_u && d.n_u <= 12 && !(d.ablate & kAblWaves6))
             hipLaunchKernelGGL((k_tick<kWavesU12, 12>), g, b, lds, w->stream, d);
         else if (use_u)

@@ -316,8 +316,6 @@ constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
 
 // k_tick register budgets (waves per SIMD) by the frame's U slot count
 constexpr int kWavesU8 = 8, kWavesU12 = 7;
-constexpr int kFanCoopT = 16;  // k_tick's fan-out: events with more recipients are expanded by the wave
-constexpr int kFanWinBytes = 24576;  // k_tick's dynamic LDS floor when it fans out (6 workgroups per CU)
 constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: at most 4 GiB reserved
 
 // NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
@@ -388,7 +386,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     constexpr int kW = kU < kMaxW ? kU : kMaxW;  // writable register slots
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
-    __shared__ uint32_t s_pb[2];   // pl_slot run of the groups with dirty events: [lo, hi)
+    __shared__ uint32_t s_pb[3];   // pl_slot run of the groups with dirty events [lo, hi), most recipients
     extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
     __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     const int tile = blockIdx.x;
@@ -398,6 +396,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         s_bytes = 0;
         s_pb[0] = 0xFFFFFFFFu;
         s_pb[1] = 0;
+        s_pb[2] = 1;
     }
     {
         const int words = d.n_class * (NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS) / 4;
@@ -468,13 +467,15 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     __syncthreads();  // s_pflags
     // dirty diff against the frame-start values, and each dirty event's fan-out message count
     uint32_t dm = 0;
-    unsigned nmsg = 0;
+    unsigned nmsg = 0, nmax = 0;
     const unsigned cls = (unsigned)(desc >> 60);
 #pragma unroll
     for (int j = 0; j < kW; j++)
         if (((wm >> j) & 1) && v[j] != s_o[j * kTPB + threadIdx.x]) {
             dm |= 1u << j;
-            nmsg += event_msgs(desc, s_pflags[cls][d.u_pid[j]]);
+            const unsigned n = event_msgs(desc, s_pflags[cls][d.u_pid[j]]);
+            nmsg += n;
+            nmax = max(nmax, n);
         }
     const unsigned nd = __builtin_popcount(dm);
     const unsigned nf = __builtin_popcount(fired);
@@ -485,10 +486,12 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         for (int m = 32; m >= 1; m >>= 1) {
             lo = min(lo, (uint32_t)__shfl_xor((int)lo, m, 64));
             hi = max(hi, (uint32_t)__shfl_xor((int)hi, m, 64));
+            nmax = max(nmax, (uint32_t)__shfl_xor((int)nmax, m, 64));
         }
         if ((threadIdx.x & 63) == 0 && hi) {
             atomicMin(&s_pb[0], lo);
             atomicMax(&s_pb[1], hi);
+            atomicMax(&s_pb[2], nmax);
         }
     }
 
@@ -540,11 +543,12 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         bytes += 4;
     }
     if (!fuse && !(d.ablate & kAblNoEmit)) bytes += 4 * nd;  // ev_moff
-    // Fan-out of the tile's events (GetBroadCastObject, AOI:531-593; see k_fanout), at the tile's
-    // fixed-stride run mb.  The LDS region of the frame-start image is reused: a chunk of the
-    // tile's events as (first message, first player | slot, count | rank | public) triples, the
-    // groups' player run, and a message window.  Every thread takes whole events of the chunk, so
-    // the lanes stay busy whichever entities the events belong to; the window is stored coalesced.
+    // Fan-out of the tile's events (GetBroadCastObject, AOI:531-593; see k_fanout), into the
+    // tile's fixed-stride run mb.  The LDS region of the frame-start image is reused for a chunk
+    // of the tile's events as (first message, first player | slot, count | rank | public) triples
+    // and the groups' player run; each event is then expanded by a group of L lanes (L = the
+    // tile's largest recipient count rounded up to a power of two), so consecutive lane groups
+    // store consecutive events' runs: every store instruction covers one contiguous span.
     if (fuse) {
         __syncthreads();  // s_pb; every read of s_o and s_rem is done: the region is reused
         const unsigned mb = (unsigned)tile * d.msg_tcap;
@@ -565,12 +569,14 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         } else {
             const unsigned R = (unsigned)d.lds_words;
             const uint32_t pb_lo = s_pb[0], npl = s_pb[1] > s_pb[0] ? s_pb[1] - s_pb[0] : 0u;
-            const bool staged = npl <= R / 4;
-            const unsigned ecap = min((tev + 3u) & ~3u, (R / 6u) & ~3u);  // events per chunk
-            const unsigned W = (R - 3u * ecap - (staged ? npl : 0u)) & ~3u;  // window entries
+            const bool staged = npl <= R / 2;
+            const unsigned ecap = min(tev, (R - (staged ? npl : 0u)) / 3u);  // events per chunk
+            const uint32_t nm = s_pb[2];
+            const uint32_t L = nm <= 1 ? 1u : nm >= 64 ? 64u : 1u << (32 - __builtin_clz(nm - 1));
+            const uint32_t sub = threadIdx.x & (L - 1);
             uint32_t* s_ev = (uint32_t*)s_o;
-            uint32_t* s_win = s_ev + 3u * ecap;
-            uint32_t* s_pl = s_win + W;
+            uint32_t* s_pl = s_ev + (R - npl);
+            uint32_t* out = d.msg_rcpt + mb;
             if (staged) {
                 for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = (uint32_t)d.pl_slot[pb_lo + i];
                 bytes += 4 * ((npl + kTPB - 1 - threadIdx.x) / kTPB);
@@ -599,41 +605,19 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     }
                 }
                 __syncthreads();
-                const unsigned last = 3u * (c1 - c0 - 1u);
-                const unsigned m_lo = s_ev[0], m_hi = s_ev[last] + (s_ev[last + 2] & 0x3FFFu);
-                for (unsigned w0 = m_lo; w0 < m_hi; w0 += W) {  // uniform
-                    const unsigned w1 = min(m_hi, w0 + W);
-                    for (unsigned i = threadIdx.x; i < c1 - c0; i += kTPB) {
-                        const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
-                        const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
-                        if (n == 0 || ms >= w1 || ms + n <= w0) continue;
-                        if (!(b >> 31)) {  // private & !upload: the entity itself
-                            s_win[ms - w0] = a;
-                            continue;
-                        }
-                        const uint32_t np = n + (r1 ? 1u : 0u);  // every player of the group but self
-                        uint32_t k = ms;
-                        for (uint32_t p = 0; p < np; p++) {
-                            if (p + 1 == r1) continue;
-                            if (k >= w0 && k < w1)
-                                s_win[k - w0] = staged ? s_pl[a - pb_lo + p] : (uint32_t)d.pl_slot[a + p];
-                            k++;
-                        }
+                for (uint32_t i = threadIdx.x / L; i < c1 - c0; i += kTPB / L) {
+                    const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
+                    const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
+                    if (!(b >> 31)) {  // private & !upload: the entity itself (n is 0 or 1)
+                        if (sub < n) out[ms] = a;
+                        continue;
                     }
-                    __syncthreads();
-                    const uint32_t n = w1 - w0;
-                    if ((w0 & 3u) == 0) {  // mb is a multiple of 4 (msg_tcap is): 16-byte stores
-                        const uint32_t n4 = n >> 2;
-                        uint4* dst4 = (uint4*)(d.msg_rcpt + mb + w0);
-                        const uint4* src4 = (const uint4*)s_win;
-                        for (uint32_t i = threadIdx.x; i < n4; i += kTPB) dst4[i] = src4[i];
-                        if (threadIdx.x < (n & 3u)) d.msg_rcpt[mb + w0 + 4 * n4 + threadIdx.x] = s_win[4 * n4 + threadIdx.x];
-                    } else {
-                        for (uint32_t i = threadIdx.x; i < n; i += kTPB) d.msg_rcpt[mb + w0 + i] = s_win[i];
+                    for (uint32_t p = sub; p < n; p += L) {  // every player of the group but self
+                        const uint32_t pp = p + ((r1 && p + 1 >= r1) ? 1u : 0u);
+                        out[ms + p] = staged ? s_pl[a - pb_lo + pp] : (uint32_t)d.pl_slot[a + pp];
                     }
-                    __syncthreads();
                 }
-                if (c1 < tev) __syncthreads();  // s_ev[0] / s_ev[last] are read before the next chunk
+                if (c1 < tev) __syncthreads();  // s_ev is refilled
             }
         }
     }
