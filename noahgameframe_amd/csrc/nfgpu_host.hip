@@ -1510,6 +1510,13 @@ int nfk_execute(void* world, int64_t now_ms) {
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
         size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;
+        if (d.fuse_fan) {  // the fan-out's message window takes what LDS the variant's occupancy
+                           // leaves (waves per SIMD = workgroups per CU; ~2.3 KB static each)
+            const int waves = (d.n_u <= 8 && !(d.ablate & kAblWaves6)) ? kWavesU8
+                              : (d.n_u <= 12 && !(d.ablate & kAblWaves6)) ? ((d.ablate & kAblWaves8) ? 8 : kWavesU12)
+                                                                          : 6;
+            lds = std::max(lds, (size_t)(163840 / waves - 2560) & ~(size_t)1023);
+        }
         d.lds_words = (int32_t)(lds / 4);
         // the variant whose register slots hold the frame's working set (no spills at 6 or more
         // waves per SIMD)

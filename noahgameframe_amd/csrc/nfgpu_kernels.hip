@@ -548,7 +548,9 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     // of the tile's events as (first message, first player | slot, count | rank | public) triples
     // and the groups' player run; each event is then expanded by a group of L lanes (L = the
     // tile's largest recipient count rounded up to a power of two), so consecutive lane groups
-    // store consecutive events' runs: every store instruction covers one contiguous span.
+    // store consecutive events' runs.  Runs of 16 or more recipients are stored straight to HBM;
+    // shorter ones go through an LDS message window stored with 16-byte stores (short runs
+    // stored directly leave lines partly written by several waves).
     if (fuse) {
         __syncthreads();  // s_pb; every read of s_o and s_rem is done: the region is reused
         const unsigned mb = (unsigned)tile * d.msg_tcap;
@@ -569,12 +571,17 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         } else {
             const unsigned R = (unsigned)d.lds_words;
             const uint32_t pb_lo = s_pb[0], npl = s_pb[1] > s_pb[0] ? s_pb[1] - s_pb[0] : 0u;
-            const bool staged = npl <= R / 2;
-            const unsigned ecap = min(tev, (R - (staged ? npl : 0u)) / 3u);  // events per chunk
             const uint32_t nm = s_pb[2];
             const uint32_t L = nm <= 1 ? 1u : nm >= 64 ? 64u : 1u << (32 - __builtin_clz(nm - 1));
             const uint32_t sub = threadIdx.x & (L - 1);
+            const bool win = L < 16;
+            const bool staged = npl <= R / 4;
+            const unsigned room = R - (staged ? npl : 0u);
+            // events per chunk: all of them, or what leaves the window half of the room
+            const unsigned ecap = (min(tev, win ? room / 6u : room / 3u) + 3u) & ~3u;
+            const unsigned W = win ? (room - 3u * ecap) & ~3u : 0u;  // window entries
             uint32_t* s_ev = (uint32_t*)s_o;
+            uint32_t* s_win = s_ev + 3u * ecap;
             uint32_t* s_pl = s_ev + (R - npl);
             uint32_t* out = d.msg_rcpt + mb;
             if (staged) {
@@ -605,16 +612,51 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     }
                 }
                 __syncthreads();
-                for (uint32_t i = threadIdx.x / L; i < c1 - c0; i += kTPB / L) {
-                    const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
-                    const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
-                    if (!(b >> 31)) {  // private & !upload: the entity itself (n is 0 or 1)
-                        if (sub < n) out[ms] = a;
-                        continue;
+                if (!win) {
+                    for (uint32_t i = threadIdx.x / L; i < c1 - c0; i += kTPB / L) {
+                        const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
+                        const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
+                        if (!(b >> 31)) {  // private & !upload: the entity itself (n is 0 or 1)
+                            if (sub < n) out[ms] = a;
+                            continue;
+                        }
+                        for (uint32_t p = sub; p < n; p += L) {  // every player of the group but self
+                            const uint32_t pp = p + ((r1 && p + 1 >= r1) ? 1u : 0u);
+                            out[ms + p] = staged ? s_pl[a - pb_lo + pp] : (uint32_t)d.pl_slot[a + pp];
+                        }
                     }
-                    for (uint32_t p = sub; p < n; p += L) {  // every player of the group but self
-                        const uint32_t pp = p + ((r1 && p + 1 >= r1) ? 1u : 0u);
-                        out[ms + p] = staged ? s_pl[a - pb_lo + pp] : (uint32_t)d.pl_slot[a + pp];
+                } else {
+                    const unsigned last = 3u * (c1 - c0 - 1u);
+                    const unsigned m_lo = s_ev[0], m_hi = s_ev[last] + (s_ev[last + 2] & 0x3FFFu);
+                    for (unsigned w0 = m_lo; w0 < m_hi; w0 += W) {  // uniform
+                        const unsigned w1 = min(m_hi, w0 + W);
+                        for (uint32_t i = threadIdx.x / L; i < c1 - c0; i += kTPB / L) {
+                            const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
+                            const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
+                            if (ms >= w1 || ms + n <= w0) continue;
+                            if (!(b >> 31)) {
+                                if (sub < n) s_win[ms - w0] = a;
+                                continue;
+                            }
+                            for (uint32_t p = sub; p < n; p += L) {
+                                const uint32_t k = ms + p;
+                                if (k < w0 || k >= w1) continue;
+                                const uint32_t pp = p + ((r1 && p + 1 >= r1) ? 1u : 0u);
+                                s_win[k - w0] = staged ? s_pl[a - pb_lo + pp] : (uint32_t)d.pl_slot[a + pp];
+                            }
+                        }
+                        __syncthreads();
+                        const uint32_t n = w1 - w0;
+                        if ((w0 & 3u) == 0) {  // mb is a multiple of 4 (msg_tcap is): 16-byte stores
+                            const uint32_t n4 = n >> 2;
+                            uint4* dst4 = (uint4*)(out + w0);
+                            const uint4* src4 = (const uint4*)s_win;
+                            for (uint32_t i = threadIdx.x; i < n4; i += kTPB) dst4[i] = src4[i];
+                            if (threadIdx.x < (n & 3u)) out[w0 + 4 * n4 + threadIdx.x] = s_win[4 * n4 + threadIdx.x];
+                        } else {
+                            for (uint32_t i = threadIdx.x; i < n; i += kTPB) out[w0 + i] = s_win[i];
+                        }
+                        __syncthreads();
                     }
                 }
                 if (c1 < tev) __syncthreads();  // s_ev is refilled
