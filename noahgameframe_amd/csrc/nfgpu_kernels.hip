@@ -548,9 +548,10 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     // of the tile's events as (first message, first player | slot, count | rank | public) triples
     // and the groups' player run; each event is then expanded by a group of L lanes (L = the
     // tile's largest recipient count rounded up to a power of two), so consecutive lane groups
-    // store consecutive events' runs.  Runs of 16 or more recipients are stored straight to HBM;
-    // shorter ones go through an LDS message window stored with 16-byte stores (short runs
-    // stored directly leave lines partly written by several waves).
+    // store consecutive events' runs.  Runs of 16 or more recipients are stored that way straight
+    // to HBM; shorter ones are written one thread per event into an LDS message window stored
+    // with 16-byte stores (short runs stored directly leave lines partly written by several
+    // waves, and lane groups would re-read each event's triple once per lane).
     if (fuse) {
         __syncthreads();  // s_pb; every read of s_o and s_rem is done: the region is reused
         const unsigned mb = (unsigned)tile * d.msg_tcap;
@@ -630,19 +631,22 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     const unsigned m_lo = s_ev[0], m_hi = s_ev[last] + (s_ev[last + 2] & 0x3FFFu);
                     for (unsigned w0 = m_lo; w0 < m_hi; w0 += W) {  // uniform
                         const unsigned w1 = min(m_hi, w0 + W);
-                        for (uint32_t i = threadIdx.x / L; i < c1 - c0; i += kTPB / L) {
+                        // short runs: one thread per event (fewer LDS reads than lane groups)
+                        for (uint32_t i = threadIdx.x; i < c1 - c0; i += kTPB) {
                             const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
                             const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
-                            if (ms >= w1 || ms + n <= w0) continue;
+                            if (n == 0 || ms >= w1 || ms + n <= w0) continue;
                             if (!(b >> 31)) {
-                                if (sub < n) s_win[ms - w0] = a;
+                                s_win[ms - w0] = a;
                                 continue;
                             }
-                            for (uint32_t p = sub; p < n; p += L) {
-                                const uint32_t k = ms + p;
-                                if (k < w0 || k >= w1) continue;
-                                const uint32_t pp = p + ((r1 && p + 1 >= r1) ? 1u : 0u);
-                                s_win[k - w0] = staged ? s_pl[a - pb_lo + pp] : (uint32_t)d.pl_slot[a + pp];
+                            const uint32_t np = n + (r1 ? 1u : 0u);
+                            uint32_t k = ms;
+                            for (uint32_t p = 0; p < np; p++) {
+                                if (p + 1 == r1) continue;
+                                if (k >= w0 && k < w1)
+                                    s_win[k - w0] = staged ? s_pl[a - pb_lo + p] : (uint32_t)d.pl_slot[a + p];
+                                k++;
                             }
                         }
                         __syncthreads();
