@@ -54,6 +54,7 @@ constexpr unsigned kAblPerKind = 8;  // not an ablation: force the per-kind oper
 constexpr unsigned kAblWaves6 = 16, kAblWaves8 = 32;  // k_tick register budgets (outputs stay exact)
 constexpr unsigned kAblWaves5 = 8192;                  // (6 is the default)
 constexpr unsigned kAblNoRun = 512, kAblNoLoads = 1024, kAblNoEmit = 2048;  // timing only (k_tick)
+constexpr unsigned kAblScanInFrame = 131072;  // k_scan_tiles in every frame, not on first read
 constexpr unsigned kAblNoFuse = 4096;  // fan-out in k_fanout instead of k_tick's tail (outputs stay exact)
 
 // record op compiled from the kind programs, sorted by (rec, col)

@@ -138,6 +138,8 @@ struct World {
 
     int32_t ticks = 0;
     uint32_t last_tcap = 0;  // Dev::msg_tcap of the last launched frame
+    bool scan_pending = false;  // the last frame's dense ranks (k_scan_tiles) are built on first read
+    Dev scan_dev;               // ... with that frame's Dev
     int64_t last_rec_msgs = 0;  // record-tile messages of the last summarised frame (capacity hint)
     int32_t max_np = 0;    // most players in one scene group (an upper bound between full re-layouts)
 
@@ -1546,7 +1548,15 @@ int nfk_execute(void* world, int64_t now_ms) {
                            (const int32_t*)(S + off_qc), (const int64_t*)(S + off_qt), (int32_t)npost, d);
         HIPCHK(hipGetLastError());
     }
-    {
+    // Dense global ranks of the tile-staged outputs (ev_base, fi_base, totals): the frame's own
+    // work needs them only when k_fanout runs after it (record tiles, unfused property tiles).
+    // Otherwise the frame's outputs are complete as tiles + per-tile counts, and the ranks are
+    // built on the first read (nfk_summary_get, nfk_outputs_get, nfk_read_*).
+    w->scan_pending = false;
+    if (d.fuse_fan && !d.has_recops && !(d.ablate & kAblScanInFrame)) {
+        w->scan_pending = true;
+        w->scan_dev = d;
+    } else {
         TimeScope ts(w, KT_SCAN);
         hipLaunchKernelGGL(k_scan_tiles, dim3(5), dim3(kScanTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
@@ -1570,6 +1580,23 @@ int nfk_sync(void* world) {
     return NFK_OK;
 }
 
+static int ensure_ranks(World* w) {
+    if (!w->scan_pending) return NFK_OK;
+    w->scan_pending = false;
+    TimeScope ts(w, KT_SCAN);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(5), dim3(kScanTPB), 0, w->stream, w->scan_dev);
+    HIPCHK(hipGetLastError());
+    return NFK_OK;
+}
+
+static int read_ctrl(World* w, Ctrl* c) {
+    int r = ensure_ranks(w);
+    if (r) return r;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    HIPCHK(hipMemcpy(c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+    return NFK_OK;
+}
+
 // messages of the last frame: the runs are dense unless k_tick placed property tiles at a stride
 static int64_t frame_msgs(const World* w, const Ctrl& c) {
     if (!w->last_tcap) return (int64_t)c.msg_extent;
@@ -1580,9 +1607,11 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     World* w = (World*)world;
     if (!w || !out) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
-    HIPCHK(hipStreamSynchronize(w->stream));
     Ctrl c;
-    HIPCHK(hipMemcpy(&c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+    {
+        int r = read_ctrl(w, &c);
+        if (r) return r;
+    }
     memset(out, 0, sizeof *out);
     {
         int64_t live = 0;
@@ -1642,6 +1671,8 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     World* w = (World*)world;
     if (!w || !o) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    int r = ensure_ranks(w);  // (asynchronous, on the world's stream like the frame)
+    if (r) return r;
     const Dev& d = w->d;
     o->n_tiles = d.n_tiles; o->tile_slots = kTile;
     o->n_rtiles = d.has_recops ? d.n_rtiles : 0; o->rtile_slots = kRTile;
@@ -1653,12 +1684,6 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     o->fi_slot = d.fi_slot; o->fi_kind = d.fi_kind; o->fi_remain = d.fi_remain;
     o->msg_rcpt = d.msg_rcpt;
     o->slot_obj = w->slot_obj_d;
-    return NFK_OK;
-}
-
-static int read_ctrl(World* w, Ctrl* c) {
-    HIPCHK(hipStreamSynchronize(w->stream));
-    HIPCHK(hipMemcpy(c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
     return NFK_OK;
 }
 
