@@ -230,7 +230,7 @@ def main():
     d = kern[dom]
     achieved = d["alg_bytes_per_launch"] / (d["avg_us"] * 1e-6) / 1e9
     traffic, traffic_src = None, None
-    if os.path.exists(args.pmc_json):
+    if os.path.exists(args.pmc_json) and args.config == 1 and not migrating:  # (measured on config[1])
         try:
             pm = json.load(open(args.pmc_json))
             traffic = pm.get(dom, {}).get("hbm_bytes_per_launch")

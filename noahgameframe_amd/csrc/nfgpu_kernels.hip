@@ -828,10 +828,12 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
 
 // ---------------------------------------------------------------------------------
 // Record effects: one wave per 64-slot record tile, lane = row; the wave walks its slots in
-// order, four at a time with every cell load of the group issued before any is consumed.
+// order, kGroup at a time with every cell load of the group issued before any is consumed.
 // Cells [cap][cols][rows] so a wave reads one (slot, col) row-vector contiguously.
-constexpr int kRecGroup = 4;
 
+// kOps: register slots for the record ops (>= n_rops), kGroup: slots whose cells are in flight
+// together; instantiated so that a frame's op count does not pay for NFK_MAX_OPS registers.
+template <int kOps, int kGroup>
 __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
     for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
@@ -858,22 +860,22 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     unsigned pos = 0, pmsg = 0;  // tile-local
     const size_t re0 = (size_t)rt * d.re_tcap;
     while (work) {
-        // next group of up to kRecGroup slots with record work, in slot order; every cell load of
+        // next group of up to kGroup slots with record work, in slot order; every cell load of
         // the group is issued before any is consumed
-        int js[kRecGroup];
-        uint32_t masks[kRecGroup];
-        uint64_t used[kRecGroup][NFK_MAX_OPS];
-        uint64_t cur[kRecGroup][NFK_MAX_OPS];
+        int js[kGroup];
+        uint32_t masks[kGroup];
+        uint64_t used[kGroup][kOps];
+        uint64_t cur[kGroup][kOps];
 #pragma unroll
-        for (int g = 0; g < kRecGroup; g++) {
+        for (int g = 0; g < kGroup; g++) {
             js[g] = work ? __builtin_ctzll(work) : -1;
             if (work) work &= work - 1;
             masks[g] = js[g] >= 0 ? (uint32_t)__shfl((int)my_mask, js[g], 64) : 0u;
         }
 #pragma unroll
-        for (int g = 0; g < kRecGroup; g++)
+        for (int g = 0; g < kGroup; g++)
 #pragma unroll
-            for (int j = 0; j < NFK_MAX_OPS; j++) {
+            for (int j = 0; j < kOps; j++) {
                 used[g][j] = 0;
                 cur[g][j] = 0;
                 if (j < nro && js[g] >= 0 && ((masks[g] >> d.rops[j].kind) & 1)) {
@@ -884,15 +886,15 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                 }
             }
 #pragma unroll
-        for (int g = 0; g < kRecGroup; g++) {
+        for (int g = 0; g < kGroup; g++) {
             if (js[g] < 0) break;
             const int e = s0 + js[g];
             const uint64_t desc = (uint64_t)__shfl((long long)my_desc, js[g], 64);
             const unsigned cls = (unsigned)(desc >> 60);
-            bool ch[NFK_MAX_OPS];
-            uint64_t nv[NFK_MAX_OPS];
+            bool ch[kOps];
+            uint64_t nv[kOps];
 #pragma unroll
-            for (int j = 0; j < NFK_MAX_OPS; j++) {
+            for (int j = 0; j < kOps; j++) {
                 ch[j] = false;
                 nv[j] = 0;
                 if (j >= nro || !((masks[g] >> d.rops[j].kind) & 1)) continue;
@@ -926,19 +928,19 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             }
             // per-slot event order (rec, row, col): records outer, lanes (rows), cols inner
 #pragma unroll
-            for (int j0 = 0; j0 < NFK_MAX_OPS; j0++) {
+            for (int j0 = 0; j0 < kOps; j0++) {
                 if (j0 >= nro || d.rops[j0].gfirst != j0) continue;  // j0 opens a record's op span
                 const int j1 = d.rops[j0].glast;
                 unsigned c = 0;
 #pragma unroll
-                for (int j = 0; j < NFK_MAX_OPS; j++) c += (j >= j0 && j <= j1 && ch[j]) ? 1 : 0;
+                for (int j = 0; j < kOps; j++) c += (j >= j0 && j <= j1 && ch[j]) ? 1 : 0;
                 const unsigned inc = wave_incl_scan_u32(c);
                 const unsigned n = (unsigned)__shfl((int)inc, 63, 64);
                 if (n == 0) continue;  // wave-uniform
                 unsigned p = pos + inc - c;
                 const unsigned per = event_msgs(desc, s_rflags[cls][d.rops[j0].rec]);
 #pragma unroll
-                for (int j = 0; j < NFK_MAX_OPS; j++) {
+                for (int j = 0; j < kOps; j++) {
                     if (!(j >= j0 && j <= j1 && ch[j])) continue;
                     const size_t at = re0 + p;
                     d.re_slot[at] = (uint32_t)e;
