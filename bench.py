@@ -49,8 +49,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--migrate", type=int, default=256,
-                   help="N>1: entities per rank per frame that SwitchScene into the next rank's scene "
-                        "(state rows over RCCL all_to_all; BASELINE config[2])")
+                   help="N>1: entities per rank that SwitchScene into the next rank's scene every "
+                        "--migrate-every frames (state rows over RCCL all_to_all; BASELINE config[2])")
+    p.add_argument("--migrate-every", type=int, default=8,
+                   help="frames between migration batches (8 = 256 entities per GPU every 0.8 s)")
     p.add_argument("--slack", type=int, default=None, help="free slots per 256 scene-group members")
     p.add_argument("--config", type=int, default=1, choices=[1, 3, 4],
                    help="BASELINE config: 1 = 1M entities/GPU (the metric's configuration; with --gpus > 1 "
@@ -91,43 +93,58 @@ def cpu_baseline(args, w_full):
 
 
 class Migration:
-    """BASELINE config[2]: every frame each rank's game logic sends `per_frame` of its entities
-    into the next rank's scene (SwitchScene across shards, same group id, new position).  The
-    frame's tickets are decided and all-gathered over a gloo group while the previous frame runs on
-    the GPU; at the frame start the state rows travel GPU-to-GPU with one RCCL all_to_all."""
+    """BASELINE config[2]: every `every`-th frame each rank's game logic sends `per_frame` of its
+    entities into the next rank's scene (SwitchScene across shards, same group id, new position).
+    The tickets (one int64 array, shard.TICKET_COLS) are decided and all-gathered over a gloo group
+    while the previous frame runs on the GPU; at the frame start the state rows travel GPU-to-GPU
+    with one RCCL all_to_all.  Frames without migrations make no collective call at all."""
 
-    def __init__(self, m, w, rank, world, per_frame, dev):
-        import numpy as np
+    def __init__(self, m, w, rank, world, per_frame, every, dev):
         import torch.distributed as dist
-        from collections import deque
         from noahgameframe_amd.shard import SceneShard
-        self.np, self.dist = np, dist
+        self.dist = dist
         self.meta = dist.new_group(backend="gloo")
         own = lambda scene: int(scene) - 1
         self.shard = SceneShard(m, rank, world, own, w["scene_props"], group=dist.group.WORLD,
                                 meta_group=self.meta, device=dev)
-        self.rank, self.world, self.per_frame = rank, world, per_frame
-        # entities this rank owns: (guid head, guid data, group, cls, is_player), oldest first
-        self.owned = deque(zip(w["guid_head"].tolist(), w["guid_data"].tolist(), w["group"].tolist(),
-                               w["cls"].tolist(), w["is_player"].tolist()))
+        self.rank, self.world, self.per_frame, self.every = rank, world, per_frame, max(1, every)
+        # entities this rank owns (guid head, guid data, group, cls, is_player), oldest first
+        self.owned = np.stack([w["guid_head"], w["guid_data"], w["group"], w["cls"], w["is_player"]],
+                              axis=1).astype(np.int64)
+        self.head = 0
         self.rng = np.random.default_rng(77 + rank)
+        self.frames = 0
         self.plan = None
         self.after_frame()
 
     def before_frame(self):
-        recv = self.shard.migrate([], plan=self.plan)
-        for t in recv:
-            self.owned.append((t.guid_head, t.guid_data, t.group, t.cls, t.is_player))
+        from noahgameframe_amd.shard import T_GH, T_GD, T_GROUP, T_CLS, T_PL
+        if self.plan is not None:
+            recv = self.shard.migrate_array(self.plan)
+            if len(recv):
+                self.owned = np.concatenate([self.owned[self.head:],
+                                             recv[:, [T_GH, T_GD, T_GROUP, T_CLS, T_PL]]])
+                self.head = 0
+        self.plan = None
 
     def after_frame(self):
-        from noahgameframe_amd.shard import Ticket
+        """The next frame's tickets (only on every `every`-th frame, the same frames on every rank)."""
+        from noahgameframe_amd.shard import T_GH, T_GD, T_CLS, T_PL, T_SCENE, T_GROUP, T_X, T_Y, T_Z, T_SRC, T_DST
+        self.frames += 1
+        if self.frames % self.every:
+            return
         dst = (self.rank + 1) % self.world
-        out = []
-        for _ in range(min(self.per_frame, len(self.owned))):
-            gh, gd, gr, cl, pl = self.owned.popleft()
-            x, y = self.rng.uniform(-500, 500, 2)
-            out.append(Ticket(gh, gd, cl, pl, dst + 1, gr, float(x), float(y), 0.0, self.rank, dst))
-        self.plan = self.shard._exchange_tickets(out)
+        n = min(self.per_frame, len(self.owned) - self.head)
+        o = self.owned[self.head:self.head + n]
+        self.head += n
+        out = np.zeros((n, 11), np.int64)
+        out[:, T_GH], out[:, T_GD], out[:, T_GROUP], out[:, T_CLS], out[:, T_PL] = o[:, 0], o[:, 1], o[:, 2], o[:, 3], o[:, 4]
+        out[:, T_SCENE] = dst + 1
+        xy = self.rng.uniform(-500, 500, (n, 2)).astype(np.float32).astype(np.float64)
+        out[:, T_X], out[:, T_Y] = xy[:, 0].view(np.int64), xy[:, 1].view(np.int64)
+        out[:, T_Z] = np.zeros(n, np.float64).view(np.int64)
+        out[:, T_SRC], out[:, T_DST] = self.rank, dst
+        self.plan = self.shard.exchange_ticket_array(out)
 
 
 def main():
@@ -183,7 +200,7 @@ def main():
     tick = 0
     mig = None
     if migrating:
-        mig = Migration(m, w, rank, world, args.migrate, dev)
+        mig = Migration(m, w, rank, world, args.migrate, args.migrate_every, dev)
 
     def frame():
         nonlocal tick
@@ -246,15 +263,16 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "int64/f64", "data": "synthetic",
         "config": {"workload": CONFIG_NAMES[args.config] if args.config != 1 else (
                                f"BASELINE config[2]: {world} scene shards (scene r+1 on GPU r), "
-                                f"{args.migrate} SwitchScene migrations per rank per frame into the next "
-                                "shard (state rows over RCCL all_to_all); per GPU: " if migrating else
+                                f"{args.migrate} SwitchScene migrations per rank every {args.migrate_every} "
+                                "frames into the next shard (state rows over RCCL all_to_all); per GPU: "
+                                if migrating else
                                 "BASELINE config[1]: ") + "1M NPC/Player entities per GPU in one scene, "
                                f"{args.groups} groups x {args.entities // args.groups}, "
                                f"{args.players_per_group} players/group, heartbeats HPRegen 1s/MPRegen 2s/"
                                f"Move 0.1s/Patrol 3s/Poison 0.5s, {args.tick_ms} ms frames",
                    "entities_per_gpu": args.entities, "groups": args.groups,
                    "players_per_group": args.players_per_group, "parallelism": f"scene-shard x{world}",
-                   "migrations_per_rank_per_frame": args.migrate if migrating else 0},
+                   "migrations_per_rank_per_frame": args.migrate / args.migrate_every if migrating else 0},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src},

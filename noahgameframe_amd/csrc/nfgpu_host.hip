@@ -95,6 +95,12 @@ struct World {
     void* mlist = nullptr;         // device copy of the membership lists
     size_t mlist_cap = 0;
     std::vector<char> mhost;       // host staging of the membership lists
+    // pinned double buffer the lists are uploaded from, so no upload waits for the stream
+    char* mpin[2] = {nullptr, nullptr};
+    size_t mpin_cap[2] = {0, 0};
+    hipEvent_t mpin_done[2] = {nullptr, nullptr};
+    bool mpin_pending[2] = {false, false};
+    int mpin_slot = 0;
     uint64_t* fan_desc_w = nullptr;
     int32_t* pl_slot_w = nullptr;
     int64_t n_relayout_full = 0, n_relayout_seg = 0;
@@ -378,6 +384,32 @@ int dev_reserve(World* w, void** p, size_t* cap, size_t bytes) {
     return NFK_OK;
 }
 
+// w->mhost -> w->mlist, asynchronously on the world's stream (through a pinned double buffer:
+// a buffer is refilled only once the copy from it two uploads ago has completed)
+int upload_mhost(World* w) {
+    int r = dev_reserve(w, &w->mlist, &w->mlist_cap, w->mhost.size() + 16);
+    if (r) return r;
+    const int s = w->mpin_slot;
+    w->mpin_slot ^= 1;
+    if (w->mpin_pending[s]) {
+        HIPCHK(hipEventSynchronize(w->mpin_done[s]));
+        w->mpin_pending[s] = false;
+    }
+    if (w->mhost.size() > w->mpin_cap[s]) {
+        if (w->mpin[s]) HIPCHK(hipHostFree(w->mpin[s]));
+        w->mpin[s] = nullptr;
+        const size_t c = std::max(w->mhost.size(), 2 * w->mpin_cap[s]);
+        HIPCHK(hipHostMalloc((void**)&w->mpin[s], c, hipHostMallocDefault));
+        w->mpin_cap[s] = c;
+    }
+    if (w->mhost.empty()) return NFK_OK;
+    memcpy(w->mpin[s], w->mhost.data(), w->mhost.size());
+    HIPCHK(hipMemcpyAsync(w->mlist, w->mpin[s], w->mhost.size(), hipMemcpyHostToDevice, w->stream));
+    HIPCHK(hipEventRecord(w->mpin_done[s], w->stream));
+    w->mpin_pending[s] = true;
+    return NFK_OK;
+}
+
 template <typename T>
 size_t stage_list(World* w, const std::vector<T>& v) {
     const size_t off = align16(w->mhost.size());
@@ -501,11 +533,10 @@ int apply_membership(World* w) {
     const size_t o_ps = stage_list(w, pack_src), o_ud = stage_list(w, un_dst), o_us = stage_list(w, un_src);
     const size_t o_ms = stage_list(w, m.slot), o_mo = stage_list(w, m.obj), o_md = stage_list(w, m.desc);
     const size_t o_mp = stage_list(w, m.pl);
-    int r = dev_reserve(w, &w->mlist, &w->mlist_cap, w->mhost.size() + 16);
+    int r = dev_reserve(w, (void**)&w->mv_rows, &w->mv_cap, std::max<size_t>(pack_src.size(), 1) * rw * 8);
     if (r) return r;
-    r = dev_reserve(w, (void**)&w->mv_rows, &w->mv_cap, std::max<size_t>(pack_src.size(), 1) * rw * 8);
+    r = upload_mhost(w);
     if (r) return r;
-    HIPCHK(hipMemcpyAsync(w->mlist, w->mhost.data(), w->mhost.size(), hipMemcpyHostToDevice, w->stream));
     char* L = (char*)w->mlist;
     if (!pack_src.empty())
         hipLaunchKernelGGL(k_pack, dim3(grid_for(pack_src.size() * rw)), dim3(kTPB), 0, w->stream, d,
@@ -520,8 +551,6 @@ int apply_membership(World* w) {
                            (const int32_t*)(L + o_mp), (int32_t)m.slot.size(), w->slot_obj_d, w->fan_desc_w,
                            w->pl_slot_w);
     HIPCHK(hipGetLastError());
-    // the pageable staging must outlive the copy
-    HIPCHK(hipStreamSynchronize(w->stream));
 
     // host maps
     if (full) {
@@ -608,7 +637,9 @@ int nfk_create(const nfk_config* cfg, void** out) {
         }
         w->own_stream = true;
     }
-    if (hipEventCreateWithFlags(&w->pin_done, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&w->pin_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->mpin_done[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->mpin_done[1], hipEventDisableTiming) != hipSuccess) {
         delete w;
         return fail(NFK_ERR_HIP, "hipEventCreate failed");
     }
@@ -637,6 +668,10 @@ int nfk_destroy(void* world) {
     }
     for (auto e : w->evpool) (void)hipEventDestroy(e);
     if (w->pin_done) (void)hipEventDestroy(w->pin_done);
+    for (int i = 0; i < 2; i++) {
+        if (w->mpin_done[i]) (void)hipEventDestroy(w->mpin_done[i]);
+        if (w->mpin[i]) (void)hipHostFree(w->mpin[i]);
+    }
     if (w->own_stream) (void)hipStreamDestroy(w->stream);
     delete w;
     return NFK_OK;
@@ -1226,13 +1261,11 @@ int nfk_export_objects(void* world, int32_t n, const int64_t* gh, const int64_t*
     }
     w->mhost.clear();
     const size_t o_src = stage_list(w, src);
-    int r = dev_reserve(w, &w->mlist, &w->mlist_cap, w->mhost.size() + 16);
+    int r = upload_mhost(w);
     if (r) return r;
-    HIPCHK(hipMemcpyAsync(w->mlist, w->mhost.data(), w->mhost.size(), hipMemcpyHostToDevice, w->stream));
     hipLaunchKernelGGL(k_pack, dim3(grid_for((size_t)n * w->row_words)), dim3(kTPB), 0, w->stream, w->d,
                        (const int32_t*)((char*)w->mlist + o_src), n, w->row_words, rows_dev);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(w->stream));  // the pageable staging must outlive the copy
     for (int32_t i = 0; i < n; i++) {
         w->obj_of.erase(GuidKey{gh[i], gd[i]});
         w->alive[objs[i]] = 0;

@@ -36,6 +36,27 @@ class Ticket:
     dst: int = -1   # destination rank
 
 
+# A batch of tickets as one int64 array [n, 11] (x, y, z as float64 bit patterns): the form the
+# per-frame exchange moves, so a frame's migration costs a few array operations, not n objects.
+TICKET_COLS = ("guid_head", "guid_data", "cls", "is_player", "scene", "group", "x", "y", "z", "src", "dst")
+T_GH, T_GD, T_CLS, T_PL, T_SCENE, T_GROUP, T_X, T_Y, T_Z, T_SRC, T_DST = range(11)
+
+
+def tickets_to_array(tickets):
+    a = np.zeros((len(tickets), 11), np.int64)
+    for i, t in enumerate(tickets):
+        a[i] = (t.guid_head, t.guid_data, t.cls, t.is_player, t.scene, t.group, _f64(t.x).view(np.int64),
+                _f64(t.y).view(np.int64), _f64(t.z).view(np.int64), t.src, t.dst)
+    return a
+
+
+def array_to_tickets(a):
+    f = a[:, T_X:T_Z + 1].copy().view(np.float64)
+    return [Ticket(int(r[T_GH]), int(r[T_GD]), int(r[T_CLS]), int(r[T_PL]), int(r[T_SCENE]), int(r[T_GROUP]),
+                   float(f[i, 0]), float(f[i, 1]), float(f[i, 2]), int(r[T_SRC]), int(r[T_DST]))
+            for i, r in enumerate(a)]
+
+
 def scene_ranges(scenes, world_size):
     """Contiguous scene ranges, one per rank: returns owner(scene) -> rank."""
     scenes = sorted(set(int(s) for s in scenes))
@@ -84,49 +105,68 @@ class SceneShard:
         dist.all_gather_object(allt, out, group=self.meta_pg)
         return [t for lst in allt for t in lst]
 
+    def exchange_ticket_array(self, out):
+        """All-gather every rank's outgoing ticket array over the meta group (counts first, then
+        the rows padded to the largest count); returns the global plan in (source rank, call) order."""
+        torch = self.torch
+        import torch.distributed as dist
+        out = np.ascontiguousarray(out, np.int64).reshape(-1, 11)
+        n = torch.tensor([len(out)], dtype=torch.int64)
+        ns = [torch.zeros(1, dtype=torch.int64) for _ in range(self.ws)]
+        dist.all_gather(ns, n, group=self.meta_pg)
+        ns = [int(x.item()) for x in ns]
+        mx = max(ns)
+        if mx == 0:
+            return np.zeros((0, 11), np.int64)
+        pad = torch.zeros((mx, 11), dtype=torch.int64)
+        pad[:len(out)] = torch.from_numpy(out)
+        allp = [torch.zeros((mx, 11), dtype=torch.int64) for _ in range(self.ws)]
+        dist.all_gather(allp, pad, group=self.meta_pg)
+        return np.concatenate([a[:c].numpy() for a, c in zip(allp, ns)])
+
     def migrate(self, out, plan=None):
         """Collective (every rank calls it once per frame, possibly with nothing to send).
         `out`: this rank's outgoing tickets.  `plan`: optionally the frame's global ticket list in
         (source rank, call) order, known to every rank; otherwise tickets are all-gathered over
         the meta group.  Returns the tickets this rank received."""
-        torch = self.torch
         tickets = plan if plan is not None else self._exchange_tickets(out)
-        send = [t for t in tickets if t.src == self.rank]
-        recv = [t for t in tickets if t.dst == self.rank]
-        send.sort(key=lambda t: t.dst)   # stable: call order within a destination
-        recv.sort(key=lambda t: t.src)
-        scount = [0] * self.ws
-        rcount = [0] * self.ws
-        for t in send:
-            scount[t.dst] += 1
-        for t in recv:
-            rcount[t.src] += 1
-        if not tickets:   # the same decision on every rank: the collective below is skipped by all
-            return []
+        return array_to_tickets(self.migrate_array(tickets_to_array(tickets)))
+
+    def migrate_array(self, plan):
+        """migrate() on a ticket array (TICKET_COLS) holding the frame's global plan in (source
+        rank, call) order; returns this rank's received tickets as an array."""
+        torch = self.torch
+        plan = np.asarray(plan, np.int64).reshape(-1, 11)
+        if len(plan) == 0:   # the same decision on every rank: the collective below is skipped by all
+            return plan
+        send = plan[plan[:, T_SRC] == self.rank]
+        recv = plan[plan[:, T_DST] == self.rank]
+        send = send[np.argsort(send[:, T_DST], kind="stable")]   # call order within a destination
+        recv = recv[np.argsort(recv[:, T_SRC], kind="stable")]
+        scount = np.bincount(send[:, T_DST], minlength=self.ws)
+        rcount = np.bincount(recv[:, T_SRC], minlength=self.ws)
         rw = self.rw
         sbuf = torch.empty((len(send), rw), dtype=torch.int64, device=self.device)
-        if send:
-            self.m.export_objects([t.guid_head for t in send], [t.guid_data for t in send], sbuf.data_ptr())
+        if len(send):
+            self.m.export_objects(send[:, T_GH], send[:, T_GD], sbuf.data_ptr())
         if self.device.type == "cuda" and self.m.stream != torch.cuda.current_stream(self.device).cuda_stream:
             self.m.synchronize()   # the rows were packed on the world's own stream
         rbuf = torch.empty((len(recv), rw), dtype=torch.int64, device=self.device)
-        self._all_to_all(rbuf, sbuf, [c * rw for c in rcount], [c * rw for c in scount])
-        if recv:
-            self.m.import_objects([t.guid_head for t in recv], [t.guid_data for t in recv],
-                                  [t.scene for t in recv], [t.group for t in recv], [t.cls for t in recv],
-                                  [t.is_player for t in recv], rbuf.data_ptr())
-            # the SwitchScene property writes (KM:930-942); the scene always changes here
-            gh, gd, pid, bits = [], [], [], []
-            for t in recv:
-                for p, b in ((self.pid_group, 0), (self.pid_scene, t.scene),
-                             (self.pid_x, _f64(t.x)), (self.pid_y, _f64(t.y)), (self.pid_z, _f64(t.z)),
-                             (self.pid_group, t.group)):
-                    if p >= 0:
-                        gh.append(t.guid_head)
-                        gd.append(t.guid_data)
-                        pid.append(p)
-                        bits.append(np.int64(b).view(np.uint64) if not isinstance(b, np.uint64) else b)
-            self.m.set_props(gh, gd, pid, np.array(bits, np.uint64))
+        self._all_to_all(rbuf, sbuf, [int(c) * rw for c in rcount], [int(c) * rw for c in scount])
+        if len(recv):
+            self.m.import_objects(recv[:, T_GH], recv[:, T_GD], recv[:, T_SCENE], recv[:, T_GROUP], recv[:, T_CLS],
+                                  recv[:, T_PL], rbuf.data_ptr())
+            # the SwitchScene property writes (KM:930-942), per entity in this order; the scene
+            # always changes here
+            cols = [(self.pid_group, np.zeros(len(recv), np.int64)), (self.pid_scene, recv[:, T_SCENE]),
+                    (self.pid_x, recv[:, T_X]), (self.pid_y, recv[:, T_Y]), (self.pid_z, recv[:, T_Z]),
+                    (self.pid_group, recv[:, T_GROUP])]
+            cols = [(p, v) for p, v in cols if p >= 0]
+            if cols:
+                k = len(cols)
+                self.m.set_props(np.repeat(recv[:, T_GH], k), np.repeat(recv[:, T_GD], k),
+                                 np.tile(np.array([p for p, _ in cols], np.int32), len(recv)),
+                                 np.stack([v for _, v in cols], axis=1).reshape(-1).view(np.uint64))
         self.migrated_out += len(send)
         self.migrated_in += len(recv)
         return recv

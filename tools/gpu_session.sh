@@ -33,6 +33,9 @@ for step in "$@"; do
     bench2g) run bench2g 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                --master-port 29561 bench.py --gpus 2 --steps 20 --warmup 3 --backend gloo --cpu-baseline off \
                --entities 262144 --groups 1024 --migrate 128 ;;
+    bench2g1) run bench2g1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+               --master-port 29562 bench.py --gpus 2 --steps 20 --warmup 3 --backend gloo --cpu-baseline off \
+               --entities 262144 --groups 1024 --migrate 128 --migrate-every 1 ;;
     ablate) run ablate 600 python tools/ablate.py --variants ${ABL:-0,8,4} ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
              python bench.py --steps 50 --warmup 5 --cpu-baseline off ;;
