@@ -202,13 +202,23 @@ def main():
     if migrating:
         mig = Migration(m, w, rank, world, args.migrate, args.migrate_every, dev)
 
+    trace = {} if os.environ.get("NFGPU_BENCH_TRACE") else None  # host seconds per phase (stderr)
+
+    def timed(name, fn):
+        if trace is None:
+            return fn()
+        t = time.perf_counter()
+        r = fn()
+        trace[name] = trace.get(name, 0.0) + time.perf_counter() - t
+        return r
+
     def frame():
         nonlocal tick
         if mig:
-            mig.before_frame()
-        m.Execute(t0 + tick * args.tick_ms)
+            timed("migrate", mig.before_frame)
+        timed("execute", lambda: m.Execute(t0 + tick * args.tick_ms))
         if mig:
-            mig.after_frame()   # next frame's tickets, exchanged while this frame runs on the GPU
+            timed("tickets", mig.after_frame)   # next frame's tickets, exchanged while this frame runs on the GPU
         tick += 1
 
     for _ in range(args.warmup):
@@ -223,6 +233,10 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - ts
+    if trace is not None:
+        print(json.dumps({"rank": rank, "host_ms_per_frame": {k: 1000 * v / (args.warmup + args.steps)
+                                                              for k, v in trace.items()},
+                          "frame_ms": 1000 * elapsed / args.steps}), file=sys.stderr, flush=True)
     s = m.summary()
     # ... then the same number of frames again with HIP events around every kernel, for the
     # per-kernel durations and algorithmic bytes of the roofline
