@@ -152,6 +152,7 @@ struct Dev {
     uint64_t* u_col[kMaxU];   // property of slot e at u_col[j][e * u_str[j]]
     int32_t u_str[kMaxU];
     int32_t u_order[kMaxW];
+    uint64_t u_cf[kMaxW];     // property flags of writable slot j by class: 4 bits per class id
     const uint8_t* u_slot;  // [n_prop], only when n_x > 0
     // tiles: property/fired tile t = slots [t*kTile, (t+1)*kTile); record tile r = slots
     // [r*kRTile, (r+1)*kRTile).  Outputs of a tile sit at [t*tile_cap, t*tile_cap + count).
@@ -234,6 +235,8 @@ __host__ __device__ __forceinline__ bool desc_dead(uint64_t desc) { return (desc
 
 // Recipients of one dirty event (NFCSceneAOIModule::GetBroadCastObject, AOI:531-593):
 // public -> every player of the group but self; private && !upload -> self; else none.
+// flags of writable slot j's property for class cls, from the kernel-argument table (Dev::u_cf)
+__device__ __forceinline__ uint8_t u_flags(uint64_t cf, unsigned cls) { return (uint8_t)((cf >> (4 * cls)) & 0xF); }
 __device__ __forceinline__ unsigned event_msgs(uint64_t desc, uint8_t fl) {
     if (fl & NFK_PUBLIC) {
         const unsigned np = (unsigned)((desc >> 32) & 0x3FFF);

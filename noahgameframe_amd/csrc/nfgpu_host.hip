@@ -1458,6 +1458,12 @@ int nfk_execute(void* world, int64_t now_ms) {
             d.u_col[j] = p < 0 ? nullptr : d.pmem + w->tab.p_off[p];
             d.u_str[j] = p < 0 ? 0 : w->tab.p_str[p];
         }
+        for (int j = 0; j < kMaxW; j++) {  // property flags by class, read by k_tick as scalars
+            d.u_cf[j] = 0;
+            if (j < n_w)
+                for (int c = 0; c < NFK_MAX_CLASSES; c++)
+                    d.u_cf[j] |= (uint64_t)(w->tab.pflags[c][d.u_pid[j]] & 0xF) << (4 * c);
+        }
     }
     if (!use_u) uslot.clear();
 

@@ -320,54 +320,72 @@ constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: 
 
 // NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
 // order).  The hot records of a chunk of kinds are loaded together (independent 16 B loads).
-// Returns the fired-kind mask; rescheduled / removed records are stored back.
-__device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& bytes, int32_t* s_rem = nullptr) {
-    uint32_t fired = 0;
-    bool taken = false;  // std::map remove-list key already owned (SM:68)
-    if (d.has_pre) {
-        taken = d.e_flags[e] & 1;
-        bytes += 1;
+// Rescheduled / removed records are stored back.  Every load is issued without a branch and before
+// the first use of any of them: a load under a branch is followed by a wait at the join, and a
+// first use after the record stores would make the wave wait for the stores too (the vector
+// memory counter retires in order), i.e. one round trip per kind or per store batch.
+template <bool kFirst>
+__device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigned& bytes, uint64_t& desc,
+                                            bool& dead, bool& taken, uint32_t& fired, int32_t* s_rem,
+                                            bool oob) {
+    SchedHot h[kKindChunk];
+    // kinds past n_kind re-read the chunk's first record (a cache hit)
+    const SchedHot* base = d.s_hot + (size_t)k0 * d.cap + e;
+    const int nk = d.n_kind - k0;
+#pragma unroll
+    for (int j = 0; j < kKindChunk; j++) h[j] = base[(size_t)(j < nk ? j : 0) * d.cap];
+    if constexpr (kFirst) {
+        desc = d.fan_desc[e];
+        const uint8_t ef = d.e_flags[e];  // (always allocated)
+        __builtin_amdgcn_sched_barrier(0);  // the scheduler would hoist the first use and its wait
+        dead = oob || desc_dead(desc);  // a slack slot has no schedules; dead slots store nothing
+        taken = d.has_pre && (ef & 1);  // std::map remove-list key already owned (SM:68)
+        bytes += d.has_pre ? 1 : 0;
     }
-    for (int k0 = 0; k0 < d.n_kind; k0 += kKindChunk) {
-        SchedHot h[kKindChunk];
 #pragma unroll
-        for (int j = 0; j < kKindChunk; j++)
-            if (k0 + j < d.n_kind) h[j] = d.s_hot[(size_t)(k0 + j) * d.cap + e];
-#pragma unroll
-        for (int j = 0; j < kKindChunk; j++) {
-            const int k = k0 + j;
-            if (k >= d.n_kind) break;
-            bytes += 16;
-            if (!(h[j].state & kStPresent) || !(d.now > h[j].next)) continue;
-            const bool forever = h[j].state & kStForever;
-            if (!(h[j].remain > 0 || forever)) continue;
-            h[j].remain -= 1;
-            fired |= 1u << k;
-            const uint32_t st = h[j].state;
-            if (h[j].remain <= 0 && !forever) {
-                if (!taken) {  // insert into the remove list succeeds for the first one only
-                    h[j].state = 0;
-                    taken = true;
-                }
-            } else {
-                const bool first = !(st & kStFired);
-                if ((st & kStStep) && (first || !forever || h[j].remain < 0)) {
-                    // next = start + step * (all - remain) without the cold record (see kSt*)
-                    if (!first) h[j].next += st_step(st);
-                } else {
-                    const SchedCold c = d.s_cold[(size_t)k * d.cap + e];
-                    bytes += 16;
-                    const int64_t step = (int64_t)(c.interval * 1000.0f);
-                    const int32_t done = (int32_t)((uint32_t)c.all - (uint32_t)h[j].remain);
-                    h[j].next = c.start + step * (int64_t)done;
-                }
-                h[j].state = st | kStFired;
+    for (int j = 0; j < kKindChunk; j++) {
+        const int k = k0 + j;
+        if (k >= d.n_kind) break;
+        bytes += 16;
+        if (dead || !(h[j].state & kStPresent) || !(d.now > h[j].next)) continue;
+        const bool forever = h[j].state & kStForever;
+        if (!(h[j].remain > 0 || forever)) continue;
+        h[j].remain -= 1;
+        fired |= 1u << k;
+        const uint32_t st = h[j].state;
+        if (h[j].remain <= 0 && !forever) {
+            if (!taken) {  // insert into the remove list succeeds for the first one only
+                h[j].state = 0;
+                taken = true;
             }
-            d.s_hot[(size_t)k * d.cap + e] = h[j];
-            if (s_rem) s_rem[k * kTPB + threadIdx.x] = h[j].remain;  // for the fired list
-            bytes += 16;
+        } else {
+            const bool first = !(st & kStFired);
+            if ((st & kStStep) && (first || !forever || h[j].remain < 0)) {
+                // next = start + step * (all - remain) without the cold record (see kSt*)
+                if (!first) h[j].next += st_step(st);
+            } else {
+                const SchedCold c = d.s_cold[(size_t)k * d.cap + e];
+                bytes += 16;
+                const int64_t step = (int64_t)(c.interval * 1000.0f);
+                const int32_t done = (int32_t)((uint32_t)c.all - (uint32_t)h[j].remain);
+                h[j].next = c.start + step * (int64_t)done;
+            }
+            h[j].state = st | kStFired;
         }
+        d.s_hot[(size_t)k * d.cap + e] = h[j];
+        if (s_rem) s_rem[k * kTPB + threadIdx.x] = h[j].remain;  // for the fired list
+        bytes += 16;
     }
+}
+// Loads desc = fan_desc[e] with the first chunk; returns the fired-kind mask.  oob: a slot past N
+// (e is then a valid slot re-read, treated as dead).
+__device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& bytes, uint64_t& desc,
+                                               int32_t* s_rem = nullptr, bool oob = false) {
+    uint32_t fired = 0;
+    bool dead = true, taken = false;
+    sched_chunk<true>(d, e, 0, bytes, desc, dead, taken, fired, s_rem, oob);
+    for (int k0 = kKindChunk; k0 < d.n_kind; k0 += kKindChunk)
+        sched_chunk<false>(d, e, k0, bytes, desc, dead, taken, fired, s_rem, oob);
     return fired;
 }
 
@@ -388,7 +406,6 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     __shared__ unsigned s_bytes;
     __shared__ uint32_t s_pb[3];   // pl_slot run of the groups with dirty events [lo, hi), most recipients
     extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
-    __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     const int tile = blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
     const bool fuse = d.msg_tcap != 0;  // this tile's fan-out is written here, at tile * msg_tcap
@@ -398,11 +415,6 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         s_pb[1] = 0;
         s_pb[2] = 1;
     }
-    {
-        const int words = d.n_class * (NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS) / 4;
-        for (int i = threadIdx.x; i < words; i += kTPB)
-            ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
-    }
     int32_t* s_rem = (int32_t*)(s_o + (size_t)d.n_w * kTPB);  // [n_kind][kTPB] remain after a fire
     unsigned bytes = 0;
     uint32_t fired = 0, xh = 0, wm = 0;
@@ -410,12 +422,13 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     uint64_t v[kU];
 #pragma unroll
     for (int j = 0; j < kU; j++) v[j] = 0;
-    if (e < d.N) {
-        // descriptor and schedule records in one round trip: a slack slot has no schedules, so
-        // the scan needs no liveness test
-        desc = d.fan_desc[e];
-        bytes += 8;
-        fired = sched_scan(d, e, bytes, s_rem);  // NFCScheduleModule::Execute (SM:51-81)
+    {
+        // descriptor and schedule records in one round trip, without a branch: slots past N (the
+        // last tile) re-read slot N-1 and count as dead; a dead slot stores nothing
+        const int ec = e < d.N ? e : d.N - 1;
+        fired = sched_scan(d, ec, bytes, desc, s_rem, e >= d.N);  // NFCScheduleModule::Execute (SM:51-81)
+        desc = e < d.N ? desc : kDeadDesc;
+        bytes = e < d.N ? bytes + 8 : 0u;
     }
     const bool live = !desc_dead(desc);
     if (live) {
@@ -464,7 +477,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         // the fired heartbeats' effect programs, in schedule-name order
         if (!(d.ablate & (kAblPrograms | kAblNoRun)) && fired) run_programs_u(v, wm, d.tab, fired, d.n_kind, d.n_w);
     }
-    __syncthreads();  // s_pflags
+    __syncthreads();  // s_pb / s_bytes initialised
     // dirty diff against the frame-start values, and each dirty event's fan-out message count
     uint32_t dm = 0;
     unsigned nmsg = 0, nmax = 0;
@@ -473,7 +486,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     for (int j = 0; j < kW; j++)
         if (((wm >> j) & 1) && v[j] != s_o[j * kTPB + threadIdx.x]) {
             dm |= 1u << j;
-            const unsigned n = event_msgs(desc, s_pflags[cls][d.u_pid[j]]);
+            const unsigned n = event_msgs(desc, u_flags(d.u_cf[j], cls));
             nmsg += n;
             nmax = max(nmax, n);
         }
@@ -520,7 +533,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                 d.ev_old[at] = s_o[j * kTPB + threadIdx.x];
                 d.ev_new[at] = nv;
                 if (!fuse) d.ev_moff[at] = pmsg;  // tile-local; k_fanout adds the tile's message base
-                pmsg += event_msgs(desc, s_pflags[cls][pid]);
+                pmsg += event_msgs(desc, u_flags(d.u_cf[j], cls));
                 pev++;
                 bytes += 8 + 24;
             }
@@ -565,7 +578,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     const uint32_t j = d.u_order[q];
                     if (!((dm >> j) & 1)) continue;
                     d.ev_moff[ev0 + at] = mb + m;
-                    m += event_msgs(desc, s_pflags[cls][d.u_pid[j]]);
+                    m += event_msgs(desc, u_flags(d.u_cf[j], cls));
                     at++;
                     bytes += 4;
                 }
@@ -597,7 +610,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     for (int q = 0; q < d.n_w; q++) {
                         const uint32_t j = d.u_order[q];
                         if (!((dm >> j) & 1)) continue;
-                        const uint8_t fl = s_pflags[cls][d.u_pid[j]];
+                        const uint8_t fl = u_flags(d.u_cf[j], cls);
                         const uint32_t n = event_msgs(desc, fl);
                         if (at >= c0 && at < c1) {
                             const bool pub = fl & NFK_PUBLIC;
@@ -729,7 +742,7 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
             }
         }
         // 2. NFCScheduleModule::Execute (SM:51-81)
-        fired = sched_scan(d, e, en.bytes);
+        fired = sched_scan(d, e, en.bytes, desc);
         // 3. the fired heartbeats' effect programs, in schedule-name order
         if (!(d.ablate & kAblPrograms) && fired) {
             for (int k = 0; k < d.n_kind; k++)
