@@ -54,6 +54,13 @@ constexpr unsigned kAblPerKind = 8;  // not an ablation: force the per-kind oper
 constexpr unsigned kAblWaves6 = 16, kAblWaves8 = 32;  // k_tick register budgets (outputs stay exact)
 constexpr unsigned kAblWaves5 = 8192;                  // (6 is the default)
 constexpr unsigned kAblNoRun = 512, kAblNoLoads = 1024, kAblNoEmit = 2048;  // timing only (k_tick)
+constexpr unsigned kAblNoWriteBack = 1u << 18, kAblNoSchedStore = 1u << 19;  // timing only (k_tick)
+constexpr unsigned kAblGroupColumns = 1u << 20, kAblSigGroups = 1u << 21;  // column layouts (outputs exact)
+constexpr unsigned kAblNoPad = 1u << 22;  // columns / schedule kinds at power-of-two strides (outputs exact)
+// Pad between consecutive property columns and schedule-kind arrays (bytes): with cap a power of
+// two, unpadded columns sit exactly 2^k bytes apart and one entity's values of every column fall
+// on the same HBM channel.
+constexpr int64_t kColPad = 2304;
 constexpr unsigned kAblScanInFrame = 131072;  // k_scan_tiles in every frame, not on first read
 constexpr unsigned kAblNoFuse = 4096;  // fan-out in k_fanout instead of k_tick's tail (outputs stay exact)
 
@@ -111,6 +118,7 @@ struct Tables {
 // Everything a kernel needs, passed by value.
 struct Dev {
     int32_t N, cap, n_int, n_flt, n_kind, n_rec, n_class;
+    int32_t s_kstr;  // kind stride of s_hot / s_cold in records: cap + a pad (see kColPad)
     int64_t now;
     int32_t has_recops;
     int32_t has_pre;     // RemoveSchedule(self, name) calls are queued this frame (e_flags live)
@@ -152,7 +160,10 @@ struct Dev {
     uint64_t* u_col[kMaxU];   // property of slot e at u_col[j][e * u_str[j]]
     int32_t u_str[kMaxU];
     int32_t u_order[kMaxW];
-    uint64_t u_cf[kMaxW];     // property flags of writable slot j by class: 4 bits per class id
+    uint32_t u_lower[kMaxW];  // writable slots whose property id is below slot j's (event order)
+    // per class: writable slots whose events go to the scene group (public, bits 0-15) and to the
+    // entity itself only (private & !upload & !public, bits 16-31); GetBroadCastObject (AOI:531)
+    uint32_t u_cmask[NFK_MAX_CLASSES];
     const uint8_t* u_slot;  // [n_prop], only when n_x > 0
     // tiles: property/fired tile t = slots [t*kTile, (t+1)*kTile); record tile r = slots
     // [r*kRTile, (r+1)*kRTile).  Outputs of a tile sit at [t*tile_cap, t*tile_cap + count).
@@ -235,8 +246,12 @@ __host__ __device__ __forceinline__ bool desc_dead(uint64_t desc) { return (desc
 
 // Recipients of one dirty event (NFCSceneAOIModule::GetBroadCastObject, AOI:531-593):
 // public -> every player of the group but self; private && !upload -> self; else none.
-// flags of writable slot j's property for class cls, from the kernel-argument table (Dev::u_cf)
-__device__ __forceinline__ uint8_t u_flags(uint64_t cf, unsigned cls) { return (uint8_t)((cf >> (4 * cls)) & 0xF); }
+// a store at a 32-bit byte offset from a wave-uniform base (global store, SGPR base + VGPR offset:
+// no 64-bit address arithmetic per lane); i * sizeof(T) must fit 32 bits
+template <typename T>
+__device__ __forceinline__ void st_off(T* base, uint32_t i, T x) {
+    *(T*)((char*)base + i * (uint32_t)sizeof(T)) = x;
+}
 __device__ __forceinline__ unsigned event_msgs(uint64_t desc, uint8_t fl) {
     if (fl & NFK_PUBLIC) {
         const unsigned np = (unsigned)((desc >> 32) & 0x3FFF);

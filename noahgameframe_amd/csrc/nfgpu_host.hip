@@ -876,11 +876,51 @@ int nfk_commit(void* world) {
     if (w->n_dst_union > NFK_MAX_TOUCH)
         return fail(NFK_ERR_TOUCH, "programs write more than NFK_MAX_TOUCH distinct properties");
 
-    // property column groups (Tables::p_off / p_str): the properties one heartbeat program
-    // touches are stored interleaved, at most kGroupMax per group, so that a heartbeat firing for
-    // a few entities of a line reads and writes one line per entity instead of one per property
+    // property columns (Tables::p_off / p_str): one plain column per property.  Two interleaved
+    // layouts are kept as timing variants (NFGPU_ABLATE): kAblGroupColumns, the properties one
+    // heartbeat program touches interleaved (one line per entity for a sparse kind), and
+    // kAblSigGroups, properties with the same access signature interleaved.  Plain columns measured
+    // fastest on config[1] (profiles/r01zo_ablate.log: 99.8 us vs 110.7 grouped, 104.8 by
+    // signature): a dense kind's strided 8-byte accesses cost twice the L2 requests per load and
+    // its write-backs cover half lines, while a sparse kind's extra lines are few.
     std::vector<std::vector<int>> pgroups;
-    {
+    const char* ab_env = getenv("NFGPU_ABLATE");
+    const uint32_t ab_layout = ab_env ? (uint32_t)strtoul(ab_env, nullptr, 0) : 0u;
+    if (!(ab_layout & kAblGroupColumns)) {
+        // plain columns, or groups of properties with the same access signature (the set of
+        // (kind, read / write) that touch them): every access covers a group
+        const int NP = w->n_prop;
+        std::vector<std::vector<int>> sig(NP);
+        for (int k = 0; k < NK && (ab_layout & kAblSigGroups); k++)
+            for (int i = 0; i < w->tab.nops[k]; i++) {
+                const nfk_op& op = w->tab.ops[k][i];
+                auto add = [&](int p, int rw) { if (p >= 0 && p < NP) sig[p].push_back(2 * k + rw); };
+                if (op.code == NFK_OP_IADD_CLAMP) {
+                    add(op.dst, 1);
+                    if (op.flags & NFK_A_PROP) add((int)op.a, 0);
+                    if (op.flags & NFK_LO_PROP) add((int)op.b, 0);
+                    if (op.flags & NFK_HI_PROP) add((int)op.c, 0);
+                } else if (op.code == NFK_OP_FLERP) {
+                    add(op.dst, 1);
+                    add((int)op.a, 0);
+                } else if (op.code == NFK_OP_FAFFINE) {
+                    add(op.dst, 1);
+                }
+            }
+        std::map<std::vector<int>, int> gi;
+        for (int p = 0; p < NP; p++) {
+            auto& g = sig[p];
+            std::sort(g.begin(), g.end());
+            g.erase(std::unique(g.begin(), g.end()), g.end());
+            auto it = g.empty() ? gi.end() : gi.find(g);
+            if (it != gi.end() && pgroups[it->second].size() < 8) {
+                pgroups[it->second].push_back(p);
+            } else {
+                if (!g.empty()) gi[g] = (int)pgroups.size();
+                pgroups.push_back({p});
+            }
+        }
+    } else {
         const int NP = w->n_prop;
         constexpr int kGroupMax = 8;
         std::vector<int> par(NP), sz(NP, 1);
@@ -958,7 +998,9 @@ int nfk_commit(void* world) {
     ALLOC(w->tab_d, sizeof(Tables));
     ALLOC(d.tally, (size_t)3 * kTallyN * 8 * 8);
     ALLOC(w->ctrl, sizeof(Ctrl));
-    ALLOC(d.pmem, (size_t)std::max(w->n_prop, 1) * cap * 8);
+    const int64_t cpad = (ab_layout & kAblNoPad) ? 0 : kColPad / 8;  // column pad in values
+    d.s_kstr = cap + (int32_t)((ab_layout & kAblNoPad) ? 0 : kColPad / (int64_t)sizeof(SchedHot));
+    ALLOC(d.pmem, ((size_t)cap + cpad) * (size_t)std::max(w->n_prop, 1) * 8);
     {
         int64_t off = 0;
         for (const auto& g : pgroups) {
@@ -966,11 +1008,11 @@ int nfk_commit(void* world) {
                 w->tab.p_off[g[i]] = off + (int64_t)i;
                 w->tab.p_str[g[i]] = (int32_t)g.size();
             }
-            off += (int64_t)g.size() * cap;
+            off += (int64_t)g.size() * cap + cpad;
         }
     }
-    ALLOC(d.s_hot, (size_t)std::max(NK, 1) * cap * sizeof(SchedHot));
-    ALLOC(d.s_cold, (size_t)std::max(NK, 1) * cap * sizeof(SchedCold));
+    ALLOC(d.s_hot, (size_t)std::max(NK, 1) * d.s_kstr * sizeof(SchedHot));
+    ALLOC(d.s_cold, (size_t)std::max(NK, 1) * d.s_kstr * sizeof(SchedCold));
     ALLOC(d.e_flags, cap);
     ALLOC(d.ext_head, (size_t)cap * 4);
     ALLOC(d.fired_mask, (size_t)cap * 4);
@@ -1071,8 +1113,8 @@ int nfk_commit(void* world) {
         HIPCHK(hipMemcpy(d.rcells[r], cells.data(), cells.size() * 8, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(d.rused[r], used.data(), used.size() * 8, hipMemcpyHostToDevice));
     }
-    HIPCHK(hipMemset(d.s_hot, 0, (size_t)std::max(NK, 1) * cap * sizeof(SchedHot)));
-    HIPCHK(hipMemset(d.s_cold, 0, (size_t)std::max(NK, 1) * cap * sizeof(SchedCold)));
+    HIPCHK(hipMemset(d.s_hot, 0, (size_t)std::max(NK, 1) * d.s_kstr * sizeof(SchedHot)));
+    HIPCHK(hipMemset(d.s_cold, 0, (size_t)std::max(NK, 1) * d.s_kstr * sizeof(SchedCold)));
     {
         std::vector<uint64_t> fd(cap, kDeadDesc);
         std::vector<int32_t> pls(cap, 0), so(cap, -1);
@@ -1458,11 +1500,20 @@ int nfk_execute(void* world, int64_t now_ms) {
             d.u_col[j] = p < 0 ? nullptr : d.pmem + w->tab.p_off[p];
             d.u_str[j] = p < 0 ? 0 : w->tab.p_str[p];
         }
-        for (int j = 0; j < kMaxW; j++) {  // property flags by class, read by k_tick as scalars
-            d.u_cf[j] = 0;
-            if (j < n_w)
-                for (int c = 0; c < NFK_MAX_CLASSES; c++)
-                    d.u_cf[j] |= (uint64_t)(w->tab.pflags[c][d.u_pid[j]] & 0xF) << (4 * c);
+        // event order and fan-out classes of the writable slots, read by k_tick as scalars
+        for (int j = 0; j < kMaxW; j++) {
+            d.u_lower[j] = 0;
+            for (int i = 0; i < n_w && j < n_w; i++)
+                if (d.u_pid[i] < d.u_pid[j]) d.u_lower[j] |= 1u << i;
+        }
+        for (int c = 0; c < NFK_MAX_CLASSES; c++) {
+            uint32_t pub = 0, priv = 0;
+            for (int j = 0; j < n_w && c != 15; j++) {  // (class 15 marks a free slot)
+                const uint8_t f = w->tab.pflags[c][d.u_pid[j]];
+                if (f & NFK_PUBLIC) pub |= 1u << j;
+                else if ((f & NFK_PRIVATE) && !(f & NFK_UPLOAD)) priv |= 1u << j;
+            }
+            d.u_cmask[c] = pub | (priv << 16);
         }
     }
     if (!use_u) uslot.clear();
@@ -1520,7 +1571,7 @@ int nfk_execute(void* world, int64_t now_ms) {
         if (npre)
             hipLaunchKernelGGL(k_pre_hostops, dim3((unsigned)((npre + 255) / 256)), dim3(256), 0, w->stream,
                                (const uint32_t*)(S + off_ps), (const uint32_t*)(S + off_po), (int32_t)npre,
-                               d.e_flags, d.s_hot, d.n_kind, d.cap);
+                               d.e_flags, d.s_hot, d.n_kind, d.s_kstr);
         HIPCHK(hipGetLastError());
     }
     // k_tick writes its tiles' fan-out itself (its LDS image is reused for the events): property
@@ -1770,7 +1821,7 @@ int nfk_read_schedules(void* world, int64_t* next_ms, int32_t* remain, uint8_t* 
     HIPCHK(hipStreamSynchronize(w->stream));
     const Dev& d = w->d;
     const int NK = d.n_kind;
-    std::vector<SchedHot> hot((size_t)NK * d.cap);
+    std::vector<SchedHot> hot((size_t)NK * d.s_kstr);
     if (NK) HIPCHK(hipMemcpy(hot.data(), d.s_hot, hot.size() * sizeof(SchedHot), hipMemcpyDeviceToHost));
     memset(state, 0, (size_t)NK * w->n_obj);
     memset(next_ms, 0, (size_t)NK * w->n_obj * 8);
@@ -1778,7 +1829,7 @@ int nfk_read_schedules(void* world, int64_t* next_ms, int32_t* remain, uint8_t* 
     for (int k = 0; k < NK; k++)
         for (int32_t s = 0; s < d.N; s++) {
             if (w->obj_of_slot[s] < 0) continue;
-            size_t o = (size_t)k * w->n_obj + w->obj_of_slot[s], a = (size_t)k * d.cap + s;
+            size_t o = (size_t)k * w->n_obj + w->obj_of_slot[s], a = (size_t)k * d.s_kstr + s;
             const SchedHot& h = hot[a];
             state[o] = (uint8_t)(h.state & (kStPresent | kStForever));
             next_ms[o] = (h.state & 1) ? h.next : 0;

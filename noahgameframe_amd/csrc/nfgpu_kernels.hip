@@ -31,13 +31,13 @@ __global__ void k_ext_scatter(const uint32_t* __restrict__ x_slot, int32_t n, ui
 // op: 1 = RemoveSchedule(self, name) queued (owns the remove-list key), 2 = RemoveSchedule(self)
 __global__ void k_pre_hostops(const uint32_t* __restrict__ slot, const uint32_t* __restrict__ op, int32_t n,
                               uint8_t* __restrict__ e_flags, SchedHot* __restrict__ s_hot, int32_t n_kind,
-                              int32_t cap) {
+                              int32_t kstr) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = slot[i];
     if (op[i] == 1) e_flags[s] |= 1;
     if (op[i] == 2)
-        for (int k = 0; k < n_kind; k++) s_hot[(size_t)k * cap + s].state = 0;
+        for (int k = 0; k < n_kind; k++) s_hot[(size_t)k * kstr + s].state = 0;
 }
 
 // post-scan host ops, one entry per (slot, kind): bit0 remove, bit1 add (remove first), bit2 clear key
@@ -48,7 +48,7 @@ __global__ void k_post_hostops(const uint32_t* __restrict__ slot, const uint32_t
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = slot[i];
-    const size_t at = (size_t)kind[i] * d.cap + s;
+    const size_t at = (size_t)kind[i] * d.s_kstr + s;
     SchedHot h = d.s_hot[at];
     if (op[i] & 1) h.state = 0;
     if (op[i] & 4) d.e_flags[s] = 0;
@@ -330,10 +330,10 @@ __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigne
                                             bool oob) {
     SchedHot h[kKindChunk];
     // kinds past n_kind re-read the chunk's first record (a cache hit)
-    const SchedHot* base = d.s_hot + (size_t)k0 * d.cap + e;
+    const SchedHot* base = d.s_hot + (size_t)k0 * d.s_kstr + e;
     const int nk = d.n_kind - k0;
 #pragma unroll
-    for (int j = 0; j < kKindChunk; j++) h[j] = base[(size_t)(j < nk ? j : 0) * d.cap];
+    for (int j = 0; j < kKindChunk; j++) h[j] = base[(size_t)(j < nk ? j : 0) * d.s_kstr];
     if constexpr (kFirst) {
         desc = d.fan_desc[e];
         const uint8_t ef = d.e_flags[e];  // (always allocated)
@@ -364,7 +364,7 @@ __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigne
                 // next = start + step * (all - remain) without the cold record (see kSt*)
                 if (!first) h[j].next += st_step(st);
             } else {
-                const SchedCold c = d.s_cold[(size_t)k * d.cap + e];
+                const SchedCold c = d.s_cold[(size_t)k * d.s_kstr + e];
                 bytes += 16;
                 const int64_t step = (int64_t)(c.interval * 1000.0f);
                 const int32_t done = (int32_t)((uint32_t)c.all - (uint32_t)h[j].remain);
@@ -372,7 +372,7 @@ __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigne
             }
             h[j].state = st | kStFired;
         }
-        d.s_hot[(size_t)k * d.cap + e] = h[j];
+        if (!(d.ablate & kAblNoSchedStore)) d.s_hot[(size_t)k * d.s_kstr + e] = h[j];
         if (s_rem) s_rem[k * kTPB + threadIdx.x] = h[j].remain;  // for the fired list
         bytes += 16;
     }
@@ -405,6 +405,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
     __shared__ uint32_t s_pb[3];   // pl_slot run of the groups with dirty events [lo, hi), most recipients
+    __shared__ uint32_t s_cm[NFK_MAX_CLASSES];  // Dev::u_cmask
     extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
     const int tile = blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
@@ -477,21 +478,30 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         // the fired heartbeats' effect programs, in schedule-name order
         if (!(d.ablate & (kAblPrograms | kAblNoRun)) && fired) run_programs_u(v, wm, d.tab, fired, d.n_kind, d.n_w);
     }
-    __syncthreads();  // s_pb / s_bytes initialised
-    // dirty diff against the frame-start values, and each dirty event's fan-out message count
+    if (threadIdx.x < NFK_MAX_CLASSES) {  // (a select over kernel-argument scalars, no indexed copy)
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < NFK_MAX_CLASSES; i++) c = threadIdx.x == (unsigned)i ? d.u_cmask[i] : c;
+        s_cm[threadIdx.x] = c;
+    }
+    __syncthreads();  // s_pb / s_bytes / s_cm initialised
+    // dirty diff against the frame-start values
     uint32_t dm = 0;
-    unsigned nmsg = 0, nmax = 0;
-    const unsigned cls = (unsigned)(desc >> 60);
 #pragma unroll
     for (int j = 0; j < kW; j++)
-        if (((wm >> j) & 1) && v[j] != s_o[j * kTPB + threadIdx.x]) {
-            dm |= 1u << j;
-            const unsigned n = event_msgs(desc, u_flags(d.u_cf[j], cls));
-            nmsg += n;
-            nmax = max(nmax, n);
-        }
+        if (((wm >> j) & 1) && v[j] != s_o[j * kTPB + threadIdx.x]) dm |= 1u << j;
+    // fan-out message counts (event_msgs): a public property's event goes to every player of the
+    // group but the entity itself, a private & !upload one to the entity only.  The message offset
+    // of a slot's event = the counts of the dirty slots with lower property ids (Dev::u_lower).
+    const uint32_t cm = s_cm[desc >> 60];  // (class 15, a free slot: no slots)
+    const uint32_t pubm = cm & 0xFFFFu, privm = cm >> 16;
+    const uint32_t r1 = (uint32_t)((desc >> 46) & 0x3FFF);
+    const uint32_t npub = (uint32_t)((desc >> 32) & 0x3FFF) - (r1 ? 1u : 0u);
+    const unsigned nmsg = npub * __builtin_popcount(dm & pubm) + __builtin_popcount(dm & privm);
+    unsigned nmax = (dm & pubm) ? npub : ((dm & privm) ? 1u : 0u);
     const unsigned nd = __builtin_popcount(dm);
     const unsigned nf = __builtin_popcount(fired);
+    const uint32_t dm_ = dm;
     if (fuse) {  // the pl_slot run of the groups whose members have messages (they are contiguous)
         const uint32_t np = (uint32_t)((desc >> 32) & 0x3FFF);
         uint32_t lo = nmsg ? (uint32_t)desc : 0xFFFFFFFFu, hi = nmsg ? (uint32_t)desc + np : 0u;
@@ -512,40 +522,48 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     unsigned long long tot;
     const unsigned long long excl =
         block_excl_scan(((unsigned long long)nf << 48) | ((unsigned long long)nd << 32) | nmsg, s_w, tot);
-    unsigned pev = (unsigned)((excl >> 32) & 0xFFFF);
+    const unsigned pev0 = (unsigned)((excl >> 32) & 0xFFFF);
     unsigned pfi = (unsigned)(excl >> 48);
-    unsigned pmsg = (unsigned)excl;
-    const unsigned pev0 = pev, pmsg0 = pmsg, tmsg = (unsigned)tot;
+    const unsigned pmsg0 = (unsigned)excl, tmsg = (unsigned)tot;
+    // this tile's output runs (wave-uniform bases, tile-local 32-bit offsets)
     const size_t ev0 = (size_t)tile * d.ev_tcap, fi0 = (size_t)tile * d.fi_tcap;
+    uint32_t* const t_evm = d.ev_moff + ev0;
 
     if (live) {
-        // write back the changed values; their events in property-id order
+        // write back the changed values; their events in property-id order (rank among the
+        // entity's dirty slots by Dev::u_lower)
         if (dm && !(d.ablate & kAblNoEmit)) {
-            for (int q = 0; q < d.n_w; q++) {
-                const uint32_t j = d.u_order[q];
-                if (!((dm >> j) & 1)) continue;
-                const uint64_t nv = uget(v, j);
-                const uint32_t pid = (uint32_t)d.u_pid[j];
-                d.u_col[j][(size_t)e * d.u_str[j]] = nv;
-                const size_t at = ev0 + pev;
-                d.ev_slot[at] = (uint32_t)e;
-                d.ev_pid[at] = pid;
-                d.ev_old[at] = s_o[j * kTPB + threadIdx.x];
-                d.ev_new[at] = nv;
-                if (!fuse) d.ev_moff[at] = pmsg;  // tile-local; k_fanout adds the tile's message base
-                pmsg += event_msgs(desc, u_flags(d.u_cf[j], cls));
-                pev++;
+            uint32_t* const t_evs = d.ev_slot + ev0;
+            uint32_t* const t_evp = d.ev_pid + ev0;
+            uint64_t* const t_evo = d.ev_old + ev0;
+            uint64_t* const t_evn = d.ev_new + ev0;
+#pragma unroll
+            for (int j = 0; j < kW; j++) {
+                if (j >= d.n_w || !((dm >> j) & 1)) continue;
+                const uint32_t below = dm & d.u_lower[j];
+                const uint32_t at = pev0 + __builtin_popcount(below);
+                const uint64_t nv = v[j];
+                if (!(d.ablate & kAblNoWriteBack)) d.u_col[j][(size_t)e * d.u_str[j]] = nv;
+                st_off(t_evs, at, (uint32_t)e);
+                st_off(t_evp, at, (uint32_t)d.u_pid[j]);
+                st_off(t_evo, at, s_o[j * kTPB + threadIdx.x]);
+                st_off(t_evn, at, nv);
+                if (!fuse)  // tile-local; k_fanout adds the tile's message base
+                    st_off(t_evm, at, pmsg0 + npub * __builtin_popcount(below & pubm) +
+                                          __builtin_popcount(below & privm));
                 bytes += 8 + 24;
             }
         }
+        uint32_t* const t_fis = d.fi_slot + fi0;
+        uint32_t* const t_fik = d.fi_kind + fi0;
+        int32_t* const t_fir = d.fi_remain + fi0;
         uint32_t fl = fired;
         while (fl) {
             const int k = __builtin_ctz(fl);
             fl &= fl - 1;
-            const size_t at = fi0 + pfi;
-            d.fi_slot[at] = (uint32_t)e;
-            d.fi_kind[at] = (uint32_t)k;
-            d.fi_remain[at] = s_rem[k * kTPB + threadIdx.x];
+            st_off(t_fis, pfi, (uint32_t)e);
+            st_off(t_fik, pfi, (uint32_t)k);
+            st_off(t_fir, pfi, s_rem[k * kTPB + threadIdx.x]);
             pfi++;
             bytes += 12;
         }
@@ -567,19 +585,19 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     // waves, and lane groups would re-read each event's triple once per lane).
     if (fuse) {
         __syncthreads();  // s_pb; every read of s_o and s_rem is done: the region is reused
+        uint32_t dm = dm_;
         const unsigned mb = (unsigned)tile * d.msg_tcap;
         const unsigned tev = (unsigned)((tot >> 32) & 0xFFFF);
         const bool fan = tmsg && tmsg <= d.msg_tcap;
         if (tmsg > d.msg_tcap && threadIdx.x == 0) atomicOr(&d.ctrl->err, kErrFanBound);  // (host bound)
         if (!fan) {  // ev_moff only
-            unsigned m = pmsg0, at = pev0;
             if (dm)
-                for (int q = 0; q < d.n_w; q++) {
-                    const uint32_t j = d.u_order[q];
-                    if (!((dm >> j) & 1)) continue;
-                    d.ev_moff[ev0 + at] = mb + m;
-                    m += event_msgs(desc, u_flags(d.u_cf[j], cls));
-                    at++;
+#pragma unroll
+                for (int j = 0; j < kW; j++) {
+                    if (j >= d.n_w || !((dm >> j) & 1)) continue;
+                    const uint32_t below = dm & d.u_lower[j];
+                    st_off(t_evm, pev0 + __builtin_popcount(below),
+                           mb + pmsg0 + npub * __builtin_popcount(below & pubm) + __builtin_popcount(below & privm));
                     bytes += 4;
                 }
         } else {
@@ -605,24 +623,25 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             bytes += 4 * nmsg;
             for (unsigned c0 = 0; c0 < tev; c0 += ecap) {  // uniform
                 const unsigned c1 = min(tev, c0 + ecap);
-                if (dm && pev0 < c1 && pev0 + nd > c0) {  // this thread's events of the chunk
-                    unsigned m = pmsg0, at = pev0;
-                    for (int q = 0; q < d.n_w; q++) {
-                        const uint32_t j = d.u_order[q];
+                // a runtime loop over the slots (an unrolled one gets hoisted out of the chunk loop
+                // and spills: 12 slots x 4 values)
+                if (dm && pev0 < c1 && pev0 + nd > c0) {
+#pragma unroll 1
+                    for (int j = 0; j < d.n_w; j++) {
                         if (!((dm >> j) & 1)) continue;
-                        const uint8_t fl = u_flags(d.u_cf[j], cls);
-                        const uint32_t n = event_msgs(desc, fl);
-                        if (at >= c0 && at < c1) {
-                            const bool pub = fl & NFK_PUBLIC;
-                            uint32_t* x = s_ev + 3u * (at - c0);
-                            x[0] = m;
-                            x[1] = pub ? (uint32_t)desc : (uint32_t)e;
-                            x[2] = n | ((uint32_t)((desc >> 46) & 0x3FFF) << 14) | (pub ? 0x80000000u : 0u);
-                            d.ev_moff[ev0 + at] = mb + m;
-                            bytes += 4;
-                        }
-                        m += n;
-                        at++;
+                        const uint32_t below = dm & d.u_lower[j];
+                        const uint32_t at = pev0 + __builtin_popcount(below);
+                        if (at < c0 || at >= c1) continue;
+                        const bool pub = (pubm >> j) & 1;
+                        const uint32_t m = pmsg0 + npub * __builtin_popcount(below & pubm) +
+                                           __builtin_popcount(below & privm);
+                        const uint32_t n = pub ? npub : ((privm >> j) & 1u);
+                        uint32_t* x = s_ev + 3u * (at - c0);
+                        x[0] = m;
+                        x[1] = pub ? (uint32_t)desc : (uint32_t)e;
+                        x[2] = n | (r1 << 14) | (pub ? 0x80000000u : 0u);
+                        st_off(t_evm, at, mb + m);
+                        bytes += 4;
                     }
                 }
                 __syncthreads();
@@ -817,7 +836,7 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
             const size_t at = fi0 + pfi;
             d.fi_slot[at] = (uint32_t)e;
             d.fi_kind[at] = (uint32_t)k;
-            d.fi_remain[at] = d.s_hot[(size_t)k * d.cap + e].remain;
+            d.fi_remain[at] = d.s_hot[(size_t)k * d.s_kstr + e].remain;
             pfi++;
             en.bytes += 12;
         }
@@ -1258,8 +1277,8 @@ __device__ __forceinline__ uint64_t* row_word(const Dev& d, int32_t s, int w) {
     w -= d.n_int + d.n_flt;
     if (w < 4 * d.n_kind) {
         const int k = w >> 2, q = w & 3;
-        return q < 2 ? (uint64_t*)&d.s_hot[(size_t)k * d.cap + s] + q
-                     : (uint64_t*)&d.s_cold[(size_t)k * d.cap + s] + (q - 2);
+        return q < 2 ? (uint64_t*)&d.s_hot[(size_t)k * d.s_kstr + s] + q
+                     : (uint64_t*)&d.s_cold[(size_t)k * d.s_kstr + s] + (q - 2);
     }
     w -= 4 * d.n_kind;
     for (int r = 0; r < d.n_rec; r++) {

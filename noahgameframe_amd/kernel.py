@@ -16,7 +16,7 @@ import numpy as np
 from . import workload as wl
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnfgpu.so")
+LIB_PATH = os.environ.get("NFGPU_LIB") or os.path.join(_HERE, "libnfgpu.so")  # (NFGPU_LIB: A/B timing of library builds)
 
 NFK_OK = 0
 _ERRS = {-1: "NFK_ERR_ARG", -2: "NFK_ERR_HIP", -3: "NFK_ERR_STATE", -4: "NFK_ERR_CAPACITY",
