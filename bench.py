@@ -31,7 +31,8 @@ CONFIG_NAMES = {
     3: "BASELINE config[3]: 256 scenes x 64 groups, 2M entities per GPU, 32 players per group "
        "(scene-group sync-list fan-out dominated), heartbeats as config[1], 100 ms frames",
     4: "BASELINE config[4]: 500k players per GPU, 64-row skill record each (int cooldown + f64 charge "
-       "columns updated by a 100 ms SkillCD heartbeat), groups of 16 players, 100 ms frames",
+       "columns updated by a 100 ms SkillCD heartbeat; steady state: cooldowns of hours, so every frame "
+       "updates the same share of cells), groups of 16 players, 100 ms frames",
 }
 
 
@@ -178,7 +179,7 @@ def main():
                                   guid_heads=(7 + 16 * rank, 9 + 16 * rank))
         w["scene"] += 256 * rank
     elif args.config == 4:
-        w = workload.record_world(n_ticks=1, tick_ms=args.tick_ms, seed=2028 + rank,
+        w = workload.record_world(n_ticks=1, tick_ms=args.tick_ms, seed=2028 + rank, steady=True,
                                   guid_heads=(7 + 16 * rank, 9 + 16 * rank))
         w["scene"][:] = rank + 1
     else:

@@ -119,7 +119,8 @@ typedef struct nfk_summary {
  * tiles) are one run of msg_cnt[t] recipients at msg_rcpt[msg_base[t]], in event order.  Runs
  * follow each other in tile order; when the frame's k_tick fanned out its own tiles, property
  * tile runs start at a fixed stride (msg_base[t] = t x an upper bound of a tile's messages) and
- * the record tiles' runs follow densely.  ev_moff / re_moff hold the index in msg_rcpt of the
+ * the record tiles' runs follow, densely or (when k_records fanned them out too) at a fixed
+ * stride of their own.  Always walk tiles by msg_base / msg_cnt.  ev_moff / re_moff hold the index in msg_rcpt of the
  * event's first recipient; its recipients end where the next event of its tile begins
  * (msg_base[t] + msg_cnt[t] after the tile's last).
  * Recipients are slots; slot_obj maps slot -> object index.  nfk_read_fanout returns the dense

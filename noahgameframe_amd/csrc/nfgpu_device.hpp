@@ -20,7 +20,7 @@ constexpr unsigned kErrMsgCap = 4, kErrTouch = 8, kErrFanBound = 16;
 struct alignas(64) Ctrl {
     unsigned err, pad_u[3];                                             // 16 B
     unsigned long long n_ev, n_fi, n_re, n_msgs;                        // 32 B
-    unsigned long long msg_extent, n_msgs_ptiles;                       // 16 B
+    unsigned long long msg_extent, n_msgs_ptiles;  // n_msgs_ptiles: messages of fixed-stride tiles
     unsigned long long bytes_tick, bytes_rec, bytes_fan, pad2;          // accumulated across frames
 };
 
@@ -181,6 +181,12 @@ struct Dev {
     // t * msg_tcap (an upper bound of one tile's messages this frame); record tiles follow densely
     uint32_t msg_tcap;
     int32_t fuse_fan;
+    // fuse_rec: k_records writes its record tiles' fan-out itself (only with fuse_fan), record
+    // tile r's messages at msg_rb0 + r * msg_rtcap (msg_rb0 = n_tiles * msg_tcap; msg_rtcap = an
+    // upper bound of one record tile's messages: slots x cells the record ops may change x the
+    // most recipients of one record event)
+    int32_t fuse_rec;
+    uint32_t msg_rb0, msg_rtcap;
     int32_t lds_words; // k_tick's dynamic LDS in 4-byte words (message window + staged players)
     // outputs (tile-staged)
     uint32_t* ev_slot; uint32_t* ev_pid; uint64_t* ev_old; uint64_t* ev_new; uint32_t* ev_moff;

@@ -144,6 +144,7 @@ struct World {
 
     int32_t ticks = 0;
     uint32_t last_tcap = 0;  // Dev::msg_tcap of the last launched frame
+    uint32_t last_rtcap = 0; // Dev::msg_rtcap of the last launched frame (0: records not fused)
     bool scan_pending = false;  // the last frame's dense ranks (k_scan_tiles) are built on first read
     Dev scan_dev;               // ... with that frame's Dev
     int64_t last_rec_msgs = 0;  // record-tile messages of the last summarised frame (capacity hint)
@@ -1578,10 +1579,30 @@ int nfk_execute(void* world, int64_t now_ms) {
     // tile t's messages sit at t * msg_tcap, msg_tcap = writable properties x slots x most
     // recipients of one event, so no tile waits for another tile's count.  Worlds whose bound
     // would reserve more than kMsgStrideLimit run k_fanout after k_scan_tiles instead.
+    // With the property tiles at a fixed stride, k_records fans out its record tiles the same way
+    // after them: msg_rtcap = slots x cells the record ops may change x most recipients of one
+    // record event (the scene group's players for a public record, 1 for a private one).
     d.msg_tcap = 0;
+    d.fuse_rec = 0;
+    d.msg_rb0 = d.msg_rtcap = 0;
     if (use_u && d.n_tiles && !(d.ablate & (kAblNoFuse | kAblNoEmit))) {
         const int64_t tcap = (int64_t)std::max(d.n_w, 1) * kTile * std::max(w->max_np, 1);
-        const int64_t need = tcap * d.n_tiles + w->last_rec_msgs + w->last_rec_msgs / 4 + 1024;
+        int64_t rtcap = 0;
+        bool rfuse = false;
+        if (d.has_recops && d.n_rtiles) {
+            int64_t cells = 0, per = 0;
+            for (int j = 0; j < d.n_rops; j++) cells += d.rops[j].rows;
+            for (int c = 0; c < NFK_MAX_CLASSES; c++)
+                for (int j = 0; j < d.n_rops; j++) {
+                    const uint8_t f = w->tab.rflags[c][d.rops[j].rec];
+                    per = std::max<int64_t>(per, (f & NFK_PUBLIC) ? std::max(w->max_np, 1)
+                                                 : ((f & NFK_PRIVATE) && !(f & NFK_UPLOAD)) ? 1 : 0);
+                }
+            rtcap = ((int64_t)kRTile * cells * per + 3) & ~(int64_t)3;  // (16-byte aligned runs)
+            rfuse = tcap * d.n_tiles + rtcap * d.n_rtiles <= kMsgStrideLimit;
+        }
+        const int64_t need = tcap * d.n_tiles + (rfuse ? rtcap * d.n_rtiles
+                                                       : w->last_rec_msgs + w->last_rec_msgs / 4) + 1024;
         if (tcap * d.n_tiles <= kMsgStrideLimit) {
             if (need > w->d.msg_cap) {  // grow before the frame (the previous frame's messages are dropped)
                 HIPCHK(hipStreamSynchronize(w->stream));
@@ -1595,10 +1616,16 @@ int nfk_execute(void* world, int64_t now_ms) {
                 d.msg_cap = need;
             }
             d.msg_tcap = (uint32_t)tcap;
+            if (rfuse) {
+                d.fuse_rec = 1;
+                d.msg_rb0 = (uint32_t)(tcap * d.n_tiles);
+                d.msg_rtcap = (uint32_t)rtcap;
+            }
         }
     }
     d.fuse_fan = d.msg_tcap != 0;
     w->last_tcap = d.msg_tcap;
+    w->last_rtcap = d.fuse_rec ? d.msg_rtcap : 0u;
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
         size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;
@@ -1649,7 +1676,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     // Otherwise the frame's outputs are complete as tiles + per-tile counts, and the ranks are
     // built on the first read (nfk_summary_get, nfk_outputs_get, nfk_read_*).
     w->scan_pending = false;
-    if (d.fuse_fan && !d.has_recops && !(d.ablate & kAblScanInFrame)) {
+    if (d.fuse_fan && (!d.has_recops || d.fuse_rec) && !(d.ablate & kAblScanInFrame)) {
         w->scan_pending = true;
         w->scan_dev = d;
     } else {
@@ -1657,9 +1684,10 @@ int nfk_execute(void* world, int64_t now_ms) {
         hipLaunchKernelGGL(k_scan_tiles, dim3(5), dim3(kScanTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
-    // the tiles k_tick did not fan out: record tiles, and property tiles after k_tick_touch
+    // the tiles k_tick / k_records did not fan out: record tiles, and property tiles after
+    // k_tick_touch
     const int fan0 = d.fuse_fan ? d.n_tiles : 0;
-    const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0) - fan0;
+    const int nfan = d.n_tiles + (d.has_recops && !d.fuse_rec ? d.n_rtiles : 0) - fan0;
     if (nfan > 0 && !(d.ablate & kAblNoEmit)) {  // (timing ablation: events were not written)
         TimeScope ts(w, KT_FAN);
         hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, (int32_t)fan0);
@@ -1693,10 +1721,16 @@ static int read_ctrl(World* w, Ctrl* c) {
     return NFK_OK;
 }
 
+// entries of msg_rcpt reserved by the fixed-stride tiles of the last frame (property tiles, and
+// record tiles when k_records fanned them out)
+static int64_t fixed_msgs_reserved(const World* w) {
+    return (int64_t)w->last_tcap * w->d.n_tiles + (int64_t)w->last_rtcap * (w->d.has_recops ? w->d.n_rtiles : 0);
+}
+
 // messages of the last frame: the runs are dense unless k_tick placed property tiles at a stride
 static int64_t frame_msgs(const World* w, const Ctrl& c) {
     if (!w->last_tcap) return (int64_t)c.msg_extent;
-    return (int64_t)c.n_msgs_ptiles + (int64_t)c.msg_extent - (int64_t)w->last_tcap * w->d.n_tiles;
+    return (int64_t)c.n_msgs_ptiles + (int64_t)c.msg_extent - fixed_msgs_reserved(w);
 }
 
 int nfk_summary_get(void* world, nfk_summary* out) {
@@ -1738,7 +1772,7 @@ int nfk_summary_get(void* world, nfk_summary* out) {
         int r = alloc_track(w, (void**)&grown, (size_t)need * 4);
         if (r) return r;
         if (w->last_tcap)
-            HIPCHK(hipMemcpy(grown, w->d.msg_rcpt, (size_t)w->last_tcap * w->d.n_tiles * 4, hipMemcpyDeviceToDevice));
+            HIPCHK(hipMemcpy(grown, w->d.msg_rcpt, (size_t)fixed_msgs_reserved(w) * 4, hipMemcpyDeviceToDevice));
         HIPCHK(hipFree(w->d.msg_rcpt));
         w->allocs.erase(std::remove(w->allocs.begin(), w->allocs.end(), (void*)w->d.msg_rcpt), w->allocs.end());
         w->d.msg_rcpt = grown;
@@ -1746,7 +1780,7 @@ int nfk_summary_get(void* world, nfk_summary* out) {
         HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
         Dev d = w->d;
         const int fan0 = w->last_tcap ? d.n_tiles : 0;
-        const int nfan = d.n_tiles + (d.has_recops ? d.n_rtiles : 0) - fan0;
+        const int nfan = d.n_tiles + (d.has_recops && !w->last_rtcap ? d.n_rtiles : 0) - fan0;
         if (nfan > 0) hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, (int32_t)fan0);
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(w->stream));

@@ -891,6 +891,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     unsigned long long work = __ballot(my_mask != 0);
     unsigned pos = 0, pmsg = 0;  // tile-local
     const size_t re0 = (size_t)rt * d.re_tcap;
+    const uint32_t mrb = d.fuse_rec ? d.msg_rb0 + (uint32_t)rt * d.msg_rtcap : 0u;  // fused: this tile's run
     while (work) {
         // next group of up to kGroup slots with record work, in slot order; every cell load of
         // the group is issued before any is consumed
@@ -970,16 +971,35 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                 const unsigned n = (unsigned)__shfl((int)inc, 63, 64);
                 if (n == 0) continue;  // wave-uniform
                 unsigned p = pos + inc - c;
-                const unsigned per = event_msgs(desc, s_rflags[cls][d.rops[j0].rec]);
+                const uint8_t rfl = s_rflags[cls][d.rops[j0].rec];
+                const unsigned per = event_msgs(desc, rfl);
 #pragma unroll
                 for (int j = 0; j < kOps; j++) {
                     if (!(j >= j0 && j <= j1 && ch[j])) continue;
                     const size_t at = re0 + p;
+                    const uint32_t lmo = pmsg + per * (p - pos);
                     d.re_slot[at] = (uint32_t)e;
                     d.re_rrc[at] = ((uint32_t)d.rops[j].rec << 16) | ((uint32_t)lane << 8) | (uint32_t)d.rops[j].col;
                     d.re_old[at] = cur[g][j];
                     d.re_new[at] = nv[j];
-                    d.re_moff[at] = pmsg + per * (p - pos);
+                    d.re_moff[at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
+                    if (d.fuse_rec && per) {
+                        // GetBroadCastObject (AOI:531-593) for the record event, into the tile's run
+                        uint32_t* out = d.msg_rcpt + mrb + lmo;
+                        if (!(rfl & NFK_PUBLIC)) {
+                            out[0] = (uint32_t)e;  // private & !upload: the entity itself
+                        } else {  // every player of the group but self
+                            const uint32_t np = (uint32_t)((desc >> 32) & 0x3FFF);
+                            const uint32_t r1 = (uint32_t)((desc >> 46) & 0x3FFF);
+                            uint32_t k = 0;
+                            for (uint32_t q = 0; q < np; q++) {
+                                if (q + 1 == r1) continue;
+                                out[k++] = (uint32_t)d.pl_slot[(uint32_t)desc + q];
+                            }
+                            bytes += 4 * np;
+                        }
+                        bytes += 4 * per;
+                    }
                     p++;
                     bytes += 28;
                 }
@@ -1037,10 +1057,12 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nrt = d.has_recops ? d.n_rtiles : 0;
     const int a = blockIdx.x;
-    if (a == 4) {  // sum of the property tiles' message counts
+    if (a == 4) {  // sum of the message counts of the fixed-stride tiles (property, fused record)
         unsigned long long v = 0;
         if (d.msg_tcap)
             for (int i = tid; i < d.n_tiles; i += kScanTPB) v += d.t_msg[i];
+        if (d.fuse_rec)
+            for (int i = tid; i < nrt; i += kScanTPB) v += d.t_msg[d.n_tiles + i];
         v = wave_sum(v);
         if (lane == 0) s_w[w] = v;
         __syncthreads();
@@ -1054,8 +1076,10 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
     const uint32_t* cnt = a == 0 ? d.t_ev : a == 1 ? d.t_fi : a == 2 ? d.t_re : d.t_msg;
     uint32_t* base = a == 0 ? d.ev_base : a == 1 ? d.fi_base : a == 2 ? d.re_base : d.msg_base;
     const int len = a < 2 ? d.n_tiles : a == 2 ? nrt : d.n_tiles + nrt;
-    // message runs: property tiles fanned out by k_tick take msg_tcap each
+    // message runs: property tiles fanned out by k_tick take msg_tcap each, record tiles fanned
+    // out by k_records msg_rtcap each
     const int fixed = (a == 3 && d.msg_tcap) ? d.n_tiles : 0;
+    const int rfixed = (a == 3 && d.fuse_rec) ? nrt : 0;
     unsigned long long carry = 0;
     for (int c0 = 0; c0 < len; c0 += kScanTPB * kScanPer) {
         const int i0 = c0 + tid * kScanPer;
@@ -1066,6 +1090,7 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
 #pragma unroll
             for (int q = 0; q < kScanPer; q++) {
                 if (i0 + q < fixed) x.v[q] = d.msg_tcap;
+                else if (i0 + q < fixed + rfixed) x.v[q] = d.msg_rtcap;
                 x.sum += x.v[q];
             }
         }

@@ -103,7 +103,7 @@ def _names(lst):
 def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4, n_ticks=8,
                tick_ms=100, seed=1, ext_frac=0.05, host_ops=True, records=False, rec_rows=64,
                t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, sched_edges=False,
-               switch_frac=0.0, switch_new_groups=False):
+               switch_frac=0.0, switch_new_groups=False, rec_steady=False):
     rng = np.random.default_rng(seed)
     n_groups = n_scenes * groups_per_scene
     # ---- objects ----
@@ -319,10 +319,12 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
         w["rec_flags"] = rf
         cells = np.zeros((n_obj, cols, rows), np.uint64)
         cells[:, 0, :] = rng.integers(1000, 2000, (n_obj, rows)).astype(np.uint64)
-        cd = rng.integers(0, 3000, (n_obj, rows))
+        # rec_steady: cooldowns of hours and charges far above the threshold, so that every frame
+        # of a bench run updates the same share of cells (the default decays within ~30 frames)
+        cd = rng.integers(0, 3000, (n_obj, rows)) + (3_600_000 if rec_steady else 0)
         cd[rng.random((n_obj, rows)) < 0.3] = 0
         cells[:, 1, :] = cd.astype(np.uint64)
-        ch = rng.uniform(0.0, 100.0, (n_obj, rows))
+        ch = rng.uniform(0.0, 100.0, (n_obj, rows)) * (2.0 ** 200 if rec_steady else 1.0)
         ch[rng.random((n_obj, rows)) < 0.2] = 0.0005    # below the 0.001 record threshold
         cells[:, 2, :] = ch.view(np.uint64)
         used = rng.integers(0, 2 ** 63, n_obj, dtype=np.int64).astype(np.uint64)
@@ -348,10 +350,10 @@ def fanout_world(n_ticks=4, seed=2027, n_obj=1 << 21, scenes=256, groups=64, pla
                       host_ops=kw.pop("host_ops", False), **kw)
 
 
-def record_world(n_ticks=4, seed=2028, n_obj=500_000, groups=31_250, rec_rows=64, **kw):
+def record_world(n_ticks=4, seed=2028, n_obj=500_000, groups=31_250, rec_rows=64, steady=False, **kw):
     """config[4]: 500k players, each with a 64-row skill record whose cooldown (int) and charge
     (f64) columns a 100 ms SkillCD heartbeat updates every frame; groups of 16 players."""
     per = n_obj // groups
     return make_world(n_obj=n_obj, n_scenes=1, groups_per_scene=groups, players_per_group=per, n_ticks=n_ticks,
                       seed=seed, records=True, rec_rows=rec_rows, ext_frac=kw.pop("ext_frac", 0.0),
-                      host_ops=kw.pop("host_ops", False), **kw)
+                      host_ops=kw.pop("host_ops", False), rec_steady=steady, **kw)
