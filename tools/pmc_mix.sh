@@ -15,7 +15,7 @@ for abl in "${@:-0}"; do
     eval "C=\$$set"
     echo "=== abl=$abl set=$set"
     NFGPU_ABLATE=$abl timeout -k 5 -s KILL 90 rocprofv3 --pmc $C --output-format csv -d "$OUT/a${abl}_$set" -o run -- \
-      python bench.py --steps 10 --warmup 2 --cpu-baseline off > "$OUT/a${abl}_$set.log" 2>&1
+      python bench.py --steps 10 --warmup 2 --cpu-baseline off ${BENCH_ARGS:-} > "$OUT/a${abl}_$set.log" 2>&1
     rc=$?
     echo "rc=$rc"
     [ $rc -eq 0 ] || { tail -5 "$OUT/a${abl}_$set.log"; exit $rc; }
@@ -31,7 +31,7 @@ for a in abls:
     r = {}
     for s in "AB":
         c = load_counters(os.path.join(out, f"a{a}_{s}"))
-        k = [x for x in c if x.startswith("k_tick")][0]
+        k = [x for x in c if x.startswith(os.environ.get("KERN", "k_tick"))][0]
         for name, per in c[k].items():
             v = sorted(per.values() if isinstance(per, dict) else per)
             r[name] = v[len(v) // 2]
