@@ -1656,11 +1656,11 @@ int nfk_execute(void* world, int64_t now_ms) {
         TimeScope ts(w, KT_REC);
         const dim3 g((unsigned)((d.n_rtiles + 3) / 4)), b(kTPB);
         if (d.n_rops <= 1)
-            hipLaunchKernelGGL((k_records<1, 8>), g, b, 0, w->stream, d);
+            hipLaunchKernelGGL((k_records<1, 4>), g, b, 0, w->stream, d);
         else if (d.n_rops <= 2)
             hipLaunchKernelGGL((k_records<2, 4>), g, b, 0, w->stream, d);
         else
-            hipLaunchKernelGGL((k_records<NFK_MAX_OPS, 4>), g, b, 0, w->stream, d);
+            hipLaunchKernelGGL((k_records<NFK_MAX_OPS, 2>), g, b, 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
     if (npost) {

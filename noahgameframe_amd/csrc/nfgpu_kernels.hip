@@ -866,6 +866,14 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
 // kOps: register slots for the record ops (>= n_rops), kGroup: slots whose cells are in flight
 // together; instantiated so that a frame's op count does not pay for NFK_MAX_OPS registers.
 template <int kOps, int kGroup>
+struct RecGrp {  // one group of slots with record work: their cells and used-row masks
+    int js[kGroup];
+    uint32_t masks[kGroup];
+    uint64_t used[kGroup][kOps];
+    uint64_t cur[kGroup][kOps];
+};
+
+template <int kOps, int kGroup>
 __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
     for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
@@ -892,37 +900,38 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     unsigned pos = 0, pmsg = 0;  // tile-local
     const size_t re0 = (size_t)rt * d.re_tcap;
     const uint32_t mrb = d.fuse_rec ? d.msg_rb0 + (uint32_t)rt * d.msg_rtcap : 0u;  // fused: this tile's run
-    while (work) {
+    // Two groups in flight: the next group's cell loads are issued before the current group's
+    // stores, so its wait covers the stores' acknowledgements (vmcnt counts loads and stores in
+    // issue order) instead of a full HBM round trip after them.
+    auto pick_load = [&](RecGrp<kOps, kGroup>& G) {
         // next group of up to kGroup slots with record work, in slot order; every cell load of
         // the group is issued before any is consumed
-        int js[kGroup];
-        uint32_t masks[kGroup];
-        uint64_t used[kGroup][kOps];
-        uint64_t cur[kGroup][kOps];
 #pragma unroll
         for (int g = 0; g < kGroup; g++) {
-            js[g] = work ? __builtin_ctzll(work) : -1;
+            G.js[g] = work ? __builtin_ctzll(work) : -1;
             if (work) work &= work - 1;
-            masks[g] = js[g] >= 0 ? (uint32_t)__shfl((int)my_mask, js[g], 64) : 0u;
+            G.masks[g] = G.js[g] >= 0 ? (uint32_t)__shfl((int)my_mask, G.js[g], 64) : 0u;
         }
 #pragma unroll
         for (int g = 0; g < kGroup; g++)
 #pragma unroll
             for (int j = 0; j < kOps; j++) {
-                used[g][j] = 0;
-                cur[g][j] = 0;
-                if (j < nro && js[g] >= 0 && ((masks[g] >> d.rops[j].kind) & 1)) {
-                    const int e = s0 + js[g];
-                    used[g][j] = d.rops[j].used[e];
+                G.used[g][j] = 0;
+                G.cur[g][j] = 0;
+                if (j < nro && G.js[g] >= 0 && ((G.masks[g] >> d.rops[j].kind) & 1)) {
+                    const int e = s0 + G.js[g];
+                    G.used[g][j] = d.rops[j].used[e];
                     if (lane < d.rops[j].rows)
-                        cur[g][j] = d.rops[j].cells[((size_t)e * d.rops[j].cols + d.rops[j].col) * d.rops[j].rows + lane];
+                        G.cur[g][j] = d.rops[j].cells[((size_t)e * d.rops[j].cols + d.rops[j].col) * d.rops[j].rows + lane];
                 }
             }
+    };
+    auto process = [&](RecGrp<kOps, kGroup>& G) {
 #pragma unroll
         for (int g = 0; g < kGroup; g++) {
-            if (js[g] < 0) break;
-            const int e = s0 + js[g];
-            const uint64_t desc = (uint64_t)__shfl((long long)my_desc, js[g], 64);
+            if (G.js[g] < 0) break;
+            const int e = s0 + G.js[g];
+            const uint64_t desc = (uint64_t)__shfl((long long)my_desc, G.js[g], 64);
             const unsigned cls = (unsigned)(desc >> 60);
             bool ch[kOps];
             uint64_t nv[kOps];
@@ -930,11 +939,11 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             for (int j = 0; j < kOps; j++) {
                 ch[j] = false;
                 nv[j] = 0;
-                if (j >= nro || !((masks[g] >> d.rops[j].kind) & 1)) continue;
+                if (j >= nro || !((G.masks[g] >> d.rops[j].kind) & 1)) continue;
                 const RecOpX& ro = d.rops[j];
                 if (lane == 0) bytes += 8;
-                if (lane >= ro.rows || !((used[g][j] >> lane) & 1)) continue;
-                const uint64_t c = cur[g][j];
+                if (lane >= ro.rows || !((G.used[g][j] >> lane) & 1)) continue;
+                const uint64_t c = G.cur[g][j];
                 bytes += 8;
                 uint64_t nb;
                 bool changed;
@@ -980,7 +989,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     const uint32_t lmo = pmsg + per * (p - pos);
                     d.re_slot[at] = (uint32_t)e;
                     d.re_rrc[at] = ((uint32_t)d.rops[j].rec << 16) | ((uint32_t)lane << 8) | (uint32_t)d.rops[j].col;
-                    d.re_old[at] = cur[g][j];
+                    d.re_old[at] = G.cur[g][j];
                     d.re_new[at] = nv[j];
                     d.re_moff[at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
                     if (d.fuse_rec && per) {
@@ -1007,6 +1016,15 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                 pmsg += per * n;
             }
         }
+    };
+    RecGrp<kOps, kGroup> A, B;
+    pick_load(A);
+    while (A.js[0] >= 0) {
+        pick_load(B);
+        process(A);
+        if (B.js[0] < 0) break;
+        pick_load(A);
+        process(B);
     }
     if (lane == 0) {
         d.t_re[rt] = pos;
