@@ -39,6 +39,8 @@ for step in "$@"; do
     ablate) run ablate 600 python tools/ablate.py --variants ${ABL:-0,8,4} ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
              python bench.py --steps 50 --warmup 5 --cpu-baseline off ;;
+    prof4) run prof4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof4" -o run -- \
+             python bench.py --config 4 --steps 20 --warmup 3 --cpu-baseline off ;;
     pmc)
       run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o run -- \
         tools/_bin/pmc_calib
