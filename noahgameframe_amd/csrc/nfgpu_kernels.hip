@@ -898,7 +898,13 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     }
     unsigned long long work = __ballot(my_mask != 0);
     unsigned pos = 0, pmsg = 0;  // tile-local
+    // this tile's output runs as wave-uniform base pointers, indexed by 32-bit tile-local offsets
     const size_t re0 = (size_t)rt * d.re_tcap;
+    uint32_t* const t_slot = d.re_slot + re0;
+    uint32_t* const t_rrc = d.re_rrc + re0;
+    uint64_t* const t_old = d.re_old + re0;
+    uint64_t* const t_new = d.re_new + re0;
+    uint32_t* const t_moff = d.re_moff + re0;
     const uint32_t mrb = d.fuse_rec ? d.msg_rb0 + (uint32_t)rt * d.msg_rtcap : 0u;  // fused: this tile's run
     // Two groups in flight: the next group's cell loads are issued before the current group's
     // stores, so its wait covers the stores' acknowledgements (vmcnt counts loads and stores in
@@ -922,7 +928,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     const int e = s0 + G.js[g];
                     G.used[g][j] = d.rops[j].used[e];
                     if (lane < d.rops[j].rows)
-                        G.cur[g][j] = d.rops[j].cells[((size_t)e * d.rops[j].cols + d.rops[j].col) * d.rops[j].rows + lane];
+                        G.cur[g][j] = (d.rops[j].cells + ((size_t)e * d.rops[j].cols + d.rops[j].col) * d.rops[j].rows)[lane];
                 }
             }
     };
@@ -962,7 +968,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     nb = (uint64_t)__double_as_longlong(v);
                 }
                 if (changed) {
-                    ro.cells[((size_t)e * ro.cols + ro.col) * ro.rows + lane] = nb;
+                    (ro.cells + ((size_t)e * ro.cols + ro.col) * ro.rows)[lane] = nb;
                     bytes += 8;
                     ch[j] = nb != c;  // coalesced diff: bits must differ
                     nv[j] = nb;
@@ -985,13 +991,12 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
 #pragma unroll
                 for (int j = 0; j < kOps; j++) {
                     if (!(j >= j0 && j <= j1 && ch[j])) continue;
-                    const size_t at = re0 + p;
                     const uint32_t lmo = pmsg + per * (p - pos);
-                    d.re_slot[at] = (uint32_t)e;
-                    d.re_rrc[at] = ((uint32_t)d.rops[j].rec << 16) | ((uint32_t)lane << 8) | (uint32_t)d.rops[j].col;
-                    d.re_old[at] = G.cur[g][j];
-                    d.re_new[at] = nv[j];
-                    d.re_moff[at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
+                    t_slot[p] = (uint32_t)e;
+                    t_rrc[p] = ((uint32_t)d.rops[j].rec << 16) | ((uint32_t)lane << 8) | (uint32_t)d.rops[j].col;
+                    t_old[p] = G.cur[g][j];
+                    t_new[p] = nv[j];
+                    t_moff[p] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
                     if (d.fuse_rec && per) {
                         // GetBroadCastObject (AOI:531-593) for the record event, into the tile's run
                         uint32_t* out = d.msg_rcpt + mrb + lmo;
