@@ -876,6 +876,8 @@ struct RecGrp {  // one group of slots with record work: their cells and used-ro
 template <int kOps, int kGroup>
 __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
+    __shared__ uint64_t s_eold[kTPB / 64][kOps * 64], s_enew[kTPB / 64][kOps * 64];  // a span's events,
+    __shared__ uint32_t s_errc[kTPB / 64][kOps * 64];                                // per wave
     for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
         ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
     __syncthreads();
@@ -988,15 +990,29 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                 unsigned p = pos + inc - c;
                 const uint8_t rfl = s_rflags[cls][d.rops[j0].rec];
                 const unsigned per = event_msgs(desc, rfl);
+                // stage the span's events in this wave's LDS rows at their span index, then write
+                // them back dense: lane q stores event q of every output array (full, contiguous
+                // runs instead of one sparse store per op and array)
+                unsigned q = p - pos;
 #pragma unroll
                 for (int j = 0; j < kOps; j++) {
                     if (!(j >= j0 && j <= j1 && ch[j])) continue;
-                    const uint32_t lmo = pmsg + per * (p - pos);
-                    t_slot[p] = (uint32_t)e;
-                    t_rrc[p] = ((uint32_t)d.rops[j].rec << 16) | ((uint32_t)lane << 8) | (uint32_t)d.rops[j].col;
-                    t_old[p] = G.cur[g][j];
-                    t_new[p] = nv[j];
-                    t_moff[p] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
+                    s_eold[w][q] = G.cur[g][j];
+                    s_enew[w][q] = nv[j];
+                    s_errc[w][q] = ((uint32_t)d.rops[j].rec << 16) | ((uint32_t)lane << 8) | (uint32_t)d.rops[j].col;
+                    q++;
+                }
+                __builtin_amdgcn_wave_barrier();  // (one wave's LDS operations complete in order)
+                for (unsigned q0 = 0; q0 < n; q0 += 64) {
+                    const unsigned qq = q0 + (unsigned)lane;
+                    if (qq >= n) break;
+                    const unsigned at = pos + qq;
+                    const uint32_t lmo = pmsg + per * qq;
+                    t_slot[at] = (uint32_t)e;
+                    t_rrc[at] = s_errc[w][qq];
+                    t_old[at] = s_eold[w][qq];
+                    t_new[at] = s_enew[w][qq];
+                    t_moff[at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
                     if (d.fuse_rec && per) {
                         // GetBroadCastObject (AOI:531-593) for the record event, into the tile's run
                         uint32_t* out = d.msg_rcpt + mrb + lmo;
@@ -1006,17 +1022,17 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                             const uint32_t np = (uint32_t)((desc >> 32) & 0x3FFF);
                             const uint32_t r1 = (uint32_t)((desc >> 46) & 0x3FFF);
                             uint32_t k = 0;
-                            for (uint32_t q = 0; q < np; q++) {
-                                if (q + 1 == r1) continue;
-                                out[k++] = (uint32_t)d.pl_slot[(uint32_t)desc + q];
+                            for (uint32_t u = 0; u < np; u++) {
+                                if (u + 1 == r1) continue;
+                                out[k++] = (uint32_t)d.pl_slot[(uint32_t)desc + u];
                             }
                             bytes += 4 * np;
                         }
                         bytes += 4 * per;
                     }
-                    p++;
                     bytes += 28;
                 }
+                __builtin_amdgcn_wave_barrier();
                 pos += n;
                 pmsg += per * n;
             }
