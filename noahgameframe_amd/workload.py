@@ -67,7 +67,7 @@ def _prop_flags():
     return f
 
 
-def programs(with_records, rec_float_op=True):
+def programs(with_records, rec_float_op=True, rec_skill_op=False):
     ops = np.zeros((len(KINDS), MAX_OPS), OP_DTYPE)
     n_ops = np.zeros(len(KINDS), np.int32)
 
@@ -88,6 +88,8 @@ def programs(with_records, rec_float_op=True):
         lst = [(OP_RIADD_CLAMP, 0, (0 << 8) | 1, 0, -100, 0, I64_MAX)]
         if rec_float_op:
             lst.append((OP_RFAFFINE, 0, (0 << 8) | 2, 0, f64bits(0.5), f64bits(0.0), 0))
+        if rec_skill_op:  # a third column op (skill id +1, clamped to [1000, 1999]), after cols 1, 2
+            lst.append((OP_RIADD_CLAMP, 0, (0 << 8) | 0, 0, 1, 1000, 1999))
         put("SkillCD", lst)
     return ops, n_ops
 
@@ -102,7 +104,7 @@ def _names(lst):
 
 def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4, n_ticks=8,
                tick_ms=100, seed=1, ext_frac=0.05, host_ops=True, records=False, rec_rows=64,
-               t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, sched_edges=False,
+               t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, rec_skill_op=False, sched_edges=False,
                switch_frac=0.0, switch_new_groups=False, rec_steady=False):
     rng = np.random.default_rng(seed)
     n_groups = n_scenes * groups_per_scene
@@ -159,7 +161,7 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
     still = rng.random(n_obj) < 0.02
     init_f[fi["X"], still] = init_f[fi["TargetX"], still]
 
-    ops, n_ops = programs(records, rec_float_op)
+    ops, n_ops = programs(records, rec_float_op, rec_skill_op)
     n_kind = len(KINDS) if records else len(KINDS) - 1
 
     # ---- heartbeats registered before the first frame ----

@@ -45,6 +45,9 @@ def test_golden_fixtures_are_nontrivial():
     (5, dict(n_obj=700, n_scenes=2, groups_per_scene=5, players_per_group=3, sched_edges=True)),
     (6, dict(n_obj=800, n_scenes=3, groups_per_scene=4, players_per_group=3, switch_frac=0.05,
              switch_new_groups=True)),
+    # two int column ops in one program, the second on a lower column (event order is (row, col))
+    (7, dict(n_obj=400, n_scenes=2, groups_per_scene=3, players_per_group=4, records=True, rec_rows=24,
+             rec_float_op=False, rec_skill_op=True)),
 ])
 def test_oracle_matches_reference(seed, kw):
     w = workload.make_world(n_ticks=9, seed=seed, **kw)
