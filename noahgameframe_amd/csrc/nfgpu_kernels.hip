@@ -860,7 +860,9 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
 
 // ---------------------------------------------------------------------------------
 // Record effects: one wave per 64-slot record tile, lane = row; the wave walks its slots in
-// order, kGroup at a time with every cell load of the group issued before any is consumed.
+// order, kGroup at a time with every cell load of the group issued before any is consumed and
+// the next group's loads issued before this group's stores.  A record span's events are staged
+// in the wave's LDS rows and stored dense; changed cells are written back non-temporally.
 // Cells [cap][cols][rows] so a wave reads one (slot, col) row-vector contiguously.
 
 // kOps: register slots for the record ops (>= n_rops), kGroup: slots whose cells are in flight
