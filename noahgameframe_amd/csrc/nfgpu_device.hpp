@@ -106,6 +106,9 @@ struct Tables {
     int32_t p_str[kMaxProps];
     uint32_t umask[NFK_MAX_KINDS];                 // kind k's U slots: writable bits | read-only indices << 16
     uint8_t opu[NFK_MAX_KINDS][NFK_MAX_OPS][4];    // U slot of dst, a, b, c (0x80 | r: read-only r; kNoU = immediate)
+    // property -> writable U slot (a program destination), kNoU otherwise.  A queued Set of a
+    // property with a slot joins that slot's diff; any other queued Set is a "standalone" event.
+    uint8_t w_slot[kMaxProps];
     int32_t nops[NFK_MAX_KINDS];
     uint8_t pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
     uint8_t rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
@@ -130,12 +133,18 @@ struct Dev {
     SchedHot* s_hot;
     SchedCold* s_cold;
     uint8_t* e_flags;  // bit0: a RemoveSchedule(self, name) is queued (owns the remove-list key)
-    // queued SetProperty* calls, sorted by slot (stable)
-    uint32_t* ext_head;  // [cap] 0 = none, else 1 + first op index
+    // queued SetProperty* calls folded into (slot, property) GROUPS, sorted by (slot, property);
+    // group g's calls are x_bits[x_first[g], x_first[g + 1]) in call order.  k_sets applies each
+    // group through the change predicates before the frame's heartbeat scan and leaves the
+    // frame-start value in x_old[g] and the value after the group in x_new[g].
+    uint32_t* ext_head;  // [cap] 0 = none, else 1 + first group of the slot
     const uint32_t* x_slot;
     const uint32_t* x_pid;
+    const uint32_t* x_first;  // [n_x + 1]
     const uint64_t* x_bits;
-    int32_t n_x;
+    uint64_t* x_old;
+    uint64_t* x_new;
+    int32_t n_x;              // groups
     uint32_t* fired_mask;  // [cap]
     // records: cells [cap][cols][rows], used masks [cap]
     uint64_t* rcells[NFK_MAX_RECORDS];
@@ -153,8 +162,8 @@ struct Dev {
     // algorithmic-byte tallies: [3 kernels][kTallyN][8] (one 64-byte line per counter), spread
     // over kTallyN addresses so that workgroups do not serialise on one atomic
     unsigned long long* tally;
-    // frame working set (k_tick): properties of the U slots, their columns, writable slots in
-    // property-id order, and the slot of each property queued by SetProperty this frame
+    // working set of the programs (k_tick, fixed at commit): properties of the U slots, their
+    // columns, writable slots in property-id order
     int32_t n_w, n_u;         // writable slots [0, n_w), read-only slots [n_w, n_u)
     int32_t u_pid[kMaxU];
     uint64_t* u_col[kMaxU];   // property of slot e at u_col[j][e * u_str[j]]
@@ -164,7 +173,6 @@ struct Dev {
     // per class: writable slots whose events go to the scene group (public, bits 0-15) and to the
     // entity itself only (private & !upload & !public, bits 16-31); GetBroadCastObject (AOI:531)
     uint32_t u_cmask[NFK_MAX_CLASSES];
-    const uint8_t* u_slot;  // [n_prop], only when n_x > 0
     // tiles: property/fired tile t = slots [t*kTile, (t+1)*kTile); record tile r = slots
     // [r*kRTile, (r+1)*kRTile).  Outputs of a tile sit at [t*tile_cap, t*tile_cap + count).
     int32_t n_tiles, n_rtiles;

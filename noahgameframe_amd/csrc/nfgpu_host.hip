@@ -107,6 +107,7 @@ struct World {
     std::vector<std::vector<uint64_t>> init_props;
     std::vector<std::vector<uint64_t>> init_rcells, init_rused;
     std::vector<bool> rec_defined;
+    uint8_t rec_ctype[NFK_MAX_RECORDS][NFK_MAX_REC_COLS] = {};  // 0 = int64, 1 = f64
 
     Tables tab{};
     bool kind_defined[NFK_MAX_KINDS] = {};
@@ -131,6 +132,11 @@ struct World {
     // window's membership changes
     struct XOp { uint32_t slot, pid; uint64_t bits; };
     std::vector<XOp> xops;
+    // per-frame SetProperty groups (host scratch kept across frames) and their device results
+    std::vector<uint32_t> g_slot, g_pid, g_first, xord, xord_t;
+    std::vector<uint64_t> xkey, xkey_t;
+    void* xs_buf = nullptr;  // x_old / x_new
+    size_t xs_cap = 0;
     struct HOp { int32_t code; uint32_t slot, kind; float interval; int32_t count; int64_t time; };
     std::vector<HOp> hops;
 
@@ -148,6 +154,11 @@ struct World {
     bool scan_pending = false;  // the last frame's dense ranks (k_scan_tiles) are built on first read
     Dev scan_dev;               // ... with that frame's Dev
     int64_t last_rec_msgs = 0;  // record-tile messages of the last summarised frame (capacity hint)
+    // the last frame ran k_fanout: its error word is copied to err_pin (event err_done) and
+    // checked before anything reads or replaces that frame's fan-out (check_fanout)
+    bool fan_unchecked = false;
+    unsigned* err_pin = nullptr;
+    hipEvent_t err_done = nullptr;
     int32_t max_np = 0;    // most players in one scene group (an upper bound between full re-layouts)
 
     bool profiling = false;
@@ -385,6 +396,99 @@ int dev_reserve(World* w, void** p, size_t* cap, size_t bytes) {
     return NFK_OK;
 }
 
+// stable LSD radix sort of (key, value) pairs on the low `bits` bits of the keys (11-bit digits;
+// a digit that every key shares is skipped)
+void radix_sort_stable(std::vector<uint64_t>& k, std::vector<uint32_t>& v, std::vector<uint64_t>& tk,
+                       std::vector<uint32_t>& tv, int bits) {
+    const size_t n = k.size();
+    if (n < 2) return;
+    tk.resize(n);
+    tv.resize(n);
+    for (int sh = 0; sh < bits; sh += 11) {
+        size_t cnt[2048] = {};
+        for (size_t i = 0; i < n; i++) cnt[(k[i] >> sh) & 2047]++;
+        if (cnt[(k[0] >> sh) & 2047] == n) continue;
+        size_t acc = 0;
+        for (int b = 0; b < 2048; b++) {
+            const size_t c = cnt[b];
+            cnt[b] = acc;
+            acc += c;
+        }
+        for (size_t i = 0; i < n; i++) {
+            const size_t at = cnt[(k[i] >> sh) & 2047]++;
+            tk[at] = k[i];
+            tv[at] = v[i];
+        }
+        k.swap(tk);
+        v.swap(tv);
+    }
+}
+
+// replace a tracked device allocation by a bigger one (contents dropped)
+int regrow(World* w, void** p, size_t bytes) {
+    if (*p) {
+        HIPCHK(hipFree(*p));
+        w->allocs.erase(std::remove(w->allocs.begin(), w->allocs.end(), *p), w->allocs.end());
+        *p = nullptr;
+    }
+    return alloc_track(w, p, bytes);
+}
+
+// the property-event tiles with room for `per_tile` events each (a frame with many standalone
+// SetProperty groups in one tile); the previous frame's events are dropped
+int grow_event_tiles(World* w, int64_t per_tile) {
+    Dev& d = w->d;
+    const int64_t tcap = (per_tile + kTile - 1) / kTile * kTile;
+    if (tcap > 0xFFFF) return fail(NFK_ERR_CAPACITY, "more than 65535 property events in one 256-slot tile");
+    HIPCHK(hipStreamSynchronize(w->stream));
+    const size_t n = (size_t)(d.cap / kTile) * (size_t)tcap;
+    int r;
+    if ((r = regrow(w, (void**)&d.ev_slot, n * 4)) || (r = regrow(w, (void**)&d.ev_pid, n * 4)) ||
+        (r = regrow(w, (void**)&d.ev_old, n * 8)) || (r = regrow(w, (void**)&d.ev_new, n * 8)) ||
+        (r = regrow(w, (void**)&d.ev_moff, n * 4))) {
+        d.ev_tcap = 0;
+        return r;
+    }
+    d.ev_tcap = (int32_t)tcap;
+    w->scan_pending = false;
+    return NFK_OK;
+}
+
+// the programs' working set (Dev::u_*): writable slots = program destinations in property-id
+// order, then the properties programs only read; event order and fan-out classes of the writable
+// slots, all read by k_tick as scalars
+void set_working_set(World* w) {
+    Dev& d = w->d;
+    const int n_w = (int)w->u_wp.size(), n_r = (int)w->u_rp.size();
+    for (int j = 0; j < kMaxU; j++) d.u_pid[j] = -1;
+    d.n_w = d.n_u = 0;
+    if (!w->u_ok) return;
+    for (int i = 0; i < n_w; i++) d.u_pid[i] = w->u_wp[i];
+    for (int i = 0; i < n_r; i++) d.u_pid[n_w + i] = w->u_rp[i];
+    d.n_w = n_w;
+    d.n_u = n_w + n_r;
+    for (int i = 0; i < kMaxW; i++) d.u_order[i] = i < n_w ? i : 0;  // (u_wp is in property-id order)
+    for (int j = 0; j < kMaxU; j++) {
+        const int p = d.u_pid[j];
+        d.u_col[j] = p < 0 ? nullptr : d.pmem + w->tab.p_off[p];
+        d.u_str[j] = p < 0 ? 0 : w->tab.p_str[p];
+    }
+    for (int j = 0; j < kMaxW; j++) {
+        d.u_lower[j] = 0;
+        for (int i = 0; i < n_w && j < n_w; i++)
+            if (d.u_pid[i] < d.u_pid[j]) d.u_lower[j] |= 1u << i;
+    }
+    for (int c = 0; c < NFK_MAX_CLASSES; c++) {
+        uint32_t pub = 0, priv = 0;
+        for (int j = 0; j < n_w && c != 15; j++) {  // (class 15 marks a free slot)
+            const uint8_t f = w->tab.pflags[c][d.u_pid[j]];
+            if (f & NFK_PUBLIC) pub |= 1u << j;
+            else if ((f & NFK_PRIVATE) && !(f & NFK_UPLOAD)) priv |= 1u << j;
+        }
+        d.u_cmask[c] = pub | (priv << 16);
+    }
+}
+
 // w->mhost -> w->mlist, asynchronously on the world's stream (through a pinned double buffer:
 // a buffer is refilled only once the copy from it two uploads ago has completed)
 int upload_mhost(World* w) {
@@ -429,14 +533,18 @@ int apply_membership(World* w) {
     if (w->touched.empty()) return NFK_OK;
     Dev& d = w->d;
     const auto cmp = [w](int32_t a, int32_t b) { return guid_less(w, a, b); };
+    // The new member lists are built on copies of the affected segments; nothing of the world
+    // changes before every check has passed (a failure leaves the window's calls queued).
     bool full = false;
     std::vector<int32_t> aff;
-    std::vector<char> is_aff(w->segs.size(), 0);
-    auto mark = [&](int32_t g) {
-        if (!is_aff[g]) {
-            is_aff[g] = 1;
+    std::map<int32_t, World::Seg> edit;  // affected segment -> its new member list
+    auto seg_copy = [&](int32_t g) -> World::Seg& {
+        auto it = edit.find(g);
+        if (it == edit.end()) {
+            it = edit.emplace(g, w->segs[g]).first;
             aff.push_back(g);
         }
+        return it->second;
     };
     auto seg_at = [&](int32_t slot) {
         int32_t lo = 0, hi = (int32_t)w->segs.size() - 1;
@@ -450,11 +558,9 @@ int apply_membership(World* w) {
     for (int32_t o : w->touched) {
         const int32_t s = w->slot_of_obj[o];
         if (s < 0) continue;
-        const int32_t g = seg_at(s);
-        auto& v = w->segs[g].objs;
+        auto& v = seg_copy(seg_at(s)).objs;
         auto it = std::lower_bound(v.begin(), v.end(), o, cmp);
         if (it != v.end() && *it == o) v.erase(it);
-        mark(g);
     }
     for (int32_t o : w->touched) {
         if (!w->alive[o]) continue;
@@ -463,22 +569,22 @@ int apply_membership(World* w) {
             full = true;
             continue;
         }
-        auto& v = w->segs[f->second].objs;
+        auto& v = seg_copy(f->second).objs;
         v.insert(std::lower_bound(v.begin(), v.end(), o, cmp), o);
-        mark(f->second);
     }
     for (int32_t g : aff)
-        if ((int32_t)w->segs[g].objs.size() > w->segs[g].cap) full = true;
+        if ((int32_t)edit[g].objs.size() > edit[g].cap) full = true;
 
     std::vector<int32_t> pack_src, un_dst;
     std::vector<int64_t> un_src;
     MetaLists m;
     std::vector<World::Seg> nsegs;
+    const int32_t max_np0 = w->max_np;
     if (full) {
         int64_t total = plan_segments(w, w->slack, nsegs);
         if (total > d.cap) total = plan_segments(w, 0, nsegs);
+        if (total > d.cap) return fail(NFK_ERR_CAPACITY, "entity capacity exceeded (nothing of the window applied)");
         w->max_np = 0;  // recomputed by seg_meta over every segment below
-        if (total > d.cap) return fail(NFK_ERR_CAPACITY, "entity capacity exceeded");
         for (const auto& g : nsegs) {
             for (int32_t i = 0; i < g.cap; i++) {
                 const int32_t ns = g.base + i;
@@ -497,12 +603,14 @@ int apply_membership(World* w) {
                 }
             }
             int r = seg_meta(w, g, m);
-            if (r) return r;
+            if (r) {
+                w->max_np = max_np0;
+                return r;
+            }
         }
-        w->n_relayout_full++;
     } else {
         for (int32_t gi : aff) {
-            const World::Seg& g = w->segs[gi];
+            const World::Seg& g = edit[gi];
             for (int32_t i = 0; i < g.cap; i++) {
                 const int32_t ns = g.base + i;
                 if (i >= (int32_t)g.objs.size()) {
@@ -523,9 +631,11 @@ int apply_membership(World* w) {
                 }
             }
             int r = seg_meta(w, g, m);
-            if (r) return r;
+            if (r) {
+                w->max_np = max_np0;
+                return r;
+            }
         }
-        w->n_relayout_seg++;
     }
 
     // device: pack movers (old slots), then unpack into the new layout, then the metadata
@@ -555,6 +665,7 @@ int apply_membership(World* w) {
 
     // host maps
     if (full) {
+        w->n_relayout_full++;
         w->segs = std::move(nsegs);
         w->seg_of.clear();
         for (size_t g = 0; g < w->segs.size(); g++) w->seg_of[{w->segs[g].scene, w->segs[g].group}] = (int32_t)g;
@@ -565,6 +676,9 @@ int apply_membership(World* w) {
         set_tiles(d, (int32_t)total);
         aff.clear();
         for (size_t g = 0; g < w->segs.size(); g++) aff.push_back((int32_t)g);
+    } else {
+        w->n_relayout_seg++;
+        for (int32_t gi : aff) w->segs[gi].objs = std::move(edit[gi].objs);
     }
     for (int32_t o : w->touched)
         if (!w->alive[o]) w->slot_of_obj[o] = -1;
@@ -614,6 +728,8 @@ void touch(World* w, int32_t o) {
 
 extern "C" {
 
+static int check_fanout(World* w);
+
 const char* nfk_last_error(void) { return g_err.c_str(); }
 
 int nfk_create(const nfk_config* cfg, void** out) {
@@ -640,7 +756,9 @@ int nfk_create(const nfk_config* cfg, void** out) {
     }
     if (hipEventCreateWithFlags(&w->pin_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&w->mpin_done[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&w->mpin_done[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&w->mpin_done[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->err_done, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc((void**)&w->err_pin, 64, hipHostMallocDefault) != hipSuccess) {
         delete w;
         return fail(NFK_ERR_HIP, "hipEventCreate failed");
     }
@@ -663,12 +781,15 @@ int nfk_destroy(void* world) {
     if (w->ins_rows) (void)hipFree(w->ins_rows);
     if (w->mv_rows) (void)hipFree(w->mv_rows);
     if (w->mlist) (void)hipFree(w->mlist);
+    if (w->xs_buf) (void)hipFree(w->xs_buf);
     for (auto& p : w->pend) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
     }
     for (auto e : w->evpool) (void)hipEventDestroy(e);
     if (w->pin_done) (void)hipEventDestroy(w->pin_done);
+    if (w->err_done) (void)hipEventDestroy(w->err_done);
+    if (w->err_pin) (void)hipHostFree(w->err_pin);
     for (int i = 0; i < 2; i++) {
         if (w->mpin_done[i]) (void)hipEventDestroy(w->mpin_done[i]);
         if (w->mpin[i]) (void)hipHostFree(w->mpin[i]);
@@ -695,8 +816,11 @@ int nfk_define_record(void* world, int32_t rec, int32_t rows, int32_t cols, cons
     w->tab.rec_rows[rec] = rows;
     w->tab.rec_cols[rec] = cols;
     for (int c = 0; c < w->cfg.n_class; c++) w->tab.rflags[c][rec] = flags_per_class[c];
+    for (int c = 0; c < cols; c++) {
+        if (col_types && col_types[c] > 1) return fail(NFK_ERR_ARG, "record column type must be 0 (int64) or 1 (f64)");
+        w->rec_ctype[rec][c] = col_types ? col_types[c] : 0;
+    }
     w->rec_defined[rec] = true;
-    (void)col_types;  // cell type is carried by the op (RIADD_CLAMP = int64, RFAFFINE = f64)
     return NFK_OK;
 }
 
@@ -727,6 +851,10 @@ int nfk_define_kind(void* world, int32_t kind, const nfk_op* ops, int32_t n_ops)
             int r = op.dst >> 8, col = op.dst & 255;
             if (r >= w->cfg.n_rec || !w->rec_defined[r] || col >= w->tab.rec_cols[r])
                 return fail(NFK_ERR_ARG, "record op on undefined record/col");
+            // NFCRecord::SetInt / SetFloat refuse a cell of the other type (RC:189, RC:250): such
+            // an op could never change a cell, so it is rejected with the kind
+            if (w->rec_ctype[r][col] != (op.code == NFK_OP_RFAFFINE ? 1 : 0))
+                return fail(NFK_ERR_ARG, "record op type does not match the column type");
             break;
         }
         case NFK_OP_NOP:
@@ -839,6 +967,8 @@ int nfk_commit(void* world) {
         w->u_ok = (int)W.size() <= kMaxW && (int)(W.size() + R.size()) <= kMaxU;
         w->u_wp.assign(W.begin(), W.end());
         w->u_rp.assign(R.begin(), R.end());
+        memset(w->tab.w_slot, kNoU, sizeof w->tab.w_slot);
+        for (size_t i = 0; i < W.size() && i < (size_t)kMaxW; i++) w->tab.w_slot[W[i]] = (uint8_t)i;
         auto slot = [&](int64_t p) -> uint8_t {
             auto it = std::lower_bound(W.begin(), W.end(), (int)p);
             if (it != W.end() && *it == p) return (uint8_t)(it - W.begin());
@@ -1012,6 +1142,7 @@ int nfk_commit(void* world) {
             off += (int64_t)g.size() * cap + cpad;
         }
     }
+    set_working_set(w);
     ALLOC(d.s_hot, (size_t)std::max(NK, 1) * d.s_kstr * sizeof(SchedHot));
     ALLOC(d.s_cold, (size_t)std::max(NK, 1) * d.s_kstr * sizeof(SchedCold));
     ALLOC(d.e_flags, cap);
@@ -1033,7 +1164,7 @@ int nfk_commit(void* world) {
     }
     d.pl_slot = w->pl_slot_w;
     // output staging sized for every tile of the slot capacity
-    d.ev_tcap = kTile * std::min(NFK_MAX_TOUCH, std::max(w->n_prop, 1));
+    d.ev_tcap = kTile * std::max(w->n_dst_union, 1);  // grows for frames with standalone SetProperty groups
     d.fi_tcap = kTile * std::max(NK, 1);
     d.re_tcap = (int32_t)(kRTile * std::max<size_t>(rec_events_per_ent, 1));
     const size_t nt = cap / kTile, nrt = cap / kRTile;
@@ -1376,14 +1507,14 @@ int nfk_execute(void* world, int64_t now_ms) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    {
+        int r = check_fanout(w);  // the last frame's fan-out is complete before it is replaced
+        if (r) return r;
+    }
     // ---- membership changes of this window, then queued calls: object -> slot ----
     {
         int r = apply_membership(w);
-        if (r) {
-            w->xops.clear();
-            w->hops.clear();
-            return r;
-        }
+        if (r) return r;  // nothing of the window applied; its calls stay queued
         size_t k = 0;
         for (size_t i = 0; i < w->xops.size(); i++) {
             const int32_t sl = w->slot_of_obj[w->xops[i].slot];
@@ -1405,24 +1536,60 @@ int nfk_execute(void* world, int64_t now_ms) {
     d.now = now_ms;
 
     // ---- host-side preparation of queued calls ----
-    // SetProperty*: stable by slot keeps call order per entity
-    std::stable_sort(w->xops.begin(), w->xops.end(), [](const World::XOp& a, const World::XOp& b) { return a.slot < b.slot; });
-    // touch-capacity check: written props per entity (programs' union + queued sets)
-    for (size_t i = 0; i < w->xops.size();) {
-        size_t j = i;
-        uint64_t m0 = w->dst_union_mask[0], m1 = w->dst_union_mask[1];
-        while (j < w->xops.size() && w->xops[j].slot == w->xops[i].slot) {
-            uint32_t p = w->xops[j].pid;
-            if (p < 64) m0 |= 1ull << p;
-            else m1 |= 1ull << (p - 64);
-            j++;
+    // SetProperty*: (slot, property) groups, each group's calls in call order (a stable radix sort
+    // by slot << 7 | property); the most standalone groups (properties no program writes) of one
+    // 256-slot tile bounds the tile's events beside the program slots
+    const size_t nxc = w->xops.size();
+    std::vector<uint32_t>& g_slot = w->g_slot;
+    std::vector<uint32_t>& g_pid = w->g_pid;
+    std::vector<uint32_t>& g_first = w->g_first;
+    g_slot.clear();
+    g_pid.clear();
+    g_first.clear();
+    int64_t max_sa = 0;
+    if (nxc) {
+        std::vector<uint64_t>& key = w->xkey;
+        std::vector<uint32_t>& ord = w->xord;
+        key.resize(nxc);
+        ord.resize(nxc);
+        for (size_t i = 0; i < nxc; i++) {
+            key[i] = ((uint64_t)w->xops[i].slot << 7) | w->xops[i].pid;
+            ord[i] = (uint32_t)i;
         }
-        if (__builtin_popcountll(m0) + __builtin_popcountll(m1) > NFK_MAX_TOUCH) {
-            w->xops.clear();
-            w->hops.clear();
-            return fail(NFK_ERR_TOUCH, "more than NFK_MAX_TOUCH properties written for one entity in one frame");
+        radix_sort_stable(key, ord, w->xkey_t, w->xord_t, 31 + 7);
+        int64_t tile_sa = 0;
+        uint32_t cur_tile = 0xFFFFFFFFu;
+        for (size_t i = 0; i < nxc; i++) {
+            if (i == 0 || key[i] != key[i - 1]) {
+                const uint32_t sl = (uint32_t)(key[i] >> 7), pid = (uint32_t)(key[i] & 127);
+                g_slot.push_back(sl);
+                g_pid.push_back(pid);
+                g_first.push_back((uint32_t)i);
+                if (w->tab.w_slot[pid] == kNoU) {
+                    if (sl / kTile != cur_tile) {
+                        cur_tile = sl / kTile;
+                        tile_sa = 0;
+                    }
+                    max_sa = std::max(max_sa, ++tile_sa);
+                }
+            }
         }
-        i = j;
+        g_first.push_back((uint32_t)nxc);
+    }
+    // a tile's events: its slots' program destinations plus its standalone Set groups
+    {
+        const int64_t need_ev = (int64_t)kTile * std::max(w->n_dst_union, 1) + max_sa;
+        if (need_ev > w->d.ev_tcap) {
+            int r = grow_event_tiles(w, need_ev);
+            if (r) {
+                w->xops.clear();
+                w->hops.clear();
+                return r;
+            }
+            d.ev_tcap = w->d.ev_tcap;
+            d.ev_slot = w->d.ev_slot; d.ev_pid = w->d.ev_pid; d.ev_old = w->d.ev_old;
+            d.ev_new = w->d.ev_new; d.ev_moff = w->d.ev_moff;
+        }
     }
     // schedule calls: pre-scan (remove-list key owner, RemoveSchedule(self)) and post-scan (remove, add)
     std::vector<uint32_t> pre_slot, pre_op;
@@ -1466,76 +1633,33 @@ int nfk_execute(void* world, int64_t now_ms) {
         }
     }
 
-    // ---- frame working set of k_tick (Dev::u_*): program slots + this frame's SetProperty
-    //      properties; a frame whose set does not fit runs k_tick_touch instead ----
-    bool use_u = w->u_ok && !(d.ablate & kAblPerKind);
-    std::vector<uint8_t> uslot;
-    if (use_u) {
-        int n_w = (int)w->u_wp.size();
-        for (int j = 0; j < kMaxU; j++) d.u_pid[j] = -1;
-        for (int i = 0; i < n_w; i++) d.u_pid[i] = w->u_wp[i];
-        const int n_r = (int)w->u_rp.size();
-        if (!w->xops.empty()) {
-            uslot.assign(w->n_prop, 0xFF);
-            for (int i = 0; i < n_w; i++) uslot[w->u_wp[i]] = (uint8_t)i;
-            for (const auto& x : w->xops) {
-                if (uslot[x.pid] != 0xFF) continue;
-                if (std::binary_search(w->u_rp.begin(), w->u_rp.end(), (int)x.pid) || n_w == kMaxW ||
-                    n_w + n_r == kMaxU) {
-                    use_u = false;
-                    break;
-                }
-                uslot[x.pid] = (uint8_t)n_w;
-                d.u_pid[n_w++] = (int32_t)x.pid;
-            }
-        }
-        d.n_w = n_w;
-        for (int i = 0; i < n_r; i++) d.u_pid[n_w + i] = w->u_rp[i];
-        d.n_u = n_w + n_r;
-        std::vector<int> ord(n_w);
-        for (int i = 0; i < n_w; i++) ord[i] = i;
-        std::sort(ord.begin(), ord.end(), [&](int a, int b) { return d.u_pid[a] < d.u_pid[b]; });
-        for (int i = 0; i < n_w; i++) d.u_order[i] = ord[i];
-        for (int j = 0; j < kMaxU; j++) {
-            const int p = d.u_pid[j];
-            d.u_col[j] = p < 0 ? nullptr : d.pmem + w->tab.p_off[p];
-            d.u_str[j] = p < 0 ? 0 : w->tab.p_str[p];
-        }
-        // event order and fan-out classes of the writable slots, read by k_tick as scalars
-        for (int j = 0; j < kMaxW; j++) {
-            d.u_lower[j] = 0;
-            for (int i = 0; i < n_w && j < n_w; i++)
-                if (d.u_pid[i] < d.u_pid[j]) d.u_lower[j] |= 1u << i;
-        }
-        for (int c = 0; c < NFK_MAX_CLASSES; c++) {
-            uint32_t pub = 0, priv = 0;
-            for (int j = 0; j < n_w && c != 15; j++) {  // (class 15 marks a free slot)
-                const uint8_t f = w->tab.pflags[c][d.u_pid[j]];
-                if (f & NFK_PUBLIC) pub |= 1u << j;
-                else if ((f & NFK_PRIVATE) && !(f & NFK_UPLOAD)) priv |= 1u << j;
-            }
-            d.u_cmask[c] = pub | (priv << 16);
-        }
-    }
-    if (!use_u) uslot.clear();
+    // k_tick runs the programs on the working set fixed at commit (Dev::u_*); a schema whose
+    // working set does not fit the register slots runs k_tick_touch
+    const bool use_u = w->u_ok && !(d.ablate & kAblPerKind);
 
     // ---- uploads through the pinned arena ----
-    const size_t nx = w->xops.size(), npre = pre_slot.size(), npost = post.size();
-    size_t off_xs = 0, off_xp = align16(off_xs + nx * 4), off_xb = align16(off_xp + nx * 4);
-    size_t off_ps = align16(off_xb + nx * 8), off_po = align16(off_ps + npre * 4);
+    const size_t ng = g_slot.size(), npre = pre_slot.size(), npost = post.size();
+    size_t off_xs = 0, off_xp = align16(off_xs + ng * 4), off_xf = align16(off_xp + ng * 4);
+    size_t off_xb = align16(off_xf + (ng + 1) * 4);
+    size_t off_ps = align16(off_xb + nxc * 8), off_po = align16(off_ps + npre * 4);
     size_t off_qs = align16(off_po + npre * 4), off_qk = align16(off_qs + npost * 4);
     size_t off_qo = align16(off_qk + npost * 4), off_qi = align16(off_qo + npost * 4);
     size_t off_qc = align16(off_qi + npost * 4), off_qt = align16(off_qc + npost * 4);
-    size_t off_us = align16(off_qt + npost * 8);
-    size_t total = align16(off_us + uslot.size());
-    if (total > 0 && (nx || npre || npost)) {
+    size_t total = align16(off_qt + npost * 8);
+    if (ng) {
+        int r = dev_reserve(w, (void**)&w->xs_buf, &w->xs_cap, ng * 16);
+        if (r) return r;
+    }
+    if (total > 0 && (ng || npre || npost)) {
         int r = pin_reserve(w, total);
         if (r) return r;
         char* P = (char*)w->pin;
-        for (size_t i = 0; i < nx; i++) {
-            ((uint32_t*)(P + off_xs))[i] = w->xops[i].slot;
-            ((uint32_t*)(P + off_xp))[i] = w->xops[i].pid;
-            ((uint64_t*)(P + off_xb))[i] = w->xops[i].bits;
+        if (ng) {
+            memcpy(P + off_xs, g_slot.data(), ng * 4);
+            memcpy(P + off_xp, g_pid.data(), ng * 4);
+            memcpy(P + off_xf, g_first.data(), (ng + 1) * 4);
+            uint64_t* xb = (uint64_t*)(P + off_xb);
+            for (size_t i = 0; i < nxc; i++) xb[i] = w->xops[w->xord[i]].bits;
         }
         for (size_t i = 0; i < npre; i++) {
             ((uint32_t*)(P + off_ps))[i] = pre_slot[i];
@@ -1549,26 +1673,29 @@ int nfk_execute(void* world, int64_t now_ms) {
             ((int32_t*)(P + off_qc))[i] = post[i].count;
             ((int64_t*)(P + off_qt))[i] = post[i].time;
         }
-        if (!uslot.empty()) memcpy(P + off_us, uslot.data(), uslot.size());
         HIPCHK(hipMemcpyAsync(w->stage, w->pin, total, hipMemcpyHostToDevice, w->stream));
         HIPCHK(hipEventRecord(w->pin_done, w->stream));
         w->pin_pending = true;
     }
     char* S = (char*)w->stage;
-    d.n_x = (int32_t)nx;
-    d.x_slot = nx ? (const uint32_t*)(S + off_xs) : nullptr;
-    d.x_pid = nx ? (const uint32_t*)(S + off_xp) : nullptr;
-    d.x_bits = nx ? (const uint64_t*)(S + off_xb) : nullptr;
-    d.u_slot = uslot.empty() ? nullptr : (const uint8_t*)(S + off_us);
+    d.n_x = (int32_t)ng;
+    d.x_slot = ng ? (const uint32_t*)(S + off_xs) : nullptr;
+    d.x_pid = ng ? (const uint32_t*)(S + off_xp) : nullptr;
+    d.x_first = ng ? (const uint32_t*)(S + off_xf) : nullptr;
+    d.x_bits = ng ? (const uint64_t*)(S + off_xb) : nullptr;
+    d.x_old = ng ? (uint64_t*)w->xs_buf : nullptr;
+    d.x_new = ng ? (uint64_t*)w->xs_buf + ng : nullptr;
     w->xops.clear();
     w->hops.clear();
 
     d.has_pre = npre > 0;
-    if (nx || npre) {
+    if (ng || npre) {
         TimeScope ts(w, KT_AUX);
-        if (nx)
-            hipLaunchKernelGGL(k_ext_scatter, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, w->stream,
-                               d.x_slot, (int32_t)nx, d.ext_head);
+        if (ng) {
+            hipLaunchKernelGGL(k_ext_scatter, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, w->stream,
+                               d.x_slot, (int32_t)ng, d.ext_head);
+            hipLaunchKernelGGL(k_sets, dim3((unsigned)((ng + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, d);
+        }
         if (npre)
             hipLaunchKernelGGL(k_pre_hostops, dim3((unsigned)((npre + 255) / 256)), dim3(256), 0, w->stream,
                                (const uint32_t*)(S + off_ps), (const uint32_t*)(S + off_po), (int32_t)npre,
@@ -1586,7 +1713,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     d.fuse_rec = 0;
     d.msg_rb0 = d.msg_rtcap = 0;
     if (use_u && d.n_tiles && !(d.ablate & (kAblNoFuse | kAblNoEmit))) {
-        const int64_t tcap = (int64_t)std::max(d.n_w, 1) * kTile * std::max(w->max_np, 1);
+        const int64_t tcap = (((int64_t)std::max(d.n_w, 1) * kTile + max_sa) * std::max(w->max_np, 1) + 3) & ~(int64_t)3;
         int64_t rtcap = 0;
         bool rfuse = false;
         if (d.has_recops && d.n_rtiles) {
@@ -1606,11 +1733,11 @@ int nfk_execute(void* world, int64_t now_ms) {
         if (tcap * d.n_tiles <= kMsgStrideLimit) {
             if (need > w->d.msg_cap) {  // grow before the frame (the previous frame's messages are dropped)
                 HIPCHK(hipStreamSynchronize(w->stream));
-                HIPCHK(hipFree(w->d.msg_rcpt));
-                w->allocs.erase(std::remove(w->allocs.begin(), w->allocs.end(), (void*)w->d.msg_rcpt),
-                                w->allocs.end());
-                int r = alloc_track(w, (void**)&w->d.msg_rcpt, (size_t)need * 4);
-                if (r) return r;
+                int r = regrow(w, (void**)&w->d.msg_rcpt, (size_t)need * 4);
+                if (r) {
+                    w->d.msg_cap = 0;
+                    return r;
+                }
                 w->d.msg_cap = need;
                 d.msg_rcpt = w->d.msg_rcpt;
                 d.msg_cap = need;
@@ -1689,9 +1816,14 @@ int nfk_execute(void* world, int64_t now_ms) {
     const int fan0 = d.fuse_fan ? d.n_tiles : 0;
     const int nfan = d.n_tiles + (d.has_recops && !d.fuse_rec ? d.n_rtiles : 0) - fan0;
     if (nfan > 0 && !(d.ablate & kAblNoEmit)) {  // (timing ablation: events were not written)
-        TimeScope ts(w, KT_FAN);
-        hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, (int32_t)fan0);
-        HIPCHK(hipGetLastError());
+        {
+            TimeScope ts(w, KT_FAN);
+            hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, (int32_t)fan0);
+            HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipMemcpyAsync(w->err_pin, &w->ctrl->err, sizeof(unsigned), hipMemcpyDeviceToHost, w->stream));
+        HIPCHK(hipEventRecord(w->err_done, w->stream));
+        w->fan_unchecked = true;
     }
     w->ticks++;
     return NFK_OK;
@@ -1733,11 +1865,56 @@ static int64_t frame_msgs(const World* w, const Ctrl& c) {
     return (int64_t)c.n_msgs_ptiles + (int64_t)c.msg_extent - fixed_msgs_reserved(w);
 }
 
+// The last frame's k_fanout found msg_rcpt too small: it wrote nothing (it checks the scanned
+// extent first) and only reads the event tiles and the membership CSR, so grow the message buffer
+// (keeping what k_tick's / k_records' own fan-out wrote) and re-run it for that frame.
+static int regrow_fanout(World* w, Ctrl& c) {
+    const int64_t extent = (int64_t)c.msg_extent;
+    const int64_t need = extent + extent / 4 + 1024;
+    if (need > 0xFFFFFFFFll) return fail(NFK_ERR_CAPACITY, "fan-out exceeds 2^32 messages per frame");
+    uint32_t* grown = nullptr;
+    int r = alloc_track(w, (void**)&grown, (size_t)need * 4);
+    if (r) return r;
+    if (w->last_tcap)
+        HIPCHK(hipMemcpy(grown, w->d.msg_rcpt, (size_t)fixed_msgs_reserved(w) * 4, hipMemcpyDeviceToDevice));
+    HIPCHK(hipFree(w->d.msg_rcpt));
+    w->allocs.erase(std::remove(w->allocs.begin(), w->allocs.end(), (void*)w->d.msg_rcpt), w->allocs.end());
+    w->d.msg_rcpt = grown;
+    w->d.msg_cap = need;
+    HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
+    Dev d = w->d;
+    const int fan0 = w->last_tcap ? d.n_tiles : 0;
+    const int nfan = d.n_tiles + (d.has_recops && !w->last_rtcap ? d.n_rtiles : 0) - fan0;
+    if (nfan > 0) hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, (int32_t)fan0);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(w->stream));
+    HIPCHK(hipMemcpy(&c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+    return NFK_OK;
+}
+
+// Before anything reads or replaces the last frame's fan-out: if its k_fanout overflowed the
+// message buffer, recover that frame now (whether or not nfk_summary_get was called).
+static int check_fanout(World* w) {
+    if (!w->fan_unchecked) return NFK_OK;
+    HIPCHK(hipEventSynchronize(w->err_done));
+    w->fan_unchecked = false;
+    if (!(*w->err_pin & kErrMsgCap)) return NFK_OK;
+    Ctrl c;
+    int r = read_ctrl(w, &c);
+    if (r) return r;
+    if (c.err & ~kErrMsgCap) return NFK_OK;  // (another device error: reported by nfk_summary_get)
+    return regrow_fanout(w, c);
+}
+
 int nfk_summary_get(void* world, nfk_summary* out) {
     World* w = (World*)world;
     if (!w || !out) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     Ctrl c;
+    {
+        int r = check_fanout(w);
+        if (r) return r;
+    }
     {
         int r = read_ctrl(w, &c);
         if (r) return r;
@@ -1762,29 +1939,8 @@ int nfk_summary_get(void* world, nfk_summary* out) {
         for (int k = 0; k < 3; k++) w->last_bytes[k] = tb[k];
     }
     if ((c.err & kErrMsgCap) && !(c.err & ~kErrMsgCap)) {
-        // k_fanout wrote nothing (it checks the scanned extent first) and only reads the event
-        // tiles and the membership CSR, so grow the message buffer (keeping what k_tick's own
-        // fan-out wrote) and re-run it for this frame.
-        const int64_t extent = (int64_t)c.msg_extent;
-        const int64_t need = extent + extent / 4 + 1024;
-        if (need > 0xFFFFFFFFll) return fail(NFK_ERR_CAPACITY, "fan-out exceeds 2^32 messages per frame");
-        uint32_t* grown = nullptr;
-        int r = alloc_track(w, (void**)&grown, (size_t)need * 4);
+        int r = regrow_fanout(w, c);
         if (r) return r;
-        if (w->last_tcap)
-            HIPCHK(hipMemcpy(grown, w->d.msg_rcpt, (size_t)fixed_msgs_reserved(w) * 4, hipMemcpyDeviceToDevice));
-        HIPCHK(hipFree(w->d.msg_rcpt));
-        w->allocs.erase(std::remove(w->allocs.begin(), w->allocs.end(), (void*)w->d.msg_rcpt), w->allocs.end());
-        w->d.msg_rcpt = grown;
-        w->d.msg_cap = need;
-        HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
-        Dev d = w->d;
-        const int fan0 = w->last_tcap ? d.n_tiles : 0;
-        const int nfan = d.n_tiles + (d.has_recops && !w->last_rtcap ? d.n_rtiles : 0) - fan0;
-        if (nfan > 0) hipLaunchKernelGGL(k_fanout, dim3((unsigned)nfan), dim3(kTPB), 0, w->stream, d, (int32_t)fan0);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(w->stream));
-        HIPCHK(hipMemcpy(&c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
     }
     w->last_rec_msgs = frame_msgs(w, c) - (int64_t)c.n_msgs_ptiles;
     out->device_error = (int32_t)c.err;
@@ -1801,7 +1957,9 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     World* w = (World*)world;
     if (!w || !o) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
-    int r = ensure_ranks(w);  // (asynchronous, on the world's stream like the frame)
+    int r = check_fanout(w);  // (synchronises only after a frame that ran k_fanout)
+    if (r) return r;
+    r = ensure_ranks(w);  // (asynchronous, on the world's stream like the frame)
     if (r) return r;
     const Dev& d = w->d;
     o->n_tiles = d.n_tiles; o->tile_slots = kTile;
@@ -1930,9 +2088,11 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
     if (!w) return fail(NFK_ERR_ARG, "null world");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     Ctrl c;
-    int r = read_ctrl(w, &c);
+    int r = check_fanout(w);
     if (r) return r;
-    if (c.msg_extent > (unsigned long long)w->d.msg_cap) return fail(NFK_ERR_CAPACITY, "call nfk_summary_get first");
+    r = read_ctrl(w, &c);
+    if (r) return r;
+    if (c.msg_extent > (unsigned long long)w->d.msg_cap) return fail(NFK_ERR_CAPACITY, "fan-out not recovered");
     const Dev& d = w->d;
     const size_t nm = (size_t)frame_msgs(w, c);
     // each tile's messages are one run at msg_base[tile]; the dense CSR walks tiles in order

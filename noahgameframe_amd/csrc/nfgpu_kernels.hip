@@ -22,10 +22,55 @@
 namespace nfgpu {
 
 // ---------------------------------------------------------------------------------
+// ext_head[slot] = 1 + the slot's first SetProperty group (groups sorted by slot)
 __global__ void k_ext_scatter(const uint32_t* __restrict__ x_slot, int32_t n, uint32_t* __restrict__ ext_head) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     if (i == 0 || x_slot[i] != x_slot[i - 1]) ext_head[x_slot[i]] = (uint32_t)i + 1;
+}
+
+// The SetProperty* calls queued before this frame (NFCKernelModule::SetPropertyInt/Float,
+// KM:323-347), one thread per (slot, property) group, in call order through the reference's
+// change predicates: NFCProperty::SetInt stores only a different value (PR:254-293), SetFloat
+// only when !IsZeroDouble(v - cur) with eps 1e-15 (PR:295-334, NFPlatform.h:362).  Calls on
+// different properties never interact and every call precedes the frame's heartbeat scan, so the
+// groups are independent.  The column gets the value after the group; x_old / x_new keep the
+// frame-start value and that value for the frame's diff.
+__global__ __launch_bounds__(kTPB) void k_sets(Dev d) {
+    const int g = blockIdx.x * kTPB + threadIdx.x;
+    if (g >= d.n_x) return;
+    const uint32_t pid = d.x_pid[g];
+    uint64_t* p = prop_ptr(d, pid, (int)d.x_slot[g]);
+    const uint64_t start = *p;
+    uint64_t cur = start;
+    const uint32_t i1 = d.x_first[g + 1];
+    const bool isint = (int)pid < d.n_int;
+    for (uint32_t i = d.x_first[g]; i < i1; i++) {
+        const uint64_t b = d.x_bits[i];
+        const bool set = isint ? b != cur
+                               : !(fabs(__longlong_as_double((long long)b) - __longlong_as_double((long long)cur)) <= 1e-15);
+        cur = set ? b : cur;
+    }
+    if (cur != start) *p = cur;
+    d.x_old[g] = start;
+    d.x_new[g] = cur;
+}
+
+// The next "standalone" dirty Set group of slot e at or after g: a queued Set of a property that
+// no program writes, whose value changed over the frame (x_old != x_new).  Returns n_x when none.
+__device__ __forceinline__ int next_standalone(const Dev& d, int g, int e) {
+    for (; g < d.n_x && d.x_slot[g] == (uint32_t)e; g++)
+        if (d.tab->w_slot[d.x_pid[g]] == kNoU && d.x_old[g] != d.x_new[g]) return g;
+    return d.n_x;
+}
+// recipients of a property event (GetBroadCastObject, AOI:531-593) of slot e's class
+struct EvFan {
+    uint32_t n;    // messages
+    bool pub;      // to the scene group's players but self (else to self)
+};
+__device__ __forceinline__ EvFan ev_fan(const Dev& d, uint64_t desc, uint32_t pid) {
+    const uint8_t fl = d.tab->pflags[desc >> 60][pid];
+    return EvFan{event_msgs(desc, fl), (fl & NFK_PUBLIC) != 0};
 }
 
 // op: 1 = RemoveSchedule(self, name) queued (owns the remove-list key), 2 = RemoveSchedule(self)
@@ -123,17 +168,18 @@ struct Ent {
     }
     __device__ __forceinline__ int64_t geti(uint32_t p) { return (int64_t)getb(p); }
     __device__ __forceinline__ double getf(uint32_t p) { return __longlong_as_double((long long)getb(p)); }
-    // NFCProperty::SetInt (PR:254): stored (and an event fired) only when the value changes
-    __device__ __forceinline__ void seti(uint32_t p, int64_t v) {
-        const int64_t c = geti(p);
-        if (v == c) return;
-        tput(p, (uint64_t)c, (uint64_t)v);
-    }
-    // NFCProperty::SetFloat (PR:295): IsZeroDouble(v - cur), eps 1e-15 (NFPlatform.h:362)
-    __device__ __forceinline__ void setf(uint32_t p, double v) {
-        const double c = getf(p);
-        if (fabs(v - c) <= 1e-15) return;
-        tput(p, (uint64_t)__double_as_longlong(c), (uint64_t)__double_as_longlong(v));
+    // a program destination whose queued Set group (k_sets) already ran: frame-start value and
+    // the value the programs start from
+    __device__ __forceinline__ void tinit(uint32_t p, uint64_t oldv, uint64_t curv) {
+#pragma unroll
+        for (int j = 0; j < NFK_MAX_TOUCH; j++)
+            if (j == n) {
+                pid[j] = p;
+                cur[j] = curv;
+            }
+        if (n < NFK_MAX_TOUCH) old[n * kTPB] = oldv;
+        else ovf = true;
+        n++;
     }
 };
 
@@ -233,20 +279,6 @@ __device__ __forceinline__ void uput(uint64_t (&v)[kU], uint32_t j, uint64_t x) 
 #undef NFK_C
     }
 }
-// j per lane (queued SetProperty calls differ between entities): select over the writable slots
-template <int kU>
-__device__ __forceinline__ uint64_t uget_lane(const uint64_t (&v)[kU], uint32_t j) {
-    uint64_t r = 0;
-#pragma unroll
-    for (int i = 0; i < (kU < kMaxW ? kU : kMaxW); i++) r = (j == (uint32_t)i) ? v[i] : r;
-    return r;
-}
-template <int kU>
-__device__ __forceinline__ void uput_lane(uint64_t (&v)[kU], uint32_t j, uint64_t x) {
-#pragma unroll
-    for (int i = 0; i < (kU < kMaxW ? kU : kMaxW); i++) v[i] = (j == (uint32_t)i) ? x : v[i];
-}
-
 // The fired kinds' programs in schedule-name order on the register working set.  A Set that
 // fails the reference's change predicate leaves the value as it was; wm collects the slots a
 // Set changed at least once.
@@ -389,16 +421,17 @@ __device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& by
     return fired;
 }
 
-// One thread per slot, one workgroup per 256-slot tile.  Outputs of tile t are written densely
-// at [t * tile_cap, t * tile_cap + count); k_scan_tiles turns the counts into global ranks.
-// k_tick: one thread per slot, one workgroup per 256-slot tile, on the frame working set
-// (Dev::u_*).  Every value the entity's frame touches is loaded in ONE batch of independent loads
-// into registers; the queued SetProperty calls and the fired kinds' programs run on those
-// registers with wave-uniform slot numbers; the slots a Set changed are diffed against their
-// frame-start values (kept in LDS).  Outputs of tile t are written densely at
-// [t * tile_cap, t * tile_cap + count); k_scan_tiles turns the counts into global ranks.
-// kWPE: waves per SIMD the register allocation aims at (5 fits without spilling).  The LDS image
-// of the frame-start values is dynamic: n_w writable slots x kTPB.
+// k_tick: one thread per slot, one workgroup per 256-slot tile, on the programs' working set
+// (Dev::u_*, fixed at commit).  Every value the entity's frame touches is loaded in ONE batch of
+// independent loads into registers; the fired kinds' programs run on those registers with
+// wave-uniform slot numbers; the slots a program or a queued Set changed are diffed against their
+// frame-start values (kept in LDS).  Queued SetProperty calls were applied by k_sets: a Set of a
+// program destination joins that slot's diff (frame-start value = the group's x_old), a Set of any
+// other property is a "standalone" event (x_old -> x_new) merged into the entity's events in
+// property-id order.  Outputs of tile t are written densely at [t * tile_cap, t * tile_cap + count);
+// k_scan_tiles turns the counts into global ranks.
+// kWPE: waves per SIMD the register allocation aims at.  The LDS image of the frame-start values
+// is dynamic: n_w writable slots x kTPB.
 template <int kWPE, int kU>
 __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8))) void k_tick(Dev d) {
     constexpr int kW = kU < kMaxW ? kU : kMaxW;  // writable register slots
@@ -432,15 +465,20 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         bytes = e < d.N ? bytes + 8 : 0u;
     }
     const bool live = !desc_dead(desc);
+    // queued Set groups of this slot (k_sets ran them): program destinations among them
+    uint32_t xset = 0;
+    if (live && d.n_x) {
+        xh = d.ext_head[e];
+        bytes += 4;
+        if (xh)
+            for (int g = (int)xh - 1; g < d.n_x && d.x_slot[g] == (uint32_t)e; g++) {
+                const uint32_t j = d.tab->w_slot[d.x_pid[g]];
+                xset |= j != kNoU ? 1u << j : 0u;
+                bytes += 8;
+            }
+    }
     if (live) {
-        uint32_t need = 0;
-        if (d.n_x) {
-            xh = d.ext_head[e];
-            bytes += 4;
-            if (xh)
-                for (int i = (int)xh - 1; i < d.n_x && d.x_slot[i] == (uint32_t)e; i++)
-                    need |= 1u << d.u_slot[d.x_pid[i]];
-        }
+        uint32_t need = xset;
         if (!(d.ablate & kAblPrograms))
             for (int k = 0; k < d.n_kind; k++)
                 if ((fired >> k) & 1) {
@@ -457,23 +495,14 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
 #pragma unroll
         for (int j = 0; j < kW; j++)
             if (j < d.n_w && ((need >> j) & 1)) s_o[j * kTPB + threadIdx.x] = v[j];
-        // SetProperty* calls queued before this frame, in call order (PR:254 / PR:295 predicates)
-        if (xh) {
-            for (int i = (int)xh - 1; i < d.n_x && d.x_slot[i] == (uint32_t)e; i++) {
-                const uint32_t pid = d.x_pid[i];
-                const uint64_t b = d.x_bits[i];
-                bytes += 16;
-                const uint32_t j = d.u_slot[pid];
-                const uint64_t cur = uget_lane(v, j);
-                const bool set = (int)pid < d.n_int
-                                     ? (int64_t)b != (int64_t)cur
-                                     : !(fabs(__longlong_as_double((long long)b) -
-                                              __longlong_as_double((long long)cur)) <= 1e-15);
-                if (set) {
-                    uput_lane(v, j, b);
-                    wm |= 1u << j;
-                }
+        // a Set program destination: its frame-start value is the value before the Set group
+        if (xset) {
+            for (int g = (int)xh - 1; g < d.n_x && d.x_slot[g] == (uint32_t)e; g++) {
+                const uint32_t j = d.tab->w_slot[d.x_pid[g]];
+                if (j != kNoU) s_o[j * kTPB + threadIdx.x] = d.x_old[g];
+                bytes += j != kNoU ? 8 : 0;
             }
+            wm = xset;
         }
         // the fired heartbeats' effect programs, in schedule-name order
         if (!(d.ablate & (kAblPrograms | kAblNoRun)) && fired) run_programs_u(v, wm, d.tab, fired, d.n_kind, d.n_w);
@@ -497,9 +526,47 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     const uint32_t pubm = cm & 0xFFFFu, privm = cm >> 16;
     const uint32_t r1 = (uint32_t)((desc >> 46) & 0x3FFF);
     const uint32_t npub = (uint32_t)((desc >> 32) & 0x3FFF) - (r1 ? 1u : 0u);
-    const unsigned nmsg = npub * __builtin_popcount(dm & pubm) + __builtin_popcount(dm & privm);
+    unsigned nmsg = npub * __builtin_popcount(dm & pubm) + __builtin_popcount(dm & privm);
     unsigned nmax = (dm & pubm) ? npub : ((dm & privm) ? 1u : 0u);
-    const unsigned nd = __builtin_popcount(dm);
+    unsigned nd = __builtin_popcount(dm);
+    // standalone Set events (properties no program writes): counted here, merged in property-id
+    // order with the slots' events below
+    unsigned nsd = 0;
+    if (xh) {
+        for (int g = next_standalone(d, (int)xh - 1, e); g < d.n_x; g = next_standalone(d, g + 1, e)) {
+            const EvFan f = ev_fan(d, desc, d.x_pid[g]);
+            nsd++;
+            nmsg += f.n;
+            nmax = max(nmax, f.n);
+            bytes += 8;
+        }
+        nd += nsd;
+    }
+    // the entity's events in property-id order: dirty slots (u_order) merged with the standalone
+    // groups; emit(rank, message offset, pid, slot or -1, group, recipients) per event
+    auto walk = [&](auto&& emit) {
+        int g = next_standalone(d, (int)xh - 1, e);
+        unsigned at = 0, m = 0;
+#pragma unroll 1
+        for (int i = 0; i <= d.n_w; i++) {
+            const int j = i < d.n_w ? d.u_order[i] : -1;
+            const uint32_t pj = j >= 0 ? (uint32_t)d.u_pid[j] : 0xFFFFFFFFu;
+            while (g < d.n_x && d.x_pid[g] < pj) {
+                const EvFan f = ev_fan(d, desc, d.x_pid[g]);
+                emit(at, m, d.x_pid[g], -1, g, f);
+                at++;
+                m += f.n;
+                g = next_standalone(d, g + 1, e);
+            }
+            if (j >= 0 && ((dm >> j) & 1)) {
+                const bool pub = (pubm >> j) & 1;
+                const EvFan f{pub ? npub : ((privm >> j) & 1u), pub};
+                emit(at, m, pj, j, 0, f);
+                at++;
+                m += f.n;
+            }
+        }
+    };
     const unsigned nf = __builtin_popcount(fired);
     const uint32_t dm_ = dm;
     if (fuse) {  // the pl_slot run of the groups whose members have messages (they are contiguous)
@@ -532,28 +599,66 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     if (live) {
         // write back the changed values; their events in property-id order (rank among the
         // entity's dirty slots by Dev::u_lower)
-        if (dm && !(d.ablate & kAblNoEmit)) {
+        if (nd && !(d.ablate & kAblNoEmit)) {
             uint32_t* const t_evs = d.ev_slot + ev0;
             uint32_t* const t_evp = d.ev_pid + ev0;
             uint64_t* const t_evo = d.ev_old + ev0;
             uint64_t* const t_evn = d.ev_new + ev0;
+            if (!nsd) {
 #pragma unroll
-            for (int j = 0; j < kW; j++) {
-                if (j >= d.n_w || !((dm >> j) & 1)) continue;
-                const uint32_t below = dm & d.u_lower[j];
-                const uint32_t at = pev0 + __builtin_popcount(below);
-                const uint64_t nv = v[j];
-                if (!(d.ablate & kAblNoWriteBack)) d.u_col[j][(size_t)e * d.u_str[j]] = nv;
-                st_off(t_evs, at, (uint32_t)e);
-                st_off(t_evp, at, (uint32_t)d.u_pid[j]);
-                st_off(t_evo, at, s_o[j * kTPB + threadIdx.x]);
-                st_off(t_evn, at, nv);
-                if (!fuse)  // tile-local; k_fanout adds the tile's message base
-                    st_off(t_evm, at, pmsg0 + npub * __builtin_popcount(below & pubm) +
-                                          __builtin_popcount(below & privm));
-                bytes += 8 + 24;
+                for (int j = 0; j < kW; j++) {
+                    if (j >= d.n_w || !((dm >> j) & 1)) continue;
+                    const uint32_t below = dm & d.u_lower[j];
+                    const uint32_t at = pev0 + __builtin_popcount(below);
+                    const uint64_t nv = v[j];
+                    if (!(d.ablate & kAblNoWriteBack)) d.u_col[j][(size_t)e * d.u_str[j]] = nv;
+                    st_off(t_evs, at, (uint32_t)e);
+                    st_off(t_evp, at, (uint32_t)d.u_pid[j]);
+                    st_off(t_evo, at, s_o[j * kTPB + threadIdx.x]);
+                    st_off(t_evn, at, nv);
+                    if (!fuse)  // tile-local; k_fanout adds the tile's message base
+                        st_off(t_evm, at, pmsg0 + npub * __builtin_popcount(below & pubm) +
+                                              __builtin_popcount(below & privm));
+                    bytes += 8 + 24;
+                }
+            } else {
+                // (rare: an entity with standalone Set events) write back the slots, then every
+                // event by the merged walk, which reads the slots' new values back from their
+                // columns so that no register of the working set stays live in it
+#pragma unroll
+                for (int j = 0; j < kW; j++)
+                    if (j < d.n_w && ((dm >> j) & 1)) {
+                        d.u_col[j][(size_t)e * d.u_str[j]] = v[j];
+                        bytes += 8;
+                    }
+                walk([&](unsigned at, unsigned m, uint32_t pid, int j, int g, EvFan) {
+                    uint64_t ov, nv;
+                    if (j >= 0) {
+                        ov = s_o[j * kTPB + threadIdx.x];
+                        nv = __hip_atomic_load(d.u_col[j] + (size_t)e * d.u_str[j], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    } else {  // (k_sets wrote the column)
+                        ov = d.x_old[g];
+                        nv = d.x_new[g];
+                    }
+                    st_off(t_evs, pev0 + at, (uint32_t)e);
+                    st_off(t_evp, pev0 + at, pid);
+                    st_off(t_evo, pev0 + at, ov);
+                    st_off(t_evn, pev0 + at, nv);
+                    if (!fuse) st_off(t_evm, pev0 + at, pmsg0 + m);
+                    bytes += 24;
+                });
             }
         }
+        // a Set program destination that a program moved back to its frame-start value has no
+        // event, but k_sets changed its column: write it back
+        if (xset & ~dm)
+#pragma unroll
+            for (int j = 0; j < kW; j++)
+                if (j < d.n_w && ((xset & ~dm) >> j) & 1) {
+                    d.u_col[j][(size_t)e * d.u_str[j]] = v[j];
+                    bytes += 8;
+                }
         uint32_t* const t_fis = d.fi_slot + fi0;
         uint32_t* const t_fik = d.fi_kind + fi0;
         int32_t* const t_fir = d.fi_remain + fi0;
@@ -591,7 +696,10 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         const bool fan = tmsg && tmsg <= d.msg_tcap;
         if (tmsg > d.msg_tcap && threadIdx.x == 0) atomicOr(&d.ctrl->err, kErrFanBound);  // (host bound)
         if (!fan) {  // ev_moff only
-            if (dm)
+            if (nsd) {
+                walk([&](unsigned at, unsigned m, uint32_t, int, int, EvFan) { st_off(t_evm, pev0 + at, mb + pmsg0 + m); });
+                bytes += 4 * nd;
+            } else if (dm) {
 #pragma unroll
                 for (int j = 0; j < kW; j++) {
                     if (j >= d.n_w || !((dm >> j) & 1)) continue;
@@ -600,6 +708,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                            mb + pmsg0 + npub * __builtin_popcount(below & pubm) + __builtin_popcount(below & privm));
                     bytes += 4;
                 }
+            }
         } else {
             const unsigned R = (unsigned)d.lds_words;
             const uint32_t pb_lo = s_pb[0], npl = s_pb[1] > s_pb[0] ? s_pb[1] - s_pb[0] : 0u;
@@ -625,23 +734,36 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                 const unsigned c1 = min(tev, c0 + ecap);
                 // a runtime loop over the slots (an unrolled one gets hoisted out of the chunk loop
                 // and spills: 12 slots x 4 values)
-                if (dm && pev0 < c1 && pev0 + nd > c0) {
+                if (nd && pev0 < c1 && pev0 + nd > c0) {
+                    if (nsd) {
+                        walk([&](unsigned at, unsigned m, uint32_t, int, int, EvFan f) {
+                            const unsigned a = pev0 + at;
+                            if (a < c0 || a >= c1) return;
+                            uint32_t* x = s_ev + 3u * (a - c0);
+                            x[0] = pmsg0 + m;
+                            x[1] = f.pub ? (uint32_t)desc : (uint32_t)e;
+                            x[2] = f.n | (r1 << 14) | (f.pub ? 0x80000000u : 0u);
+                            st_off(t_evm, a, mb + pmsg0 + m);
+                            bytes += 4;
+                        });
+                    } else {
 #pragma unroll 1
-                    for (int j = 0; j < d.n_w; j++) {
-                        if (!((dm >> j) & 1)) continue;
-                        const uint32_t below = dm & d.u_lower[j];
-                        const uint32_t at = pev0 + __builtin_popcount(below);
-                        if (at < c0 || at >= c1) continue;
-                        const bool pub = (pubm >> j) & 1;
-                        const uint32_t m = pmsg0 + npub * __builtin_popcount(below & pubm) +
-                                           __builtin_popcount(below & privm);
-                        const uint32_t n = pub ? npub : ((privm >> j) & 1u);
-                        uint32_t* x = s_ev + 3u * (at - c0);
-                        x[0] = m;
-                        x[1] = pub ? (uint32_t)desc : (uint32_t)e;
-                        x[2] = n | (r1 << 14) | (pub ? 0x80000000u : 0u);
-                        st_off(t_evm, at, mb + m);
-                        bytes += 4;
+                        for (int j = 0; j < d.n_w; j++) {
+                            if (!((dm >> j) & 1)) continue;
+                            const uint32_t below = dm & d.u_lower[j];
+                            const uint32_t at = pev0 + __builtin_popcount(below);
+                            if (at < c0 || at >= c1) continue;
+                            const bool pub = (pubm >> j) & 1;
+                            const uint32_t m = pmsg0 + npub * __builtin_popcount(below & pubm) +
+                                               __builtin_popcount(below & privm);
+                            const uint32_t n = pub ? npub : ((privm >> j) & 1u);
+                            uint32_t* x = s_ev + 3u * (at - c0);
+                            x[0] = m;
+                            x[1] = pub ? (uint32_t)desc : (uint32_t)e;
+                            x[2] = n | (r1 << 14) | (pub ? 0x80000000u : 0u);
+                            st_off(t_evm, at, mb + m);
+                            bytes += 4;
+                        }
                     }
                 }
                 __syncthreads();
@@ -711,8 +833,10 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     }
 }
 
-// k_tick_touch: the general path, used when a frame's property working set does not fit the U
-// slots (see k_tick): a per-entity written-property list, one operand round trip per fired kind.
+// k_tick_touch: the general path, used when the programs' working set does not fit the U slots
+// (see k_tick): a per-entity written-property list, one operand round trip per fired kind.  The
+// list holds program destinations only (at most NFK_MAX_TOUCH, checked at commit); queued Sets
+// of other properties are standalone events merged at emission.
 __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
@@ -745,20 +869,21 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
     en.bytes = dbytes;
     uint32_t fired = 0;
     uint32_t xh = 0;
+    int n_set = 0;
     if (live) {
-        // 1. SetProperty* calls queued before this frame, in call order
+        // 1. SetProperty* calls queued before this frame: k_sets applied them; a program
+        //    destination enters the written-property list with its frame-start value
         if (d.n_x) {
             xh = d.ext_head[e];
             en.bytes += 4;
-            if (xh) {
-                for (int i = (int)xh - 1; i < d.n_x && d.x_slot[i] == (uint32_t)e; i++) {
-                    const uint32_t pid = d.x_pid[i];
-                    const uint64_t b = d.x_bits[i];
+            if (xh)
+                for (int g = (int)xh - 1; g < d.n_x && d.x_slot[g] == (uint32_t)e; g++) {
+                    en.bytes += 8;
+                    if (d.tab->w_slot[d.x_pid[g]] == kNoU) continue;  // standalone: merged at emission
+                    en.tinit(d.x_pid[g], d.x_old[g], d.x_new[g]);
                     en.bytes += 16;
-                    if ((int)pid < d.n_int) en.seti(pid, (int64_t)b);
-                    else en.setf(pid, __longlong_as_double((long long)b));
                 }
-            }
+            n_set = en.n;
         }
         // 2. NFCScheduleModule::Execute (SM:51-81)
         fired = sched_scan(d, e, en.bytes, desc);
@@ -780,7 +905,14 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
             dmask |= 1u << j;
             nmsg += event_msgs(desc, s_pflags[cls][en.pid[j]]);
         }
-    const unsigned nd = __builtin_popcount(dmask);
+    // standalone Set events (properties no program writes)
+    unsigned nd = __builtin_popcount(dmask);
+    if (xh)
+        for (int g = next_standalone(d, (int)xh - 1, e); g < d.n_x; g = next_standalone(d, g + 1, e)) {
+            nd++;
+            nmsg += event_msgs(desc, s_pflags[cls][d.x_pid[g]]);
+            en.bytes += 8;
+        }
     const unsigned nf = __builtin_popcount(fired);
     if (en.ovf) atomicOr(&d.ctrl->err, kErrTouch);
 
@@ -794,16 +926,18 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
     const size_t ev0 = (size_t)tile * d.ev_tcap, fi0 = (size_t)tile * d.fi_tcap;
 
     if (live) {
-        // write back changed columns
+        // write back changed columns, and every Set program destination (k_sets changed its
+        // column; the list's first n_set entries)
 #pragma unroll
         for (int j = 0; j < NFK_MAX_TOUCH; j++) {
-            if (!((dmask >> j) & 1)) continue;
+            if (!((dmask >> j) & 1) && j >= n_set) continue;
             const uint32_t pid = en.pid[j];
             *prop_ptr(d, pid, e) = en.cur[j];
             en.bytes += 8;
         }
-        // events in property-id order
+        // events in property-id order: the written-property list merged with the standalone groups
         uint32_t left = dmask;
+        int g = xh ? next_standalone(d, (int)xh - 1, e) : d.n_x;
         for (unsigned q = 0; q < nd; q++) {
             uint32_t best = 0xFFFFFFFFu;
             int bj = 0;
@@ -813,12 +947,19 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
                     best = en.pid[j];
                     bj = j;
                 }
-            uint64_t nv = 0;
+            uint64_t nv = 0, ov;
+            if (g < d.n_x && d.x_pid[g] < best) {
+                best = d.x_pid[g];
+                ov = d.x_old[g];
+                nv = d.x_new[g];
+                g = next_standalone(d, g + 1, e);
+            } else {
 #pragma unroll
-            for (int j = 0; j < NFK_MAX_TOUCH; j++)
-                if (j == bj) nv = en.cur[j];
-            const uint64_t ov = en.old[bj * kTPB];
-            left &= ~(1u << bj);
+                for (int j = 0; j < NFK_MAX_TOUCH; j++)
+                    if (j == bj) nv = en.cur[j];
+                ov = en.old[bj * kTPB];
+                left &= ~(1u << bj);
+            }
             const size_t at = ev0 + pev;
             d.ev_slot[at] = (uint32_t)e;
             d.ev_pid[at] = best;

@@ -154,8 +154,14 @@ class SceneShard:
         rbuf = torch.empty((len(recv), rw), dtype=torch.int64, device=self.device)
         self._all_to_all(rbuf, sbuf, [int(c) * rw for c in rcount], [int(c) * rw for c in scount])
         if len(recv):
+            other_stream = (self.device.type == "cuda" and
+                            self.m.stream != torch.cuda.current_stream(self.device).cuda_stream)
+            if other_stream:   # the rows arrived on torch's stream; the import copies on the world's
+                torch.cuda.current_stream(self.device).synchronize()
             self.m.import_objects(recv[:, T_GH], recv[:, T_GD], recv[:, T_SCENE], recv[:, T_GROUP], recv[:, T_CLS],
                                   recv[:, T_PL], rbuf.data_ptr())
+            if other_stream:   # rbuf returns to torch's allocator: the world's copy out of it is done
+                self.m.synchronize()
             # the SwitchScene property writes (KM:930-942), per entity in this order; the scene
             # always changes here
             cols = [(self.pid_group, np.zeros(len(recv), np.int64)), (self.pid_scene, recv[:, T_SCENE]),

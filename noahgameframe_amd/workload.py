@@ -105,7 +105,8 @@ def _names(lst):
 def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4, n_ticks=8,
                tick_ms=100, seed=1, ext_frac=0.05, host_ops=True, records=False, rec_rows=64,
                t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, rec_skill_op=False, sched_edges=False,
-               switch_frac=0.0, switch_new_groups=False, rec_steady=False):
+               switch_frac=0.0, switch_new_groups=False, rec_steady=False, ext_props=None, burst_frac=0.0,
+               burst_props=20):
     rng = np.random.default_rng(seed)
     n_groups = n_scenes * groups_per_scene
     # ---- objects ----
@@ -212,34 +213,62 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
 
     # ---- SetProperty calls between frames (call order matters) ----
     xt, xo, xp, xb = [], [], [], []
-    ext_props = [PID["HP"], PID["Gold"], PID["EXP"], PID["TargetX"]]
+    # ext_props: the properties game logic sets ("all": every property but SceneID / GroupID, which
+    # only SwitchScene writes, so program operands such as MAXHP / HPREGEN too)
+    if ext_props is None:
+        ext_props = [PID["HP"], PID["Gold"], PID["EXP"], PID["TargetX"]]
+    elif ext_props == "all":
+        ext_props = [i for i, n in enumerate(PROPS) if n not in ("SceneID", "GroupID")]
+    settable = [i for i, n in enumerate(PROPS) if n not in ("SceneID", "GroupID")]
+
+    def set_value(o, p):
+        if p == PID["HP"]:
+            v = int(rng.integers(1, maxhp[o] + 1))
+            if rng.random() < 0.1:
+                v = int(init_i[PID["HP"], o])  # often unchanged -> no event
+            return np.uint64(v & (2 ** 64 - 1))
+        if p in (PID["Gold"], PID["EXP"]):
+            return np.uint64(int(rng.integers(0, 10 ** 6)))
+        if p < N_INT:
+            v = int(rng.integers(0, 5000))
+            if rng.random() < 0.1:
+                v = int(init_i[p, o])
+            return np.uint64(v & (2 ** 64 - 1))
+        return np.uint64(f64bits(coord(1)[0]) & (2 ** 64 - 1))
+
     for t in range(n_ticks):
         k = int(ext_frac * n_obj)
-        if k == 0:
-            continue
-        objs = rng.integers(0, n_obj, k)
-        props = rng.choice(ext_props, k)
-        vals = np.zeros(k, np.uint64)
-        for j, p in enumerate(props):
-            o = objs[j]
-            if p == PID["HP"]:
-                v = int(rng.integers(1, maxhp[o] + 1))
-                if rng.random() < 0.1:
-                    v = int(init_i[PID["HP"], o])  # often unchanged -> no event
-                vals[j] = np.uint64(v & (2 ** 64 - 1))
-            elif p in (PID["Gold"], PID["EXP"]):
-                vals[j] = np.uint64(int(rng.integers(0, 10 ** 6)))
-            else:
-                vals[j] = np.uint64(f64bits(coord(1)[0]) & (2 ** 64 - 1))
-        # duplicates: same (object, property) set twice in one frame (coalesced)
-        dup = rng.random(k) < 0.05
-        objs = np.concatenate([objs, objs[dup]])
-        props = np.concatenate([props, props[dup]])
-        vals = np.concatenate([vals, vals[dup][::-1]])
-        xt.append(np.full(len(objs), t))
-        xo.append(objs)
-        xp.append(props)
-        xb.append(vals)
+        if k > 0:
+            objs = rng.integers(0, n_obj, k)
+            props = rng.choice(ext_props, k)
+            vals = np.zeros(k, np.uint64)
+            for j, p in enumerate(props):
+                vals[j] = set_value(objs[j], p)
+            # duplicates: same (object, property) set twice in one frame (coalesced)
+            dup = rng.random(k) < 0.05
+            objs = np.concatenate([objs, objs[dup]])
+            props = np.concatenate([props, props[dup]])
+            vals = np.concatenate([vals, vals[dup][::-1]])
+            xt.append(np.full(len(objs), t))
+            xo.append(objs)
+            xp.append(props)
+            xb.append(vals)
+        kb = int(burst_frac * n_obj)
+        if kb > 0:
+            # bursts: an entity gets `burst_props` distinct properties set in one frame (more than
+            # the programs' working set), some of them twice
+            bo, bp, bv = [], [], []
+            for o in rng.choice(n_obj, size=min(kb, n_obj), replace=False):
+                ps = rng.choice(settable, size=min(burst_props, len(settable)), replace=False)
+                ps = np.concatenate([ps, ps[rng.random(len(ps)) < 0.2]])
+                for p in ps:
+                    bo.append(o)
+                    bp.append(p)
+                    bv.append(set_value(o, p))
+            xt.append(np.full(len(bo), t))
+            xo.append(np.array(bo))
+            xp.append(np.array(bp))
+            xb.append(np.array(bv, np.uint64))
     cat = lambda lst, dt: np.concatenate(lst).astype(dt) if lst else np.zeros(0, dt)
     x_tick, x_obj, x_pid, x_bits = cat(xt, np.int32), cat(xo, np.int32), cat(xp, np.int32), cat(xb, np.uint64)
 

@@ -26,6 +26,10 @@ FIXTURES = {
     # SwitchScene between frames (KM:901-951): group/scene changes, own-cell switches, new groups
     "switch": dict(n_obj=400, n_scenes=3, groups_per_scene=4, players_per_group=3, n_ticks=8, seed=404,
                    ext_frac=0.05, switch_frac=0.05, switch_new_groups=True),
+    # SetProperty on every property (program operands MAXHP / HPREGEN / TargetX included) and
+    # bursts of 20 distinct properties on one entity in one frame (beyond the programs' working set)
+    "wide_sets": dict(n_obj=500, n_scenes=2, groups_per_scene=5, players_per_group=4, n_ticks=8, seed=505,
+                      ext_frac=0.1, ext_props="all", burst_frac=0.03, burst_props=20, host_ops=True),
 }
 
 

@@ -48,6 +48,9 @@ def test_golden_fixtures_are_nontrivial():
     # two int column ops in one program, the second on a lower column (event order is (row, col))
     (7, dict(n_obj=400, n_scenes=2, groups_per_scene=3, players_per_group=4, records=True, rec_rows=24,
              rec_float_op=False, rec_skill_op=True)),
+    # SetProperty on any property (program operands too) and 24-property bursts per entity
+    (8, dict(n_obj=600, n_scenes=2, groups_per_scene=4, players_per_group=3, ext_frac=0.15, ext_props="all",
+             burst_frac=0.04, burst_props=24, host_ops=True, switch_frac=0.02)),
 ])
 def test_oracle_matches_reference(seed, kw):
     w = workload.make_world(n_ticks=9, seed=seed, **kw)
