@@ -2,7 +2,13 @@
 
 One "step" = one server frame over this GPU's 1M-entity scene shard: heartbeat scan +
 effect programs (property mutation) + dirty diff + scene-group fan-out
-(NFCScheduleModule::Execute + NFCKernelModule::Execute + NFCSceneAOIModule fan-out).
+(NFCScheduleModule::Execute + NFCKernelModule::Execute + NFCSceneAOIModule fan-out), and the
+consumer's nfk_outputs_get (the frame's dense event / message ranks) every frame.
+
+The default line (config[1]) also carries "host_calls": the same world with game logic between
+frames (5 % of the entities get a SetProperty, 1/64 an AddSchedule / RemoveSchedule call, every
+frame), timed the same way, with the host milliseconds per frame of queueing the calls and of
+nfk_execute's host preparation.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
@@ -28,6 +34,9 @@ METRIC = "entity-ticks/sec (update+dirty-diff+fanout) at 1M entities/GPU, 1/2/4/
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 KNAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles"]
 CONFIG_NAMES = {
+    0: "BASELINE config[0]: Tutorial3 (HelloWorld3Module.cpp) scaled to 10k NPC objects in scene 1 group 0: "
+       "AddSchedule(self, \"OnHeartBeat\", 5.0, 10) per object (effect: World += 1, so its property callback "
+       "fires), OnEvent SetPropertyInt(World) on 1 % of the objects per frame, 100 ms frames",
     3: "BASELINE config[3]: 256 scenes x 64 groups, 2M entities per GPU, 32 players per group "
        "(scene-group sync-list fan-out dominated), heartbeats as config[1], 100 ms frames",
     4: "BASELINE config[4]: 500k players per GPU, 64-row skill record each (int cooldown + f64 charge "
@@ -55,8 +64,11 @@ def parse():
     p.add_argument("--migrate-every", type=int, default=8,
                    help="frames between migration batches (8 = 256 entities per GPU every 0.8 s)")
     p.add_argument("--slack", type=int, default=None, help="free slots per 256 scene-group members")
-    p.add_argument("--config", type=int, default=1, choices=[1, 3, 4],
-                   help="BASELINE config: 1 = 1M entities/GPU (the metric's configuration; with --gpus > 1 "
+    p.add_argument("--host-calls", choices=["auto", "off"], default="auto",
+                   help="config[1], 1 GPU: also time frames with game-logic SetProperty / schedule calls")
+    p.add_argument("--config", type=int, default=1, choices=[0, 1, 3, 4],
+                   help="BASELINE config: 0 = Tutorial3 at 10k NPCs (the reference's CPU case), "
+                        "1 = 1M entities/GPU (the metric's configuration; with --gpus > 1 "
                         "it becomes config[2]: scene shards + migration), 3 = 256 scenes x 64 groups, 2M "
                         "entities, 32 players/group (fan-out dominated), 4 = 500k players x 64-row records")
     p.add_argument("--backend", default="nccl", help="process group backend (nccl = RCCL; gloo only to rehearse "
@@ -64,17 +76,35 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(args, w_full):
-    """The reference's own classes (oracle/_ref) on a bounded slice of the same workload."""
+def cpu_baseline(args):
+    """The reference's own classes (oracle/_ref/nf_ref_harness: NFCProperty / NFCRecord /
+    NFCScheduleModule compiled from the reference sources, per-Set GetBroadCastObject lists) on a
+    bounded sample of the same workload, one host core."""
     from noahgameframe_amd import nfio, workload
     exe = os.path.join(ROOT, "oracle", "_ref", "nf_ref_harness")
     if not os.path.exists(exe):
         return None
-    n = min(args.cpu_sample, args.entities)
-    groups = max(1, n * args.groups // args.entities)
     ticks = 400
-    w = workload.bench_world(n_obj=n, groups=groups, players_per_group=args.players_per_group, n_ticks=ticks,
-                             tick_ms=args.tick_ms, seed=2026)
+    if args.config == 0:
+        n = 10_000
+        w = workload.tutorial3_world(n_obj=n, n_ticks=ticks * 2, tick_ms=args.tick_ms)
+        what = f"the full config[0] workload ({n} NPC objects)"
+    elif args.config == 3:
+        n = 32768  # 4 scenes x 64 groups of 128, 32 players per group
+        w = workload.fanout_world(n_ticks=ticks, n_obj=n, scenes=4, groups=64, players_per_group=32)
+        what = f"{n} entities (4 scenes x 64 groups x 128, 32 players/group)"
+    elif args.config == 4:
+        n = 4096  # 64-row skill records; the int cooldown column only (see below)
+        w = workload.record_world(n_ticks=ticks, n_obj=n, groups=256, steady=True, rec_float_op=False)
+        what = (f"{n} players (groups of 16) x 64-row records, the int cooldown column op only: the reference's "
+                "NFCRecord::SetFloat stores an int64 variant and cannot run the f64 charge op "
+                "(tests/test_oracle.py::test_reference_record_setfloat_bug)")
+    else:
+        n = min(args.cpu_sample, args.entities)
+        groups = max(1, n * args.groups // args.entities)
+        w = workload.bench_world(n_obj=n, groups=groups, players_per_group=args.players_per_group, n_ticks=ticks,
+                                 tick_ms=args.tick_ms, seed=2026)
+        what = f"{n} entities ({groups} groups x {n // groups}, {args.players_per_group} players/group)"
     with tempfile.TemporaryDirectory() as d:
         wp = os.path.join(d, "w.nfio")
         nfio.write(wp, w)
@@ -82,13 +112,12 @@ def cpu_baseline(args, w_full):
         r = json.loads(subprocess.run([exe, "--bench", wp, "4"], check=True, capture_output=True,
                                       text=True).stdout)
         per_tick = r["seconds"] / max(r["ticks"], 1)
-        t = int(min(ticks, max(4, args.cpu_seconds / max(per_tick, 1e-6))))
+        t = int(min(int(w["cfg"][7]), max(4, args.cpu_seconds / max(per_tick, 1e-6))))
         r = json.loads(subprocess.run([exe, "--bench", wp, str(t)], check=True, capture_output=True,
                                       text=True).stdout)
     return {"value": r["entity_ticks_per_s"], "unit": "entity-ticks/s", "cores": 1, "kind": "reference",
-            "sample": f"{n} entities ({groups} groups x {n // groups}, {args.players_per_group} players/group), "
-                      f"{r['ticks']} frames of the same heartbeat workload through the reference's "
-                      f"NFCPropertyManager/NFCProperty + NFCScheduleModule + per-Set GetBroadCastObject "
+            "sample": f"{what}, {r['ticks']} frames of the same workload through the reference's "
+                      f"NFCPropertyManager/NFCProperty/NFCRecord + NFCScheduleModule + per-Set GetBroadCastObject "
                       f"lists (GetGroupObjectList over the group's player and other maps, KM:1270), "
                       f"single thread, {r['seconds']:.1f} s"}
 
@@ -174,7 +203,11 @@ def main():
     from noahgameframe_amd import kernel, workload
 
     # this rank's scene shard: 1M entities in scene rank+1 (GUID heads differ per rank)
-    if args.config == 3:
+    if args.config == 0:
+        w = workload.tutorial3_world(n_ticks=1, tick_ms=args.tick_ms, seed=3 + rank, guid_head=rank)
+        w["scene"][:] = rank + 1
+        w["init_i"][workload.T3_PID["SceneID"]] = w["scene"]
+    elif args.config == 3:
         w = workload.fanout_world(n_ticks=1, tick_ms=args.tick_ms, seed=2027 + rank,
                                   guid_heads=(7 + 16 * rank, 9 + 16 * rank))
         w["scene"] += 256 * rank
@@ -187,7 +220,8 @@ def main():
                                  n_ticks=1, tick_ms=args.tick_ms, seed=2026 + rank,
                                  guid_heads=(7 + 16 * rank, 9 + 16 * rank))
         w["scene"][:] = rank + 1
-    w["init_i"][workload.PID["SceneID"]] = w["scene"]
+    if args.config != 0:
+        w["init_i"][workload.PID["SceneID"]] = w["scene"]
     args.entities = len(w["guid_head"])
     cells = np.unique(w["scene"].astype(np.int64) * (1 << 32) + w["group"], return_counts=True)[1]
     args.groups = len(cells)
@@ -218,6 +252,7 @@ def main():
         if mig:
             timed("migrate", mig.before_frame)
         timed("execute", lambda: m.Execute(t0 + tick * args.tick_ms))
+        m.outputs_raw()   # the consumer's read of the frame's outputs (dense ranks: k_scan_tiles)
         if mig:
             timed("tickets", mig.after_frame)   # next frame's tickets, exchanged while this frame runs on the GPU
         tick += 1
@@ -252,6 +287,7 @@ def main():
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    m.close()
 
     # per-kernel averages over the timed region (HIP events on the world's stream)
     kern = {}
@@ -263,29 +299,33 @@ def main():
     d = kern[dom]
     achieved = d["alg_bytes_per_launch"] / (d["avg_us"] * 1e-6) / 1e9
     traffic, traffic_src = None, None
-    if os.path.exists(args.pmc_json) and args.config == 1 and not migrating:  # (measured on config[1])
+    if os.path.exists(args.pmc_json) and not migrating:
         try:
             pm = json.load(open(args.pmc_json))
-            traffic = pm.get(dom, {}).get("hbm_bytes_per_launch")
-            traffic_src = pm.get("source")
+            ent = pm.get(f"config{args.config}", {}).get(dom) or (pm.get(dom) if args.config == 1 else None)
+            traffic = (ent or {}).get("hbm_bytes_per_launch")
+            traffic_src = pm.get("source") if traffic else None
         except Exception:
             traffic = None
     total_alg = sum(v["alg_bytes_per_launch"] or 0 for v in kern.values())
     value = world * args.entities * args.steps / elapsed
 
+    if args.config == 1:
+        wl_name = ((f"BASELINE config[2]: {world} scene shards (scene r+1 on GPU r), "
+                    f"{args.migrate} SwitchScene migrations per rank every {args.migrate_every} "
+                    "frames into the next shard (state rows over RCCL all_to_all); per GPU: ")
+                   if migrating else "BASELINE config[1]: ") + (
+            "1M NPC/Player entities per GPU in one scene, "
+            f"{args.groups} groups x {args.entities // args.groups}, "
+            f"{args.players_per_group} players/group, heartbeats HPRegen 1s/MPRegen 2s/"
+            f"Move 0.1s/Patrol 3s/Poison 0.5s, {args.tick_ms} ms frames")
+    else:
+        wl_name = CONFIG_NAMES[args.config]
     out = {
         "metric": METRIC, "value": value, "unit": "entity-ticks/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int64/f64", "data": "synthetic",
-        "config": {"workload": CONFIG_NAMES[args.config] if args.config != 1 else (
-                               f"BASELINE config[2]: {world} scene shards (scene r+1 on GPU r), "
-                                f"{args.migrate} SwitchScene migrations per rank every {args.migrate_every} "
-                                "frames into the next shard (state rows over RCCL all_to_all); per GPU: "
-                                if migrating else
-                                "BASELINE config[1]: ") + "1M NPC/Player entities per GPU in one scene, "
-                               f"{args.groups} groups x {args.entities // args.groups}, "
-                               f"{args.players_per_group} players/group, heartbeats HPRegen 1s/MPRegen 2s/"
-                               f"Move 0.1s/Patrol 3s/Poison 0.5s, {args.tick_ms} ms frames",
+        "config": {"workload": wl_name,
                    "entities_per_gpu": args.entities, "groups": args.groups,
                    "players_per_group": args.players_per_group, "parallelism": f"scene-shard x{world}",
                    "migrations_per_rank_per_frame": args.migrate / args.migrate_every if migrating else 0},
@@ -298,13 +338,71 @@ def main():
                       "frame_GBps_alg": total_alg / (elapsed / args.steps) / 1e9},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and args.cpu_baseline == "auto" and args.config == 1:
-        out["cpu_baseline"] = cpu_baseline(args, w)
+    if rank == 0 and world == 1 and args.config == 1 and args.host_calls == "auto":
+        out["host_calls"] = host_calls_run(args, torch, kernel, workload)
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    m.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_calls_run(args, torch, kernel, workload):
+    """config[1] with game logic between frames: every frame 5 % of the entities get a SetProperty
+    (HP / Gold / EXP / TargetX, 5 % of them twice) and 1/64 of them an AddSchedule or
+    RemoveSchedule call (batched per frame, call order kept).  Timed like the headline (warmup,
+    then K frames between device syncs); host ms per frame of queueing the calls through the C-ABI
+    and of nfk_execute (GUID lookups, (slot, property) grouping, schedule-call folding, uploads,
+    launches), which overlap the previous frame on the GPU."""
+    frames = args.warmup + args.steps
+    w = workload.bench_world(n_obj=args.entities, groups=args.groups, players_per_group=args.players_per_group,
+                             n_ticks=frames, tick_ms=args.tick_ms, seed=2031, ext_frac=0.05, host_ops=True)
+    m = kernel.world_from_workload(w, stream=torch.cuda.current_stream().cuda_stream, slack_per_256=-1)
+    gh, gd = w["guid_head"], w["guid_data"]
+    xs = np.searchsorted(w["x_tick"], np.arange(frames + 1))
+    hs = np.searchsorted(w["h_tick"], np.arange(frames + 1))
+    t_calls = t_exec = 0.0
+
+    def frame(t):
+        nonlocal t_calls, t_exec
+        c0 = time.perf_counter()
+        a, b = hs[t], hs[t + 1]
+        if b > a:
+            ho = w["h_obj"][a:b]
+            m.schedule_calls(w["h_op"][a:b], gh[ho], gd[ho], w["h_kind"][a:b], w["h_interval"][a:b],
+                             w["h_count"][a:b], w["h_time"][a:b])
+        a, b = xs[t], xs[t + 1]
+        if b > a:
+            xo = w["x_obj"][a:b]
+            m.set_props(gh[xo], gd[xo], w["x_pid"][a:b], w["x_bits"][a:b])
+        c1 = time.perf_counter()
+        m.Execute(int(w["tick_time"][t]))
+        m.outputs_raw()
+        c2 = time.perf_counter()
+        t_calls += c1 - c0
+        t_exec += c2 - c1
+
+    for t in range(args.warmup):
+        frame(t)
+    m.summary()
+    torch.cuda.synchronize()
+    t_calls = t_exec = 0.0
+    ts = time.perf_counter()
+    for t in range(args.warmup, frames):
+        frame(t)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - ts
+    s = m.summary()
+    m.close()
+    n_set = int(np.sum((w["x_tick"] >= args.warmup))) / args.steps
+    n_sched = int(np.sum((w["h_tick"] >= args.warmup))) / args.steps
+    return {"value": args.entities * args.steps / elapsed, "unit": "entity-ticks/s",
+            "ms_per_step": 1000.0 * elapsed / args.steps,
+            "host_ms_per_frame": {"queue_calls": 1000.0 * t_calls / args.steps,
+                                  "nfk_execute": 1000.0 * t_exec / args.steps},
+            "set_calls_per_frame": n_set, "schedule_calls_per_frame": n_sched,
+            "last_frame": {"prop_events": s["n_prop_events"], "fired": s["n_fired"], "msgs": s["n_msgs"]}}
 
 
 if __name__ == "__main__":

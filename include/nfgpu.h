@@ -217,6 +217,11 @@ int nfk_add_schedules(void* world, int32_t n, const int64_t* guid_head, const in
                       const int64_t* now_ms);
 int nfk_remove_schedule(void* world, int64_t guid_head, int64_t guid_data, int32_t kind);
 int nfk_remove_all_schedules(void* world, int64_t guid_head, int64_t guid_data);
+/* the three calls above batched, in call order: op 1 = AddSchedule(self, kind, interval_s, count)
+ * made at now_ms, 2 = RemoveSchedule(self, kind), 3 = RemoveSchedule(self); every GUID and kind is
+ * checked before any call is queued */
+int nfk_schedule_calls(void* world, int32_t n, const int32_t* op, const int64_t* guid_head, const int64_t* guid_data,
+                       const int32_t* kind, const float* interval_s, const int32_t* count, const int64_t* now_ms);
 
 /* ---- one server frame: NFCScheduleModule::Execute (SM:49) + NFCKernelModule::Execute (KM:70)
  * + NFCSceneAOIModule::OnPropertyCommonEvent/GetBroadCastObject fan-out (AOI:227,260,531).

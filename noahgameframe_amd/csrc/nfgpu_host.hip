@@ -30,18 +30,88 @@ int fail(int code, const std::string& msg) {
             return fail(NFK_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(_e));     \
     } while (0)
 
-struct GuidKey {
-    int64_t h, d;
-    bool operator==(const GuidKey& o) const { return h == o.h && d == o.d; }
-};
-struct GuidHash {
-    size_t operator()(const GuidKey& k) const {
-        uint64_t x = (uint64_t)k.h * 0x9E3779B97F4A7C15ull ^ (uint64_t)k.d;
+// NFGUID -> object index (the reference's NFMapEx<NFGUID, NFIObject> lookup, KM:323): open
+// addressing, linear probing, backward-shift deletion; every SetProperty / schedule call does one
+// lookup, so this is the host's per-call cost
+class GuidMap {
+public:
+    int32_t find(int64_t h, int64_t d) const {
+        if (cap_ == 0) return -1;
+        for (size_t i = slot(h, d);; i = (i + 1) & (cap_ - 1)) {
+            const E& e = t_[i];
+            if (e.v < 0) return -1;
+            if (e.h == h && e.d == d) return e.v;
+        }
+    }
+    bool count(int64_t h, int64_t d) const { return find(h, d) >= 0; }
+    // n lookups with the home slots of the lookups kPre ahead prefetched (a batch of calls is
+    // bound by the table's cache misses, not by the probing)
+    void find_many(int32_t n, const int64_t* h, const int64_t* d, int32_t* out) const {
+        constexpr int32_t kPre = 16;
+        if (cap_ == 0) {
+            for (int32_t i = 0; i < n; i++) out[i] = -1;
+            return;
+        }
+        for (int32_t i = 0; i < n && i < kPre; i++) __builtin_prefetch(&t_[slot(h[i], d[i])]);
+        for (int32_t i = 0; i < n; i++) {
+            if (i + kPre < n) __builtin_prefetch(&t_[slot(h[i + kPre], d[i + kPre])]);
+            out[i] = find(h[i], d[i]);
+        }
+    }
+    void insert(int64_t h, int64_t d, int32_t v) {
+        if ((n_ + 1) * 2 > cap_) rehash(std::max<size_t>(64, cap_ * 2));
+        size_t i = slot(h, d);
+        for (; t_[i].v >= 0; i = (i + 1) & (cap_ - 1))
+            if (t_[i].h == h && t_[i].d == d) {
+                t_[i].v = v;
+                return;
+            }
+        t_[i] = E{h, d, v};
+        n_++;
+    }
+    void erase(int64_t h, int64_t d) {
+        if (cap_ == 0) return;
+        size_t i = slot(h, d);
+        for (;; i = (i + 1) & (cap_ - 1)) {
+            if (t_[i].v < 0) return;
+            if (t_[i].h == h && t_[i].d == d) break;
+        }
+        // backward shift: pull later members of the probe run into the hole
+        for (size_t j = (i + 1) & (cap_ - 1);; j = (j + 1) & (cap_ - 1)) {
+            if (t_[j].v < 0) break;
+            const size_t home = slot(t_[j].h, t_[j].d);
+            if (((j - home) & (cap_ - 1)) >= ((j - i) & (cap_ - 1))) {
+                t_[i] = t_[j];
+                i = j;
+            }
+        }
+        t_[i].v = -1;
+        n_--;
+    }
+
+private:
+    struct E {
+        int64_t h, d;
+        int32_t v = -1;
+    };
+    size_t slot(int64_t h, int64_t d) const {
+        uint64_t x = (uint64_t)h * 0x9E3779B97F4A7C15ull ^ (uint64_t)d;
         x ^= x >> 31;
         x *= 0xBF58476D1CE4E5B9ull;
         x ^= x >> 29;
-        return (size_t)x;
+        return (size_t)x & (cap_ - 1);
     }
+    void rehash(size_t c) {
+        std::vector<E> old;
+        old.swap(t_);
+        t_.assign(c, E{});
+        cap_ = c;
+        n_ = 0;
+        for (const E& e : old)
+            if (e.v >= 0) insert(e.h, e.d, e.v);
+    }
+    std::vector<E> t_;
+    size_t cap_ = 0, n_ = 0;
 };
 
 template <typename T>
@@ -72,7 +142,7 @@ struct World {
     std::vector<int64_t> gh, gd;
     std::vector<int32_t> scene, group;
     std::vector<uint8_t> cls, isplayer;
-    std::unordered_map<GuidKey, int32_t, GuidHash> obj_of;
+    GuidMap obj_of;
     std::vector<int32_t> slot_of_obj, obj_of_slot;  // -1: not resident / slack slot
     std::vector<uint8_t> alive;                       // object exists (not destroyed / exported)
     std::vector<int64_t> src_row;                     // >= 0: arrives from row src_row of ins_rows
@@ -135,6 +205,9 @@ struct World {
     // per-frame SetProperty groups (host scratch kept across frames) and their device results
     std::vector<uint32_t> g_slot, g_pid, g_first, xord, xord_t;
     std::vector<uint64_t> xkey, xkey_t;
+    std::vector<uint64_t> hkey, hkey_t;  // schedule-call folding scratch
+    std::vector<int32_t> look;           // GUID lookups of one batched call
+    std::vector<uint32_t> hord, hord_t;
     void* xs_buf = nullptr;  // x_old / x_new
     size_t xs_cap = 0;
     struct HOp { int32_t code; uint32_t slot, kind; float interval; int32_t count; int64_t time; };
@@ -255,10 +328,8 @@ int pin_reserve(World* w, size_t bytes) {
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 int lookup(World* w, int64_t h, int64_t d, int32_t* obj) {
-    auto it = w->obj_of.find(GuidKey{h, d});
-    if (it == w->obj_of.end())
-        return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(h) + "-" + std::to_string(d));
-    *obj = it->second;
+    *obj = w->obj_of.find(h, d);
+    if (*obj < 0) return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(h) + "-" + std::to_string(d));
     return NFK_OK;
 }
 
@@ -703,7 +774,7 @@ int apply_membership(World* w) {
 // a new object index (creation order in this world)
 int32_t add_object(World* w, int64_t gh, int64_t gd, int32_t scene, int32_t group, uint8_t cls, uint8_t pl) {
     const int32_t o = w->n_obj++;
-    w->obj_of[GuidKey{gh, gd}] = o;
+    w->obj_of.insert(gh, gd, o);
     w->gh.push_back(gh);
     w->gd.push_back(gd);
     w->scene.push_back(scene);
@@ -879,8 +950,7 @@ int nfk_create_objects(void* world, int32_t n, const int64_t* gh, const int64_t*
     for (int32_t i = 0; i < n; i++) {
         if (cls[i] >= w->cfg.n_class) return fail(NFK_ERR_ARG, "class id out of range");
         if (group[i] < 0) return fail(NFK_ERR_ARG, "negative group");
-        GuidKey k{gh[i], gd[i]};
-        if (w->obj_of.count(k)) return fail(NFK_ERR_ARG, "The object has Exists");  // KM:131
+        if (w->obj_of.count(gh[i], gd[i])) return fail(NFK_ERR_ARG, "The object has Exists");  // KM:131
     }
     for (int32_t i = 0; i < n; i++) add_object(w, gh[i], gd[i], scene[i], group[i], cls[i], isplayer[i]);
     return NFK_OK;
@@ -1282,14 +1352,22 @@ int nfk_set_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
     World* w = (World*)world;
     if (!w || n < 0 || (n && (!gh || !gd || !pid || !bits))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    // every call is checked before any is queued; one GUID lookup per call
+    const size_t at = w->xops.size();
+    w->xops.resize(at + (size_t)n);
+    World::XOp* x = w->xops.data() + at;
+    w->look.resize(n);
+    w->obj_of.find_many(n, gh, gd, w->look.data());
     for (int32_t i = 0; i < n; i++) {
-        int32_t obj;
-        int r = lookup(w, gh[i], gd[i], &obj);
-        if (r) return r;  // NFCKernelModule logs "There is no object" and returns false (KM:331)
-        if (pid[i] < 0 || pid[i] >= w->n_prop) return fail(NFK_ERR_ARG, "bad property id");
+        const int32_t obj = w->look[i];
+        if (obj < 0 || pid[i] < 0 || pid[i] >= w->n_prop) {
+            w->xops.resize(at);
+            if (obj < 0)  // NFCKernelModule logs "There is no object" and returns false (KM:331)
+                return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
+            return fail(NFK_ERR_ARG, "bad property id");
+        }
+        x[i] = World::XOp{(uint32_t)obj, (uint32_t)pid[i], bits[i]};
     }
-    for (int32_t i = 0; i < n; i++)
-        w->xops.push_back({(uint32_t)w->obj_of[GuidKey{gh[i], gd[i]}], (uint32_t)pid[i], bits[i]});
     return NFK_OK;
 }
 
@@ -1299,17 +1377,15 @@ int nfk_add_schedules(void* world, int32_t n, const int64_t* gh, const int64_t* 
     if (!w || n < 0 || (n && (!gh || !gd || !kind || !interval || !count || !now_ms)))
         return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    std::vector<int32_t> obj(n);
     for (int32_t i = 0; i < n; i++) {
-        int32_t obj;
-        int r = lookup(w, gh[i], gd[i], &obj);
+        int r = lookup(w, gh[i], gd[i], &obj[i]);
         if (r) return r;
         if (kind[i] < 0 || kind[i] >= w->cfg.n_kind || !w->kind_defined[kind[i]])
             return fail(NFK_ERR_ARG, "undefined heartbeat kind");
     }
-    for (int32_t i = 0; i < n; i++) {
-        int32_t obj = w->obj_of[GuidKey{gh[i], gd[i]}];
-        w->hops.push_back({1, (uint32_t)obj, (uint32_t)kind[i], interval[i], count[i], now_ms[i]});
-    }
+    for (int32_t i = 0; i < n; i++)
+        w->hops.push_back({1, (uint32_t)obj[i], (uint32_t)kind[i], interval[i], count[i], now_ms[i]});
     return NFK_OK;
 }
 
@@ -1333,6 +1409,28 @@ int nfk_remove_all_schedules(void* world, int64_t gh, int64_t gd) {
     int r = lookup(w, gh, gd, &obj);
     if (r) return r;
     w->hops.push_back({3, (uint32_t)obj, 0u, 0.f, 0, 0});
+    return NFK_OK;
+}
+
+int nfk_schedule_calls(void* world, int32_t n, const int32_t* op, const int64_t* gh, const int64_t* gd,
+                       const int32_t* kind, const float* interval, const int32_t* count, const int64_t* now_ms) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!op || !gh || !gd || !kind || !interval || !count || !now_ms)))
+        return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    std::vector<int32_t>& obj = w->look;
+    obj.resize(n);
+    w->obj_of.find_many(n, gh, gd, obj.data());
+    for (int32_t i = 0; i < n; i++) {
+        if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
+        if (op[i] < 1 || op[i] > 3) return fail(NFK_ERR_ARG, "schedule call op must be 1, 2 or 3");
+        if (op[i] == 1 && (kind[i] < 0 || kind[i] >= w->cfg.n_kind || !w->kind_defined[kind[i]]))
+            return fail(NFK_ERR_ARG, "undefined heartbeat kind");
+        if (op[i] == 2 && (kind[i] < 0 || kind[i] >= w->cfg.n_kind)) return fail(NFK_ERR_ARG, "bad kind");
+    }
+    for (int32_t i = 0; i < n; i++)
+        w->hops.push_back({op[i], (uint32_t)obj[i], op[i] == 3 ? 0u : (uint32_t)kind[i], op[i] == 1 ? interval[i] : 0.f,
+                           op[i] == 1 ? count[i] : 0, op[i] == 1 ? now_ms[i] : 0});
     return NFK_OK;
 }
 
@@ -1397,8 +1495,8 @@ int nfk_destroy_objects(void* world, int32_t n, const int64_t* gh, const int64_t
         if (r) return r;
     }
     for (int32_t i = 0; i < n; i++) {
-        const int32_t o = w->obj_of[GuidKey{gh[i], gd[i]}];
-        w->obj_of.erase(GuidKey{gh[i], gd[i]});
+        const int32_t o = w->obj_of.find(gh[i], gd[i]);
+        w->obj_of.erase(gh[i], gd[i]);
         w->alive[o] = 0;
         touch(w, o);
     }
@@ -1441,7 +1539,7 @@ int nfk_export_objects(void* world, int32_t n, const int64_t* gh, const int64_t*
                        (const int32_t*)((char*)w->mlist + o_src), n, w->row_words, rows_dev);
     HIPCHK(hipGetLastError());
     for (int32_t i = 0; i < n; i++) {
-        w->obj_of.erase(GuidKey{gh[i], gd[i]});
+        w->obj_of.erase(gh[i], gd[i]);
         w->alive[objs[i]] = 0;
         touch(w, objs[i]);
     }
@@ -1458,7 +1556,7 @@ static int import_common(World* w, int32_t n, const int64_t* gh, const int64_t* 
     for (int32_t i = 0; i < n; i++) {
         if (cls[i] >= w->cfg.n_class) return fail(NFK_ERR_ARG, "class id out of range");
         if (group[i] < 0) return fail(NFK_ERR_ARG, "negative group");
-        if (w->obj_of.count(GuidKey{gh[i], gd[i]})) return fail(NFK_ERR_ARG, "The object has Exists");  // KM:131
+        if (w->obj_of.count(gh[i], gd[i])) return fail(NFK_ERR_ARG, "The object has Exists");  // KM:131
         for (int32_t j = 0; j < i; j++)
             if (gh[j] == gh[i] && gd[j] == gd[i]) return fail(NFK_ERR_ARG, "The object has Exists");
     }
@@ -1591,45 +1689,67 @@ int nfk_execute(void* world, int64_t now_ms) {
             d.ev_new = w->d.ev_new; d.ev_moff = w->d.ev_moff;
         }
     }
-    // schedule calls: pre-scan (remove-list key owner, RemoveSchedule(self)) and post-scan (remove, add)
+    // schedule calls: pre-scan (remove-list key owner, RemoveSchedule(self)) and post-scan (remove,
+    // add), folded per (slot, kind) in call order (a stable radix sort by slot << 5 | kind):
+    //  * RemoveSchedule(self) erases the object's schedules at once (SM:240-243);
+    //  * RemoveSchedule(self, name) inserts into the std::map<NFGUID, name> remove list, so only the
+    //    object's first one in the window owns the key (SM:245-249), and it also blocks the scan's
+    //    own insert (SM:68);
+    //  * remove runs before add at the end of Execute (SM:83-119); AddSchedule keeps an existing
+    //    name, so of several adds of one (object, name) the first wins (SM:108-116).
     std::vector<uint32_t> pre_slot, pre_op;
     struct Post { uint32_t slot, kind, op; float interval; int32_t count; int64_t time; };
     std::vector<Post> post;
-    {
-        std::unordered_map<uint64_t, size_t> post_at;   // (slot, kind) -> index in post
-        std::unordered_map<uint32_t, bool> rm_owner;     // slot owns the remove-list key
-        for (const auto& h : w->hops) {
-            if (h.code == 3) {
-                pre_slot.push_back(h.slot);
+    if (!w->hops.empty()) {
+        const size_t nh = w->hops.size();
+        std::vector<uint64_t>& key = w->hkey;
+        std::vector<uint32_t>& ord = w->hord;
+        key.resize(nh);
+        ord.resize(nh);
+        for (size_t i = 0; i < nh; i++) {
+            key[i] = ((uint64_t)w->hops[i].slot << 5) | (w->hops[i].code == 3 ? 0u : w->hops[i].kind);
+            ord[i] = (uint32_t)i;
+        }
+        radix_sort_stable(key, ord, w->hkey_t, w->hord_t, 31 + 5);
+        for (size_t a = 0; a < nh;) {
+            const uint32_t slot = (uint32_t)(key[a] >> 5);
+            size_t b = a;
+            uint32_t owner_seq = 0xFFFFFFFFu, owner_kind = 0;
+            bool erase_all = false;
+            for (; b < nh && (uint32_t)(key[b] >> 5) == slot; b++) {
+                const World::HOp& h = w->hops[ord[b]];
+                if (h.code == 3) erase_all = true;
+                if (h.code == 2 && ord[b] < owner_seq) {
+                    owner_seq = ord[b];
+                    owner_kind = h.kind;
+                }
+            }
+            if (erase_all) {
+                pre_slot.push_back(slot);
                 pre_op.push_back(2);
-                continue;
             }
-            uint64_t key = ((uint64_t)h.slot << 8) | h.kind;
-            if (h.code == 2) {
-                if (rm_owner.count(h.slot)) continue;  // std::map insert: first (self, name) wins
-                rm_owner[h.slot] = true;
-                pre_slot.push_back(h.slot);
+            if (owner_seq != 0xFFFFFFFFu) {
+                pre_slot.push_back(slot);
                 pre_op.push_back(1);
-                auto it = post_at.find(key);
-                if (it == post_at.end()) {
-                    post_at[key] = post.size();
-                    post.push_back({h.slot, h.kind, 1u | 4u, 0.f, 0, 0});
-                } else {
-                    post[it->second].op |= 1u | 4u;
-                }
-            } else if (h.code == 1) {
-                auto it = post_at.find(key);
-                if (it == post_at.end()) {
-                    post_at[key] = post.size();
-                    post.push_back({h.slot, h.kind, 2u, h.interval, h.count, h.time});
-                } else if (!(post[it->second].op & 2u)) {
-                    Post& p = post[it->second];
-                    p.op |= 2u;
-                    p.interval = h.interval;
-                    p.count = h.count;
-                    p.time = h.time;
-                }
             }
+            for (size_t c = a; c < b;) {
+                const uint32_t kind = (uint32_t)(key[c] & 31);
+                size_t e = c;
+                Post p{slot, kind, 0u, 0.f, 0, 0};
+                if (owner_seq != 0xFFFFFFFFu && owner_kind == kind) p.op |= 1u | 4u;
+                for (; e < b && (uint32_t)(key[e] & 31) == kind; e++) {
+                    const World::HOp& h = w->hops[ord[e]];
+                    if (h.code == 1 && !(p.op & 2u)) {
+                        p.op |= 2u;
+                        p.interval = h.interval;
+                        p.count = h.count;
+                        p.time = h.time;
+                    }
+                }
+                if (p.op) post.push_back(p);
+                c = e;
+            }
+            a = b;
         }
     }
 

@@ -519,6 +519,16 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
 #pragma unroll
     for (int j = 0; j < kW; j++)
         if (((wm >> j) & 1) && v[j] != s_o[j * kTPB + threadIdx.x]) dm |= 1u << j;
+    // a Set program destination that a program moved back to its frame-start value has no event,
+    // but k_sets changed its column: write it back here (the dirty slots are written with their
+    // events)
+    if (xset & ~dm)
+#pragma unroll
+        for (int j = 0; j < kW; j++)
+            if (j < d.n_w && ((xset & ~dm) >> j) & 1) {
+                d.u_col[j][(size_t)e * d.u_str[j]] = v[j];
+                bytes += 8;
+            }
     // fan-out message counts (event_msgs): a public property's event goes to every player of the
     // group but the entity itself, a private & !upload one to the entity only.  The message offset
     // of a slot's event = the counts of the dirty slots with lower property ids (Dev::u_lower).
@@ -650,15 +660,6 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                 });
             }
         }
-        // a Set program destination that a program moved back to its frame-start value has no
-        // event, but k_sets changed its column: write it back
-        if (xset & ~dm)
-#pragma unroll
-            for (int j = 0; j < kW; j++)
-                if (j < d.n_w && ((xset & ~dm) >> j) & 1) {
-                    d.u_col[j][(size_t)e * d.u_str[j]] = v[j];
-                    bytes += 8;
-                }
         uint32_t* const t_fis = d.fi_slot + fi0;
         uint32_t* const t_fik = d.fi_kind + fi0;
         int32_t* const t_fir = d.fi_remain + fi0;

@@ -221,29 +221,29 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
         ext_props = [i for i, n in enumerate(PROPS) if n not in ("SceneID", "GroupID")]
     settable = [i for i, n in enumerate(PROPS) if n not in ("SceneID", "GroupID")]
 
-    def set_value(o, p):
-        if p == PID["HP"]:
-            v = int(rng.integers(1, maxhp[o] + 1))
-            if rng.random() < 0.1:
-                v = int(init_i[PID["HP"], o])  # often unchanged -> no event
-            return np.uint64(v & (2 ** 64 - 1))
-        if p in (PID["Gold"], PID["EXP"]):
-            return np.uint64(int(rng.integers(0, 10 ** 6)))
-        if p < N_INT:
-            v = int(rng.integers(0, 5000))
-            if rng.random() < 0.1:
-                v = int(init_i[p, o])
-            return np.uint64(v & (2 ** 64 - 1))
-        return np.uint64(f64bits(coord(1)[0]) & (2 ** 64 - 1))
+    def set_values(objs, props):
+        """values of SetProperty calls (vectorised): HP within [1, MAXHP], Gold / EXP anything
+        up to 1e6, other ints small; 10 % of HP / small-int sets repeat the creation value (no
+        change -> no event); floats are coordinates"""
+        objs, props = np.asarray(objs, np.int64), np.asarray(props, np.int64)
+        n = len(objs)
+        hp = rng.integers(1, maxhp[objs] + 1)
+        big = rng.integers(0, 10 ** 6, n)
+        small = rng.integers(0, 5000, n)
+        same = rng.random(n) < 0.1
+        fl = coord(n).view(np.int64)
+        init = init_i[np.minimum(props, N_INT - 1), objs]
+        v = np.where(props == PID["HP"], np.where(same, init, hp),
+                     np.where((props == PID["Gold"]) | (props == PID["EXP"]), big,
+                              np.where(props < N_INT, np.where(same, init, small), fl)))
+        return v.astype(np.int64).view(np.uint64)
 
     for t in range(n_ticks):
         k = int(ext_frac * n_obj)
         if k > 0:
             objs = rng.integers(0, n_obj, k)
             props = rng.choice(ext_props, k)
-            vals = np.zeros(k, np.uint64)
-            for j, p in enumerate(props):
-                vals[j] = set_value(objs[j], p)
+            vals = set_values(objs, props)
             # duplicates: same (object, property) set twice in one frame (coalesced)
             dup = rng.random(k) < 0.05
             objs = np.concatenate([objs, objs[dup]])
@@ -257,18 +257,17 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
         if kb > 0:
             # bursts: an entity gets `burst_props` distinct properties set in one frame (more than
             # the programs' working set), some of them twice
-            bo, bp, bv = [], [], []
+            bo, bp = [], []
             for o in rng.choice(n_obj, size=min(kb, n_obj), replace=False):
                 ps = rng.choice(settable, size=min(burst_props, len(settable)), replace=False)
                 ps = np.concatenate([ps, ps[rng.random(len(ps)) < 0.2]])
-                for p in ps:
-                    bo.append(o)
-                    bp.append(p)
-                    bv.append(set_value(o, p))
+                bo.append(np.full(len(ps), o))
+                bp.append(ps)
+            bo, bp = np.concatenate(bo), np.concatenate(bp)
             xt.append(np.full(len(bo), t))
-            xo.append(np.array(bo))
-            xp.append(np.array(bp))
-            xb.append(np.array(bv, np.uint64))
+            xo.append(bo)
+            xp.append(bp)
+            xb.append(set_values(bo, bp))
     cat = lambda lst, dt: np.concatenate(lst).astype(dt) if lst else np.zeros(0, dt)
     x_tick, x_obj, x_pid, x_bits = cat(xt, np.int32), cat(xo, np.int32), cat(xp, np.int32), cat(xb, np.uint64)
 
@@ -277,24 +276,21 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
     if host_ops:
         for t in range(1, n_ticks):
             m = max(1, n_obj // 64)
-            for _ in range(m):
-                o = int(rng.integers(0, n_obj))
-                r = rng.random()
-                if r < 0.45:
-                    op, kind = 1, KID["Poison"]
-                elif r < 0.75:
-                    op, kind = 2, int(rng.choice([KID["Patrol"], KID["Poison"], KID["MPRegen"]]))
-                elif r < 0.85:
-                    op, kind = 3, 0
-                else:
-                    op, kind = 1, int(rng.choice([KID["HPRegen"], KID["Patrol"]]))
-                ht.append(t)
-                hop.append(op)
-                hob.append(o)
-                hk.append(kind)
-                hiv.append(0.5 if kind == KID["Poison"] else 1.0)
-                hc.append(int(rng.integers(1, 5)) if kind == KID["Poison"] else -1)
-                htm.append(int(tick_time[t - 1]) + int(rng.integers(0, tick_ms)))
+            o = rng.integers(0, n_obj, m)
+            r = rng.random(m)
+            rm_kind = rng.choice([KID["Patrol"], KID["Poison"], KID["MPRegen"]], m)
+            add_kind = rng.choice([KID["HPRegen"], KID["Patrol"]], m)
+            op = np.where(r < 0.45, 1, np.where(r < 0.75, 2, np.where(r < 0.85, 3, 1)))
+            kind = np.where(r < 0.45, KID["Poison"], np.where(r < 0.75, rm_kind, np.where(r < 0.85, 0, add_kind)))
+            ht.append(np.full(m, t))
+            hop.append(op)
+            hob.append(o)
+            hk.append(kind)
+            hiv.append(np.where(kind == KID["Poison"], 0.5, 1.0))
+            hc.append(np.where(kind == KID["Poison"], rng.integers(1, 5, m), -1))
+            htm.append(int(tick_time[t - 1]) + rng.integers(0, tick_ms, m))
+    cat1 = lambda lst: np.concatenate(lst) if lst else np.zeros(0)
+    ht, hop, hob, hk, hiv, hc, htm = (cat1(x) for x in (ht, hop, hob, hk, hiv, hc, htm))
     h = dict(h_tick=np.array(ht, np.int32), h_op=np.array(hop, np.int32), h_obj=np.array(hob, np.int32),
              h_kind=np.array(hk, np.int32), h_interval=np.array(hiv, np.float32),
              h_count=np.array(hc, np.int32), h_time=np.array(htm, np.int64))
@@ -388,3 +384,67 @@ def record_world(n_ticks=4, seed=2028, n_obj=500_000, groups=31_250, rec_rows=64
     return make_world(n_obj=n_obj, n_scenes=1, groups_per_scene=groups, players_per_group=per, n_ticks=n_ticks,
                       seed=seed, records=True, rec_rows=rec_rows, ext_frac=kw.pop("ext_frac", 0.0),
                       host_ops=kw.pop("host_ops", False), rec_steady=steady, **kw)
+
+
+# ---- BASELINE config[0]: Tutorial3 scaled to 10k NPCs ----------------------------------------
+# Tutorial/Tutorial3/HelloWorld3Module.cpp: on COE_CREATE_HASDATA every object gets the heartbeat
+# AddSchedule(self, "OnHeartBeat", 5.0f, 10) (:49-56) and an int property "World" with a property
+# callback (:96-104, OnPropertyCallBackEvent); game events set "World" (:16-22, OnEvent).  Scaled
+# to 10k NPC objects in scene 1 group 0.  The tutorial's heartbeat only prints; here its effect
+# program increments "World", so that every heartbeat fires the property callback.  "World" is
+# added at runtime in the tutorial (NFCProperty defaults: not public, not private, so the AOI
+# module sends it to nobody); SceneID / GroupID are private (IObject.xml), X / Y / Z public.
+T3_INT_PROPS = ["SceneID", "GroupID", "World"]
+T3_FLT_PROPS = ["X", "Y", "Z"]
+T3_PROPS = T3_INT_PROPS + T3_FLT_PROPS
+T3_PID = {n: i for i, n in enumerate(T3_PROPS)}
+T3_KINDS = ["OnHeartBeat"]
+
+
+def tutorial3_world(n_obj=10_000, n_ticks=120, tick_ms=100, seed=3, event_frac=0.01, t0=1_700_000_000_000,
+                    guid_head=0):
+    rng = np.random.default_rng(seed)
+    ni, nf = len(T3_INT_PROPS), len(T3_FLT_PROPS)
+    # NFGUID(0, 10) in the tutorial; here NFGUID(guid_head, 10 + i)
+    gdata = (10 + np.arange(n_obj)).astype(np.int64)
+    ghead = np.full(n_obj, guid_head, np.int64)
+    scene = np.ones(n_obj, np.int32)
+    group = np.zeros(n_obj, np.int32)
+    flags = np.zeros((1, len(T3_PROPS)), np.uint8)
+    flags[0, T3_PID["SceneID"]] = PRIVATE
+    flags[0, T3_PID["GroupID"]] = PRIVATE
+    for n in ("X", "Y", "Z"):
+        flags[0, T3_PID[n]] = PUBLIC | PRIVATE
+    init_i = np.zeros((ni, n_obj), np.int64)
+    init_i[T3_PID["SceneID"]] = 1
+    init_i[T3_PID["World"]] = 1111   # pObject->SetPropertyInt("World", 1111) (:99)
+    init_f = rng.uniform(-100.0, 100.0, (nf, n_obj))
+    ops = np.zeros((1, MAX_OPS), OP_DTYPE)
+    ops[0, 0] = (OP_IADD_CLAMP, 0, T3_PID["World"], 0, 1, I64_MIN, I64_MAX)
+    n_ops = np.array([1], np.int32)
+    # objects created over the first 5 s (so the 5 s heartbeats do not all fire in one frame)
+    s_time = (t0 - rng.integers(0, 5000, n_obj)).astype(np.int64)
+    tick_time = (t0 + tick_ms * np.arange(1, n_ticks + 1)).astype(np.int64)
+    # OnEvent -> SetPropertyInt(self, "World", arg.Int(0)) for a share of the objects every frame
+    xt, xo, xb = [], [], []
+    k = int(event_frac * n_obj)
+    for t in range(n_ticks):
+        if k:
+            xt.append(np.full(k, t))
+            xo.append(rng.integers(0, n_obj, k))
+            xb.append(rng.integers(0, 1000, k).astype(np.uint64))
+    cat = lambda lst, dt: np.concatenate(lst).astype(dt) if lst else np.zeros(0, dt)
+    x_tick, x_obj, x_bits = cat(xt, np.int32), cat(xo, np.int32), cat(xb, np.uint64)
+    e32, e64, ef = np.zeros(0, np.int32), np.zeros(0, np.int64), np.zeros(0, np.float32)
+    return dict(
+        cfg=np.array([n_obj, ni, nf, 1, 1, 0, n_obj, n_ticks], np.int64),
+        prop_flags=flags, prop_names=_names(T3_PROPS), kind_names=_names(T3_KINDS), ops=ops, n_ops=n_ops,
+        guid_head=ghead, guid_data=gdata, scene=scene, group=group, cls=np.zeros(n_obj, np.uint8),
+        is_player=np.zeros(n_obj, np.uint8), init_i=init_i, init_f=init_f,
+        s_obj=np.arange(n_obj, dtype=np.int32), s_kind=np.zeros(n_obj, np.int32),
+        s_interval=np.full(n_obj, 5.0, np.float32), s_count=np.full(n_obj, 10, np.int32), s_time=s_time,
+        tick_time=tick_time, x_tick=x_tick, x_obj=x_obj, x_pid=np.full(len(x_obj), T3_PID["World"], np.int32),
+        x_bits=x_bits, h_tick=e32, h_op=e32, h_obj=e32, h_kind=e32, h_interval=ef, h_count=e32, h_time=e64,
+        sw_tick=e32, sw_obj=e32, sw_scene=e32, sw_group=e32, sw_x=ef, sw_y=ef, sw_z=ef,
+        scene_props=np.array([T3_PID["SceneID"], T3_PID["GroupID"], T3_PID["X"], T3_PID["Y"], T3_PID["Z"]],
+                             np.int32))

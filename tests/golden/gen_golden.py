@@ -33,12 +33,16 @@ FIXTURES = {
 }
 
 
+# BASELINE config[0]: Tutorial3 (HelloWorld3Module.cpp) heartbeats + property callbacks, scaled down
+TUTORIAL3 = {"tutorial3": dict(n_obj=2000, n_ticks=80, seed=606)}
+
+
 def main(names=None):
     exe = os.path.join(ROOT, "oracle", "_ref", "nf_ref_harness")
-    for name, kw in FIXTURES.items():
+    for name, kw in {**FIXTURES, **TUTORIAL3}.items():
         if names and name not in names:
             continue
-        w = workload.make_world(**kw)
+        w = workload.tutorial3_world(**kw) if name in TUTORIAL3 else workload.make_world(**kw)
         wp = os.path.join(HERE, f"{name}.workload.nfio")
         ep = os.path.join(HERE, f"{name}.expected.nfio")
         nfio.write(wp, w)

@@ -19,7 +19,7 @@ PATHS = pytest.mark.parametrize("path", [0, 8], ids=["k_tick", "k_tick_touch"])
 
 
 @PATHS
-@pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets"])
+@pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets", "tutorial3"])
 def test_gpu_matches_reference_golden(gpu_available, monkeypatch, name, path):
     monkeypatch.setenv("NFGPU_ABLATE", str(path))
     w = nfio.read(os.path.join(GOLDEN, f"{name}.workload.nfio"))
@@ -77,6 +77,13 @@ def test_switch_scene_layouts(gpu_available, slack):
     w = workload.make_world(n_obj=3000, n_scenes=2, groups_per_scene=5, players_per_group=3, n_ticks=8,
                             seed=31 + slack, switch_frac=0.03, switch_new_groups=True, records=True, rec_rows=8)
     compare_runs(run_gpu(w, slack_per_256=slack), run_oracle(w))
+
+
+def test_gpu_full_size_config0_tutorial3(gpu_available):
+    """BASELINE config[0]: Tutorial3 (HelloWorld3Module.cpp) at 10k NPCs, 120 frames (every object's
+    5 s x 10 "OnHeartBeat" fires twice or three times; OnEvent sets of "World" every frame)."""
+    w = workload.tutorial3_world(n_ticks=120)
+    compare_runs(run_gpu(w), run_oracle(w))
 
 
 def test_gpu_full_size_config1(gpu_available):

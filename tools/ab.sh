@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 for r in $(seq 1 "$R"); do
   for lib in "$@"; do
     n=$(basename "$lib" .so)
-    NFGPU_LIB=$PWD/$lib timeout -k 5 120 python bench.py --steps 50 --warmup 5 --cpu-baseline off ${BENCH_ARGS:-} \
+    NFGPU_LIB=$PWD/$lib timeout -k 5 120 python bench.py --steps 50 --warmup 5 --cpu-baseline off --host-calls off ${BENCH_ARGS:-} \
       > "$OUT/${n}_$r.log" 2>&1 || { echo "fail $n"; tail -3 "$OUT/${n}_$r.log"; exit 1; }
     python -c "
 import json; d=json.loads(open('$OUT/${n}_$r.log').read().strip().splitlines()[-1])

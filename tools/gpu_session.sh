@@ -28,8 +28,9 @@ for step in "$@"; do
     tests) run tests 900 python -u -m pytest tests -m gpu -v --maxfail=5 -p no:cacheprovider \
              --timeout 300 --timeout-method thread ;;
     bench) run bench 600 python bench.py --steps 50 --warmup 5 ;;
-    bench3) run bench3 600 python bench.py --config 3 --steps 20 --warmup 3 --cpu-baseline off ;;
-    bench4) run bench4 600 python bench.py --config 4 --steps 20 --warmup 3 --cpu-baseline off ;;
+    bench0) run bench0 600 python bench.py --config 0 --steps 50 --warmup 5 ;;
+    bench3) run bench3 600 python bench.py --config 3 --steps 20 --warmup 3 ${CPUB:---cpu-baseline off} ;;
+    bench4) run bench4 600 python bench.py --config 4 --steps 20 --warmup 3 ${CPUB:---cpu-baseline off} ;;
     bench2g) NFGPU_BENCH_TRACE=1 run bench2g 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                --master-port 29561 bench.py --gpus 2 --steps 20 --warmup 3 --backend gloo --cpu-baseline off \
                --entities 262144 --groups 1024 --migrate 128 ;;
