@@ -14,13 +14,22 @@
 //   NFComm/NFPluginModule/NFIModule.h           Init / AfterInit / Execute / BeforeShut / Shut
 //   NFComm/NFPluginModule/NFIRankRedisModule.h  GetRange (leaderboard over a property)
 //
-// Differences a plugin author must know (DESIGN.md §5):
+// Differences a plugin author must know (DESIGN.md §1):
 //   * A heartbeat's state change is a device effect program (nfk_op list) registered once per
-//     schedule name; the C++ functor passed to AddSchedule still runs, after the device frame,
-//     with the reference's arguments (self, name, fTime, nCount).
+//     schedule name before AfterInit (an empty list for a functor-only heartbeat); the C++
+//     functor passed to AddSchedule still runs, after the device frame, with the reference's
+//     arguments (self, name, fTime, nCount), objects in NFGUID order and each object's schedules
+//     in name order, as NFCScheduleModule::Execute walks its maps (SM:52-80).  Its own Set calls
+//     land in the next frame.
 //   * SetProperty* calls are queued and applied at the start of the next Execute, in call order,
-//     through the reference's change predicates; callbacks see coalesced (first old, last new)
-//     events once per frame, in (scene, group, guid, property) order.
+//     through the reference's change predicates; GetProperty* sees them at once (read-your-writes);
+//     callbacks see coalesced (first old, last new) events once per frame, in (scene, group,
+//     guid, property) order.
+//   * Time comes from SetTimeSource (default: NFGetTime(), system clock milliseconds,
+//     NFPlatform.h:367), read by AddSchedule and Execute like the reference.
+//   * Limits: 64 int + 64 float frame properties, 15 classes, 32 schedule names, 8 records of at
+//     most 64 rows x 16 columns, 4 ops per heartbeat program, 12 properties written by programs,
+//     16383 players per scene group (nfgpu.h).
 //   * String / Vector properties stay host-side (not on the frame path).
 #pragma once
 #include <cstdint>
@@ -70,10 +79,67 @@ using PROPERTY_EVENT_FUNCTOR = std::function<int(const NFGUID&, const std::strin
 using RECORD_EVENT_FUNCTOR =
     std::function<int(const NFGUID&, const RECORD_EVENT_DATA&, const TData&, const TData&)>;
 using OBJECT_SCHEDULE_FUNCTOR = std::function<int(const NFGUID&, const std::string&, const float, const int)>;
+using MODULE_SCHEDULE_FUNCTOR = std::function<int(const std::string&, const float, const int)>;
 using PROPERTY_SINGLE_EVENT_FUNCTOR = std::function<int(const NFGUID&, const std::string&, const TData&,
                                                         const TData&, const std::vector<NFGUID>&)>;
 using RECORD_SINGLE_EVENT_FUNCTOR = std::function<int(const NFGUID&, const std::string&, const RECORD_EVENT_DATA&,
                                                       const TData&, const TData&, const std::vector<NFGUID>&)>;
+
+// Module schedules of NFIScheduleModule (no object: AddSchedule(name, cb, fTime, nCount),
+// RemoveSchedule(name), ExistSchedule(name)), restating NFCScheduleModule (SM:123-176 Execute,
+// SM:184-216 calls) on the host: they are not entity state, so they stay off the device.
+class ModuleScheduler {
+public:
+    struct Element {  // NFCScheduleElement of a module schedule
+        std::string name;
+        float interval = 0.f;
+        int64_t next = 0, start = 0;
+        int remain = 0, all = 0;
+        bool forever = false;
+        MODULE_SCHEDULE_FUNCTOR cb;
+    };
+    bool AddSchedule(const std::string& name, const MODULE_SCHEDULE_FUNCTOR& cb, float fTime, int nCount,
+                     int64_t now) {
+        Element e;
+        e.name = name;
+        e.interval = fTime;
+        e.next = now + (int64_t)(fTime * 1000);
+        e.start = now;
+        e.remain = e.all = nCount;
+        e.forever = nCount < 0;
+        e.cb = cb;
+        add_.push_back(e);  // mModuleAddList
+        return true;
+    }
+    bool RemoveSchedule(const std::string& name) {
+        remove_.push_back(name);  // mModuleRemoveList
+        return true;
+    }
+    bool ExistSchedule(const std::string& name) const { return map_.count(name) != 0; }
+    // the module part of NFCScheduleModule::Execute: fire (name order), remove list, add list (an
+    // add replaces a schedule of the same name)
+    void Execute(const std::function<int64_t()>& now) {
+        for (auto& kv : map_) {
+            Element& e = kv.second;
+            if (!(now() > e.next) || !(e.remain > 0 || e.forever)) continue;
+            e.remain--;
+            if (e.cb) e.cb(e.name, e.interval, e.remain);
+            if (e.remain <= 0 && !e.forever)
+                remove_.push_back(e.name);
+            else
+                e.next = e.start + (int64_t)(e.interval * 1000) * (int64_t)(e.all - e.remain);
+        }
+        for (const auto& nm : remove_) map_.erase(nm);
+        remove_.clear();
+        for (auto& e : add_) map_[e.name] = e;
+        add_.clear();
+    }
+
+private:
+    std::map<std::string, Element> map_;  // mModuleScheduleMap (name order)
+    std::vector<Element> add_;
+    std::vector<std::string> remove_;
+};
 
 class NFGPUKernelModule {
 public:
@@ -101,9 +167,12 @@ public:
     // ---- NFIModule lifecycle ----
     bool Init();
     bool AfterInit();  // commits the layout (objects created before AfterInit)
-    bool Execute(int64_t now_ms);
+    bool Execute();    // one frame at the time source's now
     bool BeforeShut();
     bool Shut();
+    // the clock AddSchedule and Execute read (NFGetTime() by default)
+    void SetTimeSource(std::function<int64_t()> now_ms);
+    int64_t Now() const { return clock_(); }
 
     // ---- NFIKernelModule ----
     bool CreateScene(int nSceneID);
@@ -113,18 +182,25 @@ public:
     bool SetPropertyFloat(const NFGUID& self, const std::string& name, double v);
     int64_t GetPropertyInt(const NFGUID& self, const std::string& name);
     double GetPropertyFloat(const NFGUID& self, const std::string& name);
-    // NFCKernelModule::SwitchScene (KM:901-951); writes SceneID/GroupID/X/Y/Z when the schema has them
-    bool SwitchScene(const NFGUID& self, int nTargetSceneID, int nTargetGroupID, float fX, float fY, float fZ);
+    // NFCKernelModule::SwitchScene (KM:901-951); writes SceneID/GroupID/X/Y/Z when the schema has
+    // them; like the reference, fOrient and arg are not used
+    bool SwitchScene(const NFGUID& self, int nTargetSceneID, int nTargetGroupID, float fX, float fY, float fZ,
+                     float fOrient = 0.0f, const std::vector<TData>& arg = {});
     // NFCKernelModule::DestroyObject (KM:273-308): leaves its group, its schedules go with it
     bool DestroyObject(const NFGUID& self);
     bool RegisterCommonPropertyEvent(const PROPERTY_EVENT_FUNCTOR& cb);
     bool RegisterCommonRecordEvent(const RECORD_EVENT_FUNCTOR& cb);
 
-    // ---- NFIScheduleModule ----
+    // ---- NFIScheduleModule: object schedules (SM:218-285) ----
     bool AddSchedule(const NFGUID& self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb, float fTime,
-                     int nCount, int64_t now_ms);
+                     int nCount);
     bool RemoveSchedule(const NFGUID& self, const std::string& name);
     bool RemoveSchedule(const NFGUID& self);
+    bool ExistSchedule(const NFGUID& self, const std::string& name);
+    // ---- NFIScheduleModule: module schedules (SM:123-216; host-side, not entity state) ----
+    bool AddSchedule(const std::string& name, const MODULE_SCHEDULE_FUNCTOR& cb, float fTime, int nCount);
+    bool RemoveSchedule(const std::string& name);
+    bool ExistSchedule(const std::string& name);
 
     // ---- NFIRankRedisModule::GetRange(type, 0, k - 1, memberScoreVec) over a property ----
     bool GetRange(const std::string& prop, int k, std::vector<std::pair<std::string, double>>& memberScoreVec);
@@ -139,6 +215,7 @@ public:
 
 private:
     void check(int rc, const char* what) const;
+    void DeliverEvents();
     void* world_ = nullptr;
     int capacity_;
     void* stream_;
@@ -165,6 +242,10 @@ private:
     std::vector<RECORD_SINGLE_EVENT_FUNCTOR> aoi_rec_cb_;
     std::map<std::pair<int, int>, OBJECT_SCHEDULE_FUNCTOR> sched_cb_;   // (object, kind)
     std::map<std::pair<int, int>, float> sched_time_;
+    // pending functors of AddSchedule calls in this window ((object, kind), first call wins)
+    std::map<std::pair<int, int>, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> sched_add_;
+    ModuleScheduler module_sched_;
+    std::function<int64_t()> clock_;
     nfk_summary summary_{};
 };
 

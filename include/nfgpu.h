@@ -211,10 +211,21 @@ int nfk_spawn_objects(void* world, int32_t n, const int64_t* guid_head, const in
 int nfk_set_props(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
                   const int32_t* pid, const uint64_t* bits);
 
+/* ---- property reads: NFIKernelModule::GetPropertyInt/Float (KM:401-425) ----
+ * The value the reference would return now: the world's value after the last frame (waits for
+ * the world's stream) with this window's queued SetProperty* / SwitchScene writes to that
+ * property applied on top in call order through the change predicates (read-your-writes).  One
+ * 8-byte device read per (entity, property) not read since the last nfk_execute; n > 8 reads are
+ * gathered by one kernel.  NFK_ERR_NOTFOUND for an unknown GUID ("There is no object", KM:411). */
+int nfk_get_props(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data, const int32_t* pid,
+                  uint64_t* bits);
+
 /* ---- heartbeats: NFIScheduleModule (SM:218,240,245,251) ---- */
 int nfk_add_schedules(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
                       const int32_t* kind, const float* interval_s, const int32_t* count,
                       const int64_t* now_ms);
+/* kind -1: RemoveSchedule(self, name) of a name that has no device program — it removes nothing
+ * but still takes the object's remove-list key for this frame (SM:245-249) */
 int nfk_remove_schedule(void* world, int64_t guid_head, int64_t guid_data, int32_t kind);
 int nfk_remove_all_schedules(void* world, int64_t guid_head, int64_t guid_data);
 /* the three calls above batched, in call order: op 1 = AddSchedule(self, kind, interval_s, count)
@@ -222,6 +233,15 @@ int nfk_remove_all_schedules(void* world, int64_t guid_head, int64_t guid_data);
  * checked before any call is queued */
 int nfk_schedule_calls(void* world, int32_t n, const int32_t* op, const int64_t* guid_head, const int64_t* guid_data,
                        const int32_t* kind, const float* interval_s, const int32_t* count, const int64_t* now_ms);
+/* NFIScheduleModule::ExistSchedule(self, name) (SM:276-285): the object's schedule map as the
+ * reference holds it between frames — schedules present after the last frame, minus a
+ * RemoveSchedule(self) queued in this window (it erases at once, SM:240); AddSchedule and
+ * RemoveSchedule(self, name) take effect in the next Execute.  An unknown GUID reads 0. */
+int nfk_exist_schedule(void* world, int64_t guid_head, int64_t guid_data, int32_t kind, int32_t* exists);
+/* the AddSchedule calls of the last frame that created a schedule — the (object, name) had none
+ * after the frame's removals, so the call's functor is the one that fires from now on (SM:108-116);
+ * at most cap entries, *n = how many there are */
+int nfk_read_added(void* world, int32_t cap, int32_t* n, int64_t* guid_head, int64_t* guid_data, int32_t* kind);
 
 /* ---- one server frame: NFCScheduleModule::Execute (SM:49) + NFCKernelModule::Execute (KM:70)
  * + NFCSceneAOIModule::OnPropertyCommonEvent/GetBroadCastObject fan-out (AOI:227,260,531).

@@ -1,6 +1,7 @@
 // nfgpu_host.hip — C-ABI implementation (include/nfgpu.h): world lifetime, schema,
 // membership layout, queued SetProperty / schedule calls, frame launch, readback.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -207,6 +208,18 @@ struct World {
     std::vector<uint64_t> xkey, xkey_t;
     std::vector<uint64_t> hkey, hkey_t;  // schedule-call folding scratch
     std::vector<int32_t> look;           // GUID lookups of one batched call
+    // GetProperty* (nfk_get_props): device values read since the last frame, and the queued
+    // SetProperty chain of each (object, property): ov_last[key] = its last xop, ov_prev links back
+    std::unordered_map<uint64_t, uint64_t> dcache;
+    std::unordered_map<uint64_t, uint32_t> ov_last;
+    std::vector<uint32_t> ov_prev;
+    uint64_t* gat = nullptr;             // device scratch of gathered reads
+    size_t gat_cap = 0;
+    // the last frame's AddSchedule entries (object or -1, kind) and whether each created a schedule
+    std::vector<int32_t> post_obj;
+    std::vector<uint32_t> post_kind;
+    uint8_t* added_d = nullptr;
+    size_t added_cap = 0;
     std::vector<uint32_t> hord, hord_t;
     void* xs_buf = nullptr;  // x_old / x_new
     size_t xs_cap = 0;
@@ -242,6 +255,8 @@ struct World {
     int64_t kt_bytes[KT_N] = {};
     uint64_t last_bytes[3] = {0, 0, 0};
 };
+
+constexpr uint32_t kNoKind = 0xFFFFFFFFu;  // HOp::kind of a RemoveSchedule(self, name) with no device program
 
 int alloc_track(World* w, void** p, size_t bytes) {
     *p = nullptr;
@@ -853,6 +868,8 @@ int nfk_destroy(void* world) {
     if (w->mv_rows) (void)hipFree(w->mv_rows);
     if (w->mlist) (void)hipFree(w->mlist);
     if (w->xs_buf) (void)hipFree(w->xs_buf);
+    if (w->gat) (void)hipFree(w->gat);
+    if (w->added_d) (void)hipFree(w->added_d);
     for (auto& p : w->pend) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -1396,8 +1413,8 @@ int nfk_remove_schedule(void* world, int64_t gh, int64_t gd, int32_t kind) {
     int32_t obj;
     int r = lookup(w, gh, gd, &obj);
     if (r) return r;
-    if (kind < 0 || kind >= w->cfg.n_kind) return fail(NFK_ERR_ARG, "bad kind");
-    w->hops.push_back({2, (uint32_t)obj, (uint32_t)kind, 0.f, 0, 0});
+    if (kind < -1 || kind >= w->cfg.n_kind) return fail(NFK_ERR_ARG, "bad kind");
+    w->hops.push_back({2, (uint32_t)obj, kind < 0 ? kNoKind : (uint32_t)kind, 0.f, 0, 0});
     return NFK_OK;
 }
 
@@ -1426,11 +1443,142 @@ int nfk_schedule_calls(void* world, int32_t n, const int32_t* op, const int64_t*
         if (op[i] < 1 || op[i] > 3) return fail(NFK_ERR_ARG, "schedule call op must be 1, 2 or 3");
         if (op[i] == 1 && (kind[i] < 0 || kind[i] >= w->cfg.n_kind || !w->kind_defined[kind[i]]))
             return fail(NFK_ERR_ARG, "undefined heartbeat kind");
-        if (op[i] == 2 && (kind[i] < 0 || kind[i] >= w->cfg.n_kind)) return fail(NFK_ERR_ARG, "bad kind");
+        if (op[i] == 2 && (kind[i] < -1 || kind[i] >= w->cfg.n_kind)) return fail(NFK_ERR_ARG, "bad kind");
     }
     for (int32_t i = 0; i < n; i++)
-        w->hops.push_back({op[i], (uint32_t)obj[i], op[i] == 3 ? 0u : (uint32_t)kind[i], op[i] == 1 ? interval[i] : 0.f,
+        w->hops.push_back({op[i], (uint32_t)obj[i],
+                           op[i] == 3 ? 0u : (kind[i] < 0 ? kNoKind : (uint32_t)kind[i]), op[i] == 1 ? interval[i] : 0.f,
                            op[i] == 1 ? count[i] : 0, op[i] == 1 ? now_ms[i] : 0});
+    return NFK_OK;
+}
+
+int nfk_get_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid, uint64_t* bits) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !pid || !bits))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    std::vector<int32_t> obj(n);
+    w->obj_of.find_many(n, gh, gd, obj.data());
+    for (int32_t i = 0; i < n; i++) {
+        if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
+        if (pid[i] < 0 || pid[i] >= w->n_prop) return fail(NFK_ERR_ARG, "bad property id");
+    }
+    // 1. the world's values after the last frame (a per-window cache of device reads)
+    std::vector<uint64_t> src;
+    std::vector<int32_t> miss;
+    for (int32_t i = 0; i < n; i++) {
+        const uint64_t key = ((uint64_t)obj[i] << 7) | (uint32_t)pid[i];
+        auto it = w->dcache.find(key);
+        if (it != w->dcache.end()) {
+            bits[i] = it->second;
+            continue;
+        }
+        const int32_t o = obj[i], sl = w->slot_of_obj[o];
+        if (w->src_row[o] >= 0)  // entered in this window: its row of the import buffer
+            src.push_back((1ull << 63) | ((uint64_t)w->src_row[o] * w->row_words + pid[i]));
+        else if (sl >= 0)
+            src.push_back((uint64_t)(w->tab.p_off[pid[i]] + (int64_t)sl * w->tab.p_str[pid[i]]));
+        else
+            return fail(NFK_ERR_STATE, "object without a slot");
+        miss.push_back(i);
+    }
+    if (!miss.empty()) {
+        HIPCHK(hipStreamSynchronize(w->stream));
+        std::vector<uint64_t> got(miss.size());
+        if (miss.size() <= 8) {
+            for (size_t q = 0; q < miss.size(); q++) {
+                const uint64_t* a = (src[q] >> 63) ? w->ins_rows + (src[q] & ~(1ull << 63)) : w->d.pmem + src[q];
+                HIPCHK(hipMemcpy(&got[q], a, 8, hipMemcpyDeviceToHost));
+            }
+        } else {
+            int r = dev_reserve(w, (void**)&w->gat, &w->gat_cap, miss.size() * 16);
+            if (r) return r;
+            HIPCHK(hipMemcpy(w->gat, src.data(), miss.size() * 8, hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(k_gather_words, dim3((unsigned)((miss.size() + kTPB - 1) / kTPB)), dim3(kTPB), 0,
+                               w->stream, (const uint64_t*)w->gat, (int32_t)miss.size(), (const uint64_t*)w->d.pmem,
+                               (const uint64_t*)w->ins_rows, w->gat + miss.size());
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(got.data(), w->gat + miss.size(), miss.size() * 8, hipMemcpyDeviceToHost, w->stream));
+            HIPCHK(hipStreamSynchronize(w->stream));
+        }
+        for (size_t q = 0; q < miss.size(); q++) {
+            const int32_t i = miss[q];
+            bits[i] = got[q];
+            w->dcache[((uint64_t)obj[i] << 7) | (uint32_t)pid[i]] = got[q];
+        }
+    }
+    // 2. this window's queued writes of the property on top, in call order (PR:254 / PR:295)
+    for (size_t i = w->ov_prev.size(); i < w->xops.size(); i++) {
+        const uint64_t key = ((uint64_t)w->xops[i].slot << 7) | w->xops[i].pid;
+        auto it = w->ov_last.find(key);
+        w->ov_prev.push_back(it == w->ov_last.end() ? 0xFFFFFFFFu : it->second);
+        w->ov_last[key] = (uint32_t)i;
+    }
+    std::vector<uint32_t> chain;
+    for (int32_t i = 0; i < n; i++) {
+        auto it = w->ov_last.find(((uint64_t)obj[i] << 7) | (uint32_t)pid[i]);
+        if (it == w->ov_last.end()) continue;
+        chain.clear();
+        for (uint32_t x = it->second; x != 0xFFFFFFFFu; x = w->ov_prev[x]) chain.push_back(x);
+        uint64_t v = bits[i];
+        for (size_t c = chain.size(); c-- > 0;) {
+            const uint64_t b = w->xops[chain[c]].bits;
+            if (pid[i] < w->cfg.n_int) {
+                v = b;
+            } else {
+                double bd, vd;
+                memcpy(&bd, &b, 8);
+                memcpy(&vd, &v, 8);
+                if (!(fabs(bd - vd) <= 1e-15)) v = b;
+            }
+        }
+        bits[i] = v;
+    }
+    return NFK_OK;
+}
+
+int nfk_exist_schedule(void* world, int64_t gh, int64_t gd, int32_t kind, int32_t* exists) {
+    World* w = (World*)world;
+    if (!w || !exists) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    if (kind < 0 || kind >= w->cfg.n_kind) return fail(NFK_ERR_ARG, "bad kind");
+    *exists = 0;
+    const int32_t o = w->obj_of.find(gh, gd);
+    if (o < 0) return NFK_OK;  // no schedule map for the object
+    for (const auto& h : w->hops)
+        if (h.code == 3 && h.slot == (uint32_t)o) return NFK_OK;  // RemoveSchedule(self) erased it
+    uint64_t word = 0;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    if (w->src_row[o] >= 0) {
+        HIPCHK(hipMemcpy(&word, w->ins_rows + (size_t)w->src_row[o] * w->row_words + w->n_prop + 4 * kind + 1, 8,
+                         hipMemcpyDeviceToHost));
+    } else if (w->slot_of_obj[o] >= 0) {
+        HIPCHK(hipMemcpy(&word, (const char*)(w->d.s_hot + (size_t)kind * w->d.s_kstr + w->slot_of_obj[o]) + 8, 8,
+                         hipMemcpyDeviceToHost));
+    }
+    *exists = (int32_t)((word >> 32) & kStPresent);
+    return NFK_OK;
+}
+
+int nfk_read_added(void* world, int32_t cap, int32_t* n, int64_t* gh, int64_t* gd, int32_t* kind) {
+    World* w = (World*)world;
+    if (!w || !n || cap < 0 || (cap && (!gh || !gd || !kind))) return fail(NFK_ERR_ARG, "null argument");
+    *n = 0;
+    const size_t np = w->post_obj.size();
+    if (np == 0) return NFK_OK;
+    std::vector<uint8_t> added(np);
+    HIPCHK(hipStreamSynchronize(w->stream));
+    HIPCHK(hipMemcpy(added.data(), w->added_d, np, hipMemcpyDeviceToHost));
+    int32_t k = 0;
+    for (size_t i = 0; i < np; i++) {
+        if (!added[i] || w->post_obj[i] < 0) continue;
+        if (k < cap) {
+            gh[k] = w->gh[w->post_obj[i]];
+            gd[k] = w->gd[w->post_obj[i]];
+            kind[k] = (int32_t)w->post_kind[i];
+        }
+        k++;
+    }
+    *n = k;
     return NFK_OK;
 }
 
@@ -1707,7 +1855,8 @@ int nfk_execute(void* world, int64_t now_ms) {
         key.resize(nh);
         ord.resize(nh);
         for (size_t i = 0; i < nh; i++) {
-            key[i] = ((uint64_t)w->hops[i].slot << 5) | (w->hops[i].code == 3 ? 0u : w->hops[i].kind);
+            const uint32_t k = w->hops[i].kind;
+            key[i] = ((uint64_t)w->hops[i].slot << 5) | (w->hops[i].code == 3 || k == kNoKind ? 0u : k);
             ord[i] = (uint32_t)i;
         }
         radix_sort_stable(key, ord, w->hkey_t, w->hord_t, 31 + 5);
@@ -1731,6 +1880,7 @@ int nfk_execute(void* world, int64_t now_ms) {
             if (owner_seq != 0xFFFFFFFFu) {
                 pre_slot.push_back(slot);
                 pre_op.push_back(1);
+                if (owner_kind == kNoKind) post.push_back(Post{slot, 0u, 8u, 0.f, 0, 0});  // release the key only
             }
             for (size_t c = a; c < b;) {
                 const uint32_t kind = (uint32_t)(key[c] & 31);
@@ -1807,7 +1957,16 @@ int nfk_execute(void* world, int64_t now_ms) {
     d.x_new = ng ? (uint64_t*)w->xs_buf + ng : nullptr;
     w->xops.clear();
     w->hops.clear();
+    w->dcache.clear();
+    w->ov_last.clear();
+    w->ov_prev.clear();
 
+    w->post_obj.clear();
+    w->post_kind.clear();
+    for (const Post& q : post) {
+        w->post_obj.push_back((q.op & 2u) ? w->obj_of_slot[q.slot] : -1);
+        w->post_kind.push_back(q.kind);
+    }
     d.has_pre = npre > 0;
     if (ng || npre) {
         TimeScope ts(w, KT_AUX);
@@ -1912,10 +2071,13 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     if (npost) {
         TimeScope ts(w, KT_AUX);
+        int r = dev_reserve(w, (void**)&w->added_d, &w->added_cap, npost);
+        if (r) return r;
         hipLaunchKernelGGL(k_post_hostops, dim3((unsigned)((npost + 255) / 256)), dim3(256), 0, w->stream,
                            (const uint32_t*)(S + off_qs), (const uint32_t*)(S + off_qk),
                            (const uint32_t*)(S + off_qo), (const float*)(S + off_qi),
-                           (const int32_t*)(S + off_qc), (const int64_t*)(S + off_qt), (int32_t)npost, d);
+                           (const int32_t*)(S + off_qc), (const int64_t*)(S + off_qt), (int32_t)npost,
+                           w->added_d, d);
         HIPCHK(hipGetLastError());
     }
     // Dense global ranks of the tile-staged outputs (ev_base, fi_base, totals): the frame's own

@@ -85,18 +85,25 @@ __global__ void k_pre_hostops(const uint32_t* __restrict__ slot, const uint32_t*
         for (int k = 0; k < n_kind; k++) s_hot[(size_t)k * kstr + s].state = 0;
 }
 
-// post-scan host ops, one entry per (slot, kind): bit0 remove, bit1 add (remove first), bit2 clear key
+// post-scan host ops, one entry per (slot, kind): bit0 remove, bit1 add (remove first), bit2 clear
+// key, bit3 clear key only (a kind-less remove-list owner); added[i] = the add created the schedule
 __global__ void k_post_hostops(const uint32_t* __restrict__ slot, const uint32_t* __restrict__ kind,
                                const uint32_t* __restrict__ op, const float* __restrict__ interval,
                                const int32_t* __restrict__ count, const int64_t* __restrict__ time, int32_t n,
-                               Dev d) {
+                               uint8_t* __restrict__ added, Dev d) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = slot[i];
+    if (op[i] & 8) {
+        d.e_flags[s] = 0;
+        added[i] = 0;
+        return;
+    }
     const size_t at = (size_t)kind[i] * d.s_kstr + s;
     SchedHot h = d.s_hot[at];
     if (op[i] & 1) h.state = 0;
     if (op[i] & 4) d.e_flags[s] = 0;
+    added[i] = (op[i] & 2) && !(h.state & 1);
     if ((op[i] & 2) && !(h.state & 1)) {  // AddSchedule (SM:218): an existing name wins
         const float f = interval[i];
         const int32_t c = count[i];
@@ -1574,6 +1581,18 @@ __global__ __launch_bounds__(kTPB) void k_rank_collect(Dev d, int32_t pid, uint6
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------------
+// GetProperty* reads (nfk_get_props): word src[i] of the property memory, or (bit 63) of the rows of
+// entities imported in this window
+__global__ __launch_bounds__(kTPB) void k_gather_words(const uint64_t* __restrict__ src, int32_t n,
+                                                       const uint64_t* __restrict__ pmem,
+                                                       const uint64_t* __restrict__ ins, uint64_t* __restrict__ out) {
+    const int i = blockIdx.x * kTPB + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t s = src[i];
+    out[i] = (s >> 63) ? ins[s & ~(1ull << 63)] : pmem[s];
 }
 
 // ---------------------------------------------------------------------------------

@@ -2,14 +2,25 @@
 #include "NFGPUKernelModule.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <numeric>
 
 namespace nfgpu {
 
 static uint64_t bits_of(double d) { uint64_t u; std::memcpy(&u, &d, 8); return u; }
 static double dbl_of(uint64_t u) { double d; std::memcpy(&d, &u, 8); return d; }
 
-NFGPUKernelModule::NFGPUKernelModule(int capacity, void* hip_stream) : capacity_(capacity), stream_(hip_stream) {}
+// NFGetTime() (NFPlatform.h:367): system clock milliseconds since the epoch
+static int64_t nf_get_time() {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+
+NFGPUKernelModule::NFGPUKernelModule(int capacity, void* hip_stream)
+    : capacity_(capacity), stream_(hip_stream), clock_(nf_get_time) {}
+
+void NFGPUKernelModule::SetTimeSource(std::function<int64_t()> now_ms) { clock_ = now_ms ? now_ms : nf_get_time; }
 
 NFGPUKernelModule::~NFGPUKernelModule() {
     if (world_) nfk_destroy(world_);
@@ -195,7 +206,7 @@ bool NFGPUKernelModule::AfterInit() {
 }
 
 bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int nTargetGroupID, float fX, float fY,
-                                    float fZ) {
+                                    float fZ, float /*fOrient*/, const std::vector<TData>& /*arg*/) {
     if (!committed_ || ObjectIndex(self) < 0) return false;  // "There is no object" (KM:948)
     if (!scenes_.count(nTargetSceneID)) return false;       // "no this container" (KM:917)
     check(nfk_switch_scene(world_, self.nHead64, self.nData64, nTargetSceneID, nTargetGroupID, fX, fY, fZ),
@@ -213,6 +224,8 @@ bool NFGPUKernelModule::DestroyObject(const NFGUID& self) {
     obj_of_.erase(self);  // its object index stays reserved; later calls find no object
     for (auto it = sched_cb_.begin(); it != sched_cb_.end();)
         it = it->first.first == o ? sched_cb_.erase(it) : std::next(it);
+    for (auto it = sched_add_.begin(); it != sched_add_.end();)
+        it = it->first.first == o ? sched_add_.erase(it) : std::next(it);
     return true;
 }
 
@@ -250,20 +263,26 @@ bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& 
     return nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) == NFK_OK;
 }
 
+// NFCKernelModule::GetPropertyInt/Float (KM:401-425): the value after this window's queued Sets
+// (nfk_get_props, one element); an unknown object or property, or one of the other type, reads
+// NULL_INT / NULL_FLOAT (TData::GetInt / GetFloat of a mismatched type)
 int64_t NFGPUKernelModule::GetPropertyInt(const NFGUID& self, const std::string& name) {
-    int o = ObjectIndex(self);
-    if (o < 0) return 0;  // NULL_INT (KM:411)
-    std::vector<uint64_t> col(guids_.size());
-    check(nfk_read_prop(world_, PropertyId(name), col.data()), "nfk_read_prop");
-    return (int64_t)col[o];
+    auto it = prop_id_.find(name);
+    if (!committed_ || ObjectIndex(self) < 0 || it == prop_id_.end() || props_[it->second].type != TDATA_INT) return 0;
+    const int32_t pid = PropertyId(name);
+    uint64_t b = 0;
+    check(nfk_get_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b), "nfk_get_props");
+    return (int64_t)b;
 }
 
 double NFGPUKernelModule::GetPropertyFloat(const NFGUID& self, const std::string& name) {
-    int o = ObjectIndex(self);
-    if (o < 0) return 0.0;
-    std::vector<uint64_t> col(guids_.size());
-    check(nfk_read_prop(world_, PropertyId(name), col.data()), "nfk_read_prop");
-    return dbl_of(col[o]);
+    auto it = prop_id_.find(name);
+    if (!committed_ || ObjectIndex(self) < 0 || it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT)
+        return 0.0;
+    const int32_t pid = PropertyId(name);
+    uint64_t b = 0;
+    check(nfk_get_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b), "nfk_get_props");
+    return dbl_of(b);
 }
 
 bool NFGPUKernelModule::RegisterCommonPropertyEvent(const PROPERTY_EVENT_FUNCTOR& cb) {
@@ -283,50 +302,101 @@ bool NFGPUKernelModule::AddRecordEventCallBack(const RECORD_SINGLE_EVENT_FUNCTOR
     return true;
 }
 
+// NFCScheduleModule::AddSchedule (SM:257-275): queued, added at the end of the next Execute unless
+// the (object, name) still has a schedule then; the functor of the call that creates it is the one
+// that fires (nfk_read_added tells which)
 bool NFGPUKernelModule::AddSchedule(const NFGUID& self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb,
-                                    float fTime, int nCount, int64_t now_ms) {
+                                    float fTime, int nCount) {
     int o = ObjectIndex(self);
     auto k = hb_id_.find(name);
-    if (o < 0 || k == hb_id_.end()) return false;
+    if (!committed_ || o < 0 || k == hb_id_.end()) return false;
     int32_t kind = k->second;
-    check(nfk_add_schedules(world_, 1, &self.nHead64, &self.nData64, &kind, &fTime, &nCount, &now_ms),
+    const int64_t now = clock_();
+    check(nfk_add_schedules(world_, 1, &self.nHead64, &self.nData64, &kind, &fTime, &nCount, &now),
           "nfk_add_schedules");
-    if (!sched_cb_.count({o, kind})) {  // an existing name keeps its functor (SM:108)
-        sched_cb_[{o, kind}] = cb;
-        sched_time_[{o, kind}] = fTime;
-    }
+    sched_add_.emplace(std::make_pair(o, kind), std::make_pair(cb, fTime));  // the window's first call wins
     return true;
 }
 
+// SM:245-249: into the remove list (first call per object per frame owns the key); a name with no
+// device program removes nothing but still takes the key
 bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self, const std::string& name) {
     auto k = hb_id_.find(name);
-    if (ObjectIndex(self) < 0 || k == hb_id_.end()) return false;
-    check(nfk_remove_schedule(world_, self.nHead64, self.nData64, k->second), "nfk_remove_schedule");
+    if (!committed_ || ObjectIndex(self) < 0) return false;
+    check(nfk_remove_schedule(world_, self.nHead64, self.nData64, k == hb_id_.end() ? -1 : k->second),
+          "nfk_remove_schedule");
     return true;
 }
 
+// SM:240-243: erases the object's schedules at once
 bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self) {
-    if (ObjectIndex(self) < 0) return false;
+    if (!committed_ || ObjectIndex(self) < 0) return false;
     check(nfk_remove_all_schedules(world_, self.nHead64, self.nData64), "nfk_remove_all_schedules");
     return true;
 }
 
-bool NFGPUKernelModule::Execute(int64_t now_ms) {
-    check(nfk_execute(world_, now_ms), "nfk_execute");
+// SM:276-285
+bool NFGPUKernelModule::ExistSchedule(const NFGUID& self, const std::string& name) {
+    auto k = hb_id_.find(name);
+    if (!committed_ || ObjectIndex(self) < 0 || k == hb_id_.end()) return false;
+    int32_t e = 0;
+    check(nfk_exist_schedule(world_, self.nHead64, self.nData64, k->second, &e), "nfk_exist_schedule");
+    return e != 0;
+}
+
+// module schedules (SM:184-216): host-side (ModuleScheduler), executed after the object schedules
+bool NFGPUKernelModule::AddSchedule(const std::string& name, const MODULE_SCHEDULE_FUNCTOR& cb, float fTime,
+                                    int nCount) {
+    return module_sched_.AddSchedule(name, cb, fTime, nCount, clock_());
+}
+
+bool NFGPUKernelModule::RemoveSchedule(const std::string& name) { return module_sched_.RemoveSchedule(name); }
+
+bool NFGPUKernelModule::ExistSchedule(const std::string& name) { return module_sched_.ExistSchedule(name); }
+
+bool NFGPUKernelModule::Execute() {
+    check(nfk_execute(world_, clock_()), "nfk_execute");
     check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
     const bool want_events = !common_prop_cb_.empty() || !aoi_prop_cb_.empty() || !common_rec_cb_.empty() ||
                              !aoi_rec_cb_.empty();
-    // heartbeat functors, (scene, group, guid, name) order, with the reference's arguments
+    // heartbeat functors with the reference's arguments, in the order NFCScheduleModule::Execute
+    // walks mObjectScheduleMap: objects in NFGUID order, each object's schedules in name order
     if (summary_.n_fired && !sched_cb_.empty()) {
         std::vector<int32_t> fo(summary_.n_fired), fk(summary_.n_fired), fr(summary_.n_fired);
         check(nfk_read_fired(world_, fo.data(), fk.data(), fr.data()), "nfk_read_fired");
-        for (int64_t i = 0; i < summary_.n_fired; i++) {
+        std::vector<int64_t> ord(summary_.n_fired);
+        std::iota(ord.begin(), ord.end(), 0);
+        std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
+            return guids_[fo[a]] < guids_[fo[b]] || (guids_[fo[a]] == guids_[fo[b]] && fk[a] < fk[b]);
+        });
+        for (int64_t i : ord) {
             auto it = sched_cb_.find({fo[i], fk[i]});
             if (it != sched_cb_.end())
                 it->second(guids_[fo[i]], heartbeats_[fk[i]].name, sched_time_[{fo[i], fk[i]}], fr[i]);
         }
     }
-    if (!want_events) return true;
+    // this window's AddSchedule calls that created a schedule: their functors fire from now on
+    if (!sched_add_.empty()) {
+        const int32_t cap = (int32_t)sched_add_.size();
+        std::vector<int64_t> ah(cap), ad(cap);
+        std::vector<int32_t> ak(cap);
+        int32_t n = 0;
+        check(nfk_read_added(world_, cap, &n, ah.data(), ad.data(), ak.data()), "nfk_read_added");
+        for (int32_t i = 0; i < std::min(n, cap); i++) {
+            const int o = ObjectIndex(NFGUID(ah[i], ad[i]));
+            auto it = sched_add_.find({o, ak[i]});
+            if (it == sched_add_.end()) continue;
+            sched_cb_[{o, ak[i]}] = it->second.first;
+            sched_time_[{o, ak[i]}] = it->second.second;
+        }
+        sched_add_.clear();
+    }
+    if (want_events) DeliverEvents();
+    module_sched_.Execute(clock_);  // module schedules (SM:123-176)
+    return true;
+}
+
+void NFGPUKernelModule::DeliverEvents() {
     const int64_t ne = summary_.n_prop_events, nr = summary_.n_rec_events;
     std::vector<int32_t> eo(ne), ep(ne);
     std::vector<uint64_t> eold(ne), enew(ne);
@@ -385,7 +455,6 @@ bool NFGPUKernelModule::Execute(int64_t now_ms) {
             for (auto& cb : aoi_rec_cb_) cb(self, ev.strRecordName, ev, a, b, rcpt);
         }
     }
-    return true;
 }
 
 bool NFGPUKernelModule::BeforeShut() { return true; }

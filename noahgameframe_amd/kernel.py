@@ -79,6 +79,7 @@ def load_library(path=LIB_PATH):
         "nfk_add_schedules": [VP, I32, VP, VP, VP, VP, VP, VP],
         "nfk_remove_schedule": [VP, I64, I64, I32], "nfk_remove_all_schedules": [VP, I64, I64],
         "nfk_schedule_calls": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
+        "nfk_get_props": [VP, I32, VP, VP, VP, VP], "nfk_exist_schedule": [VP, I64, I64, I32, VP],
         "nfk_execute": [VP, I64], "nfk_summary_get": [VP, P(Summary)], "nfk_outputs_get": [VP, P(Outputs)],
         "nfk_read_prop": [VP, I32, VP], "nfk_read_record": [VP, I32, VP], "nfk_read_schedules": [VP, VP, VP, VP],
         "nfk_read_events": [VP, VP, VP, VP, VP], "nfk_read_rec_events": [VP, VP, VP, VP, VP],
@@ -312,8 +313,27 @@ class NFKernelModule:
         self._chk(self.lib.nfk_read_prop(self.h, pid, _p(out)))
         return out.view(np.int64) if pid < self.n_int else out.view(np.float64)
 
+    def get_props(self, guid_head, guid_data, pid):
+        """NFIKernelModule::GetProperty* for n (entity, property) pairs: the value after the last
+        frame with this window's queued writes applied (read-your-writes); raw 64-bit patterns."""
+        a = [np.ascontiguousarray(x, t) for x, t in ((guid_head, np.int64), (guid_data, np.int64), (pid, np.int32))]
+        out = np.zeros(len(a[0]), np.uint64)
+        self._chk(self.lib.nfk_get_props(self.h, len(a[0]), *[_p(x) for x in a], _p(out)))
+        return out
+
     def GetPropertyInt(self, guid, prop):
-        raise NotImplementedError("use read_prop for bulk reads")
+        pid = wl.PID[prop] if isinstance(prop, str) else prop
+        return int(self.get_props([guid[0]], [guid[1]], [pid]).view(np.int64)[0])
+
+    def GetPropertyFloat(self, guid, prop):
+        pid = wl.PID[prop] if isinstance(prop, str) else prop
+        return float(self.get_props([guid[0]], [guid[1]], [pid]).view(np.float64)[0])
+
+    def ExistSchedule(self, guid, name):
+        kind = wl.KID[name] if isinstance(name, str) else name
+        e = ctypes.c_int32()
+        self._chk(self.lib.nfk_exist_schedule(self.h, int(guid[0]), int(guid[1]), int(kind), ctypes.byref(e)))
+        return bool(e.value)
 
     def read_record(self, rec):
         cols, rows = self.rec_shape[rec]
@@ -410,7 +430,24 @@ def run_workload(m, w, tick, collect=True):
                          w["h_count"][hsel], w["h_time"][hsel])
     xsel = np.nonzero(w["x_tick"] == tick)[0]
     if len(xsel):
-        xo = w["x_obj"][xsel]
-        m.set_props(gh[xo], gd[xo], w["x_pid"][xsel], w["x_bits"][xsel])
+        mode = w["x_mode"][xsel] if "x_mode" in w else np.zeros(len(xsel), np.uint8)
+        # runs of plain SetProperty calls go as one batch; a read-modify-write call (mode 1:
+        # SetProperty(p, GetProperty(p) + delta)) reads through nfk_get_props first
+        cut = np.nonzero(np.diff(np.concatenate([[2], mode, [2]])))[0]
+        for a, b in zip(cut[:-1], cut[1:]):
+            sel = xsel[a:b]
+            xo = w["x_obj"][sel]
+            if mode[a] == 0:
+                m.set_props(gh[xo], gd[xo], w["x_pid"][sel], w["x_bits"][sel])
+                continue
+            for i in sel:
+                o, p = int(w["x_obj"][i]), int(w["x_pid"][i])
+                cur = m.get_props([gh[o]], [gd[o]], [p])
+                d = w["x_bits"][i:i + 1]
+                if p < m.n_int:
+                    v = (cur.view(np.int64) + d.view(np.int64)).view(np.uint64)
+                else:
+                    v = (cur.view(np.float64) + d.view(np.float64)).view(np.uint64)
+                m.set_props([gh[o]], [gd[o]], [p], v)
     m.Execute(int(w["tick_time"][tick]))
     return m.read_tick() if collect else None

@@ -106,7 +106,7 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
                tick_ms=100, seed=1, ext_frac=0.05, host_ops=True, records=False, rec_rows=64,
                t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, rec_skill_op=False, sched_edges=False,
                switch_frac=0.0, switch_new_groups=False, rec_steady=False, ext_props=None, burst_frac=0.0,
-               burst_props=20):
+               burst_props=20, rmw_frac=0.0):
     rng = np.random.default_rng(seed)
     n_groups = n_scenes * groups_per_scene
     # ---- objects ----
@@ -212,7 +212,7 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
     tick_time = (t0 + tick_ms * np.arange(1, n_ticks + 1)).astype(np.int64)
 
     # ---- SetProperty calls between frames (call order matters) ----
-    xt, xo, xp, xb = [], [], [], []
+    xt, xo, xp, xb, xm = [], [], [], [], []
     # ext_props: the properties game logic sets ("all": every property but SceneID / GroupID, which
     # only SwitchScene writes, so program operands such as MAXHP / HPREGEN too)
     if ext_props is None:
@@ -253,6 +253,7 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
             xo.append(objs)
             xp.append(props)
             xb.append(vals)
+            xm.append(np.zeros(len(objs), np.uint8))
         kb = int(burst_frac * n_obj)
         if kb > 0:
             # bursts: an entity gets `burst_props` distinct properties set in one frame (more than
@@ -268,8 +269,28 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
             xo.append(bo)
             xp.append(bp)
             xb.append(set_values(bo, bp))
+            xm.append(np.zeros(len(bo), np.uint8))
+        kr = int(rmw_frac * n_obj)
+        if kr > 0:
+            # read-modify-write game logic: SetProperty(p, GetProperty(p) + delta) (x_mode 1: x_bits is
+            # the delta), half of them twice on the same (entity, property) in the same window, so
+            # the second Get must see the first Set (KM:401 after KM:323)
+            ro = rng.integers(0, n_obj, kr)
+            rp = rng.choice(ext_props, kr)
+            again = rng.random(kr) < 0.5
+            ro = np.concatenate([ro, ro[again]])
+            rp = np.concatenate([rp, rp[again]])
+            di = rng.integers(-50, 51, len(ro))
+            di[di == 0] = 7
+            df = rng.uniform(-5.0, 5.0, len(ro)).view(np.int64)
+            xt.append(np.full(len(ro), t))
+            xo.append(ro)
+            xp.append(rp)
+            xb.append(np.where(rp < N_INT, di, df).astype(np.int64).view(np.uint64))
+            xm.append(np.ones(len(ro), np.uint8))
     cat = lambda lst, dt: np.concatenate(lst).astype(dt) if lst else np.zeros(0, dt)
     x_tick, x_obj, x_pid, x_bits = cat(xt, np.int32), cat(xo, np.int32), cat(xp, np.int32), cat(xb, np.uint64)
+    x_mode = cat(xm, np.uint8)
 
     # ---- AddSchedule / RemoveSchedule calls between frames ----
     ht, hop, hob, hk, hiv, hc, htm = [], [], [], [], [], [], []
@@ -324,7 +345,8 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
               sw_z=np.array(sz, np.float32))
 
     n_rec = 1 if records else 0
-    w = dict(
+    extra = {"x_mode": x_mode} if rmw_frac > 0 else {}
+    w = dict(**extra,
         cfg=np.array([n_obj, N_INT, N_FLT, 2, n_kind, n_rec, len(s_obj), n_ticks], np.int64),
         prop_flags=_prop_flags(), prop_names=_names(PROPS), kind_names=_names(KINDS[:n_kind]),
         ops=ops[:n_kind].copy(), n_ops=n_ops[:n_kind].copy(),

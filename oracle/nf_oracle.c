@@ -372,6 +372,8 @@ int main(int argc, char** argv) {
     int32_t* x_obj = (int32_t*)GET("x_obj")->data;
     int32_t* x_pid = (int32_t*)GET("x_pid")->data;
     uint64_t* x_bits = (uint64_t*)GET("x_bits")->data;
+    nfio_arr* xma = nfio_get(&wf, "x_mode");  /* optional: 1 = SetProperty(p, GetProperty(p) + delta) */
+    uint8_t* x_mode = xma ? (uint8_t*)xma->data : NULL;
     nfio_arr* ha = GET("h_tick");
     int64_t NH = (int64_t)ha->shape[0];
     int32_t* h_tick = (int32_t*)ha->data;
@@ -472,11 +474,13 @@ int main(int argc, char** argv) {
             }
             hi++;
         }
-        /* SetProperty* calls made before this Execute, in call order */
+        /* SetProperty* calls made before this Execute, in call order; a read-modify-write call
+         * reads the current value first (NFCKernelModule::GetPropertyInt/Float, KM:401-425) */
         while (xi < NX && x_tick[xi] == t) {
-            int32_t pid = x_pid[xi];
-            if (pid < NI) set_int(x_obj[xi], pid, (int64_t)x_bits[xi]);
-            else set_flt(x_obj[xi], pid, bitsd(x_bits[xi]));
+            int32_t pid = x_pid[xi], o = x_obj[xi];
+            const int rmw = x_mode && x_mode[xi];
+            if (pid < NI) set_int(o, pid, rmw ? (int64_t)((uint64_t)iget(o, pid) + x_bits[xi]) : (int64_t)x_bits[xi]);
+            else set_flt(o, pid, rmw ? fget(o, pid) + bitsd(x_bits[xi]) : bitsd(x_bits[xi]));
             xi++;
         }
         sched_execute(now);

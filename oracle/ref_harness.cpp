@@ -272,8 +272,47 @@ static int repro_record_float() {
     _exit(0);
 }
 
+// The reference's module schedules (NFCScheduleModule, SM:123-216) driven by a script (see
+// tests/cpp/module_sched.cpp for the format); prints what the functors see.
+static int module_script(const char* path) {
+    FILE* f = fopen(path, "r");
+    if (!f) return 2;
+    SchedProbe sched(nullptr);
+    auto cb = MODULE_SCHEDULE_FUNCTOR_PTR(new MODULE_SCHEDULE_FUNCTOR(
+        [](const std::string& name, const float t, const int remain) {
+            printf("fire %lld %s %.3f %d\n", (long long)g_now_ms, name.c_str(), t, remain);
+            return 0;
+        }));
+    char op[16], name[64];
+    long long t;
+    while (fscanf(f, "%lld %15s", &t, op) == 2) {
+        g_now_ms = t;
+        std::string o(op);
+        if (o == "add") {
+            float ft;
+            int cnt;
+            if (fscanf(f, "%63s %f %d", name, &ft, &cnt) != 3) return 3;
+            sched.AddSchedule(std::string(name), cb, ft, cnt);
+        } else if (o == "remove") {
+            if (fscanf(f, "%63s", name) != 1) return 3;
+            sched.RemoveSchedule(std::string(name));
+        } else if (o == "exist") {
+            if (fscanf(f, "%63s", name) != 1) return 3;
+            printf("exist %lld %s %d\n", (long long)g_now_ms, name, sched.ExistSchedule(std::string(name)) ? 1 : 0);
+        } else if (o == "exec") {
+            sched.Execute();
+        } else {
+            return 3;
+        }
+    }
+    fclose(f);
+    fflush(stdout);
+    _exit(0);
+}
+
 int main(int argc, char** argv) {
     if (argc == 2 && strcmp(argv[1], "--repro-record-float") == 0) return repro_record_float();
+    if (argc == 3 && strcmp(argv[1], "--module-script") == 0) return module_script(argv[2]);
     bool bench = argc == 4 && strcmp(argv[1], "--bench") == 0;
     if (!bench && argc != 3) {
         fprintf(stderr, "usage: nf_ref_harness <workload.nfio> <out.nfio> | --bench <workload.nfio> <ticks>\n");
@@ -419,6 +458,8 @@ int main(int argc, char** argv) {
     int32_t* x_obj = (int32_t*)GET(wf, "x_obj")->data;
     int32_t* x_pid = (int32_t*)GET(wf, "x_pid")->data;
     uint64_t* x_bits = (uint64_t*)GET(wf, "x_bits")->data;
+    nfio_arr* xma = nfio_get(&wf, "x_mode");  // optional: 1 = SetProperty(p, GetProperty(p) + delta)
+    uint8_t* x_mode = xma ? (uint8_t*)xma->data : nullptr;
     nfio_arr* ha = GET(wf, "h_tick");
     int64_t NH = (int64_t)ha->shape[0];
     int32_t* h_tick = (int32_t*)ha->data;
@@ -517,8 +558,11 @@ int main(int argc, char** argv) {
         auto t0 = std::chrono::steady_clock::now();
         while (xi < NX && x_tick[xi] == t) {
             NFGUID self = W.id[x_obj[xi]];
-            if (x_pid[xi] < W.NI) SetInt(self, x_pid[xi], (int64_t)x_bits[xi]);
-            else SetFloat(self, x_pid[xi], bitsd(x_bits[xi]));
+            const bool rmw = x_mode && x_mode[xi];  // game logic: Set(p, Get(p) + delta) (KM:401 then KM:323)
+            if (x_pid[xi] < W.NI)
+                SetInt(self, x_pid[xi], rmw ? (int64_t)((uint64_t)GetInt(self, x_pid[xi]) + x_bits[xi]) : (int64_t)x_bits[xi]);
+            else
+                SetFloat(self, x_pid[xi], rmw ? GetFloat(self, x_pid[xi]) + bitsd(x_bits[xi]) : bitsd(x_bits[xi]));
             xi++;
         }
         g_now_ms = tick_time[t];

@@ -15,6 +15,9 @@
 
 using namespace nfgpu;
 
+// the time source of the module (NFGetTime() in a server): the workload's call and frame times
+static int64_t g_now = 0;
+
 static std::string cstr(const uint8_t* p) { return std::string((const char*)p, strnlen((const char*)p, 32)); }
 
 int main(int argc, char** argv) {
@@ -36,6 +39,7 @@ int main(int argc, char** argv) {
     int32_t* nops = (int32_t*)A("n_ops")->data;
 
     NFGPUKernelModule km((int)N);
+    km.SetTimeSource([] { return g_now; });
     std::vector<std::string> pname(NP), kname(NK), cname = {"NPC", "Player"};
     for (int p = 0; p < NP; p++) {
         pname[p] = cstr(pnames + 32 * p);
@@ -152,8 +156,10 @@ int main(int argc, char** argv) {
     float* s_int = (float*)A("s_interval")->data;
     int32_t* s_cnt = (int32_t*)A("s_count")->data;
     int64_t* s_time = (int64_t*)A("s_time")->data;
-    for (int64_t i = 0; i < NS; i++)
-        km.AddSchedule(NFGUID(gh[s_obj[i]], gd[s_obj[i]]), kname[s_kind[i]], hb, s_int[i], s_cnt[i], s_time[i]);
+    for (int64_t i = 0; i < NS; i++) {
+        g_now = s_time[i];
+        km.AddSchedule(NFGUID(gh[s_obj[i]], gd[s_obj[i]]), kname[s_kind[i]], hb, s_int[i], s_cnt[i]);
+    }
 
     int64_t* tick_time = (int64_t*)A("tick_time")->data;
     nfio_arr* xa = A("x_tick");
@@ -162,6 +168,8 @@ int main(int argc, char** argv) {
     int32_t* x_obj = (int32_t*)A("x_obj")->data;
     int32_t* x_pid = (int32_t*)A("x_pid")->data;
     uint64_t* x_bits = (uint64_t*)A("x_bits")->data;
+    nfio_arr* xma = nfio_get(&wf, "x_mode");  // 1: SetProperty(p, GetProperty(p) + delta)
+    uint8_t* x_mode = xma ? (uint8_t*)xma->data : nullptr;
     nfio_arr* ha = A("h_tick");
     int64_t NH = (int64_t)ha->shape[0];
     int32_t* h_tick = (int32_t*)ha->data;
@@ -199,16 +207,25 @@ int main(int argc, char** argv) {
         }
         for (; hi < NH && h_tick[hi] == t; hi++) {
             NFGUID g(gh[h_obj[hi]], gd[h_obj[hi]]);
-            if (h_op[hi] == 1) km.AddSchedule(g, kname[h_kind[hi]], hb, h_int[hi], h_cnt[hi], h_time[hi]);
+            g_now = h_time[hi];
+            if (h_op[hi] == 1) km.AddSchedule(g, kname[h_kind[hi]], hb, h_int[hi], h_cnt[hi]);
             else if (h_op[hi] == 2) km.RemoveSchedule(g, kname[h_kind[hi]]);
             else km.RemoveSchedule(g);
         }
         for (; xi < NX && x_tick[xi] == t; xi++) {
             NFGUID g(gh[x_obj[xi]], gd[x_obj[xi]]);
-            if (x_pid[xi] < NI) km.SetPropertyInt(g, pname[x_pid[xi]], (int64_t)x_bits[xi]);
-            else { double v; memcpy(&v, &x_bits[xi], 8); km.SetPropertyFloat(g, pname[x_pid[xi]], v); }
+            const std::string& pn = pname[x_pid[xi]];
+            const bool rmw = x_mode && x_mode[xi];  // game logic reading its own writes (KM:401 after KM:323)
+            if (x_pid[xi] < NI) {
+                km.SetPropertyInt(g, pn, rmw ? (int64_t)((uint64_t)km.GetPropertyInt(g, pn) + x_bits[xi]) : (int64_t)x_bits[xi]);
+            } else {
+                double v;
+                memcpy(&v, &x_bits[xi], 8);
+                km.SetPropertyFloat(g, pn, rmw ? km.GetPropertyFloat(g, pn) + v : v);
+            }
         }
-        km.Execute(tick_time[t]);
+        g_now = tick_time[t];
+        km.Execute();
         moff.push_back((uint32_t)mr.size());
         // prop events then record events share one CSR in the oracle layout
         char nm[32];
@@ -254,6 +271,12 @@ int main(int argc, char** argv) {
         snprintf(nm, sizeof nm, "rank_p%d_score", p);
         nfio_put1(&w, nm, NFIO_F64, ts.data(), ts.size(), 8);
     }
+    // NFIScheduleModule::ExistSchedule(self, name) for every object and name after the last frame
+    std::vector<uint8_t> present((size_t)NK * N);
+    for (int k = 0; k < NK; k++)
+        for (int64_t o = 0; o < N; o++) present[(size_t)k * N + o] = km.ExistSchedule(NFGUID(gh[o], gd[o]), kname[k]);
+    uint64_t sp[2] = {(uint64_t)NK, (uint64_t)N};
+    nfio_put(&w, "final_s_present", NFIO_U8, 2, sp, present.data(), present.size());
     uint64_t sh[2] = {(uint64_t)NI, (uint64_t)N};
     nfio_put(&w, "final_i", NFIO_I64, 2, sh, fi.data(), fi.size() * 8);
     uint64_t sf[2] = {(uint64_t)NF, (uint64_t)N};

@@ -30,6 +30,10 @@ FIXTURES = {
     # bursts of 20 distinct properties on one entity in one frame (beyond the programs' working set)
     "wide_sets": dict(n_obj=500, n_scenes=2, groups_per_scene=5, players_per_group=4, n_ticks=8, seed=505,
                       ext_frac=0.1, ext_props="all", burst_frac=0.03, burst_props=20, host_ops=True),
+    # read-modify-write game logic: SetProperty(p, GetProperty(p) + delta), often twice on one
+    # (entity, property) in one window, so the second Get must see the first Set (KM:401 after KM:323)
+    "rmw": dict(n_obj=500, n_scenes=2, groups_per_scene=4, players_per_group=3, n_ticks=8, seed=707,
+                ext_frac=0.05, ext_props="all", rmw_frac=0.06, host_ops=True, switch_frac=0.02),
 }
 
 

@@ -68,3 +68,60 @@ def test_missing_library_raises(tmp_path):
             kernel.load_library(str(tmp_path / "nope.so"))
         finally:
             kernel._lib = None
+
+
+REF_TREE = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF_TREE, "NFComm")), reason="reference tree not present")
+def test_integration_adapter_compiles_against_reference_headers():
+    """integration/NFGPUKernelPlugin.cpp is the reference-side plugin: it
+    implements every NFIScheduleModule pure virtual (NFIScheduleModule.h:23-39) and overrides
+    NFIKernelModule's frame-path calls (NFIKernelModule.h:103-148) against the reference's own
+    headers; REGISTER_MODULE instantiates both adapters, so a missing override fails here."""
+    subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-I", REF_TREE, "-I", os.path.join(REF_TREE, "Dependencies"),
+                    "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "integration", "NFGPUKernelPlugin.cpp")],
+                   check=True)
+
+
+def _module_script(rng, n_lines=400):
+    """a random module-schedule session: adds (sometimes of an existing name, count 0, forever),
+    removes (of existing and unknown names), ExistSchedule probes, Execute every ~100 ms"""
+    names = ["Alpha", "Beta", "Gamma", "Delta"]
+    now, lines = 1_700_000_000_000, []
+    for _ in range(n_lines):
+        now += int(rng.integers(0, 60))
+        r = rng.random()
+        nm = names[int(rng.integers(0, len(names)))]
+        if r < 0.25:
+            ft = float(rng.choice([0.05, 0.1, 0.25, 0.5, -0.05]))
+            cnt = int(rng.choice([1, 2, 3, 5, 0, -1]))
+            lines.append(f"{now} add {nm} {ft} {cnt}")
+        elif r < 0.35:
+            lines.append(f"{now} remove {nm}")
+        elif r < 0.5:
+            lines.append(f"{now} exist {nm}")
+        else:
+            lines.append(f"{now} exec")
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "nf_ref_harness")),
+                    reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_module_schedules_match_reference(tmp_path, seed):
+    """NFIScheduleModule module schedules (AddSchedule(name, cb, fTime, nCount) / RemoveSchedule /
+    ExistSchedule, SM:123-216): the plugin's host-side ModuleScheduler against the reference's
+    compiled NFCScheduleModule on the same script — every functor call and every probe."""
+    import numpy as np
+    exe = os.path.join(ROOT, "tests", "cpp", "_bin", "module_sched")
+    if not os.path.exists(exe):
+        import __graft_entry__
+        __graft_entry__.build_plugin()
+    sp = tmp_path / "s.txt"
+    sp.write_text(_module_script(np.random.default_rng(seed)))
+    ref = subprocess.run([os.path.join(ROOT, "oracle", "_ref", "nf_ref_harness"), "--module-script", str(sp)],
+                         check=True, capture_output=True, text=True).stdout
+    got = subprocess.run([exe, str(sp)], check=True, capture_output=True, text=True).stdout
+    assert ref.count("fire") > 20 and ref.count("exist") > 20
+    assert got == ref

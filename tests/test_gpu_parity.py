@@ -19,7 +19,7 @@ PATHS = pytest.mark.parametrize("path", [0, 8], ids=["k_tick", "k_tick_touch"])
 
 
 @PATHS
-@pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets", "tutorial3"])
+@pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets", "tutorial3", "rmw"])
 def test_gpu_matches_reference_golden(gpu_available, monkeypatch, name, path):
     monkeypatch.setenv("NFGPU_ABLATE", str(path))
     w = nfio.read(os.path.join(GOLDEN, f"{name}.workload.nfio"))
@@ -46,6 +46,8 @@ CASES = {
     # SetProperty on every property (program operands included), 20-property bursts per entity
     "wide_sets": dict(n_obj=5000, n_scenes=2, groups_per_scene=9, players_per_group=4, ext_frac=0.2,
                       ext_props="all", burst_frac=0.05, burst_props=20, host_ops=True),
+    "read_modify_write": dict(n_obj=3000, n_scenes=2, groups_per_scene=6, players_per_group=4, ext_frac=0.05,
+                              ext_props="all", rmw_frac=0.03, switch_frac=0.01, host_ops=True),
     "wide_sets_records": dict(n_obj=3000, n_scenes=2, groups_per_scene=5, players_per_group=6, records=True,
                               rec_rows=32, ext_frac=0.1, ext_props="all", burst_frac=0.02, burst_props=24,
                               switch_frac=0.01),
@@ -84,6 +86,46 @@ def test_gpu_full_size_config0_tutorial3(gpu_available):
     5 s x 10 "OnHeartBeat" fires twice or three times; OnEvent sets of "World" every frame)."""
     w = workload.tutorial3_world(n_ticks=120)
     compare_runs(run_gpu(w), run_oracle(w))
+
+
+def test_read_your_writes_and_exist_schedule(gpu_available):
+    """GetPropertyInt/Float see the window's queued Sets (KM:401 after KM:323) and
+    ExistSchedule(self, name) follows SM:276-285: RemoveSchedule(self) erases at once, AddSchedule
+    and RemoveSchedule(self, name) wait for Execute."""
+    w = workload.make_world(n_obj=300, n_scenes=1, groups_per_scene=3, players_per_group=2, n_ticks=2, seed=5,
+                            ext_frac=0.0, host_ops=False)
+    m = kernel.world_from_workload(w)
+    m.Execute(int(w["tick_time"][0]))
+    g0, g1 = (int(w["guid_head"][0]), int(w["guid_data"][0])), (int(w["guid_head"][1]), int(w["guid_data"][1]))
+    hp = m.GetPropertyInt(g0, "HP")
+    assert hp == int(m.read_prop(workload.PID["HP"])[0])
+    m.SetPropertyInt(g0, "HP", hp - 7)
+    assert m.GetPropertyInt(g0, "HP") == hp - 7
+    m.SetPropertyInt(g0, "HP", m.GetPropertyInt(g0, "HP") - 5)
+    assert m.GetPropertyInt(g0, "HP") == hp - 12
+    x = m.GetPropertyFloat(g0, "X")
+    m.SetPropertyFloat(g0, "X", x + 1e-16)   # |dv| <= 1e-15: SetFloat keeps the old value (PR:314)
+    assert m.GetPropertyFloat(g0, "X") == x
+    m.SetPropertyFloat(g0, "X", x + 0.5)
+    assert m.GetPropertyFloat(g0, "X") == x + 0.5
+    # many reads in one call (the gathered path) agree with the single reads
+    pids = [workload.PID[p] for p in ("HP", "MP", "Level", "Gold", "X", "Y", "TargetX", "AtkDis", "SceneID", "EXP")]
+    many = m.get_props([g0[0]] * len(pids), [g0[1]] * len(pids), pids)
+    one = np.concatenate([m.get_props([g0[0]], [g0[1]], [p]) for p in pids])
+    np.testing.assert_array_equal(many, one)
+    assert m.ExistSchedule(g1, "Move")
+    m.RemoveSchedule(g1, "Move")
+    assert m.ExistSchedule(g1, "Move")        # in the remove list until Execute
+    m.RemoveSchedule(g1)
+    assert not m.ExistSchedule(g1, "Move")    # erased at once
+    m.AddSchedule(g1, "Move", 0.1, -1, int(w["tick_time"][0]))
+    assert not m.ExistSchedule(g1, "Move")    # in the add list until Execute
+    m.Execute(int(w["tick_time"][1]))
+    assert m.ExistSchedule(g1, "Move") and not m.ExistSchedule(g1, "HPRegen")
+    assert m.GetPropertyInt(g0, "HP") == int(m.read_prop(workload.PID["HP"])[0])
+    with pytest.raises(kernel.NFKError):
+        m.GetPropertyInt((123, 456), "HP")
+    m.close()
 
 
 def test_gpu_full_size_config1(gpu_available):
@@ -174,16 +216,29 @@ def test_cpp_plugin_api_replay_matches_oracle(gpu_available, tmp_path):
         __graft_entry__.build_plugin()
     from noahgameframe_amd.shard import zrevrange_order
     w = workload.make_world(n_obj=3000, n_scenes=2, groups_per_scene=6, players_per_group=5, n_ticks=8, seed=31,
-                            ext_frac=0.05, host_ops=True, switch_frac=0.01, switch_new_groups=True)
-    assert len(w["sw_tick"]) > 0
+                            ext_frac=0.05, host_ops=True, switch_frac=0.01, switch_new_groups=True, rmw_frac=0.02,
+                            ext_props="all")
+    assert len(w["sw_tick"]) > 0 and w["x_mode"].sum() > 100
     wp, op = str(tmp_path / "w.nfio"), str(tmp_path / "o.nfio")
     nfio.write(wp, w)
     subprocess.run([exe, wp, op], check=True)
     got = nfio.read(op)
     ref = run_oracle(w)
+    # heartbeat functors run in NFCScheduleModule::Execute's order (SM:52-80: mObjectScheduleMap is
+    # keyed by NFGUID, each object's schedules by name); the oracle lists them in (scene, group,
+    # guid, kind) order: check the plugin's order, then compare in the oracle's
+    for t in range(int(w["cfg"][7])):
+        fo, fk = got[f"fi_t{t}_obj"], got[f"fi_t{t}_kind"]
+        key = np.lexsort((fk, w["guid_data"][fo], w["guid_head"][fo]))
+        assert np.array_equal(key, np.arange(len(fo))), f"frame {t}: functors not in NFGUID order"
+        o = np.lexsort((got[f"fi_t{t}_kind"], got[f"fi_t{t}_obj"]))
+        r = np.lexsort((ref[f"fi_t{t}_kind"], ref[f"fi_t{t}_obj"]))
+        for k in ("obj", "kind", "rem"):
+            got[f"fi_t{t}_{k}"] = got[f"fi_t{t}_{k}"][o]
+            ref[f"fi_t{t}_{k}"] = ref[f"fi_t{t}_{k}"][r]
     compare_runs({k: v for k, v in got.items() if not k.startswith("rank_")},
                  {k: v for k, v in ref.items() if k in got})
-    assert len(got) == 13 * 8 + 2 + 6
+    assert len(got) == 13 * 8 + 3 + 6   # per frame, final_i / final_f / final_s_present (ExistSchedule), ranks
     # GetRange (NFIRankRedisModule, ZREVRANGE 0..99) over the final oracle state
     n_int = w["cfg"][1]
     for p, final in ((0, ref["final_i"][0].astype(np.float64)), (n_int, ref["final_f"][0])):
