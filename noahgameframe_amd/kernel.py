@@ -397,13 +397,17 @@ def world_from_workload(w, capacity=None, msg_capacity=0, stream=None, slack_per
                         w["rec_flags"][:, r])
     for k in range(n_kind):
         m.define_kind(k, w["ops"][k][: int(w["n_ops"][k])])
-    m.create_objects(w["guid_head"], w["guid_data"], w["scene"], w["group"], w["cls"], w["is_player"])
+    # objects created before frame 0 (a workload's later objects, born[o] >= 0, are the last ones
+    # and enter through nfk_spawn_objects in their window: run_workload)
+    n0 = int(np.sum(w["born"] < 0)) if "born" in w else n_obj
+    m.create_objects(w["guid_head"][:n0], w["guid_data"][:n0], w["scene"][:n0], w["group"][:n0], w["cls"][:n0],
+                     w["is_player"][:n0])
     for p in range(n_int):
-        m.load_prop(p, w["init_i"][p])
+        m.load_prop(p, w["init_i"][p][:n0])
     for p in range(n_flt):
-        m.load_prop(n_int + p, w["init_f"][p])
+        m.load_prop(n_int + p, w["init_f"][p][:n0])
     for r in range(n_rec):
-        m.load_record(r, w[f"rec{r}_cells"], w[f"rec{r}_used"])
+        m.load_record(r, w[f"rec{r}_cells"][:n0], w[f"rec{r}_used"][:n0])
     m.commit()
     gh, gd = w["guid_head"], w["guid_data"]
     so = w["s_obj"]
@@ -412,9 +416,17 @@ def world_from_workload(w, capacity=None, msg_capacity=0, stream=None, slack_per
 
 
 def run_workload(m, w, tick, collect=True):
-    """Replay the between-frame calls of frame `tick` (SwitchScene first, then schedule calls,
-    then SetProperty calls, as the oracle does), then Execute it."""
+    """Replay the between-frame calls of frame `tick` in the oracle's window order — CreateObject
+    (nfk_spawn_objects), SwitchScene, schedule calls, SetProperty calls, DestroyObject — then
+    Execute it."""
     gh, gd = w["guid_head"], w["guid_data"]
+    if "born" in w:
+        new = np.nonzero(w["born"] == tick)[0]
+        if len(new):
+            props = np.concatenate([w["init_i"][:, new].astype(np.int64).view(np.uint64),
+                                    w["init_f"][:, new].astype(np.float64).view(np.uint64)]).T
+            m.spawn_objects(gh[new], gd[new], w["scene"][new], w["group"][new], w["cls"][new], w["is_player"][new],
+                            np.ascontiguousarray(props))
     if "sw_tick" in w:
         for i in np.nonzero(w["sw_tick"] == tick)[0]:
             o = int(w["sw_obj"][i])
@@ -449,5 +461,9 @@ def run_workload(m, w, tick, collect=True):
                 else:
                     v = (cur.view(np.float64) + d.view(np.float64)).view(np.uint64)
                 m.set_props([gh[o]], [gd[o]], [p], v)
+    if "d_tick" in w:
+        dead = w["d_obj"][w["d_tick"] == tick]
+        if len(dead):
+            m.destroy_objects(gh[dead], gd[dead])
     m.Execute(int(w["tick_time"][tick]))
     return m.read_tick() if collect else None

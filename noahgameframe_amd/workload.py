@@ -106,7 +106,9 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
                tick_ms=100, seed=1, ext_frac=0.05, host_ops=True, records=False, rec_rows=64,
                t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, rec_skill_op=False, sched_edges=False,
                switch_frac=0.0, switch_new_groups=False, rec_steady=False, ext_props=None, burst_frac=0.0,
-               burst_props=20, rmw_frac=0.0):
+               burst_props=20, rmw_frac=0.0, spawn_frac=0.0, destroy_frac=0.0):
+    if spawn_frac > 0 or destroy_frac > 0:
+        return _lifecycle_world(locals())
     rng = np.random.default_rng(seed)
     n_groups = n_scenes * groups_per_scene
     # ---- objects ----
@@ -381,6 +383,86 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
             used &= np.uint64((1 << rows) - 1)
         w["rec0_cells"] = cells
         w["rec0_used"] = used
+    return w
+
+
+def _lifecycle_world(kw):
+    """make_world with objects created and destroyed between frames (NFCKernelModule::CreateObject
+    after start, KM:101-271; DestroyObject, KM:273-308).  Every frame t >= 1, spawn_frac x n_obj new
+    objects are created (appended to the object arrays in call order, `born` = t; they get their
+    AddSchedule calls in the same window, after the creation) and destroy_frac x n_obj live objects
+    are destroyed (`d_tick`, `d_obj`, the window's last calls).  A window's calls run: creations,
+    SwitchScene, schedule calls, SetProperty calls, destructions.  Calls on an object before its
+    creation or after its destruction are dropped, and so are schedule and SwitchScene calls in its
+    destruction window (the reference would keep an AddSchedule queued for an object destroyed in
+    the same window as a schedule of a dead GUID)."""
+    kw = dict(kw)
+    spawn_frac, destroy_frac = kw.pop("spawn_frac"), kw.pop("destroy_frac")
+    n0, n_ticks, seed = kw["n_obj"], kw["n_ticks"], kw["seed"]
+    per = int(spawn_frac * n0)
+    n_new = per * max(n_ticks - 1, 0)
+    kw["n_obj"] = n0 + n_new
+    w = make_world(**kw, spawn_frac=0.0, destroy_frac=0.0)
+    rng = np.random.default_rng(seed + 991)
+    N = n0 + n_new
+    born = np.full(N, -1, np.int32)
+    for t in range(1, n_ticks):
+        born[n0 + (t - 1) * per: n0 + t * per] = t
+    # destructions: live objects (born before the window), each destroyed once
+    died = np.full(N, 1 << 30, np.int64)
+    dt, do = [], []
+    kd = int(destroy_frac * n0)
+    for t in range(1, n_ticks):
+        cand = np.nonzero((born < t) & (died > t))[0]
+        pick = rng.choice(cand, size=min(kd, len(cand)), replace=False) if kd and len(cand) else np.zeros(0, np.int64)
+        died[pick] = t
+        dt.append(np.full(len(pick), t))
+        do.append(np.sort(pick))
+    d_tick = np.concatenate(dt).astype(np.int32) if dt else np.zeros(0, np.int32)
+    d_obj = np.concatenate(do).astype(np.int32) if do else np.zeros(0, np.int32)
+
+    def alive_at(o, t, last_window_ok):
+        b = born[o]
+        ok = (b < 0) | (b <= t)
+        return ok & ((t < died[o]) | (last_window_ok & (t == died[o])))
+
+    # calls: SetProperty allowed in the destruction window (dropped with the object), schedule and
+    # SwitchScene calls not
+    keep = alive_at(w["x_obj"], w["x_tick"], True)
+    for k in ("x_tick", "x_obj", "x_pid", "x_bits", "x_mode"):
+        if k in w:
+            w[k] = w[k][keep]
+    keep = alive_at(w["h_obj"], w["h_tick"], False)
+    for k in ("h_tick", "h_op", "h_obj", "h_kind", "h_interval", "h_count", "h_time"):
+        w[k] = w[k][keep]
+    keep = alive_at(w["sw_obj"], w["sw_tick"], False)
+    for k in ("sw_tick", "sw_obj", "sw_scene", "sw_group", "sw_x", "sw_y", "sw_z"):
+        w[k] = w[k][keep]
+    # the late objects' AddSchedule calls move from before frame 0 to their creation window
+    late = born[w["s_obj"]] >= 0
+    s_late = {k: w[k][late] for k in ("s_obj", "s_kind", "s_interval", "s_count", "s_time")}
+    for k in ("s_obj", "s_kind", "s_interval", "s_count", "s_time"):
+        w[k] = w[k][~late]
+    bt = born[s_late["s_obj"]]
+    order = np.argsort(bt, kind="stable")
+    tt = w["tick_time"]
+    h_new = dict(h_tick=bt[order], h_op=np.ones(len(order), np.int32), h_obj=s_late["s_obj"][order],
+                 h_kind=s_late["s_kind"][order], h_interval=s_late["s_interval"][order],
+                 h_count=s_late["s_count"][order],
+                 h_time=(tt[np.maximum(bt[order] - 1, 0)] + (s_late["s_time"][order] - s_late["s_time"][order].min()) % 100
+                         ).astype(np.int64))
+    # the window's schedule calls: the creations' AddSchedule first, then the generator's
+    ht = np.concatenate([h_new["h_tick"], w["h_tick"]])
+    first = np.concatenate([np.zeros(len(order), np.int8), np.ones(len(w["h_tick"]), np.int8)])
+    o2 = np.lexsort((first, ht))
+    for k in h_new:
+        w[k] = np.concatenate([h_new[k], w[k]])[o2].astype(w[k].dtype)
+    w["cfg"][6] = len(w["s_obj"])
+    if int(w["cfg"][5]):   # late objects start with empty records
+        w["rec0_cells"][born >= 0] = 0
+        w["rec0_used"][born >= 0] = 0
+    w["born"] = born
+    w["d_tick"], w["d_obj"] = d_tick, d_obj
     return w
 
 

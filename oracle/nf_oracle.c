@@ -19,6 +19,12 @@
  *   add_schedule   NFComm/NFKernelPlugin/NFCScheduleModule.cpp:218-238
  *   switch_scene   NFComm/NFKernelPlugin/NFCKernelModule.cpp:901-951 (group leave/join, the
  *                  SceneID/GroupID/X/Y/Z writes in call order)
+ *   create_object  NFComm/NFKernelPlugin/NFCKernelModule.cpp:101-271 after start (the object
+ *                  joins its scene group with its creation-time values; no schedules until an
+ *                  AddSchedule; creation values are not dirty events)
+ *   destroy_object NFComm/NFKernelPlugin/NFCKernelModule.cpp:273-308 (RemoveObjectFromGroup,
+ *                  RemoveSchedule(self) which erases at once, NFCScheduleModule.cpp:240; the
+ *                  object's events of the window are dropped with it)
  *   fanout         NFComm/NFKernelPlugin/NFCSceneAOIModule.cpp:227-290 and 531-593
  *                  (GetBroadCastObject: public -> group players except self in NFGUID
  *                  order (NFCSceneGroupInfo::mxPlayerList, std::map), private&&!upload
@@ -76,6 +82,8 @@ static uint8_t *cls, *isplayer;
 static sched_t *S; /* [N][NK] */
 static int32_t *pend_rm_kind; /* [N], -2 = none, -1 = name not a kind */
 static int64_t *orank;         /* canonical (scene, group, guid) rank of each object */
+static uint8_t *alive;         /* created and not destroyed */
+static int64_t NLIVE;          /* live objects (the first NLIVE of sorted_objs) */
 
 static setlog_t *slog;
 static int64_t nslog, capslog, seq;
@@ -234,6 +242,7 @@ static void log_fired(int32_t obj, int32_t kind, int32_t rem) {
  * order does not change state (callbacks only touch their own object). */
 static void sched_execute(int64_t now) {
     for (int32_t o = 0; o < N; o++) {
+        if (!alive[o]) continue;
         /* mObjectRemoveList is std::map<NFGUID, name>: a RemoveSchedule(self, name)
          * queued before this Execute owns the key, later inserts for self fail. */
         int taken = pend_rm_kind[o] != -2;
@@ -299,12 +308,15 @@ static int64_t* seg_end_of_obj;
 
 /* canonical (scene, group, guid) order and each object's segment; rebuilt after SwitchScene */
 static void build_order(void) {
-    for (int32_t o = 0; o < N; o++) sorted_objs[o] = o;
-    qsort(sorted_objs, N, 4, cmp_obj_key);
-    for (int64_t i = 0; i < N; i++) orank[sorted_objs[i]] = i;
-    for (int64_t i = 0; i < N;) {
+    NLIVE = 0;
+    for (int32_t o = 0; o < N; o++)
+        if (alive[o]) sorted_objs[NLIVE++] = o;
+    qsort(sorted_objs, NLIVE, 4, cmp_obj_key);
+    for (int64_t o = 0; o < N; o++) orank[o] = -1;
+    for (int64_t i = 0; i < NLIVE; i++) orank[sorted_objs[i]] = i;
+    for (int64_t i = 0; i < NLIVE;) {
         int64_t j = i;
-        while (j < N && scene[sorted_objs[j]] == scene[sorted_objs[i]] && group[sorted_objs[j]] == group[sorted_objs[i]]) j++;
+        while (j < NLIVE && scene[sorted_objs[j]] == scene[sorted_objs[i]] && group[sorted_objs[j]] == group[sorted_objs[i]]) j++;
         for (int64_t k = i; k < j; k++) {
             seg_begin_of_obj[sorted_objs[k]] = i;
             seg_end_of_obj[sorted_objs[k]] = j;
@@ -388,6 +400,18 @@ int main(int argc, char** argv) {
     pend_rm_kind = (int32_t*)malloc(N * 4);
     for (int64_t o = 0; o < N; o++) pend_rm_kind[o] = -2;
 
+    /* objects created after start (optional: born[o] = the frame whose window creates it, -1 =
+     * before frame 0) and destroyed between frames (optional d_tick / d_obj, in call order) */
+    nfio_arr* ba = nfio_get(&wf, "born");
+    int32_t* born = ba ? (int32_t*)ba->data : NULL;
+    nfio_arr* dta = nfio_get(&wf, "d_tick");
+    int64_t ND = dta ? (int64_t)dta->shape[0] : 0;
+    int32_t* d_tick = ND ? (int32_t*)dta->data : NULL;
+    int32_t* d_obj = ND ? (int32_t*)GET("d_obj")->data : NULL;
+    int64_t di = 0;
+    alive = (uint8_t*)malloc(N);
+    for (int64_t o = 0; o < N; o++) alive[o] = born ? born[o] < 0 : 1;
+
     /* canonical rank */
     sorted_objs = (int32_t*)malloc(N * 4);
     orank = (int64_t*)malloc(N * 8);
@@ -440,6 +464,15 @@ int main(int argc, char** argv) {
          * [GroupID = 0, SceneID = target when the scene changes], X/Y/Z = (double)float,
          * GroupID = target, join the target group.  sw_scene < 0: the object's own cell. */
         int relayout = 0;
+        /* CreateObject (KM:101-271) of this window's new objects, made first in the window */
+        if (born)
+            for (int64_t o = 0; o < N; o++)
+                if (born[o] == t) {
+                    alive[o] = 1;
+                    relayout = 1;
+                }
+        if (relayout) build_order();
+        relayout = 0;
         while (swi < NSW && sw_tick[swi] == t) {
             int32_t o = sw_obj[swi];
             int32_t ns = sw_scene[swi] < 0 ? scene[o] : sw_scene[swi];
@@ -478,10 +511,34 @@ int main(int argc, char** argv) {
          * reads the current value first (NFCKernelModule::GetPropertyInt/Float, KM:401-425) */
         while (xi < NX && x_tick[xi] == t) {
             int32_t pid = x_pid[xi], o = x_obj[xi];
+            if (!alive[o]) {  /* "There is no object" (KM:331) */
+                xi++;
+                continue;
+            }
             const int rmw = x_mode && x_mode[xi];
             if (pid < NI) set_int(o, pid, rmw ? (int64_t)((uint64_t)iget(o, pid) + x_bits[xi]) : (int64_t)x_bits[xi]);
             else set_flt(o, pid, rmw ? fget(o, pid) + bitsd(x_bits[xi]) : bitsd(x_bits[xi]));
             xi++;
+        }
+        /* DestroyObject (KM:273-308), the window's last calls: the object leaves its group,
+         * RemoveSchedule(self) erases its schedules at once (SM:240), and its events of this
+         * window go with it */
+        {
+            int destroyed = 0;
+            while (di < ND && d_tick[di] == t) {
+                int32_t o = d_obj[di++];
+                alive[o] = 0;
+                pend_rm_kind[o] = -2;
+                for (int k = 0; k < NK; k++) memset(&S[(int64_t)o * NK + k], 0, sizeof(sched_t));
+                destroyed = 1;
+            }
+            if (destroyed) {
+                int64_t k = 0;
+                for (int64_t i = 0; i < nslog; i++)
+                    if (alive[slog[i].obj]) slog[k++] = slog[i];
+                nslog = k;
+                build_order();
+            }
         }
         sched_execute(now);
         /* remove list (SM:83-98) */
@@ -497,7 +554,7 @@ int main(int argc, char** argv) {
         /* add list (SM:100-119): AddSchedule(SM:218) fields; an existing name wins */
         for (int64_t i = 0; i < nadds; i++) {
             sched_t* s = &S[(int64_t)adds[i].obj * NK + adds[i].kind];
-            if (s->present) continue;
+            if (s->present || !alive[adds[i].obj]) continue;
             memset(s, 0, sizeof *s);
             s->present = 1;
             s->interval = adds[i].interval;
@@ -608,7 +665,14 @@ int main(int argc, char** argv) {
         free(fl); free(fo); free(fk); free(fr); free(moff); free(mr);
     }
 
-    /* final state */
+    /* final state (objects no longer in the world read 0) */
+    for (int64_t o = 0; o < N; o++) {
+        if (alive[o]) continue;
+        for (int64_t p = 0; p < NI; p++) I[p * N + o] = 0;
+        for (int64_t p = 0; p < NF; p++) F[p * N + o] = 0.0;
+        for (int r = 0; r < NR; r++) memset(cell(r, (int32_t)o, 0, 0), 0, (size_t)rec_cols[r] * rec_rows[r] * 8);
+        for (int k = 0; k < NK; k++) S[o * NK + k].present = 0;
+    }
     {
         uint64_t sh[2] = {(uint64_t)NI, (uint64_t)N};
         nfio_put(&w, "final_i", NFIO_I64, 2, sh, I, NI * N * 8);

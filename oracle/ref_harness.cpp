@@ -84,7 +84,7 @@ struct World {
     std::vector<NF_SHARE_PTR<NFIPropertyManager>> class_pm;  // class templates carry the flags
     std::vector<uint8_t> rflags;  // [NC][NR]
     std::vector<int32_t> scene, group;
-    std::vector<uint8_t> cls, isplayer;
+    std::vector<uint8_t> cls, isplayer, alive;
     std::map<int, NF_SHARE_PTR<NFCSceneInfo>> scenes;
     nfk_op ops[NFK_MAX_KINDS][NFK_MAX_OPS];
     int32_t nops[NFK_MAX_KINDS];
@@ -383,11 +383,18 @@ int main(int argc, char** argv) {
     W.cls.assign(cl, cl + W.N);
     W.isplayer.assign(ip, ip + W.N);
 
-    // objects: NFCKernelModule::CreateObject (KM:101-271) property part + scene group maps
-    for (int64_t o = 0; o < W.N; o++) {
-        NFGUID id(gh[o], gd[o]);
-        W.id.push_back(id);
+    // objects: NFCKernelModule::CreateObject (KM:101-271) property part + scene group maps; an
+    // object with born[o] >= 0 is created in frame born[o]'s window (CreateObject after start)
+    nfio_arr* ba = nfio_get(&wf, "born");
+    int32_t* born = ba ? (int32_t*)ba->data : nullptr;
+    W.alive.assign(W.N, 0);
+    W.pm.resize(W.N);
+    W.rec.resize(W.N);
+    for (int64_t o = 0; o < W.N; o++) W.id.push_back(NFGUID(gh[o], gd[o]));
+    auto create = [&](int64_t o) {
+        const NFGUID id = W.id[o];
         W.obj_of[id] = (int)o;
+        W.alive[o] = 1;
         NF_SHARE_PTR<NFIPropertyManager> pm(new NFCPropertyManager(id));
         for (int p = 0; p < NP; p++) {
             auto tmpl = W.class_pm[W.cls[o]]->GetElement(W.pname[p]);
@@ -403,7 +410,7 @@ int main(int argc, char** argv) {
                     return OnPropertyEvent(obj, pid, a, b);
                 })));
         }
-        W.pm.push_back(pm);
+        W.pm[o] = pm;
         std::vector<NF_SHARE_PTR<NFIRecord>> recs;
         for (int r = 0; r < W.NR; r++) {
             NF_SHARE_PTR<NFIDataList> types(new NFCDataList());
@@ -431,14 +438,21 @@ int main(int argc, char** argv) {
                 })));
             recs.push_back(R);
         }
-        W.rec.push_back(recs);
+        W.rec[o] = recs;
         // NFCSceneInfo::AddObjectToGroup (NFISceneAOIModule.h) — the group's player / other maps
         auto& si = W.scenes[W.scene[o]];
         if (!si) si = NF_SHARE_PTR<NFCSceneInfo>(new NFCSceneInfo(W.scene[o]));
         if (!si->GetElement(W.group[o]))
             si->AddElement(W.group[o], NF_SHARE_PTR<NFCSceneGroupInfo>(new NFCSceneGroupInfo(W.scene[o], W.group[o])));
         si->AddObjectToGroup(W.group[o], id, W.isplayer[o] != 0);
-    }
+    };
+    for (int64_t o = 0; o < W.N; o++)
+        if (!born || born[o] < 0) create(o);
+    nfio_arr* dta = nfio_get(&wf, "d_tick");
+    const int64_t ND = dta ? (int64_t)dta->shape[0] : 0;
+    int32_t* d_tick = ND ? (int32_t*)dta->data : nullptr;
+    int32_t* d_obj = ND ? (int32_t*)GET(wf, "d_obj")->data : nullptr;
+    int64_t di = 0;
 
     SchedProbe sched(nullptr);
     auto hb = OBJECT_SCHEDULE_FUNCTOR_PTR(new OBJECT_SCHEDULE_FUNCTOR(OnHeartBeat));
@@ -470,17 +484,21 @@ int main(int argc, char** argv) {
     int32_t* h_count = (int32_t*)GET(wf, "h_count")->data;
     int64_t* h_time = (int64_t*)GET(wf, "h_time")->data;
 
-    // canonical rank (scene, group, guid); recomputed after SwitchScene
-    std::vector<int32_t> sorted(W.N);
+    // canonical rank (scene, group, guid) of the live objects; recomputed after SwitchScene,
+    // CreateObject and DestroyObject
+    std::vector<int32_t> sorted;
     std::vector<int64_t> orank(W.N);
     auto build_order = [&]() {
-        for (int64_t i = 0; i < W.N; i++) sorted[i] = (int32_t)i;
+        sorted.clear();
+        for (int64_t i = 0; i < W.N; i++)
+            if (W.alive[i]) sorted.push_back((int32_t)i);
         std::sort(sorted.begin(), sorted.end(), [](int32_t a, int32_t b) {
             if (W.scene[a] != W.scene[b]) return W.scene[a] < W.scene[b];
             if (W.group[a] != W.group[b]) return W.group[a] < W.group[b];
             return W.id[a] < W.id[b];
         });
-        for (int64_t i = 0; i < W.N; i++) orank[sorted[i]] = i;
+        for (int64_t i = 0; i < W.N; i++) orank[i] = -1;
+        for (size_t i = 0; i < sorted.size(); i++) orank[sorted[i]] = (int64_t)i;
     };
     build_order();
 
@@ -519,6 +537,13 @@ int main(int argc, char** argv) {
         // group maps and property manager; made first in the window.  The target group is
         // created on demand (NFCKernelModule::RequestGroupScene).
         bool relayout = false;
+        // CreateObject after start (KM:101-271), the window's first calls
+        if (born)
+            for (int64_t o = 0; o < W.N; o++)
+                if (born[o] == t) {
+                    create(o);
+                    relayout = true;
+                }
         while (swi < NSW && sw_tick[swi] == t) {
             const int32_t o = sw_obj[swi];
             const NFGUID self = W.id[o];
@@ -564,6 +589,26 @@ int main(int argc, char** argv) {
             else
                 SetFloat(self, x_pid[xi], rmw ? GetFloat(self, x_pid[xi]) + bitsd(x_bits[xi]) : bitsd(x_bits[xi]));
             xi++;
+        }
+        // DestroyObject (KM:273-308), the window's last calls: RemoveObjectFromGroup, then the
+        // reference scheduler's RemoveSchedule(self) (SM:240); the object's events go with it
+        {
+            bool destroyed = false;
+            while (di < ND && d_tick[di] == t) {
+                const int32_t o = d_obj[di++];
+                W.scenes[W.scene[o]]->RemoveObjectFromGroup(W.group[o], W.id[o], W.isplayer[o] != 0);
+                sched.RemoveSchedule(W.id[o]);
+                W.obj_of.erase(W.id[o]);
+                W.alive[o] = 0;
+                destroyed = true;
+            }
+            if (destroyed) {
+                W.slog.erase(std::remove_if(W.slog.begin(), W.slog.end(), [](const SetEv& e) { return !W.alive[e.obj]; }),
+                             W.slog.end());
+                W.rlog.erase(std::remove_if(W.rlog.begin(), W.rlog.end(), [](const RSetEv& e) { return !W.alive[e.obj]; }),
+                             W.rlog.end());
+                build_order();
+            }
         }
         g_now_ms = tick_time[t];
         sched.Execute();
@@ -653,6 +698,7 @@ int main(int argc, char** argv) {
     std::vector<int64_t> fi(W.NI * W.N);
     std::vector<double> ff(W.NF * W.N);
     for (int64_t o = 0; o < W.N; o++) {
+        if (!W.alive[o]) continue;  // objects no longer in the world read 0
         for (int p = 0; p < W.NI; p++) fi[p * W.N + o] = W.pm[o]->GetPropertyInt(W.pname[p]);
         for (int p = 0; p < W.NF; p++) ff[p * W.N + o] = W.pm[o]->GetPropertyFloat(W.pname[W.NI + p]);
     }
@@ -663,7 +709,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < W.NR; r++) {
         std::vector<uint64_t> cells((size_t)W.N * W.rec_cols[r] * W.rec_rows[r]);
         for (int64_t o = 0; o < W.N; o++)
-            for (int c = 0; c < W.rec_cols[r]; c++)
+            for (int c = 0; c < W.rec_cols[r] && W.alive[o]; c++)
                 for (int row = 0; row < W.rec_rows[r]; row++) {
                     auto& R = W.rec[o][r];
                     uint64_t b = rcells[r][((int64_t)o * W.rec_cols[r] + c) * W.rec_rows[r] + row];

@@ -79,7 +79,10 @@ int main(int argc, char** argv) {
     uint8_t* cl = (uint8_t*)A("cls")->data;
     int64_t* ii = (int64_t*)A("init_i")->data;
     double* ff = (double*)A("init_f")->data;
-    for (int64_t o = 0; o < N; o++) {
+    // objects with born[o] >= 0 are created in frame born[o]'s window (CreateObject after start)
+    nfio_arr* ba = nfio_get(&wf, "born");
+    int32_t* born = ba ? (int32_t*)ba->data : nullptr;
+    auto create = [&](int64_t o) {
         km.CreateScene(sc[o]);
         std::map<std::string, TData> init;
         for (int p = 0; p < NP; p++) {
@@ -89,8 +92,14 @@ int main(int argc, char** argv) {
             else t.f = ff[(p - NI) * N + o];
             init[pname[p]] = t;
         }
-        if (!km.CreateObject(NFGUID(gh[o], gd[o]), sc[o], gr[o], cname[cl[o]], init)) return 3;
-    }
+        return km.CreateObject(NFGUID(gh[o], gd[o]), sc[o], gr[o], cname[cl[o]], init);
+    };
+    for (int64_t o = 0; o < N; o++)
+        if ((!born || born[o] < 0) && !create(o)) return 3;
+    nfio_arr* dta = nfio_get(&wf, "d_tick");
+    const int64_t ND = dta ? (int64_t)dta->shape[0] : 0;
+    int32_t* d_tick = ND ? (int32_t*)dta->data : nullptr;
+    int32_t* d_obj = ND ? (int32_t*)A("d_obj")->data : nullptr;
     km.AfterInit();
     for (int r = 0; r < NR; r++) {  // record contents: creation-time rows through the C-ABI
         char nm[32];
@@ -194,11 +203,14 @@ int main(int argc, char** argv) {
 
     nfio_writer w;
     if (nfio_wopen(&w, argv[2])) return 2;
-    int64_t xi = 0, hi = 0, wi = 0;
+    int64_t xi = 0, hi = 0, wi = 0, di = 0;
     for (int t = 0; t < NT; t++) {
         ev_obj.clear(); ev_pid.clear(); ev_old.clear(); ev_new.clear();
         re_obj.clear(); re_rrc.clear(); re_old.clear(); re_new.clear();
         fi_obj.clear(); fi_kind.clear(); fi_rem.clear(); mr.clear(); moff.clear();
+        if (born)  // CreateObject after AfterInit: the entity enters at the next Execute
+            for (int64_t o = 0; o < N; o++)
+                if (born[o] == t && !create(o)) return 8;
         for (; wi < NW && sw_tick[wi] == t; wi++) {
             const int o = sw_obj[wi];
             if (sw_scene[wi] >= 0) { cur_sc[o] = sw_scene[wi]; cur_gr[o] = sw_group[wi]; }
@@ -224,6 +236,8 @@ int main(int argc, char** argv) {
                 km.SetPropertyFloat(g, pn, rmw ? km.GetPropertyFloat(g, pn) + v : v);
             }
         }
+        for (; di < ND && d_tick[di] == t; di++)  // DestroyObject (KM:273-308), the window's last calls
+            if (!km.DestroyObject(NFGUID(gh[d_obj[di]], gd[d_obj[di]]))) return 9;
         g_now = tick_time[t];
         km.Execute();
         moff.push_back((uint32_t)mr.size());

@@ -34,6 +34,11 @@ FIXTURES = {
     # (entity, property) in one window, so the second Get must see the first Set (KM:401 after KM:323)
     "rmw": dict(n_obj=500, n_scenes=2, groups_per_scene=4, players_per_group=3, n_ticks=8, seed=707,
                 ext_frac=0.05, ext_props="all", rmw_frac=0.06, host_ops=True, switch_frac=0.02),
+    # CreateObject after start (KM:101-271) and DestroyObject (KM:273-308) between frames, with
+    # SwitchScene, read-modify-write Sets and schedule calls around them; int record column
+    "lifecycle": dict(n_obj=600, n_scenes=2, groups_per_scene=4, players_per_group=3, n_ticks=8, seed=808,
+                      ext_frac=0.05, host_ops=True, switch_frac=0.02, rmw_frac=0.02, spawn_frac=0.03,
+                      destroy_frac=0.03, records=True, rec_rows=12, rec_float_op=False),
 }
 
 

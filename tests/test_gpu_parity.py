@@ -19,7 +19,8 @@ PATHS = pytest.mark.parametrize("path", [0, 8], ids=["k_tick", "k_tick_touch"])
 
 
 @PATHS
-@pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets", "tutorial3", "rmw"])
+@pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets", "tutorial3", "rmw",
+                                  "lifecycle"])
 def test_gpu_matches_reference_golden(gpu_available, monkeypatch, name, path):
     monkeypatch.setenv("NFGPU_ABLATE", str(path))
     w = nfio.read(os.path.join(GOLDEN, f"{name}.workload.nfio"))
@@ -46,6 +47,11 @@ CASES = {
     # SetProperty on every property (program operands included), 20-property bursts per entity
     "wide_sets": dict(n_obj=5000, n_scenes=2, groups_per_scene=9, players_per_group=4, ext_frac=0.2,
                       ext_props="all", burst_frac=0.05, burst_props=20, host_ops=True),
+    # CreateObject after start / DestroyObject between frames (nfk_spawn_objects / nfk_destroy_objects)
+    "lifecycle": dict(n_obj=4000, n_scenes=3, groups_per_scene=5, players_per_group=4, ext_frac=0.05,
+                      switch_frac=0.01, rmw_frac=0.01, spawn_frac=0.02, destroy_frac=0.02, host_ops=True),
+    "lifecycle_records": dict(n_obj=2500, n_scenes=2, groups_per_scene=4, players_per_group=5, records=True,
+                              rec_rows=32, spawn_frac=0.03, destroy_frac=0.03, switch_frac=0.01),
     "read_modify_write": dict(n_obj=3000, n_scenes=2, groups_per_scene=6, players_per_group=4, ext_frac=0.05,
                               ext_props="all", rmw_frac=0.03, switch_frac=0.01, host_ops=True),
     "wide_sets_records": dict(n_obj=3000, n_scenes=2, groups_per_scene=5, players_per_group=6, records=True,
@@ -86,6 +92,56 @@ def test_gpu_full_size_config0_tutorial3(gpu_available):
     5 s x 10 "OnHeartBeat" fires twice or three times; OnEvent sets of "World" every frame)."""
     w = workload.tutorial3_world(n_ticks=120)
     compare_runs(run_gpu(w), run_oracle(w))
+
+
+@pytest.mark.parametrize("slack", [-1, 64])
+def test_cpp_plugin_replay_create_destroy(gpu_available, tmp_path, slack):
+    """CreateObject after AfterInit and DestroyObject through the C++ plugin, SwitchScene and
+    read-modify-write Sets around them, against the oracle (KM:101-308)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "_bin", "plugin_replay")
+    w = workload.make_world(n_obj=2000, n_scenes=2, groups_per_scene=4, players_per_group=4, n_ticks=6, seed=41 + slack,
+                            ext_frac=0.03, host_ops=True, switch_frac=0.01, rmw_frac=0.01, spawn_frac=0.03,
+                            destroy_frac=0.03)
+    wp, op = str(tmp_path / "w.nfio"), str(tmp_path / "o.nfio")
+    nfio.write(wp, w)
+    subprocess.run([exe, wp, op], check=True)
+    got, ref = nfio.read(op), run_oracle(w)
+    for t in range(6):   # functors in NFGUID order (see test_cpp_plugin_api_replay_matches_oracle)
+        o = np.lexsort((got[f"fi_t{t}_kind"], got[f"fi_t{t}_obj"]))
+        r = np.lexsort((ref[f"fi_t{t}_kind"], ref[f"fi_t{t}_obj"]))
+        for k in ("obj", "kind", "rem"):
+            got[f"fi_t{t}_{k}"], ref[f"fi_t{t}_{k}"] = got[f"fi_t{t}_{k}"][o], ref[f"fi_t{t}_{k}"][r]
+    compare_runs({k: v for k, v in got.items() if not k.startswith("rank_")}, {k: v for k, v in ref.items() if k in got})
+
+
+def test_membership_failure_keeps_window_queued(gpu_available):
+    """A frame whose membership changes do not fit (here: a scene group of more than 16383
+    players) fails without applying anything (nfgpu_host.hip apply_membership); the window's calls
+    stay queued, and once a later call makes them fit, Execute applies all of them."""
+    n = 20000
+    w = workload.make_world(n_obj=n, n_scenes=1, groups_per_scene=2, players_per_group=9000, n_ticks=2, seed=3,
+                            ext_frac=0.0, host_ops=False)
+    m = kernel.world_from_workload(w, slack_per_256=-1)
+    m.Execute(int(w["tick_time"][0]))
+    gh, gd, grp, pl = w["guid_head"], w["guid_data"], w["group"], w["is_player"]
+    movers = np.nonzero((grp == 2) & (pl == 1))[0][:8000]          # 9000 + 8000 players > 16383
+    hp0 = m.read_prop(workload.PID["HP"]).copy()
+    for o in movers:
+        m.SwitchScene((int(gh[o]), int(gd[o])), 1, 1, 0.0, 0.0, 0.0)
+    m.SetPropertyInt((int(gh[0]), int(gd[0])), "HP", 77)
+    with pytest.raises(kernel.NFKError):
+        m.Execute(int(w["tick_time"][1]))
+    np.testing.assert_array_equal(m.read_prop(workload.PID["HP"]), hp0)   # nothing applied
+    for o in movers[:2000]:                                          # back: 15000 players, fits
+        m.SwitchScene((int(gh[o]), int(gd[o])), 1, 2, 0.0, 0.0, 0.0)
+    m.Execute(int(w["tick_time"][1]))
+    gid = m.read_prop(workload.PID["GroupID"])
+    assert np.all(gid[movers[2000:]] == 1) and np.all(gid[movers[:2000]] == 2)
+    assert m.read_prop(workload.PID["HP"])[0] == 77
+    s = m.summary()
+    assert s["n_entities"] == n
+    m.close()
 
 
 def test_read_your_writes_and_exist_schedule(gpu_available):
