@@ -272,6 +272,20 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj);
 int nfk_rank_top(void* world, int32_t pid, int32_t k, int32_t* n_out, int64_t* guid_head, int64_t* guid_data,
                  double* score);
 
+/* ---- schema specialisation ----
+ * At nfk_commit k_tick is compiled for the world's schema (its heartbeat programs as straight-line
+ * code, its working set and event tables as constants) with hipRTC for gfx950, from the same
+ * device source as the library's generic k_tick; the results are bit-identical.  NFGPU_JIT=0 (or
+ * a failed compile) keeps the generic kernel. */
+/* whether this world's frames run the specialised k_tick; msg: its kernel name or why not */
+int nfk_jit_status(void* world, int32_t* on, char* msg, int32_t cap);
+/* the specialisation for a schema without a world or a GPU: the generated policy source, and with
+ * compile != 0 the hipRTC build for gfx950 (*ok = 1 on success, msg = the compiler log) */
+int nfk_jit_preview(int32_t n_int, int32_t n_flt, int32_t n_class, int32_t n_kind,
+                    const uint8_t* prop_flags /* [n_class][n_int + n_flt] */,
+                    const nfk_op* ops /* [n_kind][NFK_MAX_OPS] */, const int32_t* n_ops /* [n_kind] */,
+                    int32_t compile, int32_t* ok, char* src, int32_t src_cap, char* msg, int32_t msg_cap);
+
 /* ---- measurement ---- */
 int nfk_set_profiling(void* world, int32_t on);
 /* accumulated device time (ms), launch count and algorithmic bytes per kernel:

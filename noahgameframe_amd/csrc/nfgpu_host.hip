@@ -7,10 +7,14 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
+#include <mutex>
+
+#include "nfgpu_jit.hpp"
 #include "nfgpu_kernels.hip"
 
 using namespace nfgpu;
@@ -233,6 +237,11 @@ struct World {
     bool pin_pending = false;
     void* stage = nullptr;
     size_t stage_cap = 0;
+
+    // k_tick specialised to this world's schema (nfgpu_jit.hpp); null: the generic instantiations
+    hipFunction_t jit_fn = nullptr;
+    int jit_waves = 0, jit_u = 0;
+    std::string jit_msg = "not compiled";
 
     int32_t ticks = 0;
     uint32_t last_tcap = 0;  // Dev::msg_tcap of the last launched frame
@@ -540,24 +549,94 @@ int grow_event_tiles(World* w, int64_t per_tile) {
     return NFK_OK;
 }
 
-// the programs' working set (Dev::u_*): writable slots = program destinations in property-id
-// order, then the properties programs only read; event order and fan-out classes of the writable
-// slots, all read by k_tick as scalars
-void set_working_set(World* w) {
-    Dev& d = w->d;
-    const int n_w = (int)w->u_wp.size(), n_r = (int)w->u_rp.size();
+// The programs' working set: program destinations -> writable U slots [0, n_w) and the operands
+// programs only read -> slots [n_w, n_u), each group in property-id order; the tables name
+// read-only operand r as 0x80 | r.  Fills the kinds' U-slot tables (opu, umask, opx, w_slot);
+// false when the set does not fit k_tick's register slots (k_tick_touch runs instead).
+bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>& rp) {
+    bool u_ok = false;
+    {
+        std::vector<int> W, R;
+        for (int k = 0; k < NK; k++)
+            for (int i = 0; i < tab.nops[k]; i++) {
+                const nfk_op& op = tab.ops[k][i];
+                if (op.code == NFK_OP_IADD_CLAMP || op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE)
+                    W.push_back(op.dst);
+            }
+        std::sort(W.begin(), W.end());
+        W.erase(std::unique(W.begin(), W.end()), W.end());
+        auto is_w = [&](int64_t p) { return std::binary_search(W.begin(), W.end(), (int)p); };
+        for (int k = 0; k < NK; k++)
+            for (int i = 0; i < tab.nops[k]; i++) {
+                const nfk_op& op = tab.ops[k][i];
+                if (op.code == NFK_OP_IADD_CLAMP) {
+                    if ((op.flags & NFK_A_PROP) && !is_w(op.a)) R.push_back((int)op.a);
+                    if ((op.flags & NFK_LO_PROP) && !is_w(op.b)) R.push_back((int)op.b);
+                    if ((op.flags & NFK_HI_PROP) && !is_w(op.c)) R.push_back((int)op.c);
+                } else if (op.code == NFK_OP_FLERP && !is_w(op.a)) {
+                    R.push_back((int)op.a);
+                }
+            }
+        std::sort(R.begin(), R.end());
+        R.erase(std::unique(R.begin(), R.end()), R.end());
+        u_ok = (int)W.size() <= kMaxW && (int)(W.size() + R.size()) <= kMaxU;
+        wp.assign(W.begin(), W.end());
+        rp.assign(R.begin(), R.end());
+        memset(tab.w_slot, kNoU, sizeof tab.w_slot);
+        for (size_t i = 0; i < W.size() && i < (size_t)kMaxW; i++) tab.w_slot[W[i]] = (uint8_t)i;
+        auto slot = [&](int64_t p) -> uint8_t {
+            auto it = std::lower_bound(W.begin(), W.end(), (int)p);
+            if (it != W.end() && *it == p) return (uint8_t)(it - W.begin());
+            it = std::lower_bound(R.begin(), R.end(), (int)p);
+            return (uint8_t)(0x80 | (it - R.begin()));
+        };
+        for (int k = 0; k < NK && u_ok; k++) {
+            tab.umask[k] = 0;
+            for (int i = 0; i < tab.nops[k]; i++) {
+                const nfk_op& op = tab.ops[k][i];
+                uint8_t* u = tab.opu[k][i];
+                u[0] = u[1] = u[2] = u[3] = kNoU;
+                if (op.code == NFK_OP_IADD_CLAMP) {
+                    u[0] = slot(op.dst);
+                    if (op.flags & NFK_A_PROP) u[1] = slot(op.a);
+                    if (op.flags & NFK_LO_PROP) u[2] = slot(op.b);
+                    if (op.flags & NFK_HI_PROP) u[3] = slot(op.c);
+                } else if (op.code == NFK_OP_FLERP) {
+                    u[0] = slot(op.dst);
+                    u[1] = slot(op.a);
+                } else if (op.code == NFK_OP_FAFFINE) {
+                    u[0] = slot(op.dst);
+                }
+                for (int q = 0; q < 4; q++)  // writable bits | read-only bits << 16
+                    if (u[q] != kNoU) tab.umask[k] |= (u[q] & 0x80) ? 1u << (16 + (u[q] & 0x7F)) : 1u << u[q];
+                OpX& x = tab.opx[k][i];
+                x.cfd = (uint32_t)op.code | ((uint32_t)op.flags << 8) | ((uint32_t)op.dst << 16);
+                x.slots = (uint32_t)u[0] | ((uint32_t)u[1] << 8) | ((uint32_t)u[2] << 16) | ((uint32_t)u[3] << 24);
+                x.a = op.a;
+                x.b = op.b;
+                x.c = op.c;
+            }
+        }
+    }
+    return u_ok;
+}
+
+// Dev::u_* from the working set: slot properties, event order and fan-out classes of the
+// writable slots (all read by k_tick as scalars); columns only once the world has property memory
+void fill_u_dev(Dev& d, const Tables& tab, const std::vector<int>& wp, const std::vector<int>& rp, bool u_ok) {
+    const int n_w = (int)wp.size(), n_r = (int)rp.size();
     for (int j = 0; j < kMaxU; j++) d.u_pid[j] = -1;
     d.n_w = d.n_u = 0;
-    if (!w->u_ok) return;
-    for (int i = 0; i < n_w; i++) d.u_pid[i] = w->u_wp[i];
-    for (int i = 0; i < n_r; i++) d.u_pid[n_w + i] = w->u_rp[i];
+    if (!u_ok) return;
+    for (int i = 0; i < n_w; i++) d.u_pid[i] = wp[i];
+    for (int i = 0; i < n_r; i++) d.u_pid[n_w + i] = rp[i];
     d.n_w = n_w;
     d.n_u = n_w + n_r;
-    for (int i = 0; i < kMaxW; i++) d.u_order[i] = i < n_w ? i : 0;  // (u_wp is in property-id order)
+    for (int i = 0; i < kMaxW; i++) d.u_order[i] = i < n_w ? i : 0;  // (wp is in property-id order)
     for (int j = 0; j < kMaxU; j++) {
         const int p = d.u_pid[j];
-        d.u_col[j] = p < 0 ? nullptr : d.pmem + w->tab.p_off[p];
-        d.u_str[j] = p < 0 ? 0 : w->tab.p_str[p];
+        d.u_col[j] = (p < 0 || !d.pmem) ? nullptr : d.pmem + tab.p_off[p];
+        d.u_str[j] = p < 0 ? 0 : tab.p_str[p];
     }
     for (int j = 0; j < kMaxW; j++) {
         d.u_lower[j] = 0;
@@ -567,12 +646,64 @@ void set_working_set(World* w) {
     for (int c = 0; c < NFK_MAX_CLASSES; c++) {
         uint32_t pub = 0, priv = 0;
         for (int j = 0; j < n_w && c != 15; j++) {  // (class 15 marks a free slot)
-            const uint8_t f = w->tab.pflags[c][d.u_pid[j]];
+            const uint8_t f = tab.pflags[c][d.u_pid[j]];
             if (f & NFK_PUBLIC) pub |= 1u << j;
             else if ((f & NFK_PRIVATE) && !(f & NFK_UPLOAD)) priv |= 1u << j;
         }
         d.u_cmask[c] = pub | (priv << 16);
     }
+}
+
+void set_working_set(World* w) { fill_u_dev(w->d, w->tab, w->u_wp, w->u_rp, w->u_ok); }
+
+// waves per SIMD k_tick's register budget aims at, by the working set's size
+int tick_waves(int n_u, uint32_t ablate) {
+    if (ablate & kAblWaves6) return 6;
+    if (n_u <= 8) return kWavesU8;
+    if (n_u <= 12) return (ablate & kAblWaves8) ? 8 : kWavesU12;
+    return 6;
+}
+
+// Specialised k_tick kernels built in this process, by (device, variant, policy source): a
+// schema compiles once however many worlds use it.
+std::mutex g_jit_mu;
+std::map<std::string, hipFunction_t> g_jit;
+
+void build_jit(World* w) {
+    w->jit_fn = nullptr;
+    const char* env = getenv("NFGPU_JIT");
+    if (env && env[0] == '0') {
+        w->jit_msg = "disabled (NFGPU_JIT=0)";
+        return;
+    }
+    if (!w->u_ok) {
+        w->jit_msg = "working set does not fit k_tick (k_tick_touch runs)";
+        return;
+    }
+    const int u = std::max(w->d.n_u, 1);
+    int waves = tick_waves(w->d.n_u, w->d.ablate);
+    if (const char* ew = getenv("NFGPU_JIT_WAVES")) waves = std::max(1, std::min(8, atoi(ew)));
+    const std::string src = jit_schema_source(w->tab, w->d);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const std::string key = std::to_string(dev) + "|" + std::to_string(waves) + "|" + std::to_string(u) + "|" + src;
+    std::lock_guard<std::mutex> lk(g_jit_mu);
+    auto it = g_jit.find(key);
+    if (it == g_jit.end()) {
+        JitBuild b = jit_compile(src, waves, u);
+        hipModule_t mod = nullptr;
+        hipFunction_t fn = nullptr;
+        if (!b.ok || hipModuleLoadData(&mod, b.code.data()) != hipSuccess ||
+            hipModuleGetFunction(&fn, mod, b.lowered.c_str()) != hipSuccess) {
+            w->jit_msg = "hipRTC build failed: " + b.log.substr(0, 2000);
+            return;
+        }
+        it = g_jit.emplace(key, fn).first;
+    }
+    w->jit_fn = it->second;
+    w->jit_waves = waves;
+    w->jit_u = u;
+    w->jit_msg = jit_kernel_name(waves, u);
 }
 
 // w->mhost -> w->mlist, asynchronously on the world's stream (through a pinned double buffer:
@@ -1023,73 +1154,9 @@ int nfk_commit(void* world) {
         if (w->tab.recops[i].rec == w->tab.recops[i - 1].rec && w->tab.recops[i].col == w->tab.recops[i - 1].col)
             return fail(NFK_ERR_ARG, "two record ops on the same (record, col)");
     w->tab.n_recops = nro;
-    // frame working set (k_tick): program destinations -> writable slots [0, n_wp) and
-    // read-only operands -> slots [n_w, n_w + n_rp) of the frame (n_w >= n_wp also counts the
-    // frame's SetProperty properties), each group in property-id order; tables name read-only
-    // operand r as 0x80 | r
-    {
-        std::vector<int> W, R;
-        for (int k = 0; k < NK; k++)
-            for (int i = 0; i < w->tab.nops[k]; i++) {
-                const nfk_op& op = w->tab.ops[k][i];
-                if (op.code == NFK_OP_IADD_CLAMP || op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE)
-                    W.push_back(op.dst);
-            }
-        std::sort(W.begin(), W.end());
-        W.erase(std::unique(W.begin(), W.end()), W.end());
-        auto is_w = [&](int64_t p) { return std::binary_search(W.begin(), W.end(), (int)p); };
-        for (int k = 0; k < NK; k++)
-            for (int i = 0; i < w->tab.nops[k]; i++) {
-                const nfk_op& op = w->tab.ops[k][i];
-                if (op.code == NFK_OP_IADD_CLAMP) {
-                    if ((op.flags & NFK_A_PROP) && !is_w(op.a)) R.push_back((int)op.a);
-                    if ((op.flags & NFK_LO_PROP) && !is_w(op.b)) R.push_back((int)op.b);
-                    if ((op.flags & NFK_HI_PROP) && !is_w(op.c)) R.push_back((int)op.c);
-                } else if (op.code == NFK_OP_FLERP && !is_w(op.a)) {
-                    R.push_back((int)op.a);
-                }
-            }
-        std::sort(R.begin(), R.end());
-        R.erase(std::unique(R.begin(), R.end()), R.end());
-        w->u_ok = (int)W.size() <= kMaxW && (int)(W.size() + R.size()) <= kMaxU;
-        w->u_wp.assign(W.begin(), W.end());
-        w->u_rp.assign(R.begin(), R.end());
-        memset(w->tab.w_slot, kNoU, sizeof w->tab.w_slot);
-        for (size_t i = 0; i < W.size() && i < (size_t)kMaxW; i++) w->tab.w_slot[W[i]] = (uint8_t)i;
-        auto slot = [&](int64_t p) -> uint8_t {
-            auto it = std::lower_bound(W.begin(), W.end(), (int)p);
-            if (it != W.end() && *it == p) return (uint8_t)(it - W.begin());
-            it = std::lower_bound(R.begin(), R.end(), (int)p);
-            return (uint8_t)(0x80 | (it - R.begin()));
-        };
-        for (int k = 0; k < NK && w->u_ok; k++) {
-            w->tab.umask[k] = 0;
-            for (int i = 0; i < w->tab.nops[k]; i++) {
-                const nfk_op& op = w->tab.ops[k][i];
-                uint8_t* u = w->tab.opu[k][i];
-                u[0] = u[1] = u[2] = u[3] = kNoU;
-                if (op.code == NFK_OP_IADD_CLAMP) {
-                    u[0] = slot(op.dst);
-                    if (op.flags & NFK_A_PROP) u[1] = slot(op.a);
-                    if (op.flags & NFK_LO_PROP) u[2] = slot(op.b);
-                    if (op.flags & NFK_HI_PROP) u[3] = slot(op.c);
-                } else if (op.code == NFK_OP_FLERP) {
-                    u[0] = slot(op.dst);
-                    u[1] = slot(op.a);
-                } else if (op.code == NFK_OP_FAFFINE) {
-                    u[0] = slot(op.dst);
-                }
-                for (int q = 0; q < 4; q++)  // writable bits | read-only bits << 16
-                    if (u[q] != kNoU) w->tab.umask[k] |= (u[q] & 0x80) ? 1u << (16 + (u[q] & 0x7F)) : 1u << u[q];
-                OpX& x = w->tab.opx[k][i];
-                x.cfd = (uint32_t)op.code | ((uint32_t)op.flags << 8) | ((uint32_t)op.dst << 16);
-                x.slots = (uint32_t)u[0] | ((uint32_t)u[1] << 8) | ((uint32_t)u[2] << 16) | ((uint32_t)u[3] << 24);
-                x.a = op.a;
-                x.b = op.b;
-                x.c = op.c;
-            }
-        }
-    }
+    // the programs' working set (k_tick): program destinations -> writable U slots, read-only
+    // operands after them (build_u_tables)
+    w->u_ok = build_u_tables(w->tab, NK, w->u_wp, w->u_rp);
     w->n_dst_union = __builtin_popcountll(w->dst_union_mask[0]) + __builtin_popcountll(w->dst_union_mask[1]);
     if (w->n_dst_union > NFK_MAX_TOUCH)
         return fail(NFK_ERR_TOUCH, "programs write more than NFK_MAX_TOUCH distinct properties");
@@ -1360,6 +1427,7 @@ int nfk_commit(void* world) {
     // creation-time values are now on the device
     for (auto& v : w->init_props) std::vector<uint64_t>().swap(v);
     for (auto& v : w->init_rcells) std::vector<uint64_t>().swap(v);
+    build_jit(w);  // k_tick for this schema (hipRTC); the generic kernel stays when it cannot be built
     w->committed = true;
     return NFK_OK;
 }
@@ -2035,18 +2103,21 @@ int nfk_execute(void* world, int64_t now_ms) {
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
         size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;
+        const bool jit = use_u && w->jit_fn;
         if (d.fuse_fan) {  // the fan-out's message window takes what LDS the variant's occupancy
                            // leaves (waves per SIMD = workgroups per CU; ~2.3 KB static each)
-            const int waves = (d.n_u <= 8 && !(d.ablate & kAblWaves6)) ? kWavesU8
-                              : (d.n_u <= 12 && !(d.ablate & kAblWaves6)) ? ((d.ablate & kAblWaves8) ? 8 : kWavesU12)
-                                                                          : 6;
+            const int waves = jit ? w->jit_waves : tick_waves(d.n_u, d.ablate);
             lds = std::max(lds, (size_t)(163840 / waves - 2560) & ~(size_t)1023);
         }
         d.lds_words = (int32_t)(lds / 4);
         // the variant whose register slots hold the frame's working set (no spills at 6 or more
-        // waves per SIMD)
+        // waves per SIMD): this schema's own k_tick, else a generic instantiation
         const dim3 g((unsigned)d.n_tiles), b(kTPB);
-        if (use_u && d.n_u <= 8 && !(d.ablate & kAblWaves6))
+        if (jit) {
+            void* args[] = {&d};
+            HIPCHK(hipModuleLaunchKernel(w->jit_fn, (unsigned)d.n_tiles, 1, 1, kTPB, 1, 1, (unsigned)lds, w->stream,
+                                         args, nullptr));
+        } else if (use_u && d.n_u <= 8 && !(d.ablate & kAblWaves6))
             hipLaunchKernelGGL((k_tick<kWavesU8, 8>), g, b, lds, w->stream, d);
         else if (use_u && d.n_u <= 12 && (d.ablate & kAblWaves8))  // (8 waves, a few spills)
             hipLaunchKernelGGL((k_tick<8, 12>), g, b, lds, w->stream, d);
@@ -2489,6 +2560,60 @@ int nfk_rank_top(void* world, int32_t pid, int32_t k, int32_t* n_out, int64_t* g
         score[i] = cs[i].s;
     }
     *n_out = n;
+    return NFK_OK;
+}
+
+static void copy_msg(const std::string& m, char* out, int32_t cap) {
+    if (!out || cap <= 0) return;
+    const size_t n = std::min(m.size(), (size_t)cap - 1);
+    memcpy(out, m.data(), n);
+    out[n] = 0;
+}
+
+int nfk_jit_status(void* world, int32_t* on, char* msg, int32_t cap) {
+    World* w = (World*)world;
+    if (!w || !on) return fail(NFK_ERR_ARG, "null argument");
+    *on = w->jit_fn != nullptr;
+    copy_msg(w->jit_msg, msg, cap);
+    return NFK_OK;
+}
+
+int nfk_jit_preview(int32_t n_int, int32_t n_flt, int32_t n_class, int32_t n_kind, const uint8_t* prop_flags,
+                    const nfk_op* ops, const int32_t* n_ops, int32_t compile, int32_t* ok, char* src, int32_t src_cap,
+                    char* msg, int32_t msg_cap) {
+    if (!ok || !prop_flags || (n_kind && (!ops || !n_ops)) || n_int < 0 || n_flt < 0 || n_int > NFK_MAX_INT_PROPS ||
+        n_flt > NFK_MAX_FLT_PROPS || n_class <= 0 || n_class >= NFK_MAX_CLASSES || n_kind < 0 || n_kind > NFK_MAX_KINDS)
+        return fail(NFK_ERR_ARG, "bad schema");
+    *ok = 0;
+    std::unique_ptr<Tables> tab(new Tables());
+    memset(tab.get(), 0, sizeof(Tables));
+    const int np = n_int + n_flt;
+    for (int c = 0; c < n_class; c++)
+        for (int p = 0; p < np; p++) tab->pflags[c][p] = prop_flags[(size_t)c * np + p];
+    for (int k = 0; k < n_kind; k++) {
+        if (n_ops[k] < 0 || n_ops[k] > NFK_MAX_OPS) return fail(NFK_ERR_ARG, "bad op count");
+        tab->nops[k] = n_ops[k];
+        for (int i = 0; i < n_ops[k]; i++) tab->ops[k][i] = ops[(size_t)k * NFK_MAX_OPS + i];
+    }
+    std::vector<int> wp, rp;
+    const bool u_ok = build_u_tables(*tab, n_kind, wp, rp);
+    Dev d{};
+    d.n_kind = n_kind;
+    fill_u_dev(d, *tab, wp, rp, u_ok);
+    if (!u_ok) {
+        copy_msg("working set does not fit k_tick (k_tick_touch runs)", msg, msg_cap);
+        return NFK_OK;
+    }
+    const std::string s = jit_schema_source(*tab, d);
+    copy_msg(s, src, src_cap);
+    if (!compile) {
+        *ok = 1;
+        return NFK_OK;
+    }
+    const int u = std::max(d.n_u, 1), waves = tick_waves(d.n_u, 0);
+    JitBuild b = jit_compile(s, waves, u);
+    *ok = b.ok;
+    copy_msg(b.ok ? b.lowered + " (" + std::to_string(b.code.size()) + " B code object)\n" + b.log : b.log, msg, msg_cap);
     return NFK_OK;
 }
 

@@ -1,0 +1,646 @@
+// nfgpu_tick.hpp — k_tick, the frame kernel, and its helpers, written over a SCHEMA POLICY:
+// DynSchema reads the programs and the working set from Dev / Tables at run time (the kernels
+// compiled into libnfgpu.so); a world's own policy, generated from its schema at commit
+// (nfgpu_host.hip, jit_*), bakes them in as constants and straight-line code and is compiled
+// with this same header by hipRTC.
+#pragma once
+#include "nfgpu_device.hpp"
+
+namespace nfgpu {
+
+// The next "standalone" dirty Set group of slot e at or after g: a queued Set of a property that
+// no program writes, whose value changed over the frame (x_old != x_new).  Returns n_x when none.
+__device__ __forceinline__ int next_standalone(const Dev& d, int g, int e) {
+    for (; g < d.n_x && d.x_slot[g] == (uint32_t)e; g++)
+        if (d.tab->w_slot[d.x_pid[g]] == kNoU && d.x_old[g] != d.x_new[g]) return g;
+    return d.n_x;
+}
+// recipients of a property event (GetBroadCastObject, AOI:531-593) of slot e's class
+struct EvFan {
+    uint32_t n;    // messages
+    bool pub;      // to the scene group's players but self (else to self)
+};
+__device__ __forceinline__ EvFan ev_fan(const Dev& d, uint64_t desc, uint32_t pid) {
+    const uint8_t fl = d.tab->pflags[desc >> 60][pid];
+    return EvFan{event_msgs(desc, fl), (fl & NFK_PUBLIC) != 0};
+}
+
+// ---------------------------------------------------------------------------------
+// Frame working set (k_tick).  A thread keeps its entity's values of the U slots in registers;
+// program operands are addressed by wave-uniform slot numbers (Tables::opu), so a program runs
+// without searching a written-property list.
+#define NFK_U16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
+static_assert(kMaxU == 16, "NFK_U16 enumerates kMaxU slots");
+
+// A frame's U slots: the writable ones [0, n_w), then the read-only ones [n_w, n_w + n_r).  The
+// kind tables name a read-only operand by its index r as 0x80 | r, so one table serves every
+// frame; kU (template) = the register slots a k_tick variant keeps (n_w + n_r <= kU).
+__device__ __forceinline__ uint32_t uslot(uint32_t raw, uint32_t n_w) {
+    return (raw & 0x80u) ? n_w + (raw & 0x7Fu) : raw;
+}
+// j wave-uniform: a scalar branch to one register move
+template <int kU>
+__device__ __forceinline__ uint64_t uget(const uint64_t (&v)[kU], uint32_t j) {
+    switch (__builtin_amdgcn_readfirstlane(j)) {
+#define NFK_C(i) \
+    case i:      \
+        return v[(i) < kU ? (i) : 0];
+        NFK_U16(NFK_C)
+#undef NFK_C
+    }
+    return 0;
+}
+template <int kU>
+__device__ __forceinline__ void uput(uint64_t (&v)[kU], uint32_t j, uint64_t x) {
+    switch (__builtin_amdgcn_readfirstlane(j)) {
+#define NFK_C(i)                   \
+    case i:                        \
+        v[(i) < kU ? (i) : 0] = x; \
+        break;
+        NFK_U16(NFK_C)
+#undef NFK_C
+    }
+}
+// The fired kinds' programs in schedule-name order on the register working set.  A Set that
+// fails the reference's change predicate leaves the value as it was; wm collects the slots a
+// Set changed at least once.
+template <int kU>
+__device__ __forceinline__ void run_programs_u(uint64_t (&v)[kU], uint32_t& wm, const Tables* __restrict__ tab_,
+                                               uint32_t fired, int n_kind, uint32_t n_w) {
+    CTables* tab = ctab(tab_);
+    for (int k = 0; k < n_kind; k++) {
+        if (!((fired >> k) & 1)) continue;
+        const int n = tab->nops[k];
+        for (int i = 0; i < n; i++) {
+            const uint32_t cfd = tab->opx[k][i].cfd, sl = tab->opx[k][i].slots;
+            const uint32_t code = cfd & 0xFF, flags = (cfd >> 8) & 0xFF;
+            const uint32_t u0 = uslot(sl & 0xFF, n_w), u1 = uslot((sl >> 8) & 0xFF, n_w);
+            const uint32_t u2 = uslot((sl >> 16) & 0xFF, n_w), u3 = uslot(sl >> 24, n_w);
+            if (code == NFK_OP_IADD_CLAMP) {
+                const int64_t cur = (int64_t)uget(v, u0);
+                const int64_t a = (flags & NFK_A_PROP) ? (int64_t)uget(v, u1) : tab->opx[k][i].a;
+                const int64_t lo = (flags & NFK_LO_PROP) ? (int64_t)uget(v, u2) : tab->opx[k][i].b;
+                const int64_t hi = (flags & NFK_HI_PROP) ? (int64_t)uget(v, u3) : tab->opx[k][i].c;
+                int64_t r = (int64_t)((uint64_t)cur + (uint64_t)a);
+                r = r < lo ? lo : r;
+                r = r > hi ? hi : r;
+                uput(v, u0, (uint64_t)r);  // NFCProperty::SetInt (PR:273): r == cur changes nothing
+                wm |= (r != cur) ? (1u << u0) : 0u;
+            } else if (code == NFK_OP_FLERP || code == NFK_OP_FAFFINE) {
+                const uint64_t xb = uget(v, u0);
+                const double x = __longlong_as_double((long long)xb);
+                double r;
+                if (code == NFK_OP_FLERP) {
+                    const double tg = __longlong_as_double((long long)uget(v, u1));
+                    const double dd = tg - x;
+                    const double m = dd * __longlong_as_double(tab->opx[k][i].b);
+                    r = x + m;
+                } else {
+                    const double m = x * __longlong_as_double(tab->opx[k][i].a);
+                    r = m + __longlong_as_double(tab->opx[k][i].b);
+                }
+                const bool set = !(fabs(r - x) <= 1e-15);  // NFCProperty::SetFloat (PR:314): IsZeroDouble(v - cur)
+                uput(v, u0, set ? (uint64_t)__double_as_longlong(r) : xb);
+                wm |= set ? (1u << u0) : 0u;
+            }
+            // record ops run in k_records
+        }
+    }
+}
+
+// Block-wide exclusive scan of a packed 64-bit value (fields must not overflow into each other).
+__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v, unsigned long long* s_w,
+                                                              unsigned long long& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long inc = wave_incl_scan(v);
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    unsigned long long before = 0;
+    total = 0;
+#pragma unroll
+    for (int i = 0; i < kTPB / 64; i++) {
+        const unsigned long long x = s_w[i];
+        before += (i < w) ? x : 0ull;
+        total += x;
+    }
+    return before + inc - v;
+}
+
+// The schema k_tick runs: the heartbeat kinds, the programs' working set (U slots) and its event
+// order and fan-out classes.  DynSchema reads it at run time (Dev, kernel-argument scalars, and
+// Tables through the constant address space); a generated policy (nfgpu_host.hip, jit_source)
+// has the same members as constants and the programs as straight-line code on the registers.
+struct DynSchema {
+    static constexpr bool kStatic = false;
+    static constexpr int kNK = NFK_MAX_KINDS;  // (an upper bound only)
+    __device__ static int n_kind(const Dev& d) { return d.n_kind; }
+    __device__ static int n_w(const Dev& d) { return d.n_w; }
+    __device__ static uint32_t u_lower(const Dev& d, int j) { return d.u_lower[j]; }
+    __device__ static int u_pid(const Dev& d, int j) { return d.u_pid[j]; }
+    __device__ static int u_order(const Dev& d, int i) { return d.u_order[i]; }
+    __device__ static uint32_t cmask(const Dev& d, int c) { return d.u_cmask[c]; }
+    // the U slots the fired kinds read or write
+    __device__ static uint32_t need(const Dev& d, uint32_t fired) {
+        uint32_t need = 0;
+        for (int k = 0; k < d.n_kind; k++)
+            if ((fired >> k) & 1) {
+                const uint32_t um = ctab(d.tab)->umask[k];  // writable bits | read-only bits << 16
+                need |= (um & 0xFFFFu) | ((um >> 16) << d.n_w);
+            }
+        return need;
+    }
+    template <int kU>
+    __device__ static void run(uint64_t (&v)[kU], uint32_t& wm, const Dev& d, uint32_t fired) {
+        run_programs_u(v, wm, d.tab, fired, d.n_kind, d.n_w);
+    }
+};
+
+constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
+
+// k_tick register budgets (waves per SIMD) by the frame's U slot count
+constexpr int kWavesU8 = 8, kWavesU12 = 7;
+constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: at most 4 GiB reserved
+
+// NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
+// order).  The hot records of a chunk of kinds are loaded together (independent 16 B loads).
+// Rescheduled / removed records are stored back.  Every load is issued without a branch and before
+// the first use of any of them: a load under a branch is followed by a wait at the join, and a
+// first use after the record stores would make the wave wait for the stores too (the vector
+// memory counter retires in order), i.e. one round trip per kind or per store batch.
+template <class S, bool kFirst>
+__device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigned& bytes, uint64_t& desc,
+                                            bool& dead, bool& taken, uint32_t& fired, int32_t* s_rem,
+                                            bool oob) {
+    SchedHot h[kKindChunk];
+    // kinds past n_kind re-read the chunk's first record (a cache hit); a static schema loads
+    // exactly its kinds
+    const SchedHot* base = d.s_hot + (size_t)k0 * d.s_kstr + e;
+    const int nk = S::n_kind(d) - k0;
+#pragma unroll
+    for (int j = 0; j < kKindChunk; j++)
+        if (!S::kStatic || j < nk) h[j] = base[(size_t)(j < nk ? j : 0) * d.s_kstr];
+    if constexpr (kFirst) {
+        desc = d.fan_desc[e];
+        const uint8_t ef = d.e_flags[e];  // (always allocated)
+        __builtin_amdgcn_sched_barrier(0);  // the scheduler would hoist the first use and its wait
+        dead = oob || desc_dead(desc);  // a slack slot has no schedules; dead slots store nothing
+        taken = d.has_pre && (ef & 1);  // std::map remove-list key already owned (SM:68)
+        bytes += d.has_pre ? 1 : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kKindChunk; j++) {
+        const int k = k0 + j;
+        if (k >= S::n_kind(d)) break;
+        bytes += 16;
+        if (dead || !(h[j].state & kStPresent) || !(d.now > h[j].next)) continue;
+        const bool forever = h[j].state & kStForever;
+        if (!(h[j].remain > 0 || forever)) continue;
+        h[j].remain -= 1;
+        fired |= 1u << k;
+        const uint32_t st = h[j].state;
+        if (h[j].remain <= 0 && !forever) {
+            if (!taken) {  // insert into the remove list succeeds for the first one only
+                h[j].state = 0;
+                taken = true;
+            }
+        } else {
+            const bool first = !(st & kStFired);
+            if ((st & kStStep) && (first || !forever || h[j].remain < 0)) {
+                // next = start + step * (all - remain) without the cold record (see kSt*)
+                if (!first) h[j].next += st_step(st);
+            } else {
+                const SchedCold c = d.s_cold[(size_t)k * d.s_kstr + e];
+                bytes += 16;
+                const int64_t step = (int64_t)(c.interval * 1000.0f);
+                const int32_t done = (int32_t)((uint32_t)c.all - (uint32_t)h[j].remain);
+                h[j].next = c.start + step * (int64_t)done;
+            }
+            h[j].state = st | kStFired;
+        }
+        if (!(d.ablate & kAblNoSchedStore)) d.s_hot[(size_t)k * d.s_kstr + e] = h[j];
+        if (s_rem) s_rem[k * kTPB + threadIdx.x] = h[j].remain;  // for the fired list
+        bytes += 16;
+    }
+}
+// Loads desc = fan_desc[e] with the first chunk; returns the fired-kind mask.  oob: a slot past N
+// (e is then a valid slot re-read, treated as dead).
+template <class S = DynSchema>
+__device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& bytes, uint64_t& desc,
+                                               int32_t* s_rem = nullptr, bool oob = false) {
+    uint32_t fired = 0;
+    bool dead = true, taken = false;
+    sched_chunk<S, true>(d, e, 0, bytes, desc, dead, taken, fired, s_rem, oob);
+    for (int k0 = kKindChunk; k0 < S::n_kind(d); k0 += kKindChunk)
+        sched_chunk<S, false>(d, e, k0, bytes, desc, dead, taken, fired, s_rem, oob);
+    return fired;
+}
+
+// k_tick: one thread per slot, one workgroup per 256-slot tile, on the programs' working set
+// (Dev::u_*, fixed at commit).  Every value the entity's frame touches is loaded in ONE batch of
+// independent loads into registers; the fired kinds' programs run on those registers with
+// wave-uniform slot numbers; the slots a program or a queued Set changed are diffed against their
+// frame-start values (kept in LDS).  Queued SetProperty calls were applied by k_sets: a Set of a
+// program destination joins that slot's diff (frame-start value = the group's x_old), a Set of any
+// other property is a "standalone" event (x_old -> x_new) merged into the entity's events in
+// property-id order.  Outputs of tile t are written densely at [t * tile_cap, t * tile_cap + count);
+// k_scan_tiles turns the counts into global ranks.
+// kWPE: waves per SIMD the register allocation aims at.  The LDS image of the frame-start values
+// is dynamic: n_w writable slots x kTPB.
+template <int kWPE, int kU, class S = DynSchema>
+__global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8))) void k_tick(Dev d) {
+    constexpr int kW = kU < kMaxW ? kU : kMaxW;  // writable register slots
+    __shared__ unsigned long long s_w[kTPB / 64];
+    __shared__ unsigned s_bytes;
+    __shared__ uint32_t s_pb[3];   // pl_slot run of the groups with dirty events [lo, hi), most recipients
+    __shared__ uint32_t s_cm[NFK_MAX_CLASSES];  // Dev::u_cmask
+    extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
+    const int tile = blockIdx.x;
+    const int e = tile * kTile + (int)threadIdx.x;
+    const bool fuse = d.msg_tcap != 0;  // this tile's fan-out is written here, at tile * msg_tcap
+    if (threadIdx.x == 0) {
+        s_bytes = 0;
+        s_pb[0] = 0xFFFFFFFFu;
+        s_pb[1] = 0;
+        s_pb[2] = 1;
+    }
+    int32_t* s_rem = (int32_t*)(s_o + (size_t)S::n_w(d) * kTPB);  // [n_kind][kTPB] remain after a fire
+    unsigned bytes = 0;
+    uint32_t fired = 0, xh = 0, wm = 0;
+    uint64_t desc = kDeadDesc;
+    uint64_t v[kU];
+#pragma unroll
+    for (int j = 0; j < kU; j++) v[j] = 0;
+    {
+        // descriptor and schedule records in one round trip, without a branch: slots past N (the
+        // last tile) re-read slot N-1 and count as dead; a dead slot stores nothing
+        const int ec = e < d.N ? e : d.N - 1;
+        fired = sched_scan<S>(d, ec, bytes, desc, s_rem, e >= d.N);  // NFCScheduleModule::Execute (SM:51-81)
+        desc = e < d.N ? desc : kDeadDesc;
+        bytes = e < d.N ? bytes + 8 : 0u;
+    }
+    const bool live = !desc_dead(desc);
+    // queued Set groups of this slot (k_sets ran them): program destinations among them
+    uint32_t xset = 0;
+    if (live && d.n_x) {
+        xh = d.ext_head[e];
+        bytes += 4;
+        if (xh)
+            for (int g = (int)xh - 1; g < d.n_x && d.x_slot[g] == (uint32_t)e; g++) {
+                const uint32_t j = d.tab->w_slot[d.x_pid[g]];
+                xset |= j != kNoU ? 1u << j : 0u;
+                bytes += 8;
+            }
+    }
+    if (live) {
+        uint32_t need = xset;
+        if (!(d.ablate & kAblPrograms)) need |= S::need(d, fired);
+        // one batch of independent loads: every value this entity's frame reads or writes
+#pragma unroll
+        for (int j = 0; j < kU; j++)
+            if (((need >> j) & 1) && !(d.ablate & kAblNoLoads)) {
+                v[j] = d.u_col[j][(size_t)e * d.u_str[j]];
+                bytes += 8;
+            }
+#pragma unroll
+        for (int j = 0; j < kW; j++)
+            if (j < S::n_w(d) && ((need >> j) & 1)) s_o[j * kTPB + threadIdx.x] = v[j];
+        // a Set program destination: its frame-start value is the value before the Set group
+        if (xset) {
+            for (int g = (int)xh - 1; g < d.n_x && d.x_slot[g] == (uint32_t)e; g++) {
+                const uint32_t j = d.tab->w_slot[d.x_pid[g]];
+                if (j != kNoU) s_o[j * kTPB + threadIdx.x] = d.x_old[g];
+                bytes += j != kNoU ? 8 : 0;
+            }
+            wm = xset;
+        }
+        // the fired heartbeats' effect programs, in schedule-name order
+        if (!(d.ablate & (kAblPrograms | kAblNoRun)) && fired) S::run(v, wm, d, fired);
+    }
+    if (threadIdx.x < NFK_MAX_CLASSES) {  // (a select over kernel-argument scalars, no indexed copy)
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < NFK_MAX_CLASSES; i++) c = threadIdx.x == (unsigned)i ? S::cmask(d, i) : c;
+        s_cm[threadIdx.x] = c;
+    }
+    __syncthreads();  // s_pb / s_bytes / s_cm initialised
+    // dirty diff against the frame-start values
+    uint32_t dm = 0;
+#pragma unroll
+    for (int j = 0; j < kW; j++)
+        if (((wm >> j) & 1) && v[j] != s_o[j * kTPB + threadIdx.x]) dm |= 1u << j;
+    // a Set program destination that a program moved back to its frame-start value has no event,
+    // but k_sets changed its column: write it back here (the dirty slots are written with their
+    // events)
+    if (xset & ~dm)
+#pragma unroll
+        for (int j = 0; j < kW; j++)
+            if (j < S::n_w(d) && ((xset & ~dm) >> j) & 1) {
+                d.u_col[j][(size_t)e * d.u_str[j]] = v[j];
+                bytes += 8;
+            }
+    // fan-out message counts (event_msgs): a public property's event goes to every player of the
+    // group but the entity itself, a private & !upload one to the entity only.  The message offset
+    // of a slot's event = the counts of the dirty slots with lower property ids (Dev::u_lower).
+    const uint32_t cm = s_cm[desc >> 60];  // (class 15, a free slot: no slots)
+    const uint32_t pubm = cm & 0xFFFFu, privm = cm >> 16;
+    const uint32_t r1 = (uint32_t)((desc >> 46) & 0x3FFF);
+    const uint32_t npub = (uint32_t)((desc >> 32) & 0x3FFF) - (r1 ? 1u : 0u);
+    unsigned nmsg = npub * __builtin_popcount(dm & pubm) + __builtin_popcount(dm & privm);
+    unsigned nmax = (dm & pubm) ? npub : ((dm & privm) ? 1u : 0u);
+    unsigned nd = __builtin_popcount(dm);
+    // standalone Set events (properties no program writes): counted here, merged in property-id
+    // order with the slots' events below
+    unsigned nsd = 0;
+    if (xh) {
+        for (int g = next_standalone(d, (int)xh - 1, e); g < d.n_x; g = next_standalone(d, g + 1, e)) {
+            const EvFan f = ev_fan(d, desc, d.x_pid[g]);
+            nsd++;
+            nmsg += f.n;
+            nmax = max(nmax, f.n);
+            bytes += 8;
+        }
+        nd += nsd;
+    }
+    // the entity's events in property-id order: dirty slots (u_order) merged with the standalone
+    // groups; emit(rank, message offset, pid, slot or -1, group, recipients) per event
+    auto walk = [&](auto&& emit) {
+        int g = next_standalone(d, (int)xh - 1, e);
+        unsigned at = 0, m = 0;
+#pragma unroll 1
+        for (int i = 0; i <= S::n_w(d); i++) {
+            const int j = i < S::n_w(d) ? S::u_order(d, i) : -1;
+            const uint32_t pj = j >= 0 ? (uint32_t)S::u_pid(d, j) : 0xFFFFFFFFu;
+            while (g < d.n_x && d.x_pid[g] < pj) {
+                const EvFan f = ev_fan(d, desc, d.x_pid[g]);
+                emit(at, m, d.x_pid[g], -1, g, f);
+                at++;
+                m += f.n;
+                g = next_standalone(d, g + 1, e);
+            }
+            if (j >= 0 && ((dm >> j) & 1)) {
+                const bool pub = (pubm >> j) & 1;
+                const EvFan f{pub ? npub : ((privm >> j) & 1u), pub};
+                emit(at, m, pj, j, 0, f);
+                at++;
+                m += f.n;
+            }
+        }
+    };
+    const unsigned nf = __builtin_popcount(fired);
+    const uint32_t dm_ = dm;
+    if (fuse) {  // the pl_slot run of the groups whose members have messages (they are contiguous)
+        const uint32_t np = (uint32_t)((desc >> 32) & 0x3FFF);
+        uint32_t lo = nmsg ? (uint32_t)desc : 0xFFFFFFFFu, hi = nmsg ? (uint32_t)desc + np : 0u;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, m, 64));
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, m, 64));
+            nmax = max(nmax, (uint32_t)__shfl_xor((int)nmax, m, 64));
+        }
+        if ((threadIdx.x & 63) == 0 && hi) {
+            atomicMin(&s_pb[0], lo);
+            atomicMax(&s_pb[1], hi);
+            atomicMax(&s_pb[2], nmax);
+        }
+    }
+
+    // tile-local compaction: one block scan of (fired:16 | events:16 | messages:32)
+    unsigned long long tot;
+    const unsigned long long excl =
+        block_excl_scan(((unsigned long long)nf << 48) | ((unsigned long long)nd << 32) | nmsg, s_w, tot);
+    const unsigned pev0 = (unsigned)((excl >> 32) & 0xFFFF);
+    unsigned pfi = (unsigned)(excl >> 48);
+    const unsigned pmsg0 = (unsigned)excl, tmsg = (unsigned)tot;
+    // this tile's output runs (wave-uniform bases, tile-local 32-bit offsets)
+    const size_t ev0 = (size_t)tile * d.ev_tcap, fi0 = (size_t)tile * d.fi_tcap;
+    uint32_t* const t_evm = d.ev_moff + ev0;
+
+    if (live) {
+        // write back the changed values; their events in property-id order (rank among the
+        // entity's dirty slots by Dev::u_lower)
+        if (nd && !(d.ablate & kAblNoEmit)) {
+            uint32_t* const t_evs = d.ev_slot + ev0;
+            uint32_t* const t_evp = d.ev_pid + ev0;
+            uint64_t* const t_evo = d.ev_old + ev0;
+            uint64_t* const t_evn = d.ev_new + ev0;
+            if (!nsd) {
+#pragma unroll
+                for (int j = 0; j < kW; j++) {
+                    if (j >= S::n_w(d) || !((dm >> j) & 1)) continue;
+                    const uint32_t below = dm & S::u_lower(d, j);
+                    const uint32_t at = pev0 + __builtin_popcount(below);
+                    const uint64_t nv = v[j];
+                    if (!(d.ablate & kAblNoWriteBack)) d.u_col[j][(size_t)e * d.u_str[j]] = nv;
+                    st_off(t_evs, at, (uint32_t)e);
+                    st_off(t_evp, at, (uint32_t)S::u_pid(d, j));
+                    st_off(t_evo, at, s_o[j * kTPB + threadIdx.x]);
+                    st_off(t_evn, at, nv);
+                    if (!fuse)  // tile-local; k_fanout adds the tile's message base
+                        st_off(t_evm, at, pmsg0 + npub * __builtin_popcount(below & pubm) +
+                                              __builtin_popcount(below & privm));
+                    bytes += 8 + 24;
+                }
+            } else {
+                // (rare: an entity with standalone Set events) write back the slots, then every
+                // event by the merged walk, which reads the slots' new values back from their
+                // columns so that no register of the working set stays live in it
+#pragma unroll
+                for (int j = 0; j < kW; j++)
+                    if (j < S::n_w(d) && ((dm >> j) & 1)) {
+                        d.u_col[j][(size_t)e * d.u_str[j]] = v[j];
+                        bytes += 8;
+                    }
+                walk([&](unsigned at, unsigned m, uint32_t pid, int j, int g, EvFan) {
+                    uint64_t ov, nv;
+                    if (j >= 0) {
+                        ov = s_o[j * kTPB + threadIdx.x];
+                        nv = __hip_atomic_load(d.u_col[j] + (size_t)e * d.u_str[j], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    } else {  // (k_sets wrote the column)
+                        ov = d.x_old[g];
+                        nv = d.x_new[g];
+                    }
+                    st_off(t_evs, pev0 + at, (uint32_t)e);
+                    st_off(t_evp, pev0 + at, pid);
+                    st_off(t_evo, pev0 + at, ov);
+                    st_off(t_evn, pev0 + at, nv);
+                    if (!fuse) st_off(t_evm, pev0 + at, pmsg0 + m);
+                    bytes += 24;
+                });
+            }
+        }
+        uint32_t* const t_fis = d.fi_slot + fi0;
+        uint32_t* const t_fik = d.fi_kind + fi0;
+        int32_t* const t_fir = d.fi_remain + fi0;
+        uint32_t fl = fired;
+        while (fl) {
+            const int k = __builtin_ctz(fl);
+            fl &= fl - 1;
+            st_off(t_fis, pfi, (uint32_t)e);
+            st_off(t_fik, pfi, (uint32_t)k);
+            st_off(t_fir, pfi, s_rem[k * kTPB + threadIdx.x]);
+            pfi++;
+            bytes += 12;
+        }
+        if (xh) d.ext_head[e] = 0;
+    }
+    if (d.has_recops && e < d.N) {  // slack slots too: a slot's previous occupant left a mask
+        d.fired_mask[e] = fired;
+        bytes += 4;
+    }
+    if (!fuse && !(d.ablate & kAblNoEmit)) bytes += 4 * nd;  // ev_moff
+    // Fan-out of the tile's events (GetBroadCastObject, AOI:531-593; see k_fanout), into the
+    // tile's fixed-stride run mb.  The LDS region of the frame-start image is reused for a chunk
+    // of the tile's events as (first message, first player | slot, count | rank | public) triples
+    // and the groups' player run; each event is then expanded by a group of L lanes (L = the
+    // tile's largest recipient count rounded up to a power of two), so consecutive lane groups
+    // store consecutive events' runs.  Runs of 16 or more recipients are stored that way straight
+    // to HBM; shorter ones are written one thread per event into an LDS message window stored
+    // with 16-byte stores (short runs stored directly leave lines partly written by several
+    // waves, and lane groups would re-read each event's triple once per lane).
+    if (fuse) {
+        __syncthreads();  // s_pb; every read of s_o and s_rem is done: the region is reused
+        uint32_t dm = dm_;
+        const unsigned mb = (unsigned)tile * d.msg_tcap;
+        const unsigned tev = (unsigned)((tot >> 32) & 0xFFFF);
+        const bool fan = tmsg && tmsg <= d.msg_tcap;
+        if (tmsg > d.msg_tcap && threadIdx.x == 0) atomicOr(&d.ctrl->err, kErrFanBound);  // (host bound)
+        if (!fan) {  // ev_moff only
+            if (nsd) {
+                walk([&](unsigned at, unsigned m, uint32_t, int, int, EvFan) { st_off(t_evm, pev0 + at, mb + pmsg0 + m); });
+                bytes += 4 * nd;
+            } else if (dm) {
+#pragma unroll
+                for (int j = 0; j < kW; j++) {
+                    if (j >= S::n_w(d) || !((dm >> j) & 1)) continue;
+                    const uint32_t below = dm & S::u_lower(d, j);
+                    st_off(t_evm, pev0 + __builtin_popcount(below),
+                           mb + pmsg0 + npub * __builtin_popcount(below & pubm) + __builtin_popcount(below & privm));
+                    bytes += 4;
+                }
+            }
+        } else {
+            const unsigned R = (unsigned)d.lds_words;
+            const uint32_t pb_lo = s_pb[0], npl = s_pb[1] > s_pb[0] ? s_pb[1] - s_pb[0] : 0u;
+            const uint32_t nm = s_pb[2];
+            const uint32_t L = nm <= 1 ? 1u : nm >= 64 ? 64u : 1u << (32 - __builtin_clz(nm - 1));
+            const uint32_t sub = threadIdx.x & (L - 1);
+            const bool win = L < 16;
+            const bool staged = npl <= R / 4;
+            const unsigned room = R - (staged ? npl : 0u);
+            // events per chunk: all of them, or what leaves the window half of the room
+            const unsigned ecap = (min(tev, win ? room / 6u : room / 3u) + 3u) & ~3u;
+            const unsigned W = win ? (room - 3u * ecap) & ~3u : 0u;  // window entries
+            uint32_t* s_ev = (uint32_t*)s_o;
+            uint32_t* s_win = s_ev + 3u * ecap;
+            uint32_t* s_pl = s_ev + (R - npl);
+            uint32_t* out = d.msg_rcpt + mb;
+            if (staged) {
+                for (uint32_t i = threadIdx.x; i < npl; i += kTPB) s_pl[i] = (uint32_t)d.pl_slot[pb_lo + i];
+                bytes += 4 * ((npl + kTPB - 1 - threadIdx.x) / kTPB);
+            }
+            bytes += 4 * nmsg;
+            for (unsigned c0 = 0; c0 < tev; c0 += ecap) {  // uniform
+                const unsigned c1 = min(tev, c0 + ecap);
+                // a runtime loop over the slots (an unrolled one gets hoisted out of the chunk loop
+                // and spills: 12 slots x 4 values)
+                if (nd && pev0 < c1 && pev0 + nd > c0) {
+                    if (nsd) {
+                        walk([&](unsigned at, unsigned m, uint32_t, int, int, EvFan f) {
+                            const unsigned a = pev0 + at;
+                            if (a < c0 || a >= c1) return;
+                            uint32_t* x = s_ev + 3u * (a - c0);
+                            x[0] = pmsg0 + m;
+                            x[1] = f.pub ? (uint32_t)desc : (uint32_t)e;
+                            x[2] = f.n | (r1 << 14) | (f.pub ? 0x80000000u : 0u);
+                            st_off(t_evm, a, mb + pmsg0 + m);
+                            bytes += 4;
+                        });
+                    } else {
+#pragma unroll 1
+                        for (int j = 0; j < S::n_w(d); j++) {
+                            if (!((dm >> j) & 1)) continue;
+                            const uint32_t below = dm & S::u_lower(d, j);
+                            const uint32_t at = pev0 + __builtin_popcount(below);
+                            if (at < c0 || at >= c1) continue;
+                            const bool pub = (pubm >> j) & 1;
+                            const uint32_t m = pmsg0 + npub * __builtin_popcount(below & pubm) +
+                                               __builtin_popcount(below & privm);
+                            const uint32_t n = pub ? npub : ((privm >> j) & 1u);
+                            uint32_t* x = s_ev + 3u * (at - c0);
+                            x[0] = m;
+                            x[1] = pub ? (uint32_t)desc : (uint32_t)e;
+                            x[2] = n | (r1 << 14) | (pub ? 0x80000000u : 0u);
+                            st_off(t_evm, at, mb + m);
+                            bytes += 4;
+                        }
+                    }
+                }
+                __syncthreads();
+                if (!win) {
+                    for (uint32_t i = threadIdx.x / L; i < c1 - c0; i += kTPB / L) {
+                        const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
+                        const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
+                        if (!(b >> 31)) {  // private & !upload: the entity itself (n is 0 or 1)
+                            if (sub < n) out[ms] = a;
+                            continue;
+                        }
+                        for (uint32_t p = sub; p < n; p += L) {  // every player of the group but self
+                            const uint32_t pp = p + ((r1 && p + 1 >= r1) ? 1u : 0u);
+                            out[ms + p] = staged ? s_pl[a - pb_lo + pp] : (uint32_t)d.pl_slot[a + pp];
+                        }
+                    }
+                } else {
+                    const unsigned last = 3u * (c1 - c0 - 1u);
+                    const unsigned m_lo = s_ev[0], m_hi = s_ev[last] + (s_ev[last + 2] & 0x3FFFu);
+                    for (unsigned w0 = m_lo; w0 < m_hi; w0 += W) {  // uniform
+                        const unsigned w1 = min(m_hi, w0 + W);
+                        // short runs: one thread per event (fewer LDS reads than lane groups)
+                        for (uint32_t i = threadIdx.x; i < c1 - c0; i += kTPB) {
+                            const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
+                            const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
+                            if (n == 0 || ms >= w1 || ms + n <= w0) continue;
+                            if (!(b >> 31)) {
+                                s_win[ms - w0] = a;
+                                continue;
+                            }
+                            const uint32_t np = n + (r1 ? 1u : 0u);
+                            uint32_t k = ms;
+                            for (uint32_t p = 0; p < np; p++) {
+                                if (p + 1 == r1) continue;
+                                if (k >= w0 && k < w1)
+                                    s_win[k - w0] = staged ? s_pl[a - pb_lo + p] : (uint32_t)d.pl_slot[a + p];
+                                k++;
+                            }
+                        }
+                        __syncthreads();
+                        const uint32_t n = w1 - w0;
+                        if ((w0 & 3u) == 0) {  // mb is a multiple of 4 (msg_tcap is): 16-byte stores
+                            const uint32_t n4 = n >> 2;
+                            uint4* dst4 = (uint4*)(out + w0);
+                            const uint4* src4 = (const uint4*)s_win;
+                            for (uint32_t i = threadIdx.x; i < n4; i += kTPB) dst4[i] = src4[i];
+                            if (threadIdx.x < (n & 3u)) out[w0 + 4 * n4 + threadIdx.x] = s_win[4 * n4 + threadIdx.x];
+                        } else {
+                            for (uint32_t i = threadIdx.x; i < n; i += kTPB) out[w0 + i] = s_win[i];
+                        }
+                        __syncthreads();
+                    }
+                }
+                if (c1 < tev) __syncthreads();  // s_ev is refilled
+            }
+        }
+    }
+    // tile counts and algorithmic-byte tally
+    const unsigned wb = (unsigned)wave_sum(bytes);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&s_bytes, wb);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        d.t_ev[tile] = (unsigned)((tot >> 32) & 0xFFFF);
+        d.t_fi[tile] = (unsigned)(tot >> 48);
+        d.t_msg[tile] = (unsigned)tot;
+        tally_add(d, kTallyTick, (unsigned long long)(s_bytes + 12 + (fuse ? 16 : 0)));
+    }
+}
+
+}  // namespace nfgpu
