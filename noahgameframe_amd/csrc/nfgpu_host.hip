@@ -1971,6 +1971,12 @@ int nfk_execute(void* world, int64_t now_ms) {
         }
     }
 
+    // k_post_hostops' entries kind-major, slot order: a mass AddSchedule (server start, a wave of
+    // spawns) then sweeps each kind's schedule records in address order
+    if (post.size() > 1)
+        std::sort(post.begin(), post.end(),
+                  [](const Post& a, const Post& b) { return a.kind != b.kind ? a.kind < b.kind : a.slot < b.slot; });
+
     // k_tick runs the programs on the working set fixed at commit (Dev::u_*); a schema whose
     // working set does not fit the register slots runs k_tick_touch
     const bool use_u = w->u_ok && !(d.ablate & kAblPerKind);

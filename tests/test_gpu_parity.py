@@ -270,7 +270,7 @@ def test_cpp_plugin_api_replay_matches_oracle(gpu_available, tmp_path):
     if not os.path.exists(exe):
         import __graft_entry__
         __graft_entry__.build_plugin()
-    from noahgameframe_amd.shard import zrevrange_order
+    from tests.redis_zset import zrevrange_top
     w = workload.make_world(n_obj=3000, n_scenes=2, groups_per_scene=6, players_per_group=5, n_ticks=8, seed=31,
                             ext_frac=0.05, host_ops=True, switch_frac=0.01, switch_new_groups=True, rmw_frac=0.02,
                             ext_props="all")
@@ -298,7 +298,7 @@ def test_cpp_plugin_api_replay_matches_oracle(gpu_available, tmp_path):
     # GetRange (NFIRankRedisModule, ZREVRANGE 0..99) over the final oracle state
     n_int = w["cfg"][1]
     for p, final in ((0, ref["final_i"][0].astype(np.float64)), (n_int, ref["final_f"][0])):
-        order = zrevrange_order(w["guid_head"], w["guid_data"], final)[:100]
+        order = np.asarray(zrevrange_top(w["guid_head"], w["guid_data"], final, 100), np.int64)
         np.testing.assert_array_equal(got[f"rank_p{p}_head"], w["guid_head"][order])
         np.testing.assert_array_equal(got[f"rank_p{p}_data"], w["guid_data"][order])
         np.testing.assert_array_equal(got[f"rank_p{p}_score"], final[order])
@@ -308,7 +308,7 @@ def test_cpp_plugin_api_replay_matches_oracle(gpu_available, tmp_path):
 def test_rank_top_matches_zrevrange(gpu_available, prop, k):
     """nfk_rank_top = Redis ZREVRANGE 0..k-1 over the property (NFCRankRedisModule.cpp:109): score
     desc, equal scores by NFGUID::ToString() desc — heavy ties (Level, Camp) included."""
-    from noahgameframe_amd.shard import zrevrange_order
+    from tests.redis_zset import zrevrange_top
     w = workload.make_world(n_obj=30000, n_scenes=2, groups_per_scene=20, players_per_group=5, n_ticks=3, seed=91,
                             switch_frac=0.01)
     m = kernel.world_from_workload(w, slack_per_256=32)
@@ -317,7 +317,7 @@ def test_rank_top_matches_zrevrange(gpu_available, prop, k):
     pid = workload.PID[prop]
     vals = m.read_prop(pid).astype(np.float64)
     gh, gd, sc = m.rank_top(prop, k)
-    o = zrevrange_order(w["guid_head"], w["guid_data"], vals)[:k]
+    o = np.asarray(zrevrange_top(w["guid_head"], w["guid_data"], vals, k), np.int64)
     assert list(zip(gh.tolist(), gd.tolist())) == list(zip(w["guid_head"][o].tolist(), w["guid_data"][o].tolist()))
     np.testing.assert_array_equal(sc, vals[o])
     m.close()
