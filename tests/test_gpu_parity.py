@@ -138,9 +138,18 @@ def test_membership_failure_keeps_window_queued(gpu_available):
     m.Execute(int(w["tick_time"][1]))
     gid = m.read_prop(workload.PID["GroupID"])
     assert np.all(gid[movers[2000:]] == 1) and np.all(gid[movers[:2000]] == 2)
-    assert m.read_prop(workload.PID["HP"])[0] == 77
+    # the Set landed before the frame's heartbeats, as on a twin world that never failed
+    t = kernel.world_from_workload(w, slack_per_256=-1)
+    t.Execute(int(w["tick_time"][0]))
+    for o in movers[2000:]:
+        t.SwitchScene((int(gh[o]), int(gd[o])), 1, 1, 0.0, 0.0, 0.0)
+    t.SetPropertyInt((int(gh[0]), int(gd[0])), "HP", 77)
+    t.Execute(int(w["tick_time"][1]))
+    for pid in ("HP", "GroupID", "SceneID"):
+        np.testing.assert_array_equal(m.read_prop(workload.PID[pid]), t.read_prop(workload.PID[pid]))
     s = m.summary()
     assert s["n_entities"] == n
+    t.close()
     m.close()
 
 
