@@ -92,6 +92,8 @@ def load_library(path=LIB_PATH):
         "nfk_import_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
         "nfk_spawn_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP], "nfk_sync": [VP],
         "nfk_rank_top": [VP, I32, I32, VP, VP, VP, VP],
+        "nfk_jit_status": [VP, VP, VP, I32],
+        "nfk_jit_preview": [I32, I32, I32, I32, VP, VP, VP, I32, VP, VP, I32, VP, I32],
     }
     for name, args in sig.items():
         if not hasattr(lib, name) and os.environ.get("NFGPU_LIB"):
@@ -243,6 +245,13 @@ class NFKernelModule:
         self._chk(self.lib.nfk_object_count(self.h, ctypes.byref(n)))
         return n.value
 
+    def jit_status(self):
+        """(True, message) when k_tick runs the hipRTC specialisation built at commit"""
+        on = ctypes.c_int32()
+        msg = ctypes.create_string_buffer(4096)
+        self._chk(self.lib.nfk_jit_status(self.h, ctypes.byref(on), msg, len(msg)))
+        return bool(on.value), msg.value.decode()
+
     def row_words(self):
         n = ctypes.c_int32()
         self._chk(self.lib.nfk_row_words(self.h, ctypes.byref(n)))
@@ -378,6 +387,25 @@ class NFKernelModule:
 
     def reset_kernel_times(self):
         self._chk(self.lib.nfk_reset_kernel_times(self.h))
+
+
+def jit_preview(w, compile=False):
+    """nfk_jit_preview: the k_tick schema policy (JitSchema source) nfk_commit would generate for a
+    workload's schema, and with compile=True whether hipRTC builds k_tick<.., JitSchema> for gfx950
+    from it.  Needs no GPU.  Returns (source, ok, message)."""
+    lib = load_library()
+    _, n_int, n_flt, n_cls, n_kind = (int(x) for x in w["cfg"][:5])
+    flags = np.ascontiguousarray(np.asarray(w["prop_flags"])[:n_cls], np.uint8)
+    ops = np.ascontiguousarray(w["ops"][:n_kind])
+    n_ops = np.ascontiguousarray(w["n_ops"][:n_kind], np.int32)
+    ok = ctypes.c_int32()
+    src = ctypes.create_string_buffer(1 << 20)
+    msg = ctypes.create_string_buffer(1 << 16)
+    rc = lib.nfk_jit_preview(n_int, n_flt, n_cls, n_kind, _p(flags), _p(ops), _p(n_ops), int(compile),
+                             ctypes.byref(ok), src, len(src), msg, len(msg))
+    if rc != NFK_OK:
+        raise NFKError(rc, lib.nfk_last_error().decode())
+    return src.value.decode(), bool(ok.value), msg.value.decode()
 
 
 def world_from_workload(w, capacity=None, msg_capacity=0, stream=None, slack_per_256=0):

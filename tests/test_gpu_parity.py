@@ -13,16 +13,23 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
-# NFGPU_ABLATE=8 runs every frame through k_tick_touch (the per-entity written-property list used
-# when a schema's program working set does not fit k_tick's register slots); outputs stay exact
-PATHS = pytest.mark.parametrize("path", [0, 8], ids=["k_tick", "k_tick_touch"])
+# k_tick: the hipRTC specialisation built at nfk_commit (the default); k_tick_dyn: the library's
+# DynSchema instantiations (NFGPU_JIT=0); k_tick_touch: NFGPU_ABLATE=8 runs every frame through the
+# per-entity written-property list used when a schema's program working set does not fit k_tick's
+# register slots.  Outputs are exact on every path.
+PATHS = pytest.mark.parametrize("path", ["k_tick", "k_tick_dyn", "k_tick_touch"])
+
+
+def set_path(monkeypatch, path):
+    monkeypatch.setenv("NFGPU_ABLATE", "8" if path == "k_tick_touch" else "0")
+    monkeypatch.setenv("NFGPU_JIT", "0" if path == "k_tick_dyn" else "1")
 
 
 @PATHS
 @pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets", "tutorial3", "rmw",
                                   "lifecycle"])
 def test_gpu_matches_reference_golden(gpu_available, monkeypatch, name, path):
-    monkeypatch.setenv("NFGPU_ABLATE", str(path))
+    set_path(monkeypatch, path)
     w = nfio.read(os.path.join(GOLDEN, f"{name}.workload.nfio"))
     expected = nfio.read(os.path.join(GOLDEN, f"{name}.expected.nfio"))
     compare_runs(run_gpu(w), expected)
@@ -63,7 +70,7 @@ CASES = {
 @PATHS
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_gpu_matches_oracle(gpu_available, monkeypatch, case, path):
-    monkeypatch.setenv("NFGPU_ABLATE", str(path))
+    set_path(monkeypatch, path)
     w = workload.make_world(n_ticks=10, seed=sum(map(ord, case)), **CASES[case])
     compare_runs(run_gpu(w), run_oracle(w))
 
@@ -72,7 +79,7 @@ def test_gpu_matches_oracle(gpu_available, monkeypatch, case, path):
 def test_every_property_set_on_one_entity(gpu_available, monkeypatch, path):
     """One entity gets every property set in one frame, several of them twice, while its heartbeats
     fire: no per-entity limit (NFCKernelModule::SetPropertyInt/Float, KM:323-347, has none)."""
-    monkeypatch.setenv("NFGPU_ABLATE", str(path))
+    set_path(monkeypatch, path)
     w = workload.make_world(n_obj=700, n_scenes=1, groups_per_scene=3, players_per_group=5, n_ticks=6, seed=12,
                             ext_frac=0.0, burst_frac=0.01, burst_props=len(workload.PROPS))
     compare_runs(run_gpu(w), run_oracle(w))
@@ -330,3 +337,19 @@ def test_rank_top_matches_zrevrange(gpu_available, prop, k):
     assert list(zip(gh.tolist(), gd.tolist())) == list(zip(w["guid_head"][o].tolist(), w["guid_data"][o].tolist()))
     np.testing.assert_array_equal(sc, vals[o])
     m.close()
+
+
+def test_jit_specialisation_is_what_runs(gpu_available, monkeypatch):
+    """nfk_jit_status: with the default environment a world whose working set fits k_tick runs the
+    hipRTC build of k_tick for its schema; NFGPU_JIT=0 keeps the library's kernels."""
+    w = workload.make_world(n_obj=600, n_scenes=1, groups_per_scene=3, players_per_group=4, n_ticks=1, seed=5)
+    monkeypatch.setenv("NFGPU_JIT", "1")
+    m = kernel.world_from_workload(w)
+    on, msg = m.jit_status()
+    m.close()
+    assert on, msg
+    monkeypatch.setenv("NFGPU_JIT", "0")
+    m = kernel.world_from_workload(w)
+    on, msg = m.jit_status()
+    m.close()
+    assert not on and "NFGPU_JIT=0" in msg
