@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "entity-ticks/sec (update+dirty-diff+fanout) at 1M entities/GPU, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-KNAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles"]
+KNAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles", "membership"]
 CONFIG_NAMES = {
     0: "BASELINE config[0]: Tutorial3 (HelloWorld3Module.cpp) scaled to 10k NPC objects in scene 1 group 0: "
        "AddSchedule(self, \"OnHeartBeat\", 5.0, 10) per object (effect: World += 1, so its property callback "

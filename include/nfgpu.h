@@ -289,9 +289,14 @@ int nfk_jit_preview(int32_t n_int, int32_t n_flt, int32_t n_class, int32_t n_kin
 /* ---- measurement ---- */
 int nfk_set_profiling(void* world, int32_t on);
 /* accumulated device time (ms), launch count and algorithmic bytes per kernel:
- * 0 k_tick, 1 k_records, 2 k_fanout, 3 aux (queued host calls), 4 k_scan_tiles */
-#define NFK_N_KERNEL_TIMERS 5
-int nfk_kernel_times(void* world, double* ms /* [5] */, int64_t* launches /* [5] */, int64_t* bytes /* [5] */);
+ * 0 k_tick, 1 k_records, 2 k_fanout, 3 aux (queued host calls), 4 k_scan_tiles,
+ * 5 membership changes (k_seg_lists / k_pack / k_unpack / k_meta) */
+#define NFK_N_KERNEL_TIMERS 6
+int nfk_kernel_times(void* world, double* ms /* [6] */, int64_t* launches /* [6] */, int64_t* bytes /* [6] */);
+/* membership changes applied so far: windows that rewrote only the changed scene-group segments
+ * (n_seg) or rebuilt the segment table (n_full: a new scene group, or a segment out of slack), and
+ * the host milliseconds nfk_execute spent planning them (the device part is timer 5 above) */
+int nfk_membership_stats(void* world, int64_t* n_full, int64_t* n_seg, double* host_ms_full, double* host_ms_seg);
 int nfk_reset_kernel_times(void* world);
 
 #ifdef __cplusplus

@@ -1,6 +1,7 @@
 // nfgpu_host.hip — C-ABI implementation (include/nfgpu.h): world lifetime, schema,
 // membership layout, queued SetProperty / schedule calls, frame launch, readback.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -128,7 +129,7 @@ int dalloc(T** p, size_t n) {
     return NFK_OK;
 }
 
-enum { KT_TICK = 0, KT_REC = 1, KT_FAN = 2, KT_AUX = 3, KT_SCAN = 4, KT_N = 5 };
+enum { KT_TICK = 0, KT_REC = 1, KT_FAN = 2, KT_AUX = 3, KT_SCAN = 4, KT_MEM = 5, KT_N = 6 };
 
 struct PendingTiming {
     int kind;
@@ -156,6 +157,7 @@ struct World {
     // scene-group segments in (scene, group) order; slot range [base, base + cap)
     struct Seg {
         int32_t scene, group, base, cap;
+        int32_t np = 0;             // players among objs (set by seg_meta)
         std::vector<int32_t> objs;  // live objects, NFGUID order
     };
     std::vector<Seg> segs;
@@ -179,6 +181,9 @@ struct World {
     uint64_t* fan_desc_w = nullptr;
     int32_t* pl_slot_w = nullptr;
     int64_t n_relayout_full = 0, n_relayout_seg = 0;
+    double ms_relayout_full = 0, ms_relayout_seg = 0;  // host time in apply_membership
+    void* glist = nullptr;  // device-generated membership lists (untouched segments of a full re-layout)
+    size_t glist_cap = 0;
     std::vector<std::vector<uint64_t>> init_props;
     std::vector<std::vector<uint64_t>> init_rcells, init_rused;
     std::vector<bool> rec_defined;
@@ -448,10 +453,66 @@ struct MetaLists {
     std::vector<uint64_t> desc;
 };
 
-int seg_meta(World* w, const World::Seg& g, MetaLists& m) {
+// The pack / unpack lists and metadata of one rewritten segment in one pass over its members
+// (the per-object host arrays are read once per member, prefetched a few members ahead: members
+// are in NFGUID order, so their object indices are scattered).  all: every slot of the segment is
+// rewritten (a full re-layout); else only the slots whose occupant changes.
+int seg_lists(World* w, World::Seg& g, bool all, MetaLists& m, std::vector<int32_t>& pack_src,
+              std::vector<int32_t>& un_dst, std::vector<int64_t>& un_src) {
+    const int32_t n = (int32_t)g.objs.size();
+    const size_t at = m.slot.size();
+    m.slot.resize(at + g.cap);
+    m.obj.resize(at + g.cap);
+    m.desc.resize(at + g.cap);
+    m.pl.resize(at + g.cap, 0);
+    int32_t rank = 0;
+    for (int32_t i = 0; i < g.cap; i++) {
+        const int32_t ns = g.base + i;
+        m.slot[at + i] = ns;
+        if (i >= n) {
+            m.obj[at + i] = -1;
+            m.desc[at + i] = kDeadDesc;
+            if (all || w->obj_of_slot[ns] >= 0) {  // an entity left this slot: clear it
+                un_dst.push_back(ns);
+                un_src.push_back(kZeroRow);
+            }
+            continue;
+        }
+        if (i + 8 < n) {
+            const int32_t p = g.objs[i + 8];
+            __builtin_prefetch(&w->isplayer[p]);
+            __builtin_prefetch(&w->cls[p]);
+            __builtin_prefetch(&w->src_row[p]);
+            __builtin_prefetch(&w->slot_of_obj[p]);
+        }
+        const int32_t o = g.objs[i];
+        const bool pl = w->isplayer[o];
+        m.obj[at + i] = o;
+        m.desc[at + i] = (uint64_t)(uint32_t)g.base | ((uint64_t)(pl ? rank + 1 : 0) << 46) | ((uint64_t)w->cls[o] << 60);
+        if (pl) m.pl[at + rank++] = ns;
+        const int64_t sr = w->src_row[o];
+        const int32_t os = w->slot_of_obj[o];
+        if (sr >= 0) {
+            un_dst.push_back(ns);
+            un_src.push_back(-1 - sr);
+        } else if (all || os != ns) {
+            un_dst.push_back(ns);
+            un_src.push_back((int64_t)pack_src.size());
+            pack_src.push_back(os);
+        }
+    }
+    if (rank > 0x3FFF) return fail(NFK_ERR_ARG, "more than 16383 players in one scene group");
+    for (int32_t i = 0; i < n; i++) m.desc[at + i] |= (uint64_t)rank << 32;
+    g.np = rank;
+    w->max_np = std::max(w->max_np, rank);
+    return NFK_OK;
+}
+
+int seg_meta(World* w, World::Seg& g, MetaLists& m) {
     int32_t np = 0;
     for (int32_t o : g.objs) np += w->isplayer[o] ? 1 : 0;
     if (np > 0x3FFF) return fail(NFK_ERR_ARG, "more than 16383 players in one scene group");
+    g.np = np;
     w->max_np = std::max(w->max_np, np);
     const size_t at = m.slot.size();
     int32_t rank = 0;
@@ -748,6 +809,9 @@ unsigned grid_for(size_t work) { return (unsigned)std::max<size_t>(1, std::min<s
 // whose slack ran out rebuilds the whole layout.
 int apply_membership(World* w) {
     if (w->touched.empty()) return NFK_OK;
+    using clk = std::chrono::steady_clock;
+    const auto t_host = clk::now();
+    clk::time_point t_edit, t_lists, t_dev;
     Dev& d = w->d;
     const auto cmp = [w](int32_t a, int32_t b) { return guid_less(w, a, b); };
     // The new member lists are built on copies of the affected segments; nothing of the world
@@ -796,30 +860,78 @@ int apply_membership(World* w) {
     std::vector<int64_t> un_src;
     MetaLists m;
     std::vector<World::Seg> nsegs;
+    std::vector<int32_t> nsrc;   // full: nsegs[i] is untouched segment nsrc[i] (members kept), or -1
+    std::vector<SegMove> moves;  // full: untouched segments whose slot range changes
+    int32_t mv_rows_dev = 0, mv_list_dev = 0;
     const int32_t max_np0 = w->max_np;
+    t_edit = clk::now();
     if (full) {
-        int64_t total = plan_segments(w, w->slack, nsegs);
-        if (total > d.cap) total = plan_segments(w, 0, nsegs);
-        if (total > d.cap) return fail(NFK_ERR_CAPACITY, "entity capacity exceeded (nothing of the window applied)");
-        w->max_np = 0;  // recomputed by seg_meta over every segment below
-        for (const auto& g : nsegs) {
-            for (int32_t i = 0; i < g.cap; i++) {
-                const int32_t ns = g.base + i;
-                if (i >= (int32_t)g.objs.size()) {
-                    un_dst.push_back(ns);
-                    un_src.push_back(kZeroRow);
-                    continue;
-                }
-                const int32_t o = g.objs[i];
-                un_dst.push_back(ns);
-                if (w->src_row[o] >= 0) {
-                    un_src.push_back(-1 - w->src_row[o]);
-                } else {
-                    un_src.push_back((int64_t)pack_src.size());
-                    pack_src.push_back(w->slot_of_obj[o]);
-                }
+        // The (scene, group)-ordered segment table is rebuilt from the member lists: untouched
+        // segments keep theirs, edited ones take their edit copies, the objects of new (scene,
+        // group) pairs form new NFGUID-sorted segments, empty segments are dropped, and every
+        // segment gets a fresh base and slack.  Nothing of the world is sorted — the result is
+        // the layout a sort of every live object by (scene, group, NFGUID) would give.  The slot
+        // lists of edited and new segments are built here; those of the untouched segments (the
+        // bulk of the world) are generated on the device from their old and new ranges.
+        std::map<std::pair<int32_t, int32_t>, std::vector<int32_t>> fresh;
+        for (int32_t o : w->touched)
+            if (w->alive[o] && !w->seg_of.count({w->scene[o], w->group[o]}))
+                fresh[{w->scene[o], w->group[o]}].push_back(o);
+        for (auto& f : fresh) std::sort(f.second.begin(), f.second.end(), cmp);
+        auto fit = fresh.begin();
+        auto push_fresh = [&]() {
+            World::Seg g;
+            g.scene = fit->first.first;
+            g.group = fit->first.second;
+            g.objs = std::move(fit->second);
+            nsegs.push_back(std::move(g));
+            nsrc.push_back(-1);
+            ++fit;
+        };
+        for (int32_t gi = 0; gi < (int32_t)w->segs.size(); gi++) {
+            const World::Seg& old = w->segs[gi];
+            const std::pair<int32_t, int32_t> key{old.scene, old.group};
+            while (fit != fresh.end() && fit->first < key) push_fresh();
+            auto e = edit.find(gi);
+            if ((e != edit.end() ? e->second.objs : old.objs).empty()) continue;
+            World::Seg g;
+            g.scene = old.scene;
+            g.group = old.group;
+            if (e != edit.end()) g.objs = std::move(e->second.objs);
+            nsegs.push_back(std::move(g));
+            nsrc.push_back(e != edit.end() ? -1 : gi);
+        }
+        while (fit != fresh.end()) push_fresh();
+        auto members = [&](size_t i) -> const std::vector<int32_t>& {
+            return nsrc[i] >= 0 ? w->segs[nsrc[i]].objs : nsegs[i].objs;
+        };
+        auto assign = [&](int32_t sl) {
+            int64_t base = 0;
+            for (size_t i = 0; i < nsegs.size(); i++) {
+                const int32_t n = (int32_t)members(i).size();
+                nsegs[i].base = (int32_t)std::min<int64_t>(base, INT32_MAX);
+                nsegs[i].cap = n + seg_slack(sl, n);
+                base += nsegs[i].cap;
             }
-            int r = seg_meta(w, g, m);
+            return base;
+        };
+        int64_t total = assign(w->slack);
+        if (total > d.cap) total = assign(0);
+        if (total > d.cap) return fail(NFK_ERR_CAPACITY, "entity capacity exceeded (nothing of the window applied)");
+        w->max_np = 0;  // recomputed over every segment below
+        for (size_t i = 0; i < nsegs.size(); i++) {
+            World::Seg& g = nsegs[i];
+            if (nsrc[i] >= 0) {
+                const World::Seg& old = w->segs[nsrc[i]];
+                g.np = old.np;
+                w->max_np = std::max(w->max_np, g.np);
+                if (old.base == g.base && old.cap == g.cap) continue;  // stays where it is
+                moves.push_back({old.base, g.base, (int32_t)old.objs.size(), g.cap, old.np, mv_rows_dev, mv_list_dev, 0});
+                mv_rows_dev += (int32_t)old.objs.size();
+                mv_list_dev += g.cap;
+                continue;
+            }
+            int r = seg_lists(w, g, true, m, pack_src, un_dst, un_src);
             if (r) {
                 w->max_np = max_np0;
                 return r;
@@ -827,27 +939,8 @@ int apply_membership(World* w) {
         }
     } else {
         for (int32_t gi : aff) {
-            const World::Seg& g = edit[gi];
-            for (int32_t i = 0; i < g.cap; i++) {
-                const int32_t ns = g.base + i;
-                if (i >= (int32_t)g.objs.size()) {
-                    if (w->obj_of_slot[ns] >= 0) {  // an entity left this slot: clear it
-                        un_dst.push_back(ns);
-                        un_src.push_back(kZeroRow);
-                    }
-                    continue;
-                }
-                const int32_t o = g.objs[i];
-                if (w->src_row[o] >= 0) {
-                    un_dst.push_back(ns);
-                    un_src.push_back(-1 - w->src_row[o]);
-                } else if (w->slot_of_obj[o] != ns) {
-                    un_dst.push_back(ns);
-                    un_src.push_back((int64_t)pack_src.size());
-                    pack_src.push_back(w->slot_of_obj[o]);
-                }
-            }
-            int r = seg_meta(w, g, m);
+            World::Seg& g = edit[gi];
+            int r = seg_lists(w, g, false, m, pack_src, un_dst, un_src);
             if (r) {
                 w->max_np = max_np0;
                 return r;
@@ -855,34 +948,72 @@ int apply_membership(World* w) {
         }
     }
 
-    // device: pack movers (old slots), then unpack into the new layout, then the metadata
+    t_lists = clk::now();
+    // device: pack movers (old slots), then unpack into the new layout, then the metadata.  The
+    // untouched segments' lists (full re-layout) are generated first, from the old metadata.
     const int32_t rw = w->row_words;
     w->mhost.clear();
     const size_t o_ps = stage_list(w, pack_src), o_ud = stage_list(w, un_dst), o_us = stage_list(w, un_src);
     const size_t o_ms = stage_list(w, m.slot), o_mo = stage_list(w, m.obj), o_md = stage_list(w, m.desc);
-    const size_t o_mp = stage_list(w, m.pl);
-    int r = dev_reserve(w, (void**)&w->mv_rows, &w->mv_cap, std::max<size_t>(pack_src.size(), 1) * rw * 8);
+    const size_t o_mp = stage_list(w, m.pl), o_mv = stage_list(w, moves);
+    const size_t hp = pack_src.size();
+    int r = dev_reserve(w, (void**)&w->mv_rows, &w->mv_cap, std::max<size_t>(hp + (size_t)mv_rows_dev, 1) * rw * 8);
     if (r) return r;
+    // device-generated lists: pack_src | un_dst | un_src | m_slot | m_obj | m_desc | m_pl
+    const size_t nd = (size_t)mv_list_dev, npk = (size_t)mv_rows_dev;
+    const size_t g_ps = 0, g_ud = align16(g_ps + npk * 4), g_us = align16(g_ud + nd * 4), g_ms = align16(g_us + nd * 8),
+                 g_mo = align16(g_ms + nd * 4), g_md = align16(g_mo + nd * 4), g_mp = align16(g_md + nd * 8),
+                 g_end = align16(g_mp + nd * 4);
+    if (!moves.empty()) {
+        r = dev_reserve(w, (void**)&w->glist, &w->glist_cap, g_end);
+        if (r) return r;
+    }
     r = upload_mhost(w);
     if (r) return r;
-    char* L = (char*)w->mlist;
-    if (!pack_src.empty())
-        hipLaunchKernelGGL(k_pack, dim3(grid_for(pack_src.size() * rw)), dim3(kTPB), 0, w->stream, d,
-                           (const int32_t*)(L + o_ps), (int32_t)pack_src.size(), rw, w->mv_rows);
-    if (!un_dst.empty())
-        hipLaunchKernelGGL(k_unpack, dim3(grid_for(un_dst.size() * rw)), dim3(kTPB), 0, w->stream, d,
-                           (const int32_t*)(L + o_ud), (const int64_t*)(L + o_us), (int32_t)un_dst.size(), rw,
-                           (const uint64_t*)w->mv_rows, (const uint64_t*)w->ins_rows);
-    if (!m.slot.empty())
-        hipLaunchKernelGGL(k_meta, dim3(grid_for(m.slot.size())), dim3(kTPB), 0, w->stream,
-                           (const int32_t*)(L + o_ms), (const int32_t*)(L + o_mo), (const uint64_t*)(L + o_md),
-                           (const int32_t*)(L + o_mp), (int32_t)m.slot.size(), w->slot_obj_d, w->fan_desc_w,
-                           w->pl_slot_w);
-    HIPCHK(hipGetLastError());
+    {
+        TimeScope ts(w, KT_MEM);
+        char* L = (char*)w->mlist;
+        char* G = (char*)w->glist;
+        if (!moves.empty())
+            hipLaunchKernelGGL(k_seg_lists, dim3((unsigned)std::min<size_t>(moves.size(), 8192)), dim3(kTPB), 0,
+                               w->stream, (const SegMove*)(L + o_mv), (int32_t)moves.size(),
+                               (const int32_t*)w->slot_obj_d, (const uint64_t*)w->fan_desc_w,
+                               (const int32_t*)w->pl_slot_w, (int32_t*)(G + g_ps), (int32_t*)(G + g_ud),
+                               (int64_t*)(G + g_us), (int32_t*)(G + g_ms), (int32_t*)(G + g_mo), (uint64_t*)(G + g_md),
+                               (int32_t*)(G + g_mp));
+        if (hp)
+            hipLaunchKernelGGL(k_pack, dim3(grid_for(hp * rw)), dim3(kTPB), 0, w->stream, d,
+                               (const int32_t*)(L + o_ps), (int32_t)hp, rw, w->mv_rows);
+        if (npk)
+            hipLaunchKernelGGL(k_pack, dim3(grid_for(npk * rw)), dim3(kTPB), 0, w->stream, d,
+                               (const int32_t*)(G + g_ps), (int32_t)npk, rw, w->mv_rows + hp * rw);
+        if (!un_dst.empty())
+            hipLaunchKernelGGL(k_unpack, dim3(grid_for(un_dst.size() * rw)), dim3(kTPB), 0, w->stream, d,
+                               (const int32_t*)(L + o_ud), (const int64_t*)(L + o_us), (int32_t)un_dst.size(), rw,
+                               (const uint64_t*)w->mv_rows, (const uint64_t*)w->ins_rows);
+        if (nd)
+            hipLaunchKernelGGL(k_unpack, dim3(grid_for(nd * rw)), dim3(kTPB), 0, w->stream, d,
+                               (const int32_t*)(G + g_ud), (const int64_t*)(G + g_us), (int32_t)nd, rw,
+                               (const uint64_t*)(w->mv_rows + hp * rw), (const uint64_t*)w->ins_rows);
+        if (!m.slot.empty())
+            hipLaunchKernelGGL(k_meta, dim3(grid_for(m.slot.size())), dim3(kTPB), 0, w->stream,
+                               (const int32_t*)(L + o_ms), (const int32_t*)(L + o_mo), (const uint64_t*)(L + o_md),
+                               (const int32_t*)(L + o_mp), (int32_t)m.slot.size(), w->slot_obj_d, w->fan_desc_w,
+                               w->pl_slot_w);
+        if (nd)
+            hipLaunchKernelGGL(k_meta, dim3(grid_for(nd)), dim3(kTPB), 0, w->stream, (const int32_t*)(G + g_ms),
+                               (const int32_t*)(G + g_mo), (const uint64_t*)(G + g_md), (const int32_t*)(G + g_mp),
+                               (int32_t)nd, w->slot_obj_d, w->fan_desc_w, w->pl_slot_w);
+        HIPCHK(hipGetLastError());
+    }
 
+    t_dev = clk::now();
+    const size_t n_touched = w->touched.size();
     // host maps
     if (full) {
         w->n_relayout_full++;
+        for (size_t i = 0; i < nsegs.size(); i++)
+            if (nsrc[i] >= 0) nsegs[i].objs = std::move(w->segs[nsrc[i]].objs);
         w->segs = std::move(nsegs);
         w->seg_of.clear();
         for (size_t g = 0; g < w->segs.size(); g++) w->seg_of[{w->segs[g].scene, w->segs[g].group}] = (int32_t)g;
@@ -895,7 +1026,10 @@ int apply_membership(World* w) {
         for (size_t g = 0; g < w->segs.size(); g++) aff.push_back((int32_t)g);
     } else {
         w->n_relayout_seg++;
-        for (int32_t gi : aff) w->segs[gi].objs = std::move(edit[gi].objs);
+        for (int32_t gi : aff) {
+            w->segs[gi].objs = std::move(edit[gi].objs);
+            w->segs[gi].np = edit[gi].np;
+        }
     }
     for (int32_t o : w->touched)
         if (!w->alive[o]) w->slot_of_obj[o] = -1;
@@ -914,6 +1048,13 @@ int apply_membership(World* w) {
     }
     w->touched.clear();
     w->ins_n = 0;
+    const auto t_end = clk::now();
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    (full ? w->ms_relayout_full : w->ms_relayout_seg) += ms(t_host, t_end);
+    if (getenv("NFGPU_TRACE_MEMBERSHIP"))
+        fprintf(stderr, "apply_membership %s: %zu touched, edit %.3f ms, lists %.3f ms (%zu host entries, %zu moves), "
+                "upload+launch %.3f ms, host maps %.3f ms\n", full ? "full" : "seg", n_touched, ms(t_host, t_edit),
+                ms(t_edit, t_lists), un_dst.size(), moves.size(), ms(t_lists, t_dev), ms(t_dev, t_end));
     return NFK_OK;
 }
 
@@ -998,6 +1139,7 @@ int nfk_destroy(void* world) {
     if (w->ins_rows) (void)hipFree(w->ins_rows);
     if (w->mv_rows) (void)hipFree(w->mv_rows);
     if (w->mlist) (void)hipFree(w->mlist);
+    if (w->glist) (void)hipFree(w->glist);
     if (w->xs_buf) (void)hipFree(w->xs_buf);
     if (w->gat) (void)hipFree(w->gat);
     if (w->added_d) (void)hipFree(w->added_d);
@@ -1251,7 +1393,7 @@ int nfk_commit(void* world) {
     for (size_t g = 0; g < w->segs.size(); g++) w->seg_of[{w->segs[g].scene, w->segs[g].group}] = (int32_t)g;
     MetaLists meta;
     w->max_np = 0;
-    for (const auto& g : w->segs) {
+    for (auto& g : w->segs) {
         int r = seg_meta(w, g, meta);
         if (r) return r;
     }
@@ -2649,6 +2791,16 @@ int nfk_kernel_times(void* world, double* ms, int64_t* launches, int64_t* bytes)
         launches[i] = w->kt_n[i];
         bytes[i] = w->kt_bytes[i];
     }
+    return NFK_OK;
+}
+
+int nfk_membership_stats(void* world, int64_t* n_full, int64_t* n_seg, double* host_ms_full, double* host_ms_seg) {
+    World* w = (World*)world;
+    if (!w || !n_full || !n_seg || !host_ms_full || !host_ms_seg) return fail(NFK_ERR_ARG, "null argument");
+    *n_full = w->n_relayout_full;
+    *n_seg = w->n_relayout_seg;
+    *host_ms_full = w->ms_relayout_full;
+    *host_ms_seg = w->ms_relayout_seg;
     return NFK_OK;
 }
 

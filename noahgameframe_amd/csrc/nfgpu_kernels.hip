@@ -928,6 +928,47 @@ __global__ __launch_bounds__(kTPB) void k_unpack(Dev d, const int32_t* __restric
     }
 }
 
+// Full re-layout of the segments whose members did not change (only their slot range moves:
+// slack recomputed, segments inserted or dropped before them): their pack / unpack / metadata
+// lists are generated here from the segment table instead of on the host.  Reads the old
+// slot_obj / fan_desc / pl_slot (before k_meta rewrites them), rebasing descriptors and player
+// runs from ob to nb.
+struct SegMove {
+    int32_t ob, nb, n, nc;  // old base, new base, members, new slot count
+    int32_t np;             // players (the player run pl_slot[base, base + np))
+    int32_t po, lo, pad;    // first pack row, first list entry
+};
+
+__global__ __launch_bounds__(kTPB) void k_seg_lists(const SegMove* __restrict__ mv, int32_t n_mv,
+                                                    const int32_t* __restrict__ slot_obj,
+                                                    const uint64_t* __restrict__ fan_desc,
+                                                    const int32_t* __restrict__ pl_slot, int32_t* __restrict__ pack_src,
+                                                    int32_t* __restrict__ un_dst, int64_t* __restrict__ un_src,
+                                                    int32_t* __restrict__ m_slot, int32_t* __restrict__ m_obj,
+                                                    uint64_t* __restrict__ m_desc, int32_t* __restrict__ m_pl) {
+    for (int32_t g = blockIdx.x; g < n_mv; g += gridDim.x) {
+        const SegMove s = mv[g];
+        for (int32_t i = threadIdx.x; i < s.nc; i += kTPB) {
+            const int32_t at = s.lo + i, ns = s.nb + i;
+            un_dst[at] = ns;
+            m_slot[at] = ns;
+            if (i < s.n) {
+                const int32_t os = s.ob + i;
+                un_src[at] = s.po + i;
+                pack_src[s.po + i] = os;
+                m_obj[at] = slot_obj[os];
+                const uint64_t dsc = fan_desc[os];
+                m_desc[at] = (dsc & ~0xFFFFFFFFull) | (uint64_t)(uint32_t)s.nb;
+            } else {
+                un_src[at] = kZeroRow;  // a slack slot
+                m_obj[at] = -1;
+                m_desc[at] = kDeadDesc;
+            }
+            m_pl[at] = i < s.np ? pl_slot[s.ob + i] - s.ob + s.nb : 0;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kTPB) void k_meta(const int32_t* __restrict__ slot, const int32_t* __restrict__ obj,
                                                const uint64_t* __restrict__ desc, const int32_t* __restrict__ pl,
                                                int32_t n, int32_t* __restrict__ slot_obj,

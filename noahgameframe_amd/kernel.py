@@ -53,7 +53,7 @@ class Outputs(ctypes.Structure):
                   "msg_rcpt", "slot_obj"]])
 
 
-N_KERNEL_TIMERS = 5
+N_KERNEL_TIMERS = 6
 KERNEL_TIMER_NAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles"]
 
 
@@ -92,7 +92,7 @@ def load_library(path=LIB_PATH):
         "nfk_import_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
         "nfk_spawn_objects": [VP, I32, VP, VP, VP, VP, VP, VP, VP], "nfk_sync": [VP],
         "nfk_rank_top": [VP, I32, I32, VP, VP, VP, VP],
-        "nfk_jit_status": [VP, VP, VP, I32],
+        "nfk_jit_status": [VP, VP, VP, I32], "nfk_membership_stats": [VP, VP, VP, VP, VP],
         "nfk_jit_preview": [I32, I32, I32, I32, VP, VP, VP, I32, VP, VP, I32, VP, I32],
     }
     for name, args in sig.items():
@@ -244,6 +244,15 @@ class NFKernelModule:
         n = ctypes.c_int32()
         self._chk(self.lib.nfk_object_count(self.h, ctypes.byref(n)))
         return n.value
+
+    def membership_stats(self):
+        """{n_full, n_seg, host_ms_full, host_ms_seg}: membership windows applied by rebuilding the
+        segment table / by rewriting only changed segments, and their host planning time"""
+        nf, ns = ctypes.c_int64(), ctypes.c_int64()
+        mf, ms = ctypes.c_double(), ctypes.c_double()
+        self._chk(self.lib.nfk_membership_stats(self.h, ctypes.byref(nf), ctypes.byref(ns), ctypes.byref(mf),
+                                                ctypes.byref(ms)))
+        return {"n_full": nf.value, "n_seg": ns.value, "host_ms_full": mf.value, "host_ms_seg": ms.value}
 
     def jit_status(self):
         """(True, message) when k_tick runs the hipRTC specialisation built at commit"""
