@@ -313,9 +313,10 @@ def main():
     if args.config == 1:
         wl_name = ((f"BASELINE config[2]: {world} scene shards (scene r+1 on GPU r), "
                     f"{args.migrate} SwitchScene migrations per rank every {args.migrate_every} "
-                    "frames into the next shard (state rows over RCCL all_to_all); per GPU: ")
+                    f"frames into the next shard (state rows over {'RCCL' if args.backend == 'nccl' else 'gloo'} "
+                    "all_to_all); per GPU: ")
                    if migrating else "BASELINE config[1]: ") + (
-            "1M NPC/Player entities per GPU in one scene, "
+            f"{args.entities} NPC/Player entities per GPU in one scene, "
             f"{args.groups} groups x {args.entities // args.groups}, "
             f"{args.players_per_group} players/group, heartbeats HPRegen 1s/MPRegen 2s/"
             f"Move 0.1s/Patrol 3s/Poison 0.5s, {args.tick_ms} ms frames")
