@@ -9,7 +9,11 @@ namespace nfgpu {
 
 constexpr int kTPB = 256;     // 4 waves of 64
 constexpr int kTile = 256;    // slots per property/fired tile (one k_tick workgroup)
-constexpr int kRTile = 64;    // slots per record-event tile (one k_records wave)
+#ifndef NFGPU_RTILE
+#define NFGPU_RTILE 64
+#endif
+constexpr int kRTile = NFGPU_RTILE;  // slots per record-event tile (one k_records wave; <= 64)
+static_assert(kRTile >= 1 && kRTile <= 64, "a record tile is at most one wave of slots");
 
 // device error word bits (Ctrl::err)
 constexpr unsigned kErrMsgCap = 4, kErrTouch = 8, kErrFanBound = 16;
@@ -57,6 +61,7 @@ constexpr unsigned kAblNoRun = 512, kAblNoLoads = 1024, kAblNoEmit = 2048;  // t
 constexpr unsigned kAblNoWriteBack = 1u << 18, kAblNoSchedStore = 1u << 19;  // timing only (k_tick)
 constexpr unsigned kAblGroupColumns = 1u << 20, kAblSigGroups = 1u << 21;  // column layouts (outputs exact)
 constexpr unsigned kAblNoPad = 1u << 22;  // columns / schedule kinds at power-of-two strides (outputs exact)
+constexpr unsigned kAblRecVec = 1u << 23;  // k_records writes whole row-vectors back (outputs exact)
 // Pad between consecutive property columns and schedule-kind arrays (bytes): with cap a power of
 // two, unpadded columns sit exactly 2^k bytes apart and one entity's values of every column fall
 // on the same HBM channel.

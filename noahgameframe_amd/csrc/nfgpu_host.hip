@@ -742,7 +742,10 @@ void build_jit(World* w) {
         return;
     }
     const int u = std::max(w->d.n_u, 1);
-    int waves = tick_waves(w->d.n_u, w->d.ablate);
+    // The specialised kernel gets the register budget of 6 waves per SIMD: on config[1] it then
+    // allocates 78 VGPRs without spills, and at 7 (72 VGPRs, 6 spilled) it ran 6 % slower
+    // (profiles/r02t_ab_waves.txt: 101-102 vs 108 us).
+    int waves = (w->d.ablate & (kAblWaves6 | kAblWaves8 | kAblWaves5)) ? tick_waves(w->d.n_u, w->d.ablate) : kWavesJit;
     if (const char* ew = getenv("NFGPU_JIT_WAVES")) waves = std::max(1, std::min(8, atoi(ew)));
     const std::string src = jit_schema_source(w->tab, w->d);
     int dev = 0;
@@ -2758,7 +2761,7 @@ int nfk_jit_preview(int32_t n_int, int32_t n_flt, int32_t n_class, int32_t n_kin
         *ok = 1;
         return NFK_OK;
     }
-    const int u = std::max(d.n_u, 1), waves = tick_waves(d.n_u, 0);
+    const int u = std::max(d.n_u, 1), waves = kWavesJit;
     JitBuild b = jit_compile(s, waves, u);
     *ok = b.ok;
     copy_msg(b.ok ? b.lowered + " (" + std::to_string(b.code.size()) + " B code object)\n" + b.log : b.log, msg, msg_cap);

@@ -439,7 +439,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     // lane j holds slot s0 + j's fired mask and fan-out descriptor
     uint32_t my_mask = 0;
     uint64_t my_desc = 0;
-    if (s0 + lane < d.N) {
+    if (lane < kRTile && s0 + lane < d.N) {
         my_mask = d.fired_mask[s0 + lane] & d.rop_kinds;
         bytes += 4;
         if (my_mask) {
@@ -521,10 +521,23 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                 if (changed) {
                     // (non-temporal: the cell is not read again this frame; measured -7 % of k_records,
                     // while non-temporal event stores cost +30 %: profiles/r01zzf_*)
-                    __builtin_nontemporal_store(nb, ro.cells + ((size_t)e * ro.cols + ro.col) * ro.rows + lane);
+                    if (!(d.ablate & kAblRecVec))
+                        __builtin_nontemporal_store(nb, ro.cells + ((size_t)e * ro.cols + ro.col) * ro.rows + lane);
                     bytes += 8;
                     ch[j] = nb != c;  // coalesced diff: bits must differ
                     nv[j] = nb;
+                }
+            }
+            if (d.ablate & kAblRecVec) {
+                // whole row-vectors: every row of an operated column stored back (its new value or the
+                // value it had), so the column's lines are written in full
+#pragma unroll
+                for (int j = 0; j < kOps; j++) {
+                    if (j >= nro || !((G.masks[g] >> d.rops[j].kind) & 1)) continue;
+                    const RecOpX& ro = d.rops[j];
+                    if (lane < ro.rows)
+                        __builtin_nontemporal_store(ch[j] ? nv[j] : G.cur[g][j],
+                                                    ro.cells + ((size_t)e * ro.cols + ro.col) * ro.rows + lane);
                 }
             }
             // per-slot event order (rec, row, col): records outer, lanes (rows), cols inner

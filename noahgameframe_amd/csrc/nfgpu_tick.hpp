@@ -159,6 +159,7 @@ constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
 
 // k_tick register budgets (waves per SIMD) by the frame's U slot count
 constexpr int kWavesU8 = 8, kWavesU12 = 7;
+constexpr int kWavesJit = 6;  // the hipRTC specialisation (nfgpu_jit.hpp)
 constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: at most 4 GiB reserved
 
 // NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id

@@ -54,6 +54,8 @@ def main():
     low = msg2.split()[0] if ok2 else ""
     m = re.match(r"_ZN5nfgpu6k_tickILi(\d+)ELi(\d+)E", low)
     waves, u = (int(m.group(1)), int(m.group(2))) if m else (7, 12)
+    if len(sys.argv) > 2:
+        waves = int(sys.argv[2])
     with tempfile.TemporaryDirectory() as d:
         p = os.path.join(d, "jit.hip")
         with open(p, "w") as f:
@@ -62,8 +64,9 @@ def main():
             f.write(f"\ntemplate __global__ void nfgpu::k_tick<{waves}, {u}, nfgpu::JitSchema>(nfgpu::Dev);\n")
         for k in remarks(p):
             print("jit ", k)
-    for k in remarks(os.path.join(CSRC, "nfgpu_host.hip")):
-        print("lib ", k)
+    if len(sys.argv) <= 3:
+        for k in remarks(os.path.join(CSRC, "nfgpu_host.hip")):
+            print("lib ", k)
 
 
 if __name__ == "__main__":
