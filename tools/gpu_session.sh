@@ -21,7 +21,7 @@ run() {  # run <name> <seconds> <cmd...>
     *) echo "fatal rc=$rc in $name, stopping" | tee -a "$OUT/session.log"; exit $rc ;;
   esac
 }
-B="python bench.py --steps 20 --warmup 3 --cpu-baseline off ${PMCB:-}"
+B="python bench.py --steps 20 --warmup 3 --cpu-baseline off --host-calls off ${PMCB:-}"
 for step in "$@"; do
   case $step in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -39,9 +39,9 @@ for step in "$@"; do
                --entities 262144 --groups 1024 --migrate 128 --migrate-every 1 ;;
     ablate) run ablate 600 python tools/ablate.py --variants ${ABL:-0,8,4} ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-             python bench.py --steps 50 --warmup 5 --cpu-baseline off ;;
+             python bench.py --steps 50 --warmup 5 --cpu-baseline off --host-calls off ;;
     prof4) run prof4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof4" -o run -- \
-             python bench.py --config 4 --steps 20 --warmup 3 --cpu-baseline off ;;
+             python bench.py --config 4 --steps 20 --warmup 3 --cpu-baseline off --host-calls off ;;
     pmc)
       run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o run -- \
         tools/_bin/pmc_calib
