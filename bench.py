@@ -304,7 +304,7 @@ def main():
             pm = json.load(open(args.pmc_json))
             ent = pm.get(f"config{args.config}", {}).get(dom) or (pm.get(dom) if args.config == 1 else None)
             traffic = (ent or {}).get("hbm_bytes_per_launch")
-            traffic_src = pm.get("source") if traffic else None
+            traffic_src = ((pm.get(f"config{args.config}") or {}).get("source") or pm.get("source")) if traffic else None
         except Exception:
             traffic = None
     total_alg = sum(v["alg_bytes_per_launch"] or 0 for v in kern.values())

@@ -467,7 +467,8 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
         for (int g = 0; g < kGroup; g++) {
             G.js[g] = work ? __builtin_ctzll(work) : -1;
             if (work) work &= work - 1;
-            G.masks[g] = G.js[g] >= 0 ? (uint32_t)__shfl((int)my_mask, G.js[g], 64) : 0u;
+            // (js is wave-uniform: a lane read, not an LDS permute)
+            G.masks[g] = G.js[g] >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)my_mask, G.js[g]) : 0u;
         }
 #pragma unroll
         for (int g = 0; g < kGroup; g++)
@@ -488,7 +489,8 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
         for (int g = 0; g < kGroup; g++) {
             if (G.js[g] < 0) break;
             const int e = s0 + G.js[g];
-            const uint64_t desc = (uint64_t)__shfl((long long)my_desc, G.js[g], 64);
+            const uint64_t desc = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_desc, G.js[g]) |
+                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_desc >> 32), G.js[g]) << 32);
             const unsigned cls = (unsigned)(desc >> 60);
             bool ch[kOps];
             uint64_t nv[kOps];
@@ -545,13 +547,18 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             for (int j0 = 0; j0 < kOps; j0++) {
                 if (j0 >= nro || d.rops[j0].gfirst != j0) continue;  // j0 opens a record's op span
                 const int j1 = d.rops[j0].glast;
-                unsigned c = 0;
+                // the span's events before this lane's (rows below it, every column) and in total:
+                // one ballot + lane-mask count per op instead of a wave scan
+                unsigned below = 0, n = 0;
 #pragma unroll
-                for (int j = 0; j < kOps; j++) c += (j >= j0 && j <= j1 && ch[j]) ? 1 : 0;
-                const unsigned inc = wave_incl_scan_u32(c);
-                const unsigned n = (unsigned)__shfl((int)inc, 63, 64);
+                for (int j = 0; j < kOps; j++) {
+                    if (!(j >= j0 && j <= j1)) continue;
+                    const unsigned long long b = __ballot(ch[j]);
+                    below += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+                    n += (unsigned)__builtin_popcountll(b);
+                }
                 if (n == 0) continue;  // wave-uniform
-                unsigned p = pos + inc - c;
+                unsigned p = pos + below;
                 const uint8_t rfl = s_rflags[cls][d.rops[j0].rec];
                 const unsigned per = event_msgs(desc, rfl);
                 // stage the span's events in this wave's LDS rows at their span index, then write
