@@ -467,8 +467,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
         for (int g = 0; g < kGroup; g++) {
             G.js[g] = work ? __builtin_ctzll(work) : -1;
             if (work) work &= work - 1;
-            // (js is wave-uniform: a lane read, not an LDS permute)
-            G.masks[g] = G.js[g] >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)my_mask, G.js[g]) : 0u;
+            G.masks[g] = G.js[g] >= 0 ? (uint32_t)__shfl((int)my_mask, G.js[g], 64) : 0u;
         }
 #pragma unroll
         for (int g = 0; g < kGroup; g++)
@@ -489,8 +488,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
         for (int g = 0; g < kGroup; g++) {
             if (G.js[g] < 0) break;
             const int e = s0 + G.js[g];
-            const uint64_t desc = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my_desc, G.js[g]) |
-                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(my_desc >> 32), G.js[g]) << 32);
+            const uint64_t desc = (uint64_t)__shfl((long long)my_desc, G.js[g], 64);
             const unsigned cls = (unsigned)(desc >> 60);
             bool ch[kOps];
             uint64_t nv[kOps];
