@@ -435,7 +435,8 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     if (rt >= d.n_rtiles) return;  // wave-uniform; no barrier follows
     const int nro = d.n_rops;
     const int s0 = rt * kRTile;
-    unsigned bytes = 0;
+    unsigned bytes = 0;    // per lane
+    unsigned sbytes = 0;   // per wave (wave-uniform)
     // lane j holds slot s0 + j's fired mask and fan-out descriptor
     uint32_t my_mask = 0;
     uint64_t my_desc = 0;
@@ -490,18 +491,19 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             const int e = s0 + G.js[g];
             const uint64_t desc = (uint64_t)__shfl((long long)my_desc, G.js[g], 64);
             const unsigned cls = (unsigned)(desc >> 60);
-            bool ch[kOps];
+            bool ch[kOps], wr[kOps];
             uint64_t nv[kOps];
 #pragma unroll
             for (int j = 0; j < kOps; j++) {
-                ch[j] = false;
+                ch[j] = wr[j] = false;
                 nv[j] = 0;
                 if (j >= nro || !((G.masks[g] >> d.rops[j].kind) & 1)) continue;
                 const RecOpX& ro = d.rops[j];
-                if (lane == 0) bytes += 8;
+                // algorithmic bytes, counted per wave: the used mask and the used rows' cells
+                const uint64_t rowm = ro.rows >= 64 ? ~0ull : ((1ull << ro.rows) - 1);
+                sbytes += 8u + 8u * (unsigned)__builtin_popcountll(G.used[g][j] & rowm);
                 if (lane >= ro.rows || !((G.used[g][j] >> lane) & 1)) continue;
                 const uint64_t c = G.cur[g][j];
-                bytes += 8;
                 uint64_t nb;
                 bool changed;
                 if (ro.code == NFK_OP_RIADD_CLAMP) {
@@ -523,11 +525,14 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     // while non-temporal event stores cost +30 %: profiles/r01zzf_*)
                     if (!(d.ablate & kAblRecVec))
                         __builtin_nontemporal_store(nb, ro.cells + ((size_t)e * ro.cols + ro.col) * ro.rows + lane);
-                    bytes += 8;
+                    wr[j] = true;
                     ch[j] = nb != c;  // coalesced diff: bits must differ
                     nv[j] = nb;
                 }
             }
+#pragma unroll
+            for (int j = 0; j < kOps; j++)
+                if (j < nro) sbytes += 8u * (unsigned)__builtin_popcountll(__ballot(wr[j]));  // cells written
             if (d.ablate & kAblRecVec) {
                 // whole row-vectors: every row of an operated column stored back (its new value or the
                 // value it had), so the column's lines are written in full
@@ -595,12 +600,12 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                                 if (u + 1 == r1) continue;
                                 out[k++] = (uint32_t)d.pl_slot[(uint32_t)desc + u];
                             }
-                            bytes += 4 * np;
                         }
-                        bytes += 4 * per;
                     }
-                    bytes += 28;
                 }
+                // event records, their recipient words and (public) the player run read per event
+                sbytes += n * (28u + ((d.fuse_rec && per) ? 4u * per : 0u) +
+                               ((d.fuse_rec && per && (rfl & NFK_PUBLIC)) ? 4u * (uint32_t)((desc >> 32) & 0x3FFF) : 0u));
                 __builtin_amdgcn_wave_barrier();
                 pos += n;
                 pmsg += per * n;
@@ -620,7 +625,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
         d.t_re[rt] = pos;
         d.t_msg[d.n_tiles + rt] = pmsg;
     }
-    const unsigned wb = (unsigned)wave_sum(bytes);
+    const unsigned wb = (unsigned)wave_sum(bytes) + sbytes;
     if (lane == 0 && wb) tally_add(d, kTallyRec, (unsigned long long)wb + 8);
 }
 

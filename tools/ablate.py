@@ -16,12 +16,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--entities", type=int, default=1 << 20)
+    ap.add_argument("--config", type=int, default=1, help="1: bench_world, 4: record_world (steady)")
     a = ap.parse_args()
     import numpy as np
     import torch
     from noahgameframe_amd import kernel, workload
     torch.cuda.set_device(0)
-    w = workload.bench_world(n_obj=a.entities, n_ticks=1)
+    w = (workload.record_world(n_ticks=1, steady=True) if a.config == 4
+         else workload.bench_world(n_obj=a.entities, n_ticks=1))
     mods = {}
     for v in (int(x, 0) for x in a.variants.split(",")):
         os.environ["NFGPU_ABLATE"] = str(v)
@@ -33,7 +35,7 @@ def main():
         for _ in range(5):
             m.Execute(t0 + 100 * tick[v]); tick[v] += 1
         m.summary()
-    res = {v: {"k_tick": [], "k_fanout": []} for v in mods}
+    res = {v: {"k_tick": [], "k_records": [], "k_fanout": []} for v in mods}
     for r in range(a.rounds):
         for v, m in mods.items():
             m.reset_kernel_times()
@@ -43,6 +45,7 @@ def main():
             m.set_profiling(False)
             ms, n, b = m.kernel_times()
             res[v]["k_tick"].append(1000 * ms[0] / max(n[0], 1))
+            res[v]["k_records"].append(1000 * ms[1] / max(n[1], 1))
             res[v]["k_fanout"].append(1000 * ms[2] / max(n[2], 1))
     out = {v: {k: {"median_us": float(np.median(x)), "min_us": float(np.min(x))} for k, x in d.items()}
            for v, d in res.items()}
