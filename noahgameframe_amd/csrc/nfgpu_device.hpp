@@ -62,6 +62,7 @@ constexpr unsigned kAblNoWriteBack = 1u << 18, kAblNoSchedStore = 1u << 19;  // 
 constexpr unsigned kAblGroupColumns = 1u << 20, kAblSigGroups = 1u << 21;  // column layouts (outputs exact)
 constexpr unsigned kAblNoPad = 1u << 22;  // columns / schedule kinds at power-of-two strides (outputs exact)
 constexpr unsigned kAblRecVec = 1u << 23;  // k_records writes whole row-vectors back (outputs exact)
+constexpr unsigned kAblFanWin16 = 1u << 24, kAblFanWin32 = 1u << 25;  // k_tick fan-out LDS window up to 16 / 32 recipients (outputs exact)
 // Pad between consecutive property columns and schedule-kind arrays (bytes): with cap a power of
 // two, unpadded columns sit exactly 2^k bytes apart and one entity's values of every column fall
 // on the same HBM channel.

@@ -27,7 +27,7 @@ def main():
     mods = {}
     for v in (int(x, 0) for x in a.variants.split(",")):
         os.environ["NFGPU_ABLATE"] = str(v)
-        mods[v] = kernel.world_from_workload(w)
+        mods[v] = kernel.world_from_workload(w, slack_per_256=-1)  # as bench.py (no membership changes)
     os.environ.pop("NFGPU_ABLATE", None)
     t0 = int(w["tick_time"][0])
     tick = {v: 0 for v in mods}
