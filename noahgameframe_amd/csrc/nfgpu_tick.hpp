@@ -578,7 +578,36 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     }
                 }
                 __syncthreads();
-                if (!win) {
+                if (!win && !(d.ablate & kAblFan1)) {
+                    // lane groups of L/4 lanes, four consecutive recipients per lane in one 16-byte
+                    // store (dword-aligned: runs start anywhere); consecutive events' runs are
+                    // adjacent, so a wave writes 64 x 16 B of one contiguous stretch
+                    const uint32_t L4 = L >= 4 ? L / 4 : 1u, sub4 = threadIdx.x & (L4 - 1);
+                    for (uint32_t i = threadIdx.x / L4; i < c1 - c0; i += kTPB / L4) {
+                        const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
+                        const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;
+                        if (!(b >> 31)) {  // private & !upload: the entity itself (n is 0 or 1)
+                            if (sub4 == 0 && n) out[ms] = a;
+                            continue;
+                        }
+                        for (uint32_t p = 4 * sub4; p < n; p += 4 * L4) {  // every player of the group but self
+                            uint32_t x[4];
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                const uint32_t pq = p + (uint32_t)q;
+                                const uint32_t pp = pq + ((r1 && pq + 1 >= r1) ? 1u : 0u);
+                                x[q] = pq < n ? (staged ? s_pl[a - pb_lo + pp] : (uint32_t)d.pl_slot[a + pp]) : 0u;
+                            }
+                            if (p + 4 <= n) {
+                                *(u32x4_a4*)(out + ms + p) = u32x4_a4{x[0], x[1], x[2], x[3]};
+                            } else {
+#pragma unroll
+                                for (int q = 0; q < 3; q++)
+                                    if (p + (uint32_t)q < n) out[ms + p + q] = x[q];
+                            }
+                        }
+                    }
+                } else if (!win) {
                     for (uint32_t i = threadIdx.x / L; i < c1 - c0; i += kTPB / L) {
                         const uint32_t ms = s_ev[3 * i], a = s_ev[3 * i + 1], b = s_ev[3 * i + 2];
                         const uint32_t n = b & 0x3FFFu, r1 = (b >> 14) & 0x3FFFu;

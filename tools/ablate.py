@@ -16,13 +16,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--entities", type=int, default=1 << 20)
-    ap.add_argument("--config", type=int, default=1, help="1: bench_world, 4: record_world (steady)")
+    ap.add_argument("--config", type=int, default=1, help="1: bench_world, 3: fanout_world, 4: record_world (steady)")
     a = ap.parse_args()
     import numpy as np
     import torch
     from noahgameframe_amd import kernel, workload
     torch.cuda.set_device(0)
     w = (workload.record_world(n_ticks=1, steady=True) if a.config == 4
+         else workload.fanout_world(n_ticks=1) if a.config == 3
          else workload.bench_world(n_obj=a.entities, n_ticks=1))
     mods = {}
     for v in (int(x, 0) for x in a.variants.split(",")):
