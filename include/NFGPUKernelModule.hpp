@@ -19,8 +19,10 @@
 //     schedule name before AfterInit (an empty list for a functor-only heartbeat); the C++
 //     functor passed to AddSchedule still runs, after the device frame, with the reference's
 //     arguments (self, name, fTime, nCount), objects in NFGUID order and each object's schedules
-//     in name order, as NFCScheduleModule::Execute walks its maps (SM:52-80).  Its own Set calls
-//     land in the next frame.
+//     in name order, as NFCScheduleModule::Execute walks its maps (SM:52-80).  Its own Set,
+//     SwitchScene, Create/Destroy and Add/RemoveSchedule calls take effect in the same Execute
+//     (a second device pass, nfk_execute_calls; SetFunctorCallsSameFrame(false) defers them to the
+//     next frame).
 //   * SetProperty* calls are queued and applied at the start of the next Execute, in call order,
 //     through the reference's change predicates; GetProperty* sees them at once (read-your-writes);
 //     callbacks see coalesced (first old, last new) events once per frame, in (scene, group,
@@ -172,6 +174,12 @@ public:
     bool Shut();
     // the clock AddSchedule and Execute read (NFGetTime() by default)
     void SetTimeSource(std::function<int64_t()> now_ms);
+    // Calls that heartbeat functors make during Execute (Set*, SwitchScene, Create/Destroy,
+    // Add/RemoveSchedule) take effect within the same Execute, as in NFCScheduleModule::Execute
+    // (SM:65, SM:83-119): after the functors run, a second device pass applies them and their
+    // events are delivered before Execute returns (nfk_execute_calls).  Off: they land in the
+    // next frame.  Default on.
+    void SetFunctorCallsSameFrame(bool on) { same_frame_ = on; }
     int64_t Now() const { return clock_(); }
 
     // ---- NFIKernelModule ----
@@ -216,6 +224,9 @@ public:
 private:
     void check(int rc, const char* what) const;
     void DeliverEvents();
+    void TakeAddedSchedules();
+    bool same_frame_ = true;
+    int64_t pending_calls_ = 0;  // calls queued since the last device pass
     void* world_ = nullptr;
     int capacity_;
     void* stream_;

@@ -247,6 +247,13 @@ int nfk_read_added(void* world, int32_t cap, int32_t* n, int64_t* guid_head, int
  * + NFCSceneAOIModule::OnPropertyCommonEvent/GetBroadCastObject fan-out (AOI:227,260,531).
  * Asynchronous on the world's stream. */
 int nfk_execute(void* world, int64_t now_ms);
+/* The calls heartbeat functors made during a frame, applied within that frame: the queued
+ * SetProperty / SwitchScene / Create / Destroy / AddSchedule / RemoveSchedule calls take effect
+ * and their events and recipient lists replace the outputs, with no heartbeat scan (nothing is
+ * due).  In NFCScheduleModule::Execute a functor's Sets land at once (SM:65) and its
+ * Add/RemoveSchedule calls are applied at the end of the same walk (SM:83-119); the plugin calls
+ * this after running the frame's functors.  Asynchronous like nfk_execute. */
+int nfk_execute_calls(void* world);
 /* wait for everything queued on the world's stream */
 int nfk_sync(void* world);
 /* synchronise and read the counters of the last tick */

@@ -2333,6 +2333,12 @@ int nfk_execute(void* world, int64_t now_ms) {
     return NFK_OK;
 }
 
+int nfk_execute_calls(void* world) {
+    // a frame at the earliest time: `now > next` holds for no schedule, so nothing fires and no
+    // record is rescheduled; the queued calls run through the ordinary frame path
+    return nfk_execute(world, INT64_MIN);
+}
+
 int nfk_sync(void* world) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");

@@ -116,6 +116,7 @@ bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGrou
         const uint8_t cl = (uint8_t)c->second, pl = cls == "Player";
         check(nfk_spawn_objects(world_, 1, &self.nHead64, &self.nData64, &nSceneID, &nGroupID, &cl, &pl, row.data()),
               "nfk_spawn_objects");
+        pending_calls_++;
         obj_of_[self] = (int)guids_.size();
         guids_.push_back(self);
         scene_.push_back(nSceneID);
@@ -211,6 +212,7 @@ bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int 
     if (!scenes_.count(nTargetSceneID)) return false;       // "no this container" (KM:917)
     check(nfk_switch_scene(world_, self.nHead64, self.nData64, nTargetSceneID, nTargetGroupID, fX, fY, fZ),
           "nfk_switch_scene");
+    pending_calls_++;
     const int o = ObjectIndex(self);
     scene_[o] = nTargetSceneID;
     group_[o] = nTargetGroupID;
@@ -221,6 +223,7 @@ bool NFGPUKernelModule::DestroyObject(const NFGUID& self) {
     const int o = ObjectIndex(self);
     if (!committed_ || o < 0) return false;
     check(nfk_destroy_objects(world_, 1, &self.nHead64, &self.nData64), "nfk_destroy_objects");
+    pending_calls_++;
     obj_of_.erase(self);  // its object index stays reserved; later calls find no object
     for (auto it = sched_cb_.begin(); it != sched_cb_.end();)
         it = it->first.first == o ? sched_cb_.erase(it) : std::next(it);
@@ -252,7 +255,9 @@ bool NFGPUKernelModule::SetPropertyInt(const NFGUID& self, const std::string& na
     if (it == prop_id_.end() || props_[it->second].type != TDATA_INT || ObjectIndex(self) < 0) return false;
     int32_t pid = PropertyId(name);
     uint64_t b = (uint64_t)v;
-    return nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) == NFK_OK;
+    if (nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) != NFK_OK) return false;
+    pending_calls_++;
+    return true;
 }
 
 bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& name, double v) {
@@ -260,7 +265,9 @@ bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& 
     if (it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT || ObjectIndex(self) < 0) return false;
     int32_t pid = PropertyId(name);
     uint64_t b = bits_of(v);
-    return nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) == NFK_OK;
+    if (nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) != NFK_OK) return false;
+    pending_calls_++;
+    return true;
 }
 
 // NFCKernelModule::GetPropertyInt/Float (KM:401-425): the value after this window's queued Sets
@@ -315,6 +322,7 @@ bool NFGPUKernelModule::AddSchedule(const NFGUID& self, const std::string& name,
     check(nfk_add_schedules(world_, 1, &self.nHead64, &self.nData64, &kind, &fTime, &nCount, &now),
           "nfk_add_schedules");
     sched_add_.emplace(std::make_pair(o, kind), std::make_pair(cb, fTime));  // the window's first call wins
+    pending_calls_++;
     return true;
 }
 
@@ -325,6 +333,7 @@ bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self, const std::string& na
     if (!committed_ || ObjectIndex(self) < 0) return false;
     check(nfk_remove_schedule(world_, self.nHead64, self.nData64, k == hb_id_.end() ? -1 : k->second),
           "nfk_remove_schedule");
+    pending_calls_++;
     return true;
 }
 
@@ -332,6 +341,7 @@ bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self, const std::string& na
 bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self) {
     if (!committed_ || ObjectIndex(self) < 0) return false;
     check(nfk_remove_all_schedules(world_, self.nHead64, self.nData64), "nfk_remove_all_schedules");
+    pending_calls_++;
     return true;
 }
 
@@ -356,7 +366,9 @@ bool NFGPUKernelModule::ExistSchedule(const std::string& name) { return module_s
 
 bool NFGPUKernelModule::Execute() {
     check(nfk_execute(world_, clock_()), "nfk_execute");
+    pending_calls_ = 0;
     check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
+    TakeAddedSchedules();  // the AddSchedule calls this frame applied: their functors fire from now on
     const bool want_events = !common_prop_cb_.empty() || !aoi_prop_cb_.empty() || !common_rec_cb_.empty() ||
                              !aoi_rec_cb_.empty();
     // heartbeat functors with the reference's arguments, in the order NFCScheduleModule::Execute
@@ -375,25 +387,37 @@ bool NFGPUKernelModule::Execute() {
                 it->second(guids_[fo[i]], heartbeats_[fk[i]].name, sched_time_[{fo[i], fk[i]}], fr[i]);
         }
     }
-    // this window's AddSchedule calls that created a schedule: their functors fire from now on
-    if (!sched_add_.empty()) {
-        const int32_t cap = (int32_t)sched_add_.size();
-        std::vector<int64_t> ah(cap), ad(cap);
-        std::vector<int32_t> ak(cap);
-        int32_t n = 0;
-        check(nfk_read_added(world_, cap, &n, ah.data(), ad.data(), ak.data()), "nfk_read_added");
-        for (int32_t i = 0; i < std::min(n, cap); i++) {
-            const int o = ObjectIndex(NFGUID(ah[i], ad[i]));
-            auto it = sched_add_.find({o, ak[i]});
-            if (it == sched_add_.end()) continue;
-            sched_cb_[{o, ak[i]}] = it->second.first;
-            sched_time_[{o, ak[i]}] = it->second.second;
-        }
-        sched_add_.clear();
-    }
     if (want_events) DeliverEvents();
+    // what the functors called takes effect in this Execute (SM:65: their Sets land at once;
+    // SM:83-119: their Add/RemoveSchedule calls are applied at the end of the walk)
+    if (same_frame_ && pending_calls_) {
+        check(nfk_execute_calls(world_), "nfk_execute_calls");
+        pending_calls_ = 0;
+        check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
+        TakeAddedSchedules();
+        if (want_events) DeliverEvents();
+    }
     module_sched_.Execute(clock_);  // module schedules (SM:123-176)
     return true;
+}
+
+// AddSchedule calls that the last device pass applied and that created a schedule: their functors
+// fire from now on (the first call of a name wins, SM:218-238; nfk_read_added says which)
+void NFGPUKernelModule::TakeAddedSchedules() {
+    if (sched_add_.empty()) return;
+    const int32_t cap = (int32_t)sched_add_.size();
+    std::vector<int64_t> ah(cap), ad(cap);
+    std::vector<int32_t> ak(cap);
+    int32_t n = 0;
+    check(nfk_read_added(world_, cap, &n, ah.data(), ad.data(), ak.data()), "nfk_read_added");
+    for (int32_t i = 0; i < std::min(n, cap); i++) {
+        const int o = ObjectIndex(NFGUID(ah[i], ad[i]));
+        auto it = sched_add_.find({o, ak[i]});
+        if (it == sched_add_.end()) continue;
+        sched_cb_[{o, ak[i]}] = it->second.first;
+        sched_time_[{o, ak[i]}] = it->second.second;
+    }
+    sched_add_.clear();
 }
 
 void NFGPUKernelModule::DeliverEvents() {

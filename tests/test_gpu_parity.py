@@ -353,3 +353,55 @@ def test_jit_specialisation_is_what_runs(gpu_available, monkeypatch):
     on, msg = m.jit_status()
     m.close()
     assert not on and "NFGPU_JIT=0" in msg
+
+
+def _functor_frame_log(same):
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "_bin", "functor_frame")
+    out = subprocess.run([exe, str(int(same))], check=True, capture_output=True, text=True, timeout=120).stdout
+    rows = []
+    for line in out.splitlines():
+        kind, *kv = line.split()
+        d = {"kind": kind}
+        for x in kv:
+            if "=" in x:
+                k, v = x.split("=", 1)
+                d[k] = v
+            else:
+                d.setdefault("rest", []).append(x)
+        rows.append(d)
+    return rows
+
+
+def test_functor_calls_land_in_the_same_frame(gpu_available):
+    """A heartbeat functor's own calls (NFCScheduleModule::Execute runs it inside the walk, SM:65):
+    its SetPropertyInt lands in the same Execute — the property event is delivered before Execute
+    returns and GetPropertyInt after it sees the value — and its AddSchedule is applied at the end of
+    the same walk (SM:83-119), so the new schedule's functor fires from the next frame on.  With
+    SetFunctorCallsSameFrame(false) the same calls land one frame later (tests/cpp/functor_frame.cpp)."""
+    rows = _functor_frame_log(True)
+    fires = [r for r in rows if r["kind"] == "fire"]
+    events = [r for r in rows if r["kind"] == "event"]
+    regen = [r for r in fires if "Regen" in r["rest"]]
+    bonus = [r for r in fires if "Bonus" in r["rest"]]
+    assert len(regen) == 6 and sorted({r["frame"] for r in regen}) == ["1", "2", "3"]
+    for r in regen:   # every Regen fire's HP += 1 is an event of the same frame
+        assert any(e["frame"] == r["frame"] and e["obj"] == r["obj"] and "HP" in e["rest"] for e in events), r
+    # the Bonus schedule added by Regen's 2nd fire (frame 1) fires in frames 2 and 3
+    assert sorted((r["frame"], r["obj"]) for r in bonus) == [("2", "100"), ("2", "101"), ("3", "100"), ("3", "101")]
+    for r in bonus:
+        assert any(e["frame"] == r["frame"] and e["obj"] == r["obj"] and "Level" in e["rest"] for e in events), r
+    state = {(r["frame"], r["obj"]): r for r in rows if r["kind"] == "state"}
+    for f in range(6):
+        n_regen = min(max(f, 0), 3)   # fires in frames 1..3
+        for i, obj in enumerate(("100", "101")):
+            assert int(state[(str(f), obj)]["HP"]) == 10 * i + n_regen
+    assert state[("3", "100")]["Bonus"] == "0"   # exhausted in frame 3 (first in name order)
+
+    late = _functor_frame_log(False)
+    ev_late = [r for r in late if r["kind"] == "event" and "HP" in r["rest"]]
+    fires_late = [r for r in late if r["kind"] == "fire" and "Regen" in r["rest"]]
+    assert sorted({r["frame"] for r in fires_late}) == ["1", "2", "3"]
+    for r in fires_late:   # deferred: the HP event of a fire in frame f arrives in frame f + 1
+        assert any(e["frame"] == str(int(r["frame"]) + 1) and e["obj"] == r["obj"] for e in ev_late), r
+    assert not any(e["frame"] == "1" for e in ev_late)
