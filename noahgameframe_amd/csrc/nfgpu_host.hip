@@ -747,7 +747,9 @@ void build_jit(World* w) {
     // (profiles/r02t_ab_waves.txt: 101-102 vs 108 us).
     int waves = (w->d.ablate & (kAblWaves6 | kAblWaves8 | kAblWaves5)) ? tick_waves(w->d.n_u, w->d.ablate) : kWavesJit;
     if (const char* ew = getenv("NFGPU_JIT_WAVES")) waves = std::max(1, std::min(8, atoi(ew)));
-    const std::string src = jit_schema_source(w->tab, w->d);
+    const char* es = getenv("NFGPU_JIT_SPEC");
+    const bool spec = es && es[0] == '1';  // every program operand loaded with the schedule records
+    const std::string src = jit_schema_source(w->tab, w->d, spec);
     int dev = 0;
     (void)hipGetDevice(&dev);
     const std::string key = std::to_string(dev) + "|" + std::to_string(waves) + "|" + std::to_string(u) + "|" + src;
@@ -2761,7 +2763,8 @@ int nfk_jit_preview(int32_t n_int, int32_t n_flt, int32_t n_class, int32_t n_kin
         copy_msg("working set does not fit k_tick (k_tick_touch runs)", msg, msg_cap);
         return NFK_OK;
     }
-    const std::string s = jit_schema_source(*tab, d);
+    const char* es = getenv("NFGPU_JIT_SPEC");
+    const std::string s = jit_schema_source(*tab, d, es && es[0] == '1');
     copy_msg(s, src, src_cap);
     if (!compile) {
         *ok = 1;

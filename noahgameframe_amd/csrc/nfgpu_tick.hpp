@@ -132,6 +132,7 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
 // has the same members as constants and the programs as straight-line code on the registers.
 struct DynSchema {
     static constexpr bool kStatic = false;
+    static constexpr uint32_t kSpecMask = 0;  // operands loaded before the fire test (none)
     static constexpr int kNK = NFK_MAX_KINDS;  // (an upper bound only)
     __device__ static int n_kind(const Dev& d) { return d.n_kind; }
     __device__ static int n_w(const Dev& d) { return d.n_w; }
@@ -275,9 +276,18 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         // descriptor and schedule records in one round trip, without a branch: slots past N (the
         // last tile) re-read slot N-1 and count as dead; a dead slot stores nothing
         const int ec = e < d.N ? e : d.N - 1;
+        if constexpr (S::kSpecMask != 0) {
+            // a policy may load every program operand with the schedule records, before it knows
+            // which kinds fire: one round trip instead of two (sparse kinds' columns are read in
+            // lines that mostly have to be fetched anyway)
+            if (!(d.ablate & kAblNoLoads))
+#pragma unroll
+                for (int j = 0; j < kU; j++)
+                    if ((S::kSpecMask >> j) & 1) v[j] = d.u_col[j][(size_t)ec * d.u_str[j]];
+        }
         fired = sched_scan<S>(d, ec, bytes, desc, s_rem, e >= d.N);  // NFCScheduleModule::Execute (SM:51-81)
         desc = e < d.N ? desc : kDeadDesc;
-        bytes = e < d.N ? bytes + 8 : 0u;
+        bytes = e < d.N ? bytes + 8 + 8u * (uint32_t)__builtin_popcount(S::kSpecMask) : 0u;
     }
     const bool live = !desc_dead(desc);
     // queued Set groups of this slot (k_sets ran them): program destinations among them
@@ -298,7 +308,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         // one batch of independent loads: every value this entity's frame reads or writes
 #pragma unroll
         for (int j = 0; j < kU; j++)
-            if (((need >> j) & 1) && !(d.ablate & kAblNoLoads)) {
+            if (((need >> j) & 1) && !((S::kSpecMask >> j) & 1) && !(d.ablate & kAblNoLoads)) {
                 v[j] = d.u_col[j][(size_t)e * d.u_str[j]];
                 bytes += 8;
             }
