@@ -1968,6 +1968,10 @@ int nfk_execute(void* world, int64_t now_ms) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    using clk = std::chrono::steady_clock;
+    const bool trace = getenv("NFGPU_TRACE_EXEC") != nullptr;  // host phases to stderr
+    clk::time_point tp[6];
+    tp[0] = clk::now();
     {
         int r = check_fanout(w);  // the last frame's fan-out is complete before it is replaced
         if (r) return r;
@@ -1996,6 +2000,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     Dev d = w->d;
     d.now = now_ms;
 
+    tp[1] = clk::now();
     // ---- host-side preparation of queued calls ----
     // SetProperty*: (slot, property) groups, each group's calls in call order (a stable radix sort
     // by slot << 7 | property); the most standalone groups (properties no program writes) of one
@@ -2052,6 +2057,7 @@ int nfk_execute(void* world, int64_t now_ms) {
             d.ev_new = w->d.ev_new; d.ev_moff = w->d.ev_moff;
         }
     }
+    tp[2] = clk::now();
     // schedule calls: pre-scan (remove-list key owner, RemoveSchedule(self)) and post-scan (remove,
     // add), folded per (slot, kind) in call order (a stable radix sort by slot << 5 | kind):
     //  * RemoveSchedule(self) erases the object's schedules at once (SM:240-243);
@@ -2128,6 +2134,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     // working set does not fit the register slots runs k_tick_touch
     const bool use_u = w->u_ok && !(d.ablate & kAblPerKind);
 
+    tp[3] = clk::now();
     // ---- uploads through the pinned arena ----
     const size_t ng = g_slot.size(), npre = pre_slot.size(), npost = post.size();
     size_t off_xs = 0, off_xp = align16(off_xs + ng * 4), off_xf = align16(off_xp + ng * 4);
@@ -2168,6 +2175,7 @@ int nfk_execute(void* world, int64_t now_ms) {
         HIPCHK(hipEventRecord(w->pin_done, w->stream));
         w->pin_pending = true;
     }
+    tp[4] = clk::now();
     char* S = (char*)w->stage;
     d.n_x = (int32_t)ng;
     d.x_slot = ng ? (const uint32_t*)(S + off_xs) : nullptr;
@@ -2332,6 +2340,13 @@ int nfk_execute(void* world, int64_t now_ms) {
         w->fan_unchecked = true;
     }
     w->ticks++;
+    if (trace) {
+        tp[5] = clk::now();
+        auto ms = [&](int a, int b) { return std::chrono::duration<double, std::milli>(tp[b] - tp[a]).count(); };
+        fprintf(stderr, "nfk_execute: membership+slots %.3f ms, SetProperty groups %.3f ms (%zu calls), schedule "
+                "calls %.3f ms (%zu), upload %.3f ms, launches %.3f ms\n", ms(0, 1), ms(1, 2), w->xops.size(), ms(2, 3),
+                w->hops.size(), ms(3, 4), ms(4, 5));
+    }
     return NFK_OK;
 }
 
