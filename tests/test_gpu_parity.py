@@ -61,6 +61,11 @@ CASES = {
                               rec_rows=32, spawn_frac=0.03, destroy_frac=0.03, switch_frac=0.01),
     "read_modify_write": dict(n_obj=3000, n_scenes=2, groups_per_scene=6, players_per_group=4, ext_frac=0.05,
                               ext_props="all", rmw_frac=0.03, switch_frac=0.01, host_ops=True),
+    # create / destroy, switches into new groups, read-modify-write Sets, schedule calls and the
+    # rescheduling edge cases in one world (also checked oracle vs reference: test_oracle.py seed 9)
+    "combined": dict(n_obj=3000, n_scenes=3, groups_per_scene=6, players_per_group=4, ext_frac=0.05, host_ops=True,
+                     sched_edges=True, switch_frac=0.02, switch_new_groups=True, rmw_frac=0.02, spawn_frac=0.03,
+                     destroy_frac=0.03),
     "wide_sets_records": dict(n_obj=3000, n_scenes=2, groups_per_scene=5, players_per_group=6, records=True,
                               rec_rows=32, ext_frac=0.1, ext_props="all", burst_frac=0.02, burst_props=24,
                               switch_frac=0.01),

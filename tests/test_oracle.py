@@ -51,6 +51,13 @@ def test_golden_fixtures_are_nontrivial():
     # SetProperty on any property (program operands too) and 24-property bursts per entity
     (8, dict(n_obj=600, n_scenes=2, groups_per_scene=4, players_per_group=3, ext_frac=0.15, ext_props="all",
              burst_frac=0.04, burst_props=24, host_ops=True, switch_frac=0.02)),
+    # everything at once: create / destroy between frames, scene switches into new groups,
+    # read-modify-write Sets, schedule calls and the rescheduling edge cases
+    (9, dict(n_obj=700, n_scenes=3, groups_per_scene=4, players_per_group=3, ext_frac=0.05, host_ops=True,
+             sched_edges=True, switch_frac=0.02, switch_new_groups=True, rmw_frac=0.02, spawn_frac=0.03,
+             destroy_frac=0.03)),
+    # one large scene group (40 players) with Sets and schedule calls
+    (10, dict(n_obj=500, n_scenes=1, groups_per_scene=2, players_per_group=40, ext_frac=0.08, host_ops=True)),
 ])
 def test_oracle_matches_reference(seed, kw):
     w = workload.make_world(n_ticks=9, seed=seed, **kw)
