@@ -106,7 +106,8 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
                tick_ms=100, seed=1, ext_frac=0.05, host_ops=True, records=False, rec_rows=64,
                t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, rec_skill_op=False, sched_edges=False,
                switch_frac=0.0, switch_new_groups=False, rec_steady=False, ext_props=None, burst_frac=0.0,
-               burst_props=20, rmw_frac=0.0, spawn_frac=0.0, destroy_frac=0.0):
+               burst_props=20, rmw_frac=0.0, spawn_frac=0.0, destroy_frac=0.0, rec_set_frac=0.0,
+               rec_set_float=True):
     if spawn_frac > 0 or destroy_frac > 0:
         return _lifecycle_world(locals())
     rng = np.random.default_rng(seed)
@@ -383,7 +384,42 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
             used &= np.uint64((1 << rows) - 1)
         w["rec0_cells"] = cells
         w["rec0_used"] = used
+        if rec_set_frac > 0:
+            w.update(_record_sets(rng, n_obj, n_ticks, rows, cols, rec_set_frac, rec_set_float))
     return w
+
+
+def _record_sets(rng, n_obj, n_ticks, rows, cols, frac, with_float):
+    """NFIKernelModule::SetRecordInt / SetRecordFloat calls between frames (r_*, call order within
+    a window): random (object, row, col) cells of record 0 — rows used or not (a Set on an unused
+    row is refused, RC:194) — with a third of them set twice in the window (coalesced to one event)
+    and some set to the value they already hold (no event).  with_float=False keeps to the int
+    columns (the reference's own NFCRecord::SetFloat is broken, see test_reference_record_setfloat_bug)."""
+    rt, ro, rr, rw, rc, rb = [], [], [], [], [], []
+    ncol = cols if with_float else 2
+    for t in range(1, n_ticks):
+        k = int(frac * n_obj)
+        if k <= 0:
+            continue
+        o = rng.integers(0, n_obj, k)
+        row = rng.integers(0, rows, k)
+        col = rng.integers(0, ncol, k)
+        again = rng.random(k) < 0.33
+        o, row, col = (np.concatenate([x, x[again]]) for x in (o, row, col))
+        iv = rng.integers(0, 5000, len(o)).astype(np.int64)
+        iv[rng.random(len(o)) < 0.1] = 0                 # often the value a cooldown already holds
+        fv = rng.uniform(-50.0, 50.0, len(o))
+        bits = np.where(col == 2, fv.view(np.int64), iv).astype(np.int64).view(np.uint64)
+        perm = rng.permutation(len(o))                   # call order within the window
+        rt.append(np.full(len(o), t))
+        ro.append(o[perm])
+        rr.append(row[perm])
+        rw.append(col[perm])
+        rb.append(bits[perm])
+    cat = lambda lst, dt: np.concatenate(lst).astype(dt) if lst else np.zeros(0, dt)
+    n = sum(len(x) for x in rt)
+    return dict(r_tick=cat(rt, np.int32), r_obj=cat(ro, np.int32), r_rec=np.zeros(n, np.int32),
+                r_row=cat(rr, np.int32), r_col=cat(rw, np.int32), r_bits=cat(rb, np.uint64))
 
 
 def _lifecycle_world(kw):
@@ -431,6 +467,10 @@ def _lifecycle_world(kw):
     keep = alive_at(w["x_obj"], w["x_tick"], True)
     for k in ("x_tick", "x_obj", "x_pid", "x_bits", "x_mode"):
         if k in w:
+            w[k] = w[k][keep]
+    if "r_tick" in w:   # SetRecord* calls: like SetProperty
+        keep = alive_at(w["r_obj"], w["r_tick"], True)
+        for k in ("r_tick", "r_obj", "r_rec", "r_row", "r_col", "r_bits"):
             w[k] = w[k][keep]
     keep = alive_at(w["h_obj"], w["h_tick"], False)
     for k in ("h_tick", "h_op", "h_obj", "h_kind", "h_interval", "h_count", "h_time"):

@@ -22,6 +22,8 @@
  *   create_object  NFComm/NFKernelPlugin/NFCKernelModule.cpp:101-271 after start (the object
  *                  joins its scene group with its creation-time values; no schedules until an
  *                  AddSchedule; creation values are not dirty events)
+ *   set_record     NFComm/NFKernelPlugin/NFCKernelModule.cpp:505/545 (SetRecordInt/Float between
+ *                  frames) -> set_rint / set_rflt, refused on an unused row (NFCRecord.cpp:194)
  *   destroy_object NFComm/NFKernelPlugin/NFCKernelModule.cpp:273-308 (RemoveObjectFromGroup,
  *                  RemoveSchedule(self) which erases at once, NFCScheduleModule.cpp:240; the
  *                  object's events of the window are dropped with it)
@@ -453,6 +455,16 @@ int main(int argc, char** argv) {
     nfio_writer w;
     if (nfio_wopen(&w, argv[2]) != 0) die("cannot open output");
     int64_t xi = 0, hi = 0;
+    /* SetRecordInt / SetRecordFloat calls between frames (optional r_* arrays, call order) */
+    nfio_arr* rta = nfio_get(&wf, "r_tick");
+    const int64_t NRS = rta ? (int64_t)rta->shape[0] : 0;
+    int32_t* r_tick = NRS ? (int32_t*)rta->data : NULL;
+    int32_t* r_obj = NRS ? (int32_t*)GET("r_obj")->data : NULL;
+    int32_t* r_rec = NRS ? (int32_t*)GET("r_rec")->data : NULL;
+    int32_t* r_row = NRS ? (int32_t*)GET("r_row")->data : NULL;
+    int32_t* r_col = NRS ? (int32_t*)GET("r_col")->data : NULL;
+    uint64_t* r_bits = NRS ? (uint64_t*)GET("r_bits")->data : NULL;
+    int64_t ri = 0;
 
     for (int t = 0; t < NT; t++) {
         int64_t now = tick_time[t];
@@ -520,6 +532,18 @@ int main(int argc, char** argv) {
             else set_flt(o, pid, rmw ? fget(o, pid) + bitsd(x_bits[xi]) : bitsd(x_bits[xi]));
             xi++;
         }
+        /* SetRecordInt / SetRecordFloat (NFCKernelModule -> NFCRecord::SetInt / SetFloat, RC:182 /
+         * RC:243) made before this Execute, in call order: refused on a row that is not used
+         * (RC:194) or a column of the other type; the change predicates of set_rint / set_rflt */
+        while (ri < NRS && r_tick[ri] == t) {
+            int32_t o = r_obj[ri], r = r_rec[ri], row = r_row[ri], col = r_col[ri];
+            if (alive[o] && r >= 0 && r < NR && row >= 0 && row < rec_rows[r] && col >= 0 && col < rec_cols[r] &&
+                ((rused[r][o] >> row) & 1)) {
+                if (rec_ctype[r][col]) set_rflt(r, o, row, col, bitsd(r_bits[ri]));
+                else set_rint(r, o, row, col, (int64_t)r_bits[ri]);
+            }
+            ri++;
+        }
         /* DestroyObject (KM:273-308), the window's last calls: the object leaves its group,
          * RemoveSchedule(self) erases its schedules at once (SM:240), and its events of this
          * window go with it */
@@ -537,6 +561,10 @@ int main(int argc, char** argv) {
                 for (int64_t i = 0; i < nslog; i++)
                     if (alive[slog[i].obj]) slog[k++] = slog[i];
                 nslog = k;
+                k = 0;  /* and its record Sets of the window */
+                for (int64_t i = 0; i < nrlog; i++)
+                    if (alive[rlog[i].obj]) rlog[k++] = rlog[i];
+                nrlog = k;
                 build_order();
             }
         }

@@ -474,6 +474,15 @@ int main(int argc, char** argv) {
     uint64_t* x_bits = (uint64_t*)GET(wf, "x_bits")->data;
     nfio_arr* xma = nfio_get(&wf, "x_mode");  // optional: 1 = SetProperty(p, GetProperty(p) + delta)
     uint8_t* x_mode = xma ? (uint8_t*)xma->data : nullptr;
+    nfio_arr* rta = nfio_get(&wf, "r_tick");  // optional: SetRecordInt calls between frames
+    const int64_t NRS = rta ? (int64_t)rta->shape[0] : 0;
+    int32_t* r_tick = NRS ? (int32_t*)rta->data : nullptr;
+    int32_t* r_obj = NRS ? (int32_t*)GET(wf, "r_obj")->data : nullptr;
+    int32_t* r_rec = NRS ? (int32_t*)GET(wf, "r_rec")->data : nullptr;
+    int32_t* r_row = NRS ? (int32_t*)GET(wf, "r_row")->data : nullptr;
+    int32_t* r_col = NRS ? (int32_t*)GET(wf, "r_col")->data : nullptr;
+    uint64_t* r_bits = NRS ? (uint64_t*)GET(wf, "r_bits")->data : nullptr;
+    int64_t ri = 0;
     nfio_arr* ha = GET(wf, "h_tick");
     int64_t NH = (int64_t)ha->shape[0];
     int32_t* h_tick = (int32_t*)ha->data;
@@ -589,6 +598,20 @@ int main(int argc, char** argv) {
             else
                 SetFloat(self, x_pid[xi], rmw ? GetFloat(self, x_pid[xi]) + bitsd(x_bits[xi]) : bitsd(x_bits[xi]));
             xi++;
+        }
+        // SetRecordInt (KM:505 -> NFCObject -> NFCRecord::SetInt, RC:182: valid position, int
+        // column, used row, changed value; the record hook fires) made before this Execute
+        while (ri < NRS && r_tick[ri] == t) {
+            const int32_t o = r_obj[ri], r = r_rec[ri];
+            if (W.alive[o]) {
+                if (rctype[r * NFK_MAX_REC_COLS + r_col[ri]]) {
+                    fprintf(stderr, "nf_ref_harness: SetRecordFloat cannot run on the reference: "
+                                    "NFCRecord::SetFloat stores an int64 variant (see --repro-record-float)\n");
+                    return 3;
+                }
+                W.rec[o][r]->SetInt(r_row[ri], r_col[ri], (NFINT64)r_bits[ri]);
+            }
+            ri++;
         }
         // DestroyObject (KM:273-308), the window's last calls: RemoveObjectFromGroup, then the
         // reference scheduler's RemoveSchedule(self) (SM:240); the object's events go with it

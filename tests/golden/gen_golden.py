@@ -39,6 +39,11 @@ FIXTURES = {
     "lifecycle": dict(n_obj=600, n_scenes=2, groups_per_scene=4, players_per_group=3, n_ticks=8, seed=808,
                       ext_frac=0.05, host_ops=True, switch_frac=0.02, rmw_frac=0.02, spawn_frac=0.03,
                       destroy_frac=0.03, records=True, rec_rows=12, rec_float_op=False),
+    # SetRecordInt between frames (KM:505 -> NFCRecord::SetInt, RC:182): used and unused rows, cells
+    # set twice, cells the heartbeat's record ops also change in the same frame
+    "recsets": dict(n_obj=400, n_scenes=2, groups_per_scene=4, players_per_group=4, n_ticks=8, seed=909,
+                    records=True, rec_rows=24, rec_float_op=False, rec_set_frac=0.1, rec_set_float=False,
+                    ext_frac=0.03),
 }
 
 

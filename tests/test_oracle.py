@@ -58,6 +58,13 @@ def test_golden_fixtures_are_nontrivial():
              destroy_frac=0.03)),
     # one large scene group (40 players) with Sets and schedule calls
     (10, dict(n_obj=500, n_scenes=1, groups_per_scene=2, players_per_group=40, ext_frac=0.08, host_ops=True)),
+    # SetRecordInt between frames (used and unused rows, repeated cells) beside the heartbeat's
+    # record ops on the same cells, through the compiled NFCRecord::SetInt (RC:182)
+    (11, dict(n_obj=400, n_scenes=2, groups_per_scene=3, players_per_group=4, records=True, rec_rows=32,
+              rec_float_op=False, rec_set_frac=0.08, rec_set_float=False, ext_frac=0.05)),
+    (12, dict(n_obj=300, n_scenes=1, groups_per_scene=4, players_per_group=5, records=True, rec_rows=64,
+              rec_float_op=False, rec_skill_op=True, rec_set_frac=0.2, rec_set_float=False, spawn_frac=0.03,
+              destroy_frac=0.03)),
 ])
 def test_oracle_matches_reference(seed, kw):
     w = workload.make_world(n_ticks=9, seed=seed, **kw)
