@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "entity-ticks/sec (update+dirty-diff+fanout) at 1M entities/GPU, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_CEILING_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "hbm_ceiling.json")
 KNAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles", "membership"]
 CONFIG_NAMES = {
     0: "BASELINE config[0]: Tutorial3 (HelloWorld3Module.cpp) scaled to 10k NPC objects in scene 1 group 0: "
@@ -307,6 +308,20 @@ def main():
             traffic_src = ((pm.get(f"config{args.config}") or {}).get("source") or pm.get("source")) if traffic else None
         except Exception:
             traffic = None
+    # the bandwidth a perfectly coalesced stream mix with this kernel's read:write ratio reaches on
+    # an MI355X (tools/hbm_mix.hip), beside the 8 TB/s spec peak
+    ceiling = None
+    if os.path.exists(HBM_CEILING_JSON):
+        try:
+            hc = json.load(open(HBM_CEILING_JSON))
+            mix = hc["ceiling_for"].get(dom)
+            if mix:
+                ceiling = {"GBps": hc["kernels"][mix]["GBps"], "probe": mix,
+                           "frac_achieved": achieved / hc["kernels"][mix]["GBps"],
+                           "frac_traffic": (traffic / (d["avg_us"] * 1e-6) / 1e9 / hc["kernels"][mix]["GBps"])
+                           if traffic else None, "source": "profiles/hbm_ceiling.json"}
+        except Exception:
+            ceiling = None
     total_alg = sum(v["alg_bytes_per_launch"] or 0 for v in kern.values())
     value = world * args.entities * args.steps / elapsed
 
@@ -332,7 +347,7 @@ def main():
                    "migrations_per_rank_per_frame": args.migrate / args.migrate_every if migrating else 0},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src},
+                     "traffic_source": traffic_src, "mix_ceiling": ceiling},
         "kernels": kern,
         "per_frame": {"prop_events": s["n_prop_events"], "rec_events": s["n_rec_events"], "fired": s["n_fired"],
                       "msgs": s["n_msgs"], "alg_bytes_all_kernels": total_alg,
