@@ -378,20 +378,28 @@ def host_calls_run(args, torch, kernel, workload):
     gh, gd = w["guid_head"], w["guid_data"]
     xs = np.searchsorted(w["x_tick"], np.arange(frames + 1))
     hs = np.searchsorted(w["h_tick"], np.arange(frames + 1))
+    # each frame's calls as the game logic hands them over (GUIDs, ids, values), prepared before
+    # the timed frames: the timed host work is the C-ABI calls and nfk_execute
+    calls = []
+    for t in range(frames):
+        a, b = hs[t], hs[t + 1]
+        ho = w["h_obj"][a:b]
+        hc = (w["h_op"][a:b], gh[ho], gd[ho], w["h_kind"][a:b], w["h_interval"][a:b], w["h_count"][a:b],
+              w["h_time"][a:b]) if b > a else None
+        a, b = xs[t], xs[t + 1]
+        xo = w["x_obj"][a:b]
+        xc = (gh[xo], gd[xo], w["x_pid"][a:b], w["x_bits"][a:b]) if b > a else None
+        calls.append((hc, xc))
     t_calls = t_exec = 0.0
 
     def frame(t):
         nonlocal t_calls, t_exec
         c0 = time.perf_counter()
-        a, b = hs[t], hs[t + 1]
-        if b > a:
-            ho = w["h_obj"][a:b]
-            m.schedule_calls(w["h_op"][a:b], gh[ho], gd[ho], w["h_kind"][a:b], w["h_interval"][a:b],
-                             w["h_count"][a:b], w["h_time"][a:b])
-        a, b = xs[t], xs[t + 1]
-        if b > a:
-            xo = w["x_obj"][a:b]
-            m.set_props(gh[xo], gd[xo], w["x_pid"][a:b], w["x_bits"][a:b])
+        hc, xc = calls[t]
+        if hc is not None:
+            m.schedule_calls(*hc)
+        if xc is not None:
+            m.set_props(*xc)
         c1 = time.perf_counter()
         m.Execute(int(w["tick_time"][t]))
         m.outputs_raw()

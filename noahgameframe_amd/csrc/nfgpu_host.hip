@@ -53,7 +53,7 @@ public:
     // n lookups with the home slots of the lookups kPre ahead prefetched (a batch of calls is
     // bound by the table's cache misses, not by the probing)
     void find_many(int32_t n, const int64_t* h, const int64_t* d, int32_t* out) const {
-        constexpr int32_t kPre = 16;
+        constexpr int32_t kPre = 32;
         if (cap_ == 0) {
             for (int32_t i = 0; i < n; i++) out[i] = -1;
             return;
@@ -213,9 +213,7 @@ struct World {
     struct XOp { uint32_t slot, pid; uint64_t bits; };
     std::vector<XOp> xops;
     // per-frame SetProperty groups (host scratch kept across frames) and their device results
-    std::vector<uint32_t> g_slot, g_pid, g_first, xord, xord_t;
-    std::vector<uint64_t> xkey, xkey_t;
-    std::vector<uint64_t> hkey, hkey_t;  // schedule-call folding scratch
+    std::vector<uint32_t> g_slot, g_pid, g_first;
     std::vector<int32_t> look;           // GUID lookups of one batched call
     // GetProperty* (nfk_get_props): device values read since the last frame, and the queued
     // SetProperty chain of each (object, property): ov_last[key] = its last xop, ov_prev links back
@@ -229,7 +227,10 @@ struct World {
     std::vector<uint32_t> post_kind;
     uint8_t* added_d = nullptr;
     size_t added_cap = 0;
-    std::vector<uint32_t> hord, hord_t;
+    std::vector<uint64_t> xpk, xpk_t, hpk, hpk_t;  // packed (key << 32 | call index) sort scratch
+    struct Post { uint32_t slot, kind, op; float interval; int32_t count; int64_t time; };
+    std::vector<uint32_t> pre_slot, pre_op;  // schedule-call folding results of the frame
+    std::vector<Post> post, post_t;
     void* xs_buf = nullptr;  // x_old / x_new
     size_t xs_cap = 0;
     struct HOp { int32_t code; uint32_t slot, kind; float interval; int32_t count; int64_t time; };
@@ -552,33 +553,29 @@ int dev_reserve(World* w, void** p, size_t* cap, size_t bytes) {
     return NFK_OK;
 }
 
-// stable LSD radix sort of (key, value) pairs on the low `bits` bits of the keys (11-bit digits;
-// a digit that every key shares is skipped)
-void radix_sort_stable(std::vector<uint64_t>& k, std::vector<uint32_t>& v, std::vector<uint64_t>& tk,
-                       std::vector<uint32_t>& tv, int bits) {
-    const size_t n = k.size();
+// stable LSD radix sort of packed words key << shift | index on the key's low `key_bits` bits
+// (11-bit digits, a digit that every key shares is skipped): one array, 8 bytes per element and
+// pass instead of a key and a value array
+void radix_sort_packed(std::vector<uint64_t>& a, std::vector<uint64_t>& t, int shift, int key_bits) {
+    const size_t n = a.size();
     if (n < 2) return;
-    tk.resize(n);
-    tv.resize(n);
-    for (int sh = 0; sh < bits; sh += 11) {
-        size_t cnt[2048] = {};
-        for (size_t i = 0; i < n; i++) cnt[(k[i] >> sh) & 2047]++;
-        if (cnt[(k[0] >> sh) & 2047] == n) continue;
-        size_t acc = 0;
+    t.resize(n);
+    uint32_t cnt[2048];
+    for (int sh = shift; sh < shift + key_bits; sh += 11) {
+        memset(cnt, 0, sizeof cnt);
+        for (size_t i = 0; i < n; i++) cnt[(a[i] >> sh) & 2047]++;
+        if (cnt[(a[0] >> sh) & 2047] == n) continue;
+        uint32_t acc = 0;
         for (int b = 0; b < 2048; b++) {
-            const size_t c = cnt[b];
+            const uint32_t c = cnt[b];
             cnt[b] = acc;
             acc += c;
         }
-        for (size_t i = 0; i < n; i++) {
-            const size_t at = cnt[(k[i] >> sh) & 2047]++;
-            tk[at] = k[i];
-            tv[at] = v[i];
-        }
-        k.swap(tk);
-        v.swap(tv);
+        for (size_t i = 0; i < n; i++) t[cnt[(a[i] >> sh) & 2047]++] = a[i];
+        a.swap(t);
     }
 }
+int bits_for(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 1; }
 
 // replace a tracked device allocation by a bigger one (contents dropped)
 int regrow(World* w, void** p, size_t bytes) {
@@ -1976,36 +1973,25 @@ int nfk_execute(void* world, int64_t now_ms) {
         int r = check_fanout(w);  // the last frame's fan-out is complete before it is replaced
         if (r) return r;
     }
-    // ---- membership changes of this window, then queued calls: object -> slot ----
+    // ---- membership changes of this window ----
     {
         int r = apply_membership(w);
         if (r) return r;  // nothing of the window applied; its calls stay queued
-        size_t k = 0;
-        for (size_t i = 0; i < w->xops.size(); i++) {
-            const int32_t sl = w->slot_of_obj[w->xops[i].slot];
-            if (sl < 0) continue;  // destroyed / exported: "There is no object"
-            w->xops[k] = w->xops[i];
-            w->xops[k++].slot = (uint32_t)sl;
-        }
-        w->xops.resize(k);
-        k = 0;
-        for (size_t i = 0; i < w->hops.size(); i++) {
-            const int32_t sl = w->slot_of_obj[w->hops[i].slot];
-            if (sl < 0) continue;
-            w->hops[k] = w->hops[i];
-            w->hops[k++].slot = (uint32_t)sl;
-        }
-        w->hops.resize(k);
     }
     Dev d = w->d;
     d.now = now_ms;
 
     tp[1] = clk::now();
     // ---- host-side preparation of queued calls ----
-    // SetProperty*: (slot, property) groups, each group's calls in call order (a stable radix sort
-    // by slot << 7 | property); the most standalone groups (properties no program writes) of one
-    // 256-slot tile bounds the tile's events beside the program slots
-    const size_t nxc = w->xops.size();
+    // Queued calls hold object indices; each resolves to its slot after the window's membership
+    // changes (a destroyed / exported object's calls are dropped: "There is no object").  Calls
+    // are folded by a stable radix sort of packed words (key << ib | call index), ib = the bits
+    // of the largest call index, so the sort moves one array and keeps call order within a key.
+    //
+    // SetProperty*: (slot, property) groups, each group's calls in call order (key slot << 7 |
+    // property); the most standalone groups (properties no program writes) of one 256-slot tile
+    // bounds the tile's events beside the program slots
+    const size_t n_xq = w->xops.size(), n_hq = w->hops.size();  // (for the trace)
     std::vector<uint32_t>& g_slot = w->g_slot;
     std::vector<uint32_t>& g_pid = w->g_pid;
     std::vector<uint32_t>& g_first = w->g_first;
@@ -2013,21 +1999,36 @@ int nfk_execute(void* world, int64_t now_ms) {
     g_pid.clear();
     g_first.clear();
     int64_t max_sa = 0;
-    if (nxc) {
-        std::vector<uint64_t>& key = w->xkey;
-        std::vector<uint32_t>& ord = w->xord;
-        key.resize(nxc);
-        ord.resize(nxc);
-        for (size_t i = 0; i < nxc; i++) {
-            key[i] = ((uint64_t)w->xops[i].slot << 7) | w->xops[i].pid;
-            ord[i] = (uint32_t)i;
+    std::vector<uint64_t>& xpk = w->xpk;
+    xpk.clear();
+    const int xib = bits_for(n_xq);
+    const uint64_t xim = (1ull << xib) - 1;
+    if (n_xq) {
+        xpk.resize(n_xq);
+        uint64_t kor = 0;
+        size_t k = 0;
+        for (size_t i = 0; i < n_xq; i++) {
+            if (i + 16 < n_xq) __builtin_prefetch(&w->slot_of_obj[w->xops[i + 16].slot]);
+            const int32_t sl = w->slot_of_obj[w->xops[i].slot];
+            if (sl < 0) continue;
+            const uint64_t key = ((uint64_t)(uint32_t)sl << 7) | w->xops[i].pid;
+            kor |= key;
+            xpk[k++] = (key << xib) | i;
         }
-        radix_sort_stable(key, ord, w->xkey_t, w->xord_t, 31 + 7);
+        xpk.resize(k);
+        if (bits_for(kor) + xib > 64) return fail(NFK_ERR_CAPACITY, "too many queued SetProperty calls");
+        radix_sort_packed(xpk, w->xpk_t, xib, bits_for(kor));
         int64_t tile_sa = 0;
         uint32_t cur_tile = 0xFFFFFFFFu;
-        for (size_t i = 0; i < nxc; i++) {
-            if (i == 0 || key[i] != key[i - 1]) {
-                const uint32_t sl = (uint32_t)(key[i] >> 7), pid = (uint32_t)(key[i] & 127);
+        uint64_t prev = ~0ull;
+        g_slot.reserve(k);
+        g_pid.reserve(k);
+        g_first.reserve(k + 1);
+        for (size_t i = 0; i < k; i++) {
+            const uint64_t key = xpk[i] >> xib;
+            if (key != prev) {
+                prev = key;
+                const uint32_t sl = (uint32_t)(key >> 7), pid = (uint32_t)(key & 127);
                 g_slot.push_back(sl);
                 g_pid.push_back(pid);
                 g_first.push_back((uint32_t)i);
@@ -2040,8 +2041,9 @@ int nfk_execute(void* world, int64_t now_ms) {
                 }
             }
         }
-        g_first.push_back((uint32_t)nxc);
+        g_first.push_back((uint32_t)k);
     }
+    const size_t nxc = xpk.size();
     // a tile's events: its slots' program destinations plus its standalone Set groups
     {
         const int64_t need_ev = (int64_t)kTile * std::max(w->n_dst_union, 1) + max_sa;
@@ -2059,38 +2061,50 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     tp[2] = clk::now();
     // schedule calls: pre-scan (remove-list key owner, RemoveSchedule(self)) and post-scan (remove,
-    // add), folded per (slot, kind) in call order (a stable radix sort by slot << 5 | kind):
+    // add), folded per (slot, kind) in call order (key slot << 5 | kind):
     //  * RemoveSchedule(self) erases the object's schedules at once (SM:240-243);
     //  * RemoveSchedule(self, name) inserts into the std::map<NFGUID, name> remove list, so only the
     //    object's first one in the window owns the key (SM:245-249), and it also blocks the scan's
     //    own insert (SM:68);
     //  * remove runs before add at the end of Execute (SM:83-119); AddSchedule keeps an existing
     //    name, so of several adds of one (object, name) the first wins (SM:108-116).
-    std::vector<uint32_t> pre_slot, pre_op;
-    struct Post { uint32_t slot, kind, op; float interval; int32_t count; int64_t time; };
-    std::vector<Post> post;
-    if (!w->hops.empty()) {
-        const size_t nh = w->hops.size();
-        std::vector<uint64_t>& key = w->hkey;
-        std::vector<uint32_t>& ord = w->hord;
-        key.resize(nh);
-        ord.resize(nh);
-        for (size_t i = 0; i < nh; i++) {
-            const uint32_t k = w->hops[i].kind;
-            key[i] = ((uint64_t)w->hops[i].slot << 5) | (w->hops[i].code == 3 || k == kNoKind ? 0u : k);
-            ord[i] = (uint32_t)i;
+    std::vector<uint32_t>& pre_slot = w->pre_slot;
+    std::vector<uint32_t>& pre_op = w->pre_op;
+    using Post = World::Post;
+    std::vector<Post>& post = w->post;
+    pre_slot.clear();
+    pre_op.clear();
+    post.clear();
+    if (n_hq) {
+        std::vector<uint64_t>& hpk = w->hpk;
+        const int hib = bits_for(n_hq);
+        const uint64_t him = (1ull << hib) - 1;
+        hpk.resize(n_hq);
+        uint64_t kor = 0;
+        size_t nh = 0;
+        for (size_t i = 0; i < n_hq; i++) {
+            const World::HOp& h = w->hops[i];
+            if (i + 16 < n_hq) __builtin_prefetch(&w->slot_of_obj[w->hops[i + 16].slot]);
+            const int32_t sl = w->slot_of_obj[h.slot];
+            if (sl < 0) continue;
+            const uint64_t key = ((uint64_t)(uint32_t)sl << 5) | (h.code == 3 || h.kind == kNoKind ? 0u : h.kind);
+            kor |= key;
+            hpk[nh++] = (key << hib) | i;
         }
-        radix_sort_stable(key, ord, w->hkey_t, w->hord_t, 31 + 5);
+        hpk.resize(nh);
+        if (bits_for(kor) + hib > 64) return fail(NFK_ERR_CAPACITY, "too many queued schedule calls");
+        radix_sort_packed(hpk, w->hpk_t, hib, bits_for(kor));
         for (size_t a = 0; a < nh;) {
-            const uint32_t slot = (uint32_t)(key[a] >> 5);
+            const uint32_t slot = (uint32_t)((hpk[a] >> hib) >> 5);
             size_t b = a;
             uint32_t owner_seq = 0xFFFFFFFFu, owner_kind = 0;
             bool erase_all = false;
-            for (; b < nh && (uint32_t)(key[b] >> 5) == slot; b++) {
-                const World::HOp& h = w->hops[ord[b]];
+            for (; b < nh && (uint32_t)((hpk[b] >> hib) >> 5) == slot; b++) {
+                const uint32_t seq = (uint32_t)(hpk[b] & him);
+                const World::HOp& h = w->hops[seq];
                 if (h.code == 3) erase_all = true;
-                if (h.code == 2 && ord[b] < owner_seq) {
-                    owner_seq = ord[b];
+                if (h.code == 2 && seq < owner_seq) {
+                    owner_seq = seq;
                     owner_kind = h.kind;
                 }
             }
@@ -2104,12 +2118,12 @@ int nfk_execute(void* world, int64_t now_ms) {
                 if (owner_kind == kNoKind) post.push_back(Post{slot, 0u, 8u, 0.f, 0, 0});  // release the key only
             }
             for (size_t c = a; c < b;) {
-                const uint32_t kind = (uint32_t)(key[c] & 31);
+                const uint32_t kind = (uint32_t)((hpk[c] >> hib) & 31);
                 size_t e = c;
                 Post p{slot, kind, 0u, 0.f, 0, 0};
                 if (owner_seq != 0xFFFFFFFFu && owner_kind == kind) p.op |= 1u | 4u;
-                for (; e < b && (uint32_t)(key[e] & 31) == kind; e++) {
-                    const World::HOp& h = w->hops[ord[e]];
+                for (; e < b && (uint32_t)((hpk[e] >> hib) & 31) == kind; e++) {
+                    const World::HOp& h = w->hops[hpk[e] & him];
                     if (h.code == 1 && !(p.op & 2u)) {
                         p.op |= 2u;
                         p.interval = h.interval;
@@ -2125,10 +2139,16 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
 
     // k_post_hostops' entries kind-major, slot order: a mass AddSchedule (server start, a wave of
-    // spawns) then sweeps each kind's schedule records in address order
-    if (post.size() > 1)
-        std::sort(post.begin(), post.end(),
-                  [](const Post& a, const Post& b) { return a.kind != b.kind ? a.kind < b.kind : a.slot < b.slot; });
+    // spawns) then sweeps each kind's schedule records in address order.  The folding emitted them
+    // in (slot, kind) order, so a stable counting sort by kind gives (kind, slot).
+    if (post.size() > 1) {
+        uint32_t cnt[NFK_MAX_KINDS + 1] = {};
+        for (const Post& q : post) cnt[q.kind + 1]++;
+        for (int k = 0; k < NFK_MAX_KINDS; k++) cnt[k + 1] += cnt[k];
+        w->post_t.resize(post.size());
+        for (const Post& q : post) w->post_t[cnt[q.kind]++] = q;
+        post.swap(w->post_t);
+    }
 
     // k_tick runs the programs on the working set fixed at commit (Dev::u_*); a schema whose
     // working set does not fit the register slots runs k_tick_touch
@@ -2157,7 +2177,7 @@ int nfk_execute(void* world, int64_t now_ms) {
             memcpy(P + off_xp, g_pid.data(), ng * 4);
             memcpy(P + off_xf, g_first.data(), (ng + 1) * 4);
             uint64_t* xb = (uint64_t*)(P + off_xb);
-            for (size_t i = 0; i < nxc; i++) xb[i] = w->xops[w->xord[i]].bits;
+            for (size_t i = 0; i < nxc; i++) xb[i] = w->xops[xpk[i] & xim].bits;
         }
         for (size_t i = 0; i < npre; i++) {
             ((uint32_t*)(P + off_ps))[i] = pre_slot[i];
@@ -2343,9 +2363,9 @@ int nfk_execute(void* world, int64_t now_ms) {
     if (trace) {
         tp[5] = clk::now();
         auto ms = [&](int a, int b) { return std::chrono::duration<double, std::milli>(tp[b] - tp[a]).count(); };
-        fprintf(stderr, "nfk_execute: membership+slots %.3f ms, SetProperty groups %.3f ms (%zu calls), schedule "
-                "calls %.3f ms (%zu), upload %.3f ms, launches %.3f ms\n", ms(0, 1), ms(1, 2), w->xops.size(), ms(2, 3),
-                w->hops.size(), ms(3, 4), ms(4, 5));
+        fprintf(stderr, "nfk_execute: membership %.3f ms, SetProperty groups %.3f ms (%zu calls), schedule "
+                "calls %.3f ms (%zu), upload %.3f ms, launches %.3f ms\n", ms(0, 1), ms(1, 2), n_xq, ms(2, 3),
+                n_hq, ms(3, 4), ms(4, 5));
     }
     return NFK_OK;
 }

@@ -2,7 +2,7 @@
 # One GPU session: every GPU step has its own time limit; a crash/abort/timeout stops the
 # session (no further GPU work), an ordinary test failure does not.
 # usage: tools/gpu_session.sh <tag> [steps...]
-#   steps: smoke tests bench prof pmc ablate bench3 bench4
+#   steps: smoke tests bench prof pmc ablate bench3 bench4 hostprof hbmmix
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r01}; shift
@@ -37,6 +37,8 @@ for step in "$@"; do
     bench2g1) NFGPU_BENCH_TRACE=1 run bench2g1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                --master-port 29562 bench.py --gpus 2 --steps 20 --warmup 3 --backend gloo --cpu-baseline off \
                --entities 262144 --groups 1024 --migrate 128 --migrate-every 1 ;;
+    hostprof) NFGPU_TRACE_EXEC=1 run hostprof 300 python tools/host_calls_profile.py ;;
+    hbmmix) run hbmmix 120 tools/_bin/hbm_mix ;;
     ablate) run ablate 600 python tools/ablate.py --variants ${ABL:-0,8,4} ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
              python bench.py --steps 50 --warmup 5 --cpu-baseline off --host-calls off ;;
