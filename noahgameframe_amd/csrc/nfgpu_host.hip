@@ -2342,7 +2342,7 @@ int nfk_execute(void* world, int64_t now_ms) {
         w->scan_dev = d;
     } else {
         TimeScope ts(w, KT_SCAN);
-        hipLaunchKernelGGL(k_scan_tiles, dim3(5), dim3(kScanTPB), 0, w->stream, d);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(4), dim3(kScanTPB), 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
     // the tiles k_tick / k_records did not fan out: record tiles, and property tiles after
@@ -2387,7 +2387,7 @@ static int ensure_ranks(World* w) {
     if (!w->scan_pending) return NFK_OK;
     w->scan_pending = false;
     TimeScope ts(w, KT_SCAN);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(5), dim3(kScanTPB), 0, w->stream, w->scan_dev);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(4), dim3(kScanTPB), 0, w->stream, w->scan_dev);
     HIPCHK(hipGetLastError());
     return NFK_OK;
 }

@@ -643,12 +643,18 @@ struct ScanArr {
 
 __device__ __forceinline__ void scan_load(ScanArr& x, const uint32_t* __restrict__ cnt, int len, int i0) {
     x.sum = 0;
+    if (i0 + kScanPer <= len) {  // two 16-byte loads (cnt is 16-byte aligned, i0 a multiple of 8)
+        const uint4 a = ((const uint4*)(cnt + i0))[0], b = ((const uint4*)(cnt + i0))[1];
+        x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
+        x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+    } else {
 #pragma unroll
-    for (int q = 0; q < kScanPer; q++) {
-        x.v[q] = (i0 + q < len) ? cnt[i0 + q] : 0u;
-        x.sum += x.v[q];
+        for (int q = 0; q < kScanPer; q++) x.v[q] = (i0 + q < len) ? cnt[i0 + q] : 0u;
     }
+#pragma unroll
+    for (int q = 0; q < kScanPer; q++) x.sum += x.v[q];
 }
+static_assert(kScanPer == 8, "scan_load's vector path loads 8 counts");
 
 // block-scan step of one array (s_pre = exclusive prefix of the wave totals); returns the pass total
 __device__ __forceinline__ unsigned long long scan_store(ScanArr& x, const unsigned long long* s_pre,
@@ -663,29 +669,14 @@ __device__ __forceinline__ unsigned long long scan_store(ScanArr& x, const unsig
     return s_pre[kScanTPB / 64];
 }
 
-// One workgroup per count array (blockIdx.x: 0 events, 1 fired, 2 record events, 3 message runs,
-// 4 the property tiles' messages when k_tick fanned them out at a fixed stride).
+// One workgroup per count array (blockIdx.x: 0 events, 1 fired, 2 record events, 3 message runs;
+// block 3 also sums the messages of the tiles fanned out at a fixed stride).
 __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
     __shared__ unsigned long long s_w[kScanTPB / 64 + 1];  // wave totals -> exclusive prefixes, [16] = total
+    __shared__ unsigned long long s_real[kScanTPB / 64];  // (block 3) messages of the fixed-stride tiles
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nrt = d.has_recops ? d.n_rtiles : 0;
     const int a = blockIdx.x;
-    if (a == 4) {  // sum of the message counts of the fixed-stride tiles (property, fused record)
-        unsigned long long v = 0;
-        if (d.msg_tcap)
-            for (int i = tid; i < d.n_tiles; i += kScanTPB) v += d.t_msg[i];
-        if (d.fuse_rec)
-            for (int i = tid; i < nrt; i += kScanTPB) v += d.t_msg[d.n_tiles + i];
-        v = wave_sum(v);
-        if (lane == 0) s_w[w] = v;
-        __syncthreads();
-        if (tid == 0) {
-            unsigned long long t = 0;
-            for (int i = 0; i < kScanTPB / 64; i++) t += s_w[i];
-            d.ctrl->n_msgs_ptiles = t;
-        }
-        return;
-    }
     const uint32_t* cnt = a == 0 ? d.t_ev : a == 1 ? d.t_fi : a == 2 ? d.t_re : d.t_msg;
     uint32_t* base = a == 0 ? d.ev_base : a == 1 ? d.fi_base : a == 2 ? d.re_base : d.msg_base;
     const int len = a < 2 ? d.n_tiles : a == 2 ? nrt : d.n_tiles + nrt;
@@ -693,17 +684,22 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
     // out by k_records msg_rtcap each
     const int fixed = (a == 3 && d.msg_tcap) ? d.n_tiles : 0;
     const int rfixed = (a == 3 && d.fuse_rec) ? nrt : 0;
-    unsigned long long carry = 0;
+    unsigned long long carry = 0, real = 0;
     for (int c0 = 0; c0 < len; c0 += kScanTPB * kScanPer) {
         const int i0 = c0 + tid * kScanPer;
         ScanArr x;
         scan_load(x, cnt, len, i0);
-        if (fixed) {
+        if (a == 3 && (fixed || rfixed)) {  // a fixed-stride tile's run is its reservation
             x.sum = 0;
 #pragma unroll
             for (int q = 0; q < kScanPer; q++) {
-                if (i0 + q < fixed) x.v[q] = d.msg_tcap;
-                else if (i0 + q < fixed + rfixed) x.v[q] = d.msg_rtcap;
+                if (i0 + q < fixed) {
+                    real += x.v[q];
+                    x.v[q] = d.msg_tcap;
+                } else if (i0 + q >= d.n_tiles && i0 + q < d.n_tiles + rfixed) {
+                    real += x.v[q];
+                    x.v[q] = d.msg_rtcap;
+                }
                 x.sum += x.v[q];
             }
         }
@@ -733,6 +729,16 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
         if (a == 3) {
             d.ctrl->msg_extent = carry;
             if (carry > (unsigned long long)d.msg_cap) atomicOr(&d.ctrl->err, kErrMsgCap);
+        }
+    }
+    if (a == 3) {  // sum of the fixed-stride tiles' messages
+        real = wave_sum(real);
+        if (lane == 0) s_real[w] = real;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long t = 0;
+            for (int i = 0; i < kScanTPB / 64; i++) t += s_real[i];
+            d.ctrl->n_msgs_ptiles = t;
         }
     }
 }
