@@ -14,6 +14,7 @@
 #include <vector>
 
 #include <mutex>
+#include <thread>
 
 #include "nfgpu_jit.hpp"
 #include "nfgpu_kernels.hip"
@@ -454,61 +455,6 @@ struct MetaLists {
     std::vector<uint64_t> desc;
 };
 
-// The pack / unpack lists and metadata of one rewritten segment in one pass over its members
-// (the per-object host arrays are read once per member, prefetched a few members ahead: members
-// are in NFGUID order, so their object indices are scattered).  all: every slot of the segment is
-// rewritten (a full re-layout); else only the slots whose occupant changes.
-int seg_lists(World* w, World::Seg& g, bool all, MetaLists& m, std::vector<int32_t>& pack_src,
-              std::vector<int32_t>& un_dst, std::vector<int64_t>& un_src) {
-    const int32_t n = (int32_t)g.objs.size();
-    const size_t at = m.slot.size();
-    m.slot.resize(at + g.cap);
-    m.obj.resize(at + g.cap);
-    m.desc.resize(at + g.cap);
-    m.pl.resize(at + g.cap, 0);
-    int32_t rank = 0;
-    for (int32_t i = 0; i < g.cap; i++) {
-        const int32_t ns = g.base + i;
-        m.slot[at + i] = ns;
-        if (i >= n) {
-            m.obj[at + i] = -1;
-            m.desc[at + i] = kDeadDesc;
-            if (all || w->obj_of_slot[ns] >= 0) {  // an entity left this slot: clear it
-                un_dst.push_back(ns);
-                un_src.push_back(kZeroRow);
-            }
-            continue;
-        }
-        if (i + 8 < n) {
-            const int32_t p = g.objs[i + 8];
-            __builtin_prefetch(&w->isplayer[p]);
-            __builtin_prefetch(&w->cls[p]);
-            __builtin_prefetch(&w->src_row[p]);
-            __builtin_prefetch(&w->slot_of_obj[p]);
-        }
-        const int32_t o = g.objs[i];
-        const bool pl = w->isplayer[o];
-        m.obj[at + i] = o;
-        m.desc[at + i] = (uint64_t)(uint32_t)g.base | ((uint64_t)(pl ? rank + 1 : 0) << 46) | ((uint64_t)w->cls[o] << 60);
-        if (pl) m.pl[at + rank++] = ns;
-        const int64_t sr = w->src_row[o];
-        const int32_t os = w->slot_of_obj[o];
-        if (sr >= 0) {
-            un_dst.push_back(ns);
-            un_src.push_back(-1 - sr);
-        } else if (all || os != ns) {
-            un_dst.push_back(ns);
-            un_src.push_back((int64_t)pack_src.size());
-            pack_src.push_back(os);
-        }
-    }
-    if (rank > 0x3FFF) return fail(NFK_ERR_ARG, "more than 16383 players in one scene group");
-    for (int32_t i = 0; i < n; i++) m.desc[at + i] |= (uint64_t)rank << 32;
-    g.np = rank;
-    w->max_np = std::max(w->max_np, rank);
-    return NFK_OK;
-}
-
 int seg_meta(World* w, World::Seg& g, MetaLists& m) {
     int32_t np = 0;
     for (int32_t o : g.objs) np += w->isplayer[o] ? 1 : 0;
@@ -838,12 +784,19 @@ int apply_membership(World* w) {
         }
         return lo;
     };
+    // per affected segment: the old ranks its leavers had and the objects that join it
+    struct EdInfo {
+        std::vector<int32_t> rem, ins;
+    };
+    std::map<int32_t, EdInfo> info;
     for (int32_t o : w->touched) {
         const int32_t s = w->slot_of_obj[o];
         if (s < 0) continue;
-        auto& v = seg_copy(seg_at(s)).objs;
+        const int32_t gi = seg_at(s);
+        auto& v = seg_copy(gi).objs;
         auto it = std::lower_bound(v.begin(), v.end(), o, cmp);
         if (it != v.end() && *it == o) v.erase(it);
+        info[gi].rem.push_back(s - w->segs[gi].base);  // members occupy [base, base + n) in NFGUID order
     }
     for (int32_t o : w->touched) {
         if (!w->alive[o]) continue;
@@ -854,15 +807,71 @@ int apply_membership(World* w) {
         }
         auto& v = seg_copy(f->second).objs;
         v.insert(std::lower_bound(v.begin(), v.end(), o, cmp), o);
+        info[f->second].ins.push_back(o);
     }
     for (int32_t g : aff)
         if ((int32_t)edit[g].objs.size() > edit[g].cap) full = true;
 
-    std::vector<int32_t> pack_src, un_dst;
+    std::vector<int32_t> pack_src, un_dst;  // (host-built lists: none since k_seg_edit)
     std::vector<int64_t> un_src;
     MetaLists m;
+    // edited and new segments: their slot lists are generated on the device (k_seg_edit) from the
+    // removed ranks and the inserted objects at their new ranks
+    std::vector<SegEdit> edits;
+    std::vector<int32_t> ins_rank, ins_obj, rem_rank;
+    std::vector<uint64_t> ins_meta;
+    std::vector<int64_t> ins_src;
+    int32_t ed_rows = 0, ed_list = 0;
+    // ob: the old segment (-1: a new (scene, group) pair; its members are all inserted)
+    auto add_edit = [&](World::Seg& g, int32_t ob_seg, const std::vector<int32_t>* ins, const std::vector<int32_t>* rem,
+                        bool all) -> int {
+        SegEdit e{};
+        const World::Seg* old = ob_seg >= 0 ? &w->segs[ob_seg] : nullptr;
+        e.ob = old ? old->base : -1;
+        e.nb = g.base;
+        e.on = old ? (int32_t)old->objs.size() : 0;
+        e.nn = (int32_t)g.objs.size();
+        e.nc = g.cap;
+        int32_t np = old ? old->np : 0;
+        e.io = (int32_t)ins_rank.size();
+        if (ins) {
+            std::vector<std::pair<int32_t, int32_t>> r;
+            r.reserve(ins->size());
+            for (int32_t o : *ins) {
+                r.push_back({(int32_t)(std::lower_bound(g.objs.begin(), g.objs.end(), o, cmp) - g.objs.begin()), o});
+                np += w->isplayer[o] ? 1 : 0;
+            }
+            std::sort(r.begin(), r.end());
+            for (const auto& x : r) {
+                const int32_t o = x.second;
+                ins_rank.push_back(x.first);
+                ins_obj.push_back(o);
+                ins_meta.push_back(((uint64_t)w->cls[o] << 60) | (w->isplayer[o] ? 1u : 0u));
+                ins_src.push_back(w->src_row[o] >= 0 ? -1 - w->src_row[o] : (int64_t)w->slot_of_obj[o]);
+            }
+        }
+        e.ni = (int32_t)ins_rank.size() - e.io;
+        e.ro = (int32_t)rem_rank.size();
+        if (rem) {
+            const size_t r0 = rem_rank.size();
+            for (int32_t rk : *rem) {
+                rem_rank.push_back(rk);
+                np -= w->isplayer[old->objs[rk]] ? 1 : 0;
+            }
+            std::sort(rem_rank.begin() + r0, rem_rank.end());
+        }
+        e.nr = (int32_t)rem_rank.size() - e.ro;
+        if (np > 0x3FFF) return fail(NFK_ERR_ARG, "more than 16383 players in one scene group");
+        e.np = np;
+        e.all = all ? 1 : 0;
+        g.np = np;
+        w->max_np = std::max(w->max_np, np);
+        edits.push_back(e);
+        return NFK_OK;
+    };
     std::vector<World::Seg> nsegs;
     std::vector<int32_t> nsrc;   // full: nsegs[i] is untouched segment nsrc[i] (members kept), or -1
+    std::vector<int32_t> nold;   // full: nsegs[i] is edited segment nold[i], or -1 (untouched / new)
     std::vector<SegMove> moves;  // full: untouched segments whose slot range changes
     int32_t mv_rows_dev = 0, mv_list_dev = 0;
     const int32_t max_np0 = w->max_np;
@@ -888,6 +897,7 @@ int apply_membership(World* w) {
             g.objs = std::move(fit->second);
             nsegs.push_back(std::move(g));
             nsrc.push_back(-1);
+            nold.push_back(-1);
             ++fit;
         };
         for (int32_t gi = 0; gi < (int32_t)w->segs.size(); gi++) {
@@ -902,6 +912,7 @@ int apply_membership(World* w) {
             if (e != edit.end()) g.objs = std::move(e->second.objs);
             nsegs.push_back(std::move(g));
             nsrc.push_back(e != edit.end() ? -1 : gi);
+            nold.push_back(e != edit.end() ? gi : -1);
         }
         while (fit != fresh.end()) push_fresh();
         auto members = [&](size_t i) -> const std::vector<int32_t>& {
@@ -933,7 +944,13 @@ int apply_membership(World* w) {
                 mv_list_dev += g.cap;
                 continue;
             }
-            int r = seg_lists(w, g, true, m, pack_src, un_dst, un_src);
+            int r;
+            if (nold[i] >= 0) {
+                const EdInfo& x = info[nold[i]];
+                r = add_edit(g, nold[i], &x.ins, &x.rem, true);
+            } else {  // a new (scene, group) pair
+                r = add_edit(g, -1, &g.objs, nullptr, true);
+            }
             if (r) {
                 w->max_np = max_np0;
                 return r;
@@ -941,13 +958,19 @@ int apply_membership(World* w) {
         }
     } else {
         for (int32_t gi : aff) {
-            World::Seg& g = edit[gi];
-            int r = seg_lists(w, g, false, m, pack_src, un_dst, un_src);
+            const EdInfo& x = info[gi];
+            int r = add_edit(edit[gi], gi, &x.ins, &x.rem, false);
             if (r) {
                 w->max_np = max_np0;
                 return r;
             }
         }
+    }
+    for (SegEdit& e : edits) {  // their lists follow the untouched segments' (device-generated too)
+        e.po = mv_rows_dev + ed_rows;
+        e.lo = mv_list_dev + ed_list;
+        ed_rows += e.nn;
+        ed_list += e.nc;
     }
 
     t_lists = clk::now();
@@ -958,15 +981,18 @@ int apply_membership(World* w) {
     const size_t o_ps = stage_list(w, pack_src), o_ud = stage_list(w, un_dst), o_us = stage_list(w, un_src);
     const size_t o_ms = stage_list(w, m.slot), o_mo = stage_list(w, m.obj), o_md = stage_list(w, m.desc);
     const size_t o_mp = stage_list(w, m.pl), o_mv = stage_list(w, moves);
+    const size_t o_ed = stage_list(w, edits), o_ir = stage_list(w, ins_rank), o_io = stage_list(w, ins_obj);
+    const size_t o_im = stage_list(w, ins_meta), o_is = stage_list(w, ins_src), o_rr = stage_list(w, rem_rank);
     const size_t hp = pack_src.size();
-    int r = dev_reserve(w, (void**)&w->mv_rows, &w->mv_cap, std::max<size_t>(hp + (size_t)mv_rows_dev, 1) * rw * 8);
+    const size_t nd = (size_t)mv_list_dev + ed_list, npk = (size_t)mv_rows_dev + ed_rows;
+    int r = dev_reserve(w, (void**)&w->mv_rows, &w->mv_cap, std::max<size_t>(hp + npk, 1) * rw * 8);
     if (r) return r;
-    // device-generated lists: pack_src | un_dst | un_src | m_slot | m_obj | m_desc | m_pl
-    const size_t nd = (size_t)mv_list_dev, npk = (size_t)mv_rows_dev;
+    // device-generated lists (untouched segments that move, then edited / new segments):
+    // pack_src | un_dst | un_src | m_slot | m_obj | m_desc | m_pl
     const size_t g_ps = 0, g_ud = align16(g_ps + npk * 4), g_us = align16(g_ud + nd * 4), g_ms = align16(g_us + nd * 8),
                  g_mo = align16(g_ms + nd * 4), g_md = align16(g_mo + nd * 4), g_mp = align16(g_md + nd * 8),
                  g_end = align16(g_mp + nd * 4);
-    if (!moves.empty()) {
+    if (nd) {
         r = dev_reserve(w, (void**)&w->glist, &w->glist_cap, g_end);
         if (r) return r;
     }
@@ -983,6 +1009,13 @@ int apply_membership(World* w) {
                                (const int32_t*)w->pl_slot_w, (int32_t*)(G + g_ps), (int32_t*)(G + g_ud),
                                (int64_t*)(G + g_us), (int32_t*)(G + g_ms), (int32_t*)(G + g_mo), (uint64_t*)(G + g_md),
                                (int32_t*)(G + g_mp));
+        if (!edits.empty())
+            hipLaunchKernelGGL(k_seg_edit, dim3((unsigned)std::min<size_t>(edits.size(), 8192)), dim3(kTPB), 0,
+                               w->stream, (const SegEdit*)(L + o_ed), (int32_t)edits.size(), (const int32_t*)(L + o_ir),
+                               (const int32_t*)(L + o_io), (const uint64_t*)(L + o_im), (const int64_t*)(L + o_is),
+                               (const int32_t*)(L + o_rr), (const int32_t*)w->slot_obj_d, (const uint64_t*)w->fan_desc_w,
+                               (int32_t*)(G + g_ps), (int32_t*)(G + g_ud), (int64_t*)(G + g_us), (int32_t*)(G + g_ms),
+                               (int32_t*)(G + g_mo), (uint64_t*)(G + g_md), (int32_t*)(G + g_mp));
         if (hp)
             hipLaunchKernelGGL(k_pack, dim3(grid_for(hp * rw)), dim3(kTPB), 0, w->stream, d,
                                (const int32_t*)(L + o_ps), (int32_t)hp, rw, w->mv_rows);
@@ -1014,18 +1047,26 @@ int apply_membership(World* w) {
     // host maps
     if (full) {
         w->n_relayout_full++;
+        std::vector<int32_t> seg_base0(nsegs.size(), -1), seg_cap0(nsegs.size(), -1);
         for (size_t i = 0; i < nsegs.size(); i++)
-            if (nsrc[i] >= 0) nsegs[i].objs = std::move(w->segs[nsrc[i]].objs);
+            if (nsrc[i] >= 0) {
+                seg_base0[i] = w->segs[nsrc[i]].base;
+                seg_cap0[i] = w->segs[nsrc[i]].cap;
+                nsegs[i].objs = std::move(w->segs[nsrc[i]].objs);
+            }
         w->segs = std::move(nsegs);
         w->seg_of.clear();
         for (size_t g = 0; g < w->segs.size(); g++) w->seg_of[{w->segs[g].scene, w->segs[g].group}] = (int32_t)g;
-        std::fill(w->obj_of_slot.begin(), w->obj_of_slot.end(), -1);
-        std::fill(w->slot_of_obj.begin(), w->slot_of_obj.end(), -1);
         int64_t total = 0;
         for (const auto& g : w->segs) total = (int64_t)g.base + g.cap;
+        // slots past the new end held entities before; every slot below it belongs to a segment
+        for (int64_t sl = total; sl < std::min<int64_t>(d.N, (int64_t)w->obj_of_slot.size()); sl++)
+            w->obj_of_slot[sl] = -1;
         set_tiles(d, (int32_t)total);
+        // the host maps change for the segments whose slots or members changed
         aff.clear();
-        for (size_t g = 0; g < w->segs.size(); g++) aff.push_back((int32_t)g);
+        for (size_t g = 0; g < w->segs.size(); g++)
+            if (nsrc[g] < 0 || w->segs[g].base != seg_base0[g] || w->segs[g].cap != seg_cap0[g]) aff.push_back((int32_t)g);
     } else {
         w->n_relayout_seg++;
         for (int32_t gi : aff) {
@@ -1035,13 +1076,29 @@ int apply_membership(World* w) {
     }
     for (int32_t o : w->touched)
         if (!w->alive[o]) w->slot_of_obj[o] = -1;
-    for (int32_t gi : aff) {
-        const World::Seg& g = w->segs[gi];
-        for (int32_t i = 0; i < g.cap; i++) {
-            const int32_t ns = g.base + i;
-            const int32_t o = i < (int32_t)g.objs.size() ? g.objs[i] : -1;
-            w->obj_of_slot[ns] = o;
-            if (o >= 0) w->slot_of_obj[o] = ns;
+    // slot <-> object of the changed segments (disjoint slots and objects per segment: split over
+    // threads when large)
+    auto maps = [w, &aff](size_t a, size_t b) {
+        for (size_t k = a; k < b; k++) {
+            const World::Seg& g = w->segs[aff[k]];
+            for (int32_t i = 0; i < g.cap; i++) {
+                const int32_t ns = g.base + i;
+                const int32_t o = i < (int32_t)g.objs.size() ? g.objs[i] : -1;
+                w->obj_of_slot[ns] = o;
+                if (o >= 0) w->slot_of_obj[o] = ns;
+            }
+        }
+    };
+    {
+        int64_t work = 0;
+        for (int32_t gi : aff) work += w->segs[gi].cap;
+        const int nt = work >= (1 << 17) ? (int)std::min<size_t>(8, aff.size()) : 1;
+        if (nt <= 1) {
+            maps(0, aff.size());
+        } else {
+            std::vector<std::thread> th;
+            for (int t = 0; t < nt; t++) th.emplace_back(maps, aff.size() * t / nt, aff.size() * (t + 1) / nt);
+            for (auto& x : th) x.join();
         }
     }
     for (int32_t o : w->touched) {
@@ -1054,9 +1111,9 @@ int apply_membership(World* w) {
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     (full ? w->ms_relayout_full : w->ms_relayout_seg) += ms(t_host, t_end);
     if (getenv("NFGPU_TRACE_MEMBERSHIP"))
-        fprintf(stderr, "apply_membership %s: %zu touched, edit %.3f ms, lists %.3f ms (%zu host entries, %zu moves), "
+        fprintf(stderr, "apply_membership %s: %zu touched, edit %.3f ms, lists %.3f ms (%zu edited segments, %zu moves), "
                 "upload+launch %.3f ms, host maps %.3f ms\n", full ? "full" : "seg", n_touched, ms(t_host, t_edit),
-                ms(t_edit, t_lists), un_dst.size(), moves.size(), ms(t_lists, t_dev), ms(t_dev, t_end));
+                ms(t_edit, t_lists), edits.size(), moves.size(), ms(t_lists, t_dev), ms(t_dev, t_end));
     return NFK_OK;
 }
 

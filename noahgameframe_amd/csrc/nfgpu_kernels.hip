@@ -939,12 +939,13 @@ __global__ __launch_bounds__(kTPB) void k_pack(Dev d, const int32_t* __restrict_
     const size_t total = (size_t)n * rw;
     for (size_t t = (size_t)blockIdx.x * kTPB + threadIdx.x; t < total; t += (size_t)gridDim.x * kTPB) {
         const int32_t i = (int32_t)(t % (size_t)n), w = (int32_t)(t / (size_t)n);
-        rows[(size_t)i * rw + w] = *row_word(d, src[i], w);
+        if (src[i] >= 0) rows[(size_t)i * rw + w] = *row_word(d, src[i], w);  // (-1: a row nobody reads)
     }
 }
 
-// src[i] >= 0: row src[i] of mv; kZeroRow: zeros (a slack slot); else row -1 - src[i] of ins
-constexpr int64_t kZeroRow = INT64_MIN;
+// src[i] >= 0: row src[i] of mv; kZeroRow: zeros (a slack slot); kKeepRow: the slot keeps its row;
+// else row -1 - src[i] of ins
+constexpr int64_t kZeroRow = INT64_MIN, kKeepRow = INT64_MIN + 1;
 __global__ __launch_bounds__(kTPB) void k_unpack(Dev d, const int32_t* __restrict__ dst,
                                                  const int64_t* __restrict__ src, int32_t n, int32_t rw,
                                                  const uint64_t* __restrict__ mv, const uint64_t* __restrict__ ins) {
@@ -952,6 +953,7 @@ __global__ __launch_bounds__(kTPB) void k_unpack(Dev d, const int32_t* __restric
     for (size_t t = (size_t)blockIdx.x * kTPB + threadIdx.x; t < total; t += (size_t)gridDim.x * kTPB) {
         const int32_t i = (int32_t)(t % (size_t)n), w = (int32_t)(t / (size_t)n);
         const int64_t r = src[i];
+        if (r == kKeepRow) continue;
         const uint64_t x = r == kZeroRow ? 0ull : (r >= 0 ? mv[(size_t)r * rw + w] : ins[(size_t)(-1 - r) * rw + w]);
         *row_word(d, dst[i], w) = x;
     }
@@ -994,6 +996,128 @@ __global__ __launch_bounds__(kTPB) void k_seg_lists(const SegMove* __restrict__ 
                 m_desc[at] = kDeadDesc;
             }
             m_pl[at] = i < s.np ? pl_slot[s.ob + i] - s.ob + s.nb : 0;
+        }
+    }
+}
+
+// The segments whose member lists changed (SwitchScene, CreateObject, DestroyObject): each new
+// member list is the old one with some members removed and some inserted, all in NFGUID order,
+// i.e. a MERGE of the old members that stay (their slots in order) with the inserted objects at
+// their new ranks, which the host found by binary search in the NFGUID-ordered list.  The slot
+// lists are generated here per new slot: a member at new rank i is inserted object a if
+// ins_rank[a] == i (a = inserted objects ranked below i), else the (i - a)-th member that stays,
+// whose old rank follows from the removed ranks by a binary search; players are ranked by a
+// block scan.  (ob < 0: a new (scene, group) pair, all members inserted.)
+struct SegEdit {
+    int32_t ob, nb, on, nn;  // old base (-1: new segment), new base, old / new members
+    int32_t nc, np;          // new slot count, players among the new members
+    int32_t ni, io;          // inserted objects [io, io + ni) of the ins_* arrays
+    int32_t nr, ro;          // removed old ranks [ro, ro + nr) of rem_rank
+    int32_t po, lo;          // first pack row (nn rows), first list entry (nc entries)
+    int32_t all, pad;        // all: every member moves (a full re-layout), else only the ones whose slot changes
+};
+
+__global__ __launch_bounds__(kTPB) void k_seg_edit(const SegEdit* __restrict__ ed, int32_t n_ed,
+                                                   const int32_t* __restrict__ ins_rank,
+                                                   const int32_t* __restrict__ ins_obj,
+                                                   const uint64_t* __restrict__ ins_meta,  // cls << 60 | player
+                                                   const int64_t* __restrict__ ins_src,    // old slot, or -1 - import row
+                                                   const int32_t* __restrict__ rem_rank,
+                                                   const int32_t* __restrict__ slot_obj,
+                                                   const uint64_t* __restrict__ fan_desc, int32_t* __restrict__ pack_src,
+                                                   int32_t* __restrict__ un_dst, int64_t* __restrict__ un_src,
+                                                   int32_t* __restrict__ m_slot, int32_t* __restrict__ m_obj,
+                                                   uint64_t* __restrict__ m_desc, int32_t* __restrict__ m_pl) {
+    __shared__ int32_t s_w[kTPB / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int32_t g = blockIdx.x; g < n_ed; g += gridDim.x) {
+        const SegEdit s = ed[g];
+        const int32_t* ir = ins_rank + s.io;
+        const int32_t* rr = rem_rank + s.ro;
+        int32_t carry = 0;  // players at new ranks below the chunk
+        for (int32_t c0 = 0; c0 < s.nc; c0 += kTPB) {  // (block-uniform)
+            const int32_t i = c0 + (int32_t)threadIdx.x;
+            const int32_t at = s.lo + i, ns = s.nb + i;
+            bool pl = false;
+            int32_t obj = -1;
+            uint64_t meta = 0;  // cls << 60
+            int64_t src = kKeepRow;
+            int32_t psrc = -1;  // the old slot packed into row po + i (-1: none)
+            if (i < s.nn) {
+                // inserted objects ranked below i
+                int32_t lo = 0, hi = s.ni;
+                while (lo < hi) {
+                    const int32_t mid = (lo + hi) >> 1;
+                    if (ir[mid] < i) lo = mid + 1;
+                    else hi = mid;
+                }
+                if (lo < s.ni && ir[lo] == i) {
+                    obj = ins_obj[s.io + lo];
+                    meta = ins_meta[s.io + lo];
+                    pl = meta & 1;
+                    meta &= 0xFull << 60;
+                    const int64_t sr = ins_src[s.io + lo];
+                    if (sr < 0) {
+                        src = sr;  // an imported row
+                    } else {
+                        psrc = (int32_t)sr;
+                        src = s.po + i;
+                    }
+                } else {
+                    // the k-th member that stays (k = i - lo) has old rank k + j, j = removed ranks below it:
+                    // the largest j with rr[j - 1] - (j - 1) <= k
+                    const int32_t k = i - lo;
+                    int32_t a = 0, b = s.nr;
+                    while (a < b) {
+                        const int32_t mid = (a + b) >> 1;
+                        if (rr[mid] - mid <= k) a = mid + 1;
+                        else b = mid;
+                    }
+                    const int32_t os = s.ob + k + a;
+                    obj = slot_obj[os];
+                    const uint64_t od = fan_desc[os];
+                    meta = od & (0xFull << 60);
+                    pl = ((od >> 46) & 0x3FFF) != 0;
+                    if (s.all || os != ns) {
+                        psrc = os;
+                        src = s.po + i;
+                    }
+                }
+            } else if (i < s.nc) {
+                // slack: cleared if an entity occupied the slot before
+                src = (s.all || (s.ob == s.nb && i < s.on)) ? kZeroRow : kKeepRow;
+            }
+            // player rank: block scan of the player flags, carried across chunks
+            const unsigned long long bal = __ballot(pl && i < s.nn);
+            const int32_t below_w = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            if (lane == 0) s_w[wv] = (int32_t)__builtin_popcountll(bal);
+            __syncthreads();
+            int32_t before = carry, tot = 0;
+#pragma unroll
+            for (int q = 0; q < kTPB / 64; q++) {
+                before += q < wv ? s_w[q] : 0;
+                tot += s_w[q];
+            }
+            __syncthreads();
+            carry += tot;
+            if (i < s.nc) {
+                const int32_t prank = before + below_w;
+                un_dst[at] = ns;
+                un_src[at] = src;
+                m_slot[at] = ns;
+                if (i < s.nn) {
+                    m_obj[at] = obj;
+                    m_desc[at] = (uint64_t)(uint32_t)s.nb | ((uint64_t)s.np << 32) |
+                                 ((uint64_t)(pl ? prank + 1 : 0) << 46) | meta;
+                    if (pl) m_pl[s.lo + prank] = ns;
+                } else {
+                    m_obj[at] = -1;
+                    m_desc[at] = kDeadDesc;
+                }
+                if (i >= s.np) m_pl[at] = 0;
+            }
+            if (i < s.nn) pack_src[s.po + i] = psrc;
         }
     }
 }
