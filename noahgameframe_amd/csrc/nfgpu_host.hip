@@ -147,6 +147,8 @@ struct World {
     int n_prop = 0;
 
     std::vector<int64_t> gh, gd;
+    struct Guid { int64_t h, d; };
+    std::vector<Guid> guid;  // (gh, gd) side by side: one cache line per NFGUID comparison
     std::vector<int32_t> scene, group;
     std::vector<uint8_t> cls, isplayer;
     GuidMap obj_of;
@@ -412,7 +414,8 @@ int gather_tiles(World* w, const T* src, const uint32_t* base, int n_tiles, int 
 // std::map<NFGUID, ...>, so slot order is both the reference's dirty-sync order and
 // GetBroadCastObject's recipient order (AOI:572, KM:1270-1294).
 bool guid_less(const World* w, int32_t a, int32_t b) {
-    return w->gh[a] != w->gh[b] ? w->gh[a] < w->gh[b] : w->gd[a] < w->gd[b];
+    const World::Guid x = w->guid[a], y = w->guid[b];
+    return x.h != y.h ? x.h < y.h : x.d < y.d;
 }
 
 int32_t seg_slack(int32_t slack, int32_t len) {
@@ -1122,6 +1125,7 @@ int32_t add_object(World* w, int64_t gh, int64_t gd, int32_t scene, int32_t grou
     const int32_t o = w->n_obj++;
     w->obj_of.insert(gh, gd, o);
     w->gh.push_back(gh);
+    w->guid.push_back({gh, gd});
     w->gd.push_back(gd);
     w->scene.push_back(scene);
     w->group.push_back(group);
