@@ -190,6 +190,16 @@ public:
     bool SetPropertyFloat(const NFGUID& self, const std::string& name, double v);
     int64_t GetPropertyInt(const NFGUID& self, const std::string& name);
     double GetPropertyFloat(const NFGUID& self, const std::string& name);
+    // NFIKernelModule::SetRecordInt / SetRecordFloat (NFIKernelModule.h:120-121): queued like the
+    // property setters and applied at the next Execute through NFCRecord::SetInt / SetFloat; true
+    // once queued (the reference also returns false for an unused row or an unchanged value,
+    // which is only known on the device: such a call changes nothing and raises no event)
+    bool SetRecordInt(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol, int64_t nValue);
+    bool SetRecordFloat(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol, double dwValue);
+    // NFIKernelModule::GetRecordInt / GetRecordFloat (NFIKernelModule.h:134-135): read-your-writes
+    // like GetProperty*; 0 for an unused row (NFCRecord::GetInt, RC:623)
+    int64_t GetRecordInt(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol);
+    double GetRecordFloat(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol);
     // NFCKernelModule::SwitchScene (KM:901-951); writes SceneID/GroupID/X/Y/Z when the schema has
     // them; like the reference, fOrient and arg are not used
     bool SwitchScene(const NFGUID& self, int nTargetSceneID, int nTargetGroupID, float fX, float fY, float fZ,

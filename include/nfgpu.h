@@ -211,6 +211,26 @@ int nfk_spawn_objects(void* world, int32_t n, const int64_t* guid_head, const in
 int nfk_set_props(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
                   const int32_t* pid, const uint64_t* bits);
 
+/* ---- record mutation: NFIKernelModule::SetRecordInt/Float (KM:505, KM:545) ----
+ * Queued in call order, applied at the start of the next nfk_execute through NFCRecord::SetInt /
+ * SetFloat (RC:182 / RC:243): refused on a row the record does not use (RC:194); an int cell
+ * changes when the value differs, an f64 cell unless |new - cur| < 0.001 (TData::operator==).
+ * The cell's event of the frame runs from its value before the window's Sets to its value after
+ * the frame's record programs (coalesced, dropped when the bits are equal), in (rec, row, col)
+ * order beside the programs' events.  is_float (nullable: typed by the column) marks
+ * SetRecordFloat calls; a call of the other type than its column writes nothing (RC:189 /
+ * RC:250).  NFK_ERR_NOTFOUND for an unknown GUID, NFK_ERR_ARG for a cell outside the record. */
+int nfk_set_records(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data, const int32_t* rec,
+                    const int32_t* row, const int32_t* col, const uint8_t* is_float, const uint64_t* bits);
+
+/* ---- record reads: NFIKernelModule::GetRecordInt/Float (NFIKernelModule.h:134-135) ----
+ * NFCRecord::GetInt / GetFloat (RC:616): the cell after the last frame (waits for the world's
+ * stream; one 8-byte device read of the used-row mask and one of the cell per query) with this
+ * window's queued SetRecord* calls on it applied in call order (read-your-writes); 0 for a row
+ * the record does not use.  NFK_ERR_NOTFOUND / NFK_ERR_ARG as nfk_set_records. */
+int nfk_get_records(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data, const int32_t* rec,
+                    const int32_t* row, const int32_t* col, uint64_t* bits);
+
 /* ---- property reads: NFIKernelModule::GetPropertyInt/Float (KM:401-425) ----
  * The value the reference would return now: the world's value after the last frame (waits for
  * the world's stream) with this window's queued SetProperty* / SwitchScene writes to that

@@ -57,6 +57,20 @@ public:
     double GetPropertyFloat(const NFGUID& self, const std::string& name) override {  // KM:413
         return gpu_.GetPropertyFloat(to_gpu(self), name);
     }
+    bool SetRecordInt(const NFGUID& self, const std::string& rec, const int nRow, const int nCol,
+                      const NFINT64 v) override {  // KM:505
+        return gpu_.SetRecordInt(to_gpu(self), rec, nRow, nCol, v);
+    }
+    bool SetRecordFloat(const NFGUID& self, const std::string& rec, const int nRow, const int nCol,
+                        const double v) override {  // KM:545
+        return gpu_.SetRecordFloat(to_gpu(self), rec, nRow, nCol, v);
+    }
+    NFINT64 GetRecordInt(const NFGUID& self, const std::string& rec, const int nRow, const int nCol) override {
+        return gpu_.GetRecordInt(to_gpu(self), rec, nRow, nCol);  // NFIKernelModule.h:134, read-your-writes
+    }
+    double GetRecordFloat(const NFGUID& self, const std::string& rec, const int nRow, const int nCol) override {
+        return gpu_.GetRecordFloat(to_gpu(self), rec, nRow, nCol);  // NFIKernelModule.h:135
+    }
     bool SwitchScene(const NFGUID& self, const int scene, const int group, const float fX, const float fY,
                      const float fZ, const float fOrient, const NFIDataList& arg) override {  // NFIKernelModule.h:148
         NFCKernelModule::SwitchScene(self, scene, group, fX, fY, fZ, fOrient, arg);  // host-side scene lists

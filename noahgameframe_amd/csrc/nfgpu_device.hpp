@@ -125,6 +125,7 @@ struct Tables {
     int32_t n_recops;
     int32_t rec_rows[NFK_MAX_RECORDS], rec_cols[NFK_MAX_RECORDS];
     uint32_t kind_has_recop;  // bit k: kind k has record ops
+    uint8_t rec_ctype[NFK_MAX_RECORDS][NFK_MAX_REC_COLS];  // 0 = int64, 1 = f64
 };
 
 // Everything a kernel needs, passed by value.
@@ -155,6 +156,28 @@ struct Dev {
     uint64_t* x_new;
     int32_t n_x;              // groups
     uint32_t* fired_mask;  // [cap]
+    // queued SetRecordInt / SetRecordFloat calls folded into (slot, cell) GROUPS sorted by (slot,
+    // rec << 16 | row << 8 | col), each group's calls rs_bits[rs_first[g], rs_first[g + 1]) in call
+    // order.  k_rsets applies each group through NFCRecord's predicates before the frame and leaves
+    // the frame-start cell in rs_old[g] and the value after the group in rs_new[g]; k_records
+    // merges them into the slot's record events.
+    uint32_t* rs_head;  // [cap] 0 = none, else 1 + the slot's index among the SetRecord slots
+    const uint32_t* rs_slot;
+    const uint32_t* rs_rrc;
+    const uint32_t* rs_first;  // [n_rs + 1]
+    const uint64_t* rs_bits;
+    uint64_t* rs_old;
+    uint64_t* rs_new;
+    int32_t n_rs;              // groups
+    // the slots with groups (k_rset_slots: one wave each), their first group, and per slot its
+    // record events and messages (counted before k_records) and where k_records placed them
+    const uint32_t* rss_slot;
+    const uint32_t* rss_g0;
+    uint32_t* rss_ev;
+    uint32_t* rss_msg;
+    uint32_t* rss_pos;
+    uint32_t* rss_pmsg;
+    int32_t n_rss;
     // records: cells [cap][cols][rows], used masks [cap]
     uint64_t* rcells[NFK_MAX_RECORDS];
     uint64_t* rused[NFK_MAX_RECORDS];

@@ -231,6 +231,16 @@ struct World {
     uint8_t* added_d = nullptr;
     size_t added_cap = 0;
     std::vector<uint64_t> xpk, xpk_t, hpk, hpk_t;  // packed (key << 32 | call index) sort scratch
+    // queued SetRecordInt / SetRecordFloat calls (obj: object index until nfk_execute resolves it;
+    // rrc = rec << 16 | row << 8 | col) and their folding scratch
+    struct RSOp { uint32_t obj, rrc; uint64_t bits; };
+    std::vector<RSOp> rsq;
+    std::vector<uint64_t> rpk, rpk_t;
+    std::vector<uint32_t> rs_slot_h, rs_rrc_h, rs_first_h, rss_slot_h, rss_g0_h;
+    void* rs_buf = nullptr;   // rs_old / rs_new
+    size_t rs_cap = 0;
+    void* rss_buf = nullptr;  // rss_ev / rss_msg / rss_pos / rss_pmsg
+    size_t rss_cap = 0;
     struct Post { uint32_t slot, kind, op; float interval; int32_t count; int64_t time; };
     std::vector<uint32_t> pre_slot, pre_op;  // schedule-call folding results of the frame
     std::vector<Post> post, post_t;
@@ -560,6 +570,26 @@ int grow_event_tiles(World* w, int64_t per_tile) {
 // programs only read -> slots [n_w, n_u), each group in property-id order; the tables name
 // read-only operand r as 0x80 | r.  Fills the kinds' U-slot tables (opu, umask, opx, w_slot);
 // false when the set does not fit k_tick's register slots (k_tick_touch runs instead).
+// the record-event tiles grown for a frame whose SetRecord groups add events beside the record
+// programs' (contents dropped: called before the frame writes them)
+int grow_rec_tiles(World* w, int64_t per_tile) {
+    Dev& d = w->d;
+    const int64_t tcap = (per_tile + 63) / 64 * 64;
+    if (tcap > INT32_MAX / 2) return fail(NFK_ERR_CAPACITY, "too many record events in one record tile");
+    HIPCHK(hipStreamSynchronize(w->stream));
+    const size_t n = (size_t)(d.cap / kRTile) * (size_t)tcap;
+    int r;
+    if ((r = regrow(w, (void**)&d.re_slot, n * 4)) || (r = regrow(w, (void**)&d.re_rrc, n * 4)) ||
+        (r = regrow(w, (void**)&d.re_old, n * 8)) || (r = regrow(w, (void**)&d.re_new, n * 8)) ||
+        (r = regrow(w, (void**)&d.re_moff, n * 4))) {
+        d.re_tcap = 0;
+        return r;
+    }
+    d.re_tcap = (int32_t)tcap;
+    w->scan_pending = false;
+    return NFK_OK;
+}
+
 bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>& rp) {
     bool u_ok = false;
     {
@@ -1484,7 +1514,12 @@ int nfk_commit(void* world) {
     d.n_kind = NK;
     d.n_rec = NR;
     d.n_class = w->cfg.n_class;
-    d.has_recops = nro > 0;
+    // the record pipeline (fired masks, k_records, record tiles) runs in a world with record
+    // programs or with records that SetRecord* calls can change
+    bool any_rec = false;
+    for (int r = 0; r < NR; r++) any_rec = any_rec || w->rec_defined[r];
+    d.has_recops = nro > 0 || any_rec;
+    memcpy(w->tab.rec_ctype, w->rec_ctype, sizeof(w->tab.rec_ctype));
     ALLOC(w->tab_d, sizeof(Tables));
     ALLOC(d.tally, (size_t)3 * kTallyN * 8 * 8);
     ALLOC(w->ctrl, sizeof(Ctrl));
@@ -1506,6 +1541,7 @@ int nfk_commit(void* world) {
     ALLOC(d.s_cold, (size_t)std::max(NK, 1) * d.s_kstr * sizeof(SchedCold));
     ALLOC(d.e_flags, cap);
     ALLOC(d.ext_head, (size_t)cap * 4);
+    ALLOC(d.rs_head, (size_t)cap * 4);
     ALLOC(d.fired_mask, (size_t)cap * 4);
     size_t rec_events_per_ent = 0;
     for (int i = 0; i < nro; i++) rec_events_per_ent += w->tab.rec_rows[w->tab.recops[i].rec];
@@ -1527,7 +1563,7 @@ int nfk_commit(void* world) {
     d.fi_tcap = kTile * std::max(NK, 1);
     d.re_tcap = (int32_t)(kRTile * std::max<size_t>(rec_events_per_ent, 1));
     const size_t nt = cap / kTile, nrt = cap / kRTile;
-    const size_t ev_n = nt * d.ev_tcap, fi_n = nt * d.fi_tcap, re_n = nro ? nrt * d.re_tcap : 1;
+    const size_t ev_n = nt * d.ev_tcap, fi_n = nt * d.fi_tcap, re_n = d.has_recops ? nrt * d.re_tcap : 1;
     ALLOC(d.t_ev, nt * 4);
     ALLOC(d.t_fi, nt * 4);
     ALLOC(d.t_re, nrt * 4);
@@ -1620,6 +1656,7 @@ int nfk_commit(void* world) {
     }
     HIPCHK(hipMemset(d.e_flags, 0, cap));
     HIPCHK(hipMemset(d.ext_head, 0, (size_t)cap * 4));
+    HIPCHK(hipMemset(d.rs_head, 0, (size_t)cap * 4));
     HIPCHK(hipMemset(d.fired_mask, 0, (size_t)cap * 4));
     HIPCHK(hipMemset(d.t_ev, 0, nt * 4));
     HIPCHK(hipMemset(d.t_fi, 0, nt * 4));
@@ -1657,6 +1694,94 @@ int nfk_set_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
             return fail(NFK_ERR_ARG, "bad property id");
         }
         x[i] = World::XOp{(uint32_t)obj, (uint32_t)pid[i], bits[i]};
+    }
+    return NFK_OK;
+}
+
+int nfk_set_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* rec,
+                    const int32_t* row, const int32_t* col, const uint8_t* is_float, const uint64_t* bits) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !rec || !row || !col || !bits))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    // every call is checked before any is queued; one GUID lookup per call
+    w->look.resize(n);
+    w->obj_of.find_many(n, gh, gd, w->look.data());
+    for (int32_t i = 0; i < n; i++) {
+        if (w->look[i] < 0)  // NFCKernelModule logs "There is no object" and returns false (KM:505)
+            return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
+        const int32_t r = rec[i];
+        if (r < 0 || r >= w->cfg.n_rec || !w->rec_defined[r] || row[i] < 0 || row[i] >= w->tab.rec_rows[r] ||
+            col[i] < 0 || col[i] >= w->tab.rec_cols[r])
+            return fail(NFK_ERR_ARG, "record cell out of range");
+    }
+    w->rsq.reserve(w->rsq.size() + n);
+    for (int32_t i = 0; i < n; i++) {
+        // NFCRecord::SetInt / SetFloat on a column of the other type write nothing (RC:189 / RC:250)
+        if (is_float && (is_float[i] != 0) != (w->rec_ctype[rec[i]][col[i]] != 0)) continue;
+        w->rsq.push_back(World::RSOp{(uint32_t)w->look[i], ((uint32_t)rec[i] << 16) | ((uint32_t)row[i] << 8) | (uint32_t)col[i],
+                                     bits[i]});
+    }
+    return NFK_OK;
+}
+
+int nfk_get_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* rec,
+                    const int32_t* row, const int32_t* col, uint64_t* bits) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !rec || !row || !col || !bits))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    std::vector<int32_t> obj(n);
+    w->obj_of.find_many(n, gh, gd, obj.data());
+    for (int32_t i = 0; i < n; i++) {
+        if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
+        const int32_t r = rec[i];
+        if (r < 0 || r >= w->cfg.n_rec || !w->rec_defined[r] || row[i] < 0 || row[i] >= w->tab.rec_rows[r] ||
+            col[i] < 0 || col[i] >= w->tab.rec_cols[r])
+            return fail(NFK_ERR_ARG, "record cell out of range");
+    }
+    // the queued SetRecord calls of each (object, cell), in call order
+    std::unordered_map<uint64_t, std::vector<uint32_t>> q;
+    for (size_t k = 0; k < w->rsq.size(); k++) q[((uint64_t)w->rsq[k].obj << 19) | w->rsq[k].rrc].push_back((uint32_t)k);
+    HIPCHK(hipStreamSynchronize(w->stream));
+    for (int32_t i = 0; i < n; i++) {
+        const int32_t o = obj[i], r = rec[i], rows = w->tab.rec_rows[r], cols = w->tab.rec_cols[r];
+        const uint64_t* cell;
+        const uint64_t* used;
+        if (w->src_row[o] >= 0) {  // entered in this window: its row of the import buffer
+            int64_t off = w->n_prop + 4 * w->cfg.n_kind;
+            for (int x = 0; x < r; x++) off += (int64_t)w->tab.rec_rows[x] * w->tab.rec_cols[x] + 1;
+            const uint64_t* base = w->ins_rows + (size_t)w->src_row[o] * w->row_words + off;
+            cell = base + (size_t)col[i] * rows + row[i];
+            used = base + (size_t)rows * cols;
+        } else if (w->slot_of_obj[o] >= 0) {
+            const size_t sl = (size_t)w->slot_of_obj[o];
+            cell = w->d.rcells[r] + (sl * cols + col[i]) * rows + row[i];
+            used = w->d.rused[r] + sl;
+        } else {
+            return fail(NFK_ERR_STATE, "object without a slot");
+        }
+        uint64_t c = 0, u = 0;
+        HIPCHK(hipMemcpy(&u, used, 8, hipMemcpyDeviceToHost));
+        if (!((u >> row[i]) & 1)) {  // NFCRecord::GetInt / GetFloat of an unused row (RC:623): 0
+            bits[i] = 0;
+            continue;
+        }
+        HIPCHK(hipMemcpy(&c, cell, 8, hipMemcpyDeviceToHost));
+        // this window's queued Sets of the cell on top (RC:182 / RC:243)
+        auto it = q.find(((uint64_t)o << 19) | ((uint32_t)r << 16) | ((uint32_t)row[i] << 8) | (uint32_t)col[i]);
+        if (it != q.end())
+            for (uint32_t k : it->second) {
+                const uint64_t b = w->rsq[k].bits;
+                if (w->rec_ctype[r][col[i]]) {
+                    double bd, cd;
+                    memcpy(&bd, &b, 8);
+                    memcpy(&cd, &c, 8);
+                    const double df = bd - cd;
+                    if (!(df < 0.001 && df > -0.001)) c = b;
+                } else {
+                    c = b;
+                }
+            }
+        bits[i] = c;
     }
     return NFK_OK;
 }
@@ -2120,6 +2245,80 @@ int nfk_execute(void* world, int64_t now_ms) {
             d.ev_new = w->d.ev_new; d.ev_moff = w->d.ev_moff;
         }
     }
+    // SetRecordInt / SetRecordFloat: (slot, cell) groups, each group's calls in call order (key
+    // slot << 19 | rec << 16 | row << 8 | col); the slots with groups, in slot order, each run by
+    // k_rset_slots; the most groups of one record tile bounds that tile's extra events
+    const size_t n_rq = w->rsq.size();
+    std::vector<uint32_t>& rs_slot = w->rs_slot_h;
+    std::vector<uint32_t>& rs_rrc = w->rs_rrc_h;
+    std::vector<uint32_t>& rs_first = w->rs_first_h;
+    std::vector<uint32_t>& rss_slot = w->rss_slot_h;
+    std::vector<uint32_t>& rss_g0 = w->rss_g0_h;
+    rs_slot.clear();
+    rs_rrc.clear();
+    rs_first.clear();
+    rss_slot.clear();
+    rss_g0.clear();
+    std::vector<uint64_t>& rpk = w->rpk;
+    rpk.clear();
+    const int rib = bits_for(n_rq);
+    const uint64_t rim = (1ull << rib) - 1;
+    int64_t max_rs_tile = 0;
+    if (n_rq) {
+        rpk.resize(n_rq);
+        uint64_t kor = 0;
+        size_t k = 0;
+        for (size_t i = 0; i < n_rq; i++) {
+            const int32_t sl = w->slot_of_obj[w->rsq[i].obj];
+            if (sl < 0) continue;  // destroyed / exported in this window
+            const uint64_t key = ((uint64_t)(uint32_t)sl << 19) | w->rsq[i].rrc;
+            kor |= key;
+            rpk[k++] = (key << rib) | i;
+        }
+        rpk.resize(k);
+        if (bits_for(kor) + rib > 64) return fail(NFK_ERR_CAPACITY, "too many queued SetRecord calls");
+        radix_sort_packed(rpk, w->rpk_t, rib, bits_for(kor));
+        uint64_t prev = ~0ull;
+        uint32_t prev_slot = 0xFFFFFFFFu, cur_rt = 0xFFFFFFFFu;
+        int64_t tile_groups = 0;
+        for (size_t i = 0; i < k; i++) {
+            const uint64_t key = rpk[i] >> rib;
+            if (key == prev) continue;
+            prev = key;
+            const uint32_t sl = (uint32_t)(key >> 19);
+            if (sl != prev_slot) {
+                prev_slot = sl;
+                rss_slot.push_back(sl);
+                rss_g0.push_back((uint32_t)rs_slot.size());
+            }
+            if (sl / kRTile != cur_rt) {
+                cur_rt = sl / kRTile;
+                tile_groups = 0;
+            }
+            max_rs_tile = std::max(max_rs_tile, ++tile_groups);
+            rs_slot.push_back(sl);
+            rs_rrc.push_back((uint32_t)(key & 0x7FFFF));
+            rs_first.push_back((uint32_t)i);
+        }
+        rs_first.push_back((uint32_t)k);
+        // a record tile's events: its slots' record-program cells plus its SetRecord groups
+        int64_t cells = 0;
+        for (int j = 0; j < d.n_rops; j++) cells += d.rops[j].rows;
+        const int64_t need_re = (int64_t)kRTile * std::max<int64_t>(cells, 1) + max_rs_tile;
+        if (need_re > w->d.re_tcap) {
+            int r = grow_rec_tiles(w, need_re);
+            if (r) {
+                w->xops.clear();
+                w->hops.clear();
+                w->rsq.clear();
+                return r;
+            }
+            d.re_tcap = w->d.re_tcap;
+            d.re_slot = w->d.re_slot; d.re_rrc = w->d.re_rrc; d.re_old = w->d.re_old;
+            d.re_new = w->d.re_new; d.re_moff = w->d.re_moff;
+        }
+    }
+    const size_t ngr = rs_slot.size(), nrss = rss_slot.size(), nrc = rpk.size();
     tp[2] = clk::now();
     // schedule calls: pre-scan (remove-list key owner, RemoveSchedule(self)) and post-scan (remove,
     // add), folded per (slot, kind) in call order (key slot << 5 | kind):
@@ -2224,12 +2423,21 @@ int nfk_execute(void* world, int64_t now_ms) {
     size_t off_qs = align16(off_po + npre * 4), off_qk = align16(off_qs + npost * 4);
     size_t off_qo = align16(off_qk + npost * 4), off_qi = align16(off_qo + npost * 4);
     size_t off_qc = align16(off_qi + npost * 4), off_qt = align16(off_qc + npost * 4);
-    size_t total = align16(off_qt + npost * 8);
+    size_t off_rs = align16(off_qt + npost * 8), off_rr = align16(off_rs + ngr * 4);
+    size_t off_rf = align16(off_rr + ngr * 4), off_rb = align16(off_rf + (ngr + 1) * 4);
+    size_t off_ss = align16(off_rb + nrc * 8), off_sg = align16(off_ss + nrss * 4);
+    size_t total = align16(off_sg + nrss * 4);
     if (ng) {
         int r = dev_reserve(w, (void**)&w->xs_buf, &w->xs_cap, ng * 16);
         if (r) return r;
     }
-    if (total > 0 && (ng || npre || npost)) {
+    if (ngr) {
+        int r = dev_reserve(w, (void**)&w->rs_buf, &w->rs_cap, ngr * 16);
+        if (r) return r;
+        r = dev_reserve(w, (void**)&w->rss_buf, &w->rss_cap, nrss * 16);
+        if (r) return r;
+    }
+    if (total > 0 && (ng || npre || npost || ngr)) {
         int r = pin_reserve(w, total);
         if (r) return r;
         char* P = (char*)w->pin;
@@ -2243,6 +2451,15 @@ int nfk_execute(void* world, int64_t now_ms) {
         for (size_t i = 0; i < npre; i++) {
             ((uint32_t*)(P + off_ps))[i] = pre_slot[i];
             ((uint32_t*)(P + off_po))[i] = pre_op[i];
+        }
+        if (ngr) {
+            memcpy(P + off_rs, rs_slot.data(), ngr * 4);
+            memcpy(P + off_rr, rs_rrc.data(), ngr * 4);
+            memcpy(P + off_rf, rs_first.data(), (ngr + 1) * 4);
+            uint64_t* rb = (uint64_t*)(P + off_rb);
+            for (size_t i = 0; i < nrc; i++) rb[i] = w->rsq[rpk[i] & rim].bits;
+            memcpy(P + off_ss, rss_slot.data(), nrss * 4);
+            memcpy(P + off_sg, rss_g0.data(), nrss * 4);
         }
         for (size_t i = 0; i < npost; i++) {
             ((uint32_t*)(P + off_qs))[i] = post[i].slot;
@@ -2265,6 +2482,21 @@ int nfk_execute(void* world, int64_t now_ms) {
     d.x_bits = ng ? (const uint64_t*)(S + off_xb) : nullptr;
     d.x_old = ng ? (uint64_t*)w->xs_buf : nullptr;
     d.x_new = ng ? (uint64_t*)w->xs_buf + ng : nullptr;
+    d.n_rs = (int32_t)ngr;
+    d.n_rss = (int32_t)nrss;
+    d.rs_slot = ngr ? (const uint32_t*)(S + off_rs) : nullptr;
+    d.rs_rrc = ngr ? (const uint32_t*)(S + off_rr) : nullptr;
+    d.rs_first = ngr ? (const uint32_t*)(S + off_rf) : nullptr;
+    d.rs_bits = ngr ? (const uint64_t*)(S + off_rb) : nullptr;
+    d.rss_slot = ngr ? (const uint32_t*)(S + off_ss) : nullptr;
+    d.rss_g0 = ngr ? (const uint32_t*)(S + off_sg) : nullptr;
+    d.rs_old = ngr ? (uint64_t*)w->rs_buf : nullptr;
+    d.rs_new = ngr ? (uint64_t*)w->rs_buf + ngr : nullptr;
+    d.rss_ev = ngr ? (uint32_t*)w->rss_buf : nullptr;
+    d.rss_msg = ngr ? (uint32_t*)w->rss_buf + nrss : nullptr;
+    d.rss_pos = ngr ? (uint32_t*)w->rss_buf + 2 * nrss : nullptr;
+    d.rss_pmsg = ngr ? (uint32_t*)w->rss_buf + 3 * nrss : nullptr;
+    w->rsq.clear();
     w->xops.clear();
     w->hops.clear();
     w->dcache.clear();
@@ -2278,8 +2510,13 @@ int nfk_execute(void* world, int64_t now_ms) {
         w->post_kind.push_back(q.kind);
     }
     d.has_pre = npre > 0;
-    if (ng || npre) {
+    if (ng || npre || ngr) {
         TimeScope ts(w, KT_AUX);
+        if (ngr) {
+            hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)((nrss + 255) / 256)), dim3(256), 0, w->stream,
+                               d.rss_slot, (int32_t)nrss, d.rs_head);
+            hipLaunchKernelGGL(k_rsets, dim3((unsigned)((ngr + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, d);
+        }
         if (ng) {
             hipLaunchKernelGGL(k_ext_scatter, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, w->stream,
                                d.x_slot, (int32_t)ng, d.ext_head);
@@ -2308,13 +2545,18 @@ int nfk_execute(void* world, int64_t now_ms) {
         if (d.has_recops && d.n_rtiles) {
             int64_t cells = 0, per = 0;
             for (int j = 0; j < d.n_rops; j++) cells += d.rops[j].rows;
-            for (int c = 0; c < NFK_MAX_CLASSES; c++)
-                for (int j = 0; j < d.n_rops; j++) {
-                    const uint8_t f = w->tab.rflags[c][d.rops[j].rec];
+            auto rper = [&](int rec) {
+                for (int c = 0; c < NFK_MAX_CLASSES; c++) {
+                    const uint8_t f = w->tab.rflags[c][rec];
                     per = std::max<int64_t>(per, (f & NFK_PUBLIC) ? std::max(w->max_np, 1)
                                                  : ((f & NFK_PRIVATE) && !(f & NFK_UPLOAD)) ? 1 : 0);
                 }
-            rtcap = ((int64_t)kRTile * cells * per + 3) & ~(int64_t)3;  // (16-byte aligned runs)
+            };
+            for (int j = 0; j < d.n_rops; j++) rper(d.rops[j].rec);
+            if (ngr)  // SetRecord groups may hit any record
+                for (int r = 0; r < d.n_rec; r++)
+                    if (w->rec_defined[r]) rper(r);
+            rtcap = (((int64_t)kRTile * cells + max_rs_tile) * per + 3) & ~(int64_t)3;  // (16-byte aligned runs)
             rfuse = tcap * d.n_tiles + rtcap * d.n_rtiles <= kMsgStrideLimit;
         }
         const int64_t need = tcap * d.n_tiles + (rfuse ? rtcap * d.n_rtiles
@@ -2374,12 +2616,23 @@ int nfk_execute(void* world, int64_t now_ms) {
     if (d.has_recops && d.n_rtiles) {
         TimeScope ts(w, KT_REC);
         const dim3 g((unsigned)((d.n_rtiles + 3) / 4)), b(kTPB);
-        if (d.n_rops <= 1)
-            hipLaunchKernelGGL((k_records<1, 4>), g, b, 0, w->stream, d);
+        if (nrss)  // the SetRecord slots' events and messages, for k_records to reserve
+            hipLaunchKernelGGL((k_rset_slots<false>), dim3((unsigned)((nrss + 3) / 4)), b, 0, w->stream, d);
+        if (nrss) {  // (the SetRecord slots' instantiation: the fast path without them stays lean)
+            if (d.n_rops <= 1)
+                hipLaunchKernelGGL((k_records<1, 4, true>), g, b, 0, w->stream, d);
+            else if (d.n_rops <= 2)
+                hipLaunchKernelGGL((k_records<2, 4, true>), g, b, 0, w->stream, d);
+            else
+                hipLaunchKernelGGL((k_records<NFK_MAX_OPS, 2, true>), g, b, 0, w->stream, d);
+        } else if (d.n_rops <= 1)
+            hipLaunchKernelGGL((k_records<1, 4, false>), g, b, 0, w->stream, d);
         else if (d.n_rops <= 2)
-            hipLaunchKernelGGL((k_records<2, 4>), g, b, 0, w->stream, d);
+            hipLaunchKernelGGL((k_records<2, 4, false>), g, b, 0, w->stream, d);
         else
-            hipLaunchKernelGGL((k_records<NFK_MAX_OPS, 2>), g, b, 0, w->stream, d);
+            hipLaunchKernelGGL((k_records<NFK_MAX_OPS, 2, false>), g, b, 0, w->stream, d);
+        if (nrss)  // ... and written into the room k_records left
+            hipLaunchKernelGGL((k_rset_slots<true>), dim3((unsigned)((nrss + 3) / 4)), b, 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
     if (npost) {

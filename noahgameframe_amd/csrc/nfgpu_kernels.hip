@@ -406,6 +406,199 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
 }
 
 // ---------------------------------------------------------------------------------
+// NFIKernelModule::SetRecordInt / SetRecordFloat (KM:505 / KM:545) between frames: one thread per
+// (slot, cell) group applies the group's calls in call order through NFCRecord::SetInt / SetFloat
+// (RC:182 / RC:243): refused on a row that is not used (RC:194); an int cell changes when the bits
+// differ, an f64 cell unless |new - cur| < 0.001 (TData::operator==, NFIDataList.h:106-113).
+__global__ void k_rs_scatter(const uint32_t* __restrict__ rss_slot, int32_t n, uint32_t* __restrict__ rs_head) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) rs_head[rss_slot[i]] = (uint32_t)i + 1;  // 1 + the slot's index among the SetRecord slots
+}
+
+__global__ __launch_bounds__(kTPB) void k_rsets(Dev d) {
+    const int g = blockIdx.x * kTPB + threadIdx.x;
+    if (g >= d.n_rs) return;
+    const uint32_t e = d.rs_slot[g], rrc = d.rs_rrc[g];
+    const int r = (int)(rrc >> 16), row = (int)((rrc >> 8) & 0xFF), col = (int)(rrc & 0xFF);
+    const int rows = d.tab->rec_rows[r], cols = d.tab->rec_cols[r];
+    uint64_t* cells = nullptr;
+    const uint64_t* usedp = nullptr;
+#pragma unroll
+    for (int q = 0; q < NFK_MAX_RECORDS; q++)
+        if (q == r) {
+            cells = d.rcells[q];
+            usedp = d.rused[q];
+        }
+    uint64_t* cell = cells + ((size_t)e * cols + col) * rows + row;
+    const uint64_t c0 = *cell;
+    uint64_t v = c0;
+    if ((usedp[e] >> row) & 1) {
+        const bool f64 = d.tab->rec_ctype[r][col] != 0;
+        for (uint32_t k = d.rs_first[g]; k < d.rs_first[g + 1]; k++) {
+            const uint64_t x = d.rs_bits[k];
+            if (f64) {
+                const double df = __longlong_as_double((long long)x) - __longlong_as_double((long long)v);
+                if (!(df < 0.001 && df > -0.001)) v = x;
+            } else if (x != v) {
+                v = x;
+            }
+        }
+        if (v != c0) *cell = v;
+    }
+    d.rs_old[g] = c0;
+    d.rs_new[g] = v;
+}
+
+// The slots with SetRecord groups this window, one wave each (lane = row), every record of the
+// slot, every column in order: a cell's event runs from its frame-start value (the group's rs_old,
+// else the cell) to its value after the slot's fired record ops, which apply to the value the Sets
+// left (RC:182 / RC:243); it is dropped when the bits are equal.  Events in (rec, row, col) order,
+// as k_records' own.  kEmit = false: count the slot's events and messages (rss_ev, rss_msg) before
+// k_records, which reserves their room in the slot's place in its tile (rss_pos, rss_pmsg); kEmit:
+// write them there, with the cells' write-back and the fused fan-out, after it.
+template <bool kEmit>
+__global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
+    __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
+    for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
+        ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int si = blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6);
+    if (si >= d.n_rss) return;  // wave-uniform
+    const int e = (int)d.rss_slot[si], g0 = (int)d.rss_g0[si];
+    int g1 = g0;
+    while (g1 < d.n_rs && d.rs_slot[g1] == (uint32_t)e) g1++;
+    const uint32_t fmask = d.has_recops ? d.fired_mask[e] & d.rop_kinds : 0u;
+    const uint64_t desc = d.fan_desc[e];
+    const unsigned cls = (unsigned)(desc >> 60);
+    const int nro = d.n_rops;
+    const int rt = e / kRTile;
+    const size_t re0 = (size_t)rt * d.re_tcap;
+    const uint32_t mrb = d.fuse_rec ? d.msg_rb0 + (uint32_t)rt * d.msg_rtcap : 0u;
+    unsigned pos = kEmit ? d.rss_pos[si] : 0u, pmsg = kEmit ? d.rss_pmsg[si] : 0u;
+    unsigned bytes = 0;
+    for (int r = 0; r < d.n_rec; r++) {
+        const int rows = d.tab->rec_rows[r], cols = d.tab->rec_cols[r];
+        if (rows <= 0) continue;
+        // record r's arrays by a select over compile-time indices (a run-time index into the
+        // kernel-argument arrays would put them in scratch)
+        uint64_t* cells = nullptr;
+        const uint64_t* usedp = nullptr;
+#pragma unroll
+        for (int q = 0; q < NFK_MAX_RECORDS; q++)
+            if (q == r) {
+                cells = d.rcells[q];
+                usedp = d.rused[q];
+            }
+        const uint8_t rfl = s_rflags[cls][r];
+        const unsigned per = event_msgs(desc, rfl);
+        const uint64_t used = usedp[e];
+        const bool act = lane < rows;
+        // cell (r, lane, c): its event (old, new) if any, and whether a record op writes nb back
+        auto eval = [&](int c, uint64_t& ob, uint64_t& nb, bool& wb) -> bool {
+            bool op = false;
+            int code = 0;
+            int64_t oa = 0, obb = 0, oc = 0;
+#pragma unroll
+            for (int j = 0; j < NFK_MAX_OPS; j++)
+                if (j < nro && d.rops[j].rec == r && d.rops[j].col == c && ((fmask >> d.rops[j].kind) & 1)) {
+                    op = true;
+                    code = d.rops[j].code;
+                    oa = d.rops[j].a;
+                    obb = d.rops[j].b;
+                    oc = d.rops[j].c;
+                }
+            int gi = -1;
+            const uint32_t key = ((uint32_t)r << 16) | ((uint32_t)lane << 8) | (uint32_t)c;
+            for (int g = g0; g < g1; g++)
+                if (d.rs_rrc[g] == key) gi = g;
+            wb = false;
+            if (!act || (!op && gi < 0)) return false;
+            const uint64_t cur = cells[((size_t)e * cols + c) * rows + lane];
+            nb = cur;
+            if (op && ((used >> lane) & 1)) {
+                if (code == NFK_OP_RIADD_CLAMP) {
+                    int64_t v = (int64_t)(cur + (uint64_t)oa);
+                    v = v < obb ? obb : v;
+                    v = v > oc ? oc : v;
+                    if (v != (int64_t)cur) {  // TData::operator== (NFIDataList.h:98)
+                        nb = (uint64_t)v;
+                        wb = true;
+                    }
+                } else {
+                    const double x = __longlong_as_double((long long)cur);
+                    const double m = x * __longlong_as_double(oa);
+                    const double v = m + __longlong_as_double(obb);
+                    const double df = v - x;
+                    if (!(df < 0.001 && df > -0.001)) {  // NFIDataList.h:106-113
+                        nb = (uint64_t)__double_as_longlong(v);
+                        wb = true;
+                    }
+                }
+            }
+            ob = gi >= 0 ? d.rs_old[gi] : cur;
+            return ob != nb;
+        };
+        unsigned cnt = 0;
+        for (int c = 0; c < cols; c++) {
+            uint64_t ob, nb;
+            bool wb;
+            cnt += eval(c, ob, nb, wb) ? 1u : 0u;
+        }
+        const unsigned incl = wave_incl_scan_u32(cnt);
+        const unsigned total = (unsigned)__builtin_amdgcn_readlane((int)incl, 63);
+        if constexpr (kEmit) {
+            unsigned k = incl - cnt;
+            for (int c = 0; c < cols; c++) {
+                uint64_t ob, nb;
+                bool wb;
+                const bool ev = eval(c, ob, nb, wb);
+                if (wb) {
+                    __builtin_nontemporal_store(nb, cells + ((size_t)e * cols + c) * rows + lane);
+                    bytes += 8;
+                }
+                if (!ev) continue;
+                const unsigned at = pos + k;
+                const uint32_t lmo = pmsg + per * k;
+                d.re_slot[re0 + at] = (uint32_t)e;
+                d.re_rrc[re0 + at] = ((uint32_t)r << 16) | ((uint32_t)lane << 8) | (uint32_t)c;
+                d.re_old[re0 + at] = ob;
+                d.re_new[re0 + at] = nb;
+                d.re_moff[re0 + at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
+                bytes += 28;
+                if (d.fuse_rec && per) {  // GetBroadCastObject (AOI:531-593)
+                    uint32_t* out = d.msg_rcpt + mrb + lmo;
+                    if (!(rfl & NFK_PUBLIC)) {
+                        out[0] = (uint32_t)e;  // private & !upload: the entity itself
+                        bytes += 4;
+                    } else {  // every player of the group but self
+                        const uint32_t np = (uint32_t)((desc >> 32) & 0x3FFF);
+                        const uint32_t r1 = (uint32_t)((desc >> 46) & 0x3FFF);
+                        uint32_t q = 0;
+                        for (uint32_t u = 0; u < np; u++) {
+                            if (u + 1 == r1) continue;
+                            out[q++] = (uint32_t)d.pl_slot[(uint32_t)desc + u];
+                        }
+                        bytes += 4 * (per + np);
+                    }
+                }
+                k++;
+            }
+            if (act) bytes += 8u * (unsigned)cols;  // the row's cells read
+        }
+        pos += total;
+        pmsg += per * total;
+    }
+    if constexpr (kEmit) {
+        const unsigned wb = (unsigned)wave_sum(bytes);
+        if (lane == 0 && wb) tally_add(d, kTallyRec, (unsigned long long)wb + 16u * (unsigned)(g1 - g0));
+    } else if (lane == 0) {
+        d.rss_ev[si] = pos;
+        d.rss_msg[si] = pmsg;
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // Record effects: one wave per 64-slot record tile, lane = row; the wave walks its slots in
 // order, kGroup at a time with every cell load of the group issued before any is consumed and
 // the next group's loads issued before this group's stores.  A record span's events are staged
@@ -418,11 +611,13 @@ template <int kOps, int kGroup>
 struct RecGrp {  // one group of slots with record work: their cells and used-row masks
     int js[kGroup];
     uint32_t masks[kGroup];
+    uint32_t rsg[kGroup];  // 1 + the slot's index among the SetRecord slots (0: none)
     uint64_t used[kGroup][kOps];
     uint64_t cur[kGroup][kOps];
 };
 
-template <int kOps, int kGroup>
+// kSets: the frame has SetRecord slots (k_rset_slots writes theirs; here their room is reserved)
+template <int kOps, int kGroup, bool kSets>
 __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
     __shared__ uint64_t s_eold[kTPB / 64][kOps * 64], s_enew[kTPB / 64][kOps * 64];  // a span's events,
@@ -438,17 +633,21 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     unsigned bytes = 0;    // per lane
     unsigned sbytes = 0;   // per wave (wave-uniform)
     // lane j holds slot s0 + j's fired mask and fan-out descriptor
-    uint32_t my_mask = 0;
+    uint32_t my_mask = 0, my_rs = 0;
     uint64_t my_desc = 0;
     if (lane < kRTile && s0 + lane < d.N) {
         my_mask = d.fired_mask[s0 + lane] & d.rop_kinds;
         bytes += 4;
-        if (my_mask) {
+        if (kSets) {
+            my_rs = d.rs_head[s0 + lane];
+            bytes += 4;
+        }
+        if (my_mask || my_rs) {
             my_desc = d.fan_desc[s0 + lane];
             bytes += 8;
         }
     }
-    unsigned long long work = __ballot(my_mask != 0);
+    unsigned long long work = __ballot(my_mask != 0 || my_rs != 0);
     unsigned pos = 0, pmsg = 0;  // tile-local
     // this tile's output runs as wave-uniform base pointers, indexed by 32-bit tile-local offsets
     const size_t re0 = (size_t)rt * d.re_tcap;
@@ -469,6 +668,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             G.js[g] = work ? __builtin_ctzll(work) : -1;
             if (work) work &= work - 1;
             G.masks[g] = G.js[g] >= 0 ? (uint32_t)__shfl((int)my_mask, G.js[g], 64) : 0u;
+            G.rsg[g] = (kSets && G.js[g] >= 0) ? (uint32_t)__shfl((int)my_rs, G.js[g], 64) : 0u;
         }
 #pragma unroll
         for (int g = 0; g < kGroup; g++)
@@ -476,7 +676,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             for (int j = 0; j < kOps; j++) {
                 G.used[g][j] = 0;
                 G.cur[g][j] = 0;
-                if (j < nro && G.js[g] >= 0 && ((G.masks[g] >> d.rops[j].kind) & 1)) {
+                if (j < nro && G.js[g] >= 0 && !(kSets && G.rsg[g]) && ((G.masks[g] >> d.rops[j].kind) & 1)) {
                     const int e = s0 + G.js[g];
                     G.used[g][j] = d.rops[j].used[e];
                     if (lane < d.rops[j].rows)
@@ -491,6 +691,17 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             const int e = s0 + G.js[g];
             const uint64_t desc = (uint64_t)__shfl((long long)my_desc, G.js[g], 64);
             const unsigned cls = (unsigned)(desc >> 60);
+            if (kSets && G.rsg[g]) {  // (wave-uniform) a slot with SetRecord calls: k_rset_slots writes its
+                             // events into the room reserved here
+                const int i = (int)G.rsg[g] - 1;
+                if (lane == 0) {
+                    d.rss_pos[i] = pos;
+                    d.rss_pmsg[i] = pmsg;
+                }
+                pos += d.rss_ev[i];
+                pmsg += d.rss_msg[i];
+                continue;
+            }
             bool ch[kOps], wr[kOps];
             uint64_t nv[kOps];
 #pragma unroll
@@ -621,6 +832,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
         pick_load(A);
         process(B);
     }
+    if (kSets && my_rs) d.rs_head[s0 + lane] = 0;  // (the groups are consumed)
     if (lane == 0) {
         d.t_re[rt] = pos;
         d.t_msg[d.n_tiles + rt] = pmsg;

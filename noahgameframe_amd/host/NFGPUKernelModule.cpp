@@ -260,6 +260,63 @@ bool NFGPUKernelModule::SetPropertyInt(const NFGUID& self, const std::string& na
     return true;
 }
 
+bool NFGPUKernelModule::SetRecordInt(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol,
+                                     int64_t nValue) {
+    auto it = record_id_.find(strRecordName);
+    if (it == record_id_.end() || ObjectIndex(self) < 0) return false;
+    const RecordDef& rd = records_[it->second];
+    // NFCRecord::SetInt: ValidPos and the column type (RC:184-192)
+    if (nRow < 0 || nRow >= rd.rows || nCol < 0 || nCol >= (int)rd.cols.size() || rd.cols[nCol] != TDATA_INT)
+        return false;
+    const int32_t rec = it->second, row = nRow, col = nCol;
+    const uint8_t f = 0;
+    const uint64_t b = (uint64_t)nValue;
+    if (nfk_set_records(world_, 1, &self.nHead64, &self.nData64, &rec, &row, &col, &f, &b) != NFK_OK) return false;
+    pending_calls_++;
+    return true;
+}
+
+bool NFGPUKernelModule::SetRecordFloat(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol,
+                                       double dwValue) {
+    auto it = record_id_.find(strRecordName);
+    if (it == record_id_.end() || ObjectIndex(self) < 0) return false;
+    const RecordDef& rd = records_[it->second];
+    if (nRow < 0 || nRow >= rd.rows || nCol < 0 || nCol >= (int)rd.cols.size() || rd.cols[nCol] != TDATA_FLOAT)
+        return false;
+    const int32_t rec = it->second, row = nRow, col = nCol;
+    const uint8_t f = 1;
+    uint64_t b;
+    memcpy(&b, &dwValue, 8);
+    if (nfk_set_records(world_, 1, &self.nHead64, &self.nData64, &rec, &row, &col, &f, &b) != NFK_OK) return false;
+    pending_calls_++;
+    return true;
+}
+
+int64_t NFGPUKernelModule::GetRecordInt(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol) {
+    auto it = record_id_.find(strRecordName);
+    if (it == record_id_.end() || ObjectIndex(self) < 0) return 0;
+    const RecordDef& rd = records_[it->second];
+    if (nRow < 0 || nRow >= rd.rows || nCol < 0 || nCol >= (int)rd.cols.size() || rd.cols[nCol] != TDATA_INT) return 0;
+    const int32_t rec = it->second, row = nRow, col = nCol;
+    uint64_t b = 0;
+    if (nfk_get_records(world_, 1, &self.nHead64, &self.nData64, &rec, &row, &col, &b) != NFK_OK) return 0;
+    return (int64_t)b;
+}
+
+double NFGPUKernelModule::GetRecordFloat(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol) {
+    auto it = record_id_.find(strRecordName);
+    if (it == record_id_.end() || ObjectIndex(self) < 0) return 0.0;
+    const RecordDef& rd = records_[it->second];
+    if (nRow < 0 || nRow >= rd.rows || nCol < 0 || nCol >= (int)rd.cols.size() || rd.cols[nCol] != TDATA_FLOAT)
+        return 0.0;
+    const int32_t rec = it->second, row = nRow, col = nCol;
+    uint64_t b = 0;
+    if (nfk_get_records(world_, 1, &self.nHead64, &self.nData64, &rec, &row, &col, &b) != NFK_OK) return 0.0;
+    double v;
+    memcpy(&v, &b, 8);
+    return v;
+}
+
 bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& name, double v) {
     auto it = prop_id_.find(name);
     if (it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT || ObjectIndex(self) < 0) return false;

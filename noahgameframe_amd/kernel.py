@@ -75,7 +75,8 @@ def load_library(path=LIB_PATH):
         "nfk_define_kind": [VP, I32, VP, I32],
         "nfk_create_objects": [VP, I32, VP, VP, VP, VP, VP, VP], "nfk_load_prop": [VP, I32, VP],
         "nfk_load_record": [VP, I32, VP, VP], "nfk_commit": [VP],
-        "nfk_set_props": [VP, I32, VP, VP, VP, VP],
+        "nfk_set_props": [VP, I32, VP, VP, VP, VP], "nfk_set_records": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
+        "nfk_get_records": [VP, I32, VP, VP, VP, VP, VP, VP],
         "nfk_add_schedules": [VP, I32, VP, VP, VP, VP, VP, VP],
         "nfk_remove_schedule": [VP, I64, I64, I32], "nfk_remove_all_schedules": [VP, I64, I64],
         "nfk_schedule_calls": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
@@ -184,6 +185,31 @@ class NFKernelModule:
         a = [np.ascontiguousarray(x, t) for x, t in
              ((guid_head, np.int64), (guid_data, np.int64), (pid, np.int32), (bits, np.uint64))]
         self._chk(self.lib.nfk_set_props(self.h, len(a[0]), *[_p(x) for x in a]))
+
+    # ---- NFIKernelModule::SetRecordInt / SetRecordFloat ----
+    def set_records(self, guid_head, guid_data, rec, row, col, bits, is_float=None):
+        a = [np.ascontiguousarray(x, t) for x, t in
+             ((guid_head, np.int64), (guid_data, np.int64), (rec, np.int32), (row, np.int32), (col, np.int32))]
+        f = None if is_float is None else np.ascontiguousarray(is_float, np.uint8)
+        b = np.ascontiguousarray(bits, np.uint64)
+        self._chk(self.lib.nfk_set_records(self.h, len(a[0]), *[_p(x) for x in a], _p(f) if f is not None else None,
+                                           _p(b)))
+
+    def get_records(self, guid_head, guid_data, rec, row, col):
+        """NFIKernelModule::GetRecordInt/Float for n cells: raw 64-bit patterns, read-your-writes"""
+        a = [np.ascontiguousarray(x, t) for x, t in
+             ((guid_head, np.int64), (guid_data, np.int64), (rec, np.int32), (row, np.int32), (col, np.int32))]
+        out = np.zeros(len(a[0]), np.uint64)
+        self._chk(self.lib.nfk_get_records(self.h, len(a[0]), *[_p(x) for x in a], _p(out)))
+        return out
+
+    def SetRecordInt(self, guid, rec, row, col, value):
+        self.set_records([guid[0]], [guid[1]], [rec], [row], [col], [np.int64(value).view(np.uint64)], [0])
+        return True
+
+    def SetRecordFloat(self, guid, rec, row, col, value):
+        self.set_records([guid[0]], [guid[1]], [rec], [row], [col], [np.float64(value).view(np.uint64)], [1])
+        return True
 
     def SetPropertyInt(self, guid, prop, value):
         pid = wl.PID[prop] if isinstance(prop, str) else prop
@@ -454,8 +480,8 @@ def world_from_workload(w, capacity=None, msg_capacity=0, stream=None, slack_per
 
 def run_workload(m, w, tick, collect=True):
     """Replay the between-frame calls of frame `tick` in the oracle's window order — CreateObject
-    (nfk_spawn_objects), SwitchScene, schedule calls, SetProperty calls, DestroyObject — then
-    Execute it."""
+    (nfk_spawn_objects), SwitchScene, schedule calls, SetProperty calls, SetRecord calls,
+    DestroyObject — then Execute it."""
     gh, gd = w["guid_head"], w["guid_data"]
     if "born" in w:
         new = np.nonzero(w["born"] == tick)[0]
@@ -498,6 +524,11 @@ def run_workload(m, w, tick, collect=True):
                 else:
                     v = (cur.view(np.float64) + d.view(np.float64)).view(np.uint64)
                 m.set_props([gh[o]], [gd[o]], [p], v)
+    if "r_tick" in w:   # SetRecordInt / SetRecordFloat calls (typed by their column)
+        rsel = np.nonzero(w["r_tick"] == tick)[0]
+        if len(rsel):
+            ro = w["r_obj"][rsel]
+            m.set_records(gh[ro], gd[ro], w["r_rec"][rsel], w["r_row"][rsel], w["r_col"][rsel], w["r_bits"][rsel])
     if "d_tick" in w:
         dead = w["d_obj"][w["d_tick"] == tick]
         if len(dead):

@@ -27,7 +27,7 @@ def set_path(monkeypatch, path):
 
 @PATHS
 @pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets", "tutorial3", "rmw",
-                                  "lifecycle"])
+                                  "lifecycle", "recsets"])
 def test_gpu_matches_reference_golden(gpu_available, monkeypatch, name, path):
     set_path(monkeypatch, path)
     w = nfio.read(os.path.join(GOLDEN, f"{name}.workload.nfio"))
@@ -66,6 +66,18 @@ CASES = {
     "combined": dict(n_obj=3000, n_scenes=3, groups_per_scene=6, players_per_group=4, ext_frac=0.05, host_ops=True,
                      sched_edges=True, switch_frac=0.02, switch_new_groups=True, rmw_frac=0.02, spawn_frac=0.03,
                      destroy_frac=0.03),
+    # SetRecordInt between frames (used and unused rows, cells set twice, values already held) beside
+    # the heartbeat's record ops on the same cells (nfk_set_records; oracle pinned against the
+    # compiled NFCRecord::SetInt, test_oracle.py seeds 11-12)
+    "record_sets": dict(n_obj=3000, n_scenes=2, groups_per_scene=4, players_per_group=4, records=True, rec_rows=32,
+                        rec_float_op=False, rec_set_frac=0.08, rec_set_float=False, ext_frac=0.05),
+    "record_sets_three_ops": dict(n_obj=2000, n_scenes=1, groups_per_scene=4, players_per_group=5, records=True,
+                                  rec_rows=64, rec_skill_op=True, rec_set_frac=0.2, rec_set_float=False,
+                                  spawn_frac=0.03, destroy_frac=0.03),
+    # f64 cells too (SetRecordFloat; the f64 record semantics are the oracle's, since the
+    # reference's NFCRecord::SetFloat is broken: test_oracle.py::test_reference_record_setfloat_bug)
+    "record_sets_f64": dict(n_obj=2500, n_scenes=2, groups_per_scene=5, players_per_group=3, records=True, rec_rows=20,
+                            rec_set_frac=0.1, rec_set_float=True, switch_frac=0.01),
     "wide_sets_records": dict(n_obj=3000, n_scenes=2, groups_per_scene=5, players_per_group=6, records=True,
                               rec_rows=32, ext_frac=0.1, ext_props="all", burst_frac=0.02, burst_props=24,
                               switch_frac=0.01),
@@ -410,3 +422,56 @@ def test_functor_calls_land_in_the_same_frame(gpu_available):
     for r in fires_late:   # deferred: the HP event of a fire in frame f arrives in frame f + 1
         assert any(e["frame"] == str(int(r["frame"]) + 1) and e["obj"] == r["obj"] for e in ev_late), r
     assert not any(e["frame"] == "1" for e in ev_late)
+
+
+def test_record_reads_see_queued_sets(gpu_available):
+    """NFIKernelModule::GetRecordInt/Float through nfk_get_records: after frames with record
+    programs, the cell as the device holds it (0 on an unused row, RC:623); then with this
+    window's queued SetRecord calls applied in call order through NFCRecord::SetInt / SetFloat's
+    predicates (read-your-writes), checked against the predicates restated here."""
+    from noahgameframe_amd import kernel
+    w = workload.make_world(n_obj=600, n_scenes=1, groups_per_scene=3, players_per_group=4, n_ticks=4, seed=77,
+                            records=True, rec_rows=16, rec_float_op=True)
+    m = kernel.world_from_workload(w, slack_per_256=16)
+    for t in range(2):
+        kernel.run_workload(m, w, t, collect=False)
+    gh, gd = w["guid_head"], w["guid_data"]
+    cells = m.read_record(0)                      # [n_obj][cols][rows] after frame 1
+    used = w["rec0_used"]
+    rng = np.random.default_rng(5)
+    n = 400
+    o = rng.integers(0, len(gh), n)
+    row = rng.integers(0, 16, n)
+    col = rng.integers(0, 3, n)
+    got = m.get_records(gh[o], gd[o], np.zeros(n), row, col)
+    exp = np.where(((used[o] >> row.astype(np.uint64)) & np.uint64(1)) == 1, cells[o, col, row], np.uint64(0))
+    assert np.array_equal(got, exp)
+    # queue Sets (a third of them twice, some to the value held), then read them back
+    vals = np.where(col == 2, rng.uniform(-5, 5, n).view(np.uint64), rng.integers(0, 900, n).astype(np.uint64))
+    held = rng.random(n) < 0.2
+    vals[held] = cells[o[held], col[held], row[held]]   # the value the cell holds: no change
+    m.set_records(gh[o], gd[o], np.zeros(n), row, col, vals)
+    again = rng.random(n) < 0.33
+    vals2 = np.where(col == 2, (vals.view(np.float64) + 0.0004).view(np.uint64), vals + np.uint64(1))
+    m.set_records(gh[o[again]], gd[o[again]], np.zeros(again.sum()), row[again], col[again], vals2[again])
+    exp = cells[o, col, row].copy()
+    calls = [(i, vals[i]) for i in range(n)] + [(i, vals2[i]) for i in np.nonzero(again)[0]]
+    cur = {}
+    for i, b in calls:   # the predicates of NFCRecord::SetInt / SetFloat, in call order
+        k = (int(o[i]), int(row[i]), int(col[i]))
+        c = cur.get(k, int(cells[o[i], col[i], row[i]]))
+        if not ((int(used[o[i]]) >> int(row[i])) & 1):
+            continue
+        if col[i] == 2:
+            d = np.uint64(b).view(np.float64) - np.uint64(c).view(np.float64)
+            if not (-0.001 < d < 0.001):
+                c = int(b)
+        else:
+            c = int(b)
+        cur[k] = c
+    got = m.get_records(gh[o], gd[o], np.zeros(n), row, col)
+    for i in range(n):
+        k = (int(o[i]), int(row[i]), int(col[i]))
+        want = cur.get(k, int(cells[o[i], col[i], row[i]])) if (int(used[o[i]]) >> int(row[i])) & 1 else 0
+        assert int(got[i]) == want, (i, k)
+    m.close()
