@@ -7,7 +7,7 @@
 
 namespace nfgpu {
 
-constexpr int kTPB = 256;     // 4 waves of 64
+constexpr int kTPB = 256;     // 4 waves of 64 (128-slot tiles measured: not faster, profiles/r04t_ab_tile128.txt)
 constexpr int kTile = 256;    // slots per property/fired tile (one k_tick workgroup)
 #ifndef NFGPU_RTILE
 #define NFGPU_RTILE 64

@@ -2615,9 +2615,10 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     if (d.has_recops && d.n_rtiles) {
         TimeScope ts(w, KT_REC);
-        const dim3 g((unsigned)((d.n_rtiles + 3) / 4)), b(kTPB);
+        constexpr int kWpb = kTPB / 64;  // record tiles (waves) per workgroup
+        const dim3 g((unsigned)((d.n_rtiles + kWpb - 1) / kWpb)), b(kTPB);
         if (nrss)  // the SetRecord slots' events and messages, for k_records to reserve
-            hipLaunchKernelGGL((k_rset_slots<false>), dim3((unsigned)((nrss + 3) / 4)), b, 0, w->stream, d);
+            hipLaunchKernelGGL((k_rset_slots<false>), dim3((unsigned)((nrss + kWpb - 1) / kWpb)), b, 0, w->stream, d);
         if (nrss) {  // (the SetRecord slots' instantiation: the fast path without them stays lean)
             if (d.n_rops <= 1)
                 hipLaunchKernelGGL((k_records<1, 4, true>), g, b, 0, w->stream, d);
@@ -2632,7 +2633,7 @@ int nfk_execute(void* world, int64_t now_ms) {
         else
             hipLaunchKernelGGL((k_records<NFK_MAX_OPS, 2, false>), g, b, 0, w->stream, d);
         if (nrss)  // ... and written into the room k_records left
-            hipLaunchKernelGGL((k_rset_slots<true>), dim3((unsigned)((nrss + 3) / 4)), b, 0, w->stream, d);
+            hipLaunchKernelGGL((k_rset_slots<true>), dim3((unsigned)((nrss + kWpb - 1) / kWpb)), b, 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
     if (npost) {

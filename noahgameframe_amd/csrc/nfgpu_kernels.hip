@@ -1362,7 +1362,7 @@ __device__ __forceinline__ uint64_t rank_key(const Dev& d, int32_t pid, int e) {
 __global__ __launch_bounds__(kTPB) void k_rank_hist(Dev d, int32_t pid, uint64_t prefix, uint64_t pmask, int shift,
                                                     unsigned* __restrict__ hist) {
     __shared__ unsigned s_h[256];
-    s_h[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < 256; i += kTPB) s_h[i] = 0;
     __syncthreads();
     for (int e = blockIdx.x * kTPB + threadIdx.x; e < d.N; e += gridDim.x * kTPB) {
         if (desc_dead(d.fan_desc[e])) continue;
@@ -1370,7 +1370,8 @@ __global__ __launch_bounds__(kTPB) void k_rank_hist(Dev d, int32_t pid, uint64_t
         if ((k & pmask) == prefix) atomicAdd(&s_h[(k >> shift) & 255], 1u);
     }
     __syncthreads();
-    if (s_h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], s_h[threadIdx.x]);
+    for (int i = threadIdx.x; i < 256; i += kTPB)
+        if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
 }
 
 __global__ __launch_bounds__(kTPB) void k_rank_collect(Dev d, int32_t pid, uint64_t thr, unsigned* __restrict__ n,
