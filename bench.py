@@ -175,7 +175,7 @@ class Migration:
         out[:, T_X], out[:, T_Y] = xy[:, 0].view(np.int64), xy[:, 1].view(np.int64)
         out[:, T_Z] = np.zeros(n, np.float64).view(np.int64)
         out[:, T_SRC], out[:, T_DST] = self.rank, dst
-        self.plan = self.shard.exchange_ticket_array(out)
+        self.plan = self.shard.exchange_ticket_array(out, max_rows=self.per_frame)  # one all-gather
 
 
 def main():

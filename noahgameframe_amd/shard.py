@@ -105,12 +105,24 @@ class SceneShard:
         dist.all_gather_object(allt, out, group=self.meta_pg)
         return [t for lst in allt for t in lst]
 
-    def exchange_ticket_array(self, out):
+    def exchange_ticket_array(self, out, max_rows=None):
         """All-gather every rank's outgoing ticket array over the meta group (counts first, then
-        the rows padded to the largest count); returns the global plan in (source rank, call) order."""
+        the rows padded to the largest count; with `max_rows`, a bound every rank knows, one
+        all-gather of [count row | rows padded to max_rows]); returns the global plan in (source
+        rank, call) order."""
         torch = self.torch
         import torch.distributed as dist
         out = np.ascontiguousarray(out, np.int64).reshape(-1, 11)
+        if max_rows is not None:
+            if len(out) > max_rows:
+                raise ValueError("more tickets than max_rows")
+            pad = torch.zeros((max_rows + 1, 11), dtype=torch.int64)
+            pad[0, 0] = len(out)
+            pad[1:1 + len(out)] = torch.from_numpy(out)
+            allp = [torch.zeros((max_rows + 1, 11), dtype=torch.int64) for _ in range(self.ws)]
+            dist.all_gather(allp, pad, group=self.meta_pg)
+            parts = [a[1:1 + int(a[0, 0])].numpy() for a in allp]
+            return np.concatenate(parts) if parts else np.zeros((0, 11), np.int64)
         n = torch.tensor([len(out)], dtype=torch.int64)
         ns = [torch.zeros(1, dtype=torch.int64) for _ in range(self.ws)]
         dist.all_gather(ns, n, group=self.meta_pg)

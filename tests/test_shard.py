@@ -198,3 +198,36 @@ def test_sharded_replay_matches_single_world_oracle(gpu_available, tmp_path, sla
 
 def ws_owner(w, scene_of, o):
     return scene_ranges(np.unique(w["scene"]), 2)(scene_of[o])
+
+
+def _ticket_worker(rank, ws, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    sh = SceneShard(StubWorld(rank), rank, ws, scene_ranges([1, 2], ws), [16, 17, 18, 19, 20],
+                    meta_group=dist.group.WORLD)
+    out = np.arange((rank + 1) * 3 * 11, dtype=np.int64).reshape(-1, 11) + 1000 * rank  # ragged: 3 and 6 rows
+    a = sh.exchange_ticket_array(out)                 # counts, then padded rows
+    b = sh.exchange_ticket_array(out, max_rows=8)     # one all-gather under a known bound
+    c = sh.exchange_ticket_array(out[:0], max_rows=8)
+    q.put((rank, a.tolist(), b.tolist(), c.shape))
+    dist.destroy_process_group()
+
+
+def test_ticket_exchange_single_gather_gloo_cpu():
+    """exchange_ticket_array with a known bound (one all-gather) returns the same global plan, in
+    (source rank, call) order, as the two-collective form."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ticket_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((x[0], x[1:]) for x in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(timeout=60)
+    want = np.concatenate([np.arange(3 * 11).reshape(-1, 11), np.arange(6 * 11).reshape(-1, 11) + 1000]).tolist()
+    for r in (0, 1):
+        a, b, c = res[r]
+        assert a == want and b == want and tuple(c) == (0, 11)
