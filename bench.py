@@ -18,6 +18,7 @@ data-path collective).  Timing: barrier + device sync on both sides of exactly K
 max over ranks.  Rank 0 prints one JSON line.
 """
 import argparse
+import collections
 import json
 import os
 import subprocess
@@ -65,6 +66,9 @@ def parse():
     p.add_argument("--migrate-every", type=int, default=8,
                    help="frames between migration batches (8 = 256 entities per GPU every 0.8 s)")
     p.add_argument("--slack", type=int, default=None, help="free slots per 256 scene-group members")
+    p.add_argument("--self-migrate", action="store_true",
+                   help="1 GPU: run config[2]'s migration path with one rank sending its rows to itself "
+                        "(host-cost rehearsal; the migration phases are traced with NFGPU_BENCH_TRACE)")
     p.add_argument("--host-calls", choices=["auto", "off"], default="auto",
                    help="config[1], 1 GPU: also time frames with game-logic SetProperty / schedule calls")
     p.add_argument("--config", type=int, default=1, choices=[0, 1, 3, 4],
@@ -134,14 +138,16 @@ class Migration:
         import torch.distributed as dist
         from noahgameframe_amd.shard import SceneShard
         self.dist = dist
-        self.meta = dist.new_group(backend="gloo")
+        self.meta = dist.new_group(backend="gloo") if world > 1 else None
         own = lambda scene: int(scene) - 1
-        self.shard = SceneShard(m, rank, world, own, w["scene_props"], group=dist.group.WORLD,
+        self.shard = SceneShard(m, rank, world, own, w["scene_props"], group=dist.group.WORLD if world > 1 else None,
                                 meta_group=self.meta, device=dev)
         self.rank, self.world, self.per_frame, self.every = rank, world, per_frame, max(1, every)
         # entities this rank owns (guid head, guid data, group, cls, is_player), oldest first
-        self.owned = np.stack([w["guid_head"], w["guid_data"], w["group"], w["cls"], w["is_player"]],
-                              axis=1).astype(np.int64)
+        # (a queue of row chunks: arrivals append a chunk, departures take from the front, so a
+        # migrating frame never copies the whole table)
+        self.owned = collections.deque([np.stack([w["guid_head"], w["guid_data"], w["group"], w["cls"],
+                                                  w["is_player"]], axis=1).astype(np.int64)])
         self.head = 0
         self.rng = np.random.default_rng(77 + rank)
         self.frames = 0
@@ -153,9 +159,7 @@ class Migration:
         if self.plan is not None:
             recv = self.shard.migrate_array(self.plan)
             if len(recv):
-                self.owned = np.concatenate([self.owned[self.head:],
-                                             recv[:, [T_GH, T_GD, T_GROUP, T_CLS, T_PL]]])
-                self.head = 0
+                self.owned.append(recv[:, [T_GH, T_GD, T_GROUP, T_CLS, T_PL]])
         self.plan = None
 
     def after_frame(self):
@@ -165,9 +169,17 @@ class Migration:
         if self.frames % self.every:
             return
         dst = (self.rank + 1) % self.world
-        n = min(self.per_frame, len(self.owned) - self.head)
-        o = self.owned[self.head:self.head + n]
-        self.head += n
+        take = []
+        while self.owned and sum(len(c) for c in take) < self.per_frame:
+            c = self.owned[0]
+            k = min(self.per_frame - sum(len(t) for t in take), len(c) - self.head)
+            take.append(c[self.head:self.head + k])
+            self.head += k
+            if self.head == len(c):
+                self.owned.popleft()
+                self.head = 0
+        o = np.concatenate(take) if take else np.zeros((0, 5), np.int64)
+        n = len(o)
         out = np.zeros((n, 11), np.int64)
         out[:, T_GH], out[:, T_GD], out[:, T_GROUP], out[:, T_CLS], out[:, T_PL] = o[:, 0], o[:, 1], o[:, 2], o[:, 3], o[:, 4]
         out[:, T_SCENE] = dst + 1
@@ -228,7 +240,9 @@ def main():
     args.groups = len(cells)
     args.players_per_group = int(w["is_player"].sum()) // max(len(cells), 1)
     stream = torch.cuda.current_stream()
-    migrating = world > 1 and args.migrate > 0 and args.config == 1
+    # (--self-migrate: the migration path on one rank, its rows sent to itself — a host-cost
+    # rehearsal of config[2] on one GPU; never the headline line)
+    migrating = (world > 1 or args.self_migrate) and args.migrate > 0 and args.config == 1
     # config[1] has no membership changes: no slack slots; config[2] keeps 32 per 256 for arrivals
     slack = args.slack if args.slack is not None else (32 if migrating else -1)
     m = kernel.world_from_workload(w, stream=stream.cuda_stream, slack_per_256=slack)
@@ -239,6 +253,8 @@ def main():
         mig = Migration(m, w, rank, world, args.migrate, args.migrate_every, dev)
 
     trace = {} if os.environ.get("NFGPU_BENCH_TRACE") else None  # host seconds per phase (stderr)
+    if mig and trace is not None:
+        mig.shard.phase_s = trace   # (migrate_array's own phases: "export", "all_to_all", ...)
 
     def timed(name, fn):
         if trace is None:
@@ -326,11 +342,13 @@ def main():
     value = world * args.entities * args.steps / elapsed
 
     if args.config == 1:
-        wl_name = ((f"BASELINE config[2]: {world} scene shards (scene r+1 on GPU r), "
-                    f"{args.migrate} SwitchScene migrations per rank every {args.migrate_every} "
-                    f"frames into the next shard (state rows over {'RCCL' if args.backend == 'nccl' else 'gloo'} "
-                    "all_to_all); per GPU: ")
-                   if migrating else "BASELINE config[1]: ") + (
+        rehearsal = ("one-rank rehearsal of config[2]'s migration path (rows sent to the same rank): "
+                     if args.self_migrate and world == 1 else "")
+        wl_name = rehearsal + ((f"BASELINE config[2]: {world} scene shards (scene r+1 on GPU r), "
+                                f"{args.migrate} SwitchScene migrations per rank every {args.migrate_every} "
+                                f"frames into the next shard (state rows over "
+                                f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all_to_all); per GPU: ")
+                               if migrating else "BASELINE config[1]: ") + (
             f"{args.entities} NPC/Player entities per GPU in one scene, "
             f"{args.groups} groups x {args.entities // args.groups}, "
             f"{args.players_per_group} players/group, heartbeats HPRegen 1s/MPRegen 2s/"

@@ -798,16 +798,7 @@ int apply_membership(World* w) {
     // The new member lists are built on copies of the affected segments; nothing of the world
     // changes before every check has passed (a failure leaves the window's calls queued).
     bool full = false;
-    std::vector<int32_t> aff;
-    std::map<int32_t, World::Seg> edit;  // affected segment -> its new member list
-    auto seg_copy = [&](int32_t g) -> World::Seg& {
-        auto it = edit.find(g);
-        if (it == edit.end()) {
-            it = edit.emplace(g, w->segs[g]).first;
-            aff.push_back(g);
-        }
-        return it->second;
-    };
+    std::vector<int32_t> aff;  // affected segments, in first-touch order
     auto seg_at = [&](int32_t slot) {
         int32_t lo = 0, hi = (int32_t)w->segs.size() - 1;
         while (lo < hi) {
@@ -817,19 +808,29 @@ int apply_membership(World* w) {
         }
         return lo;
     };
-    // per affected segment: the old ranks its leavers had and the objects that join it
+    // per affected segment: its new member list, the old ranks its leavers had and its joiners
+    // with their new ranks (ins, sorted by rank)
     struct EdInfo {
-        std::vector<int32_t> rem, ins;
+        World::Seg seg;
+        std::vector<int32_t> rem, join;
+        std::vector<std::pair<int32_t, int32_t>> ins;  // (new rank, object)
     };
-    std::map<int32_t, EdInfo> info;
+    std::vector<int32_t> epos(w->segs.size(), -1);
+    std::vector<EdInfo> einfo;
+    einfo.reserve(2 * w->touched.size() + 1);
+    auto ed = [&](int32_t g) -> EdInfo& {
+        if (epos[g] < 0) {
+            epos[g] = (int32_t)einfo.size();
+            einfo.emplace_back();
+            aff.push_back(g);
+        }
+        return einfo[epos[g]];
+    };
     for (int32_t o : w->touched) {
         const int32_t s = w->slot_of_obj[o];
         if (s < 0) continue;
         const int32_t gi = seg_at(s);
-        auto& v = seg_copy(gi).objs;
-        auto it = std::lower_bound(v.begin(), v.end(), o, cmp);
-        if (it != v.end() && *it == o) v.erase(it);
-        info[gi].rem.push_back(s - w->segs[gi].base);  // members occupy [base, base + n) in NFGUID order
+        ed(gi).rem.push_back(s - w->segs[gi].base);  // members occupy [base, base + n) in NFGUID order
     }
     for (int32_t o : w->touched) {
         if (!w->alive[o]) continue;
@@ -838,13 +839,43 @@ int apply_membership(World* w) {
             full = true;
             continue;
         }
-        auto& v = seg_copy(f->second).objs;
-        v.insert(std::lower_bound(v.begin(), v.end(), o, cmp), o);
-        info[f->second].ins.push_back(o);
+        ed(f->second).join.push_back(o);
     }
-    for (int32_t g : aff)
-        if ((int32_t)edit[g].objs.size() > edit[g].cap) full = true;
-
+    // each new member list in one pass: the old list without its leavers (known by rank, no
+    // NFGUID comparison), the joiners (sorted) spliced in at their binary-searched places
+    for (int32_t g : aff) {
+        EdInfo& x = einfo[epos[g]];
+        const World::Seg& old = w->segs[g];
+        x.seg.scene = old.scene;
+        x.seg.group = old.group;
+        x.seg.base = old.base;
+        x.seg.cap = old.cap;
+        x.seg.np = old.np;
+        std::sort(x.rem.begin(), x.rem.end());
+        std::vector<int32_t> kept;
+        kept.reserve(old.objs.size() - x.rem.size());
+        size_t r = 0;
+        for (int32_t i = 0; i < (int32_t)old.objs.size(); i++) {
+            if (r < x.rem.size() && x.rem[r] == i) {
+                r++;
+                continue;
+            }
+            kept.push_back(old.objs[i]);
+        }
+        std::sort(x.join.begin(), x.join.end(), cmp);
+        std::vector<int32_t>& v = x.seg.objs;
+        v.reserve(kept.size() + x.join.size());
+        size_t at = 0;
+        for (int32_t o : x.join) {
+            const size_t p = (size_t)(std::lower_bound(kept.begin() + at, kept.end(), o, cmp) - kept.begin());
+            v.insert(v.end(), kept.begin() + at, kept.begin() + p);
+            x.ins.push_back({(int32_t)v.size(), o});
+            v.push_back(o);
+            at = p;
+        }
+        v.insert(v.end(), kept.begin() + at, kept.end());
+        if ((int32_t)v.size() > old.cap) full = true;
+    }
     std::vector<int32_t> pack_src, un_dst;  // (host-built lists: none since k_seg_edit)
     std::vector<int64_t> un_src;
     MetaLists m;
@@ -856,8 +887,8 @@ int apply_membership(World* w) {
     std::vector<int64_t> ins_src;
     int32_t ed_rows = 0, ed_list = 0;
     // ob: the old segment (-1: a new (scene, group) pair; its members are all inserted)
-    auto add_edit = [&](World::Seg& g, int32_t ob_seg, const std::vector<int32_t>* ins, const std::vector<int32_t>* rem,
-                        bool all) -> int {
+    auto add_edit = [&](World::Seg& g, int32_t ob_seg, const std::vector<std::pair<int32_t, int32_t>>* ins,
+                        const std::vector<int32_t>* rem, bool all) -> int {
         SegEdit e{};
         const World::Seg* old = ob_seg >= 0 ? &w->segs[ob_seg] : nullptr;
         e.ob = old ? old->base : -1;
@@ -867,16 +898,10 @@ int apply_membership(World* w) {
         e.nc = g.cap;
         int32_t np = old ? old->np : 0;
         e.io = (int32_t)ins_rank.size();
-        if (ins) {
-            std::vector<std::pair<int32_t, int32_t>> r;
-            r.reserve(ins->size());
-            for (int32_t o : *ins) {
-                r.push_back({(int32_t)(std::lower_bound(g.objs.begin(), g.objs.end(), o, cmp) - g.objs.begin()), o});
-                np += w->isplayer[o] ? 1 : 0;
-            }
-            std::sort(r.begin(), r.end());
-            for (const auto& x : r) {
+        if (ins) {  // (new rank, object), in rank order
+            for (const auto& x : *ins) {
                 const int32_t o = x.second;
+                np += w->isplayer[o] ? 1 : 0;
                 ins_rank.push_back(x.first);
                 ins_obj.push_back(o);
                 ins_meta.push_back(((uint64_t)w->cls[o] << 60) | (w->isplayer[o] ? 1u : 0u));
@@ -937,15 +962,15 @@ int apply_membership(World* w) {
             const World::Seg& old = w->segs[gi];
             const std::pair<int32_t, int32_t> key{old.scene, old.group};
             while (fit != fresh.end() && fit->first < key) push_fresh();
-            auto e = edit.find(gi);
-            if ((e != edit.end() ? e->second.objs : old.objs).empty()) continue;
+            const bool edited = epos[gi] >= 0;
+            if ((edited ? einfo[epos[gi]].seg.objs : old.objs).empty()) continue;
             World::Seg g;
             g.scene = old.scene;
             g.group = old.group;
-            if (e != edit.end()) g.objs = std::move(e->second.objs);
+            if (edited) g.objs = std::move(einfo[epos[gi]].seg.objs);
             nsegs.push_back(std::move(g));
-            nsrc.push_back(e != edit.end() ? -1 : gi);
-            nold.push_back(e != edit.end() ? gi : -1);
+            nsrc.push_back(edited ? -1 : gi);
+            nold.push_back(edited ? gi : -1);
         }
         while (fit != fresh.end()) push_fresh();
         auto members = [&](size_t i) -> const std::vector<int32_t>& {
@@ -979,10 +1004,12 @@ int apply_membership(World* w) {
             }
             int r;
             if (nold[i] >= 0) {
-                const EdInfo& x = info[nold[i]];
+                const EdInfo& x = einfo[epos[nold[i]]];
                 r = add_edit(g, nold[i], &x.ins, &x.rem, true);
-            } else {  // a new (scene, group) pair
-                r = add_edit(g, -1, &g.objs, nullptr, true);
+            } else {  // a new (scene, group) pair: every member joins, at its rank
+                std::vector<std::pair<int32_t, int32_t>> all_in(g.objs.size());
+                for (size_t k = 0; k < g.objs.size(); k++) all_in[k] = {(int32_t)k, g.objs[k]};
+                r = add_edit(g, -1, &all_in, nullptr, true);
             }
             if (r) {
                 w->max_np = max_np0;
@@ -991,8 +1018,8 @@ int apply_membership(World* w) {
         }
     } else {
         for (int32_t gi : aff) {
-            const EdInfo& x = info[gi];
-            int r = add_edit(edit[gi], gi, &x.ins, &x.rem, false);
+            EdInfo& x = einfo[epos[gi]];
+            int r = add_edit(x.seg, gi, &x.ins, &x.rem, false);
             if (r) {
                 w->max_np = max_np0;
                 return r;
@@ -1103,8 +1130,8 @@ int apply_membership(World* w) {
     } else {
         w->n_relayout_seg++;
         for (int32_t gi : aff) {
-            w->segs[gi].objs = std::move(edit[gi].objs);
-            w->segs[gi].np = edit[gi].np;
+            w->segs[gi].objs = std::move(einfo[epos[gi]].seg.objs);
+            w->segs[gi].np = einfo[epos[gi]].seg.np;
         }
     }
     for (int32_t o : w->touched)

@@ -15,6 +15,7 @@ Tickets (which entity goes where) are control-plane metadata: they are exchanged
 global migration plan, derived locally (`migrate(..., plan=...)`) so the frame has no host
 round trip at all.
 """
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -85,6 +86,14 @@ class SceneShard:
         self.rw = m.row_words()
         self.migrated_out = 0
         self.migrated_in = 0
+        self.phase_s = None   # a dict to accumulate host seconds per migrate_array phase into (tracing)
+
+    def _mark(self, name, t):
+        if self.phase_s is not None:
+            now = time.perf_counter()
+            self.phase_s[name] = self.phase_s.get(name, 0.0) + now - t
+            return now
+        return t
 
     # ---- the SwitchScene call as game logic makes it ----
     def switch_scene(self, guid, cls, is_player, scene, group, x, y, z, out):
@@ -113,6 +122,8 @@ class SceneShard:
         torch = self.torch
         import torch.distributed as dist
         out = np.ascontiguousarray(out, np.int64).reshape(-1, 11)
+        if self.ws == 1:   # (a one-rank rehearsal: the plan is this rank's own tickets)
+            return out.copy()
         if max_rows is not None:
             if len(out) > max_rows:
                 raise ValueError("more tickets than max_rows")
@@ -158,13 +169,16 @@ class SceneShard:
         scount = np.bincount(send[:, T_DST], minlength=self.ws)
         rcount = np.bincount(recv[:, T_SRC], minlength=self.ws)
         rw = self.rw
+        t = time.perf_counter()
         sbuf = torch.empty((len(send), rw), dtype=torch.int64, device=self.device)
         if len(send):
             self.m.export_objects(send[:, T_GH], send[:, T_GD], sbuf.data_ptr())
         if self.device.type == "cuda" and self.m.stream != torch.cuda.current_stream(self.device).cuda_stream:
             self.m.synchronize()   # the rows were packed on the world's own stream
+        t = self._mark("export", t)
         rbuf = torch.empty((len(recv), rw), dtype=torch.int64, device=self.device)
         self._all_to_all(rbuf, sbuf, [int(c) * rw for c in rcount], [int(c) * rw for c in scount])
+        t = self._mark("all_to_all", t)
         if len(recv):
             other_stream = (self.device.type == "cuda" and
                             self.m.stream != torch.cuda.current_stream(self.device).cuda_stream)
@@ -174,6 +188,7 @@ class SceneShard:
                                   recv[:, T_PL], rbuf.data_ptr())
             if other_stream:   # rbuf returns to torch's allocator: the world's copy out of it is done
                 self.m.synchronize()
+            t = self._mark("import", t)
             # the SwitchScene property writes (KM:930-942), per entity in this order; the scene
             # always changes here
             cols = [(self.pid_group, np.zeros(len(recv), np.int64)), (self.pid_scene, recv[:, T_SCENE]),
@@ -185,6 +200,7 @@ class SceneShard:
                 self.m.set_props(np.repeat(recv[:, T_GH], k), np.repeat(recv[:, T_GD], k),
                                  np.tile(np.array([p for p, _ in cols], np.int32), len(recv)),
                                  np.stack([v for _, v in cols], axis=1).reshape(-1).view(np.uint64))
+            self._mark("set_props", t)
         self.migrated_out += len(send)
         self.migrated_in += len(recv)
         return recv
@@ -192,7 +208,8 @@ class SceneShard:
     def _all_to_all(self, rbuf, sbuf, rsplit, ssplit):
         torch = self.torch
         import torch.distributed as dist
-        if self.ws == 1:
+        if self.ws == 1:   # (a one-rank rehearsal: the rows come back to this rank)
+            rbuf.copy_(sbuf)
             return
         if self.device.type == "cuda" and dist.get_backend(self.pg) == "gloo":
             # gloo moves host tensors: stage the rows through host memory

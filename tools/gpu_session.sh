@@ -40,6 +40,8 @@ for step in "$@"; do
     hostprof) NFGPU_TRACE_EXEC=1 run hostprof 300 python tools/host_calls_profile.py ;;
     hbmmix) run hbmmix 120 tools/_bin/hbm_mix ;;
     membership) NFGPU_TRACE_MEMBERSHIP=1 run membership 300 python tools/membership_bench.py ;;
+    selfmig) NFGPU_BENCH_TRACE=1 NFGPU_TRACE_EXEC=1 NFGPU_TRACE_MEMBERSHIP=1 run selfmig 300 python bench.py --self-migrate \
+               --steps 24 --warmup 8 --cpu-baseline off --host-calls off ;;
     ablate) run ablate 600 python tools/ablate.py --variants ${ABL:-0,8,4} ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
              python bench.py --steps 50 --warmup 5 --cpu-baseline off --host-calls off ;;
