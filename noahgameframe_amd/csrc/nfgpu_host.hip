@@ -138,6 +138,8 @@ struct PendingTiming {
     int64_t bytes_before;
 };
 
+struct MemPlan;
+
 struct World {
     nfk_config cfg{};
     hipStream_t stream = nullptr;
@@ -164,7 +166,7 @@ struct World {
         std::vector<int32_t> objs;  // live objects, NFGUID order
     };
     std::vector<Seg> segs;
-    std::map<std::pair<int32_t, int32_t>, int32_t> seg_of;
+    std::vector<uint64_t> seg_key;  // each segment's (scene, group) as seg_key_of gives it: ascending
     int32_t slack = 16;  // slack slots per 256 live (nfk_config::slack_per_256)
     int32_t pid_scene = -1, pid_group = -1, pid_x = -1, pid_y = -1, pid_z = -1;  // nfk_set_scene_props
     int32_t row_words = 0;
@@ -184,7 +186,8 @@ struct World {
     uint64_t* fan_desc_w = nullptr;
     int32_t* pl_slot_w = nullptr;
     int64_t n_relayout_full = 0, n_relayout_seg = 0;
-    double ms_relayout_full = 0, ms_relayout_seg = 0;  // host time in apply_membership
+    double ms_relayout_full = 0, ms_relayout_seg = 0;  // host time in plan/commit_membership
+    std::unique_ptr<MemPlan> mplan;            // the window's membership plan (scratch kept)
     void* glist = nullptr;  // device-generated membership lists (untouched segments of a full re-layout)
     size_t glist_cap = 0;
     std::vector<std::vector<uint64_t>> init_props;
@@ -426,6 +429,23 @@ int gather_tiles(World* w, const T* src, const uint32_t* base, int n_tiles, int 
 bool guid_less(const World* w, int32_t a, int32_t b) {
     const World::Guid x = w->guid[a], y = w->guid[b];
     return x.h != y.h ? x.h < y.h : x.d < y.d;
+}
+
+// (scene, group) as one word whose unsigned order is the pair's signed order
+uint64_t seg_key_of(int32_t scene, int32_t group) {
+    return ((uint64_t)((uint32_t)scene ^ 0x80000000u) << 32) | ((uint32_t)group ^ 0x80000000u);
+}
+
+// the segment of (scene, group), or -1
+int32_t find_seg(const World* w, int32_t scene, int32_t group) {
+    const uint64_t k = seg_key_of(scene, group);
+    const auto it = std::lower_bound(w->seg_key.begin(), w->seg_key.end(), k);
+    return it != w->seg_key.end() && *it == k ? (int32_t)(it - w->seg_key.begin()) : -1;
+}
+
+void index_segs(World* w) {
+    w->seg_key.resize(w->segs.size());
+    for (size_t g = 0; g < w->segs.size(); g++) w->seg_key[g] = seg_key_of(w->segs[g].scene, w->segs[g].group);
 }
 
 int32_t seg_slack(int32_t slack, int32_t len) {
@@ -784,21 +804,64 @@ size_t stage_list(World* w, const std::vector<T>& v) {
 
 unsigned grid_for(size_t work) { return (unsigned)std::max<size_t>(1, std::min<size_t>((work + kTPB - 1) / kTPB, 8192)); }
 
+// per affected segment: its new member list, the old ranks its leavers had and its joiners
+// with their new ranks (ins, sorted by rank)
+struct EdInfo {
+    World::Seg seg;
+    std::vector<int32_t> rem, join;
+    std::vector<std::pair<int32_t, int32_t>> ins;  // (new rank, object)
+};
+
+// A window's membership changes, planned on the host (plan_membership: the new member lists and
+// the device's edit / move plans; it changes nothing of the world) and then applied
+// (commit_membership: uploads and launches, then the host maps while the device rewrites the
+// slots).  nfk_execute plans while the previous frame still runs on the GPU and waits for that
+// frame before the commit, which rewrites slots the previous frame's fan-out recovery
+// (regrow_fanout) reads.
+struct MemPlan {
+    bool active = false, full = false;
+    int32_t max_np0 = 0;
+    std::vector<int32_t> aff, epos;
+    std::vector<EdInfo> einfo;
+    std::vector<SegEdit> edits;
+    std::vector<int32_t> ins_rank, ins_obj, rem_rank;
+    std::vector<uint64_t> ins_meta;
+    std::vector<int64_t> ins_src;
+    std::vector<SegMove> moves;
+    std::vector<World::Seg> nsegs;  // full: the new segment table
+    std::vector<int32_t> nsrc;      // full: nsegs[i] is untouched segment nsrc[i] (members kept), or -1
+    int32_t mv_rows_dev = 0, mv_list_dev = 0, ed_rows = 0, ed_list = 0;
+    std::chrono::steady_clock::time_point t_host, t_edit, t_lists;
+};
+
 // Apply this window's membership changes (SwitchScene across groups, DestroyObject, exports,
 // imports) before the frame: only the scene-group segments that changed are rewritten (the
 // entities behind the first change shift by one slot each); a new (scene, group) or a segment
 // whose slack ran out rebuilds the whole layout.
-int apply_membership(World* w) {
+int plan_membership(World* w, MemPlan& p) {
+    p.active = false;
     if (w->touched.empty()) return NFK_OK;
     using clk = std::chrono::steady_clock;
-    const auto t_host = clk::now();
-    clk::time_point t_edit, t_lists, t_dev;
+    p.t_host = clk::now();
+    p.full = false;
+    p.aff.clear();
+    p.einfo.clear();
+    p.edits.clear();
+    p.ins_rank.clear();
+    p.ins_obj.clear();
+    p.rem_rank.clear();
+    p.ins_meta.clear();
+    p.ins_src.clear();
+    p.moves.clear();
+    p.mv_rows_dev = p.mv_list_dev = p.ed_rows = p.ed_list = 0;
+    p.nsegs.clear();
+    p.nsrc.clear();
     Dev& d = w->d;
     const auto cmp = [w](int32_t a, int32_t b) { return guid_less(w, a, b); };
     // The new member lists are built on copies of the affected segments; nothing of the world
     // changes before every check has passed (a failure leaves the window's calls queued).
-    bool full = false;
-    std::vector<int32_t> aff;  // affected segments, in first-touch order
+    bool& full = p.full;
+    std::vector<int32_t>& aff = p.aff;  // affected segments, in first-touch order
     auto seg_at = [&](int32_t slot) {
         int32_t lo = 0, hi = (int32_t)w->segs.size() - 1;
         while (lo < hi) {
@@ -808,15 +871,9 @@ int apply_membership(World* w) {
         }
         return lo;
     };
-    // per affected segment: its new member list, the old ranks its leavers had and its joiners
-    // with their new ranks (ins, sorted by rank)
-    struct EdInfo {
-        World::Seg seg;
-        std::vector<int32_t> rem, join;
-        std::vector<std::pair<int32_t, int32_t>> ins;  // (new rank, object)
-    };
-    std::vector<int32_t> epos(w->segs.size(), -1);
-    std::vector<EdInfo> einfo;
+    std::vector<int32_t>& epos = p.epos;
+    epos.assign(w->segs.size(), -1);
+    std::vector<EdInfo>& einfo = p.einfo;
     einfo.reserve(2 * w->touched.size() + 1);
     auto ed = [&](int32_t g) -> EdInfo& {
         if (epos[g] < 0) {
@@ -834,12 +891,12 @@ int apply_membership(World* w) {
     }
     for (int32_t o : w->touched) {
         if (!w->alive[o]) continue;
-        auto f = w->seg_of.find({w->scene[o], w->group[o]});
-        if (f == w->seg_of.end()) {
+        const int32_t gi = find_seg(w, w->scene[o], w->group[o]);
+        if (gi < 0) {
             full = true;
             continue;
         }
-        ed(f->second).join.push_back(o);
+        ed(gi).join.push_back(o);
     }
     // each new member list in one pass: the old list without its leavers (known by rank, no
     // NFGUID comparison), the joiners (sorted) spliced in at their binary-searched places
@@ -852,40 +909,36 @@ int apply_membership(World* w) {
         x.seg.cap = old.cap;
         x.seg.np = old.np;
         std::sort(x.rem.begin(), x.rem.end());
-        std::vector<int32_t> kept;
-        kept.reserve(old.objs.size() - x.rem.size());
-        size_t r = 0;
-        for (int32_t i = 0; i < (int32_t)old.objs.size(); i++) {
-            if (r < x.rem.size() && x.rem[r] == i) {
-                r++;
-                continue;
-            }
-            kept.push_back(old.objs[i]);
-        }
         std::sort(x.join.begin(), x.join.end(), cmp);
         std::vector<int32_t>& v = x.seg.objs;
-        v.reserve(kept.size() + x.join.size());
-        size_t at = 0;
+        v.reserve(old.objs.size() - x.rem.size() + x.join.size());
+        // (a joiner's place is searched in the old list, leavers included: they are still in
+        // NFGUID order, and one that rejoins compares equal to itself and is skipped below)
+        size_t r = 0, at = 0;
+        auto copy_to = [&](size_t p) {  // old ranks [at, p) without the leavers
+            for (; at < p; at++) {
+                if (r < x.rem.size() && x.rem[r] == (int32_t)at) {
+                    r++;
+                    continue;
+                }
+                v.push_back(old.objs[at]);
+            }
+        };
         for (int32_t o : x.join) {
-            const size_t p = (size_t)(std::lower_bound(kept.begin() + at, kept.end(), o, cmp) - kept.begin());
-            v.insert(v.end(), kept.begin() + at, kept.begin() + p);
+            copy_to((size_t)(std::lower_bound(old.objs.begin() + at, old.objs.end(), o, cmp) - old.objs.begin()));
             x.ins.push_back({(int32_t)v.size(), o});
             v.push_back(o);
-            at = p;
         }
-        v.insert(v.end(), kept.begin() + at, kept.end());
+        copy_to(old.objs.size());
         if ((int32_t)v.size() > old.cap) full = true;
     }
-    std::vector<int32_t> pack_src, un_dst;  // (host-built lists: none since k_seg_edit)
-    std::vector<int64_t> un_src;
-    MetaLists m;
     // edited and new segments: their slot lists are generated on the device (k_seg_edit) from the
     // removed ranks and the inserted objects at their new ranks
-    std::vector<SegEdit> edits;
-    std::vector<int32_t> ins_rank, ins_obj, rem_rank;
-    std::vector<uint64_t> ins_meta;
-    std::vector<int64_t> ins_src;
-    int32_t ed_rows = 0, ed_list = 0;
+    std::vector<SegEdit>& edits = p.edits;
+    std::vector<int32_t>&ins_rank = p.ins_rank, &ins_obj = p.ins_obj, &rem_rank = p.rem_rank;
+    std::vector<uint64_t>& ins_meta = p.ins_meta;
+    std::vector<int64_t>& ins_src = p.ins_src;
+    int32_t &ed_rows = p.ed_rows, &ed_list = p.ed_list;
     // ob: the old segment (-1: a new (scene, group) pair; its members are all inserted)
     auto add_edit = [&](World::Seg& g, int32_t ob_seg, const std::vector<std::pair<int32_t, int32_t>>* ins,
                         const std::vector<int32_t>* rem, bool all) -> int {
@@ -927,13 +980,13 @@ int apply_membership(World* w) {
         edits.push_back(e);
         return NFK_OK;
     };
-    std::vector<World::Seg> nsegs;
-    std::vector<int32_t> nsrc;   // full: nsegs[i] is untouched segment nsrc[i] (members kept), or -1
+    std::vector<World::Seg>& nsegs = p.nsegs;
+    std::vector<int32_t>& nsrc = p.nsrc;
     std::vector<int32_t> nold;   // full: nsegs[i] is edited segment nold[i], or -1 (untouched / new)
-    std::vector<SegMove> moves;  // full: untouched segments whose slot range changes
-    int32_t mv_rows_dev = 0, mv_list_dev = 0;
-    const int32_t max_np0 = w->max_np;
-    t_edit = clk::now();
+    std::vector<SegMove>& moves = p.moves;  // full: untouched segments whose slot range changes
+    int32_t &mv_rows_dev = p.mv_rows_dev, &mv_list_dev = p.mv_list_dev;
+    const int32_t max_np0 = p.max_np0 = w->max_np;
+    p.t_edit = clk::now();
     if (full) {
         // The (scene, group)-ordered segment table is rebuilt from the member lists: untouched
         // segments keep theirs, edited ones take their edit copies, the objects of new (scene,
@@ -944,7 +997,7 @@ int apply_membership(World* w) {
         // bulk of the world) are generated on the device from their old and new ranges.
         std::map<std::pair<int32_t, int32_t>, std::vector<int32_t>> fresh;
         for (int32_t o : w->touched)
-            if (w->alive[o] && !w->seg_of.count({w->scene[o], w->group[o]}))
+            if (w->alive[o] && find_seg(w, w->scene[o], w->group[o]) < 0)
                 fresh[{w->scene[o], w->group[o]}].push_back(o);
         for (auto& f : fresh) std::sort(f.second.begin(), f.second.end(), cmp);
         auto fit = fresh.begin();
@@ -1033,7 +1086,28 @@ int apply_membership(World* w) {
         ed_list += e.nc;
     }
 
-    t_lists = clk::now();
+    p.t_lists = clk::now();
+    p.active = true;
+    return NFK_OK;
+}
+
+// the device phase of a planned window (after the previous frame has been waited for)
+int commit_membership(World* w, MemPlan& p) {
+    if (!p.active) return NFK_OK;
+    p.active = false;
+    using clk = std::chrono::steady_clock;
+    const auto t_dev = clk::now();
+    Dev& d = w->d;
+    const bool full = p.full;
+    const std::vector<SegEdit>& edits = p.edits;
+    const std::vector<int32_t>&ins_rank = p.ins_rank, &ins_obj = p.ins_obj, &rem_rank = p.rem_rank;
+    const std::vector<uint64_t>& ins_meta = p.ins_meta;
+    const std::vector<int64_t>& ins_src = p.ins_src;
+    const std::vector<SegMove>& moves = p.moves;
+    const int32_t mv_rows_dev = p.mv_rows_dev, mv_list_dev = p.mv_list_dev, ed_rows = p.ed_rows, ed_list = p.ed_list;
+    std::vector<int32_t> pack_src, un_dst;  // (host-built lists: none since k_seg_edit)
+    std::vector<int64_t> un_src;
+    MetaLists m;
     // device: pack movers (old slots), then unpack into the new layout, then the metadata.  The
     // untouched segments' lists (full re-layout) are generated first, from the old metadata.
     const int32_t rw = w->row_words;
@@ -1101,10 +1175,14 @@ int apply_membership(World* w) {
                                (int32_t)nd, w->slot_obj_d, w->fan_desc_w, w->pl_slot_w);
         HIPCHK(hipGetLastError());
     }
-
-    t_dev = clk::now();
+    const auto t_launched = clk::now();
     const size_t n_touched = w->touched.size();
-    // host maps
+    // host maps (while the device rewrites the slots)
+    std::vector<int32_t>& aff = p.aff;
+    const std::vector<int32_t>& epos = p.epos;
+    std::vector<EdInfo>& einfo = p.einfo;
+    std::vector<World::Seg>& nsegs = p.nsegs;
+    const std::vector<int32_t>& nsrc = p.nsrc;
     if (full) {
         w->n_relayout_full++;
         std::vector<int32_t> seg_base0(nsegs.size(), -1), seg_cap0(nsegs.size(), -1);
@@ -1115,8 +1193,7 @@ int apply_membership(World* w) {
                 nsegs[i].objs = std::move(w->segs[nsrc[i]].objs);
             }
         w->segs = std::move(nsegs);
-        w->seg_of.clear();
-        for (size_t g = 0; g < w->segs.size(); g++) w->seg_of[{w->segs[g].scene, w->segs[g].group}] = (int32_t)g;
+        index_segs(w);
         int64_t total = 0;
         for (const auto& g : w->segs) total = (int64_t)g.base + g.cap;
         // slots past the new end held entities before; every slot below it belongs to a segment
@@ -1134,14 +1211,29 @@ int apply_membership(World* w) {
             w->segs[gi].np = einfo[epos[gi]].seg.np;
         }
     }
+    // the ranks whose slot <-> object pairs change: [first leaver / joiner, the longer of the two
+    // lists), or only up to the last leaver / joiner when as many join as leave (the members
+    // behind it keep their ranks)
+    std::vector<int32_t> mlo(aff.size(), 0), mhi(aff.size());
+    for (size_t k = 0; k < aff.size(); k++) {
+        mhi[k] = w->segs[aff[k]].cap;
+        if (full) continue;
+        const EdInfo& x = einfo[epos[aff[k]]];
+        const int32_t nn = (int32_t)w->segs[aff[k]].objs.size(), no = nn - (int32_t)x.ins.size() + (int32_t)x.rem.size();
+        int32_t lo = INT32_MAX, last = -1;
+        if (!x.rem.empty()) lo = x.rem.front(), last = x.rem.back();
+        if (!x.ins.empty()) lo = std::min(lo, x.ins.front().first), last = std::max(last, x.ins.back().first);
+        mlo[k] = std::min(lo, mhi[k]);
+        mhi[k] = nn != no ? std::max(nn, no) : last + 1;
+    }
     for (int32_t o : w->touched)
         if (!w->alive[o]) w->slot_of_obj[o] = -1;
     // slot <-> object of the changed segments (disjoint slots and objects per segment: split over
     // threads when large)
-    auto maps = [w, &aff](size_t a, size_t b) {
+    auto maps = [w, &aff, &mlo, &mhi](size_t a, size_t b) {
         for (size_t k = a; k < b; k++) {
             const World::Seg& g = w->segs[aff[k]];
-            for (int32_t i = 0; i < g.cap; i++) {
+            for (int32_t i = mlo[k]; i < mhi[k]; i++) {
                 const int32_t ns = g.base + i;
                 const int32_t o = i < (int32_t)g.objs.size() ? g.objs[i] : -1;
                 w->obj_of_slot[ns] = o;
@@ -1151,7 +1243,7 @@ int apply_membership(World* w) {
     };
     {
         int64_t work = 0;
-        for (int32_t gi : aff) work += w->segs[gi].cap;
+        for (size_t k = 0; k < aff.size(); k++) work += mhi[k] - mlo[k];
         const int nt = work >= (1 << 17) ? (int)std::min<size_t>(8, aff.size()) : 1;
         if (nt <= 1) {
             maps(0, aff.size());
@@ -1169,11 +1261,12 @@ int apply_membership(World* w) {
     w->ins_n = 0;
     const auto t_end = clk::now();
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    (full ? w->ms_relayout_full : w->ms_relayout_seg) += ms(t_host, t_end);
+    (full ? w->ms_relayout_full : w->ms_relayout_seg) += ms(p.t_host, p.t_lists) + ms(t_dev, t_end);
     if (getenv("NFGPU_TRACE_MEMBERSHIP"))
-        fprintf(stderr, "apply_membership %s: %zu touched, edit %.3f ms, lists %.3f ms (%zu edited segments, %zu moves), "
-                "upload+launch %.3f ms, host maps %.3f ms\n", full ? "full" : "seg", n_touched, ms(t_host, t_edit),
-                ms(t_edit, t_lists), edits.size(), moves.size(), ms(t_lists, t_dev), ms(t_dev, t_end));
+        fprintf(stderr, "apply_membership %s: %zu touched, edit %.3f ms, lists %.3f ms (%zu edited segments, %zu moves; "
+                "before the previous frame is waited for), upload+launch %.3f ms, host maps %.3f ms\n",
+                full ? "full" : "seg", n_touched, ms(p.t_host, p.t_edit), ms(p.t_edit, p.t_lists), edits.size(),
+                moves.size(), ms(t_dev, t_launched), ms(t_launched, t_end));
     return NFK_OK;
 }
 
@@ -1508,9 +1601,9 @@ int nfk_commit(void* world) {
         }
     }
 
-    // membership layout: scene-group segments, NFGUID order inside (see apply_membership)
+    // membership layout: scene-group segments, NFGUID order inside (see plan_membership)
     const int64_t n_slots = plan_segments(w, w->slack, w->segs);
-    for (size_t g = 0; g < w->segs.size(); g++) w->seg_of[{w->segs[g].scene, w->segs[g].group}] = (int32_t)g;
+    index_segs(w);
     MetaLists meta;
     w->max_np = 0;
     for (auto& g : w->segs) {
@@ -2182,14 +2275,18 @@ int nfk_execute(void* world, int64_t now_ms) {
     const bool trace = getenv("NFGPU_TRACE_EXEC") != nullptr;  // host phases to stderr
     clk::time_point tp[6];
     tp[0] = clk::now();
-    {
-        int r = check_fanout(w);  // the last frame's fan-out is complete before it is replaced
-        if (r) return r;
-    }
     // ---- membership changes of this window ----
     {
-        int r = apply_membership(w);
+        // the window's host plan overlaps the previous frame still on the GPU; its device phase
+        // follows the wait for that frame
+        if (!w->mplan) w->mplan.reset(new MemPlan());
+        MemPlan& mp = *w->mplan;
+        int r = plan_membership(w, mp);
         if (r) return r;  // nothing of the window applied; its calls stay queued
+        const int rf = check_fanout(w);  // the last frame's fan-out is complete before it is replaced
+        r = commit_membership(w, mp);    // (a planned window is applied either way)
+        if (rf) return rf;
+        if (r) return r;
     }
     Dev d = w->d;
     d.now = now_ms;
