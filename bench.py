@@ -127,6 +127,36 @@ def cpu_baseline(args):
                       f"single thread, {r['seconds']:.1f} s"}
 
 
+class RowQueue:
+    """FIFO of int64 rows kept as a queue of chunks: `append` adds a chunk, `take(n)` removes the
+    oldest n rows, so neither copies the rows that stay (a migrating frame of the bench moves a
+    few hundred of a rank's million entities)."""
+
+    def __init__(self, rows):
+        self.chunks = collections.deque([rows] if len(rows) else [])
+        self.head = 0   # rows of chunks[0] already taken
+
+    def __len__(self):
+        return sum(len(c) for c in self.chunks) - self.head
+
+    def append(self, rows):
+        if len(rows):
+            self.chunks.append(rows)
+
+    def take(self, n):
+        parts, got = [], 0
+        while self.chunks and got < n:
+            c = self.chunks[0]
+            k = min(n - got, len(c) - self.head)
+            parts.append(c[self.head:self.head + k])
+            got += k
+            self.head += k
+            if self.head == len(c):
+                self.chunks.popleft()
+                self.head = 0
+        return np.concatenate(parts) if parts else None
+
+
 class Migration:
     """BASELINE config[2]: every `every`-th frame each rank's game logic sends `per_frame` of its
     entities into the next rank's scene (SwitchScene across shards, same group id, new position).
@@ -144,11 +174,8 @@ class Migration:
                                 meta_group=self.meta, device=dev)
         self.rank, self.world, self.per_frame, self.every = rank, world, per_frame, max(1, every)
         # entities this rank owns (guid head, guid data, group, cls, is_player), oldest first
-        # (a queue of row chunks: arrivals append a chunk, departures take from the front, so a
-        # migrating frame never copies the whole table)
-        self.owned = collections.deque([np.stack([w["guid_head"], w["guid_data"], w["group"], w["cls"],
-                                                  w["is_player"]], axis=1).astype(np.int64)])
-        self.head = 0
+        self.owned = RowQueue(np.stack([w["guid_head"], w["guid_data"], w["group"], w["cls"], w["is_player"]],
+                                       axis=1).astype(np.int64))
         self.rng = np.random.default_rng(77 + rank)
         self.frames = 0
         self.plan = None
@@ -169,16 +196,9 @@ class Migration:
         if self.frames % self.every:
             return
         dst = (self.rank + 1) % self.world
-        take = []
-        while self.owned and sum(len(c) for c in take) < self.per_frame:
-            c = self.owned[0]
-            k = min(self.per_frame - sum(len(t) for t in take), len(c) - self.head)
-            take.append(c[self.head:self.head + k])
-            self.head += k
-            if self.head == len(c):
-                self.owned.popleft()
-                self.head = 0
-        o = np.concatenate(take) if take else np.zeros((0, 5), np.int64)
+        o = self.owned.take(self.per_frame)
+        if o is None:
+            o = np.zeros((0, 5), np.int64)
         n = len(o)
         out = np.zeros((n, 11), np.int64)
         out[:, T_GH], out[:, T_GD], out[:, T_GROUP], out[:, T_CLS], out[:, T_PL] = o[:, 0], o[:, 1], o[:, 2], o[:, 3], o[:, 4]
