@@ -183,6 +183,13 @@ struct World {
     hipEvent_t mpin_done[2] = {nullptr, nullptr};
     bool mpin_pending[2] = {false, false};
     int mpin_slot = 0;
+    // nfk_export_objects' slot list, read by k_pack straight from pinned host memory (a few
+    // hundred rows: no copy, which behind a busy stream could wait for it)
+    int32_t* xpin = nullptr;
+    int32_t* xpin_dev = nullptr;
+    size_t xpin_cap = 0;
+    hipEvent_t xpin_done = nullptr;
+    bool xpin_pending = false;
     uint64_t* fan_desc_w = nullptr;
     int32_t* pl_slot_w = nullptr;
     int64_t n_relayout_full = 0, n_relayout_seg = 0;
@@ -1368,6 +1375,8 @@ int nfk_destroy(void* world) {
         if (w->mpin_done[i]) (void)hipEventDestroy(w->mpin_done[i]);
         if (w->mpin[i]) (void)hipHostFree(w->mpin[i]);
     }
+    if (w->xpin_done) (void)hipEventDestroy(w->xpin_done);
+    if (w->xpin) (void)hipHostFree(w->xpin);
     if (w->own_stream) (void)hipStreamDestroy(w->stream);
     delete w;
     return NFK_OK;
@@ -2189,6 +2198,8 @@ int nfk_export_objects(void* world, int32_t n, const int64_t* gh, const int64_t*
     if (!w || n < 0 || (n && (!gh || !gd || !rows_dev))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     if (n == 0) return NFK_OK;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     std::vector<int32_t> src(n), objs(n);
     for (int32_t i = 0; i < n; i++) {
         int r = lookup(w, gh[i], gd[i], &objs[i]);
@@ -2197,17 +2208,38 @@ int nfk_export_objects(void* world, int32_t n, const int64_t* gh, const int64_t*
             return fail(NFK_ERR_STATE, "export of an object whose membership already changed in this window");
         src[i] = w->slot_of_obj[objs[i]];
     }
-    w->mhost.clear();
-    const size_t o_src = stage_list(w, src);
-    int r = upload_mhost(w);
-    if (r) return r;
+    const auto t1 = clk::now();
+    // the slot list from pinned host memory (the last export's k_pack has read its copy)
+    if (!w->xpin_done) HIPCHK(hipEventCreateWithFlags(&w->xpin_done, hipEventDisableTiming));
+    if (w->xpin_pending) {
+        HIPCHK(hipEventSynchronize(w->xpin_done));
+        w->xpin_pending = false;
+    }
+    if ((size_t)n > w->xpin_cap) {
+        if (w->xpin) HIPCHK(hipHostFree(w->xpin));
+        w->xpin = nullptr;
+        const size_t c = std::max<size_t>((size_t)n, 2 * w->xpin_cap);
+        HIPCHK(hipHostMalloc((void**)&w->xpin, c * sizeof(int32_t), hipHostMallocDefault));
+        HIPCHK(hipHostGetDevicePointer((void**)&w->xpin_dev, w->xpin, 0));
+        w->xpin_cap = c;
+    }
+    memcpy(w->xpin, src.data(), (size_t)n * sizeof(int32_t));
+    const auto t2 = clk::now();
     hipLaunchKernelGGL(k_pack, dim3(grid_for((size_t)n * w->row_words)), dim3(kTPB), 0, w->stream, w->d,
-                       (const int32_t*)((char*)w->mlist + o_src), n, w->row_words, rows_dev);
+                       (const int32_t*)w->xpin_dev, n, w->row_words, rows_dev);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(w->xpin_done, w->stream));
+    w->xpin_pending = true;
+    const auto t3 = clk::now();
     for (int32_t i = 0; i < n; i++) {
         w->obj_of.erase(gh[i], gd[i]);
         w->alive[objs[i]] = 0;
         touch(w, objs[i]);
+    }
+    if (getenv("NFGPU_TRACE_MEMBERSHIP")) {
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "nfk_export_objects: %d rows, lookup %.3f ms, upload %.3f ms, launch %.3f ms, unmap %.3f ms\n", n,
+                ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, clk::now()));
     }
     return NFK_OK;
 }
