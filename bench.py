@@ -160,8 +160,9 @@ class RowQueue:
 class Migration:
     """BASELINE config[2]: every `every`-th frame each rank's game logic sends `per_frame` of its
     entities into the next rank's scene (SwitchScene across shards, same group id, new position).
-    The tickets (one int64 array, shard.TICKET_COLS) are decided and all-gathered over a gloo group
-    while the previous frame runs on the GPU; at the frame start the state rows travel GPU-to-GPU
+    The tickets (one int64 array, shard.TICKET_COLS) are decided after a frame's launch and
+    all-gathered over a gloo group asynchronously (gloo's own thread), while this rank waits for
+    and launches the next frame; the frame after that starts by moving the state rows GPU-to-GPU
     with one RCCL all_to_all.  Frames without migrations make no collective call at all."""
 
     def __init__(self, m, w, rank, world, per_frame, every, dev):
@@ -178,16 +179,21 @@ class Migration:
                                        axis=1).astype(np.int64))
         self.rng = np.random.default_rng(77 + rank)
         self.frames = 0
-        self.plan = None
+        self.pending = collections.deque()   # (frame count when started, ticket exchange in flight)
         self.after_frame()
 
     def before_frame(self):
         from noahgameframe_amd.shard import T_GH, T_GD, T_GROUP, T_CLS, T_PL
-        if self.plan is not None:
-            recv = self.shard.migrate_array(self.plan)
+        # exchanges started at least one frame ago (the same frames on every rank)
+        while self.pending and self.pending[0][0] < self.frames:
+            recv = self.shard.migrate_array(self.pending.popleft()[1].wait())
             if len(recv):
                 self.owned.append(recv[:, [T_GH, T_GD, T_GROUP, T_CLS, T_PL]])
-        self.plan = None
+
+    def finish(self):
+        """Waits for the exchanges still in flight (their tickets are not carried out)."""
+        while self.pending:
+            self.pending.popleft()[1].wait()
 
     def after_frame(self):
         """The next frame's tickets (only on every `every`-th frame, the same frames on every rank)."""
@@ -207,7 +213,7 @@ class Migration:
         out[:, T_X], out[:, T_Y] = xy[:, 0].view(np.int64), xy[:, 1].view(np.int64)
         out[:, T_Z] = np.zeros(n, np.float64).view(np.int64)
         out[:, T_SRC], out[:, T_DST] = self.rank, dst
-        self.plan = self.shard.exchange_ticket_array(out, max_rows=self.per_frame)  # one all-gather
+        self.pending.append((self.frames, self.shard.exchange_ticket_array_async(out, max_rows=self.per_frame)))
 
 
 def main():
@@ -291,10 +297,13 @@ def main():
         timed("execute", lambda: m.Execute(t0 + tick * args.tick_ms))
         m.outputs_raw()   # the consumer's read of the frame's outputs (dense ranks: k_scan_tiles)
         if mig:
-            timed("tickets", mig.after_frame)   # next frame's tickets, exchanged while this frame runs on the GPU
+            timed("tickets", mig.after_frame)   # tickets, exchanged while this and the next frame run
         tick += 1
 
-    for _ in range(args.warmup):
+    # with migration the untimed frames cover one whole migration cycle (a plan is carried out one
+    # frame after it is made), so the timed frames see its steady state, not the first arrival
+    warmup = max(args.warmup, args.migrate_every + 2) if mig else args.warmup
+    for _ in range(warmup):
         frame()
     s = m.summary()  # also surfaces any device error from warmup
     # the timed region runs without kernel instrumentation ...
@@ -319,6 +328,8 @@ def main():
     for _ in range(args.steps):
         frame()
     m.set_profiling(False)
+    if mig:
+        mig.finish()
     ms, nl, byts = m.kernel_times()
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
@@ -377,7 +388,7 @@ def main():
         wl_name = CONFIG_NAMES[args.config]
     out = {
         "metric": METRIC, "value": value, "unit": "entity-ticks/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+        "warmup": warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int64/f64", "data": "synthetic",
         "config": {"workload": wl_name,
                    "entities_per_gpu": args.entities, "groups": args.groups,

@@ -1799,6 +1799,28 @@ int nfk_commit(void* world) {
     for (auto& v : w->init_props) std::vector<uint64_t>().swap(v);
     for (auto& v : w->init_rcells) std::vector<uint64_t>().swap(v);
     build_jit(w);  // k_tick for this schema (hipRTC); the generic kernel stays when it cannot be built
+    // room for objects created or imported after commit (every arrival takes a new object index):
+    // the per-object vectors and the arrivals' row buffer grow in the background of a frame only
+    // after a quarter of the world has arrived, not on the first SwitchScene into this shard
+    {
+        const size_t room = (size_t)w->n_obj + (size_t)w->n_obj / 4 + 4096;
+        w->gh.reserve(room);
+        w->gd.reserve(room);
+        w->guid.reserve(room);
+        w->scene.reserve(room);
+        w->group.reserve(room);
+        w->cls.reserve(room);
+        w->isplayer.reserve(room);
+        w->slot_of_obj.reserve(room);
+        w->alive.reserve(room);
+        w->src_row.reserve(room);
+        w->m_flag.reserve(room);
+        if (!w->ins_rows) {
+            const size_t c = 1024;
+            HIPCHK(hipMalloc((void**)&w->ins_rows, c * (size_t)w->row_words * 8));
+            w->ins_cap = c;
+        }
+    }
     w->committed = true;
     return NFK_OK;
 }

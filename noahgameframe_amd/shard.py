@@ -125,15 +125,7 @@ class SceneShard:
         if self.ws == 1:   # (a one-rank rehearsal: the plan is this rank's own tickets)
             return out.copy()
         if max_rows is not None:
-            if len(out) > max_rows:
-                raise ValueError("more tickets than max_rows")
-            pad = torch.zeros((max_rows + 1, 11), dtype=torch.int64)
-            pad[0, 0] = len(out)
-            pad[1:1 + len(out)] = torch.from_numpy(out)
-            allp = [torch.zeros((max_rows + 1, 11), dtype=torch.int64) for _ in range(self.ws)]
-            dist.all_gather(allp, pad, group=self.meta_pg)
-            parts = [a[1:1 + int(a[0, 0])].numpy() for a in allp]
-            return np.concatenate(parts) if parts else np.zeros((0, 11), np.int64)
+            return self.exchange_ticket_array_async(out, max_rows).wait()
         n = torch.tensor([len(out)], dtype=torch.int64)
         ns = [torch.zeros(1, dtype=torch.int64) for _ in range(self.ws)]
         dist.all_gather(ns, n, group=self.meta_pg)
@@ -146,6 +138,24 @@ class SceneShard:
         allp = [torch.zeros((mx, 11), dtype=torch.int64) for _ in range(self.ws)]
         dist.all_gather(allp, pad, group=self.meta_pg)
         return np.concatenate([a[:c].numpy() for a, c in zip(allp, ns)])
+
+    def exchange_ticket_array_async(self, out, max_rows):
+        """The one-all-gather form of exchange_ticket_array, started now and finished by the
+        returned handle's wait() (-> the global plan): the gather runs on the meta group's own
+        thread while the caller goes on (bench.py starts it after a frame's launch and waits one
+        frame later).  Every rank starts its exchanges in the same order."""
+        torch = self.torch
+        import torch.distributed as dist
+        out = np.ascontiguousarray(out, np.int64).reshape(-1, 11)
+        if len(out) > max_rows:
+            raise ValueError("more tickets than max_rows")
+        if self.ws == 1:   # (a one-rank rehearsal: the plan is this rank's own tickets)
+            return _Ready(out.copy())
+        pad = torch.zeros((max_rows + 1, 11), dtype=torch.int64)
+        pad[0, 0] = len(out)
+        pad[1:1 + len(out)] = torch.from_numpy(out)
+        allp = [torch.zeros((max_rows + 1, 11), dtype=torch.int64) for _ in range(self.ws)]
+        return _Gather(dist.all_gather(allp, pad, group=self.meta_pg, async_op=True), allp)
 
     def migrate(self, out, plan=None):
         """Collective (every rank calls it once per frame, possibly with nothing to send).
@@ -219,6 +229,28 @@ class SceneShard:
             rbuf.copy_(hr)
         else:
             dist.all_to_all_single(rbuf.view(-1), sbuf.view(-1), rsplit, ssplit, group=self.pg)
+
+
+class _Ready:
+    def __init__(self, plan):
+        self.plan = plan
+
+    def wait(self):
+        return self.plan
+
+
+class _Gather:
+    """An all-gather of [count row | rows padded to the bound] per rank, in flight."""
+
+    def __init__(self, work, allp):
+        self.work, self.allp, self.plan = work, allp, None
+
+    def wait(self):
+        if self.plan is None:
+            self.work.wait()
+            parts = [a[1:1 + int(a[0, 0])].numpy() for a in self.allp]
+            self.plan = np.concatenate(parts) if parts else np.zeros((0, 11), np.int64)
+        return self.plan
 
 
 def _f64(x):

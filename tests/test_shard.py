@@ -210,7 +210,10 @@ def _ticket_worker(rank, ws, port, q):
     a = sh.exchange_ticket_array(out)                 # counts, then padded rows
     b = sh.exchange_ticket_array(out, max_rows=8)     # one all-gather under a known bound
     c = sh.exchange_ticket_array(out[:0], max_rows=8)
-    q.put((rank, a.tolist(), b.tolist(), c.shape))
+    h1 = sh.exchange_ticket_array_async(out, max_rows=8)   # two exchanges in flight, waited in order
+    h2 = sh.exchange_ticket_array_async(out[:1], max_rows=8)
+    d, e = h1.wait(), h2.wait()
+    q.put((rank, a.tolist(), b.tolist(), c.shape, d.tolist(), e.tolist()))
     dist.destroy_process_group()
 
 
@@ -228,6 +231,8 @@ def test_ticket_exchange_single_gather_gloo_cpu():
     for p in ps:
         p.join(timeout=60)
     want = np.concatenate([np.arange(3 * 11).reshape(-1, 11), np.arange(6 * 11).reshape(-1, 11) + 1000]).tolist()
+    first = [np.arange(11).tolist(), (np.arange(11) + 1000).tolist()]   # each rank's first ticket
     for r in (0, 1):
-        a, b, c = res[r]
+        a, b, c, d, e = res[r]
         assert a == want and b == want and tuple(c) == (0, 11)
+        assert d == want and e == first
