@@ -363,7 +363,9 @@ int pin_reserve(World* w, size_t bytes) {
     }
     if (bytes > w->pin_cap) {
         if (w->pin) HIPCHK(hipHostFree(w->pin));
+        w->pin = nullptr;
         size_t cap = std::max(bytes, w->pin_cap * 2);
+        w->pin_cap = 0;  // (until the new buffer exists)
         HIPCHK(hipHostMalloc(&w->pin, cap, hipHostMallocDefault));
         w->pin_cap = cap;
     }
@@ -371,7 +373,9 @@ int pin_reserve(World* w, size_t bytes) {
         // kernels of earlier frames may still read the old staging buffer
         HIPCHK(hipStreamSynchronize(w->stream));
         if (w->stage) HIPCHK(hipFree(w->stage));
+        w->stage = nullptr;
         size_t cap = std::max(bytes, w->stage_cap * 2);
+        w->stage_cap = 0;  // (until the new buffer exists)
         HIPCHK(hipMalloc(&w->stage, cap));
         w->stage_cap = cap;
     }
@@ -534,6 +538,7 @@ int dev_reserve(World* w, void** p, size_t* cap, size_t bytes) {
     if (*p) HIPCHK(hipFree(*p));
     *p = nullptr;
     const size_t c = std::max(bytes, *cap + *cap / 2);
+    *cap = 0;  // (until the new buffer exists)
     HIPCHK(hipMalloc(p, c));
     *cap = c;
     return NFK_OK;
@@ -790,6 +795,7 @@ int upload_mhost(World* w) {
         if (w->mpin[s]) HIPCHK(hipHostFree(w->mpin[s]));
         w->mpin[s] = nullptr;
         const size_t c = std::max(w->mhost.size(), 2 * w->mpin_cap[s]);
+        w->mpin_cap[s] = 0;  // (until the new buffer exists)
         HIPCHK(hipHostMalloc((void**)&w->mpin[s], c, hipHostMallocDefault));
         w->mpin_cap[s] = c;
     }
@@ -2241,6 +2247,7 @@ int nfk_export_objects(void* world, int32_t n, const int64_t* gh, const int64_t*
         if (w->xpin) HIPCHK(hipHostFree(w->xpin));
         w->xpin = nullptr;
         const size_t c = std::max<size_t>((size_t)n, 2 * w->xpin_cap);
+        w->xpin_cap = 0;  // (until the new buffer exists)
         HIPCHK(hipHostMalloc((void**)&w->xpin, c * sizeof(int32_t), hipHostMallocDefault));
         HIPCHK(hipHostGetDevicePointer((void**)&w->xpin_dev, w->xpin, 0));
         w->xpin_cap = c;
