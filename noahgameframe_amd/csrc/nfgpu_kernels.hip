@@ -846,7 +846,10 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
 // one workgroup of 1024 threads: every thread loads kScanPer consecutive counts of all four
 // arrays at once (one memory round trip per pass), then four block scans share each barrier.
 // Writes bases[n+1] (bases[n] = total) and the frame totals.
-constexpr int kScanTPB = 1024, kScanPer = 8;
+#ifndef NFGPU_SCANPER
+#define NFGPU_SCANPER 8
+#endif
+constexpr int kScanTPB = 1024, kScanPer = NFGPU_SCANPER;
 
 struct ScanArr {
     uint32_t v[kScanPer];
@@ -855,10 +858,12 @@ struct ScanArr {
 
 __device__ __forceinline__ void scan_load(ScanArr& x, const uint32_t* __restrict__ cnt, int len, int i0) {
     x.sum = 0;
-    if (i0 + kScanPer <= len) {  // two 16-byte loads (cnt is 16-byte aligned, i0 a multiple of 8)
-        const uint4 a = ((const uint4*)(cnt + i0))[0], b = ((const uint4*)(cnt + i0))[1];
-        x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
-        x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+    if (i0 + kScanPer <= len) {  // 16-byte loads (cnt is 16-byte aligned, i0 a multiple of kScanPer)
+#pragma unroll
+        for (int q = 0; q < kScanPer / 4; q++) {
+            const uint4 a = ((const uint4*)(cnt + i0))[q];
+            x.v[4 * q] = a.x; x.v[4 * q + 1] = a.y; x.v[4 * q + 2] = a.z; x.v[4 * q + 3] = a.w;
+        }
     } else {
 #pragma unroll
         for (int q = 0; q < kScanPer; q++) x.v[q] = (i0 + q < len) ? cnt[i0 + q] : 0u;
@@ -866,7 +871,7 @@ __device__ __forceinline__ void scan_load(ScanArr& x, const uint32_t* __restrict
 #pragma unroll
     for (int q = 0; q < kScanPer; q++) x.sum += x.v[q];
 }
-static_assert(kScanPer == 8, "scan_load's vector path loads 8 counts");
+static_assert(kScanPer % 4 == 0, "scan_load's vector path loads 4 counts at a time");
 
 // block-scan step of one array (s_pre = exclusive prefix of the wave totals); returns the pass total
 __device__ __forceinline__ unsigned long long scan_store(ScanArr& x, const unsigned long long* s_pre,
