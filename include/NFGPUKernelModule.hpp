@@ -29,10 +29,11 @@
 //     guid, property) order.
 //   * Time comes from SetTimeSource (default: NFGetTime(), system clock milliseconds,
 //     NFPlatform.h:367), read by AddSchedule and Execute like the reference.
-//   * Limits: 64 int + 64 float frame properties, 15 classes, 32 schedule names, 8 records of at
+//   * Limits: 64 int + 64 float + 32 object frame properties (128 in all), 15 classes, 32 schedule names, 8 records of at
 //     most 64 rows x 16 columns, 4 ops per heartbeat program, 12 properties written by programs,
 //     16383 players per scene group (nfgpu.h).
-//   * String / Vector properties stay host-side (not on the frame path).
+//   * String / Vector properties stay host-side (not on the frame path); object (NFGUID) properties
+//     are device columns like the int / float ones.
 #pragma once
 #include <cstdint>
 #include <functional>
@@ -65,9 +66,11 @@ struct TData {
     TDATA_TYPE type = TDATA_UNKNOWN;
     int64_t i = 0;
     double f = 0.0;
+    NFGUID o;
     TDATA_TYPE GetType() const { return type; }
     int64_t GetInt() const { return type == TDATA_INT ? i : 0; }
     double GetFloat() const { return type == TDATA_FLOAT ? f : 0.0; }
+    NFGUID GetObject() const { return type == TDATA_OBJECT ? o : NFGUID(); }
 };
 
 struct RECORD_EVENT_DATA {
@@ -157,7 +160,7 @@ public:
     // ---- schema (what NFIClassModule loads from Struct/Class/*.xml) ----
     explicit NFGPUKernelModule(int capacity, void* hip_stream = nullptr);
     ~NFGPUKernelModule();
-    int AddProperty(const std::string& name, TDATA_TYPE type);  // returns property id
+    int AddProperty(const std::string& name, TDATA_TYPE type);  // TDATA_INT / FLOAT / OBJECT; returns its index
     int AddClass(const std::string& name);
     void SetPropertyFlags(const std::string& cls, const std::string& prop, bool pub, bool priv, bool upload);
     int AddRecord(const std::string& name, int rows, const std::vector<TDATA_TYPE>& cols);
@@ -190,6 +193,10 @@ public:
     bool SetPropertyFloat(const NFGUID& self, const std::string& name, double v);
     int64_t GetPropertyInt(const NFGUID& self, const std::string& name);
     double GetPropertyFloat(const NFGUID& self, const std::string& name);
+    // NFIKernelModule::SetPropertyObject / GetPropertyObject (KM:362 / KM:440): an NFGUID column on
+    // the device (16 bytes per entity), queued and read like the int / float properties
+    bool SetPropertyObject(const NFGUID& self, const std::string& name, const NFGUID& v);
+    NFGUID GetPropertyObject(const NFGUID& self, const std::string& name);
     // NFIKernelModule::SetRecordInt / SetRecordFloat (NFIKernelModule.h:120-121): queued like the
     // property setters and applied at the next Execute through NFCRecord::SetInt / SetFloat; true
     // once queued (the reference also returns false for an unused row or an unchanged value,

@@ -33,6 +33,8 @@ extern "C" {
 
 #define NFK_MAX_INT_PROPS 64
 #define NFK_MAX_FLT_PROPS 64
+#define NFK_MAX_OBJ_PROPS 32 /* object (NFGUID) properties; n_int + n_flt + n_obj <= NFK_MAX_PROPS */
+#define NFK_MAX_PROPS 128
 #define NFK_MAX_CLASSES 16 /* class id 15 is reserved (marks a free slot on the device) */
 #define NFK_MAX_KINDS 32
 #define NFK_MAX_OPS 4
@@ -90,6 +92,8 @@ typedef struct nfk_config {
     int32_t slack_per_256; /* free slots kept per 256 members of a scene group for arrivals
                               (SwitchScene / imports) without a full re-layout:
                               0 = default 16, < 0 = none */
+    int32_t n_obj;        /* object (NFGUID) property columns, prop ids [n_int+n_flt, +n_obj):
+                             16 bytes per entity (data, head), TDATA_OBJECT (NFIDataList.h) */
 } nfk_config;
 
 typedef struct nfk_summary {
@@ -142,6 +146,10 @@ typedef struct nfk_outputs {
     const uint32_t* fi_slot; const uint32_t* fi_kind; const int32_t* fi_remain;
     const uint32_t* msg_rcpt; /* one run per tile (see above) */
     const int32_t* slot_obj;  /* slot -> object index */
+    /* object-property events (ev_pid >= n_int + n_flt): ev_old / ev_new hold the NFGUID's data
+     * half (nData64), these its head half (nHead64); other events leave them unwritten.  NULL in a
+     * world without object properties. */
+    const uint64_t* ev_old_h; const uint64_t* ev_new_h;
 } nfk_outputs;
 
 /* ---- lifetime: NFCKernelModule ctor/Init/AfterInit (KM:17,51,1490) ---- */
@@ -164,6 +172,8 @@ int nfk_create_objects(void* world, int32_t n, const int64_t* guid_head, const i
                        const uint8_t* is_player);
 /* creation-time property values (CreateObject's config SetProperty, KM:193-208), creation order */
 int nfk_load_prop(void* world, int32_t pid, const uint64_t* bits /* [n_objects] */);
+/* creation-time object property values (NFGUID head / data halves), creation order */
+int nfk_load_object(void* world, int32_t pid, const int64_t* head /* [n_objects] */, const int64_t* data);
 /* creation-time record contents, cells [n_objects][cols][rows] as bit patterns, used-row masks */
 int nfk_load_record(void* world, int32_t rec, const uint64_t* cells, const uint64_t* used_mask);
 /* build the device layout: slots sorted by (scene, group, guid) (NFCSceneInfo group maps) */
@@ -185,7 +195,8 @@ int nfk_switch_scene(void* world, int64_t guid_head, int64_t guid_data, int32_t 
 int nfk_destroy_objects(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data);
 /* objects ever created in this world (creation-order indices of the nfk_read_* arrays) */
 int nfk_object_count(void* world, int32_t* n);
-/* An entity's state as a ROW of 64-bit words: properties (prop id order), per heartbeat kind its
+/* An entity's state as a ROW of 64-bit words: properties (prop id order; an object property is two
+ * words, data then head), per heartbeat kind its
  * schedule (next, remain|state, start, all|interval), per record its cells [cols][rows] and its
  * used-row mask.  Rows let a scene shard hand entities to another (SwitchScene across GPUs). */
 int nfk_row_words(void* world, int32_t* words);
@@ -200,7 +211,8 @@ int nfk_import_objects(void* world, int32_t n, const int64_t* guid_head, const i
                        const int32_t* scene, const int32_t* group, const uint8_t* cls, const uint8_t* is_player,
                        const uint64_t* rows_dev);
 /* CreateObject after commit with creation-time property values from host memory
- * (props [n][n_int + n_flt] bit patterns; no schedules, empty records) */
+ * (props [n][n_int + n_flt + 2 n_obj] words: int / f64 bit patterns, then each object property's
+ * data and head halves; no schedules, empty records) */
 int nfk_spawn_objects(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
                       const int32_t* scene, const int32_t* group, const uint8_t* cls, const uint8_t* is_player,
                       const uint64_t* props);
@@ -210,6 +222,16 @@ int nfk_spawn_objects(void* world, int32_t n, const int64_t* guid_head, const in
  * reference's change predicates.  bits = int64 or f64 bit pattern. */
 int nfk_set_props(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
                   const int32_t* pid, const uint64_t* bits);
+
+/* ---- object properties: NFIKernelModule::SetPropertyObject (KM:362) -> NFCProperty::SetObject
+ * (PR:377-416): queued in call order with the other Sets, applied at the start of the next
+ * nfk_execute; a value equal to the current NFGUID (both halves) changes nothing and raises no
+ * event.  pid must be an object property. */
+int nfk_set_objects(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data, const int32_t* pid,
+                    const int64_t* val_head, const int64_t* val_data);
+/* NFIKernelModule::GetPropertyObject (KM:440): read-your-writes like nfk_get_props */
+int nfk_get_objects(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data, const int32_t* pid,
+                    int64_t* val_head, int64_t* val_data);
 
 /* ---- record mutation: NFIKernelModule::SetRecordInt/Float (KM:505, KM:545) ----
  * Queued in call order, applied at the start of the next nfk_execute through NFCRecord::SetInt /
@@ -282,10 +304,14 @@ int nfk_outputs_get(void* world, nfk_outputs* out);
 
 /* ---- host copies (synchronising) ---- */
 int nfk_read_prop(void* world, int32_t pid, uint64_t* bits /* [n_objects], creation order */);
+/* an object property's values, creation order */
+int nfk_read_object(void* world, int32_t pid, int64_t* head /* [n_objects] */, int64_t* data);
 int nfk_read_record(void* world, int32_t rec, uint64_t* cells /* [n_objects][cols][rows] */);
 /* schedule table in creation order: arrays [n_kind][n_objects] */
 int nfk_read_schedules(void* world, int64_t* next_ms, int32_t* remain, uint8_t* state);
 int nfk_read_events(void* world, int32_t* ev_obj, int32_t* ev_pid, uint64_t* ev_old, uint64_t* ev_new);
+/* the head halves of the object-property events, dense like nfk_read_events (0 for other events) */
+int nfk_read_events_obj(void* world, uint64_t* ev_old_h, uint64_t* ev_new_h);
 int nfk_read_rec_events(void* world, int32_t* re_obj, uint32_t* re_rrc, uint64_t* re_old, uint64_t* re_new);
 int nfk_read_fired(void* world, int32_t* fi_obj, int32_t* fi_kind, int32_t* fi_remain);
 /* dense CSR over [prop events ++ record events]: msg_off[n_ev + n_re + 1], recipients as objects */

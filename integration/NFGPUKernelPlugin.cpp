@@ -77,8 +77,11 @@ public:
         return gpu_.SwitchScene(to_gpu(self), scene, group, fX, fY, fZ, fOrient);
     }
     bool DestroyObject(const NFGUID& self) override {  // KM:273
+        // the reference's DestroyObject reads SceneID / GroupID through GetPropertyInt (KM:283-284),
+        // which this adapter answers from the device: it runs while the object is still there
+        const bool ok = NFCKernelModule::DestroyObject(self);
         gpu_.DestroyObject(to_gpu(self));
-        return NFCKernelModule::DestroyObject(self);
+        return ok;
     }
     nfgpu::NFGPUKernelModule gpu_;
 };

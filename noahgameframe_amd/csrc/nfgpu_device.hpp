@@ -63,7 +63,8 @@ constexpr unsigned kAblGroupColumns = 1u << 20, kAblSigGroups = 1u << 21;  // co
 constexpr unsigned kAblNoPad = 1u << 22;  // columns / schedule kinds at power-of-two strides (outputs exact)
 constexpr unsigned kAblRecVec = 1u << 23;  // k_records writes whole row-vectors back (outputs exact)
 constexpr unsigned kAblFanWin16 = 1u << 24, kAblFanWin32 = 1u << 25;  // k_tick fan-out LDS window up to 16 / 32 recipients (outputs exact)
-constexpr unsigned kAblFan1 = 1u << 26;  // k_tick fan-out: one recipient per lane (the round-1 form; outputs exact)
+constexpr unsigned kAblFan1 = 1u << 26;
+constexpr unsigned kAblTinyTcap = 1u << 27;  // test hook: k_tick's fan-out bound set to 4 messages (kErrFanBound)  // k_tick fan-out: one recipient per lane (the round-1 form; outputs exact)
 // four u32 at a dword-aligned address (gfx950 global memory allows it; one 16-byte store)
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Pad between consecutive property columns and schedule-kind arrays (bytes): with cap a power of
@@ -95,7 +96,8 @@ struct RecOpX {
     int32_t kind, rec, col, code, rows, cols, gfirst, glast;
 };
 
-constexpr int kMaxProps = NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS;
+constexpr int kMaxProps = NFK_MAX_PROPS;
+static_assert(NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS <= NFK_MAX_PROPS, "property id space");
 
 // a kind-program op in scalar-loadable form (32/64-bit fields only: gfx950 has no byte-sized
 // scalar loads): code | flags << 8 | dst << 16, and the U slots of dst/a/b/c one per byte
@@ -119,7 +121,7 @@ struct Tables {
     // property with a slot joins that slot's diff; any other queued Set is a "standalone" event.
     uint8_t w_slot[kMaxProps];
     int32_t nops[NFK_MAX_KINDS];
-    uint8_t pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
+    uint8_t pflags[NFK_MAX_CLASSES][kMaxProps];
     uint8_t rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
     RecOp recops[NFK_MAX_OPS];
     int32_t n_recops;
@@ -131,6 +133,8 @@ struct Tables {
 // Everything a kernel needs, passed by value.
 struct Dev {
     int32_t N, cap, n_int, n_flt, n_kind, n_rec, n_class;
+    int32_t n_obj;   // object (NFGUID) properties: prop ids [n_if, n_if + n_obj), two words per entity
+    int32_t n_if;    // n_int + n_flt: the first object property id
     int32_t s_kstr;  // kind stride of s_hot / s_cold in records: cap + a pad (see kColPad)
     int64_t now;
     int32_t has_recops;
@@ -154,6 +158,11 @@ struct Dev {
     const uint64_t* x_bits;
     uint64_t* x_old;
     uint64_t* x_new;
+    // object-property groups (x_pid >= n_if): the NFGUID head halves of the calls and of the
+    // group's frame-start / after values (x_bits / x_old / x_new hold the data halves)
+    const uint64_t* x_bits_h;
+    uint64_t* x_old_h;
+    uint64_t* x_new_h;
     int32_t n_x;              // groups
     uint32_t* fired_mask;  // [cap]
     // queued SetRecordInt / SetRecordFloat calls folded into (slot, cell) GROUPS sorted by (slot,
@@ -233,7 +242,16 @@ struct Dev {
     uint32_t* fi_slot; uint32_t* fi_kind; int32_t* fi_remain;
     uint32_t* re_slot; uint32_t* re_rrc; uint64_t* re_old; uint64_t* re_new; uint32_t* re_moff;
     uint32_t* msg_rcpt; int64_t msg_cap;
+    uint64_t* ev_old_h; uint64_t* ev_new_h;  // head halves of object-property events (n_obj > 0)
+    // host-mapped error word: a kernel that sets a bit of ctrl->err also stores it here, so the
+    // host sees it without a device read (nfk_outputs_get, nfk_execute)
+    unsigned* err_host;
 };
+
+__device__ __forceinline__ void dev_error(const Dev& d, unsigned bit) {
+    atomicOr(&d.ctrl->err, bit);
+    if (d.err_host) __hip_atomic_store(d.err_host, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 constexpr int kTallyN = 64, kTallyTick = 0, kTallyRec = 1, kTallyFan = 2;
 __device__ __forceinline__ void tally_add(const Dev& d, int k, unsigned long long v) {

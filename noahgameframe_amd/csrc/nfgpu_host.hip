@@ -146,7 +146,12 @@ struct World {
     bool own_stream = false;
     int32_t n_obj = 0;
     bool committed = false;
-    int n_prop = 0;
+    int n_prop = 0;  // properties: int [0, n_int), f64 [n_int, n_if), object (NFGUID) [n_if, n_prop)
+    int n_if = 0;    // n_int + n_flt
+    int n_pw = 0;    // property words of a row: n_if + 2 object halves per object property
+    // host-mapped error word (Dev::err_host): device error bits, seen without a device read
+    unsigned* err_host = nullptr;
+    unsigned* err_host_d = nullptr;
 
     std::vector<int64_t> gh, gd;
     struct Guid { int64_t h, d; };
@@ -225,6 +230,7 @@ struct World {
     // window's membership changes
     struct XOp { uint32_t slot, pid; uint64_t bits; };
     std::vector<XOp> xops;
+    std::vector<uint64_t> xops_h;  // the NFGUID head half of each queued call (worlds with object properties)
     // per-frame SetProperty groups (host scratch kept across frames) and their device results
     std::vector<uint32_t> g_slot, g_pid, g_first;
     std::vector<int32_t> look;           // GUID lookups of one batched call
@@ -254,7 +260,7 @@ struct World {
     struct Post { uint32_t slot, kind, op; float interval; int32_t count; int64_t time; };
     std::vector<uint32_t> pre_slot, pre_op;  // schedule-call folding results of the frame
     std::vector<Post> post, post_t;
-    void* xs_buf = nullptr;  // x_old / x_new
+    void* xs_buf = nullptr;  // x_old / x_new (/ x_old_h / x_new_h)
     size_t xs_cap = 0;
     struct HOp { int32_t code; uint32_t slot, kind; float interval; int32_t count; int64_t time; };
     std::vector<HOp> hops;
@@ -295,6 +301,26 @@ struct World {
 };
 
 constexpr uint32_t kNoKind = 0xFFFFFFFFu;  // HOp::kind of a RemoveSchedule(self, name) with no device program
+
+// word of property pid (its data half for an object property) in an entity row
+inline int64_t prop_word(const World* w, int32_t pid) {
+    return pid < w->n_if ? pid : w->n_if + 2 * (int64_t)(pid - w->n_if);
+}
+
+// Every failure of nfk_execute after the window's membership changes are applied drops the
+// window's remaining queued calls (SetProperty / SetObject, SetRecord, schedule calls) with it: the
+// membership part cannot be undone, so none of the window's calls is applied out of its order in
+// a later frame.  (A failure before that keeps every queue.)
+int drop_window(World* w, int r) {
+    w->xops.clear();
+    w->xops_h.clear();
+    w->hops.clear();
+    w->rsq.clear();
+    w->dcache.clear();
+    w->ov_last.clear();
+    w->ov_prev.clear();
+    return r;
+}
 
 int alloc_track(World* w, void** p, size_t bytes) {
     *p = nullptr;
@@ -589,7 +615,8 @@ int grow_event_tiles(World* w, int64_t per_tile) {
     int r;
     if ((r = regrow(w, (void**)&d.ev_slot, n * 4)) || (r = regrow(w, (void**)&d.ev_pid, n * 4)) ||
         (r = regrow(w, (void**)&d.ev_old, n * 8)) || (r = regrow(w, (void**)&d.ev_new, n * 8)) ||
-        (r = regrow(w, (void**)&d.ev_moff, n * 4))) {
+        (r = regrow(w, (void**)&d.ev_moff, n * 4)) ||
+        (d.n_obj && ((r = regrow(w, (void**)&d.ev_old_h, n * 8)) || (r = regrow(w, (void**)&d.ev_new_h, n * 8))))) {
         d.ev_tcap = 0;
         return r;
     }
@@ -1320,14 +1347,17 @@ int nfk_create(const nfk_config* cfg, void** out) {
     if (!cfg || !out) return fail(NFK_ERR_ARG, "null argument");
     if (cfg->capacity <= 0 || cfg->n_int < 0 || cfg->n_int > NFK_MAX_INT_PROPS || cfg->n_flt < 0 ||
         cfg->n_flt > NFK_MAX_FLT_PROPS || cfg->n_class <= 0 || cfg->n_class > NFK_MAX_CLASSES - 1 ||
-        cfg->n_kind < 0 || cfg->n_kind > NFK_MAX_KINDS || cfg->n_rec < 0 || cfg->n_rec > NFK_MAX_RECORDS)
+        cfg->n_kind < 0 || cfg->n_kind > NFK_MAX_KINDS || cfg->n_rec < 0 || cfg->n_rec > NFK_MAX_RECORDS ||
+        cfg->n_obj < 0 || cfg->n_obj > NFK_MAX_OBJ_PROPS || cfg->n_int + cfg->n_flt + cfg->n_obj > NFK_MAX_PROPS)
         return fail(NFK_ERR_ARG, "config out of range");
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev == 0) return fail(NFK_ERR_HIP, "no HIP device available");
     World* w = new World();
     w->cfg = *cfg;
-    w->n_prop = cfg->n_int + cfg->n_flt;
+    w->n_if = cfg->n_int + cfg->n_flt;
+    w->n_prop = w->n_if + cfg->n_obj;
+    w->n_pw = w->n_if + 2 * cfg->n_obj;
     w->slack = cfg->slack_per_256 == 0 ? 16 : std::max(cfg->slack_per_256, 0);
     if (cfg->stream) {
         w->stream = (hipStream_t)cfg->stream;
@@ -1342,10 +1372,13 @@ int nfk_create(const nfk_config* cfg, void** out) {
         hipEventCreateWithFlags(&w->mpin_done[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&w->mpin_done[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&w->err_done, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc((void**)&w->err_pin, 64, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void**)&w->err_pin, 64, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&w->err_host, 64, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&w->err_host_d, w->err_host, 0) != hipSuccess) {
         delete w;
         return fail(NFK_ERR_HIP, "hipEventCreate failed");
     }
+    *(volatile unsigned*)w->err_host = 0;
     w->init_props.resize(w->n_prop);
     w->init_rcells.resize(cfg->n_rec);
     w->init_rused.resize(cfg->n_rec);
@@ -1377,6 +1410,7 @@ int nfk_destroy(void* world) {
     if (w->pin_done) (void)hipEventDestroy(w->pin_done);
     if (w->err_done) (void)hipEventDestroy(w->err_done);
     if (w->err_pin) (void)hipHostFree(w->err_pin);
+    if (w->err_host) (void)hipHostFree(w->err_host);
     for (int i = 0; i < 2; i++) {
         if (w->mpin_done[i]) (void)hipEventDestroy(w->mpin_done[i]);
         if (w->mpin[i]) (void)hipHostFree(w->mpin[i]);
@@ -1420,7 +1454,7 @@ int nfk_define_kind(void* world, int32_t kind, const nfk_op* ops, int32_t n_ops)
     if (w->committed) return fail(NFK_ERR_STATE, "schema is fixed after commit");
     for (int i = 0; i < n_ops; i++) {
         const nfk_op& op = ops[i];
-        const int np = w->n_prop, ni = w->cfg.n_int;
+        const int np = w->n_if, ni = w->cfg.n_int;  // (object properties are no program operands)
         auto isint = [&](int64_t p) { return p >= 0 && p < ni; };
         auto isflt = [&](int64_t p) { return p >= ni && p < np; };
         switch (op.code) {
@@ -1476,9 +1510,22 @@ int nfk_create_objects(void* world, int32_t n, const int64_t* gh, const int64_t*
 
 int nfk_load_prop(void* world, int32_t pid, const uint64_t* bits) {
     World* w = (World*)world;
-    if (!w || pid < 0 || pid >= w->n_prop || !bits) return fail(NFK_ERR_ARG, "bad property");
+    if (!w || pid < 0 || pid >= w->n_if || !bits) return fail(NFK_ERR_ARG, "bad property (object properties: nfk_load_object)");
     if (w->committed) return fail(NFK_ERR_STATE, "load before commit");
     w->init_props[pid].assign(bits, bits + w->n_obj);
+    return NFK_OK;
+}
+
+int nfk_load_object(void* world, int32_t pid, const int64_t* head, const int64_t* data) {
+    World* w = (World*)world;
+    if (!w || pid < w->n_if || pid >= w->n_prop || !head || !data) return fail(NFK_ERR_ARG, "bad object property");
+    if (w->committed) return fail(NFK_ERR_STATE, "load before commit");
+    std::vector<uint64_t>& v = w->init_props[pid];  // (data, head) per object
+    v.resize((size_t)2 * w->n_obj);
+    for (int32_t o = 0; o < w->n_obj; o++) {
+        v[2 * (size_t)o] = (uint64_t)data[o];
+        v[2 * (size_t)o + 1] = (uint64_t)head[o];
+    }
     return NFK_OK;
 }
 
@@ -1544,7 +1591,7 @@ int nfk_commit(void* world) {
     if (!(ab_layout & kAblGroupColumns)) {
         // plain columns, or groups of properties with the same access signature (the set of
         // (kind, read / write) that touch them): every access covers a group
-        const int NP = w->n_prop;
+        const int NP = w->n_if;
         std::vector<std::vector<int>> sig(NP);
         for (int k = 0; k < NK && (ab_layout & kAblSigGroups); k++)
             for (int i = 0; i < w->tab.nops[k]; i++) {
@@ -1576,7 +1623,7 @@ int nfk_commit(void* world) {
             }
         }
     } else {
-        const int NP = w->n_prop;
+        const int NP = w->n_if;
         constexpr int kGroupMax = 8;
         std::vector<int> par(NP), sz(NP, 1);
         for (int p = 0; p < NP; p++) par[p] = p;
@@ -1637,7 +1684,7 @@ int nfk_commit(void* world) {
         w->obj_of_slot[meta.slot[i]] = meta.obj[i];
         if (meta.obj[i] >= 0) w->slot_of_obj[meta.obj[i]] = meta.slot[i];
     }
-    w->row_words = w->n_prop + 4 * NK;
+    w->row_words = w->n_pw + 4 * NK;
     for (int r = 0; r < NR; r++) w->row_words += w->tab.rec_rows[r] * w->tab.rec_cols[r] + 1;
 
     // device allocation
@@ -1646,6 +1693,9 @@ int nfk_commit(void* world) {
     set_tiles(d, (int32_t)n_slots);
     d.n_int = NI;
     d.n_flt = NF;
+    d.n_if = NI + NF;
+    d.n_obj = w->cfg.n_obj;
+    d.err_host = w->err_host_d;
     d.n_kind = NK;
     d.n_rec = NR;
     d.n_class = w->cfg.n_class;
@@ -1660,7 +1710,7 @@ int nfk_commit(void* world) {
     ALLOC(w->ctrl, sizeof(Ctrl));
     const int64_t cpad = (ab_layout & kAblNoPad) ? 0 : kColPad / 8;  // column pad in values
     d.s_kstr = cap + (int32_t)((ab_layout & kAblNoPad) ? 0 : kColPad / (int64_t)sizeof(SchedHot));
-    ALLOC(d.pmem, ((size_t)cap + cpad) * (size_t)std::max(w->n_prop, 1) * 8);
+    ALLOC(d.pmem, ((size_t)cap + cpad) * (size_t)std::max(w->n_pw, 1) * 8);
     {
         int64_t off = 0;
         for (const auto& g : pgroups) {
@@ -1669,6 +1719,12 @@ int nfk_commit(void* world) {
                 w->tab.p_str[g[i]] = (int32_t)g.size();
             }
             off += (int64_t)g.size() * cap + cpad;
+        }
+        // an object property is one 16-byte column: (data, head) of slot e at p_off + 2e
+        for (int p = w->n_if; p < w->n_prop; p++) {
+            w->tab.p_off[p] = off;
+            w->tab.p_str[p] = 2;
+            off += 2 * (int64_t)cap + cpad;
         }
     }
     set_working_set(w);
@@ -1714,6 +1770,10 @@ int nfk_commit(void* world) {
     ALLOC(d.ev_old, ev_n * 8);
     ALLOC(d.ev_new, ev_n * 8);
     ALLOC(d.ev_moff, ev_n * 4);
+    if (w->cfg.n_obj) {
+        ALLOC(d.ev_old_h, ev_n * 8);
+        ALLOC(d.ev_new_h, ev_n * 8);
+    }
     ALLOC(d.fi_slot, fi_n * 4);
     ALLOC(d.fi_kind, fi_n * 4);
     ALLOC(d.fi_remain, fi_n * 4);
@@ -1761,6 +1821,16 @@ int nfk_commit(void* world) {
                 for (int32_t s = 0; s < d.N; s++)
                     if (w->obj_of_slot[s] >= 0) blk[(size_t)s * gs + i] = w->init_props[g[i]][w->obj_of_slot[s]];
         HIPCHK(hipMemcpy(d.pmem + w->tab.p_off[g[0]], blk.data(), blk.size() * 8, hipMemcpyHostToDevice));
+    }
+    for (int p = w->n_if; p < w->n_prop; p++) {
+        std::vector<uint64_t> blk((size_t)cap * 2, 0);
+        if (!w->init_props[p].empty())
+            for (int32_t s = 0; s < d.N; s++)
+                if (w->obj_of_slot[s] >= 0) {
+                    blk[(size_t)s * 2] = w->init_props[p][(size_t)w->obj_of_slot[s] * 2];
+                    blk[(size_t)s * 2 + 1] = w->init_props[p][(size_t)w->obj_of_slot[s] * 2 + 1];
+                }
+        HIPCHK(hipMemcpy(d.pmem + w->tab.p_off[p], blk.data(), blk.size() * 8, hipMemcpyHostToDevice));
     }
     for (int r = 0; r < NR; r++) {
         size_t per = (size_t)w->tab.rec_rows[r] * w->tab.rec_cols[r];
@@ -1844,13 +1914,36 @@ int nfk_set_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
     w->obj_of.find_many(n, gh, gd, w->look.data());
     for (int32_t i = 0; i < n; i++) {
         const int32_t obj = w->look[i];
-        if (obj < 0 || pid[i] < 0 || pid[i] >= w->n_prop) {
+        if (obj < 0 || pid[i] < 0 || pid[i] >= w->n_if) {
             w->xops.resize(at);
             if (obj < 0)  // NFCKernelModule logs "There is no object" and returns false (KM:331)
                 return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
-            return fail(NFK_ERR_ARG, "bad property id");
+            return fail(NFK_ERR_ARG, pid[i] >= w->n_if && pid[i] < w->n_prop ? "object property: use nfk_set_objects"
+                                                                              : "bad property id");
         }
         x[i] = World::XOp{(uint32_t)obj, (uint32_t)pid[i], bits[i]};
+    }
+    if (w->cfg.n_obj) w->xops_h.resize(w->xops.size(), 0);
+    return NFK_OK;
+}
+
+int nfk_set_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid,
+                    const int64_t* vh, const int64_t* vd) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !pid || !vh || !vd))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    w->look.resize(n);
+    w->obj_of.find_many(n, gh, gd, w->look.data());
+    for (int32_t i = 0; i < n; i++) {
+        if (w->look[i] < 0)  // "There is no object" (KM:370)
+            return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
+        if (pid[i] < w->n_if || pid[i] >= w->n_prop) return fail(NFK_ERR_ARG, "not an object property");
+    }
+    // one queue with the int / f64 Sets: the call order across properties is kept
+    w->xops_h.resize(w->xops.size(), 0);
+    for (int32_t i = 0; i < n; i++) {
+        w->xops.push_back(World::XOp{(uint32_t)w->look[i], (uint32_t)pid[i], (uint64_t)vd[i]});
+        w->xops_h.push_back((uint64_t)vh[i]);
     }
     return NFK_OK;
 }
@@ -1904,7 +1997,7 @@ int nfk_get_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd
         const uint64_t* cell;
         const uint64_t* used;
         if (w->src_row[o] >= 0) {  // entered in this window: its row of the import buffer
-            int64_t off = w->n_prop + 4 * w->cfg.n_kind;
+            int64_t off = w->n_pw + 4 * w->cfg.n_kind;
             for (int x = 0; x < r; x++) off += (int64_t)w->tab.rec_rows[x] * w->tab.rec_cols[x] + 1;
             const uint64_t* base = w->ins_rows + (size_t)w->src_row[o] * w->row_words + off;
             cell = base + (size_t)col[i] * rows + row[i];
@@ -2007,6 +2100,84 @@ int nfk_schedule_calls(void* world, int32_t n, const int32_t* op, const int64_t*
     return NFK_OK;
 }
 
+// The world's values of property words after the last frame (waits for the world's stream): src
+// entries are pmem word offsets, or (1 << 63 | word index in ins_rows) for an object that entered
+// in this window; at most 8 single-element reads, else one gather kernel
+static int read_words(World* w, const std::vector<uint64_t>& src, uint64_t* got) {
+    if (src.empty()) return NFK_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    if (src.size() <= 8) {
+        for (size_t q = 0; q < src.size(); q++) {
+            const uint64_t* a = (src[q] >> 63) ? w->ins_rows + (src[q] & ~(1ull << 63)) : w->d.pmem + src[q];
+            HIPCHK(hipMemcpy(&got[q], a, 8, hipMemcpyDeviceToHost));
+        }
+        return NFK_OK;
+    }
+    int r = dev_reserve(w, (void**)&w->gat, &w->gat_cap, src.size() * 16);
+    if (r) return r;
+    HIPCHK(hipMemcpy(w->gat, src.data(), src.size() * 8, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_gather_words, dim3((unsigned)((src.size() + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream,
+                       (const uint64_t*)w->gat, (int32_t)src.size(), (const uint64_t*)w->d.pmem,
+                       (const uint64_t*)w->ins_rows, w->gat + src.size());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(got, w->gat + src.size(), src.size() * 8, hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    return NFK_OK;
+}
+
+// where property word `half` (0 data, 1 head) of pid of object o is read from (see read_words)
+static int word_src(World* w, int32_t o, int32_t pid, int half, uint64_t* src) {
+    const int32_t sl = w->slot_of_obj[o];
+    if (w->src_row[o] >= 0)  // entered in this window: its row of the import buffer
+        *src = (1ull << 63) | ((uint64_t)w->src_row[o] * w->row_words + (uint64_t)(prop_word(w, pid) + half));
+    else if (sl >= 0)
+        *src = (uint64_t)(w->tab.p_off[pid] + (int64_t)sl * w->tab.p_str[pid] + half);
+    else
+        return fail(NFK_ERR_STATE, "object without a slot");
+    return NFK_OK;
+}
+
+// index the queued Set calls by (object, property) (ov_last / ov_prev chains, call order)
+static void index_queued_sets(World* w) {
+    for (size_t i = w->ov_prev.size(); i < w->xops.size(); i++) {
+        const uint64_t key = ((uint64_t)w->xops[i].slot << 7) | w->xops[i].pid;
+        auto it = w->ov_last.find(key);
+        w->ov_prev.push_back(it == w->ov_last.end() ? 0xFFFFFFFFu : it->second);
+        w->ov_last[key] = (uint32_t)i;
+    }
+}
+
+int nfk_get_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid, int64_t* vh,
+                    int64_t* vd) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !pid || !vh || !vd))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    std::vector<int32_t> obj(n);
+    w->obj_of.find_many(n, gh, gd, obj.data());
+    std::vector<uint64_t> src(2 * (size_t)n), got(2 * (size_t)n);
+    for (int32_t i = 0; i < n; i++) {
+        if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
+        if (pid[i] < w->n_if || pid[i] >= w->n_prop) return fail(NFK_ERR_ARG, "not an object property");
+        for (int h = 0; h < 2; h++) {
+            int r = word_src(w, obj[i], pid[i], h, &src[2 * (size_t)i + h]);
+            if (r) return r;
+        }
+    }
+    int r = read_words(w, src, got.data());
+    if (r) return r;
+    // this window's queued SetObject calls on top: NFCProperty::SetObject keeps the last value
+    index_queued_sets(w);
+    for (int32_t i = 0; i < n; i++) {
+        vd[i] = (int64_t)got[2 * (size_t)i];
+        vh[i] = (int64_t)got[2 * (size_t)i + 1];
+        auto it = w->ov_last.find(((uint64_t)obj[i] << 7) | (uint32_t)pid[i]);
+        if (it == w->ov_last.end()) continue;
+        vd[i] = (int64_t)w->xops[it->second].bits;
+        vh[i] = (int64_t)w->xops_h[it->second];
+    }
+    return NFK_OK;
+}
+
 int nfk_get_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid, uint64_t* bits) {
     World* w = (World*)world;
     if (!w || n < 0 || (n && (!gh || !gd || !pid || !bits))) return fail(NFK_ERR_ARG, "null argument");
@@ -2015,7 +2186,7 @@ int nfk_get_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
     w->obj_of.find_many(n, gh, gd, obj.data());
     for (int32_t i = 0; i < n; i++) {
         if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
-        if (pid[i] < 0 || pid[i] >= w->n_prop) return fail(NFK_ERR_ARG, "bad property id");
+        if (pid[i] < 0 || pid[i] >= w->n_if) return fail(NFK_ERR_ARG, "bad property id (object properties: nfk_get_objects)");
     }
     // 1. the world's values after the last frame (a per-window cache of device reads)
     std::vector<uint64_t> src;
@@ -2027,34 +2198,16 @@ int nfk_get_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
             bits[i] = it->second;
             continue;
         }
-        const int32_t o = obj[i], sl = w->slot_of_obj[o];
-        if (w->src_row[o] >= 0)  // entered in this window: its row of the import buffer
-            src.push_back((1ull << 63) | ((uint64_t)w->src_row[o] * w->row_words + pid[i]));
-        else if (sl >= 0)
-            src.push_back((uint64_t)(w->tab.p_off[pid[i]] + (int64_t)sl * w->tab.p_str[pid[i]]));
-        else
-            return fail(NFK_ERR_STATE, "object without a slot");
+        uint64_t a;
+        int r = word_src(w, obj[i], pid[i], 0, &a);
+        if (r) return r;
+        src.push_back(a);
         miss.push_back(i);
     }
     if (!miss.empty()) {
-        HIPCHK(hipStreamSynchronize(w->stream));
         std::vector<uint64_t> got(miss.size());
-        if (miss.size() <= 8) {
-            for (size_t q = 0; q < miss.size(); q++) {
-                const uint64_t* a = (src[q] >> 63) ? w->ins_rows + (src[q] & ~(1ull << 63)) : w->d.pmem + src[q];
-                HIPCHK(hipMemcpy(&got[q], a, 8, hipMemcpyDeviceToHost));
-            }
-        } else {
-            int r = dev_reserve(w, (void**)&w->gat, &w->gat_cap, miss.size() * 16);
-            if (r) return r;
-            HIPCHK(hipMemcpy(w->gat, src.data(), miss.size() * 8, hipMemcpyHostToDevice));
-            hipLaunchKernelGGL(k_gather_words, dim3((unsigned)((miss.size() + kTPB - 1) / kTPB)), dim3(kTPB), 0,
-                               w->stream, (const uint64_t*)w->gat, (int32_t)miss.size(), (const uint64_t*)w->d.pmem,
-                               (const uint64_t*)w->ins_rows, w->gat + miss.size());
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(got.data(), w->gat + miss.size(), miss.size() * 8, hipMemcpyDeviceToHost, w->stream));
-            HIPCHK(hipStreamSynchronize(w->stream));
-        }
+        int r = read_words(w, src, got.data());
+        if (r) return r;
         for (size_t q = 0; q < miss.size(); q++) {
             const int32_t i = miss[q];
             bits[i] = got[q];
@@ -2062,12 +2215,7 @@ int nfk_get_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
         }
     }
     // 2. this window's queued writes of the property on top, in call order (PR:254 / PR:295)
-    for (size_t i = w->ov_prev.size(); i < w->xops.size(); i++) {
-        const uint64_t key = ((uint64_t)w->xops[i].slot << 7) | w->xops[i].pid;
-        auto it = w->ov_last.find(key);
-        w->ov_prev.push_back(it == w->ov_last.end() ? 0xFFFFFFFFu : it->second);
-        w->ov_last[key] = (uint32_t)i;
-    }
+    index_queued_sets(w);
     std::vector<uint32_t> chain;
     for (int32_t i = 0; i < n; i++) {
         auto it = w->ov_last.find(((uint64_t)obj[i] << 7) | (uint32_t)pid[i]);
@@ -2104,7 +2252,7 @@ int nfk_exist_schedule(void* world, int64_t gh, int64_t gd, int32_t kind, int32_
     uint64_t word = 0;
     HIPCHK(hipStreamSynchronize(w->stream));
     if (w->src_row[o] >= 0) {
-        HIPCHK(hipMemcpy(&word, w->ins_rows + (size_t)w->src_row[o] * w->row_words + w->n_prop + 4 * kind + 1, 8,
+        HIPCHK(hipMemcpy(&word, w->ins_rows + (size_t)w->src_row[o] * w->row_words + w->n_pw + 4 * kind + 1, 8,
                          hipMemcpyDeviceToHost));
     } else if (w->slot_of_obj[o] >= 0) {
         HIPCHK(hipMemcpy(&word, (const char*)(w->d.s_hot + (size_t)kind * w->d.s_kstr + w->slot_of_obj[o]) + 8, 8,
@@ -2143,7 +2291,7 @@ int nfk_set_scene_props(void* world, int32_t pid_scene, int32_t pid_group, int32
     if (!w) return fail(NFK_ERR_ARG, "null world");
     const int NI = w->cfg.n_int;
     auto ok_i = [&](int32_t p) { return p == -1 || (p >= 0 && p < NI); };
-    auto ok_f = [&](int32_t p) { return p == -1 || (p >= NI && p < w->n_prop); };
+    auto ok_f = [&](int32_t p) { return p == -1 || (p >= NI && p < w->n_if); };
     if (!ok_i(pid_scene) || !ok_i(pid_group) || !ok_f(pid_x) || !ok_f(pid_y) || !ok_f(pid_z))
         return fail(NFK_ERR_ARG, "SceneID/GroupID must be int properties, X/Y/Z float properties");
     w->pid_scene = pid_scene;
@@ -2324,7 +2472,7 @@ int nfk_spawn_objects(void* world, int32_t n, const int64_t* gh, const int64_t* 
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first (before it, use nfk_create_objects)");
     std::vector<uint64_t> rows((size_t)std::max(n, 0) * w->row_words, 0);
     for (int32_t i = 0; i < n; i++)
-        memcpy(&rows[(size_t)i * w->row_words], props + (size_t)i * w->n_prop, (size_t)w->n_prop * 8);
+        memcpy(&rows[(size_t)i * w->row_words], props + (size_t)i * w->n_pw, (size_t)w->n_pw * 8);
     return import_common(w, n, gh, gd, scene, group, cls, isplayer, rows.data(), hipMemcpyHostToDevice);
 }
 
@@ -2332,6 +2480,12 @@ int nfk_execute(void* world, int64_t now_ms) {
     World* w = (World*)world;
     if (!w) return fail(NFK_ERR_ARG, "null world");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    // a device error of an earlier frame (host-mapped, no device read): that frame's outputs are
+    // incomplete, so no further frame runs until nfk_summary_get has reported and cleared it
+    if (const unsigned e = *(volatile unsigned*)w->err_host; e & (kErrFanBound | kErrTouch))
+        return fail(NFK_ERR_DEVICE, std::string("device error of an earlier frame: ") +
+                                        ((e & kErrFanBound) ? "a tile's fan-out exceeded its bound" : "touch list overflow") +
+                                        " (nfk_summary_get reports and clears it)");
     using clk = std::chrono::steady_clock;
     const bool trace = getenv("NFGPU_TRACE_EXEC") != nullptr;  // host phases to stderr
     clk::time_point tp[6];
@@ -2346,9 +2500,13 @@ int nfk_execute(void* world, int64_t now_ms) {
         if (r) return r;  // nothing of the window applied; its calls stay queued
         const int rf = check_fanout(w);  // the last frame's fan-out is complete before it is replaced
         r = commit_membership(w, mp);    // (a planned window is applied either way)
-        if (rf) return rf;
-        if (r) return r;
+        if (rf) return drop_window(w, rf);
+        if (r) return drop_window(w, r);
     }
+    // test hook: a failure right after the window's membership changes (tests/test_gpu_parity.py)
+    if (const char* inj = getenv("NFGPU_INJECT_EXEC_FAIL"); inj && inj[0] == '1')
+        return drop_window(w, fail(NFK_ERR_CAPACITY, "injected failure after the membership changes"));
+    if (w->cfg.n_obj) w->xops_h.resize(w->xops.size(), 0);
     Dev d = w->d;
     d.now = now_ms;
 
@@ -2387,7 +2545,7 @@ int nfk_execute(void* world, int64_t now_ms) {
             xpk[k++] = (key << xib) | i;
         }
         xpk.resize(k);
-        if (bits_for(kor) + xib > 64) return fail(NFK_ERR_CAPACITY, "too many queued SetProperty calls");
+        if (bits_for(kor) + xib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued SetProperty calls"));
         radix_sort_packed(xpk, w->xpk_t, xib, bits_for(kor));
         int64_t tile_sa = 0;
         uint32_t cur_tile = 0xFFFFFFFFu;
@@ -2420,14 +2578,11 @@ int nfk_execute(void* world, int64_t now_ms) {
         const int64_t need_ev = (int64_t)kTile * std::max(w->n_dst_union, 1) + max_sa;
         if (need_ev > w->d.ev_tcap) {
             int r = grow_event_tiles(w, need_ev);
-            if (r) {
-                w->xops.clear();
-                w->hops.clear();
-                return r;
-            }
+            if (r) return drop_window(w, r);
             d.ev_tcap = w->d.ev_tcap;
             d.ev_slot = w->d.ev_slot; d.ev_pid = w->d.ev_pid; d.ev_old = w->d.ev_old;
             d.ev_new = w->d.ev_new; d.ev_moff = w->d.ev_moff;
+            d.ev_old_h = w->d.ev_old_h; d.ev_new_h = w->d.ev_new_h;
         }
     }
     // SetRecordInt / SetRecordFloat: (slot, cell) groups, each group's calls in call order (key
@@ -2461,7 +2616,7 @@ int nfk_execute(void* world, int64_t now_ms) {
             rpk[k++] = (key << rib) | i;
         }
         rpk.resize(k);
-        if (bits_for(kor) + rib > 64) return fail(NFK_ERR_CAPACITY, "too many queued SetRecord calls");
+        if (bits_for(kor) + rib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued SetRecord calls"));
         radix_sort_packed(rpk, w->rpk_t, rib, bits_for(kor));
         uint64_t prev = ~0ull;
         uint32_t prev_slot = 0xFFFFFFFFu, cur_rt = 0xFFFFFFFFu;
@@ -2492,12 +2647,7 @@ int nfk_execute(void* world, int64_t now_ms) {
         const int64_t need_re = (int64_t)kRTile * std::max<int64_t>(cells, 1) + max_rs_tile;
         if (need_re > w->d.re_tcap) {
             int r = grow_rec_tiles(w, need_re);
-            if (r) {
-                w->xops.clear();
-                w->hops.clear();
-                w->rsq.clear();
-                return r;
-            }
+            if (r) return drop_window(w, r);
             d.re_tcap = w->d.re_tcap;
             d.re_slot = w->d.re_slot; d.re_rrc = w->d.re_rrc; d.re_old = w->d.re_old;
             d.re_new = w->d.re_new; d.re_moff = w->d.re_moff;
@@ -2537,7 +2687,7 @@ int nfk_execute(void* world, int64_t now_ms) {
             hpk[nh++] = (key << hib) | i;
         }
         hpk.resize(nh);
-        if (bits_for(kor) + hib > 64) return fail(NFK_ERR_CAPACITY, "too many queued schedule calls");
+        if (bits_for(kor) + hib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued schedule calls"));
         radix_sort_packed(hpk, w->hpk_t, hib, bits_for(kor));
         for (size_t a = 0; a < nh;) {
             const uint32_t slot = (uint32_t)((hpk[a] >> hib) >> 5);
@@ -2611,20 +2761,22 @@ int nfk_execute(void* world, int64_t now_ms) {
     size_t off_rs = align16(off_qt + npost * 8), off_rr = align16(off_rs + ngr * 4);
     size_t off_rf = align16(off_rr + ngr * 4), off_rb = align16(off_rf + (ngr + 1) * 4);
     size_t off_ss = align16(off_rb + nrc * 8), off_sg = align16(off_ss + nrss * 4);
-    size_t total = align16(off_sg + nrss * 4);
+    const bool objs = w->cfg.n_obj > 0;
+    size_t off_xh = align16(off_sg + nrss * 4);  // head halves of the calls (object properties)
+    size_t total = align16(off_xh + (objs ? nxc * 8 : 0));
     if (ng) {
-        int r = dev_reserve(w, (void**)&w->xs_buf, &w->xs_cap, ng * 16);
-        if (r) return r;
+        int r = dev_reserve(w, (void**)&w->xs_buf, &w->xs_cap, ng * (objs ? 32 : 16));
+        if (r) return drop_window(w, r);
     }
     if (ngr) {
         int r = dev_reserve(w, (void**)&w->rs_buf, &w->rs_cap, ngr * 16);
-        if (r) return r;
+        if (r) return drop_window(w, r);
         r = dev_reserve(w, (void**)&w->rss_buf, &w->rss_cap, nrss * 16);
-        if (r) return r;
+        if (r) return drop_window(w, r);
     }
     if (total > 0 && (ng || npre || npost || ngr)) {
         int r = pin_reserve(w, total);
-        if (r) return r;
+        if (r) return drop_window(w, r);
         char* P = (char*)w->pin;
         if (ng) {
             memcpy(P + off_xs, g_slot.data(), ng * 4);
@@ -2632,6 +2784,10 @@ int nfk_execute(void* world, int64_t now_ms) {
             memcpy(P + off_xf, g_first.data(), (ng + 1) * 4);
             uint64_t* xb = (uint64_t*)(P + off_xb);
             for (size_t i = 0; i < nxc; i++) xb[i] = w->xops[xpk[i] & xim].bits;
+            if (objs) {
+                uint64_t* xh = (uint64_t*)(P + off_xh);
+                for (size_t i = 0; i < nxc; i++) xh[i] = w->xops_h[xpk[i] & xim];
+            }
         }
         for (size_t i = 0; i < npre; i++) {
             ((uint32_t*)(P + off_ps))[i] = pre_slot[i];
@@ -2667,6 +2823,9 @@ int nfk_execute(void* world, int64_t now_ms) {
     d.x_bits = ng ? (const uint64_t*)(S + off_xb) : nullptr;
     d.x_old = ng ? (uint64_t*)w->xs_buf : nullptr;
     d.x_new = ng ? (uint64_t*)w->xs_buf + ng : nullptr;
+    d.x_bits_h = ng && objs ? (const uint64_t*)(S + off_xh) : nullptr;
+    d.x_old_h = ng && objs ? (uint64_t*)w->xs_buf + 2 * ng : nullptr;
+    d.x_new_h = ng && objs ? (uint64_t*)w->xs_buf + 3 * ng : nullptr;
     d.n_rs = (int32_t)ngr;
     d.n_rss = (int32_t)nrss;
     d.rs_slot = ngr ? (const uint32_t*)(S + off_rs) : nullptr;
@@ -2683,6 +2842,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     d.rss_pmsg = ngr ? (uint32_t*)w->rss_buf + 3 * nrss : nullptr;
     w->rsq.clear();
     w->xops.clear();
+    w->xops_h.clear();
     w->hops.clear();
     w->dcache.clear();
     w->ov_last.clear();
@@ -2724,7 +2884,8 @@ int nfk_execute(void* world, int64_t now_ms) {
     d.fuse_rec = 0;
     d.msg_rb0 = d.msg_rtcap = 0;
     if (use_u && d.n_tiles && !(d.ablate & (kAblNoFuse | kAblNoEmit))) {
-        const int64_t tcap = (((int64_t)std::max(d.n_w, 1) * kTile + max_sa) * std::max(w->max_np, 1) + 3) & ~(int64_t)3;
+        int64_t tcap = (((int64_t)std::max(d.n_w, 1) * kTile + max_sa) * std::max(w->max_np, 1) + 3) & ~(int64_t)3;
+        if (d.ablate & kAblTinyTcap) tcap = 4;  // test hook: a bound every busy tile exceeds (kErrFanBound)
         int64_t rtcap = 0;
         bool rfuse = false;
         if (d.has_recops && d.n_rtiles) {
@@ -2752,7 +2913,7 @@ int nfk_execute(void* world, int64_t now_ms) {
                 int r = regrow(w, (void**)&w->d.msg_rcpt, (size_t)need * 4);
                 if (r) {
                     w->d.msg_cap = 0;
-                    return r;
+                    return drop_window(w, r);
                 }
                 w->d.msg_cap = need;
                 d.msg_rcpt = w->d.msg_rcpt;
@@ -2993,6 +3154,7 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     out->device_error = (int32_t)c.err;
     out->tick = w->ticks;
     if (c.err) HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
+    *(volatile unsigned*)w->err_host = 0;  // (the stream is idle: read_ctrl synchronised it)
     if (c.err & kErrTouch) return fail(NFK_ERR_TOUCH, "device touch list overflow");
     if (c.err & kErrFanBound) return fail(NFK_ERR_STATE, "a tile's fan-out exceeded its bound");
     if (c.err & kErrMsgCap)
@@ -3006,6 +3168,11 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     int r = check_fanout(w);  // (synchronises only after a frame that ran k_fanout)
     if (r) return r;
+    // a device error of a frame that has completed (host-mapped word, no device read); a frame
+    // still running reports through the next call that waits for it (nfk_execute, nfk_summary_get)
+    if (const unsigned e = *(volatile unsigned*)w->err_host; e & (kErrFanBound | kErrTouch))
+        return fail(NFK_ERR_DEVICE, (e & kErrFanBound) ? "a tile's fan-out exceeded its bound: the recipient lists are truncated"
+                                                       : "touch list overflow: events are missing");
     r = ensure_ranks(w);  // (asynchronous, on the world's stream like the frame)
     if (r) return r;
     const Dev& d = w->d;
@@ -3019,12 +3186,32 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     o->fi_slot = d.fi_slot; o->fi_kind = d.fi_kind; o->fi_remain = d.fi_remain;
     o->msg_rcpt = d.msg_rcpt;
     o->slot_obj = w->slot_obj_d;
+    o->ev_old_h = d.ev_old_h;
+    o->ev_new_h = d.ev_new_h;
+    return NFK_OK;
+}
+
+int nfk_read_object(void* world, int32_t pid, int64_t* head, int64_t* data) {
+    World* w = (World*)world;
+    if (!w || !head || !data || pid < w->n_if || pid >= w->n_prop) return fail(NFK_ERR_ARG, "bad argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    HIPCHK(hipStreamSynchronize(w->stream));
+    const Dev& d = w->d;
+    std::vector<uint64_t> col(2 * (size_t)std::max(d.N, 1));
+    if (d.N) HIPCHK(hipMemcpy(col.data(), d.pmem + w->tab.p_off[pid], (size_t)d.N * 16, hipMemcpyDeviceToHost));
+    memset(head, 0, (size_t)w->n_obj * 8);  // objects no longer in this world read the null NFGUID
+    memset(data, 0, (size_t)w->n_obj * 8);
+    for (int32_t s = 0; s < d.N; s++)
+        if (w->obj_of_slot[s] >= 0) {
+            data[w->obj_of_slot[s]] = (int64_t)col[2 * (size_t)s];
+            head[w->obj_of_slot[s]] = (int64_t)col[2 * (size_t)s + 1];
+        }
     return NFK_OK;
 }
 
 int nfk_read_prop(void* world, int32_t pid, uint64_t* bits) {
     World* w = (World*)world;
-    if (!w || !bits || pid < 0 || pid >= w->n_prop) return fail(NFK_ERR_ARG, "bad argument");
+    if (!w || !bits || pid < 0 || pid >= w->n_if) return fail(NFK_ERR_ARG, "bad argument (object properties: nfk_read_object)");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     HIPCHK(hipStreamSynchronize(w->stream));
     const Dev& d = w->d;
@@ -3092,6 +3279,29 @@ int nfk_read_events(void* world, int32_t* ev_obj, int32_t* ev_pid, uint64_t* ev_
     GATHER(w, d.ev_old, d.ev_base, d.n_tiles, d.ev_tcap, n, ev_old);
     GATHER(w, d.ev_new, d.ev_base, d.n_tiles, d.ev_tcap, n, ev_new);
     for (size_t i = 0; i < n; i++) ev_obj[i] = w->obj_of_slot[sl[i]];
+    return NFK_OK;
+}
+
+int nfk_read_events_obj(void* world, uint64_t* ev_old_h, uint64_t* ev_new_h) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    Ctrl c;
+    int r = read_ctrl(w, &c);
+    if (r) return r;
+    const Dev& d = w->d;
+    const size_t n = c.n_ev;
+    if (!d.n_obj) {
+        memset(ev_old_h, 0, n * 8);
+        memset(ev_new_h, 0, n * 8);
+        return NFK_OK;
+    }
+    std::vector<uint32_t> pid(n);
+    GATHER(w, d.ev_pid, d.ev_base, d.n_tiles, d.ev_tcap, n, pid.data());
+    GATHER(w, d.ev_old_h, d.ev_base, d.n_tiles, d.ev_tcap, n, ev_old_h);
+    GATHER(w, d.ev_new_h, d.ev_base, d.n_tiles, d.ev_tcap, n, ev_new_h);
+    for (size_t i = 0; i < n; i++)
+        if ((int)pid[i] < d.n_if) ev_old_h[i] = ev_new_h[i] = 0;  // (unwritten for other events)
     return NFK_OK;
 }
 
@@ -3183,7 +3393,7 @@ int nfk_rank_top(void* world, int32_t pid, int32_t k, int32_t* n_out, int64_t* g
     World* w = (World*)world;
     if (!w || !n_out || (k > 0 && (!guid_head || !guid_data || !score))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
-    if (pid < 0 || pid >= w->n_prop || k < 0) return fail(NFK_ERR_ARG, "bad property / k");
+    if (pid < 0 || pid >= w->n_if || k < 0) return fail(NFK_ERR_ARG, "bad property / k (int or float properties rank)");
     *n_out = 0;
     const Dev& d = w->d;
     if (k == 0 || d.N == 0) return NFK_OK;

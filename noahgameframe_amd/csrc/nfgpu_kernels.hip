@@ -44,6 +44,26 @@ __global__ __launch_bounds__(kTPB) void k_sets(Dev d) {
     const uint64_t start = *p;
     uint64_t cur = start;
     const uint32_t i1 = d.x_first[g + 1];
+    if ((int)pid >= d.n_if) {
+        // NFCProperty::SetObject (PR:377-416): the NFGUID changes when either half differs; the
+        // column holds (data, head) side by side
+        const uint64_t start_h = p[1];
+        uint64_t cur_h = start_h;
+        for (uint32_t i = d.x_first[g]; i < i1; i++) {
+            const uint64_t b = d.x_bits[i], bh = d.x_bits_h[i];
+            cur = b;
+            cur_h = bh;
+        }
+        if (cur != start || cur_h != start_h) {
+            p[0] = cur;
+            p[1] = cur_h;
+        }
+        d.x_old[g] = start;
+        d.x_new[g] = cur;
+        d.x_old_h[g] = start_h;
+        d.x_new_h[g] = cur_h;
+        return;
+    }
     const bool isint = (int)pid < d.n_int;
     for (uint32_t i = d.x_first[g]; i < i1; i++) {
         const uint64_t b = d.x_bits[i];
@@ -247,7 +267,7 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
     __shared__ uint64_t s_old[NFK_MAX_TOUCH * kTPB];
-    __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
+    __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][kMaxProps];
     const int tile = blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
     uint64_t desc = kDeadDesc;
@@ -259,7 +279,7 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
     const bool live = !desc_dead(desc);
     if (threadIdx.x == 0) s_bytes = 0;
     {
-        const int words = d.n_class * (NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS) / 4;
+        const int words = d.n_class * kMaxProps / 4;
         for (int i = threadIdx.x; i < words; i += kTPB)
             ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
     }
@@ -320,7 +340,7 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
             en.bytes += 8;
         }
     const unsigned nf = __builtin_popcount(fired);
-    if (en.ovf) atomicOr(&d.ctrl->err, kErrTouch);
+    if (en.ovf) dev_error(d, kErrTouch);
 
     // 5. tile-local compaction: one block scan of (fired:16 | events:16 | messages:32)
     unsigned long long tot;
@@ -358,6 +378,11 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
                 best = d.x_pid[g];
                 ov = d.x_old[g];
                 nv = d.x_new[g];
+                if ((int)best >= d.n_if) {  // an object property: its head halves beside
+                    d.ev_old_h[ev0 + pev] = d.x_old_h[g];
+                    d.ev_new_h[ev0 + pev] = d.x_new_h[g];
+                    en.bytes += 16;
+                }
                 g = next_standalone(d, g + 1, e);
             } else {
 #pragma unroll
@@ -945,7 +970,7 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
         if (a == 2) d.ctrl->n_re = carry;
         if (a == 3) {
             d.ctrl->msg_extent = carry;
-            if (carry > (unsigned long long)d.msg_cap) atomicOr(&d.ctrl->err, kErrMsgCap);
+            if (carry > (unsigned long long)d.msg_cap) dev_error(d, kErrMsgCap);
         }
     }
     if (a == 3) {  // sum of the fixed-stride tiles' messages
@@ -982,7 +1007,7 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
     __shared__ uint32_t s_ev[3 * kTPB * kFanPer];       // a pass's event triples
     __shared__ uint32_t s_pb[3], s_m[2];                // player run [lo, hi), largest count
     __shared__ unsigned s_bytes;
-    __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS];
+    __shared__ uint8_t s_pflags[NFK_MAX_CLASSES][kMaxProps];
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
     if (d.ctrl->msg_extent > (unsigned long long)d.msg_cap) return;  // uniform: host re-runs
     const int tg = (int)blockIdx.x + blk0;  // tile: property tiles, then record tiles
@@ -1015,7 +1040,7 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
         for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
             ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
     } else {
-        const int words = d.n_class * (NFK_MAX_INT_PROPS + NFK_MAX_FLT_PROPS) / 4;
+        const int words = d.n_class * kMaxProps / 4;
         for (int i = threadIdx.x; i < words; i += kTPB)
             ((uint32_t*)s_pflags)[i] = ((const uint32_t*)d.tab->pflags)[i];
     }
@@ -1134,8 +1159,10 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
 // membership metadata of the scene-group segments that changed.  Thread t handles word
 // t / n of row t % n, so a wave reads one column across consecutive slots.
 __device__ __forceinline__ uint64_t* row_word(const Dev& d, int32_t s, int w) {
-    if (w < d.n_int + d.n_flt) return prop_ptr(d, (uint32_t)w, s);
-    w -= d.n_int + d.n_flt;
+    if (w < d.n_if) return prop_ptr(d, (uint32_t)w, s);
+    w -= d.n_if;
+    if (w < 2 * d.n_obj) return prop_ptr(d, (uint32_t)(d.n_if + (w >> 1)), s) + (w & 1);  // (data, head)
+    w -= 2 * d.n_obj;
     if (w < 4 * d.n_kind) {
         const int k = w >> 2, q = w & 3;
         return q < 2 ? (uint64_t*)&d.s_hot[(size_t)k * d.s_kstr + s] + q

@@ -12,7 +12,9 @@ namespace nfgpu {
 // no program writes, whose value changed over the frame (x_old != x_new).  Returns n_x when none.
 __device__ __forceinline__ int next_standalone(const Dev& d, int g, int e) {
     for (; g < d.n_x && d.x_slot[g] == (uint32_t)e; g++)
-        if (d.tab->w_slot[d.x_pid[g]] == kNoU && d.x_old[g] != d.x_new[g]) return g;
+        if (d.tab->w_slot[d.x_pid[g]] == kNoU &&
+            (d.x_old[g] != d.x_new[g] || ((int)d.x_pid[g] >= d.n_if && d.x_old_h[g] != d.x_new_h[g])))
+            return g;
     return d.n_x;
 }
 // recipients of a property event (GetBroadCastObject, AOI:531-593) of slot e's class
@@ -470,6 +472,11 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     } else {  // (k_sets wrote the column)
                         ov = d.x_old[g];
                         nv = d.x_new[g];
+                        if ((int)pid >= d.n_if) {  // an object property: its head halves beside
+                            st_off(d.ev_old_h + ev0, pev0 + at, d.x_old_h[g]);
+                            st_off(d.ev_new_h + ev0, pev0 + at, d.x_new_h[g]);
+                            bytes += 16;
+                        }
                     }
                     st_off(t_evs, pev0 + at, (uint32_t)e);
                     st_off(t_evp, pev0 + at, pid);
@@ -515,7 +522,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         const unsigned mb = (unsigned)tile * d.msg_tcap;
         const unsigned tev = (unsigned)((tot >> 32) & 0xFFFF);
         const bool fan = tmsg && tmsg <= d.msg_tcap;
-        if (tmsg > d.msg_tcap && threadIdx.x == 0) atomicOr(&d.ctrl->err, kErrFanBound);  // (host bound)
+        if (tmsg > d.msg_tcap && threadIdx.x == 0) dev_error(d, kErrFanBound);  // (host bound)
         if (!fan) {  // ev_moff only
             if (nsd) {
                 walk([&](unsigned at, unsigned m, uint32_t, int, int, EvFan) { st_off(t_evm, pev0 + at, mb + pmsg0 + m); });

@@ -32,7 +32,8 @@ void NFGPUKernelModule::check(int rc, const char* what) const {
 
 int NFGPUKernelModule::AddProperty(const std::string& name, TDATA_TYPE type) {
     if (committed_) throw std::runtime_error("AddProperty after AfterInit");
-    if (type != TDATA_INT && type != TDATA_FLOAT) throw std::runtime_error("frame-path properties are int or float");
+    if (type != TDATA_INT && type != TDATA_FLOAT && type != TDATA_OBJECT)
+        throw std::runtime_error("frame-path properties are int, float or object");
     auto it = prop_id_.find(name);
     if (it != prop_id_.end()) return it->second;
     props_.push_back({name, type});
@@ -71,19 +72,28 @@ void NFGPUKernelModule::AddHeartBeatProgram(const std::string& name, const std::
     heartbeats_.push_back({name, ops});
 }
 
-// property ids on the device: int properties first, then float ones, each in definition order
+// property ids on the device: int properties first, then float ones, then object ones, each in
+// definition order
 int NFGPUKernelModule::PropertyId(const std::string& name) const {
-    int pid = prop_id_.at(name);
-    int n_int = 0, before_int = 0, before_flt = 0;
+    const int pid = prop_id_.at(name);
+    int n[3] = {0, 0, 0}, before = 0;
+    const int t = props_[pid].type == TDATA_INT ? 0 : props_[pid].type == TDATA_FLOAT ? 1 : 2;
     for (int i = 0; i < (int)props_.size(); i++) {
-        if (props_[i].type == TDATA_INT) {
-            n_int++;
-            if (i < pid) before_int++;
-        } else if (i < pid) {
-            before_flt++;
-        }
+        const int ti = props_[i].type == TDATA_INT ? 0 : props_[i].type == TDATA_FLOAT ? 1 : 2;
+        n[ti]++;
+        if (ti == t && i < pid) before++;
     }
-    return props_[pid].type == TDATA_INT ? before_int : n_int + before_flt;
+    return (t >= 1 ? n[0] : 0) + (t == 2 ? n[1] : 0) + before;
+}
+
+// a property's value as its row words (int / f64 bits: one; NFGUID: data then head)
+static void put_words(std::vector<uint64_t>& row, int at, TDATA_TYPE type, const TData& v) {
+    if (type == TDATA_INT) row[at] = (uint64_t)v.GetInt();
+    else if (type == TDATA_FLOAT) row[at] = bits_of(v.GetFloat());
+    else {
+        row[at] = (uint64_t)v.GetObject().nData64;
+        row[at + 1] = (uint64_t)v.GetObject().nHead64;
+    }
 }
 
 bool NFGPUKernelModule::Init() { return true; }
@@ -102,11 +112,12 @@ bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGrou
         if (obj_of_.count(self)) return false;  // "The object has Exists" (KM:131)
         auto c = class_id_.find(cls);
         if (c == class_id_.end()) return false;
-        std::vector<uint64_t> row(props_.size(), 0);
+        int n_if = 0;
+        for (auto& p : props_) n_if += p.type != TDATA_OBJECT;
+        std::vector<uint64_t> row(props_.size() * 2, 0);  // property words (nfk_spawn_objects)
         for (auto& kv : init) {
-            int p = prop_id_.at(kv.first);
-            row[PropertyId(kv.first)] =
-                props_[p].type == TDATA_INT ? (uint64_t)kv.second.GetInt() : bits_of(kv.second.GetFloat());
+            const int p = prop_id_.at(kv.first), id = PropertyId(kv.first);
+            put_words(row, id < n_if ? id : n_if + 2 * (id - n_if), props_[p].type, kv.second);
         }
         for (const char* nm : {"SceneID", "GroupID"}) {  // CreateObject sets them (KM:248-249)
             auto it = prop_id_.find(nm);
@@ -136,27 +147,29 @@ bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGrou
     cls_.push_back((uint8_t)c->second);
     isplayer_.push_back(cls == "Player");  // NFCKernelModule.cpp:146
     if (init_.size() < props_.size()) init_.resize(props_.size());
-    for (auto& v : init_) v.push_back(0);
+    for (size_t p = 0; p < init_.size(); p++) init_[p].resize(init_[p].size() + (props_[p].type == TDATA_OBJECT ? 2 : 1), 0);
     for (auto& kv : init) {
-        int p = prop_id_.at(kv.first);
-        init_[p].back() = props_[p].type == TDATA_INT ? (uint64_t)kv.second.GetInt() : bits_of(kv.second.GetFloat());
+        const int p = prop_id_.at(kv.first);
+        std::vector<uint64_t>& v = init_[p];
+        put_words(v, (int)v.size() - (props_[p].type == TDATA_OBJECT ? 2 : 1), props_[p].type, kv.second);
     }
     return true;
 }
 
 bool NFGPUKernelModule::AfterInit() {
-    int n_int = 0, n_flt = 0;
-    for (auto& p : props_) (p.type == TDATA_INT ? n_int : n_flt)++;
+    int n_int = 0, n_flt = 0, n_obj = 0;
+    for (auto& p : props_) (p.type == TDATA_INT ? n_int : p.type == TDATA_FLOAT ? n_flt : n_obj)++;
     nfk_config cfg{};
     cfg.capacity = std::max(capacity_, 1);
     cfg.n_int = n_int;
     cfg.n_flt = n_flt;
+    cfg.n_obj = n_obj;
     cfg.n_class = (int)classes_.size();
     cfg.n_kind = (int)heartbeats_.size();
     cfg.n_rec = (int)records_.size();
     cfg.stream = stream_;
     check(nfk_create(&cfg, &world_), "nfk_create");
-    const int np = n_int + n_flt;
+    const int np = n_int + n_flt + n_obj;
     for (int c = 0; c < (int)classes_.size(); c++) {
         std::vector<uint8_t> fl(np, 0);
         for (auto& kv : classes_[c].prop_flags) fl[PropertyId(kv.first)] = kv.second;
@@ -189,9 +202,19 @@ bool NFGPUKernelModule::AfterInit() {
     check(nfk_create_objects(world_, n, gh.data(), gd.data(), scene_.data(), group_.data(), cls_.data(),
                              isplayer_.data()),
           "nfk_create_objects");
-    for (int p = 0; p < (int)props_.size(); p++)
-        if (p < (int)init_.size() && !init_[p].empty())
+    for (int p = 0; p < (int)props_.size(); p++) {
+        if (p >= (int)init_.size() || init_[p].empty()) continue;
+        if (props_[p].type != TDATA_OBJECT) {
             check(nfk_load_prop(world_, PropertyId(props_[p].name), init_[p].data()), "nfk_load_prop");
+            continue;
+        }
+        std::vector<int64_t> h(n), d(n);  // init_ holds (data, head) per object
+        for (int i = 0; i < n; i++) {
+            d[i] = (int64_t)init_[p][2 * (size_t)i];
+            h[i] = (int64_t)init_[p][2 * (size_t)i + 1];
+        }
+        check(nfk_load_object(world_, PropertyId(props_[p].name), h.data(), d.data()), "nfk_load_object");
+    }
     check(nfk_commit(world_), "nfk_commit");
     {
         auto pid_of = [&](const char* nm, TDATA_TYPE t) {
@@ -349,6 +372,26 @@ double NFGPUKernelModule::GetPropertyFloat(const NFGUID& self, const std::string
     return dbl_of(b);
 }
 
+bool NFGPUKernelModule::SetPropertyObject(const NFGUID& self, const std::string& name, const NFGUID& v) {
+    auto it = prop_id_.find(name);
+    if (it == prop_id_.end() || props_[it->second].type != TDATA_OBJECT || ObjectIndex(self) < 0) return false;
+    const int32_t pid = PropertyId(name);
+    if (nfk_set_objects(world_, 1, &self.nHead64, &self.nData64, &pid, &v.nHead64, &v.nData64) != NFK_OK) return false;
+    pending_calls_++;
+    return true;
+}
+
+// NFCKernelModule::GetPropertyObject (KM:440): NULL_OBJECT for an unknown object or property
+NFGUID NFGPUKernelModule::GetPropertyObject(const NFGUID& self, const std::string& name) {
+    auto it = prop_id_.find(name);
+    if (!committed_ || ObjectIndex(self) < 0 || it == prop_id_.end() || props_[it->second].type != TDATA_OBJECT)
+        return NFGUID();
+    const int32_t pid = PropertyId(name);
+    NFGUID v;
+    check(nfk_get_objects(world_, 1, &self.nHead64, &self.nData64, &pid, &v.nHead64, &v.nData64), "nfk_get_objects");
+    return v;
+}
+
 bool NFGPUKernelModule::RegisterCommonPropertyEvent(const PROPERTY_EVENT_FUNCTOR& cb) {
     common_prop_cb_.push_back(cb);
     return true;
@@ -480,8 +523,15 @@ void NFGPUKernelModule::TakeAddedSchedules() {
 void NFGPUKernelModule::DeliverEvents() {
     const int64_t ne = summary_.n_prop_events, nr = summary_.n_rec_events;
     std::vector<int32_t> eo(ne), ep(ne);
-    std::vector<uint64_t> eold(ne), enew(ne);
+    std::vector<uint64_t> eold(ne), enew(ne), eoh, enh;
     check(nfk_read_events(world_, eo.data(), ep.data(), eold.data(), enew.data()), "nfk_read_events");
+    bool has_obj = false;
+    for (auto& p : props_) has_obj |= p.type == TDATA_OBJECT;
+    if (has_obj) {
+        eoh.resize(ne);
+        enh.resize(ne);
+        check(nfk_read_events_obj(world_, eoh.data(), enh.data()), "nfk_read_events_obj");
+    }
     std::vector<int32_t> ro(nr);
     std::vector<uint32_t> rrc(nr);
     std::vector<uint64_t> rold(nr), rnew(nr);
@@ -500,9 +550,12 @@ void NFGPUKernelModule::DeliverEvents() {
         if (pd.type == TDATA_INT) {
             a.i = (int64_t)eold[e];
             b.i = (int64_t)enew[e];
-        } else {
+        } else if (pd.type == TDATA_FLOAT) {
             a.f = dbl_of(eold[e]);
             b.f = dbl_of(enew[e]);
+        } else {
+            a.o = NFGUID((int64_t)eoh[e], (int64_t)eold[e]);
+            b.o = NFGUID((int64_t)enh[e], (int64_t)enew[e]);
         }
         const NFGUID& self = guids_[eo[e]];
         for (auto& cb : common_prop_cb_) cb(self, pd.name, a, b);

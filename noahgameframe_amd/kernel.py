@@ -32,7 +32,8 @@ class NFKError(RuntimeError):
 class Config(ctypes.Structure):
     _fields_ = [("capacity", ctypes.c_int32), ("n_int", ctypes.c_int32), ("n_flt", ctypes.c_int32),
                 ("n_class", ctypes.c_int32), ("n_kind", ctypes.c_int32), ("n_rec", ctypes.c_int32),
-                ("msg_capacity", ctypes.c_int64), ("stream", ctypes.c_void_p), ("slack_per_256", ctypes.c_int32)]
+                ("msg_capacity", ctypes.c_int64), ("stream", ctypes.c_void_p), ("slack_per_256", ctypes.c_int32),
+                ("n_obj", ctypes.c_int32)]
 
 
 class Summary(ctypes.Structure):
@@ -50,7 +51,7 @@ class Outputs(ctypes.Structure):
                 [(n, ctypes.c_void_p) for n in
                  ["ev_base", "fi_base", "re_base", "msg_base", "msg_cnt", "ev_slot", "ev_pid", "ev_old", "ev_new", "ev_moff",
                   "re_slot", "re_rrc", "re_old", "re_new", "re_moff", "fi_slot", "fi_kind", "fi_remain",
-                  "msg_rcpt", "slot_obj"]])
+                  "msg_rcpt", "slot_obj", "ev_old_h", "ev_new_h"]])
 
 
 N_KERNEL_TIMERS = 6
@@ -95,6 +96,9 @@ def load_library(path=LIB_PATH):
         "nfk_rank_top": [VP, I32, I32, VP, VP, VP, VP],
         "nfk_jit_status": [VP, VP, VP, I32], "nfk_membership_stats": [VP, VP, VP, VP, VP],
         "nfk_jit_preview": [I32, I32, I32, I32, VP, VP, VP, I32, VP, VP, I32, VP, I32],
+        "nfk_load_object": [VP, I32, VP, VP], "nfk_set_objects": [VP, I32, VP, VP, VP, VP, VP],
+        "nfk_get_objects": [VP, I32, VP, VP, VP, VP, VP], "nfk_read_object": [VP, I32, VP, VP],
+        "nfk_read_events_obj": [VP, VP, VP],
     }
     for name, args in sig.items():
         if not hasattr(lib, name) and os.environ.get("NFGPU_LIB"):
@@ -114,9 +118,10 @@ class NFKernelModule:
     """One GPU-resident world (the entities of one scene shard)."""
 
     def __init__(self, capacity, n_int=wl.N_INT, n_flt=wl.N_FLT, n_class=2, n_kind=len(wl.KINDS), n_rec=0,
-                 msg_capacity=0, stream=None, slack_per_256=0):
+                 msg_capacity=0, stream=None, slack_per_256=0, n_oprops=0):
         self.lib = load_library()
-        cfg = Config(capacity, n_int, n_flt, n_class, n_kind, n_rec, msg_capacity, stream, slack_per_256)
+        cfg = Config(capacity, n_int, n_flt, n_class, n_kind, n_rec, msg_capacity, stream, slack_per_256, n_oprops)
+        self.n_oprops = n_oprops
         h = ctypes.c_void_p()
         self._chk(self.lib.nfk_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -172,6 +177,11 @@ class NFKernelModule:
         bits = v.view(np.uint64) if v.dtype.itemsize == 8 else v.astype(np.int64).view(np.uint64)
         self._chk(self.lib.nfk_load_prop(self.h, pid, _p(np.ascontiguousarray(bits))))
 
+    def load_object(self, pid, head, data):
+        h = np.ascontiguousarray(head, np.int64)
+        d = np.ascontiguousarray(data, np.int64)
+        self._chk(self.lib.nfk_load_object(self.h, pid, _p(h), _p(d)))
+
     def load_record(self, rec, cells, used):
         c = np.ascontiguousarray(cells, np.uint64)
         u = np.ascontiguousarray(used, np.uint64)
@@ -185,6 +195,34 @@ class NFKernelModule:
         a = [np.ascontiguousarray(x, t) for x, t in
              ((guid_head, np.int64), (guid_data, np.int64), (pid, np.int32), (bits, np.uint64))]
         self._chk(self.lib.nfk_set_props(self.h, len(a[0]), *[_p(x) for x in a]))
+
+    # ---- NFIKernelModule::SetPropertyObject / GetPropertyObject (KM:362 / KM:440) ----
+    def set_objects(self, guid_head, guid_data, pid, val_head, val_data):
+        a = [np.ascontiguousarray(x, t) for x, t in
+             ((guid_head, np.int64), (guid_data, np.int64), (pid, np.int32), (val_head, np.int64),
+              (val_data, np.int64))]
+        self._chk(self.lib.nfk_set_objects(self.h, len(a[0]), *[_p(x) for x in a]))
+
+    def get_objects(self, guid_head, guid_data, pid):
+        a = [np.ascontiguousarray(x, t) for x, t in ((guid_head, np.int64), (guid_data, np.int64), (pid, np.int32))]
+        vh = np.zeros(len(a[0]), np.int64)
+        vd = np.zeros(len(a[0]), np.int64)
+        self._chk(self.lib.nfk_get_objects(self.h, len(a[0]), *[_p(x) for x in a], _p(vh), _p(vd)))
+        return vh, vd
+
+    def SetPropertyObject(self, guid, pid, value):
+        self.set_objects([guid[0]], [guid[1]], [pid], [value[0]], [value[1]])
+        return True
+
+    def GetPropertyObject(self, guid, pid):
+        vh, vd = self.get_objects([guid[0]], [guid[1]], [pid])
+        return int(vh[0]), int(vd[0])
+
+    def read_object(self, pid):
+        h = np.zeros(self.n_obj, np.int64)
+        d = np.zeros(self.n_obj, np.int64)
+        self._chk(self.lib.nfk_read_object(self.h, pid, _p(h), _p(d)))
+        return h, d
 
     # ---- NFIKernelModule::SetRecordInt / SetRecordFloat ----
     def set_records(self, guid_head, guid_data, rec, row, col, bits, is_float=None):
@@ -405,9 +443,14 @@ class NFKernelModule:
         mo = np.zeros(ne + nr + 1, np.uint32)
         mr = np.zeros(nm, np.int32)
         self._chk(self.lib.nfk_read_fanout(self.h, _p(mo), _p(mr)))
-        return dict(ev_obj=ev[0], ev_pid=ev[1], ev_old=ev[2], ev_new=ev[3],
-                    re_obj=re[0], re_rrc=re[1], re_old=re[2], re_new=re[3],
-                    fi_obj=fi[0], fi_kind=fi[1], fi_rem=fi[2], mo_off=mo, mr_obj=mr, summary=s)
+        out = dict(ev_obj=ev[0], ev_pid=ev[1], ev_old=ev[2], ev_new=ev[3],
+                   re_obj=re[0], re_rrc=re[1], re_old=re[2], re_new=re[3],
+                   fi_obj=fi[0], fi_kind=fi[1], fi_rem=fi[2], mo_off=mo, mr_obj=mr, summary=s)
+        if self.n_oprops:
+            oh = [np.zeros(ne, np.uint64), np.zeros(ne, np.uint64)]
+            self._chk(self.lib.nfk_read_events_obj(self.h, *[_p(x) for x in oh]))
+            out["ev_oldh"], out["ev_newh"] = oh
+        return out
 
     # ---- measurement ----
     def set_profiling(self, on):
@@ -448,7 +491,9 @@ def world_from_workload(w, capacity=None, msg_capacity=0, stream=None, slack_per
     kinds, objects, creation-time values, then the AddSchedule calls made before frame 0."""
     cfg = w["cfg"]
     n_obj, n_int, n_flt, n_cls, n_kind, n_rec = (int(x) for x in cfg[:6])
-    m = NFKernelModule(capacity or n_obj, n_int, n_flt, n_cls, n_kind, n_rec, msg_capacity, stream, slack_per_256)
+    n_op = int(w["n_oprops"][0]) if "n_oprops" in w else 0
+    m = NFKernelModule(capacity or n_obj, n_int, n_flt, n_cls, n_kind, n_rec, msg_capacity, stream, slack_per_256,
+                       n_op)
     if "scene_props" in w:
         m.set_scene_props(*(int(x) for x in w["scene_props"]))
     m.cur_scene = np.array(w["scene"], np.int32)   # membership as SwitchScene calls change it
@@ -469,6 +514,8 @@ def world_from_workload(w, capacity=None, msg_capacity=0, stream=None, slack_per
         m.load_prop(p, w["init_i"][p][:n0])
     for p in range(n_flt):
         m.load_prop(n_int + p, w["init_f"][p][:n0])
+    for p in range(n_op):
+        m.load_object(n_int + n_flt + p, w["init_oh"][p][:n0], w["init_od"][p][:n0])
     for r in range(n_rec):
         m.load_record(r, w[f"rec{r}_cells"][:n0], w[f"rec{r}_used"][:n0])
     m.commit()
@@ -486,8 +533,13 @@ def run_workload(m, w, tick, collect=True):
     if "born" in w:
         new = np.nonzero(w["born"] == tick)[0]
         if len(new):
-            props = np.concatenate([w["init_i"][:, new].astype(np.int64).view(np.uint64),
-                                    w["init_f"][:, new].astype(np.float64).view(np.uint64)]).T
+            parts = [w["init_i"][:, new].astype(np.int64).view(np.uint64),
+                     w["init_f"][:, new].astype(np.float64).view(np.uint64)]
+            if m.n_oprops:   # each object property as (data, head)
+                od = w["init_od"][:, new].astype(np.int64).view(np.uint64)
+                oh = w["init_oh"][:, new].astype(np.int64).view(np.uint64)
+                parts.append(np.stack([od, oh], 1).reshape(-1, len(new)))
+            props = np.concatenate(parts).T
             m.spawn_objects(gh[new], gd[new], w["scene"][new], w["group"][new], w["cls"][new], w["is_player"][new],
                             np.ascontiguousarray(props))
     if "sw_tick" in w:
@@ -513,7 +565,14 @@ def run_workload(m, w, tick, collect=True):
             sel = xsel[a:b]
             xo = w["x_obj"][sel]
             if mode[a] == 0:
-                m.set_props(gh[xo], gd[xo], w["x_pid"][sel], w["x_bits"][sel])
+                pid = w["x_pid"][sel]
+                isobj = pid >= m.n_int + m.n_flt
+                # (calls on different properties never interact: the object calls go as their own batch)
+                if (~isobj).any():
+                    m.set_props(gh[xo[~isobj]], gd[xo[~isobj]], pid[~isobj], w["x_bits"][sel][~isobj])
+                if isobj.any():
+                    m.set_objects(gh[xo[isobj]], gd[xo[isobj]], pid[isobj], w["x_bits_h"][sel][isobj].view(np.int64),
+                                  w["x_bits"][sel][isobj].view(np.int64))
                 continue
             for i in sel:
                 o, p = int(w["x_obj"][i]), int(w["x_pid"][i])

@@ -25,6 +25,10 @@ PROPS = INT_PROPS + FLT_PROPS
 PID = {n: i for i, n in enumerate(PROPS)}
 N_INT, N_FLT = len(INT_PROPS), len(FLT_PROPS)
 
+# object (NFGUID) properties, TDATA_OBJECT (NFIDataList.h): prop ids after the int and float ones
+# (a world has them with make_world(obj_props=True))
+OBJ_PROPS = ["LastAttacker", "MasterID", "TargetID"]
+
 PUBLIC, PRIVATE, UPLOAD = 1, 2, 4
 CLS_NPC, CLS_PLAYER = 0, 1
 
@@ -49,8 +53,8 @@ def f64bits(x):
     return struct.unpack("<q", struct.pack("<d", float(x)))[0]
 
 
-def _prop_flags():
-    f = np.zeros((2, len(PROPS)), np.uint8)
+def _prop_flags(n_oprops=0):
+    f = np.zeros((2, len(PROPS) + n_oprops), np.uint8)
     pubpriv = PUBLIC | PRIVATE
     for c in (CLS_NPC, CLS_PLAYER):
         for n in ["HP", "MAXHP", "HPREGEN", "MP", "MAXMP", "MPREGEN", "SP", "MAXSP", "SPREGEN",
@@ -64,6 +68,12 @@ def _prop_flags():
         f[c, PID["SceneID"]] = PRIVATE
         f[c, PID["GroupID"]] = PRIVATE
     # NPCType, TargetX, TargetY, AtkDis: Public=0 Private=0 (no sync)
+    if n_oprops:  # LastAttacker public, MasterID private, TargetID private & upload (to nobody)
+        base = len(PROPS)
+        for c in (CLS_NPC, CLS_PLAYER):
+            f[c, base + 0] = PUBLIC | PRIVATE
+            f[c, base + 1] = PRIVATE
+            f[c, base + 2] = PRIVATE | UPLOAD
     return f
 
 
@@ -107,7 +117,7 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
                t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, rec_skill_op=False, sched_edges=False,
                switch_frac=0.0, switch_new_groups=False, rec_steady=False, ext_props=None, burst_frac=0.0,
                burst_props=20, rmw_frac=0.0, spawn_frac=0.0, destroy_frac=0.0, rec_set_frac=0.0,
-               rec_set_float=True):
+               rec_set_float=True, obj_props=False, obj_set_frac=0.05, rec_row_frac=0.0):
     if spawn_frac > 0 or destroy_frac > 0:
         return _lifecycle_world(locals())
     rng = np.random.default_rng(seed)
@@ -294,6 +304,10 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
     cat = lambda lst, dt: np.concatenate(lst).astype(dt) if lst else np.zeros(0, dt)
     x_tick, x_obj, x_pid, x_bits = cat(xt, np.int32), cat(xo, np.int32), cat(xp, np.int32), cat(xb, np.uint64)
     x_mode = cat(xm, np.uint8)
+    obj_extra = {}
+    if obj_props:
+        obj_extra, (x_tick, x_obj, x_pid, x_bits, x_mode) = _object_props(
+            rng, n_obj, n_ticks, ghead, gdata, obj_set_frac, x_tick, x_obj, x_pid, x_bits, x_mode)
 
     # ---- AddSchedule / RemoveSchedule calls between frames ----
     ht, hop, hob, hk, hiv, hc, htm = [], [], [], [], [], [], []
@@ -349,9 +363,10 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
 
     n_rec = 1 if records else 0
     extra = {"x_mode": x_mode} if rmw_frac > 0 else {}
-    w = dict(**extra,
+    n_op = len(OBJ_PROPS) if obj_props else 0
+    w = dict(**extra, **obj_extra,
         cfg=np.array([n_obj, N_INT, N_FLT, 2, n_kind, n_rec, len(s_obj), n_ticks], np.int64),
-        prop_flags=_prop_flags(), prop_names=_names(PROPS), kind_names=_names(KINDS[:n_kind]),
+        prop_flags=_prop_flags(n_op), prop_names=_names(PROPS + OBJ_PROPS[:n_op]), kind_names=_names(KINDS[:n_kind]),
         ops=ops[:n_kind].copy(), n_ops=n_ops[:n_kind].copy(),
         guid_head=ghead, guid_data=gdata, scene=scene, group=group, cls=cls, is_player=isplayer,
         init_i=init_i, init_f=init_f,
@@ -384,22 +399,81 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
             used &= np.uint64((1 << rows) - 1)
         w["rec0_cells"] = cells
         w["rec0_used"] = used
-        if rec_set_frac > 0:
-            w.update(_record_sets(rng, n_obj, n_ticks, rows, cols, rec_set_frac, rec_set_float))
+        if rec_set_frac > 0 or rec_row_frac > 0:
+            w.update(_record_sets(rng, n_obj, n_ticks, rows, cols, rec_set_frac, rec_set_float, rec_row_frac))
     return w
 
 
-def _record_sets(rng, n_obj, n_ticks, rows, cols, frac, with_float):
+def _object_props(rng, n_obj, n_ticks, ghead, gdata, frac, x_tick, x_obj, x_pid, x_bits, x_mode):
+    """Object (NFGUID) properties: creation-time values (init_oh / init_od: other objects of the
+    world, or the null NFGUID) and NFIKernelModule::SetPropertyObject calls (KM:362) merged into the
+    SetProperty call stream of each window (x_pid >= N_INT + N_FLT, x_bits = nData64, x_bits_h =
+    nHead64; 0 for the int / f64 calls).  Values: another object's GUID, the null GUID, the current
+    value again (no change, PR:396), or a GUID that differs from the current one in its head half only
+    (NFGUID::operator== compares both halves)."""
+    no = len(OBJ_PROPS)
+    base = N_INT + N_FLT
+    pick = rng.integers(0, n_obj, (no, n_obj))
+    null = rng.random((no, n_obj)) < 0.3
+    init_oh = np.where(null, 0, ghead[pick]).astype(np.int64)
+    init_od = np.where(null, 0, gdata[pick]).astype(np.int64)
+    x_bits_h = np.zeros(len(x_tick), np.uint64)
+    cur_h, cur_d = init_oh.copy(), init_od.copy()   # (the generator's view: only these calls change them)
+    ts, os_, ps, bs, hs = [], [], [], [], []
+    for t in range(n_ticks):
+        k = int(frac * n_obj)
+        if k <= 0:
+            continue
+        o = rng.integers(0, n_obj, k)
+        p = rng.integers(0, no, k)
+        again = rng.random(k) < 0.1                      # the same (object, property) twice
+        o, p = np.concatenate([o, o[again]]), np.concatenate([p, p[again]])
+        r = rng.random(len(o))
+        q = rng.integers(0, n_obj, len(o))
+        vh = ghead[q].astype(np.int64)
+        vd = gdata[q].astype(np.int64)
+        vh = np.where(r < 0.15, 0, vh)                   # the null NFGUID
+        vd = np.where(r < 0.15, 0, vd)
+        same = (r >= 0.15) & (r < 0.3)                   # the value it holds: no change, no event
+        vh = np.where(same, cur_h[p, o], vh)
+        vd = np.where(same, cur_d[p, o], vd)
+        headonly = (r >= 0.3) & (r < 0.4)                # head half differs only
+        vh = np.where(headonly, cur_h[p, o] ^ 3, vh)
+        vd = np.where(headonly, cur_d[p, o], vd)
+        for i in range(len(o)):
+            cur_h[p[i], o[i]], cur_d[p[i], o[i]] = vh[i], vd[i]
+        ts.append(np.full(len(o), t))
+        os_.append(o)
+        ps.append(base + p)
+        bs.append(vd.view(np.uint64))
+        hs.append(vh.view(np.uint64))
+    if ts:
+        ot, oo, op_, ob, oh = (np.concatenate(x) for x in (ts, os_, ps, bs, hs))
+        # interleave with the window's other Set calls: order by tick, random within a tick
+        t_all = np.concatenate([x_tick, ot]).astype(np.int32)
+        key = np.lexsort((rng.random(len(t_all)), t_all))
+        x_tick = t_all[key]
+        x_obj = np.concatenate([x_obj, oo]).astype(np.int32)[key]
+        x_pid = np.concatenate([x_pid, op_]).astype(np.int32)[key]
+        x_bits = np.concatenate([x_bits, ob]).astype(np.uint64)[key]
+        x_mode = np.concatenate([x_mode, np.zeros(len(ot), np.uint8)])[key]
+        x_bits_h = np.concatenate([x_bits_h, oh]).astype(np.uint64)[key]
+    extra = dict(n_oprops=np.array([no], np.int64), init_oh=init_oh, init_od=init_od, x_bits_h=x_bits_h)
+    return extra, (x_tick, x_obj, x_pid, x_bits, x_mode)
+
+
+def _record_sets(rng, n_obj, n_ticks, rows, cols, frac, with_float, row_frac=0.0):
     """NFIKernelModule::SetRecordInt / SetRecordFloat calls between frames (r_*, call order within
     a window): random (object, row, col) cells of record 0 — rows used or not (a Set on an unused
     row is refused, RC:194) — with a third of them set twice in the window (coalesced to one event)
     and some set to the value they already hold (no event).  with_float=False keeps to the int
     columns (the reference's own NFCRecord::SetFloat is broken, see test_reference_record_setfloat_bug)."""
-    rt, ro, rr, rw, rc, rb = [], [], [], [], [], []
+    rt, ro, rr, rw, rc, rb, rop, rv = [], [], [], [], [], [], [], []
     ncol = cols if with_float else 2
     for t in range(1, n_ticks):
         k = int(frac * n_obj)
-        if k <= 0:
+        kr = int(row_frac * n_obj)
+        if k <= 0 and kr <= 0:
             continue
         o = rng.integers(0, n_obj, k)
         row = rng.integers(0, rows, k)
@@ -410,16 +484,43 @@ def _record_sets(rng, n_obj, n_ticks, rows, cols, frac, with_float):
         iv[rng.random(len(o)) < 0.1] = 0                 # often the value a cooldown already holds
         fv = rng.uniform(-50.0, 50.0, len(o))
         bits = np.where(col == 2, fv.view(np.int64), iv).astype(np.int64).view(np.uint64)
+        op = np.zeros(len(o), np.uint8)
+        vals = np.zeros((len(o), MAX_REC_COLS), np.uint64)
+        if kr > 0:
+            # record row operations (NFCRecord::AddRow / Remove, NFCKernelModule::ClearRecord): AddRow
+            # at the first unused row (-1) or at a given row (a used one is covered), Remove of used
+            # and unused rows, Clear; their objects also get SetRecord calls in the same window
+            qo = np.concatenate([rng.integers(0, n_obj, kr // 2), o[:kr - kr // 2]]) if k else rng.integers(0, n_obj, kr)
+            r = rng.random(len(qo))
+            qop = np.where(r < 0.45, 1, np.where(r < 0.88, 2, 3)).astype(np.uint8)
+            qrow = rng.integers(0, rows, len(qo))
+            qrow[(qop == 1) & (rng.random(len(qo)) < 0.5)] = -1
+            qv = np.zeros((len(qo), MAX_REC_COLS), np.uint64)
+            qv[:, 0] = rng.integers(1000, 2000, len(qo)).astype(np.uint64)
+            qv[:, 1] = rng.integers(0, 3000, len(qo)).astype(np.uint64)
+            qv[:, 2] = rng.uniform(0.0, 100.0, len(qo)).view(np.uint64)
+            o = np.concatenate([o, qo])
+            row = np.concatenate([row, qrow])
+            col = np.concatenate([col, np.zeros(len(qo), np.int64)])
+            bits = np.concatenate([bits, np.zeros(len(qo), np.uint64)])
+            op = np.concatenate([op, qop])
+            vals = np.concatenate([vals, qv])
         perm = rng.permutation(len(o))                   # call order within the window
         rt.append(np.full(len(o), t))
         ro.append(o[perm])
         rr.append(row[perm])
         rw.append(col[perm])
         rb.append(bits[perm])
+        rop.append(op[perm])
+        rv.append(vals[perm])
     cat = lambda lst, dt: np.concatenate(lst).astype(dt) if lst else np.zeros(0, dt)
     n = sum(len(x) for x in rt)
-    return dict(r_tick=cat(rt, np.int32), r_obj=cat(ro, np.int32), r_rec=np.zeros(n, np.int32),
-                r_row=cat(rr, np.int32), r_col=cat(rw, np.int32), r_bits=cat(rb, np.uint64))
+    out = dict(r_tick=cat(rt, np.int32), r_obj=cat(ro, np.int32), r_rec=np.zeros(n, np.int32),
+               r_row=cat(rr, np.int32), r_col=cat(rw, np.int32), r_bits=cat(rb, np.uint64))
+    if row_frac > 0:
+        out["r_op"] = cat(rop, np.uint8)
+        out["r_vals"] = np.concatenate(rv).astype(np.uint64) if rv else np.zeros((0, MAX_REC_COLS), np.uint64)
+    return out
 
 
 def _lifecycle_world(kw):
@@ -465,13 +566,14 @@ def _lifecycle_world(kw):
     # calls: SetProperty allowed in the destruction window (dropped with the object), schedule and
     # SwitchScene calls not
     keep = alive_at(w["x_obj"], w["x_tick"], True)
-    for k in ("x_tick", "x_obj", "x_pid", "x_bits", "x_mode"):
+    for k in ("x_tick", "x_obj", "x_pid", "x_bits", "x_mode", "x_bits_h"):
         if k in w:
             w[k] = w[k][keep]
     if "r_tick" in w:   # SetRecord* calls: like SetProperty
         keep = alive_at(w["r_obj"], w["r_tick"], True)
-        for k in ("r_tick", "r_obj", "r_rec", "r_row", "r_col", "r_bits"):
-            w[k] = w[k][keep]
+        for k in ("r_tick", "r_obj", "r_rec", "r_row", "r_col", "r_bits", "r_op", "r_vals"):
+            if k in w:
+                w[k] = w[k][keep]
     keep = alive_at(w["h_obj"], w["h_tick"], False)
     for k in ("h_tick", "h_op", "h_obj", "h_kind", "h_interval", "h_count", "h_time"):
         w[k] = w[k][keep]

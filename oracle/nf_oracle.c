@@ -10,6 +10,8 @@
  *   set_int        NFComm/NFCore/NFCProperty.cpp:254-293  (exact compare; null == 0)
  *   set_flt        NFComm/NFCore/NFCProperty.cpp:295-334  (IsZeroDouble(v-cur), eps 1e-15,
  *                  NFComm/NFPluginModule/NFPlatform.h:362)
+ *   set_obj        NFComm/NFCore/NFCProperty.cpp:377-416  (NFGUID ==: both halves; null == (0, 0)),
+ *                  reached through NFCKernelModule::SetPropertyObject (KM:362)
  *   set_rint       NFComm/NFCore/NFCRecord.cpp:182-241    (TData::operator== exact)
  *   set_rflt       NFComm/NFCore/NFCRecord.cpp:243-303    (TData::operator== |d| < 0.001,
  *                  NFComm/NFCore/NFIDataList.h:106-113)
@@ -24,6 +26,13 @@
  *                  AddSchedule; creation values are not dirty events)
  *   set_record     NFComm/NFKernelPlugin/NFCKernelModule.cpp:505/545 (SetRecordInt/Float between
  *                  frames) -> set_rint / set_rflt, refused on an unused row (NFCRecord.cpp:194)
+ *   add_row        NFComm/NFCore/NFCRecord.cpp:106-180 (AddRow(row, values): row -1 = the first
+ *                  unused row; a used row is covered; cells written without Update events; one Add
+ *                  or Cover event at (row, col 0))
+ *   remove_row     NFComm/NFCore/NFCRecord.cpp:1086-1107 (Del event while the row is still used,
+ *                  then unused; cells keep their values)
+ *   clear_record   NFComm/NFCore/NFCRecord.cpp:1109-1117 (Remove from the last row to the first),
+ *                  NFComm/NFKernelPlugin/NFCKernelModule.cpp:492 (ClearRecord)
  *   destroy_object NFComm/NFKernelPlugin/NFCKernelModule.cpp:273-308 (RemoveObjectFromGroup,
  *                  RemoveSchedule(self) which erases at once, NFCScheduleModule.cpp:240; the
  *                  object's events of the window are dropped with it)
@@ -32,7 +41,9 @@
  *                  order (NFCSceneGroupInfo::mxPlayerList, std::map), private&&!upload
  *                  -> self)
  * Dirty diff: per tick, the Set events of one (entity, property) are coalesced
- * to (first old, last new) and dropped when the bits are unchanged.
+ * to (first old, last new) and dropped when the bits are unchanged.  Record events of an entity:
+ * per record, its row events (Add / Del / Cover, rrc bits 24-27 = 1 / 2 / 3) in call order, then
+ * its coalesced cell Update events in (row, col) order.
  *
  * Usage: nf_oracle <workload.nfio> <out.nfio>
  * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off).
@@ -56,6 +67,7 @@ typedef struct {
 typedef struct {
     int32_t obj, pid;
     uint64_t old_bits, new_bits;
+    uint64_t old_h, new_h; /* object properties: the NFGUID head halves (old/new_bits = data) */
     int64_t seq;
 } setlog_t;
 
@@ -67,9 +79,10 @@ typedef struct {
 } rsetlog_t;
 
 /* ---------------- world ---------------- */
-static int64_t N, NI, NF, NC, NK, NR;
+static int64_t N, NI, NF, NC, NK, NR, NO;
 static int64_t *I;  /* [NI][N] */
 static double *F;   /* [NF][N] */
+static int64_t *OH, *OD; /* [NO][N] object properties: NFGUID head / data */
 static uint8_t *pflags; /* [NC][NI+NF] */
 static int32_t rec_rows[NFK_MAX_RECORDS], rec_cols[NFK_MAX_RECORDS];
 static uint8_t rec_ctype[NFK_MAX_RECORDS][NFK_MAX_REC_COLS];
@@ -103,14 +116,15 @@ static void die(const char* m) {
 static uint64_t dbits(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
 static double bitsd(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
 
-static void log_set(int32_t obj, int32_t pid, uint64_t o, uint64_t n) {
+static void log_set2(int32_t obj, int32_t pid, uint64_t o, uint64_t n, uint64_t oh, uint64_t nh) {
     if (nslog == capslog) {
         capslog = capslog ? capslog * 2 : 4096;
         slog = (setlog_t*)realloc(slog, capslog * sizeof(setlog_t));
     }
-    setlog_t e = {obj, pid, o, n, seq++};
+    setlog_t e = {obj, pid, o, n, oh, nh, seq++};
     slog[nslog++] = e;
 }
+static void log_set(int32_t obj, int32_t pid, uint64_t o, uint64_t n) { log_set2(obj, pid, o, n, 0, 0); }
 
 static void log_rset(int32_t obj, uint32_t rrc, uint64_t o, uint64_t n) {
     if (nrlog == caprlog) {
@@ -138,8 +152,46 @@ static void set_flt(int32_t obj, int32_t pid, double v) {
     log_set(obj, pid, dbits(cur), dbits(v));
 }
 
+/* NFCProperty::SetObject (PR:377): no event when the NFGUID equals the current one (both halves) */
+static void set_obj(int32_t obj, int32_t pid, int64_t h, int64_t d) {
+    int64_t q = (pid - NI - NF) * N + obj;
+    if (OH[q] == h && OD[q] == d) return;
+    log_set2(obj, pid, (uint64_t)OD[q], (uint64_t)d, (uint64_t)OH[q], (uint64_t)h);
+    OH[q] = h;
+    OD[q] = d;
+}
+
 static uint64_t* cell(int r, int32_t obj, int row, int col) {
     return &rcells[r][((int64_t)obj * rec_cols[r] + col) * rec_rows[r] + row];
+}
+
+/* record events: rrc = op << 24 | rec << 16 | row << 8 | col; op 0 = Update, else a row event */
+enum { RE_UPDATE = 0, RE_ADD = 1, RE_DEL = 2, RE_COVER = 3 };
+
+/* NFCRecord::AddRow (RC:111-180) with the row's values (NULL: the record's initial values, 0) */
+static void add_row(int r, int32_t obj, int row, const uint64_t* vals) {
+    if (row >= rec_rows[r]) return;  /* -1 */
+    int cover = 0;
+    if (row < 0) {
+        for (int i = 0; i < rec_rows[r]; i++)
+            if (!((rused[r][obj] >> i) & 1)) {
+                row = i;
+                break;
+            }
+        if (row < 0) return;  /* no unused row: -1 */
+    } else {
+        cover = (int)((rused[r][obj] >> row) & 1);
+    }
+    rused[r][obj] |= 1ull << row;
+    for (int c = 0; c < rec_cols[r]; c++) *cell(r, obj, row, c) = vals ? vals[c] : 0;
+    log_rset(obj, ((uint32_t)(cover ? RE_COVER : RE_ADD) << 24) | ((uint32_t)r << 16) | ((uint32_t)row << 8), 0, 0);
+}
+
+/* NFCRecord::Remove (RC:1086-1107): the Del event fires while the row is still used */
+static void remove_row(int r, int32_t obj, int row) {
+    if (row < 0 || row >= rec_rows[r] || !((rused[r][obj] >> row) & 1)) return;
+    log_rset(obj, ((uint32_t)RE_DEL << 24) | ((uint32_t)r << 16) | ((uint32_t)row << 8), 0, 0);
+    rused[r][obj] &= ~(1ull << row);
 }
 
 /* NFCRecord::SetInt (RC:182) */
@@ -289,10 +341,15 @@ static int cmp_slog(const void* a, const void* b) {
     return x->seq < y->seq ? -1 : (x->seq > y->seq);
 }
 
+/* per object, per record: row events in call order, then cell Updates by (row, col), call order */
 static int cmp_rlog(const void* a, const void* b) {
     const rsetlog_t *x = (const rsetlog_t*)a, *y = (const rsetlog_t*)b;
     if (orank[x->obj] != orank[y->obj]) return orank[x->obj] < orank[y->obj] ? -1 : 1;
-    if (x->rrc != y->rrc) return x->rrc < y->rrc ? -1 : 1;
+    const uint32_t rx = (x->rrc >> 16) & 0xFF, ry = (y->rrc >> 16) & 0xFF;
+    if (rx != ry) return rx < ry ? -1 : 1;
+    const int ux = (x->rrc >> 24) == RE_UPDATE, uy = (y->rrc >> 24) == RE_UPDATE;
+    if (ux != uy) return ux < uy ? -1 : 1;
+    if (ux && x->rrc != y->rrc) return x->rrc < y->rrc ? -1 : 1;
     return x->seq < y->seq ? -1 : (x->seq > y->seq);
 }
 
@@ -342,7 +399,9 @@ int main(int argc, char** argv) {
     int64_t* cfg = (int64_t*)GET("cfg")->data;
     N = cfg[0]; NI = cfg[1]; NF = cfg[2]; NC = cfg[3]; NK = cfg[4]; NR = cfg[5];
     int64_t NS = cfg[6], NT = cfg[7];
-    int64_t NP = NI + NF;
+    nfio_arr* noa = nfio_get(&wf, "n_oprops");  /* optional: object (NFGUID) properties */
+    NO = noa ? ((int64_t*)noa->data)[0] : 0;
+    int64_t NP = NI + NF + NO;
     pflags = (uint8_t*)GET("prop_flags")->data;
     if (NR > 0) {
         int32_t* rr = (int32_t*)GET("rec_rows")->data;
@@ -374,6 +433,10 @@ int main(int argc, char** argv) {
     isplayer = (uint8_t*)GET("is_player")->data;
     I = (int64_t*)GET("init_i")->data;
     F = (double*)GET("init_f")->data;
+    if (NO) {
+        OH = (int64_t*)GET("init_oh")->data;
+        OD = (int64_t*)GET("init_od")->data;
+    }
     int32_t* s_obj = (int32_t*)GET("s_obj")->data;
     int32_t* s_kind = (int32_t*)GET("s_kind")->data;
     float* s_interval = (float*)GET("s_interval")->data;
@@ -388,6 +451,7 @@ int main(int argc, char** argv) {
     uint64_t* x_bits = (uint64_t*)GET("x_bits")->data;
     nfio_arr* xma = nfio_get(&wf, "x_mode");  /* optional: 1 = SetProperty(p, GetProperty(p) + delta) */
     uint8_t* x_mode = xma ? (uint8_t*)xma->data : NULL;
+    uint64_t* x_bits_h = NO ? (uint64_t*)GET("x_bits_h")->data : NULL;  /* SetPropertyObject: head half */
     nfio_arr* ha = GET("h_tick");
     int64_t NH = (int64_t)ha->shape[0];
     int32_t* h_tick = (int32_t*)ha->data;
@@ -464,6 +528,11 @@ int main(int argc, char** argv) {
     int32_t* r_row = NRS ? (int32_t*)GET("r_row")->data : NULL;
     int32_t* r_col = NRS ? (int32_t*)GET("r_col")->data : NULL;
     uint64_t* r_bits = NRS ? (uint64_t*)GET("r_bits")->data : NULL;
+    /* optional: record row operations in the same call stream (r_op 0 = SetRecord*, 1 = AddRow(r_row,
+     * r_vals[i] [16 words]; r_row -1 = first unused row), 2 = Remove(r_row), 3 = ClearRecord) */
+    nfio_arr* roa = NRS ? nfio_get(&wf, "r_op") : NULL;
+    uint8_t* r_op = roa ? (uint8_t*)roa->data : NULL;
+    uint64_t* r_vals = roa ? (uint64_t*)GET("r_vals")->data : NULL;
     int64_t ri = 0;
 
     for (int t = 0; t < NT; t++) {
@@ -529,7 +598,8 @@ int main(int argc, char** argv) {
             }
             const int rmw = x_mode && x_mode[xi];
             if (pid < NI) set_int(o, pid, rmw ? (int64_t)((uint64_t)iget(o, pid) + x_bits[xi]) : (int64_t)x_bits[xi]);
-            else set_flt(o, pid, rmw ? fget(o, pid) + bitsd(x_bits[xi]) : bitsd(x_bits[xi]));
+            else if (pid < NI + NF) set_flt(o, pid, rmw ? fget(o, pid) + bitsd(x_bits[xi]) : bitsd(x_bits[xi]));
+            else set_obj(o, pid, (int64_t)x_bits_h[xi], (int64_t)x_bits[xi]);
             xi++;
         }
         /* SetRecordInt / SetRecordFloat (NFCKernelModule -> NFCRecord::SetInt / SetFloat, RC:182 /
@@ -537,7 +607,16 @@ int main(int argc, char** argv) {
          * (RC:194) or a column of the other type; the change predicates of set_rint / set_rflt */
         while (ri < NRS && r_tick[ri] == t) {
             int32_t o = r_obj[ri], r = r_rec[ri], row = r_row[ri], col = r_col[ri];
-            if (alive[o] && r >= 0 && r < NR && row >= 0 && row < rec_rows[r] && col >= 0 && col < rec_cols[r] &&
+            const int op = r_op ? r_op[ri] : 0;
+            if (op && alive[o] && r >= 0 && r < NR) {
+                if (op == 1) add_row(r, o, row, r_vals + ri * NFK_MAX_REC_COLS);
+                else if (op == 2) remove_row(r, o, row);
+                else if (op == 3)
+                    for (int q = rec_rows[r] - 1; q >= 0; q--) remove_row(r, o, q);
+                ri++;
+                continue;
+            }
+            if (!op && alive[o] && r >= 0 && r < NR && row >= 0 && row < rec_rows[r] && col >= 0 && col < rec_cols[r] &&
                 ((rused[r][o] >> row) & 1)) {
                 if (rec_ctype[r][col]) set_rflt(r, o, row, col, bitsd(r_bits[ri]));
                 else set_rint(r, o, row, col, (int64_t)r_bits[ri]);
@@ -601,14 +680,18 @@ int main(int argc, char** argv) {
         int32_t* ev_pid = (int32_t*)malloc((nslog + 1) * 4);
         uint64_t* ev_old = (uint64_t*)malloc((nslog + 1) * 8);
         uint64_t* ev_new = (uint64_t*)malloc((nslog + 1) * 8);
+        uint64_t* ev_oldh = (uint64_t*)malloc((nslog + 1) * 8);
+        uint64_t* ev_newh = (uint64_t*)malloc((nslog + 1) * 8);
         for (int64_t i = 0; i < nslog;) {
             int64_t j = i;
             while (j < nslog && slog[j].obj == slog[i].obj && slog[j].pid == slog[i].pid) j++;
-            if (slog[i].old_bits != slog[j - 1].new_bits) {
+            if (slog[i].old_bits != slog[j - 1].new_bits || slog[i].old_h != slog[j - 1].new_h) {
                 ev_obj[ne] = slog[i].obj;
                 ev_pid[ne] = slog[i].pid;
                 ev_old[ne] = slog[i].old_bits;
                 ev_new[ne] = slog[j - 1].new_bits;
+                ev_oldh[ne] = slog[i].old_h;
+                ev_newh[ne] = slog[j - 1].new_h;
                 ne++;
             }
             i = j;
@@ -620,9 +703,10 @@ int main(int argc, char** argv) {
         uint64_t* re_old = (uint64_t*)malloc((nrlog + 1) * 8);
         uint64_t* re_new = (uint64_t*)malloc((nrlog + 1) * 8);
         for (int64_t i = 0; i < nrlog;) {
-            int64_t j = i;
-            while (j < nrlog && rlog[j].obj == rlog[i].obj && rlog[j].rrc == rlog[i].rrc) j++;
-            if (rlog[i].old_bits != rlog[j - 1].new_bits) {
+            int64_t j = i + 1;
+            if ((rlog[i].rrc >> 24) == RE_UPDATE)  /* row events are not coalesced */
+                while (j < nrlog && rlog[j].obj == rlog[i].obj && rlog[j].rrc == rlog[i].rrc) j++;
+            if (rlog[i].old_bits != rlog[j - 1].new_bits || (rlog[i].rrc >> 24) != RE_UPDATE) {
                 re_obj[nre] = rlog[i].obj;
                 re_rrc[nre] = rlog[i].rrc;
                 re_old[nre] = rlog[i].old_bits;
@@ -654,7 +738,7 @@ int main(int argc, char** argv) {
         for (int64_t e = 0; e < ne + nre; e++) {
             moff[e] = (uint32_t)nm;
             int32_t o = e < ne ? ev_obj[e] : re_obj[e - ne];
-            uint8_t fl8 = e < ne ? pflags[cls[o] * NP + ev_pid[e]] : rflags[cls[o] * NR + (re_rrc[e - ne] >> 16)];
+            uint8_t fl8 = e < ne ? pflags[cls[o] * NP + ev_pid[e]] : rflags[cls[o] * NR + ((re_rrc[e - ne] >> 16) & 0xFF)];
             if (fl8 & NFK_PUBLIC) {
                 for (int64_t k = seg_begin_of_obj[o]; k < seg_end_of_obj[o]; k++) {
                     int32_t p = sorted_objs[k];
@@ -679,6 +763,10 @@ int main(int argc, char** argv) {
         put_tick(&w, t, "ev", "pid", NFIO_I32, ev_pid, ne, 4);
         put_tick(&w, t, "ev", "old", NFIO_U64, ev_old, ne, 8);
         put_tick(&w, t, "ev", "new", NFIO_U64, ev_new, ne, 8);
+        if (NO) {
+            put_tick(&w, t, "ev", "oldh", NFIO_U64, ev_oldh, ne, 8);
+            put_tick(&w, t, "ev", "newh", NFIO_U64, ev_newh, ne, 8);
+        }
         put_tick(&w, t, "re", "obj", NFIO_I32, re_obj, nre, 4);
         put_tick(&w, t, "re", "rrc", NFIO_U32, re_rrc, nre, 4);
         put_tick(&w, t, "re", "old", NFIO_U64, re_old, nre, 8);
@@ -688,7 +776,7 @@ int main(int argc, char** argv) {
         put_tick(&w, t, "fi", "rem", NFIO_I32, fr, nfired, 4);
         put_tick(&w, t, "mo", "off", NFIO_U32, moff, ne + nre + 1, 4);
         put_tick(&w, t, "mr", "obj", NFIO_I32, mr, nm, 4);
-        free(ev_obj); free(ev_pid); free(ev_old); free(ev_new);
+        free(ev_obj); free(ev_pid); free(ev_old); free(ev_new); free(ev_oldh); free(ev_newh);
         free(re_obj); free(re_rrc); free(re_old); free(re_new);
         free(fl); free(fo); free(fk); free(fr); free(moff); free(mr);
     }
@@ -698,6 +786,7 @@ int main(int argc, char** argv) {
         if (alive[o]) continue;
         for (int64_t p = 0; p < NI; p++) I[p * N + o] = 0;
         for (int64_t p = 0; p < NF; p++) F[p * N + o] = 0.0;
+        for (int64_t p = 0; p < NO; p++) OH[p * N + o] = OD[p * N + o] = 0;
         for (int r = 0; r < NR; r++) memset(cell(r, (int32_t)o, 0, 0), 0, (size_t)rec_cols[r] * rec_rows[r] * 8);
         for (int k = 0; k < NK; k++) S[o * NK + k].present = 0;
     }
@@ -706,6 +795,11 @@ int main(int argc, char** argv) {
         nfio_put(&w, "final_i", NFIO_I64, 2, sh, I, NI * N * 8);
         uint64_t sf[2] = {(uint64_t)NF, (uint64_t)N};
         nfio_put(&w, "final_f", NFIO_F64, 2, sf, F, NF * N * 8);
+        if (NO) {
+            uint64_t so[2] = {(uint64_t)NO, (uint64_t)N};
+            nfio_put(&w, "final_oh", NFIO_I64, 2, so, OH, NO * N * 8);
+            nfio_put(&w, "final_od", NFIO_I64, 2, so, OD, NO * N * 8);
+        }
         for (int r = 0; r < NR; r++) {
             char nm[32];
             snprintf(nm, sizeof nm, "final_rec%d", r);

@@ -6,7 +6,7 @@
 //
 // Reference classes used unmodified (flyish/NoahGameFrame):
 //   NFCPropertyManager / NFCProperty   NFComm/NFCore/NFCPropertyManager.cpp, NFCProperty.cpp
-//   NFCRecord                          NFComm/NFCore/NFCRecord.cpp
+//   NFCRecord                          NFComm/NFCore/NFCRecord.cpp (SetInt, AddRow, Remove, Clear)
 //   NFCScheduleModule                  NFComm/NFKernelPlugin/NFCScheduleModule.cpp
 //   NFCSceneInfo / NFCSceneGroupInfo   NFComm/NFPluginModule/NFISceneAOIModule.h (group maps)
 // Restated here (the kernel/AOI modules need the full plugin manager to build):
@@ -69,12 +69,12 @@ struct SchedProbe : public NFCScheduleModule {
     }
 };
 
-struct SetEv { int32_t obj, pid; uint64_t o, n; int64_t seq; };
+struct SetEv { int32_t obj, pid; uint64_t o, n, oh, nh; int64_t seq; };
 struct RSetEv { int32_t obj; uint32_t rrc; uint64_t o, n; int64_t seq; };
 struct Fired { int32_t obj, kind, rem; };
 
 struct World {
-    int64_t N, NI, NF, NC, NK, NR;
+    int64_t N, NI, NF, NC, NK, NR, NO;
     std::vector<std::string> pname, kname;
     std::map<std::string, int> kind_of;
     std::vector<NFGUID> id;
@@ -138,14 +138,28 @@ static int OnPropertyEvent(int32_t obj, int32_t pid, const NFIDataList::TData& o
         W.bench_msgs += lst.GetCount();
         return 0;
     }
+    if (pid >= W.NI + W.NF) {  // TDATA_OBJECT: NFGUID (data, head)
+        const NFGUID a = oldv.GetObject(), b = newv.GetObject();
+        W.slog.push_back({obj, pid, (uint64_t)a.nData64, (uint64_t)b.nData64, (uint64_t)a.nHead64,
+                          (uint64_t)b.nHead64, W.seq++});
+        return 0;
+    }
     uint64_t o = pid < W.NI ? (uint64_t)oldv.GetInt() : dbits(oldv.GetFloat());
     uint64_t n = pid < W.NI ? (uint64_t)newv.GetInt() : dbits(newv.GetFloat());
-    W.slog.push_back({obj, pid, o, n, W.seq++});
+    W.slog.push_back({obj, pid, o, n, 0, 0, W.seq++});
     return 0;
 }
 
 static int OnRecordEvent(int32_t obj, int32_t r, const RECORD_EVENT_DATA& ev, const NFIDataList::TData& oldv,
                          const NFIDataList::TData& newv) {
+    if (ev.nOpType == RECORD_EVENT_DATA::Add || ev.nOpType == RECORD_EVENT_DATA::Del ||
+        ev.nOpType == RECORD_EVENT_DATA::Cover) {  // row events: rrc bits 24-27 = 1 Add, 2 Del, 3 Cover
+        if (W.bench) return 0;
+        const uint32_t op = ev.nOpType == RECORD_EVENT_DATA::Add ? 1u : ev.nOpType == RECORD_EVENT_DATA::Del ? 2u : 3u;
+        W.rlog.push_back({obj, (op << 24) | ((uint32_t)r << 16) | ((uint32_t)ev.nRow << 8) | (uint32_t)ev.nCol, 0, 0,
+                          W.seq++});
+        return 0;
+    }
     if (ev.nOpType != RECORD_EVENT_DATA::Update) return 0;
     bool isint = newv.GetType() == TDATA_INT;
     if (W.bench) {
@@ -324,7 +338,10 @@ int main(int argc, char** argv) {
     int64_t* cfg = (int64_t*)GET(wf, "cfg")->data;
     W.N = cfg[0]; W.NI = cfg[1]; W.NF = cfg[2]; W.NC = cfg[3]; W.NK = cfg[4]; W.NR = cfg[5];
     int64_t NS = cfg[6], NT = cfg[7];
-    int64_t NP = W.NI + W.NF;
+    nfio_arr* noa = nfio_get(&wf, "n_oprops");  // optional: object (NFGUID) properties
+    W.NO = noa ? ((int64_t*)noa->data)[0] : 0;
+    int64_t NP = W.NI + W.NF + W.NO;
+    auto ptype = [&](int64_t p) { return p < W.NI ? TDATA_INT : p < W.NI + W.NF ? TDATA_FLOAT : TDATA_OBJECT; };
     if (bench) NT = std::min<int64_t>(NT, atoll(argv[3]));
     uint8_t* pnames = (uint8_t*)GET(wf, "prop_names")->data;
     uint8_t* knames = (uint8_t*)GET(wf, "kind_names")->data;
@@ -346,7 +363,7 @@ int main(int argc, char** argv) {
     for (int c = 0; c < W.NC; c++) {
         NF_SHARE_PTR<NFIPropertyManager> cpm(new NFCPropertyManager(NFGUID()));
         for (int p = 0; p < NP; p++) {
-            auto pr = cpm->AddProperty(NFGUID(), W.pname[p], p < W.NI ? TDATA_INT : TDATA_FLOAT);
+            auto pr = cpm->AddProperty(NFGUID(), W.pname[p], ptype(p));
             uint8_t f = pflags[c * NP + p];
             pr->SetPublic(f & NFK_PUBLIC);
             pr->SetPrivate(f & NFK_PRIVATE);
@@ -378,6 +395,8 @@ int main(int argc, char** argv) {
     uint8_t* ip = (uint8_t*)GET(wf, "is_player")->data;
     int64_t* init_i = (int64_t*)GET(wf, "init_i")->data;
     double* init_f = (double*)GET(wf, "init_f")->data;
+    int64_t* init_oh = W.NO ? (int64_t*)GET(wf, "init_oh")->data : nullptr;
+    int64_t* init_od = W.NO ? (int64_t*)GET(wf, "init_od")->data : nullptr;
     W.scene.assign(sc, sc + W.N);
     W.group.assign(gr, gr + W.N);
     W.cls.assign(cl, cl + W.N);
@@ -398,12 +417,13 @@ int main(int argc, char** argv) {
         NF_SHARE_PTR<NFIPropertyManager> pm(new NFCPropertyManager(id));
         for (int p = 0; p < NP; p++) {
             auto tmpl = W.class_pm[W.cls[o]]->GetElement(W.pname[p]);
-            auto pr = pm->AddProperty(id, W.pname[p], p < W.NI ? TDATA_INT : TDATA_FLOAT);
+            auto pr = pm->AddProperty(id, W.pname[p], ptype(p));
             pr->SetPublic(tmpl->GetPublic());
             pr->SetPrivate(tmpl->GetPrivate());
             pr->SetUpload(tmpl->GetUpload());
             if (p < W.NI) pr->SetInt(init_i[p * W.N + o]);
-            else pr->SetFloat(init_f[(p - W.NI) * W.N + o]);
+            else if (p < W.NI + W.NF) pr->SetFloat(init_f[(p - W.NI) * W.N + o]);
+            else pr->SetObject(NFGUID(init_oh[(p - W.NI - W.NF) * W.N + o], init_od[(p - W.NI - W.NF) * W.N + o]));
             int32_t obj = (int32_t)o, pid = p;
             pr->RegisterCallback(PROPERTY_EVENT_FUNCTOR_PTR(new PROPERTY_EVENT_FUNCTOR(
                 [obj, pid](const NFGUID&, const std::string&, const NFIDataList::TData& a, const NFIDataList::TData& b) {
@@ -474,6 +494,7 @@ int main(int argc, char** argv) {
     uint64_t* x_bits = (uint64_t*)GET(wf, "x_bits")->data;
     nfio_arr* xma = nfio_get(&wf, "x_mode");  // optional: 1 = SetProperty(p, GetProperty(p) + delta)
     uint8_t* x_mode = xma ? (uint8_t*)xma->data : nullptr;
+    uint64_t* x_bits_h = W.NO ? (uint64_t*)GET(wf, "x_bits_h")->data : nullptr;  // SetPropertyObject: head
     nfio_arr* rta = nfio_get(&wf, "r_tick");  // optional: SetRecordInt calls between frames
     const int64_t NRS = rta ? (int64_t)rta->shape[0] : 0;
     int32_t* r_tick = NRS ? (int32_t*)rta->data : nullptr;
@@ -482,6 +503,11 @@ int main(int argc, char** argv) {
     int32_t* r_row = NRS ? (int32_t*)GET(wf, "r_row")->data : nullptr;
     int32_t* r_col = NRS ? (int32_t*)GET(wf, "r_col")->data : nullptr;
     uint64_t* r_bits = NRS ? (uint64_t*)GET(wf, "r_bits")->data : nullptr;
+    // optional record row operations in the same stream: r_op 1 AddRow(r_row, r_vals), 2 Remove(r_row),
+    // 3 ClearRecord (KM:492 -> NFCRecord::Clear)
+    nfio_arr* roa = NRS ? nfio_get(&wf, "r_op") : nullptr;
+    uint8_t* r_op = roa ? (uint8_t*)roa->data : nullptr;
+    uint64_t* r_vals = roa ? (uint64_t*)GET(wf, "r_vals")->data : nullptr;
     int64_t ri = 0;
     nfio_arr* ha = GET(wf, "h_tick");
     int64_t NH = (int64_t)ha->shape[0];
@@ -593,7 +619,9 @@ int main(int argc, char** argv) {
         while (xi < NX && x_tick[xi] == t) {
             NFGUID self = W.id[x_obj[xi]];
             const bool rmw = x_mode && x_mode[xi];  // game logic: Set(p, Get(p) + delta) (KM:401 then KM:323)
-            if (x_pid[xi] < W.NI)
+            if (x_pid[xi] >= W.NI + W.NF)  // NFCKernelModule::SetPropertyObject (KM:362) -> NFCProperty::SetObject
+                W.pm[W.obj_of[self]]->SetPropertyObject(W.pname[x_pid[xi]], NFGUID((int64_t)x_bits_h[xi], (int64_t)x_bits[xi]));
+            else if (x_pid[xi] < W.NI)
                 SetInt(self, x_pid[xi], rmw ? (int64_t)((uint64_t)GetInt(self, x_pid[xi]) + x_bits[xi]) : (int64_t)x_bits[xi]);
             else
                 SetFloat(self, x_pid[xi], rmw ? GetFloat(self, x_pid[xi]) + bitsd(x_bits[xi]) : bitsd(x_bits[xi]));
@@ -603,7 +631,26 @@ int main(int argc, char** argv) {
         // column, used row, changed value; the record hook fires) made before this Execute
         while (ri < NRS && r_tick[ri] == t) {
             const int32_t o = r_obj[ri], r = r_rec[ri];
-            if (W.alive[o]) {
+            const int op = r_op ? r_op[ri] : 0;
+            if (op && W.alive[o]) {
+                auto& R = W.rec[o][r];
+                if (op == 1) {  // NFCRecord::AddRow(nRow, var) (RC:111)
+                    NFCDataList rowv;
+                    for (int c = 0; c < W.rec_cols[r]; c++) {
+                        const uint64_t b = r_vals[ri * NFK_MAX_REC_COLS + c];
+                        if (rctype[r * NFK_MAX_REC_COLS + c] == 0) rowv.Add((NFINT64)b);
+                        else rowv.Add(bitsd(b));
+                    }
+                    R->AddRow(r_row[ri], rowv);
+                } else if (op == 2) {
+                    R->Remove(r_row[ri]);  // RC:1086
+                } else if (op == 3) {
+                    R->Clear();  // NFCKernelModule::ClearRecord (KM:492) -> RC:1109
+                }
+                ri++;
+                continue;
+            }
+            if (!op && W.alive[o]) {
                 if (rctype[r * NFK_MAX_REC_COLS + r_col[ri]]) {
                     fprintf(stderr, "nf_ref_harness: SetRecordFloat cannot run on the reference: "
                                     "NFCRecord::SetFloat stores an int64 variant (see --repro-record-float)\n");
@@ -645,29 +692,38 @@ int main(int argc, char** argv) {
             return a.pid < b.pid;
         });
         std::vector<int32_t> ev_obj, ev_pid;
-        std::vector<uint64_t> ev_old, ev_new;
+        std::vector<uint64_t> ev_old, ev_new, ev_oldh, ev_newh;
         for (size_t i = 0; i < W.slog.size();) {
             size_t j = i;
             while (j < W.slog.size() && W.slog[j].obj == W.slog[i].obj && W.slog[j].pid == W.slog[i].pid) j++;
-            if (W.slog[i].o != W.slog[j - 1].n) {
+            if (W.slog[i].o != W.slog[j - 1].n || W.slog[i].oh != W.slog[j - 1].nh) {
                 ev_obj.push_back(W.slog[i].obj);
                 ev_pid.push_back(W.slog[i].pid);
                 ev_old.push_back(W.slog[i].o);
                 ev_new.push_back(W.slog[j - 1].n);
+                ev_oldh.push_back(W.slog[i].oh);
+                ev_newh.push_back(W.slog[j - 1].nh);
             }
             i = j;
         }
+        // per object, per record: row events in call order, then cell Updates by (row, col)
         std::stable_sort(W.rlog.begin(), W.rlog.end(), [&](const RSetEv& a, const RSetEv& b) {
             if (orank[a.obj] != orank[b.obj]) return orank[a.obj] < orank[b.obj];
-            return a.rrc < b.rrc;
+            const uint32_t ra = (a.rrc >> 16) & 0xFF, rb = (b.rrc >> 16) & 0xFF;
+            if (ra != rb) return ra < rb;
+            const bool ua = (a.rrc >> 24) == 0, ub = (b.rrc >> 24) == 0;
+            if (ua != ub) return ub;
+            return ua ? a.rrc < b.rrc : false;
         });
         std::vector<int32_t> re_obj;
         std::vector<uint32_t> re_rrc;
         std::vector<uint64_t> re_old, re_new;
         for (size_t i = 0; i < W.rlog.size();) {
-            size_t j = i;
-            while (j < W.rlog.size() && W.rlog[j].obj == W.rlog[i].obj && W.rlog[j].rrc == W.rlog[i].rrc) j++;
-            if (W.rlog[i].o != W.rlog[j - 1].n) {
+            size_t j = i + 1;
+            const bool upd = (W.rlog[i].rrc >> 24) == 0;  // row events are not coalesced
+            if (upd)
+                while (j < W.rlog.size() && W.rlog[j].obj == W.rlog[i].obj && W.rlog[j].rrc == W.rlog[i].rrc) j++;
+            if (W.rlog[i].o != W.rlog[j - 1].n || !upd) {
                 re_obj.push_back(W.rlog[i].obj);
                 re_rrc.push_back(W.rlog[i].rrc);
                 re_old.push_back(W.rlog[i].o);
@@ -688,7 +744,7 @@ int main(int argc, char** argv) {
         for (size_t e = 0; e < ne + nre; e++) {
             moff.push_back((uint32_t)mr.size());
             int32_t o = e < ne ? ev_obj[e] : re_obj[e - ne];
-            uint8_t fl = e < ne ? prop_flags(o, ev_pid[e]) : W.rflags[W.cls[o] * W.NR + (re_rrc[e - ne] >> 16)];
+            uint8_t fl = e < ne ? prop_flags(o, ev_pid[e]) : W.rflags[W.cls[o] * W.NR + ((re_rrc[e - ne] >> 16) & 0xFF)];
             NFCDataList lst;
             broadcast_list(o, fl, lst);
             for (int i = 0; i < lst.GetCount(); i++) mr.push_back(W.obj_of[lst.Object(i)]);
@@ -700,6 +756,10 @@ int main(int argc, char** argv) {
         PUT("ev", "pid", NFIO_I32, ev_pid, 4);
         PUT("ev", "old", NFIO_U64, ev_old, 8);
         PUT("ev", "new", NFIO_U64, ev_new, 8);
+        if (W.NO) {
+            PUT("ev", "oldh", NFIO_U64, ev_oldh, 8);
+            PUT("ev", "newh", NFIO_U64, ev_newh, 8);
+        }
         PUT("re", "obj", NFIO_I32, re_obj, 4);
         PUT("re", "rrc", NFIO_U32, re_rrc, 4);
         PUT("re", "old", NFIO_U64, re_old, 8);
@@ -729,6 +789,20 @@ int main(int argc, char** argv) {
     nfio_put(&w, "final_i", NFIO_I64, 2, sh, fi.data(), fi.size() * 8);
     uint64_t sf[2] = {(uint64_t)W.NF, (uint64_t)W.N};
     nfio_put(&w, "final_f", NFIO_F64, 2, sf, ff.data(), ff.size() * 8);
+    if (W.NO) {
+        std::vector<int64_t> foh(W.NO * W.N, 0), fod(W.NO * W.N, 0);
+        for (int64_t o = 0; o < W.N; o++) {
+            if (!W.alive[o]) continue;
+            for (int p = 0; p < W.NO; p++) {
+                const NFGUID g = W.pm[o]->GetPropertyObject(W.pname[W.NI + W.NF + p]);
+                foh[p * W.N + o] = g.nHead64;
+                fod[p * W.N + o] = g.nData64;
+            }
+        }
+        uint64_t so[2] = {(uint64_t)W.NO, (uint64_t)W.N};
+        nfio_put(&w, "final_oh", NFIO_I64, 2, so, foh.data(), foh.size() * 8);
+        nfio_put(&w, "final_od", NFIO_I64, 2, so, fod.data(), fod.size() * 8);
+    }
     for (int r = 0; r < W.NR; r++) {
         std::vector<uint64_t> cells((size_t)W.N * W.rec_cols[r] * W.rec_rows[r]);
         for (int64_t o = 0; o < W.N; o++)
@@ -736,8 +810,12 @@ int main(int argc, char** argv) {
                 for (int row = 0; row < W.rec_rows[r]; row++) {
                     auto& R = W.rec[o][r];
                     uint64_t b = rcells[r][((int64_t)o * W.rec_cols[r] + c) * W.rec_rows[r] + row];
-                    if (R->IsUsed(row))
+                    if (R->IsUsed(row)) {
                         b = rctype[r * NFK_MAX_REC_COLS + c] == 0 ? (uint64_t)R->GetInt(row, c) : dbits(R->GetFloat(row, c));
+                    } else if (auto& pv = R->GetRecordVec().at((size_t)row * W.rec_cols[r] + c)) {
+                        // a row used once and removed keeps its cells (NFCRecord::Remove, RC:1086)
+                        b = rctype[r * NFK_MAX_REC_COLS + c] == 0 ? (uint64_t)pv->GetInt() : dbits(pv->GetFloat());
+                    }
                     cells[((size_t)o * W.rec_cols[r] + c) * W.rec_rows[r] + row] = b;
                 }
         char nm[32];

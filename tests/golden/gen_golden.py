@@ -44,6 +44,12 @@ FIXTURES = {
     "recsets": dict(n_obj=400, n_scenes=2, groups_per_scene=4, players_per_group=4, n_ticks=8, seed=909,
                     records=True, rec_rows=24, rec_float_op=False, rec_set_frac=0.1, rec_set_float=False,
                     ext_frac=0.03),
+    # object (NFGUID) properties: SetPropertyObject (KM:362 -> NFCProperty::SetObject, PR:377) among
+    # the window's other Sets — other objects' GUIDs, the null GUID, unchanged values, head-only
+    # changes — with create / destroy and scene switches around them
+    "objects": dict(n_obj=500, n_scenes=2, groups_per_scene=4, players_per_group=3, n_ticks=8, seed=1010,
+                    ext_frac=0.05, ext_props="all", obj_props=True, obj_set_frac=0.08, host_ops=True,
+                    switch_frac=0.02, spawn_frac=0.03, destroy_frac=0.03),
 }
 
 

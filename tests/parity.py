@@ -50,11 +50,18 @@ def run_gpu(w, msg_capacity=0, slack_per_256=0):
             out[f"{pfx}_t{t}_{nm}"] = r[k]
         out[f"mo_t{t}_off"] = r["mo_off"]
         out[f"mr_t{t}_obj"] = r["mr_obj"]
+        if "ev_oldh" in r:
+            out[f"ev_t{t}_oldh"] = r["ev_oldh"]
+            out[f"ev_t{t}_newh"] = r["ev_newh"]
     n_int, n_flt, n_rec = int(w["cfg"][1]), int(w["cfg"][2]), int(w["cfg"][5])
     out["final_i"] = np.stack([m.read_prop(p) for p in range(n_int)])
     out["final_f"] = np.stack([m.read_prop(n_int + p) for p in range(n_flt)])
     for r in range(n_rec):
         out[f"final_rec{r}"] = m.read_record(r)
+    if m.n_oprops:
+        hd = [m.read_object(n_int + n_flt + p) for p in range(m.n_oprops)]
+        out["final_oh"] = np.stack([h for h, _ in hd])
+        out["final_od"] = np.stack([d for _, d in hd])
     nx, rm, st = m.read_schedules()
     out["final_s_next"] = nx
     out["final_s_remain"] = rm

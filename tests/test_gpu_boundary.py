@@ -1,0 +1,102 @@
+"""GPU: boundary behaviour of the C-ABI beyond the frame outputs — object-property reads,
+device errors surfacing on the asynchronous read path, and the failure policy of nfk_execute."""
+import numpy as np
+import pytest
+
+from noahgameframe_amd import kernel, workload
+
+pytestmark = pytest.mark.gpu
+
+
+def test_object_reads_see_queued_sets(gpu_available):
+    """NFIKernelModule::GetPropertyObject (KM:440) through nfk_get_objects: the NFGUID the device
+    holds after the last frame, then this window's SetPropertyObject calls on top (the last one
+    wins: NFCProperty::SetObject stores any different value, PR:377-416)."""
+    w = workload.make_world(n_obj=800, n_scenes=1, groups_per_scene=4, players_per_group=3, n_ticks=3, seed=21,
+                            obj_props=True, obj_set_frac=0.1, ext_frac=0.02)
+    m = kernel.world_from_workload(w)
+    for t in range(2):
+        kernel.run_workload(m, w, t, collect=False)
+    base = workload.N_INT + workload.N_FLT
+    gh, gd = w["guid_head"], w["guid_data"]
+    fin = [m.read_object(base + p) for p in range(len(workload.OBJ_PROPS))]
+    rng = np.random.default_rng(3)
+    n = 300   # more than 8 words: the gathered read path
+    o = rng.integers(0, len(gh), n)
+    p = rng.integers(0, len(workload.OBJ_PROPS), n)
+    vh, vd = m.get_objects(gh[o], gd[o], base + p)
+    np.testing.assert_array_equal(vh, np.array([fin[q][0][i] for q, i in zip(p, o)]))
+    np.testing.assert_array_equal(vd, np.array([fin[q][1][i] for q, i in zip(p, o)]))
+    h1, d1 = m.get_objects(gh[o[:3]], gd[o[:3]], base + p[:3])   # the single-read path agrees
+    np.testing.assert_array_equal(h1, vh[:3])
+    np.testing.assert_array_equal(d1, vd[:3])
+    g = (int(gh[5]), int(gd[5]))
+    m.SetPropertyObject(g, base + 1, (int(gh[7]), int(gd[7])))
+    assert m.GetPropertyObject(g, base + 1) == (int(gh[7]), int(gd[7]))
+    m.SetPropertyObject(g, base + 1, (0, 0))
+    assert m.GetPropertyObject(g, base + 1) == (0, 0)
+    m.Execute(int(w["tick_time"][2]))
+    assert m.GetPropertyObject(g, base + 1) == (0, 0)
+    with pytest.raises(kernel.NFKError):   # an int property is not an object property
+        m.get_objects([gh[0]], [gd[0]], [0])
+    with pytest.raises(kernel.NFKError):   # and SetPropertyInt refuses an object property
+        m.set_props([gh[0]], [gd[0]], [base], [1])
+    m.close()
+
+
+def test_fanout_bound_error_surfaces_on_outputs(gpu_available, monkeypatch):
+    """kErrFanBound (a tile's fan-out past the bound its run was placed with, nfgpu_tick.hpp) is
+    reported on the asynchronous consumer path: nfk_outputs_get fails once the frame has completed,
+    the next nfk_execute refuses to run, and nfk_summary_get reports and clears it.  The bound is
+    forced to 4 messages per tile with the kAblTinyTcap test hook."""
+    monkeypatch.setenv("NFGPU_ABLATE", str(1 << 27))
+    w = workload.make_world(n_obj=3000, n_scenes=1, groups_per_scene=4, players_per_group=20, n_ticks=3, seed=8,
+                            ext_frac=0.05)
+    m = kernel.world_from_workload(w)
+    kernel.run_workload(m, w, 0, collect=False)
+    m.synchronize()
+    with pytest.raises(kernel.NFKError) as e:
+        m.outputs_raw()
+    assert e.value.code == -6 and "bound" in str(e.value)
+    with pytest.raises(kernel.NFKError) as e:
+        m.Execute(int(w["tick_time"][1]))
+    assert e.value.code == -6
+    with pytest.raises(kernel.NFKError) as e:
+        m.summary()
+    assert "bound" in str(e.value)
+    # reported and cleared: the next frame runs (and fails the same way, the hook is still on)
+    m.Execute(int(w["tick_time"][1]))
+    m.close()
+
+
+def test_failed_frame_drops_the_whole_window(gpu_available, monkeypatch):
+    """A failure of nfk_execute after the window's membership changes were applied drops every
+    queued call of the window (SetProperty, SetRecord, schedule calls alike), so none of them is
+    applied out of order in a later frame (NFGPU_INJECT_EXEC_FAIL test hook): the world then runs
+    exactly like a twin that never had those calls."""
+    w = workload.make_world(n_obj=1000, n_scenes=1, groups_per_scene=4, players_per_group=3, n_ticks=3, seed=9,
+                            records=True, rec_rows=16, rec_float_op=False, ext_frac=0.0, host_ops=False)
+    m = kernel.world_from_workload(w)
+    twin = kernel.world_from_workload(w)
+    for x in (m, twin):
+        x.Execute(int(w["tick_time"][0]))
+    gh, gd = w["guid_head"], w["guid_data"]
+    g = (int(gh[3]), int(gd[3]))
+    row = int(np.nonzero([(int(w["rec0_used"][3]) >> r) & 1 for r in range(16)])[0][0])
+    m.SetPropertyInt(g, "HP", m.GetPropertyInt(g, "HP") + 1)
+    m.SetRecordInt(g, 0, row, 1, 987654)
+    m.AddSchedule((int(gh[4]), int(gd[4])), "SkillCD", 0.1, -1, int(w["tick_time"][0]))
+    monkeypatch.setenv("NFGPU_INJECT_EXEC_FAIL", "1")
+    with pytest.raises(kernel.NFKError):
+        m.Execute(int(w["tick_time"][1]))
+    monkeypatch.setenv("NFGPU_INJECT_EXEC_FAIL", "0")
+    for x in (m, twin):
+        x.Execute(int(w["tick_time"][1]))
+        x.Execute(int(w["tick_time"][2]))
+    for p in range(workload.N_INT + workload.N_FLT):
+        np.testing.assert_array_equal(m.read_prop(p), twin.read_prop(p))
+    np.testing.assert_array_equal(m.read_record(0), twin.read_record(0))
+    for a, b in zip(m.read_schedules(), twin.read_schedules()):
+        np.testing.assert_array_equal(a, b)
+    m.close()
+    twin.close()

@@ -65,6 +65,12 @@ def test_golden_fixtures_are_nontrivial():
     (12, dict(n_obj=300, n_scenes=1, groups_per_scene=4, players_per_group=5, records=True, rec_rows=64,
               rec_float_op=False, rec_skill_op=True, rec_set_frac=0.2, rec_set_float=False, spawn_frac=0.03,
               destroy_frac=0.03)),
+    # object (NFGUID) properties through the compiled NFCProperty::SetObject (PR:377): null GUIDs,
+    # unchanged values and head-only changes, beside rmw Sets, switches, create / destroy
+    (13, dict(n_obj=500, n_scenes=2, groups_per_scene=4, players_per_group=3, obj_props=True, obj_set_frac=0.12,
+              ext_frac=0.05, ext_props="all", rmw_frac=0.02, switch_frac=0.02, spawn_frac=0.03, destroy_frac=0.03)),
+    (14, dict(n_obj=300, n_scenes=1, groups_per_scene=2, players_per_group=30, obj_props=True, obj_set_frac=0.3,
+              ext_frac=0.0, host_ops=False)),
 ])
 def test_oracle_matches_reference(seed, kw):
     w = workload.make_world(n_ticks=9, seed=seed, **kw)
