@@ -189,6 +189,11 @@ public:
     bool CreateScene(int nSceneID);
     bool CreateObject(const NFGUID& self, int nSceneID, int nGroupID, const std::string& strClassName,
                       const std::map<std::string, TData>& init = {});
+    // Before AfterInit: an object's creation-time record contents (the rows game logic filled before
+    // the layout, cells [cols][rows] as int64 / f64 bit patterns, the used-row mask); they are the
+    // record's state at frame 0, not events.  After AfterInit use AddRow.
+    bool SetCreationRecord(const NFGUID& self, const std::string& strRecordName, uint64_t used,
+                           const std::vector<uint64_t>& cells);
     bool SetPropertyInt(const NFGUID& self, const std::string& name, int64_t v);
     bool SetPropertyFloat(const NFGUID& self, const std::string& name, double v);
     int64_t GetPropertyInt(const NFGUID& self, const std::string& name);
@@ -198,11 +203,21 @@ public:
     bool SetPropertyObject(const NFGUID& self, const std::string& name, const NFGUID& v);
     NFGUID GetPropertyObject(const NFGUID& self, const std::string& name);
     // NFIKernelModule::SetRecordInt / SetRecordFloat (NFIKernelModule.h:120-121): queued like the
-    // property setters and applied at the next Execute through NFCRecord::SetInt / SetFloat; true
-    // once queued (the reference also returns false for an unused row or an unchanged value,
-    // which is only known on the device: such a call changes nothing and raises no event)
+    // property setters and applied at the next Execute through NFCRecord::SetInt / SetFloat.  False
+    // for a row the record does not use (RC:194: its used-row mask as the reference holds it now,
+    // nfk_get_used_rows, one device read per (object, record) per frame); true once queued otherwise
+    // (the reference also returns false for a value the cell already holds: such a call changes
+    // nothing and raises no event)
     bool SetRecordInt(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol, int64_t nValue);
     bool SetRecordFloat(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol, double dwValue);
+    // Record rows (NFCRecord::AddRow / Remove / IsUsed, NFIKernelModule::ClearRecord; RC:111, 1086,
+    // 1209, KM:492), queued in call order with the SetRecord calls; Add / Del / Cover record events
+    // are delivered with the frame.  AddRow returns the row it takes (-1 = the first unused row; no
+    // unused row or a row outside the record: -1), values per column (none: the initial 0s).
+    int AddRow(const NFGUID& self, const std::string& strRecordName, int nRow, const std::vector<TData>& values = {});
+    bool RemoveRow(const NFGUID& self, const std::string& strRecordName, int nRow);
+    bool ClearRecord(const NFGUID& self, const std::string& strRecordName);
+    bool IsUsed(const NFGUID& self, const std::string& strRecordName, int nRow);
     // NFIKernelModule::GetRecordInt / GetRecordFloat (NFIKernelModule.h:134-135): read-your-writes
     // like GetProperty*; 0 for an unused row (NFCRecord::GetInt, RC:623)
     int64_t GetRecordInt(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol);
@@ -241,6 +256,7 @@ public:
 private:
     void check(int rc, const char* what) const;
     void DeliverEvents();
+    uint64_t UsedRows(const NFGUID& self, int rec);
     void TakeAddedSchedules();
     bool same_frame_ = true;
     int64_t pending_calls_ = 0;  // calls queued since the last device pass
@@ -263,6 +279,7 @@ private:
     std::vector<int32_t> scene_, group_;
     std::vector<uint8_t> cls_, isplayer_;
     std::vector<std::vector<uint64_t>> init_;
+    std::map<std::pair<int, int>, std::pair<uint64_t, std::vector<uint64_t>>> rec_init_;  // (object, record)
     // callbacks
     std::vector<PROPERTY_EVENT_FUNCTOR> common_prop_cb_;
     std::vector<RECORD_EVENT_FUNCTOR> common_rec_cb_;

@@ -117,7 +117,10 @@ typedef struct nfk_summary {
  * i < <x>_base[t+1] - <x>_base[t]; its rank in the global order is <x>_base[t] + i.  Walking
  * tiles in order and each tile's entries in order gives exactly the reference order:
  *   property events  (scene, group, guid, prop)
- *   record events    (scene, group, guid, rec, row, col); rrc = rec<<16 | row<<8 | col
+ *   record events    (scene, group, guid, rec, ...): per record its row events (AddRow / Remove /
+ *                    ClearRecord, in call order) then its cell Updates in (row, col) order;
+ *                    rrc = op<<24 | rec<<16 | row<<8 | col, op 0 = Update (RECORD_EVENT_DATA::Update,
+ *                    old / new the cell), 1 = Add, 2 = Del, 3 = Cover (row events: col 0, old = new = 0)
  *   fired heartbeats (scene, group, guid, kind)
  * Fan-out (GetBroadCastObject recipients): the messages of tile t (property tiles, then record
  * tiles) are one run of msg_cnt[t] recipients at msg_rcpt[msg_base[t]], in event order.  Runs
@@ -245,11 +248,32 @@ int nfk_get_objects(void* world, int32_t n, const int64_t* guid_head, const int6
 int nfk_set_records(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data, const int32_t* rec,
                     const int32_t* row, const int32_t* col, const uint8_t* is_float, const uint64_t* bits);
 
+/* ---- record row operations, queued in call order with the SetRecord calls:
+ *   op 1  NFCRecord::AddRow(row, values) (RC:111-180): row -1 = the first unused row (none: nothing
+ *         happens); a used row is covered (Cover event, else Add); values [n][NFK_MAX_REC_COLS] words
+ *         (NULL or a call without values: the record's initial values, 0), written without Update events
+ *   op 2  NFCRecord::Remove(row) (RC:1086-1107): a used row's Del event, then the row is unused (its
+ *         cells keep their values)
+ *   op 3  NFIKernelModule::ClearRecord (KM:492) -> NFCRecord::Clear (RC:1109): Remove of every row,
+ *         the last row first
+ * A Set on a row is accepted or refused by the row's used state at that call (RC:194).  The row
+ * events are delivered with the frame's record events (rrc op bits, see nfk_outputs).
+ * NFK_ERR_NOTFOUND for an unknown GUID, NFK_ERR_ARG for a row outside the record. */
+int nfk_record_rows(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data, const int32_t* rec,
+                    const int32_t* op, const int32_t* row, const uint64_t* values);
+
+/* NFCRecord::IsUsed (RC:1209) for n (object, record) pairs: the used-row masks as the reference holds
+ * them now — the device's after the last frame (one read per pair per window, cached until the next
+ * nfk_execute) with this window's queued row operations replayed in call order.  What AddRow(-1)
+ * would take is the lowest clear bit below the record's rows. */
+int nfk_get_used_rows(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data, const int32_t* rec,
+                      uint64_t* masks);
+
 /* ---- record reads: NFIKernelModule::GetRecordInt/Float (NFIKernelModule.h:134-135) ----
  * NFCRecord::GetInt / GetFloat (RC:616): the cell after the last frame (waits for the world's
- * stream; one 8-byte device read of the used-row mask and one of the cell per query) with this
- * window's queued SetRecord* calls on it applied in call order (read-your-writes); 0 for a row
- * the record does not use.  NFK_ERR_NOTFOUND / NFK_ERR_ARG as nfk_set_records. */
+ * stream; the used-row masks and cells of all queries in one gather) with this window's queued
+ * SetRecord* and row operations on the record replayed in call order (read-your-writes); 0 for a
+ * row the record does not use.  NFK_ERR_NOTFOUND / NFK_ERR_ARG as nfk_set_records. */
 int nfk_get_records(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data, const int32_t* rec,
                     const int32_t* row, const int32_t* col, uint64_t* bits);
 

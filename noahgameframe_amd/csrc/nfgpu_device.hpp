@@ -177,7 +177,24 @@ struct Dev {
     const uint64_t* rs_bits;
     uint64_t* rs_old;
     uint64_t* rs_new;
-    int32_t n_rs;              // groups
+    uint8_t* rs_has;           // the group's calls logged an Update: rs_old / rs_new = first old / last new
+    int32_t n_rs;              // groups (rs_rrc bit 31: a group of a row-operation list, run by k_rrows)
+    // record row operations (NFCRecord::AddRow / Remove, NFCKernelModule::ClearRecord) of this window:
+    // one LIST per (slot, record) with row operations, sorted by (slot, record); a list's calls (its
+    // row operations and that pair's SetRecord calls) in call order.  k_rrows runs each list; its row
+    // events (op << 8 | row) go to rl_ev[rl_ev0[l] ...], rl_cnt[l] of them.
+    int32_t n_rl;
+    const uint32_t* rl_slot;
+    const uint32_t* rl_rec;
+    const uint32_t* rl_c0;     // [n_rl + 1] call range
+    const uint32_t* rl_ev0;
+    uint32_t* rl_cnt;
+    uint32_t* rl_ev;
+    const uint32_t* rc_code;   // op | row << 8 | col << 16 (op 0 SetRecord, 1 AddRow (row 0xFF: -1), 2 Remove, 3 Clear)
+    const uint32_t* rc_aux;    // SetRecord: its group; AddRow: its values' index (0xFFFFFFFF: the initial 0s)
+    const uint64_t* rc_bits;   // SetRecord: the value
+    const uint64_t* rvals;     // AddRow values [][NFK_MAX_REC_COLS]
+    const uint32_t* rss_l0;    // [n_rss] the slot's first list
     // the slots with groups (k_rset_slots: one wave each), their first group, and per slot its
     // record events and messages (counted before k_records) and where k_records placed them
     const uint32_t* rss_slot;

@@ -249,8 +249,16 @@ struct World {
     std::vector<uint64_t> xpk, xpk_t, hpk, hpk_t;  // packed (key << 32 | call index) sort scratch
     // queued SetRecordInt / SetRecordFloat calls (obj: object index until nfk_execute resolves it;
     // rrc = rec << 16 | row << 8 | col) and their folding scratch
-    struct RSOp { uint32_t obj, rrc; uint64_t bits; };
+    // op 0 SetRecord*, 1 AddRow (row 0xFF: -1; aux = its values' index in rvals, or 0xFFFFFFFF),
+    // 2 Remove, 3 ClearRecord
+    struct RSOp { uint32_t obj, rrc; uint64_t bits; uint32_t op, aux; };
     std::vector<RSOp> rsq;
+    std::vector<uint64_t> rvals;  // AddRow values, NFK_MAX_REC_COLS words each
+    std::unordered_map<uint64_t, std::vector<uint32_t>> rq_index;  // (object << 3 | record) -> its queued calls
+    std::unordered_map<uint64_t, uint64_t> ucache;  // (object << 3 | record) -> used mask read this window
+    std::vector<uint64_t> rowpairs;  // (slot << 3 | record) with row operations this window (nfk_execute)
+    void* rl_buf = nullptr;          // rs_has / rl_cnt / rl_ev
+    size_t rl_cap = 0;
     std::vector<uint64_t> rpk, rpk_t;
     std::vector<uint32_t> rs_slot_h, rs_rrc_h, rs_first_h, rss_slot_h, rss_g0_h;
     void* rs_buf = nullptr;   // rs_old / rs_new
@@ -316,6 +324,9 @@ int drop_window(World* w, int r) {
     w->xops_h.clear();
     w->hops.clear();
     w->rsq.clear();
+    w->rvals.clear();
+    w->rq_index.clear();
+    w->ucache.clear();
     w->dcache.clear();
     w->ov_last.clear();
     w->ov_prev.clear();
@@ -1968,9 +1979,136 @@ int nfk_set_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     for (int32_t i = 0; i < n; i++) {
         // NFCRecord::SetInt / SetFloat on a column of the other type write nothing (RC:189 / RC:250)
         if (is_float && (is_float[i] != 0) != (w->rec_ctype[rec[i]][col[i]] != 0)) continue;
+        w->rq_index[((uint64_t)w->look[i] << 3) | (uint32_t)rec[i]].push_back((uint32_t)w->rsq.size());
         w->rsq.push_back(World::RSOp{(uint32_t)w->look[i], ((uint32_t)rec[i] << 16) | ((uint32_t)row[i] << 8) | (uint32_t)col[i],
-                                     bits[i]});
+                                     bits[i], 0u, 0u});
     }
+    return NFK_OK;
+}
+
+int nfk_record_rows(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* rec, const int32_t* op,
+                    const int32_t* row, const uint64_t* values) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !rec || !op || !row))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    w->look.resize(n);
+    w->obj_of.find_many(n, gh, gd, w->look.data());
+    for (int32_t i = 0; i < n; i++) {
+        if (w->look[i] < 0)  // FindRecord: "There is no object" (KM:487)
+            return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
+        const int32_t r = rec[i];
+        if (r < 0 || r >= w->cfg.n_rec || !w->rec_defined[r] || op[i] < 1 || op[i] > 3)
+            return fail(NFK_ERR_ARG, "bad record or row operation");
+        if ((op[i] == 1 && (row[i] < -1 || row[i] >= w->tab.rec_rows[r])) ||
+            (op[i] == 2 && (row[i] < 0 || row[i] >= w->tab.rec_rows[r])))
+            return fail(NFK_ERR_ARG, "row out of range");
+    }
+    for (int32_t i = 0; i < n; i++) {
+        uint32_t aux = 0;
+        const uint32_t rr = op[i] == 3 ? 0u : (row[i] < 0 ? 0xFFu : (uint32_t)row[i]);
+        if (op[i] == 1) {
+            aux = 0xFFFFFFFFu;
+            if (values) {
+                aux = (uint32_t)(w->rvals.size() / NFK_MAX_REC_COLS);
+                w->rvals.insert(w->rvals.end(), values + (size_t)i * NFK_MAX_REC_COLS,
+                                values + (size_t)(i + 1) * NFK_MAX_REC_COLS);
+            }
+        }
+        w->rq_index[((uint64_t)w->look[i] << 3) | (uint32_t)rec[i]].push_back((uint32_t)w->rsq.size());
+        w->rsq.push_back(World::RSOp{(uint32_t)w->look[i], ((uint32_t)rec[i] << 16) | (rr << 8), 0ull, (uint32_t)op[i], aux});
+    }
+    return NFK_OK;
+}
+
+// device address of object o's used-row mask of record r (its import row in this window, or its slot)
+static int used_addr(World* w, int32_t o, int32_t r, const uint64_t** used) {
+    const int rows = w->tab.rec_rows[r], cols = w->tab.rec_cols[r];
+    if (w->src_row[o] >= 0) {
+        int64_t off = w->n_pw + 4 * w->cfg.n_kind;
+        for (int x = 0; x < r; x++) off += (int64_t)w->tab.rec_rows[x] * w->tab.rec_cols[x] + 1;
+        *used = w->ins_rows + (size_t)w->src_row[o] * w->row_words + off + (size_t)rows * cols;
+    } else if (w->slot_of_obj[o] >= 0) {
+        *used = w->d.rused[r] + w->slot_of_obj[o];
+    } else {
+        return fail(NFK_ERR_STATE, "object without a slot");
+    }
+    return NFK_OK;
+}
+
+// 8-byte device words at absolute addresses (waits for the world's stream)
+static int read_abs(World* w, const std::vector<uint64_t>& addr, uint64_t* got) {
+    if (addr.empty()) return NFK_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    if (addr.size() <= 4) {
+        for (size_t q = 0; q < addr.size(); q++)
+            HIPCHK(hipMemcpy(&got[q], (const void*)(uintptr_t)addr[q], 8, hipMemcpyDeviceToHost));
+        return NFK_OK;
+    }
+    int r = dev_reserve(w, (void**)&w->gat, &w->gat_cap, addr.size() * 16);
+    if (r) return r;
+    HIPCHK(hipMemcpy(w->gat, addr.data(), addr.size() * 8, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_gather_abs, dim3((unsigned)((addr.size() + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream,
+                       (const uint64_t*)w->gat, (int32_t)addr.size(), w->gat + addr.size());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(got, w->gat + addr.size(), addr.size() * 8, hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    return NFK_OK;
+}
+
+// the queued row operations of (object o, record r) replayed on a used-row mask
+static uint64_t replay_rows(const World* w, int32_t o, int32_t r, uint64_t u) {
+    auto it = w->rq_index.find(((uint64_t)o << 3) | (uint32_t)r);
+    if (it == w->rq_index.end()) return u;
+    const int rows = w->tab.rec_rows[r];
+    for (uint32_t k : it->second) {
+        const World::RSOp& x = w->rsq[k];
+        const int xr = (int)((x.rrc >> 8) & 0xFF);
+        if (x.op == 1) {
+            if (xr == 0xFF) {
+                const uint64_t fr = ~u & (rows >= 64 ? ~0ull : ((1ull << rows) - 1));
+                if (fr) u |= fr & (~fr + 1);
+            } else {
+                u |= 1ull << xr;
+            }
+        } else if (x.op == 2) {
+            u &= ~(1ull << xr);
+        } else if (x.op == 3) {
+            u = 0;
+        }
+    }
+    return u;
+}
+
+int nfk_get_used_rows(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* rec, uint64_t* masks) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!gh || !gd || !rec || !masks))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    std::vector<int32_t> obj(n);
+    w->obj_of.find_many(n, gh, gd, obj.data());
+    std::vector<uint64_t> addr;
+    std::vector<int32_t> miss;
+    for (int32_t i = 0; i < n; i++) {
+        if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
+        if (rec[i] < 0 || rec[i] >= w->cfg.n_rec || !w->rec_defined[rec[i]]) return fail(NFK_ERR_ARG, "bad record");
+        auto it = w->ucache.find(((uint64_t)obj[i] << 3) | (uint32_t)rec[i]);
+        if (it != w->ucache.end()) {
+            masks[i] = it->second;
+            continue;
+        }
+        const uint64_t* u;
+        int r = used_addr(w, obj[i], rec[i], &u);
+        if (r) return r;
+        addr.push_back((uint64_t)(uintptr_t)u);
+        miss.push_back(i);
+    }
+    std::vector<uint64_t> got(addr.size());
+    int r = read_abs(w, addr, got.data());
+    if (r) return r;
+    for (size_t q = 0; q < miss.size(); q++) {
+        masks[miss[q]] = got[q];
+        w->ucache[((uint64_t)obj[miss[q]] << 3) | (uint32_t)rec[miss[q]]] = got[q];
+    }
+    for (int32_t i = 0; i < n; i++) masks[i] = replay_rows(w, obj[i], rec[i], masks[i]);
     return NFK_OK;
 }
 
@@ -1988,10 +2126,8 @@ int nfk_get_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd
             col[i] < 0 || col[i] >= w->tab.rec_cols[r])
             return fail(NFK_ERR_ARG, "record cell out of range");
     }
-    // the queued SetRecord calls of each (object, cell), in call order
-    std::unordered_map<uint64_t, std::vector<uint32_t>> q;
-    for (size_t k = 0; k < w->rsq.size(); k++) q[((uint64_t)w->rsq[k].obj << 19) | w->rsq[k].rrc].push_back((uint32_t)k);
-    HIPCHK(hipStreamSynchronize(w->stream));
+    // every query's used-row mask and cell, in one gather (a few single reads for small n)
+    std::vector<uint64_t> addr(2 * (size_t)n), got(2 * (size_t)n);
     for (int32_t i = 0; i < n; i++) {
         const int32_t o = obj[i], r = rec[i], rows = w->tab.rec_rows[r], cols = w->tab.rec_cols[r];
         const uint64_t* cell;
@@ -2009,29 +2145,53 @@ int nfk_get_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd
         } else {
             return fail(NFK_ERR_STATE, "object without a slot");
         }
-        uint64_t c = 0, u = 0;
-        HIPCHK(hipMemcpy(&u, used, 8, hipMemcpyDeviceToHost));
-        if (!((u >> row[i]) & 1)) {  // NFCRecord::GetInt / GetFloat of an unused row (RC:623): 0
-            bits[i] = 0;
-            continue;
-        }
-        HIPCHK(hipMemcpy(&c, cell, 8, hipMemcpyDeviceToHost));
-        // this window's queued Sets of the cell on top (RC:182 / RC:243)
-        auto it = q.find(((uint64_t)o << 19) | ((uint32_t)r << 16) | ((uint32_t)row[i] << 8) | (uint32_t)col[i]);
-        if (it != q.end())
+        addr[2 * (size_t)i] = (uint64_t)(uintptr_t)used;
+        addr[2 * (size_t)i + 1] = (uint64_t)(uintptr_t)cell;
+    }
+    {
+        int r = read_abs(w, addr, got.data());
+        if (r) return r;
+    }
+    for (int32_t i = 0; i < n; i++) {
+        const int32_t o = obj[i], r = rec[i], rows = w->tab.rec_rows[r];
+        uint64_t u = got[2 * (size_t)i], c = got[2 * (size_t)i + 1];
+        // this window's queued calls on the record replayed in call order: SetRecord* through
+        // RC:182 / RC:243 on the row's used state at that call, AddRow / Remove / ClearRecord on the
+        // used-row mask (RC:111, RC:1086, RC:1109)
+        auto it = w->rq_index.find(((uint64_t)o << 3) | (uint32_t)r);
+        if (it != w->rq_index.end())
             for (uint32_t k : it->second) {
-                const uint64_t b = w->rsq[k].bits;
-                if (w->rec_ctype[r][col[i]]) {
-                    double bd, cd;
-                    memcpy(&bd, &b, 8);
-                    memcpy(&cd, &c, 8);
-                    const double df = bd - cd;
-                    if (!(df < 0.001 && df > -0.001)) c = b;
+                const World::RSOp& x = w->rsq[k];
+                const int xr = (int)((x.rrc >> 8) & 0xFF), xc = (int)(x.rrc & 0xFF);
+                if (x.op == 0) {
+                    if (xr != row[i] || xc != col[i] || !((u >> xr) & 1)) continue;
+                    const uint64_t b = x.bits;
+                    if (w->rec_ctype[r][col[i]]) {
+                        double bd, cd;
+                        memcpy(&bd, &b, 8);
+                        memcpy(&cd, &c, 8);
+                        const double df = bd - cd;
+                        if (!(df < 0.001 && df > -0.001)) c = b;
+                    } else {
+                        c = b;
+                    }
+                } else if (x.op == 1) {
+                    int rr = xr;
+                    if (xr == 0xFF) {
+                        const uint64_t fr = ~u & (rows >= 64 ? ~0ull : ((1ull << rows) - 1));
+                        if (!fr) continue;
+                        rr = __builtin_ctzll(fr);
+                    }
+                    u |= 1ull << rr;
+                    if (rr == row[i]) c = x.aux == 0xFFFFFFFFu ? 0ull : w->rvals[(size_t)x.aux * NFK_MAX_REC_COLS + col[i]];
+                } else if (x.op == 2) {
+                    u &= ~(1ull << xr);
                 } else {
-                    c = b;
+                    u = 0;
                 }
             }
-        bits[i] = c;
+        // NFCRecord::GetInt / GetFloat of an unused row (RC:623): 0
+        bits[i] = ((u >> row[i]) & 1) ? c : 0;
     }
     return NFK_OK;
 }
@@ -2586,8 +2746,11 @@ int nfk_execute(void* world, int64_t now_ms) {
         }
     }
     // SetRecordInt / SetRecordFloat: (slot, cell) groups, each group's calls in call order (key
-    // slot << 19 | rec << 16 | row << 8 | col); the slots with groups, in slot order, each run by
-    // k_rset_slots; the most groups of one record tile bounds that tile's extra events
+    // slot << 19 | rec << 16 | row << 8 | col).  Record row operations (AddRow / Remove /
+    // ClearRecord): one list per (slot, record) that has any, with every call on that pair (its
+    // SetRecord calls too, whose groups k_rsets then leaves to k_rrows: rs_rrc bit 31) in call
+    // order.  The slots with groups or lists, in slot order, are each run by k_rset_slots; a record
+    // tile's extra events are bounded by its groups plus its lists' row events.
     const size_t n_rq = w->rsq.size();
     std::vector<uint32_t>& rs_slot = w->rs_slot_h;
     std::vector<uint32_t>& rs_rrc = w->rs_rrc_h;
@@ -2599,16 +2762,35 @@ int nfk_execute(void* world, int64_t now_ms) {
     rs_first.clear();
     rss_slot.clear();
     rss_g0.clear();
+    std::vector<uint32_t> rss_l0, rl_slot, rl_rec, rl_c0, rl_ev0, rc_code, rc_aux;
+    std::vector<uint64_t> rc_bits;
+    std::vector<uint64_t>& rowpairs = w->rowpairs;
+    rowpairs.clear();
     std::vector<uint64_t>& rpk = w->rpk;
     rpk.clear();
     const int rib = bits_for(n_rq);
     const uint64_t rim = (1ull << rib) - 1;
     int64_t max_rs_tile = 0;
+    size_t n_rev = 0;  // row-event bound of the window
     if (n_rq) {
+        for (size_t i = 0; i < n_rq; i++)
+            if (w->rsq[i].op) {
+                const int32_t sl = w->slot_of_obj[w->rsq[i].obj];
+                if (sl >= 0) rowpairs.push_back(((uint64_t)(uint32_t)sl << 3) | (w->rsq[i].rrc >> 16));
+            }
+        std::sort(rowpairs.begin(), rowpairs.end());
+        rowpairs.erase(std::unique(rowpairs.begin(), rowpairs.end()), rowpairs.end());
+        auto pair_of = [&](uint32_t sl, uint32_t rec) -> int64_t {
+            if (rowpairs.empty()) return -1;
+            const uint64_t key = ((uint64_t)sl << 3) | rec;
+            auto it = std::lower_bound(rowpairs.begin(), rowpairs.end(), key);
+            return (it != rowpairs.end() && *it == key) ? (int64_t)(it - rowpairs.begin()) : -1;
+        };
         rpk.resize(n_rq);
         uint64_t kor = 0;
         size_t k = 0;
         for (size_t i = 0; i < n_rq; i++) {
+            if (w->rsq[i].op) continue;
             const int32_t sl = w->slot_of_obj[w->rsq[i].obj];
             if (sl < 0) continue;  // destroyed / exported in this window
             const uint64_t key = ((uint64_t)(uint32_t)sl << 19) | w->rsq[i].rrc;
@@ -2619,28 +2801,96 @@ int nfk_execute(void* world, int64_t now_ms) {
         if (bits_for(kor) + rib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued SetRecord calls"));
         radix_sort_packed(rpk, w->rpk_t, rib, bits_for(kor));
         uint64_t prev = ~0ull;
-        uint32_t prev_slot = 0xFFFFFFFFu, cur_rt = 0xFFFFFFFFu;
-        int64_t tile_groups = 0;
         for (size_t i = 0; i < k; i++) {
             const uint64_t key = rpk[i] >> rib;
             if (key == prev) continue;
             prev = key;
-            const uint32_t sl = (uint32_t)(key >> 19);
-            if (sl != prev_slot) {
-                prev_slot = sl;
-                rss_slot.push_back(sl);
-                rss_g0.push_back((uint32_t)rs_slot.size());
-            }
-            if (sl / kRTile != cur_rt) {
-                cur_rt = sl / kRTile;
-                tile_groups = 0;
-            }
-            max_rs_tile = std::max(max_rs_tile, ++tile_groups);
+            const uint32_t sl = (uint32_t)(key >> 19), rrc = (uint32_t)(key & 0x7FFFF);
             rs_slot.push_back(sl);
-            rs_rrc.push_back((uint32_t)(key & 0x7FFFF));
+            rs_rrc.push_back(rrc | (pair_of(sl, rrc >> 16) >= 0 ? 0x80000000u : 0u));
             rs_first.push_back((uint32_t)i);
         }
         rs_first.push_back((uint32_t)k);
+        // the row-operation lists (one per pair, pair order), their calls in call order
+        const size_t npair = rowpairs.size();
+        if (npair) {
+            std::vector<uint32_t> cnt(npair + 1, 0);
+            std::vector<int64_t> call_pair(n_rq, -1);
+            for (size_t i = 0; i < n_rq; i++) {
+                const int32_t sl = w->slot_of_obj[w->rsq[i].obj];
+                if (sl < 0) continue;
+                call_pair[i] = pair_of((uint32_t)sl, w->rsq[i].rrc >> 16);
+                if (call_pair[i] >= 0) cnt[call_pair[i]]++;
+            }
+            rl_c0.assign(npair + 1, 0);
+            for (size_t q = 0; q < npair; q++) rl_c0[q + 1] = rl_c0[q] + cnt[q];
+            rc_code.assign(rl_c0[npair], 0);
+            rc_aux.assign(rl_c0[npair], 0);
+            rc_bits.assign(rl_c0[npair], 0);
+            rl_ev0.assign(npair, 0);
+            std::vector<uint32_t> fill(rl_c0.begin(), rl_c0.end() - 1), evb(npair, 0);
+            for (size_t i = 0; i < n_rq; i++) {
+                if (call_pair[i] < 0) continue;
+                const World::RSOp& x = w->rsq[i];
+                const int64_t q = call_pair[i];
+                const uint32_t at = fill[q]++;
+                const uint32_t rec = x.rrc >> 16, row = (x.rrc >> 8) & 0xFF, col = x.rrc & 0xFF;
+                rc_code[at] = x.op | (row << 8) | (col << 16);
+                rc_bits[at] = x.bits;
+                if (x.op == 0) {  // its cell's group (binary search over the sorted groups)
+                    const uint64_t key = ((uint64_t)(rowpairs[q] >> 3) << 19) | (x.rrc & 0x7FFFF);
+                    size_t lo = 0, hi = rs_slot.size();
+                    while (lo < hi) {
+                        const size_t m = (lo + hi) / 2;
+                        const uint64_t km = ((uint64_t)rs_slot[m] << 19) | (rs_rrc[m] & 0x7FFFF);
+                        if (km < key) lo = m + 1;
+                        else hi = m;
+                    }
+                    rc_aux[at] = (uint32_t)lo;
+                } else {
+                    rc_aux[at] = x.aux;
+                    evb[q] += x.op == 3 ? (uint32_t)w->tab.rec_rows[rec] : 1u;
+                }
+            }
+            for (size_t q = 0; q < npair; q++) {
+                rl_slot.push_back((uint32_t)(rowpairs[q] >> 3));
+                rl_rec.push_back((uint32_t)(rowpairs[q] & 7));
+                rl_ev0[q] = (uint32_t)n_rev;
+                n_rev += evb[q];
+            }
+            // the tile bound: per record tile, its groups plus its lists' row-event bounds
+            std::vector<std::pair<uint32_t, uint32_t>> per_tile;  // (record tile, events)
+            for (size_t g = 0; g < rs_slot.size(); g++) per_tile.push_back({rs_slot[g] / kRTile, 1u});
+            for (size_t q = 0; q < npair; q++) per_tile.push_back({rl_slot[q] / kRTile, evb[q]});
+            std::sort(per_tile.begin(), per_tile.end());
+            for (size_t a = 0; a < per_tile.size();) {
+                int64_t t = 0;
+                size_t b = a;
+                for (; b < per_tile.size() && per_tile[b].first == per_tile[a].first; b++) t += per_tile[b].second;
+                max_rs_tile = std::max(max_rs_tile, t);
+                a = b;
+            }
+        } else {
+            uint32_t cur_rt = 0xFFFFFFFFu;
+            int64_t tile_groups = 0;
+            for (size_t g = 0; g < rs_slot.size(); g++) {
+                if (rs_slot[g] / kRTile != cur_rt) {
+                    cur_rt = rs_slot[g] / kRTile;
+                    tile_groups = 0;
+                }
+                max_rs_tile = std::max(max_rs_tile, ++tile_groups);
+            }
+        }
+        // the slots with record work: groups or lists, in slot order
+        for (size_t gi = 0, pi = 0; gi < rs_slot.size() || pi < rl_slot.size();) {
+            const uint32_t sl = std::min(gi < rs_slot.size() ? rs_slot[gi] : 0xFFFFFFFFu,
+                                         pi < rl_slot.size() ? rl_slot[pi] : 0xFFFFFFFFu);
+            rss_slot.push_back(sl);
+            rss_g0.push_back((uint32_t)gi);
+            rss_l0.push_back((uint32_t)pi);
+            while (gi < rs_slot.size() && rs_slot[gi] == sl) gi++;
+            while (pi < rl_slot.size() && rl_slot[pi] == sl) pi++;
+        }
         // a record tile's events: its slots' record-program cells plus its SetRecord groups
         int64_t cells = 0;
         for (int j = 0; j < d.n_rops; j++) cells += d.rops[j].rows;
@@ -2763,18 +3013,28 @@ int nfk_execute(void* world, int64_t now_ms) {
     size_t off_ss = align16(off_rb + nrc * 8), off_sg = align16(off_ss + nrss * 4);
     const bool objs = w->cfg.n_obj > 0;
     size_t off_xh = align16(off_sg + nrss * 4);  // head halves of the calls (object properties)
-    size_t total = align16(off_xh + (objs ? nxc * 8 : 0));
+    // record row-operation lists
+    const size_t nrl = rl_slot.size(), nrcall = rc_code.size(), nval = w->rvals.size();
+    size_t off_l0 = align16(off_xh + (objs ? nxc * 8 : 0)), off_ls = align16(off_l0 + (nrl ? nrss * 4 : 0));
+    size_t off_lr = align16(off_ls + nrl * 4), off_lc = align16(off_lr + nrl * 4);
+    size_t off_le = align16(off_lc + (nrl ? (nrl + 1) * 4 : 0)), off_cc = align16(off_le + nrl * 4);
+    size_t off_ca = align16(off_cc + nrcall * 4), off_cb = align16(off_ca + nrcall * 4);
+    size_t off_rv = align16(off_cb + nrcall * 8);
+    size_t total = align16(off_rv + (nrl ? nval * 8 : 0));
     if (ng) {
         int r = dev_reserve(w, (void**)&w->xs_buf, &w->xs_cap, ng * (objs ? 32 : 16));
         if (r) return drop_window(w, r);
     }
-    if (ngr) {
-        int r = dev_reserve(w, (void**)&w->rs_buf, &w->rs_cap, ngr * 16);
+    if (nrss) {
+        int r = dev_reserve(w, (void**)&w->rs_buf, &w->rs_cap, std::max<size_t>(ngr, 1) * 16);
         if (r) return drop_window(w, r);
         r = dev_reserve(w, (void**)&w->rss_buf, &w->rss_cap, nrss * 16);
         if (r) return drop_window(w, r);
+        // rs_has [ngr] bytes, then (with lists) rl_cnt [nrl] and rl_ev [row-event bound]
+        r = dev_reserve(w, &w->rl_buf, &w->rl_cap, align16(std::max<size_t>(ngr, 1)) + (nrl + n_rev + 1) * 4);
+        if (r) return drop_window(w, r);
     }
-    if (total > 0 && (ng || npre || npost || ngr)) {
+    if (total > 0 && (ng || npre || npost || nrss)) {
         int r = pin_reserve(w, total);
         if (r) return drop_window(w, r);
         char* P = (char*)w->pin;
@@ -2793,7 +3053,7 @@ int nfk_execute(void* world, int64_t now_ms) {
             ((uint32_t*)(P + off_ps))[i] = pre_slot[i];
             ((uint32_t*)(P + off_po))[i] = pre_op[i];
         }
-        if (ngr) {
+        if (nrss) {
             memcpy(P + off_rs, rs_slot.data(), ngr * 4);
             memcpy(P + off_rr, rs_rrc.data(), ngr * 4);
             memcpy(P + off_rf, rs_first.data(), (ngr + 1) * 4);
@@ -2801,6 +3061,17 @@ int nfk_execute(void* world, int64_t now_ms) {
             for (size_t i = 0; i < nrc; i++) rb[i] = w->rsq[rpk[i] & rim].bits;
             memcpy(P + off_ss, rss_slot.data(), nrss * 4);
             memcpy(P + off_sg, rss_g0.data(), nrss * 4);
+        }
+        if (nrl) {
+            memcpy(P + off_l0, rss_l0.data(), nrss * 4);
+            memcpy(P + off_ls, rl_slot.data(), nrl * 4);
+            memcpy(P + off_lr, rl_rec.data(), nrl * 4);
+            memcpy(P + off_lc, rl_c0.data(), (nrl + 1) * 4);
+            memcpy(P + off_le, rl_ev0.data(), nrl * 4);
+            memcpy(P + off_cc, rc_code.data(), nrcall * 4);
+            memcpy(P + off_ca, rc_aux.data(), nrcall * 4);
+            memcpy(P + off_cb, rc_bits.data(), nrcall * 8);
+            if (nval) memcpy(P + off_rv, w->rvals.data(), nval * 8);
         }
         for (size_t i = 0; i < npost; i++) {
             ((uint32_t*)(P + off_qs))[i] = post[i].slot;
@@ -2828,19 +3099,35 @@ int nfk_execute(void* world, int64_t now_ms) {
     d.x_new_h = ng && objs ? (uint64_t*)w->xs_buf + 3 * ng : nullptr;
     d.n_rs = (int32_t)ngr;
     d.n_rss = (int32_t)nrss;
-    d.rs_slot = ngr ? (const uint32_t*)(S + off_rs) : nullptr;
-    d.rs_rrc = ngr ? (const uint32_t*)(S + off_rr) : nullptr;
-    d.rs_first = ngr ? (const uint32_t*)(S + off_rf) : nullptr;
-    d.rs_bits = ngr ? (const uint64_t*)(S + off_rb) : nullptr;
-    d.rss_slot = ngr ? (const uint32_t*)(S + off_ss) : nullptr;
-    d.rss_g0 = ngr ? (const uint32_t*)(S + off_sg) : nullptr;
-    d.rs_old = ngr ? (uint64_t*)w->rs_buf : nullptr;
-    d.rs_new = ngr ? (uint64_t*)w->rs_buf + ngr : nullptr;
-    d.rss_ev = ngr ? (uint32_t*)w->rss_buf : nullptr;
-    d.rss_msg = ngr ? (uint32_t*)w->rss_buf + nrss : nullptr;
-    d.rss_pos = ngr ? (uint32_t*)w->rss_buf + 2 * nrss : nullptr;
-    d.rss_pmsg = ngr ? (uint32_t*)w->rss_buf + 3 * nrss : nullptr;
+    d.rs_slot = nrss ? (const uint32_t*)(S + off_rs) : nullptr;
+    d.rs_rrc = nrss ? (const uint32_t*)(S + off_rr) : nullptr;
+    d.rs_first = nrss ? (const uint32_t*)(S + off_rf) : nullptr;
+    d.rs_bits = nrss ? (const uint64_t*)(S + off_rb) : nullptr;
+    d.rss_slot = nrss ? (const uint32_t*)(S + off_ss) : nullptr;
+    d.rss_g0 = nrss ? (const uint32_t*)(S + off_sg) : nullptr;
+    d.rs_old = nrss ? (uint64_t*)w->rs_buf : nullptr;
+    d.rs_new = nrss ? (uint64_t*)w->rs_buf + ngr : nullptr;
+    d.rs_has = nrss ? (uint8_t*)w->rl_buf : nullptr;
+    d.rss_ev = nrss ? (uint32_t*)w->rss_buf : nullptr;
+    d.rss_msg = nrss ? (uint32_t*)w->rss_buf + nrss : nullptr;
+    d.rss_pos = nrss ? (uint32_t*)w->rss_buf + 2 * nrss : nullptr;
+    d.rss_pmsg = nrss ? (uint32_t*)w->rss_buf + 3 * nrss : nullptr;
+    d.n_rl = (int32_t)nrl;
+    d.rss_l0 = nrl ? (const uint32_t*)(S + off_l0) : nullptr;
+    d.rl_slot = nrl ? (const uint32_t*)(S + off_ls) : nullptr;
+    d.rl_rec = nrl ? (const uint32_t*)(S + off_lr) : nullptr;
+    d.rl_c0 = nrl ? (const uint32_t*)(S + off_lc) : nullptr;
+    d.rl_ev0 = nrl ? (const uint32_t*)(S + off_le) : nullptr;
+    d.rc_code = nrl ? (const uint32_t*)(S + off_cc) : nullptr;
+    d.rc_aux = nrl ? (const uint32_t*)(S + off_ca) : nullptr;
+    d.rc_bits = nrl ? (const uint64_t*)(S + off_cb) : nullptr;
+    d.rvals = nrl ? (const uint64_t*)(S + off_rv) : nullptr;
+    d.rl_cnt = nrl ? (uint32_t*)((char*)w->rl_buf + align16(std::max<size_t>(ngr, 1))) : nullptr;
+    d.rl_ev = nrl ? d.rl_cnt + nrl : nullptr;
     w->rsq.clear();
+    w->rvals.clear();
+    w->rq_index.clear();
+    w->ucache.clear();
     w->xops.clear();
     w->xops_h.clear();
     w->hops.clear();
@@ -2855,12 +3142,15 @@ int nfk_execute(void* world, int64_t now_ms) {
         w->post_kind.push_back(q.kind);
     }
     d.has_pre = npre > 0;
-    if (ng || npre || ngr) {
+    if (ng || npre || nrss) {
         TimeScope ts(w, KT_AUX);
-        if (ngr) {
+        if (nrss) {
             hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)((nrss + 255) / 256)), dim3(256), 0, w->stream,
                                d.rss_slot, (int32_t)nrss, d.rs_head);
-            hipLaunchKernelGGL(k_rsets, dim3((unsigned)((ngr + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, d);
+            if (ngr)
+                hipLaunchKernelGGL(k_rsets, dim3((unsigned)((ngr + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, d);
+            if (nrl)  // after k_rsets: it clears the has-flags of the lists' groups
+                hipLaunchKernelGGL(k_rrows, dim3((unsigned)((nrl + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, d);
         }
         if (ng) {
             hipLaunchKernelGGL(k_ext_scatter, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, w->stream,
@@ -2899,7 +3189,7 @@ int nfk_execute(void* world, int64_t now_ms) {
                 }
             };
             for (int j = 0; j < d.n_rops; j++) rper(d.rops[j].rec);
-            if (ngr)  // SetRecord groups may hit any record
+            if (nrss)  // SetRecord groups and row operations may hit any record
                 for (int r = 0; r < d.n_rec; r++)
                     if (w->rec_defined[r]) rper(r);
             rtcap = (((int64_t)kRTile * cells + max_rs_tile) * per + 3) & ~(int64_t)3;  // (16-byte aligned runs)

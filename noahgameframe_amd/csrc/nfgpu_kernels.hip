@@ -444,6 +444,8 @@ __global__ __launch_bounds__(kTPB) void k_rsets(Dev d) {
     const int g = blockIdx.x * kTPB + threadIdx.x;
     if (g >= d.n_rs) return;
     const uint32_t e = d.rs_slot[g], rrc = d.rs_rrc[g];
+    d.rs_has[g] = 0;
+    if (rrc >> 31) return;  // a row-operation list's cell: k_rrows applies its calls in call order
     const int r = (int)(rrc >> 16), row = (int)((rrc >> 8) & 0xFF), col = (int)(rrc & 0xFF);
     const int rows = d.tab->rec_rows[r], cols = d.tab->rec_cols[r];
     uint64_t* cells = nullptr;
@@ -459,19 +461,105 @@ __global__ __launch_bounds__(kTPB) void k_rsets(Dev d) {
     uint64_t v = c0;
     if ((usedp[e] >> row) & 1) {
         const bool f64 = d.tab->rec_ctype[r][col] != 0;
+        bool logged = false;
         for (uint32_t k = d.rs_first[g]; k < d.rs_first[g + 1]; k++) {
             const uint64_t x = d.rs_bits[k];
             if (f64) {
                 const double df = __longlong_as_double((long long)x) - __longlong_as_double((long long)v);
-                if (!(df < 0.001 && df > -0.001)) v = x;
+                if (!(df < 0.001 && df > -0.001)) {
+                    v = x;
+                    logged = true;
+                }
             } else if (x != v) {
                 v = x;
+                logged = true;
             }
         }
         if (v != c0) *cell = v;
+        d.rs_has[g] = logged ? 1 : 0;
     }
     d.rs_old[g] = c0;
     d.rs_new[g] = v;
+}
+
+// Record row operations between frames, one thread per (slot, record) list, every call of the
+// list in call order on the cells and the used-row mask:
+//   SetRecordInt / Float (RC:182 / RC:243): as k_rsets, on the row's used state at that call;
+//       the cell's group keeps the first logged old value and the last logged new one;
+//   AddRow(row, values) (RC:111-180): row -1 takes the first unused row (none: nothing); a used
+//       row is covered; the cells are written without Update events; one Add / Cover event;
+//   Remove(row) (RC:1086-1107): a used row's Del event, then the row is unused (cells kept);
+//   ClearRecord (KM:492 -> RC:1109): Remove from the last row to the first.
+__global__ __launch_bounds__(kTPB) void k_rrows(Dev d) {
+    const int l = blockIdx.x * kTPB + threadIdx.x;
+    if (l >= d.n_rl) return;
+    const uint32_t e = d.rl_slot[l];
+    const int r = (int)d.rl_rec[l];
+    const int rows = d.tab->rec_rows[r], cols = d.tab->rec_cols[r];
+    uint64_t* cells = nullptr;
+    uint64_t* usedp = nullptr;
+#pragma unroll
+    for (int q = 0; q < NFK_MAX_RECORDS; q++)
+        if (q == r) {
+            cells = d.rcells[q];
+            usedp = d.rused[q];
+        }
+    cells += (size_t)e * cols * rows;
+    const uint64_t rowm = rows >= 64 ? ~0ull : ((1ull << rows) - 1);
+    uint64_t used = usedp[e];
+    uint32_t* ev = d.rl_ev + d.rl_ev0[l];
+    unsigned nev = 0;
+    for (uint32_t k = d.rl_c0[l]; k < d.rl_c0[l + 1]; k++) {
+        const uint32_t code = d.rc_code[k];
+        const uint32_t op = code & 0xFF, row = (code >> 8) & 0xFF, col = (code >> 16) & 0xFF;
+        if (op == 0) {
+            if (!((used >> row) & 1)) continue;  // RC:194
+            const uint32_t g = d.rc_aux[k];
+            uint64_t* c = cells + (size_t)col * rows + row;
+            const uint64_t cur = *c, x = d.rc_bits[k];
+            bool changed;
+            if (d.tab->rec_ctype[r][col]) {
+                const double df = __longlong_as_double((long long)x) - __longlong_as_double((long long)cur);
+                changed = !(df < 0.001 && df > -0.001);
+            } else {
+                changed = x != cur;
+            }
+            if (!changed) continue;
+            if (!d.rs_has[g]) {
+                d.rs_old[g] = cur;
+                d.rs_has[g] = 1;
+            }
+            d.rs_new[g] = x;
+            *c = x;
+        } else if (op == 1) {
+            int rr = (int)row;
+            bool cover = false;
+            if (row == 0xFF) {
+                const uint64_t fr = ~used & rowm;
+                if (!fr) continue;  // no unused row: AddRow returns -1
+                rr = __builtin_ctzll(fr);
+            } else {
+                cover = (used >> rr) & 1;
+            }
+            used |= 1ull << rr;
+            const uint32_t vi = d.rc_aux[k];
+            for (int c = 0; c < cols; c++)
+                cells[(size_t)c * rows + rr] = vi == 0xFFFFFFFFu ? 0ull : d.rvals[(size_t)vi * NFK_MAX_REC_COLS + c];
+            ev[nev++] = ((cover ? 3u : 1u) << 8) | (uint32_t)rr;
+        } else if (op == 2) {
+            if (!((used >> row) & 1)) continue;
+            ev[nev++] = (2u << 8) | row;
+            used &= ~(1ull << row);
+        } else {
+            for (int q = rows - 1; q >= 0; q--)
+                if ((used >> q) & 1) {
+                    ev[nev++] = (2u << 8) | (uint32_t)q;
+                    used &= ~(1ull << q);
+                }
+        }
+    }
+    usedp[e] = used;
+    d.rl_cnt[l] = nev;
 }
 
 // The slots with SetRecord groups this window, one wave each (lane = row), every record of the
@@ -493,6 +581,7 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
     const int e = (int)d.rss_slot[si], g0 = (int)d.rss_g0[si];
     int g1 = g0;
     while (g1 < d.n_rs && d.rs_slot[g1] == (uint32_t)e) g1++;
+    int li = d.n_rl ? (int)d.rss_l0[si] : 0;  // the slot's row-operation lists (by record)
     const uint32_t fmask = d.has_recops ? d.fired_mask[e] & d.rop_kinds : 0u;
     const uint64_t desc = d.fan_desc[e];
     const unsigned cls = (unsigned)(desc >> 60);
@@ -519,6 +608,45 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
         const unsigned per = event_msgs(desc, rfl);
         const uint64_t used = usedp[e];
         const bool act = lane < rows;
+        // GetBroadCastObject (AOI:531-593) of one record event into its run at lmo
+        auto fan = [&](uint32_t lmo) {
+            uint32_t* out = d.msg_rcpt + mrb + lmo;
+            if (!(rfl & NFK_PUBLIC)) {
+                out[0] = (uint32_t)e;  // private & !upload: the entity itself
+                bytes += 4;
+            } else {  // every player of the group but self
+                const uint32_t np = (uint32_t)((desc >> 32) & 0x3FFF);
+                const uint32_t r1 = (uint32_t)((desc >> 46) & 0x3FFF);
+                uint32_t q = 0;
+                for (uint32_t u = 0; u < np; u++) {
+                    if (u + 1 == r1) continue;
+                    out[q++] = (uint32_t)d.pl_slot[(uint32_t)desc + u];
+                }
+                bytes += 4 * (per + np);
+            }
+        };
+        // the record's row events first (AddRow / Remove / Clear, in call order: k_rrows)
+        if (li < d.n_rl && d.rl_slot[li] == (uint32_t)e && d.rl_rec[li] == (uint32_t)r) {
+            const unsigned nrow = d.rl_cnt[li];
+            if constexpr (kEmit) {
+                const uint32_t* rev = d.rl_ev + d.rl_ev0[li];
+                for (unsigned q = (unsigned)lane; q < nrow; q += 64) {
+                    const uint32_t x = rev[q];
+                    const unsigned at = pos + q;
+                    const uint32_t lmo = pmsg + per * q;
+                    d.re_slot[re0 + at] = (uint32_t)e;
+                    d.re_rrc[re0 + at] = ((x >> 8) << 24) | ((uint32_t)r << 16) | ((x & 0xFF) << 8);
+                    d.re_old[re0 + at] = 0;
+                    d.re_new[re0 + at] = 0;
+                    d.re_moff[re0 + at] = mrb + lmo;
+                    bytes += 32;
+                    if (d.fuse_rec && per) fan(lmo);
+                }
+            }
+            pos += nrow;
+            pmsg += per * nrow;
+            li++;
+        }
         // cell (r, lane, c): its event (old, new) if any, and whether a record op writes nb back
         auto eval = [&](int c, uint64_t& ob, uint64_t& nb, bool& wb) -> bool {
             bool op = false;
@@ -536,9 +664,10 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
             int gi = -1;
             const uint32_t key = ((uint32_t)r << 16) | ((uint32_t)lane << 8) | (uint32_t)c;
             for (int g = g0; g < g1; g++)
-                if (d.rs_rrc[g] == key) gi = g;
+                if ((d.rs_rrc[g] & 0x7FFFFFFFu) == key) gi = g;
             wb = false;
             if (!act || (!op && gi < 0)) return false;
+            const bool has = gi >= 0 && d.rs_has[gi];
             const uint64_t cur = cells[((size_t)e * cols + c) * rows + lane];
             nb = cur;
             if (op && ((used >> lane) & 1)) {
@@ -561,7 +690,10 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
                     }
                 }
             }
-            ob = gi >= 0 ? d.rs_old[gi] : cur;
+            // coalesced (first logged old, last logged new): a cell AddRow rewrote after its Sets
+            // keeps the Sets' last value as the event's new one unless a record op changed it
+            ob = has ? d.rs_old[gi] : cur;
+            if (!wb && has) nb = d.rs_new[gi];
             return ob != nb;
         };
         unsigned cnt = 0;
@@ -591,22 +723,7 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
                 d.re_new[re0 + at] = nb;
                 d.re_moff[re0 + at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
                 bytes += 28;
-                if (d.fuse_rec && per) {  // GetBroadCastObject (AOI:531-593)
-                    uint32_t* out = d.msg_rcpt + mrb + lmo;
-                    if (!(rfl & NFK_PUBLIC)) {
-                        out[0] = (uint32_t)e;  // private & !upload: the entity itself
-                        bytes += 4;
-                    } else {  // every player of the group but self
-                        const uint32_t np = (uint32_t)((desc >> 32) & 0x3FFF);
-                        const uint32_t r1 = (uint32_t)((desc >> 46) & 0x3FFF);
-                        uint32_t q = 0;
-                        for (uint32_t u = 0; u < np; u++) {
-                            if (u + 1 == r1) continue;
-                            out[q++] = (uint32_t)d.pl_slot[(uint32_t)desc + u];
-                        }
-                        bytes += 4 * (per + np);
-                    }
-                }
+                if (d.fuse_rec && per) fan(lmo);  // GetBroadCastObject (AOI:531-593)
                 k++;
             }
             if (act) bytes += 8u * (unsigned)cols;  // the row's cells read
@@ -1029,7 +1146,7 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
         slot[q] = key[q] = lm[q] = 0;
         if (i < tcap) {
             slot[q] = slots[off0 + i];
-            key[q] = rec ? (d.re_rrc[off0 + i] >> 16) : d.ev_pid[off0 + i];
+            key[q] = rec ? ((d.re_rrc[off0 + i] >> 16) & 0xFF) : d.ev_pid[off0 + i];
             lm[q] = moff[off0 + i];
         }
     }
@@ -1054,7 +1171,7 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
                 const unsigned i = c0 + q * kTPB + threadIdx.x;
                 if (i < cnt) {
                     slot[q] = slots[off0 + i];
-                    key[q] = rec ? (d.re_rrc[off0 + i] >> 16) : d.ev_pid[off0 + i];
+                    key[q] = rec ? ((d.re_rrc[off0 + i] >> 16) & 0xFF) : d.ev_pid[off0 + i];
                     lm[q] = moff[off0 + i];
                 }
             }
@@ -1430,6 +1547,14 @@ __global__ __launch_bounds__(kTPB) void k_gather_words(const uint64_t* __restric
     if (i >= n) return;
     const uint64_t s = src[i];
     out[i] = (s >> 63) ? ins[s & ~(1ull << 63)] : pmem[s];
+}
+
+// GetRecord* reads (nfk_get_records): 8-byte words at device addresses (used masks and cells)
+__global__ __launch_bounds__(kTPB) void k_gather_abs(const uint64_t* __restrict__ addr, int32_t n,
+                                                     uint64_t* __restrict__ out) {
+    const int i = blockIdx.x * kTPB + threadIdx.x;
+    if (i >= n) return;
+    out[i] = *(const uint64_t*)(uintptr_t)addr[i];
 }
 
 // ---------------------------------------------------------------------------------

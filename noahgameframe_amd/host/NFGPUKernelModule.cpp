@@ -156,6 +156,17 @@ bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGrou
     return true;
 }
 
+bool NFGPUKernelModule::SetCreationRecord(const NFGUID& self, const std::string& strRecordName, uint64_t used,
+                                          const std::vector<uint64_t>& cells) {
+    auto it = record_id_.find(strRecordName);
+    const int o = ObjectIndex(self);
+    if (committed_ || it == record_id_.end() || o < 0) return false;
+    const RecordDef& rd = records_[it->second];
+    if (cells.size() != (size_t)rd.rows * rd.cols.size()) return false;
+    rec_init_[{o, it->second}] = {used & (rd.rows >= 64 ? ~0ull : ((1ull << rd.rows) - 1)), cells};
+    return true;
+}
+
 bool NFGPUKernelModule::AfterInit() {
     int n_int = 0, n_flt = 0, n_obj = 0;
     for (auto& p : props_) (p.type == TDATA_INT ? n_int : p.type == TDATA_FLOAT ? n_flt : n_obj)++;
@@ -215,6 +226,19 @@ bool NFGPUKernelModule::AfterInit() {
         }
         check(nfk_load_object(world_, PropertyId(props_[p].name), h.data(), d.data()), "nfk_load_object");
     }
+    for (int r = 0; r < (int)records_.size(); r++) {  // creation-time record contents
+        const size_t per = (size_t)records_[r].rows * records_[r].cols.size();
+        std::vector<uint64_t> cells(per * (size_t)n, 0), used((size_t)n, 0);
+        bool any = false;
+        for (auto& kv : rec_init_) {
+            if (kv.first.second != r) continue;
+            any = true;
+            used[kv.first.first] = kv.second.first;
+            std::copy(kv.second.second.begin(), kv.second.second.end(), cells.begin() + per * kv.first.first);
+        }
+        if (any) check(nfk_load_record(world_, r, cells.data(), used.data()), "nfk_load_record");
+    }
+    rec_init_.clear();
     check(nfk_commit(world_), "nfk_commit");
     {
         auto pid_of = [&](const char* nm, TDATA_TYPE t) {
@@ -291,6 +315,7 @@ bool NFGPUKernelModule::SetRecordInt(const NFGUID& self, const std::string& strR
     // NFCRecord::SetInt: ValidPos and the column type (RC:184-192)
     if (nRow < 0 || nRow >= rd.rows || nCol < 0 || nCol >= (int)rd.cols.size() || rd.cols[nCol] != TDATA_INT)
         return false;
+    if (!((UsedRows(self, it->second) >> nRow) & 1)) return false;  // RC:194
     const int32_t rec = it->second, row = nRow, col = nCol;
     const uint8_t f = 0;
     const uint64_t b = (uint64_t)nValue;
@@ -306,11 +331,75 @@ bool NFGPUKernelModule::SetRecordFloat(const NFGUID& self, const std::string& st
     const RecordDef& rd = records_[it->second];
     if (nRow < 0 || nRow >= rd.rows || nCol < 0 || nCol >= (int)rd.cols.size() || rd.cols[nCol] != TDATA_FLOAT)
         return false;
+    if (!((UsedRows(self, it->second) >> nRow) & 1)) return false;  // RC:255
     const int32_t rec = it->second, row = nRow, col = nCol;
     const uint8_t f = 1;
     uint64_t b;
     memcpy(&b, &dwValue, 8);
     if (nfk_set_records(world_, 1, &self.nHead64, &self.nData64, &rec, &row, &col, &f, &b) != NFK_OK) return false;
+    pending_calls_++;
+    return true;
+}
+
+uint64_t NFGPUKernelModule::UsedRows(const NFGUID& self, int rec) {
+    const int32_t r = rec;
+    uint64_t m = 0;
+    check(nfk_get_used_rows(world_, 1, &self.nHead64, &self.nData64, &r, &m), "nfk_get_used_rows");
+    return m;
+}
+
+bool NFGPUKernelModule::IsUsed(const NFGUID& self, const std::string& strRecordName, int nRow) {
+    auto it = record_id_.find(strRecordName);
+    if (!committed_ || it == record_id_.end() || ObjectIndex(self) < 0 || nRow < 0 || nRow >= records_[it->second].rows)
+        return false;
+    return (UsedRows(self, it->second) >> nRow) & 1;
+}
+
+// NFCRecord::AddRow (RC:111-180): the row it takes is known here from the used-row mask as the
+// reference holds it now, so the call is queued with that explicit row
+int NFGPUKernelModule::AddRow(const NFGUID& self, const std::string& strRecordName, int nRow,
+                              const std::vector<TData>& values) {
+    auto it = record_id_.find(strRecordName);
+    if (!committed_ || it == record_id_.end() || ObjectIndex(self) < 0) return -1;
+    const RecordDef& rd = records_[it->second];
+    if (nRow >= rd.rows || nRow < -1) return -1;
+    if (!values.empty() && values.size() != rd.cols.size()) return -1;  // RC:120
+    for (size_t c = 0; c < values.size(); c++)
+        if (values[c].GetType() != rd.cols[c]) return -1;  // RC:149-155
+    if (nRow < 0) {
+        const uint64_t used = UsedRows(self, it->second);
+        const uint64_t fr = ~used & (rd.rows >= 64 ? ~0ull : ((1ull << rd.rows) - 1));
+        if (!fr) return -1;
+        nRow = __builtin_ctzll(fr);
+    }
+    uint64_t v[NFK_MAX_REC_COLS] = {};
+    for (size_t c = 0; c < values.size(); c++)
+        v[c] = rd.cols[c] == TDATA_INT ? (uint64_t)values[c].GetInt() : bits_of(values[c].GetFloat());
+    const int32_t rec = it->second, op = 1, row = nRow;
+    if (nfk_record_rows(world_, 1, &self.nHead64, &self.nData64, &rec, &op, &row, values.empty() ? nullptr : v) != NFK_OK)
+        return -1;
+    pending_calls_++;
+    return nRow;
+}
+
+// NFCRecord::Remove (RC:1086): true when the row was used
+bool NFGPUKernelModule::RemoveRow(const NFGUID& self, const std::string& strRecordName, int nRow) {
+    auto it = record_id_.find(strRecordName);
+    if (!committed_ || it == record_id_.end() || ObjectIndex(self) < 0 || nRow < 0 || nRow >= records_[it->second].rows)
+        return false;
+    if (!((UsedRows(self, it->second) >> nRow) & 1)) return false;
+    const int32_t rec = it->second, op = 2, row = nRow;
+    if (nfk_record_rows(world_, 1, &self.nHead64, &self.nData64, &rec, &op, &row, nullptr) != NFK_OK) return false;
+    pending_calls_++;
+    return true;
+}
+
+// NFCKernelModule::ClearRecord (KM:492) -> NFCRecord::Clear (RC:1109)
+bool NFGPUKernelModule::ClearRecord(const NFGUID& self, const std::string& strRecordName) {
+    auto it = record_id_.find(strRecordName);
+    if (!committed_ || it == record_id_.end() || ObjectIndex(self) < 0) return false;
+    const int32_t rec = it->second, op = 3, row = 0;
+    if (nfk_record_rows(world_, 1, &self.nHead64, &self.nData64, &rec, &op, &row, nullptr) != NFK_OK) return false;
     pending_calls_++;
     return true;
 }
@@ -566,15 +655,18 @@ void NFGPUKernelModule::DeliverEvents() {
         }
     }
     for (int64_t e = 0; e < nr; e++) {
-        const int r = rrc[e] >> 16, row = (rrc[e] >> 8) & 0xFF, col = rrc[e] & 0xFF;
+        const int r = (rrc[e] >> 16) & 0xFF, row = (rrc[e] >> 8) & 0xFF, col = rrc[e] & 0xFF, op = rrc[e] >> 24;
         RECORD_EVENT_DATA ev;
-        ev.nOpType = RECORD_EVENT_DATA::Update;
+        // row events (AddRow / Remove / Clear) carry empty values, as NFCRecord raises them (RC:177, 1098)
+        ev.nOpType = op == 1 ? RECORD_EVENT_DATA::Add : op == 2 ? RECORD_EVENT_DATA::Del
+                   : op == 3 ? RECORD_EVENT_DATA::Cover : RECORD_EVENT_DATA::Update;
         ev.nRow = row;
         ev.nCol = col;
         ev.strRecordName = records_[r].name;
         TData a, b;
-        a.type = b.type = records_[r].cols[col];
-        if (a.type == TDATA_INT) {
+        a.type = b.type = op ? TDATA_UNKNOWN : records_[r].cols[col];
+        if (op) {
+        } else if (a.type == TDATA_INT) {
             a.i = (int64_t)rold[e];
             b.i = (int64_t)rnew[e];
         } else {

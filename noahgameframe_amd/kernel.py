@@ -98,7 +98,7 @@ def load_library(path=LIB_PATH):
         "nfk_jit_preview": [I32, I32, I32, I32, VP, VP, VP, I32, VP, VP, I32, VP, I32],
         "nfk_load_object": [VP, I32, VP, VP], "nfk_set_objects": [VP, I32, VP, VP, VP, VP, VP],
         "nfk_get_objects": [VP, I32, VP, VP, VP, VP, VP], "nfk_read_object": [VP, I32, VP, VP],
-        "nfk_read_events_obj": [VP, VP, VP],
+        "nfk_read_events_obj": [VP, VP, VP], "nfk_record_rows": [VP, I32, VP, VP, VP, VP, VP, VP],
     }
     for name, args in sig.items():
         if not hasattr(lib, name) and os.environ.get("NFGPU_LIB"):
@@ -232,6 +232,26 @@ class NFKernelModule:
         b = np.ascontiguousarray(bits, np.uint64)
         self._chk(self.lib.nfk_set_records(self.h, len(a[0]), *[_p(x) for x in a], _p(f) if f is not None else None,
                                            _p(b)))
+
+    def record_rows(self, guid_head, guid_data, rec, op, row, values=None):
+        """NFCRecord::AddRow (op 1, row -1 = first unused, values [n][16] words) / Remove (op 2) /
+        NFIKernelModule::ClearRecord (op 3), queued in call order with the SetRecord calls"""
+        a = [np.ascontiguousarray(x, t) for x, t in
+             ((guid_head, np.int64), (guid_data, np.int64), (rec, np.int32), (op, np.int32), (row, np.int32))]
+        v = None if values is None else np.ascontiguousarray(values, np.uint64).reshape(len(a[0]), 16)
+        self._chk(self.lib.nfk_record_rows(self.h, len(a[0]), *[_p(x) for x in a], _p(v)))
+
+    def AddRow(self, guid, rec, row=-1, values=None):
+        self.record_rows([guid[0]], [guid[1]], [rec], [1], [row], None if values is None else [values])
+        return True
+
+    def RemoveRow(self, guid, rec, row):
+        self.record_rows([guid[0]], [guid[1]], [rec], [2], [row])
+        return True
+
+    def ClearRecord(self, guid, rec):
+        self.record_rows([guid[0]], [guid[1]], [rec], [3], [0])
+        return True
 
     def get_records(self, guid_head, guid_data, rec, row, col):
         """NFIKernelModule::GetRecordInt/Float for n cells: raw 64-bit patterns, read-your-writes"""
@@ -583,11 +603,19 @@ def run_workload(m, w, tick, collect=True):
                 else:
                     v = (cur.view(np.float64) + d.view(np.float64)).view(np.uint64)
                 m.set_props([gh[o]], [gd[o]], [p], v)
-    if "r_tick" in w:   # SetRecordInt / SetRecordFloat calls (typed by their column)
+    if "r_tick" in w:   # SetRecordInt / SetRecordFloat calls (typed by their column), row operations
         rsel = np.nonzero(w["r_tick"] == tick)[0]
         if len(rsel):
-            ro = w["r_obj"][rsel]
-            m.set_records(gh[ro], gd[ro], w["r_rec"][rsel], w["r_row"][rsel], w["r_col"][rsel], w["r_bits"][rsel])
+            ops = w["r_op"][rsel] if "r_op" in w else np.zeros(len(rsel), np.uint8)
+            cut = np.nonzero(np.diff(np.concatenate([[-1], (ops != 0).astype(np.int8), [-1]])))[0]
+            for a, b in zip(cut[:-1], cut[1:]):   # runs of Sets / of row operations, in call order
+                sel = rsel[a:b]
+                ro = w["r_obj"][sel]
+                if ops[a] == 0:
+                    m.set_records(gh[ro], gd[ro], w["r_rec"][sel], w["r_row"][sel], w["r_col"][sel], w["r_bits"][sel])
+                else:
+                    m.record_rows(gh[ro], gd[ro], w["r_rec"][sel], ops[a:b].astype(np.int32), w["r_row"][sel],
+                                  w["r_vals"][sel])
     if "d_tick" in w:
         dead = w["d_obj"][w["d_tick"] == tick]
         if len(dead):

@@ -50,6 +50,12 @@ FIXTURES = {
     "objects": dict(n_obj=500, n_scenes=2, groups_per_scene=4, players_per_group=3, n_ticks=8, seed=1010,
                     ext_frac=0.05, ext_props="all", obj_props=True, obj_set_frac=0.08, host_ops=True,
                     switch_frac=0.02, spawn_frac=0.03, destroy_frac=0.03),
+    # record row operations: AddRow (first unused row / a given row, covering a used one), Remove,
+    # ClearRecord (NFCRecord.cpp:111, 1086, 1109; KM:492) interleaved with SetRecordInt calls on the
+    # same rows, beside the heartbeat's cooldown op, with create / destroy
+    "rowops": dict(n_obj=400, n_scenes=2, groups_per_scene=4, players_per_group=4, n_ticks=8, seed=1111,
+                   records=True, rec_rows=24, rec_float_op=False, rec_set_frac=0.08, rec_set_float=False,
+                   rec_row_frac=0.08, ext_frac=0.03, spawn_frac=0.02, destroy_frac=0.02),
 }
 
 

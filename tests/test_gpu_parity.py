@@ -27,7 +27,7 @@ def set_path(monkeypatch, path):
 
 @PATHS
 @pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets", "tutorial3", "rmw",
-                                  "lifecycle", "recsets", "objects"])
+                                  "lifecycle", "recsets", "objects", "rowops"])
 def test_gpu_matches_reference_golden(gpu_available, monkeypatch, name, path):
     set_path(monkeypatch, path)
     w = nfio.read(os.path.join(GOLDEN, f"{name}.workload.nfio"))
@@ -41,6 +41,13 @@ CASES = {
     "objects": dict(n_obj=4000, n_scenes=3, groups_per_scene=5, players_per_group=4, obj_props=True,
                     obj_set_frac=0.1, ext_frac=0.05, ext_props="all", rmw_frac=0.02, switch_frac=0.02,
                     spawn_frac=0.02, destroy_frac=0.02, host_ops=True),
+    # record row operations (nfk_record_rows: AddRow / Remove / ClearRecord) among SetRecord calls on
+    # the same rows, with the record programs (int and f64 columns) and create / destroy
+    "record_rows": dict(n_obj=3000, n_scenes=2, groups_per_scene=4, players_per_group=4, records=True, rec_rows=32,
+                        rec_set_frac=0.05, rec_set_float=True, rec_row_frac=0.05, spawn_frac=0.02,
+                        destroy_frac=0.02, switch_frac=0.01),
+    "record_rows_64": dict(n_obj=2000, n_scenes=1, groups_per_scene=4, players_per_group=8, records=True, rec_rows=64,
+                           rec_skill_op=True, rec_set_frac=0.1, rec_set_float=False, rec_row_frac=0.15),
     "objects_dense": dict(n_obj=3000, n_scenes=1, groups_per_scene=3, players_per_group=40, obj_props=True,
                           obj_set_frac=0.5, ext_frac=0.0, host_ops=False),
     "props_multi_scene": dict(n_obj=5000, n_scenes=3, groups_per_scene=7, players_per_group=4, ext_frac=0.1),

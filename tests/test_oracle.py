@@ -71,6 +71,13 @@ def test_golden_fixtures_are_nontrivial():
               ext_frac=0.05, ext_props="all", rmw_frac=0.02, switch_frac=0.02, spawn_frac=0.03, destroy_frac=0.03)),
     (14, dict(n_obj=300, n_scenes=1, groups_per_scene=2, players_per_group=30, obj_props=True, obj_set_frac=0.3,
               ext_frac=0.0, host_ops=False)),
+    # record row operations through the compiled NFCRecord::AddRow / Remove / Clear (RC:111, 1086,
+    # 1109), interleaved with SetRecordInt on the same rows and the heartbeat's record ops
+    (15, dict(n_obj=400, n_scenes=2, groups_per_scene=3, players_per_group=4, records=True, rec_rows=24,
+              rec_float_op=False, rec_set_frac=0.08, rec_set_float=False, rec_row_frac=0.1)),
+    (16, dict(n_obj=300, n_scenes=1, groups_per_scene=2, players_per_group=5, records=True, rec_rows=64,
+              rec_float_op=False, rec_skill_op=True, rec_set_frac=0.2, rec_set_float=False, rec_row_frac=0.2,
+              spawn_frac=0.03, destroy_frac=0.03)),
 ])
 def test_oracle_matches_reference(seed, kw):
     w = workload.make_world(n_ticks=9, seed=seed, **kw)

@@ -145,22 +145,27 @@ def _oracle_per_rank(w, ref, ws):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("slack", [0, -1])
-def test_sharded_replay_matches_single_world_oracle(gpu_available, tmp_path, slack):
+@pytest.mark.parametrize("ws,n_obj,n_scenes,slack", [(2, 4000, 4, 0), (2, 4000, 4, -1), (8, 48000, 16, 0)],
+                         ids=["2shards", "2shards-noslack", "8shards-config2-shape"])
+def test_sharded_replay_matches_single_world_oracle(gpu_available, tmp_path, ws, n_obj, n_scenes, slack):
+    """A sharded replay (one rank per scene range, gloo between ranks on the one GPU) matches the
+    single-world oracle rank by rank.  The 8-rank case is BASELINE config[2]'s shape scaled to one
+    GPU: 8 scene shards, SwitchScene moving entities into other shards every frame."""
     from tests.parity import run_oracle
-    w = workload.make_world(n_obj=4000, n_scenes=4, groups_per_scene=5, players_per_group=3, n_ticks=8, seed=71,
-                            switch_frac=0.03, switch_new_groups=True, ext_frac=0.05, records=True, rec_rows=8)
+    w = workload.make_world(n_obj=n_obj, n_scenes=n_scenes, groups_per_scene=5, players_per_group=3, n_ticks=8,
+                            seed=71 + ws, switch_frac=0.03, switch_new_groups=True, ext_frac=0.05, records=True,
+                            rec_rows=8)
     ref = run_oracle(w)
     wp = str(tmp_path / "w.nfio")
     nfio.write(wp, w)
     env = dict(os.environ, NFK_SLACK=str(slack))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ws),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "tests", "shard_worker.py"), wp, str(tmp_path)]
     subprocess.run(cmd, check=True, env=env, timeout=240)
-    per, final_scene = _oracle_per_rank(w, ref, 2)
+    per, final_scene = _oracle_per_rank(w, ref, ws)
     moved = 0
-    for r in range(2):
+    for r in range(ws):
         got = pickle.load(open(tmp_path / f"rank{r}.pkl", "rb"))
         moved += got["out"]
         for t, (g, e) in enumerate(zip(got["frames"], per[r])):
@@ -175,7 +180,7 @@ def test_sharded_replay_matches_single_world_oracle(gpu_available, tmp_path, sla
             assert lists == e["ev_rcpt"] + e["re_rcpt"], f"rank {r} frame {t} fan-out"
         n_int = int(w["cfg"][1])
         for o, (props, nx, rm, st, recs) in got["final"].items():
-            assert ws_owner(w, final_scene, o) == r
+            assert ws_owner(w, final_scene, o, ws) == r
             np.testing.assert_array_equal(props[:n_int].view(np.int64), ref["final_i"][:, o])
             np.testing.assert_array_equal(props[n_int:].view(np.float64).view(np.uint64),
                                           ref["final_f"][:, o].view(np.uint64))
@@ -183,21 +188,21 @@ def test_sharded_replay_matches_single_world_oracle(gpu_available, tmp_path, sla
             np.testing.assert_array_equal(rm, ref["final_s_remain"][:, o])
             np.testing.assert_array_equal(st, ref["final_s_present"][:, o])
             np.testing.assert_array_equal(recs[0], ref["final_rec0"][o])
-    assert moved > 50   # entities did cross shards
+    assert moved > 50 * (ws // 2)   # entities did cross shards
     # global leaderboards (rank_top_global over RCCL/gloo) equal ZREVRANGE over the oracle's final state
     from tests.redis_zset import zrevrange_top   # (independent of shard.zrevrange_order, the merge)
     for prop, k in (("Level", 50), ("Gold", 20), ("X", 30)):
         pid = workload.PID[prop]
         vals = ref["final_i"][pid].astype(np.float64) if pid < n_int else ref["final_f"][pid - n_int]
         o = np.asarray(zrevrange_top(w["guid_head"], w["guid_data"], vals, k), np.int64)
-        for r in range(2):
+        for r in range(ws):
             gh, gd, sc = pickle.load(open(tmp_path / f"rank{r}.pkl", "rb"))["ranks"][prop]
             assert list(zip(gh.tolist(), gd.tolist())) == list(zip(w["guid_head"][o].tolist(), w["guid_data"][o].tolist()))
             np.testing.assert_array_equal(sc, vals[o])
 
 
-def ws_owner(w, scene_of, o):
-    return scene_ranges(np.unique(w["scene"]), 2)(scene_of[o])
+def ws_owner(w, scene_of, o, ws=2):
+    return scene_ranges(np.unique(w["scene"]), ws)(scene_of[o])
 
 
 def _ticket_worker(rank, ws, port, q):
