@@ -71,6 +71,8 @@ def parse():
                         "(host-cost rehearsal; the migration phases are traced with NFGPU_BENCH_TRACE)")
     p.add_argument("--host-calls", choices=["auto", "off"], default="auto",
                    help="config[1], 1 GPU: also time frames with game-logic SetProperty / schedule calls")
+    p.add_argument("--plugin-frame", choices=["auto", "off"], default="auto",
+                   help="config[1], 1 GPU: also time the C++ plugin's frame (tests/cpp/plugin_bench)")
     p.add_argument("--config", type=int, default=1, choices=[0, 1, 3, 4],
                    help="BASELINE config: 0 = Tutorial3 at 10k NPCs (the reference's CPU case), "
                         "1 = 1M entities/GPU (the metric's configuration; with --gpus > 1 "
@@ -110,6 +112,7 @@ def cpu_baseline(args):
         w = workload.bench_world(n_obj=n, groups=groups, players_per_group=args.players_per_group, n_ticks=ticks,
                                  tick_ms=args.tick_ms, seed=2026)
         what = f"{n} entities ({groups} groups x {n // groups}, {args.players_per_group} players/group)"
+    from noahgameframe_amd import nfio
     with tempfile.TemporaryDirectory() as d:
         wp = os.path.join(d, "w.nfio")
         nfio.write(wp, w)
@@ -405,12 +408,42 @@ def main():
     }
     if rank == 0 and world == 1 and args.config == 1 and args.host_calls == "auto":
         out["host_calls"] = host_calls_run(args, torch, kernel, workload)
+    if rank == 0 and world == 1 and args.config == 1 and args.plugin_frame == "auto":
+        out["plugin_frame"] = plugin_frame_run(args, workload)
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def plugin_frame_run(args, workload):
+    """The C++ plugin's frame (NFGPUKernelModule::Execute, tests/cpp/plugin_bench.cpp, no Python in
+    the loop) on the host_calls world: a functor on every schedule, a common property callback and
+    an AOI recipient callback registered; once without and once with the game logic's calls between
+    frames.  Host ms per frame and its phases (device frame, functors, event read-back, delivery)."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "cpp", "_bin", "plugin_bench")
+    if not os.path.exists(exe):
+        return None
+    frames = args.warmup + args.steps
+    w = workload.bench_world(n_obj=args.entities, groups=args.groups, players_per_group=args.players_per_group,
+                             n_ticks=frames, tick_ms=args.tick_ms, seed=2031, ext_frac=0.05, host_ops=True)
+    res = {}
+    from noahgameframe_amd import nfio
+    with tempfile.TemporaryDirectory() as d:
+        wp = os.path.join(d, "w.nfio")
+        nfio.write(wp, w)
+        for calls in (0, 1):
+            r = subprocess.run([exe, wp, str(args.warmup), str(args.steps), str(calls)], capture_output=True,
+                               text=True, timeout=600)
+            if r.returncode != 0:
+                res["with_calls" if calls else "no_calls"] = {"error": r.stderr[-400:]}
+                continue
+            res["with_calls" if calls else "no_calls"] = json.loads(r.stdout.strip().splitlines()[-1])
+    return res
 
 
 def host_calls_run(args, torch, kernel, workload):

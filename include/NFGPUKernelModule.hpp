@@ -44,6 +44,7 @@
 #include <vector>
 
 #include "nfgpu.h"
+#include "NFGPUSceneShard.hpp"
 
 namespace nfgpu {
 
@@ -155,7 +156,12 @@ public:
         std::map<std::string, uint8_t> record_flags;
     };
     struct RecordDef { std::string name; int rows; std::vector<TDATA_TYPE> cols; };
-    struct HeartBeatDef { std::string name; std::vector<nfk_op> ops; };
+    struct HeartBeatDef {
+        std::string name;
+        std::vector<nfk_op> ops;
+        std::vector<std::string> props, records;  // symbolic operands (empty: ids)
+        bool symbolic = false;
+    };
 
     // ---- schema (what NFIClassModule loads from Struct/Class/*.xml) ----
     explicit NFGPUKernelModule(int capacity, void* hip_stream = nullptr);
@@ -165,8 +171,16 @@ public:
     void SetPropertyFlags(const std::string& cls, const std::string& prop, bool pub, bool priv, bool upload);
     int AddRecord(const std::string& name, int rows, const std::vector<TDATA_TYPE>& cols);
     void SetRecordFlags(const std::string& cls, const std::string& rec, bool pub, bool priv, bool upload);
-    // the device-side effect of a heartbeat name (see nfgpu.h op list)
+    // the device-side effect of a heartbeat name (see nfgpu.h op list): operands as device
+    // property ids (PropertyId) and record ids
     void AddHeartBeatProgram(const std::string& name, const std::vector<nfk_op>& ops);
+    // the same with operands by NAME, for a module that registers its programs before the schema
+    // exists (before AfterInit, e.g. the reference-side adapter, whose schema comes from the class
+    // module): a property operand (dst of a property op, a / lo / hi under NFK_A_PROP / NFK_LO_PROP /
+    // NFK_HI_PROP, FLERP's a) is an index into props, a record op's dst is index << 8 | column with
+    // the index into records; resolved at AfterInit
+    void AddHeartBeatProgram(const std::string& name, const std::vector<nfk_op>& ops,
+                             const std::vector<std::string>& props, const std::vector<std::string>& records = {});
     int PropertyId(const std::string& name) const;
 
     // ---- NFIModule lifecycle ----
@@ -242,6 +256,26 @@ public:
     bool RemoveSchedule(const std::string& name);
     bool ExistSchedule(const std::string& name);
 
+    // ---- scene shards (include/NFGPUSceneShard.hpp): one process per GPU, a scene range each ----
+    // With a shard attached, SwitchScene into a scene another shard owns queues the entity's
+    // departure: from that call on the entity is no longer this module's (later calls on it in the
+    // window return false, as after DestroyObject), and at the start of the next Execute every rank
+    // exchanges its departures (SceneShard::Migrate, collective: every rank's Execute calls it) and
+    // the arrivals enter this world with the SwitchScene property writes.  The row that travels is
+    // the entity's state after the last frame: Set calls queued on it earlier in the same window are
+    // dropped with it (make the SwitchScene its first call of the window).  Arrivals' schedules call
+    // the functor registered for their name with SetKindFunctor (functors cannot cross processes).
+    void AttachShard(SceneShard* shard) { shard_ = shard; }
+    // the departures queued so far leave now and the arrivals enter (collective: every rank calls
+    // it the same number of times; Execute also calls it first), so calls made after it in the
+    // window find the arrivals here
+    void MigrateNow() {
+        if (shard_) MigrateShard();
+    }
+    void SetKindFunctor(const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb, float fTime);
+    int64_t MigratedOut() const { return shard_ ? shard_->migrated_out : 0; }
+    int64_t MigratedIn() const { return shard_ ? shard_->migrated_in : 0; }
+
     // ---- NFIRankRedisModule::GetRange(type, 0, k - 1, memberScoreVec) over a property ----
     bool GetRange(const std::string& prop, int k, std::vector<std::pair<std::string, double>>& memberScoreVec);
 
@@ -251,11 +285,19 @@ public:
 
     void* World() const { return world_; }
     const nfk_summary& LastSummary() const { return summary_; }
+    // host wall time of the last Execute by phase (ms): the device frame (nfk_execute and the wait
+    // for its counters), the heartbeat functors (fired list read + order + calls), the event lists
+    // (read back), their delivery to the callbacks, the functors' own calls (second device pass
+    // and its delivery) and module schedules
+    struct FrameStats {
+        double device, functors, events_read, deliver, calls, total;
+    };
+    const FrameStats& LastFrameStats() const { return stats_; }
     int ObjectIndex(const NFGUID& g) const;
 
 private:
     void check(int rc, const char* what) const;
-    void DeliverEvents();
+    void DeliverEvents(const nfk_frame_host& f);
     uint64_t UsedRows(const NFGUID& self, int rec);
     void TakeAddedSchedules();
     bool same_frame_ = true;
@@ -285,13 +327,25 @@ private:
     std::vector<RECORD_EVENT_FUNCTOR> common_rec_cb_;
     std::vector<PROPERTY_SINGLE_EVENT_FUNCTOR> aoi_prop_cb_;
     std::vector<RECORD_SINGLE_EVENT_FUNCTOR> aoi_rec_cb_;
-    std::map<std::pair<int, int>, OBJECT_SCHEDULE_FUNCTOR> sched_cb_;   // (object, kind)
-    std::map<std::pair<int, int>, float> sched_time_;
+    // the functor of each (object, kind) schedule: cb_slot_[object * n_kind + kind] indexes
+    // cb_pool_ / cb_time_ (-1: none); freed entries are reused
+    std::vector<int32_t> cb_slot_;
+    std::vector<OBJECT_SCHEDULE_FUNCTOR> cb_pool_;
+    std::vector<float> cb_time_;
+    std::vector<int32_t> cb_free_;
+    int64_t n_cb_ = 0;
+    void SetFunctor(int o, int k, const OBJECT_SCHEDULE_FUNCTOR& f, float t);
+    void DropFunctors(int o);
+    std::vector<int> def_of_pid_;  // device property id -> props_ index
     // pending functors of AddSchedule calls in this window ((object, kind), first call wins)
     std::map<std::pair<int, int>, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> sched_add_;
     ModuleScheduler module_sched_;
+    SceneShard* shard_ = nullptr;
+    std::map<std::string, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> kind_cb_;  // arrivals' functors
+    void MigrateShard();
     std::function<int64_t()> clock_;
     nfk_summary summary_{};
+    FrameStats stats_{};
 };
 
 }  // namespace nfgpu

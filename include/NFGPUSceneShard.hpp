@@ -1,0 +1,137 @@
+// NFGPUSceneShard.hpp — scene shards across GPUs for a C++ game server, the C++
+// counterpart of noahgameframe_amd/shard.py.
+//
+// One process per GPU owns a range of scenes and runs its own world; a scene group never spans two
+// shards, so frames need no collective.  The only exchange on the path is a SwitchScene
+// (NFCKernelModule::SwitchScene, KM:901-951) into a scene another shard owns: the entity's state
+// row leaves the source world (nfk_export_objects), travels with one all-to-all per frame (RCCL
+// over xGMI: ncclSend / ncclRecv on the world's stream, device to device), and enters the owner's
+// world (nfk_import_objects), where the SwitchScene property writes follow (GroupID = 0, SceneID,
+// X, Y, Z, GroupID; KM:930-942), so that frame's events come from the new scene group as on a
+// single world.  Tickets (which entity goes where) are all-gathered first; a frame with no ticket
+// anywhere moves nothing else.
+//
+// Transports: RcclTransport (librccl, one rank per GPU, the production path) and HostTransport
+// (ranks as threads of one process exchanging through shared host memory: the protocol test's
+// stand-in, tests/cpp/shard_protocol.cpp).
+#pragma once
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <vector>
+
+namespace nfgpu {
+
+// one cross-shard SwitchScene; on the wire an int64[11] row (x, y, z as f64 bit patterns)
+struct Ticket {
+    int64_t guid_head = 0, guid_data = 0;
+    int32_t cls = 0, is_player = 0, scene = 0, group = 0;
+    double x = 0, y = 0, z = 0;
+    int32_t src = -1, dst = -1;
+};
+constexpr int kTicketWords = 11;
+
+// where rows live (device memory for a GPU world; host memory for a host stand-in world)
+struct RowMemory {
+    std::function<void*(size_t)> alloc;
+    std::function<void(void*)> release;
+    // copy between two row buffers of this memory (host stand-in transports use it)
+    std::function<void(void*, const void*, size_t)> copy;
+};
+RowMemory DeviceRowMemory();  // hipMalloc / hipFree / hipMemcpy device to device
+inline RowMemory HostRowMemory() {
+    return RowMemory{[](size_t n) { return (void*)new uint8_t[n ? n : 1]; }, [](void* p) { delete[] (uint8_t*)p; },
+                     [](void* d, const void* s, size_t n) {
+                         for (size_t i = 0; i < n; i++) ((uint8_t*)d)[i] = ((const uint8_t*)s)[i];
+                     }};
+}
+
+class ShardTransport {
+public:
+    virtual ~ShardTransport() = default;
+    virtual int Rank() const = 0;
+    virtual int Size() const = 0;
+    // every rank's int64 words, concatenated in rank order (collective)
+    virtual int AllGather(const std::vector<int64_t>& mine, std::vector<int64_t>& all) = 0;
+    // rows: send[r] / recv[r] words to / from rank r, buffers packed in rank order (collective);
+    // stream: the world's stream (RCCL enqueues there; host transports wait for it first)
+    virtual int AllToAllV(const uint64_t* send, const std::vector<size_t>& scount, uint64_t* recv,
+                          const std::vector<size_t>& rcount, void* stream) = 0;
+    // the rows must be complete in memory before AllToAllV (host transports)
+    virtual bool NeedsHostSync() const = 0;
+};
+
+// Ranks as threads of one process: every collective meets at a barrier in shared state.
+class HostTransport : public ShardTransport {
+public:
+    struct Shared;
+    static std::shared_ptr<Shared> MakeShared(int size);
+    HostTransport(std::shared_ptr<Shared> s, int rank, RowMemory mem);
+    int Rank() const override { return rank_; }
+    int Size() const override;
+    int AllGather(const std::vector<int64_t>& mine, std::vector<int64_t>& all) override;
+    int AllToAllV(const uint64_t* send, const std::vector<size_t>& scount, uint64_t* recv,
+                  const std::vector<size_t>& rcount, void* stream) override;
+    bool NeedsHostSync() const override { return true; }
+
+private:
+    std::shared_ptr<Shared> s_;
+    int rank_;
+    RowMemory mem_;
+};
+
+// RCCL (ncclComm per process, one GPU each): tickets by ncclAllGather (count, then the rows padded
+// to the largest count), rows by grouped ncclSend / ncclRecv on the world's stream.
+class RcclTransport : public ShardTransport {
+public:
+    // unique_id: the 128-byte ncclUniqueId rank 0 made (NewUniqueId) and every rank received out
+    // of band (the game server's own cluster channel)
+    static std::vector<uint8_t> NewUniqueId();
+    RcclTransport(const std::vector<uint8_t>& unique_id, int rank, int size, void* stream);
+    ~RcclTransport() override;
+    int Rank() const override { return rank_; }
+    int Size() const override { return size_; }
+    int AllGather(const std::vector<int64_t>& mine, std::vector<int64_t>& all) override;
+    int AllToAllV(const uint64_t* send, const std::vector<size_t>& scount, uint64_t* recv,
+                  const std::vector<size_t>& rcount, void* stream) override;
+    bool NeedsHostSync() const override { return false; }
+
+private:
+    void* comm_ = nullptr;
+    void* stream_ = nullptr;
+    int rank_, size_;
+    int64_t* buf_ = nullptr;  // device staging of the ticket all-gather
+    size_t buf_cap_ = 0;
+};
+
+class SceneShard {
+public:
+    // owner(scene) -> rank; scene-property ids of the world (nfk_set_scene_props; -1: absent)
+    SceneShard(void* world, ShardTransport* t, std::function<int(int)> owner, int pid_scene, int pid_group, int pid_x,
+               int pid_y, int pid_z, RowMemory mem = DeviceRowMemory(), void* stream = nullptr);
+    ~SceneShard();
+    bool Owns(int scene) const { return owner_(scene) == t_->Rank(); }
+    int Owner(int scene) const { return owner_(scene); }
+    // a SwitchScene whose target this shard does not own: queued for the next Migrate (the entity
+    // leaves at the start of the next frame)
+    void QueueSwitch(int64_t guid_head, int64_t guid_data, int cls, int is_player, int scene, int group, float x,
+                     float y, float z);
+    // collective, once per frame before the frame runs on every rank: tickets, rows, imports and the
+    // SwitchScene property writes on arrival.  sent / received: this rank's tickets.
+    int Migrate(std::vector<Ticket>* sent = nullptr, std::vector<Ticket>* received = nullptr);
+    int64_t migrated_out = 0, migrated_in = 0;
+
+private:
+    void* world_;
+    ShardTransport* t_;
+    std::function<int(int)> owner_;
+    int pid_scene_, pid_group_, pid_x_, pid_y_, pid_z_;
+    RowMemory mem_;
+    void* stream_;
+    std::vector<Ticket> out_;
+    uint64_t* sbuf_ = nullptr;
+    uint64_t* rbuf_ = nullptr;
+    size_t scap_ = 0, rcap_ = 0;
+};
+
+}  // namespace nfgpu

@@ -341,6 +341,32 @@ int nfk_read_fired(void* world, int32_t* fi_obj, int32_t* fi_kind, int32_t* fi_r
 /* dense CSR over [prop events ++ record events]: msg_off[n_ev + n_re + 1], recipients as objects */
 int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj);
 
+/* ---- the frame's outputs for a host consumer in ONE read-back ----
+ * The host plugin's delivery path (heartbeat functors, common property / record callbacks, AOI
+ * recipient lists): the selected outputs of the last frame are compacted on the device into dense
+ * arrays in object-index terms (slot -> object, message offsets rebased to a dense CSR over
+ * [property events ++ record events]), the fired list optionally ordered by (NFGUID, kind) — the
+ * order NFCScheduleModule::Execute walks mObjectScheduleMap (SM:52-80) — with a device radix sort,
+ * and copied with one asynchronous copy into a pinned host buffer owned by the world.  The
+ * pointers stay valid until the next nfk_execute / nfk_execute_calls / nfk_read_frame.  Arrays not
+ * selected are NULL; ev_old_h / ev_new_h are NULL in a world without object properties (0 for
+ * the other events). */
+#define NFK_READ_FIRED 1u
+#define NFK_READ_FIRED_GUID_ORDER 2u /* with NFK_READ_FIRED: (NFGUID, kind) order; else frame order */
+#define NFK_READ_EVENTS 4u           /* property and record events */
+#define NFK_READ_FANOUT 8u           /* with NFK_READ_EVENTS: the recipient CSR */
+typedef struct nfk_frame_host {
+    int64_t n_ev, n_re, n_fi, n_msgs;
+    const int32_t* ev_obj; const int32_t* ev_pid; const uint64_t* ev_old; const uint64_t* ev_new;
+    const uint64_t* ev_old_h; const uint64_t* ev_new_h;
+    const int32_t* re_obj; const uint32_t* re_rrc; const uint64_t* re_old; const uint64_t* re_new;
+    const int32_t* fi_obj; const int32_t* fi_kind; const int32_t* fi_remain;
+    const uint32_t* msg_off;   /* [n_ev + n_re + 1] */
+    const int32_t* msg_rcpt;   /* [n_msgs] object indices */
+    int64_t bytes;             /* bytes copied to the host */
+} nfk_frame_host;
+int nfk_read_frame(void* world, uint32_t what, nfk_frame_host* out);
+
 /* ---- leaderboards: NFIRankRedisModule::GetRange (NFCRankRedisModule.cpp:109, a Redis
  * ZREVRANGE 0..k-1 WITH SCORES) with the property as the rank value (SetRankValue takes a double):
  * the k entities of this world with the highest score, ties by NFGUID::ToString() descending

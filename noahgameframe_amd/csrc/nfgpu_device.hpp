@@ -333,6 +333,54 @@ template <typename T>
 __device__ __forceinline__ void st_off(T* base, uint32_t i, T x) {
     *(T*)((char*)base + i * (uint32_t)sizeof(T)) = x;
 }
+// loads / stores with the non-temporal hint when NT (global_load / global_store ... nt): data
+// streamed once per frame, not worth keeping in L2 / the Infinity Cache for this frame
+typedef uint32_t u32x4_v __attribute__((ext_vector_type(4)));
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_nt(const T* p) {
+    if constexpr (!NT) {
+        return *p;
+    } else if constexpr (sizeof(T) == 16) {
+        const u32x4_v v = __builtin_nontemporal_load((const u32x4_v*)p);
+        T r;
+        __builtin_memcpy(&r, &v, 16);
+        return r;
+    } else if constexpr (sizeof(T) == 8) {
+        const uint64_t v = __builtin_nontemporal_load((const uint64_t*)p);
+        T r;
+        __builtin_memcpy(&r, &v, 8);
+        return r;
+    } else {
+        static_assert(sizeof(T) == 4, "ld_nt: 4, 8 or 16 bytes");
+        const uint32_t v = __builtin_nontemporal_load((const uint32_t*)p);
+        T r;
+        __builtin_memcpy(&r, &v, 4);
+        return r;
+    }
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st_nt(T* p, T x) {
+    if constexpr (!NT) {
+        *p = x;
+    } else if constexpr (sizeof(T) == 16) {
+        u32x4_v v;
+        __builtin_memcpy(&v, &x, 16);
+        __builtin_nontemporal_store(v, (u32x4_v*)p);
+    } else if constexpr (sizeof(T) == 8) {
+        uint64_t v;
+        __builtin_memcpy(&v, &x, 8);
+        __builtin_nontemporal_store(v, (uint64_t*)p);
+    } else {
+        static_assert(sizeof(T) == 4, "st_nt: 4, 8 or 16 bytes");
+        uint32_t v;
+        __builtin_memcpy(&v, &x, 4);
+        __builtin_nontemporal_store(v, (uint32_t*)p);
+    }
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st_off_nt(T* base, uint32_t i, T x) {
+    st_nt<NT>((T*)((char*)base + i * (uint32_t)sizeof(T)), x);
+}
 __device__ __forceinline__ unsigned event_msgs(uint64_t desc, uint8_t fl) {
     if (fl & NFK_PUBLIC) {
         const unsigned np = (unsigned)((desc >> 32) & 0x3FFF);

@@ -9,12 +9,15 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <numeric>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
 #include <mutex>
 #include <thread>
+
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "nfgpu_jit.hpp"
 #include "nfgpu_kernels.hip"
@@ -224,6 +227,17 @@ struct World {
     // dense readback scratch (nfk_read_*), grown on demand
     void* dense = nullptr;
     size_t dense_cap = 0;
+    // nfk_read_frame: the dense region on the device and its pinned host copy, device scratch, and
+    // the NFGUID order of the objects (guid_sorted; rank_d[object] on the device for rank_n objects)
+    void* fr_dev = nullptr;
+    char* fr_pin = nullptr;
+    size_t fr_cap = 0;
+    void* fr_scr = nullptr;
+    size_t fr_scap = 0;
+    std::vector<int32_t> guid_sorted;
+    int32_t* rank_d = nullptr;
+    size_t rank_cap = 0;
+    int32_t rank_n = 0;
 
     // queued calls
     // queued calls; `slot` holds the object index until nfk_execute resolves it after the
@@ -771,6 +785,9 @@ int tick_waves(int n_u, uint32_t ablate) {
     return 6;
 }
 
+// the non-temporal hints the specialised k_tick is built with (A/B: NFGPU_JIT_NT)
+constexpr uint32_t kJitNtDefault = 0;
+
 // Specialised k_tick kernels built in this process, by (device, variant, policy source): a
 // schema compiles once however many worlds use it.
 std::mutex g_jit_mu;
@@ -795,7 +812,10 @@ void build_jit(World* w) {
     if (const char* ew = getenv("NFGPU_JIT_WAVES")) waves = std::max(1, std::min(8, atoi(ew)));
     const char* es = getenv("NFGPU_JIT_SPEC");
     const bool spec = es && es[0] == '1';  // every program operand loaded with the schedule records
-    const std::string src = jit_schema_source(w->tab, w->d, spec);
+    // non-temporal hints (kNt* bits of nfgpu_tick.hpp); NFGPU_JIT_NT overrides the default
+    uint32_t nt = kJitNtDefault;
+    if (const char* en = getenv("NFGPU_JIT_NT")) nt = (uint32_t)strtoul(en, nullptr, 0);
+    const std::string src = jit_schema_source(w->tab, w->d, spec, nt);
     int dev = 0;
     (void)hipGetDevice(&dev);
     const std::string key = std::to_string(dev) + "|" + std::to_string(waves) + "|" + std::to_string(u) + "|" + src;
@@ -1406,6 +1426,10 @@ int nfk_destroy(void* world) {
     if (w->pin) (void)hipHostFree(w->pin);
     if (w->stage) (void)hipFree(w->stage);
     if (w->dense) (void)hipFree(w->dense);
+    if (w->fr_dev) (void)hipFree(w->fr_dev);
+    if (w->fr_pin) (void)hipHostFree(w->fr_pin);
+    if (w->fr_scr) (void)hipFree(w->fr_scr);
+    if (w->rank_d) (void)hipFree(w->rank_d);
     if (w->ins_rows) (void)hipFree(w->ins_rows);
     if (w->mv_rows) (void)hipFree(w->mv_rows);
     if (w->mlist) (void)hipFree(w->mlist);
@@ -3678,6 +3702,205 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
     return NFK_OK;
 }
 
+// The rank of every object's NFGUID among all objects of the world (rank_d, on the device), for
+// ordering the fired list as mObjectScheduleMap does: the sorted order is kept and new objects are
+// merged into it (an O(n) merge in frames that created objects).
+static int update_guid_ranks(World* w) {
+    if (w->rank_n == w->n_obj && w->rank_d) return NFK_OK;
+    std::vector<int32_t> fresh(w->n_obj - w->rank_n);
+    std::iota(fresh.begin(), fresh.end(), w->rank_n);
+    auto less = [w](int32_t a, int32_t b) { return guid_less(w, a, b); };
+    std::sort(fresh.begin(), fresh.end(), less);
+    std::vector<int32_t> merged(w->n_obj);
+    std::merge(w->guid_sorted.begin(), w->guid_sorted.end(), fresh.begin(), fresh.end(), merged.begin(), less);
+    w->guid_sorted.swap(merged);
+    std::vector<int32_t> rank(w->n_obj);
+    for (int32_t i = 0; i < w->n_obj; i++) rank[w->guid_sorted[i]] = i;
+    if ((size_t)w->n_obj > w->rank_cap) {
+        HIPCHK(hipStreamSynchronize(w->stream));
+        if (w->rank_d) HIPCHK(hipFree(w->rank_d));
+        w->rank_d = nullptr;
+        w->rank_cap = (size_t)w->n_obj + w->n_obj / 4 + 1024;
+        HIPCHK(hipMalloc((void**)&w->rank_d, w->rank_cap * 4));
+    }
+    HIPCHK(hipMemcpy(w->rank_d, rank.data(), rank.size() * 4, hipMemcpyHostToDevice));
+    w->rank_n = w->n_obj;
+    return NFK_OK;
+}
+
+int nfk_read_frame(void* world, uint32_t what, nfk_frame_host* o) {
+    World* w = (World*)world;
+    if (!w || !o) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    memset(o, 0, sizeof *o);
+    int r = check_fanout(w);
+    if (r) return r;
+    Ctrl c;
+    r = read_ctrl(w, &c);
+    if (r) return r;
+    if (c.err & (kErrFanBound | kErrTouch))
+        return fail(NFK_ERR_DEVICE, "the frame's outputs are incomplete (device error " + std::to_string(c.err) + ")");
+    if (c.msg_extent > (unsigned long long)w->d.msg_cap) return fail(NFK_ERR_CAPACITY, "fan-out not recovered");
+    const Dev& d = w->d;
+    const bool fired = what & NFK_READ_FIRED, order = fired && (what & NFK_READ_FIRED_GUID_ORDER);
+    const bool events = what & NFK_READ_EVENTS, fan = events && (what & NFK_READ_FANOUT);
+    const bool heads = events && d.n_obj > 0;
+    const size_t ne = events ? c.n_ev : 0, nr = events && d.has_recops ? c.n_re : 0, nf = fired ? c.n_fi : 0;
+    const size_t nm = fan ? (size_t)frame_msgs(w, c) : 0;
+    const int ntt = d.n_tiles + (d.has_recops ? d.n_rtiles : 0);
+    // one region, the same layout on the device and in pinned host memory
+    size_t at = 0;
+    auto take = [&](size_t bytes) {
+        const size_t a = at;
+        at += (bytes + 255) & ~(size_t)255;
+        return a;
+    };
+    const size_t o_eo = take(ne * 4), o_ep = take(ne * 4), o_eold = take(ne * 8), o_enew = take(ne * 8);
+    const size_t o_eoh = take(heads ? ne * 8 : 0), o_enh = take(heads ? ne * 8 : 0);
+    const size_t o_ro = take(nr * 4), o_rr = take(nr * 4), o_rold = take(nr * 8), o_rnew = take(nr * 8);
+    const size_t o_fo = take(nf * 4), o_fk = take(nf * 4), o_fr = take(nf * 4);
+    const size_t o_mo = take(fan ? (ne + nr + 1) * 4 : 0), o_mr = take(nm * 4);
+    const size_t total = at;
+    // device scratch: dense message bases, and the fired sort's keys / indices / unsorted copies
+    const size_t s_db = 0, s_keys = (((size_t)ntt + 1) * 4 + 255) & ~(size_t)255;
+    const size_t s_k2 = s_keys + ((nf * 8 + 255) & ~(size_t)255), s_i1 = s_k2 + ((nf * 8 + 255) & ~(size_t)255);
+    const size_t s_i2 = s_i1 + ((nf * 4 + 255) & ~(size_t)255), s_f = s_i2 + ((nf * 4 + 255) & ~(size_t)255);
+    size_t s_tmp = s_f + 3 * ((nf * 4 + 255) & ~(size_t)255);
+    size_t sort_bytes = 0;
+    int key_bits = 5;
+    if (order) {
+        r = update_guid_ranks(w);
+        if (r) return r;
+        while ((1ll << (key_bits - 5)) < (long long)std::max(w->n_obj, 1)) key_bits++;
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                         (uint32_t*)nullptr, (uint32_t*)nullptr, nf, 0, key_bits, w->stream));
+    }
+    const size_t scratch = s_tmp + sort_bytes + 256;
+    if (total > w->fr_cap || scratch > w->fr_scap) {
+        HIPCHK(hipStreamSynchronize(w->stream));
+        if (total > w->fr_cap) {
+            if (w->fr_dev) HIPCHK(hipFree(w->fr_dev));
+            if (w->fr_pin) HIPCHK(hipHostFree(w->fr_pin));
+            w->fr_dev = nullptr;
+            w->fr_pin = nullptr;
+            w->fr_cap = total + total / 4 + 4096;
+            HIPCHK(hipMalloc(&w->fr_dev, w->fr_cap));
+            HIPCHK(hipHostMalloc((void**)&w->fr_pin, w->fr_cap, hipHostMallocDefault));
+        }
+        if (scratch > w->fr_scap) {
+            if (w->fr_scr) HIPCHK(hipFree(w->fr_scr));
+            w->fr_scr = nullptr;
+            w->fr_scap = scratch + scratch / 4 + 4096;
+            HIPCHK(hipMalloc(&w->fr_scr, w->fr_scap));
+        }
+    }
+    char* D = (char*)w->fr_dev;
+    char* S = (char*)w->fr_scr;
+    const unsigned gt = (unsigned)std::max(1, std::min(d.n_tiles, 4096));
+    const unsigned grt = (unsigned)std::max(1, std::min(d.n_rtiles, 4096));
+    const int32_t* so = w->slot_obj_d;
+    if (ne) {
+        hipLaunchKernelGGL(k_compact_obj, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_slot, (int32_t*)(D + o_eo),
+                           d.ev_base, d.n_tiles, d.ev_tcap, so);
+        hipLaunchKernelGGL(k_compact<uint32_t>, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_pid, (uint32_t*)(D + o_ep),
+                           d.ev_base, d.n_tiles, d.ev_tcap);
+        hipLaunchKernelGGL(k_compact<uint64_t>, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_old, (uint64_t*)(D + o_eold),
+                           d.ev_base, d.n_tiles, d.ev_tcap);
+        hipLaunchKernelGGL(k_compact<uint64_t>, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_new, (uint64_t*)(D + o_enew),
+                           d.ev_base, d.n_tiles, d.ev_tcap);
+        if (heads) {
+            hipLaunchKernelGGL(k_compact_h, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_old_h, (uint64_t*)(D + o_eoh),
+                               d.ev_pid, d.ev_base, d.n_tiles, d.ev_tcap, d.n_if);
+            hipLaunchKernelGGL(k_compact_h, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_new_h, (uint64_t*)(D + o_enh),
+                               d.ev_pid, d.ev_base, d.n_tiles, d.ev_tcap, d.n_if);
+        }
+    }
+    if (nr) {
+        hipLaunchKernelGGL(k_compact_obj, dim3(grt), dim3(kTPB), 0, w->stream, d.re_slot, (int32_t*)(D + o_ro),
+                           d.re_base, d.n_rtiles, d.re_tcap, so);
+        hipLaunchKernelGGL(k_compact<uint32_t>, dim3(grt), dim3(kTPB), 0, w->stream, d.re_rrc, (uint32_t*)(D + o_rr),
+                           d.re_base, d.n_rtiles, d.re_tcap);
+        hipLaunchKernelGGL(k_compact<uint64_t>, dim3(grt), dim3(kTPB), 0, w->stream, d.re_old, (uint64_t*)(D + o_rold),
+                           d.re_base, d.n_rtiles, d.re_tcap);
+        hipLaunchKernelGGL(k_compact<uint64_t>, dim3(grt), dim3(kTPB), 0, w->stream, d.re_new, (uint64_t*)(D + o_rnew),
+                           d.re_base, d.n_rtiles, d.re_tcap);
+    }
+    if (fan && ntt) {
+        uint32_t* db = (uint32_t*)(S + s_db);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, w->stream, d.t_msg, db, ntt);
+        if (ne)
+            hipLaunchKernelGGL(k_compact_moff, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_moff, (uint32_t*)(D + o_mo),
+                               d.ev_base, d.n_tiles, d.ev_tcap, d.msg_base, db);
+        if (nr)
+            hipLaunchKernelGGL(k_compact_moff, dim3(grt), dim3(kTPB), 0, w->stream, d.re_moff,
+                               (uint32_t*)(D + o_mo) + ne, d.re_base, d.n_rtiles, d.re_tcap, d.msg_base + d.n_tiles,
+                               db + d.n_tiles);
+        // the CSR's last offset: the frame's message count
+        HIPCHK(hipMemcpyAsync(D + o_mo + (ne + nr) * 4, db + ntt, 4, hipMemcpyDeviceToDevice, w->stream));
+        if (nm)
+            hipLaunchKernelGGL(k_runs_obj, dim3((unsigned)std::min(ntt, 8192)), dim3(kTPB), 0, w->stream, d.msg_rcpt,
+                               (int32_t*)(D + o_mr), d.msg_base, d.t_msg, db, ntt, so);
+    } else if (fan) {
+        HIPCHK(hipMemsetAsync(D + o_mo, 0, 4, w->stream));
+    }
+    if (nf) {
+        int32_t* fo = (int32_t*)(order ? S + s_f : D + o_fo);
+        int32_t* fk = (int32_t*)(order ? S + s_f + ((nf * 4 + 255) & ~(size_t)255) : D + o_fk);
+        int32_t* fr = (int32_t*)(order ? S + s_f + 2 * ((nf * 4 + 255) & ~(size_t)255) : D + o_fr);
+        hipLaunchKernelGGL(k_compact_obj, dim3(gt), dim3(kTPB), 0, w->stream, d.fi_slot, fo, d.fi_base, d.n_tiles,
+                           d.fi_tcap, so);
+        hipLaunchKernelGGL(k_compact<uint32_t>, dim3(gt), dim3(kTPB), 0, w->stream, d.fi_kind, (uint32_t*)fk,
+                           d.fi_base, d.n_tiles, d.fi_tcap);
+        hipLaunchKernelGGL(k_compact<int32_t>, dim3(gt), dim3(kTPB), 0, w->stream, d.fi_remain, fr, d.fi_base,
+                           d.n_tiles, d.fi_tcap);
+        if (order) {
+            const unsigned g = (unsigned)((nf + kTPB - 1) / kTPB);
+            uint64_t* k1 = (uint64_t*)(S + s_keys);
+            uint64_t* k2 = (uint64_t*)(S + s_k2);
+            uint32_t* i1 = (uint32_t*)(S + s_i1);
+            uint32_t* i2 = (uint32_t*)(S + s_i2);
+            hipLaunchKernelGGL(k_fired_keys, dim3(g), dim3(kTPB), 0, w->stream, fo, fk, w->rank_d, k1, i1, (int)nf);
+            size_t sb = sort_bytes;
+            HIPCHK(rocprim::radix_sort_pairs(S + s_tmp, sb, k1, k2, i1, i2, nf, 0, key_bits, w->stream));
+            hipLaunchKernelGGL(k_permute3, dim3(g), dim3(kTPB), 0, w->stream, i2, fo, fk, fr, (int32_t*)(D + o_fo),
+                               (int32_t*)(D + o_fk), (int32_t*)(D + o_fr), (int)nf);
+        }
+    }
+    HIPCHK(hipGetLastError());
+    if (total) HIPCHK(hipMemcpyAsync(w->fr_pin, D, total, hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    char* H = w->fr_pin;
+    o->n_ev = (int64_t)ne;
+    o->n_re = (int64_t)nr;
+    o->n_fi = (int64_t)nf;
+    o->n_msgs = (int64_t)nm;
+    o->bytes = (int64_t)total;
+    if (events) {
+        o->ev_obj = (const int32_t*)(H + o_eo);
+        o->ev_pid = (const int32_t*)(H + o_ep);
+        o->ev_old = (const uint64_t*)(H + o_eold);
+        o->ev_new = (const uint64_t*)(H + o_enew);
+        if (heads) {
+            o->ev_old_h = (const uint64_t*)(H + o_eoh);
+            o->ev_new_h = (const uint64_t*)(H + o_enh);
+        }
+        o->re_obj = (const int32_t*)(H + o_ro);
+        o->re_rrc = (const uint32_t*)(H + o_rr);
+        o->re_old = (const uint64_t*)(H + o_rold);
+        o->re_new = (const uint64_t*)(H + o_rnew);
+    }
+    if (fired) {
+        o->fi_obj = (const int32_t*)(H + o_fo);
+        o->fi_kind = (const int32_t*)(H + o_fk);
+        o->fi_remain = (const int32_t*)(H + o_fr);
+    }
+    if (fan) {
+        o->msg_off = (const uint32_t*)(H + o_mo);
+        o->msg_rcpt = (const int32_t*)(H + o_mr);
+    }
+    return NFK_OK;
+}
+
 int nfk_rank_top(void* world, int32_t pid, int32_t k, int32_t* n_out, int64_t* guid_head, int64_t* guid_data,
                  double* score) {
     World* w = (World*)world;
@@ -3799,7 +4022,9 @@ int nfk_jit_preview(int32_t n_int, int32_t n_flt, int32_t n_class, int32_t n_kin
         return NFK_OK;
     }
     const char* es = getenv("NFGPU_JIT_SPEC");
-    const std::string s = jit_schema_source(*tab, d, es && es[0] == '1');
+    uint32_t nt = kJitNtDefault;
+    if (const char* en = getenv("NFGPU_JIT_NT")) nt = (uint32_t)strtoul(en, nullptr, 0);
+    const std::string s = jit_schema_source(*tab, d, es && es[0] == '1', nt);
     copy_msg(s, src, src_cap);
     if (!compile) {
         *ok = 1;

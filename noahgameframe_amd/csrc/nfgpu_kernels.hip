@@ -1568,4 +1568,89 @@ __global__ __launch_bounds__(kTPB) void k_compact(const T* __restrict__ src, T* 
     }
 }
 
+// ---------------------------------------------------------------------------------
+// nfk_read_frame: the frame's outputs as dense host-ready arrays, in object-index terms.
+// tile-staged slots -> dense object indices
+__global__ __launch_bounds__(kTPB) void k_compact_obj(const uint32_t* __restrict__ src, int32_t* __restrict__ dst,
+                                                      const uint32_t* __restrict__ base, int n_tiles, int tcap,
+                                                      const int32_t* __restrict__ slot_obj) {
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const uint32_t b = base[t], n = base[t + 1] - b;
+        for (uint32_t i = threadIdx.x; i < n; i += kTPB) dst[b + i] = slot_obj[src[(size_t)t * tcap + i]];
+    }
+}
+// object-property head halves: 0 for the other events (their entries are unwritten)
+__global__ __launch_bounds__(kTPB) void k_compact_h(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
+                                                    const uint32_t* __restrict__ pid, const uint32_t* __restrict__ base,
+                                                    int n_tiles, int tcap, int n_if) {
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const uint32_t b = base[t], n = base[t + 1] - b;
+        for (uint32_t i = threadIdx.x; i < n; i += kTPB) {
+            const size_t s = (size_t)t * tcap + i;
+            dst[b + i] = (int)pid[s] >= n_if ? src[s] : 0ull;
+        }
+    }
+}
+// exclusive scan of n counts (one workgroup of 1024: a contiguous chunk per thread)
+__global__ __launch_bounds__(1024) void k_scan_counts(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ out,
+                                                      int n) {
+    __shared__ uint32_t s[1024];
+    const int per = (n + 1023) / 1024, i0 = min(n, (int)threadIdx.x * per), i1 = min(n, i0 + per);
+    uint32_t sum = 0;
+    for (int i = i0; i < i1; i++) sum += cnt[i];
+    s[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan of the chunk sums
+        const uint32_t v = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t acc = s[threadIdx.x] - sum;
+    for (int i = i0; i < i1; i++) {
+        out[i] = acc;
+        acc += cnt[i];
+    }
+    if (threadIdx.x == 1023) out[n] = s[1023];
+}
+// message offsets of tile-staged events: the tile's run start mb[t] -> its dense start db[t]
+__global__ __launch_bounds__(kTPB) void k_compact_moff(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                       const uint32_t* __restrict__ base, int n_tiles, int tcap,
+                                                       const uint32_t* __restrict__ mb, const uint32_t* __restrict__ db) {
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const uint32_t b = base[t], n = base[t + 1] - b, d0 = db[t] - mb[t];
+        for (uint32_t i = threadIdx.x; i < n; i += kTPB) dst[b + i] = src[(size_t)t * tcap + i] + d0;
+    }
+}
+// every tile's recipient run, mb[t] -> db[t], slots -> objects
+__global__ __launch_bounds__(kTPB) void k_runs_obj(const uint32_t* __restrict__ rcpt, int32_t* __restrict__ dst,
+                                                   const uint32_t* __restrict__ mb, const uint32_t* __restrict__ mc,
+                                                   const uint32_t* __restrict__ db, int ntt,
+                                                   const int32_t* __restrict__ slot_obj) {
+    for (int t = blockIdx.x; t < ntt; t += gridDim.x) {
+        const uint32_t s0 = mb[t], n = mc[t], d0 = db[t];
+        for (uint32_t i = threadIdx.x; i < n; i += kTPB) dst[d0 + i] = slot_obj[rcpt[(size_t)s0 + i]];
+    }
+}
+// fired entries' sort keys: (rank of the object's NFGUID, kind) and their dense index
+__global__ __launch_bounds__(kTPB) void k_fired_keys(const int32_t* __restrict__ fobj, const int32_t* __restrict__ fkind,
+                                                     const int32_t* __restrict__ rank, uint64_t* __restrict__ keys,
+                                                     uint32_t* __restrict__ idx, int n) {
+    const int i = blockIdx.x * kTPB + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = ((uint64_t)(uint32_t)rank[fobj[i]] << 5) | (uint64_t)fkind[i];
+    idx[i] = (uint32_t)i;
+}
+__global__ __launch_bounds__(kTPB) void k_permute3(const uint32_t* __restrict__ idx, const int32_t* __restrict__ a,
+                                                   const int32_t* __restrict__ b, const int32_t* __restrict__ c,
+                                                   int32_t* __restrict__ ao, int32_t* __restrict__ bo,
+                                                   int32_t* __restrict__ co, int n) {
+    const int i = blockIdx.x * kTPB + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t j = idx[i];
+    ao[i] = a[j];
+    bo[i] = b[j];
+    co[i] = c[j];
+}
+
 }  // namespace nfgpu

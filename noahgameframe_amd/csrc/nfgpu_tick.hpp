@@ -135,6 +135,8 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
 struct DynSchema {
     static constexpr bool kStatic = false;
     static constexpr uint32_t kSpecMask = 0;  // operands loaded before the fire test (none)
+    // non-temporal hints (kNt* bits): none in the library's instantiations
+    static constexpr uint32_t kNt = 0;
     static constexpr int kNK = NFK_MAX_KINDS;  // (an upper bound only)
     __device__ static int n_kind(const Dev& d) { return d.n_kind; }
     __device__ static int n_w(const Dev& d) { return d.n_w; }
@@ -159,6 +161,8 @@ struct DynSchema {
 };
 
 constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
+// non-temporal hint bits of a schema policy's kNt (NFGPU_JIT_NT for the hipRTC specialisation)
+constexpr uint32_t kNtSchedLoad = 1, kNtColLoad = 2, kNtEventStore = 4, kNtStateStore = 8, kNtFanStore = 16;
 
 // k_tick register budgets (waves per SIMD) by the frame's U slot count
 constexpr int kWavesU8 = 8, kWavesU12 = 7;
@@ -182,9 +186,9 @@ __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigne
     const int nk = S::n_kind(d) - k0;
 #pragma unroll
     for (int j = 0; j < kKindChunk; j++)
-        if (!S::kStatic || j < nk) h[j] = base[(size_t)(j < nk ? j : 0) * d.s_kstr];
+        if (!S::kStatic || j < nk) h[j] = ld_nt<(S::kNt & kNtSchedLoad) != 0>(base + (size_t)(j < nk ? j : 0) * d.s_kstr);
     if constexpr (kFirst) {
-        desc = d.fan_desc[e];
+        desc = ld_nt<(S::kNt & kNtSchedLoad) != 0>(d.fan_desc + e);
         const uint8_t ef = d.e_flags[e];  // (always allocated)
         __builtin_amdgcn_sched_barrier(0);  // the scheduler would hoist the first use and its wait
         dead = oob || desc_dead(desc);  // a slack slot has no schedules; dead slots store nothing
@@ -221,7 +225,7 @@ __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigne
             }
             h[j].state = st | kStFired;
         }
-        if (!(d.ablate & kAblNoSchedStore)) d.s_hot[(size_t)k * d.s_kstr + e] = h[j];
+        if (!(d.ablate & kAblNoSchedStore)) st_nt<(S::kNt & kNtStateStore) != 0>(d.s_hot + (size_t)k * d.s_kstr + e, h[j]);
         if (s_rem) s_rem[k * kTPB + threadIdx.x] = h[j].remain;  // for the fired list
         bytes += 16;
     }
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
 #pragma unroll
         for (int j = 0; j < kU; j++)
             if (((need >> j) & 1) && !((S::kSpecMask >> j) & 1) && !(d.ablate & kAblNoLoads)) {
-                v[j] = d.u_col[j][(size_t)e * d.u_str[j]];
+                v[j] = ld_nt<(S::kNt & kNtColLoad) != 0>(d.u_col[j] + (size_t)e * d.u_str[j]);
                 bytes += 8;
             }
 #pragma unroll
@@ -443,11 +447,12 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                     const uint32_t below = dm & S::u_lower(d, j);
                     const uint32_t at = pev0 + __builtin_popcount(below);
                     const uint64_t nv = v[j];
-                    if (!(d.ablate & kAblNoWriteBack)) d.u_col[j][(size_t)e * d.u_str[j]] = nv;
-                    st_off(t_evs, at, (uint32_t)e);
-                    st_off(t_evp, at, (uint32_t)S::u_pid(d, j));
-                    st_off(t_evo, at, s_o[j * kTPB + threadIdx.x]);
-                    st_off(t_evn, at, nv);
+                    constexpr bool kNE = (S::kNt & kNtEventStore) != 0;
+                    if (!(d.ablate & kAblNoWriteBack)) st_nt<(S::kNt & kNtStateStore) != 0>(d.u_col[j] + (size_t)e * d.u_str[j], nv);
+                    st_off_nt<kNE>(t_evs, at, (uint32_t)e);
+                    st_off_nt<kNE>(t_evp, at, (uint32_t)S::u_pid(d, j));
+                    st_off_nt<kNE>(t_evo, at, s_o[j * kTPB + threadIdx.x]);
+                    st_off_nt<kNE>(t_evn, at, nv);
                     if (!fuse)  // tile-local; k_fanout adds the tile's message base
                         st_off(t_evm, at, pmsg0 + npub * __builtin_popcount(below & pubm) +
                                               __builtin_popcount(below & privm));
@@ -494,9 +499,10 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         while (fl) {
             const int k = __builtin_ctz(fl);
             fl &= fl - 1;
-            st_off(t_fis, pfi, (uint32_t)e);
-            st_off(t_fik, pfi, (uint32_t)k);
-            st_off(t_fir, pfi, s_rem[k * kTPB + threadIdx.x]);
+            constexpr bool kNE = (S::kNt & kNtEventStore) != 0;
+            st_off_nt<kNE>(t_fis, pfi, (uint32_t)e);
+            st_off_nt<kNE>(t_fik, pfi, (uint32_t)k);
+            st_off_nt<kNE>(t_fir, pfi, s_rem[k * kTPB + threadIdx.x]);
             pfi++;
             bytes += 12;
         }
@@ -532,7 +538,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                 for (int j = 0; j < kW; j++) {
                     if (j >= S::n_w(d) || !((dm >> j) & 1)) continue;
                     const uint32_t below = dm & S::u_lower(d, j);
-                    st_off(t_evm, pev0 + __builtin_popcount(below),
+                    st_off_nt<(S::kNt & kNtEventStore) != 0>(t_evm, pev0 + __builtin_popcount(below),
                            mb + pmsg0 + npub * __builtin_popcount(below & pubm) + __builtin_popcount(below & privm));
                     bytes += 4;
                 }
@@ -571,7 +577,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                             x[0] = pmsg0 + m;
                             x[1] = f.pub ? (uint32_t)desc : (uint32_t)e;
                             x[2] = f.n | (r1 << 14) | (f.pub ? 0x80000000u : 0u);
-                            st_off(t_evm, a, mb + pmsg0 + m);
+                            st_off_nt<(S::kNt & kNtEventStore) != 0>(t_evm, a, mb + pmsg0 + m);
                             bytes += 4;
                         });
                     } else {
@@ -589,7 +595,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                             x[0] = m;
                             x[1] = pub ? (uint32_t)desc : (uint32_t)e;
                             x[2] = n | (r1 << 14) | (pub ? 0x80000000u : 0u);
-                            st_off(t_evm, at, mb + m);
+                            st_off_nt<(S::kNt & kNtEventStore) != 0>(t_evm, at, mb + m);
                             bytes += 4;
                         }
                     }
@@ -616,7 +622,10 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                                 x[q] = pq < n ? (staged ? s_pl[a - pb_lo + pp] : (uint32_t)d.pl_slot[a + pp]) : 0u;
                             }
                             if (p + 4 <= n) {
-                                *(u32x4_a4*)(out + ms + p) = u32x4_a4{x[0], x[1], x[2], x[3]};
+                                if constexpr ((S::kNt & kNtFanStore) != 0)
+                                    __builtin_nontemporal_store(u32x4_a4{x[0], x[1], x[2], x[3]}, (u32x4_a4*)(out + ms + p));
+                                else
+                                    *(u32x4_a4*)(out + ms + p) = u32x4_a4{x[0], x[1], x[2], x[3]};
                             } else {
 #pragma unroll
                                 for (int q = 0; q < 3; q++)
@@ -666,7 +675,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                             const uint32_t n4 = n >> 2;
                             uint4* dst4 = (uint4*)(out + w0);
                             const uint4* src4 = (const uint4*)s_win;
-                            for (uint32_t i = threadIdx.x; i < n4; i += kTPB) dst4[i] = src4[i];
+                            for (uint32_t i = threadIdx.x; i < n4; i += kTPB) st_nt<(S::kNt & kNtFanStore) != 0>(dst4 + i, src4[i]);
                             if (threadIdx.x < (n & 3u)) out[w0 + 4 * n4 + threadIdx.x] = s_win[4 * n4 + threadIdx.x];
                         } else {
                             for (uint32_t i = threadIdx.x; i < n; i += kTPB) out[w0 + i] = s_win[i];

@@ -69,7 +69,50 @@ void NFGPUKernelModule::SetRecordFlags(const std::string& cls, const std::string
 
 void NFGPUKernelModule::AddHeartBeatProgram(const std::string& name, const std::vector<nfk_op>& ops) {
     if (committed_) throw std::runtime_error("AddHeartBeatProgram after AfterInit");
-    heartbeats_.push_back({name, ops});
+    heartbeats_.push_back({name, ops, {}, {}, false});
+}
+
+void NFGPUKernelModule::AddHeartBeatProgram(const std::string& name, const std::vector<nfk_op>& ops,
+                                            const std::vector<std::string>& props,
+                                            const std::vector<std::string>& records) {
+    if (committed_) throw std::runtime_error("AddHeartBeatProgram after AfterInit");
+    heartbeats_.push_back({name, ops, props, records, true});
+}
+
+// a symbolic program's operands as device ids (AfterInit, once the schema is complete)
+static void resolve_program(std::vector<nfk_op>& ops, const std::vector<std::string>& props,
+                            const std::vector<std::string>& records, const std::function<int(const std::string&)>& pid,
+                            const std::function<int(const std::string&)>& rid) {
+    for (nfk_op& op : ops) {
+        auto P = [&](int64_t i) {
+            if (i < 0 || i >= (int64_t)props.size()) throw std::runtime_error("heartbeat program: property operand out of range");
+            return (int64_t)pid(props[(size_t)i]);
+        };
+        switch (op.code) {
+            case NFK_OP_IADD_CLAMP:
+                op.dst = (uint16_t)P(op.dst);
+                if (op.flags & NFK_A_PROP) op.a = P(op.a);
+                if (op.flags & NFK_LO_PROP) op.b = P(op.b);
+                if (op.flags & NFK_HI_PROP) op.c = P(op.c);
+                break;
+            case NFK_OP_FLERP:
+                op.dst = (uint16_t)P(op.dst);
+                op.a = P(op.a);
+                break;
+            case NFK_OP_FAFFINE:
+                op.dst = (uint16_t)P(op.dst);
+                break;
+            case NFK_OP_RIADD_CLAMP:
+            case NFK_OP_RFAFFINE: {
+                const size_t r = op.dst >> 8;
+                if (r >= records.size()) throw std::runtime_error("heartbeat program: record operand out of range");
+                op.dst = (uint16_t)((rid(records[r]) << 8) | (op.dst & 0xFF));
+                break;
+            }
+            default:
+                break;
+        }
+    }
 }
 
 // property ids on the device: int properties first, then float ones, then object ones, each in
@@ -201,6 +244,10 @@ bool NFGPUKernelModule::AfterInit() {
               [](const HeartBeatDef& a, const HeartBeatDef& b) { return a.name < b.name; });
     for (int k = 0; k < (int)heartbeats_.size(); k++) {
         hb_id_[heartbeats_[k].name] = k;
+        if (heartbeats_[k].symbolic)
+            resolve_program(heartbeats_[k].ops, heartbeats_[k].props, heartbeats_[k].records,
+                            [this](const std::string& n) { return PropertyId(n); },
+                            [this](const std::string& n) { return record_id_.at(n); });
         check(nfk_define_kind(world_, k, heartbeats_[k].ops.data(), (int)heartbeats_[k].ops.size()),
               "nfk_define_kind");
     }
@@ -249,6 +296,8 @@ bool NFGPUKernelModule::AfterInit() {
                                   pid_of("X", TDATA_FLOAT), pid_of("Y", TDATA_FLOAT), pid_of("Z", TDATA_FLOAT)),
               "nfk_set_scene_props");
     }
+    def_of_pid_.assign(props_.size(), 0);
+    for (int p = 0; p < (int)props_.size(); p++) def_of_pid_[PropertyId(props_[p].name)] = p;
     committed_ = true;
     return true;
 }
@@ -256,6 +305,16 @@ bool NFGPUKernelModule::AfterInit() {
 bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int nTargetGroupID, float fX, float fY,
                                     float fZ, float /*fOrient*/, const std::vector<TData>& /*arg*/) {
     if (!committed_ || ObjectIndex(self) < 0) return false;  // "There is no object" (KM:948)
+    if (shard_ && !shard_->Owns(nTargetSceneID)) {          // into another shard's scene
+        const int o = ObjectIndex(self);
+        shard_->QueueSwitch(self.nHead64, self.nData64, cls_[o], isplayer_[o], nTargetSceneID, nTargetGroupID, fX, fY,
+                            fZ);
+        obj_of_.erase(self);  // this module's no more (its index stays reserved)
+        DropFunctors(o);
+        for (auto it = sched_add_.begin(); it != sched_add_.end();)
+            it = it->first.first == o ? sched_add_.erase(it) : std::next(it);
+        return true;
+    }
     if (!scenes_.count(nTargetSceneID)) return false;       // "no this container" (KM:917)
     check(nfk_switch_scene(world_, self.nHead64, self.nData64, nTargetSceneID, nTargetGroupID, fX, fY, fZ),
           "nfk_switch_scene");
@@ -272,8 +331,7 @@ bool NFGPUKernelModule::DestroyObject(const NFGUID& self) {
     check(nfk_destroy_objects(world_, 1, &self.nHead64, &self.nData64), "nfk_destroy_objects");
     pending_calls_++;
     obj_of_.erase(self);  // its object index stays reserved; later calls find no object
-    for (auto it = sched_cb_.begin(); it != sched_cb_.end();)
-        it = it->first.first == o ? sched_cb_.erase(it) : std::next(it);
+    DropFunctors(o);
     for (auto it = sched_add_.begin(); it != sched_add_.end();)
         it = it->first.first == o ? sched_add_.erase(it) : std::next(it);
     return true;
@@ -553,41 +611,124 @@ bool NFGPUKernelModule::RemoveSchedule(const std::string& name) { return module_
 
 bool NFGPUKernelModule::ExistSchedule(const std::string& name) { return module_sched_.ExistSchedule(name); }
 
+namespace {
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace
+
+void NFGPUKernelModule::SetKindFunctor(const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb, float fTime) {
+    kind_cb_[name] = {cb, fTime};
+}
+
+// the shard exchange of this frame (collective): departures leave, arrivals become this module's
+// objects, their schedules with the functors of their names
+void NFGPUKernelModule::MigrateShard() {
+    std::vector<Ticket> sent, recv;
+    check(shard_->Migrate(&sent, &recv), "SceneShard::Migrate");
+    for (const Ticket& k : recv) {
+        const NFGUID g(k.guid_head, k.guid_data);
+        const int o = (int)guids_.size();
+        obj_of_[g] = o;
+        guids_.push_back(g);
+        scene_.push_back(k.scene);
+        group_.push_back(k.group);
+        cls_.push_back((uint8_t)k.cls);
+        isplayer_.push_back((uint8_t)k.is_player);
+        scenes_[k.scene] = true;
+        for (auto& kv : kind_cb_) {
+            auto h = hb_id_.find(kv.first);
+            if (h != hb_id_.end()) SetFunctor(o, h->second, kv.second.first, kv.second.second);
+        }
+    }
+}
+
 bool NFGPUKernelModule::Execute() {
+    const auto t0 = std::chrono::steady_clock::now();
+    stats_ = FrameStats{};
+    if (shard_) MigrateShard();
     check(nfk_execute(world_, clock_()), "nfk_execute");
     pending_calls_ = 0;
     check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
+    stats_.device = ms_since(t0);
+    auto t1 = std::chrono::steady_clock::now();
     TakeAddedSchedules();  // the AddSchedule calls this frame applied: their functors fire from now on
     const bool want_events = !common_prop_cb_.empty() || !aoi_prop_cb_.empty() || !common_rec_cb_.empty() ||
                              !aoi_rec_cb_.empty();
-    // heartbeat functors with the reference's arguments, in the order NFCScheduleModule::Execute
-    // walks mObjectScheduleMap: objects in NFGUID order, each object's schedules in name order
-    if (summary_.n_fired && !sched_cb_.empty()) {
-        std::vector<int32_t> fo(summary_.n_fired), fk(summary_.n_fired), fr(summary_.n_fired);
-        check(nfk_read_fired(world_, fo.data(), fk.data(), fr.data()), "nfk_read_fired");
-        std::vector<int64_t> ord(summary_.n_fired);
-        std::iota(ord.begin(), ord.end(), 0);
-        std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
-            return guids_[fo[a]] < guids_[fo[b]] || (guids_[fo[a]] == guids_[fo[b]] && fk[a] < fk[b]);
-        });
-        for (int64_t i : ord) {
-            auto it = sched_cb_.find({fo[i], fk[i]});
-            if (it != sched_cb_.end())
-                it->second(guids_[fo[i]], heartbeats_[fk[i]].name, sched_time_[{fo[i], fk[i]}], fr[i]);
-        }
+    const bool want_fan = !aoi_prop_cb_.empty() || !aoi_rec_cb_.empty();
+    // the frame's outputs in one read-back (nfk_read_frame): the fired list in the order
+    // NFCScheduleModule::Execute walks mObjectScheduleMap — objects in NFGUID order, each object's
+    // schedules in name order (SM:52-80), sorted on the device — and the event lists
+    uint32_t what = 0;
+    if (summary_.n_fired && n_cb_) what |= NFK_READ_FIRED | NFK_READ_FIRED_GUID_ORDER;
+    if (want_events && (summary_.n_prop_events || summary_.n_rec_events))
+        what |= NFK_READ_EVENTS | (want_fan ? NFK_READ_FANOUT : 0u);
+    nfk_frame_host fh{};
+    if (what) check(nfk_read_frame(world_, what, &fh), "nfk_read_frame");
+    stats_.events_read = ms_since(t1);
+    t1 = std::chrono::steady_clock::now();
+    // heartbeat functors with the reference's arguments
+    const int nk = (int)heartbeats_.size();
+    for (int64_t i = 0; i < fh.n_fi; i++) {
+        const int o = fh.fi_obj[i], k = fh.fi_kind[i];
+        const size_t at = (size_t)o * nk + k;
+        const int32_t c = at < cb_slot_.size() ? cb_slot_[at] : -1;
+        if (c >= 0) cb_pool_[c](guids_[o], heartbeats_[k].name, cb_time_[c], fh.fi_remain[i]);
     }
-    if (want_events) DeliverEvents();
+    stats_.functors = ms_since(t1);
+    t1 = std::chrono::steady_clock::now();
+    if (what & NFK_READ_EVENTS) DeliverEvents(fh);
+    stats_.deliver = ms_since(t1);
     // what the functors called takes effect in this Execute (SM:65: their Sets land at once;
     // SM:83-119: their Add/RemoveSchedule calls are applied at the end of the walk)
+    t1 = std::chrono::steady_clock::now();
     if (same_frame_ && pending_calls_) {
         check(nfk_execute_calls(world_), "nfk_execute_calls");
         pending_calls_ = 0;
         check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
         TakeAddedSchedules();
-        if (want_events) DeliverEvents();
+        if (want_events && (summary_.n_prop_events || summary_.n_rec_events)) {
+            nfk_frame_host f2{};
+            check(nfk_read_frame(world_, NFK_READ_EVENTS | (want_fan ? NFK_READ_FANOUT : 0u), &f2), "nfk_read_frame");
+            DeliverEvents(f2);
+        }
     }
     module_sched_.Execute(clock_);  // module schedules (SM:123-176)
+    stats_.calls = ms_since(t1);
+    stats_.total = ms_since(t0);
     return true;
+}
+
+void NFGPUKernelModule::SetFunctor(int o, int k, const OBJECT_SCHEDULE_FUNCTOR& f, float t) {
+    const size_t nk = heartbeats_.size(), at = (size_t)o * nk + k;
+    if (cb_slot_.size() < guids_.size() * nk) cb_slot_.resize(guids_.size() * nk + nk * 1024, -1);
+    int32_t c = cb_slot_[at];
+    if (c < 0) {
+        if (!cb_free_.empty()) {
+            c = cb_free_.back();
+            cb_free_.pop_back();
+        } else {
+            c = (int32_t)cb_pool_.size();
+            cb_pool_.emplace_back();
+            cb_time_.push_back(0.0f);
+        }
+        cb_slot_[at] = c;
+        n_cb_++;
+    }
+    cb_pool_[c] = f;
+    cb_time_[c] = t;
+}
+
+void NFGPUKernelModule::DropFunctors(int o) {
+    const size_t nk = heartbeats_.size();
+    for (size_t k = 0; k < nk; k++) {
+        const size_t at = (size_t)o * nk + k;
+        if (at >= cb_slot_.size() || cb_slot_[at] < 0) continue;
+        cb_pool_[cb_slot_[at]] = nullptr;
+        cb_free_.push_back(cb_slot_[at]);
+        cb_slot_[at] = -1;
+        n_cb_--;
+    }
 }
 
 // AddSchedule calls that the last device pass applied and that created a schedule: their functors
@@ -603,59 +744,38 @@ void NFGPUKernelModule::TakeAddedSchedules() {
         const int o = ObjectIndex(NFGUID(ah[i], ad[i]));
         auto it = sched_add_.find({o, ak[i]});
         if (it == sched_add_.end()) continue;
-        sched_cb_[{o, ak[i]}] = it->second.first;
-        sched_time_[{o, ak[i]}] = it->second.second;
+        SetFunctor(o, ak[i], it->second.first, it->second.second);
     }
     sched_add_.clear();
 }
 
-void NFGPUKernelModule::DeliverEvents() {
-    const int64_t ne = summary_.n_prop_events, nr = summary_.n_rec_events;
-    std::vector<int32_t> eo(ne), ep(ne);
-    std::vector<uint64_t> eold(ne), enew(ne), eoh, enh;
-    check(nfk_read_events(world_, eo.data(), ep.data(), eold.data(), enew.data()), "nfk_read_events");
-    bool has_obj = false;
-    for (auto& p : props_) has_obj |= p.type == TDATA_OBJECT;
-    if (has_obj) {
-        eoh.resize(ne);
-        enh.resize(ne);
-        check(nfk_read_events_obj(world_, eoh.data(), enh.data()), "nfk_read_events_obj");
-    }
-    std::vector<int32_t> ro(nr);
-    std::vector<uint32_t> rrc(nr);
-    std::vector<uint64_t> rold(nr), rnew(nr);
-    check(nfk_read_rec_events(world_, ro.data(), rrc.data(), rold.data(), rnew.data()), "nfk_read_rec_events");
-    std::vector<uint32_t> moff(ne + nr + 1);
-    std::vector<int32_t> mr(summary_.n_msgs);
-    check(nfk_read_fanout(world_, moff.data(), mr.data()), "nfk_read_fanout");
-    // device pid -> definition index (for the name)
-    std::vector<int> def_of(props_.size());
-    for (int p = 0; p < (int)props_.size(); p++) def_of[PropertyId(props_[p].name)] = p;
+void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f) {
     std::vector<NFGUID> rcpt;
-    for (int64_t e = 0; e < ne; e++) {
-        const PropertyDef& pd = props_[def_of[ep[e]]];
+    for (int64_t e = 0; e < f.n_ev; e++) {
+        const PropertyDef& pd = props_[def_of_pid_[f.ev_pid[e]]];
         TData a, b;
         a.type = b.type = pd.type;
         if (pd.type == TDATA_INT) {
-            a.i = (int64_t)eold[e];
-            b.i = (int64_t)enew[e];
+            a.i = (int64_t)f.ev_old[e];
+            b.i = (int64_t)f.ev_new[e];
         } else if (pd.type == TDATA_FLOAT) {
-            a.f = dbl_of(eold[e]);
-            b.f = dbl_of(enew[e]);
+            a.f = dbl_of(f.ev_old[e]);
+            b.f = dbl_of(f.ev_new[e]);
         } else {
-            a.o = NFGUID((int64_t)eoh[e], (int64_t)eold[e]);
-            b.o = NFGUID((int64_t)enh[e], (int64_t)enew[e]);
+            a.o = NFGUID((int64_t)f.ev_old_h[e], (int64_t)f.ev_old[e]);
+            b.o = NFGUID((int64_t)f.ev_new_h[e], (int64_t)f.ev_new[e]);
         }
-        const NFGUID& self = guids_[eo[e]];
+        const NFGUID& self = guids_[f.ev_obj[e]];
         for (auto& cb : common_prop_cb_) cb(self, pd.name, a, b);
-        if (!aoi_prop_cb_.empty() && moff[e + 1] > moff[e]) {  // AOI.cpp:250: no call for empty lists
+        if (f.msg_off && !aoi_prop_cb_.empty() && f.msg_off[e + 1] > f.msg_off[e]) {  // AOI.cpp:250: no call for empty lists
             rcpt.clear();
-            for (uint32_t m = moff[e]; m < moff[e + 1]; m++) rcpt.push_back(guids_[mr[m]]);
+            for (uint32_t m = f.msg_off[e]; m < f.msg_off[e + 1]; m++) rcpt.push_back(guids_[f.msg_rcpt[m]]);
             for (auto& cb : aoi_prop_cb_) cb(self, pd.name, a, b, rcpt);
         }
     }
-    for (int64_t e = 0; e < nr; e++) {
-        const int r = (rrc[e] >> 16) & 0xFF, row = (rrc[e] >> 8) & 0xFF, col = rrc[e] & 0xFF, op = rrc[e] >> 24;
+    for (int64_t e = 0; e < f.n_re; e++) {
+        const uint32_t rrc = f.re_rrc[e];
+        const int r = (rrc >> 16) & 0xFF, row = (rrc >> 8) & 0xFF, col = rrc & 0xFF, op = rrc >> 24;
         RECORD_EVENT_DATA ev;
         // row events (AddRow / Remove / Clear) carry empty values, as NFCRecord raises them (RC:177, 1098)
         ev.nOpType = op == 1 ? RECORD_EVENT_DATA::Add : op == 2 ? RECORD_EVENT_DATA::Del
@@ -667,17 +787,17 @@ void NFGPUKernelModule::DeliverEvents() {
         a.type = b.type = op ? TDATA_UNKNOWN : records_[r].cols[col];
         if (op) {
         } else if (a.type == TDATA_INT) {
-            a.i = (int64_t)rold[e];
-            b.i = (int64_t)rnew[e];
+            a.i = (int64_t)f.re_old[e];
+            b.i = (int64_t)f.re_new[e];
         } else {
-            a.f = dbl_of(rold[e]);
-            b.f = dbl_of(rnew[e]);
+            a.f = dbl_of(f.re_old[e]);
+            b.f = dbl_of(f.re_new[e]);
         }
-        const NFGUID& self = guids_[ro[e]];
+        const NFGUID& self = guids_[f.re_obj[e]];
         for (auto& cb : common_rec_cb_) cb(self, ev, a, b);
-        if (!aoi_rec_cb_.empty()) {
+        if (f.msg_off && !aoi_rec_cb_.empty()) {
             rcpt.clear();
-            for (uint32_t m = moff[ne + e]; m < moff[ne + e + 1]; m++) rcpt.push_back(guids_[mr[m]]);
+            for (uint32_t m = f.msg_off[f.n_ev + e]; m < f.msg_off[f.n_ev + e + 1]; m++) rcpt.push_back(guids_[f.msg_rcpt[m]]);
             for (auto& cb : aoi_rec_cb_) cb(self, ev.strRecordName, ev, a, b, rcpt);
         }
     }

@@ -1,0 +1,253 @@
+// NFGPUSceneShard.cpp — the cross-shard SwitchScene exchange (include/NFGPUSceneShard.hpp) and the
+// host stand-in transport.  RCCL lives in NFGPUShardRccl.cpp.
+#include "NFGPUSceneShard.hpp"
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <utility>
+
+#include "nfgpu.h"
+
+namespace nfgpu {
+
+// ---------------- HostTransport ----------------
+struct HostTransport::Shared {
+    int size;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    int64_t generation = 0;
+    std::vector<const std::vector<int64_t>*> gather_in;
+    std::vector<const uint64_t*> send;
+    std::vector<const std::vector<size_t>*> scount;
+    // a barrier every rank passes; fn runs on the last arrival, before anyone leaves
+    void barrier(const std::function<void()>& fn = nullptr) {
+        std::unique_lock<std::mutex> lk(mu);
+        const int64_t g = generation;
+        if (++arrived == size) {
+            if (fn) fn();
+            arrived = 0;
+            generation++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != g; });
+        }
+    }
+};
+
+std::shared_ptr<HostTransport::Shared> HostTransport::MakeShared(int size) {
+    auto s = std::make_shared<Shared>();
+    s->size = size;
+    s->gather_in.assign(size, nullptr);
+    s->send.assign(size, nullptr);
+    s->scount.assign(size, nullptr);
+    return s;
+}
+
+HostTransport::HostTransport(std::shared_ptr<Shared> s, int rank, RowMemory mem)
+    : s_(std::move(s)), rank_(rank), mem_(std::move(mem)) {}
+
+int HostTransport::Size() const { return s_->size; }
+
+int HostTransport::AllGather(const std::vector<int64_t>& mine, std::vector<int64_t>& all) {
+    {
+        std::lock_guard<std::mutex> lk(s_->mu);
+        s_->gather_in[rank_] = &mine;
+    }
+    s_->barrier();  // every rank's input is published
+    all.clear();
+    for (int r = 0; r < s_->size; r++) all.insert(all.end(), s_->gather_in[r]->begin(), s_->gather_in[r]->end());
+    s_->barrier();  // every rank has read (the inputs may go)
+    return NFK_OK;
+}
+
+int HostTransport::AllToAllV(const uint64_t* send, const std::vector<size_t>& scount, uint64_t* recv,
+                             const std::vector<size_t>& rcount, void*) {
+    {
+        std::lock_guard<std::mutex> lk(s_->mu);
+        s_->send[rank_] = send;
+        s_->scount[rank_] = &scount;
+    }
+    s_->barrier();
+    // pull my part of every source's buffer: source r packs its rows in destination order
+    size_t at = 0;
+    for (int r = 0; r < s_->size; r++) {
+        const std::vector<size_t>& sc = *s_->scount[r];
+        size_t off = 0;
+        for (int q = 0; q < rank_; q++) off += sc[q];
+        if (sc[rank_] != rcount[r]) return NFK_ERR_STATE;
+        if (rcount[r]) mem_.copy(recv + at, s_->send[r] + off, rcount[r] * 8);
+        at += rcount[r];
+    }
+    s_->barrier();
+    return NFK_OK;
+}
+
+// ---------------- SceneShard ----------------
+SceneShard::SceneShard(void* world, ShardTransport* t, std::function<int(int)> owner, int pid_scene, int pid_group,
+                       int pid_x, int pid_y, int pid_z, RowMemory mem, void* stream)
+    : world_(world), t_(t), owner_(std::move(owner)), pid_scene_(pid_scene), pid_group_(pid_group), pid_x_(pid_x),
+      pid_y_(pid_y), pid_z_(pid_z), mem_(std::move(mem)), stream_(stream) {}
+
+SceneShard::~SceneShard() {
+    if (sbuf_) mem_.release(sbuf_);
+    if (rbuf_) mem_.release(rbuf_);
+}
+
+void SceneShard::QueueSwitch(int64_t gh, int64_t gd, int cls, int is_player, int scene, int group, float x, float y,
+                             float z) {
+    Ticket k;
+    k.guid_head = gh;
+    k.guid_data = gd;
+    k.cls = cls;
+    k.is_player = is_player;
+    k.scene = scene;
+    k.group = group;
+    k.x = (double)x;  // SwitchScene takes floats (KM:901); the properties are doubles
+    k.y = (double)y;
+    k.z = (double)z;
+    k.src = t_->Rank();
+    k.dst = owner_(scene);
+    out_.push_back(k);
+}
+
+static uint64_t f64_bits(double v) {
+    uint64_t b;
+    memcpy(&b, &v, 8);
+    return b;
+}
+static double bits_f64(int64_t b) {
+    double v;
+    memcpy(&v, &b, 8);
+    return v;
+}
+
+int SceneShard::Migrate(std::vector<Ticket>* sent, std::vector<Ticket>* received) {
+    const int ws = t_->Size(), me = t_->Rank();
+    // 1. the frame's global plan: every rank's tickets in (source rank, call) order
+    std::vector<int64_t> mine;
+    mine.reserve(out_.size() * kTicketWords);
+    for (const Ticket& k : out_) {
+        const int64_t w[kTicketWords] = {k.guid_head, k.guid_data, k.cls, k.is_player, k.scene, k.group,
+                                         (int64_t)f64_bits(k.x), (int64_t)f64_bits(k.y), (int64_t)f64_bits(k.z),
+                                         k.src, k.dst};
+        mine.insert(mine.end(), w, w + kTicketWords);
+    }
+    out_.clear();
+    std::vector<int64_t> plan;
+    int r = t_->AllGather(mine, plan);
+    if (r) return r;
+    const size_t n = plan.size() / kTicketWords;
+    if (sent) sent->clear();
+    if (received) received->clear();
+    if (n == 0) return NFK_OK;  // the same on every rank: no row exchange this frame
+    auto tk = [&](size_t i) {
+        const int64_t* w = &plan[i * kTicketWords];
+        Ticket k;
+        k.guid_head = w[0];
+        k.guid_data = w[1];
+        k.cls = (int32_t)w[2];
+        k.is_player = (int32_t)w[3];
+        k.scene = (int32_t)w[4];
+        k.group = (int32_t)w[5];
+        k.x = bits_f64(w[6]);
+        k.y = bits_f64(w[7]);
+        k.z = bits_f64(w[8]);
+        k.src = (int32_t)w[9];
+        k.dst = (int32_t)w[10];
+        return k;
+    };
+    std::vector<Ticket> snd, rcv;
+    for (size_t i = 0; i < n; i++) {
+        const Ticket k = tk(i);
+        if (k.src == me) snd.push_back(k);
+        if (k.dst == me) rcv.push_back(k);
+    }
+    // rows in destination order (call order within one), received in source order
+    std::stable_sort(snd.begin(), snd.end(), [](const Ticket& a, const Ticket& b) { return a.dst < b.dst; });
+    std::stable_sort(rcv.begin(), rcv.end(), [](const Ticket& a, const Ticket& b) { return a.src < b.src; });
+    int32_t rw = 0;
+    r = nfk_row_words(world_, &rw);
+    if (r) return r;
+    std::vector<size_t> scount(ws, 0), rcount(ws, 0);
+    for (const Ticket& k : snd) scount[k.dst] += (size_t)rw;
+    for (const Ticket& k : rcv) rcount[k.src] += (size_t)rw;
+    auto reserve = [&](uint64_t*& buf, size_t& cap, size_t words) {
+        if (words <= cap) return;
+        if (buf) mem_.release(buf);
+        cap = words + words / 2 + 64;
+        buf = (uint64_t*)mem_.alloc(cap * 8);
+    };
+    reserve(sbuf_, scap_, snd.size() * (size_t)rw);
+    reserve(rbuf_, rcap_, rcv.size() * (size_t)rw);
+    // 2. export (the entities leave this world; their rows packed on the world's stream)
+    if (!snd.empty()) {
+        std::vector<int64_t> gh(snd.size()), gd(snd.size());
+        for (size_t i = 0; i < snd.size(); i++) {
+            gh[i] = snd[i].guid_head;
+            gd[i] = snd[i].guid_data;
+        }
+        r = nfk_export_objects(world_, (int32_t)snd.size(), gh.data(), gd.data(), sbuf_);
+        if (r) return r;
+    }
+    if (t_->NeedsHostSync()) {
+        r = nfk_sync(world_);
+        if (r) return r;
+    }
+    // 3. the rows, rank to rank
+    r = t_->AllToAllV(sbuf_, scount, rbuf_, rcount, stream_);
+    if (r) return r;
+    // 4. import, then the SwitchScene property writes (KM:930-942): GroupID = 0, SceneID, X, Y, Z,
+    // GroupID, per entity in this order (the scene always changes here)
+    if (!rcv.empty()) {
+        const size_t m = rcv.size();
+        std::vector<int64_t> gh(m), gd(m);
+        std::vector<int32_t> sc(m), gr(m);
+        std::vector<uint8_t> cl(m), pl(m);
+        for (size_t i = 0; i < m; i++) {
+            gh[i] = rcv[i].guid_head;
+            gd[i] = rcv[i].guid_data;
+            sc[i] = rcv[i].scene;
+            gr[i] = rcv[i].group;
+            cl[i] = (uint8_t)rcv[i].cls;
+            pl[i] = (uint8_t)rcv[i].is_player;
+        }
+        r = nfk_import_objects(world_, (int32_t)m, gh.data(), gd.data(), sc.data(), gr.data(), cl.data(), pl.data(),
+                               rbuf_);
+        if (r) return r;
+        std::vector<int64_t> wh, wd;
+        std::vector<int32_t> wp;
+        std::vector<uint64_t> wb;
+        for (size_t i = 0; i < m; i++) {
+            const std::pair<int, uint64_t> cols[6] = {
+                {pid_group_, 0},
+                {pid_scene_, (uint64_t)(int64_t)rcv[i].scene},
+                {pid_x_, f64_bits(rcv[i].x)},
+                {pid_y_, f64_bits(rcv[i].y)},
+                {pid_z_, f64_bits(rcv[i].z)},
+                {pid_group_, (uint64_t)(int64_t)rcv[i].group}};
+            for (const auto& c : cols) {
+                if (c.first < 0) continue;
+                wh.push_back(gh[i]);
+                wd.push_back(gd[i]);
+                wp.push_back(c.first);
+                wb.push_back(c.second);
+            }
+        }
+        if (!wp.empty()) {
+            r = nfk_set_props(world_, (int32_t)wp.size(), wh.data(), wd.data(), wp.data(), wb.data());
+            if (r) return r;
+        }
+    }
+    migrated_out += (int64_t)snd.size();
+    migrated_in += (int64_t)rcv.size();
+    if (sent) *sent = std::move(snd);
+    if (received) *received = std::move(rcv);
+    return NFK_OK;
+}
+
+}  // namespace nfgpu

@@ -255,8 +255,13 @@ int main(int argc, char** argv) {
     pm.AddModule(typeid(NFIScheduleModule).name(), &sched);
     std::vector<NFIModule*> all = {&log, &classes, &elements, &kernel, &aoi, &events, &sched};
     kernel.gpu_.SetTimeSource([] { return g_now; });
-    for (int k = 0; k < NK; k++)  // each heartbeat name's device effect program (a logic module's Init)
-        kernel.gpu_.AddHeartBeatProgram(kname[k], std::vector<nfk_op>(ops + k * NFK_MAX_OPS, ops + k * NFK_MAX_OPS + nops[k]));
+    // each heartbeat name's device effect program (a logic module's Init), operands by name: the
+    // device's property ids come from the class module at AfterInit
+    std::vector<std::string> rname;
+    for (int r = 0; r < NR; r++) rname.push_back("rec" + std::to_string(r));
+    for (int k = 0; k < NK; k++)
+        kernel.gpu_.AddHeartBeatProgram(kname[k], std::vector<nfk_op>(ops + k * NFK_MAX_OPS, ops + k * NFK_MAX_OPS + nops[k]),
+                                        pname, rname);
     for (auto* m : all) m->Awake();
     for (auto* m : all) m->Init();
     NFIKernelModule* km = &kernel;

@@ -166,10 +166,29 @@ int nfk_row_words(void* w, int32_t* n) {
     *n = S(w)->nw;
     return NFK_OK;
 }
-int nfk_export_objects(void*, int32_t, const int64_t*, const int64_t*, uint64_t*) { return NFK_ERR_STATE; }
-int nfk_import_objects(void*, int32_t, const int64_t*, const int64_t*, const int32_t*, const int32_t*, const uint8_t*,
-                       const uint8_t*, const uint64_t*) {
-    return NFK_ERR_STATE;
+// rows = the stored property words (host memory stands for device memory here)
+int nfk_export_objects(void* w, int32_t n, const int64_t* gh, const int64_t* gd, uint64_t* rows) {
+    Stub* s = S(w);
+    for (int i = 0; i < n; i++)
+        if (find(s, gh[i], gd[i]) < 0) return NFK_ERR_NOTFOUND;
+    for (int i = 0; i < n; i++) {
+        const int o = find(s, gh[i], gd[i]);
+        memcpy(rows + (size_t)i * s->nw, s->words[o].data(), (size_t)s->nw * 8);
+        s->idx.erase({gh[i], gd[i]});
+        logf("export %lld %lld", (long long)gh[i], (long long)gd[i]);
+    }
+    return NFK_OK;
+}
+int nfk_import_objects(void* w, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* sc, const int32_t* gr,
+                       const uint8_t* cl, const uint8_t* pl, const uint64_t* rows) {
+    Stub* s = S(w);
+    for (int i = 0; i < n; i++) {
+        if (find(s, gh[i], gd[i]) >= 0) return NFK_ERR_ARG;
+        const int o = add_object(s, gh[i], gd[i]);
+        memcpy(s->words[o].data(), rows + (size_t)i * s->nw, (size_t)s->nw * 8);
+        logf("import %lld %lld %d %d %d %d", (long long)gh[i], (long long)gd[i], sc[i], gr[i], cl[i], pl[i]);
+    }
+    return NFK_OK;
 }
 int nfk_spawn_objects(void* w, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* sc, const int32_t* gr,
                       const uint8_t* cl, const uint8_t* pl, const uint64_t* props) {
@@ -355,6 +374,10 @@ int nfk_read_rec_events(void*, int32_t*, uint32_t*, uint64_t*, uint64_t*) { retu
 int nfk_read_fired(void*, int32_t*, int32_t*, int32_t*) { return NFK_OK; }
 int nfk_read_fanout(void*, uint32_t* off, int32_t*) {
     off[0] = 0;
+    return NFK_OK;
+}
+int nfk_read_frame(void*, uint32_t, nfk_frame_host* out) {
+    memset(out, 0, sizeof *out);
     return NFK_OK;
 }
 int nfk_rank_top(void*, int32_t, int32_t, int32_t* n, int64_t*, int64_t*, double*) {

@@ -1,0 +1,100 @@
+"""The C++ scene-shard exchange (include/NFGPUSceneShard.hpp, noahgameframe_amd/host/NFGPUSceneShard.cpp):
+tests/cpp/shard_protocol.cpp runs two ranks as threads with the host stand-in transport.
+
+CPU: over the recording C-ABI stub — tickets all-gathered in (source rank, call) order, rows
+exported, moved and imported intact, the arrivals' SwitchScene property writes in the reference's
+order (GroupID = 0, SceneID, X, Y, Z, GroupID; KM:930-942), departed entities gone.
+GPU: the same program over libnfgpu.so, two real worlds on the one GPU, rows device to device."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "cpp", "_bin", "shard_protocol")
+STUB = os.path.join(ROOT, "tests", "cpp", "_stub")
+
+
+def _build():
+    if not (os.path.exists(EXE) and os.path.exists(os.path.join(STUB, "libnfgpu.so"))):
+        import __graft_entry__
+        __graft_entry__.build_plugin()
+
+
+def test_shard_protocol_host_stub(tmp_path):
+    _build()
+    log = str(tmp_path / "stub.log")
+    env = dict(os.environ, NFGPU_STUB_LOG=log, LD_LIBRARY_PATH=STUB + ":" + os.environ.get("LD_LIBRARY_PATH", ""))
+    r = subprocess.run([EXE, "host"], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = [ln.split() for ln in open(log)]
+    exports = [(int(x[1]), int(x[2])) for x in lines if x[0] == "export"]
+    assert sorted(exports) == sorted([(7, i) for i in (0, 2, 4)] + [(7, 100 + i) for i in (0, 2, 4)])
+    imports = [x for x in lines if x[0] == "import"]
+    assert len(imports) == 6
+    # per arrival, its writes in order: GroupID 0, SceneID, X, Y, Z, GroupID (pids 1, 0, 3, 4, 5, 1)
+    sets = [x for x in lines if x[0] == "set"]
+    by = {}
+    for x in sets:
+        by.setdefault((int(x[1]), int(x[2])), []).append((int(x[3]), int(x[4])))
+    for (h, d), w in by.items():
+        assert [p for p, _ in w] == [1, 0, 3, 4, 5, 1], (d, w)
+        assert w[0][1] == 0 and w[-1][1] == 5 + d % 100
+
+
+@pytest.mark.gpu
+def test_shard_protocol_device(gpu_available):
+    _build()
+    r = subprocess.run([EXE, "device"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "ok" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_plugin_shard_replay_matches_oracle(gpu_available, tmp_path, ranks):
+    """Scene shards through the C++ plugin (NFGPUKernelModule::AttachShard + SceneShard), ranks as
+    threads on the one GPU: every rank's callbacks (events, recipient lists, heartbeat functors) and
+    final state equal the single-world oracle restricted to the objects that rank holds, while
+    SwitchScene moves entities across shards every frame (KM:901-951)."""
+    import numpy as np
+    from noahgameframe_amd import nfio, workload
+    from tests.parity import run_oracle
+    from tests.test_shard import _oracle_per_rank
+    exe = os.path.join(ROOT, "tests", "cpp", "_bin", "plugin_shard_replay")
+    _build()
+    w = workload.make_world(n_obj=4000, n_scenes=4, groups_per_scene=5, players_per_group=3, n_ticks=8, seed=81 + ranks,
+                            switch_frac=0.03, switch_new_groups=True, ext_frac=0.05, records=True, rec_rows=8,
+                            rec_float_op=False)
+    ref = run_oracle(w)
+    wp = str(tmp_path / "w.nfio")
+    nfio.write(wp, w)
+    r = subprocess.run([exe, wp, str(tmp_path), str(ranks)], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    per, _ = _oracle_per_rank(w, ref, ranks)
+    moved = 0
+    owned = np.zeros(len(w["guid_head"]), np.int64)
+    for k in range(ranks):
+        got = nfio.read(str(tmp_path / f"rank{k}.nfio"))
+        moved += int(got["migrated"][0])
+        for t, e in enumerate(per[k]):
+            for p in ("ev", "re"):
+                for f in ("obj", "pid", "old", "new", "rrc"):
+                    if f"{p}_{f}" in e:
+                        np.testing.assert_array_equal(got[f"{p}_t{t}_{f}"].view(np.uint8), e[f"{p}_{f}"].view(np.uint8),
+                                                      err_msg=f"rank {k} frame {t} {p}_{f}")
+            # functors in NFGUID order (SM:52-80), the oracle in slot order: compare sorted
+            a = np.lexsort((got[f"fi_t{t}_kind"], got[f"fi_t{t}_obj"]))
+            b = np.lexsort((e["fi_kind"], e["fi_obj"]))
+            for f in ("obj", "kind", "rem"):
+                np.testing.assert_array_equal(got[f"fi_t{t}_{f}"][a], e[f"fi_{f}"][b], err_msg=f"rank {k} frame {t} fi_{f}")
+            off = got[f"mo_t{t}_off"].astype(np.int64)
+            lists = [got[f"mr_t{t}_obj"][off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
+            assert lists == e["ev_rcpt"] + e["re_rcpt"], f"rank {k} frame {t} fan-out"
+        own = got["final_own"].astype(bool)
+        owned += own
+        np.testing.assert_array_equal(got["final_i"][:, own], ref["final_i"][:, own])
+        np.testing.assert_array_equal(got["final_f"][:, own].view(np.uint64), ref["final_f"][:, own].view(np.uint64))
+        np.testing.assert_array_equal(got["final_s_present"][:, own], ref["final_s_present"][:, own])
+    assert np.all(owned == 1)        # every entity on exactly one shard
+    assert moved > 40 * ranks // 2   # entities did cross shards

@@ -10,7 +10,7 @@ for r in $(seq 1 "$R"); do
   i=0
   for e in "$@"; do
     i=$((i+1))
-    env $e timeout -k 5 180 python bench.py --steps 50 --warmup 5 --cpu-baseline off --host-calls off ${BENCH_ARGS:-} \
+    env $e timeout -k 5 180 python bench.py --steps 50 --warmup 5 --cpu-baseline off --host-calls off --plugin-frame off ${BENCH_ARGS:-} \
       > "$OUT/v${i}_$r.log" 2>&1 || { echo "fail $e"; tail -3 "$OUT/v${i}_$r.log"; exit 1; }
     python -c "
 import json; d=json.loads(open('$OUT/v${i}_$r.log').read().strip().splitlines()[-1])

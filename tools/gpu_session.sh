@@ -2,7 +2,7 @@
 # One GPU session: every GPU step has its own time limit; a crash/abort/timeout stops the
 # session (no further GPU work), an ordinary test failure does not.
 # usage: tools/gpu_session.sh <tag> [steps...]
-#   steps: smoke tests bench prof pmc ablate bench3 bench4 hostprof hbmmix
+#   steps: smoke tests bench prof pmc ablate bench3 bench4 hostprof hbmmix hbmstream pluginbench
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r01}; shift
@@ -21,7 +21,7 @@ run() {  # run <name> <seconds> <cmd...>
     *) echo "fatal rc=$rc in $name, stopping" | tee -a "$OUT/session.log"; exit $rc ;;
   esac
 }
-B="python bench.py --steps 20 --warmup 3 --cpu-baseline off --host-calls off ${PMCB:-}"
+B="python bench.py --steps 20 --warmup 3 --cpu-baseline off --host-calls off --plugin-frame off ${PMCB:-}"
 for step in "$@"; do
   case $step in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -39,14 +39,16 @@ for step in "$@"; do
                --entities 262144 --groups 1024 --migrate 128 --migrate-every 1 ;;
     hostprof) NFGPU_TRACE_EXEC=1 run hostprof 300 python tools/host_calls_profile.py ;;
     hbmmix) run hbmmix 120 tools/_bin/hbm_mix ;;
+    hbmstream) run hbmstream 240 tools/_bin/hbm_stream ;;
+    pluginbench) run pluginbench 600 python bench.py --steps 20 --warmup 3 --cpu-baseline off --host-calls off ;;
     membership) NFGPU_TRACE_MEMBERSHIP=1 run membership 300 python tools/membership_bench.py ;;
     selfmig) NFGPU_BENCH_TRACE=1 NFGPU_TRACE_EXEC=1 NFGPU_TRACE_MEMBERSHIP=1 run selfmig 300 python bench.py --self-migrate \
                --steps 24 --warmup 8 --cpu-baseline off --host-calls off ;;
     ablate) run ablate 600 python tools/ablate.py --variants ${ABL:-0,8,4} ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-             python bench.py --steps 50 --warmup 5 --cpu-baseline off --host-calls off ;;
+             python bench.py --steps 50 --warmup 5 --cpu-baseline off --host-calls off --plugin-frame off ;;
     prof4) run prof4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof4" -o run -- \
-             python bench.py --config 4 --steps 20 --warmup 3 --cpu-baseline off --host-calls off ;;
+             python bench.py --config 4 --steps 20 --warmup 3 --cpu-baseline off --host-calls off --plugin-frame off ;;
     pmc)
       run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o run -- \
         tools/_bin/pmc_calib
