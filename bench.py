@@ -421,8 +421,10 @@ def main():
 def plugin_frame_run(args, workload):
     """The C++ plugin's frame (NFGPUKernelModule::Execute, tests/cpp/plugin_bench.cpp, no Python in
     the loop) on the host_calls world: a functor on every schedule, a common property callback and
-    an AOI recipient callback registered; once without and once with the game logic's calls between
-    frames.  Host ms per frame and its phases (device frame, functors, event read-back, delivery)."""
+    an AOI recipient callback registered (the reference's per-call API), once without and once with
+    the game logic's calls between frames; then with the calls and one frame batch consumer
+    (AddFrameCallBack), and with no host consumer.  Host ms per frame and its phases (device frame,
+    functors, event read-back, delivery)."""
     import subprocess
     import tempfile
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "cpp", "_bin", "plugin_bench")
@@ -436,13 +438,15 @@ def plugin_frame_run(args, workload):
     with tempfile.TemporaryDirectory() as d:
         wp = os.path.join(d, "w.nfio")
         nfio.write(wp, w)
-        for calls in (0, 1):
-            r = subprocess.run([exe, wp, str(args.warmup), str(args.steps), str(calls)], capture_output=True,
-                               text=True, timeout=600)
+        # (key, game-logic calls between frames, consumer: 0 per-call API, 1 frame batch, 2 none)
+        for key, calls, consumer in (("no_calls", 0, 0), ("with_calls", 1, 0),
+                                     ("with_calls_frame_batch", 1, 1), ("with_calls_no_consumer", 1, 2)):
+            r = subprocess.run([exe, wp, str(args.warmup), str(args.steps), str(calls), str(consumer)],
+                               capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
-                res["with_calls" if calls else "no_calls"] = {"error": r.stderr[-400:]}
+                res[key] = {"error": r.stderr[-400:]}
                 continue
-            res["with_calls" if calls else "no_calls"] = json.loads(r.stdout.strip().splitlines()[-1])
+            res[key] = json.loads(r.stdout.strip().splitlines()[-1])
     return res
 
 

@@ -41,9 +41,11 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "nfgpu.h"
+#include "nfgpu_guidmap.hpp"
 #include "NFGPUSceneShard.hpp"
 
 namespace nfgpu {
@@ -283,6 +285,16 @@ public:
     bool AddPropertyEventCallBack(const PROPERTY_SINGLE_EVENT_FUNCTOR& cb);
     bool AddRecordEventCallBack(const RECORD_SINGLE_EVENT_FUNCTOR& cb);
 
+    // ---- frame batch consumers: one call per device pass instead of one per event ----
+    // The pass's outputs as arrays (nfk_read_frame's nfk_frame_host: the fired list, property and
+    // record events, the recipient CSR, all in object-index terms; objects[i] is object i's
+    // NFGUID), called after the per-event callbacks of the same pass.  `what` = the NFK_READ_* bits
+    // the consumer needs (fired in NFGUID order only with NFK_READ_FIRED_GUID_ORDER).  A network
+    // layer that packs the dirty-sync messages itself reads them this way: the per-event std::function
+    // calls of the reference's callback API then cost nothing.  The arrays are valid during the call.
+    using FRAME_FUNCTOR = std::function<void(const nfk_frame_host&, const NFGUID* objects)>;
+    bool AddFrameCallBack(const FRAME_FUNCTOR& cb, uint32_t what);
+
     void* World() const { return world_; }
     const nfk_summary& LastSummary() const { return summary_; }
     // host wall time of the last Execute by phase (ms): the device frame (nfk_execute and the wait
@@ -307,17 +319,18 @@ private:
     void* stream_;
     bool committed_ = false;
     std::vector<PropertyDef> props_;
-    std::map<std::string, int> prop_id_;
+    std::unordered_map<std::string, int> prop_id_;
+    std::vector<int> dev_pid_;  // props_ index -> device property id (AfterInit)
     std::vector<ClassDef> classes_;
     std::map<std::string, int> class_id_;
     std::vector<RecordDef> records_;
-    std::map<std::string, int> record_id_;
+    std::unordered_map<std::string, int> record_id_;
     std::vector<HeartBeatDef> heartbeats_;
-    std::map<std::string, int> hb_id_;
+    std::unordered_map<std::string, int> hb_id_;
     std::map<int, bool> scenes_;
     // objects
     std::vector<NFGUID> guids_;
-    std::map<NFGUID, int> obj_of_;
+    nfgpu_detail::GuidMap obj_of_;  // NFGUID -> object index (open addressing)
     std::vector<int32_t> scene_, group_;
     std::vector<uint8_t> cls_, isplayer_;
     std::vector<std::vector<uint64_t>> init_;
@@ -327,6 +340,9 @@ private:
     std::vector<RECORD_EVENT_FUNCTOR> common_rec_cb_;
     std::vector<PROPERTY_SINGLE_EVENT_FUNCTOR> aoi_prop_cb_;
     std::vector<RECORD_SINGLE_EVENT_FUNCTOR> aoi_rec_cb_;
+    std::vector<FRAME_FUNCTOR> frame_cb_;
+    uint32_t frame_what_ = 0;  // union of the frame consumers' NFK_READ_* bits
+    uint32_t ReadMask(bool per_event_fired) const;
     // the functor of each (object, kind) schedule: cb_slot_[object * n_kind + kind] indexes
     // cb_pool_ / cb_time_ (-1: none); freed entries are reused
     std::vector<int32_t> cb_slot_;
@@ -338,7 +354,8 @@ private:
     void DropFunctors(int o);
     std::vector<int> def_of_pid_;  // device property id -> props_ index
     // pending functors of AddSchedule calls in this window ((object, kind), first call wins)
-    std::map<std::pair<int, int>, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> sched_add_;
+    // key: object << 8 | kind
+    std::unordered_map<uint64_t, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> sched_add_;
     ModuleScheduler module_sched_;
     SceneShard* shard_ = nullptr;
     std::map<std::string, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> kind_cb_;  // arrivals' functors

@@ -1,0 +1,95 @@
+// nfgpu_guidmap.hpp — NFGUID -> index hash table shared by libnfgpu.so and the C++ plugin (an
+// internal helper, not part of the C-ABI).
+#pragma once
+#include <algorithm>
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace nfgpu_detail {
+
+// NFGUID -> object index (the reference's NFMapEx<NFGUID, NFIObject> lookup, KM:323): open
+// addressing, linear probing, backward-shift deletion; every SetProperty / schedule call does one
+// lookup, so this is the host's per-call cost
+class GuidMap {
+public:
+    int32_t find(int64_t h, int64_t d) const {
+        if (cap_ == 0) return -1;
+        for (size_t i = slot(h, d);; i = (i + 1) & (cap_ - 1)) {
+            const E& e = t_[i];
+            if (e.v < 0) return -1;
+            if (e.h == h && e.d == d) return e.v;
+        }
+    }
+    bool count(int64_t h, int64_t d) const { return find(h, d) >= 0; }
+    // n lookups with the home slots of the lookups kPre ahead prefetched (a batch of calls is
+    // bound by the table's cache misses, not by the probing)
+    void find_many(int32_t n, const int64_t* h, const int64_t* d, int32_t* out) const {
+        constexpr int32_t kPre = 32;
+        if (cap_ == 0) {
+            for (int32_t i = 0; i < n; i++) out[i] = -1;
+            return;
+        }
+        for (int32_t i = 0; i < n && i < kPre; i++) __builtin_prefetch(&t_[slot(h[i], d[i])]);
+        for (int32_t i = 0; i < n; i++) {
+            if (i + kPre < n) __builtin_prefetch(&t_[slot(h[i + kPre], d[i + kPre])]);
+            out[i] = find(h[i], d[i]);
+        }
+    }
+    void insert(int64_t h, int64_t d, int32_t v) {
+        if ((n_ + 1) * 2 > cap_) rehash(std::max<size_t>(64, cap_ * 2));
+        size_t i = slot(h, d);
+        for (; t_[i].v >= 0; i = (i + 1) & (cap_ - 1))
+            if (t_[i].h == h && t_[i].d == d) {
+                t_[i].v = v;
+                return;
+            }
+        t_[i] = E{h, d, v};
+        n_++;
+    }
+    void erase(int64_t h, int64_t d) {
+        if (cap_ == 0) return;
+        size_t i = slot(h, d);
+        for (;; i = (i + 1) & (cap_ - 1)) {
+            if (t_[i].v < 0) return;
+            if (t_[i].h == h && t_[i].d == d) break;
+        }
+        // backward shift: pull later members of the probe run into the hole
+        for (size_t j = (i + 1) & (cap_ - 1);; j = (j + 1) & (cap_ - 1)) {
+            if (t_[j].v < 0) break;
+            const size_t home = slot(t_[j].h, t_[j].d);
+            if (((j - home) & (cap_ - 1)) >= ((j - i) & (cap_ - 1))) {
+                t_[i] = t_[j];
+                i = j;
+            }
+        }
+        t_[i].v = -1;
+        n_--;
+    }
+
+private:
+    struct E {
+        int64_t h, d;
+        int32_t v = -1;
+    };
+    size_t slot(int64_t h, int64_t d) const {
+        uint64_t x = (uint64_t)h * 0x9E3779B97F4A7C15ull ^ (uint64_t)d;
+        x ^= x >> 31;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 29;
+        return (size_t)x & (cap_ - 1);
+    }
+    void rehash(size_t c) {
+        std::vector<E> old;
+        old.swap(t_);
+        t_.assign(c, E{});
+        cap_ = c;
+        n_ = 0;
+        for (const E& e : old)
+            if (e.v >= 0) insert(e.h, e.d, e.v);
+    }
+    std::vector<E> t_;
+    size_t cap_ = 0, n_ = 0;
+};
+
+}  // namespace nfgpu_detail

@@ -21,6 +21,8 @@
 
 #include "nfgpu_jit.hpp"
 #include "nfgpu_kernels.hip"
+#include "../../include/nfgpu_guidmap.hpp"
+#include "nfgpu_pool.hpp"
 
 using namespace nfgpu;
 
@@ -40,89 +42,8 @@ int fail(int code, const std::string& msg) {
             return fail(NFK_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(_e));     \
     } while (0)
 
-// NFGUID -> object index (the reference's NFMapEx<NFGUID, NFIObject> lookup, KM:323): open
-// addressing, linear probing, backward-shift deletion; every SetProperty / schedule call does one
-// lookup, so this is the host's per-call cost
-class GuidMap {
-public:
-    int32_t find(int64_t h, int64_t d) const {
-        if (cap_ == 0) return -1;
-        for (size_t i = slot(h, d);; i = (i + 1) & (cap_ - 1)) {
-            const E& e = t_[i];
-            if (e.v < 0) return -1;
-            if (e.h == h && e.d == d) return e.v;
-        }
-    }
-    bool count(int64_t h, int64_t d) const { return find(h, d) >= 0; }
-    // n lookups with the home slots of the lookups kPre ahead prefetched (a batch of calls is
-    // bound by the table's cache misses, not by the probing)
-    void find_many(int32_t n, const int64_t* h, const int64_t* d, int32_t* out) const {
-        constexpr int32_t kPre = 32;
-        if (cap_ == 0) {
-            for (int32_t i = 0; i < n; i++) out[i] = -1;
-            return;
-        }
-        for (int32_t i = 0; i < n && i < kPre; i++) __builtin_prefetch(&t_[slot(h[i], d[i])]);
-        for (int32_t i = 0; i < n; i++) {
-            if (i + kPre < n) __builtin_prefetch(&t_[slot(h[i + kPre], d[i + kPre])]);
-            out[i] = find(h[i], d[i]);
-        }
-    }
-    void insert(int64_t h, int64_t d, int32_t v) {
-        if ((n_ + 1) * 2 > cap_) rehash(std::max<size_t>(64, cap_ * 2));
-        size_t i = slot(h, d);
-        for (; t_[i].v >= 0; i = (i + 1) & (cap_ - 1))
-            if (t_[i].h == h && t_[i].d == d) {
-                t_[i].v = v;
-                return;
-            }
-        t_[i] = E{h, d, v};
-        n_++;
-    }
-    void erase(int64_t h, int64_t d) {
-        if (cap_ == 0) return;
-        size_t i = slot(h, d);
-        for (;; i = (i + 1) & (cap_ - 1)) {
-            if (t_[i].v < 0) return;
-            if (t_[i].h == h && t_[i].d == d) break;
-        }
-        // backward shift: pull later members of the probe run into the hole
-        for (size_t j = (i + 1) & (cap_ - 1);; j = (j + 1) & (cap_ - 1)) {
-            if (t_[j].v < 0) break;
-            const size_t home = slot(t_[j].h, t_[j].d);
-            if (((j - home) & (cap_ - 1)) >= ((j - i) & (cap_ - 1))) {
-                t_[i] = t_[j];
-                i = j;
-            }
-        }
-        t_[i].v = -1;
-        n_--;
-    }
-
-private:
-    struct E {
-        int64_t h, d;
-        int32_t v = -1;
-    };
-    size_t slot(int64_t h, int64_t d) const {
-        uint64_t x = (uint64_t)h * 0x9E3779B97F4A7C15ull ^ (uint64_t)d;
-        x ^= x >> 31;
-        x *= 0xBF58476D1CE4E5B9ull;
-        x ^= x >> 29;
-        return (size_t)x & (cap_ - 1);
-    }
-    void rehash(size_t c) {
-        std::vector<E> old;
-        old.swap(t_);
-        t_.assign(c, E{});
-        cap_ = c;
-        n_ = 0;
-        for (const E& e : old)
-            if (e.v >= 0) insert(e.h, e.d, e.v);
-    }
-    std::vector<E> t_;
-    size_t cap_ = 0, n_ = 0;
-};
+using nfgpu_detail::GuidMap;
+using nfgpu_detail::HostPool;
 
 template <typename T>
 int dalloc(T** p, size_t n) {
@@ -261,6 +182,9 @@ struct World {
     uint8_t* added_d = nullptr;
     size_t added_cap = 0;
     std::vector<uint64_t> xpk, xpk_t, hpk, hpk_t;  // packed (key << 32 | call index) sort scratch
+    // host worker threads for large call batches (NFGPU_HOST_THREADS, default 4 in all; 1 = none)
+    std::unique_ptr<HostPool> pool;
+    size_t par_calls = 16384;  // batches from this size on use the pool (NFGPU_PAR_CALLS: tests)
     // queued SetRecordInt / SetRecordFloat calls (obj: object index until nfk_execute resolves it;
     // rrc = rec << 16 | row << 8 | col) and their folding scratch
     // op 0 SetRecord*, 1 AddRow (row 0xFF: -1; aux = its values' index in rvals, or 0xFFFFFFFF),
@@ -619,6 +543,103 @@ void radix_sort_packed(std::vector<uint64_t>& a, std::vector<uint64_t>& t, int s
 }
 int bits_for(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 1; }
 
+// radix_sort_packed on a range a[0, n) with scratch t[0, n); the result is in a
+void radix_sort_range(uint64_t* a, uint64_t* t, size_t n, int shift, int key_bits) {
+    if (n < 2) return;
+    uint32_t cnt[2048];
+    bool in_t = false;
+    for (int sh = shift; sh < shift + key_bits; sh += 11) {
+        memset(cnt, 0, sizeof cnt);
+        for (size_t i = 0; i < n; i++) cnt[(a[i] >> sh) & 2047]++;
+        if (cnt[(a[0] >> sh) & 2047] == n) continue;
+        uint32_t acc = 0;
+        for (int b = 0; b < 2048; b++) {
+            const uint32_t c = cnt[b];
+            cnt[b] = acc;
+            acc += c;
+        }
+        for (size_t i = 0; i < n; i++) t[cnt[(a[i] >> sh) & 2047]++] = a[i];
+        std::swap(a, t);
+        in_t = !in_t;
+    }
+    if (in_t) memcpy(t, a, n * 8);  // (a and t swapped: copy back into the caller's a)
+}
+
+// GuidMap::find_many split over the host pool for a large batch
+void find_many_par(World* w, int32_t n, const int64_t* gh, const int64_t* gd, int32_t* out) {
+    if ((size_t)n < w->par_calls || w->pool->threads() < 2) {
+        w->obj_of.find_many(n, gh, gd, out);
+        return;
+    }
+    const int P = w->pool->threads();
+    w->pool->run(P, [&](int c) {
+        const int32_t a = (int32_t)((int64_t)n * c / P), b = (int32_t)((int64_t)n * (c + 1) / P);
+        w->obj_of.find_many(b - a, gh + a, gd + a, out + a);
+    });
+}
+
+// A window's calls folded into a packed array (key << ib | call index) sorted by key, call order
+// within a key — radix_sort_packed's result — on the host pool: key(i) gives call i's key (or
+// ~0ull: dropped), whose slot is key >> slot_shift.  The keys are split by slot range into P
+// buckets, each a run of whole 256-slot tiles (so no (slot, *) group and no tile straddles two),
+// scattered into bucket order in call order, and each bucket is radix-sorted by one thread.
+// bucket_end[b] = where bucket b ends in out.  Returns the OR of the keys.
+template <class KeyFn>
+uint64_t fold_sorted(World* w, size_t n, int ib, int slot_shift, KeyFn key, std::vector<uint64_t>& out,
+                     std::vector<uint64_t>& tmp, std::vector<size_t>& bucket_end) {
+    HostPool& pool = *w->pool;
+    const int P = pool.threads();
+    const int C = P;  // call chunks
+    const size_t span = ((size_t)(w->d.cap + P - 1) / P + kTile - 1) / kTile * kTile;
+    std::vector<uint32_t> cnt((size_t)C * P, 0);
+    std::vector<uint64_t> kor_c(C, 0);
+    tmp.resize(n);
+    out.resize(n);
+    pool.run(C, [&](int c) {
+        const size_t a = n * c / C, b = n * (c + 1) / C;
+        uint32_t* cc = &cnt[(size_t)c * P];
+        uint64_t kor = 0;
+        for (size_t i = a; i < b; i++) {
+            const uint64_t k = key(i);
+            if (k == ~0ull) {
+                tmp[i] = ~0ull;
+                continue;
+            }
+            kor |= k;
+            tmp[i] = (k << ib) | i;
+            cc[(k >> slot_shift) / span]++;
+        }
+        kor_c[c] = kor;
+    });
+    uint64_t kor = 0;
+    for (int c = 0; c < C; c++) kor |= kor_c[c];
+    // (bucket, chunk) offsets: bucket-major, chunks in call order
+    std::vector<size_t> off((size_t)C * P);
+    bucket_end.assign(P, 0);
+    size_t acc = 0;
+    for (int b = 0; b < P; b++) {
+        for (int c = 0; c < C; c++) {
+            off[(size_t)c * P + b] = acc;
+            acc += cnt[(size_t)c * P + b];
+        }
+        bucket_end[b] = acc;
+    }
+    out.resize(acc);
+    if (bits_for(kor) + ib > 64) return kor;  // (the caller reports the capacity failure)
+    pool.run(C, [&](int c) {
+        const size_t a = n * c / C, b = n * (c + 1) / C;
+        size_t* oc = &off[(size_t)c * P];
+        for (size_t i = a; i < b; i++)
+            if (tmp[i] != ~0ull) out[oc[((tmp[i] >> ib) >> slot_shift) / span]++] = tmp[i];
+    });
+    const int kb = bits_for(kor);
+    pool.run(P, [&](int b) {
+        const size_t a = b ? bucket_end[b - 1] : 0, e = bucket_end[b];
+        radix_sort_range(out.data() + a, tmp.data() + a, e - a, ib, kb);
+    });
+    return kor;
+}
+
 // replace a tracked device allocation by a bigger one (contents dropped)
 int regrow(World* w, void** p, size_t bytes) {
     if (*p) {
@@ -785,8 +806,11 @@ int tick_waves(int n_u, uint32_t ablate) {
     return 6;
 }
 
-// the non-temporal hints the specialised k_tick is built with (A/B: NFGPU_JIT_NT)
-constexpr uint32_t kJitNtDefault = 0;
+// the non-temporal hints the specialised k_tick is built with (A/B: NFGPU_JIT_NT): the schedule
+// records / descriptor loads and the fan-out's recipient stores stream past the caches (config[1]:
+// 90 vs 115 us with none, 102 with the fan-out stores alone; event-array stores non-temporal run
+// 160 us; profiles/r07a_ntab.txt)
+constexpr uint32_t kJitNtDefault = kNtSchedLoad | kNtFanStore;
 
 // Specialised k_tick kernels built in this process, by (device, variant, policy source): a
 // schema compiles once however many worlds use it.
@@ -1385,6 +1409,12 @@ int nfk_create(const nfk_config* cfg, void** out) {
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev == 0) return fail(NFK_ERR_HIP, "no HIP device available");
     World* w = new World();
+    {
+        int nt = 4;  // host threads for large call batches (the caller and nt - 1 workers)
+        if (const char* e = getenv("NFGPU_HOST_THREADS")) nt = std::max(1, std::min(64, atoi(e)));
+        w->pool.reset(new HostPool(nt - 1));
+        if (const char* e = getenv("NFGPU_PAR_CALLS")) w->par_calls = (size_t)std::max(1, atoi(e));
+    }
     w->cfg = *cfg;
     w->n_if = cfg->n_int + cfg->n_flt;
     w->n_prop = w->n_if + cfg->n_obj;
@@ -1946,7 +1976,7 @@ int nfk_set_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
     w->xops.resize(at + (size_t)n);
     World::XOp* x = w->xops.data() + at;
     w->look.resize(n);
-    w->obj_of.find_many(n, gh, gd, w->look.data());
+    find_many_par(w, n, gh, gd, w->look.data());
     for (int32_t i = 0; i < n; i++) {
         const int32_t obj = w->look[i];
         if (obj < 0 || pid[i] < 0 || pid[i] >= w->n_if) {
@@ -1968,7 +1998,7 @@ int nfk_set_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     if (!w || n < 0 || (n && (!gh || !gd || !pid || !vh || !vd))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     w->look.resize(n);
-    w->obj_of.find_many(n, gh, gd, w->look.data());
+    find_many_par(w, n, gh, gd, w->look.data());
     for (int32_t i = 0; i < n; i++) {
         if (w->look[i] < 0)  // "There is no object" (KM:370)
             return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
@@ -1990,7 +2020,7 @@ int nfk_set_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     // every call is checked before any is queued; one GUID lookup per call
     w->look.resize(n);
-    w->obj_of.find_many(n, gh, gd, w->look.data());
+    find_many_par(w, n, gh, gd, w->look.data());
     for (int32_t i = 0; i < n; i++) {
         if (w->look[i] < 0)  // NFCKernelModule logs "There is no object" and returns false (KM:505)
             return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
@@ -2016,7 +2046,7 @@ int nfk_record_rows(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     if (!w || n < 0 || (n && (!gh || !gd || !rec || !op || !row))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     w->look.resize(n);
-    w->obj_of.find_many(n, gh, gd, w->look.data());
+    find_many_par(w, n, gh, gd, w->look.data());
     for (int32_t i = 0; i < n; i++) {
         if (w->look[i] < 0)  // FindRecord: "There is no object" (KM:487)
             return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
@@ -2108,7 +2138,7 @@ int nfk_get_used_rows(void* world, int32_t n, const int64_t* gh, const int64_t* 
     if (!w || n < 0 || (n && (!gh || !gd || !rec || !masks))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     std::vector<int32_t> obj(n);
-    w->obj_of.find_many(n, gh, gd, obj.data());
+    find_many_par(w, n, gh, gd, obj.data());
     std::vector<uint64_t> addr;
     std::vector<int32_t> miss;
     for (int32_t i = 0; i < n; i++) {
@@ -2142,7 +2172,7 @@ int nfk_get_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     if (!w || n < 0 || (n && (!gh || !gd || !rec || !row || !col || !bits))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     std::vector<int32_t> obj(n);
-    w->obj_of.find_many(n, gh, gd, obj.data());
+    find_many_par(w, n, gh, gd, obj.data());
     for (int32_t i = 0; i < n; i++) {
         if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
         const int32_t r = rec[i];
@@ -2269,7 +2299,7 @@ int nfk_schedule_calls(void* world, int32_t n, const int32_t* op, const int64_t*
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     std::vector<int32_t>& obj = w->look;
     obj.resize(n);
-    w->obj_of.find_many(n, gh, gd, obj.data());
+    find_many_par(w, n, gh, gd, obj.data());
     for (int32_t i = 0; i < n; i++) {
         if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
         if (op[i] < 1 || op[i] > 3) return fail(NFK_ERR_ARG, "schedule call op must be 1, 2 or 3");
@@ -2337,7 +2367,7 @@ int nfk_get_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     if (!w || n < 0 || (n && (!gh || !gd || !pid || !vh || !vd))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     std::vector<int32_t> obj(n);
-    w->obj_of.find_many(n, gh, gd, obj.data());
+    find_many_par(w, n, gh, gd, obj.data());
     std::vector<uint64_t> src(2 * (size_t)n), got(2 * (size_t)n);
     for (int32_t i = 0; i < n; i++) {
         if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
@@ -2367,7 +2397,7 @@ int nfk_get_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
     if (!w || n < 0 || (n && (!gh || !gd || !pid || !bits))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     std::vector<int32_t> obj(n);
-    w->obj_of.find_many(n, gh, gd, obj.data());
+    find_many_par(w, n, gh, gd, obj.data());
     for (int32_t i = 0; i < n; i++) {
         if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
         if (pid[i] < 0 || pid[i] >= w->n_if) return fail(NFK_ERR_ARG, "bad property id (object properties: nfk_get_objects)");
@@ -2717,44 +2747,75 @@ int nfk_execute(void* world, int64_t now_ms) {
     const int xib = bits_for(n_xq);
     const uint64_t xim = (1ull << xib) - 1;
     if (n_xq) {
-        xpk.resize(n_xq);
-        uint64_t kor = 0;
-        size_t k = 0;
-        for (size_t i = 0; i < n_xq; i++) {
-            if (i + 16 < n_xq) __builtin_prefetch(&w->slot_of_obj[w->xops[i + 16].slot]);
-            const int32_t sl = w->slot_of_obj[w->xops[i].slot];
-            if (sl < 0) continue;
-            const uint64_t key = ((uint64_t)(uint32_t)sl << 7) | w->xops[i].pid;
-            kor |= key;
-            xpk[k++] = (key << xib) | i;
-        }
-        xpk.resize(k);
-        if (bits_for(kor) + xib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued SetProperty calls"));
-        radix_sort_packed(xpk, w->xpk_t, xib, bits_for(kor));
-        int64_t tile_sa = 0;
-        uint32_t cur_tile = 0xFFFFFFFFu;
-        uint64_t prev = ~0ull;
-        g_slot.reserve(k);
-        g_pid.reserve(k);
-        g_first.reserve(k + 1);
-        for (size_t i = 0; i < k; i++) {
-            const uint64_t key = xpk[i] >> xib;
-            if (key != prev) {
+        // the (slot, property) groups of xpk[a, e) (sorted): group starts, and the most
+        // standalone groups of one tile
+        auto group_range = [&](size_t a, size_t e, std::vector<uint32_t>& gs, std::vector<uint32_t>& gp,
+                               std::vector<uint32_t>& gf, int64_t& msa) {
+            int64_t tile_sa = 0;
+            uint32_t cur_tile = 0xFFFFFFFFu;
+            uint64_t prev = ~0ull;
+            for (size_t i = a; i < e; i++) {
+                const uint64_t key = xpk[i] >> xib;
+                if (key == prev) continue;
                 prev = key;
                 const uint32_t sl = (uint32_t)(key >> 7), pid = (uint32_t)(key & 127);
-                g_slot.push_back(sl);
-                g_pid.push_back(pid);
-                g_first.push_back((uint32_t)i);
+                gs.push_back(sl);
+                gp.push_back(pid);
+                gf.push_back((uint32_t)i);
                 if (w->tab.w_slot[pid] == kNoU) {
                     if (sl / kTile != cur_tile) {
                         cur_tile = sl / kTile;
                         tile_sa = 0;
                     }
-                    max_sa = std::max(max_sa, ++tile_sa);
+                    msa = std::max(msa, ++tile_sa);
                 }
             }
+        };
+        if (n_xq >= w->par_calls && w->pool->threads() > 1) {
+            // on the host pool: slot ranges folded by one thread each (fold_sorted), then grouped
+            // per range and concatenated (a group never straddles two ranges)
+            std::vector<size_t> bend;
+            const uint64_t kor = fold_sorted(
+                w, n_xq, xib, 7,
+                [&](size_t i) -> uint64_t {
+                    if (i + 16 < n_xq) __builtin_prefetch(&w->slot_of_obj[w->xops[i + 16].slot]);
+                    const int32_t sl = w->slot_of_obj[w->xops[i].slot];
+                    return sl < 0 ? ~0ull : (((uint64_t)(uint32_t)sl << 7) | w->xops[i].pid);
+                },
+                xpk, w->xpk_t, bend);
+            if (bits_for(kor) + xib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued SetProperty calls"));
+            const int P = (int)bend.size();
+            std::vector<std::vector<uint32_t>> bs(P), bp(P), bf(P);
+            std::vector<int64_t> bm(P, 0);
+            w->pool->run(P, [&](int b) { group_range(b ? bend[b - 1] : 0, bend[b], bs[b], bp[b], bf[b], bm[b]); });
+            for (int b = 0; b < P; b++) {
+                g_slot.insert(g_slot.end(), bs[b].begin(), bs[b].end());
+                g_pid.insert(g_pid.end(), bp[b].begin(), bp[b].end());
+                g_first.insert(g_first.end(), bf[b].begin(), bf[b].end());
+                max_sa = std::max(max_sa, bm[b]);
+            }
+            g_first.push_back((uint32_t)xpk.size());
+        } else {
+            xpk.resize(n_xq);
+            uint64_t kor = 0;
+            size_t k = 0;
+            for (size_t i = 0; i < n_xq; i++) {
+                if (i + 16 < n_xq) __builtin_prefetch(&w->slot_of_obj[w->xops[i + 16].slot]);
+                const int32_t sl = w->slot_of_obj[w->xops[i].slot];
+                if (sl < 0) continue;
+                const uint64_t key = ((uint64_t)(uint32_t)sl << 7) | w->xops[i].pid;
+                kor |= key;
+                xpk[k++] = (key << xib) | i;
+            }
+            xpk.resize(k);
+            if (bits_for(kor) + xib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued SetProperty calls"));
+            radix_sort_packed(xpk, w->xpk_t, xib, bits_for(kor));
+            g_slot.reserve(k);
+            g_pid.reserve(k);
+            g_first.reserve(k + 1);
+            group_range(0, k, g_slot, g_pid, g_first, max_sa);
+            g_first.push_back((uint32_t)k);
         }
-        g_first.push_back((uint32_t)k);
     }
     const size_t nxc = xpk.size();
     // a tile's events: its slots' program destinations plus its standalone Set groups
@@ -2948,62 +3009,86 @@ int nfk_execute(void* world, int64_t now_ms) {
         std::vector<uint64_t>& hpk = w->hpk;
         const int hib = bits_for(n_hq);
         const uint64_t him = (1ull << hib) - 1;
-        hpk.resize(n_hq);
-        uint64_t kor = 0;
-        size_t nh = 0;
-        for (size_t i = 0; i < n_hq; i++) {
+        // the per-slot folding of hpk[a0, e0) (sorted) into pre-scan and post-scan entries
+        auto fold_range = [&](size_t a0, size_t e0, std::vector<uint32_t>& ps, std::vector<uint32_t>& po,
+                              std::vector<Post>& pq) {
+            for (size_t a = a0; a < e0;) {
+                const uint32_t slot = (uint32_t)((hpk[a] >> hib) >> 5);
+                size_t b = a;
+                uint32_t owner_seq = 0xFFFFFFFFu, owner_kind = 0;
+                bool erase_all = false;
+                for (; b < e0 && (uint32_t)((hpk[b] >> hib) >> 5) == slot; b++) {
+                    const uint32_t seq = (uint32_t)(hpk[b] & him);
+                    const World::HOp& h = w->hops[seq];
+                    if (h.code == 3) erase_all = true;
+                    if (h.code == 2 && seq < owner_seq) {
+                        owner_seq = seq;
+                        owner_kind = h.kind;
+                    }
+                }
+                if (erase_all) {
+                    ps.push_back(slot);
+                    po.push_back(2);
+                }
+                if (owner_seq != 0xFFFFFFFFu) {
+                    ps.push_back(slot);
+                    po.push_back(1);
+                    if (owner_kind == kNoKind) pq.push_back(Post{slot, 0u, 8u, 0.f, 0, 0});  // release the key only
+                }
+                for (size_t c = a; c < b;) {
+                    const uint32_t kind = (uint32_t)((hpk[c] >> hib) & 31);
+                    size_t e = c;
+                    Post p{slot, kind, 0u, 0.f, 0, 0};
+                    if (owner_seq != 0xFFFFFFFFu && owner_kind == kind) p.op |= 1u | 4u;
+                    for (; e < b && (uint32_t)((hpk[e] >> hib) & 31) == kind; e++) {
+                        const World::HOp& h = w->hops[hpk[e] & him];
+                        if (h.code == 1 && !(p.op & 2u)) {
+                            p.op |= 2u;
+                            p.interval = h.interval;
+                            p.count = h.count;
+                            p.time = h.time;
+                        }
+                    }
+                    if (p.op) pq.push_back(p);
+                    c = e;
+                }
+                a = b;
+            }
+        };
+        auto hkey = [&](size_t i) -> uint64_t {
             const World::HOp& h = w->hops[i];
             if (i + 16 < n_hq) __builtin_prefetch(&w->slot_of_obj[w->hops[i + 16].slot]);
             const int32_t sl = w->slot_of_obj[h.slot];
-            if (sl < 0) continue;
-            const uint64_t key = ((uint64_t)(uint32_t)sl << 5) | (h.code == 3 || h.kind == kNoKind ? 0u : h.kind);
-            kor |= key;
-            hpk[nh++] = (key << hib) | i;
-        }
-        hpk.resize(nh);
-        if (bits_for(kor) + hib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued schedule calls"));
-        radix_sort_packed(hpk, w->hpk_t, hib, bits_for(kor));
-        for (size_t a = 0; a < nh;) {
-            const uint32_t slot = (uint32_t)((hpk[a] >> hib) >> 5);
-            size_t b = a;
-            uint32_t owner_seq = 0xFFFFFFFFu, owner_kind = 0;
-            bool erase_all = false;
-            for (; b < nh && (uint32_t)((hpk[b] >> hib) >> 5) == slot; b++) {
-                const uint32_t seq = (uint32_t)(hpk[b] & him);
-                const World::HOp& h = w->hops[seq];
-                if (h.code == 3) erase_all = true;
-                if (h.code == 2 && seq < owner_seq) {
-                    owner_seq = seq;
-                    owner_kind = h.kind;
-                }
+            if (sl < 0) return ~0ull;
+            return ((uint64_t)(uint32_t)sl << 5) | (h.code == 3 || h.kind == kNoKind ? 0u : h.kind);
+        };
+        if (n_hq >= w->par_calls && w->pool->threads() > 1) {
+            std::vector<size_t> bend;
+            const uint64_t kor = fold_sorted(w, n_hq, hib, 5, hkey, hpk, w->hpk_t, bend);
+            if (bits_for(kor) + hib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued schedule calls"));
+            const int P = (int)bend.size();
+            std::vector<std::vector<uint32_t>> bs(P), bo(P);
+            std::vector<std::vector<Post>> bq(P);
+            w->pool->run(P, [&](int b) { fold_range(b ? bend[b - 1] : 0, bend[b], bs[b], bo[b], bq[b]); });
+            for (int b = 0; b < P; b++) {
+                pre_slot.insert(pre_slot.end(), bs[b].begin(), bs[b].end());
+                pre_op.insert(pre_op.end(), bo[b].begin(), bo[b].end());
+                post.insert(post.end(), bq[b].begin(), bq[b].end());
             }
-            if (erase_all) {
-                pre_slot.push_back(slot);
-                pre_op.push_back(2);
+        } else {
+            hpk.resize(n_hq);
+            uint64_t kor = 0;
+            size_t nh = 0;
+            for (size_t i = 0; i < n_hq; i++) {
+                const uint64_t key = hkey(i);
+                if (key == ~0ull) continue;
+                kor |= key;
+                hpk[nh++] = (key << hib) | i;
             }
-            if (owner_seq != 0xFFFFFFFFu) {
-                pre_slot.push_back(slot);
-                pre_op.push_back(1);
-                if (owner_kind == kNoKind) post.push_back(Post{slot, 0u, 8u, 0.f, 0, 0});  // release the key only
-            }
-            for (size_t c = a; c < b;) {
-                const uint32_t kind = (uint32_t)((hpk[c] >> hib) & 31);
-                size_t e = c;
-                Post p{slot, kind, 0u, 0.f, 0, 0};
-                if (owner_seq != 0xFFFFFFFFu && owner_kind == kind) p.op |= 1u | 4u;
-                for (; e < b && (uint32_t)((hpk[e] >> hib) & 31) == kind; e++) {
-                    const World::HOp& h = w->hops[hpk[e] & him];
-                    if (h.code == 1 && !(p.op & 2u)) {
-                        p.op |= 2u;
-                        p.interval = h.interval;
-                        p.count = h.count;
-                        p.time = h.time;
-                    }
-                }
-                if (p.op) post.push_back(p);
-                c = e;
-            }
-            a = b;
+            hpk.resize(nh);
+            if (bits_for(kor) + hib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued schedule calls"));
+            radix_sort_packed(hpk, w->hpk_t, hib, bits_for(kor));
+            fold_range(0, nh, pre_slot, pre_op, post);
         }
     }
 
@@ -3067,11 +3152,14 @@ int nfk_execute(void* world, int64_t now_ms) {
             memcpy(P + off_xp, g_pid.data(), ng * 4);
             memcpy(P + off_xf, g_first.data(), (ng + 1) * 4);
             uint64_t* xb = (uint64_t*)(P + off_xb);
-            for (size_t i = 0; i < nxc; i++) xb[i] = w->xops[xpk[i] & xim].bits;
-            if (objs) {
-                uint64_t* xh = (uint64_t*)(P + off_xh);
-                for (size_t i = 0; i < nxc; i++) xh[i] = w->xops_h[xpk[i] & xim];
-            }
+            uint64_t* xh = objs ? (uint64_t*)(P + off_xh) : nullptr;
+            const int np = nxc >= w->par_calls ? w->pool->threads() : 1;
+            w->pool->run(np, [&](int c) {
+                const size_t a = nxc * c / np, e = nxc * (c + 1) / np;
+                for (size_t i = a; i < e; i++) xb[i] = w->xops[xpk[i] & xim].bits;
+                if (xh)
+                    for (size_t i = a; i < e; i++) xh[i] = w->xops_h[xpk[i] & xim];
+            });
         }
         for (size_t i = 0; i < npre; i++) {
             ((uint32_t*)(P + off_ps))[i] = pre_slot[i];

@@ -119,6 +119,7 @@ static void resolve_program(std::vector<nfk_op>& ops, const std::vector<std::str
 // definition order
 int NFGPUKernelModule::PropertyId(const std::string& name) const {
     const int pid = prop_id_.at(name);
+    if (committed_) return dev_pid_[(size_t)pid];
     int n[3] = {0, 0, 0}, before = 0;
     const int t = props_[pid].type == TDATA_INT ? 0 : props_[pid].type == TDATA_FLOAT ? 1 : 2;
     for (int i = 0; i < (int)props_.size(); i++) {
@@ -152,7 +153,7 @@ bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGrou
     if (!scenes_.count(nSceneID)) return false;  // "There is no scene" (KM:107)
     if (committed_) {
         // after AfterInit: the entity enters at the start of the next frame (nfk_spawn_objects)
-        if (obj_of_.count(self)) return false;  // "The object has Exists" (KM:131)
+        if (obj_of_.count(self.nHead64, self.nData64)) return false;  // "The object has Exists" (KM:131)
         auto c = class_id_.find(cls);
         if (c == class_id_.end()) return false;
         int n_if = 0;
@@ -171,7 +172,7 @@ bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGrou
         check(nfk_spawn_objects(world_, 1, &self.nHead64, &self.nData64, &nSceneID, &nGroupID, &cl, &pl, row.data()),
               "nfk_spawn_objects");
         pending_calls_++;
-        obj_of_[self] = (int)guids_.size();
+        obj_of_.insert(self.nHead64, self.nData64, (int)guids_.size());
         guids_.push_back(self);
         scene_.push_back(nSceneID);
         group_.push_back(nGroupID);
@@ -179,12 +180,12 @@ bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGrou
         isplayer_.push_back(pl);
         return true;
     }
-    if (obj_of_.count(self)) return false;       // "The object has Exists" (KM:131)
+    if (obj_of_.count(self.nHead64, self.nData64)) return false;       // "The object has Exists" (KM:131)
     auto c = class_id_.find(cls);
     if (c == class_id_.end()) return false;
     int o = (int)guids_.size();
     guids_.push_back(self);
-    obj_of_[self] = o;
+    obj_of_.insert(self.nHead64, self.nData64, o);
     scene_.push_back(nSceneID);
     group_.push_back(nGroupID);
     cls_.push_back((uint8_t)c->second);
@@ -297,7 +298,11 @@ bool NFGPUKernelModule::AfterInit() {
               "nfk_set_scene_props");
     }
     def_of_pid_.assign(props_.size(), 0);
-    for (int p = 0; p < (int)props_.size(); p++) def_of_pid_[PropertyId(props_[p].name)] = p;
+    dev_pid_.assign(props_.size(), 0);
+    for (int p = 0; p < (int)props_.size(); p++) {
+        dev_pid_[p] = PropertyId(props_[p].name);
+        def_of_pid_[dev_pid_[p]] = p;
+    }
     committed_ = true;
     return true;
 }
@@ -309,10 +314,10 @@ bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int 
         const int o = ObjectIndex(self);
         shard_->QueueSwitch(self.nHead64, self.nData64, cls_[o], isplayer_[o], nTargetSceneID, nTargetGroupID, fX, fY,
                             fZ);
-        obj_of_.erase(self);  // this module's no more (its index stays reserved)
+        obj_of_.erase(self.nHead64, self.nData64);  // this module's no more (its index stays reserved)
         DropFunctors(o);
         for (auto it = sched_add_.begin(); it != sched_add_.end();)
-            it = it->first.first == o ? sched_add_.erase(it) : std::next(it);
+            it = (int)(it->first >> 8) == o ? sched_add_.erase(it) : std::next(it);
         return true;
     }
     if (!scenes_.count(nTargetSceneID)) return false;       // "no this container" (KM:917)
@@ -330,10 +335,10 @@ bool NFGPUKernelModule::DestroyObject(const NFGUID& self) {
     if (!committed_ || o < 0) return false;
     check(nfk_destroy_objects(world_, 1, &self.nHead64, &self.nData64), "nfk_destroy_objects");
     pending_calls_++;
-    obj_of_.erase(self);  // its object index stays reserved; later calls find no object
+    obj_of_.erase(self.nHead64, self.nData64);  // its object index stays reserved; later calls find no object
     DropFunctors(o);
     for (auto it = sched_add_.begin(); it != sched_add_.end();)
-        it = it->first.first == o ? sched_add_.erase(it) : std::next(it);
+        it = (int)(it->first >> 8) == o ? sched_add_.erase(it) : std::next(it);
     return true;
 }
 
@@ -350,15 +355,12 @@ bool NFGPUKernelModule::GetRange(const std::string& prop, int k,
     return true;
 }
 
-int NFGPUKernelModule::ObjectIndex(const NFGUID& g) const {
-    auto it = obj_of_.find(g);
-    return it == obj_of_.end() ? -1 : it->second;
-}
+int NFGPUKernelModule::ObjectIndex(const NFGUID& g) const { return obj_of_.find(g.nHead64, g.nData64); }
 
 bool NFGPUKernelModule::SetPropertyInt(const NFGUID& self, const std::string& name, int64_t v) {
     auto it = prop_id_.find(name);
-    if (it == prop_id_.end() || props_[it->second].type != TDATA_INT || ObjectIndex(self) < 0) return false;
-    int32_t pid = PropertyId(name);
+    if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_INT || ObjectIndex(self) < 0) return false;
+    int32_t pid = dev_pid_[(size_t)it->second];
     uint64_t b = (uint64_t)v;
     if (nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) != NFK_OK) return false;
     pending_calls_++;
@@ -489,8 +491,8 @@ double NFGPUKernelModule::GetRecordFloat(const NFGUID& self, const std::string& 
 
 bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& name, double v) {
     auto it = prop_id_.find(name);
-    if (it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT || ObjectIndex(self) < 0) return false;
-    int32_t pid = PropertyId(name);
+    if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT || ObjectIndex(self) < 0) return false;
+    int32_t pid = dev_pid_[(size_t)it->second];
     uint64_t b = bits_of(v);
     if (nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) != NFK_OK) return false;
     pending_calls_++;
@@ -503,7 +505,7 @@ bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& 
 int64_t NFGPUKernelModule::GetPropertyInt(const NFGUID& self, const std::string& name) {
     auto it = prop_id_.find(name);
     if (!committed_ || ObjectIndex(self) < 0 || it == prop_id_.end() || props_[it->second].type != TDATA_INT) return 0;
-    const int32_t pid = PropertyId(name);
+    const int32_t pid = dev_pid_[(size_t)it->second];
     uint64_t b = 0;
     check(nfk_get_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b), "nfk_get_props");
     return (int64_t)b;
@@ -513,7 +515,7 @@ double NFGPUKernelModule::GetPropertyFloat(const NFGUID& self, const std::string
     auto it = prop_id_.find(name);
     if (!committed_ || ObjectIndex(self) < 0 || it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT)
         return 0.0;
-    const int32_t pid = PropertyId(name);
+    const int32_t pid = dev_pid_[(size_t)it->second];
     uint64_t b = 0;
     check(nfk_get_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b), "nfk_get_props");
     return dbl_of(b);
@@ -521,8 +523,8 @@ double NFGPUKernelModule::GetPropertyFloat(const NFGUID& self, const std::string
 
 bool NFGPUKernelModule::SetPropertyObject(const NFGUID& self, const std::string& name, const NFGUID& v) {
     auto it = prop_id_.find(name);
-    if (it == prop_id_.end() || props_[it->second].type != TDATA_OBJECT || ObjectIndex(self) < 0) return false;
-    const int32_t pid = PropertyId(name);
+    if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_OBJECT || ObjectIndex(self) < 0) return false;
+    const int32_t pid = dev_pid_[(size_t)it->second];
     if (nfk_set_objects(world_, 1, &self.nHead64, &self.nData64, &pid, &v.nHead64, &v.nData64) != NFK_OK) return false;
     pending_calls_++;
     return true;
@@ -533,7 +535,7 @@ NFGUID NFGPUKernelModule::GetPropertyObject(const NFGUID& self, const std::strin
     auto it = prop_id_.find(name);
     if (!committed_ || ObjectIndex(self) < 0 || it == prop_id_.end() || props_[it->second].type != TDATA_OBJECT)
         return NFGUID();
-    const int32_t pid = PropertyId(name);
+    const int32_t pid = dev_pid_[(size_t)it->second];
     NFGUID v;
     check(nfk_get_objects(world_, 1, &self.nHead64, &self.nData64, &pid, &v.nHead64, &v.nData64), "nfk_get_objects");
     return v;
@@ -556,6 +558,28 @@ bool NFGPUKernelModule::AddRecordEventCallBack(const RECORD_SINGLE_EVENT_FUNCTOR
     return true;
 }
 
+bool NFGPUKernelModule::AddFrameCallBack(const FRAME_FUNCTOR& cb, uint32_t what) {
+    if (!cb) return false;
+    frame_cb_.push_back(cb);
+    frame_what_ |= what;
+    return true;
+}
+
+// what one device pass reads back for the registered consumers (nfk_read_frame bits)
+uint32_t NFGPUKernelModule::ReadMask(bool per_event_fired) const {
+    const bool cb_events = !common_prop_cb_.empty() || !aoi_prop_cb_.empty() || !common_rec_cb_.empty() ||
+                           !aoi_rec_cb_.empty();
+    const bool cb_fan = !aoi_prop_cb_.empty() || !aoi_rec_cb_.empty();
+    uint32_t what = 0;
+    if (summary_.n_fired && ((per_event_fired && n_cb_) || (frame_what_ & NFK_READ_FIRED))) {
+        what |= NFK_READ_FIRED;
+        if ((per_event_fired && n_cb_) || (frame_what_ & NFK_READ_FIRED_GUID_ORDER)) what |= NFK_READ_FIRED_GUID_ORDER;
+    }
+    if ((cb_events || (frame_what_ & NFK_READ_EVENTS)) && (summary_.n_prop_events || summary_.n_rec_events))
+        what |= NFK_READ_EVENTS | ((cb_fan || (frame_what_ & NFK_READ_FANOUT)) ? NFK_READ_FANOUT : 0u);
+    return what;
+}
+
 // NFCScheduleModule::AddSchedule (SM:257-275): queued, added at the end of the next Execute unless
 // the (object, name) still has a schedule then; the functor of the call that creates it is the one
 // that fires (nfk_read_added tells which)
@@ -568,7 +592,7 @@ bool NFGPUKernelModule::AddSchedule(const NFGUID& self, const std::string& name,
     const int64_t now = clock_();
     check(nfk_add_schedules(world_, 1, &self.nHead64, &self.nData64, &kind, &fTime, &nCount, &now),
           "nfk_add_schedules");
-    sched_add_.emplace(std::make_pair(o, kind), std::make_pair(cb, fTime));  // the window's first call wins
+    sched_add_.emplace(((uint64_t)o << 8) | (uint32_t)kind, std::make_pair(cb, fTime));  // the window's first call wins
     pending_calls_++;
     return true;
 }
@@ -629,7 +653,7 @@ void NFGPUKernelModule::MigrateShard() {
     for (const Ticket& k : recv) {
         const NFGUID g(k.guid_head, k.guid_data);
         const int o = (int)guids_.size();
-        obj_of_[g] = o;
+        obj_of_.insert(g.nHead64, g.nData64, o);
         guids_.push_back(g);
         scene_.push_back(k.scene);
         group_.push_back(k.group);
@@ -653,31 +677,47 @@ bool NFGPUKernelModule::Execute() {
     stats_.device = ms_since(t0);
     auto t1 = std::chrono::steady_clock::now();
     TakeAddedSchedules();  // the AddSchedule calls this frame applied: their functors fire from now on
-    const bool want_events = !common_prop_cb_.empty() || !aoi_prop_cb_.empty() || !common_rec_cb_.empty() ||
-                             !aoi_rec_cb_.empty();
-    const bool want_fan = !aoi_prop_cb_.empty() || !aoi_rec_cb_.empty();
     // the frame's outputs in one read-back (nfk_read_frame): the fired list in the order
     // NFCScheduleModule::Execute walks mObjectScheduleMap — objects in NFGUID order, each object's
     // schedules in name order (SM:52-80), sorted on the device — and the event lists
-    uint32_t what = 0;
-    if (summary_.n_fired && n_cb_) what |= NFK_READ_FIRED | NFK_READ_FIRED_GUID_ORDER;
-    if (want_events && (summary_.n_prop_events || summary_.n_rec_events))
-        what |= NFK_READ_EVENTS | (want_fan ? NFK_READ_FANOUT : 0u);
+    const uint32_t what = ReadMask(true);
     nfk_frame_host fh{};
     if (what) check(nfk_read_frame(world_, what, &fh), "nfk_read_frame");
     stats_.events_read = ms_since(t1);
     t1 = std::chrono::steady_clock::now();
-    // heartbeat functors with the reference's arguments
-    const int nk = (int)heartbeats_.size();
-    for (int64_t i = 0; i < fh.n_fi; i++) {
+    // heartbeat functors with the reference's arguments.  The fired list is in NFGUID order, so
+    // its (object, kind) functor slots, pooled functors and NFGUIDs are scattered host reads: they
+    // are prefetched two stages ahead (slot and NFGUID, then the functor the slot names), so the
+    // loop is bound by the calls, not by one cache miss after another
+    const size_t nk = heartbeats_.size(), nslot = cb_slot_.size();
+    const int64_t nfi = n_cb_ ? fh.n_fi : 0;  // (a frame consumer may read the list without functors)
+    constexpr int64_t kPre = 16;
+    for (int64_t i = 0; i < nfi; i++) {
+        if (i + 2 * kPre < nfi) {
+            const int64_t j = i + 2 * kPre;
+            const size_t at = (size_t)fh.fi_obj[j] * nk + (size_t)fh.fi_kind[j];
+            if (at < nslot) __builtin_prefetch(&cb_slot_[at]);
+            __builtin_prefetch(&guids_[(size_t)fh.fi_obj[j]]);
+        }
+        if (i + kPre < nfi) {
+            const int64_t j = i + kPre;
+            const size_t at = (size_t)fh.fi_obj[j] * nk + (size_t)fh.fi_kind[j];
+            const int32_t c = at < nslot ? cb_slot_[at] : -1;
+            if (c >= 0) {
+                __builtin_prefetch(&cb_pool_[(size_t)c]);
+                __builtin_prefetch(&cb_time_[(size_t)c]);
+            }
+        }
         const int o = fh.fi_obj[i], k = fh.fi_kind[i];
-        const size_t at = (size_t)o * nk + k;
-        const int32_t c = at < cb_slot_.size() ? cb_slot_[at] : -1;
+        const size_t at = (size_t)o * nk + (size_t)k;
+        const int32_t c = at < nslot ? cb_slot_[at] : -1;
         if (c >= 0) cb_pool_[c](guids_[o], heartbeats_[k].name, cb_time_[c], fh.fi_remain[i]);
     }
     stats_.functors = ms_since(t1);
     t1 = std::chrono::steady_clock::now();
     if (what & NFK_READ_EVENTS) DeliverEvents(fh);
+    if (what)
+        for (auto& fc : frame_cb_) fc(fh, guids_.data());
     stats_.deliver = ms_since(t1);
     // what the functors called takes effect in this Execute (SM:65: their Sets land at once;
     // SM:83-119: their Add/RemoveSchedule calls are applied at the end of the walk)
@@ -687,10 +727,13 @@ bool NFGPUKernelModule::Execute() {
         pending_calls_ = 0;
         check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
         TakeAddedSchedules();
-        if (want_events && (summary_.n_prop_events || summary_.n_rec_events)) {
+        // the second pass fires no heartbeats: only its events
+        const uint32_t w2 = ReadMask(false) & ~(NFK_READ_FIRED | NFK_READ_FIRED_GUID_ORDER);
+        if (w2) {
             nfk_frame_host f2{};
-            check(nfk_read_frame(world_, NFK_READ_EVENTS | (want_fan ? NFK_READ_FANOUT : 0u), &f2), "nfk_read_frame");
+            check(nfk_read_frame(world_, w2, &f2), "nfk_read_frame");
             DeliverEvents(f2);
+            for (auto& fc : frame_cb_) fc(f2, guids_.data());
         }
     }
     module_sched_.Execute(clock_);  // module schedules (SM:123-176)
@@ -703,6 +746,15 @@ void NFGPUKernelModule::SetFunctor(int o, int k, const OBJECT_SCHEDULE_FUNCTOR& 
     const size_t nk = heartbeats_.size(), at = (size_t)o * nk + k;
     if (cb_slot_.size() < guids_.size() * nk) cb_slot_.resize(guids_.size() * nk + nk * 1024, -1);
     int32_t c = cb_slot_[at];
+    if (!f) {  // a schedule with no host functor (its device program is all it does)
+        if (c >= 0) {
+            cb_pool_[c] = nullptr;
+            cb_free_.push_back(c);
+            cb_slot_[at] = -1;
+            n_cb_--;
+        }
+        return;
+    }
     if (c < 0) {
         if (!cb_free_.empty()) {
             c = cb_free_.back();
@@ -742,7 +794,7 @@ void NFGPUKernelModule::TakeAddedSchedules() {
     check(nfk_read_added(world_, cap, &n, ah.data(), ad.data(), ak.data()), "nfk_read_added");
     for (int32_t i = 0; i < std::min(n, cap); i++) {
         const int o = ObjectIndex(NFGUID(ah[i], ad[i]));
-        auto it = sched_add_.find({o, ak[i]});
+        auto it = sched_add_.find(((uint64_t)o << 8) | (uint32_t)ak[i]);
         if (it == sched_add_.end()) continue;
         SetFunctor(o, ak[i], it->second.first, it->second.second);
     }
@@ -750,8 +802,12 @@ void NFGPUKernelModule::TakeAddedSchedules() {
 }
 
 void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f) {
+    if (common_prop_cb_.empty() && aoi_prop_cb_.empty() && common_rec_cb_.empty() && aoi_rec_cb_.empty()) return;
     std::vector<NFGUID> rcpt;
+    uint32_t rcpt_at = 0, rcpt_n = 0xFFFFFFFFu;  // the msg_rcpt run rcpt holds
+    constexpr int64_t kPre = 16;  // events are in slot order; their objects' NFGUIDs are scattered
     for (int64_t e = 0; e < f.n_ev; e++) {
+        if (e + kPre < f.n_ev) __builtin_prefetch(&guids_[(size_t)f.ev_obj[e + kPre]]);
         const PropertyDef& pd = props_[def_of_pid_[f.ev_pid[e]]];
         TData a, b;
         a.type = b.type = pd.type;
@@ -768,8 +824,15 @@ void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f) {
         const NFGUID& self = guids_[f.ev_obj[e]];
         for (auto& cb : common_prop_cb_) cb(self, pd.name, a, b);
         if (f.msg_off && !aoi_prop_cb_.empty() && f.msg_off[e + 1] > f.msg_off[e]) {  // AOI.cpp:250: no call for empty lists
-            rcpt.clear();
-            for (uint32_t m = f.msg_off[e]; m < f.msg_off[e + 1]; m++) rcpt.push_back(guids_[f.msg_rcpt[m]]);
+            // consecutive events of a scene group mostly share their recipients: rebuild the list
+            // only when the run differs from the previous event's
+            const uint32_t m0 = f.msg_off[e], m1 = f.msg_off[e + 1];
+            if (m1 - m0 != rcpt_n || memcmp(f.msg_rcpt + m0, f.msg_rcpt + rcpt_at, (size_t)(m1 - m0) * 4) != 0) {
+                rcpt.resize(m1 - m0);
+                for (uint32_t m = m0; m < m1; m++) rcpt[m - m0] = guids_[f.msg_rcpt[m]];
+            }
+            rcpt_at = m0;
+            rcpt_n = m1 - m0;
             for (auto& cb : aoi_prop_cb_) cb(self, pd.name, a, b, rcpt);
         }
     }
@@ -796,6 +859,7 @@ void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f) {
         const NFGUID& self = guids_[f.re_obj[e]];
         for (auto& cb : common_rec_cb_) cb(self, ev, a, b);
         if (f.msg_off && !aoi_rec_cb_.empty()) {
+            rcpt_n = 0xFFFFFFFFu;
             rcpt.clear();
             for (uint32_t m = f.msg_off[f.n_ev + e]; m < f.msg_off[f.n_ev + e + 1]; m++) rcpt.push_back(guids_[f.msg_rcpt[m]]);
             for (auto& cb : aoi_rec_cb_) cb(self, ev.strRecordName, ev, a, b, rcpt);

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -32,16 +33,22 @@ struct Stub {
 FILE* g_log = nullptr;
 const char* g_err = "";
 
+// one whole line per call under a lock: the shard tests call the stub from one thread per rank
+std::mutex g_log_mu;
 void logf(const char* fmt, ...) {
+    char line[512];
+    va_list ap;
+    va_start(ap, fmt);
+    int n = vsnprintf(line, sizeof(line) - 1, fmt, ap);
+    va_end(ap);
+    n = n < 0 ? 0 : (n > (int)sizeof(line) - 2 ? (int)sizeof(line) - 2 : n);
+    line[n++] = '\n';
+    std::lock_guard<std::mutex> lk(g_log_mu);
     if (!g_log) {
         const char* p = getenv("NFGPU_STUB_LOG");
         g_log = fopen(p ? p : "/dev/null", "w");
     }
-    va_list ap;
-    va_start(ap, fmt);
-    vfprintf(g_log, fmt, ap);
-    va_end(ap);
-    fputc('\n', g_log);
+    fwrite(line, 1, (size_t)n, g_log);
     fflush(g_log);
 }
 Stub* S(void* w) { return (Stub*)w; }

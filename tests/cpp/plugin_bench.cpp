@@ -5,8 +5,14 @@
 // callback are registered (they count what they receive), and frames run back to back.  Prints one
 // JSON line: host ms per frame (median of the timed frames) and its phases (FrameStats).
 //
-// usage: plugin_bench <workload.nfio> <warmup> <frames> [calls]
+// usage: plugin_bench <workload.nfio> <warmup> <frames> [calls] [consumer]
 //   calls = 1: the workload's SetProperty / schedule calls are made between frames (game logic)
+//   consumer = 0: the reference's per-call API (a functor per schedule, common property / record and
+//                 AOI recipient callbacks per event)
+//              1: one frame batch callback (AddFrameCallBack: fired list + events + recipient CSR as
+//                 arrays), schedules without host functors
+//              2: no host consumer (schedules without functors, no callbacks: the frame's outputs stay
+//                 on the device for a device-side consumer)
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -28,6 +34,7 @@ int main(int argc, char** argv) {
     if (nfio_read(argv[1], &wf)) return 2;
     const int W = atoi(argv[2]), K = atoi(argv[3]);
     const bool calls = argc > 4 && atoi(argv[4]) != 0;
+    const int consumer = argc > 5 ? atoi(argv[5]) : 0;
     auto A = [&](const char* n) {
         nfio_arr* a = nfio_get(&wf, n);
         if (!a) {
@@ -91,6 +98,16 @@ int main(int argc, char** argv) {
     km.AfterInit();
     // the game logic's callbacks: they count what they receive
     int64_t n_prop = 0, n_rec = 0, n_rcpt = 0, n_hb = 0;
+    if (consumer == 1)
+        km.AddFrameCallBack(
+            [&](const nfk_frame_host& f, const NFGUID*) {
+                n_hb += f.n_fi;
+                n_prop += f.n_ev;
+                n_rec += f.n_re;
+                n_rcpt += f.n_msgs;
+            },
+            NFK_READ_FIRED | NFK_READ_FIRED_GUID_ORDER | NFK_READ_EVENTS | NFK_READ_FANOUT);
+    if (consumer == 0) {
     km.RegisterCommonPropertyEvent([&](const NFGUID&, const std::string&, const TData&, const TData&) {
         n_prop++;
         return 0;
@@ -104,10 +121,13 @@ int main(int argc, char** argv) {
         n_rcpt += (int64_t)to.size();
         return 0;
     });
-    auto hb = [&](const NFGUID&, const std::string&, const float, const int) {
-        n_hb++;
-        return 0;
-    };
+    }
+    OBJECT_SCHEDULE_FUNCTOR hb;
+    if (consumer == 0)
+        hb = [&](const NFGUID&, const std::string&, const float, const int) {
+            n_hb++;
+            return 0;
+        };
     int32_t* s_obj = (int32_t*)A("s_obj")->data;
     int32_t* s_kind = (int32_t*)A("s_kind")->data;
     float* s_int = (float*)A("s_interval")->data;
@@ -187,13 +207,14 @@ int main(int argc, char** argv) {
            "\"deliver\": %.3f, \"functor_calls\": %.3f, \"execute\": %.3f}, "
            "\"per_frame\": {\"fired\": %lld, \"prop_events\": %lld, \"rec_events\": %lld, \"messages\": %lld}, "
            "\"received\": {\"heartbeats\": %lld, \"prop_events\": %lld, \"recipients\": %lld}, \"build_s\": %.1f, "
-           "\"frames\": %d, \"warmup\": %d}\n",
+           "\"frames\": %d, \"warmup\": %d, \"consumer\": \"%s\"}\n",
            med(frame_ms), (long long)N, (double)N / (med(frame_ms) * 1e-3), (long long)(K ? ncalls / K : 0),
            med(call_ms), medf(&NFGPUKernelModule::FrameStats::device), medf(&NFGPUKernelModule::FrameStats::functors),
            medf(&NFGPUKernelModule::FrameStats::events_read), medf(&NFGPUKernelModule::FrameStats::deliver),
            medf(&NFGPUKernelModule::FrameStats::calls), medf(&NFGPUKernelModule::FrameStats::total),
            (long long)s.n_fired, (long long)s.n_prop_events, (long long)s.n_rec_events, (long long)s.n_msgs,
-           (long long)n_hb, (long long)n_prop, (long long)n_rcpt, build_s, K, W);
+           (long long)n_hb, (long long)n_prop, (long long)n_rcpt, build_s, K, W,
+           consumer == 0 ? "per-call" : consumer == 1 ? "frame-batch" : "none");
     fflush(stdout);
     km.Shut();
     return 0;

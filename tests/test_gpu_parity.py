@@ -106,6 +106,18 @@ def test_gpu_matches_oracle(gpu_available, monkeypatch, case, path):
     compare_runs(run_gpu(w), run_oracle(w))
 
 
+@pytest.mark.parametrize("case", ["combined", "wide_sets", "lifecycle", "sched_edges", "record_rows"])
+def test_parallel_call_folding_matches_oracle(gpu_available, monkeypatch, case):
+    """The host pool's folding of a window's calls (GUID lookups split over threads, (slot, property)
+    and (slot, kind) folds by slot range, nfgpu_host.hip fold_sorted) — used from 16384 calls per
+    batch on — forced on every batch here (NFGPU_PAR_CALLS=8), 4 and 7 host threads."""
+    for threads in ("4", "7"):
+        monkeypatch.setenv("NFGPU_PAR_CALLS", "8")
+        monkeypatch.setenv("NFGPU_HOST_THREADS", threads)
+        w = workload.make_world(n_ticks=10, seed=sum(map(ord, case)), **CASES[case])
+        compare_runs(run_gpu(w), run_oracle(w))
+
+
 @PATHS
 def test_every_property_set_on_one_entity(gpu_available, monkeypatch, path):
     """One entity gets every property set in one frame, several of them twice, while its heartbeats
