@@ -225,6 +225,11 @@ int nfk_spawn_objects(void* world, int32_t n, const int64_t* guid_head, const in
  * reference's change predicates.  bits = int64 or f64 bit pattern. */
 int nfk_set_props(void* world, int32_t n, const int64_t* guid_head, const int64_t* guid_data,
                   const int32_t* pid, const uint64_t* bits);
+/* the same with the objects as nfk's object indices (creation order in this world: the ev_obj /
+ * fi_obj of the outputs) for a caller that already resolved the NFGUID (the C++ plugin checks the
+ * object exists, KM:325, before it queues): no lookup here; NFK_ERR_NOTFOUND for an index that is
+ * not a live object */
+int nfk_set_props_obj(void* world, int32_t n, const int32_t* obj, const int32_t* pid, const uint64_t* bits);
 
 /* ---- object properties: NFIKernelModule::SetPropertyObject (KM:362) -> NFCProperty::SetObject
  * (PR:377-416): queued in call order with the other Sets, applied at the start of the next
@@ -299,6 +304,9 @@ int nfk_remove_all_schedules(void* world, int64_t guid_head, int64_t guid_data);
  * checked before any call is queued */
 int nfk_schedule_calls(void* world, int32_t n, const int32_t* op, const int64_t* guid_head, const int64_t* guid_data,
                        const int32_t* kind, const float* interval_s, const int32_t* count, const int64_t* now_ms);
+/* the same by object index (see nfk_set_props_obj) */
+int nfk_schedule_calls_obj(void* world, int32_t n, const int32_t* op, const int32_t* obj, const int32_t* kind,
+                           const float* interval_s, const int32_t* count, const int64_t* now_ms);
 /* NFIScheduleModule::ExistSchedule(self, name) (SM:276-285): the object's schedule map as the
  * reference holds it between frames — schedules present after the last frame, minus a
  * RemoveSchedule(self) queued in this window (it erases at once, SM:240); AddSchedule and

@@ -42,9 +42,11 @@ public:
         for (; t_[i].v >= 0; i = (i + 1) & (cap_ - 1))
             if (t_[i].h == h && t_[i].d == d) {
                 t_[i].v = v;
+                logged(i);
                 return;
             }
         t_[i] = E{h, d, v};
+        logged(i);
         n_++;
     }
     void erase(int64_t h, int64_t d) {
@@ -60,24 +62,43 @@ public:
             const size_t home = slot(t_[j].h, t_[j].d);
             if (((j - home) & (cap_ - 1)) >= ((j - i) & (cap_ - 1))) {
                 t_[i] = t_[j];
+                logged(i);
                 i = j;
             }
         }
         t_[i].v = -1;
+        logged(i);
         n_--;
     }
 
-private:
+    // A mirror of the table elsewhere (the world's device copy, nfgpu_host.hip find_many_dev)
+    // follows it through a log of the entries every insert / erase wrote, and a rewrite flag set
+    // when the table was rebuilt at a new capacity.
     struct E {
         int64_t h, d;
         int32_t v = -1;
     };
-    size_t slot(int64_t h, int64_t d) const {
+    void set_log(std::vector<uint32_t>* log) { log_ = log; }
+    bool take_rebuilt() {
+        const bool r = rebuilt_;
+        rebuilt_ = false;
+        return r;
+    }
+    const E* entries() const { return t_.data(); }
+    size_t capacity() const { return cap_; }
+    // the home entry of a GUID (the device mirror's lookups hash the same way)
+    static size_t home(int64_t h, int64_t d, size_t mask) {
         uint64_t x = (uint64_t)h * 0x9E3779B97F4A7C15ull ^ (uint64_t)d;
         x ^= x >> 31;
         x *= 0xBF58476D1CE4E5B9ull;
         x ^= x >> 29;
-        return (size_t)x & (cap_ - 1);
+        return (size_t)x & mask;
+    }
+
+private:
+    size_t slot(int64_t h, int64_t d) const { return home(h, d, cap_ - 1); }
+    void logged(size_t i) {
+        if (log_ && !rebuilt_) log_->push_back((uint32_t)i);
     }
     void rehash(size_t c) {
         std::vector<E> old;
@@ -85,11 +106,15 @@ private:
         t_.assign(c, E{});
         cap_ = c;
         n_ = 0;
+        rebuilt_ = true;  // (the mirror is rewritten whole; the log restarts)
+        if (log_) log_->clear();
         for (const E& e : old)
             if (e.v >= 0) insert(e.h, e.d, e.v);
     }
     std::vector<E> t_;
     size_t cap_ = 0, n_ = 0;
+    std::vector<uint32_t>* log_ = nullptr;
+    bool rebuilt_ = false;
 };
 
 }  // namespace nfgpu_detail

@@ -166,9 +166,34 @@ struct World {
     struct XOp { uint32_t slot, pid; uint64_t bits; };
     std::vector<XOp> xops;
     std::vector<uint64_t> xops_h;  // the NFGUID head half of each queued call (worlds with object properties)
-    // per-frame SetProperty groups (host scratch kept across frames) and their device results
-    std::vector<uint32_t> g_slot, g_pid, g_first;
+    // the SetProperty groups are folded on the device (k_xkeys, radix sort, k_scan_heads,
+    // k_xgroups): object -> slot after the window's membership changes (rebuilt by k_obj_slots
+    // when the membership changed), and the fold's scratch
+    int32_t* obj_slot_d = nullptr;
+    size_t obj_slot_cap = 0;
+    bool obj_slot_dirty = true;
+    void* xf_buf = nullptr;
+    size_t xf_cap = 0;
     std::vector<int32_t> look;           // GUID lookups of one batched call
+    // GUID lookups of large call batches on the device (find_many_dev): obj_of's device mirror
+    // (guid_d, same entries and hash), the log of the entries the host table wrote since the
+    // mirror was last brought up to date, the batch's pinned and device buffers, and a stream of
+    // their own (the world's stream may be running the previous frame)
+    std::vector<uint32_t> guid_log;
+    void* guid_d = nullptr;
+    size_t guid_dcap = 0;       // bytes
+    size_t guid_dmask = 0;      // capacity - 1 of the mirrored table
+    bool guid_synced = false;
+    hipStream_t look_stream = nullptr;
+    char* look_pin = nullptr;
+    size_t look_pin_cap = 0;
+    void* look_dev = nullptr;
+    size_t look_dev_cap = 0;
+    size_t dev_look_min = 4096;  // batches from this size on (NFGPU_DEV_LOOKUP; 0 = never)
+    // the window's SetProperty calls of properties no program writes, and those properties: they
+    // bound a tile's standalone events (nfk_execute)
+    int64_t sa_calls = 0;
+    uint64_t sa_pids[2] = {0, 0};
     // GetProperty* (nfk_get_props): device values read since the last frame, and the queued
     // SetProperty chain of each (object, property): ov_last[key] = its last xop, ov_prev links back
     std::unordered_map<uint64_t, uint64_t> dcache;
@@ -181,8 +206,8 @@ struct World {
     std::vector<uint32_t> post_kind;
     uint8_t* added_d = nullptr;
     size_t added_cap = 0;
-    std::vector<uint64_t> xpk, xpk_t, hpk, hpk_t;  // packed (key << 32 | call index) sort scratch
-    // host worker threads for large call batches (NFGPU_HOST_THREADS, default 4 in all; 1 = none)
+    std::vector<uint64_t> hpk, hpk_t;  // packed (key << 32 | call index) sort scratch
+    // host worker threads for large call batches (NFGPU_HOST_THREADS, default 1 = none)
     std::unique_ptr<HostPool> pool;
     size_t par_calls = 16384;  // batches from this size on use the pool (NFGPU_PAR_CALLS: tests)
     // queued SetRecordInt / SetRecordFloat calls (obj: object index until nfk_execute resolves it;
@@ -247,6 +272,15 @@ struct World {
 };
 
 constexpr uint32_t kNoKind = 0xFFFFFFFFu;  // HOp::kind of a RemoveSchedule(self, name) with no device program
+// a queued SetProperty of a property no program writes: a standalone event (see nfk_execute)
+inline void count_standalone(World* w, uint32_t pid) {
+    if (w->tab.w_slot[pid] == kNoU) {
+        w->sa_calls++;
+        w->sa_pids[pid >> 6] |= 1ull << (pid & 63);
+    }
+}
+static_assert(sizeof(World::XOp) == sizeof(XCall) && offsetof(World::XOp, bits) == offsetof(XCall, bits),
+              "k_xkeys reads the queued SetProperty calls as uploaded");
 
 // word of property pid (its data half for an object property) in an entity row
 inline int64_t prop_word(const World* w, int32_t pid) {
@@ -260,6 +294,8 @@ inline int64_t prop_word(const World* w, int32_t pid) {
 int drop_window(World* w, int r) {
     w->xops.clear();
     w->xops_h.clear();
+    w->sa_calls = 0;
+    w->sa_pids[0] = w->sa_pids[1] = 0;
     w->hops.clear();
     w->rsq.clear();
     w->rvals.clear();
@@ -565,17 +601,100 @@ void radix_sort_range(uint64_t* a, uint64_t* t, size_t n, int shift, int key_bit
     if (in_t) memcpy(t, a, n * 8);  // (a and t swapped: copy back into the caller's a)
 }
 
-// GuidMap::find_many split over the host pool for a large batch
-void find_many_par(World* w, int32_t n, const int64_t* gh, const int64_t* gd, int32_t* out) {
+// n lookups of a large batch on the device mirror of obj_of: the mirror is brought up to date
+// first (the entries the host table wrote since, or the whole table after it was rebuilt), then
+// one H2D copy of the GUIDs, k_guid_find, one D2H copy of the object indices
+int find_many_dev(World* w, int32_t n, const int64_t* gh, const int64_t* gd, int32_t* out) {
+    const size_t cap = w->obj_of.capacity();
+    if (cap == 0 || n <= 0) {
+        for (int32_t i = 0; i < n; i++) out[i] = -1;
+        return NFK_OK;
+    }
+    if (!w->look_stream) HIPCHK(hipStreamCreateWithFlags(&w->look_stream, hipStreamNonBlocking));
+    using E = GuidMap::E;
+    static_assert(sizeof(E) == sizeof(GuidEntry) && offsetof(E, v) == offsetof(GuidEntry, v), "mirror layout");
+    const size_t tbytes = cap * sizeof(E);
+    bool full = w->obj_of.take_rebuilt() || !w->guid_synced || w->guid_dmask != cap - 1;
+    size_t np = full ? 0 : w->guid_log.size();
+    if (np > cap / 8) {  // (many writes since: the whole table is the smaller upload)
+        full = true;
+        np = 0;
+    }
+    const size_t o_q = 0, o_r = align16((size_t)n * 16), o_pi = align16(o_r + (size_t)n * 4),
+                 o_pe = align16(o_pi + np * 4), tot = align16(o_pe + np * sizeof(E));
+    if (tot > w->look_pin_cap) {
+        if (w->look_pin) HIPCHK(hipHostFree(w->look_pin));
+        w->look_pin = nullptr;
+        w->look_pin_cap = 0;
+        HIPCHK(hipHostMalloc((void**)&w->look_pin, tot + tot / 2, hipHostMallocDefault));
+        w->look_pin_cap = tot + tot / 2;
+    }
+    if (tot > w->look_dev_cap) {
+        if (w->look_dev) HIPCHK(hipFree(w->look_dev));
+        w->look_dev = nullptr;
+        w->look_dev_cap = 0;
+        HIPCHK(hipMalloc(&w->look_dev, tot + tot / 2));
+        w->look_dev_cap = tot + tot / 2;
+    }
+    char* P = w->look_pin;
+    char* D = (char*)w->look_dev;
+    if (full) {
+        if (tbytes > w->guid_dcap) {
+            if (w->guid_d) HIPCHK(hipFree(w->guid_d));
+            w->guid_d = nullptr;
+            w->guid_dcap = 0;
+            HIPCHK(hipMalloc(&w->guid_d, tbytes));
+            w->guid_dcap = tbytes;
+        }
+        HIPCHK(hipMemcpyAsync(w->guid_d, w->obj_of.entries(), tbytes, hipMemcpyHostToDevice, w->look_stream));
+        w->guid_dmask = cap - 1;
+        w->guid_synced = true;
+    } else if (np) {
+        const E* t = w->obj_of.entries();
+        uint32_t* pi = (uint32_t*)(P + o_pi);
+        E* pe = (E*)(P + o_pe);
+        for (size_t i = 0; i < np; i++) {  // (an entry logged twice is written twice with its final value)
+            pi[i] = w->guid_log[i];
+            pe[i] = t[w->guid_log[i]];
+        }
+    }
+    w->guid_log.clear();
+    memcpy(P + o_q, gh, (size_t)n * 8);
+    memcpy(P + o_q + (size_t)n * 8, gd, (size_t)n * 8);
+    HIPCHK(hipMemcpyAsync(D, P, o_r, hipMemcpyHostToDevice, w->look_stream));
+    if (np) {
+        HIPCHK(hipMemcpyAsync(D + o_pi, P + o_pi, tot - o_pi, hipMemcpyHostToDevice, w->look_stream));
+        hipLaunchKernelGGL(k_guid_patch, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, w->look_stream,
+                           (GuidEntry*)w->guid_d, (const uint32_t*)(D + o_pi), (const GuidEntry*)(D + o_pe), (int32_t)np);
+    }
+    hipLaunchKernelGGL(k_guid_find, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, w->look_stream,
+                       (const GuidEntry*)w->guid_d, (uint64_t)(cap - 1), (const int64_t*)(D + o_q), n,
+                       (int32_t*)(D + o_r));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(P + o_r, D + o_r, (size_t)n * 4, hipMemcpyDeviceToHost, w->look_stream));
+    HIPCHK(hipStreamSynchronize(w->look_stream));
+    memcpy(out, P + o_r, (size_t)n * 4);
+    return NFK_OK;
+}
+
+// A batch's lookups: on the device from dev_look_min calls on, else GuidMap::find_many (split
+// over the host pool for a large batch when the pool has workers)
+int find_many_par(World* w, int32_t n, const int64_t* gh, const int64_t* gd, int32_t* out) {
+    if (w->dev_look_min && (size_t)n >= w->dev_look_min) return find_many_dev(w, n, gh, gd, out);
+    if (w->guid_log.size() > w->obj_of.capacity() / 8) {  // (the mirror is rewritten at its next use)
+        w->guid_log.clear();
+        w->guid_synced = false;
+    }
     if ((size_t)n < w->par_calls || w->pool->threads() < 2) {
         w->obj_of.find_many(n, gh, gd, out);
-        return;
+        return NFK_OK;
     }
     const int P = w->pool->threads();
     w->pool->run(P, [&](int c) {
         const int32_t a = (int32_t)((int64_t)n * c / P), b = (int32_t)((int64_t)n * (c + 1) / P);
         w->obj_of.find_many(b - a, gh + a, gd + a, out + a);
     });
+    return NFK_OK;
 }
 
 // A window's calls folded into a packed array (key << ib | call index) sorted by key, call order
@@ -1190,6 +1309,7 @@ int plan_membership(World* w, MemPlan& p) {
 int commit_membership(World* w, MemPlan& p) {
     if (!p.active) return NFK_OK;
     p.active = false;
+    w->obj_slot_dirty = true;  // (k_obj_slots before the next device fold)
     using clk = std::chrono::steady_clock;
     const auto t_dev = clk::now();
     Dev& d = w->d;
@@ -1410,10 +1530,16 @@ int nfk_create(const nfk_config* cfg, void** out) {
     if (e != hipSuccess || ndev == 0) return fail(NFK_ERR_HIP, "no HIP device available");
     World* w = new World();
     {
-        int nt = 4;  // host threads for large call batches (the caller and nt - 1 workers)
+        // host threads for large call batches (the caller and nt - 1 workers).  Default 1: on the
+        // GPU boxes the workers made the host work slower, not faster (schedule-call fold 0.85 vs
+        // 0.31 ms, the SetProperty fold 3-6 vs 0.67 ms before it moved to the device;
+        // profiles/r08b_hostprof*.log)
+        int nt = 1;
         if (const char* e = getenv("NFGPU_HOST_THREADS")) nt = std::max(1, std::min(64, atoi(e)));
         w->pool.reset(new HostPool(nt - 1));
         if (const char* e = getenv("NFGPU_PAR_CALLS")) w->par_calls = (size_t)std::max(1, atoi(e));
+        if (const char* e = getenv("NFGPU_DEV_LOOKUP")) w->dev_look_min = (size_t)std::max(0, atoi(e));
+        w->obj_of.set_log(&w->guid_log);
     }
     w->cfg = *cfg;
     w->n_if = cfg->n_int + cfg->n_flt;
@@ -1465,6 +1591,16 @@ int nfk_destroy(void* world) {
     if (w->mlist) (void)hipFree(w->mlist);
     if (w->glist) (void)hipFree(w->glist);
     if (w->xs_buf) (void)hipFree(w->xs_buf);
+    if (w->xf_buf) (void)hipFree(w->xf_buf);
+    if (w->obj_slot_d) (void)hipFree(w->obj_slot_d);
+    if (w->rs_buf) (void)hipFree(w->rs_buf);
+    if (w->rss_buf) (void)hipFree(w->rss_buf);
+    if (w->rl_buf) (void)hipFree(w->rl_buf);
+    if (w->look_stream) (void)hipStreamSynchronize(w->look_stream);
+    if (w->guid_d) (void)hipFree(w->guid_d);
+    if (w->look_dev) (void)hipFree(w->look_dev);
+    if (w->look_pin) (void)hipHostFree(w->look_pin);
+    if (w->look_stream) (void)hipStreamDestroy(w->look_stream);
     if (w->gat) (void)hipFree(w->gat);
     if (w->added_d) (void)hipFree(w->added_d);
     for (auto& p : w->pend) {
@@ -1966,30 +2102,55 @@ int nfk_commit(void* world) {
     return NFK_OK;
 }
 
+// the SetProperty* calls of a batch, their objects resolved (obj[i] < 0: no such object; gh / gd
+// name it in the error when given): every call is checked before any is queued
+static int queue_sets(World* w, int32_t n, const int32_t* obj, const int32_t* pid, const uint64_t* bits,
+                      const int64_t* gh, const int64_t* gd) {
+    for (int32_t i = 0; i < n; i++) {
+        if (obj[i] < 0)  // NFCKernelModule logs "There is no object" and returns false (KM:331)
+            return fail(NFK_ERR_NOTFOUND, gh ? "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i])
+                                             : "no object index " + std::to_string(obj[i]));
+        if (pid[i] < 0 || pid[i] >= w->n_if)
+            return fail(NFK_ERR_ARG, pid[i] >= w->n_if && pid[i] < w->n_prop ? "object property: use nfk_set_objects"
+                                                                              : "bad property id");
+    }
+    const size_t at = w->xops.size();
+    w->xops.resize(at + (size_t)n);
+    World::XOp* x = w->xops.data() + at;
+    for (int32_t i = 0; i < n; i++) {
+        x[i] = World::XOp{(uint32_t)obj[i], (uint32_t)pid[i], bits[i]};
+        count_standalone(w, (uint32_t)pid[i]);
+    }
+    if (w->cfg.n_obj) w->xops_h.resize(w->xops.size(), 0);
+    return NFK_OK;
+}
+
+// object indices as the caller holds them (nfk's creation order, the outputs' ev_obj / fi_obj):
+// -1 for one that is not a live object of this world
+static const int32_t* live_objects(World* w, int32_t n, const int32_t* obj) {
+    w->look.resize(n);
+    for (int32_t i = 0; i < n; i++) {
+        const int32_t o = obj[i];
+        w->look[i] = (o >= 0 && o < w->n_obj && w->alive[o]) ? o : -1;
+    }
+    return w->look.data();
+}
+
 int nfk_set_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid,
                   const uint64_t* bits) {
     World* w = (World*)world;
     if (!w || n < 0 || (n && (!gh || !gd || !pid || !bits))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
-    // every call is checked before any is queued; one GUID lookup per call
-    const size_t at = w->xops.size();
-    w->xops.resize(at + (size_t)n);
-    World::XOp* x = w->xops.data() + at;
-    w->look.resize(n);
-    find_many_par(w, n, gh, gd, w->look.data());
-    for (int32_t i = 0; i < n; i++) {
-        const int32_t obj = w->look[i];
-        if (obj < 0 || pid[i] < 0 || pid[i] >= w->n_if) {
-            w->xops.resize(at);
-            if (obj < 0)  // NFCKernelModule logs "There is no object" and returns false (KM:331)
-                return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
-            return fail(NFK_ERR_ARG, pid[i] >= w->n_if && pid[i] < w->n_prop ? "object property: use nfk_set_objects"
-                                                                              : "bad property id");
-        }
-        x[i] = World::XOp{(uint32_t)obj, (uint32_t)pid[i], bits[i]};
-    }
-    if (w->cfg.n_obj) w->xops_h.resize(w->xops.size(), 0);
-    return NFK_OK;
+    w->look.resize(n);  // one GUID lookup per call
+    if (int rl = find_many_par(w, n, gh, gd, w->look.data())) return rl;
+    return queue_sets(w, n, w->look.data(), pid, bits, gh, gd);
+}
+
+int nfk_set_props_obj(void* world, int32_t n, const int32_t* obj, const int32_t* pid, const uint64_t* bits) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!obj || !pid || !bits))) return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    return queue_sets(w, n, live_objects(w, n, obj), pid, bits, nullptr, nullptr);
 }
 
 int nfk_set_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid,
@@ -1998,7 +2159,7 @@ int nfk_set_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     if (!w || n < 0 || (n && (!gh || !gd || !pid || !vh || !vd))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     w->look.resize(n);
-    find_many_par(w, n, gh, gd, w->look.data());
+    if (int rl = find_many_par(w, n, gh, gd, w->look.data())) return rl;
     for (int32_t i = 0; i < n; i++) {
         if (w->look[i] < 0)  // "There is no object" (KM:370)
             return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
@@ -2009,6 +2170,7 @@ int nfk_set_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     for (int32_t i = 0; i < n; i++) {
         w->xops.push_back(World::XOp{(uint32_t)w->look[i], (uint32_t)pid[i], (uint64_t)vd[i]});
         w->xops_h.push_back((uint64_t)vh[i]);
+        count_standalone(w, (uint32_t)pid[i]);
     }
     return NFK_OK;
 }
@@ -2020,7 +2182,7 @@ int nfk_set_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     // every call is checked before any is queued; one GUID lookup per call
     w->look.resize(n);
-    find_many_par(w, n, gh, gd, w->look.data());
+    if (int rl = find_many_par(w, n, gh, gd, w->look.data())) return rl;
     for (int32_t i = 0; i < n; i++) {
         if (w->look[i] < 0)  // NFCKernelModule logs "There is no object" and returns false (KM:505)
             return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
@@ -2046,7 +2208,7 @@ int nfk_record_rows(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     if (!w || n < 0 || (n && (!gh || !gd || !rec || !op || !row))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     w->look.resize(n);
-    find_many_par(w, n, gh, gd, w->look.data());
+    if (int rl = find_many_par(w, n, gh, gd, w->look.data())) return rl;
     for (int32_t i = 0; i < n; i++) {
         if (w->look[i] < 0)  // FindRecord: "There is no object" (KM:487)
             return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
@@ -2138,7 +2300,7 @@ int nfk_get_used_rows(void* world, int32_t n, const int64_t* gh, const int64_t* 
     if (!w || n < 0 || (n && (!gh || !gd || !rec || !masks))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     std::vector<int32_t> obj(n);
-    find_many_par(w, n, gh, gd, obj.data());
+    if (int rl = find_many_par(w, n, gh, gd, obj.data())) return rl;
     std::vector<uint64_t> addr;
     std::vector<int32_t> miss;
     for (int32_t i = 0; i < n; i++) {
@@ -2172,7 +2334,7 @@ int nfk_get_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     if (!w || n < 0 || (n && (!gh || !gd || !rec || !row || !col || !bits))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     std::vector<int32_t> obj(n);
-    find_many_par(w, n, gh, gd, obj.data());
+    if (int rl = find_many_par(w, n, gh, gd, obj.data())) return rl;
     for (int32_t i = 0; i < n; i++) {
         if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
         const int32_t r = rec[i];
@@ -2291,17 +2453,14 @@ int nfk_remove_all_schedules(void* world, int64_t gh, int64_t gd) {
     return NFK_OK;
 }
 
-int nfk_schedule_calls(void* world, int32_t n, const int32_t* op, const int64_t* gh, const int64_t* gd,
-                       const int32_t* kind, const float* interval, const int32_t* count, const int64_t* now_ms) {
-    World* w = (World*)world;
-    if (!w || n < 0 || (n && (!op || !gh || !gd || !kind || !interval || !count || !now_ms)))
-        return fail(NFK_ERR_ARG, "null argument");
-    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
-    std::vector<int32_t>& obj = w->look;
-    obj.resize(n);
-    find_many_par(w, n, gh, gd, obj.data());
+// a batch of schedule calls, their objects resolved (see queue_sets)
+static int queue_schedule_calls(World* w, int32_t n, const int32_t* op, const int32_t* obj, const int32_t* kind,
+                                const float* interval, const int32_t* count, const int64_t* now_ms, const int64_t* gh,
+                                const int64_t* gd) {
     for (int32_t i = 0; i < n; i++) {
-        if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
+        if (obj[i] < 0)
+            return fail(NFK_ERR_NOTFOUND, gh ? "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i])
+                                             : "no object index " + std::to_string(obj[i]));
         if (op[i] < 1 || op[i] > 3) return fail(NFK_ERR_ARG, "schedule call op must be 1, 2 or 3");
         if (op[i] == 1 && (kind[i] < 0 || kind[i] >= w->cfg.n_kind || !w->kind_defined[kind[i]]))
             return fail(NFK_ERR_ARG, "undefined heartbeat kind");
@@ -2312,6 +2471,26 @@ int nfk_schedule_calls(void* world, int32_t n, const int32_t* op, const int64_t*
                            op[i] == 3 ? 0u : (kind[i] < 0 ? kNoKind : (uint32_t)kind[i]), op[i] == 1 ? interval[i] : 0.f,
                            op[i] == 1 ? count[i] : 0, op[i] == 1 ? now_ms[i] : 0});
     return NFK_OK;
+}
+
+int nfk_schedule_calls(void* world, int32_t n, const int32_t* op, const int64_t* gh, const int64_t* gd,
+                       const int32_t* kind, const float* interval, const int32_t* count, const int64_t* now_ms) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!op || !gh || !gd || !kind || !interval || !count || !now_ms)))
+        return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    w->look.resize(n);
+    if (int rl = find_many_par(w, n, gh, gd, w->look.data())) return rl;
+    return queue_schedule_calls(w, n, op, w->look.data(), kind, interval, count, now_ms, gh, gd);
+}
+
+int nfk_schedule_calls_obj(void* world, int32_t n, const int32_t* op, const int32_t* obj, const int32_t* kind,
+                           const float* interval, const int32_t* count, const int64_t* now_ms) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && (!op || !obj || !kind || !interval || !count || !now_ms)))
+        return fail(NFK_ERR_ARG, "null argument");
+    if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    return queue_schedule_calls(w, n, op, live_objects(w, n, obj), kind, interval, count, now_ms, nullptr, nullptr);
 }
 
 // The world's values of property words after the last frame (waits for the world's stream): src
@@ -2367,7 +2546,7 @@ int nfk_get_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     if (!w || n < 0 || (n && (!gh || !gd || !pid || !vh || !vd))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     std::vector<int32_t> obj(n);
-    find_many_par(w, n, gh, gd, obj.data());
+    if (int rl = find_many_par(w, n, gh, gd, obj.data())) return rl;
     std::vector<uint64_t> src(2 * (size_t)n), got(2 * (size_t)n);
     for (int32_t i = 0; i < n; i++) {
         if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
@@ -2397,7 +2576,7 @@ int nfk_get_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
     if (!w || n < 0 || (n && (!gh || !gd || !pid || !bits))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     std::vector<int32_t> obj(n);
-    find_many_par(w, n, gh, gd, obj.data());
+    if (int rl = find_many_par(w, n, gh, gd, obj.data())) return rl;
     for (int32_t i = 0; i < n; i++) {
         if (obj[i] < 0) return fail(NFK_ERR_NOTFOUND, "There is no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i]));
         if (pid[i] < 0 || pid[i] >= w->n_if) return fail(NFK_ERR_ARG, "bad property id (object properties: nfk_get_objects)");
@@ -2526,7 +2705,10 @@ int nfk_switch_scene(void* world, int64_t gh, int64_t gd, int32_t scene, int32_t
     if (group < 0) return fail(NFK_ERR_ARG, "negative group");
     // the property writes of KM:931-942, in call order (queued like SetProperty*)
     auto put = [&](int32_t pid, uint64_t bits) {
-        if (pid >= 0) w->xops.push_back({(uint32_t)o, (uint32_t)pid, bits});
+        if (pid >= 0) {
+            w->xops.push_back({(uint32_t)o, (uint32_t)pid, bits});
+            count_standalone(w, (uint32_t)pid);
+        }
     };
     auto dbits = [](double v) {
         uint64_t u;
@@ -2731,93 +2913,15 @@ int nfk_execute(void* world, int64_t now_ms) {
     // are folded by a stable radix sort of packed words (key << ib | call index), ib = the bits
     // of the largest call index, so the sort moves one array and keeps call order within a key.
     //
-    // SetProperty*: (slot, property) groups, each group's calls in call order (key slot << 7 |
-    // property); the most standalone groups (properties no program writes) of one 256-slot tile
-    // bounds the tile's events beside the program slots
-    const size_t n_xq = w->xops.size(), n_hq = w->hops.size();  // (for the trace)
-    std::vector<uint32_t>& g_slot = w->g_slot;
-    std::vector<uint32_t>& g_pid = w->g_pid;
-    std::vector<uint32_t>& g_first = w->g_first;
-    g_slot.clear();
-    g_pid.clear();
-    g_first.clear();
-    int64_t max_sa = 0;
-    std::vector<uint64_t>& xpk = w->xpk;
-    xpk.clear();
-    const int xib = bits_for(n_xq);
-    const uint64_t xim = (1ull << xib) - 1;
-    if (n_xq) {
-        // the (slot, property) groups of xpk[a, e) (sorted): group starts, and the most
-        // standalone groups of one tile
-        auto group_range = [&](size_t a, size_t e, std::vector<uint32_t>& gs, std::vector<uint32_t>& gp,
-                               std::vector<uint32_t>& gf, int64_t& msa) {
-            int64_t tile_sa = 0;
-            uint32_t cur_tile = 0xFFFFFFFFu;
-            uint64_t prev = ~0ull;
-            for (size_t i = a; i < e; i++) {
-                const uint64_t key = xpk[i] >> xib;
-                if (key == prev) continue;
-                prev = key;
-                const uint32_t sl = (uint32_t)(key >> 7), pid = (uint32_t)(key & 127);
-                gs.push_back(sl);
-                gp.push_back(pid);
-                gf.push_back((uint32_t)i);
-                if (w->tab.w_slot[pid] == kNoU) {
-                    if (sl / kTile != cur_tile) {
-                        cur_tile = sl / kTile;
-                        tile_sa = 0;
-                    }
-                    msa = std::max(msa, ++tile_sa);
-                }
-            }
-        };
-        if (n_xq >= w->par_calls && w->pool->threads() > 1) {
-            // on the host pool: slot ranges folded by one thread each (fold_sorted), then grouped
-            // per range and concatenated (a group never straddles two ranges)
-            std::vector<size_t> bend;
-            const uint64_t kor = fold_sorted(
-                w, n_xq, xib, 7,
-                [&](size_t i) -> uint64_t {
-                    if (i + 16 < n_xq) __builtin_prefetch(&w->slot_of_obj[w->xops[i + 16].slot]);
-                    const int32_t sl = w->slot_of_obj[w->xops[i].slot];
-                    return sl < 0 ? ~0ull : (((uint64_t)(uint32_t)sl << 7) | w->xops[i].pid);
-                },
-                xpk, w->xpk_t, bend);
-            if (bits_for(kor) + xib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued SetProperty calls"));
-            const int P = (int)bend.size();
-            std::vector<std::vector<uint32_t>> bs(P), bp(P), bf(P);
-            std::vector<int64_t> bm(P, 0);
-            w->pool->run(P, [&](int b) { group_range(b ? bend[b - 1] : 0, bend[b], bs[b], bp[b], bf[b], bm[b]); });
-            for (int b = 0; b < P; b++) {
-                g_slot.insert(g_slot.end(), bs[b].begin(), bs[b].end());
-                g_pid.insert(g_pid.end(), bp[b].begin(), bp[b].end());
-                g_first.insert(g_first.end(), bf[b].begin(), bf[b].end());
-                max_sa = std::max(max_sa, bm[b]);
-            }
-            g_first.push_back((uint32_t)xpk.size());
-        } else {
-            xpk.resize(n_xq);
-            uint64_t kor = 0;
-            size_t k = 0;
-            for (size_t i = 0; i < n_xq; i++) {
-                if (i + 16 < n_xq) __builtin_prefetch(&w->slot_of_obj[w->xops[i + 16].slot]);
-                const int32_t sl = w->slot_of_obj[w->xops[i].slot];
-                if (sl < 0) continue;
-                const uint64_t key = ((uint64_t)(uint32_t)sl << 7) | w->xops[i].pid;
-                kor |= key;
-                xpk[k++] = (key << xib) | i;
-            }
-            xpk.resize(k);
-            if (bits_for(kor) + xib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued SetProperty calls"));
-            radix_sort_packed(xpk, w->xpk_t, xib, bits_for(kor));
-            g_slot.reserve(k);
-            g_pid.reserve(k);
-            g_first.reserve(k + 1);
-            group_range(0, k, g_slot, g_pid, g_first, max_sa);
-            g_first.push_back((uint32_t)k);
-        }
-    }
-    const size_t nxc = xpk.size();
+    // SetProperty*: (slot, property) groups, each group's calls in call order, folded on the
+    // device (k_xkeys, radix sort, k_scan_heads, k_xgroups below): the host hands the calls over as
+    // queued.  A tile's events are its slots' program destinations plus its standalone groups
+    // (properties no program writes); those are bounded here without the slots: at most one per
+    // standalone call, and at most one per slot and standalone property the window sets.
+    const size_t n_xq = w->xops.size(), n_hq = w->hops.size();
+    const int64_t max_sa = n_xq ? std::min<int64_t>(w->sa_calls, (int64_t)kTile * (__builtin_popcountll(w->sa_pids[0]) +
+                                                                                   __builtin_popcountll(w->sa_pids[1])))
+                                : 0;
     // a tile's events: its slots' program destinations plus its standalone Set groups
     {
         const int64_t need_ev = (int64_t)kTile * std::max(w->n_dst_union, 1) + max_sa;
@@ -3110,10 +3214,10 @@ int nfk_execute(void* world, int64_t now_ms) {
 
     tp[3] = clk::now();
     // ---- uploads through the pinned arena ----
-    const size_t ng = g_slot.size(), npre = pre_slot.size(), npost = post.size();
-    size_t off_xs = 0, off_xp = align16(off_xs + ng * 4), off_xf = align16(off_xp + ng * 4);
-    size_t off_xb = align16(off_xf + (ng + 1) * 4);
-    size_t off_ps = align16(off_xb + nxc * 8), off_po = align16(off_ps + npre * 4);
+    // (the SetProperty calls as queued: (object, property, bits) and the head halves)
+    const size_t ng = n_xq, npre = pre_slot.size(), npost = post.size();
+    size_t off_xc = 0;
+    size_t off_ps = align16(off_xc + ng * sizeof(World::XOp)), off_po = align16(off_ps + npre * 4);
     size_t off_qs = align16(off_po + npre * 4), off_qk = align16(off_qs + npost * 4);
     size_t off_qo = align16(off_qk + npost * 4), off_qi = align16(off_qo + npost * 4);
     size_t off_qc = align16(off_qi + npost * 4), off_qt = align16(off_qc + npost * 4);
@@ -3124,15 +3228,39 @@ int nfk_execute(void* world, int64_t now_ms) {
     size_t off_xh = align16(off_sg + nrss * 4);  // head halves of the calls (object properties)
     // record row-operation lists
     const size_t nrl = rl_slot.size(), nrcall = rc_code.size(), nval = w->rvals.size();
-    size_t off_l0 = align16(off_xh + (objs ? nxc * 8 : 0)), off_ls = align16(off_l0 + (nrl ? nrss * 4 : 0));
+    size_t off_l0 = align16(off_xh + (objs ? ng * 8 : 0)), off_ls = align16(off_l0 + (nrl ? nrss * 4 : 0));
     size_t off_lr = align16(off_ls + nrl * 4), off_lc = align16(off_lr + nrl * 4);
     size_t off_le = align16(off_lc + (nrl ? (nrl + 1) * 4 : 0)), off_cc = align16(off_le + nrl * 4);
     size_t off_ca = align16(off_cc + nrcall * 4), off_cb = align16(off_ca + nrcall * 4);
     size_t off_rv = align16(off_cb + nrcall * 8);
     size_t total = align16(off_rv + (nrl ? nval * 8 : 0));
+    // device fold scratch: keys, sorted keys, call indices, sorted indices, group starts [ng + 1],
+    // the groups (slot, property, first call [ng + 1]), the sorted values (and head halves), then
+    // the radix sort's temporary storage
+    const int xkey_bits = bits_for((uint64_t)std::max(w->d.cap, 1)) + 8;  // (~0: no slot, sorts last)
+    size_t xf_sort = 0;
+    const size_t xa = (ng * 8 + 255) & ~(size_t)255, xa4 = ((ng + 1) * 4 + 255) & ~(size_t)255;
+    const size_t xo_k1 = 0, xo_k2 = xo_k1 + xa, xo_i1 = xo_k2 + xa, xo_i2 = xo_i1 + xa4, xo_gi = xo_i2 + xa4,
+                 xo_xs = xo_gi + xa4, xo_xp = xo_xs + xa4, xo_xf = xo_xp + xa4, xo_xb = xo_xf + xa4,
+                 xo_xh = xo_xb + xa, xo_tmp = xo_xh + (objs ? xa : 0);
     if (ng) {
         int r = dev_reserve(w, (void**)&w->xs_buf, &w->xs_cap, ng * (objs ? 32 : 16));
         if (r) return drop_window(w, r);
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, xf_sort, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                         (uint32_t*)nullptr, ng, 0, xkey_bits, w->stream));
+        r = dev_reserve(w, &w->xf_buf, &w->xf_cap, xo_tmp + xf_sort + 256);
+        if (r) return drop_window(w, r);
+        if (w->obj_slot_dirty || (size_t)w->n_obj * 4 > w->obj_slot_cap) {
+            r = dev_reserve(w, (void**)&w->obj_slot_d, &w->obj_slot_cap, ((size_t)w->n_obj + 1) * 4);
+            if (r) return drop_window(w, r);
+            HIPCHK(hipMemsetAsync(w->obj_slot_d, 0xFF, (size_t)w->n_obj * 4, w->stream));
+            if (d.N > 0)
+                hipLaunchKernelGGL(k_obj_slots, dim3((unsigned)((d.N + 255) / 256)), dim3(256), 0, w->stream,
+                                   (const int32_t*)w->slot_obj_d, (const uint64_t*)w->fan_desc_w, (int32_t)d.N,
+                                   w->obj_slot_d);
+            HIPCHK(hipGetLastError());
+            w->obj_slot_dirty = false;
+        }
     }
     if (nrss) {
         int r = dev_reserve(w, (void**)&w->rs_buf, &w->rs_cap, std::max<size_t>(ngr, 1) * 16);
@@ -3148,18 +3276,8 @@ int nfk_execute(void* world, int64_t now_ms) {
         if (r) return drop_window(w, r);
         char* P = (char*)w->pin;
         if (ng) {
-            memcpy(P + off_xs, g_slot.data(), ng * 4);
-            memcpy(P + off_xp, g_pid.data(), ng * 4);
-            memcpy(P + off_xf, g_first.data(), (ng + 1) * 4);
-            uint64_t* xb = (uint64_t*)(P + off_xb);
-            uint64_t* xh = objs ? (uint64_t*)(P + off_xh) : nullptr;
-            const int np = nxc >= w->par_calls ? w->pool->threads() : 1;
-            w->pool->run(np, [&](int c) {
-                const size_t a = nxc * c / np, e = nxc * (c + 1) / np;
-                for (size_t i = a; i < e; i++) xb[i] = w->xops[xpk[i] & xim].bits;
-                if (xh)
-                    for (size_t i = a; i < e; i++) xh[i] = w->xops_h[xpk[i] & xim];
-            });
+            memcpy(P + off_xc, w->xops.data(), ng * sizeof(World::XOp));
+            if (objs) memcpy(P + off_xh, w->xops_h.data(), ng * 8);
         }
         for (size_t i = 0; i < npre; i++) {
             ((uint32_t*)(P + off_ps))[i] = pre_slot[i];
@@ -3199,14 +3317,17 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     tp[4] = clk::now();
     char* S = (char*)w->stage;
+    // the groups as k_xgroups lays them out: n_x = the call count bounds the groups (entries past
+    // the frame's groups hold kNoGroupSlot)
+    char* XF = (char*)w->xf_buf;
     d.n_x = (int32_t)ng;
-    d.x_slot = ng ? (const uint32_t*)(S + off_xs) : nullptr;
-    d.x_pid = ng ? (const uint32_t*)(S + off_xp) : nullptr;
-    d.x_first = ng ? (const uint32_t*)(S + off_xf) : nullptr;
-    d.x_bits = ng ? (const uint64_t*)(S + off_xb) : nullptr;
+    d.x_slot = ng ? (const uint32_t*)(XF + xo_xs) : nullptr;
+    d.x_pid = ng ? (const uint32_t*)(XF + xo_xp) : nullptr;
+    d.x_first = ng ? (const uint32_t*)(XF + xo_xf) : nullptr;
+    d.x_bits = ng ? (const uint64_t*)(XF + xo_xb) : nullptr;
     d.x_old = ng ? (uint64_t*)w->xs_buf : nullptr;
     d.x_new = ng ? (uint64_t*)w->xs_buf + ng : nullptr;
-    d.x_bits_h = ng && objs ? (const uint64_t*)(S + off_xh) : nullptr;
+    d.x_bits_h = ng && objs ? (const uint64_t*)(XF + xo_xh) : nullptr;
     d.x_old_h = ng && objs ? (uint64_t*)w->xs_buf + 2 * ng : nullptr;
     d.x_new_h = ng && objs ? (uint64_t*)w->xs_buf + 3 * ng : nullptr;
     d.n_rs = (int32_t)ngr;
@@ -3242,6 +3363,8 @@ int nfk_execute(void* world, int64_t now_ms) {
     w->ucache.clear();
     w->xops.clear();
     w->xops_h.clear();
+    w->sa_calls = 0;
+    w->sa_pids[0] = w->sa_pids[1] = 0;
     w->hops.clear();
     w->dcache.clear();
     w->ov_last.clear();
@@ -3265,8 +3388,23 @@ int nfk_execute(void* world, int64_t now_ms) {
                 hipLaunchKernelGGL(k_rrows, dim3((unsigned)((nrl + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, d);
         }
         if (ng) {
-            hipLaunchKernelGGL(k_ext_scatter, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, w->stream,
-                               d.x_slot, (int32_t)ng, d.ext_head);
+            // the device fold: keys (slot << 7 | property) -> stable radix sort -> groups
+            const unsigned gx = (unsigned)((ng + 255) / 256);
+            const XCall* xc = (const XCall*)(S + off_xc);
+            uint64_t* k1 = (uint64_t*)(XF + xo_k1);
+            uint64_t* k2 = (uint64_t*)(XF + xo_k2);
+            uint32_t* i1 = (uint32_t*)(XF + xo_i1);
+            uint32_t* i2 = (uint32_t*)(XF + xo_i2);
+            uint32_t* gi = (uint32_t*)(XF + xo_gi);
+            hipLaunchKernelGGL(k_xkeys, dim3(gx), dim3(256), 0, w->stream, xc, (int32_t)ng,
+                               (const int32_t*)w->obj_slot_d, k1, i1, (uint32_t*)d.x_slot);
+            size_t sb = xf_sort;
+            HIPCHK(rocprim::radix_sort_pairs(XF + xo_tmp, sb, k1, k2, i1, i2, ng, 0, xkey_bits, w->stream));
+            hipLaunchKernelGGL(k_scan_heads, dim3(1), dim3(1024), 0, w->stream, (const uint64_t*)k2, (int)ng, gi);
+            hipLaunchKernelGGL(k_xgroups, dim3(gx), dim3(256), 0, w->stream, (const uint64_t*)k2, (const uint32_t*)i2,
+                               (const uint32_t*)gi, xc, objs ? (const uint64_t*)(S + off_xh) : nullptr, (int32_t)ng,
+                               (uint32_t*)d.x_slot, (uint32_t*)d.x_pid, (uint32_t*)d.x_first, (uint64_t*)d.x_bits,
+                               (uint64_t*)d.x_bits_h, d.ext_head);
             hipLaunchKernelGGL(k_sets, dim3((unsigned)((ng + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, d);
         }
         if (npre)

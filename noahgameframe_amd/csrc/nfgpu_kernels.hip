@@ -1,6 +1,7 @@
 // nfgpu_kernels.hip — hand-written gfx950 kernels for one NoahGameFrame server frame.
 //
-//   k_ext_scatter   index queued SetProperty* calls by slot
+//   k_xkeys / k_scan_heads / k_xgroups   queued SetProperty* calls folded into (slot, property)
+//                   groups (with a device radix sort between k_xkeys and k_scan_heads)
 //   k_pre_hostops   RemoveSchedule(self[, name]) effects that precede the scan
 //   k_tick          heartbeat timer scan (NFCScheduleModule::Execute, SM:49-81) + effect
 //                   programs + property change predicates (NFCProperty::SetInt/SetFloat,
@@ -22,11 +23,127 @@
 namespace nfgpu {
 
 // ---------------------------------------------------------------------------------
-// ext_head[slot] = 1 + the slot's first SetProperty group (groups sorted by slot)
-__global__ void k_ext_scatter(const uint32_t* __restrict__ x_slot, int32_t n, uint32_t* __restrict__ ext_head) {
+// The window's SetProperty* calls folded into (slot, property) groups on the device.  The host
+// hands the calls over as they were queued (object index, property, value bits, in call order);
+// each resolves to its slot after the window's membership changes, a stable radix sort by
+// (slot, property) keeps call order inside a group, and the groups are laid out as k_sets and
+// k_tick read them (Dev::x_*).  Group entries past the frame's groups hold kNoGroupSlot, so Dev::n_x
+// may be the call count (an upper bound the host knows without a read-back).
+constexpr uint32_t kNoGroupSlot = 0xFFFFFFFFu;
+struct XCall {  // (World::XOp's layout)
+    uint32_t obj, pid;
+    uint64_t bits;
+};
+
+// ---------------------------------------------------------------------------------
+// NFGUID -> object index lookups of a large call batch (NFCKernelModule's GetElement(self) of every
+// SetProperty* / schedule call, KM:323), on the device mirror of the host's open-addressing table
+// (include/nfgpu_guidmap.hpp GuidMap: same entries, same hash, linear probing, no tombstones).
+struct GuidEntry {  // (GuidMap::E's layout)
+    int64_t h, d;
+    int32_t v;
+};
+__device__ __forceinline__ uint64_t guid_home(int64_t h, int64_t d, uint64_t mask) {  // GuidMap::home
+    uint64_t x = (uint64_t)h * 0x9E3779B97F4A7C15ull ^ (uint64_t)d;
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    return x & mask;
+}
+// q = [n] heads then [n] data halves; out[i] = the object index, -1 when absent
+__global__ void k_guid_find(const GuidEntry* __restrict__ t, uint64_t mask, const int64_t* __restrict__ q, int32_t n,
+                            int32_t* __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if (i == 0 || x_slot[i] != x_slot[i - 1]) ext_head[x_slot[i]] = (uint32_t)i + 1;
+    const int64_t h = q[i], dd = q[(size_t)n + i];
+    int32_t r = -1;
+    for (uint64_t s = guid_home(h, dd, mask);; s = (s + 1) & mask) {  // (the table is at most half full)
+        const GuidEntry e = t[s];
+        if (e.v < 0) break;
+        if (e.h == h && e.d == dd) {
+            r = e.v;
+            break;
+        }
+    }
+    out[i] = r;
+}
+// the entries the host table's inserts / erases wrote since the last batch, at their indices
+__global__ void k_guid_patch(GuidEntry* __restrict__ t, const uint32_t* __restrict__ idx,
+                             const GuidEntry* __restrict__ e, int32_t n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) t[idx[i]] = e[i];
+}
+
+// obj_slot[o] = the slot object o holds (entries start at -1); slack slots are skipped
+__global__ void k_obj_slots(const int32_t* __restrict__ slot_obj, const uint64_t* __restrict__ fan_desc, int32_t n,
+                            int32_t* __restrict__ obj_slot) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const int32_t o = slot_obj[s];
+    if (o >= 0 && !desc_dead(fan_desc[s])) obj_slot[o] = s;
+}
+
+// key of call i: slot << 7 | property, ~0 when the object holds no slot ("There is no object":
+// destroyed or exported in this window); the group entries start empty
+__global__ void k_xkeys(const XCall* __restrict__ x, int32_t n, const int32_t* __restrict__ obj_slot,
+                        uint64_t* __restrict__ keys, uint32_t* __restrict__ idx, uint32_t* __restrict__ x_slot) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const XCall c = x[i];
+    const int32_t sl = obj_slot[c.obj];
+    keys[i] = sl < 0 ? ~0ull : (((uint64_t)(uint32_t)sl << 7) | c.pid);
+    idx[i] = (uint32_t)i;
+    x_slot[i] = kNoGroupSlot;
+}
+
+// gidx[i] = groups that start before sorted call i (a group starts where the key changes),
+// gidx[n] = the frame's groups; one workgroup (a window's calls: tens of thousands)
+__global__ __launch_bounds__(1024) void k_scan_heads(const uint64_t* __restrict__ keys, int n, uint32_t* __restrict__ gidx) {
+    __shared__ uint32_t s[1024];
+    const int per = (n + 1023) / 1024, i0 = min(n, (int)threadIdx.x * per), i1 = min(n, i0 + per);
+    auto head = [&](int i) -> uint32_t { return keys[i] != ~0ull && (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u; };
+    uint32_t sum = 0;
+    for (int i = i0; i < i1; i++) sum += head(i);
+    s[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const uint32_t v = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t acc = s[threadIdx.x] - sum;
+    for (int i = i0; i < i1; i++) {
+        gidx[i] = acc;
+        acc += head(i);
+    }
+    if (threadIdx.x == 1023) gidx[n] = s[1023];
+}
+
+// the groups (slot, property, first call), each slot's first group in ext_head, and the calls'
+// values in sorted order
+__global__ void k_xgroups(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ idx,
+                          const uint32_t* __restrict__ gidx, const XCall* __restrict__ x,
+                          const uint64_t* __restrict__ x_h, int32_t n, uint32_t* __restrict__ x_slot,
+                          uint32_t* __restrict__ x_pid, uint32_t* __restrict__ x_first, uint64_t* __restrict__ x_bits,
+                          uint64_t* __restrict__ x_bits_h, uint32_t* __restrict__ ext_head) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = keys[i];
+    if (k == ~0ull) return;
+    const uint32_t j = idx[i];
+    x_bits[i] = x[j].bits;
+    if (x_bits_h) x_bits_h[i] = x_h[j];
+    const uint64_t kp = i ? keys[i - 1] : ~0ull;
+    const uint32_t sl = (uint32_t)(k >> 7);
+    if (k != kp) {
+        const uint32_t g = gidx[i];
+        x_slot[g] = sl;
+        x_pid[g] = (uint32_t)(k & 127);
+        x_first[g] = (uint32_t)i;
+        if (i == 0 || (uint32_t)(kp >> 7) != sl) ext_head[sl] = g + 1;
+    }
+    if (i + 1 == n || keys[i + 1] == ~0ull) x_first[gidx[n]] = (uint32_t)i + 1;  // the last group's end
 }
 
 // The SetProperty* calls queued before this frame (NFCKernelModule::SetPropertyInt/Float,
@@ -38,7 +155,7 @@ __global__ void k_ext_scatter(const uint32_t* __restrict__ x_slot, int32_t n, ui
 // frame-start value and that value for the frame's diff.
 __global__ __launch_bounds__(kTPB) void k_sets(Dev d) {
     const int g = blockIdx.x * kTPB + threadIdx.x;
-    if (g >= d.n_x) return;
+    if (g >= d.n_x || d.x_slot[g] == kNoGroupSlot) return;
     const uint32_t pid = d.x_pid[g];
     uint64_t* p = prop_ptr(d, pid, (int)d.x_slot[g]);
     const uint64_t start = *p;

@@ -357,12 +357,15 @@ bool NFGPUKernelModule::GetRange(const std::string& prop, int k,
 
 int NFGPUKernelModule::ObjectIndex(const NFGUID& g) const { return obj_of_.find(g.nHead64, g.nData64); }
 
+// (the object index this module found is nfk's: nfk_set_props_obj queues without a second lookup)
 bool NFGPUKernelModule::SetPropertyInt(const NFGUID& self, const std::string& name, int64_t v) {
     auto it = prop_id_.find(name);
-    if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_INT || ObjectIndex(self) < 0) return false;
+    if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_INT) return false;
+    const int32_t o = ObjectIndex(self);
+    if (o < 0) return false;
     int32_t pid = dev_pid_[(size_t)it->second];
     uint64_t b = (uint64_t)v;
-    if (nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) != NFK_OK) return false;
+    if (nfk_set_props_obj(world_, 1, &o, &pid, &b) != NFK_OK) return false;
     pending_calls_++;
     return true;
 }
@@ -491,10 +494,12 @@ double NFGPUKernelModule::GetRecordFloat(const NFGUID& self, const std::string& 
 
 bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& name, double v) {
     auto it = prop_id_.find(name);
-    if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT || ObjectIndex(self) < 0) return false;
+    if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT) return false;
+    const int32_t o = ObjectIndex(self);
+    if (o < 0) return false;
     int32_t pid = dev_pid_[(size_t)it->second];
     uint64_t b = bits_of(v);
-    if (nfk_set_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b) != NFK_OK) return false;
+    if (nfk_set_props_obj(world_, 1, &o, &pid, &b) != NFK_OK) return false;
     pending_calls_++;
     return true;
 }
@@ -590,8 +595,8 @@ bool NFGPUKernelModule::AddSchedule(const NFGUID& self, const std::string& name,
     if (!committed_ || o < 0 || k == hb_id_.end()) return false;
     int32_t kind = k->second;
     const int64_t now = clock_();
-    check(nfk_add_schedules(world_, 1, &self.nHead64, &self.nData64, &kind, &fTime, &nCount, &now),
-          "nfk_add_schedules");
+    const int32_t op = 1;
+    check(nfk_schedule_calls_obj(world_, 1, &op, &o, &kind, &fTime, &nCount, &now), "nfk_schedule_calls_obj");
     sched_add_.emplace(((uint64_t)o << 8) | (uint32_t)kind, std::make_pair(cb, fTime));  // the window's first call wins
     pending_calls_++;
     return true;
@@ -601,17 +606,24 @@ bool NFGPUKernelModule::AddSchedule(const NFGUID& self, const std::string& name,
 // device program removes nothing but still takes the key
 bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self, const std::string& name) {
     auto k = hb_id_.find(name);
-    if (!committed_ || ObjectIndex(self) < 0) return false;
-    check(nfk_remove_schedule(world_, self.nHead64, self.nData64, k == hb_id_.end() ? -1 : k->second),
-          "nfk_remove_schedule");
+    const int32_t o = committed_ ? ObjectIndex(self) : -1;
+    if (o < 0) return false;
+    const int32_t op = 2, kind = k == hb_id_.end() ? -1 : k->second, cnt = 0;
+    const float t = 0.f;
+    const int64_t now = 0;
+    check(nfk_schedule_calls_obj(world_, 1, &op, &o, &kind, &t, &cnt, &now), "nfk_schedule_calls_obj");
     pending_calls_++;
     return true;
 }
 
 // SM:240-243: erases the object's schedules at once
 bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self) {
-    if (!committed_ || ObjectIndex(self) < 0) return false;
-    check(nfk_remove_all_schedules(world_, self.nHead64, self.nData64), "nfk_remove_all_schedules");
+    const int32_t o = committed_ ? ObjectIndex(self) : -1;
+    if (o < 0) return false;
+    const int32_t op = 3, kind = 0, cnt = 0;
+    const float t = 0.f;
+    const int64_t now = 0;
+    check(nfk_schedule_calls_obj(world_, 1, &op, &o, &kind, &t, &cnt, &now), "nfk_schedule_calls_obj");
     pending_calls_++;
     return true;
 }

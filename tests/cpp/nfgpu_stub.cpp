@@ -27,6 +27,7 @@ struct Stub {
     std::vector<std::vector<std::vector<uint64_t>>> cells;   // [object][rec][col * rows + row]
     std::vector<int> rows, cols;
     std::vector<std::map<int, bool>> sched;                  // [object] kind -> present
+    std::vector<std::pair<int64_t, int64_t>> guid;           // [object] (head, data)
     bool committed = false;
     int n_loaded = 0;
 };
@@ -69,6 +70,7 @@ int add_object(Stub* s, int64_t h, int64_t d) {
     for (size_t r = 0; r < s->rows.size(); r++) c.emplace_back((size_t)s->rows[r] * s->cols[r], 0);
     s->cells.push_back(c);
     s->sched.emplace_back();
+    s->guid.emplace_back(h, d);
     return o;
 }
 }  // namespace
@@ -219,6 +221,16 @@ int nfk_set_props(void* w, int32_t n, const int64_t* gh, const int64_t* gd, cons
     }
     return NFK_OK;
 }
+// the by-object entry points log as their NFGUID forms do (object index -> NFGUID, creation order)
+int nfk_set_props_obj(void* w, int32_t n, const int32_t* obj, const int32_t* pid, const uint64_t* bits) {
+    Stub* s = S(w);
+    for (int i = 0; i < n; i++) {
+        if (obj[i] < 0 || obj[i] >= (int)s->guid.size()) return NFK_ERR_NOTFOUND;
+        const int rc = nfk_set_props(w, 1, &s->guid[obj[i]].first, &s->guid[obj[i]].second, pid + i, bits + i);
+        if (rc) return rc;
+    }
+    return NFK_OK;
+}
 int nfk_set_objects(void* w, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid, const int64_t* vh,
                     const int64_t* vd) {
     Stub* s = S(w);
@@ -340,6 +352,17 @@ int nfk_schedule_calls(void* w, int32_t n, const int32_t* op, const int64_t* gh,
         const int rc = op[i] == 1 ? nfk_add_schedules(w, 1, gh + i, gd + i, kind + i, iv + i, cnt + i, now + i)
                      : op[i] == 2 ? nfk_remove_schedule(w, gh[i], gd[i], kind[i])
                                   : nfk_remove_all_schedules(w, gh[i], gd[i]);
+        if (rc) return rc;
+    }
+    return NFK_OK;
+}
+int nfk_schedule_calls_obj(void* w, int32_t n, const int32_t* op, const int32_t* obj, const int32_t* kind,
+                           const float* iv, const int32_t* cnt, const int64_t* now) {
+    Stub* s = S(w);
+    for (int i = 0; i < n; i++) {
+        if (obj[i] < 0 || obj[i] >= (int)s->guid.size()) return NFK_ERR_NOTFOUND;
+        const int rc = nfk_schedule_calls(w, 1, op + i, &s->guid[obj[i]].first, &s->guid[obj[i]].second, kind + i,
+                                          iv + i, cnt + i, now + i);
         if (rc) return rc;
     }
     return NFK_OK;

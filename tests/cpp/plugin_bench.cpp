@@ -159,11 +159,19 @@ int main(int argc, char** argv) {
     std::vector<NFGPUKernelModule::FrameStats> st;
     std::vector<double> call_ms, frame_ms;
     int64_t xi = 0, hi = 0, ncalls = 0;
+    std::vector<NFGUID> hg, xg;
     for (int t = 0; t < W + K; t++) {
+        // the frame's calls as game logic makes them, NFGUIDs in hand (gathered from the workload's
+        // object arrays before the timed region, as bench.py's host_calls leg does)
+        hg.clear();
+        xg.clear();
+        for (int64_t j = hi; j < NH && h_tick[j] == t; j++) hg.emplace_back(gh[h_obj[j]], gd[h_obj[j]]);
+        for (int64_t j = xi; j < NX && x_tick[j] == t; j++) xg.emplace_back(gh[x_obj[j]], gd[x_obj[j]]);
+        const int64_t hi0 = hi, xi0 = xi;
         const auto t0 = std::chrono::steady_clock::now();
         for (; hi < NH && h_tick[hi] == t; hi++) {
             if (!calls) continue;
-            NFGUID g(gh[h_obj[hi]], gd[h_obj[hi]]);
+            const NFGUID& g = hg[(size_t)(hi - hi0)];
             g_now = h_time[hi];
             if (h_op[hi] == 1) km.AddSchedule(g, kname[h_kind[hi]], hb, h_int[hi], h_cnt[hi]);
             else if (h_op[hi] == 2) km.RemoveSchedule(g, kname[h_kind[hi]]);
@@ -172,7 +180,7 @@ int main(int argc, char** argv) {
         }
         for (; xi < NX && x_tick[xi] == t; xi++) {
             if (!calls) continue;
-            NFGUID g(gh[x_obj[xi]], gd[x_obj[xi]]);
+            const NFGUID& g = xg[(size_t)(xi - xi0)];
             if (x_pid[xi] < NI) {
                 km.SetPropertyInt(g, pname[x_pid[xi]], (int64_t)x_bits[xi]);
             } else {

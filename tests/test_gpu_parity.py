@@ -108,14 +108,27 @@ def test_gpu_matches_oracle(gpu_available, monkeypatch, case, path):
 
 @pytest.mark.parametrize("case", ["combined", "wide_sets", "lifecycle", "sched_edges", "record_rows"])
 def test_parallel_call_folding_matches_oracle(gpu_available, monkeypatch, case):
-    """The host pool's folding of a window's calls (GUID lookups split over threads, (slot, property)
-    and (slot, kind) folds by slot range, nfgpu_host.hip fold_sorted) — used from 16384 calls per
-    batch on — forced on every batch here (NFGPU_PAR_CALLS=8), 4 and 7 host threads."""
+    """The host pool's share of a window's calls (GUID lookups split over threads, the (slot, kind)
+    fold of schedule calls by slot range, nfgpu_host.hip fold_sorted) — with NFGPU_HOST_THREADS > 1
+    used from 16384 calls per batch on — forced on every batch here (NFGPU_PAR_CALLS=8), 4 and 7
+    host threads."""
     for threads in ("4", "7"):
         monkeypatch.setenv("NFGPU_PAR_CALLS", "8")
         monkeypatch.setenv("NFGPU_HOST_THREADS", threads)
         w = workload.make_world(n_ticks=10, seed=sum(map(ord, case)), **CASES[case])
         compare_runs(run_gpu(w), run_oracle(w))
+
+
+@pytest.mark.parametrize("case", ["combined", "wide_sets", "lifecycle", "lifecycle_records", "switch_scene", "sched_edges",
+                                  "record_rows", "objects"])
+def test_device_guid_lookups_match_oracle(gpu_available, monkeypatch, case):
+    """GUID -> object lookups of a call batch on the device mirror of the host's NFGUID table
+    (nfgpu_host.hip find_many_dev; k_guid_find, k_guid_patch) — used from 4096 calls per batch on —
+    forced on every batch (NFGPU_DEV_LOOKUP=1), through creates, destroys and scene switches that
+    rewrite the table between batches."""
+    monkeypatch.setenv("NFGPU_DEV_LOOKUP", "1")
+    w = workload.make_world(n_ticks=10, seed=sum(map(ord, case)), **CASES[case])
+    compare_runs(run_gpu(w), run_oracle(w))
 
 
 @PATHS
