@@ -164,6 +164,9 @@ struct Dev {
     uint64_t* x_old_h;
     uint64_t* x_new_h;
     int32_t n_x;              // groups
+    // a calls-only pass (nfk_execute_calls: nothing fires): the tiles with SetProperty groups;
+    // k_tick's other tiles only write empty outputs.  Null: every tile runs.
+    const uint8_t* tile_work;
     uint32_t* fired_mask;  // [cap]
     // queued SetRecordInt / SetRecordFloat calls folded into (slot, cell) GROUPS sorted by (slot,
     // rec << 16 | row << 8 | col), each group's calls rs_bits[rs_first[g], rs_first[g + 1]) in call

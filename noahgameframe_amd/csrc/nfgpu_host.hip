@@ -174,6 +174,17 @@ struct World {
     bool obj_slot_dirty = true;
     void* xf_buf = nullptr;
     size_t xf_cap = 0;
+    // SetProperty calls of large batches queued on the device (set_props_dev), in two buffers used
+    // by alternate windows: the window's first xq_n calls are xq[xq_b][0, xq_n) (XOp records), the
+    // host xops the calls queued after them; xq_ev[b]: the frame that folded buffer b read it
+    void* xq[2] = {nullptr, nullptr};
+    size_t xq_cap[2] = {0, 0};  // records
+    hipEvent_t xq_ev[2] = {nullptr, nullptr};
+    bool xq_ev_set[2] = {false, false};
+    int xq_b = 0;
+    size_t xq_n = 0;
+    uint8_t* tile_work_d = nullptr;  // a calls-only pass's tiles with SetProperty groups (Dev::tile_work)
+    size_t tile_work_cap = 0;
     std::vector<int32_t> look;           // GUID lookups of one batched call
     // GUID lookups of large call batches on the device (find_many_dev): obj_of's device mirror
     // (guid_d, same entries and hash), the log of the entries the host table wrote since the
@@ -201,12 +212,6 @@ struct World {
     std::vector<uint32_t> ov_prev;
     uint64_t* gat = nullptr;             // device scratch of gathered reads
     size_t gat_cap = 0;
-    // the last frame's AddSchedule entries (object or -1, kind) and whether each created a schedule
-    std::vector<int32_t> post_obj;
-    std::vector<uint32_t> post_kind;
-    uint8_t* added_d = nullptr;
-    size_t added_cap = 0;
-    std::vector<uint64_t> hpk, hpk_t;  // packed (key << 32 | call index) sort scratch
     // host worker threads for large call batches (NFGPU_HOST_THREADS, default 1 = none)
     std::unique_ptr<HostPool> pool;
     size_t par_calls = 16384;  // batches from this size on use the pool (NFGPU_PAR_CALLS: tests)
@@ -228,9 +233,17 @@ struct World {
     size_t rs_cap = 0;
     void* rss_buf = nullptr;  // rss_ev / rss_msg / rss_pos / rss_pmsg
     size_t rss_cap = 0;
-    struct Post { uint32_t slot, kind, op; float interval; int32_t count; int64_t time; };
-    std::vector<uint32_t> pre_slot, pre_op;  // schedule-call folding results of the frame
-    std::vector<Post> post, post_t;
+    // the device fold of the schedule calls (hf_buf: keys, counts, pre / post entries, added flags);
+    // the last pass's post entries (hf_post, count at *hf_npost) stay for nfk_read_added
+    void* hf_buf = nullptr;
+    size_t hf_cap = 0;
+    bool hf_pending = false;
+    size_t hf_max = 0;         // post entries' room (2 per call)
+    const uint32_t* hf_npost = nullptr;
+    const uint32_t* hf_pslot = nullptr;
+    const uint32_t* hf_pkind = nullptr;
+    const uint32_t* hf_pop = nullptr;
+    const uint8_t* hf_added = nullptr;
     void* xs_buf = nullptr;  // x_old / x_new (/ x_old_h / x_new_h)
     size_t xs_cap = 0;
     struct HOp { int32_t code; uint32_t slot, kind; float interval; int32_t count; int64_t time; };
@@ -279,6 +292,8 @@ inline void count_standalone(World* w, uint32_t pid) {
         w->sa_pids[pid >> 6] |= 1ull << (pid & 63);
     }
 }
+static_assert(sizeof(World::HOp) == sizeof(HCall) && offsetof(World::HOp, time) == offsetof(HCall, time),
+              "k_hkeys / k_hfold read the queued schedule calls as uploaded");
 static_assert(sizeof(World::XOp) == sizeof(XCall) && offsetof(World::XOp, bits) == offsetof(XCall, bits),
               "k_xkeys reads the queued SetProperty calls as uploaded");
 
@@ -292,6 +307,7 @@ inline int64_t prop_word(const World* w, int32_t pid) {
 // membership part cannot be undone, so none of the window's calls is applied out of its order in
 // a later frame.  (A failure before that keeps every queue.)
 int drop_window(World* w, int r) {
+    w->xq_n = 0;
     w->xops.clear();
     w->xops_h.clear();
     w->sa_calls = 0;
@@ -579,40 +595,34 @@ void radix_sort_packed(std::vector<uint64_t>& a, std::vector<uint64_t>& t, int s
 }
 int bits_for(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 1; }
 
-// radix_sort_packed on a range a[0, n) with scratch t[0, n); the result is in a
-void radix_sort_range(uint64_t* a, uint64_t* t, size_t n, int shift, int key_bits) {
-    if (n < 2) return;
-    uint32_t cnt[2048];
-    bool in_t = false;
-    for (int sh = shift; sh < shift + key_bits; sh += 11) {
-        memset(cnt, 0, sizeof cnt);
-        for (size_t i = 0; i < n; i++) cnt[(a[i] >> sh) & 2047]++;
-        if (cnt[(a[0] >> sh) & 2047] == n) continue;
-        uint32_t acc = 0;
-        for (int b = 0; b < 2048; b++) {
-            const uint32_t c = cnt[b];
-            cnt[b] = acc;
-            acc += c;
-        }
-        for (size_t i = 0; i < n; i++) t[cnt[(a[i] >> sh) & 2047]++] = a[i];
-        std::swap(a, t);
-        in_t = !in_t;
+
+// look_pin / look_dev (the device lookups' pinned and device staging) hold at least `bytes`
+int look_reserve(World* w, size_t bytes) {
+    if (bytes > w->look_pin_cap) {
+        if (w->look_pin) HIPCHK(hipHostFree(w->look_pin));
+        w->look_pin = nullptr;
+        w->look_pin_cap = 0;
+        HIPCHK(hipHostMalloc((void**)&w->look_pin, bytes + bytes / 2, hipHostMallocDefault));
+        w->look_pin_cap = bytes + bytes / 2;
     }
-    if (in_t) memcpy(t, a, n * 8);  // (a and t swapped: copy back into the caller's a)
+    if (bytes > w->look_dev_cap) {
+        if (w->look_dev) HIPCHK(hipFree(w->look_dev));
+        w->look_dev = nullptr;
+        w->look_dev_cap = 0;
+        HIPCHK(hipMalloc(&w->look_dev, bytes + bytes / 2));
+        w->look_dev_cap = bytes + bytes / 2;
+    }
+    return NFK_OK;
 }
 
-// n lookups of a large batch on the device mirror of obj_of: the mirror is brought up to date
-// first (the entries the host table wrote since, or the whole table after it was rebuilt), then
-// one H2D copy of the GUIDs, k_guid_find, one D2H copy of the object indices
-int find_many_dev(World* w, int32_t n, const int64_t* gh, const int64_t* gd, int32_t* out) {
-    const size_t cap = w->obj_of.capacity();
-    if (cap == 0 || n <= 0) {
-        for (int32_t i = 0; i < n; i++) out[i] = -1;
-        return NFK_OK;
-    }
+// Brings the device mirror of obj_of up to date on look_stream (the whole table after a rebuild,
+// else the entries written since the last batch) and reserves the staging: the mirror's patch takes
+// [0, *used) of look_pin / look_dev, the caller's batch (batch_bytes) follows.
+int guid_mirror_update(World* w, size_t batch_bytes, size_t* used) {
     if (!w->look_stream) HIPCHK(hipStreamCreateWithFlags(&w->look_stream, hipStreamNonBlocking));
     using E = GuidMap::E;
     static_assert(sizeof(E) == sizeof(GuidEntry) && offsetof(E, v) == offsetof(GuidEntry, v), "mirror layout");
+    const size_t cap = w->obj_of.capacity();
     const size_t tbytes = cap * sizeof(E);
     bool full = w->obj_of.take_rebuilt() || !w->guid_synced || w->guid_dmask != cap - 1;
     size_t np = full ? 0 : w->guid_log.size();
@@ -620,22 +630,8 @@ int find_many_dev(World* w, int32_t n, const int64_t* gh, const int64_t* gd, int
         full = true;
         np = 0;
     }
-    const size_t o_q = 0, o_r = align16((size_t)n * 16), o_pi = align16(o_r + (size_t)n * 4),
-                 o_pe = align16(o_pi + np * 4), tot = align16(o_pe + np * sizeof(E));
-    if (tot > w->look_pin_cap) {
-        if (w->look_pin) HIPCHK(hipHostFree(w->look_pin));
-        w->look_pin = nullptr;
-        w->look_pin_cap = 0;
-        HIPCHK(hipHostMalloc((void**)&w->look_pin, tot + tot / 2, hipHostMallocDefault));
-        w->look_pin_cap = tot + tot / 2;
-    }
-    if (tot > w->look_dev_cap) {
-        if (w->look_dev) HIPCHK(hipFree(w->look_dev));
-        w->look_dev = nullptr;
-        w->look_dev_cap = 0;
-        HIPCHK(hipMalloc(&w->look_dev, tot + tot / 2));
-        w->look_dev_cap = tot + tot / 2;
-    }
+    const size_t o_pi = 0, o_pe = align16(np * 4), u = align16(o_pe + np * sizeof(E));
+    if (int r = look_reserve(w, u + batch_bytes)) return r;
     char* P = w->look_pin;
     char* D = (char*)w->look_dev;
     if (full) {
@@ -657,16 +653,32 @@ int find_many_dev(World* w, int32_t n, const int64_t* gh, const int64_t* gd, int
             pi[i] = w->guid_log[i];
             pe[i] = t[w->guid_log[i]];
         }
+        HIPCHK(hipMemcpyAsync(D, P, u, hipMemcpyHostToDevice, w->look_stream));
+        hipLaunchKernelGGL(k_guid_patch, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, w->look_stream,
+                           (GuidEntry*)w->guid_d, (const uint32_t*)(D + o_pi), (const GuidEntry*)(D + o_pe), (int32_t)np);
+        HIPCHK(hipGetLastError());
     }
     w->guid_log.clear();
+    *used = u;
+    return NFK_OK;
+}
+
+// n lookups of a large batch on the device mirror of obj_of: one H2D copy of the GUIDs,
+// k_guid_find, one D2H copy of the object indices
+int find_many_dev(World* w, int32_t n, const int64_t* gh, const int64_t* gd, int32_t* out) {
+    const size_t cap = w->obj_of.capacity();
+    if (cap == 0 || n <= 0) {
+        for (int32_t i = 0; i < n; i++) out[i] = -1;
+        return NFK_OK;
+    }
+    const size_t o_q = 0, o_r = align16((size_t)n * 16), tot = align16(o_r + (size_t)n * 4);
+    size_t u = 0;
+    if (int r = guid_mirror_update(w, tot, &u)) return r;
+    char* P = w->look_pin + u;
+    char* D = (char*)w->look_dev + u;
     memcpy(P + o_q, gh, (size_t)n * 8);
     memcpy(P + o_q + (size_t)n * 8, gd, (size_t)n * 8);
     HIPCHK(hipMemcpyAsync(D, P, o_r, hipMemcpyHostToDevice, w->look_stream));
-    if (np) {
-        HIPCHK(hipMemcpyAsync(D + o_pi, P + o_pi, tot - o_pi, hipMemcpyHostToDevice, w->look_stream));
-        hipLaunchKernelGGL(k_guid_patch, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, w->look_stream,
-                           (GuidEntry*)w->guid_d, (const uint32_t*)(D + o_pi), (const GuidEntry*)(D + o_pe), (int32_t)np);
-    }
     hipLaunchKernelGGL(k_guid_find, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, w->look_stream,
                        (const GuidEntry*)w->guid_d, (uint64_t)(cap - 1), (const int64_t*)(D + o_q), n,
                        (int32_t*)(D + o_r));
@@ -674,6 +686,108 @@ int find_many_dev(World* w, int32_t n, const int64_t* gh, const int64_t* gd, int
     HIPCHK(hipMemcpyAsync(P + o_r, D + o_r, (size_t)n * 4, hipMemcpyDeviceToHost, w->look_stream));
     HIPCHK(hipStreamSynchronize(w->look_stream));
     memcpy(out, P + o_r, (size_t)n * 4);
+    return NFK_OK;
+}
+
+// the window's device queue of SetProperty calls (xq[xq_b]) holds at least `recs` records; grown
+// on look_stream with its first xq_n records copied (the frame that last read the buffer is done:
+// look_stream waited for xq_ev at the window's first device batch)
+int xq_reserve(World* w, size_t recs) {
+    const int b = w->xq_b;
+    if (recs <= w->xq_cap[b]) return NFK_OK;
+    const size_t c = std::max<size_t>({recs, w->xq_cap[b] + w->xq_cap[b] / 2, 65536});
+    void* nb = nullptr;
+    HIPCHK(hipMalloc(&nb, c * sizeof(World::XOp)));
+    if (w->xq_n) HIPCHK(hipMemcpyAsync(nb, w->xq[b], w->xq_n * sizeof(World::XOp), hipMemcpyDeviceToDevice, w->look_stream));
+    HIPCHK(hipStreamSynchronize(w->look_stream));
+    if (w->xq[b]) HIPCHK(hipFree(w->xq[b]));
+    w->xq[b] = nb;
+    w->xq_cap[b] = c;
+    return NFK_OK;
+}
+
+// the same at nfk_execute, on the world's stream (the host calls queued after the last device batch
+// are appended there): a new buffer gets the device queue's calls, the old one is freed after
+int xq_reserve_exec(World* w, size_t recs) {
+    const int b = w->xq_b;
+    if (recs <= w->xq_cap[b]) return NFK_OK;
+    const size_t c = std::max<size_t>({recs, w->xq_cap[b] + w->xq_cap[b] / 2, 65536});
+    void* nb = nullptr;
+    HIPCHK(hipMalloc(&nb, c * sizeof(World::XOp)));
+    HIPCHK(hipMemcpyAsync(nb, w->xq[b], w->xq_n * sizeof(World::XOp), hipMemcpyDeviceToDevice, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    HIPCHK(hipFree(w->xq[b]));
+    w->xq[b] = nb;
+    w->xq_cap[b] = c;
+    return NFK_OK;
+}
+
+// A large batch of SetProperty* calls queued on the device (worlds without object properties):
+// the lookups run on the device mirror and each call is written straight into the window's device
+// queue (k_guid_queue), so the host touches the batch once, to stage it.  The host calls queued
+// since the last device batch go in front of it (call order); a GUID that is no object rejects the
+// whole batch, as nfk_set_props does.
+int set_props_dev(World* w, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid, const uint64_t* bits) {
+    int64_t sa = 0;
+    uint64_t sp[2] = {0, 0};
+    for (int32_t i = 0; i < n; i++) {
+        if (pid[i] < 0 || pid[i] >= w->n_if)
+            return fail(NFK_ERR_ARG, pid[i] >= w->n_if && pid[i] < w->n_prop ? "object property: use nfk_set_objects"
+                                                                              : "bad property id");
+        if (w->tab.w_slot[pid[i]] == kNoU) {
+            sa++;
+            sp[pid[i] >> 6] |= 1ull << (pid[i] & 63);
+        }
+    }
+    if (!w->look_stream) HIPCHK(hipStreamCreateWithFlags(&w->look_stream, hipStreamNonBlocking));
+    const int b = w->xq_b;
+    if (w->xq_n == 0 && w->xq_ev_set[b]) HIPCHK(hipStreamWaitEvent(w->look_stream, w->xq_ev[b], 0));
+    const size_t tail = w->xops.size();
+    if (int r = xq_reserve(w, w->xq_n + tail + (size_t)n)) return r;
+    const size_t o_t = 0, o_b = align16(tail * sizeof(World::XOp)), o_p = align16(o_b + (size_t)n * 24),
+                 o_m = align16(o_p + (size_t)n * 4), tot = o_m + 16;
+    size_t u = 0;
+    if (int r = guid_mirror_update(w, tot, &u)) return r;
+    char* P = w->look_pin + u;
+    char* D = (char*)w->look_dev + u;
+    if (tail) memcpy(P + o_t, w->xops.data(), tail * sizeof(World::XOp));
+    memcpy(P + o_b, gh, (size_t)n * 8);
+    memcpy(P + o_b + (size_t)n * 8, gd, (size_t)n * 8);
+    memcpy(P + o_b + (size_t)n * 16, bits, (size_t)n * 8);
+    memcpy(P + o_p, pid, (size_t)n * 4);
+    *(int32_t*)(P + o_m) = INT32_MAX;
+    HIPCHK(hipMemcpyAsync(D, P, tot, hipMemcpyHostToDevice, w->look_stream));
+    World::XOp* q = (World::XOp*)w->xq[b] + w->xq_n;
+    if (tail) HIPCHK(hipMemcpyAsync(q, D + o_t, tail * sizeof(World::XOp), hipMemcpyDeviceToDevice, w->look_stream));
+    hipLaunchKernelGGL(k_guid_queue, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, w->look_stream,
+                       (const GuidEntry*)w->guid_d, (uint64_t)(w->obj_of.capacity() - 1), (const int64_t*)(D + o_b),
+                       (const int32_t*)(D + o_p), n, (XCall*)(q + tail), (int32_t*)(D + o_m));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(P + o_m, D + o_m, 4, hipMemcpyDeviceToHost, w->look_stream));
+    HIPCHK(hipStreamSynchronize(w->look_stream));
+    const int32_t miss = *(const int32_t*)(P + o_m);
+    if (miss >= 0 && miss < n)  // NFCKernelModule logs "There is no object" and returns false (KM:331)
+        return fail(NFK_ERR_NOTFOUND, "no object " + std::to_string(gh[miss]) + "-" + std::to_string(gd[miss]));
+    w->xq_n += tail + (size_t)n;
+    w->xops.clear();
+    w->ov_last.clear();  // (the overlay index is rebuilt from the whole queue at the next read)
+    w->ov_prev.clear();
+    w->sa_calls += sa;
+    w->sa_pids[0] |= sp[0];
+    w->sa_pids[1] |= sp[1];
+    return NFK_OK;
+}
+
+// the window's device queue back in the host xops, in front of the calls queued after it (a read
+// of queued values — GetProperty* — needs them all on the host)
+int pull_device_queue(World* w) {
+    if (!w->xq_n) return NFK_OK;
+    std::vector<World::XOp> dq(w->xq_n);
+    HIPCHK(hipMemcpy(dq.data(), w->xq[w->xq_b], w->xq_n * sizeof(World::XOp), hipMemcpyDeviceToHost));
+    w->xops.insert(w->xops.begin(), dq.begin(), dq.end());
+    w->xq_n = 0;
+    w->ov_last.clear();
+    w->ov_prev.clear();
     return NFK_OK;
 }
 
@@ -697,67 +811,6 @@ int find_many_par(World* w, int32_t n, const int64_t* gh, const int64_t* gd, int
     return NFK_OK;
 }
 
-// A window's calls folded into a packed array (key << ib | call index) sorted by key, call order
-// within a key — radix_sort_packed's result — on the host pool: key(i) gives call i's key (or
-// ~0ull: dropped), whose slot is key >> slot_shift.  The keys are split by slot range into P
-// buckets, each a run of whole 256-slot tiles (so no (slot, *) group and no tile straddles two),
-// scattered into bucket order in call order, and each bucket is radix-sorted by one thread.
-// bucket_end[b] = where bucket b ends in out.  Returns the OR of the keys.
-template <class KeyFn>
-uint64_t fold_sorted(World* w, size_t n, int ib, int slot_shift, KeyFn key, std::vector<uint64_t>& out,
-                     std::vector<uint64_t>& tmp, std::vector<size_t>& bucket_end) {
-    HostPool& pool = *w->pool;
-    const int P = pool.threads();
-    const int C = P;  // call chunks
-    const size_t span = ((size_t)(w->d.cap + P - 1) / P + kTile - 1) / kTile * kTile;
-    std::vector<uint32_t> cnt((size_t)C * P, 0);
-    std::vector<uint64_t> kor_c(C, 0);
-    tmp.resize(n);
-    out.resize(n);
-    pool.run(C, [&](int c) {
-        const size_t a = n * c / C, b = n * (c + 1) / C;
-        uint32_t* cc = &cnt[(size_t)c * P];
-        uint64_t kor = 0;
-        for (size_t i = a; i < b; i++) {
-            const uint64_t k = key(i);
-            if (k == ~0ull) {
-                tmp[i] = ~0ull;
-                continue;
-            }
-            kor |= k;
-            tmp[i] = (k << ib) | i;
-            cc[(k >> slot_shift) / span]++;
-        }
-        kor_c[c] = kor;
-    });
-    uint64_t kor = 0;
-    for (int c = 0; c < C; c++) kor |= kor_c[c];
-    // (bucket, chunk) offsets: bucket-major, chunks in call order
-    std::vector<size_t> off((size_t)C * P);
-    bucket_end.assign(P, 0);
-    size_t acc = 0;
-    for (int b = 0; b < P; b++) {
-        for (int c = 0; c < C; c++) {
-            off[(size_t)c * P + b] = acc;
-            acc += cnt[(size_t)c * P + b];
-        }
-        bucket_end[b] = acc;
-    }
-    out.resize(acc);
-    if (bits_for(kor) + ib > 64) return kor;  // (the caller reports the capacity failure)
-    pool.run(C, [&](int c) {
-        const size_t a = n * c / C, b = n * (c + 1) / C;
-        size_t* oc = &off[(size_t)c * P];
-        for (size_t i = a; i < b; i++)
-            if (tmp[i] != ~0ull) out[oc[((tmp[i] >> ib) >> slot_shift) / span]++] = tmp[i];
-    });
-    const int kb = bits_for(kor);
-    pool.run(P, [&](int b) {
-        const size_t a = b ? bucket_end[b - 1] : 0, e = bucket_end[b];
-        radix_sort_range(out.data() + a, tmp.data() + a, e - a, ib, kb);
-    });
-    return kor;
-}
 
 // replace a tracked device allocation by a bigger one (contents dropped)
 int regrow(World* w, void** p, size_t bytes) {
@@ -1592,6 +1645,11 @@ int nfk_destroy(void* world) {
     if (w->glist) (void)hipFree(w->glist);
     if (w->xs_buf) (void)hipFree(w->xs_buf);
     if (w->xf_buf) (void)hipFree(w->xf_buf);
+    if (w->tile_work_d) (void)hipFree(w->tile_work_d);
+    for (int b = 0; b < 2; b++) {
+        if (w->xq[b]) (void)hipFree(w->xq[b]);
+        if (w->xq_ev[b]) (void)hipEventDestroy(w->xq_ev[b]);
+    }
     if (w->obj_slot_d) (void)hipFree(w->obj_slot_d);
     if (w->rs_buf) (void)hipFree(w->rs_buf);
     if (w->rss_buf) (void)hipFree(w->rss_buf);
@@ -1602,7 +1660,7 @@ int nfk_destroy(void* world) {
     if (w->look_pin) (void)hipHostFree(w->look_pin);
     if (w->look_stream) (void)hipStreamDestroy(w->look_stream);
     if (w->gat) (void)hipFree(w->gat);
-    if (w->added_d) (void)hipFree(w->added_d);
+    if (w->hf_buf) (void)hipFree(w->hf_buf);
     for (auto& p : w->pend) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -2141,6 +2199,8 @@ int nfk_set_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
     World* w = (World*)world;
     if (!w || n < 0 || (n && (!gh || !gd || !pid || !bits))) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
+    // a large batch in a world without object properties: looked up and queued on the device
+    if (w->dev_look_min && (size_t)n >= w->dev_look_min && w->cfg.n_obj == 0) return set_props_dev(w, n, gh, gd, pid, bits);
     w->look.resize(n);  // one GUID lookup per call
     if (int rl = find_many_par(w, n, gh, gd, w->look.data())) return rl;
     return queue_sets(w, n, w->look.data(), pid, bits, gh, gd);
@@ -2531,13 +2591,15 @@ static int word_src(World* w, int32_t o, int32_t pid, int half, uint64_t* src) {
 }
 
 // index the queued Set calls by (object, property) (ov_last / ov_prev chains, call order)
-static void index_queued_sets(World* w) {
+static int index_queued_sets(World* w) {
+    if (int r = pull_device_queue(w)) return r;
     for (size_t i = w->ov_prev.size(); i < w->xops.size(); i++) {
         const uint64_t key = ((uint64_t)w->xops[i].slot << 7) | w->xops[i].pid;
         auto it = w->ov_last.find(key);
         w->ov_prev.push_back(it == w->ov_last.end() ? 0xFFFFFFFFu : it->second);
         w->ov_last[key] = (uint32_t)i;
     }
+    return NFK_OK;
 }
 
 int nfk_get_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid, int64_t* vh,
@@ -2559,7 +2621,7 @@ int nfk_get_objects(void* world, int32_t n, const int64_t* gh, const int64_t* gd
     int r = read_words(w, src, got.data());
     if (r) return r;
     // this window's queued SetObject calls on top: NFCProperty::SetObject keeps the last value
-    index_queued_sets(w);
+    if (int r = index_queued_sets(w)) return r;
     for (int32_t i = 0; i < n; i++) {
         vd[i] = (int64_t)got[2 * (size_t)i];
         vh[i] = (int64_t)got[2 * (size_t)i + 1];
@@ -2608,7 +2670,7 @@ int nfk_get_props(void* world, int32_t n, const int64_t* gh, const int64_t* gd, 
         }
     }
     // 2. this window's queued writes of the property on top, in call order (PR:254 / PR:295)
-    index_queued_sets(w);
+    if (int r = index_queued_sets(w)) return r;
     std::vector<uint32_t> chain;
     for (int32_t i = 0; i < n; i++) {
         auto it = w->ov_last.find(((uint64_t)obj[i] << 7) | (uint32_t)pid[i]);
@@ -2659,18 +2721,28 @@ int nfk_read_added(void* world, int32_t cap, int32_t* n, int64_t* gh, int64_t* g
     World* w = (World*)world;
     if (!w || !n || cap < 0 || (cap && (!gh || !gd || !kind))) return fail(NFK_ERR_ARG, "null argument");
     *n = 0;
-    const size_t np = w->post_obj.size();
-    if (np == 0) return NFK_OK;
-    std::vector<uint8_t> added(np);
+    if (!w->hf_pending) return NFK_OK;
+    // the last pass's post-scan entries (the device fold's): which AddSchedule created a schedule
     HIPCHK(hipStreamSynchronize(w->stream));
-    HIPCHK(hipMemcpy(added.data(), w->added_d, np, hipMemcpyDeviceToHost));
+    uint32_t np = 0;
+    HIPCHK(hipMemcpy(&np, w->hf_npost, 4, hipMemcpyDeviceToHost));
+    np = std::min<uint32_t>(np, (uint32_t)w->hf_max);
+    if (np == 0) return NFK_OK;
+    std::vector<uint32_t> sl(np), kd(np), op(np);
+    std::vector<uint8_t> added(np);
+    HIPCHK(hipMemcpy(sl.data(), w->hf_pslot, np * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(kd.data(), w->hf_pkind, np * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(op.data(), w->hf_pop, np * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(added.data(), w->hf_added, np, hipMemcpyDeviceToHost));
     int32_t k = 0;
-    for (size_t i = 0; i < np; i++) {
-        if (!added[i] || w->post_obj[i] < 0) continue;
+    for (uint32_t i = 0; i < np; i++) {
+        if (!added[i] || !(op[i] & 2u) || sl[i] >= w->obj_of_slot.size()) continue;
+        const int32_t o = w->obj_of_slot[sl[i]];
+        if (o < 0) continue;
         if (k < cap) {
-            gh[k] = w->gh[w->post_obj[i]];
-            gd[k] = w->gd[w->post_obj[i]];
-            kind[k] = (int32_t)w->post_kind[i];
+            gh[k] = w->gh[o];
+            gd[k] = w->gd[o];
+            kind[k] = (int32_t)kd[i];
         }
         k++;
     }
@@ -2872,9 +2944,9 @@ int nfk_spawn_objects(void* world, int32_t n, const int64_t* gh, const int64_t* 
     return import_common(w, n, gh, gd, scene, group, cls, isplayer, rows.data(), hipMemcpyHostToDevice);
 }
 
-int nfk_execute(void* world, int64_t now_ms) {
-    World* w = (World*)world;
-    if (!w) return fail(NFK_ERR_ARG, "null world");
+// one device pass over the window's queued calls; calls_only: nfk_execute_calls (nothing fires,
+// k_tick runs only the tiles with SetProperty groups)
+static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     // a device error of an earlier frame (host-mapped, no device read): that frame's outputs are
     // incomplete, so no further frame runs until nfk_summary_get has reported and cleared it
@@ -2918,7 +2990,8 @@ int nfk_execute(void* world, int64_t now_ms) {
     // queued.  A tile's events are its slots' program destinations plus its standalone groups
     // (properties no program writes); those are bounded here without the slots: at most one per
     // standalone call, and at most one per slot and standalone property the window sets.
-    const size_t n_xq = w->xops.size(), n_hq = w->hops.size();
+    // (the window's SetProperty calls: xq_n on the device queue, then the host's)
+    const size_t n_xdev = w->xq_n, n_xq = n_xdev + w->xops.size(), n_hq = w->hops.size();
     const int64_t max_sa = n_xq ? std::min<int64_t>(w->sa_calls, (int64_t)kTile * (__builtin_popcountll(w->sa_pids[0]) +
                                                                                    __builtin_popcountll(w->sa_pids[1])))
                                 : 0;
@@ -3094,134 +3167,33 @@ int nfk_execute(void* world, int64_t now_ms) {
     }
     const size_t ngr = rs_slot.size(), nrss = rss_slot.size(), nrc = rpk.size();
     tp[2] = clk::now();
-    // schedule calls: pre-scan (remove-list key owner, RemoveSchedule(self)) and post-scan (remove,
-    // add), folded per (slot, kind) in call order (key slot << 5 | kind):
-    //  * RemoveSchedule(self) erases the object's schedules at once (SM:240-243);
-    //  * RemoveSchedule(self, name) inserts into the std::map<NFGUID, name> remove list, so only the
-    //    object's first one in the window owns the key (SM:245-249), and it also blocks the scan's
-    //    own insert (SM:68);
-    //  * remove runs before add at the end of Execute (SM:83-119); AddSchedule keeps an existing
-    //    name, so of several adds of one (object, name) the first wins (SM:108-116).
-    std::vector<uint32_t>& pre_slot = w->pre_slot;
-    std::vector<uint32_t>& pre_op = w->pre_op;
-    using Post = World::Post;
-    std::vector<Post>& post = w->post;
-    pre_slot.clear();
-    pre_op.clear();
-    post.clear();
-    if (n_hq) {
-        std::vector<uint64_t>& hpk = w->hpk;
-        const int hib = bits_for(n_hq);
-        const uint64_t him = (1ull << hib) - 1;
-        // the per-slot folding of hpk[a0, e0) (sorted) into pre-scan and post-scan entries
-        auto fold_range = [&](size_t a0, size_t e0, std::vector<uint32_t>& ps, std::vector<uint32_t>& po,
-                              std::vector<Post>& pq) {
-            for (size_t a = a0; a < e0;) {
-                const uint32_t slot = (uint32_t)((hpk[a] >> hib) >> 5);
-                size_t b = a;
-                uint32_t owner_seq = 0xFFFFFFFFu, owner_kind = 0;
-                bool erase_all = false;
-                for (; b < e0 && (uint32_t)((hpk[b] >> hib) >> 5) == slot; b++) {
-                    const uint32_t seq = (uint32_t)(hpk[b] & him);
-                    const World::HOp& h = w->hops[seq];
-                    if (h.code == 3) erase_all = true;
-                    if (h.code == 2 && seq < owner_seq) {
-                        owner_seq = seq;
-                        owner_kind = h.kind;
-                    }
-                }
-                if (erase_all) {
-                    ps.push_back(slot);
-                    po.push_back(2);
-                }
-                if (owner_seq != 0xFFFFFFFFu) {
-                    ps.push_back(slot);
-                    po.push_back(1);
-                    if (owner_kind == kNoKind) pq.push_back(Post{slot, 0u, 8u, 0.f, 0, 0});  // release the key only
-                }
-                for (size_t c = a; c < b;) {
-                    const uint32_t kind = (uint32_t)((hpk[c] >> hib) & 31);
-                    size_t e = c;
-                    Post p{slot, kind, 0u, 0.f, 0, 0};
-                    if (owner_seq != 0xFFFFFFFFu && owner_kind == kind) p.op |= 1u | 4u;
-                    for (; e < b && (uint32_t)((hpk[e] >> hib) & 31) == kind; e++) {
-                        const World::HOp& h = w->hops[hpk[e] & him];
-                        if (h.code == 1 && !(p.op & 2u)) {
-                            p.op |= 2u;
-                            p.interval = h.interval;
-                            p.count = h.count;
-                            p.time = h.time;
-                        }
-                    }
-                    if (p.op) pq.push_back(p);
-                    c = e;
-                }
-                a = b;
-            }
-        };
-        auto hkey = [&](size_t i) -> uint64_t {
-            const World::HOp& h = w->hops[i];
-            if (i + 16 < n_hq) __builtin_prefetch(&w->slot_of_obj[w->hops[i + 16].slot]);
-            const int32_t sl = w->slot_of_obj[h.slot];
-            if (sl < 0) return ~0ull;
-            return ((uint64_t)(uint32_t)sl << 5) | (h.code == 3 || h.kind == kNoKind ? 0u : h.kind);
-        };
-        if (n_hq >= w->par_calls && w->pool->threads() > 1) {
-            std::vector<size_t> bend;
-            const uint64_t kor = fold_sorted(w, n_hq, hib, 5, hkey, hpk, w->hpk_t, bend);
-            if (bits_for(kor) + hib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued schedule calls"));
-            const int P = (int)bend.size();
-            std::vector<std::vector<uint32_t>> bs(P), bo(P);
-            std::vector<std::vector<Post>> bq(P);
-            w->pool->run(P, [&](int b) { fold_range(b ? bend[b - 1] : 0, bend[b], bs[b], bo[b], bq[b]); });
-            for (int b = 0; b < P; b++) {
-                pre_slot.insert(pre_slot.end(), bs[b].begin(), bs[b].end());
-                pre_op.insert(pre_op.end(), bo[b].begin(), bo[b].end());
-                post.insert(post.end(), bq[b].begin(), bq[b].end());
-            }
-        } else {
-            hpk.resize(n_hq);
-            uint64_t kor = 0;
-            size_t nh = 0;
-            for (size_t i = 0; i < n_hq; i++) {
-                const uint64_t key = hkey(i);
-                if (key == ~0ull) continue;
-                kor |= key;
-                hpk[nh++] = (key << hib) | i;
-            }
-            hpk.resize(nh);
-            if (bits_for(kor) + hib > 64) return drop_window(w, fail(NFK_ERR_CAPACITY, "too many queued schedule calls"));
-            radix_sort_packed(hpk, w->hpk_t, hib, bits_for(kor));
-            fold_range(0, nh, pre_slot, pre_op, post);
-        }
-    }
-
-    // k_post_hostops' entries kind-major, slot order: a mass AddSchedule (server start, a wave of
-    // spawns) then sweeps each kind's schedule records in address order.  The folding emitted them
-    // in (slot, kind) order, so a stable counting sort by kind gives (kind, slot).
-    if (post.size() > 1) {
-        uint32_t cnt[NFK_MAX_KINDS + 1] = {};
-        for (const Post& q : post) cnt[q.kind + 1]++;
-        for (int k = 0; k < NFK_MAX_KINDS; k++) cnt[k + 1] += cnt[k];
-        w->post_t.resize(post.size());
-        for (const Post& q : post) w->post_t[cnt[q.kind]++] = q;
-        post.swap(w->post_t);
-    }
+    // schedule calls: pre-scan entries (remove-list key owner, RemoveSchedule(self)) and post-scan
+    // (slot, kind) entries (remove, add), folded on the device (k_hkeys, radix sort, k_hfold;
+    // nfgpu_kernels.hip states the reference's rules).  Their counts stay on the device: k_pre_hostops
+    // and k_post_hostops read them, nfk_read_added reads them back.
 
     // k_tick runs the programs on the working set fixed at commit (Dev::u_*); a schema whose
     // working set does not fit the register slots runs k_tick_touch
     const bool use_u = w->u_ok && !(d.ablate & kAblPerKind);
+    // a calls-only pass runs k_tick on the tiles with SetProperty groups only (k_xgroups marks them)
+    d.tile_work = nullptr;
+    if (calls_only && use_u && d.n_tiles) {
+        int r = dev_reserve(w, (void**)&w->tile_work_d, &w->tile_work_cap, (size_t)d.n_tiles);
+        if (r) return drop_window(w, r);
+        if (hipMemsetAsync(w->tile_work_d, 0, (size_t)d.n_tiles, w->stream) != hipSuccess)
+            return drop_window(w, fail(NFK_ERR_HIP, "hipMemsetAsync (tile_work)"));
+        d.tile_work = w->tile_work_d;
+    }
 
     tp[3] = clk::now();
     // ---- uploads through the pinned arena ----
     // (the SetProperty calls as queued: (object, property, bits) and the head halves)
-    const size_t ng = n_xq, npre = pre_slot.size(), npost = post.size();
+    // (schedule calls: staged as queued; pre / post entries at most 2 per call, counted on the device)
+    const size_t ng = n_xq, nhq = n_hq, npre = 2 * n_hq, npost = 2 * n_hq;
+    const size_t n_xhost = ng - n_xdev;  // (uploaded; the device queue's calls are there already)
     size_t off_xc = 0;
-    size_t off_ps = align16(off_xc + ng * sizeof(World::XOp)), off_po = align16(off_ps + npre * 4);
-    size_t off_qs = align16(off_po + npre * 4), off_qk = align16(off_qs + npost * 4);
-    size_t off_qo = align16(off_qk + npost * 4), off_qi = align16(off_qo + npost * 4);
-    size_t off_qc = align16(off_qi + npost * 4), off_qt = align16(off_qc + npost * 4);
-    size_t off_rs = align16(off_qt + npost * 8), off_rr = align16(off_rs + ngr * 4);
+    size_t off_hc = align16(off_xc + n_xhost * sizeof(World::XOp));
+    size_t off_rs = align16(off_hc + nhq * sizeof(World::HOp)), off_rr = align16(off_rs + ngr * 4);
     size_t off_rf = align16(off_rr + ngr * 4), off_rb = align16(off_rf + (ngr + 1) * 4);
     size_t off_ss = align16(off_rb + nrc * 8), off_sg = align16(off_ss + nrss * 4);
     const bool objs = w->cfg.n_obj > 0;
@@ -3250,8 +3222,27 @@ int nfk_execute(void* world, int64_t now_ms) {
                                          (uint32_t*)nullptr, ng, 0, xkey_bits, w->stream));
         r = dev_reserve(w, &w->xf_buf, &w->xf_cap, xo_tmp + xf_sort + 256);
         if (r) return drop_window(w, r);
+    }
+    // the schedule-call fold's scratch: keys, sorted keys, indices, sorted indices, per-slot counts
+    // and their scans, pre entries, post entries (slot, kind, op, interval, count, time), added
+    // flags, the sort's temporary storage
+    const int hkey_bits = bits_for((uint64_t)std::max(w->d.cap, 1)) + 6;  // (~0: no slot, sorts last)
+    size_t hf_sort = 0;
+    const size_t hn8 = (nhq * 8 + 255) & ~(size_t)255, hn4 = ((nhq + 1) * 4 + 255) & ~(size_t)255;
+    const size_t hm4 = (npost * 4 + 255) & ~(size_t)255, hm8 = (npost * 8 + 255) & ~(size_t)255;
+    const size_t ho_k1 = 0, ho_k2 = hn8, ho_i1 = 2 * hn8, ho_i2 = ho_i1 + hn4, ho_cp = ho_i2 + hn4, ho_cq = ho_cp + hn4,
+                 ho_op = ho_cq + hn4, ho_oq = ho_op + hn4, ho_ps = ho_oq + hn4, ho_po = ho_ps + hm4,
+                 ho_qs = ho_po + hm4, ho_qk = ho_qs + hm4, ho_qo = ho_qk + hm4, ho_qi = ho_qo + hm4, ho_qc = ho_qi + hm4,
+                 ho_qt = ho_qc + hm4, ho_ad = ho_qt + hm8, ho_tmp = ho_ad + hm4;
+    if (nhq) {
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, hf_sort, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                         (uint32_t*)nullptr, nhq, 0, hkey_bits, w->stream));
+        int r = dev_reserve(w, &w->hf_buf, &w->hf_cap, ho_tmp + hf_sort + 256);
+        if (r) return drop_window(w, r);
+    }
+    if (ng || nhq) {  // object -> slot after the window's membership changes
         if (w->obj_slot_dirty || (size_t)w->n_obj * 4 > w->obj_slot_cap) {
-            r = dev_reserve(w, (void**)&w->obj_slot_d, &w->obj_slot_cap, ((size_t)w->n_obj + 1) * 4);
+            int r = dev_reserve(w, (void**)&w->obj_slot_d, &w->obj_slot_cap, ((size_t)w->n_obj + 1) * 4);
             if (r) return drop_window(w, r);
             HIPCHK(hipMemsetAsync(w->obj_slot_d, 0xFF, (size_t)w->n_obj * 4, w->stream));
             if (d.N > 0)
@@ -3271,18 +3262,15 @@ int nfk_execute(void* world, int64_t now_ms) {
         r = dev_reserve(w, &w->rl_buf, &w->rl_cap, align16(std::max<size_t>(ngr, 1)) + (nrl + n_rev + 1) * 4);
         if (r) return drop_window(w, r);
     }
-    if (total > 0 && (ng || npre || npost || nrss)) {
+    if (total > 0 && (ng || nhq || nrss)) {
         int r = pin_reserve(w, total);
         if (r) return drop_window(w, r);
         char* P = (char*)w->pin;
         if (ng) {
-            memcpy(P + off_xc, w->xops.data(), ng * sizeof(World::XOp));
+            if (n_xhost) memcpy(P + off_xc, w->xops.data(), n_xhost * sizeof(World::XOp));
             if (objs) memcpy(P + off_xh, w->xops_h.data(), ng * 8);
         }
-        for (size_t i = 0; i < npre; i++) {
-            ((uint32_t*)(P + off_ps))[i] = pre_slot[i];
-            ((uint32_t*)(P + off_po))[i] = pre_op[i];
-        }
+        if (nhq) memcpy(P + off_hc, w->hops.data(), nhq * sizeof(World::HOp));
         if (nrss) {
             memcpy(P + off_rs, rs_slot.data(), ngr * 4);
             memcpy(P + off_rr, rs_rrc.data(), ngr * 4);
@@ -3302,14 +3290,6 @@ int nfk_execute(void* world, int64_t now_ms) {
             memcpy(P + off_ca, rc_aux.data(), nrcall * 4);
             memcpy(P + off_cb, rc_bits.data(), nrcall * 8);
             if (nval) memcpy(P + off_rv, w->rvals.data(), nval * 8);
-        }
-        for (size_t i = 0; i < npost; i++) {
-            ((uint32_t*)(P + off_qs))[i] = post[i].slot;
-            ((uint32_t*)(P + off_qk))[i] = post[i].kind;
-            ((uint32_t*)(P + off_qo))[i] = post[i].op;
-            ((float*)(P + off_qi))[i] = post[i].interval;
-            ((int32_t*)(P + off_qc))[i] = post[i].count;
-            ((int64_t*)(P + off_qt))[i] = post[i].time;
         }
         HIPCHK(hipMemcpyAsync(w->stage, w->pin, total, hipMemcpyHostToDevice, w->stream));
         HIPCHK(hipEventRecord(w->pin_done, w->stream));
@@ -3362,6 +3342,7 @@ int nfk_execute(void* world, int64_t now_ms) {
     w->rq_index.clear();
     w->ucache.clear();
     w->xops.clear();
+    w->xq_n = 0;
     w->xops_h.clear();
     w->sa_calls = 0;
     w->sa_pids[0] = w->sa_pids[1] = 0;
@@ -3370,14 +3351,24 @@ int nfk_execute(void* world, int64_t now_ms) {
     w->ov_last.clear();
     w->ov_prev.clear();
 
-    w->post_obj.clear();
-    w->post_kind.clear();
-    for (const Post& q : post) {
-        w->post_obj.push_back((q.op & 2u) ? w->obj_of_slot[q.slot] : -1);
-        w->post_kind.push_back(q.kind);
+    // (schedule calls queued: e_flags may be set by k_pre_hostops; they are 0 wherever it sets none)
+    d.has_pre = nhq > 0;
+    char* HF = (char*)w->hf_buf;
+    HPost hpost{};
+    if (nhq) {
+        hpost = HPost{(uint32_t*)(HF + ho_qs), (uint32_t*)(HF + ho_qk), (uint32_t*)(HF + ho_qo), (float*)(HF + ho_qi),
+                      (int32_t*)(HF + ho_qc), (int64_t*)(HF + ho_qt)};
+        w->hf_pending = true;
+        w->hf_max = npost;
+        w->hf_npost = (const uint32_t*)(HF + ho_oq) + nhq;
+        w->hf_pslot = hpost.slot;
+        w->hf_pkind = hpost.kind;
+        w->hf_pop = hpost.op;
+        w->hf_added = (const uint8_t*)(HF + ho_ad);
+    } else {
+        w->hf_pending = false;
     }
-    d.has_pre = npre > 0;
-    if (ng || npre || nrss) {
+    if (ng || nhq || nrss) {
         TimeScope ts(w, KT_AUX);
         if (nrss) {
             hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)((nrss + 255) / 256)), dim3(256), 0, w->stream,
@@ -3390,7 +3381,16 @@ int nfk_execute(void* world, int64_t now_ms) {
         if (ng) {
             // the device fold: keys (slot << 7 | property) -> stable radix sort -> groups
             const unsigned gx = (unsigned)((ng + 255) / 256);
+            // the calls in call order: the device queue's, then the host's appended to it
             const XCall* xc = (const XCall*)(S + off_xc);
+            if (n_xdev) {
+                if (int r = xq_reserve_exec(w, ng)) return drop_window(w, r);
+                World::XOp* q = (World::XOp*)w->xq[w->xq_b];
+                if (n_xhost)
+                    HIPCHK(hipMemcpyAsync(q + n_xdev, S + off_xc, n_xhost * sizeof(World::XOp), hipMemcpyDeviceToDevice,
+                                          w->stream));
+                xc = (const XCall*)q;
+            }
             uint64_t* k1 = (uint64_t*)(XF + xo_k1);
             uint64_t* k2 = (uint64_t*)(XF + xo_k2);
             uint32_t* i1 = (uint32_t*)(XF + xo_i1);
@@ -3404,13 +3404,45 @@ int nfk_execute(void* world, int64_t now_ms) {
             hipLaunchKernelGGL(k_xgroups, dim3(gx), dim3(256), 0, w->stream, (const uint64_t*)k2, (const uint32_t*)i2,
                                (const uint32_t*)gi, xc, objs ? (const uint64_t*)(S + off_xh) : nullptr, (int32_t)ng,
                                (uint32_t*)d.x_slot, (uint32_t*)d.x_pid, (uint32_t*)d.x_first, (uint64_t*)d.x_bits,
-                               (uint64_t*)d.x_bits_h, d.ext_head);
+                               (uint64_t*)d.x_bits_h, d.ext_head, (uint8_t*)d.tile_work);
+            if (n_xdev) {  // the buffer is free again once the fold has read it; the next window takes the other
+                const int b = w->xq_b;
+                if (!w->xq_ev[b]) HIPCHK(hipEventCreateWithFlags(&w->xq_ev[b], hipEventDisableTiming));
+                HIPCHK(hipEventRecord(w->xq_ev[b], w->stream));
+                w->xq_ev_set[b] = true;
+                w->xq_b ^= 1;
+            }
             hipLaunchKernelGGL(k_sets, dim3((unsigned)((ng + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, d);
         }
-        if (npre)
+        if (nhq) {
+            // the device fold of the schedule calls: keys -> stable radix sort -> per-slot counts ->
+            // scans -> pre / post entries; then the pre-scan effects
+            const unsigned gh_ = (unsigned)((nhq + 255) / 256);
+            const HCall* hc = (const HCall*)(S + off_hc);
+            uint64_t* k1 = (uint64_t*)(HF + ho_k1);
+            uint64_t* k2 = (uint64_t*)(HF + ho_k2);
+            uint32_t* i1 = (uint32_t*)(HF + ho_i1);
+            uint32_t* i2 = (uint32_t*)(HF + ho_i2);
+            uint32_t* cp = (uint32_t*)(HF + ho_cp);
+            uint32_t* cq = (uint32_t*)(HF + ho_cq);
+            uint32_t* op = (uint32_t*)(HF + ho_op);
+            uint32_t* oq = (uint32_t*)(HF + ho_oq);
+            uint32_t* ps = (uint32_t*)(HF + ho_ps);
+            uint32_t* po = (uint32_t*)(HF + ho_po);
+            hipLaunchKernelGGL(k_hkeys, dim3(gh_), dim3(256), 0, w->stream, hc, (int32_t)nhq,
+                               (const int32_t*)w->obj_slot_d, k1, i1);
+            size_t sb = hf_sort;
+            HIPCHK(rocprim::radix_sort_pairs(HF + ho_tmp, sb, k1, k2, i1, i2, nhq, 0, hkey_bits, w->stream));
+            hipLaunchKernelGGL(k_hfold<false>, dim3(gh_), dim3(256), 0, w->stream, (const uint64_t*)k2, (const uint32_t*)i2,
+                               hc, (int32_t)nhq, cp, cq, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ps, po, hpost);
+            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, w->stream, (const uint32_t*)cp, op, (int)nhq);
+            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, w->stream, (const uint32_t*)cq, oq, (int)nhq);
+            hipLaunchKernelGGL(k_hfold<true>, dim3(gh_), dim3(256), 0, w->stream, (const uint64_t*)k2, (const uint32_t*)i2,
+                               hc, (int32_t)nhq, cp, cq, (const uint32_t*)op, (const uint32_t*)oq, ps, po, hpost);
             hipLaunchKernelGGL(k_pre_hostops, dim3((unsigned)((npre + 255) / 256)), dim3(256), 0, w->stream,
-                               (const uint32_t*)(S + off_ps), (const uint32_t*)(S + off_po), (int32_t)npre,
-                               d.e_flags, d.s_hot, d.n_kind, d.s_kstr);
+                               (const uint32_t*)ps, (const uint32_t*)po, (int32_t)npre, d.e_flags, d.s_hot, d.n_kind,
+                               d.s_kstr, (const uint32_t*)op + nhq);
+        }
         HIPCHK(hipGetLastError());
     }
     // k_tick writes its tiles' fan-out itself (its LDS image is reused for the events): property
@@ -3522,15 +3554,12 @@ int nfk_execute(void* world, int64_t now_ms) {
             hipLaunchKernelGGL((k_rset_slots<true>), dim3((unsigned)((nrss + kWpb - 1) / kWpb)), b, 0, w->stream, d);
         HIPCHK(hipGetLastError());
     }
-    if (npost) {
+    if (nhq) {  // the post-scan entries (their count is the fold's, on the device)
         TimeScope ts(w, KT_AUX);
-        int r = dev_reserve(w, (void**)&w->added_d, &w->added_cap, npost);
-        if (r) return r;
         hipLaunchKernelGGL(k_post_hostops, dim3((unsigned)((npost + 255) / 256)), dim3(256), 0, w->stream,
-                           (const uint32_t*)(S + off_qs), (const uint32_t*)(S + off_qk),
-                           (const uint32_t*)(S + off_qo), (const float*)(S + off_qi),
-                           (const int32_t*)(S + off_qc), (const int64_t*)(S + off_qt), (int32_t)npost,
-                           w->added_d, d);
+                           (const uint32_t*)hpost.slot, (const uint32_t*)hpost.kind, (const uint32_t*)hpost.op,
+                           (const float*)hpost.interval, (const int32_t*)hpost.count, (const int64_t*)hpost.time,
+                           (int32_t)npost, (uint8_t*)(HF + ho_ad), d, w->hf_npost);
         HIPCHK(hipGetLastError());
     }
     // Dense global ranks of the tile-staged outputs (ev_base, fi_base, totals): the frame's own
@@ -3571,10 +3600,19 @@ int nfk_execute(void* world, int64_t now_ms) {
     return NFK_OK;
 }
 
+int nfk_execute(void* world, int64_t now_ms) {
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    return execute_frame(w, now_ms, false);
+}
+
 int nfk_execute_calls(void* world) {
     // a frame at the earliest time: `now > next` holds for no schedule, so nothing fires and no
-    // record is rescheduled; the queued calls run through the ordinary frame path
-    return nfk_execute(world, INT64_MIN);
+    // record is rescheduled; the queued calls run through the ordinary frame path, k_tick only on
+    // the tiles their SetProperty groups touch
+    World* w = (World*)world;
+    if (!w) return fail(NFK_ERR_ARG, "null world");
+    return execute_frame(w, INT64_MIN, true);
 }
 
 int nfk_sync(void* world) {

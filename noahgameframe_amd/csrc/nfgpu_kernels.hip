@@ -74,6 +74,32 @@ __global__ void k_guid_patch(GuidEntry* __restrict__ t, const uint32_t* __restri
     if (i < n) t[idx[i]] = e[i];
 }
 
+// A batch of SetProperty* calls queued on the device (nfgpu_host.hip set_props_dev): each call's
+// object looked up, the call written at its place in the window's device queue q; miss = the first
+// call whose NFGUID is no object (the batch is then not queued: "There is no object", KM:331).
+// b = [n] heads, [n] data halves, [n] values; pid = [n] property ids (checked on the host)
+__global__ void k_guid_queue(const GuidEntry* __restrict__ t, uint64_t mask, const int64_t* __restrict__ b,
+                             const int32_t* __restrict__ pid, int32_t n, XCall* __restrict__ q,
+                             int32_t* __restrict__ miss) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t h = b[i], dd = b[(size_t)n + i];
+    int32_t r = -1;
+    for (uint64_t s = guid_home(h, dd, mask);; s = (s + 1) & mask) {
+        const GuidEntry e = t[s];
+        if (e.v < 0) break;
+        if (e.h == h && e.d == dd) {
+            r = e.v;
+            break;
+        }
+    }
+    if (r < 0) {
+        atomicMin(miss, i);
+        return;
+    }
+    q[i] = XCall{(uint32_t)r, (uint32_t)pid[i], (uint64_t)b[2 * (size_t)n + i]};
+}
+
 // obj_slot[o] = the slot object o holds (entries start at -1); slack slots are skipped
 __global__ void k_obj_slots(const int32_t* __restrict__ slot_obj, const uint64_t* __restrict__ fan_desc, int32_t n,
                             int32_t* __restrict__ obj_slot) {
@@ -126,7 +152,7 @@ __global__ void k_xgroups(const uint64_t* __restrict__ keys, const uint32_t* __r
                           const uint32_t* __restrict__ gidx, const XCall* __restrict__ x,
                           const uint64_t* __restrict__ x_h, int32_t n, uint32_t* __restrict__ x_slot,
                           uint32_t* __restrict__ x_pid, uint32_t* __restrict__ x_first, uint64_t* __restrict__ x_bits,
-                          uint64_t* __restrict__ x_bits_h, uint32_t* __restrict__ ext_head) {
+                          uint64_t* __restrict__ x_bits_h, uint32_t* __restrict__ ext_head, uint8_t* __restrict__ tile_work) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t k = keys[i];
@@ -141,7 +167,10 @@ __global__ void k_xgroups(const uint64_t* __restrict__ keys, const uint32_t* __r
         x_slot[g] = sl;
         x_pid[g] = (uint32_t)(k & 127);
         x_first[g] = (uint32_t)i;
-        if (i == 0 || (uint32_t)(kp >> 7) != sl) ext_head[sl] = g + 1;
+        if (i == 0 || (uint32_t)(kp >> 7) != sl) {
+            ext_head[sl] = g + 1;
+            if (tile_work) tile_work[sl / kTile] = 1;
+        }
     }
     if (i + 1 == n || keys[i + 1] == ~0ull) x_first[gidx[n]] = (uint32_t)i + 1;  // the last group's end
 }
@@ -194,12 +223,127 @@ __global__ __launch_bounds__(kTPB) void k_sets(Dev d) {
 }
 
 
-// op: 1 = RemoveSchedule(self, name) queued (owns the remove-list key), 2 = RemoveSchedule(self)
-__global__ void k_pre_hostops(const uint32_t* __restrict__ slot, const uint32_t* __restrict__ op, int32_t n,
-                              uint8_t* __restrict__ e_flags, SchedHot* __restrict__ s_hot, int32_t n_kind,
-                              int32_t kstr) {
+// ---------------------------------------------------------------------------------
+// The window's schedule calls (AddSchedule / RemoveSchedule(self, name) / RemoveSchedule(self),
+// SM:218-251) folded on the device into the pre-scan entries (k_pre_hostops) and the post-scan
+// (slot, kind) entries (k_post_hostops), as NFCScheduleModule::Execute applies them:
+//  * RemoveSchedule(self) erases the object's schedules at once (SM:240-243);
+//  * RemoveSchedule(self, name) inserts into the std::map<NFGUID, name> remove list, so only the
+//    object's first one in the window owns the key (SM:245-249), and it also blocks the scan's own
+//    insert (SM:68);
+//  * remove runs before add at the end of Execute (SM:83-119); AddSchedule keeps an existing name,
+//    so of several adds of one (object, name) the first wins (SM:108-116).
+// Keys slot << 5 | kind (kind 0 for RemoveSchedule(self) and a name without a device program), a
+// stable radix sort (call order within a key), then one thread per slot walks its calls.
+constexpr uint32_t kHNoKind = 0xFFFFFFFFu;  // a RemoveSchedule(self, name) of a name with no device program
+struct HCall {  // (World::HOp's layout)
+    int32_t code;
+    uint32_t obj, kind;
+    float interval;
+    int32_t count;
+    int64_t time;
+};
+// the schedule calls' post-scan entries (k_post_hostops): one array per field
+struct HPost {
+    uint32_t *slot, *kind, *op;
+    float* interval;
+    int32_t* count;
+    int64_t* time;
+};
+__global__ void k_hkeys(const HCall* __restrict__ h, int32_t n, const int32_t* __restrict__ obj_slot,
+                        uint64_t* __restrict__ keys, uint32_t* __restrict__ idx) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const HCall c = h[i];
+    const int32_t sl = obj_slot[c.obj];
+    keys[i] = sl < 0 ? ~0ull : (((uint64_t)(uint32_t)sl << 5) | (c.code == 3 || c.kind == kHNoKind ? 0u : c.kind));
+    idx[i] = (uint32_t)i;
+}
+// the slot whose calls start at sorted position i (else none): its pre and post entries counted
+// (kEmit = false, into npre / npost at i) or written at the scanned positions opre[i] / opost[i]
+template <bool kEmit>
+__global__ void k_hfold(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ idx,
+                        const HCall* __restrict__ h, int32_t n, uint32_t* __restrict__ npre,
+                        uint32_t* __restrict__ npost, const uint32_t* __restrict__ opre,
+                        const uint32_t* __restrict__ opost, uint32_t* __restrict__ pre_slot,
+                        uint32_t* __restrict__ pre_op, HPost post) {
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= n) return;
+    const uint64_t ka = keys[a];
+    const uint32_t slot = (uint32_t)(ka >> 5);
+    if (ka == ~0ull || (a > 0 && (uint32_t)(keys[a - 1] >> 5) == slot && keys[a - 1] != ~0ull)) {
+        if (!kEmit) npre[a] = npost[a] = 0;
+        return;
+    }
+    int b = a;
+    uint32_t owner_seq = 0xFFFFFFFFu, owner_kind = 0;
+    bool erase_all = false;
+    for (; b < n && keys[b] != ~0ull && (uint32_t)(keys[b] >> 5) == slot; b++) {
+        const uint32_t seq = idx[b];
+        const HCall& c = h[seq];
+        if (c.code == 3) erase_all = true;
+        if (c.code == 2 && seq < owner_seq) {
+            owner_seq = seq;
+            owner_kind = c.kind;
+        }
+    }
+    uint32_t np = 0, nq = 0;
+    const uint32_t p0 = kEmit ? opre[a] : 0u, q0 = kEmit ? opost[a] : 0u;
+    auto put_pre = [&](uint32_t op) {
+        if (kEmit) {
+            pre_slot[p0 + np] = slot;
+            pre_op[p0 + np] = op;
+        }
+        np++;
+    };
+    auto put_post = [&](uint32_t kind, uint32_t op, float iv, int32_t cnt, int64_t t) {
+        if (kEmit) {
+            post.slot[q0 + nq] = slot;
+            post.kind[q0 + nq] = kind;
+            post.op[q0 + nq] = op;
+            post.interval[q0 + nq] = iv;
+            post.count[q0 + nq] = cnt;
+            post.time[q0 + nq] = t;
+        }
+        nq++;
+    };
+    if (erase_all) put_pre(2);
+    if (owner_seq != 0xFFFFFFFFu) {
+        put_pre(1);
+        if (owner_kind == kHNoKind) put_post(0, 8, 0.f, 0, 0);  // release the key only
+    }
+    for (int c = a; c < b;) {
+        const uint32_t kind = (uint32_t)(keys[c] & 31);
+        uint32_t op = (owner_seq != 0xFFFFFFFFu && owner_kind == kind) ? 1u | 4u : 0u;
+        float iv = 0.f;
+        int32_t cnt = 0;
+        int64_t t = 0;
+        int e = c;
+        for (; e < b && (uint32_t)(keys[e] & 31) == kind; e++) {
+            const HCall& x = h[idx[e]];
+            if (x.code == 1 && !(op & 2u)) {
+                op |= 2u;
+                iv = x.interval;
+                cnt = x.count;
+                t = x.time;
+            }
+        }
+        if (op) put_post(kind, op, iv, cnt, t);
+        c = e;
+    }
+    if (!kEmit) {
+        npre[a] = np;
+        npost[a] = nq;
+    }
+}
+
+// op: 1 = RemoveSchedule(self, name) queued (owns the remove-list key), 2 = RemoveSchedule(self);
+// n_dev: the entry count on the device (the device fold's), else n
+__global__ void k_pre_hostops(const uint32_t* __restrict__ slot, const uint32_t* __restrict__ op, int32_t n,
+                              uint8_t* __restrict__ e_flags, SchedHot* __restrict__ s_hot, int32_t n_kind,
+                              int32_t kstr, const uint32_t* __restrict__ n_dev) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || (n_dev && (uint32_t)i >= *n_dev)) return;
     const uint32_t s = slot[i];
     if (op[i] == 1) e_flags[s] |= 1;
     if (op[i] == 2)
@@ -211,9 +355,9 @@ __global__ void k_pre_hostops(const uint32_t* __restrict__ slot, const uint32_t*
 __global__ void k_post_hostops(const uint32_t* __restrict__ slot, const uint32_t* __restrict__ kind,
                                const uint32_t* __restrict__ op, const float* __restrict__ interval,
                                const int32_t* __restrict__ count, const int64_t* __restrict__ time, int32_t n,
-                               uint8_t* __restrict__ added, Dev d) {
+                               uint8_t* __restrict__ added, Dev d, const uint32_t* __restrict__ n_dev) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i >= n || (n_dev && (uint32_t)i >= *n_dev)) return;
     const uint32_t s = slot[i];
     if (op[i] & 8) {
         d.e_flags[s] = 0;

@@ -162,7 +162,10 @@ struct DynSchema {
 
 constexpr int kKindChunk = 8;  // schedule hot records loaded together per chunk
 // non-temporal hint bits of a schema policy's kNt (NFGPU_JIT_NT for the hipRTC specialisation)
-constexpr uint32_t kNtSchedLoad = 1, kNtColLoad = 2, kNtEventStore = 4, kNtStateStore = 8, kNtFanStore = 16;
+// kNtFanStore: the fan-out's LDS-window stores (16-byte aligned runs); kNtFanGroupStore: its lane-group
+// stores (runs of 16 or more recipients, 16-byte stores at any dword)
+constexpr uint32_t kNtSchedLoad = 1, kNtColLoad = 2, kNtEventStore = 4, kNtStateStore = 8, kNtFanStore = 16,
+                   kNtFanGroupStore = 32;
 
 // k_tick register budgets (waves per SIMD) by the frame's U slot count
 constexpr int kWavesU8 = 8, kWavesU12 = 7;
@@ -264,6 +267,15 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
     const int tile = blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
+    if (d.tile_work && !d.tile_work[tile]) {  // (block-uniform) a calls-only pass, no Set group here:
+        if (d.has_recops && e < d.N) d.fired_mask[e] = 0;  // nothing fires, nothing is dirty
+        if (threadIdx.x == 0) {
+            d.t_ev[tile] = 0;
+            d.t_fi[tile] = 0;
+            d.t_msg[tile] = 0;
+        }
+        return;
+    }
     const bool fuse = d.msg_tcap != 0;  // this tile's fan-out is written here, at tile * msg_tcap
     if (threadIdx.x == 0) {
         s_bytes = 0;
@@ -622,7 +634,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                                 x[q] = pq < n ? (staged ? s_pl[a - pb_lo + pp] : (uint32_t)d.pl_slot[a + pp]) : 0u;
                             }
                             if (p + 4 <= n) {
-                                if constexpr ((S::kNt & kNtFanStore) != 0)
+                                if constexpr ((S::kNt & kNtFanGroupStore) != 0)
                                     __builtin_nontemporal_store(u32x4_a4{x[0], x[1], x[2], x[3]}, (u32x4_a4*)(out + ms + p));
                                 else
                                     *(u32x4_a4*)(out + ms + p) = u32x4_a4{x[0], x[1], x[2], x[3]};

@@ -76,13 +76,13 @@ def load_library(path=LIB_PATH):
         "nfk_define_kind": [VP, I32, VP, I32],
         "nfk_create_objects": [VP, I32, VP, VP, VP, VP, VP, VP], "nfk_load_prop": [VP, I32, VP],
         "nfk_load_record": [VP, I32, VP, VP], "nfk_commit": [VP],
-        "nfk_set_props": [VP, I32, VP, VP, VP, VP], "nfk_set_records": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
+        "nfk_set_props": [VP, I32, VP, VP, VP, VP], "nfk_set_props_obj": [VP, I32, VP, VP, VP], "nfk_set_records": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
         "nfk_get_records": [VP, I32, VP, VP, VP, VP, VP, VP],
         "nfk_add_schedules": [VP, I32, VP, VP, VP, VP, VP, VP],
         "nfk_remove_schedule": [VP, I64, I64, I32], "nfk_remove_all_schedules": [VP, I64, I64],
-        "nfk_schedule_calls": [VP, I32, VP, VP, VP, VP, VP, VP, VP],
+        "nfk_schedule_calls": [VP, I32, VP, VP, VP, VP, VP, VP, VP], "nfk_schedule_calls_obj": [VP, I32, VP, VP, VP, VP, VP, VP],
         "nfk_get_props": [VP, I32, VP, VP, VP, VP], "nfk_exist_schedule": [VP, I64, I64, I32, VP],
-        "nfk_execute": [VP, I64], "nfk_summary_get": [VP, P(Summary)], "nfk_outputs_get": [VP, P(Outputs)],
+        "nfk_execute": [VP, I64], "nfk_execute_calls": [VP], "nfk_summary_get": [VP, P(Summary)], "nfk_outputs_get": [VP, P(Outputs)],
         "nfk_read_prop": [VP, I32, VP], "nfk_read_record": [VP, I32, VP], "nfk_read_schedules": [VP, VP, VP, VP],
         "nfk_read_events": [VP, VP, VP, VP, VP], "nfk_read_rec_events": [VP, VP, VP, VP, VP],
         "nfk_read_fired": [VP, VP, VP, VP], "nfk_read_fanout": [VP, VP, VP],
@@ -196,6 +196,11 @@ class NFKernelModule:
              ((guid_head, np.int64), (guid_data, np.int64), (pid, np.int32), (bits, np.uint64))]
         self._chk(self.lib.nfk_set_props(self.h, len(a[0]), *[_p(x) for x in a]))
 
+    def set_props_obj(self, obj, pid, bits):
+        """nfk_set_props_obj: the same calls by nfk object index (creation order; the outputs' ev_obj)."""
+        a = [np.ascontiguousarray(x, t) for x, t in ((obj, np.int32), (pid, np.int32), (bits, np.uint64))]
+        self._chk(self.lib.nfk_set_props_obj(self.h, len(a[0]), *[_p(x) for x in a]))
+
     # ---- NFIKernelModule::SetPropertyObject / GetPropertyObject (KM:362 / KM:440) ----
     def set_objects(self, guid_head, guid_data, pid, val_head, val_data):
         a = [np.ascontiguousarray(x, t) for x, t in
@@ -299,6 +304,13 @@ class NFKernelModule:
               (interval_s, np.float32), (count, np.int32), (now_ms, np.int64))]
         self._chk(self.lib.nfk_schedule_calls(self.h, len(a[0]), *[_p(x) for x in a]))
 
+    def schedule_calls_obj(self, op, obj, kind, interval_s, count, now_ms):
+        """nfk_schedule_calls_obj: schedule_calls by nfk object index."""
+        a = [np.ascontiguousarray(x, t) for x, t in
+             ((op, np.int32), (obj, np.int32), (kind, np.int32), (interval_s, np.float32), (count, np.int32),
+              (now_ms, np.int64))]
+        self._chk(self.lib.nfk_schedule_calls_obj(self.h, len(a[0]), *[_p(x) for x in a]))
+
     def RemoveSchedule(self, guid, name=None):
         if name is None:
             self._chk(self.lib.nfk_remove_all_schedules(self.h, int(guid[0]), int(guid[1])))
@@ -386,6 +398,12 @@ class NFKernelModule:
     # ---- one frame ----
     def Execute(self, now_ms):
         self._chk(self.lib.nfk_execute(self.h, int(now_ms)))
+        return True
+
+    def ExecuteCalls(self):
+        """nfk_execute_calls: the queued calls applied in a pass where nothing fires (what heartbeat
+        functors call inside NFCScheduleModule::Execute's walk, SM:65, SM:83-119)."""
+        self._chk(self.lib.nfk_execute_calls(self.h))
         return True
 
     def synchronize(self):
@@ -620,5 +638,9 @@ def run_workload(m, w, tick, collect=True):
         dead = w["d_obj"][w["d_tick"] == tick]
         if len(dead):
             m.destroy_objects(gh[dead], gd[dead])
-    m.Execute(int(w["tick_time"][tick]))
+    now = int(w["tick_time"][tick])
+    if now == np.iinfo(np.int64).min:  # a calls-only pass (nfk_execute_calls: nothing fires)
+        m.ExecuteCalls()
+    else:
+        m.Execute(now)
     return m.read_tick() if collect else None

@@ -108,26 +108,42 @@ def test_gpu_matches_oracle(gpu_available, monkeypatch, case, path):
 
 @pytest.mark.parametrize("case", ["combined", "wide_sets", "lifecycle", "sched_edges", "record_rows"])
 def test_parallel_call_folding_matches_oracle(gpu_available, monkeypatch, case):
-    """The host pool's share of a window's calls (GUID lookups split over threads, the (slot, kind)
-    fold of schedule calls by slot range, nfgpu_host.hip fold_sorted) — with NFGPU_HOST_THREADS > 1
-    used from 16384 calls per batch on — forced on every batch here (NFGPU_PAR_CALLS=8), 4 and 7
-    host threads."""
+    """The host pool's share of a window's calls (GUID lookups of a batch split over threads; with
+    NFGPU_HOST_THREADS > 1 used from 16384 calls per batch on) forced on every batch here
+    (NFGPU_PAR_CALLS=8, device lookups off), 4 and 7 host threads."""
     for threads in ("4", "7"):
         monkeypatch.setenv("NFGPU_PAR_CALLS", "8")
+        monkeypatch.setenv("NFGPU_DEV_LOOKUP", "0")
         monkeypatch.setenv("NFGPU_HOST_THREADS", threads)
         w = workload.make_world(n_ticks=10, seed=sum(map(ord, case)), **CASES[case])
         compare_runs(run_gpu(w), run_oracle(w))
 
 
 @pytest.mark.parametrize("case", ["combined", "wide_sets", "lifecycle", "lifecycle_records", "switch_scene", "sched_edges",
-                                  "record_rows", "objects"])
+                                  "record_rows", "objects", "read_modify_write", "wide_sets_records"])
 def test_device_guid_lookups_match_oracle(gpu_available, monkeypatch, case):
     """GUID -> object lookups of a call batch on the device mirror of the host's NFGUID table
     (nfgpu_host.hip find_many_dev; k_guid_find, k_guid_patch) — used from 4096 calls per batch on —
     forced on every batch (NFGPU_DEV_LOOKUP=1), through creates, destroys and scene switches that
-    rewrite the table between batches."""
+    rewrite the table between batches.  In worlds without object properties the SetProperty batches
+    are queued on the device too (set_props_dev, k_guid_queue), behind and in front of host-queued
+    calls (SwitchScene writes, single calls), and read back for GetProperty's overlay
+    (read_modify_write)."""
     monkeypatch.setenv("NFGPU_DEV_LOOKUP", "1")
     w = workload.make_world(n_ticks=10, seed=sum(map(ord, case)), **CASES[case])
+    compare_runs(run_gpu(w), run_oracle(w))
+
+
+@pytest.mark.parametrize("case", ["combined", "wide_sets", "lifecycle", "objects", "record_sets"])
+def test_calls_only_passes_match_oracle(gpu_available, case):
+    """nfk_execute_calls — the plugin's same-frame pass for what heartbeat functors call — is a frame
+    at the earliest time (nothing fires, SM:51-81 never passes `now > next`) in which k_tick runs only
+    the tiles with SetProperty groups (Dev::tile_work); the other tiles write empty outputs.  Frames
+    2 and 5 here are such passes; the oracle runs them as frames at INT64_MIN."""
+    w = workload.make_world(n_ticks=8, seed=sum(map(ord, case)) + 7, **CASES[case])
+    tt = np.asarray(w["tick_time"]).copy()
+    tt[[2, 5]] = np.iinfo(np.int64).min
+    w["tick_time"] = tt
     compare_runs(run_gpu(w), run_oracle(w))
 
 
