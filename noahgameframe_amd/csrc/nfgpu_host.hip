@@ -979,9 +979,10 @@ int tick_waves(int n_u, uint32_t ablate) {
 }
 
 // the non-temporal hints the specialised k_tick is built with (A/B: NFGPU_JIT_NT): the schedule
-// records / descriptor loads and the fan-out's recipient stores stream past the caches (config[1]:
-// 90 vs 115 us with none, 102 with the fan-out stores alone; event-array stores non-temporal run
-// 160 us; profiles/r07a_ntab.txt)
+// records / descriptor loads and the fan-out's LDS-window recipient stores stream past the caches
+// (config[1]: 90 vs 115 us with none, 102 with the fan-out stores alone; event-array stores
+// non-temporal run 160 us; profiles/r07a_ntab.txt).  Not the lane-group recipient stores
+// (kNtFanGroupStore: config[3] 377 vs 415 us, config[4] 94 vs 107 us; profiles/r08i_*)
 constexpr uint32_t kJitNtDefault = kNtSchedLoad | kNtFanStore;
 
 // Specialised k_tick kernels built in this process, by (device, variant, policy source): a
