@@ -57,7 +57,7 @@ def parse():
     p.add_argument("--players-per-group", type=int, default=8)
     p.add_argument("--tick-ms", type=int, default=100)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    p.add_argument("--cpu-sample", type=int, default=32768, help="entities in the CPU baseline sample")
+    p.add_argument("--cpu-sample", type=int, default=4096, help="entities in the CPU baseline sample (whole groups)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--migrate", type=int, default=256,
@@ -84,50 +84,56 @@ def parse():
 
 
 def cpu_baseline(args):
-    """The reference's own classes (oracle/_ref/nf_ref_harness: NFCProperty / NFCRecord /
-    NFCScheduleModule compiled from the reference sources, per-Set GetBroadCastObject lists) on a
-    bounded sample of the same workload, one host core."""
+    """The reference's own frame on one host core: oracle/_ref/nf_ref_session runs the reference's
+    NFCKernelModule, NFCScheduleModule, NFCSceneAOIModule, NFCEventModule and NFCClassModule
+    (compiled from the reference sources where they lie) with the workload's heartbeat programs as
+    functors calling NFIKernelModule::Get/SetProperty*, the window's Set / schedule calls, and a
+    property-event consumer on the AOI module's recipient lists — on a bounded sample of the same
+    workload: whole scene groups of the config's shape, fewer of them."""
     from noahgameframe_amd import nfio, workload
-    exe = os.path.join(ROOT, "oracle", "_ref", "nf_ref_harness")
+    exe = os.path.join(ROOT, "oracle", "_ref", "nf_ref_session")
     if not os.path.exists(exe):
         return None
     ticks = 400
     if args.config == 0:
-        n = 10_000
+        # (the reference's CreateObject of n objects into one group costs O(n^2) in the AOI module's
+        # enter broadcasts: 10k objects take minutes to set up, so a smaller group)
+        n = 4000
         w = workload.tutorial3_world(n_obj=n, n_ticks=ticks * 2, tick_ms=args.tick_ms)
-        what = f"the full config[0] workload ({n} NPC objects)"
+        what = f"config[0]'s workload at {n} NPC objects (one group)"
     elif args.config == 3:
-        n = 32768  # 4 scenes x 64 groups of 128, 32 players per group
-        w = workload.fanout_world(n_ticks=ticks, n_obj=n, scenes=4, groups=64, players_per_group=32)
-        what = f"{n} entities (4 scenes x 64 groups x 128, 32 players/group)"
+        n = 4096  # 1 scene x 32 groups of 128, 32 players per group (config[3]'s group shape)
+        w = workload.fanout_world(n_ticks=ticks, n_obj=n, scenes=1, groups=32, players_per_group=32)
+        what = f"{n} entities (1 scene x 32 groups x 128, 32 players/group: config[3]'s groups)"
     elif args.config == 4:
-        n = 4096  # 64-row skill records; the int cooldown column only (see below)
-        w = workload.record_world(n_ticks=ticks, n_obj=n, groups=256, steady=True, rec_float_op=False)
+        n = 1024  # 64-row skill records; the int cooldown column only (see below)
+        w = workload.record_world(n_ticks=ticks, n_obj=n, groups=64, steady=True, rec_float_op=False)
         what = (f"{n} players (groups of 16) x 64-row records, the int cooldown column op only: the reference's "
                 "NFCRecord::SetFloat stores an int64 variant and cannot run the f64 charge op "
                 "(tests/test_oracle.py::test_reference_record_setfloat_bug)")
     else:
-        n = min(args.cpu_sample, args.entities)
-        groups = max(1, n * args.groups // args.entities)
+        per_group = max(1, args.entities // max(args.groups, 1))
+        groups = max(1, min(args.cpu_sample, args.entities) // per_group)
+        n = groups * per_group
         w = workload.bench_world(n_obj=n, groups=groups, players_per_group=args.players_per_group, n_ticks=ticks,
                                  tick_ms=args.tick_ms, seed=2026)
-        what = f"{n} entities ({groups} groups x {n // groups}, {args.players_per_group} players/group)"
-    from noahgameframe_amd import nfio
+        what = f"{n} entities ({groups} groups x {per_group}, {args.players_per_group} players/group: config[1]'s groups)"
     with tempfile.TemporaryDirectory() as d:
         wp = os.path.join(d, "w.nfio")
         nfio.write(wp, w)
-        # calibrate: a short run, then a run sized to ~cpu_seconds of frame work
-        r = json.loads(subprocess.run([exe, "--bench", wp, "4"], check=True, capture_output=True,
-                                      text=True).stdout)
-        per_tick = r["seconds"] / max(r["ticks"], 1)
-        t = int(min(int(w["cfg"][7]), max(4, args.cpu_seconds / max(per_tick, 1e-6))))
-        r = json.loads(subprocess.run([exe, "--bench", wp, str(t)], check=True, capture_output=True,
-                                      text=True).stdout)
+        # calibrate: one untimed and one timed frame, then a run sized to ~cpu_seconds of frame work
+        r = json.loads(subprocess.run([exe, wp, "2", "1"], check=True, capture_output=True,
+                                      text=True).stdout.strip().splitlines()[-1])
+        per_tick = r["seconds"] / max(r["frames"], 1)
+        t = int(min(int(w["cfg"][7]) - 1, max(2, args.cpu_seconds / max(per_tick, 1e-6))))
+        r = json.loads(subprocess.run([exe, wp, str(t + 1), "1"], check=True, capture_output=True,
+                                      text=True).stdout.strip().splitlines()[-1])
     return {"value": r["entity_ticks_per_s"], "unit": "entity-ticks/s", "cores": 1, "kind": "reference",
-            "sample": f"{what}, {r['ticks']} frames of the same workload through the reference's "
-                      f"NFCPropertyManager/NFCProperty/NFCRecord + NFCScheduleModule + per-Set GetBroadCastObject "
-                      f"lists (GetGroupObjectList over the group's player and other maps, KM:1270), "
-                      f"single thread, {r['seconds']:.1f} s"}
+            "sample": f"{what}; {r['frames']} frames after one untimed frame through the reference's own "
+                      f"NFCKernelModule + NFCScheduleModule + NFCSceneAOIModule (heartbeat functors calling "
+                      f"NFIKernelModule::Get/SetProperty*, the window's SetProperty and schedule calls, a "
+                      f"property-event consumer on the AOI module's GetBroadCastObject lists: {r['msgs']} "
+                      f"recipients), single thread, {r['seconds']:.1f} s"}
 
 
 class RowQueue:

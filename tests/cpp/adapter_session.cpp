@@ -28,64 +28,7 @@
 #include "NFComm/NFConfigPlugin/NFCClassModule.h"
 #include "NFComm/NFConfigPlugin/NFCElementModule.h"
 #include "../../oracle/nfio.h"
-
-// ---- test doubles ----
-static int64_t g_now = 0;  // the session clock (ms): workload call and frame times
-
-class TestPluginManager : public NFIPluginManager {
-public:
-    std::map<std::string, NFIModule*> mods;
-    std::map<std::string, std::string> files;
-    bool ReLoadPlugin(const std::string&) override { return false; }
-    void Registered(NFIPlugin*) override {}
-    void UnRegistered(NFIPlugin*) override {}
-    NFIPlugin* FindPlugin(const std::string&) override { return nullptr; }
-    void AddModule(const std::string& n, NFIModule* m) override { mods[n] = m; }
-    void RemoveModule(const std::string& n) override { mods.erase(n); }
-    NFIModule* FindModule(const std::string& n) override {
-        auto it = mods.find(n);
-        return it == mods.end() ? nullptr : it->second;
-    }
-    int GetAppID() const override { return 6; }
-    void SetAppID(const int) override {}
-    NFINT64 GetInitTime() const override { return 0; }
-    NFINT64 GetNowTime() const override { return g_now / 1000; }
-    const std::string& GetConfigPath() const override { return path_; }
-    void SetConfigName(const std::string&) override {}
-    const std::string& GetAppName() const override { return name_; }
-    void SetAppName(const std::string&) override {}
-    const std::string& GetLogConfigName() const override { return name_; }
-    void SetLogConfigName(const std::string&) override {}
-    void SetGetFileContentFunctor(GET_FILECONTENT_FUNCTOR) override {}
-    bool GetFileContent(const std::string& f, std::string& c) override {
-        auto it = files.find(f);
-        if (it == files.end()) return false;
-        c = it->second;
-        return true;
-    }
-
-private:
-    std::string path_, name_ = "adapter_session";
-};
-
-class TestLogModule : public NFILogModule {
-public:
-    int errors = 0;
-    bool LogElement(const NF_LOG_LEVEL l, const NFGUID, const std::string&, const std::string&, const char*, int) override { return note(l); }
-    bool LogProperty(const NF_LOG_LEVEL l, const NFGUID, const std::string&, const std::string&, const char*, int) override { return note(l); }
-    bool LogObject(const NF_LOG_LEVEL l, const NFGUID, const std::string&, const char*, int) override { return note(l); }
-    bool LogRecord(const NF_LOG_LEVEL l, const NFGUID, const std::string&, const std::string&, const int, const int, const char*, int) override { return note(l); }
-    bool LogRecord(const NF_LOG_LEVEL l, const NFGUID, const std::string&, const std::string&, const char*, int) override { return note(l); }
-    bool LogNormal(const NF_LOG_LEVEL l, const NFGUID, const std::string&, const int, const char*, int) override { return note(l); }
-    bool LogNormal(const NF_LOG_LEVEL l, const NFGUID, const std::string&, const std::string&, const char*, int) override { return note(l); }
-    bool LogNormal(const NF_LOG_LEVEL l, const NFGUID, const std::ostringstream&, const char*, int) override { return note(l); }
-
-private:
-    bool note(NF_LOG_LEVEL l) {
-        errors += l >= NLL_ERROR_NORMAL;
-        return true;
-    }
-};
+#include "../../oracle/ref_server.hpp"
 
 static std::string cstr(const uint8_t* p) { return std::string((const char*)p, strnlen((const char*)p, 32)); }
 static uint64_t dbits(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
@@ -205,39 +148,7 @@ int main(int argc, char** argv) {
 
     // ---- the class schema as the reference's Struct XML (LogicClass.xml + one file per class) ----
     TestPluginManager pm;
-    {
-        auto prop = [](const std::string& id, const char* type, uint8_t f) {
-            return "<Property Id=\"" + id + "\" Type=\"" + type + "\" Public=\"" + ((f & NFK_PUBLIC) ? "1" : "0") +
-                   "\" Private=\"" + ((f & NFK_PRIVATE) ? "1" : "0") + "\" Save=\"0\" Cache=\"0\" Ref=\"0\" Upload=\"" +
-                   ((f & NFK_UPLOAD) ? "1" : "0") + "\"/>";
-        };
-        pm.files["NFDataCfg/Struct/LogicClass.xml"] =
-            "<XML><Class Id=\"IObject\" Type=\"TYPE_IOBJECT\" Path=\"NFDataCfg/Struct/Class/IObject.xml\" InstancePath=\"\">"
-            "<Class Id=\"NPC\" Type=\"TYPE_NPC\" Path=\"NFDataCfg/Struct/Class/NPC.xml\" InstancePath=\"\"/>"
-            "<Class Id=\"Player\" Type=\"TYPE_PLAYER\" Path=\"NFDataCfg/Struct/Class/Player.xml\" InstancePath=\"\"/>"
-            "</Class></XML>";
-        pm.files["NFDataCfg/Struct/Class/IObject.xml"] =
-            "<XML><Propertys>" + prop("ClassName", "string", 0) + prop("ConfigID", "string", 0) + "</Propertys></XML>";
-        for (int c = 0; c < NC; c++) {
-            std::string x = "<XML><Propertys>";
-            for (int p = 0; p < NP; p++)
-                x += prop(pname[p], p < NI ? "int" : p < NI + NF ? "float" : "object", pflags[c * NP + p]);
-            x += "</Propertys><Records>";
-            for (int r = 0; r < NR; r++) {
-                const int32_t rows = ((int32_t*)A("rec_rows")->data)[r], cols = ((int32_t*)A("rec_cols")->data)[r];
-                const uint8_t f = ((uint8_t*)A("rec_flags")->data)[c * NR + r];
-                x += "<Record Id=\"rec" + std::to_string(r) + "\" Row=\"" + std::to_string(rows) + "\" Col=\"" +
-                     std::to_string(cols) + "\" Public=\"" + ((f & NFK_PUBLIC) ? "1" : "0") + "\" Private=\"" +
-                     ((f & NFK_PRIVATE) ? "1" : "0") + "\" Save=\"0\" Cache=\"0\" Upload=\"" + ((f & NFK_UPLOAD) ? "1" : "0") + "\">";
-                for (int k = 0; k < cols; k++)
-                    x += std::string("<Col Type=\"") + (((uint8_t*)A("rec_ctype")->data)[r * NFK_MAX_REC_COLS + k] ? "float" : "int") +
-                         "\" Tag=\"c" + std::to_string(k) + "\"/>";
-                x += "</Record>";
-            }
-            x += "</Records></XML>";
-            pm.files["NFDataCfg/Struct/Class/" + cname[c] + ".xml"] = x;
-        }
-    }
+    write_class_schema(pm, wf, pname, cname, NI, NF, NC, NR);
     // ---- the server's modules (NFKernelPlugin's with the adapters, NFConfigPlugin's, a log) ----
     TestLogModule log;
     NFCClassModule classes(&pm);

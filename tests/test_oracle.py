@@ -84,6 +84,38 @@ def test_oracle_matches_reference(seed, kw):
     compare_runs(run_oracle(w), run_ref(w))
 
 
+SESSION = os.path.join(ROOT, "oracle", "_ref", "nf_ref_session")
+
+
+@pytest.mark.skipif(not os.path.exists(SESSION), reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("seed, kw", [
+    (31, dict(n_obj=1500, n_scenes=2, groups_per_scene=4, players_per_group=4, ext_frac=0.05, host_ops=True)),
+    (32, dict(n_obj=1200, n_scenes=1, groups_per_scene=3, players_per_group=6, ext_frac=0.1, ext_props="all",
+              rmw_frac=0.03, sched_edges=True, host_ops=True)),
+    (33, dict(n_obj=800, n_scenes=2, groups_per_scene=2, players_per_group=3, records=True, rec_rows=16,
+              rec_float_op=False, ext_frac=0.05)),
+])
+def test_oracle_matches_reference_server_modules(tmp_path, seed, kw):
+    """The oracle's final state against the reference's own server modules (oracle/ref_session.cpp:
+    NFCKernelModule, NFCScheduleModule, NFCSceneAOIModule, NFCClassModule compiled from the reference
+    sources; the heartbeat programs as functors calling NFIKernelModule::Get/SetProperty* and
+    SetRecordInt, the window's SetProperty / schedule calls through the interfaces): every int / f64
+    property of every object bit-exact after the frames, and the scheduler fired the same number of
+    heartbeats."""
+    w = workload.make_world(n_ticks=8, seed=seed, **kw)
+    wp, fp = str(tmp_path / "w.nfio"), str(tmp_path / "f.nfio")
+    nfio.write(wp, w)
+    r = subprocess.run([SESSION, wp, "8", "0", fp], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = nfio.read(fp)
+    ref = run_oracle(w)
+    for k in ("final_i", "final_f"):
+        a, b = np.asarray(got[k]), np.asarray(ref[k])
+        assert a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8)), k
+    fired = sum(len(ref[k]) for k in ref if k.startswith("fi_t") and k.endswith("_obj"))
+    assert int(np.asarray(got["counts"])[0]) == fired
+
+
 @pytest.mark.skipif(not have_ref, reason="oracle/_ref not built (needs /root/reference)")
 def test_reference_record_setfloat_bug():
     """NFCRecord::SetFloat stores a const double into the int64 alternative of the variant;
