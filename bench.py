@@ -461,8 +461,9 @@ def host_calls_run(args, torch, kernel, workload):
     (HP / Gold / EXP / TargetX, 5 % of them twice) and 1/64 of them an AddSchedule or
     RemoveSchedule call (batched per frame, call order kept).  Timed like the headline (warmup,
     then K frames between device syncs); host ms per frame of queueing the calls through the C-ABI
-    and of nfk_execute (GUID lookups, (slot, property) grouping, schedule-call folding, uploads,
-    launches), which overlap the previous frame on the GPU."""
+    (batches of >= 4096 calls: NFGUID lookups on the device mirror of the table, SetProperty calls
+    queued on the device) and of nfk_execute (uploads and launches: the (slot, property) and
+    (slot, kind) folds run on the device), which overlap the previous frame on the GPU."""
     frames = args.warmup + args.steps
     w = workload.bench_world(n_obj=args.entities, groups=args.groups, players_per_group=args.players_per_group,
                              n_ticks=frames, tick_ms=args.tick_ms, seed=2031, ext_frac=0.05, host_ops=True)
