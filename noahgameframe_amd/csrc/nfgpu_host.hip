@@ -18,6 +18,7 @@
 #include <thread>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "nfgpu_jit.hpp"
 #include "nfgpu_kernels.hip"
@@ -3238,6 +3239,10 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
     if (nhq) {
         HIPCHK(rocprim::radix_sort_pairs(nullptr, hf_sort, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
                                          (uint32_t*)nullptr, nhq, 0, hkey_bits, w->stream));
+        size_t scan_b = 0;  // (the per-slot count scans: device-wide, n + 1 counts, the last 0)
+        HIPCHK(rocprim::exclusive_scan(nullptr, scan_b, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, nhq + 1,
+                                       rocprim::plus<uint32_t>(), w->stream));
+        hf_sort = std::max(hf_sort, scan_b);
         int r = dev_reserve(w, &w->hf_buf, &w->hf_cap, ho_tmp + hf_sort + 256);
         if (r) return drop_window(w, r);
     }
@@ -3434,10 +3439,15 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
                                (const int32_t*)w->obj_slot_d, k1, i1);
             size_t sb = hf_sort;
             HIPCHK(rocprim::radix_sort_pairs(HF + ho_tmp, sb, k1, k2, i1, i2, nhq, 0, hkey_bits, w->stream));
-            hipLaunchKernelGGL(k_hfold<false>, dim3(gh_), dim3(256), 0, w->stream, (const uint64_t*)k2, (const uint32_t*)i2,
+            hipLaunchKernelGGL(k_hfold<false>, dim3((unsigned)((nhq + 1 + 255) / 256)), dim3(256), 0, w->stream,
+                               (const uint64_t*)k2, (const uint32_t*)i2,
                                hc, (int32_t)nhq, cp, cq, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ps, po, hpost);
-            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, w->stream, (const uint32_t*)cp, op, (int)nhq);
-            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, w->stream, (const uint32_t*)cq, oq, (int)nhq);
+            size_t tb = hf_sort;  // (a mass AddSchedule at start: millions of calls, so a device-wide scan)
+            HIPCHK(rocprim::exclusive_scan(HF + ho_tmp, tb, (const uint32_t*)cp, op, 0u, nhq + 1, rocprim::plus<uint32_t>(),
+                                           w->stream));
+            tb = hf_sort;
+            HIPCHK(rocprim::exclusive_scan(HF + ho_tmp, tb, (const uint32_t*)cq, oq, 0u, nhq + 1, rocprim::plus<uint32_t>(),
+                                           w->stream));
             hipLaunchKernelGGL(k_hfold<true>, dim3(gh_), dim3(256), 0, w->stream, (const uint64_t*)k2, (const uint32_t*)i2,
                                hc, (int32_t)nhq, cp, cq, (const uint32_t*)op, (const uint32_t*)oq, ps, po, hpost);
             hipLaunchKernelGGL(k_pre_hostops, dim3((unsigned)((npre + 255) / 256)), dim3(256), 0, w->stream,

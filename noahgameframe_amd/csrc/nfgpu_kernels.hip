@@ -268,6 +268,10 @@ __global__ void k_hfold(const uint64_t* __restrict__ keys, const uint32_t* __res
                         const uint32_t* __restrict__ opost, uint32_t* __restrict__ pre_slot,
                         uint32_t* __restrict__ pre_op, HPost post) {
     const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!kEmit && a == n) {  // (the counts' last entry: the scans' totals land at [n])
+        npre[n] = npost[n] = 0;
+        return;
+    }
     if (a >= n) return;
     const uint64_t ka = keys[a];
     const uint32_t slot = (uint32_t)(ka >> 5);
