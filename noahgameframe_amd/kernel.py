@@ -588,11 +588,18 @@ def run_workload(m, w, tick, collect=True):
                 sc, gr = int(m.cur_scene[o]), int(m.cur_group[o])
             m.SwitchScene((int(gh[o]), int(gd[o])), sc, gr, w["sw_x"][i], w["sw_y"][i], w["sw_z"][i])
             m.cur_scene[o], m.cur_group[o] = sc, gr
+    # (by_object: the calls by nfk object index — nfk_set_props_obj / nfk_schedule_calls_obj — which
+    # in a world without objects created after commit is the workload's object index)
+    by_object = os.environ.get("NFGPU_TEST_BY_OBJECT") == "1" and "born" not in w
     hsel = np.nonzero(w["h_tick"] == tick)[0]
     if len(hsel):   # call order preserved
         ho = w["h_obj"][hsel]
-        m.schedule_calls(w["h_op"][hsel], gh[ho], gd[ho], w["h_kind"][hsel], w["h_interval"][hsel],
-                         w["h_count"][hsel], w["h_time"][hsel])
+        if by_object:
+            m.schedule_calls_obj(w["h_op"][hsel], ho, w["h_kind"][hsel], w["h_interval"][hsel], w["h_count"][hsel],
+                                 w["h_time"][hsel])
+        else:
+            m.schedule_calls(w["h_op"][hsel], gh[ho], gd[ho], w["h_kind"][hsel], w["h_interval"][hsel],
+                             w["h_count"][hsel], w["h_time"][hsel])
     xsel = np.nonzero(w["x_tick"] == tick)[0]
     if len(xsel):
         mode = w["x_mode"][xsel] if "x_mode" in w else np.zeros(len(xsel), np.uint8)
@@ -606,7 +613,9 @@ def run_workload(m, w, tick, collect=True):
                 pid = w["x_pid"][sel]
                 isobj = pid >= m.n_int + m.n_flt
                 # (calls on different properties never interact: the object calls go as their own batch)
-                if (~isobj).any():
+                if (~isobj).any() and by_object:
+                    m.set_props_obj(xo[~isobj], pid[~isobj], w["x_bits"][sel][~isobj])
+                elif (~isobj).any():
                     m.set_props(gh[xo[~isobj]], gd[xo[~isobj]], pid[~isobj], w["x_bits"][sel][~isobj])
                 if isobj.any():
                     m.set_objects(gh[xo[isobj]], gd[xo[isobj]], pid[isobj], w["x_bits_h"][sel][isobj].view(np.int64),

@@ -134,6 +134,18 @@ def test_device_guid_lookups_match_oracle(gpu_available, monkeypatch, case):
     compare_runs(run_gpu(w), run_oracle(w))
 
 
+@pytest.mark.parametrize("case", ["wide_sets", "sched_edges", "switch_scene", "read_modify_write", "record_sets",
+                                  "big_group"])
+def test_calls_by_object_index_match_oracle(gpu_available, monkeypatch, case):
+    """SetProperty and schedule calls queued by nfk object index (nfk_set_props_obj,
+    nfk_schedule_calls_obj: what the C++ plugin uses after its own NFGUID check) give the oracle's
+    frames: the index is the object's creation order, no lookup on the way."""
+    monkeypatch.setenv("NFGPU_TEST_BY_OBJECT", "1")
+    w = workload.make_world(n_ticks=10, seed=sum(map(ord, case)) + 3, **CASES[case])
+    assert "born" not in w
+    compare_runs(run_gpu(w), run_oracle(w))
+
+
 @pytest.mark.parametrize("case", ["combined", "wide_sets", "lifecycle", "objects", "record_sets"])
 def test_calls_only_passes_match_oracle(gpu_available, case):
     """nfk_execute_calls — the plugin's same-frame pass for what heartbeat functors call — is a frame
