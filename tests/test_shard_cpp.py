@@ -51,6 +51,18 @@ def test_shard_protocol_device(gpu_available):
 
 
 @pytest.mark.gpu
+def test_rccl_transport_world_size_1(gpu_available):
+    """The scene shards' RCCL transport (RcclTransport: ncclAllGather of the tickets, grouped
+    ncclSend / ncclRecv of the rows on the world's stream) at world size 1 on the GPU: tickets and
+    rows come back as sent (tests/cpp/rccl_transport.cpp).  More ranks need more GPUs."""
+    exe = os.path.join(ROOT, "tests", "cpp", "_bin", "rccl_transport")
+    env = dict(os.environ, NCCL_DEBUG="WARN")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-2000:] + r.stdout
+    assert '"fails": 0' in r.stdout
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ranks", [2, 4])
 def test_plugin_shard_replay_matches_oracle(gpu_available, tmp_path, ranks):
     """Scene shards through the C++ plugin (NFGPUKernelModule::AttachShard + SceneShard), ranks as
