@@ -26,9 +26,11 @@ def main():
          else workload.fanout_world(n_ticks=1) if a.config == 3
          else workload.bench_world(n_obj=a.entities, n_ticks=1))
     mods = {}
-    for v in (int(x, 0) for x in a.variants.split(",")):
+    for i, v in enumerate(int(x, 0) for x in a.variants.split(",")):
         os.environ["NFGPU_ABLATE"] = str(v)
-        mods[v] = kernel.world_from_workload(w, slack_per_256=-1)  # as bench.py (no membership changes)
+        # (a variant listed twice gets a world of its own: key "v#i")
+        key = v if v not in mods else f"{v}#{i}"
+        mods[key] = kernel.world_from_workload(w, slack_per_256=-1)  # as bench.py (no membership changes)
     os.environ.pop("NFGPU_ABLATE", None)
     t0 = int(w["tick_time"][0])
     tick = {v: 0 for v in mods}
