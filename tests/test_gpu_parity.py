@@ -169,6 +169,27 @@ def test_every_property_set_on_one_entity(gpu_available, monkeypatch, path):
     compare_runs(run_gpu(w), run_oracle(w))
 
 
+@PATHS
+@pytest.mark.parametrize("ext", [0.0, 0.3], ids=["idle", "sets-only"])
+def test_world_without_heartbeats(gpu_available, monkeypatch, path, ext):
+    """No schedule at all (NFCScheduleModule::Execute walks an empty map, SM:49): an idle world's
+    frames have no output, and with SetProperty calls only those Sets' events and fan-out
+    (test_oracle.py::test_oracle_empty_world on the GPU)."""
+    set_path(monkeypatch, path)
+    w = workload.make_world(n_obj=1500, n_scenes=2, groups_per_scene=3, players_per_group=3, n_ticks=4, seed=5,
+                            ext_frac=ext, host_ops=False)
+    keep = w["s_obj"][:0]
+    w["s_obj"] = keep
+    for k in ("s_kind", "s_interval", "s_count", "s_time"):
+        w[k] = w[k][:0]
+    w["cfg"][6] = 0
+    got, ref = run_gpu(w), run_oracle(w)
+    compare_runs(got, ref)
+    assert all(len(ref[f"fi_t{t}_obj"]) == 0 for t in range(4))
+    if ext == 0.0:
+        assert all(len(ref[f"ev_t{t}_obj"]) == 0 for t in range(4))
+
+
 @pytest.mark.parametrize("slack", [-1, 1, 64])
 def test_switch_scene_layouts(gpu_available, slack):
     """SwitchScene with no slack (every change rebuilds the layout), tiny slack (segments overflow
