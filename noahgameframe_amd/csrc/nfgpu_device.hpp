@@ -63,8 +63,8 @@ constexpr unsigned kAblGroupColumns = 1u << 20, kAblSigGroups = 1u << 21;  // co
 constexpr unsigned kAblNoPad = 1u << 22;  // columns / schedule kinds at power-of-two strides (outputs exact)
 constexpr unsigned kAblRecVec = 1u << 23;  // k_records writes whole row-vectors back (outputs exact)
 constexpr unsigned kAblFanWin16 = 1u << 24, kAblFanWin32 = 1u << 25;  // k_tick fan-out LDS window up to 16 / 32 recipients (outputs exact)
-constexpr unsigned kAblFan1 = 1u << 26;
-constexpr unsigned kAblTinyTcap = 1u << 27;  // test hook: k_tick's fan-out bound set to 4 messages (kErrFanBound)  // k_tick fan-out: one recipient per lane (the round-1 form; outputs exact)
+constexpr unsigned kAblFan1 = 1u << 26;      // k_tick fan-out: one recipient per lane (the round-1 form; outputs exact)
+constexpr unsigned kAblTinyTcap = 1u << 27;  // test hook: k_tick's fan-out bound set to 4 messages (kErrFanBound)
 // four u32 at a dword-aligned address (gfx950 global memory allows it; one 16-byte store)
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Pad between consecutive property columns and schedule-kind arrays (bytes): with cap a power of
