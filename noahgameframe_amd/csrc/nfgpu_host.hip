@@ -1091,7 +1091,10 @@ struct MemPlan {
     bool active = false, full = false;
     int32_t max_np0 = 0;
     std::vector<int32_t> aff, epos;
+    // einfo[0, n_einfo): this plan's affected segments; the entries (and their lists' buffers)
+    // are kept from plan to plan, so a window's edits allocate nothing once they have been seen
     std::vector<EdInfo> einfo;
+    size_t n_einfo = 0;
     std::vector<SegEdit> edits;
     std::vector<int32_t> ins_rank, ins_obj, rem_rank;
     std::vector<uint64_t> ins_meta;
@@ -1114,7 +1117,7 @@ int plan_membership(World* w, MemPlan& p) {
     p.t_host = clk::now();
     p.full = false;
     p.aff.clear();
-    p.einfo.clear();
+    p.n_einfo = 0;
     p.edits.clear();
     p.ins_rank.clear();
     p.ins_obj.clear();
@@ -1146,8 +1149,13 @@ int plan_membership(World* w, MemPlan& p) {
     einfo.reserve(2 * w->touched.size() + 1);
     auto ed = [&](int32_t g) -> EdInfo& {
         if (epos[g] < 0) {
-            epos[g] = (int32_t)einfo.size();
-            einfo.emplace_back();
+            if (p.n_einfo == einfo.size()) einfo.emplace_back();
+            EdInfo& x = einfo[p.n_einfo];
+            x.rem.clear();
+            x.join.clear();
+            x.ins.clear();
+            x.seg.objs.clear();
+            epos[g] = (int32_t)p.n_einfo++;
             aff.push_back(g);
         }
         return einfo[epos[g]];
@@ -1476,8 +1484,8 @@ int commit_membership(World* w, MemPlan& p) {
             if (nsrc[g] < 0 || w->segs[g].base != seg_base0[g] || w->segs[g].cap != seg_cap0[g]) aff.push_back((int32_t)g);
     } else {
         w->n_relayout_seg++;
-        for (int32_t gi : aff) {
-            w->segs[gi].objs = std::move(einfo[epos[gi]].seg.objs);
+        for (int32_t gi : aff) {  // (the old list's buffer goes back to the plan, for the next window)
+            std::swap(w->segs[gi].objs, einfo[epos[gi]].seg.objs);
             w->segs[gi].np = einfo[epos[gi]].seg.np;
         }
     }
