@@ -72,6 +72,10 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // on the same HBM channel.
 constexpr int64_t kColPad = 2304;
 constexpr unsigned kAblScanInFrame = 131072;  // k_scan_tiles in every frame, not on first read
+constexpr unsigned kAblScanKernel = 1u << 28;  // dense ranks by k_scan_tiles in small worlds too (outputs exact)
+// k_tick ranks its own tiles up to this many (one agent-scope add per tile on one address: they
+// serialise at ~7 ns each, profiles/r08s_last_arrival_ranks_ab.txt, so only small worlds gain)
+constexpr int kLbMaxTiles = 256;
 constexpr unsigned kAblNoFuse = 4096;  // fan-out in k_fanout instead of k_tick's tail (outputs stay exact)
 
 // record op compiled from the kind programs, sorted by (rec, col)
@@ -246,6 +250,14 @@ struct Dev {
     uint32_t* fi_base; // [n_tiles + 1]
     uint32_t* re_base; // [n_rtiles + 1]
     uint32_t* msg_base;// [n_tiles + n_rtiles + 1] first message of each tile (k_scan_tiles)
+    // lb_rank (small worlds): k_tick writes ev_base / fi_base / msg_base and the frame totals
+    // itself — its last tile to publish counts scans them (lb_st [n_tiles][4] count words tagged
+    // with lb_epoch, one epoch per launch; lb_cnt the arrivals; nfgpu_tick.hpp) — and no
+    // k_scan_tiles runs for the frame
+    uint64_t* lb_st;
+    uint32_t* lb_cnt;
+    uint32_t lb_epoch;
+    int32_t lb_rank;
     // msg_tcap > 0: k_tick writes its tile's fan-out itself, property tile t's messages at
     // t * msg_tcap (an upper bound of one tile's messages this frame); record tiles follow densely
     uint32_t msg_tcap;

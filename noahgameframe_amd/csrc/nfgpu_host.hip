@@ -266,6 +266,7 @@ struct World {
     int32_t ticks = 0;
     uint32_t last_tcap = 0;  // Dev::msg_tcap of the last launched frame
     uint32_t last_rtcap = 0; // Dev::msg_rtcap of the last launched frame (0: records not fused)
+    uint32_t lb_epoch = 0;       // k_tick's own ranks: the last launch's epoch (Dev::lb_epoch)
     bool scan_pending = false;  // the last frame's dense ranks (k_scan_tiles) are built on first read
     Dev scan_dev;               // ... with that frame's Dev
     int64_t last_rec_msgs = 0;  // record-tile messages of the last summarised frame (capacity hint)
@@ -2032,6 +2033,8 @@ int nfk_commit(void* world) {
     ALLOC(d.fi_base, (nt + 1) * 4);
     ALLOC(d.re_base, (nrt + 1) * 4);
     ALLOC(d.msg_base, (nt + nrt + 1) * 4);
+    ALLOC(d.lb_st, std::min<size_t>(nt, kLbMaxTiles) * 4 * 8);
+    ALLOC(d.lb_cnt, 64);
     d.msg_cap = w->cfg.msg_capacity > 0 ? w->cfg.msg_capacity : (int64_t)cap * 32;
     if (d.msg_cap > 0xFFFFFFFFll) return fail(NFK_ERR_ARG, "msg_capacity must fit 32-bit offsets");
     ALLOC(d.ev_slot, ev_n * 4);
@@ -2140,6 +2143,9 @@ int nfk_commit(void* world) {
     HIPCHK(hipMemset(d.fi_base, 0, (nt + 1) * 4));
     HIPCHK(hipMemset(d.re_base, 0, (nrt + 1) * 4));
     HIPCHK(hipMemset(d.msg_base, 0, (nt + nrt + 1) * 4));
+    HIPCHK(hipMemset(d.lb_st, 0, std::min<size_t>(nt, kLbMaxTiles) * 4 * 8));
+    HIPCHK(hipMemset(d.lb_cnt, 0, 64));
+    w->lb_epoch = 0;
     // creation-time values are now on the device
     for (auto& v : w->init_props) std::vector<uint64_t>().swap(v);
     for (auto& v : w->init_rcells) std::vector<uint64_t>().swap(v);
@@ -3519,6 +3525,18 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
         }
     }
     d.fuse_fan = d.msg_tcap != 0;
+    // A small world with no record pipeline after k_tick: its last tile ranks the frame's tiles
+    // and the frame has no k_scan_tiles launch (profiles/r09a_*)
+    d.lb_rank = (d.fuse_fan && !d.has_recops && d.n_tiles && d.n_tiles <= kLbMaxTiles &&
+                 !(d.ablate & kAblScanKernel)) ? 1 : 0;
+    if (d.lb_rank) {
+        if (++w->lb_epoch == 0xFFFFFFFFu) {  // (clear the tags before they could repeat)
+            HIPCHK(hipMemsetAsync(w->d.lb_st, 0, std::min<size_t>(w->obj_of_slot.size() / kTile, kLbMaxTiles) * 4 * 8,
+                                  w->stream));
+            w->lb_epoch = 1;
+        }
+        d.lb_epoch = w->lb_epoch;
+    }
     w->last_tcap = d.msg_tcap;
     w->last_rtcap = d.fuse_rec ? d.msg_rtcap : 0u;
     if (d.n_tiles) {
@@ -3586,7 +3604,9 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
     // Otherwise the frame's outputs are complete as tiles + per-tile counts, and the ranks are
     // built on the first read (nfk_summary_get, nfk_outputs_get, nfk_read_*).
     w->scan_pending = false;
-    if (d.fuse_fan && (!d.has_recops || d.fuse_rec) && !(d.ablate & kAblScanInFrame)) {
+    if (d.lb_rank) {
+        // (written by k_tick's last tile)
+    } else if (d.fuse_fan && (!d.has_recops || d.fuse_rec) && !(d.ablate & kAblScanInFrame)) {
         w->scan_pending = true;
         w->scan_dev = d;
     } else {

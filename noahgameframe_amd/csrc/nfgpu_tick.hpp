@@ -246,6 +246,65 @@ __device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& by
     return fired;
 }
 
+// ---- dense ranks in k_tick (Dev::lb_rank, worlds of at most kLbMaxTiles tiles) ----
+// What k_scan_tiles computes, without its launch: every tile publishes its three counts (events,
+// fired, messages) at its block scan and counts itself in lb_cnt; the tile that arrives there last
+// computes ev_base / fi_base / msg_base and the frame totals of all tiles at its end and resets
+// lb_cnt for the next launch.  The counts are tagged with the launch's epoch (lb_st word:
+// epoch << 32 | value), so the last tile waits for a word not yet visible instead of fencing,
+// and nothing is cleared between launches.
+__device__ __forceinline__ void lb_store(const Dev& d, int tile, int q, uint32_t v) {
+    __hip_atomic_store(d.lb_st + (size_t)tile * 4 + q, ((uint64_t)d.lb_epoch << 32) | v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t lb_load(const Dev& d, int tile, int q) {
+    const uint64_t* p = d.lb_st + (size_t)tile * 4 + q;
+    uint64_t s;
+    while (((s = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != d.lb_epoch)
+        __builtin_amdgcn_s_sleep(1);
+    return (uint32_t)s;
+}
+// threads 0..2 publish; returns (thread 0) whether this tile arrived last
+__device__ __forceinline__ bool lb_arrive(const Dev& d, int tile, uint32_t ev, uint32_t fi, uint32_t msg) {
+    if (threadIdx.x < 3) lb_store(d, tile, threadIdx.x, threadIdx.x == 0 ? ev : threadIdx.x == 1 ? fi : msg);
+    if (threadIdx.x != 0) return false;
+    return __hip_atomic_fetch_add(d.lb_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)d.n_tiles - 1u;
+}
+// the whole workgroup of the last tile (n_tiles <= kLbMaxTiles = kTPB: one count per thread)
+__device__ void lb_scan_all(const Dev& d, unsigned long long* s_w) {
+    static_assert(kLbMaxTiles <= kTPB, "one tile's counts per thread");
+    const int n = d.n_tiles, t = (int)threadIdx.x;
+    uint32_t ev = 0, fi = 0, ms = 0;
+    if (t < n) {
+        ev = lb_load(d, t, 0);
+        fi = lb_load(d, t, 1);
+        ms = lb_load(d, t, 2);
+    }
+    unsigned long long tef, tm;
+    const unsigned long long xef = block_excl_scan(((unsigned long long)fi << 32) | ev, s_w, tef);
+    __syncthreads();
+    block_excl_scan(ms, s_w, tm);
+    if (t < n) {
+        d.ev_base[t] = (uint32_t)xef;
+        d.fi_base[t] = (uint32_t)(xef >> 32);
+        d.msg_base[t] = (uint32_t)t * d.msg_tcap;
+    }
+    if (t == 0) {  // (k_scan_tiles' totals; no record tiles in such a frame)
+        const unsigned long long ext = (unsigned long long)n * d.msg_tcap;
+        d.ev_base[n] = (uint32_t)tef;
+        d.fi_base[n] = (uint32_t)(tef >> 32);
+        d.msg_base[n] = (uint32_t)ext;
+        d.re_base[0] = 0;
+        d.ctrl->n_ev = (uint32_t)tef;
+        d.ctrl->n_fi = (uint32_t)(tef >> 32);
+        d.ctrl->n_re = 0;
+        d.ctrl->msg_extent = ext;
+        d.ctrl->n_msgs_ptiles = tm;
+        if (ext > (unsigned long long)d.msg_cap) dev_error(d, kErrMsgCap);
+        __hip_atomic_store(d.lb_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (every tile has arrived)
+    }
+}
+
 // k_tick: one thread per slot, one workgroup per 256-slot tile, on the programs' working set
 // (Dev::u_*, fixed at commit).  Every value the entity's frame touches is loaded in ONE batch of
 // independent loads into registers; the fired kinds' programs run on those registers with
@@ -254,7 +313,8 @@ __device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& by
 // program destination joins that slot's diff (frame-start value = the group's x_old), a Set of any
 // other property is a "standalone" event (x_old -> x_new) merged into the entity's events in
 // property-id order.  Outputs of tile t are written densely at [t * tile_cap, t * tile_cap + count);
-// k_scan_tiles turns the counts into global ranks.
+// k_scan_tiles, or in a small world this kernel's last tile (Dev::lb_rank), turns the counts into
+// global ranks.
 // kWPE: waves per SIMD the register allocation aims at.  The LDS image of the frame-start values
 // is dynamic: n_w writable slots x kTPB.
 template <int kWPE, int kU, class S = DynSchema>
@@ -262,6 +322,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     constexpr int kW = kU < kMaxW ? kU : kMaxW;  // writable register slots
     __shared__ unsigned long long s_w[kTPB / 64];
     __shared__ unsigned s_bytes;
+    __shared__ uint32_t s_lb_last;  // this tile ranks the frame's tiles (Dev::lb_rank)
     __shared__ uint32_t s_pb[3];   // pl_slot run of the groups with dirty events [lo, hi), most recipients
     __shared__ uint32_t s_cm[NFK_MAX_CLASSES];  // Dev::u_cmask
     extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
@@ -273,6 +334,12 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             d.t_ev[tile] = 0;
             d.t_fi[tile] = 0;
             d.t_msg[tile] = 0;
+        }
+        if (d.lb_rank) {
+            const bool last = lb_arrive(d, tile, 0u, 0u, 0u);
+            if (threadIdx.x == 0) s_lb_last = last;
+            __syncthreads();
+            if (s_lb_last) lb_scan_all(d, s_w);
         }
         return;
     }
@@ -440,6 +507,8 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     const unsigned pev0 = (unsigned)((excl >> 32) & 0xFFFF);
     unsigned pfi = (unsigned)(excl >> 48);
     const unsigned pmsg0 = (unsigned)excl, tmsg = (unsigned)tot;
+    // this tile's counts for the dense ranks; whether it is the last to publish them (thread 0)
+    const bool lb_last = d.lb_rank && lb_arrive(d, tile, (unsigned)((tot >> 32) & 0xFFFF), (unsigned)(tot >> 48), tmsg);
     // this tile's output runs (wave-uniform bases, tile-local 32-bit offsets)
     const size_t ev0 = (size_t)tile * d.ev_tcap, fi0 = (size_t)tile * d.fi_tcap;
     uint32_t* const t_evm = d.ev_moff + ev0;
@@ -702,13 +771,16 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     // tile counts and algorithmic-byte tally
     const unsigned wb = (unsigned)wave_sum(bytes);
     if ((threadIdx.x & 63) == 0) atomicAdd(&s_bytes, wb);
+    if (threadIdx.x == 0) s_lb_last = lb_last;
     __syncthreads();
+    const bool lb_scan = d.lb_rank && s_lb_last;
     if (threadIdx.x == 0) {
         d.t_ev[tile] = (unsigned)((tot >> 32) & 0xFFFF);
         d.t_fi[tile] = (unsigned)(tot >> 48);
         d.t_msg[tile] = (unsigned)tot;
         tally_add(d, kTallyTick, (unsigned long long)(s_bytes + 12 + (fuse ? 16 : 0)));
     }
+    if (lb_scan) lb_scan_all(d, s_w);
 }
 
 }  // namespace nfgpu
