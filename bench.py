@@ -10,7 +10,7 @@ frames (5 % of the entities get a SetProperty, 1/64 an AddSchedule / RemoveSched
 frame), timed the same way, with the host milliseconds per frame of queueing the calls and of
 nfk_execute's host preparation.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]      (N > 1: bench.py starts the N ranks itself)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 Scenes shard naturally: rank r owns scene r+1 with its own 1M entities (weak scaling, no
@@ -225,14 +225,74 @@ class Migration:
         self.pending.append((self.frames, self.shard.exchange_ticket_array_async(out, max_rows=self.per_frame)))
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(n, i, port, base=None):
+    """The environment of rank i of n started by bench.py itself (what torch.distributed.run sets)."""
+    env = dict(os.environ if base is None else base)
+    env.update({"RANK": str(i), "LOCAL_RANK": str(i), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    return env
+
+
+def spawn_ranks(n, argv, script=None):
+    """`bench.py --gpus N` with N > 1 and no launcher: start N rank processes (one per GPU, RANK /
+    LOCAL_RANK / WORLD_SIZE set, rendezvous on 127.0.0.1) and wait for them.  This process has not
+    touched the GPU (it runs before any torch import) and does not afterwards.  If a rank fails,
+    the others are stopped (by their own PIDs) and its exit code is returned; rank 0 prints the
+    one JSON line."""
+    import signal
+    port = free_port()
+    script = script or os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=rank_env(n, i, port))
+             for i in range(n)]
+    rc = 0
+    try:
+        live = set(range(n))
+        while live:
+            for i in sorted(live):
+                r = procs[i].poll()
+                if r is None:
+                    continue
+                live.discard(i)
+                if r != 0 and rc == 0:
+                    rc = r
+                    print(f"bench.py: rank {i} exited with {r}; stopping the other ranks", file=sys.stderr, flush=True)
+                    for j in live:
+                        procs[j].send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+def world_from_env(gpus):
+    """(world size, rank, local rank) from the launcher's environment, checked against --gpus."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: start one rank per GPU "
+                         f"(--nproc-per-node {gpus}) or run bench.py --gpus {gpus} without a launcher")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local = world_from_env(args.gpus)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
@@ -341,9 +401,13 @@ def main():
         mig.finish()
     ms, nl, byts = m.kernel_times()
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+    moved = torch.tensor([mig.shard.migrated_out if mig else 0, mig.shard.migrated_in if mig else 0],
+                         dtype=torch.int64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(moved, op=dist.ReduceOp.SUM)
     elapsed = float(el.item())
+    moved = [int(x) for x in moved.tolist()]
     m.close()
 
     # per-kernel averages over the timed region (HIP events on the world's stream)
@@ -403,6 +467,7 @@ def main():
                    "entities_per_gpu": args.entities, "groups": args.groups,
                    "players_per_group": args.players_per_group, "parallelism": f"scene-shard x{world}",
                    "migrations_per_rank_per_frame": args.migrate / args.migrate_every if migrating else 0},
+        "migrations": {"out": moved[0], "in": moved[1], "backend": args.backend} if migrating else None,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "mix_ceiling": ceiling},

@@ -65,6 +65,7 @@ constexpr unsigned kAblRecVec = 1u << 23;  // k_records writes whole row-vectors
 constexpr unsigned kAblFanWin16 = 1u << 24, kAblFanWin32 = 1u << 25;  // k_tick fan-out LDS window up to 16 / 32 recipients (outputs exact)
 constexpr unsigned kAblFan1 = 1u << 26;      // k_tick fan-out: one recipient per lane (the round-1 form; outputs exact)
 constexpr unsigned kAblTinyTcap = 1u << 27;  // test hook: k_tick's fan-out bound set to 4 messages (kErrFanBound)
+constexpr unsigned kAblForceMsgCap = 1u << 29;  // test hook: the frame's ranks also raise kErrMsgCap
 // four u32 at a dword-aligned address (gfx950 global memory allows it; one 16-byte store)
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Pad between consecutive property columns and schedule-kind arrays (bytes): with cap a power of
@@ -275,14 +276,17 @@ struct Dev {
     uint32_t* re_slot; uint32_t* re_rrc; uint64_t* re_old; uint64_t* re_new; uint32_t* re_moff;
     uint32_t* msg_rcpt; int64_t msg_cap;
     uint64_t* ev_old_h; uint64_t* ev_new_h;  // head halves of object-property events (n_obj > 0)
-    // host-mapped error word: a kernel that sets a bit of ctrl->err also stores it here, so the
-    // host sees it without a device read (nfk_outputs_get, nfk_execute)
+    // host-mapped error words [kErrHostWords]: a kernel that sets bit b of ctrl->err also stores 1
+    // into err_host[log2 b], so the host sees it without a device read (nfk_outputs_get, nfk_execute)
     unsigned* err_host;
 };
 
+// The host-mapped error word is one word PER BIT (err_host[log2 bit] = 1): plain stores only, no
+// read-modify-write over PCIe, and a later error never overwrites an earlier one's bit.
+constexpr int kErrHostWords = 16;
 __device__ __forceinline__ void dev_error(const Dev& d, unsigned bit) {
     atomicOr(&d.ctrl->err, bit);
-    if (d.err_host) __hip_atomic_store(d.err_host, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (d.err_host) __hip_atomic_store(d.err_host + __builtin_ctz(bit), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 constexpr int kTallyN = 64, kTallyTick = 0, kTallyRec = 1, kTallyFan = 2;

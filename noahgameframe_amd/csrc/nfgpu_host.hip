@@ -261,6 +261,7 @@ struct World {
     // k_tick specialised to this world's schema (nfgpu_jit.hpp); null: the generic instantiations
     hipFunction_t jit_fn = nullptr;
     int jit_waves = 0, jit_u = 0;
+    bool jit_lb = false;  // the specialisation keeps k_tick's in-kernel ranks (a world of <= kLbMaxTiles tiles)
     std::string jit_msg = "not compiled";
 
     int32_t ticks = 0;
@@ -285,6 +286,16 @@ struct World {
     int64_t kt_bytes[KT_N] = {};
     uint64_t last_bytes[3] = {0, 0, 0};
 };
+
+// the device error bits in the host-mapped words (dev_error: one word per bit)
+inline unsigned err_host_bits(const World* w) {
+    unsigned e = 0;
+    for (int i = 0; i < kErrHostWords; i++) e |= ((volatile const unsigned*)w->err_host)[i] ? 1u << i : 0u;
+    return e;
+}
+inline void clear_err_host(World* w) {
+    for (int i = 0; i < kErrHostWords; i++) ((volatile unsigned*)w->err_host)[i] = 0;
+}
 
 constexpr uint32_t kNoKind = 0xFFFFFFFFu;  // HOp::kind of a RemoveSchedule(self, name) with no device program
 // a queued SetProperty of a property no program writes: a standalone event (see nfk_execute)
@@ -1014,7 +1025,11 @@ void build_jit(World* w) {
     // non-temporal hints (kNt* bits of nfgpu_tick.hpp); NFGPU_JIT_NT overrides the default
     uint32_t nt = kJitNtDefault;
     if (const char* en = getenv("NFGPU_JIT_NT")) nt = (uint32_t)strtoul(en, nullptr, 0);
-    const std::string src = jit_schema_source(w->tab, w->d, spec, nt);
+    // a world whose capacity exceeds kLbMaxTiles tiles never ranks in k_tick: that code is compiled
+    // out of its specialisation (NFGPU_JIT_LB=1 keeps it, for A/B)
+    bool lb = ((int64_t)w->d.cap + kTile - 1) / kTile <= kLbMaxTiles;
+    if (const char* el = getenv("NFGPU_JIT_LB")) lb = el[0] == '1';
+    const std::string src = jit_schema_source(w->tab, w->d, spec, nt, lb);
     int dev = 0;
     (void)hipGetDevice(&dev);
     const std::string key = std::to_string(dev) + "|" + std::to_string(waves) + "|" + std::to_string(u) + "|" + src;
@@ -1032,6 +1047,7 @@ void build_jit(World* w) {
         it = g_jit.emplace(key, fn).first;
     }
     w->jit_fn = it->second;
+    w->jit_lb = lb;
     w->jit_waves = waves;
     w->jit_u = u;
     w->jit_msg = jit_kernel_name(waves, u);
@@ -1629,7 +1645,7 @@ int nfk_create(const nfk_config* cfg, void** out) {
         delete w;
         return fail(NFK_ERR_HIP, "hipEventCreate failed");
     }
-    *(volatile unsigned*)w->err_host = 0;
+    clear_err_host(w);
     w->init_props.resize(w->n_prop);
     w->init_rcells.resize(cfg->n_rec);
     w->init_rused.resize(cfg->n_rec);
@@ -2966,7 +2982,7 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     // a device error of an earlier frame (host-mapped, no device read): that frame's outputs are
     // incomplete, so no further frame runs until nfk_summary_get has reported and cleared it
-    if (const unsigned e = *(volatile unsigned*)w->err_host; e & (kErrFanBound | kErrTouch))
+    if (const unsigned e = err_host_bits(w); e & (kErrFanBound | kErrTouch))
         return fail(NFK_ERR_DEVICE, std::string("device error of an earlier frame: ") +
                                         ((e & kErrFanBound) ? "a tile's fan-out exceeded its bound" : "touch list overflow") +
                                         " (nfk_summary_get reports and clears it)");
@@ -3528,7 +3544,7 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
     // A small world with no record pipeline after k_tick: its last tile ranks the frame's tiles
     // and the frame has no k_scan_tiles launch (profiles/r09a_*)
     d.lb_rank = (d.fuse_fan && !d.has_recops && d.n_tiles && d.n_tiles <= kLbMaxTiles &&
-                 !(d.ablate & kAblScanKernel)) ? 1 : 0;
+                 !(d.ablate & kAblScanKernel) && (!(use_u && w->jit_fn) || w->jit_lb)) ? 1 : 0;
     if (d.lb_rank) {
         if (++w->lb_epoch == 0xFFFFFFFFu) {  // (clear the tags before they could repeat)
             HIPCHK(hipMemsetAsync(w->d.lb_st, 0, std::min<size_t>(w->obj_of_slot.size() / kTile, kLbMaxTiles) * 4 * 8,
@@ -3771,7 +3787,7 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     out->device_error = (int32_t)c.err;
     out->tick = w->ticks;
     if (c.err) HIPCHK(hipMemset(&w->ctrl->err, 0, sizeof(unsigned)));
-    *(volatile unsigned*)w->err_host = 0;  // (the stream is idle: read_ctrl synchronised it)
+    clear_err_host(w);  // (the stream is idle: read_ctrl synchronised it)
     if (c.err & kErrTouch) return fail(NFK_ERR_TOUCH, "device touch list overflow");
     if (c.err & kErrFanBound) return fail(NFK_ERR_STATE, "a tile's fan-out exceeded its bound");
     if (c.err & kErrMsgCap)
@@ -3787,7 +3803,7 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     if (r) return r;
     // a device error of a frame that has completed (host-mapped word, no device read); a frame
     // still running reports through the next call that waits for it (nfk_execute, nfk_summary_get)
-    if (const unsigned e = *(volatile unsigned*)w->err_host; e & (kErrFanBound | kErrTouch))
+    if (const unsigned e = err_host_bits(w); e & (kErrFanBound | kErrTouch))
         return fail(NFK_ERR_DEVICE, (e & kErrFanBound) ? "a tile's fan-out exceeded its bound: the recipient lists are truncated"
                                                        : "touch list overflow: events are missing");
     r = ensure_ranks(w);  // (asynchronous, on the world's stream like the frame)

@@ -1352,7 +1352,7 @@ __global__ __launch_bounds__(kScanTPB) void k_scan_tiles(Dev d) {
         if (a == 2) d.ctrl->n_re = carry;
         if (a == 3) {
             d.ctrl->msg_extent = carry;
-            if (carry > (unsigned long long)d.msg_cap) dev_error(d, kErrMsgCap);
+            if (carry > (unsigned long long)d.msg_cap || (d.ablate & kAblForceMsgCap)) dev_error(d, kErrMsgCap);
         }
     }
     if (a == 3) {  // sum of the fixed-stride tiles' messages

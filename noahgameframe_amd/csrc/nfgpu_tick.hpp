@@ -137,6 +137,9 @@ struct DynSchema {
     static constexpr uint32_t kSpecMask = 0;  // operands loaded before the fire test (none)
     // non-temporal hints (kNt* bits): none in the library's instantiations
     static constexpr uint32_t kNt = 0;
+    // k_tick may rank a small world's tiles itself (Dev::lb_rank); a policy for a world of more than
+    // kLbMaxTiles tiles compiles that code out (kLb = false) and the frame ranks by k_scan_tiles
+    static constexpr bool kLb = true;
     static constexpr int kNK = NFK_MAX_KINDS;  // (an upper bound only)
     __device__ static int n_kind(const Dev& d) { return d.n_kind; }
     __device__ static int n_w(const Dev& d) { return d.n_w; }
@@ -300,7 +303,7 @@ __device__ void lb_scan_all(const Dev& d, unsigned long long* s_w) {
         d.ctrl->n_re = 0;
         d.ctrl->msg_extent = ext;
         d.ctrl->n_msgs_ptiles = tm;
-        if (ext > (unsigned long long)d.msg_cap) dev_error(d, kErrMsgCap);
+        if (ext > (unsigned long long)d.msg_cap || (d.ablate & kAblForceMsgCap)) dev_error(d, kErrMsgCap);
         __hip_atomic_store(d.lb_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (every tile has arrived)
     }
 }
@@ -335,7 +338,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             d.t_fi[tile] = 0;
             d.t_msg[tile] = 0;
         }
-        if (d.lb_rank) {
+        if (S::kLb && d.lb_rank) {
             const bool last = lb_arrive(d, tile, 0u, 0u, 0u);
             if (threadIdx.x == 0) s_lb_last = last;
             __syncthreads();
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     unsigned pfi = (unsigned)(excl >> 48);
     const unsigned pmsg0 = (unsigned)excl, tmsg = (unsigned)tot;
     // this tile's counts for the dense ranks; whether it is the last to publish them (thread 0)
-    const bool lb_last = d.lb_rank && lb_arrive(d, tile, (unsigned)((tot >> 32) & 0xFFFF), (unsigned)(tot >> 48), tmsg);
+    const bool lb_last = S::kLb && d.lb_rank && lb_arrive(d, tile, (unsigned)((tot >> 32) & 0xFFFF), (unsigned)(tot >> 48), tmsg);
     // this tile's output runs (wave-uniform bases, tile-local 32-bit offsets)
     const size_t ev0 = (size_t)tile * d.ev_tcap, fi0 = (size_t)tile * d.fi_tcap;
     uint32_t* const t_evm = d.ev_moff + ev0;
@@ -771,16 +774,17 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     // tile counts and algorithmic-byte tally
     const unsigned wb = (unsigned)wave_sum(bytes);
     if ((threadIdx.x & 63) == 0) atomicAdd(&s_bytes, wb);
-    if (threadIdx.x == 0) s_lb_last = lb_last;
+    if (S::kLb && threadIdx.x == 0) s_lb_last = lb_last;
     __syncthreads();
-    const bool lb_scan = d.lb_rank && s_lb_last;
+    const bool lb_scan = S::kLb && d.lb_rank && s_lb_last;
     if (threadIdx.x == 0) {
         d.t_ev[tile] = (unsigned)((tot >> 32) & 0xFFFF);
         d.t_fi[tile] = (unsigned)(tot >> 48);
         d.t_msg[tile] = (unsigned)tot;
         tally_add(d, kTallyTick, (unsigned long long)(s_bytes + 12 + (fuse ? 16 : 0)));
     }
-    if (lb_scan) lb_scan_all(d, s_w);
+    if constexpr (S::kLb)
+        if (lb_scan) lb_scan_all(d, s_w);
 }
 
 }  // namespace nfgpu

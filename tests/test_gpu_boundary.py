@@ -69,6 +69,31 @@ def test_fanout_bound_error_surfaces_on_outputs(gpu_available, monkeypatch):
     m.close()
 
 
+def test_fanout_bound_error_survives_a_later_capacity_error(gpu_available, monkeypatch):
+    """Two device errors in one frame: k_tick's tiles raise kErrFanBound, then the frame's ranks
+    (k_tick's last tile in this small world, or k_scan_tiles) raise kErrMsgCap (the
+    kAblForceMsgCap hook).  The host-mapped error word keeps one word per bit, so the later error
+    does not hide the earlier one: nfk_outputs_get still fails on the truncated recipient lists and
+    the next nfk_execute refuses to run until nfk_summary_get has reported both."""
+    monkeypatch.setenv("NFGPU_ABLATE", str((1 << 27) | (1 << 29)))
+    w = workload.make_world(n_obj=3000, n_scenes=1, groups_per_scene=4, players_per_group=20, n_ticks=3, seed=8,
+                            ext_frac=0.05)
+    m = kernel.world_from_workload(w)
+    kernel.run_workload(m, w, 0, collect=False)
+    m.synchronize()
+    with pytest.raises(kernel.NFKError) as e:
+        m.outputs_raw()
+    assert e.value.code == -6 and "bound" in str(e.value)
+    with pytest.raises(kernel.NFKError) as e:
+        m.Execute(int(w["tick_time"][1]))
+    assert e.value.code == -6
+    with pytest.raises(kernel.NFKError) as e:
+        m.summary()
+    assert "bound" in str(e.value)
+    m.Execute(int(w["tick_time"][1]))
+    m.close()
+
+
 def test_failed_frame_drops_the_whole_window(gpu_available, monkeypatch):
     """A failure of nfk_execute after the window's membership changes were applied drops every
     queued call of the window (SetProperty, SetRecord, schedule calls alike), so none of them is

@@ -37,6 +37,9 @@ for step in "$@"; do
     bench2g1) NFGPU_BENCH_TRACE=1 run bench2g1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                --master-port 29562 bench.py --gpus 2 --steps 20 --warmup 3 --backend gloo --cpu-baseline off \
                --entities 262144 --groups 1024 --migrate 128 --migrate-every 1 ;;
+    lbab) run lbab 900 tools/ab_env.sh "$TAG/lbab" ${LBR:-4} NFGPU_JIT_LB=1 NFGPU_JIT_LB=0 ;;
+    bench2) NFGPU_BENCH_TRACE=1 run bench2 600 python bench.py --gpus 2 --steps 20 --warmup 3 --backend gloo \
+               --cpu-baseline off --entities 262144 --groups 1024 --migrate 128 ;;
     ntab) run ntab 900 tools/ab_env.sh "$TAG/ntab" 2 ${NTAB:-NFGPU_JIT_NT=0 NFGPU_JIT_NT=16 NFGPU_JIT_NT=17 NFGPU_JIT_NT=24 NFGPU_JIT_NT=20} ;;
     hostprof) NFGPU_TRACE_EXEC=1 run hostprof 300 python tools/host_calls_profile.py ;;
     hbmmix) run hbmmix 120 tools/_bin/hbm_mix ;;
