@@ -78,6 +78,9 @@ def parse():
                         "1 = 1M entities/GPU (the metric's configuration; with --gpus > 1 "
                         "it becomes config[2]: scene shards + migration), 3 = 256 scenes x 64 groups, 2M "
                         "entities, 32 players/group (fan-out dominated), 4 = 500k players x 64-row records")
+    p.add_argument("--other-configs", choices=["auto", "off"], default="auto",
+                   help="config[1], 1 GPU: also run short legs of config[0], config[3] and config[4] (each its own "
+                        "process, same --steps / --warmup) and report them under 'configs'")
     p.add_argument("--backend", default="nccl", help="process group backend (nccl = RCCL; gloo only to rehearse "
                                                      "several ranks on one GPU)")
     return p.parse_args()
@@ -483,10 +486,47 @@ def main():
         out["plugin_frame"] = plugin_frame_run(args, workload)
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0 and world == 1 and args.config == 1 and args.other_configs == "auto" and not args.self_migrate:
+        out["configs"] = other_config_legs(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def other_config_legs(args):
+    """BASELINE config[0], config[3] and config[4] as short legs of the default line: each runs
+    `bench.py --config c` in its own process (same --steps / --warmup, no CPU baseline) and reports its
+    throughput, frame time, dominant kernel and roofline fraction."""
+    legs = {}
+    for c in (0, 3, 4):
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", str(c), "--steps", str(args.steps),
+               "--warmup", str(args.warmup), "--cpu-baseline", "off", "--other-configs", "off"]
+        env = dict(os.environ)
+        for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+            env.pop(k, None)
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+        except subprocess.TimeoutExpired:
+            legs[f"config{c}"] = {"error": "timeout"}
+            continue
+        line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode != 0 or not line:
+            legs[f"config{c}"] = {"error": (r.stderr or r.stdout)[-400:]}
+            continue
+        d = json.loads(line[-1])
+        rf = d["roofline"]
+        legs[f"config{c}"] = {
+            "value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "steps": d["steps"],
+            "warmup": d["warmup"], "workload": d["config"]["workload"],
+            "entities_per_gpu": d["config"]["entities_per_gpu"],
+            "dominant_kernel": {"name": rf["kernel"], "avg_us": d["kernels"][rf["kernel"]]["avg_us"],
+                                "alg_bytes_per_launch": d["kernels"][rf["kernel"]]["alg_bytes_per_launch"]},
+            "kernels": {k: round(v["avg_us"], 2) for k, v in d["kernels"].items()},
+            "roofline": {"achieved": rf["achieved"], "peak": rf["peak"], "unit": rf["unit"], "frac": rf["frac"],
+                         "traffic": rf["traffic"], "traffic_source": rf["traffic_source"]},
+            "per_frame": d["per_frame"]}
+    return legs
 
 
 def plugin_frame_run(args, workload):
