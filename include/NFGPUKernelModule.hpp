@@ -184,6 +184,11 @@ public:
     void AddHeartBeatProgram(const std::string& name, const std::vector<nfk_op>& ops,
                              const std::vector<std::string>& props, const std::vector<std::string>& records = {});
     int PropertyId(const std::string& name) const;
+    // whether a schedule name has a device program (AddHeartBeatProgram, before or after AfterInit)
+    bool HasHeartBeat(const std::string& name) const;
+    // properties of one type (device ids: int [0, n_int), float [n_int, n_int + n_flt), object after)
+    int PropertyCount(TDATA_TYPE type) const;
+    int RecordId(const std::string& name) const { return record_id_.at(name); }
 
     // ---- NFIModule lifecycle ----
     bool Init();

@@ -8,10 +8,34 @@
 //                         records of the class schema live on the device (nfgpu::NFGPUKernelModule);
 //                         strings, vectors, object lists, scenes and class events stay in the host
 //                         NFCKernelModule.  The schema is read from NFIClassModule in AfterInit.
-//   NFGPUScheduleAdapter  NFIScheduleModule (NFIScheduleModule.h:23-39): object schedules on the
-//                         device, module schedules on the host.
+//                         The host objects stay a mirror of the device ones (below), so per-object
+//                         callbacks and direct NFIObject / NFIRecord access keep working.
+//   NFGPUScheduleAdapter  NFIScheduleModule (NFIScheduleModule.h:23-39): object schedules whose name
+//                         has a device program on the device; every other schedule (functor-only
+//                         heartbeats, module schedules) on the reference's own NFCScheduleModule.
+//
+// Host objects as a mirror of the device (NFIKernelModule.h:28-45 AddPropertyCallBack /
+// AddRecordCallBack register on the host NFCObject's NFCProperty / NFCRecord, NFCProperty.h:71):
+//   * every write to a device property or int record cell goes to the HOST object first — through
+//     NFIKernelModule (SetPropertyInt / Float / Object, SetRecordInt, ClearRecord) or straight
+//     through the object (GetObject(self)->SetPropertyInt, FindRecord(self, r)->SetInt / AddRow /
+//     Remove) — so the reference's change predicates and per-object callbacks run at call time as in
+//     the reference; the host common event of that write is forwarded to the device (queued there)
+//     instead of reaching the common callbacks;
+//   * the common callbacks (the AOI module's client sync) receive the device's coalesced frame
+//     events (the dirty-sync list), exactly as before;
+//   * when Execute returns, every (object, property) and int cell that had a device event or a host
+//     write this window is read back from the device and written into the host object where it
+//     differs: the heartbeat programs' effects reach GetObject(self)->Get* and fire the per-object
+//     callbacks (old = the host value, new = the device value).
+//   f64 record cells are the exception: NFCRecord::SetFloat stores a double into the int64 alternative
+//   of the cell (RC:243-297; tests/test_oracle.py::test_reference_record_setfloat_bug), so they are
+//   device-only (SetRecordFloat / GetRecordFloat through NFIKernelModule read and write the device).
 //   NFGPUKernelPlugin     the NFIPlugin that registers both (NFKernelPlugin.cpp:40-46 pattern).
+#include <algorithm>
 #include <cstring>
+#include <stdexcept>
+#include <tuple>
 #include <map>
 #include <memory>
 #include <set>
@@ -20,6 +44,7 @@
 
 #include "NFComm/NFKernelPlugin/NFCEventModule.h"
 #include "NFComm/NFKernelPlugin/NFCKernelModule.h"
+#include "NFComm/NFKernelPlugin/NFCScheduleModule.h"
 #include "NFComm/NFKernelPlugin/NFCSceneAOIModule.h"
 #include "NFComm/NFMessageDefine/NFProtocolDefine.hpp"
 #include "NFComm/NFPluginModule/NFIClassModule.h"
@@ -97,12 +122,46 @@ public:
             MirrorObject(o);
             MirrorRecords(o);
         }
+        // host writes of device state -> the device (first in the host common lists: the modules
+        // register their common callbacks in their own AfterInit, after this one)
+        NFCKernelModule::RegisterCommonPropertyEvent(PROPERTY_EVENT_FUNCTOR_PTR(new PROPERTY_EVENT_FUNCTOR(
+            [this](const NFGUID& self, const std::string& name, const NFIDataList::TData&, const NFIDataList::TData& v) {
+                return ForwardProperty(self, name, v);
+            })));
+        NFCKernelModule::RegisterCommonRecordEvent(RECORD_EVENT_FUNCTOR_PTR(new RECORD_EVENT_FUNCTOR(
+            [this](const NFGUID& self, const RECORD_EVENT_DATA& ev, const NFIDataList::TData&, const NFIDataList::TData&) {
+                return ForwardRecord(self, ev);
+            })));
+        // the device's frame events -> the common callbacks, and their (object, property / cell) to
+        // the host mirror when Execute returns
+        gpu_.RegisterCommonPropertyEvent(
+            [this](const nfgpu::NFGUID& self, const std::string& name, const nfgpu::TData& a, const nfgpu::TData& b) {
+                const NFGUID s = to_ref(self);
+                for (auto& cb : prop_cb_) (*cb)(s, name, to_ref(a), to_ref(b));
+                sync_props_.emplace_back(s, name);
+                return 0;
+            });
+        gpu_.RegisterCommonRecordEvent(
+            [this](const nfgpu::NFGUID& self, const nfgpu::RECORD_EVENT_DATA& e, const nfgpu::TData& a, const nfgpu::TData& b) {
+                RECORD_EVENT_DATA ev;
+                ev.nOpType = (RECORD_EVENT_DATA::RecordOptype)e.nOpType;
+                ev.nRow = e.nRow;
+                ev.nCol = e.nCol;
+                ev.strRecordName = e.strRecordName;
+                const NFGUID s = to_ref(self);
+                for (auto& cb : rec_cb_) (*cb)(s, ev, to_ref(a), to_ref(b));
+                if (e.nOpType == nfgpu::RECORD_EVENT_DATA::Update && b.type == nfgpu::TDATA_INT)
+                    sync_cells_.push_back({s, e.strRecordName, e.nRow, e.nCol});
+                return 0;
+            });
         return gpu_.AfterInit();
     }
 
     bool Execute() override {  // NFCKernelModule::Execute (KM:70) + NFCScheduleModule::Execute (SM:49) + AOI fan-out
         NFCKernelModule::Execute();
-        return gpu_.Execute();
+        const bool ok = gpu_.Execute();
+        SyncHostObjects();
+        return ok;
     }
 
     bool CreateScene(const int nSceneID) override {  // KM:981
@@ -136,17 +195,9 @@ public:
         return ok;
     }
 
-    bool SetPropertyInt(const NFGUID& self, const std::string& name, const NFINT64 v) override {  // KM:323
-        return DevProp(self, name) ? gpu_.SetPropertyInt(to_gpu(self), name, v) : NFCKernelModule::SetPropertyInt(self, name, v);
-    }
-    bool SetPropertyFloat(const NFGUID& self, const std::string& name, const double v) override {  // KM:336
-        return DevProp(self, name) ? gpu_.SetPropertyFloat(to_gpu(self), name, v)
-                                      : NFCKernelModule::SetPropertyFloat(self, name, v);
-    }
-    bool SetPropertyObject(const NFGUID& self, const std::string& name, const NFGUID& v) override {  // KM:362
-        return DevProp(self, name) ? gpu_.SetPropertyObject(to_gpu(self), name, to_gpu(v))
-                                      : NFCKernelModule::SetPropertyObject(self, name, v);
-    }
+    // SetPropertyInt / Float / Object, SetRecordInt (by column and by tag), ClearRecord: the
+    // reference's own NFCKernelModule on the host object (KM:323-372, 492-544); ForwardProperty /
+    // ForwardRecord queue the accepted writes on the device.
     NFINT64 GetPropertyInt(const NFGUID& self, const std::string& name) override {  // KM:401, read-your-writes
         return DevProp(self, name) ? gpu_.GetPropertyInt(to_gpu(self), name) : NFCKernelModule::GetPropertyInt(self, name);
     }
@@ -158,29 +209,14 @@ public:
         obj_scratch_ = to_ref(gpu_.GetPropertyObject(to_gpu(self), name));
         return obj_scratch_;
     }
-
-    bool ClearRecord(const NFGUID& self, const std::string& rec) override {  // KM:492
-        return DevRecord(self, rec) ? gpu_.ClearRecord(to_gpu(self), rec) : NFCKernelModule::ClearRecord(self, rec);
-    }
-    bool SetRecordInt(const NFGUID& self, const std::string& rec, const int nRow, const int nCol,
-                      const NFINT64 v) override {  // KM:505
-        return DevRecord(self, rec) ? gpu_.SetRecordInt(to_gpu(self), rec, nRow, nCol, v)
-                                       : NFCKernelModule::SetRecordInt(self, rec, nRow, nCol, v);
-    }
+    // f64 record cells: device only (see the header)
     bool SetRecordFloat(const NFGUID& self, const std::string& rec, const int nRow, const int nCol,
                         const double v) override {  // KM:545
         return DevRecord(self, rec) ? gpu_.SetRecordFloat(to_gpu(self), rec, nRow, nCol, v)
                                        : NFCKernelModule::SetRecordFloat(self, rec, nRow, nCol, v);
     }
-    // the column-tag forms (NFIKernelModule.h:127-128, KM:525): NFCRecord::GetCol of the tag
-    bool SetRecordInt(const NFGUID& self, const std::string& rec, const int nRow, const std::string& tag,
-                      const NFINT64 v) override {
-        if (!DevRecord(self, rec)) return NFCKernelModule::SetRecordInt(self, rec, nRow, tag, v);
-        const int c = ColOf(rec, tag);
-        return c >= 0 && gpu_.SetRecordInt(to_gpu(self), rec, nRow, c, v);
-    }
     bool SetRecordFloat(const NFGUID& self, const std::string& rec, const int nRow, const std::string& tag,
-                        const double v) override {
+                        const double v) override {  // NFIKernelModule.h:128
         if (!DevRecord(self, rec)) return NFCKernelModule::SetRecordFloat(self, rec, nRow, tag, v);
         const int c = ColOf(rec, tag);
         return c >= 0 && gpu_.SetRecordFloat(to_gpu(self), rec, nRow, c, v);
@@ -206,7 +242,12 @@ public:
 
     bool SwitchScene(const NFGUID& self, const int scene, const int group, const float fX, const float fY,
                      const float fZ, const float fOrient, const NFIDataList& arg) override {  // NFIKernelModule.h:148
-        NFCKernelModule::SwitchScene(self, scene, group, fX, fY, fZ, fOrient, arg);  // host-side scene lists
+        // the host-side scene lists and the host object's SceneID / GroupID / X / Y / Z writes
+        // (KM:930-942: its per-object callbacks fire here); the device queues the same writes with
+        // the membership change itself, so they are not forwarded
+        ++quiet_;
+        NFCKernelModule::SwitchScene(self, scene, group, fX, fY, fZ, fOrient, arg);
+        --quiet_;
         return gpu_.SwitchScene(to_gpu(self), scene, group, fX, fY, fZ, fOrient);
     }
 
@@ -223,10 +264,8 @@ protected:
                 return DevProp(self, name) ? 0 : (*cb)(self, name, a, b);
             }));
         NFCKernelModule::RegisterCommonPropertyEvent(host);
-        return gpu_.RegisterCommonPropertyEvent(
-            [cb](const nfgpu::NFGUID& self, const std::string& name, const nfgpu::TData& a, const nfgpu::TData& b) {
-                return (*cb)(to_ref(self), name, to_ref(a), to_ref(b));
-            });
+        prop_cb_.push_back(cb);
+        return true;
     }
     bool RegisterCommonRecordEvent(const RECORD_EVENT_FUNCTOR_PTR& cb) override {
         RECORD_EVENT_FUNCTOR_PTR host(new RECORD_EVENT_FUNCTOR(
@@ -234,18 +273,170 @@ protected:
                 return DevRecord(self, ev.strRecordName) ? 0 : (*cb)(self, ev, a, b);
             }));
         NFCKernelModule::RegisterCommonRecordEvent(host);
-        return gpu_.RegisterCommonRecordEvent(
-            [cb](const nfgpu::NFGUID& self, const nfgpu::RECORD_EVENT_DATA& e, const nfgpu::TData& a, const nfgpu::TData& b) {
-                RECORD_EVENT_DATA ev;
-                ev.nOpType = (RECORD_EVENT_DATA::RecordOptype)e.nOpType;
-                ev.nRow = e.nRow;
-                ev.nCol = e.nCol;
-                ev.strRecordName = e.strRecordName;
-                return (*cb)(to_ref(self), ev, to_ref(a), to_ref(b));
-            });
+        rec_cb_.push_back(cb);
+        return true;
     }
 
 private:
+    struct Cell {
+        NFGUID self;
+        std::string rec;
+        int row, col;
+    };
+
+    // an accepted host write of a device property (NFCProperty::SetInt / SetFloat / SetObject raised
+    // the common event): queued on the device in call order
+    int ForwardProperty(const NFGUID& self, const std::string& name, const NFIDataList::TData& v) {
+        if (quiet_ || !DevProp(self, name)) return 0;
+        const nfgpu::NFGUID g = to_gpu(self);
+        if (v.GetType() == TDATA_INT) gpu_.SetPropertyInt(g, name, v.GetInt());
+        else if (v.GetType() == TDATA_FLOAT) gpu_.SetPropertyFloat(g, name, v.GetFloat());
+        else if (v.GetType() == TDATA_OBJECT) gpu_.SetPropertyObject(g, name, to_gpu(v.GetObject()));
+        else return 0;
+        sync_props_.emplace_back(self, name);
+        return 0;
+    }
+    // an accepted host write of a device record (NFCRecord's Update / Add / Cover / Del events,
+    // RC:170-177, 225-231, 1092-1098): the same call queued on the device
+    int ForwardRecord(const NFGUID& self, const RECORD_EVENT_DATA& ev) {
+        if (quiet_ || !DevRecord(self, ev.strRecordName)) return 0;
+        NF_SHARE_PTR<NFIRecord> r = NFCKernelModule::FindRecord(self, ev.strRecordName);
+        if (!r) return 0;
+        const nfgpu::NFGUID g = to_gpu(self);
+        switch (ev.nOpType) {
+            case RECORD_EVENT_DATA::Update:
+                // (an f64 cell written on the host holds the double in the int64 alternative and
+                // cannot be read back: f64 record cells are device-only)
+                if (r->GetColType(ev.nCol) == TDATA_INT) {
+                    gpu_.SetRecordInt(g, ev.strRecordName, ev.nRow, ev.nCol, r->GetInt(ev.nRow, ev.nCol));
+                    sync_cells_.push_back({self, ev.strRecordName, ev.nRow, ev.nCol});
+                }
+                break;
+            case RECORD_EVENT_DATA::Add:
+            case RECORD_EVENT_DATA::Cover: {  // the row as AddRow left it (values already stored)
+                std::vector<nfgpu::TData> vals((size_t)r->GetCols());
+                for (int c = 0; c < r->GetCols(); c++) {
+                    vals[c].type = to_gpu(r->GetColType(c));
+                    if (vals[c].type == nfgpu::TDATA_INT) vals[c].i = r->GetInt(ev.nRow, c);
+                    else vals[c].f = r->GetFloat(ev.nRow, c);
+                }
+                gpu_.AddRow(g, ev.strRecordName, ev.nRow, vals);
+                break;
+            }
+            case RECORD_EVENT_DATA::Del:  // raised while the row is still used (RC:1092)
+                gpu_.RemoveRow(g, ev.strRecordName, ev.nRow);
+                break;
+            default:  // Swap / Sort / Create / Cleared: no device counterpart
+                break;
+        }
+        return 0;
+    }
+
+    // When Execute returns: the device values of the window's written and evented properties and
+    // int cells, written into the host objects where they differ (one batched device read each);
+    // the host NFCProperty / NFCRecord then fires the per-object callbacks for the difference.
+    void SyncHostObjects() {
+        std::vector<std::pair<NFGUID, std::string>> props;
+        props.swap(sync_props_);
+        std::vector<Cell> cells;
+        cells.swap(sync_cells_);
+        std::sort(props.begin(), props.end());
+        props.erase(std::unique(props.begin(), props.end()), props.end());
+        std::vector<int64_t> gh, gd, oh;
+        std::vector<int32_t> pid;
+        std::vector<uint64_t> val;
+        std::vector<size_t> at;  // props index of each device read
+        for (size_t i = 0; i < props.size(); i++) {
+            if (!DevProp(props[i].first, props[i].second)) continue;  // (destroyed / left the shard)
+            at.push_back(i);
+            gh.push_back(props[i].first.nHead64);
+            gd.push_back(props[i].first.nData64);
+            pid.push_back(gpu_.PropertyId(props[i].second));
+        }
+        if (!at.empty()) {
+            // int / f64 words, and the object columns' NFGUIDs (nfk_get_props refuses those)
+            std::vector<size_t> w, o;
+            for (size_t k = 0; k < at.size(); k++) (pid[k] < ObjectBase() ? w : o).push_back(k);
+            val.assign(at.size(), 0);
+            oh.assign(at.size(), 0);
+            auto gather = [&](const std::vector<size_t>& ks, bool obj) {
+                if (ks.empty()) return;
+                std::vector<int64_t> h(ks.size()), d(ks.size()), vh(ks.size()), vd(ks.size());
+                std::vector<int32_t> p(ks.size());
+                std::vector<uint64_t> v(ks.size());
+                for (size_t j = 0; j < ks.size(); j++) {
+                    h[j] = gh[ks[j]];
+                    d[j] = gd[ks[j]];
+                    p[j] = pid[ks[j]];
+                }
+                const int rc = obj ? nfk_get_objects(gpu_.World(), (int32_t)ks.size(), h.data(), d.data(), p.data(), vh.data(), vd.data())
+                                   : nfk_get_props(gpu_.World(), (int32_t)ks.size(), h.data(), d.data(), p.data(), v.data());
+                if (rc != NFK_OK) throw std::runtime_error(std::string("host mirror read: ") + nfk_last_error());
+                for (size_t j = 0; j < ks.size(); j++) {
+                    val[ks[j]] = obj ? (uint64_t)vd[j] : v[j];
+                    oh[ks[j]] = obj ? vh[j] : 0;
+                }
+            };
+            gather(w, false);
+            gather(o, true);
+        }
+        ++quiet_;
+        for (size_t k = 0; k < at.size(); k++) {
+            const NFGUID& self = props[at[k]].first;
+            const std::string& name = props[at[k]].second;
+            NF_SHARE_PTR<NFIObject> ob = GetElement(self);
+            NF_SHARE_PTR<NFIProperty> p = ob ? ob->GetPropertyManager()->GetElement(name) : nullptr;
+            if (!p) continue;
+            if (p->GetType() == TDATA_INT) {
+                if (p->GetInt() != (NFINT64)val[k]) p->SetInt((NFINT64)val[k]);
+            } else if (p->GetType() == TDATA_FLOAT) {
+                double v;
+                memcpy(&v, &val[k], 8);
+                const double h = p->GetFloat();
+                if (memcmp(&h, &v, 8) != 0 && !p->SetFloat(v)) {
+                    // (a coalesced change within NFCProperty::SetFloat's 1e-15, PR:314: stored as is)
+                    NFIDataList::TData t;
+                    t.SetFloat(v);
+                    p->SetValue(t);
+                }
+            } else if (p->GetType() == TDATA_OBJECT) {
+                const NFGUID v(oh[k], (int64_t)val[k]);
+                if (p->GetObject() != v) p->SetObject(v);
+            }
+        }
+        // int record cells
+        std::sort(cells.begin(), cells.end(), [](const Cell& a, const Cell& b) {
+            return std::tie(a.self, a.rec, a.row, a.col) < std::tie(b.self, b.rec, b.row, b.col);
+        });
+        cells.erase(std::unique(cells.begin(), cells.end(), [](const Cell& a, const Cell& b) {
+            return a.self == b.self && a.rec == b.rec && a.row == b.row && a.col == b.col;
+        }), cells.end());
+        std::vector<int64_t> ch, cd;
+        std::vector<int32_t> cr, crow, ccol;
+        std::vector<const Cell*> live;
+        for (const Cell& c : cells) {
+            if (!DevRecord(c.self, c.rec)) continue;
+            live.push_back(&c);
+            ch.push_back(c.self.nHead64);
+            cd.push_back(c.self.nData64);
+            cr.push_back(gpu_.RecordId(c.rec));
+            crow.push_back(c.row);
+            ccol.push_back(c.col);
+        }
+        if (!live.empty()) {
+            std::vector<uint64_t> cv(live.size());
+            if (nfk_get_records(gpu_.World(), (int32_t)live.size(), ch.data(), cd.data(), cr.data(), crow.data(),
+                                ccol.data(), cv.data()) != NFK_OK)
+                throw std::runtime_error(std::string("host mirror read: ") + nfk_last_error());
+            for (size_t k = 0; k < live.size(); k++) {
+                NF_SHARE_PTR<NFIRecord> r = NFCKernelModule::FindRecord(live[k]->self, live[k]->rec);
+                if (r && r->IsUsed(live[k]->row) && r->GetInt(live[k]->row, live[k]->col) != (NFINT64)cv[k])
+                    r->SetInt(live[k]->row, live[k]->col, (NFINT64)cv[k]);
+            }
+        }
+        --quiet_;
+    }
+
     // the host object's device properties as the device object's creation-time values
     void MirrorObject(const NF_SHARE_PTR<NFIObject>& o) {
         std::map<std::string, nfgpu::TData> init;
@@ -304,50 +495,67 @@ private:
         auto c = r->second.find(tag);
         return c == r->second.end() ? -1 : c->second;
     }
+    int ObjectBase() const {  // the first object property id (int, then float, then object ids)
+        return gpu_.PropertyCount(nfgpu::TDATA_INT) + gpu_.PropertyCount(nfgpu::TDATA_FLOAT);
+    }
 
     NFIClassModule* m_pClassModule = nullptr;
     std::set<std::string> dev_props_, dev_records_;
     std::map<std::string, std::map<std::string, int>> col_tags_;
     std::set<int> scenes_;
     NFGUID obj_scratch_;
+    int quiet_ = 0;  // > 0: host writes are the adapter's own (mirror, SwitchScene), not forwarded
+    std::vector<PROPERTY_EVENT_FUNCTOR_PTR> prop_cb_;
+    std::vector<RECORD_EVENT_FUNCTOR_PTR> rec_cb_;
+    std::vector<std::pair<NFGUID, std::string>> sync_props_;  // this window's written / evented pairs
+    std::vector<Cell> sync_cells_;
 };
 
 class NFGPUScheduleAdapter : public NFIScheduleModule {
 public:
-    explicit NFGPUScheduleAdapter(NFIPluginManager* p) { pPluginManager = p; }
+    explicit NFGPUScheduleAdapter(NFIPluginManager* p) : host_(p) { pPluginManager = p; }
+    bool Init() override { return host_.Init(); }
 
-    // ---- module schedules (NFIScheduleModule.h:23-25) ----
+    // ---- module schedules (NFIScheduleModule.h:23-25): the reference's own NFCScheduleModule ----
     bool AddSchedule(const std::string& name, const MODULE_SCHEDULE_FUNCTOR_PTR& cb, const float fTime,
                      const int nCount) override {
-        return gpu().AddSchedule(name,
-                                 [cb](const std::string& n, const float t, const int c) { return (*cb)(n, t, c); },
-                                 fTime, nCount);
+        return host_.AddSchedule(name, cb, fTime, nCount);
     }
-    bool RemoveSchedule(const std::string& name) override { return gpu().RemoveSchedule(name); }
-    bool ExistSchedule(const std::string& name) override { return gpu().ExistSchedule(name); }
+    bool RemoveSchedule(const std::string& name) override { return host_.RemoveSchedule(name); }
+    bool ExistSchedule(const std::string& name) override { return host_.ExistSchedule(name); }
 
-    // ---- object schedules (NFIScheduleModule.h:36-39) ----
+    // ---- object schedules (NFIScheduleModule.h:36-39): a name with a device program runs on the
+    // device (its functor after the device frame); any other name — a functor-only heartbeat such as
+    // Tutorial3's OnHeartBeat (HelloWorld3Module.cpp:47) — on the host NFCScheduleModule, whose
+    // Execute runs at this module's Execute as in the reference ----
     bool AddSchedule(const NFGUID self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR_PTR& cb,
                      const float fTime, const int nCount) override {  // SM:257
+        if (!gpu().HasHeartBeat(name)) return host_.AddSchedule(self, name, cb, fTime, nCount);
         return gpu().AddSchedule(
             to_gpu(self), name,
             [cb](const nfgpu::NFGUID& g, const std::string& n, const float t, const int c) { return (*cb)(to_ref(g), n, t, c); },
             fTime, nCount);
     }
-    bool RemoveSchedule(const NFGUID self) override { return gpu().RemoveSchedule(to_gpu(self)); }  // SM:240
-    bool RemoveSchedule(const NFGUID self, const std::string& name) override {                       // SM:245
-        return gpu().RemoveSchedule(to_gpu(self), name);
+    bool RemoveSchedule(const NFGUID self) override {  // SM:240
+        const bool d = gpu().RemoveSchedule(to_gpu(self));
+        const bool h = host_.RemoveSchedule(self);
+        return d || h;
+    }
+    bool RemoveSchedule(const NFGUID self, const std::string& name) override {  // SM:245
+        return gpu().HasHeartBeat(name) ? gpu().RemoveSchedule(to_gpu(self), name) : host_.RemoveSchedule(self, name);
     }
     bool ExistSchedule(const NFGUID self, const std::string& name) override {  // SM:276
-        return gpu().ExistSchedule(to_gpu(self), name);
+        return gpu().HasHeartBeat(name) ? gpu().ExistSchedule(to_gpu(self), name) : host_.ExistSchedule(self, name);
     }
-    // the frame (object and module schedules) runs in NFGPUKernelAdapter::Execute
-    bool Execute() override { return true; }
+    // the device frame (its object schedules) runs in NFGPUKernelAdapter::Execute; the host
+    // schedules here
+    bool Execute() override { return host_.Execute(); }
 
 private:
     nfgpu::NFGPUKernelModule& gpu() {
         return dynamic_cast<NFGPUKernelAdapter*>(pPluginManager->FindModule<NFIKernelModule>())->gpu_;
     }
+    NFCScheduleModule host_;
 };
 
 class NFGPUKernelPlugin : public NFIPlugin {

@@ -115,6 +115,19 @@ static void resolve_program(std::vector<nfk_op>& ops, const std::vector<std::str
     }
 }
 
+bool NFGPUKernelModule::HasHeartBeat(const std::string& name) const {
+    if (committed_) return hb_id_.count(name) != 0;
+    for (const HeartBeatDef& h : heartbeats_)
+        if (h.name == name) return true;
+    return false;
+}
+
+int NFGPUKernelModule::PropertyCount(TDATA_TYPE type) const {
+    int n = 0;
+    for (const PropertyDef& p : props_) n += p.type == type;
+    return n;
+}
+
 // property ids on the device: int properties first, then float ones, then object ones, each in
 // definition order
 int NFGPUKernelModule::PropertyId(const std::string& name) const {

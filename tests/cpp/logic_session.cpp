@@ -1,0 +1,524 @@
+// logic_session.cpp — game logic written against the reference's plugin interfaces, run on two
+// servers and logged the same way, so tests/test_logic_session.py can compare them frame by frame:
+//
+//   LOGIC_REF   the reference's own NFCKernelModule + NFCScheduleModule (with NFCSceneAOIModule,
+//               NFCEventModule, NFCClassModule, NFCElementModule), compiled from /root/reference
+//               where they lie — the heartbeat effect programs run as functors through
+//               NFIKernelModule (as oracle/ref_session.cpp does);
+//   (default)   the reference-side GPU plugin (integration/NFGPUKernelPlugin.cpp: NFGPUKernelAdapter +
+//               NFGPUScheduleAdapter) in the same modules' place — the programs run on the device.
+//
+// The logic uses what the reference's game modules use beyond the frame path:
+//   * Tutorial3's own sequence (Tutorial/Tutorial3/HelloWorld3Module.cpp:40-110, restated): a class
+//     callback on Player that, at COE_CREATE_HASDATA, registers an object event callback and a
+//     functor-only heartbeat AddSchedule(self, "OnHeartBeat", 5.0f, 10); the object NFGUID(0, 10)
+//     with the dynamic properties Hello (string) and World (int), per-object callbacks on both,
+//     pObject->SetPropertyString / SetPropertyInt, and DoEvent(self, 1, [int, string]) whose
+//     handler calls SetPropertyInt / SetPropertyString through NFIKernelModule — once at start and
+//     once per frame;
+//   * per-object callbacks (NFIKernelModule::AddPropertyCallBack / AddRecordCallBack,
+//     NFIKernelModule.h:28-45) on every workload object's HP, MP, X, TargetX, Gold, Level and rec0;
+//   * the workload's window calls split between NFIKernelModule (SetProperty*, SetRecordInt,
+//     ClearRecord) and the objects themselves (GetObject(self)->SetProperty*,
+//     FindRecord(self, r)->SetInt / AddRow / Remove), read-modify-write Sets included; schedule
+//     calls; DestroyObject and CreateObject after start.
+//
+// Logged per frame t: per-object property and record callbacks with the phase they fired in (0 =
+// the window's calls, 1 = Execute), the heartbeat functors, Tutorial3's callback lines, and every
+// object's device properties and rec0 int cells read through the HOST objects
+// (GetObject(self)->GetProperty*, FindRecord(self, r)->GetInt) and through NFIKernelModule.
+//
+// TEST INFRASTRUCTURE ONLY.  usage: logic_session <workload.nfio> <out.nfio>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <string>
+#include <vector>
+
+#ifdef LOGIC_REF
+#include "NFComm/NFKernelPlugin/NFCEventModule.h"
+#include "NFComm/NFKernelPlugin/NFCKernelModule.h"
+#include "NFComm/NFKernelPlugin/NFCScheduleModule.h"
+#include "NFComm/NFKernelPlugin/NFCSceneAOIModule.h"
+#else
+#include "../../integration/NFGPUKernelPlugin.cpp"
+#endif
+#include "NFComm/NFConfigPlugin/NFCClassModule.h"
+#include "NFComm/NFConfigPlugin/NFCElementModule.h"
+#include "NFComm/NFMessageDefine/NFProtocolDefine.hpp"
+#include "../../oracle/nfio.h"
+#include "../../oracle/ref_server.hpp"
+
+// NFGetTime() (NFPlatform.h:367) reads CLOCK_REALTIME: the session's virtual clock, so both servers'
+// schedules (NFCScheduleModule's and the device's) see the workload's call and frame times
+extern "C" int clock_gettime(clockid_t clk, struct timespec* ts) {
+    if (clk == CLOCK_REALTIME) {
+        ts->tv_sec = g_now / 1000;
+        ts->tv_nsec = (g_now % 1000) * 1000000;
+        return 0;
+    }
+    return (int)syscall(SYS_clock_gettime, clk, ts);
+}
+
+static std::string cstr(const uint8_t* p) { return std::string((const char*)p, strnlen((const char*)p, 32)); }
+static uint64_t dbits(double d) {
+    uint64_t u;
+    memcpy(&u, &d, 8);
+    return u;
+}
+static double bitsd(uint64_t u) {
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+}
+
+struct Logic {
+    NFIKernelModule* km = nullptr;
+    NFIScheduleModule* sm = nullptr;
+    NFIEventModule* em = nullptr;
+    std::map<std::string, int> pid, kid;
+    std::map<NFGUID, int> obj;
+    int ni = 0, phase = 0, frame = -1;
+    // per-object callbacks: (phase, obj, pid, old, new) / (phase, obj, rrc, old, new)
+    std::vector<int32_t> pc_phase, pc_obj, pc_pid, rc_phase, rc_obj;
+    std::vector<uint32_t> rc_rrc;
+    std::vector<uint64_t> pc_old, pc_new, rc_old, rc_new;
+    std::vector<int32_t> fi_obj, fi_kind, fi_rem;
+    std::string t3;  // Tutorial3's callback lines
+    void clear() {
+        for (auto* v : {&pc_phase, &pc_obj, &pc_pid, &rc_phase, &rc_obj, &fi_obj, &fi_kind, &fi_rem}) v->clear();
+        rc_rrc.clear();
+        for (auto* v : {&pc_old, &pc_new, &rc_old, &rc_new}) v->clear();
+        t3.clear();
+    }
+    int ObjOf(const NFGUID& g) const {
+        auto it = obj.find(g);
+        return it == obj.end() ? -1 : it->second;
+    }
+
+    // ---- per-object callbacks on the workload objects ----
+    int OnObjProp(const NFGUID& self, const std::string& name, const NFIDataList::TData& a, const NFIDataList::TData& b) {
+        const int p = pid.at(name);
+        pc_phase.push_back(phase);
+        pc_obj.push_back(ObjOf(self));
+        pc_pid.push_back(p);
+        pc_old.push_back(p < ni ? (uint64_t)a.GetInt() : dbits(a.GetFloat()));
+        pc_new.push_back(p < ni ? (uint64_t)b.GetInt() : dbits(b.GetFloat()));
+        return 0;
+    }
+    int OnObjRecord(const NFGUID& self, const RECORD_EVENT_DATA& ev, const NFIDataList::TData& a, const NFIDataList::TData& b) {
+        const uint32_t op = ev.nOpType == RECORD_EVENT_DATA::Add ? 1u : ev.nOpType == RECORD_EVENT_DATA::Del ? 2u
+                          : ev.nOpType == RECORD_EVENT_DATA::Cover ? 3u : 0u;
+        rc_phase.push_back(phase);
+        rc_obj.push_back(ObjOf(self));
+        rc_rrc.push_back((op << 24) | ((uint32_t)std::stoi(ev.strRecordName.substr(3)) << 16) | ((uint32_t)ev.nRow << 8) |
+                         (uint32_t)ev.nCol);
+        rc_old.push_back(op ? 0 : (uint64_t)a.GetInt());
+        rc_new.push_back(op ? 0 : (uint64_t)b.GetInt());
+        return 0;
+    }
+    void Watch(const NFGUID& g) {
+        for (const char* n : {"HP", "MP", "X", "TargetX", "Gold", "Level"}) km->AddPropertyCallBack(g, n, this, &Logic::OnObjProp);
+        km->AddRecordCallBack(g, "rec0", this, &Logic::OnObjRecord);
+    }
+    // the heartbeat functor's log (both servers); the effect runs in Effect (reference) or on the device
+    void Fired(const NFGUID& self, const std::string& name, int nCount) {
+        fi_obj.push_back(ObjOf(self));
+        fi_kind.push_back(kid.at(name));
+        fi_rem.push_back(nCount);
+    }
+
+    // ---- Tutorial3 (HelloWorld3Module.cpp, restated) ----
+    void Line(const std::string& s) { t3 += std::to_string(frame) + " " + s + "\n"; }
+    int OnEvent(const NFGUID& self, const NFEventDefine event, const NFIDataList& arg) {  // :13-22
+        Line("OnEvent " + std::to_string((int)event) + " " + std::to_string(self.nData64) + " " +
+             std::to_string(arg.Int(0)) + " " + arg.String(1));
+        const bool a = km->SetPropertyInt(self, "Hello", arg.Int(0));  // (a string property: refused)
+        const bool b = km->SetPropertyString(self, "Hello", arg.String(1));
+        Line(std::string("OnEvent sets ") + (a ? "1" : "0") + (b ? "1" : "0"));
+        return 0;
+    }
+    int OnHeartBeat(const NFGUID& self, const std::string& name, const float fTime, const int nCount) {  // :24-34
+        Line("OnHeartBeat " + std::to_string(self.nHead64) + "-" + std::to_string(self.nData64) + " " + name + " " +
+             std::to_string(fTime) + " " + std::to_string(nCount));
+        return 0;
+    }
+    int OnClassEvent(const NFGUID& self, const std::string& cls, const CLASS_OBJECT_EVENT event, const NFIDataList&) {  // :36-50
+        Line("OnClassCallBackEvent " + cls + " " + std::to_string(self.nData64) + " " + std::to_string((int)event));
+        if (event == COE_CREATE_HASDATA) {
+            em->AddEventCallBack(self, NFEventDefine(1), this, &Logic::OnEvent);
+            sm->AddSchedule(self, "OnHeartBeat", this, &Logic::OnHeartBeat, 5.0f, 10);
+        }
+        return 0;
+    }
+    int OnWorld(const NFGUID& self, const std::string& name, const NFIDataList::TData& a, const NFIDataList::TData& b) {  // :52-58
+        Line("OnPropertyCallBackEvent " + std::to_string(self.nData64) + " " + name + " " + std::to_string(a.GetInt()) +
+             " " + std::to_string(b.GetInt()));
+        return 0;
+    }
+    int OnHello(const NFGUID& self, const std::string& name, const NFIDataList::TData& a, const NFIDataList::TData& b) {  // :60-66
+        Line("OnPropertyStrCallBackEvent " + std::to_string(self.nData64) + " " + name + " " + a.GetString() + " " +
+             b.GetString());
+        return 0;
+    }
+    NFGUID t3_self;
+    bool Tutorial3(int scene) {  // HelloWorld3Module::AfterInit (:68-100)
+        km->AddClassCallBack(NFrame::Player::ThisName(), this, &Logic::OnClassEvent);
+        NF_SHARE_PTR<NFIObject> o = km->CreateObject(NFGUID(0, 10), scene, 0, NFrame::Player::ThisName(), "", NFCDataList());
+        if (!o) return false;
+        t3_self = o->Self();
+        o->GetPropertyManager()->AddProperty(o->Self(), "Hello", TDATA_STRING);
+        o->GetPropertyManager()->AddProperty(o->Self(), "World", TDATA_INT);
+        o->AddPropertyCallBack("Hello", this, &Logic::OnHello);
+        o->AddPropertyCallBack("World", this, &Logic::OnWorld);
+        o->SetPropertyString("Hello", "hello,World");
+        o->SetPropertyInt("World", 1111);
+        em->DoEvent(o->Self(), NFEventDefine(1), NFCDataList() << int(100) << "200");
+        return true;
+    }
+};
+
+int main(int argc, char** argv) {
+    if (argc != 3) return 2;
+    nfio_file wf;
+    if (nfio_read(argv[1], &wf)) return 2;
+    auto A = [&](const char* n) {
+        nfio_arr* a = nfio_get(&wf, n);
+        if (!a) {
+            fprintf(stderr, "missing %s\n", n);
+            exit(2);
+        }
+        return a;
+    };
+    int64_t* cfg = (int64_t*)A("cfg")->data;
+    const int64_t N = cfg[0], NI = cfg[1], NF = cfg[2], NC = cfg[3], NK = cfg[4], NR = cfg[5], NS = cfg[6], NT = cfg[7];
+    nfio_arr* noa = nfio_get(&wf, "n_oprops");
+    if ((noa && ((int64_t*)noa->data)[0]) || (nfio_get(&wf, "sw_tick") && A("sw_tick")->shape[0] > 0) || NR != 1) {
+        fprintf(stderr, "logic_session: int/float properties, one record, no SwitchScene\n");
+        return 5;
+    }
+    const int64_t NP = NI + NF;
+    uint8_t* pnames = (uint8_t*)A("prop_names")->data;
+    uint8_t* knames = (uint8_t*)A("kind_names")->data;
+    nfk_op* ops = (nfk_op*)A("ops")->data;
+    int32_t* nops = (int32_t*)A("n_ops")->data;
+    std::vector<std::string> pname(NP), kname(NK), cname = {"NPC", "Player"};
+    for (int p = 0; p < NP; p++) pname[p] = cstr(pnames + 32 * p);
+    for (int k = 0; k < NK; k++) kname[k] = cstr(knames + 32 * k);
+    uint8_t* rct = (uint8_t*)A("rec_ctype")->data;
+    const int32_t rows = ((int32_t*)A("rec_rows")->data)[0], cols = ((int32_t*)A("rec_cols")->data)[0];
+    for (int c = 0; c < cols; c++)
+        if (rct[c]) {
+            fprintf(stderr, "logic_session: int record columns only (NFCRecord::SetFloat, see test_oracle.py)\n");
+            return 5;
+        }
+
+    TestPluginManager pm;
+    write_class_schema(pm, wf, pname, cname, NI, NF, NC, NR);
+    TestLogModule log;
+    NFCClassModule classes(&pm);
+    NFCElementModule elements(&pm);
+#ifdef LOGIC_REF
+    NFCKernelModule kernel(&pm);
+    NFCScheduleModule sched(&pm);
+#else
+    NFGPUKernelAdapter kernel(&pm);
+    NFGPUScheduleAdapter sched(&pm);
+#endif
+    NFCSceneAOIModule aoi(&pm);
+    NFCEventModule events(&pm);
+    pm.AddModule(typeid(NFILogModule).name(), &log);
+    pm.AddModule(typeid(NFIClassModule).name(), &classes);
+    pm.AddModule(typeid(NFIElementModule).name(), &elements);
+    pm.AddModule(typeid(NFIKernelModule).name(), &kernel);
+    pm.AddModule(typeid(NFISceneAOIModule).name(), &aoi);
+    pm.AddModule(typeid(NFIEventModule).name(), &events);
+    pm.AddModule(typeid(NFIScheduleModule).name(), &sched);
+    std::vector<NFIModule*> all = {&log, &classes, &elements, &kernel, &aoi, &events, &sched};
+    std::vector<std::string> rname = {"rec0"};
+#ifndef LOGIC_REF
+    // each heartbeat name's device effect program (a logic module's Init); OnHeartBeat has none
+    for (int k = 0; k < NK; k++)
+        kernel.gpu_.AddHeartBeatProgram(kname[k], std::vector<nfk_op>(ops + k * NFK_MAX_OPS, ops + k * NFK_MAX_OPS + nops[k]),
+                                        pname, rname);
+#endif
+    for (auto* m : all) m->Awake();
+    for (auto* m : all) m->Init();
+    Logic L;
+    L.km = &kernel;
+    L.sm = &sched;
+    L.em = &events;
+    L.ni = (int)NI;
+    for (int p = 0; p < NP; p++) L.pid[pname[p]] = p;
+    for (int k = 0; k < NK; k++) L.kid[kname[k]] = k;
+    NFIKernelModule* km = &kernel;
+    NFIScheduleModule* sm = &sched;
+
+    int64_t* gh = (int64_t*)A("guid_head")->data;
+    int64_t* gd = (int64_t*)A("guid_data")->data;
+    int32_t* sc = (int32_t*)A("scene")->data;
+    int32_t* gr = (int32_t*)A("group")->data;
+    uint8_t* cl = (uint8_t*)A("cls")->data;
+    int64_t* ii = (int64_t*)A("init_i")->data;
+    double* ff = (double*)A("init_f")->data;
+    nfio_arr* ba = nfio_get(&wf, "born");
+    int32_t* born = ba ? (int32_t*)ba->data : nullptr;
+    for (int64_t o = 0; o < N; o++) L.obj[NFGUID(gh[o], gd[o])] = (int)o;
+    L.obj[NFGUID(0, 10)] = (int)N;  // Tutorial3's object
+    {
+        std::map<int, int> groups;
+        for (int64_t o = 0; o < N; o++) groups[sc[o]] = std::max(groups[sc[o]], gr[o]);
+        for (auto& kv : groups) {
+            km->CreateScene(kv.first);
+            for (int g = 1; g <= kv.second; g++)
+                if (km->RequestGroupScene(kv.first) != g) return 3;
+        }
+    }
+    auto create = [&](int64_t o) {
+        NFCDataList arg;
+        for (int p = 0; p < NP; p++) {
+            if (pname[p] == "SceneID" || pname[p] == "GroupID") continue;
+            arg.Add(pname[p]);
+            if (p < NI) arg.Add((NFINT64)ii[p * N + o]);
+            else arg.Add(ff[(p - NI) * N + o]);
+        }
+        return km->CreateObject(NFGUID(gh[o], gd[o]), sc[o], gr[o], cname[cl[o]], "", arg) != nullptr;
+    };
+    for (int64_t o = 0; o < N; o++)
+        if ((!born || born[o] < 0) && !create(o)) return 3;
+    uint64_t* cells0 = (uint64_t*)A("rec0_cells")->data;
+    uint64_t* used0 = (uint64_t*)A("rec0_used")->data;
+    auto fill_rows = [&](int64_t o) {  // creation-time rows (NFCRecord::AddRow)
+        NF_SHARE_PTR<NFIRecord> R = km->GetObject(NFGUID(gh[o], gd[o]))->GetRecordManager()->GetElement("rec0");
+        for (int row = 0; row < rows; row++) {
+            if (!((used0[o] >> row) & 1)) continue;
+            NFCDataList v;
+            for (int c = 0; c < cols; c++) v.Add((NFINT64)cells0[((size_t)o * cols + c) * rows + row]);
+            R->AddRow(row, v);
+        }
+    };
+    for (int64_t o = 0; o < N; o++)
+        if (!born || born[o] < 0) fill_rows(o);
+    for (auto* m : all) m->AfterInit();
+    for (auto* m : all) m->ReadyExecute();
+    std::vector<uint8_t> alive(N, 1);
+    if (born)
+        for (int64_t o = 0; o < N; o++) alive[o] = born[o] < 0;
+    for (int64_t o = 0; o < N; o++)
+        if (alive[o]) L.Watch(NFGUID(gh[o], gd[o]));
+
+    // the heartbeat functor: the effect program through NFIKernelModule on the reference; on the
+    // device the program ran before the functor, which only logs
+    std::function<int(const NFGUID&, const std::string&, const float, const int)> heartbeat =
+        [&](const NFGUID& self, const std::string& name, const float, const int nCount) -> int {
+        L.Fired(self, name, nCount);
+#ifdef LOGIC_REF
+        const int k = L.kid.at(name);
+        for (int i = 0; i < nops[k]; i++) {
+            const nfk_op& op = ops[k * NFK_MAX_OPS + i];
+            if (op.code == NFK_OP_IADD_CLAMP) {
+                const std::string& d = pname[op.dst];
+                const int64_t cur = km->GetPropertyInt(self, d);
+                const int64_t a = (op.flags & NFK_A_PROP) ? km->GetPropertyInt(self, pname[op.a]) : op.a;
+                const int64_t lo = (op.flags & NFK_LO_PROP) ? km->GetPropertyInt(self, pname[op.b]) : op.b;
+                const int64_t hi = (op.flags & NFK_HI_PROP) ? km->GetPropertyInt(self, pname[op.c]) : op.c;
+                int64_t v = (int64_t)((uint64_t)cur + (uint64_t)a);
+                if (v < lo) v = lo;
+                if (v > hi) v = hi;
+                km->SetPropertyInt(self, d, v);
+            } else if (op.code == NFK_OP_FLERP) {
+                const std::string& d = pname[op.dst];
+                const double x = km->GetPropertyFloat(self, d);
+                const double t = km->GetPropertyFloat(self, pname[op.a]);
+                const double dd = t - x;
+                const double m = dd * bitsd((uint64_t)op.b);
+                km->SetPropertyFloat(self, d, x + m);
+            } else if (op.code == NFK_OP_FAFFINE) {
+                const std::string& d = pname[op.dst];
+                const double x = km->GetPropertyFloat(self, d);
+                const double m = x * bitsd((uint64_t)op.a);
+                km->SetPropertyFloat(self, d, m + bitsd((uint64_t)op.b));
+            } else if (op.code == NFK_OP_RIADD_CLAMP) {
+                NF_SHARE_PTR<NFIRecord> R = km->FindRecord(self, rname[op.dst >> 8]);
+                const int col = op.dst & 255;
+                for (int row = 0; R && row < R->GetRows(); row++) {
+                    if (!R->IsUsed(row)) continue;
+                    int64_t v = (int64_t)((uint64_t)km->GetRecordInt(self, "rec0", row, col) + (uint64_t)op.a);
+                    if (v < op.b) v = op.b;
+                    if (v > op.c) v = op.c;
+                    km->SetRecordInt(self, "rec0", row, col, v);
+                }
+            }
+        }
+#endif
+        return 0;
+    };
+    OBJECT_SCHEDULE_FUNCTOR_PTR hb(new OBJECT_SCHEDULE_FUNCTOR(heartbeat));
+    int32_t* s_obj = (int32_t*)A("s_obj")->data;
+    int32_t* s_kind = (int32_t*)A("s_kind")->data;
+    float* s_int = (float*)A("s_interval")->data;
+    int32_t* s_cnt = (int32_t*)A("s_count")->data;
+    int64_t* s_time = (int64_t*)A("s_time")->data;
+    for (int64_t i = 0; i < NS; i++) {
+        g_now = s_time[i];
+        sm->AddSchedule(NFGUID(gh[s_obj[i]], gd[s_obj[i]]), kname[s_kind[i]], hb, s_int[i], s_cnt[i]);
+    }
+    int64_t* tick_time = (int64_t*)A("tick_time")->data;
+    g_now = tick_time[0] - 1000;
+    L.frame = -1;
+    if (!L.Tutorial3(sc[0])) return 4;
+    const std::string t3_setup = L.t3;
+
+    nfio_arr* xa = A("x_tick");
+    const int64_t NX = (int64_t)xa->shape[0];
+    int32_t* x_tick = (int32_t*)xa->data;
+    int32_t* x_obj = (int32_t*)A("x_obj")->data;
+    int32_t* x_pid = (int32_t*)A("x_pid")->data;
+    uint64_t* x_bits = (uint64_t*)A("x_bits")->data;
+    nfio_arr* xma = nfio_get(&wf, "x_mode");
+    uint8_t* x_mode = xma ? (uint8_t*)xma->data : nullptr;
+    nfio_arr* ha = A("h_tick");
+    const int64_t NH = (int64_t)ha->shape[0];
+    int32_t* h_tick = (int32_t*)ha->data;
+    int32_t* h_op = (int32_t*)A("h_op")->data;
+    int32_t* h_obj = (int32_t*)A("h_obj")->data;
+    int32_t* h_kind = (int32_t*)A("h_kind")->data;
+    float* h_int = (float*)A("h_interval")->data;
+    int32_t* h_cnt = (int32_t*)A("h_count")->data;
+    int64_t* h_time = (int64_t*)A("h_time")->data;
+    nfio_arr* rsa = nfio_get(&wf, "r_tick");
+    const int64_t NRS = rsa ? (int64_t)rsa->shape[0] : 0;
+    int32_t* r_tick = NRS ? (int32_t*)rsa->data : nullptr;
+    int32_t* r_obj = NRS ? (int32_t*)A("r_obj")->data : nullptr;
+    int32_t* r_row = NRS ? (int32_t*)A("r_row")->data : nullptr;
+    int32_t* r_col = NRS ? (int32_t*)A("r_col")->data : nullptr;
+    uint64_t* r_bits = NRS ? (uint64_t*)A("r_bits")->data : nullptr;
+    nfio_arr* roa = NRS ? nfio_get(&wf, "r_op") : nullptr;
+    uint8_t* r_op = roa ? (uint8_t*)roa->data : nullptr;
+    uint64_t* r_vals = roa ? (uint64_t*)A("r_vals")->data : nullptr;
+    nfio_arr* dta = nfio_get(&wf, "d_tick");
+    const int64_t ND = dta ? (int64_t)dta->shape[0] : 0;
+    int32_t* d_tick = ND ? (int32_t*)dta->data : nullptr;
+    int32_t* d_obj = ND ? (int32_t*)A("d_obj")->data : nullptr;
+
+    nfio_writer w;
+    if (nfio_wopen(&w, argv[2])) return 2;
+    {
+        std::vector<uint8_t> s(t3_setup.begin(), t3_setup.end());
+        nfio_put1(&w, "t3_setup", NFIO_U8, s.data(), s.size(), 1);
+    }
+    int64_t xi = 0, hi = 0, di = 0, ri = 0;
+    for (int t = 0; t < NT; t++) {
+        L.clear();
+        L.frame = t;
+        L.phase = 0;
+        g_now = tick_time[t] - 50;  // the window's calls, between the frames
+        if (born)  // CreateObject after start
+            for (int64_t o = 0; o < N; o++)
+                if (born[o] == t) {
+                    if (!create(o)) return 8;
+                    alive[o] = 1;
+                    L.Watch(NFGUID(gh[o], gd[o]));
+                }
+        events.DoEvent(L.t3_self, NFEventDefine(1), NFCDataList() << (NFINT64)(1000 + t) << ("s" + std::to_string(t)));
+        for (; hi < NH && h_tick[hi] == t; hi++) {
+            const NFGUID g(gh[h_obj[hi]], gd[h_obj[hi]]);
+            g_now = h_time[hi];
+            if (h_op[hi] == 1) sm->AddSchedule(g, kname[h_kind[hi]], hb, h_int[hi], h_cnt[hi]);
+            else if (h_op[hi] == 2) sm->RemoveSchedule(g, kname[h_kind[hi]]);
+            else sm->RemoveSchedule(g);
+        }
+        for (; xi < NX && x_tick[xi] == t; xi++) {
+            const NFGUID g(gh[x_obj[xi]], gd[x_obj[xi]]);
+            if (!alive[x_obj[xi]]) continue;
+            const std::string& pn = pname[x_pid[xi]];
+            const bool rmw = x_mode && x_mode[xi];
+            const bool direct = xi % 3 == 1;  // GetObject(self)->SetProperty* (NFIObject.h)
+            NF_SHARE_PTR<NFIObject> ob = km->GetObject(g);
+            if (x_pid[xi] < NI) {
+                const int64_t cur = direct ? ob->GetPropertyInt(pn) : km->GetPropertyInt(g, pn);
+                const int64_t v = rmw ? (int64_t)((uint64_t)cur + x_bits[xi]) : (int64_t)x_bits[xi];
+                if (direct) ob->SetPropertyInt(pn, v);
+                else km->SetPropertyInt(g, pn, v);
+            } else {
+                const double cur = direct ? ob->GetPropertyFloat(pn) : km->GetPropertyFloat(g, pn);
+                const double v = rmw ? cur + bitsd(x_bits[xi]) : bitsd(x_bits[xi]);
+                if (direct) ob->SetPropertyFloat(pn, v);
+                else km->SetPropertyFloat(g, pn, v);
+            }
+        }
+        for (; ri < NRS && r_tick[ri] == t; ri++) {
+            const NFGUID g(gh[r_obj[ri]], gd[r_obj[ri]]);
+            if (!alive[r_obj[ri]]) continue;
+            NF_SHARE_PTR<NFIRecord> R = km->FindRecord(g, "rec0");
+            const int op = r_op ? r_op[ri] : 0;
+            if (op == 1) {  // NFCRecord::AddRow on the object's record
+                NFCDataList v;
+                for (int c = 0; c < cols; c++) v.Add((NFINT64)r_vals[ri * NFK_MAX_REC_COLS + c]);
+                R->AddRow(r_row[ri], v);
+            } else if (op == 2) {
+                R->Remove(r_row[ri]);
+            } else if (op == 3) {
+                km->ClearRecord(g, "rec0");  // KM:492
+            } else if (ri % 2) {
+                R->SetInt(r_row[ri], r_col[ri], (int64_t)r_bits[ri]);  // FindRecord(self, r)->SetInt
+            } else {
+                km->SetRecordInt(g, "rec0", r_row[ri], r_col[ri], (int64_t)r_bits[ri]);  // KM:505
+            }
+        }
+        for (; di < ND && d_tick[di] == t; di++) {  // DestroyObject (KM:273)
+            if (!km->DestroyObject(NFGUID(gh[d_obj[di]], gd[d_obj[di]]))) return 9;
+            alive[d_obj[di]] = 0;
+        }
+        g_now = tick_time[t];
+        L.phase = 1;
+        for (auto* m : all) m->Execute();
+        char nm[48];
+#define PUT(pfx, s, code, vec, es) snprintf(nm, sizeof nm, "%s_t%d_%s", pfx, t, s); nfio_put1(&w, nm, code, vec.data(), vec.size(), es);
+        PUT("pc", "phase", NFIO_I32, L.pc_phase, 4);
+        PUT("pc", "obj", NFIO_I32, L.pc_obj, 4);
+        PUT("pc", "pid", NFIO_I32, L.pc_pid, 4);
+        PUT("pc", "old", NFIO_U64, L.pc_old, 8);
+        PUT("pc", "new", NFIO_U64, L.pc_new, 8);
+        PUT("rc", "phase", NFIO_I32, L.rc_phase, 4);
+        PUT("rc", "obj", NFIO_I32, L.rc_obj, 4);
+        PUT("rc", "rrc", NFIO_U32, L.rc_rrc, 4);
+        PUT("rc", "old", NFIO_U64, L.rc_old, 8);
+        PUT("rc", "new", NFIO_U64, L.rc_new, 8);
+        PUT("fi", "obj", NFIO_I32, L.fi_obj, 4);
+        PUT("fi", "kind", NFIO_I32, L.fi_kind, 4);
+        PUT("fi", "rem", NFIO_I32, L.fi_rem, 4);
+        std::vector<uint8_t> t3(L.t3.begin(), L.t3.end());
+        PUT("t3", "log", NFIO_U8, t3, 1);
+        // every object's properties through the host object and through NFIKernelModule, and its
+        // rec0 used rows' int cells through the host record
+        std::vector<uint64_t> vh((size_t)NP * N, 0), vk((size_t)NP * N, 0), rv((size_t)N * cols * rows, 0), ru(N, 0);
+        for (int64_t o = 0; o < N; o++) {
+            if (!alive[o]) continue;
+            const NFGUID g(gh[o], gd[o]);
+            NF_SHARE_PTR<NFIObject> ob = km->GetObject(g);
+            for (int p = 0; p < NP; p++) {
+                vh[(size_t)p * N + o] = p < NI ? (uint64_t)ob->GetPropertyInt(pname[p]) : dbits(ob->GetPropertyFloat(pname[p]));
+                vk[(size_t)p * N + o] = p < NI ? (uint64_t)km->GetPropertyInt(g, pname[p]) : dbits(km->GetPropertyFloat(g, pname[p]));
+            }
+            NF_SHARE_PTR<NFIRecord> R = ob->GetRecordManager()->GetElement("rec0");
+            for (int row = 0; row < rows; row++) {
+                if (!R->IsUsed(row)) continue;
+                ru[o] |= 1ull << row;
+                for (int c = 0; c < cols; c++) rv[((size_t)o * cols + c) * rows + row] = (uint64_t)R->GetInt(row, c);
+            }
+        }
+        PUT("v", "host", NFIO_U64, vh, 8);
+        PUT("v", "kernel", NFIO_U64, vk, 8);
+        PUT("r", "cells", NFIO_U64, rv, 8);
+        PUT("r", "used", NFIO_U64, ru, 8);
+    }
+    nfio_wclose(&w);
+    fflush(stdout);
+    _exit(0);  // (static destructors: NFMemoryCounter's static map dies before the modules' objects)
+}

@@ -53,12 +53,13 @@ def _normalise(out, w, n_ticks):
     layout and its property ids by the class module's (name-ordered) property list, the oracle by
     the workload's; within an object each property has one coalesced event, and each record's
     events keep their order (row events in call order, then cell updates).  Recipient lists are
-    compared as sets (the AOI module lists a group's players in its own map order)."""
+    compared IN ORDER: the AOI module lists a group's players in NFCSceneGroupInfo's player-map order
+    (std::map by NFGUID, AOI:531-593), which the device's pl_slot runs keep."""
     r = dict(out)
     for t in range(n_ticks):
         moff = np.asarray(out[f"mo_t{t}_off"], np.int64)
         mr = np.asarray(out[f"mr_t{t}_obj"])
-        rc = [np.sort(mr[moff[i]:moff[i + 1]]) for i in range(len(moff) - 1)]
+        rc = [mr[moff[i]:moff[i + 1]] for i in range(len(moff) - 1)]
         ne = len(out[f"ev_t{t}_obj"])
         pe = np.lexsort((out[f"ev_t{t}_pid"], out[f"ev_t{t}_obj"]))
         rrc = np.asarray(out[f"re_t{t}_rrc"])
