@@ -37,8 +37,9 @@ HBM_CEILING_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pro
 KNAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles", "membership"]
 CONFIG_NAMES = {
     0: "BASELINE config[0]: Tutorial3 (HelloWorld3Module.cpp) scaled to 10k NPC objects in scene 1 group 0: "
-       "AddSchedule(self, \"OnHeartBeat\", 5.0, 10) per object (effect: World += 1, so its property callback "
-       "fires), OnEvent SetPropertyInt(World) on 1 % of the objects per frame, 100 ms frames",
+       "AddSchedule(self, \"OnHeartBeat\", 5.0, 10) per object (the tutorial's functor-only heartbeat: no "
+       "device effect, the fired list goes to the host functor), OnEvent SetPropertyInt(World) on 1 % of the "
+       "objects per frame (World's per-object callback), 100 ms frames",
     3: "BASELINE config[3]: 256 scenes x 64 groups, 2M entities per GPU, 32 players per group "
        "(scene-group sync-list fan-out dominated), heartbeats as config[1], 100 ms frames",
     4: "BASELINE config[4]: 500k players per GPU, 64-row skill record each (int cooldown + f64 charge "

@@ -636,8 +636,12 @@ def record_world(n_ticks=4, seed=2028, n_obj=500_000, groups=31_250, rec_rows=64
 # Tutorial/Tutorial3/HelloWorld3Module.cpp: on COE_CREATE_HASDATA every object gets the heartbeat
 # AddSchedule(self, "OnHeartBeat", 5.0f, 10) (:49-56) and an int property "World" with a property
 # callback (:96-104, OnPropertyCallBackEvent); game events set "World" (:16-22, OnEvent).  Scaled
-# to 10k NPC objects in scene 1 group 0.  The tutorial's heartbeat only prints; here its effect
-# program increments "World", so that every heartbeat fires the property callback.  "World" is
+# to 10k NPC objects in scene 1 group 0.  The tutorial's heartbeat only prints (:24-34), so its
+# device program is empty: the frame scans the schedules, reschedules the fired ones and hands them
+# to the host functor (the fired list), and the OnEvent Sets of "World" are the dirty events.
+# (world_effect=True gives the heartbeat a "World += 1" program instead: the golden fixture
+# tests/golden/tutorial3 was made that way, to exercise an effect on a per-object-callback
+# property.)  "World" is
 # added at runtime in the tutorial (NFCProperty defaults: not public, not private, so the AOI
 # module sends it to nobody); SceneID / GroupID are private (IObject.xml), X / Y / Z public.
 T3_INT_PROPS = ["SceneID", "GroupID", "World"]
@@ -648,7 +652,7 @@ T3_KINDS = ["OnHeartBeat"]
 
 
 def tutorial3_world(n_obj=10_000, n_ticks=120, tick_ms=100, seed=3, event_frac=0.01, t0=1_700_000_000_000,
-                    guid_head=0):
+                    guid_head=0, world_effect=False):
     rng = np.random.default_rng(seed)
     ni, nf = len(T3_INT_PROPS), len(T3_FLT_PROPS)
     # NFGUID(0, 10) in the tutorial; here NFGUID(guid_head, 10 + i)
@@ -666,8 +670,9 @@ def tutorial3_world(n_obj=10_000, n_ticks=120, tick_ms=100, seed=3, event_frac=0
     init_i[T3_PID["World"]] = 1111   # pObject->SetPropertyInt("World", 1111) (:99)
     init_f = rng.uniform(-100.0, 100.0, (nf, n_obj))
     ops = np.zeros((1, MAX_OPS), OP_DTYPE)
-    ops[0, 0] = (OP_IADD_CLAMP, 0, T3_PID["World"], 0, 1, I64_MIN, I64_MAX)
-    n_ops = np.array([1], np.int32)
+    if world_effect:
+        ops[0, 0] = (OP_IADD_CLAMP, 0, T3_PID["World"], 0, 1, I64_MIN, I64_MAX)
+    n_ops = np.array([1 if world_effect else 0], np.int32)
     # objects created over the first 5 s (so the 5 s heartbeats do not all fire in one frame)
     s_time = (t0 - rng.integers(0, 5000, n_obj)).astype(np.int64)
     tick_time = (t0 + tick_ms * np.arange(1, n_ticks + 1)).astype(np.int64)

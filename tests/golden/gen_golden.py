@@ -60,7 +60,30 @@ FIXTURES = {
 
 
 # BASELINE config[0]: Tutorial3 (HelloWorld3Module.cpp) heartbeats + property callbacks, scaled down
-TUTORIAL3 = {"tutorial3": dict(n_obj=2000, n_ticks=80, seed=606)}
+TUTORIAL3 = {"tutorial3": dict(n_obj=2000, n_ticks=80, seed=606, world_effect=True)}
+
+
+# fixtures whose frames are also pinned on the reference's own server modules
+# (oracle/_ref/nf_ref_session per-frame mode: NFCKernelModule / NFCScheduleModule / NFCSceneAOIModule
+# compiled from the reference): <name>.session.nfio holds what those modules raised in every frame
+# (property / record events in call order, fired heartbeats, GetBroadCastObject lists at the frame's
+# end) and their final state; tests/test_oracle.py derives each frame's dirty-sync list from it
+SESSION_FIXTURES = ["switch", "lifecycle", "rowops", "objects"]
+
+
+def session(name, w, wp):
+    exe = os.path.join(ROOT, "oracle", "_ref", "nf_ref_session")
+    sp = os.path.join(HERE, f"{name}.session.nfio")
+    fp = sp + ".final"
+    nt = str(int(w["cfg"][7]))
+    subprocess.run([exe, wp, nt, "0", fp, sp], check=True, stdout=subprocess.DEVNULL)
+    out = nfio.read(sp)
+    for k, v in nfio.read(fp).items():
+        if k.startswith("final_"):
+            out[k] = v
+    os.remove(fp)
+    nfio.write(sp, out)
+    return sp
 
 
 def main(names=None):
@@ -74,6 +97,8 @@ def main(names=None):
         nfio.write(wp, w)
         subprocess.run([exe, wp, ep], check=True)
         print(name, os.path.getsize(wp), os.path.getsize(ep))
+        if name in SESSION_FIXTURES:
+            print(name, "session", os.path.getsize(session(name, w, wp)))
 
 
 if __name__ == "__main__":

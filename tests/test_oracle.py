@@ -116,6 +116,134 @@ def test_oracle_matches_reference_server_modules(tmp_path, seed, kw):
     assert int(np.asarray(got["counts"])[0]) == fired
 
 
+def _dirty_sync_from_reference(fr, t, n_oprops):
+    """The frame's dirty-sync list from what the reference's modules raised (nf_ref_session's
+    per-frame mode): property events per (object, property) coalesced to (first old, last new) and
+    dropped when the bits are unchanged; per (object, record) the row events (Add / Del / Cover) in
+    call order, then the cell Updates coalesced per (row, col) in (row, col) order; events of objects
+    that left the world in the window dropped; each event's recipients = the compiled
+    GetBroadCastObject list of its (object, property / record) at the frame's end."""
+    alive = np.asarray(fr[f"al_t{t}_ive"]).astype(bool)
+    bc = {}
+    off = np.asarray(fr[f"bc_t{t}_off"])
+    rc = np.asarray(fr[f"bc_t{t}_rcpt"])
+    for i, (o, k) in enumerate(zip(fr[f"bc_t{t}_obj"], fr[f"bc_t{t}_key"])):
+        bc[(int(o), int(k))] = [int(x) for x in rc[off[i]:off[i + 1]]]
+    first, last, order = {}, {}, []
+    for o, p, a, b, ah, bh in zip(fr[f"pe_t{t}_obj"], fr[f"pe_t{t}_pid"], fr[f"pe_t{t}_old"], fr[f"pe_t{t}_new"],
+                                  fr[f"pe_t{t}_oldh"], fr[f"pe_t{t}_newh"]):
+        key = (int(o), int(p))
+        if key not in first:
+            first[key] = (int(a), int(ah))
+            order.append(key)
+        last[key] = (int(b), int(bh))
+    props = {k: (first[k], last[k], bc.get(k, [])) for k in order if alive[k[0]] and first[k] != last[k]}
+    rows, upd = {}, {}
+    for o, rrc, a, b in zip(fr[f"rr_t{t}_obj"], fr[f"rr_t{t}_rrc"], fr[f"rr_t{t}_old"], fr[f"rr_t{t}_new"]):
+        o, rrc = int(o), int(rrc)
+        if not alive[o]:
+            continue
+        rec = (rrc >> 16) & 0xFF
+        if rrc >> 24:
+            rows.setdefault((o, rec), []).append((rrc, 0, 0))
+        else:
+            u = upd.setdefault((o, rec), {})
+            u[rrc] = (u[rrc][0] if rrc in u else int(a), int(b))
+    recs = {}
+    for key in set(rows) | set(upd):
+        ev = list(rows.get(key, [])) + [(rrc, a, b) for rrc, (a, b) in sorted(upd.get(key, {}).items()) if a != b]
+        if ev:
+            recs[key] = (ev, bc.get((key[0], 0x10000 | key[1]), []))
+    fired = sorted(zip(*(np.asarray(fr[f"fi_t{t}_{k}"]).tolist() for k in ("obj", "kind", "rem"))))
+    return props, recs, fired
+
+
+def _dirty_sync_from_oracle(o, t, n_oprops):
+    moff = np.asarray(o[f"mo_t{t}_off"])
+    mr = np.asarray(o[f"mr_t{t}_obj"])
+    ne = len(o[f"ev_t{t}_obj"])
+    oh = o.get(f"ev_t{t}_oldh", np.zeros(ne, np.uint64))
+    nh = o.get(f"ev_t{t}_newh", np.zeros(ne, np.uint64))
+    props = {}
+    for e, (ob, p, a, b) in enumerate(zip(o[f"ev_t{t}_obj"], o[f"ev_t{t}_pid"], o[f"ev_t{t}_old"], o[f"ev_t{t}_new"])):
+        props[(int(ob), int(p))] = ((int(a), int(oh[e])), (int(b), int(nh[e])), [int(x) for x in mr[moff[e]:moff[e + 1]]])
+    recs = {}
+    for e, (ob, rrc, a, b) in enumerate(zip(o[f"re_t{t}_obj"], o[f"re_t{t}_rrc"], o[f"re_t{t}_old"], o[f"re_t{t}_new"])):
+        key = (int(ob), (int(rrc) >> 16) & 0xFF)
+        ev, lists = recs.setdefault(key, ([], []))
+        ev.append((int(rrc), int(a) if not int(rrc) >> 24 else 0, int(b) if not int(rrc) >> 24 else 0))
+        lists.append([int(x) for x in mr[moff[ne + e]:moff[ne + e + 1]]])
+    fired = sorted(zip(*(np.asarray(o[f"fi_t{t}_{k}"]).tolist() for k in ("obj", "kind", "rem"))))
+    return props, recs, fired
+
+
+@pytest.mark.skipif(not os.path.exists(SESSION), reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("seed", [6, 9, 13, 15])
+def test_oracle_matches_reference_modules_per_frame(tmp_path, seed):
+    """Frame by frame against the reference's own NFCKernelModule / NFCScheduleModule /
+    NFCSceneAOIModule (nf_ref_session per-frame mode, compiled from the reference's sources): the
+    worlds of test_oracle_matches_reference with SwitchScene into new groups (KM:901-951), CreateObject
+    after start and DestroyObject (KM:101, 273-308), object properties (PR:377) and record row
+    operations with SetRecordInt (RC:111, 182, 1086, 1109).  Every frame's dirty-sync list — events,
+    their recipient lists IN ORDER (GetBroadCastObject, AOI:531-593, at the frame's end), record
+    events — and fired heartbeats equal the oracle's, and so does the final state."""
+    kw = {6: dict(n_obj=800, n_scenes=3, groups_per_scene=4, players_per_group=3, switch_frac=0.05,
+                  switch_new_groups=True),
+          9: dict(n_obj=700, n_scenes=3, groups_per_scene=4, players_per_group=3, ext_frac=0.05, host_ops=True,
+                  sched_edges=True, switch_frac=0.02, switch_new_groups=True, rmw_frac=0.02, spawn_frac=0.03,
+                  destroy_frac=0.03),
+          13: dict(n_obj=500, n_scenes=2, groups_per_scene=4, players_per_group=3, obj_props=True, obj_set_frac=0.12,
+                   ext_frac=0.05, ext_props="all", rmw_frac=0.02, switch_frac=0.02, spawn_frac=0.03,
+                   destroy_frac=0.03),
+          15: dict(n_obj=400, n_scenes=2, groups_per_scene=3, players_per_group=4, records=True, rec_rows=24,
+                   rec_float_op=False, rec_set_frac=0.08, rec_set_float=False, rec_row_frac=0.1)}[seed]
+    nt = 9
+    w = workload.make_world(n_ticks=nt, seed=seed, **kw)
+    wp, fp, pp = str(tmp_path / "w.nfio"), str(tmp_path / "f.nfio"), str(tmp_path / "p.nfio")
+    nfio.write(wp, w)
+    r = subprocess.run([SESSION, wp, str(nt), "0", fp, pp], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    fr = nfio.read(pp)
+    fr.update({k: v for k, v in nfio.read(fp).items() if k.startswith("final_")})
+    no = len(workload.OBJ_PROPS) if kw.get("obj_props") else 0
+    n_ev, n_msg = _compare_dirty_sync(fr, run_oracle(w), nt, no)
+    assert n_ev > 300 and n_msg > 300, (n_ev, n_msg)
+
+
+def _compare_dirty_sync(fr, o, nt, n_oprops):
+    n_ev = n_msg = 0
+    for t in range(nt):
+        rp, rr, rf = _dirty_sync_from_reference(fr, t, n_oprops)
+        op, orr, of = _dirty_sync_from_oracle(o, t, n_oprops)
+        assert rf == of, f"frame {t}: fired"
+        assert rp == op, f"frame {t}: property events / recipients"
+        assert set(rr) == set(orr), f"frame {t}: record events"
+        for key, (ev, lst) in rr.items():
+            assert ev == orr[key][0] and all(x == lst for x in orr[key][1]), f"frame {t}: record events of {key}"
+        n_ev += len(rp) + sum(len(v[0]) for v in rr.values())
+        n_msg += sum(len(v[2]) for v in rp.values())
+    for k in ("final_i", "final_f"):
+        a, b = np.asarray(fr[k]), np.asarray(o[k])
+        assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), k
+    return n_ev, n_msg
+
+
+@pytest.mark.parametrize("name", sorted(os.path.basename(p)[:-len(".session.nfio")]
+                                        for p in glob.glob(os.path.join(GOLDEN, "*.session.nfio"))))
+def test_oracle_matches_session_golden(name):
+    """tests/golden/<name>.session.nfio: what the reference's own NFCKernelModule / NFCScheduleModule /
+    NFCSceneAOIModule raised in every frame of the fixture's workload (tests/golden/gen_golden.py,
+    oracle/_ref/nf_ref_session per-frame mode).  The oracle's every frame — events, ordered recipient
+    lists, record row and cell events, fired heartbeats — and final state equal them: the membership
+    (switch, lifecycle), object-property and row-operation fixtures are pinned on the compiled modules
+    frame by frame, not only on the harness's restatement."""
+    w = nfio.read(os.path.join(GOLDEN, f"{name}.workload.nfio"))
+    fr = nfio.read(os.path.join(GOLDEN, f"{name}.session.nfio"))
+    no = int(np.asarray(w["n_oprops"])[0]) if "n_oprops" in w else 0
+    n_ev, n_msg = _compare_dirty_sync(fr, run_oracle(w), int(w["cfg"][7]), no)
+    assert n_ev > 300 and n_msg > 300
+
+
 @pytest.mark.skipif(not have_ref, reason="oracle/_ref not built (needs /root/reference)")
 def test_reference_record_setfloat_bug():
     """NFCRecord::SetFloat stores a const double into the int64 alternative of the variant;
