@@ -84,6 +84,11 @@ def parse():
                         "process, same --steps / --warmup) and report them under 'configs'")
     p.add_argument("--backend", default="nccl", help="process group backend (nccl = RCCL; gloo only to rehearse "
                                                      "several ranks on one GPU)")
+    p.add_argument("--shard", choices=["auto", "cpp", "py"], default="auto",
+                   help="config[2]'s exchange: cpp = the C++ SceneShard over its own RCCL communicators (the "
+                        "plugin's production path, include/nfgpu_shard.h); py = noahgameframe_amd/shard.py over "
+                        "the process group; auto = cpp with --backend nccl, py with gloo (RCCL refuses two ranks "
+                        "on one GPU)")
     return p.parse_args()
 
 
@@ -178,14 +183,22 @@ class Migration:
     and launches the next frame; the frame after that starts by moving the state rows GPU-to-GPU
     with one RCCL all_to_all.  Frames without migrations make no collective call at all."""
 
-    def __init__(self, m, w, rank, world, per_frame, every, dev):
+    def __init__(self, m, w, rank, world, per_frame, every, dev, impl="py"):
         import torch.distributed as dist
-        from noahgameframe_amd.shard import SceneShard
+        from noahgameframe_amd.shard import CppSceneShard, SceneShard
         self.dist = dist
         self.meta = dist.new_group(backend="gloo") if world > 1 else None
-        own = lambda scene: int(scene) - 1
-        self.shard = SceneShard(m, rank, world, own, w["scene_props"], group=dist.group.WORLD if world > 1 else None,
-                                meta_group=self.meta, device=dev)
+        self.impl = impl
+        if impl == "cpp":
+            # scene r + 1 belongs to rank r; tickets gathered on every `every`-th frame (the frames
+            # this harness queues them on), so the other frames make no transport call
+            self.cshard = CppSceneShard(m, rank, world, [-1] + list(range(world)), w["scene_props"],
+                                        meta_group=self.meta, exchange_every=max(1, every))
+            self.shard = None
+        else:
+            own = lambda scene: int(scene) - 1
+            self.shard = SceneShard(m, rank, world, own, w["scene_props"], group=dist.group.WORLD if world > 1 else None,
+                                    meta_group=self.meta, device=dev)
         self.rank, self.world, self.per_frame, self.every = rank, world, per_frame, max(1, every)
         # entities this rank owns (guid head, guid data, group, cls, is_player), oldest first
         self.owned = RowQueue(np.stack([w["guid_head"], w["guid_data"], w["group"], w["cls"], w["is_player"]],
@@ -197,6 +210,11 @@ class Migration:
 
     def before_frame(self):
         from noahgameframe_amd.shard import T_GH, T_GD, T_GROUP, T_CLS, T_PL
+        if self.impl == "cpp":  # SceneShard::BeginFrame: the rows of the gather the last frame started
+            recv = self.cshard.begin_frame()
+            if len(recv):
+                self.owned.append(recv[:, [T_GH, T_GD, T_GROUP, T_CLS, T_PL]])
+            return
         # exchanges started at least one frame ago (the same frames on every rank)
         while self.pending and self.pending[0][0] < self.frames:
             recv = self.shard.migrate_array(self.pending.popleft()[1].wait())
@@ -205,14 +223,24 @@ class Migration:
 
     def finish(self):
         """Waits for the exchanges still in flight (their tickets are not carried out)."""
+        if self.impl == "cpp":
+            self.cshard.close()   # (its destructor takes the gather in flight, on every rank)
+            return
         while self.pending:
             self.pending.popleft()[1].wait()
+
+    def moved(self):
+        if self.impl == "cpp":
+            return self.cshard.stats()[:2]
+        return self.shard.migrated_out, self.shard.migrated_in
 
     def after_frame(self):
         """The next frame's tickets (only on every `every`-th frame, the same frames on every rank)."""
         from noahgameframe_amd.shard import T_GH, T_GD, T_CLS, T_PL, T_SCENE, T_GROUP, T_X, T_Y, T_Z, T_SRC, T_DST
         self.frames += 1
         if self.frames % self.every:
+            if self.impl == "cpp":
+                self.cshard.end_frame()   # (not an exchange frame: no transport call)
             return
         dst = (self.rank + 1) % self.world
         o = self.owned.take(self.per_frame)
@@ -226,6 +254,10 @@ class Migration:
         out[:, T_X], out[:, T_Y] = xy[:, 0].view(np.int64), xy[:, 1].view(np.int64)
         out[:, T_Z] = np.zeros(n, np.float64).view(np.int64)
         out[:, T_SRC], out[:, T_DST] = self.rank, dst
+        if self.impl == "cpp":
+            self.cshard.queue(out)
+            self.cshard.end_frame()   # the gather starts on the C++ shard's worker thread
+            return
         self.pending.append((self.frames, self.shard.exchange_ticket_array_async(out, max_rows=self.per_frame)))
 
 
@@ -348,11 +380,12 @@ def main():
     t0 = int(w["tick_time"][0])
     tick = 0
     mig = None
+    shard_impl = args.shard if args.shard != "auto" else ("cpp" if args.backend == "nccl" else "py")
     if migrating:
-        mig = Migration(m, w, rank, world, args.migrate, args.migrate_every, dev)
+        mig = Migration(m, w, rank, world, args.migrate, args.migrate_every, dev, impl=shard_impl)
 
     trace = {} if os.environ.get("NFGPU_BENCH_TRACE") else None  # host seconds per phase (stderr)
-    if mig and trace is not None:
+    if mig and trace is not None and mig.shard is not None:
         mig.shard.phase_s = trace   # (migrate_array's own phases: "export", "all_to_all", ...)
 
     def timed(name, fn):
@@ -401,12 +434,12 @@ def main():
     for _ in range(args.steps):
         frame()
     m.set_profiling(False)
+    moved_here = list(mig.moved()) if mig else [0, 0]
     if mig:
         mig.finish()
     ms, nl, byts = m.kernel_times()
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
-    moved = torch.tensor([mig.shard.migrated_out if mig else 0, mig.shard.migrated_in if mig else 0],
-                         dtype=torch.int64, device=dev if args.backend == "nccl" else "cpu")
+    moved = torch.tensor(moved_here, dtype=torch.int64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(moved, op=dist.ReduceOp.SUM)
@@ -471,7 +504,10 @@ def main():
                    "entities_per_gpu": args.entities, "groups": args.groups,
                    "players_per_group": args.players_per_group, "parallelism": f"scene-shard x{world}",
                    "migrations_per_rank_per_frame": args.migrate / args.migrate_every if migrating else 0},
-        "migrations": {"out": moved[0], "in": moved[1], "backend": args.backend} if migrating else None,
+        "migrations": {"out": moved[0], "in": moved[1], "backend": args.backend,
+                       "exchange": "C++ SceneShard (RCCL side communicator for tickets, ncclSend/Recv rows)"
+                       if shard_impl == "cpp" else "noahgameframe_amd/shard.py (process group)"}
+        if migrating else None,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "mix_ceiling": ceiling},

@@ -265,19 +265,20 @@ public:
 
     // ---- scene shards (include/NFGPUSceneShard.hpp): one process per GPU, a scene range each ----
     // With a shard attached, SwitchScene into a scene another shard owns queues the entity's
-    // departure: from that call on the entity is no longer this module's (later calls on it in the
-    // window return false, as after DestroyObject), and at the start of the next Execute every rank
-    // exchanges its departures (SceneShard::Migrate, collective: every rank's Execute calls it) and
-    // the arrivals enter this world with the SwitchScene property writes.  The row that travels is
-    // the entity's state after the last frame: Set calls queued on it earlier in the same window are
-    // dropped with it (make the SwitchScene its first call of the window).  Arrivals' schedules call
-    // the functor registered for their name with SetKindFunctor (functors cannot cross processes).
+    // departure: from that call on the entity is no longer this module's (later calls on it return
+    // false, as after DestroyObject).  Execute ends by starting the all-gather of the departures'
+    // tickets (SceneShard::EndFrame, on an exchange frame; off the world's stream) and the next
+    // Execute begins by moving their rows (SceneShard::BeginFrame, collective: every rank's Execute
+    // makes it; no collective when no rank has a departure): the entity leaves at the start of the
+    // frame after the one its SwitchScene was queued before, with its state after that frame, and
+    // enters the owner's world with the SwitchScene property writes.  Arrivals' schedules call the
+    // functor registered for their name with SetKindFunctor (functors cannot cross processes).
     void AttachShard(SceneShard* shard) { shard_ = shard; }
-    // the departures queued so far leave now and the arrivals enter (collective: every rank calls
-    // it the same number of times; Execute also calls it first), so calls made after it in the
-    // window find the arrivals here
+    // the departures queued so far leave now and the arrivals enter (synchronous; collective: every
+    // rank calls it the same number of times), so calls made after it in the window find the
+    // arrivals here
     void MigrateNow() {
-        if (shard_) MigrateShard();
+        if (shard_) MigrateShard(true);
     }
     void SetKindFunctor(const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb, float fTime);
     int64_t MigratedOut() const { return shard_ ? shard_->migrated_out : 0; }
@@ -364,7 +365,7 @@ private:
     ModuleScheduler module_sched_;
     SceneShard* shard_ = nullptr;
     std::map<std::string, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> kind_cb_;  // arrivals' functors
-    void MigrateShard();
+    void MigrateShard(bool sync);
     std::function<int64_t()> clock_;
     nfk_summary summary_{};
     FrameStats stats_{};

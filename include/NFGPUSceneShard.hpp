@@ -14,9 +14,25 @@
 // Transports: RcclTransport (librccl, one rank per GPU, the production path) and HostTransport
 // (ranks as threads of one process exchanging through shared host memory: the protocol test's
 // stand-in, tests/cpp/shard_protocol.cpp).
+//
+// Per frame (NFGPUKernelModule::Execute, or a server loop of its own):
+//   BeginFrame()  before the frame's device pass: finishes the ticket all-gather started at the end
+//                 of the previous frame; when its plan is not empty, the departures' rows leave the
+//                 world (nfk_export_objects), every rank's export status is all-gathered (so all
+//                 ranks go on to the row exchange or all stop: a failed export never leaves a peer
+//                 waiting in a collective), the rows move and the arrivals enter with their
+//                 SwitchScene property writes.  An empty plan makes no collective at all.
+//   EndFrame()    after the frame: on an exchange frame (every `exchange_every`-th, the same on
+//                 every rank) starts the all-gather of the tickets queued so far on a worker thread
+//                 and the transport's side channel (RCCL: a communicator split off the rows' one, on
+//                 its own stream), so it runs while the game logic prepares the next frame; on other
+//                 frames it makes no transport call.
+// A SwitchScene into another shard therefore takes effect at the start of the frame after the
+// next exchange frame.  Migrate() is the synchronous form (gather now, rows now).
 #pragma once
 #include <cstdint>
 #include <functional>
+#include <future>
 #include <memory>
 #include <vector>
 
@@ -51,7 +67,8 @@ public:
     virtual ~ShardTransport() = default;
     virtual int Rank() const = 0;
     virtual int Size() const = 0;
-    // every rank's int64 words, concatenated in rank order (collective)
+    // every rank's int64 words, concatenated in rank order (collective; the tickets' channel, which
+    // may run on a worker thread while the rows' channel is idle)
     virtual int AllGather(const std::vector<int64_t>& mine, std::vector<int64_t>& all) = 0;
     // rows: send[r] / recv[r] words to / from rank r, buffers packed in rank order (collective);
     // stream: the world's stream (RCCL enqueues there; host transports wait for it first)
@@ -80,8 +97,10 @@ private:
     RowMemory mem_;
 };
 
-// RCCL (ncclComm per process, one GPU each): tickets by ncclAllGather (count, then the rows padded
-// to the largest count), rows by grouped ncclSend / ncclRecv on the world's stream.
+// RCCL (ncclComm per process, one GPU each): rows by grouped ncclSend / ncclRecv on the world's
+// stream (the stream AllToAllV is given); tickets by ncclAllGather (count, then the rows padded to
+// the largest count) on a communicator split off the rows' one and a stream of its own, so a ticket
+// gather on a worker thread neither waits for nor blocks the world's stream.
 class RcclTransport : public ShardTransport {
 public:
     // unique_id: the 128-byte ncclUniqueId rank 0 made (NewUniqueId) and every rank received out
@@ -97,8 +116,11 @@ public:
     bool NeedsHostSync() const override { return false; }
 
 private:
-    void* comm_ = nullptr;
-    void* stream_ = nullptr;
+    void* comm_ = nullptr;       // rows
+    void* meta_comm_ = nullptr;  // tickets
+    void* stream_ = nullptr;     // rows, when AllToAllV is given no stream
+    void* meta_stream_ = nullptr;
+    int device_ = 0;
     int rank_, size_;
     int64_t* buf_ = nullptr;  // device staging of the ticket all-gather
     size_t buf_cap_ = 0;
@@ -106,22 +128,33 @@ private:
 
 class SceneShard {
 public:
-    // owner(scene) -> rank; scene-property ids of the world (nfk_set_scene_props; -1: absent)
+    // owner(scene) -> rank; scene-property ids of the world (nfk_set_scene_props; -1: absent);
+    // stream: the world's stream (nullptr: asked from the world, nfk_get_stream)
     SceneShard(void* world, ShardTransport* t, std::function<int(int)> owner, int pid_scene, int pid_group, int pid_x,
                int pid_y, int pid_z, RowMemory mem = DeviceRowMemory(), void* stream = nullptr);
     ~SceneShard();
     bool Owns(int scene) const { return owner_(scene) == t_->Rank(); }
     int Owner(int scene) const { return owner_(scene); }
-    // a SwitchScene whose target this shard does not own: queued for the next Migrate (the entity
-    // leaves at the start of the next frame)
+    // a SwitchScene whose target this shard does not own: queued for the next exchange (the entity
+    // leaves when that exchange's rows move)
     void QueueSwitch(int64_t guid_head, int64_t guid_data, int cls, int is_player, int scene, int group, float x,
                      float y, float z);
-    // collective, once per frame before the frame runs on every rank: tickets, rows, imports and the
-    // SwitchScene property writes on arrival.  sent / received: this rank's tickets.
+    // tickets are all-gathered every `every`-th EndFrame (the same on every rank; default 1)
+    void SetExchangeEvery(int every) { every_ = every < 1 ? 1 : every; }
+    // collective, before every frame on every rank (see the header): the rows of the plan gathered
+    // one frame ago.  sent / received: this rank's tickets of that plan.
+    int BeginFrame(std::vector<Ticket>* sent = nullptr, std::vector<Ticket>* received = nullptr);
+    // collective, after every frame on every rank: starts the next ticket gather on an exchange frame
+    int EndFrame();
+    // synchronous exchange of the tickets queued so far (collective): gather, then rows
     int Migrate(std::vector<Ticket>* sent = nullptr, std::vector<Ticket>* received = nullptr);
     int64_t migrated_out = 0, migrated_in = 0;
+    int64_t transport_calls = 0;  // collective calls this shard made (AllGather, AllToAllV)
+    int64_t frames = 0;           // EndFrame calls
 
 private:
+    std::vector<int64_t> TakeTickets();
+    int Rows(const std::vector<int64_t>& plan, std::vector<Ticket>* sent, std::vector<Ticket>* received);
     void* world_;
     ShardTransport* t_;
     std::function<int(int)> owner_;
@@ -132,6 +165,9 @@ private:
     uint64_t* sbuf_ = nullptr;
     uint64_t* rbuf_ = nullptr;
     size_t scap_ = 0, rcap_ = 0;
+    int every_ = 1;
+    std::future<int> pending_;  // the ticket gather started by the last exchange EndFrame
+    std::vector<int64_t> pending_plan_;
 };
 
 }  // namespace nfgpu

@@ -330,6 +330,9 @@ int nfk_execute(void* world, int64_t now_ms);
 int nfk_execute_calls(void* world);
 /* wait for everything queued on the world's stream */
 int nfk_sync(void* world);
+/* the hipStream_t the world launches on (nfk_config.stream, or the library's own): a caller that
+ * moves the world's rows (the scene shards' RCCL transport) orders its work on it */
+int nfk_get_stream(void* world, void** stream);
 /* synchronise and read the counters of the last tick */
 int nfk_summary_get(void* world, nfk_summary* out);
 int nfk_outputs_get(void* world, nfk_outputs* out);

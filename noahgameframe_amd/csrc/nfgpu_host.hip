@@ -3677,6 +3677,13 @@ int nfk_sync(void* world) {
     return NFK_OK;
 }
 
+int nfk_get_stream(void* world, void** stream) {
+    World* w = (World*)world;
+    if (!w || !stream) return fail(NFK_ERR_ARG, "null argument");
+    *stream = (void*)w->stream;
+    return NFK_OK;
+}
+
 static int ensure_ranks(World* w) {
     if (!w->scan_pending) return NFK_OK;
     w->scan_pending = false;

@@ -670,11 +670,13 @@ void NFGPUKernelModule::SetKindFunctor(const std::string& name, const OBJECT_SCH
     kind_cb_[name] = {cb, fTime};
 }
 
-// the shard exchange of this frame (collective): departures leave, arrivals become this module's
-// objects, their schedules with the functors of their names
-void NFGPUKernelModule::MigrateShard() {
+// the shard exchange (collective): departures leave, arrivals become this module's objects, their
+// schedules with the functors of their names.  sync: gather the tickets now (MigrateNow); else the
+// rows of the gather the previous Execute started (SceneShard::BeginFrame)
+void NFGPUKernelModule::MigrateShard(bool sync) {
     std::vector<Ticket> sent, recv;
-    check(shard_->Migrate(&sent, &recv), "SceneShard::Migrate");
+    if (sync) check(shard_->Migrate(&sent, &recv), "SceneShard::Migrate");
+    else check(shard_->BeginFrame(&sent, &recv), "SceneShard::BeginFrame");
     for (const Ticket& k : recv) {
         const NFGUID g(k.guid_head, k.guid_data);
         const int o = (int)guids_.size();
@@ -695,7 +697,7 @@ void NFGPUKernelModule::MigrateShard() {
 bool NFGPUKernelModule::Execute() {
     const auto t0 = std::chrono::steady_clock::now();
     stats_ = FrameStats{};
-    if (shard_) MigrateShard();
+    if (shard_) MigrateShard(false);
     check(nfk_execute(world_, clock_()), "nfk_execute");
     pending_calls_ = 0;
     check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
@@ -762,6 +764,9 @@ bool NFGPUKernelModule::Execute() {
         }
     }
     module_sched_.Execute(clock_);  // module schedules (SM:123-176)
+    // the departures queued up to now (this window's and the functors'): their tickets are
+    // gathered off the world's stream while the next window's game logic runs
+    if (shard_) check(shard_->EndFrame(), "SceneShard::EndFrame");
     stats_.calls = ms_since(t1);
     stats_.total = ms_since(t0);
     return true;

@@ -74,26 +74,35 @@ int HostTransport::AllToAllV(const uint64_t* send, const std::vector<size_t>& sc
     }
     s_->barrier();
     // pull my part of every source's buffer: source r packs its rows in destination order
+    int rc = NFK_OK;
     size_t at = 0;
-    for (int r = 0; r < s_->size; r++) {
+    for (int r = 0; r < s_->size && rc == NFK_OK; r++) {
         const std::vector<size_t>& sc = *s_->scount[r];
         size_t off = 0;
         for (int q = 0; q < rank_; q++) off += sc[q];
-        if (sc[rank_] != rcount[r]) return NFK_ERR_STATE;
+        if (sc[rank_] != rcount[r]) {
+            rc = NFK_ERR_STATE;  // (still through the second barrier: the peers are waiting at it)
+            break;
+        }
         if (rcount[r]) mem_.copy(recv + at, s_->send[r] + off, rcount[r] * 8);
         at += rcount[r];
     }
     s_->barrier();
-    return NFK_OK;
+    return rc;
 }
 
 // ---------------- SceneShard ----------------
 SceneShard::SceneShard(void* world, ShardTransport* t, std::function<int(int)> owner, int pid_scene, int pid_group,
                        int pid_x, int pid_y, int pid_z, RowMemory mem, void* stream)
     : world_(world), t_(t), owner_(std::move(owner)), pid_scene_(pid_scene), pid_group_(pid_group), pid_x_(pid_x),
-      pid_y_(pid_y), pid_z_(pid_z), mem_(std::move(mem)), stream_(stream) {}
+      pid_y_(pid_y), pid_z_(pid_z), mem_(std::move(mem)), stream_(stream) {
+    // the rows are packed and unpacked on the world's stream: an RCCL transport sends and receives
+    // on that same stream (stream order, no host synchronisation)
+    if (!stream_ && world_) (void)nfk_get_stream(world_, &stream_);
+}
 
 SceneShard::~SceneShard() {
+    if (pending_.valid()) (void)pending_.get();  // (a gather still in flight: the peers need this rank in it)
     if (sbuf_) mem_.release(sbuf_);
     if (rbuf_) mem_.release(rbuf_);
 }
@@ -126,9 +135,8 @@ static double bits_f64(int64_t b) {
     return v;
 }
 
-int SceneShard::Migrate(std::vector<Ticket>* sent, std::vector<Ticket>* received) {
-    const int ws = t_->Size(), me = t_->Rank();
-    // 1. the frame's global plan: every rank's tickets in (source rank, call) order
+// this rank's queued tickets as words (TICKET layout), taken off the queue
+std::vector<int64_t> SceneShard::TakeTickets() {
     std::vector<int64_t> mine;
     mine.reserve(out_.size() * kTicketWords);
     for (const Ticket& k : out_) {
@@ -138,13 +146,53 @@ int SceneShard::Migrate(std::vector<Ticket>* sent, std::vector<Ticket>* received
         mine.insert(mine.end(), w, w + kTicketWords);
     }
     out_.clear();
-    std::vector<int64_t> plan;
-    int r = t_->AllGather(mine, plan);
-    if (r) return r;
-    const size_t n = plan.size() / kTicketWords;
+    return mine;
+}
+
+int SceneShard::EndFrame() {
+    frames++;
+    if (pending_.valid()) return NFK_ERR_STATE;  // the last gather was never taken by BeginFrame
+    if (frames % every_) return NFK_OK;          // not an exchange frame: no transport call
+    std::vector<int64_t> mine = TakeTickets();
+    transport_calls++;
+    pending_plan_.clear();
+    // on a worker thread: the game logic of the next window runs meanwhile
+    pending_ = std::async(std::launch::async,
+                          [this, mine = std::move(mine)]() { return t_->AllGather(mine, pending_plan_); });
+    return NFK_OK;
+}
+
+int SceneShard::BeginFrame(std::vector<Ticket>* sent, std::vector<Ticket>* received) {
     if (sent) sent->clear();
     if (received) received->clear();
-    if (n == 0) return NFK_OK;  // the same on every rank: no row exchange this frame
+    if (!pending_.valid()) return NFK_OK;  // no gather since the last one: nothing to move
+    const int r = pending_.get();
+    if (r) return r;
+    std::vector<int64_t> plan;
+    plan.swap(pending_plan_);
+    return Rows(plan, sent, received);
+}
+
+int SceneShard::Migrate(std::vector<Ticket>* sent, std::vector<Ticket>* received) {
+    // (a gather EndFrame started is finished first: every rank makes its collectives in one order)
+    std::vector<Ticket> s0, r0;
+    int r = BeginFrame(&s0, &r0);
+    if (r) return r;
+    std::vector<int64_t> plan;
+    transport_calls++;
+    r = t_->AllGather(TakeTickets(), plan);
+    if (r) return r;
+    r = Rows(plan, sent, received);
+    if (sent) sent->insert(sent->begin(), s0.begin(), s0.end());
+    if (received) received->insert(received->begin(), r0.begin(), r0.end());
+    return r;
+}
+
+// the rows of a global plan (every rank's tickets in (source rank, call) order), rank to rank
+int SceneShard::Rows(const std::vector<int64_t>& plan, std::vector<Ticket>* sent, std::vector<Ticket>* received) {
+    const int ws = t_->Size(), me = t_->Rank();
+    const size_t n = plan.size() / kTicketWords;
+    if (n == 0) return NFK_OK;  // the same on every rank: no row exchange
     auto tk = [&](size_t i) {
         const int64_t* w = &plan[i * kTicketWords];
         Ticket k;
@@ -170,36 +218,50 @@ int SceneShard::Migrate(std::vector<Ticket>* sent, std::vector<Ticket>* received
     // rows in destination order (call order within one), received in source order
     std::stable_sort(snd.begin(), snd.end(), [](const Ticket& a, const Ticket& b) { return a.dst < b.dst; });
     std::stable_sort(rcv.begin(), rcv.end(), [](const Ticket& a, const Ticket& b) { return a.src < b.src; });
+    // 1. the local half: buffers and the export (the entities leave this world; rows packed on the
+    // world's stream).  A failure here does not return yet: every rank first learns every rank's status
     int32_t rw = 0;
-    r = nfk_row_words(world_, &rw);
-    if (r) return r;
+    int status = nfk_row_words(world_, &rw);
     std::vector<size_t> scount(ws, 0), rcount(ws, 0);
-    for (const Ticket& k : snd) scount[k.dst] += (size_t)rw;
-    for (const Ticket& k : rcv) rcount[k.src] += (size_t)rw;
-    auto reserve = [&](uint64_t*& buf, size_t& cap, size_t words) {
-        if (words <= cap) return;
-        if (buf) mem_.release(buf);
-        cap = words + words / 2 + 64;
-        buf = (uint64_t*)mem_.alloc(cap * 8);
-    };
-    reserve(sbuf_, scap_, snd.size() * (size_t)rw);
-    reserve(rbuf_, rcap_, rcv.size() * (size_t)rw);
-    // 2. export (the entities leave this world; their rows packed on the world's stream)
-    if (!snd.empty()) {
+    if (!status) {
+        for (const Ticket& k : snd) scount[k.dst] += (size_t)rw;
+        for (const Ticket& k : rcv) rcount[k.src] += (size_t)rw;
+        auto reserve = [&](uint64_t*& buf, size_t& cap, size_t words) {
+            if (words <= cap) return;
+            if (buf) mem_.release(buf);
+            buf = nullptr;
+            cap = 0;
+            buf = (uint64_t*)mem_.alloc((words + words / 2 + 64) * 8);
+            cap = words + words / 2 + 64;
+        };
+        try {
+            reserve(sbuf_, scap_, snd.size() * (size_t)rw);
+            reserve(rbuf_, rcap_, rcv.size() * (size_t)rw);
+        } catch (const std::exception&) {
+            status = NFK_ERR_HIP;
+        }
+    }
+    if (!status && !snd.empty()) {
         std::vector<int64_t> gh(snd.size()), gd(snd.size());
         for (size_t i = 0; i < snd.size(); i++) {
             gh[i] = snd[i].guid_head;
             gd[i] = snd[i].guid_data;
         }
-        r = nfk_export_objects(world_, (int32_t)snd.size(), gh.data(), gd.data(), sbuf_);
-        if (r) return r;
+        status = nfk_export_objects(world_, (int32_t)snd.size(), gh.data(), gd.data(), sbuf_);
     }
-    if (t_->NeedsHostSync()) {
-        r = nfk_sync(world_);
+    if (!status && t_->NeedsHostSync()) status = nfk_sync(world_);
+    // 2. every rank's status (collective): all ranks go on to the row exchange, or none does
+    {
+        std::vector<int64_t> mine(1, (int64_t)status), all;
+        transport_calls++;
+        const int r = t_->AllGather(mine, all);
         if (r) return r;
+        for (int64_t v : all)
+            if (v) return status ? status : NFK_ERR_STATE;  // (a peer failed: its rows never come)
     }
-    // 3. the rows, rank to rank
-    r = t_->AllToAllV(sbuf_, scount, rbuf_, rcount, stream_);
+    // 3. the rows, rank to rank (on the world's stream for RCCL)
+    transport_calls++;
+    int r = t_->AllToAllV(sbuf_, scount, rbuf_, rcount, stream_);
     if (r) return r;
     // 4. import, then the SwitchScene property writes (KM:930-942): GroupID = 0, SceneID, X, Y, Z,
     // GroupID, per entity in this order (the scene always changes here)

@@ -231,6 +231,95 @@ class SceneShard:
             dist.all_to_all_single(rbuf.view(-1), sbuf.view(-1), rsplit, ssplit, group=self.pg)
 
 
+class CppSceneShard:
+    """The C++ scene shard (include/NFGPUSceneShard.hpp: SceneShard over RcclTransport, through
+    include/nfgpu_shard.h in libnfgpu_plugin.so) for this rank's world `m` (kernel.NFKernelModule):
+    the production exchange a C++ game server runs.  Per frame: begin_frame() before the world's
+    Execute (rows of the tickets gathered one frame ago; no collective when nobody migrates), then
+    queue() the window's departures and end_frame() after it (the ticket all-gather starts on a
+    worker thread and RCCL's side communicator).  `owner`: owner[scene] = rank.  The RCCL id is made
+    by rank 0 and broadcast over `meta_group` (gloo)."""
+
+    def __init__(self, m, rank, world_size, owner, scene_props, meta_group=None, exchange_every=1):
+        import ctypes
+        import os
+        import torch.distributed as dist
+        self.ct = ctypes
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnfgpu_plugin.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is not built (python -c 'import __graft_entry__ as g; g.build()')")
+        lib = self.lib = ctypes.CDLL(path)
+        P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        lib.nfs_rccl_unique_id.argtypes = [P]
+        lib.nfs_create_rccl.argtypes = [P, P, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, ctypes.POINTER(P)]
+        lib.nfs_destroy.argtypes = [P]
+        lib.nfs_destroy.restype = None
+        lib.nfs_queue_switch.argtypes = [P, I32] + [P] * 9
+        lib.nfs_begin_frame.argtypes = [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]
+        lib.nfs_received.argtypes = [P, I64] + [P] * 6
+        lib.nfs_end_frame.argtypes = [P]
+        lib.nfs_stats.argtypes = [P, P]
+        uid = np.zeros(128, np.uint8)
+        if rank == 0 and lib.nfs_rccl_unique_id(uid.ctypes.data):
+            raise RuntimeError("nfs_rccl_unique_id failed")
+        if world_size > 1:
+            box = [uid if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0, group=meta_group)
+            uid = np.ascontiguousarray(box[0], np.uint8)
+        self.owner = np.ascontiguousarray(owner, np.int32)
+        ps, pg, px, py, pz = (int(p) for p in scene_props)
+        h = ctypes.c_void_p()
+        r = lib.nfs_create_rccl(m.h, uid.ctypes.data, rank, world_size, self.owner.ctypes.data,
+                                len(self.owner), ps, pg, px, py, pz, int(exchange_every), ctypes.byref(h))
+        if r:
+            raise RuntimeError(f"nfs_create_rccl failed ({r})")
+        self.h = h
+        self.m, self.rank, self.ws = m, rank, world_size
+
+    def queue(self, tickets):
+        """Departures as a ticket array (TICKET_COLS)."""
+        t = np.ascontiguousarray(tickets, np.int64).reshape(-1, 11)
+        if not len(t):
+            return
+        i32 = lambda c: np.ascontiguousarray(t[:, c], np.int32)
+        f32 = lambda c: np.ascontiguousarray(t[:, c].view(np.float64), np.float32)
+        cols = [np.ascontiguousarray(t[:, T_GH]), np.ascontiguousarray(t[:, T_GD]), i32(T_CLS), i32(T_PL),
+                i32(T_SCENE), i32(T_GROUP), f32(T_X), f32(T_Y), f32(T_Z)]
+        if self.lib.nfs_queue_switch(self.h, len(t), *[c.ctypes.data for c in cols]):
+            raise RuntimeError("nfs_queue_switch failed")
+
+    def begin_frame(self):
+        """Collective: the rows of the last gather; returns the arrivals as a ticket array."""
+        ns, nr = self.ct.c_int64(), self.ct.c_int64()
+        r = self.lib.nfs_begin_frame(self.h, self.ct.byref(ns), self.ct.byref(nr))
+        if r:
+            raise RuntimeError(f"SceneShard::BeginFrame failed ({r})")
+        n = nr.value
+        out = np.zeros((n, 11), np.int64)
+        if n:
+            gh, gd = np.zeros(n, np.int64), np.zeros(n, np.int64)
+            cl, pl, sc, gr = (np.zeros(n, np.int32) for _ in range(4))
+            self.lib.nfs_received(self.h, n, *[a.ctypes.data for a in (gh, gd, cl, pl, sc, gr)])
+            out[:, T_GH], out[:, T_GD], out[:, T_CLS], out[:, T_PL], out[:, T_SCENE], out[:, T_GROUP] = gh, gd, cl, pl, sc, gr
+            out[:, T_DST] = self.rank
+        return out
+
+    def end_frame(self):
+        if self.lib.nfs_end_frame(self.h):
+            raise RuntimeError("SceneShard::EndFrame failed")
+
+    def stats(self):
+        """(migrated out, migrated in, transport calls, frames)"""
+        a = np.zeros(4, np.int64)
+        self.lib.nfs_stats(self.h, a.ctypes.data)
+        return tuple(int(x) for x in a)
+
+    def close(self):
+        if self.h:
+            self.lib.nfs_destroy(self.h)
+            self.h = None
+
+
 class _Ready:
     def __init__(self, plan):
         self.plan = plan

@@ -385,6 +385,10 @@ int nfk_execute_calls(void* w) {
     return NFK_OK;
 }
 int nfk_sync(void*) { return NFK_OK; }
+int nfk_get_stream(void*, void** s) {
+    *s = nullptr;
+    return NFK_OK;
+}
 int nfk_summary_get(void* w, nfk_summary* out) {
     memset(out, 0, sizeof *out);
     out->n_entities = (int64_t)S(w)->idx.size();

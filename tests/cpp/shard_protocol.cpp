@@ -148,6 +148,66 @@ int main(int argc, char** argv) {
     }
     nfk_destroy(worlds[0]);
     nfk_destroy(worlds[1]);
+    if (g_fail) return g_fail;
+
+    // ---- the per-frame protocol (BeginFrame / EndFrame) with an exchange every 3rd frame: tickets
+    // queued in window 2 are gathered by frame 3's EndFrame (on a worker thread) and their rows move
+    // at frame 4's BeginFrame; a frame that is not an exchange frame, or follows an empty gather,
+    // makes no transport call at all ----
+    void* w2[2] = {make_world(0), make_world(1)};
+    auto shared2 = HostTransport::MakeShared(2);
+    int64_t calls[2][10] = {}, moved[2] = {0, 0};
+    auto rank_frames = [&](int r) {
+        HostTransport t(shared2, r, mem);
+        SceneShard sh(w2[r], &t, [](int scene) { return scene == 1 ? 0 : 1; }, P_SCENE, P_GROUP, P_X, P_Y, P_Z, mem);
+        sh.SetExchangeEvery(3);
+        for (int f = 1; f <= 9; f++) {
+            const int64_t c0 = sh.transport_calls;
+            if (f == 2) sh.QueueSwitch(7, 100 * r + 1, 0, 0, 2 - r, 9, 1.0f, 2.0f, 3.0f);
+            std::vector<Ticket> s, rv;
+            CHECK(sh.BeginFrame(&s, &rv) == NFK_OK, "rank %d BeginFrame %d", r, f);
+            if (f == 4) CHECK(s.size() == 1 && rv.size() == 1, "rank %d frame 4 moved %zu %zu", r, s.size(), rv.size());
+            else CHECK(s.empty() && rv.empty(), "rank %d frame %d moved entities", r, f);
+            CHECK(sh.EndFrame() == NFK_OK, "rank %d EndFrame %d", r, f);
+            calls[r][f] = sh.transport_calls - c0;
+        }
+        moved[r] = sh.migrated_out + sh.migrated_in;
+    };
+    std::thread f0(rank_frames, 0), f1(rank_frames, 1);
+    f0.join();
+    f1.join();
+    const int64_t want[10] = {0, 0, 0, 1, 2, 0, 1, 0, 0, 1};
+    for (int r = 0; r < 2; r++) {
+        for (int f = 1; f <= 9; f++)
+            CHECK(calls[r][f] == want[f], "rank %d frame %d: %lld transport calls, want %lld", r, f, (long long)calls[r][f],
+                  (long long)want[f]);
+        CHECK(moved[r] == 2, "rank %d moved %lld", r, (long long)moved[r]);
+        int64_t h = 7, d = 100 * (1 - r) + 1;
+        int32_t p = P_GROUP;
+        uint64_t b = 0;
+        CHECK(nfk_get_props(w2[r], 1, &h, &d, &p, &b) == NFK_OK && b == 9, "rank %d arrival group %llu", r,
+              (unsigned long long)b);
+    }
+    nfk_destroy(w2[0]);
+    nfk_destroy(w2[1]);
+
+    // ---- a departure that cannot leave (no such entity on rank 0): every rank learns every rank's
+    // export status before the row exchange, so both fail and neither waits for the other ----
+    void* w3[2] = {make_world(0), make_world(1)};
+    auto shared3 = HostTransport::MakeShared(2);
+    int rc3[2] = {0, 0};
+    auto rank_fail = [&](int r) {
+        HostTransport t(shared3, r, mem);
+        SceneShard sh(w3[r], &t, [](int scene) { return scene == 1 ? 0 : 1; }, P_SCENE, P_GROUP, P_X, P_Y, P_Z, mem);
+        sh.QueueSwitch(7, r == 0 ? 999 : 101, 0, 0, 2 - r, 3, 0.f, 0.f, 0.f);
+        rc3[r] = sh.Migrate();
+    };
+    std::thread g0(rank_fail, 0), g1(rank_fail, 1);
+    g0.join();
+    g1.join();
+    CHECK(rc3[0] != NFK_OK && rc3[1] != NFK_OK, "a failed export: statuses %d %d", rc3[0], rc3[1]);
+    nfk_destroy(w3[0]);
+    nfk_destroy(w3[1]);
     if (!g_fail) printf("shard_protocol %s: ok\n", device ? "device" : "host");
     return g_fail;
 }

@@ -22,6 +22,10 @@ def _build():
 
 
 def test_shard_protocol_host_stub(tmp_path):
+    """Also: the per-frame protocol (SceneShard::BeginFrame / EndFrame) with an exchange every 3rd
+    frame makes no transport call on a frame that is not an exchange frame or that follows an empty
+    gather, moves the rows one frame after the gather, and a failed export on one rank makes every
+    rank fail instead of leaving a peer waiting in the row exchange (tests/cpp/shard_protocol.cpp)."""
     _build()
     log = str(tmp_path / "stub.log")
     env = dict(os.environ, NFGPU_STUB_LOG=log, LD_LIBRARY_PATH=STUB + ":" + os.environ.get("LD_LIBRARY_PATH", ""))
@@ -29,9 +33,12 @@ def test_shard_protocol_host_stub(tmp_path):
     assert r.returncode == 0, r.stderr
     lines = [ln.split() for ln in open(log)]
     exports = [(int(x[1]), int(x[2])) for x in lines if x[0] == "export"]
-    assert sorted(exports) == sorted([(7, i) for i in (0, 2, 4)] + [(7, 100 + i) for i in (0, 2, 4)])
+    # the synchronous Migrate of the first scenario, then the per-frame exchange's one entity per rank,
+    # then the failing scenario's rank 1 (its export runs before the status exchange stops both ranks)
+    assert sorted(exports[:6]) == sorted([(7, i) for i in (0, 2, 4)] + [(7, 100 + i) for i in (0, 2, 4)])
+    assert sorted(exports[6:8]) == [(7, 1), (7, 101)] and exports[8:] == [(7, 101)]
     imports = [x for x in lines if x[0] == "import"]
-    assert len(imports) == 6
+    assert len(imports) == 8
     # per arrival, its writes in order: GroupID 0, SceneID, X, Y, Z, GroupID (pids 1, 0, 3, 4, 5, 1)
     sets = [x for x in lines if x[0] == "set"]
     by = {}
@@ -39,7 +46,7 @@ def test_shard_protocol_host_stub(tmp_path):
         by.setdefault((int(x[1]), int(x[2])), []).append((int(x[3]), int(x[4])))
     for (h, d), w in by.items():
         assert [p for p, _ in w] == [1, 0, 3, 4, 5, 1], (d, w)
-        assert w[0][1] == 0 and w[-1][1] == 5 + d % 100
+        assert w[0][1] == 0 and w[-1][1] == (9 if d % 100 == 1 else 5 + d % 100)
 
 
 @pytest.mark.gpu

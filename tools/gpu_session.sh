@@ -48,6 +48,8 @@ for step in "$@"; do
     hbmstream) run hbmstream 240 tools/_bin/hbm_stream ;;
     pluginbench) run pluginbench 600 python bench.py --steps 20 --warmup 3 --cpu-baseline off --host-calls off ;;
     membership) NFGPU_TRACE_MEMBERSHIP=1 run membership 300 python tools/membership_bench.py ;;
+    selfmigcpp) run selfmigcpp 300 python bench.py --self-migrate --shard cpp --steps 24 --warmup 8 --cpu-baseline off \
+               --host-calls off --plugin-frame off --other-configs off ;;
     selfmig) NFGPU_BENCH_TRACE=1 NFGPU_TRACE_EXEC=1 NFGPU_TRACE_MEMBERSHIP=1 run selfmig 300 python bench.py --self-migrate \
                --steps 24 --warmup 8 --cpu-baseline off --host-calls off ;;
     ablate) run ablate 600 python tools/ablate.py --variants ${ABL:-0,8,4} ;;
