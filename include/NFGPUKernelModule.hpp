@@ -36,6 +36,7 @@
 //     are device columns like the int / float ones.
 #pragma once
 #include <cstdint>
+#include <cstring>
 #include <functional>
 #include <map>
 #include <memory>
@@ -47,6 +48,64 @@
 #include "nfgpu.h"
 #include "nfgpu_guidmap.hpp"
 #include "NFGPUSceneShard.hpp"
+
+namespace nfgpu_detail {
+// property / record name -> index for the per-call API: open addressing on an FNV-1a hash of the
+// name's bytes, the table at most a quarter full (a lookup is one hash and, mostly, one compare;
+// std::unordered_map<std::string> cost ~25 ns per SetProperty call, profiles/r10e_*)
+class NameIndex {
+public:
+    void insert(const std::string& k, int v) {
+        if ((n_ + 1) * 4 > t_.size()) grow();
+        put(k, v);
+    }
+    int find(const std::string& k) const {
+        if (t_.empty()) return -1;
+        for (size_t i = hash(k.data(), k.size()) & mask_;; i = (i + 1) & mask_) {
+            const E& e = t_[i];
+            if (e.v < 0) return -1;
+            if (e.k.size() == k.size() && std::memcmp(e.k.data(), k.data(), k.size()) == 0) return e.v;
+        }
+    }
+
+private:
+    struct E {
+        std::string k;
+        int v = -1;
+    };
+    static uint64_t hash(const char* p, size_t n) {
+        uint64_t h = 0xcbf29ce484222325ull;
+        for (size_t i = 0; i < n; i++) h = (h ^ (uint8_t)p[i]) * 0x100000001b3ull;
+        return h ^ (h >> 29);
+    }
+    void put(const std::string& k, int v) {
+        for (size_t i = hash(k.data(), k.size()) & mask_;; i = (i + 1) & mask_) {
+            E& e = t_[i];
+            if (e.v < 0) {
+                e.k = k;
+                e.v = v;
+                n_++;
+                return;
+            }
+            if (e.k == k) {
+                e.v = v;
+                return;
+            }
+        }
+    }
+    void grow() {
+        std::vector<E> old;
+        old.swap(t_);
+        t_.assign(std::max<size_t>(16, old.size() * 2), E{});
+        mask_ = t_.size() - 1;
+        n_ = 0;
+        for (E& e : old)
+            if (e.v >= 0) put(e.k, e.v);
+    }
+    std::vector<E> t_;
+    size_t mask_ = 0, n_ = 0;
+};
+}  // namespace nfgpu_detail
 
 namespace nfgpu {
 
@@ -301,7 +360,9 @@ public:
     using FRAME_FUNCTOR = std::function<void(const nfk_frame_host&, const NFGUID* objects)>;
     bool AddFrameCallBack(const FRAME_FUNCTOR& cb, uint32_t what);
 
+    // the world (nfk C-ABI); Flush() first hands it the buffered SetProperty calls
     void* World() const { return world_; }
+    void Flush();
     const nfk_summary& LastSummary() const { return summary_; }
     // host wall time of the last Execute by phase (ms): the device frame (nfk_execute and the wait
     // for its counters), the heartbeat functors (fired list read + order + calls), the event lists
@@ -326,6 +387,11 @@ private:
     bool committed_ = false;
     std::vector<PropertyDef> props_;
     std::unordered_map<std::string, int> prop_id_;
+    nfgpu_detail::NameIndex prop_ix_;  // prop_id_ for the per-call API
+    // SetPropertyInt / Float calls buffered on the host (checked, in call order) and handed to the
+    // world in one nfk_set_props_obj before anything that must see them (Flush)
+    std::vector<int32_t> qs_obj_, qs_pid_;
+    std::vector<uint64_t> qs_bits_;
     std::vector<int> dev_pid_;  // props_ index -> device property id (AfterInit)
     std::vector<ClassDef> classes_;
     std::map<std::string, int> class_id_;
@@ -361,7 +427,19 @@ private:
     std::vector<int> def_of_pid_;  // device property id -> props_ index
     // pending functors of AddSchedule calls in this window ((object, kind), first call wins)
     // key: object << 8 | kind
-    std::unordered_map<uint64_t, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> sched_add_;
+    struct PendingAdd {
+        uint64_t key;  // object << 8 | kind
+        OBJECT_SCHEDULE_FUNCTOR cb;
+        float t;
+    };
+    std::vector<PendingAdd> sched_add_;  // in call order; the first call of a key wins
+    // schedule calls buffered like the Sets (nfk_schedule_calls_obj in Flush)
+    std::vector<int32_t> qh_op_, qh_obj_, qh_kind_, qh_cnt_;
+    std::vector<float> qh_t_;
+    std::vector<int64_t> qh_now_;
+    nfgpu_detail::NameIndex hb_ix_;  // schedule name -> kind (AfterInit)
+    void QueueScheduleCall(int32_t op, int32_t o, int32_t kind, float t, int32_t cnt, int64_t now);
+    void DropPendingAdds(int o);
     ModuleScheduler module_sched_;
     SceneShard* shard_ = nullptr;
     std::map<std::string, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> kind_cb_;  // arrivals' functors

@@ -336,6 +336,7 @@ private:
     // int cells, written into the host objects where they differ (one batched device read each);
     // the host NFCProperty / NFCRecord then fires the per-object callbacks for the difference.
     void SyncHostObjects() {
+        gpu_.Flush();  // (this reads the world through the C-ABI)
         std::vector<std::pair<NFGUID, std::string>> props;
         props.swap(sync_props_);
         std::vector<Cell> cells;

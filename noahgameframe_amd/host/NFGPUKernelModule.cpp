@@ -38,6 +38,7 @@ int NFGPUKernelModule::AddProperty(const std::string& name, TDATA_TYPE type) {
     if (it != prop_id_.end()) return it->second;
     props_.push_back({name, type});
     prop_id_[name] = (int)props_.size() - 1;
+    prop_ix_.insert(name, (int)props_.size() - 1);
     return prop_id_[name];
 }
 
@@ -163,6 +164,7 @@ bool NFGPUKernelModule::CreateScene(int nSceneID) {
 
 bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGroupID, const std::string& cls,
                                      const std::map<std::string, TData>& init) {
+    Flush();  // (the buffered Set calls first: call order)
     if (!scenes_.count(nSceneID)) return false;  // "There is no scene" (KM:107)
     if (committed_) {
         // after AfterInit: the entity enters at the start of the next frame (nfk_spawn_objects)
@@ -258,6 +260,7 @@ bool NFGPUKernelModule::AfterInit() {
               [](const HeartBeatDef& a, const HeartBeatDef& b) { return a.name < b.name; });
     for (int k = 0; k < (int)heartbeats_.size(); k++) {
         hb_id_[heartbeats_[k].name] = k;
+        hb_ix_.insert(heartbeats_[k].name, k);
         if (heartbeats_[k].symbolic)
             resolve_program(heartbeats_[k].ops, heartbeats_[k].props, heartbeats_[k].records,
                             [this](const std::string& n) { return PropertyId(n); },
@@ -322,6 +325,7 @@ bool NFGPUKernelModule::AfterInit() {
 
 bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int nTargetGroupID, float fX, float fY,
                                     float fZ, float /*fOrient*/, const std::vector<TData>& /*arg*/) {
+    Flush();  // (the buffered Set calls first: call order)
     if (!committed_ || ObjectIndex(self) < 0) return false;  // "There is no object" (KM:948)
     if (shard_ && !shard_->Owns(nTargetSceneID)) {          // into another shard's scene
         const int o = ObjectIndex(self);
@@ -329,8 +333,7 @@ bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int 
                             fZ);
         obj_of_.erase(self.nHead64, self.nData64);  // this module's no more (its index stays reserved)
         DropFunctors(o);
-        for (auto it = sched_add_.begin(); it != sched_add_.end();)
-            it = (int)(it->first >> 8) == o ? sched_add_.erase(it) : std::next(it);
+        DropPendingAdds(o);
         return true;
     }
     if (!scenes_.count(nTargetSceneID)) return false;       // "no this container" (KM:917)
@@ -344,19 +347,20 @@ bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int 
 }
 
 bool NFGPUKernelModule::DestroyObject(const NFGUID& self) {
+    Flush();  // (the buffered Set calls first: call order)
     const int o = ObjectIndex(self);
     if (!committed_ || o < 0) return false;
     check(nfk_destroy_objects(world_, 1, &self.nHead64, &self.nData64), "nfk_destroy_objects");
     pending_calls_++;
     obj_of_.erase(self.nHead64, self.nData64);  // its object index stays reserved; later calls find no object
     DropFunctors(o);
-    for (auto it = sched_add_.begin(); it != sched_add_.end();)
-        it = (int)(it->first >> 8) == o ? sched_add_.erase(it) : std::next(it);
+    DropPendingAdds(o);
     return true;
 }
 
 bool NFGPUKernelModule::GetRange(const std::string& prop, int k,
                                  std::vector<std::pair<std::string, double>>& memberScoreVec) {
+    Flush();  // (the buffered Set calls first: call order)
     memberScoreVec.clear();
     if (!committed_ || !prop_id_.count(prop) || k <= 0) return false;
     std::vector<int64_t> gh(k), gd(k);
@@ -370,21 +374,42 @@ bool NFGPUKernelModule::GetRange(const std::string& prop, int k,
 
 int NFGPUKernelModule::ObjectIndex(const NFGUID& g) const { return obj_of_.find(g.nHead64, g.nData64); }
 
-// (the object index this module found is nfk's: nfk_set_props_obj queues without a second lookup)
+// (the object index this module found is nfk's: nfk_set_props_obj queues without a second lookup.
+// The call is checked here — the object is this module's, the property an int one — and buffered;
+// Flush hands the buffer to the world in one call)
 bool NFGPUKernelModule::SetPropertyInt(const NFGUID& self, const std::string& name, int64_t v) {
-    auto it = prop_id_.find(name);
-    if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_INT) return false;
+    const int p = prop_ix_.find(name);
+    if (!committed_ || p < 0 || props_[(size_t)p].type != TDATA_INT) return false;
     const int32_t o = ObjectIndex(self);
     if (o < 0) return false;
-    int32_t pid = dev_pid_[(size_t)it->second];
-    uint64_t b = (uint64_t)v;
-    if (nfk_set_props_obj(world_, 1, &o, &pid, &b) != NFK_OK) return false;
+    qs_obj_.push_back(o);
+    qs_pid_.push_back(dev_pid_[(size_t)p]);
+    qs_bits_.push_back((uint64_t)v);
     pending_calls_++;
     return true;
 }
 
+void NFGPUKernelModule::Flush() {
+    if (!qs_obj_.empty()) {
+        const int rc = nfk_set_props_obj(world_, (int32_t)qs_obj_.size(), qs_obj_.data(), qs_pid_.data(), qs_bits_.data());
+        qs_obj_.clear();
+        qs_pid_.clear();
+        qs_bits_.clear();
+        check(rc, "nfk_set_props_obj");
+    }
+    if (!qh_op_.empty()) {
+        const int rc = nfk_schedule_calls_obj(world_, (int32_t)qh_op_.size(), qh_op_.data(), qh_obj_.data(),
+                                              qh_kind_.data(), qh_t_.data(), qh_cnt_.data(), qh_now_.data());
+        for (auto* v : {&qh_op_, &qh_obj_, &qh_kind_, &qh_cnt_}) v->clear();
+        qh_t_.clear();
+        qh_now_.clear();
+        check(rc, "nfk_schedule_calls_obj");
+    }
+}
+
 bool NFGPUKernelModule::SetRecordInt(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol,
                                      int64_t nValue) {
+    Flush();  // (the buffered Set calls first: call order)
     auto it = record_id_.find(strRecordName);
     if (it == record_id_.end() || ObjectIndex(self) < 0) return false;
     const RecordDef& rd = records_[it->second];
@@ -402,6 +427,7 @@ bool NFGPUKernelModule::SetRecordInt(const NFGUID& self, const std::string& strR
 
 bool NFGPUKernelModule::SetRecordFloat(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol,
                                        double dwValue) {
+    Flush();  // (the buffered Set calls first: call order)
     auto it = record_id_.find(strRecordName);
     if (it == record_id_.end() || ObjectIndex(self) < 0) return false;
     const RecordDef& rd = records_[it->second];
@@ -425,6 +451,7 @@ uint64_t NFGPUKernelModule::UsedRows(const NFGUID& self, int rec) {
 }
 
 bool NFGPUKernelModule::IsUsed(const NFGUID& self, const std::string& strRecordName, int nRow) {
+    Flush();  // (the buffered Set calls first: call order)
     auto it = record_id_.find(strRecordName);
     if (!committed_ || it == record_id_.end() || ObjectIndex(self) < 0 || nRow < 0 || nRow >= records_[it->second].rows)
         return false;
@@ -435,6 +462,7 @@ bool NFGPUKernelModule::IsUsed(const NFGUID& self, const std::string& strRecordN
 // reference holds it now, so the call is queued with that explicit row
 int NFGPUKernelModule::AddRow(const NFGUID& self, const std::string& strRecordName, int nRow,
                               const std::vector<TData>& values) {
+    Flush();  // (the buffered Set calls first: call order)
     auto it = record_id_.find(strRecordName);
     if (!committed_ || it == record_id_.end() || ObjectIndex(self) < 0) return -1;
     const RecordDef& rd = records_[it->second];
@@ -460,6 +488,7 @@ int NFGPUKernelModule::AddRow(const NFGUID& self, const std::string& strRecordNa
 
 // NFCRecord::Remove (RC:1086): true when the row was used
 bool NFGPUKernelModule::RemoveRow(const NFGUID& self, const std::string& strRecordName, int nRow) {
+    Flush();  // (the buffered Set calls first: call order)
     auto it = record_id_.find(strRecordName);
     if (!committed_ || it == record_id_.end() || ObjectIndex(self) < 0 || nRow < 0 || nRow >= records_[it->second].rows)
         return false;
@@ -472,6 +501,7 @@ bool NFGPUKernelModule::RemoveRow(const NFGUID& self, const std::string& strReco
 
 // NFCKernelModule::ClearRecord (KM:492) -> NFCRecord::Clear (RC:1109)
 bool NFGPUKernelModule::ClearRecord(const NFGUID& self, const std::string& strRecordName) {
+    Flush();  // (the buffered Set calls first: call order)
     auto it = record_id_.find(strRecordName);
     if (!committed_ || it == record_id_.end() || ObjectIndex(self) < 0) return false;
     const int32_t rec = it->second, op = 3, row = 0;
@@ -481,6 +511,7 @@ bool NFGPUKernelModule::ClearRecord(const NFGUID& self, const std::string& strRe
 }
 
 int64_t NFGPUKernelModule::GetRecordInt(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol) {
+    Flush();  // (the buffered Set calls first: call order)
     auto it = record_id_.find(strRecordName);
     if (it == record_id_.end() || ObjectIndex(self) < 0) return 0;
     const RecordDef& rd = records_[it->second];
@@ -492,6 +523,7 @@ int64_t NFGPUKernelModule::GetRecordInt(const NFGUID& self, const std::string& s
 }
 
 double NFGPUKernelModule::GetRecordFloat(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol) {
+    Flush();  // (the buffered Set calls first: call order)
     auto it = record_id_.find(strRecordName);
     if (it == record_id_.end() || ObjectIndex(self) < 0) return 0.0;
     const RecordDef& rd = records_[it->second];
@@ -506,13 +538,13 @@ double NFGPUKernelModule::GetRecordFloat(const NFGUID& self, const std::string& 
 }
 
 bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& name, double v) {
-    auto it = prop_id_.find(name);
-    if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT) return false;
+    const int p = prop_ix_.find(name);
+    if (!committed_ || p < 0 || props_[(size_t)p].type != TDATA_FLOAT) return false;
     const int32_t o = ObjectIndex(self);
     if (o < 0) return false;
-    int32_t pid = dev_pid_[(size_t)it->second];
-    uint64_t b = bits_of(v);
-    if (nfk_set_props_obj(world_, 1, &o, &pid, &b) != NFK_OK) return false;
+    qs_obj_.push_back(o);
+    qs_pid_.push_back(dev_pid_[(size_t)p]);
+    qs_bits_.push_back(bits_of(v));
     pending_calls_++;
     return true;
 }
@@ -521,25 +553,27 @@ bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& 
 // (nfk_get_props, one element); an unknown object or property, or one of the other type, reads
 // NULL_INT / NULL_FLOAT (TData::GetInt / GetFloat of a mismatched type)
 int64_t NFGPUKernelModule::GetPropertyInt(const NFGUID& self, const std::string& name) {
-    auto it = prop_id_.find(name);
-    if (!committed_ || ObjectIndex(self) < 0 || it == prop_id_.end() || props_[it->second].type != TDATA_INT) return 0;
-    const int32_t pid = dev_pid_[(size_t)it->second];
+    const int p = prop_ix_.find(name);
+    if (!committed_ || ObjectIndex(self) < 0 || p < 0 || props_[(size_t)p].type != TDATA_INT) return 0;
+    Flush();
+    const int32_t pid = dev_pid_[(size_t)p];
     uint64_t b = 0;
     check(nfk_get_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b), "nfk_get_props");
     return (int64_t)b;
 }
 
 double NFGPUKernelModule::GetPropertyFloat(const NFGUID& self, const std::string& name) {
-    auto it = prop_id_.find(name);
-    if (!committed_ || ObjectIndex(self) < 0 || it == prop_id_.end() || props_[it->second].type != TDATA_FLOAT)
-        return 0.0;
-    const int32_t pid = dev_pid_[(size_t)it->second];
+    const int p = prop_ix_.find(name);
+    if (!committed_ || ObjectIndex(self) < 0 || p < 0 || props_[(size_t)p].type != TDATA_FLOAT) return 0.0;
+    Flush();
+    const int32_t pid = dev_pid_[(size_t)p];
     uint64_t b = 0;
     check(nfk_get_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b), "nfk_get_props");
     return dbl_of(b);
 }
 
 bool NFGPUKernelModule::SetPropertyObject(const NFGUID& self, const std::string& name, const NFGUID& v) {
+    Flush();  // (the buffered Set calls first: call order)
     auto it = prop_id_.find(name);
     if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_OBJECT || ObjectIndex(self) < 0) return false;
     const int32_t pid = dev_pid_[(size_t)it->second];
@@ -550,6 +584,7 @@ bool NFGPUKernelModule::SetPropertyObject(const NFGUID& self, const std::string&
 
 // NFCKernelModule::GetPropertyObject (KM:440): NULL_OBJECT for an unknown object or property
 NFGUID NFGPUKernelModule::GetPropertyObject(const NFGUID& self, const std::string& name) {
+    Flush();  // (the buffered Set calls first: call order)
     auto it = prop_id_.find(name);
     if (!committed_ || ObjectIndex(self) < 0 || it == prop_id_.end() || props_[it->second].type != TDATA_OBJECT)
         return NFGUID();
@@ -603,29 +638,20 @@ uint32_t NFGPUKernelModule::ReadMask(bool per_event_fired) const {
 // that fires (nfk_read_added tells which)
 bool NFGPUKernelModule::AddSchedule(const NFGUID& self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb,
                                     float fTime, int nCount) {
-    int o = ObjectIndex(self);
-    auto k = hb_id_.find(name);
-    if (!committed_ || o < 0 || k == hb_id_.end()) return false;
-    int32_t kind = k->second;
-    const int64_t now = clock_();
-    const int32_t op = 1;
-    check(nfk_schedule_calls_obj(world_, 1, &op, &o, &kind, &fTime, &nCount, &now), "nfk_schedule_calls_obj");
-    sched_add_.emplace(((uint64_t)o << 8) | (uint32_t)kind, std::make_pair(cb, fTime));  // the window's first call wins
-    pending_calls_++;
+    const int o = ObjectIndex(self);
+    const int kind = hb_ix_.find(name);
+    if (!committed_ || o < 0 || kind < 0) return false;
+    QueueScheduleCall(1, o, kind, fTime, nCount, clock_());
+    sched_add_.push_back({((uint64_t)o << 8) | (uint32_t)kind, cb, fTime});  // the window's first call wins
     return true;
 }
 
 // SM:245-249: into the remove list (first call per object per frame owns the key); a name with no
 // device program removes nothing but still takes the key
 bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self, const std::string& name) {
-    auto k = hb_id_.find(name);
     const int32_t o = committed_ ? ObjectIndex(self) : -1;
     if (o < 0) return false;
-    const int32_t op = 2, kind = k == hb_id_.end() ? -1 : k->second, cnt = 0;
-    const float t = 0.f;
-    const int64_t now = 0;
-    check(nfk_schedule_calls_obj(world_, 1, &op, &o, &kind, &t, &cnt, &now), "nfk_schedule_calls_obj");
-    pending_calls_++;
+    QueueScheduleCall(2, o, hb_ix_.find(name), 0.f, 0, 0);
     return true;
 }
 
@@ -633,16 +659,30 @@ bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self, const std::string& na
 bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self) {
     const int32_t o = committed_ ? ObjectIndex(self) : -1;
     if (o < 0) return false;
-    const int32_t op = 3, kind = 0, cnt = 0;
-    const float t = 0.f;
-    const int64_t now = 0;
-    check(nfk_schedule_calls_obj(world_, 1, &op, &o, &kind, &t, &cnt, &now), "nfk_schedule_calls_obj");
-    pending_calls_++;
+    QueueScheduleCall(3, o, 0, 0.f, 0, 0);
     return true;
+}
+
+// (buffered; Flush hands them to the world in one nfk_schedule_calls_obj, call order kept)
+void NFGPUKernelModule::QueueScheduleCall(int32_t op, int32_t o, int32_t kind, float t, int32_t cnt, int64_t now) {
+    qh_op_.push_back(op);
+    qh_obj_.push_back(o);
+    qh_kind_.push_back(kind);
+    qh_t_.push_back(t);
+    qh_cnt_.push_back(cnt);
+    qh_now_.push_back(now);
+    pending_calls_++;
+}
+
+void NFGPUKernelModule::DropPendingAdds(int o) {
+    sched_add_.erase(std::remove_if(sched_add_.begin(), sched_add_.end(),
+                                    [o](const PendingAdd& a) { return (int)(a.key >> 8) == o; }),
+                     sched_add_.end());
 }
 
 // SM:276-285
 bool NFGPUKernelModule::ExistSchedule(const NFGUID& self, const std::string& name) {
+    Flush();  // (the buffered Set calls first: call order)
     auto k = hb_id_.find(name);
     if (!committed_ || ObjectIndex(self) < 0 || k == hb_id_.end()) return false;
     int32_t e = 0;
@@ -674,6 +714,7 @@ void NFGPUKernelModule::SetKindFunctor(const std::string& name, const OBJECT_SCH
 // schedules with the functors of their names.  sync: gather the tickets now (MigrateNow); else the
 // rows of the gather the previous Execute started (SceneShard::BeginFrame)
 void NFGPUKernelModule::MigrateShard(bool sync) {
+    Flush();  // (the buffered Set calls first: call order)
     std::vector<Ticket> sent, recv;
     if (sync) check(shard_->Migrate(&sent, &recv), "SceneShard::Migrate");
     else check(shard_->BeginFrame(&sent, &recv), "SceneShard::BeginFrame");
@@ -698,6 +739,7 @@ bool NFGPUKernelModule::Execute() {
     const auto t0 = std::chrono::steady_clock::now();
     stats_ = FrameStats{};
     if (shard_) MigrateShard(false);
+    Flush();
     check(nfk_execute(world_, clock_()), "nfk_execute");
     pending_calls_ = 0;
     check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
@@ -750,6 +792,7 @@ bool NFGPUKernelModule::Execute() {
     // SM:83-119: their Add/RemoveSchedule calls are applied at the end of the walk)
     t1 = std::chrono::steady_clock::now();
     if (same_frame_ && pending_calls_) {
+        Flush();
         check(nfk_execute_calls(world_), "nfk_execute_calls");
         pending_calls_ = 0;
         check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
@@ -817,6 +860,9 @@ void NFGPUKernelModule::DropFunctors(int o) {
 // fire from now on (the first call of a name wins, SM:218-238; nfk_read_added says which)
 void NFGPUKernelModule::TakeAddedSchedules() {
     if (sched_add_.empty()) return;
+    // by key, call order kept within a key: the first call of each key leads its run
+    std::stable_sort(sched_add_.begin(), sched_add_.end(),
+                     [](const PendingAdd& a, const PendingAdd& b) { return a.key < b.key; });
     const int32_t cap = (int32_t)sched_add_.size();
     std::vector<int64_t> ah(cap), ad(cap);
     std::vector<int32_t> ak(cap);
@@ -824,9 +870,11 @@ void NFGPUKernelModule::TakeAddedSchedules() {
     check(nfk_read_added(world_, cap, &n, ah.data(), ad.data(), ak.data()), "nfk_read_added");
     for (int32_t i = 0; i < std::min(n, cap); i++) {
         const int o = ObjectIndex(NFGUID(ah[i], ad[i]));
-        auto it = sched_add_.find(((uint64_t)o << 8) | (uint32_t)ak[i]);
-        if (it == sched_add_.end()) continue;
-        SetFunctor(o, ak[i], it->second.first, it->second.second);
+        const uint64_t key = ((uint64_t)o << 8) | (uint32_t)ak[i];
+        auto it = std::lower_bound(sched_add_.begin(), sched_add_.end(), key,
+                                   [](const PendingAdd& a, uint64_t k) { return a.key < k; });
+        if (it == sched_add_.end() || it->key != key) continue;
+        SetFunctor(o, ak[i], it->cb, it->t);
     }
     sched_add_.clear();
 }
