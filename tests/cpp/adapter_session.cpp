@@ -339,17 +339,16 @@ int main(int argc, char** argv) {
             NFGUID g(gh[r_obj[ri]], gd[r_obj[ri]]);
             const std::string rn = "rec" + std::to_string(r_rec[ri]);
             const int op = r_op ? r_op[ri] : 0;
-            if (op == 1) {  // NFCRecord::AddRow (the adapter's device record)
-                std::vector<nfgpu::TData> v(((int32_t*)A("rec_cols")->data)[r_rec[ri]]);
-                for (size_t c = 0; c < v.size(); c++) {
+            if (op == 1) {  // NFCRecord::AddRow on the object's record (FindRecord(self, r)->AddRow, RC:111)
+                NFCDataList v;
+                for (int c = 0; c < ((int32_t*)A("rec_cols")->data)[r_rec[ri]]; c++) {
                     const uint64_t b = r_vals[ri * NFK_MAX_REC_COLS + c];
-                    v[c].type = r_ct[r_rec[ri] * NFK_MAX_REC_COLS + c] ? nfgpu::TDATA_FLOAT : nfgpu::TDATA_INT;
-                    v[c].i = (int64_t)b;
-                    v[c].f = bitsd(b);
+                    if (r_ct[r_rec[ri] * NFK_MAX_REC_COLS + c]) v.Add(bitsd(b));
+                    else v.Add((NFINT64)b);
                 }
-                kernel.gpu_.AddRow(nfgpu::NFGUID(g.nHead64, g.nData64), rn, r_row[ri], v);
+                km->FindRecord(g, rn)->AddRow(r_row[ri], v);
             } else if (op == 2) {
-                kernel.gpu_.RemoveRow(nfgpu::NFGUID(g.nHead64, g.nData64), rn, r_row[ri]);
+                km->FindRecord(g, rn)->Remove(r_row[ri]);  // RC:1086
             } else if (op == 3) {
                 km->ClearRecord(g, rn);  // KM:492
             } else if (r_ct[r_rec[ri] * NFK_MAX_REC_COLS + r_col[ri]]) {
