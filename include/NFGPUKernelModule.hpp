@@ -35,13 +35,17 @@
 //   * String / Vector properties stay host-side (not on the frame path); object (NFGUID) properties
 //     are device columns like the int / float ones.
 #pragma once
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -104,6 +108,72 @@ private:
     }
     std::vector<E> t_;
     size_t mask_ = 0, n_ = 0;
+};
+// A few persistent worker threads for data-parallel host loops that run no game code (gathers of
+// scattered reads into dense arrays): Run(n, fn) calls fn(0) .. fn(n-1) on the workers and the
+// calling thread and returns when every call has returned.
+class WorkerPool {
+public:
+    explicit WorkerPool(int workers) {
+        for (int i = 0; i < workers; i++) th_.emplace_back([this] { Loop(); });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int Workers() const { return (int)th_.size(); }
+    void Run(int64_t n, const std::function<void(int64_t)>& fn) {
+        if (n <= 0) return;
+        auto job = std::make_shared<Job>();
+        job->fn = &fn;
+        job->n = n;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = job;
+        }
+        cv_.notify_all();
+        Work(*job);
+        while (job->done.load(std::memory_order_acquire) < n) std::this_thread::yield();
+        std::lock_guard<std::mutex> lk(mu_);
+        if (job_ == job) job_.reset();
+    }
+
+private:
+    // one Run's calls: a worker holding a finished job finds no index left and never calls fn
+    struct Job {
+        const std::function<void(int64_t)>* fn = nullptr;
+        int64_t n = 0;
+        std::atomic<int64_t> next{0}, done{0};
+    };
+    static void Work(Job& j) {
+        int64_t i;
+        while ((i = j.next.fetch_add(1, std::memory_order_relaxed)) < j.n) {
+            (*j.fn)(i);
+            j.done.fetch_add(1, std::memory_order_release);
+        }
+    }
+    void Loop() {
+        std::shared_ptr<Job> last;
+        for (;;) {
+            std::shared_ptr<Job> j;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || (job_ && job_ != last); });
+                if (stop_) return;
+                j = last = job_;
+            }
+            Work(*j);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::shared_ptr<Job> job_;
+    bool stop_ = false;
 };
 }  // namespace nfgpu_detail
 
@@ -370,13 +440,14 @@ public:
     // and its delivery) and module schedules
     struct FrameStats {
         double device, functors, events_read, deliver, calls, total;
+        double gather;  // (of functors: the worker pool's gather of the frame's scattered reads)
     };
     const FrameStats& LastFrameStats() const { return stats_; }
     int ObjectIndex(const NFGUID& g) const;
 
 private:
     void check(int rc, const char* what) const;
-    void DeliverEvents(const nfk_frame_host& f);
+    void DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_self = nullptr, const NFGUID* re_self = nullptr);
     uint64_t UsedRows(const NFGUID& self, int rec);
     void TakeAddedSchedules();
     bool same_frame_ = true;
@@ -388,9 +459,11 @@ private:
     std::vector<PropertyDef> props_;
     std::unordered_map<std::string, int> prop_id_;
     nfgpu_detail::NameIndex prop_ix_;  // prop_id_ for the per-call API
-    // SetPropertyInt / Float calls buffered on the host (checked, in call order) and handed to the
-    // world in one nfk_set_props_obj before anything that must see them (Flush)
-    std::vector<int32_t> qs_obj_, qs_pid_;
+    // SetPropertyInt / Float calls buffered on the host in call order (property checked, object
+    // not yet: no NFGUID lookup per call) and handed to the world in one nfk_set_props before
+    // anything that must see them (Flush); the world looks a large batch up on the device
+    std::vector<int64_t> qs_h_, qs_d_;
+    std::vector<int32_t> qs_pid_;
     std::vector<uint64_t> qs_bits_;
     std::vector<int> dev_pid_;  // props_ index -> device property id (AfterInit)
     std::vector<ClassDef> classes_;
@@ -425,21 +498,47 @@ private:
     void SetFunctor(int o, int k, const OBJECT_SCHEDULE_FUNCTOR& f, float t);
     void DropFunctors(int o);
     std::vector<int> def_of_pid_;  // device property id -> props_ index
-    // pending functors of AddSchedule calls in this window ((object, kind), first call wins)
-    // key: object << 8 | kind
+    // pending functors of AddSchedule calls in this window ((NFGUID, kind), first call wins)
     struct PendingAdd {
-        uint64_t key;  // object << 8 | kind
+        int64_t h, d;
+        int32_t kind;
         OBJECT_SCHEDULE_FUNCTOR cb;
         float t;
     };
     std::vector<PendingAdd> sched_add_;  // in call order; the first call of a key wins
-    // schedule calls buffered like the Sets (nfk_schedule_calls_obj in Flush)
-    std::vector<int32_t> qh_op_, qh_obj_, qh_kind_, qh_cnt_;
+    struct AddKey {  // (NFGUID, kind, call index) of a pending add
+        int64_t h, d;
+        int32_t kind, i;
+        bool operator<(const AddKey& o) const {
+            return h != o.h ? h < o.h : d != o.d ? d < o.d : kind != o.kind ? kind < o.kind : i < o.i;
+        }
+    };
+    // (TakeAddedSchedules' buffers, kept: a fresh large allocation per frame costs page faults)
+    std::vector<AddKey> ta_key_;
+    std::vector<int64_t> ta_h_, ta_d_;
+    std::vector<int32_t> ta_k_;
+    // schedule calls buffered like the Sets, by NFGUID (nfk_schedule_calls in Flush)
+    std::vector<int32_t> qh_op_, qh_kind_, qh_cnt_;
+    std::vector<int64_t> qh_h_, qh_d_;
     std::vector<float> qh_t_;
     std::vector<int64_t> qh_now_;
     nfgpu_detail::NameIndex hb_ix_;  // schedule name -> kind (AfterInit)
-    void QueueScheduleCall(int32_t op, int32_t o, int32_t kind, float t, int32_t cnt, int64_t now);
-    void DropPendingAdds(int o);
+    void QueueScheduleCall(int32_t op, const NFGUID& self, int32_t kind, float t, int32_t cnt, int64_t now);
+    void DropPendingAdds(const NFGUID& g);
+    // objects that left for another shard and whose rows have not left the world yet: buffered
+    // calls on them are dropped at Flush, as calls on an object this module no longer has
+    nfgpu_detail::GuidMap departed_;
+    int FlushSets();
+    int FlushScheduleCalls();
+    // the functor walk's and the deliveries' scattered host reads (functor slot, NFGUID, interval
+    // per fired schedule; NFGUID per event) gathered into dense arrays by worker threads before
+    // any functor runs, so the calls themselves stream (NFGPU_PLUGIN_THREADS workers, default 4)
+    std::unique_ptr<nfgpu_detail::WorkerPool> pool_;
+    std::vector<int32_t> fg_c_;
+    std::vector<NFGUID> fg_g_, ev_self_, re_self_;
+    std::vector<float> fg_t_;
+    bool in_walk_ = false;  // (freed functor entries are not reused while the fired list is walked)
+    bool GatherFrame(const nfk_frame_host& fh, int64_t nfi);
     ModuleScheduler module_sched_;
     SceneShard* shard_ = nullptr;
     std::map<std::string, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> kind_cb_;  // arrivals' functors

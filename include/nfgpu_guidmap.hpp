@@ -86,6 +86,7 @@ public:
     }
     const E* entries() const { return t_.data(); }
     size_t capacity() const { return cap_; }
+    size_t size() const { return n_; }
     // the home entry of a GUID (the device mirror's lookups hash the same way)
     static size_t home(int64_t h, int64_t d, size_t mask) {
         uint64_t x = (uint64_t)h * 0x9E3779B97F4A7C15ull ^ (uint64_t)d;

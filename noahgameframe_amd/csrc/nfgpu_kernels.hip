@@ -1077,22 +1077,18 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             G.masks[g] = G.js[g] >= 0 ? (uint32_t)__shfl((int)my_mask, G.js[g], 64) : 0u;
             G.rsg[g] = (kSets && G.js[g] >= 0) ? (uint32_t)__shfl((int)my_rs, G.js[g], 64) : 0u;
         }
-        // Every load is issued without a branch (a slot or op with no work re-reads a valid cell
-        // and drops the value): a load under a branch ends in a wait at the join, and the waits
-        // of a branchy group cannot be counted (vmcnt), so the compiler drained everything in
-        // flight — the next group's loads and the previous group's stores — before each group
-        // (s_waitcnt vmcnt(0)).  Branch-free, the wait before a group's first use leaves the next
-        // group's loads in flight.
 #pragma unroll
         for (int g = 0; g < kGroup; g++)
 #pragma unroll
             for (int j = 0; j < kOps; j++) {
-                // (raw values: process() skips a slot, op or row without work before reading them)
-                const int jj = j < nro ? j : 0;  // (an op slot past the frame's ops reads op 0's cells)
-                const int e = s0 + (G.js[g] >= 0 ? G.js[g] : 0);
-                const int rows = d.rops[jj].rows;
-                G.used[g][j] = d.rops[jj].used[e];
-                G.cur[g][j] = (d.rops[jj].cells + ((size_t)e * d.rops[jj].cols + d.rops[jj].col) * rows)[lane < rows ? lane : 0];
+                G.used[g][j] = 0;
+                G.cur[g][j] = 0;
+                if (j < nro && G.js[g] >= 0 && !(kSets && G.rsg[g]) && ((G.masks[g] >> d.rops[j].kind) & 1)) {
+                    const int e = s0 + G.js[g];
+                    G.used[g][j] = d.rops[j].used[e];
+                    if (lane < d.rops[j].rows)
+                        G.cur[g][j] = (d.rops[j].cells + ((size_t)e * d.rops[j].cols + d.rops[j].col) * d.rops[j].rows)[lane];
+                }
             }
     };
     auto process = [&](RecGrp<kOps, kGroup>& G) {

@@ -41,10 +41,13 @@ public:
             return;
         }
         const uint64_t g = (gen_.load(std::memory_order_relaxed) + 1) & 0xFFFFFFFFull;
+        // (generation, next piece) first: a worker still in the previous generation's work() then
+        // fails its claim on the old counter, whatever parts_ it reads; parts_ last, with release,
+        // so a worker that reads the new parts_ also sees the new counter
+        next_.store(g << 32, std::memory_order_relaxed);
         f_.store(&f, std::memory_order_relaxed);
-        parts_.store(parts, std::memory_order_relaxed);
         done_.store(0, std::memory_order_relaxed);
-        next_.store(g << 32, std::memory_order_relaxed);  // (generation, next piece)
+        parts_.store(parts, std::memory_order_release);
         {
             std::lock_guard<std::mutex> lk(mu_);
             gen_.store(g, std::memory_order_release);
@@ -61,7 +64,7 @@ private:
             uint64_t x = next_.load(std::memory_order_acquire);
             int p;
             do {
-                if ((x >> 32) != g || (int)(x & 0xFFFFFFFFu) >= parts_.load(std::memory_order_relaxed)) return;
+                if ((x >> 32) != g || (int)(x & 0xFFFFFFFFu) >= parts_.load(std::memory_order_acquire)) return;
                 p = (int)(x & 0xFFFFFFFFu);
             } while (!next_.compare_exchange_weak(x, x + 1, std::memory_order_acq_rel));
             (*f_.load(std::memory_order_relaxed))(p);

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 
@@ -23,6 +24,7 @@ NFGPUKernelModule::NFGPUKernelModule(int capacity, void* hip_stream)
 void NFGPUKernelModule::SetTimeSource(std::function<int64_t()> now_ms) { clock_ = now_ms ? now_ms : nf_get_time; }
 
 NFGPUKernelModule::~NFGPUKernelModule() {
+    pool_.reset();
     if (world_) nfk_destroy(world_);
 }
 
@@ -332,8 +334,9 @@ bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int 
         shard_->QueueSwitch(self.nHead64, self.nData64, cls_[o], isplayer_[o], nTargetSceneID, nTargetGroupID, fX, fY,
                             fZ);
         obj_of_.erase(self.nHead64, self.nData64);  // this module's no more (its index stays reserved)
+        departed_.insert(self.nHead64, self.nData64, o);
         DropFunctors(o);
-        DropPendingAdds(o);
+        DropPendingAdds(self);
         return true;
     }
     if (!scenes_.count(nTargetSceneID)) return false;       // "no this container" (KM:917)
@@ -354,7 +357,7 @@ bool NFGPUKernelModule::DestroyObject(const NFGUID& self) {
     pending_calls_++;
     obj_of_.erase(self.nHead64, self.nData64);  // its object index stays reserved; later calls find no object
     DropFunctors(o);
-    DropPendingAdds(o);
+    DropPendingAdds(self);
     return true;
 }
 
@@ -374,15 +377,16 @@ bool NFGPUKernelModule::GetRange(const std::string& prop, int k,
 
 int NFGPUKernelModule::ObjectIndex(const NFGUID& g) const { return obj_of_.find(g.nHead64, g.nData64); }
 
-// (the object index this module found is nfk's: nfk_set_props_obj queues without a second lookup.
-// The call is checked here — the object is this module's, the property an int one — and buffered;
-// Flush hands the buffer to the world in one call)
+// The call is checked here (the property is an int one) and buffered by NFGUID; Flush hands the
+// buffer to the world in one nfk_set_props, whose NFGUID lookups of a large batch run on the
+// device.  A call on an object this module does not have is dropped there (NFCKernelModule logs
+// "There is no object" and returns false, KM:331; this returns true, as it does for a value the
+// property already holds, where NFCProperty::SetInt returns false, PR:273).
 bool NFGPUKernelModule::SetPropertyInt(const NFGUID& self, const std::string& name, int64_t v) {
     const int p = prop_ix_.find(name);
     if (!committed_ || p < 0 || props_[(size_t)p].type != TDATA_INT) return false;
-    const int32_t o = ObjectIndex(self);
-    if (o < 0) return false;
-    qs_obj_.push_back(o);
+    qs_h_.push_back(self.nHead64);
+    qs_d_.push_back(self.nData64);
     qs_pid_.push_back(dev_pid_[(size_t)p]);
     qs_bits_.push_back((uint64_t)v);
     pending_calls_++;
@@ -390,21 +394,96 @@ bool NFGPUKernelModule::SetPropertyInt(const NFGUID& self, const std::string& na
 }
 
 void NFGPUKernelModule::Flush() {
-    if (!qs_obj_.empty()) {
-        const int rc = nfk_set_props_obj(world_, (int32_t)qs_obj_.size(), qs_obj_.data(), qs_pid_.data(), qs_bits_.data());
-        qs_obj_.clear();
+    if (!qs_h_.empty()) {
+        const int rc = FlushSets();
+        qs_h_.clear();
+        qs_d_.clear();
         qs_pid_.clear();
         qs_bits_.clear();
-        check(rc, "nfk_set_props_obj");
+        check(rc, "nfk_set_props");
     }
     if (!qh_op_.empty()) {
-        const int rc = nfk_schedule_calls_obj(world_, (int32_t)qh_op_.size(), qh_op_.data(), qh_obj_.data(),
-                                              qh_kind_.data(), qh_t_.data(), qh_cnt_.data(), qh_now_.data());
-        for (auto* v : {&qh_op_, &qh_obj_, &qh_kind_, &qh_cnt_}) v->clear();
+        const int rc = FlushScheduleCalls();
+        for (auto* v : {&qh_op_, &qh_kind_, &qh_cnt_}) v->clear();
+        qh_h_.clear();
+        qh_d_.clear();
         qh_t_.clear();
         qh_now_.clear();
-        check(rc, "nfk_schedule_calls_obj");
+        check(rc, "nfk_schedule_calls");
     }
+}
+
+// the buffered Sets: one nfk_set_props (it rejects a batch naming an object the world does not
+// have, queueing none of it); then the calls on objects this module has, resolved here, by object
+// index.  Calls on objects that left for another shard are dropped first.
+int NFGPUKernelModule::FlushSets() {
+    int32_t n = (int32_t)qs_h_.size();
+    if (departed_.size()) {
+        int32_t k = 0;
+        for (int32_t i = 0; i < n; i++) {
+            if (departed_.count(qs_h_[i], qs_d_[i])) continue;
+            qs_h_[k] = qs_h_[i];
+            qs_d_[k] = qs_d_[i];
+            qs_pid_[k] = qs_pid_[i];
+            qs_bits_[k] = qs_bits_[i];
+            k++;
+        }
+        n = k;
+    }
+    if (!n) return NFK_OK;
+    const int rc = nfk_set_props(world_, n, qs_h_.data(), qs_d_.data(), qs_pid_.data(), qs_bits_.data());
+    if (rc != NFK_ERR_NOTFOUND) return rc;
+    std::vector<int32_t> obj, pid;
+    std::vector<uint64_t> bits;
+    for (int32_t i = 0; i < n; i++) {
+        const int32_t o = obj_of_.find(qs_h_[i], qs_d_[i]);
+        if (o < 0) continue;  // "There is no object" (KM:331)
+        obj.push_back(o);
+        pid.push_back(qs_pid_[i]);
+        bits.push_back(qs_bits_[i]);
+    }
+    return obj.empty() ? NFK_OK : nfk_set_props_obj(world_, (int32_t)obj.size(), obj.data(), pid.data(), bits.data());
+}
+
+// the buffered schedule calls, as FlushSets (the reference's schedule module keeps no object
+// table: a call naming no object of this module changes nothing)
+int NFGPUKernelModule::FlushScheduleCalls() {
+    int32_t n = (int32_t)qh_op_.size();
+    if (departed_.size()) {
+        int32_t k = 0;
+        for (int32_t i = 0; i < n; i++) {
+            if (departed_.count(qh_h_[i], qh_d_[i])) continue;
+            qh_op_[k] = qh_op_[i];
+            qh_h_[k] = qh_h_[i];
+            qh_d_[k] = qh_d_[i];
+            qh_kind_[k] = qh_kind_[i];
+            qh_t_[k] = qh_t_[i];
+            qh_cnt_[k] = qh_cnt_[i];
+            qh_now_[k] = qh_now_[i];
+            k++;
+        }
+        n = k;
+    }
+    if (!n) return NFK_OK;
+    const int rc = nfk_schedule_calls(world_, n, qh_op_.data(), qh_h_.data(), qh_d_.data(), qh_kind_.data(),
+                                      qh_t_.data(), qh_cnt_.data(), qh_now_.data());
+    if (rc != NFK_ERR_NOTFOUND) return rc;
+    int32_t k = 0;
+    std::vector<int32_t> obj;
+    for (int32_t i = 0; i < n; i++) {
+        const int32_t o = obj_of_.find(qh_h_[i], qh_d_[i]);
+        if (o < 0) continue;
+        obj.push_back(o);
+        qh_op_[k] = qh_op_[i];
+        qh_kind_[k] = qh_kind_[i];
+        qh_t_[k] = qh_t_[i];
+        qh_cnt_[k] = qh_cnt_[i];
+        qh_now_[k] = qh_now_[i];
+        k++;
+    }
+    return k ? nfk_schedule_calls_obj(world_, k, qh_op_.data(), obj.data(), qh_kind_.data(), qh_t_.data(),
+                                      qh_cnt_.data(), qh_now_.data())
+             : NFK_OK;
 }
 
 bool NFGPUKernelModule::SetRecordInt(const NFGUID& self, const std::string& strRecordName, int nRow, int nCol,
@@ -540,9 +619,8 @@ double NFGPUKernelModule::GetRecordFloat(const NFGUID& self, const std::string& 
 bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& name, double v) {
     const int p = prop_ix_.find(name);
     if (!committed_ || p < 0 || props_[(size_t)p].type != TDATA_FLOAT) return false;
-    const int32_t o = ObjectIndex(self);
-    if (o < 0) return false;
-    qs_obj_.push_back(o);
+    qs_h_.push_back(self.nHead64);
+    qs_d_.push_back(self.nData64);
     qs_pid_.push_back(dev_pid_[(size_t)p]);
     qs_bits_.push_back(bits_of(v));
     pending_calls_++;
@@ -636,37 +714,38 @@ uint32_t NFGPUKernelModule::ReadMask(bool per_event_fired) const {
 // NFCScheduleModule::AddSchedule (SM:257-275): queued, added at the end of the next Execute unless
 // the (object, name) still has a schedule then; the functor of the call that creates it is the one
 // that fires (nfk_read_added tells which)
+// (buffered by NFGUID like the Sets: SM:218-238 returns true without an object table, and a call
+// on an object this module does not have is dropped at Flush)
 bool NFGPUKernelModule::AddSchedule(const NFGUID& self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb,
                                     float fTime, int nCount) {
-    const int o = ObjectIndex(self);
     const int kind = hb_ix_.find(name);
-    if (!committed_ || o < 0 || kind < 0) return false;
-    QueueScheduleCall(1, o, kind, fTime, nCount, clock_());
-    sched_add_.push_back({((uint64_t)o << 8) | (uint32_t)kind, cb, fTime});  // the window's first call wins
+    if (!committed_ || kind < 0) return false;
+    QueueScheduleCall(1, self, kind, fTime, nCount, clock_());
+    sched_add_.push_back({self.nHead64, self.nData64, kind, cb, fTime});  // the window's first call wins
     return true;
 }
 
 // SM:245-249: into the remove list (first call per object per frame owns the key); a name with no
 // device program removes nothing but still takes the key
 bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self, const std::string& name) {
-    const int32_t o = committed_ ? ObjectIndex(self) : -1;
-    if (o < 0) return false;
-    QueueScheduleCall(2, o, hb_ix_.find(name), 0.f, 0, 0);
+    if (!committed_) return false;
+    QueueScheduleCall(2, self, hb_ix_.find(name), 0.f, 0, 0);
     return true;
 }
 
 // SM:240-243: erases the object's schedules at once
 bool NFGPUKernelModule::RemoveSchedule(const NFGUID& self) {
-    const int32_t o = committed_ ? ObjectIndex(self) : -1;
-    if (o < 0) return false;
-    QueueScheduleCall(3, o, 0, 0.f, 0, 0);
+    if (!committed_) return false;
+    QueueScheduleCall(3, self, 0, 0.f, 0, 0);
     return true;
 }
 
-// (buffered; Flush hands them to the world in one nfk_schedule_calls_obj, call order kept)
-void NFGPUKernelModule::QueueScheduleCall(int32_t op, int32_t o, int32_t kind, float t, int32_t cnt, int64_t now) {
+// (buffered; Flush hands them to the world in one nfk_schedule_calls, call order kept)
+void NFGPUKernelModule::QueueScheduleCall(int32_t op, const NFGUID& self, int32_t kind, float t, int32_t cnt,
+                                          int64_t now) {
     qh_op_.push_back(op);
-    qh_obj_.push_back(o);
+    qh_h_.push_back(self.nHead64);
+    qh_d_.push_back(self.nData64);
     qh_kind_.push_back(kind);
     qh_t_.push_back(t);
     qh_cnt_.push_back(cnt);
@@ -674,9 +753,9 @@ void NFGPUKernelModule::QueueScheduleCall(int32_t op, int32_t o, int32_t kind, f
     pending_calls_++;
 }
 
-void NFGPUKernelModule::DropPendingAdds(int o) {
+void NFGPUKernelModule::DropPendingAdds(const NFGUID& g) {
     sched_add_.erase(std::remove_if(sched_add_.begin(), sched_add_.end(),
-                                    [o](const PendingAdd& a) { return (int)(a.key >> 8) == o; }),
+                                    [&g](const PendingAdd& a) { return a.h == g.nHead64 && a.d == g.nData64; }),
                      sched_add_.end());
 }
 
@@ -718,6 +797,7 @@ void NFGPUKernelModule::MigrateShard(bool sync) {
     std::vector<Ticket> sent, recv;
     if (sync) check(shard_->Migrate(&sent, &recv), "SceneShard::Migrate");
     else check(shard_->BeginFrame(&sent, &recv), "SceneShard::BeginFrame");
+    for (const Ticket& k : sent) departed_.erase(k.guid_head, k.guid_data);  // (their rows have left the world)
     for (const Ticket& k : recv) {
         const NFGUID g(k.guid_head, k.guid_data);
         const int o = (int)guids_.size();
@@ -754,37 +834,54 @@ bool NFGPUKernelModule::Execute() {
     if (what) check(nfk_read_frame(world_, what, &fh), "nfk_read_frame");
     stats_.events_read = ms_since(t1);
     t1 = std::chrono::steady_clock::now();
-    // heartbeat functors with the reference's arguments.  The fired list is in NFGUID order, so
-    // its (object, kind) functor slots, pooled functors and NFGUIDs are scattered host reads: they
-    // are prefetched two stages ahead (slot and NFGUID, then the functor the slot names), so the
-    // loop is bound by the calls, not by one cache miss after another
-    const size_t nk = heartbeats_.size(), nslot = cb_slot_.size();
+    // heartbeat functors with the reference's arguments, objects in NFGUID order (the fired list's)
     const int64_t nfi = n_cb_ ? fh.n_fi : 0;  // (a frame consumer may read the list without functors)
-    constexpr int64_t kPre = 16;
-    for (int64_t i = 0; i < nfi; i++) {
-        if (i + 2 * kPre < nfi) {
-            const int64_t j = i + 2 * kPre;
-            const size_t at = (size_t)fh.fi_obj[j] * nk + (size_t)fh.fi_kind[j];
-            if (at < nslot) __builtin_prefetch(&cb_slot_[at]);
-            __builtin_prefetch(&guids_[(size_t)fh.fi_obj[j]]);
+    const bool gathered = GatherFrame(fh, nfi);
+    stats_.gather = ms_since(t1);
+    in_walk_ = true;
+    if (gathered) {
+        // the functor entries, NFGUIDs and intervals are dense arrays now: only the functor objects
+        // themselves are scattered (prefetched ahead)
+        constexpr int64_t kPre = 16;
+        for (int64_t i = 0; i < nfi; i++) {
+            if (i + kPre < nfi && fg_c_[(size_t)(i + kPre)] >= 0) __builtin_prefetch(&cb_pool_[(size_t)fg_c_[(size_t)(i + kPre)]]);
+            const int32_t c = fg_c_[(size_t)i];
+            // (empty: a functor earlier in this walk destroyed the object or moved it to another shard)
+            if (c >= 0 && cb_pool_[(size_t)c]) cb_pool_[(size_t)c](fg_g_[(size_t)i], heartbeats_[(size_t)fh.fi_kind[i]].name, fg_t_[(size_t)i], fh.fi_remain[i]);
         }
-        if (i + kPre < nfi) {
-            const int64_t j = i + kPre;
-            const size_t at = (size_t)fh.fi_obj[j] * nk + (size_t)fh.fi_kind[j];
-            const int32_t c = at < nslot ? cb_slot_[at] : -1;
-            if (c >= 0) {
-                __builtin_prefetch(&cb_pool_[(size_t)c]);
-                __builtin_prefetch(&cb_time_[(size_t)c]);
+    } else {
+        // (a small frame, or no workers) its (object, kind) functor slots, pooled functors and NFGUIDs
+        // are scattered host reads, prefetched two stages ahead
+        const size_t nk = heartbeats_.size(), nslot = cb_slot_.size();
+        constexpr int64_t kPre = 16;
+        for (int64_t i = 0; i < nfi; i++) {
+            if (i + 2 * kPre < nfi) {
+                const int64_t j = i + 2 * kPre;
+                const size_t at = (size_t)fh.fi_obj[j] * nk + (size_t)fh.fi_kind[j];
+                if (at < nslot) __builtin_prefetch(&cb_slot_[at]);
+                __builtin_prefetch(&guids_[(size_t)fh.fi_obj[j]]);
             }
+            if (i + kPre < nfi) {
+                const int64_t j = i + kPre;
+                const size_t at = (size_t)fh.fi_obj[j] * nk + (size_t)fh.fi_kind[j];
+                const int32_t c = at < nslot ? cb_slot_[at] : -1;
+                if (c >= 0) {
+                    __builtin_prefetch(&cb_pool_[(size_t)c]);
+                    __builtin_prefetch(&cb_time_[(size_t)c]);
+                }
+            }
+            const int o = fh.fi_obj[i], k = fh.fi_kind[i];
+            const size_t at = (size_t)o * nk + (size_t)k;
+            const int32_t c = at < cb_slot_.size() ? cb_slot_[at] : -1;
+            if (c >= 0) cb_pool_[c](guids_[o], heartbeats_[k].name, cb_time_[c], fh.fi_remain[i]);
         }
-        const int o = fh.fi_obj[i], k = fh.fi_kind[i];
-        const size_t at = (size_t)o * nk + (size_t)k;
-        const int32_t c = at < nslot ? cb_slot_[at] : -1;
-        if (c >= 0) cb_pool_[c](guids_[o], heartbeats_[k].name, cb_time_[c], fh.fi_remain[i]);
     }
+    in_walk_ = false;
     stats_.functors = ms_since(t1);
     t1 = std::chrono::steady_clock::now();
-    if (what & NFK_READ_EVENTS) DeliverEvents(fh);
+    if (what & NFK_READ_EVENTS)
+        DeliverEvents(fh, gathered && !ev_self_.empty() ? ev_self_.data() : nullptr,
+                      gathered && !re_self_.empty() ? re_self_.data() : nullptr);
     if (what)
         for (auto& fc : frame_cb_) fc(fh, guids_.data());
     stats_.deliver = ms_since(t1);
@@ -829,7 +926,7 @@ void NFGPUKernelModule::SetFunctor(int o, int k, const OBJECT_SCHEDULE_FUNCTOR& 
         return;
     }
     if (c < 0) {
-        if (!cb_free_.empty()) {
+        if (!cb_free_.empty() && !in_walk_) {  // (a gathered entry of the walk stays what it was)
             c = cb_free_.back();
             cb_free_.pop_back();
         } else {
@@ -861,31 +958,90 @@ void NFGPUKernelModule::DropFunctors(int o) {
 void NFGPUKernelModule::TakeAddedSchedules() {
     if (sched_add_.empty()) return;
     // by key, call order kept within a key: the first call of each key leads its run
-    std::stable_sort(sched_add_.begin(), sched_add_.end(),
-                     [](const PendingAdd& a, const PendingAdd& b) { return a.key < b.key; });
     const int32_t cap = (int32_t)sched_add_.size();
-    std::vector<int64_t> ah(cap), ad(cap);
-    std::vector<int32_t> ak(cap);
+    ta_key_.resize((size_t)cap);
+    for (int32_t i = 0; i < cap; i++) ta_key_[(size_t)i] = {sched_add_[(size_t)i].h, sched_add_[(size_t)i].d, sched_add_[(size_t)i].kind, i};
+    std::sort(ta_key_.begin(), ta_key_.end());
+    ta_h_.resize((size_t)cap);
+    ta_d_.resize((size_t)cap);
+    ta_k_.resize((size_t)cap);
     int32_t n = 0;
-    check(nfk_read_added(world_, cap, &n, ah.data(), ad.data(), ak.data()), "nfk_read_added");
+    check(nfk_read_added(world_, cap, &n, ta_h_.data(), ta_d_.data(), ta_k_.data()), "nfk_read_added");
     for (int32_t i = 0; i < std::min(n, cap); i++) {
-        const int o = ObjectIndex(NFGUID(ah[i], ad[i]));
-        const uint64_t key = ((uint64_t)o << 8) | (uint32_t)ak[i];
-        auto it = std::lower_bound(sched_add_.begin(), sched_add_.end(), key,
-                                   [](const PendingAdd& a, uint64_t k) { return a.key < k; });
-        if (it == sched_add_.end() || it->key != key) continue;
-        SetFunctor(o, ak[i], it->cb, it->t);
+        const int o = ObjectIndex(NFGUID(ta_h_[(size_t)i], ta_d_[(size_t)i]));
+        if (o < 0) continue;
+        const AddKey q{ta_h_[(size_t)i], ta_d_[(size_t)i], ta_k_[(size_t)i], -1};
+        auto it = std::lower_bound(ta_key_.begin(), ta_key_.end(), q);
+        if (it == ta_key_.end() || it->h != q.h || it->d != q.d || it->kind != q.kind) continue;
+        const PendingAdd& pa = sched_add_[(size_t)it->i];
+        SetFunctor(o, q.kind, pa.cb, pa.t);
     }
     sched_add_.clear();
 }
 
-void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f) {
+// Before any functor of the frame runs (so no game code changes the tables under the workers):
+// the fired list's functor entries, NFGUIDs and intervals, and the events' NFGUIDs, gathered in
+// chunks by the worker pool.  False for a frame too small to pay for it, or with no workers.
+bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
+    const bool ev = !(common_prop_cb_.empty() && aoi_prop_cb_.empty() && common_rec_cb_.empty() && aoi_rec_cb_.empty());
+    const int64_t nev = ev ? fh.n_ev : 0, nre = ev ? fh.n_re : 0;
+    ev_self_.clear();
+    re_self_.clear();
+    static const int64_t kMin = getenv("NFGPU_PLUGIN_GATHER_MIN") ? atoll(getenv("NFGPU_PLUGIN_GATHER_MIN")) : (1 << 15);
+    if (nfi + nev + nre < std::max<int64_t>(kMin, 1)) return false;
+    if (!pool_) {
+        const char* e = getenv("NFGPU_PLUGIN_THREADS");
+        const int nw = e ? atoi(e) : 4;
+        if (nw <= 0) return false;
+        pool_.reset(new nfgpu_detail::WorkerPool(nw));
+    }
+    fg_c_.resize((size_t)nfi);
+    fg_g_.resize((size_t)nfi);
+    fg_t_.resize((size_t)nfi);
+    ev_self_.resize((size_t)nev);
+    re_self_.resize((size_t)nre);
+    constexpr int64_t kChunk = 1 << 14, kPre = 16;
+    const int64_t cf = (nfi + kChunk - 1) / kChunk, ce = (nev + kChunk - 1) / kChunk, cr = (nre + kChunk - 1) / kChunk;
+    const size_t nk = heartbeats_.size(), nslot = cb_slot_.size();
+    pool_->Run(cf + ce + cr, [&](int64_t q) {
+        if (q < cf) {
+            const int64_t i0 = q * kChunk, i1 = std::min(nfi, i0 + kChunk);
+            for (int64_t i = i0; i < i1; i++) {
+                if (i + kPre < i1) {
+                    const size_t at = (size_t)fh.fi_obj[i + kPre] * nk + (size_t)fh.fi_kind[i + kPre];
+                    if (at < nslot) __builtin_prefetch(&cb_slot_[at]);
+                    __builtin_prefetch(&guids_[(size_t)fh.fi_obj[i + kPre]]);
+                }
+                const size_t at = (size_t)fh.fi_obj[i] * nk + (size_t)fh.fi_kind[i];
+                const int32_t c = at < nslot ? cb_slot_[at] : -1;
+                fg_c_[(size_t)i] = c;
+                fg_g_[(size_t)i] = guids_[(size_t)fh.fi_obj[i]];
+                fg_t_[(size_t)i] = c >= 0 ? cb_time_[(size_t)c] : 0.f;
+            }
+        } else if (q < cf + ce) {
+            const int64_t i0 = (q - cf) * kChunk, i1 = std::min(nev, i0 + kChunk);
+            for (int64_t i = i0; i < i1; i++) {
+                if (i + kPre < i1) __builtin_prefetch(&guids_[(size_t)fh.ev_obj[i + kPre]]);
+                ev_self_[(size_t)i] = guids_[(size_t)fh.ev_obj[i]];
+            }
+        } else {
+            const int64_t i0 = (q - cf - ce) * kChunk, i1 = std::min(nre, i0 + kChunk);
+            for (int64_t i = i0; i < i1; i++) {
+                if (i + kPre < i1) __builtin_prefetch(&guids_[(size_t)fh.re_obj[i + kPre]]);
+                re_self_[(size_t)i] = guids_[(size_t)fh.re_obj[i]];
+            }
+        }
+    });
+    return true;
+}
+
+void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_self, const NFGUID* re_self) {
     if (common_prop_cb_.empty() && aoi_prop_cb_.empty() && common_rec_cb_.empty() && aoi_rec_cb_.empty()) return;
     std::vector<NFGUID> rcpt;
     uint32_t rcpt_at = 0, rcpt_n = 0xFFFFFFFFu;  // the msg_rcpt run rcpt holds
     constexpr int64_t kPre = 16;  // events are in slot order; their objects' NFGUIDs are scattered
     for (int64_t e = 0; e < f.n_ev; e++) {
-        if (e + kPre < f.n_ev) __builtin_prefetch(&guids_[(size_t)f.ev_obj[e + kPre]]);
+        if (!ev_self && e + kPre < f.n_ev) __builtin_prefetch(&guids_[(size_t)f.ev_obj[e + kPre]]);
         const PropertyDef& pd = props_[def_of_pid_[f.ev_pid[e]]];
         TData a, b;
         a.type = b.type = pd.type;
@@ -899,7 +1055,7 @@ void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f) {
             a.o = NFGUID((int64_t)f.ev_old_h[e], (int64_t)f.ev_old[e]);
             b.o = NFGUID((int64_t)f.ev_new_h[e], (int64_t)f.ev_new[e]);
         }
-        const NFGUID& self = guids_[f.ev_obj[e]];
+        const NFGUID& self = ev_self ? ev_self[e] : guids_[f.ev_obj[e]];
         for (auto& cb : common_prop_cb_) cb(self, pd.name, a, b);
         if (f.msg_off && !aoi_prop_cb_.empty() && f.msg_off[e + 1] > f.msg_off[e]) {  // AOI.cpp:250: no call for empty lists
             // consecutive events of a scene group mostly share their recipients: rebuild the list
@@ -934,7 +1090,7 @@ void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f) {
             a.f = dbl_of(f.re_old[e]);
             b.f = dbl_of(f.re_new[e]);
         }
-        const NFGUID& self = guids_[f.re_obj[e]];
+        const NFGUID& self = re_self ? re_self[e] : guids_[f.re_obj[e]];
         for (auto& cb : common_rec_cb_) cb(self, ev, a, b);
         if (f.msg_off && !aoi_rec_cb_.empty()) {
             rcpt_n = 0xFFFFFFFFu;

@@ -211,8 +211,11 @@ int nfk_spawn_objects(void* w, int32_t n, const int64_t* gh, const int64_t* gd, 
     }
     return NFK_OK;
 }
+// (a batch naming an unknown object is refused whole, as the library refuses it: nothing queued)
 int nfk_set_props(void* w, int32_t n, const int64_t* gh, const int64_t* gd, const int32_t* pid, const uint64_t* bits) {
     Stub* s = S(w);
+    for (int i = 0; i < n; i++)
+        if (find(s, gh[i], gd[i]) < 0) return NFK_ERR_NOTFOUND;
     for (int i = 0; i < n; i++) {
         const int o = find(s, gh[i], gd[i]);
         if (o < 0) return NFK_ERR_NOTFOUND;
@@ -348,6 +351,8 @@ int nfk_remove_all_schedules(void* w, int64_t h, int64_t d) {
 }
 int nfk_schedule_calls(void* w, int32_t n, const int32_t* op, const int64_t* gh, const int64_t* gd, const int32_t* kind,
                        const float* iv, const int32_t* cnt, const int64_t* now) {
+    for (int i = 0; i < n; i++)
+        if (find(S(w), gh[i], gd[i]) < 0) return NFK_ERR_NOTFOUND;
     for (int i = 0; i < n; i++) {
         const int rc = op[i] == 1 ? nfk_add_schedules(w, 1, gh + i, gd + i, kind + i, iv + i, cnt + i, now + i)
                      : op[i] == 2 ? nfk_remove_schedule(w, gh[i], gd[i], kind[i])

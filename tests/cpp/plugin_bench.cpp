@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -212,17 +213,19 @@ int main(int argc, char** argv) {
     const nfk_summary& s = km.LastSummary();
     printf("{\"plugin_frame_ms\": %.3f, \"entities\": %lld, \"entity_ticks_per_s\": %.4g, \"calls_per_frame\": %lld, "
            "\"phases_ms\": {\"calls\": %.3f, \"device\": %.3f, \"functors\": %.3f, \"events_read\": %.3f, "
-           "\"deliver\": %.3f, \"functor_calls\": %.3f, \"execute\": %.3f}, "
+           "\"deliver\": %.3f, \"functor_calls\": %.3f, \"execute\": %.3f, \"gather\": %.3f}, "
            "\"per_frame\": {\"fired\": %lld, \"prop_events\": %lld, \"rec_events\": %lld, \"messages\": %lld}, "
            "\"received\": {\"heartbeats\": %lld, \"prop_events\": %lld, \"recipients\": %lld}, \"build_s\": %.1f, "
-           "\"frames\": %d, \"warmup\": %d, \"consumer\": \"%s\"}\n",
+           "\"frames\": %d, \"warmup\": %d, \"consumer\": \"%s\", \"threads\": \"%s\"}\n",
            med(frame_ms), (long long)N, (double)N / (med(frame_ms) * 1e-3), (long long)(K ? ncalls / K : 0),
            med(call_ms), medf(&NFGPUKernelModule::FrameStats::device), medf(&NFGPUKernelModule::FrameStats::functors),
            medf(&NFGPUKernelModule::FrameStats::events_read), medf(&NFGPUKernelModule::FrameStats::deliver),
            medf(&NFGPUKernelModule::FrameStats::calls), medf(&NFGPUKernelModule::FrameStats::total),
+           medf(&NFGPUKernelModule::FrameStats::gather),
            (long long)s.n_fired, (long long)s.n_prop_events, (long long)s.n_rec_events, (long long)s.n_msgs,
            (long long)n_hb, (long long)n_prop, (long long)n_rcpt, build_s, K, W,
-           consumer == 0 ? "per-call" : consumer == 1 ? "frame-batch" : "none");
+           consumer == 0 ? "per-call" : consumer == 1 ? "frame-batch" : "none",
+           getenv("NFGPU_PLUGIN_THREADS") ? getenv("NFGPU_PLUGIN_THREADS") : "default");
     fflush(stdout);
     km.Shut();
     return 0;

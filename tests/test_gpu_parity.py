@@ -206,10 +206,12 @@ def test_gpu_full_size_config0_tutorial3(gpu_available):
     compare_runs(run_gpu(w), run_oracle(w))
 
 
-@pytest.mark.parametrize("slack", [-1, 64])
-def test_cpp_plugin_replay_create_destroy(gpu_available, tmp_path, slack):
+@pytest.mark.parametrize("slack,gather", [(-1, ""), (64, ""), (64, "1")])
+def test_cpp_plugin_replay_create_destroy(gpu_available, tmp_path, slack, gather):
     """CreateObject after AfterInit and DestroyObject through the C++ plugin, SwitchScene and
-    read-modify-write Sets around them, against the oracle (KM:101-308)."""
+    read-modify-write Sets around them, against the oracle (KM:101-308); Sets and schedule calls
+    on destroyed objects are dropped when the plugin hands its buffer over (gather: see
+    test_cpp_plugin_api_replay_matches_oracle)."""
     import subprocess
     exe = os.path.join(ROOT, "tests", "cpp", "_bin", "plugin_replay")
     w = workload.make_world(n_obj=2000, n_scenes=2, groups_per_scene=4, players_per_group=4, n_ticks=6, seed=41 + slack,
@@ -217,7 +219,7 @@ def test_cpp_plugin_replay_create_destroy(gpu_available, tmp_path, slack):
                             destroy_frac=0.03)
     wp, op = str(tmp_path / "w.nfio"), str(tmp_path / "o.nfio")
     nfio.write(wp, w)
-    subprocess.run([exe, wp, op], check=True)
+    subprocess.run([exe, wp, op], check=True, env=dict(os.environ, NFGPU_PLUGIN_GATHER_MIN=gather) if gather else None)
     got, ref = nfio.read(op), run_oracle(w)
     for t in range(6):   # functors in NFGUID order (see test_cpp_plugin_api_replay_matches_oracle)
         o = np.lexsort((got[f"fi_t{t}_kind"], got[f"fi_t{t}_obj"]))
@@ -382,10 +384,13 @@ def test_device_outputs_and_counters(gpu_available):
     m.close()
 
 
-def test_cpp_plugin_api_replay_matches_oracle(gpu_available, tmp_path):
+@pytest.mark.parametrize("gather", ["", "1"], ids=["default", "gathered"])
+def test_cpp_plugin_api_replay_matches_oracle(gpu_available, tmp_path, gather):
     """The C++ host plugin (include/NFGPUKernelModule.hpp), driven like a NoahGameFrame logic
     module (AddSchedule functors, RegisterCommonPropertyEvent, AddPropertyEventCallBack), sees
-    exactly the oracle's coalesced events, heartbeat calls and recipient lists."""
+    exactly the oracle's coalesced events, heartbeat calls and recipient lists.  gathered: every
+    frame takes the worker-gathered functor walk and delivery (NFGPU_PLUGIN_GATHER_MIN=1; by
+    default only frames of >= 32k fired schedules and events do)."""
     import subprocess
     exe = os.path.join(ROOT, "tests", "cpp", "_bin", "plugin_replay")
     if not os.path.exists(exe):
@@ -398,7 +403,8 @@ def test_cpp_plugin_api_replay_matches_oracle(gpu_available, tmp_path):
     assert len(w["sw_tick"]) > 0 and w["x_mode"].sum() > 100
     wp, op = str(tmp_path / "w.nfio"), str(tmp_path / "o.nfio")
     nfio.write(wp, w)
-    subprocess.run([exe, wp, op], check=True)
+    env = dict(os.environ, NFGPU_PLUGIN_GATHER_MIN=gather) if gather else None
+    subprocess.run([exe, wp, op], check=True, env=env)
     got = nfio.read(op)
     ref = run_oracle(w)
     # heartbeat functors run in NFCScheduleModule::Execute's order (SM:52-80: mObjectScheduleMap is
@@ -460,10 +466,11 @@ def test_jit_specialisation_is_what_runs(gpu_available, monkeypatch):
     assert not on and "NFGPU_JIT=0" in msg
 
 
-def _functor_frame_log(same):
+def _functor_frame_log(same, gather=""):
     import subprocess
     exe = os.path.join(ROOT, "tests", "cpp", "_bin", "functor_frame")
-    out = subprocess.run([exe, str(int(same))], check=True, capture_output=True, text=True, timeout=120).stdout
+    env = dict(os.environ, NFGPU_PLUGIN_GATHER_MIN=gather) if gather else None
+    out = subprocess.run([exe, str(int(same))], check=True, capture_output=True, text=True, timeout=120, env=env).stdout
     rows = []
     for line in out.splitlines():
         kind, *kv = line.split()
@@ -478,13 +485,14 @@ def _functor_frame_log(same):
     return rows
 
 
-def test_functor_calls_land_in_the_same_frame(gpu_available):
+@pytest.mark.parametrize("gather", ["", "1"], ids=["default", "gathered"])
+def test_functor_calls_land_in_the_same_frame(gpu_available, gather):
     """A heartbeat functor's own calls (NFCScheduleModule::Execute runs it inside the walk, SM:65):
     its SetPropertyInt lands in the same Execute — the property event is delivered before Execute
     returns and GetPropertyInt after it sees the value — and its AddSchedule is applied at the end of
     the same walk (SM:83-119), so the new schedule's functor fires from the next frame on.  With
     SetFunctorCallsSameFrame(false) the same calls land one frame later (tests/cpp/functor_frame.cpp)."""
-    rows = _functor_frame_log(True)
+    rows = _functor_frame_log(True, gather)
     fires = [r for r in rows if r["kind"] == "fire"]
     events = [r for r in rows if r["kind"] == "event"]
     regen = [r for r in fires if "Regen" in r["rest"]]
@@ -503,7 +511,7 @@ def test_functor_calls_land_in_the_same_frame(gpu_available):
             assert int(state[(str(f), obj)]["HP"]) == 10 * i + n_regen
     assert state[("3", "100")]["Bonus"] == "0"   # exhausted in frame 3 (first in name order)
 
-    late = _functor_frame_log(False)
+    late = _functor_frame_log(False, gather)
     ev_late = [r for r in late if r["kind"] == "event" and "HP" in r["rest"]]
     fires_late = [r for r in late if r["kind"] == "fire" and "Regen" in r["rest"]]
     assert sorted({r["frame"] for r in fires_late}) == ["1", "2", "3"]

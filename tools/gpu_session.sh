@@ -48,6 +48,9 @@ for step in "$@"; do
     hostprof) NFGPU_TRACE_EXEC=1 run hostprof 300 python tools/host_calls_profile.py ;;
     hbmmix) run hbmmix 120 tools/_bin/hbm_mix ;;
     hbmstream) run hbmstream 240 tools/_bin/hbm_stream ;;
+    plugintests) run plugintests 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread \
+                     -k "plugin or functor or adapter or logic_session or shard" ;;
+    pluginab) run pluginab 900 python tools/plugin_frame_ab.py --rounds ${PABR:-2} ${PAB:-NFGPU_PLUGIN_THREADS=0 NFGPU_PLUGIN_THREADS=4 NFGPU_PLUGIN_THREADS=8} ;;
     pluginbench) run pluginbench 600 python bench.py --steps 20 --warmup 3 --cpu-baseline off --host-calls off ;;
     membership) NFGPU_TRACE_MEMBERSHIP=1 run membership 300 python tools/membership_bench.py ;;
     selfmigcpp) run selfmigcpp 300 python bench.py --self-migrate --shard cpp --steps 24 --warmup 8 --cpu-baseline off \
