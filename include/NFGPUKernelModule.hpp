@@ -474,7 +474,9 @@ private:
     std::unordered_map<std::string, int> hb_id_;
     std::map<int, bool> scenes_;
     // objects
-    std::vector<NFGUID> guids_;
+    template <class T>
+    using HVec = std::vector<T, nfgpu_detail::HugeAlloc<T>>;  // (tables read at random: huge pages)
+    HVec<NFGUID> guids_;
     nfgpu_detail::GuidMap obj_of_;  // NFGUID -> object index (open addressing)
     std::vector<int32_t> scene_, group_;
     std::vector<uint8_t> cls_, isplayer_;
@@ -490,9 +492,9 @@ private:
     uint32_t ReadMask(bool per_event_fired) const;
     // the functor of each (object, kind) schedule: cb_slot_[object * n_kind + kind] indexes
     // cb_pool_ / cb_time_ (-1: none); freed entries are reused
-    std::vector<int32_t> cb_slot_;
-    std::vector<OBJECT_SCHEDULE_FUNCTOR> cb_pool_;
-    std::vector<float> cb_time_;
+    HVec<int32_t> cb_slot_;
+    HVec<OBJECT_SCHEDULE_FUNCTOR> cb_pool_;
+    HVec<float> cb_time_;
     std::vector<int32_t> cb_free_;
     int64_t n_cb_ = 0;
     void SetFunctor(int o, int k, const OBJECT_SCHEDULE_FUNCTOR& f, float t);
@@ -534,9 +536,9 @@ private:
     // per fired schedule; NFGUID per event) gathered into dense arrays by worker threads before
     // any functor runs, so the calls themselves stream (NFGPU_PLUGIN_THREADS workers, default 4)
     std::unique_ptr<nfgpu_detail::WorkerPool> pool_;
-    std::vector<int32_t> fg_c_;
-    std::vector<NFGUID> fg_g_, ev_self_, re_self_;
-    std::vector<float> fg_t_;
+    HVec<int32_t> fg_c_;
+    HVec<NFGUID> fg_g_, ev_self_, re_self_;
+    HVec<float> fg_t_;
     bool in_walk_ = false;  // (freed functor entries are not reused while the fired list is walked)
     bool GatherFrame(const nfk_frame_host& fh, int64_t nfi);
     ModuleScheduler module_sched_;

@@ -6,6 +6,8 @@
 #include <cstdint>
 #include <vector>
 
+#include "nfgpu_hugealloc.hpp"
+
 namespace nfgpu_detail {
 
 // NFGUID -> object index (the reference's NFMapEx<NFGUID, NFIObject> lookup, KM:323): open
@@ -102,7 +104,7 @@ private:
         if (log_ && !rebuilt_) log_->push_back((uint32_t)i);
     }
     void rehash(size_t c) {
-        std::vector<E> old;
+        std::vector<E, HugeAlloc<E>> old;
         old.swap(t_);
         t_.assign(c, E{});
         cap_ = c;
@@ -112,7 +114,7 @@ private:
         for (const E& e : old)
             if (e.v >= 0) insert(e.h, e.d, e.v);
     }
-    std::vector<E> t_;
+    std::vector<E, HugeAlloc<E>> t_;
     size_t cap_ = 0, n_ = 0;
     std::vector<uint32_t>* log_ = nullptr;
     bool rebuilt_ = false;
