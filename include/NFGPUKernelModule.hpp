@@ -447,7 +447,8 @@ public:
 
 private:
     void check(int rc, const char* what) const;
-    void DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_self = nullptr, const NFGUID* re_self = nullptr);
+    void DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_self = nullptr, const NFGUID* re_self = nullptr,
+                       const uint8_t* ev_same = nullptr);
     uint64_t UsedRows(const NFGUID& self, int rec);
     void TakeAddedSchedules();
     bool same_frame_ = true;
@@ -518,7 +519,7 @@ private:
     // (TakeAddedSchedules' buffers, kept: a fresh large allocation per frame costs page faults)
     std::vector<AddKey> ta_key_;
     std::vector<int64_t> ta_h_, ta_d_;
-    std::vector<int32_t> ta_k_;
+    std::vector<int32_t> ta_k_, ta_ord_;
     // schedule calls buffered like the Sets, by NFGUID (nfk_schedule_calls in Flush)
     std::vector<int32_t> qh_op_, qh_kind_, qh_cnt_;
     std::vector<int64_t> qh_h_, qh_d_;
@@ -534,11 +535,12 @@ private:
     int FlushScheduleCalls();
     // the functor walk's and the deliveries' scattered host reads (functor slot, NFGUID, interval
     // per fired schedule; NFGUID per event) gathered into dense arrays by worker threads before
-    // any functor runs, so the calls themselves stream (NFGPU_PLUGIN_THREADS workers, default 4)
+    // any functor runs, so the calls themselves stream (NFGPU_PLUGIN_THREADS workers, default 8)
     std::unique_ptr<nfgpu_detail::WorkerPool> pool_;
     HVec<int32_t> fg_c_;
     HVec<NFGUID> fg_g_, ev_self_, re_self_;
     HVec<float> fg_t_;
+    HVec<uint8_t> ev_same_;
     bool in_walk_ = false;  // (freed functor entries are not reused while the fired list is walked)
     bool GatherFrame(const nfk_frame_host& fh, int64_t nfi);
     ModuleScheduler module_sched_;

@@ -66,6 +66,9 @@ constexpr unsigned kAblFanWin16 = 1u << 24, kAblFanWin32 = 1u << 25;  // k_tick 
 constexpr unsigned kAblFan1 = 1u << 26;      // k_tick fan-out: one recipient per lane (the round-1 form; outputs exact)
 constexpr unsigned kAblTinyTcap = 1u << 27;  // test hook: k_tick's fan-out bound set to 4 messages (kErrFanBound)
 constexpr unsigned kAblForceMsgCap = 1u << 29;  // test hook: the frame's ranks also raise kErrMsgCap
+// timing only (k_records): a private record event's recipient word and message offset not stored /
+// its slot word not stored (what an implicit-self or per-span event format would save)
+constexpr unsigned kAblRecNoMsg = 1u << 30, kAblRecNoSlot = 1u << 31;
 // four u32 at a dword-aligned address (gfx950 global memory allows it; one 16-byte store)
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Pad between consecutive property columns and schedule-kind arrays (bytes): with cap a power of

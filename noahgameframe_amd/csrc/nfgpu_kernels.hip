@@ -1200,12 +1200,13 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     if (qq >= n) break;
                     const unsigned at = pos + qq;
                     const uint32_t lmo = pmsg + per * qq;
-                    t_slot[at] = (uint32_t)e;
+                    const bool skip_msg = (d.ablate & kAblRecNoMsg) && !(rfl & NFK_PUBLIC);  // (timing only)
+                    if (!(d.ablate & kAblRecNoSlot)) t_slot[at] = (uint32_t)e;
                     t_rrc[at] = s_errc[w][qq];
                     t_old[at] = s_eold[w][qq];
                     t_new[at] = s_enew[w][qq];
-                    t_moff[at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
-                    if (d.fuse_rec && per) {
+                    if (!skip_msg) t_moff[at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
+                    if (d.fuse_rec && per && !skip_msg) {
                         // GetBroadCastObject (AOI:531-593) for the record event, into the tile's run
                         uint32_t* out = d.msg_rcpt + mrb + lmo;
                         if (!(rfl & NFK_PUBLIC)) {

@@ -881,7 +881,8 @@ bool NFGPUKernelModule::Execute() {
     t1 = std::chrono::steady_clock::now();
     if (what & NFK_READ_EVENTS)
         DeliverEvents(fh, gathered && !ev_self_.empty() ? ev_self_.data() : nullptr,
-                      gathered && !re_self_.empty() ? re_self_.data() : nullptr);
+                      gathered && !re_self_.empty() ? re_self_.data() : nullptr,
+                      gathered && !ev_same_.empty() ? ev_same_.data() : nullptr);
     if (what)
         for (auto& fc : frame_cb_) fc(fh, guids_.data());
     stats_.deliver = ms_since(t1);
@@ -967,7 +968,20 @@ void NFGPUKernelModule::TakeAddedSchedules() {
     ta_k_.resize((size_t)cap);
     int32_t n = 0;
     check(nfk_read_added(world_, cap, &n, ta_h_.data(), ta_d_.data(), ta_k_.data()), "nfk_read_added");
-    for (int32_t i = 0; i < std::min(n, cap); i++) {
+    n = std::min(n, cap);
+    // the new functor entries are taken in the order the heartbeat walk reads them (NFGUID, then
+    // kind): the pool the walk streams through is then in walk order for every batch of adds (an
+    // (object, kind) added again later reuses its entry)
+    ta_ord_.resize((size_t)n);
+    for (int32_t i = 0; i < n; i++) ta_ord_[(size_t)i] = i;
+    static const bool ordered = !(getenv("NFGPU_PLUGIN_POOL_ORDER") && getenv("NFGPU_PLUGIN_POOL_ORDER")[0] == '0');
+    if (ordered)
+        std::sort(ta_ord_.begin(), ta_ord_.end(), [&](int32_t a, int32_t b) {
+            const NFGUID ga(ta_h_[(size_t)a], ta_d_[(size_t)a]), gb(ta_h_[(size_t)b], ta_d_[(size_t)b]);
+            return ga < gb || (ga == gb && ta_k_[(size_t)a] < ta_k_[(size_t)b]);
+        });
+    for (int32_t j = 0; j < n; j++) {
+        const int32_t i = ta_ord_[(size_t)j];
         const int o = ObjectIndex(NFGUID(ta_h_[(size_t)i], ta_d_[(size_t)i]));
         if (o < 0) continue;
         const AddKey q{ta_h_[(size_t)i], ta_d_[(size_t)i], ta_k_[(size_t)i], -1};
@@ -991,7 +1005,7 @@ bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
     if (nfi + nev + nre < std::max<int64_t>(kMin, 1)) return false;
     if (!pool_) {
         const char* e = getenv("NFGPU_PLUGIN_THREADS");
-        const int nw = e ? atoi(e) : 4;
+        const int nw = e ? atoi(e) : 8;
         if (nw <= 0) return false;
         pool_.reset(new nfgpu_detail::WorkerPool(nw));
     }
@@ -1000,6 +1014,11 @@ bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
     fg_t_.resize((size_t)nfi);
     ev_self_.resize((size_t)nev);
     re_self_.resize((size_t)nre);
+    // (per property event: its recipient run equals the previous event's, so the delivery reuses the
+    // NFGUID list it built; consecutive events of a scene group mostly share their recipients)
+    static const bool same_on = !(getenv("NFGPU_PLUGIN_SAME") && getenv("NFGPU_PLUGIN_SAME")[0] == '0');
+    const bool runs = same_on && fh.msg_off && !aoi_prop_cb_.empty();
+    ev_same_.resize(runs ? (size_t)nev : 0);
     constexpr int64_t kChunk = 1 << 14, kPre = 16;
     const int64_t cf = (nfi + kChunk - 1) / kChunk, ce = (nev + kChunk - 1) / kChunk, cr = (nre + kChunk - 1) / kChunk;
     const size_t nk = heartbeats_.size(), nslot = cb_slot_.size();
@@ -1024,6 +1043,23 @@ bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
                 if (i + kPre < i1) __builtin_prefetch(&guids_[(size_t)fh.ev_obj[i + kPre]]);
                 ev_self_[(size_t)i] = guids_[(size_t)fh.ev_obj[i]];
             }
+            if (runs) {
+                // against the last event before it with a non-empty run (the one the delivery's
+                // list then holds: events with no recipients make no AOI call)
+                int64_t p = i0 - 1;
+                while (p >= 0 && fh.msg_off[p + 1] == fh.msg_off[p]) p--;
+                for (int64_t i = i0; i < i1; i++) {
+                    const uint32_t m0 = fh.msg_off[i], m1 = fh.msg_off[i + 1];
+                    if (m1 == m0) {
+                        ev_same_[(size_t)i] = 0;
+                        continue;
+                    }
+                    const uint32_t q0 = p >= 0 ? fh.msg_off[p] : 0u, q1 = p >= 0 ? fh.msg_off[p + 1] : 0u;
+                    ev_same_[(size_t)i] = p >= 0 && m1 - m0 == q1 - q0 &&
+                                          std::memcmp(fh.msg_rcpt + m0, fh.msg_rcpt + q0, (size_t)(m1 - m0) * 4) == 0;
+                    p = i;
+                }
+            }
         } else {
             const int64_t i0 = (q - cf - ce) * kChunk, i1 = std::min(nre, i0 + kChunk);
             for (int64_t i = i0; i < i1; i++) {
@@ -1035,15 +1071,17 @@ bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
     return true;
 }
 
-void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_self, const NFGUID* re_self) {
+void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_self, const NFGUID* re_self,
+                                      const uint8_t* ev_same) {
     if (common_prop_cb_.empty() && aoi_prop_cb_.empty() && common_rec_cb_.empty() && aoi_rec_cb_.empty()) return;
     std::vector<NFGUID> rcpt;
     uint32_t rcpt_at = 0, rcpt_n = 0xFFFFFFFFu;  // the msg_rcpt run rcpt holds
     constexpr int64_t kPre = 16;  // events are in slot order; their objects' NFGUIDs are scattered
+    TData a, b;
     for (int64_t e = 0; e < f.n_ev; e++) {
         if (!ev_self && e + kPre < f.n_ev) __builtin_prefetch(&guids_[(size_t)f.ev_obj[e + kPre]]);
         const PropertyDef& pd = props_[def_of_pid_[f.ev_pid[e]]];
-        TData a, b;
+        a = b = TData{};
         a.type = b.type = pd.type;
         if (pd.type == TDATA_INT) {
             a.i = (int64_t)f.ev_old[e];
@@ -1059,9 +1097,11 @@ void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_
         for (auto& cb : common_prop_cb_) cb(self, pd.name, a, b);
         if (f.msg_off && !aoi_prop_cb_.empty() && f.msg_off[e + 1] > f.msg_off[e]) {  // AOI.cpp:250: no call for empty lists
             // consecutive events of a scene group mostly share their recipients: rebuild the list
-            // only when the run differs from the previous event's
+            // only when the run differs from the last one delivered (ev_same: compared by the workers)
             const uint32_t m0 = f.msg_off[e], m1 = f.msg_off[e + 1];
-            if (m1 - m0 != rcpt_n || memcmp(f.msg_rcpt + m0, f.msg_rcpt + rcpt_at, (size_t)(m1 - m0) * 4) != 0) {
+            const bool same = ev_same ? ev_same[e] != 0
+                                      : m1 - m0 == rcpt_n && memcmp(f.msg_rcpt + m0, f.msg_rcpt + rcpt_at, (size_t)(m1 - m0) * 4) == 0;
+            if (!same) {
                 rcpt.resize(m1 - m0);
                 for (uint32_t m = m0; m < m1; m++) rcpt[m - m0] = guids_[f.msg_rcpt[m]];
             }
