@@ -22,8 +22,12 @@ RowMemory DeviceRowMemory() {
                          return p;
                      },
                      [](void* p) { (void)hipFree(p); },
+                     // complete when it returns: a device-to-device hipMemcpy may return before the
+                     // copy is done, and the rows' readers (the import's copy on the world's stream,
+                     // the source's next export) are not ordered after the null stream
                      [](void* d, const void* s, size_t n) {
-                         if (hipMemcpy(d, s, n, hipMemcpyDeviceToDevice) != hipSuccess)
+                         if (hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, nullptr) != hipSuccess ||
+                             hipStreamSynchronize(nullptr) != hipSuccess)
                              throw std::runtime_error("hipMemcpy (shard rows)");
                      }};
 }

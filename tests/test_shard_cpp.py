@@ -97,6 +97,12 @@ def test_plugin_shard_replay_matches_oracle(gpu_available, tmp_path, ranks):
         got = nfio.read(str(tmp_path / f"rank{k}.nfio"))
         moved += int(got["migrated"][0])
         for t, e in enumerate(per[k]):
+            if len(got[f"ev_t{t}_obj"]) != len(e["ev_obj"]):  # name the events that differ
+                rows = lambda d, pf: {(int(o), int(q), int(a), int(b)) for o, q, a, b in zip(
+                    d[f"{pf}obj"], d[f"{pf}pid"], d[f"{pf}old"].view(np.int64), d[f"{pf}new"].view(np.int64))}
+                g_, e_ = rows(got, f"ev_t{t}_"), rows(e, "ev_")
+                raise AssertionError(f"rank {k} frame {t}: events only here {sorted(g_ - e_)[:8]}, "
+                                     f"only in the oracle {sorted(e_ - g_)[:8]}")
             for p in ("ev", "re"):
                 for f in ("obj", "pid", "old", "new", "rrc"):
                     if f"{p}_{f}" in e:

@@ -52,6 +52,7 @@ for step in "$@"; do
                      -k "plugin or functor or adapter or logic_session or shard" ;;
     pluginab) run pluginab 900 python tools/plugin_frame_ab.py --rounds ${PABR:-2} ${PAB:-NFGPU_PLUGIN_THREADS=0 NFGPU_PLUGIN_THREADS=4 NFGPU_PLUGIN_THREADS=8} ;;
     repeat) run repeat 900 tools/repeat_test.sh "$TAG/repeat" ${RR:-3} "${RK:-plugin_shard_replay}" ;;
+    repeatpack) LIBDIR=ab/pack run repeatpack 900 tools/repeat_test.sh "$TAG/repeatpack" ${RR:-3} "${RK:-plugin_shard_replay}" ;;
     repeatbase) LIBDIR=ab/base run repeatbase 900 tools/repeat_test.sh "$TAG/repeatbase" ${RR:-3} "${RK:-plugin_shard_replay}" ;;
     pluginbench) run pluginbench 600 python bench.py --steps 20 --warmup 3 --cpu-baseline off --host-calls off ;;
     membership) NFGPU_TRACE_MEMBERSHIP=1 run membership 300 python tools/membership_bench.py ;;
