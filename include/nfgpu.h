@@ -120,7 +120,10 @@ typedef struct nfk_summary {
  *   record events    (scene, group, guid, rec, ...): per record its row events (AddRow / Remove /
  *                    ClearRecord, in call order) then its cell Updates in (row, col) order;
  *                    rrc = op<<24 | rec<<16 | row<<8 | col, op 0 = Update (RECORD_EVENT_DATA::Update,
- *                    old / new the cell), 1 = Add, 2 = Del, 3 = Cover (row events: col 0, old = new = 0)
+ *                    old / new the cell), 1 = Add, 2 = Del, 3 = Cover (row events: col 0, old = new = 0).
+ *                    In the raw tiles (nfk_outputs) the word also carries the event's slot: bits
+ *                    26-31 = slot - tile * rtile_slots (the record tile the event sits in), op in
+ *                    bits 24-25; re_slot is NULL.  The nfk_read_* arrays carry the word above.
  *   fired heartbeats (scene, group, guid, kind)
  * Fan-out (GetBroadCastObject recipients): the messages of tile t (property tiles, then record
  * tiles) are one run of msg_cnt[t] recipients at msg_rcpt[msg_base[t]], in event order.  Runs
@@ -144,7 +147,8 @@ typedef struct nfk_outputs {
     const uint32_t* msg_cnt;   /* [n_tiles + n_rtiles] messages of each tile */
     const uint32_t* ev_slot; const uint32_t* ev_pid; const uint64_t* ev_old; const uint64_t* ev_new;
     const uint32_t* ev_moff;
-    const uint32_t* re_slot; const uint32_t* re_rrc; const uint64_t* re_old; const uint64_t* re_new;
+    const uint32_t* re_slot; /* NULL: a record event's slot is in its re_rrc word (above) */
+    const uint32_t* re_rrc; const uint64_t* re_old; const uint64_t* re_new;
     const uint32_t* re_moff;
     const uint32_t* fi_slot; const uint32_t* fi_kind; const int32_t* fi_remain;
     const uint32_t* msg_rcpt; /* one run per tile (see above) */

@@ -14,6 +14,12 @@ constexpr int kTile = 256;    // slots per property/fired tile (one k_tick workg
 #endif
 constexpr int kRTile = NFGPU_RTILE;  // slots per record-event tile (one k_records wave; <= 64)
 static_assert(kRTile >= 1 && kRTile <= 64, "a record tile is at most one wave of slots");
+// A record event's word in the raw device outputs (re_rrc): record << 16 | row << 8 | column, the
+// row-event op (0 a cell's update, 1 AddRow, 2 Remove, 3 Clear / Cover) in bits 24-25, and the slot's
+// index within its record tile in bits 26-31 (the tile is where the event sits), so no slot word is
+// stored per event.  The host formats carry op << 24 | record << 16 | row << 8 | column.
+constexpr uint32_t kRrcHost = 0x03FFFFFFu;
+constexpr int kRrcSitShift = 26;
 
 // device error word bits (Ctrl::err)
 constexpr unsigned kErrMsgCap = 4, kErrTouch = 8, kErrFanBound = 16;
@@ -66,9 +72,9 @@ constexpr unsigned kAblFanWin16 = 1u << 24, kAblFanWin32 = 1u << 25;  // k_tick 
 constexpr unsigned kAblFan1 = 1u << 26;      // k_tick fan-out: one recipient per lane (the round-1 form; outputs exact)
 constexpr unsigned kAblTinyTcap = 1u << 27;  // test hook: k_tick's fan-out bound set to 4 messages (kErrFanBound)
 constexpr unsigned kAblForceMsgCap = 1u << 29;  // test hook: the frame's ranks also raise kErrMsgCap
-// timing only (k_records): a private record event's recipient word and message offset not stored /
-// its slot word not stored (what an implicit-self or per-span event format would save)
-constexpr unsigned kAblRecNoMsg = 1u << 30, kAblRecNoSlot = 1u << 31;
+// timing only (k_records): a private record event's recipient word and message offset not stored
+// (what an implicit-self message format would save)
+constexpr unsigned kAblRecNoMsg = 1u << 30;
 // four u32 at a dword-aligned address (gfx950 global memory allows it; one 16-byte store)
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Pad between consecutive property columns and schedule-kind arrays (bytes): with cap a power of
@@ -276,7 +282,7 @@ struct Dev {
     // outputs (tile-staged)
     uint32_t* ev_slot; uint32_t* ev_pid; uint64_t* ev_old; uint64_t* ev_new; uint32_t* ev_moff;
     uint32_t* fi_slot; uint32_t* fi_kind; int32_t* fi_remain;
-    uint32_t* re_slot; uint32_t* re_rrc; uint64_t* re_old; uint64_t* re_new; uint32_t* re_moff;
+    uint32_t* re_rrc; uint64_t* re_old; uint64_t* re_new; uint32_t* re_moff;  // (re_rrc: see kRrcHost)
     uint32_t* msg_rcpt; int64_t msg_cap;
     uint64_t* ev_old_h; uint64_t* ev_new_h;  // head halves of object-property events (n_obj > 0)
     // host-mapped error words [kErrHostWords]: a kernel that sets bit b of ctrl->err also stores 1

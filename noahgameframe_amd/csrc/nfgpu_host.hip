@@ -869,7 +869,7 @@ int grow_rec_tiles(World* w, int64_t per_tile) {
     HIPCHK(hipStreamSynchronize(w->stream));
     const size_t n = (size_t)(d.cap / kRTile) * (size_t)tcap;
     int r;
-    if ((r = regrow(w, (void**)&d.re_slot, n * 4)) || (r = regrow(w, (void**)&d.re_rrc, n * 4)) ||
+    if ((r = regrow(w, (void**)&d.re_rrc, n * 4)) ||
         (r = regrow(w, (void**)&d.re_old, n * 8)) || (r = regrow(w, (void**)&d.re_new, n * 8)) ||
         (r = regrow(w, (void**)&d.re_moff, n * 4))) {
         d.re_tcap = 0;
@@ -2065,7 +2065,6 @@ int nfk_commit(void* world) {
     ALLOC(d.fi_slot, fi_n * 4);
     ALLOC(d.fi_kind, fi_n * 4);
     ALLOC(d.fi_remain, fi_n * 4);
-    ALLOC(d.re_slot, re_n * 4);
     ALLOC(d.re_rrc, re_n * 4);
     ALLOC(d.re_old, re_n * 8);
     ALLOC(d.re_new, re_n * 8);
@@ -3193,7 +3192,7 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
             int r = grow_rec_tiles(w, need_re);
             if (r) return drop_window(w, r);
             d.re_tcap = w->d.re_tcap;
-            d.re_slot = w->d.re_slot; d.re_rrc = w->d.re_rrc; d.re_old = w->d.re_old;
+            d.re_rrc = w->d.re_rrc; d.re_old = w->d.re_old;
             d.re_new = w->d.re_new; d.re_moff = w->d.re_moff;
         }
     }
@@ -3822,7 +3821,8 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     o->ev_base = d.ev_base; o->fi_base = d.fi_base; o->re_base = d.re_base; o->msg_base = d.msg_base;
     o->msg_cnt = d.t_msg;
     o->ev_slot = d.ev_slot; o->ev_pid = d.ev_pid; o->ev_old = d.ev_old; o->ev_new = d.ev_new; o->ev_moff = d.ev_moff;
-    o->re_slot = d.re_slot; o->re_rrc = d.re_rrc; o->re_old = d.re_old; o->re_new = d.re_new; o->re_moff = d.re_moff;
+    o->re_slot = nullptr;  // (a record event's slot is in its word: nfgpu.h)
+    o->re_rrc = d.re_rrc; o->re_old = d.re_old; o->re_new = d.re_new; o->re_moff = d.re_moff;
     o->fi_slot = d.fi_slot; o->fi_kind = d.fi_kind; o->fi_remain = d.fi_remain;
     o->msg_rcpt = d.msg_rcpt;
     o->slot_obj = w->slot_obj_d;
@@ -3954,12 +3954,17 @@ int nfk_read_rec_events(void* world, int32_t* re_obj, uint32_t* re_rrc, uint64_t
     if (r) return r;
     const Dev& d = w->d;
     const size_t n = c.n_re;
-    std::vector<uint32_t> sl(n);
-    GATHER(w, d.re_slot, d.re_base, d.n_rtiles, d.re_tcap, n, sl.data());
     GATHER(w, d.re_rrc, d.re_base, d.n_rtiles, d.re_tcap, n, re_rrc);
     GATHER(w, d.re_old, d.re_base, d.n_rtiles, d.re_tcap, n, re_old);
     GATHER(w, d.re_new, d.re_base, d.n_rtiles, d.re_tcap, n, re_new);
-    for (size_t i = 0; i < n; i++) re_obj[i] = w->obj_of_slot[sl[i]];
+    // each event's slot: its record tile's first slot + the slot field of its word (kRrcHost)
+    std::vector<uint32_t> rb((size_t)d.n_rtiles + 1, 0);
+    if (n) HIPCHK(hipMemcpy(rb.data(), d.re_base, rb.size() * 4, hipMemcpyDeviceToHost));
+    for (int t = 0; t < d.n_rtiles; t++)
+        for (uint32_t i = rb[(size_t)t]; i < rb[(size_t)t + 1] && i < n; i++) {
+            re_obj[i] = w->obj_of_slot[(size_t)t * kRTile + (re_rrc[i] >> kRrcSitShift)];
+            re_rrc[i] &= kRrcHost;
+        }
     return NFK_OK;
 }
 
@@ -4142,10 +4147,8 @@ int nfk_read_frame(void* world, uint32_t what, nfk_frame_host* o) {
         }
     }
     if (nr) {
-        hipLaunchKernelGGL(k_compact_obj, dim3(grt), dim3(kTPB), 0, w->stream, d.re_slot, (int32_t*)(D + o_ro),
-                           d.re_base, d.n_rtiles, d.re_tcap, so);
-        hipLaunchKernelGGL(k_compact<uint32_t>, dim3(grt), dim3(kTPB), 0, w->stream, d.re_rrc, (uint32_t*)(D + o_rr),
-                           d.re_base, d.n_rtiles, d.re_tcap);
+        hipLaunchKernelGGL(k_compact_rec, dim3(grt), dim3(kTPB), 0, w->stream, d.re_rrc, (int32_t*)(D + o_ro),
+                           (uint32_t*)(D + o_rr), d.re_base, d.n_rtiles, d.re_tcap, so);
         hipLaunchKernelGGL(k_compact<uint64_t>, dim3(grt), dim3(kTPB), 0, w->stream, d.re_old, (uint64_t*)(D + o_rold),
                            d.re_base, d.n_rtiles, d.re_tcap);
         hipLaunchKernelGGL(k_compact<uint64_t>, dim3(grt), dim3(kTPB), 0, w->stream, d.re_new, (uint64_t*)(D + o_rnew),

@@ -853,6 +853,7 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
     const int nro = d.n_rops;
     const int rt = e / kRTile;
     const size_t re0 = (size_t)rt * d.re_tcap;
+    const uint32_t sit = (uint32_t)(e - rt * kRTile) << kRrcSitShift;  // (the event word's slot field)
     const uint32_t mrb = d.fuse_rec ? d.msg_rb0 + (uint32_t)rt * d.msg_rtcap : 0u;
     unsigned pos = kEmit ? d.rss_pos[si] : 0u, pmsg = kEmit ? d.rss_pmsg[si] : 0u;
     unsigned bytes = 0;
@@ -899,12 +900,11 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
                     const uint32_t x = rev[q];
                     const unsigned at = pos + q;
                     const uint32_t lmo = pmsg + per * q;
-                    d.re_slot[re0 + at] = (uint32_t)e;
-                    d.re_rrc[re0 + at] = ((x >> 8) << 24) | ((uint32_t)r << 16) | ((x & 0xFF) << 8);
+                    d.re_rrc[re0 + at] = sit | ((x >> 8) << 24) | ((uint32_t)r << 16) | ((x & 0xFF) << 8);
                     d.re_old[re0 + at] = 0;
                     d.re_new[re0 + at] = 0;
                     d.re_moff[re0 + at] = mrb + lmo;
-                    bytes += 32;
+                    bytes += 28;
                     if (d.fuse_rec && per) fan(lmo);
                 }
             }
@@ -982,12 +982,11 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
                 if (!ev) continue;
                 const unsigned at = pos + k;
                 const uint32_t lmo = pmsg + per * k;
-                d.re_slot[re0 + at] = (uint32_t)e;
-                d.re_rrc[re0 + at] = ((uint32_t)r << 16) | ((uint32_t)lane << 8) | (uint32_t)c;
+                d.re_rrc[re0 + at] = sit | ((uint32_t)r << 16) | ((uint32_t)lane << 8) | (uint32_t)c;
                 d.re_old[re0 + at] = ob;
                 d.re_new[re0 + at] = nb;
                 d.re_moff[re0 + at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
-                bytes += 28;
+                bytes += 24;
                 if (d.fuse_rec && per) fan(lmo);  // GetBroadCastObject (AOI:531-593)
                 k++;
             }
@@ -1058,7 +1057,6 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     unsigned pos = 0, pmsg = 0;  // tile-local
     // this tile's output runs as wave-uniform base pointers, indexed by 32-bit tile-local offsets
     const size_t re0 = (size_t)rt * d.re_tcap;
-    uint32_t* const t_slot = d.re_slot + re0;
     uint32_t* const t_rrc = d.re_rrc + re0;
     uint64_t* const t_old = d.re_old + re0;
     uint64_t* const t_new = d.re_new + re0;
@@ -1191,7 +1189,8 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     if (!(j >= j0 && j <= j1 && ch[j])) continue;
                     s_eold[w][q] = G.cur[g][j];
                     s_enew[w][q] = nv[j];
-                    s_errc[w][q] = ((uint32_t)d.rops[j].rec << 16) | ((uint32_t)lane << 8) | (uint32_t)d.rops[j].col;
+                    s_errc[w][q] = ((uint32_t)G.js[g] << kRrcSitShift) | ((uint32_t)d.rops[j].rec << 16) |
+                                   ((uint32_t)lane << 8) | (uint32_t)d.rops[j].col;
                     q++;
                 }
                 __builtin_amdgcn_wave_barrier();  // (one wave's LDS operations complete in order)
@@ -1201,7 +1200,6 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     const unsigned at = pos + qq;
                     const uint32_t lmo = pmsg + per * qq;
                     const bool skip_msg = (d.ablate & kAblRecNoMsg) && !(rfl & NFK_PUBLIC);  // (timing only)
-                    if (!(d.ablate & kAblRecNoSlot)) t_slot[at] = (uint32_t)e;
                     t_rrc[at] = s_errc[w][qq];
                     t_old[at] = s_eold[w][qq];
                     t_new[at] = s_enew[w][qq];
@@ -1223,7 +1221,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     }
                 }
                 // event records, their recipient words and (public) the player run read per event
-                sbytes += n * (28u + ((d.fuse_rec && per) ? 4u * per : 0u) +
+                sbytes += n * (24u + ((d.fuse_rec && per) ? 4u * per : 0u) +
                                ((d.fuse_rec && per && (rfl & NFK_PUBLIC)) ? 4u * (uint32_t)((desc >> 32) & 0x3FFF) : 0u));
                 __builtin_amdgcn_wave_barrier();
                 pos += n;
@@ -1399,7 +1397,8 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
     const uint32_t* base = rec ? d.re_base : d.ev_base;
     const unsigned tcap = (unsigned)(rec ? d.re_tcap : d.ev_tcap);
     const size_t off0 = (size_t)t * tcap;
-    const uint32_t* slots = rec ? d.re_slot : d.ev_slot;
+    const uint32_t* slots = rec ? d.re_rrc : d.ev_slot;  // (a record event's slot is in its word)
+    const uint32_t s_base = (uint32_t)t * (uint32_t)kRTile;
     uint32_t* moff = rec ? d.re_moff : d.ev_moff;
     // one round trip: the tile's counts, its message range and (speculatively, inside the tile's
     // staging capacity) the first pass's events
@@ -1411,8 +1410,9 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
         const unsigned i = q * kTPB + threadIdx.x;
         slot[q] = key[q] = lm[q] = 0;
         if (i < tcap) {
-            slot[q] = slots[off0 + i];
-            key[q] = rec ? ((d.re_rrc[off0 + i] >> 16) & 0xFF) : d.ev_pid[off0 + i];
+            const uint32_t x = slots[off0 + i];
+            slot[q] = rec ? s_base + (x >> kRrcSitShift) : x;
+            key[q] = rec ? ((x >> 16) & 0xFF) : d.ev_pid[off0 + i];
             lm[q] = moff[off0 + i];
         }
     }
@@ -1436,8 +1436,9 @@ __global__ __launch_bounds__(kTPB) void k_fanout(Dev d, int32_t blk0) {
             for (int q = 0; q < kFanPer; q++) {
                 const unsigned i = c0 + q * kTPB + threadIdx.x;
                 if (i < cnt) {
-                    slot[q] = slots[off0 + i];
-                    key[q] = rec ? ((d.re_rrc[off0 + i] >> 16) & 0xFF) : d.ev_pid[off0 + i];
+                    const uint32_t x = slots[off0 + i];
+                    slot[q] = rec ? s_base + (x >> kRrcSitShift) : x;
+                    key[q] = rec ? ((x >> 16) & 0xFF) : d.ev_pid[off0 + i];
                     lm[q] = moff[off0 + i];
                 }
             }
@@ -1843,6 +1844,19 @@ __global__ __launch_bounds__(kTPB) void k_compact_obj(const uint32_t* __restrict
     for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
         const uint32_t b = base[t], n = base[t + 1] - b;
         for (uint32_t i = threadIdx.x; i < n; i += kTPB) dst[b + i] = slot_obj[src[(size_t)t * tcap + i]];
+    }
+}
+// record events: the slot from the event word and its tile, the word in the host format
+__global__ __launch_bounds__(kTPB) void k_compact_rec(const uint32_t* __restrict__ src, int32_t* __restrict__ obj,
+                                                      uint32_t* __restrict__ rrc, const uint32_t* __restrict__ base,
+                                                      int n_tiles, int tcap, const int32_t* __restrict__ slot_obj) {
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const uint32_t b = base[t], n = base[t + 1] - b;
+        for (uint32_t i = threadIdx.x; i < n; i += kTPB) {
+            const uint32_t x = src[(size_t)t * tcap + i];
+            obj[b + i] = slot_obj[(uint32_t)t * (uint32_t)kRTile + (x >> kRrcSitShift)];
+            rrc[b + i] = x & kRrcHost;
+        }
     }
 }
 // object-property head halves: 0 for the other events (their entries are unwritten)
