@@ -3822,7 +3822,8 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     o->msg_cnt = d.t_msg;
     o->ev_slot = d.ev_slot; o->ev_pid = d.ev_pid; o->ev_old = d.ev_old; o->ev_new = d.ev_new; o->ev_moff = d.ev_moff;
     o->re_slot = nullptr;  // (a record event's slot is in its word: nfgpu.h)
-    o->re_rrc = d.re_rrc; o->re_old = d.re_old; o->re_new = d.re_new; o->re_moff = d.re_moff;
+    o->re_rrc = d.re_rrc; o->re_old = d.re_old; o->re_new = d.re_new;
+    o->re_moff = w->last_rtcap ? nullptr : d.re_moff;  // (fused record tiles store none: nfgpu.h)
     o->fi_slot = d.fi_slot; o->fi_kind = d.fi_kind; o->fi_remain = d.fi_remain;
     o->msg_rcpt = d.msg_rcpt;
     o->slot_obj = w->slot_obj_d;
@@ -4014,15 +4015,33 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
     }
     if (acc != nm) return fail(NFK_ERR_STATE, "message cursor and tile counts disagree");
     GATHER(w, d.ev_moff, d.ev_base, d.n_tiles, d.ev_tcap, (size_t)c.n_ev, msg_off);
-    if (d.has_recops) GATHER(w, d.re_moff, d.re_base, d.n_rtiles, d.re_tcap, (size_t)c.n_re, msg_off + c.n_ev);
+    const bool rec_counted = d.has_recops && w->last_rtcap;  // (fused record tiles store no offsets)
+    if (d.has_recops && !rec_counted)
+        GATHER(w, d.re_moff, d.re_base, d.n_rtiles, d.re_tcap, (size_t)c.n_re, msg_off + c.n_ev);
     for (int t = 0; t < d.n_tiles; t++)
         for (uint32_t i = eb[t]; i < eb[t + 1]; i++) msg_off[i] = (uint32_t)(msg_off[i] - mb[t] + db[t]);
-    if (d.has_recops)
+    if (d.has_recops && !rec_counted)
         for (int t = 0; t < d.n_rtiles; t++)
             for (uint32_t i = rb[t]; i < rb[t + 1]; i++) {
                 const int tg = d.n_tiles + t;
                 msg_off[c.n_ev + i] = (uint32_t)(msg_off[c.n_ev + i] - mb[tg] + db[tg]);
             }
+    if (rec_counted && c.n_re) {  // counted on the device (k_rec_moff) from the dense bases
+        std::vector<uint32_t> dbv(ntt);
+        for (int t = 0; t < ntt; t++) dbv[t] = (uint32_t)db[t];
+        uint32_t* tmp = nullptr;
+        HIPCHK(hipMalloc((void**)&tmp, ((size_t)ntt + (size_t)c.n_re) * 4));
+        HIPCHK(hipMemcpy(tmp, dbv.data(), (size_t)ntt * 4, hipMemcpyHostToDevice));
+        const unsigned grt = (unsigned)std::max(1, std::min(d.n_rtiles, 4096));
+        hipLaunchKernelGGL(k_rec_moff, dim3(grt), dim3(kTPB), 0, w->stream, d, tmp + ntt, (const uint32_t*)tmp);
+        const hipError_t le = hipGetLastError();
+        hipError_t ce = le == hipSuccess ? hipMemcpyAsync(msg_off + c.n_ev, tmp + ntt, (size_t)c.n_re * 4,
+                                                          hipMemcpyDeviceToHost, w->stream)
+                                         : le;
+        if (ce == hipSuccess) ce = hipStreamSynchronize(w->stream);
+        (void)hipFree(tmp);
+        if (ce != hipSuccess) return fail(NFK_ERR_HIP, std::string("k_rec_moff: ") + hipGetErrorString(ce));
+    }
     msg_off[c.n_ev + c.n_re] = (uint32_t)nm;
     // the runs cover [0, extent) with gaps when property tiles sit at a stride
     const size_t ext = (size_t)c.msg_extent;
@@ -4160,7 +4179,9 @@ int nfk_read_frame(void* world, uint32_t what, nfk_frame_host* o) {
         if (ne)
             hipLaunchKernelGGL(k_compact_moff, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_moff, (uint32_t*)(D + o_mo),
                                d.ev_base, d.n_tiles, d.ev_tcap, d.msg_base, db);
-        if (nr)
+        if (nr && w->last_rtcap)  // (k_records fanned them out: no stored offsets, counted here)
+            hipLaunchKernelGGL(k_rec_moff, dim3(grt), dim3(kTPB), 0, w->stream, d, (uint32_t*)(D + o_mo) + ne, db);
+        else if (nr)
             hipLaunchKernelGGL(k_compact_moff, dim3(grt), dim3(kTPB), 0, w->stream, d.re_moff,
                                (uint32_t*)(D + o_mo) + ne, d.re_base, d.n_rtiles, d.re_tcap, d.msg_base + d.n_tiles,
                                db + d.n_tiles);

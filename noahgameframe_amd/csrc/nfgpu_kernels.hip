@@ -903,8 +903,8 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
                     d.re_rrc[re0 + at] = sit | ((x >> 8) << 24) | ((uint32_t)r << 16) | ((x & 0xFF) << 8);
                     d.re_old[re0 + at] = 0;
                     d.re_new[re0 + at] = 0;
-                    d.re_moff[re0 + at] = mrb + lmo;
-                    bytes += 28;
+                    if (!d.fuse_rec) d.re_moff[re0 + at] = lmo;  // (fused: the readers count, k_rec_moff)
+                    bytes += d.fuse_rec ? 24 : 28;
                     if (d.fuse_rec && per) fan(lmo);
                 }
             }
@@ -985,8 +985,8 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
                 d.re_rrc[re0 + at] = sit | ((uint32_t)r << 16) | ((uint32_t)lane << 8) | (uint32_t)c;
                 d.re_old[re0 + at] = ob;
                 d.re_new[re0 + at] = nb;
-                d.re_moff[re0 + at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
-                bytes += 24;
+                if (!d.fuse_rec) d.re_moff[re0 + at] = lmo;  // tile-local: k_fanout adds the base
+                bytes += d.fuse_rec ? 20 : 24;
                 if (d.fuse_rec && per) fan(lmo);  // GetBroadCastObject (AOI:531-593)
                 k++;
             }
@@ -1203,7 +1203,9 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     t_rrc[at] = s_errc[w][qq];
                     t_old[at] = s_eold[w][qq];
                     t_new[at] = s_enew[w][qq];
-                    if (!skip_msg) t_moff[at] = mrb + lmo;  // fused: global; else tile-local (k_fanout adds the base)
+                    // unfused: the tile-local offset k_fanout expands the event at; fused, the run is
+                    // dense in event order and the readers count their way through it (k_rec_moff)
+                    if (!d.fuse_rec) t_moff[at] = lmo;
                     if (d.fuse_rec && per && !skip_msg) {
                         // GetBroadCastObject (AOI:531-593) for the record event, into the tile's run
                         uint32_t* out = d.msg_rcpt + mrb + lmo;
@@ -1221,7 +1223,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     }
                 }
                 // event records, their recipient words and (public) the player run read per event
-                sbytes += n * (24u + ((d.fuse_rec && per) ? 4u * per : 0u) +
+                sbytes += n * ((d.fuse_rec ? 20u : 24u) + ((d.fuse_rec && per) ? 4u * per : 0u) +
                                ((d.fuse_rec && per && (rfl & NFK_PUBLIC)) ? 4u * (uint32_t)((desc >> 32) & 0x3FFF) : 0u));
                 __builtin_amdgcn_wave_barrier();
                 pos += n;
@@ -1856,6 +1858,46 @@ __global__ __launch_bounds__(kTPB) void k_compact_rec(const uint32_t* __restrict
             const uint32_t x = src[(size_t)t * tcap + i];
             obj[b + i] = slot_obj[(uint32_t)t * (uint32_t)kRTile + (x >> kRrcSitShift)];
             rrc[b + i] = x & kRrcHost;
+        }
+    }
+}
+// Record tiles k_records fanned out (no per-event message offsets stored): a tile's run holds its
+// events' recipients in event order, so an event's dense CSR offset is the tile's dense base (db)
+// plus the recipient counts (event_msgs, as k_records counted them) of the events before it.
+__global__ __launch_bounds__(kTPB) void k_rec_moff(Dev d, uint32_t* __restrict__ dst, const uint32_t* __restrict__ db) {
+    __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
+    __shared__ uint32_t s_w[kTPB / 64 + 1];
+    for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
+        ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int t = blockIdx.x; t < d.n_rtiles; t += gridDim.x) {
+        const uint32_t b = d.re_base[t], n = d.re_base[t + 1] - b;
+        uint32_t carry = db[d.n_tiles + t];
+        for (uint32_t c0 = 0; c0 < n; c0 += kTPB) {  // uniform
+            const uint32_t i = c0 + threadIdx.x;
+            uint32_t per = 0;
+            if (i < n) {
+                const uint32_t x = d.re_rrc[(size_t)t * d.re_tcap + i];
+                const uint64_t desc = d.fan_desc[(uint32_t)t * (uint32_t)kRTile + (x >> kRrcSitShift)];
+                per = event_msgs(desc, s_rflags[desc >> 60][(x >> 16) & 0xFF]);
+            }
+            const uint32_t incl = wave_incl_scan_u32(per);
+            if (lane == 63) s_w[w] = incl;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t a = 0;
+                for (int q = 0; q < kTPB / 64; q++) {
+                    const uint32_t v = s_w[q];
+                    s_w[q] = a;
+                    a += v;
+                }
+                s_w[kTPB / 64] = a;
+            }
+            __syncthreads();
+            if (i < n) dst[b + i] = carry + s_w[w] + incl - per;
+            carry += s_w[kTPB / 64];
+            __syncthreads();  // (s_w is rewritten by the next chunk)
         }
     }
 }
