@@ -132,10 +132,11 @@ typedef struct nfk_summary {
  * the record tiles' runs follow, densely or (when k_records fanned them out too) at a fixed
  * stride of their own.  Always walk tiles by msg_base / msg_cnt.  ev_moff / re_moff hold the index in msg_rcpt of the
  * event's first recipient; its recipients end where the next event of its tile begins
- * (msg_base[t] + msg_cnt[t] after the tile's last).  When k_records fanned the record tiles out
- * (fixed-stride record runs) re_moff is NULL: a record tile's run holds its events' recipients in
- * event order, the count of each the recipient count of its record's flags for the entity's class
- * (private & !upload: 1, the entity itself; public: the players of its group but itself).
+ * (msg_base[t] + msg_cnt[t] after the tile's last).  When k_tick fanned the property tiles out
+ * (fixed-stride runs) ev_moff is NULL, and when k_records fanned the record tiles out re_moff is
+ * NULL: such a tile's run holds its events' recipients in event order, the count of each the
+ * recipient count of its property's / record's flags for the entity's class (private & !upload: 1,
+ * the entity itself; public: the players of its group but itself; else 0).
  * Recipients are slots; slot_obj maps slot -> object index.  nfk_read_fanout returns the dense
  * CSR over [property events ++ record events].
  * nfk_read_* return the same data as dense arrays in object-index terms. */

@@ -3820,7 +3820,8 @@ int nfk_outputs_get(void* world, nfk_outputs* o) {
     o->ev_tile_cap = d.ev_tcap; o->fi_tile_cap = d.fi_tcap; o->re_tile_cap = d.re_tcap;
     o->ev_base = d.ev_base; o->fi_base = d.fi_base; o->re_base = d.re_base; o->msg_base = d.msg_base;
     o->msg_cnt = d.t_msg;
-    o->ev_slot = d.ev_slot; o->ev_pid = d.ev_pid; o->ev_old = d.ev_old; o->ev_new = d.ev_new; o->ev_moff = d.ev_moff;
+    o->ev_slot = d.ev_slot; o->ev_pid = d.ev_pid; o->ev_old = d.ev_old; o->ev_new = d.ev_new;
+    o->ev_moff = w->last_tcap ? nullptr : d.ev_moff;  // (tiles k_tick fanned out store none: nfgpu.h)
     o->re_slot = nullptr;  // (a record event's slot is in its word: nfgpu.h)
     o->re_rrc = d.re_rrc; o->re_old = d.re_old; o->re_new = d.re_new;
     o->re_moff = w->last_rtcap ? nullptr : d.re_moff;  // (fused record tiles store none: nfgpu.h)
@@ -4014,33 +4015,46 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
         acc += mc[t];
     }
     if (acc != nm) return fail(NFK_ERR_STATE, "message cursor and tile counts disagree");
-    GATHER(w, d.ev_moff, d.ev_base, d.n_tiles, d.ev_tcap, (size_t)c.n_ev, msg_off);
-    const bool rec_counted = d.has_recops && w->last_rtcap;  // (fused record tiles store no offsets)
+    // (tiles k_tick / k_records fanned out themselves store no offsets: counted on the device below)
+    const bool ev_counted = w->last_tcap != 0, rec_counted = d.has_recops && w->last_rtcap;
+    if (!ev_counted) GATHER(w, d.ev_moff, d.ev_base, d.n_tiles, d.ev_tcap, (size_t)c.n_ev, msg_off);
     if (d.has_recops && !rec_counted)
         GATHER(w, d.re_moff, d.re_base, d.n_rtiles, d.re_tcap, (size_t)c.n_re, msg_off + c.n_ev);
-    for (int t = 0; t < d.n_tiles; t++)
-        for (uint32_t i = eb[t]; i < eb[t + 1]; i++) msg_off[i] = (uint32_t)(msg_off[i] - mb[t] + db[t]);
+    if (!ev_counted)
+        for (int t = 0; t < d.n_tiles; t++)
+            for (uint32_t i = eb[t]; i < eb[t + 1]; i++) msg_off[i] = (uint32_t)(msg_off[i] - mb[t] + db[t]);
     if (d.has_recops && !rec_counted)
         for (int t = 0; t < d.n_rtiles; t++)
             for (uint32_t i = rb[t]; i < rb[t + 1]; i++) {
                 const int tg = d.n_tiles + t;
                 msg_off[c.n_ev + i] = (uint32_t)(msg_off[c.n_ev + i] - mb[tg] + db[tg]);
             }
-    if (rec_counted && c.n_re) {  // counted on the device (k_rec_moff) from the dense bases
+    const size_t ncnt = (ev_counted ? (size_t)c.n_ev : 0) + (rec_counted ? (size_t)c.n_re : 0);
+    if (ncnt) {  // counted on the device (k_counted_moff) from the dense bases
         std::vector<uint32_t> dbv(ntt);
         for (int t = 0; t < ntt; t++) dbv[t] = (uint32_t)db[t];
         uint32_t* tmp = nullptr;
-        HIPCHK(hipMalloc((void**)&tmp, ((size_t)ntt + (size_t)c.n_re) * 4));
+        HIPCHK(hipMalloc((void**)&tmp, ((size_t)ntt + (size_t)c.n_ev + (size_t)c.n_re) * 4));
         HIPCHK(hipMemcpy(tmp, dbv.data(), (size_t)ntt * 4, hipMemcpyHostToDevice));
-        const unsigned grt = (unsigned)std::max(1, std::min(d.n_rtiles, 4096));
-        hipLaunchKernelGGL(k_rec_moff, dim3(grt), dim3(kTPB), 0, w->stream, d, tmp + ntt, (const uint32_t*)tmp);
-        const hipError_t le = hipGetLastError();
-        hipError_t ce = le == hipSuccess ? hipMemcpyAsync(msg_off + c.n_ev, tmp + ntt, (size_t)c.n_re * 4,
-                                                          hipMemcpyDeviceToHost, w->stream)
-                                         : le;
+        uint32_t* out = tmp + ntt;  // [n_ev ++ n_re], as msg_off
+        hipError_t ce = hipSuccess;
+        if (ev_counted && c.n_ev) {
+            const unsigned g = (unsigned)std::max(1, std::min(d.n_tiles, 4096));
+            hipLaunchKernelGGL(k_counted_moff, dim3(g), dim3(kTPB), 0, w->stream, d, 0, out, (const uint32_t*)tmp);
+            ce = hipGetLastError();
+            if (ce == hipSuccess)
+                ce = hipMemcpyAsync(msg_off, out, (size_t)c.n_ev * 4, hipMemcpyDeviceToHost, w->stream);
+        }
+        if (ce == hipSuccess && rec_counted && c.n_re) {
+            const unsigned g = (unsigned)std::max(1, std::min(d.n_rtiles, 4096));
+            hipLaunchKernelGGL(k_counted_moff, dim3(g), dim3(kTPB), 0, w->stream, d, 1, out + c.n_ev, (const uint32_t*)tmp);
+            ce = hipGetLastError();
+            if (ce == hipSuccess)
+                ce = hipMemcpyAsync(msg_off + c.n_ev, out + c.n_ev, (size_t)c.n_re * 4, hipMemcpyDeviceToHost, w->stream);
+        }
         if (ce == hipSuccess) ce = hipStreamSynchronize(w->stream);
         (void)hipFree(tmp);
-        if (ce != hipSuccess) return fail(NFK_ERR_HIP, std::string("k_rec_moff: ") + hipGetErrorString(ce));
+        if (ce != hipSuccess) return fail(NFK_ERR_HIP, std::string("k_counted_moff: ") + hipGetErrorString(ce));
     }
     msg_off[c.n_ev + c.n_re] = (uint32_t)nm;
     // the runs cover [0, extent) with gaps when property tiles sit at a stride
@@ -4176,11 +4190,14 @@ int nfk_read_frame(void* world, uint32_t what, nfk_frame_host* o) {
     if (fan && ntt) {
         uint32_t* db = (uint32_t*)(S + s_db);
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, w->stream, d.t_msg, db, ntt);
-        if (ne)
+        // (tiles k_tick / k_records fanned out themselves store no offsets: counted here)
+        if (ne && w->last_tcap)
+            hipLaunchKernelGGL(k_counted_moff, dim3(gt), dim3(kTPB), 0, w->stream, d, 0, (uint32_t*)(D + o_mo), db);
+        else if (ne)
             hipLaunchKernelGGL(k_compact_moff, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_moff, (uint32_t*)(D + o_mo),
                                d.ev_base, d.n_tiles, d.ev_tcap, d.msg_base, db);
-        if (nr && w->last_rtcap)  // (k_records fanned them out: no stored offsets, counted here)
-            hipLaunchKernelGGL(k_rec_moff, dim3(grt), dim3(kTPB), 0, w->stream, d, (uint32_t*)(D + o_mo) + ne, db);
+        if (nr && w->last_rtcap)
+            hipLaunchKernelGGL(k_counted_moff, dim3(grt), dim3(kTPB), 0, w->stream, d, 1, (uint32_t*)(D + o_mo) + ne, db);
         else if (nr)
             hipLaunchKernelGGL(k_compact_moff, dim3(grt), dim3(kTPB), 0, w->stream, d.re_moff,
                                (uint32_t*)(D + o_mo) + ne, d.re_base, d.n_rtiles, d.re_tcap, d.msg_base + d.n_tiles,

@@ -903,7 +903,7 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
                     d.re_rrc[re0 + at] = sit | ((x >> 8) << 24) | ((uint32_t)r << 16) | ((x & 0xFF) << 8);
                     d.re_old[re0 + at] = 0;
                     d.re_new[re0 + at] = 0;
-                    if (!d.fuse_rec) d.re_moff[re0 + at] = lmo;  // (fused: the readers count, k_rec_moff)
+                    if (!d.fuse_rec) d.re_moff[re0 + at] = lmo;  // (fused: the readers count, k_counted_moff)
                     bytes += d.fuse_rec ? 24 : 28;
                     if (d.fuse_rec && per) fan(lmo);
                 }
@@ -1204,7 +1204,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     t_old[at] = s_eold[w][qq];
                     t_new[at] = s_enew[w][qq];
                     // unfused: the tile-local offset k_fanout expands the event at; fused, the run is
-                    // dense in event order and the readers count their way through it (k_rec_moff)
+                    // dense in event order and the readers count their way through it (k_counted_moff)
                     if (!d.fuse_rec) t_moff[at] = lmo;
                     if (d.fuse_rec && per && !skip_msg) {
                         // GetBroadCastObject (AOI:531-593) for the record event, into the tile's run
@@ -1861,26 +1861,41 @@ __global__ __launch_bounds__(kTPB) void k_compact_rec(const uint32_t* __restrict
         }
     }
 }
-// Record tiles k_records fanned out (no per-event message offsets stored): a tile's run holds its
-// events' recipients in event order, so an event's dense CSR offset is the tile's dense base (db)
-// plus the recipient counts (event_msgs, as k_records counted them) of the events before it.
-__global__ __launch_bounds__(kTPB) void k_rec_moff(Dev d, uint32_t* __restrict__ dst, const uint32_t* __restrict__ db) {
-    __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
+// Tiles whose fan-out k_tick (property tiles) or k_records (record tiles) wrote itself store no
+// per-event message offsets: a tile's run holds its events' recipients in event order, so an
+// event's dense CSR offset is the tile's dense base (db) plus the recipient counts (event_msgs of
+// the event's property / record flags for the entity's class, as the frame counted them) of the
+// events before it in its tile.  rec: the record tiles, else the property tiles.
+__global__ __launch_bounds__(kTPB) void k_counted_moff(Dev d, int rec, uint32_t* __restrict__ dst,
+                                                       const uint32_t* __restrict__ db) {
+    __shared__ uint8_t s_fl[NFK_MAX_CLASSES * kMaxProps];  // pflags, or rflags (NFK_MAX_RECORDS per class)
     __shared__ uint32_t s_w[kTPB / 64 + 1];
-    for (int i = threadIdx.x; i < (int)sizeof(s_rflags) / 4; i += kTPB)
-        ((uint32_t*)s_rflags)[i] = ((const uint32_t*)d.tab->rflags)[i];
+    const int fw = rec ? NFK_MAX_RECORDS : kMaxProps;  // flags per class
+    const uint8_t* fl = rec ? &d.tab->rflags[0][0] : &d.tab->pflags[0][0];
+    for (int i = threadIdx.x; i < NFK_MAX_CLASSES * fw; i += kTPB) s_fl[i] = fl[i];
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int t = blockIdx.x; t < d.n_rtiles; t += gridDim.x) {
-        const uint32_t b = d.re_base[t], n = d.re_base[t + 1] - b;
-        uint32_t carry = db[d.n_tiles + t];
+    const int nt = rec ? d.n_rtiles : d.n_tiles;
+    const uint32_t* base = rec ? d.re_base : d.ev_base;
+    const size_t tcap = (size_t)(rec ? d.re_tcap : d.ev_tcap);
+    for (int t = blockIdx.x; t < nt; t += gridDim.x) {
+        const uint32_t b = base[t], n = base[t + 1] - b;
+        uint32_t carry = db[(rec ? d.n_tiles : 0) + t];
         for (uint32_t c0 = 0; c0 < n; c0 += kTPB) {  // uniform
             const uint32_t i = c0 + threadIdx.x;
             uint32_t per = 0;
             if (i < n) {
-                const uint32_t x = d.re_rrc[(size_t)t * d.re_tcap + i];
-                const uint64_t desc = d.fan_desc[(uint32_t)t * (uint32_t)kRTile + (x >> kRrcSitShift)];
-                per = event_msgs(desc, s_rflags[desc >> 60][(x >> 16) & 0xFF]);
+                uint32_t slot, key;
+                if (rec) {
+                    const uint32_t x = d.re_rrc[(size_t)t * tcap + i];
+                    slot = (uint32_t)t * (uint32_t)kRTile + (x >> kRrcSitShift);
+                    key = (x >> 16) & 0xFF;
+                } else {
+                    slot = d.ev_slot[(size_t)t * tcap + i];
+                    key = d.ev_pid[(size_t)t * tcap + i];
+                }
+                const uint64_t desc = d.fan_desc[slot];
+                per = event_msgs(desc, s_fl[(uint32_t)(desc >> 60) * (uint32_t)fw + key]);
             }
             const uint32_t incl = wave_incl_scan_u32(per);
             if (lane == 63) s_w[w] = incl;

@@ -613,21 +613,9 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         const unsigned tev = (unsigned)((tot >> 32) & 0xFFFF);
         const bool fan = tmsg && tmsg <= d.msg_tcap;
         if (tmsg > d.msg_tcap && threadIdx.x == 0) dev_error(d, kErrFanBound);  // (host bound)
-        if (!fan) {  // ev_moff only
-            if (nsd) {
-                walk([&](unsigned at, unsigned m, uint32_t, int, int, EvFan) { st_off(t_evm, pev0 + at, mb + pmsg0 + m); });
-                bytes += 4 * nd;
-            } else if (dm) {
-#pragma unroll
-                for (int j = 0; j < kW; j++) {
-                    if (j >= S::n_w(d) || !((dm >> j) & 1)) continue;
-                    const uint32_t below = dm & S::u_lower(d, j);
-                    st_off_nt<(S::kNt & kNtEventStore) != 0>(t_evm, pev0 + __builtin_popcount(below),
-                           mb + pmsg0 + npub * __builtin_popcount(below & pubm) + __builtin_popcount(below & privm));
-                    bytes += 4;
-                }
-            }
-        } else {
+        // No per-event message offsets: the tile's run holds its events' recipients in event order
+        // (the readers count through it: k_counted_moff)
+        if (fan) {
             const unsigned R = (unsigned)d.lds_words;
             const uint32_t pb_lo = s_pb[0], npl = s_pb[1] > s_pb[0] ? s_pb[1] - s_pb[0] : 0u;
             const uint32_t nm = s_pb[2];
@@ -661,8 +649,6 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                             x[0] = pmsg0 + m;
                             x[1] = f.pub ? (uint32_t)desc : (uint32_t)e;
                             x[2] = f.n | (r1 << 14) | (f.pub ? 0x80000000u : 0u);
-                            st_off_nt<(S::kNt & kNtEventStore) != 0>(t_evm, a, mb + pmsg0 + m);
-                            bytes += 4;
                         });
                     } else {
 #pragma unroll 1
@@ -679,8 +665,6 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                             x[0] = m;
                             x[1] = pub ? (uint32_t)desc : (uint32_t)e;
                             x[2] = n | (r1 << 14) | (pub ? 0x80000000u : 0u);
-                            st_off_nt<(S::kNt & kNtEventStore) != 0>(t_evm, at, mb + m);
-                            bytes += 4;
                         }
                     }
                 }

@@ -375,7 +375,8 @@ def test_device_outputs_and_counters(gpu_available):
     # fan-out bytes are tallied by the kernel that writes them (k_tick when it fans out itself)
     assert s["alg_bytes_tick"] > 0 and s["alg_bytes_fan"] >= 0
     o = m.outputs()
-    assert all(o[k] for k in ("ev_slot", "ev_moff", "ev_base", "msg_base", "msg_rcpt", "slot_obj"))
+    assert all(o[k] for k in ("ev_slot", "ev_base", "msg_base", "msg_rcpt", "slot_obj"))
+    assert not o["ev_moff"]  # k_tick fanned its tiles out: no per-event message offsets (nfgpu.h)
     # slots = members + per-group slack (nfk_config.slack_per_256, default 16 per 256)
     assert s["n_entities"] == 5000 and 5000 <= o["n_tiles"] * 256 <= 5000 * 1.1 + 256 * 2
     # a tile's event capacity: its slots' program destinations (+ standalone SetProperty groups)

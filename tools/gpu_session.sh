@@ -39,6 +39,8 @@ for step in "$@"; do
                --entities 262144 --groups 1024 --migrate 128 --migrate-every 1 ;;
     adapter) run adapter 600 python -u -m pytest tests/test_adapter.py tests/test_logic_session.py -m gpu -v -p no:cacheprovider \
              --timeout 300 --timeout-method thread ;;
+    abtick) BENCH_ARGS="--other-configs off --plugin-frame off" run abtick 900 tools/ab.sh "$TAG/abtick" ${ABR:-3} $ABLIBS ;;
+    abfan) BENCH_ARGS="--config 3 --other-configs off --plugin-frame off" run abfan 900 tools/ab.sh "$TAG/abfan" ${ABR:-2} $ABLIBS ;;
     abrec) BENCH_ARGS="--config 4 --other-configs off --plugin-frame off" run abrec 900 tools/ab.sh "$TAG/abrec" ${ABR:-3} $ABLIBS ;;
     rectests) run rectests 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "record or rec or config4 or golden" ;;
     lbab) run lbab 900 tools/ab_env.sh "$TAG/lbab" ${LBR:-4} NFGPU_JIT_LB=1 NFGPU_JIT_LB=0 ;;
