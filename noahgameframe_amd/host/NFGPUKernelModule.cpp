@@ -1071,25 +1071,31 @@ bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
     return true;
 }
 
+// An event's old / new values as TData: built per event with each field written once and without a
+// branch on the type (resetting and rewriting two long-lived TData objects, and a branch that the
+// mixed int / float events of a frame mispredict, cost more than the callbacks); the object values
+// are the caller's
+static inline void TDataOf(TDATA_TYPE t, uint64_t vo, uint64_t vn, TData* a, TData* b) {
+    const uint64_t mi = 0 - (uint64_t)(t == TDATA_INT), mf = 0 - (uint64_t)(t == TDATA_FLOAT);
+    a->type = b->type = t;
+    a->i = (int64_t)(vo & mi);
+    b->i = (int64_t)(vn & mi);
+    a->f = dbl_of(vo & mf);
+    b->f = dbl_of(vn & mf);
+}
+
 void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_self, const NFGUID* re_self,
                                       const uint8_t* ev_same) {
     if (common_prop_cb_.empty() && aoi_prop_cb_.empty() && common_rec_cb_.empty() && aoi_rec_cb_.empty()) return;
     std::vector<NFGUID> rcpt;
     uint32_t rcpt_at = 0, rcpt_n = 0xFFFFFFFFu;  // the msg_rcpt run rcpt holds
     constexpr int64_t kPre = 16;  // events are in slot order; their objects' NFGUIDs are scattered
-    TData a, b;
     for (int64_t e = 0; e < f.n_ev; e++) {
         if (!ev_self && e + kPre < f.n_ev) __builtin_prefetch(&guids_[(size_t)f.ev_obj[e + kPre]]);
         const PropertyDef& pd = props_[def_of_pid_[f.ev_pid[e]]];
-        a = b = TData{};
-        a.type = b.type = pd.type;
-        if (pd.type == TDATA_INT) {
-            a.i = (int64_t)f.ev_old[e];
-            b.i = (int64_t)f.ev_new[e];
-        } else if (pd.type == TDATA_FLOAT) {
-            a.f = dbl_of(f.ev_old[e]);
-            b.f = dbl_of(f.ev_new[e]);
-        } else {
+        TData a, b;
+        TDataOf(pd.type, f.ev_old[e], f.ev_new[e], &a, &b);
+        if (pd.type == TDATA_OBJECT) {
             a.o = NFGUID((int64_t)f.ev_old_h[e], (int64_t)f.ev_old[e]);
             b.o = NFGUID((int64_t)f.ev_new_h[e], (int64_t)f.ev_new[e]);
         }
@@ -1110,26 +1116,22 @@ void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_
             for (auto& cb : aoi_prop_cb_) cb(self, pd.name, a, b, rcpt);
         }
     }
+    RECORD_EVENT_DATA ev;
+    int ev_r = -1;  // the record ev.strRecordName holds (a name copy per event would allocate)
     for (int64_t e = 0; e < f.n_re; e++) {
         const uint32_t rrc = f.re_rrc[e];
-        const int r = (rrc >> 16) & 0xFF, row = (rrc >> 8) & 0xFF, col = rrc & 0xFF, op = rrc >> 24;
-        RECORD_EVENT_DATA ev;
+        const int r = (rrc >> 16) & 0xFF, row = (rrc >> 8) & 0xFF, col = rrc & 0xFF, op = (rrc >> 24) & 3;
         // row events (AddRow / Remove / Clear) carry empty values, as NFCRecord raises them (RC:177, 1098)
         ev.nOpType = op == 1 ? RECORD_EVENT_DATA::Add : op == 2 ? RECORD_EVENT_DATA::Del
                    : op == 3 ? RECORD_EVENT_DATA::Cover : RECORD_EVENT_DATA::Update;
         ev.nRow = row;
         ev.nCol = col;
-        ev.strRecordName = records_[r].name;
-        TData a, b;
-        a.type = b.type = op ? TDATA_UNKNOWN : records_[r].cols[col];
-        if (op) {
-        } else if (a.type == TDATA_INT) {
-            a.i = (int64_t)f.re_old[e];
-            b.i = (int64_t)f.re_new[e];
-        } else {
-            a.f = dbl_of(f.re_old[e]);
-            b.f = dbl_of(f.re_new[e]);
+        if (r != ev_r) {
+            ev.strRecordName = records_[r].name;
+            ev_r = r;
         }
+        TData a, b;
+        TDataOf(op ? TDATA_UNKNOWN : records_[r].cols[col], f.re_old[e], f.re_new[e], &a, &b);
         const NFGUID& self = re_self ? re_self[e] : guids_[f.re_obj[e]];
         for (auto& cb : common_rec_cb_) cb(self, ev, a, b);
         if (f.msg_off && !aoi_rec_cb_.empty()) {
