@@ -35,6 +35,7 @@
 //   * String / Vector properties stay host-side (not on the frame path); object (NFGUID) properties
 //     are device columns like the int / float ones.
 #pragma once
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -111,9 +112,18 @@ private:
 };
 // A few persistent worker threads for data-parallel host loops that run no game code (gathers of
 // scattered reads into dense arrays): Run(n, fn) calls fn(0) .. fn(n-1) on the workers and the
-// calling thread and returns when every call has returned.
+// calling thread and returns when every call has returned; Start(n, fn) hands the calls to the
+// workers alone and returns at once (claimed in index order), Wait(job) returns when every call has
+// returned (the calling thread takes what is left).
 class WorkerPool {
 public:
+    // one job's calls: a worker holding a finished job finds no index left and never calls fn
+    struct Job {
+        std::function<void(int64_t)> own;  // (Start: the job keeps its function)
+        const std::function<void(int64_t)>* fn = nullptr;
+        int64_t n = 0;
+        std::atomic<int64_t> next{0}, done{0};
+    };
     explicit WorkerPool(int workers) {
         for (int i = 0; i < workers; i++) th_.emplace_back([this] { Loop(); });
     }
@@ -136,19 +146,31 @@ public:
             job_ = job;
         }
         cv_.notify_all();
+        Wait(job);
+    }
+    std::shared_ptr<Job> Start(int64_t n, std::function<void(int64_t)> fn) {
+        auto job = std::make_shared<Job>();
+        job->own = std::move(fn);
+        job->fn = &job->own;
+        job->n = std::max<int64_t>(n, 0);
+        if (n > 0) {
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                job_ = job;
+            }
+            cv_.notify_all();
+        }
+        return job;
+    }
+    void Wait(const std::shared_ptr<Job>& job) {
+        if (!job) return;
         Work(*job);
-        while (job->done.load(std::memory_order_acquire) < n) std::this_thread::yield();
+        while (job->done.load(std::memory_order_acquire) < job->n) std::this_thread::yield();
         std::lock_guard<std::mutex> lk(mu_);
         if (job_ == job) job_.reset();
     }
 
 private:
-    // one Run's calls: a worker holding a finished job finds no index left and never calls fn
-    struct Job {
-        const std::function<void(int64_t)>* fn = nullptr;
-        int64_t n = 0;
-        std::atomic<int64_t> next{0}, done{0};
-    };
     static void Work(Job& j) {
         int64_t i;
         while ((i = j.next.fetch_add(1, std::memory_order_relaxed)) < j.n) {
@@ -534,15 +556,23 @@ private:
     int FlushSets();
     int FlushScheduleCalls();
     // the functor walk's and the deliveries' scattered host reads (functor slot, NFGUID, interval
-    // per fired schedule; NFGUID per event) gathered into dense arrays by worker threads before
-    // any functor runs, so the calls themselves stream (NFGPU_PLUGIN_THREADS workers, default 8)
+    // per fired schedule; NFGUID per event) gathered into dense arrays by worker threads
+    // (NFGPU_PLUGIN_THREADS workers, default 8), so the calls themselves stream.  The gather runs
+    // beside the walk: the fired list in chunks ahead of it (fg_ready_), the events while it
+    // runs.  The workers read guids_, cb_slot_ and cb_time_: every write to those waits for the
+    // gather first (WaitGather), so a functor that creates objects or drops schedules sees no race.
     std::unique_ptr<nfgpu_detail::WorkerPool> pool_;
+    std::shared_ptr<nfgpu_detail::WorkerPool::Job> gather_job_;
+    std::unique_ptr<std::atomic<uint8_t>[]> fg_ready_;  // [fired chunk] gathered
+    size_t fg_ready_cap_ = 0;
     HVec<int32_t> fg_c_;
     HVec<NFGUID> fg_g_, ev_self_, re_self_;
     HVec<float> fg_t_;
     HVec<uint8_t> ev_same_;
     bool in_walk_ = false;  // (freed functor entries are not reused while the fired list is walked)
+    static constexpr int64_t kGatherChunk = 1 << 14;
     bool GatherFrame(const nfk_frame_host& fh, int64_t nfi);
+    void WaitGather();
     ModuleScheduler module_sched_;
     SceneShard* shard_ = nullptr;
     std::map<std::string, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> kind_cb_;  // arrivals' functors

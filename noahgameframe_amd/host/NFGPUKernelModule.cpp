@@ -24,6 +24,7 @@ NFGPUKernelModule::NFGPUKernelModule(int capacity, void* hip_stream)
 void NFGPUKernelModule::SetTimeSource(std::function<int64_t()> now_ms) { clock_ = now_ms ? now_ms : nf_get_time; }
 
 NFGPUKernelModule::~NFGPUKernelModule() {
+    WaitGather();
     pool_.reset();
     if (world_) nfk_destroy(world_);
 }
@@ -189,6 +190,7 @@ bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGrou
         check(nfk_spawn_objects(world_, 1, &self.nHead64, &self.nData64, &nSceneID, &nGroupID, &cl, &pl, row.data()),
               "nfk_spawn_objects");
         pending_calls_++;
+        WaitGather();  // (the gather's workers read guids_)
         obj_of_.insert(self.nHead64, self.nData64, (int)guids_.size());
         guids_.push_back(self);
         scene_.push_back(nSceneID);
@@ -200,6 +202,7 @@ bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGrou
     if (obj_of_.count(self.nHead64, self.nData64)) return false;       // "The object has Exists" (KM:131)
     auto c = class_id_.find(cls);
     if (c == class_id_.end()) return false;
+    WaitGather();  // (the gather's workers read guids_)
     int o = (int)guids_.size();
     guids_.push_back(self);
     obj_of_.insert(self.nHead64, self.nData64, o);
@@ -793,6 +796,7 @@ void NFGPUKernelModule::SetKindFunctor(const std::string& name, const OBJECT_SCH
 // schedules with the functors of their names.  sync: gather the tickets now (MigrateNow); else the
 // rows of the gather the previous Execute started (SceneShard::BeginFrame)
 void NFGPUKernelModule::MigrateShard(bool sync) {
+    WaitGather();  // (the gather's workers read guids_)
     Flush();  // (the buffered Set calls first: call order)
     std::vector<Ticket> sent, recv;
     if (sync) check(shard_->Migrate(&sent, &recv), "SceneShard::Migrate");
@@ -831,23 +835,37 @@ bool NFGPUKernelModule::Execute() {
     // schedules in name order (SM:52-80), sorted on the device — and the event lists
     const uint32_t what = ReadMask(true);
     nfk_frame_host fh{};
+    // (the gather reads fh: it is waited for before fh goes, however Execute leaves)
+    struct GatherGuard {
+        NFGPUKernelModule* m;
+        ~GatherGuard() { m->WaitGather(); }
+    } gather_guard{this};
     if (what) check(nfk_read_frame(world_, what, &fh), "nfk_read_frame");
     stats_.events_read = ms_since(t1);
     t1 = std::chrono::steady_clock::now();
     // heartbeat functors with the reference's arguments, objects in NFGUID order (the fired list's)
     const int64_t nfi = n_cb_ ? fh.n_fi : 0;  // (a frame consumer may read the list without functors)
     const bool gathered = GatherFrame(fh, nfi);
-    stats_.gather = ms_since(t1);
+    double gather_ms = ms_since(t1);
     in_walk_ = true;
     if (gathered) {
-        // the functor entries, NFGUIDs and intervals are dense arrays now: only the functor objects
-        // themselves are scattered (prefetched ahead)
+        // the functor entries, NFGUIDs and intervals are dense arrays, gathered chunk by chunk
+        // ahead of the walk: only the functor objects themselves are scattered (prefetched ahead)
         constexpr int64_t kPre = 16;
-        for (int64_t i = 0; i < nfi; i++) {
-            if (i + kPre < nfi && fg_c_[(size_t)(i + kPre)] >= 0) __builtin_prefetch(&cb_pool_[(size_t)fg_c_[(size_t)(i + kPre)]]);
-            const int32_t c = fg_c_[(size_t)i];
-            // (empty: a functor earlier in this walk destroyed the object or moved it to another shard)
-            if (c >= 0 && cb_pool_[(size_t)c]) cb_pool_[(size_t)c](fg_g_[(size_t)i], heartbeats_[(size_t)fh.fi_kind[i]].name, fg_t_[(size_t)i], fh.fi_remain[i]);
+        for (int64_t i0 = 0, k = 0; i0 < nfi; i0 += kGatherChunk, k++) {
+            if (!fg_ready_[(size_t)k].load(std::memory_order_acquire)) {
+                const auto tw = std::chrono::steady_clock::now();
+                // (a functor that wrote guids_ / cb_slot_ / cb_time_ waited for the whole gather)
+                while (gather_job_ && !fg_ready_[(size_t)k].load(std::memory_order_acquire)) std::this_thread::yield();
+                gather_ms += ms_since(tw);
+            }
+            const int64_t i1 = std::min(nfi, i0 + kGatherChunk);
+            for (int64_t i = i0; i < i1; i++) {
+                if (i + kPre < i1 && fg_c_[(size_t)(i + kPre)] >= 0) __builtin_prefetch(&cb_pool_[(size_t)fg_c_[(size_t)(i + kPre)]]);
+                const int32_t c = fg_c_[(size_t)i];
+                // (empty: a functor earlier in this walk destroyed the object or moved it to another shard)
+                if (c >= 0 && cb_pool_[(size_t)c]) cb_pool_[(size_t)c](fg_g_[(size_t)i], heartbeats_[(size_t)fh.fi_kind[i]].name, fg_t_[(size_t)i], fh.fi_remain[i]);
+            }
         }
     } else {
         // (a small frame, or no workers) its (object, kind) functor slots, pooled functors and NFGUIDs
@@ -877,7 +895,13 @@ bool NFGPUKernelModule::Execute() {
         }
     }
     in_walk_ = false;
-    stats_.functors = ms_since(t1);
+    {
+        const auto tw = std::chrono::steady_clock::now();
+        WaitGather();  // the events' part, gathered while the walk ran
+        gather_ms += ms_since(tw);
+    }
+    stats_.functors = ms_since(t1) - gather_ms;
+    stats_.gather = gather_ms;
     t1 = std::chrono::steady_clock::now();
     if (what & NFK_READ_EVENTS)
         DeliverEvents(fh, gathered && !ev_self_.empty() ? ev_self_.data() : nullptr,
@@ -914,6 +938,7 @@ bool NFGPUKernelModule::Execute() {
 }
 
 void NFGPUKernelModule::SetFunctor(int o, int k, const OBJECT_SCHEDULE_FUNCTOR& f, float t) {
+    WaitGather();  // (the gather's workers read cb_slot_ and cb_time_)
     const size_t nk = heartbeats_.size(), at = (size_t)o * nk + k;
     if (cb_slot_.size() < guids_.size() * nk) cb_slot_.resize(guids_.size() * nk + nk * 1024, -1);
     int32_t c = cb_slot_[at];
@@ -943,6 +968,7 @@ void NFGPUKernelModule::SetFunctor(int o, int k, const OBJECT_SCHEDULE_FUNCTOR& 
 }
 
 void NFGPUKernelModule::DropFunctors(int o) {
+    WaitGather();  // (the gather's workers read cb_slot_)
     const size_t nk = heartbeats_.size();
     for (size_t k = 0; k < nk; k++) {
         const size_t at = (size_t)o * nk + k;
@@ -993,10 +1019,19 @@ void NFGPUKernelModule::TakeAddedSchedules() {
     sched_add_.clear();
 }
 
-// Before any functor of the frame runs (so no game code changes the tables under the workers):
-// the fired list's functor entries, NFGUIDs and intervals, and the events' NFGUIDs, gathered in
-// chunks by the worker pool.  False for a frame too small to pay for it, or with no workers.
+void NFGPUKernelModule::WaitGather() {
+    if (!gather_job_) return;
+    pool_->Wait(gather_job_);
+    gather_job_.reset();
+}
+
+// Started before any functor of the frame runs: the fired list's functor entries, NFGUIDs and
+// intervals, and the events' NFGUIDs, gathered in chunks by the worker pool while the walk runs —
+// the fired chunks first, in order, each flagged in fg_ready_ when done (the walk waits for its
+// chunk), then the events.  No game code writes what the workers read while they run (WaitGather
+// before every such write).  False for a frame too small to pay for it, or with no workers.
 bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
+    WaitGather();
     const bool ev = !(common_prop_cb_.empty() && aoi_prop_cb_.empty() && common_rec_cb_.empty() && aoi_rec_cb_.empty());
     const int64_t nev = ev ? fh.n_ev : 0, nre = ev ? fh.n_re : 0;
     ev_self_.clear();
@@ -1019,10 +1054,18 @@ bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
     static const bool same_on = !(getenv("NFGPU_PLUGIN_SAME") && getenv("NFGPU_PLUGIN_SAME")[0] == '0');
     const bool runs = same_on && fh.msg_off && !aoi_prop_cb_.empty();
     ev_same_.resize(runs ? (size_t)nev : 0);
-    constexpr int64_t kChunk = 1 << 14, kPre = 16;
+    constexpr int64_t kChunk = kGatherChunk, kPre = 16;
     const int64_t cf = (nfi + kChunk - 1) / kChunk, ce = (nev + kChunk - 1) / kChunk, cr = (nre + kChunk - 1) / kChunk;
     const size_t nk = heartbeats_.size(), nslot = cb_slot_.size();
-    pool_->Run(cf + ce + cr, [&](int64_t q) {
+    if ((size_t)cf > fg_ready_cap_) {
+        fg_ready_cap_ = (size_t)cf + (size_t)cf / 4 + 16;
+        fg_ready_.reset(new std::atomic<uint8_t>[fg_ready_cap_]);
+    }
+    for (int64_t k = 0; k < cf; k++) fg_ready_[(size_t)k].store(0, std::memory_order_relaxed);
+    // (fh lives until Execute returns; Execute waits for the job before it does)
+    const nfk_frame_host* fp = &fh;
+    gather_job_ = pool_->Start(cf + ce + cr, [this, fp, nfi, nev, nre, cf, ce, nk, nslot, runs](int64_t q) {
+        const nfk_frame_host& fh = *fp;
         if (q < cf) {
             const int64_t i0 = q * kChunk, i1 = std::min(nfi, i0 + kChunk);
             for (int64_t i = i0; i < i1; i++) {
@@ -1037,6 +1080,7 @@ bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
                 fg_g_[(size_t)i] = guids_[(size_t)fh.fi_obj[i]];
                 fg_t_[(size_t)i] = c >= 0 ? cb_time_[(size_t)c] : 0.f;
             }
+            fg_ready_[(size_t)q].store(1, std::memory_order_release);
         } else if (q < cf + ce) {
             const int64_t i0 = (q - cf) * kChunk, i1 = std::min(nev, i0 + kChunk);
             for (int64_t i = i0; i < i1; i++) {
@@ -1146,6 +1190,7 @@ void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_
 bool NFGPUKernelModule::BeforeShut() { return true; }
 
 bool NFGPUKernelModule::Shut() {
+    WaitGather();
     if (world_) nfk_destroy(world_);
     world_ = nullptr;
     return true;
