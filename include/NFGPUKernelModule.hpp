@@ -577,6 +577,21 @@ private:
     SceneShard* shard_ = nullptr;
     std::map<std::string, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> kind_cb_;  // arrivals' functors
     void MigrateShard(bool sync);
+    // cross-shard SwitchScene of an entity whose membership changed in this window (spawned, or
+    // switched within the shard): deferred until the frame has applied that change (an export of
+    // it would be refused, and every rank would fail the exchange)
+    struct DeferredSwitch {
+        NFGUID self;
+        int scene, group;
+        float x, y, z;
+    };
+    std::vector<DeferredSwitch> deferred_;
+    std::vector<uint8_t> moved_flag_;  // [object] membership changed in this window (with a shard)
+    std::vector<int> moved_;
+    void MarkMoved(int o);
+    void DropDeferred(const NFGUID& self);
+    void Depart(int o, const NFGUID& self, int scene, int group, float x, float y, float z);
+    void WindowApplied();
     std::function<int64_t()> clock_;
     nfk_summary summary_{};
     FrameStats stats_{};

@@ -197,6 +197,7 @@ bool NFGPUKernelModule::CreateObject(const NFGUID& self, int nSceneID, int nGrou
         group_.push_back(nGroupID);
         cls_.push_back(cl);
         isplayer_.push_back(pl);
+        MarkMoved((int)guids_.size() - 1);
         return true;
     }
     if (obj_of_.count(self.nHead64, self.nData64)) return false;       // "The object has Exists" (KM:131)
@@ -334,28 +335,69 @@ bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int 
     if (!committed_ || ObjectIndex(self) < 0) return false;  // "There is no object" (KM:948)
     if (shard_ && !shard_->Owns(nTargetSceneID)) {          // into another shard's scene
         const int o = ObjectIndex(self);
-        shard_->QueueSwitch(self.nHead64, self.nData64, cls_[o], isplayer_[o], nTargetSceneID, nTargetGroupID, fX, fY,
-                            fZ);
-        obj_of_.erase(self.nHead64, self.nData64);  // this module's no more (its index stays reserved)
-        departed_.insert(self.nHead64, self.nData64, o);
-        DropFunctors(o);
-        DropPendingAdds(self);
+        // an entity spawned or switched in this window has no row to export until the frame applies
+        // that: its departure is deferred to the end of the next Execute's device frame
+        if ((size_t)o < moved_flag_.size() && moved_flag_[(size_t)o]) {
+            deferred_.push_back({self, nTargetSceneID, nTargetGroupID, fX, fY, fZ});
+            return true;
+        }
+        Depart(o, self, nTargetSceneID, nTargetGroupID, fX, fY, fZ);
         return true;
     }
     if (!scenes_.count(nTargetSceneID)) return false;       // "no this container" (KM:917)
+    DropDeferred(self);  // (a later switch within the shard supersedes a deferred departure)
     check(nfk_switch_scene(world_, self.nHead64, self.nData64, nTargetSceneID, nTargetGroupID, fX, fY, fZ),
           "nfk_switch_scene");
     pending_calls_++;
     const int o = ObjectIndex(self);
     scene_[o] = nTargetSceneID;
     group_[o] = nTargetGroupID;
+    MarkMoved(o);
     return true;
+}
+
+void NFGPUKernelModule::Depart(int o, const NFGUID& self, int scene, int group, float x, float y, float z) {
+    shard_->QueueSwitch(self.nHead64, self.nData64, cls_[o], isplayer_[o], scene, group, x, y, z);
+    obj_of_.erase(self.nHead64, self.nData64);  // this module's no more (its index stays reserved)
+    departed_.insert(self.nHead64, self.nData64, o);
+    DropFunctors(o);
+    DropPendingAdds(self);
+}
+
+void NFGPUKernelModule::DropDeferred(const NFGUID& self) {
+    for (size_t i = 0; i < deferred_.size();)
+        if (deferred_[i].self == self) deferred_.erase(deferred_.begin() + (std::ptrdiff_t)i);
+        else i++;
+}
+
+void NFGPUKernelModule::MarkMoved(int o) {
+    if (!shard_) return;
+    if (moved_flag_.size() <= (size_t)o) moved_flag_.resize((size_t)o + 1 + moved_flag_.size() / 2, 0);
+    if (!moved_flag_[(size_t)o]) {
+        moved_flag_[(size_t)o] = 1;
+        moved_.push_back(o);
+    }
+}
+
+// after the device frame applied the window's membership changes: nothing has moved in the new
+// window yet, and the departures deferred in the last one leave now (still objects of this module
+// unless the game destroyed or departed them since)
+void NFGPUKernelModule::WindowApplied() {
+    for (int o : moved_) moved_flag_[(size_t)o] = 0;
+    moved_.clear();
+    std::vector<DeferredSwitch> dv;
+    dv.swap(deferred_);
+    for (const DeferredSwitch& q : dv) {
+        const int o = ObjectIndex(q.self);
+        if (o >= 0) Depart(o, q.self, q.scene, q.group, q.x, q.y, q.z);
+    }
 }
 
 bool NFGPUKernelModule::DestroyObject(const NFGUID& self) {
     Flush();  // (the buffered Set calls first: call order)
     const int o = ObjectIndex(self);
     if (!committed_ || o < 0) return false;
+    DropDeferred(self);
     check(nfk_destroy_objects(world_, 1, &self.nHead64, &self.nData64), "nfk_destroy_objects");
     pending_calls_++;
     obj_of_.erase(self.nHead64, self.nData64);  // its object index stays reserved; later calls find no object
@@ -826,6 +868,7 @@ bool NFGPUKernelModule::Execute() {
     Flush();
     check(nfk_execute(world_, clock_()), "nfk_execute");
     pending_calls_ = 0;
+    if (shard_) WindowApplied();
     check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
     stats_.device = ms_since(t0);
     auto t1 = std::chrono::steady_clock::now();

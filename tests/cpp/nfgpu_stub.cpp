@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <mutex>
 #include <string>
 #include <utility>
@@ -30,6 +31,9 @@ struct Stub {
     std::vector<std::pair<int64_t, int64_t>> guid;           // [object] (head, data)
     bool committed = false;
     int n_loaded = 0;
+    // objects spawned or switched in this window: the library refuses to export them until
+    // nfk_execute has applied that (nfgpu_host.hip nfk_export_objects), and so does the stub
+    std::set<std::pair<int64_t, int64_t>> moved;
 };
 FILE* g_log = nullptr;
 const char* g_err = "";
@@ -157,7 +161,9 @@ int nfk_set_scene_props(void* w, int32_t a, int32_t b, int32_t x, int32_t y, int
 }
 int nfk_switch_scene(void* w, int64_t h, int64_t d, int32_t sc, int32_t gr, float, float, float) {
     logf("switch %lld %lld %d %d", (long long)h, (long long)d, sc, gr);
-    return find(S(w), h, d) < 0 ? NFK_ERR_NOTFOUND : NFK_OK;
+    if (find(S(w), h, d) < 0) return NFK_ERR_NOTFOUND;
+    S(w)->moved.insert({h, d});
+    return NFK_OK;
 }
 int nfk_destroy_objects(void* w, int32_t n, const int64_t* gh, const int64_t* gd) {
     for (int i = 0; i < n; i++) {
@@ -178,8 +184,13 @@ int nfk_row_words(void* w, int32_t* n) {
 // rows = the stored property words (host memory stands for device memory here)
 int nfk_export_objects(void* w, int32_t n, const int64_t* gh, const int64_t* gd, uint64_t* rows) {
     Stub* s = S(w);
-    for (int i = 0; i < n; i++)
+    for (int i = 0; i < n; i++) {
         if (find(s, gh[i], gd[i]) < 0) return NFK_ERR_NOTFOUND;
+        if (s->moved.count({gh[i], gd[i]})) {
+            g_err = "export of an object whose membership already changed in this window";
+            return NFK_ERR_STATE;
+        }
+    }
     for (int i = 0; i < n; i++) {
         const int o = find(s, gh[i], gd[i]);
         memcpy(rows + (size_t)i * s->nw, s->words[o].data(), (size_t)s->nw * 8);
@@ -204,6 +215,7 @@ int nfk_spawn_objects(void* w, int32_t n, const int64_t* gh, const int64_t* gd, 
     Stub* s = S(w);
     for (int i = 0; i < n; i++) {
         const int o = add_object(s, gh[i], gd[i]);
+        s->moved.insert({gh[i], gd[i]});
         memcpy(s->words[o].data(), props + (size_t)i * s->nw, s->nw * 8);
         std::string t;
         for (int k = 0; k < s->nw; k++) t += " " + std::to_string(props[(size_t)i * s->nw + k]);
@@ -383,6 +395,7 @@ int nfk_read_added(void*, int32_t, int32_t* n, int64_t*, int64_t*, int32_t*) {
 }
 int nfk_execute(void* w, int64_t now) {
     logf("execute %lld", (long long)now);
+    S(w)->moved.clear();
     return NFK_OK;
 }
 int nfk_execute_calls(void* w) {

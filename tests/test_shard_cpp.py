@@ -16,7 +16,7 @@ STUB = os.path.join(ROOT, "tests", "cpp", "_stub")
 
 
 def _build():
-    if not (os.path.exists(EXE) and os.path.exists(os.path.join(STUB, "libnfgpu.so"))):
+    if not (os.path.exists(EXE) and os.path.exists(DEFER) and os.path.exists(os.path.join(STUB, "libnfgpu.so"))):
         import __graft_entry__
         __graft_entry__.build_plugin()
 
@@ -47,6 +47,36 @@ def test_shard_protocol_host_stub(tmp_path):
     for (h, d), w in by.items():
         assert [p for p, _ in w] == [1, 0, 3, 4, 5, 1], (d, w)
         assert w[0][1] == 0 and w[-1][1] == (9 if d % 100 == 1 else 5 + d % 100)
+
+
+DEFER = os.path.join(ROOT, "tests", "cpp", "_bin", "shard_defer")
+
+
+def test_plugin_defers_cross_shard_switch_of_moved_entity(tmp_path):
+    """A cross-shard SwitchScene of an entity spawned or switched within its shard in the same window
+    is deferred until the frame applied that change (the export would be refused and every rank's
+    exchange would fail, losing the entity); a settled entity leaves at once.  Stub worlds, whose
+    export refuses such an entity as the library's does (tests/cpp/shard_defer.cpp)."""
+    _build()
+    env = dict(os.environ, NFGPU_STUB_LOG=str(tmp_path / "stub.log"),
+               LD_LIBRARY_PATH=STUB + ":" + os.environ.get("LD_LIBRARY_PATH", ""))
+    r = subprocess.run([DEFER, "host"], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr + r.stdout
+    lines = [ln.split() for ln in open(tmp_path / "stub.log")]
+    ev = [(x[0], int(x[2]) if x[0] == "export" else 0) for x in lines
+          if x[0] == "execute" or (x[0] == "export" and int(x[1]) == 9)]
+    exports = [i for i, x in enumerate(ev) if x[0] == "export"]
+    # G at MigrateNow (before the window's frame); E and F only after a frame applied their change
+    assert [ev[i][1] for i in exports] == [2, 500, 1]
+    assert any(x[0] == "execute" for x in ev[exports[0]:exports[1]])
+
+
+@pytest.mark.gpu
+def test_plugin_defers_cross_shard_switch_device(gpu_available):
+    _build()
+    r = subprocess.run([DEFER, "device"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "ok" in r.stdout
 
 
 @pytest.mark.gpu
