@@ -43,6 +43,7 @@ for step in "$@"; do
     abfan) BENCH_ARGS="--config 3 --other-configs off --plugin-frame off" run abfan 900 tools/ab.sh "$TAG/abfan" ${ABR:-2} $ABLIBS ;;
     abrec) BENCH_ARGS="--config 4 --other-configs off --plugin-frame off" run abrec 900 tools/ab.sh "$TAG/abrec" ${ABR:-3} $ABLIBS ;;
     rectests) run rectests 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "record or rec or config4 or golden" ;;
+    pfab) BENCH_ARGS="--other-configs off ${PFB:-}" run pfab 900 tools/ab_env.sh "$TAG/pfab" ${PFR:-3} ${PFAB:-NFGPU_TICK_PF=0 NFGPU_TICK_PF=1536 NFGPU_TICK_PF=768 NFGPU_TICK_PF=3072} ;;
     lbab) run lbab 900 tools/ab_env.sh "$TAG/lbab" ${LBR:-4} NFGPU_JIT_LB=1 NFGPU_JIT_LB=0 ;;
     bench2) NFGPU_BENCH_TRACE=1 run bench2 600 python bench.py --gpus 2 --steps 20 --warmup 3 --backend gloo \
                --cpu-baseline off --entities 262144 --groups 1024 --migrate 128 ;;
