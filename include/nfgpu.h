@@ -58,6 +58,8 @@ extern "C" {
  *   FAFFINE     dst(f64) = dst * f64(a) + f64(b)
  *   RIADD_CLAMP record cell(int) = clamp(cell + a, b, c) for every used row
  *   RFAFFINE    record cell(f64) = cell * f64(a) + f64(b) for every used row
+ *   ISET        dst(int) = A                                  A imm or prop (NFK_A_PROP)
+ *   FSET        dst(f64) = A                                  A f64(a) or f64 prop (NFK_A_PROP)
  * clamp(v, lo, hi): v < lo -> lo; then v > hi -> hi.  Integer adds wrap.
  * Record ops: dst = (rec << 8) | col. */
 enum {
@@ -66,7 +68,9 @@ enum {
     NFK_OP_FLERP = 2,
     NFK_OP_FAFFINE = 3,
     NFK_OP_RIADD_CLAMP = 4,
-    NFK_OP_RFAFFINE = 5
+    NFK_OP_RFAFFINE = 5,
+    NFK_OP_ISET = 6,
+    NFK_OP_FSET = 7
 };
 #define NFK_A_PROP 1
 #define NFK_LO_PROP 2

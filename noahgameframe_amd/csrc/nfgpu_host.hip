@@ -880,6 +880,12 @@ int grow_rec_tiles(World* w, int64_t per_tile) {
     return NFK_OK;
 }
 
+// the property ops (a program's Get + Set on a property column; record ops run in k_records)
+static bool prop_op(int code) {
+    return code == NFK_OP_IADD_CLAMP || code == NFK_OP_FLERP || code == NFK_OP_FAFFINE || code == NFK_OP_ISET ||
+           code == NFK_OP_FSET;
+}
+
 bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>& rp) {
     bool u_ok = false;
     {
@@ -887,8 +893,7 @@ bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>&
         for (int k = 0; k < NK; k++)
             for (int i = 0; i < tab.nops[k]; i++) {
                 const nfk_op& op = tab.ops[k][i];
-                if (op.code == NFK_OP_IADD_CLAMP || op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE)
-                    W.push_back(op.dst);
+                if (prop_op(op.code)) W.push_back(op.dst);
             }
         std::sort(W.begin(), W.end());
         W.erase(std::unique(W.begin(), W.end()), W.end());
@@ -901,6 +906,8 @@ bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>&
                     if ((op.flags & NFK_LO_PROP) && !is_w(op.b)) R.push_back((int)op.b);
                     if ((op.flags & NFK_HI_PROP) && !is_w(op.c)) R.push_back((int)op.c);
                 } else if (op.code == NFK_OP_FLERP && !is_w(op.a)) {
+                    R.push_back((int)op.a);
+                } else if ((op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) && (op.flags & NFK_A_PROP) && !is_w(op.a)) {
                     R.push_back((int)op.a);
                 }
             }
@@ -933,6 +940,9 @@ bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>&
                     u[1] = slot(op.a);
                 } else if (op.code == NFK_OP_FAFFINE) {
                     u[0] = slot(op.dst);
+                } else if (op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) {
+                    u[0] = slot(op.dst);
+                    if (op.flags & NFK_A_PROP) u[1] = slot(op.a);
                 }
                 for (int q = 0; q < 4; q++)  // writable bits | read-only bits << 16
                     if (u[q] != kNoU) tab.umask[k] |= (u[q] & 0x80) ? 1u << (16 + (u[q] & 0x7F)) : 1u << u[q];
@@ -1755,6 +1765,14 @@ int nfk_define_kind(void* world, int32_t kind, const nfk_op* ops, int32_t n_ops)
         case NFK_OP_FAFFINE:
             if (!isflt(op.dst)) return fail(NFK_ERR_ARG, "FAFFINE dst must be a float property");
             break;
+        case NFK_OP_ISET:
+            if (!isint(op.dst) || ((op.flags & NFK_A_PROP) && !isint(op.a)))
+                return fail(NFK_ERR_ARG, "ISET operands must be int properties");
+            break;
+        case NFK_OP_FSET:
+            if (!isflt(op.dst) || ((op.flags & NFK_A_PROP) && !isflt(op.a)))
+                return fail(NFK_ERR_ARG, "FSET operands must be float properties");
+            break;
         case NFK_OP_RIADD_CLAMP:
         case NFK_OP_RFAFFINE: {
             int r = op.dst >> 8, col = op.dst & 255;
@@ -1846,7 +1864,7 @@ int nfk_commit(void* world) {
                 RecOp ro{k, op.dst >> 8, op.dst & 255, op.code, op.a, op.b, op.c};
                 w->tab.recops[nro++] = ro;
                 w->tab.kind_has_recop |= 1u << k;
-            } else if (op.code == NFK_OP_IADD_CLAMP || op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE) {
+            } else if (prop_op(op.code)) {
                 w->dst_union_mask[op.dst >> 6] |= 1ull << (op.dst & 63);
             }
         }
@@ -1893,6 +1911,9 @@ int nfk_commit(void* world) {
                     add((int)op.a, 0);
                 } else if (op.code == NFK_OP_FAFFINE) {
                     add(op.dst, 1);
+                } else if (op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) {
+                    add(op.dst, 1);
+                    if (op.flags & NFK_A_PROP) add((int)op.a, 0);
                 }
             }
         std::map<std::vector<int>, int> gi;
@@ -1928,6 +1949,9 @@ int nfk_commit(void* world) {
                     ps.push_back((int)op.a);
                 } else if (op.code == NFK_OP_FAFFINE) {
                     ps.push_back(op.dst);
+                } else if (op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) {
+                    ps.push_back(op.dst);
+                    if (op.flags & NFK_A_PROP) ps.push_back((int)op.a);
                 }
             }
             for (size_t i = 1; i < ps.size(); i++) {

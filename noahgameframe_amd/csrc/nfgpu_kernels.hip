@@ -470,13 +470,15 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
     for (int i = 0; i < NFK_MAX_OPS; i++) {
         if (i >= n) break;
         const nfk_op op = tab->ops[k][i];
-        if (op.code != NFK_OP_IADD_CLAMP && op.code != NFK_OP_FLERP && op.code != NFK_OP_FAFFINE) continue;
+        if (op.code != NFK_OP_IADD_CLAMP && op.code != NFK_OP_FLERP && op.code != NFK_OP_FAFFINE &&
+            op.code != NFK_OP_ISET && op.code != NFK_OP_FSET)
+            continue;
         const uint32_t p0 = op.dst;
         const bool isf = op.code != NFK_OP_IADD_CLAMP;
         (void)isf;
         pre[i][0] = *prop_ptr(*en.dv, p0, en.e);
         en.bytes += 8;
-        if (op.code == NFK_OP_FLERP) {
+        if (op.code == NFK_OP_FLERP || ((op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) && (op.flags & NFK_A_PROP))) {
             pre[i][1] = *prop_ptr(*en.dv, (uint32_t)op.a, en.e);
             en.bytes += 8;
         } else if (op.code == NFK_OP_IADD_CLAMP) {
@@ -514,6 +516,14 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
             }
             if (!(fabs(v - x) <= 1e-15))  // NFCProperty::SetFloat (PR:314): IsZeroDouble(v - cur)
                 en.tput(op.dst, (uint64_t)__double_as_longlong(x), (uint64_t)__double_as_longlong(v));
+        } else if (op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) {
+            uint64_t t;
+            const uint64_t cur = en.tget(op.dst, t) ? t : pre[i][0];
+            const uint64_t r = (op.flags & NFK_A_PROP) ? (en.tget((uint32_t)op.a, t) ? t : pre[i][1]) : (uint64_t)op.a;
+            const bool set = op.code == NFK_OP_ISET
+                                 ? r != cur  // NFCProperty::SetInt (PR:273)
+                                 : !(fabs(__longlong_as_double((long long)r) - __longlong_as_double((long long)cur)) <= 1e-15);
+            if (set) en.tput(op.dst, cur, r);
         }
         // record ops run in k_records
     }

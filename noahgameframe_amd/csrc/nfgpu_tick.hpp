@@ -104,6 +104,18 @@ __device__ __forceinline__ void run_programs_u(uint64_t (&v)[kU], uint32_t& wm, 
                 const bool set = !(fabs(r - x) <= 1e-15);  // NFCProperty::SetFloat (PR:314): IsZeroDouble(v - cur)
                 uput(v, u0, set ? (uint64_t)__double_as_longlong(r) : xb);
                 wm |= set ? (1u << u0) : 0u;
+            } else if (code == NFK_OP_ISET) {
+                const uint64_t cur = uget(v, u0);
+                const uint64_t r = (flags & NFK_A_PROP) ? uget(v, u1) : (uint64_t)tab->opx[k][i].a;
+                uput(v, u0, r);  // NFCProperty::SetInt (PR:273): r == cur changes nothing
+                wm |= (r != cur) ? (1u << u0) : 0u;
+            } else if (code == NFK_OP_FSET) {
+                const uint64_t xb = uget(v, u0);
+                const uint64_t rb = (flags & NFK_A_PROP) ? uget(v, u1) : (uint64_t)tab->opx[k][i].a;
+                const double x = __longlong_as_double((long long)xb), r = __longlong_as_double((long long)rb);
+                const bool set = !(fabs(r - x) <= 1e-15);  // NFCProperty::SetFloat (PR:314)
+                uput(v, u0, set ? rb : xb);
+                wm |= set ? (1u << u0) : 0u;
             }
             // record ops run in k_records
         }

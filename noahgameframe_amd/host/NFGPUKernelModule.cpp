@@ -106,6 +106,11 @@ static void resolve_program(std::vector<nfk_op>& ops, const std::vector<std::str
             case NFK_OP_FAFFINE:
                 op.dst = (uint16_t)P(op.dst);
                 break;
+            case NFK_OP_ISET:
+            case NFK_OP_FSET:
+                op.dst = (uint16_t)P(op.dst);
+                if (op.flags & NFK_A_PROP) op.a = P(op.a);
+                break;
             case NFK_OP_RIADD_CLAMP:
             case NFK_OP_RFAFFINE: {
                 const size_t r = op.dst >> 8;

@@ -38,7 +38,7 @@ assert KINDS == sorted(KINDS)
 KID = {n: i for i, n in enumerate(KINDS)}
 
 # op codes / flags (include/nfgpu.h)
-OP_IADD_CLAMP, OP_FLERP, OP_FAFFINE, OP_RIADD_CLAMP, OP_RFAFFINE = 1, 2, 3, 4, 5
+OP_IADD_CLAMP, OP_FLERP, OP_FAFFINE, OP_RIADD_CLAMP, OP_RFAFFINE, OP_ISET, OP_FSET = 1, 2, 3, 4, 5, 6, 7
 A_PROP, LO_PROP, HI_PROP = 1, 2, 4
 MAX_OPS = 4
 MAX_REC_COLS = 16
@@ -77,7 +77,7 @@ def _prop_flags(n_oprops=0):
     return f
 
 
-def programs(with_records, rec_float_op=True, rec_skill_op=False):
+def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False):
     ops = np.zeros((len(KINDS), MAX_OPS), OP_DTYPE)
     n_ops = np.zeros(len(KINDS), np.int32)
 
@@ -93,6 +93,19 @@ def programs(with_records, rec_float_op=True, rec_skill_op=False):
     put("Patrol", [(OP_FAFFINE, 0, PID["TargetX"], 0, f64bits(-1.0), f64bits(0.0), 0),
                    (OP_FAFFINE, 0, PID["TargetY"], 0, f64bits(-1.0), f64bits(0.0), 0)])
     put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 1, PID["MAXHP"])])
+    if set_ops:
+        # plain assignments a functor makes (SetPropertyInt / SetPropertyFloat with a constant or
+        # another property's value): first Sets change the value, repeated ones raise no event
+        put("MPRegen", [(OP_IADD_CLAMP, A_PROP | HI_PROP, PID["MP"], 0, PID["MPREGEN"], 0, PID["MAXMP"]),
+                        (OP_ISET, A_PROP, PID["EXP"], 0, PID["Level"], 0, 0)])
+        put("Move", [(OP_FLERP, 0, PID["X"], 0, PID["TargetX"], f64bits(0.125), 0),
+                     (OP_FLERP, 0, PID["Y"], 0, PID["TargetY"], f64bits(0.125), 0),
+                     (OP_FSET, A_PROP, PID["Z"], 0, PID["TargetX"], 0, 0)])
+        put("Patrol", [(OP_FAFFINE, 0, PID["TargetX"], 0, f64bits(-1.0), f64bits(0.0), 0),
+                       (OP_FAFFINE, 0, PID["TargetY"], 0, f64bits(-1.0), f64bits(0.0), 0),
+                       (OP_FSET, 0, PID["AtkDis"], 0, f64bits(2.5), 0, 0)])
+        put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 1, PID["MAXHP"]),
+                       (OP_ISET, 0, PID["SP"], 0, 7, 0, 0)])
     if with_records:
         # skill table: col 1 = cooldown ms (int), col 2 = charge (f64) decays
         lst = [(OP_RIADD_CLAMP, 0, (0 << 8) | 1, 0, -100, 0, I64_MAX)]
@@ -117,7 +130,7 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
                t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, rec_skill_op=False, sched_edges=False,
                switch_frac=0.0, switch_new_groups=False, rec_steady=False, ext_props=None, burst_frac=0.0,
                burst_props=20, rmw_frac=0.0, spawn_frac=0.0, destroy_frac=0.0, rec_set_frac=0.0,
-               rec_set_float=True, obj_props=False, obj_set_frac=0.05, rec_row_frac=0.0):
+               rec_set_float=True, obj_props=False, obj_set_frac=0.05, rec_row_frac=0.0, set_ops=False):
     if spawn_frac > 0 or destroy_frac > 0:
         return _lifecycle_world(locals())
     rng = np.random.default_rng(seed)
@@ -175,7 +188,7 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
     still = rng.random(n_obj) < 0.02
     init_f[fi["X"], still] = init_f[fi["TargetX"], still]
 
-    ops, n_ops = programs(records, rec_float_op, rec_skill_op)
+    ops, n_ops = programs(records, rec_float_op, rec_skill_op, set_ops)
     n_kind = len(KINDS) if records else len(KINDS) - 1
 
     # ---- heartbeats registered before the first frame ----

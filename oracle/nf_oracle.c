@@ -251,6 +251,12 @@ static void run_program(int32_t obj, int kind) {
             set_flt(obj, op->dst, m + bitsd((uint64_t)op->b));
             break;
         }
+        case NFK_OP_ISET: /* a functor's SetPropertyInt(self, dst, A) (KM:323 -> PR:254) */
+            set_int(obj, op->dst, opnd(obj, op, NFK_A_PROP, op->a));
+            break;
+        case NFK_OP_FSET: /* SetPropertyFloat(self, dst, A) (KM:335 -> PR:295) */
+            set_flt(obj, op->dst, (op->flags & NFK_A_PROP) ? fget(obj, op->a) : bitsd((uint64_t)op->a));
+            break;
         case NFK_OP_RIADD_CLAMP: {
             int r = op->dst >> 8, col = op->dst & 255;
             for (int row = 0; row < rec_rows[r]; row++) {

@@ -222,6 +222,12 @@ static int OnHeartBeat(const NFGUID& self, const std::string& name, const float,
             SetFloat(self, op.dst, m + bitsd((uint64_t)op.b));
             break;
         }
+        case NFK_OP_ISET:
+            SetInt(self, op.dst, (op.flags & NFK_A_PROP) ? GetInt(self, (int)op.a) : op.a);
+            break;
+        case NFK_OP_FSET:
+            SetFloat(self, op.dst, (op.flags & NFK_A_PROP) ? GetFloat(self, (int)op.a) : bitsd((uint64_t)op.a));
+            break;
         case NFK_OP_RIADD_CLAMP:
         case NFK_OP_RFAFFINE: {
             int r = op.dst >> 8, col = op.dst & 255;

@@ -361,6 +361,14 @@ int main(int argc, char** argv) {
                 km->SetPropertyFloat(self, d, m + bitsd((uint64_t)op.b));
                 break;
             }
+            case NFK_OP_ISET:
+                km->SetPropertyInt(self, pname[op.dst],
+                                   (op.flags & NFK_A_PROP) ? km->GetPropertyInt(self, pname[op.a]) : op.a);
+                break;
+            case NFK_OP_FSET:
+                km->SetPropertyFloat(self, pname[op.dst], (op.flags & NFK_A_PROP) ? km->GetPropertyFloat(self, pname[op.a])
+                                                                                  : bitsd((uint64_t)op.a));
+                break;
             case NFK_OP_RIADD_CLAMP: {  // every used row of the column (NFCRecord::SetInt, RC:182)
                 const std::string& rn = rname[op.dst >> 8];
                 const int col = op.dst & 255;

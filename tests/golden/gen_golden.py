@@ -53,6 +53,12 @@ FIXTURES = {
     # record row operations: AddRow (first unused row / a given row, covering a used one), Remove,
     # ClearRecord (NFCRecord.cpp:111, 1086, 1109; KM:492) interleaved with SetRecordInt calls on the
     # same rows, beside the heartbeat's cooldown op, with create / destroy
+    # assignment ops in the heartbeat programs (ISET / FSET: SetPropertyInt / SetPropertyFloat with a
+    # constant or another property's value) beside the add / lerp / affine ones, SetProperty calls on
+    # their operands, records
+    "setops": dict(n_obj=500, n_scenes=2, groups_per_scene=4, players_per_group=3, n_ticks=10, seed=1212,
+                   ext_frac=0.05, ext_props="all", host_ops=True, set_ops=True, records=True, rec_rows=16,
+                   rec_float_op=False),
     "rowops": dict(n_obj=400, n_scenes=2, groups_per_scene=4, players_per_group=4, n_ticks=8, seed=1111,
                    records=True, rec_rows=24, rec_float_op=False, rec_set_frac=0.08, rec_set_float=False,
                    rec_row_frac=0.08, ext_frac=0.03, spawn_frac=0.02, destroy_frac=0.02),
@@ -68,7 +74,7 @@ TUTORIAL3 = {"tutorial3": dict(n_obj=2000, n_ticks=80, seed=606, world_effect=Tr
 # compiled from the reference): <name>.session.nfio holds what those modules raised in every frame
 # (property / record events in call order, fired heartbeats, GetBroadCastObject lists at the frame's
 # end) and their final state; tests/test_oracle.py derives each frame's dirty-sync list from it
-SESSION_FIXTURES = ["switch", "lifecycle", "rowops", "objects"]
+SESSION_FIXTURES = ["switch", "lifecycle", "rowops", "objects", "setops"]
 
 
 def session(name, w, wp):

@@ -27,7 +27,7 @@ def set_path(monkeypatch, path):
 
 @PATHS
 @pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets", "tutorial3", "rmw",
-                                  "lifecycle", "recsets", "objects", "rowops"])
+                                  "lifecycle", "recsets", "objects", "rowops", "setops"])
 def test_gpu_matches_reference_golden(gpu_available, monkeypatch, name, path):
     set_path(monkeypatch, path)
     w = nfio.read(os.path.join(GOLDEN, f"{name}.workload.nfio"))
@@ -92,6 +92,11 @@ CASES = {
     # reference's NFCRecord::SetFloat is broken: test_oracle.py::test_reference_record_setfloat_bug)
     "record_sets_f64": dict(n_obj=2500, n_scenes=2, groups_per_scene=5, players_per_group=3, records=True, rec_rows=20,
                             rec_set_frac=0.1, rec_set_float=True, switch_frac=0.01),
+    # assignment ops (ISET / FSET, a constant or another property's value) in the programs, with
+    # SetProperty calls on their operands and destinations, create / destroy and scene switches
+    "set_ops": dict(n_obj=4000, n_scenes=2, groups_per_scene=6, players_per_group=4, set_ops=True, ext_frac=0.1,
+                    ext_props="all", rmw_frac=0.02, switch_frac=0.02, spawn_frac=0.02, destroy_frac=0.02,
+                    host_ops=True, records=True, rec_rows=32),
     "wide_sets_records": dict(n_obj=3000, n_scenes=2, groups_per_scene=5, players_per_group=6, records=True,
                               rec_rows=32, ext_frac=0.1, ext_props="all", burst_frac=0.02, burst_props=24,
                               switch_frac=0.01),
