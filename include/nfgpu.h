@@ -61,7 +61,10 @@ extern "C" {
  *   ISET        dst(int) = A                                  A imm or prop (NFK_A_PROP)
  *   FSET        dst(f64) = A                                  A f64(a) or f64 prop (NFK_A_PROP)
  * clamp(v, lo, hi): v < lo -> lo; then v > hi -> hi.  Integer adds wrap.
- * Record ops: dst = (rec << 8) | col. */
+ * Record ops: dst = (rec << 8) | col.
+ * NFK_GUARD (property ops only): the op runs only when int property (guard & 0xFFFF), as the
+ * program has left it so far, compares to 0 as NFK_GUARD_* in (guard >> 16) & 3 says — a functor's
+ * `if (GetPropertyInt(self, g) > 0) SetProperty...(...)`. */
 enum {
     NFK_OP_NOP = 0,
     NFK_OP_IADD_CLAMP = 1,
@@ -75,12 +78,17 @@ enum {
 #define NFK_A_PROP 1
 #define NFK_LO_PROP 2
 #define NFK_HI_PROP 4
+#define NFK_GUARD 8
+#define NFK_GUARD_GT0 0 /* g > 0 */
+#define NFK_GUARD_LE0 1 /* g <= 0 */
+#define NFK_GUARD_NE0 2 /* g != 0 */
+#define NFK_GUARD_EQ0 3 /* g == 0 */
 
 typedef struct nfk_op {
     uint8_t code;
     uint8_t flags;
     uint16_t dst;
-    uint32_t pad;
+    uint32_t guard; /* with NFK_GUARD: property id | NFK_GUARD_* << 16; else 0 */
     int64_t a, b, c;
 } nfk_op; /* 32 bytes */
 

@@ -910,6 +910,7 @@ bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>&
                 } else if ((op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) && (op.flags & NFK_A_PROP) && !is_w(op.a)) {
                     R.push_back((int)op.a);
                 }
+                if ((op.flags & NFK_GUARD) && !is_w(op.guard & 0xFFFF)) R.push_back((int)(op.guard & 0xFFFF));
             }
         std::sort(R.begin(), R.end());
         R.erase(std::unique(R.begin(), R.end()), R.end());
@@ -944,14 +945,18 @@ bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>&
                     u[0] = slot(op.dst);
                     if (op.flags & NFK_A_PROP) u[1] = slot(op.a);
                 }
-                for (int q = 0; q < 4; q++)  // writable bits | read-only bits << 16
-                    if (u[q] != kNoU) tab.umask[k] |= (u[q] & 0x80) ? 1u << (16 + (u[q] & 0x7F)) : 1u << u[q];
+                tab.opg[k][i] = (op.flags & NFK_GUARD) ? slot(op.guard & 0xFFFF) : kNoU;
+                for (int q = 0; q < 5; q++) {  // writable bits | read-only bits << 16
+                    const uint8_t uq = q < 4 ? u[q] : tab.opg[k][i];
+                    if (uq != kNoU) tab.umask[k] |= (uq & 0x80) ? 1u << (16 + (uq & 0x7F)) : 1u << uq;
+                }
                 OpX& x = tab.opx[k][i];
                 x.cfd = (uint32_t)op.code | ((uint32_t)op.flags << 8) | ((uint32_t)op.dst << 16);
                 x.slots = (uint32_t)u[0] | ((uint32_t)u[1] << 8) | ((uint32_t)u[2] << 16) | ((uint32_t)u[3] << 24);
                 x.a = op.a;
                 x.b = op.b;
                 x.c = op.c;
+                x.gd = (op.flags & NFK_GUARD) ? 0x80000000u | (((op.guard >> 16) & 3u) << 8) | tab.opg[k][i] : 0u;
             }
         }
     }
@@ -1753,6 +1758,13 @@ int nfk_define_kind(void* world, int32_t kind, const nfk_op* ops, int32_t n_ops)
         const int np = w->n_if, ni = w->cfg.n_int;  // (object properties are no program operands)
         auto isint = [&](int64_t p) { return p >= 0 && p < ni; };
         auto isflt = [&](int64_t p) { return p >= ni && p < np; };
+        if (op.flags & NFK_GUARD) {
+            const bool rec = op.code == NFK_OP_RIADD_CLAMP || op.code == NFK_OP_RFAFFINE;
+            if (rec || op.code == NFK_OP_NOP || !isint(op.guard & 0xFFFF) || (op.guard >> 18))
+                return fail(NFK_ERR_ARG, "NFK_GUARD: a property op guarded by an int property");
+        } else if (op.guard) {
+            return fail(NFK_ERR_ARG, "nfk_op.guard without NFK_GUARD");
+        }
         switch (op.code) {
         case NFK_OP_IADD_CLAMP:
             if (!isint(op.dst) || ((op.flags & NFK_A_PROP) && !isint(op.a)) ||
@@ -1915,6 +1927,7 @@ int nfk_commit(void* world) {
                     add(op.dst, 1);
                     if (op.flags & NFK_A_PROP) add((int)op.a, 0);
                 }
+                if (op.flags & NFK_GUARD) add((int)(op.guard & 0xFFFF), 0);
             }
         std::map<std::vector<int>, int> gi;
         for (int p = 0; p < NP; p++) {
@@ -1953,6 +1966,7 @@ int nfk_commit(void* world) {
                     ps.push_back(op.dst);
                     if (op.flags & NFK_A_PROP) ps.push_back((int)op.a);
                 }
+                if (op.flags & NFK_GUARD) ps.push_back((int)(op.guard & 0xFFFF));
             }
             for (size_t i = 1; i < ps.size(); i++) {
                 const int a = find(ps[0]), b = find(ps[i]);

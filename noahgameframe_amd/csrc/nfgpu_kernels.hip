@@ -465,7 +465,7 @@ struct Ent {
 // queued SetProperty) wrote it, else from the prefetched column value.
 __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ tab, int k) {
     const int n = tab->nops[k];
-    uint64_t pre[NFK_MAX_OPS][4];
+    uint64_t pre[NFK_MAX_OPS][5];  // dst, a, b, c, guard
 #pragma unroll
     for (int i = 0; i < NFK_MAX_OPS; i++) {
         if (i >= n) break;
@@ -478,6 +478,10 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
         (void)isf;
         pre[i][0] = *prop_ptr(*en.dv, p0, en.e);
         en.bytes += 8;
+        if (op.flags & NFK_GUARD) {
+            pre[i][4] = *prop_ptr(*en.dv, op.guard & 0xFFFFu, en.e);
+            en.bytes += 8;
+        }
         if (op.code == NFK_OP_FLERP || ((op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) && (op.flags & NFK_A_PROP))) {
             pre[i][1] = *prop_ptr(*en.dv, (uint32_t)op.a, en.e);
             en.bytes += 8;
@@ -491,6 +495,11 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
     for (int i = 0; i < NFK_MAX_OPS; i++) {
         if (i >= n) break;
         const nfk_op op = tab->ops[k][i];
+        if (op.flags & NFK_GUARD) {
+            uint64_t t;
+            const int64_t g = en.tget(op.guard & 0xFFFFu, t) ? (int64_t)t : (int64_t)pre[i][4];
+            if (!guard_ok((op.guard >> 16) & 3u, g)) continue;
+        }
         if (op.code == NFK_OP_IADD_CLAMP) {
             uint64_t t;
             const int64_t cur = en.tget(op.dst, t) ? (int64_t)t : (int64_t)pre[i][0];

@@ -92,6 +92,7 @@ static void resolve_program(std::vector<nfk_op>& ops, const std::vector<std::str
             if (i < 0 || i >= (int64_t)props.size()) throw std::runtime_error("heartbeat program: property operand out of range");
             return (int64_t)pid(props[(size_t)i]);
         };
+        if (op.flags & NFK_GUARD) op.guard = (op.guard & ~0xFFFFu) | (uint32_t)P(op.guard & 0xFFFF);
         switch (op.code) {
             case NFK_OP_IADD_CLAMP:
                 op.dst = (uint16_t)P(op.dst);

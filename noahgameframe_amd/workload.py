@@ -39,12 +39,20 @@ KID = {n: i for i, n in enumerate(KINDS)}
 
 # op codes / flags (include/nfgpu.h)
 OP_IADD_CLAMP, OP_FLERP, OP_FAFFINE, OP_RIADD_CLAMP, OP_RFAFFINE, OP_ISET, OP_FSET = 1, 2, 3, 4, 5, 6, 7
-A_PROP, LO_PROP, HI_PROP = 1, 2, 4
+A_PROP, LO_PROP, HI_PROP, GUARD = 1, 2, 4, 8
+GUARD_GT0, GUARD_LE0, GUARD_NE0, GUARD_EQ0 = 0, 1, 2, 3
+
+
+def guard(pid, cmp):
+    """nfk_op.guard of an NFK_GUARD op: the int property and its comparison with 0"""
+    return pid | (cmp << 16)
+
+
 MAX_OPS = 4
 MAX_REC_COLS = 16
 I64_MIN, I64_MAX = -(2 ** 63), 2 ** 63 - 1
 
-OP_DTYPE = np.dtype([("code", "u1"), ("flags", "u1"), ("dst", "<u2"), ("pad", "<u4"),
+OP_DTYPE = np.dtype([("code", "u1"), ("flags", "u1"), ("dst", "<u2"), ("guard", "<u4"),
                      ("a", "<i8"), ("b", "<i8"), ("c", "<i8")])
 assert OP_DTYPE.itemsize == 32
 
@@ -95,17 +103,20 @@ def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False)
     put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 1, PID["MAXHP"])])
     if set_ops:
         # plain assignments a functor makes (SetPropertyInt / SetPropertyFloat with a constant or
-        # another property's value): first Sets change the value, repeated ones raise no event
+        # another property's value): first Sets change the value, repeated ones raise no event; some
+        # under a guard on an int property (a functor's `if (GetPropertyInt(self, g) ...)`), one of
+        # them on a value the same program wrote just before
         put("MPRegen", [(OP_IADD_CLAMP, A_PROP | HI_PROP, PID["MP"], 0, PID["MPREGEN"], 0, PID["MAXMP"]),
-                        (OP_ISET, A_PROP, PID["EXP"], 0, PID["Level"], 0, 0)])
+                        (OP_ISET, A_PROP | GUARD, PID["EXP"], guard(PID["Camp"], GUARD_NE0), PID["Level"], 0, 0)])
         put("Move", [(OP_FLERP, 0, PID["X"], 0, PID["TargetX"], f64bits(0.125), 0),
                      (OP_FLERP, 0, PID["Y"], 0, PID["TargetY"], f64bits(0.125), 0),
-                     (OP_FSET, A_PROP, PID["Z"], 0, PID["TargetX"], 0, 0)])
+                     (OP_FSET, A_PROP | GUARD, PID["Z"], guard(PID["Camp"], GUARD_GT0), PID["TargetX"], 0, 0)])
         put("Patrol", [(OP_FAFFINE, 0, PID["TargetX"], 0, f64bits(-1.0), f64bits(0.0), 0),
                        (OP_FAFFINE, 0, PID["TargetY"], 0, f64bits(-1.0), f64bits(0.0), 0),
-                       (OP_FSET, 0, PID["AtkDis"], 0, f64bits(2.5), 0, 0)])
+                       (OP_IADD_CLAMP, 0, PID["Camp"], 0, -1, 0, 3),
+                       (OP_FSET, GUARD, PID["AtkDis"], guard(PID["Camp"], GUARD_EQ0), f64bits(2.5), 0, 0)])
         put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 1, PID["MAXHP"]),
-                       (OP_ISET, 0, PID["SP"], 0, 7, 0, 0)])
+                       (OP_ISET, GUARD, PID["SP"], guard(PID["Camp"], GUARD_LE0), 7, 0, 0)])
     if with_records:
         # skill table: col 1 = cooldown ms (int), col 2 = charge (f64) decays
         lst = [(OP_RIADD_CLAMP, 0, (0 << 8) | 1, 0, -100, 0, I64_MAX)]

@@ -224,6 +224,11 @@ static int64_t opnd(int32_t obj, const nfk_op* op, int bit, int64_t x) {
 static void run_program(int32_t obj, int kind) {
     for (int i = 0; i < nops[kind]; i++) {
         const nfk_op* op = &ops[kind][i];
+        if (op->flags & NFK_GUARD) { /* the functor's `if (GetPropertyInt(self, g) ...)` */
+            int64_t g = iget(obj, op->guard & 0xFFFF);
+            int c = (op->guard >> 16) & 3;
+            if (!(c == NFK_GUARD_GT0 ? g > 0 : c == NFK_GUARD_LE0 ? g <= 0 : c == NFK_GUARD_NE0 ? g != 0 : g == 0)) continue;
+        }
         switch (op->code) {
         case NFK_OP_IADD_CLAMP: {
             int64_t cur = iget(obj, op->dst);

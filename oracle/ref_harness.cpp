@@ -196,6 +196,11 @@ static int OnHeartBeat(const NFGUID& self, const std::string& name, const float,
     if (!W.bench) W.fired.push_back({obj, kind, nCount});
     for (int i = 0; i < W.nops[kind]; i++) {
         const nfk_op& op = W.ops[kind][i];
+        if (op.flags & NFK_GUARD) {
+            const int64_t g = GetInt(self, (int)(op.guard & 0xFFFF));
+            const int c = (op.guard >> 16) & 3;
+            if (!(c == NFK_GUARD_GT0 ? g > 0 : c == NFK_GUARD_LE0 ? g <= 0 : c == NFK_GUARD_NE0 ? g != 0 : g == 0)) continue;
+        }
         switch (op.code) {
         case NFK_OP_IADD_CLAMP: {
             int64_t cur = GetInt(self, op.dst);

@@ -332,6 +332,12 @@ int main(int argc, char** argv) {
         }
         for (int i = 0; i < nops[k]; i++) {
             const nfk_op& op = ops[k * NFK_MAX_OPS + i];
+            if (op.flags & NFK_GUARD) {
+                const int64_t g = km->GetPropertyInt(self, pname[op.guard & 0xFFFF]);
+                const int c = (op.guard >> 16) & 3;
+                if (!(c == NFK_GUARD_GT0 ? g > 0 : c == NFK_GUARD_LE0 ? g <= 0 : c == NFK_GUARD_NE0 ? g != 0 : g == 0))
+                    continue;
+            }
             switch (op.code) {
             case NFK_OP_IADD_CLAMP: {
                 const std::string& d = pname[op.dst];

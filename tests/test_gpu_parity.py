@@ -470,6 +470,12 @@ def test_jit_specialisation_is_what_runs(gpu_available, monkeypatch):
     on, msg = m.jit_status()
     m.close()
     assert not on and "NFGPU_JIT=0" in msg
+    # the guarded assignment programs (16 U slots: 11 destinations, 5 read-only operands) still fit
+    monkeypatch.setenv("NFGPU_JIT", "1")
+    m = kernel.world_from_workload(nfio.read(os.path.join(GOLDEN, "setops.workload.nfio")))
+    on, msg = m.jit_status()
+    m.close()
+    assert on, msg
 
 
 def _functor_frame_log(same, gather=""):
