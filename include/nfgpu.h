@@ -37,7 +37,8 @@ extern "C" {
 #define NFK_MAX_PROPS 128
 #define NFK_MAX_CLASSES 16 /* class id 15 is reserved (marks a free slot on the device) */
 #define NFK_MAX_KINDS 32
-#define NFK_MAX_OPS 4
+#define NFK_MAX_OPS 8     /* ops per heartbeat program */
+#define NFK_MAX_REC_OPS 4 /* record ops across all programs (distinct record columns) */
 #define NFK_MAX_RECORDS 8
 #define NFK_MAX_REC_ROWS 64
 #define NFK_MAX_REC_COLS 16

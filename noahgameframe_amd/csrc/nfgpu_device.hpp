@@ -143,7 +143,7 @@ struct Tables {
     int32_t nops[NFK_MAX_KINDS];
     uint8_t pflags[NFK_MAX_CLASSES][kMaxProps];
     uint8_t rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
-    RecOp recops[NFK_MAX_OPS];
+    RecOp recops[NFK_MAX_REC_OPS];
     int32_t n_recops;
     int32_t rec_rows[NFK_MAX_RECORDS], rec_cols[NFK_MAX_RECORDS];
     uint32_t kind_has_recop;  // bit k: kind k has record ops
@@ -237,7 +237,7 @@ struct Dev {
     // 60-63 class id
     const uint64_t* fan_desc;
     uint32_t ablate;
-    RecOpX rops[NFK_MAX_OPS];  // record ops sorted by (rec, col)
+    RecOpX rops[NFK_MAX_REC_OPS];  // record ops sorted by (rec, col)
     int32_t n_rops;
     uint32_t rop_kinds;        // kinds with record ops
     // algorithmic-byte tallies: [3 kernels][kTallyN][8] (one 64-byte line per counter), spread

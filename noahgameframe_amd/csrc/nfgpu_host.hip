@@ -1872,7 +1872,7 @@ int nfk_commit(void* world) {
         for (int i = 0; i < w->tab.nops[k]; i++) {
             const nfk_op& op = w->tab.ops[k][i];
             if (op.code == NFK_OP_RIADD_CLAMP || op.code == NFK_OP_RFAFFINE) {
-                if (nro == NFK_MAX_OPS) return fail(NFK_ERR_ARG, "at most 4 record ops across all kinds");
+                if (nro == NFK_MAX_REC_OPS) return fail(NFK_ERR_ARG, "at most NFK_MAX_REC_OPS record ops across all kinds");
                 RecOp ro{k, op.dst >> 8, op.dst & 255, op.code, op.a, op.b, op.c};
                 w->tab.recops[nro++] = ro;
                 w->tab.kind_has_recop |= 1u << k;
@@ -3633,13 +3633,13 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
             else if (d.n_rops <= 2)
                 hipLaunchKernelGGL((k_records<2, 4, true>), g, b, 0, w->stream, d);
             else
-                hipLaunchKernelGGL((k_records<NFK_MAX_OPS, 2, true>), g, b, 0, w->stream, d);
+                hipLaunchKernelGGL((k_records<NFK_MAX_REC_OPS, 2, true>), g, b, 0, w->stream, d);
         } else if (d.n_rops <= 1)
             hipLaunchKernelGGL((k_records<1, 4, false>), g, b, 0, w->stream, d);
         else if (d.n_rops <= 2)
             hipLaunchKernelGGL((k_records<2, 4, false>), g, b, 0, w->stream, d);
         else
-            hipLaunchKernelGGL((k_records<NFK_MAX_OPS, 2, false>), g, b, 0, w->stream, d);
+            hipLaunchKernelGGL((k_records<NFK_MAX_REC_OPS, 2, false>), g, b, 0, w->stream, d);
         if (nrss)  // ... and written into the room k_records left
             hipLaunchKernelGGL((k_rset_slots<true>), dim3((unsigned)((nrss + kWpb - 1) / kWpb)), b, 0, w->stream, d);
         HIPCHK(hipGetLastError());

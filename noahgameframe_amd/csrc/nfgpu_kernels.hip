@@ -463,11 +463,11 @@ struct Ent {
 // program at once (independent loads, one memory round trip); pass 2 runs the ops in order,
 // reading a property from the frame's written-property list when an earlier op (or kind, or
 // queued SetProperty) wrote it, else from the prefetched column value.
-__device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ tab, int k) {
-    const int n = tab->nops[k];
-    uint64_t pre[NFK_MAX_OPS][5];  // dst, a, b, c, guard
+__device__ __forceinline__ void run_program_chunk(Ent& en, const Tables* __restrict__ tab, int k, int i0, int n) {
+    uint64_t pre[4][5];  // dst, a, b, c, guard
 #pragma unroll
-    for (int i = 0; i < NFK_MAX_OPS; i++) {
+    for (int ii = 0; ii < 4; ii++) {
+        const int i = i0 + ii;
         if (i >= n) break;
         const nfk_op op = tab->ops[k][i];
         if (op.code != NFK_OP_IADD_CLAMP && op.code != NFK_OP_FLERP && op.code != NFK_OP_FAFFINE &&
@@ -476,46 +476,47 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
         const uint32_t p0 = op.dst;
         const bool isf = op.code != NFK_OP_IADD_CLAMP;
         (void)isf;
-        pre[i][0] = *prop_ptr(*en.dv, p0, en.e);
+        pre[ii][0] = *prop_ptr(*en.dv, p0, en.e);
         en.bytes += 8;
         if (op.flags & NFK_GUARD) {
-            pre[i][4] = *prop_ptr(*en.dv, op.guard & 0xFFFFu, en.e);
+            pre[ii][4] = *prop_ptr(*en.dv, op.guard & 0xFFFFu, en.e);
             en.bytes += 8;
         }
         if (op.code == NFK_OP_FLERP || ((op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) && (op.flags & NFK_A_PROP))) {
-            pre[i][1] = *prop_ptr(*en.dv, (uint32_t)op.a, en.e);
+            pre[ii][1] = *prop_ptr(*en.dv, (uint32_t)op.a, en.e);
             en.bytes += 8;
         } else if (op.code == NFK_OP_IADD_CLAMP) {
-            if (op.flags & NFK_A_PROP) { pre[i][1] = *prop_ptr(*en.dv, (uint32_t)op.a, en.e); en.bytes += 8; }
-            if (op.flags & NFK_LO_PROP) { pre[i][2] = *prop_ptr(*en.dv, (uint32_t)op.b, en.e); en.bytes += 8; }
-            if (op.flags & NFK_HI_PROP) { pre[i][3] = *prop_ptr(*en.dv, (uint32_t)op.c, en.e); en.bytes += 8; }
+            if (op.flags & NFK_A_PROP) { pre[ii][1] = *prop_ptr(*en.dv, (uint32_t)op.a, en.e); en.bytes += 8; }
+            if (op.flags & NFK_LO_PROP) { pre[ii][2] = *prop_ptr(*en.dv, (uint32_t)op.b, en.e); en.bytes += 8; }
+            if (op.flags & NFK_HI_PROP) { pre[ii][3] = *prop_ptr(*en.dv, (uint32_t)op.c, en.e); en.bytes += 8; }
         }
     }
 #pragma unroll
-    for (int i = 0; i < NFK_MAX_OPS; i++) {
+    for (int ii = 0; ii < 4; ii++) {
+        const int i = i0 + ii;
         if (i >= n) break;
         const nfk_op op = tab->ops[k][i];
         if (op.flags & NFK_GUARD) {
             uint64_t t;
-            const int64_t g = en.tget(op.guard & 0xFFFFu, t) ? (int64_t)t : (int64_t)pre[i][4];
+            const int64_t g = en.tget(op.guard & 0xFFFFu, t) ? (int64_t)t : (int64_t)pre[ii][4];
             if (!guard_ok((op.guard >> 16) & 3u, g)) continue;
         }
         if (op.code == NFK_OP_IADD_CLAMP) {
             uint64_t t;
-            const int64_t cur = en.tget(op.dst, t) ? (int64_t)t : (int64_t)pre[i][0];
-            const int64_t a = (op.flags & NFK_A_PROP) ? (en.tget((uint32_t)op.a, t) ? (int64_t)t : (int64_t)pre[i][1]) : op.a;
-            const int64_t lo = (op.flags & NFK_LO_PROP) ? (en.tget((uint32_t)op.b, t) ? (int64_t)t : (int64_t)pre[i][2]) : op.b;
-            const int64_t hi = (op.flags & NFK_HI_PROP) ? (en.tget((uint32_t)op.c, t) ? (int64_t)t : (int64_t)pre[i][3]) : op.c;
+            const int64_t cur = en.tget(op.dst, t) ? (int64_t)t : (int64_t)pre[ii][0];
+            const int64_t a = (op.flags & NFK_A_PROP) ? (en.tget((uint32_t)op.a, t) ? (int64_t)t : (int64_t)pre[ii][1]) : op.a;
+            const int64_t lo = (op.flags & NFK_LO_PROP) ? (en.tget((uint32_t)op.b, t) ? (int64_t)t : (int64_t)pre[ii][2]) : op.b;
+            const int64_t hi = (op.flags & NFK_HI_PROP) ? (en.tget((uint32_t)op.c, t) ? (int64_t)t : (int64_t)pre[ii][3]) : op.c;
             int64_t v = (int64_t)((uint64_t)cur + (uint64_t)a);
             v = v < lo ? lo : v;
             v = v > hi ? hi : v;
             if (v != cur) en.tput(op.dst, (uint64_t)cur, (uint64_t)v);  // NFCProperty::SetInt (PR:273)
         } else if (op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE) {
             uint64_t t;
-            const double x = __longlong_as_double((long long)(en.tget(op.dst, t) ? t : pre[i][0]));
+            const double x = __longlong_as_double((long long)(en.tget(op.dst, t) ? t : pre[ii][0]));
             double v;
             if (op.code == NFK_OP_FLERP) {
-                const double tg = __longlong_as_double((long long)(en.tget((uint32_t)op.a, t) ? t : pre[i][1]));
+                const double tg = __longlong_as_double((long long)(en.tget((uint32_t)op.a, t) ? t : pre[ii][1]));
                 const double dd = tg - x;
                 const double m = dd * __longlong_as_double(op.b);
                 v = x + m;
@@ -527,8 +528,8 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
                 en.tput(op.dst, (uint64_t)__double_as_longlong(x), (uint64_t)__double_as_longlong(v));
         } else if (op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) {
             uint64_t t;
-            const uint64_t cur = en.tget(op.dst, t) ? t : pre[i][0];
-            const uint64_t r = (op.flags & NFK_A_PROP) ? (en.tget((uint32_t)op.a, t) ? t : pre[i][1]) : (uint64_t)op.a;
+            const uint64_t cur = en.tget(op.dst, t) ? t : pre[ii][0];
+            const uint64_t r = (op.flags & NFK_A_PROP) ? (en.tget((uint32_t)op.a, t) ? t : pre[ii][1]) : (uint64_t)op.a;
             const bool set = op.code == NFK_OP_ISET
                                  ? r != cur  // NFCProperty::SetInt (PR:273)
                                  : !(fabs(__longlong_as_double((long long)r) - __longlong_as_double((long long)cur)) <= 1e-15);
@@ -536,6 +537,14 @@ __device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ 
         }
         // record ops run in k_records
     }
+}
+
+__device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ tab, int k) {
+    const int n = tab->nops[k];
+    // (ops in chunks of 4: an operand an earlier op wrote is read from the written list either way)
+#pragma unroll 1
+    for (int i0 = 0; i0 < n; i0 += 4)
+        run_program_chunk(en, tab, k, i0, min(n, i0 + 4));
 }
 
 }  // namespace nfgpu
@@ -937,7 +946,7 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
             int code = 0;
             int64_t oa = 0, obb = 0, oc = 0;
 #pragma unroll
-            for (int j = 0; j < NFK_MAX_OPS; j++)
+            for (int j = 0; j < NFK_MAX_REC_OPS; j++)
                 if (j < nro && d.rops[j].rec == r && d.rops[j].col == c && ((fmask >> d.rops[j].kind) & 1)) {
                     op = true;
                     code = d.rops[j].code;
@@ -1031,7 +1040,7 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
 // Cells [cap][cols][rows] so a wave reads one (slot, col) row-vector contiguously.
 
 // kOps: register slots for the record ops (>= n_rops), kGroup: slots whose cells are in flight
-// together; instantiated so that a frame's op count does not pay for NFK_MAX_OPS registers.
+// together; instantiated so that a frame's op count does not pay for NFK_MAX_REC_OPS registers.
 template <int kOps, int kGroup>
 struct RecGrp {  // one group of slots with record work: their cells and used-row masks
     int js[kGroup];

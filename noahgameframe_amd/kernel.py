@@ -15,6 +15,8 @@ import numpy as np
 
 from . import workload as wl
 
+NFK_MAX_OPS = 8  # include/nfgpu.h: ops per heartbeat program
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NFGPU_LIB") or os.path.join(_HERE, "libnfgpu.so")  # (NFGPU_LIB: A/B timing of library builds)
 
@@ -512,7 +514,11 @@ def jit_preview(w, compile=False):
     lib = load_library()
     _, n_int, n_flt, n_cls, n_kind = (int(x) for x in w["cfg"][:5])
     flags = np.ascontiguousarray(np.asarray(w["prop_flags"])[:n_cls], np.uint8)
-    ops = np.ascontiguousarray(w["ops"][:n_kind])
+    src_ops = np.asarray(w["ops"][:n_kind])
+    if src_ops.dtype != wl.OP_DTYPE:  # (raw records from a workload file)
+        src_ops = src_ops.view(wl.OP_DTYPE).reshape(n_kind, -1)
+    ops = np.zeros((n_kind, NFK_MAX_OPS), wl.OP_DTYPE)  # [n_kind][NFK_MAX_OPS] (nfgpu.h)
+    ops[:, :src_ops.shape[1]] = src_ops
     n_ops = np.ascontiguousarray(w["n_ops"][:n_kind], np.int32)
     ok = ctypes.c_int32()
     src = ctypes.create_string_buffer(1 << 20)

@@ -48,7 +48,7 @@ def guard(pid, cmp):
     return pid | (cmp << 16)
 
 
-MAX_OPS = 4
+MAX_OPS = 8  # include/nfgpu.h NFK_MAX_OPS (workload files written before round 4 hold 4 per kind)
 MAX_REC_COLS = 16
 I64_MIN, I64_MAX = -(2 ** 63), 2 ** 63 - 1
 
@@ -114,7 +114,9 @@ def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False)
         put("Patrol", [(OP_FAFFINE, 0, PID["TargetX"], 0, f64bits(-1.0), f64bits(0.0), 0),
                        (OP_FAFFINE, 0, PID["TargetY"], 0, f64bits(-1.0), f64bits(0.0), 0),
                        (OP_IADD_CLAMP, 0, PID["Camp"], 0, -1, 0, 3),
-                       (OP_FSET, GUARD, PID["AtkDis"], guard(PID["Camp"], GUARD_EQ0), f64bits(2.5), 0, 0)])
+                       (OP_FSET, GUARD, PID["AtkDis"], guard(PID["Camp"], GUARD_EQ0), f64bits(2.5), 0, 0),
+                       (OP_FAFFINE, GUARD, PID["AtkDis"], guard(PID["Camp"], GUARD_GT0), f64bits(1.5), f64bits(0.25), 0),
+                       (OP_IADD_CLAMP, A_PROP, PID["SP"], 0, PID["Level"], 0, 1000)])  # (6 ops: > 4 per program)
         put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 1, PID["MAXHP"]),
                        (OP_ISET, GUARD, PID["SP"], guard(PID["Camp"], GUARD_LE0), 7, 0, 0)])
     if with_records:

@@ -434,7 +434,12 @@ int main(int argc, char** argv) {
             rused[r] = (uint64_t*)a->data;
         }
     }
-    memcpy(ops, GET("ops")->data, NK * NFK_MAX_OPS * sizeof(nfk_op));
+    {
+        const nfio_arr* oa = GET("ops");
+        const int opk = nfio_ops_per_kind(oa);
+        if (opk <= 0 || opk > NFK_MAX_OPS) die("bad ops array");
+        for (int k = 0; k < NK; k++) memcpy(ops[k], (const nfk_op*)oa->data + (size_t)k * opk, (size_t)opk * sizeof(nfk_op));
+    }
     memcpy(nops, GET("n_ops")->data, NK * 4);
     ghead = (int64_t*)GET("guid_head")->data;
     gdata = (int64_t*)GET("guid_data")->data;

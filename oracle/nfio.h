@@ -109,4 +109,11 @@ static inline void nfio_wclose(nfio_writer* w) {
     fclose(w->fp);
     w->fp = NULL;
 }
+
+/* ops arrays (nfk_op records, written as raw bytes [n_kind][ops per kind][32]): ops per kind.
+ * Workloads written before NFK_MAX_OPS grew hold 4 per kind, newer ones NFK_MAX_OPS. */
+static inline int nfio_ops_per_kind(const nfio_arr* a) {
+    return a && a->ndim >= 2 ? (int)a->shape[1] : 0;
+}
+
 #endif

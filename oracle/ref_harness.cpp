@@ -361,7 +361,16 @@ int main(int argc, char** argv) {
         W.kname.push_back(cstr(knames + 32 * k, 32));
         W.kind_of[W.kname.back()] = k;
     }
-    memcpy(W.ops, GET(wf, "ops")->data, W.NK * NFK_MAX_OPS * sizeof(nfk_op));
+    {
+        const nfio_arr* oa = GET(wf, "ops");
+        const int opk = nfio_ops_per_kind(oa);
+        if (opk <= 0 || opk > NFK_MAX_OPS) {
+            fprintf(stderr, "bad ops array\n");
+            exit(2);
+        }
+        for (int k = 0; k < W.NK; k++)
+            memcpy(W.ops[k], (const nfk_op*)oa->data + (size_t)k * opk, (size_t)opk * sizeof(nfk_op));
+    }
     memcpy(W.nops, GET(wf, "n_ops")->data, W.NK * 4);
     for (int k = 0; k < W.NK; k++)
         for (int i = 0; i < W.nops[k]; i++)

@@ -190,13 +190,14 @@ int main(int argc, char** argv) {
     uint8_t* pnames = (uint8_t*)A("prop_names")->data;
     uint8_t* knames = (uint8_t*)A("kind_names")->data;
     nfk_op* ops = (nfk_op*)A("ops")->data;
+    const int OPK = nfio_ops_per_kind(A("ops"));  // ops per kind in the file
     int32_t* nops = (int32_t*)A("n_ops")->data;
     std::vector<std::string> pname(NP), kname(NK), cname = {"NPC", "Player"};
     for (int p = 0; p < NP; p++) pname[p] = cstr(pnames + 32 * p);
     for (int k = 0; k < NK; k++) kname[k] = cstr(knames + 32 * k);
     for (int k = 0; k < NK; k++)
         for (int i = 0; i < nops[k]; i++)
-            if (ops[k * NFK_MAX_OPS + i].code == NFK_OP_RFAFFINE) {
+            if (ops[k * OPK + i].code == NFK_OP_RFAFFINE) {
                 fprintf(stderr, "nf_ref_session: record f64 ops cannot run on the reference (NFCRecord::SetFloat, "
                                 "see nf_ref_harness --repro-record-float)\n");
                 return 3;
@@ -331,7 +332,7 @@ int main(int argc, char** argv) {
             fl.fi_rem.push_back(nCount);
         }
         for (int i = 0; i < nops[k]; i++) {
-            const nfk_op& op = ops[k * NFK_MAX_OPS + i];
+            const nfk_op& op = ops[k * OPK + i];
             if (op.flags & NFK_GUARD) {
                 const int64_t g = km->GetPropertyInt(self, pname[op.guard & 0xFFFF]);
                 const int c = (op.guard >> 16) & 3;

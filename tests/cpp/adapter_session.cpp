@@ -141,6 +141,7 @@ int main(int argc, char** argv) {
     uint8_t* knames = (uint8_t*)A("kind_names")->data;
     uint8_t* pflags = (uint8_t*)A("prop_flags")->data;
     nfk_op* ops = (nfk_op*)A("ops")->data;
+    const int OPK = nfio_ops_per_kind(A("ops"));  // ops per kind in the file
     int32_t* nops = (int32_t*)A("n_ops")->data;
     std::vector<std::string> pname(NP), kname(NK), cname = {"NPC", "Player"};
     for (int p = 0; p < NP; p++) pname[p] = cstr(pnames + 32 * p);
@@ -171,7 +172,7 @@ int main(int argc, char** argv) {
     std::vector<std::string> rname;
     for (int r = 0; r < NR; r++) rname.push_back("rec" + std::to_string(r));
     for (int k = 0; k < NK; k++)
-        kernel.gpu_.AddHeartBeatProgram(kname[k], std::vector<nfk_op>(ops + k * NFK_MAX_OPS, ops + k * NFK_MAX_OPS + nops[k]),
+        kernel.gpu_.AddHeartBeatProgram(kname[k], std::vector<nfk_op>(ops + k * OPK, ops + k * OPK + nops[k]),
                                         pname, rname);
     for (auto* m : all) m->Awake();
     for (auto* m : all) m->Init();

@@ -206,6 +206,7 @@ int main(int argc, char** argv) {
     uint8_t* pnames = (uint8_t*)A("prop_names")->data;
     uint8_t* knames = (uint8_t*)A("kind_names")->data;
     nfk_op* ops = (nfk_op*)A("ops")->data;
+    const int OPK = nfio_ops_per_kind(A("ops"));  // ops per kind in the file
     int32_t* nops = (int32_t*)A("n_ops")->data;
     std::vector<std::string> pname(NP), kname(NK), cname = {"NPC", "Player"};
     for (int p = 0; p < NP; p++) pname[p] = cstr(pnames + 32 * p);
@@ -244,7 +245,7 @@ int main(int argc, char** argv) {
 #ifndef LOGIC_REF
     // each heartbeat name's device effect program (a logic module's Init); OnHeartBeat has none
     for (int k = 0; k < NK; k++)
-        kernel.gpu_.AddHeartBeatProgram(kname[k], std::vector<nfk_op>(ops + k * NFK_MAX_OPS, ops + k * NFK_MAX_OPS + nops[k]),
+        kernel.gpu_.AddHeartBeatProgram(kname[k], std::vector<nfk_op>(ops + k * OPK, ops + k * OPK + nops[k]),
                                         pname, rname);
 #endif
     for (auto* m : all) m->Awake();
@@ -320,7 +321,7 @@ int main(int argc, char** argv) {
 #ifdef LOGIC_REF
         const int k = L.kid.at(name);
         for (int i = 0; i < nops[k]; i++) {
-            const nfk_op& op = ops[k * NFK_MAX_OPS + i];
+            const nfk_op& op = ops[k * OPK + i];
             if (op.code == NFK_OP_IADD_CLAMP) {
                 const std::string& d = pname[op.dst];
                 const int64_t cur = km->GetPropertyInt(self, d);

@@ -37,6 +37,7 @@ int main(int argc, char** argv) {
     uint8_t* knames = (uint8_t*)A("kind_names")->data;
     uint8_t* pflags = (uint8_t*)A("prop_flags")->data;
     nfk_op* ops = (nfk_op*)A("ops")->data;
+    const int OPK = nfio_ops_per_kind(A("ops"));  // ops per kind in the file
     int32_t* nops = (int32_t*)A("n_ops")->data;
 
     NFGPUKernelModule km((int)N);
@@ -70,7 +71,7 @@ int main(int argc, char** argv) {
     }
     for (int k = 0; k < NK; k++) {
         kname[k] = cstr(knames + 32 * k);
-        km.AddHeartBeatProgram(kname[k], std::vector<nfk_op>(ops + k * NFK_MAX_OPS, ops + k * NFK_MAX_OPS + nops[k]));
+        km.AddHeartBeatProgram(kname[k], std::vector<nfk_op>(ops + k * OPK, ops + k * OPK + nops[k]));
     }
     km.Init();
     int64_t* gh = (int64_t*)A("guid_head")->data;

@@ -55,7 +55,7 @@ CASES = {
                         rec_rows=64),
     "records_rows_20": dict(n_obj=777, n_scenes=1, groups_per_scene=3, players_per_group=2, records=True,
                             rec_rows=20),
-    # three record ops (cols 1, 2, then 0) in one program: the k_records<NFK_MAX_OPS, 2> instantiation
+    # three record ops (cols 1, 2, then 0) in one program: the k_records<NFK_MAX_REC_OPS, 2> instantiation
     "records_three_ops": dict(n_obj=2500, n_scenes=2, groups_per_scene=5, players_per_group=5, records=True,
                               rec_rows=64, rec_skill_op=True),
     "one_object": dict(n_obj=1, n_scenes=1, groups_per_scene=1, players_per_group=1, ext_frac=1.0),
