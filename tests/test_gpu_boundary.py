@@ -148,7 +148,7 @@ def test_program_op_validation(gpu_available):
             ops((W.OP_ISET, 0, P["SP"], W.guard(P["Camp"], W.GUARD_GT0), 7, 0, 0)),
             ops((W.OP_ISET, 0, P["X"], 0, 7, 0, 0)),
             ops((W.OP_FSET, W.A_PROP, P["X"], 0, P["HP"], 0, 0)),
-            ops(*[(W.OP_ISET, 0, P["SP"], 0, i, 0, 0)] * 9),
+            ops(*[(W.OP_ISET, 0, P["SP"], 0, 7, 0, 0)] * 9),
         ]
         for a in bad:
             with pytest.raises(kernel.NFKError):
