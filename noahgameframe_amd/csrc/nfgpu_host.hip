@@ -1030,9 +1030,10 @@ void build_jit(World* w) {
         return;
     }
     const int u = std::max(w->d.n_u, 1);
-    // The specialised kernel gets the register budget of 6 waves per SIMD: on config[1] it then
-    // allocates 78 VGPRs without spills, and at 7 (72 VGPRs, 6 spilled) it ran 6 % slower
-    // (profiles/r02t_ab_waves.txt: 101-102 vs 108 us).
+    // The specialised kernel gets the register budget of 5 waves per SIMD (round 4: no spills, and
+    // the fan-out's LDS window grows with the budget): config[1] 82.7-83.7 vs 83.7-84.1 us at 6
+    // (12 VGPRs spilled), 97 at 7, 122 at 8; config[3] 342-344 vs 347-348 us
+    // (profiles/r11j_jit_waves_ab.txt; round 2's r02t_ab_waves.txt chose 6 over 7).
     int waves = (w->d.ablate & (kAblWaves6 | kAblWaves8 | kAblWaves5)) ? tick_waves(w->d.n_u, w->d.ablate) : kWavesJit;
     if (const char* ew = getenv("NFGPU_JIT_WAVES")) waves = std::max(1, std::min(8, atoi(ew)));
     const char* es = getenv("NFGPU_JIT_SPEC");

@@ -186,7 +186,7 @@ constexpr uint32_t kNtSchedLoad = 1, kNtColLoad = 2, kNtEventStore = 4, kNtState
 
 // k_tick register budgets (waves per SIMD) by the frame's U slot count
 constexpr int kWavesU8 = 8, kWavesU12 = 7;
-constexpr int kWavesJit = 6;  // the hipRTC specialisation (nfgpu_jit.hpp)
+constexpr int kWavesJit = 5;  // the hipRTC specialisation (nfgpu_jit.hpp; profiles/r11j_jit_waves_ab.txt)
 constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: at most 4 GiB reserved
 
 // NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
