@@ -285,6 +285,9 @@ struct Dev {
     int32_t fuse_rec;
     uint32_t msg_rb0, msg_rtcap;
     int32_t lds_words; // k_tick's dynamic LDS in 4-byte words (message window + staged players)
+    // xcd_map: k_tick's workgroup b runs tile xcd_tile(b): the workgroups the dispatcher deals to
+    // one XCD (b mod 8) take one contiguous range of tiles (their L2 holds neighbouring tiles)
+    int32_t xcd_map;
     // outputs (tile-staged)
     uint32_t* ev_slot; uint32_t* ev_pid; uint64_t* ev_old; uint64_t* ev_new; uint32_t* ev_moff;
     uint32_t* fi_slot; uint32_t* fi_kind; int32_t* fi_remain;

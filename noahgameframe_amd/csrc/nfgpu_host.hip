@@ -3603,6 +3603,11 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
             lds = std::max(lds, (size_t)(163840 / waves - 2560) & ~(size_t)1023);
         }
         d.lds_words = (int32_t)(lds / 4);
+        {  // XCD-contiguous tiles (Dev::xcd_map; NFGPU_TICK_XCD=0 deals them round-robin):
+           // config[3] 342 -> 331 us, config[1] unchanged (profiles/r11o_ktick_xcd_map_ab.txt)
+            static const int xm = getenv("NFGPU_TICK_XCD") ? atoi(getenv("NFGPU_TICK_XCD")) : 1;
+            d.xcd_map = xm;
+        }
         // the variant whose register slots hold the frame's working set (no spills at 6 or more
         // waves per SIMD): this schema's own k_tick, else a generic instantiation
         const dim3 g((unsigned)d.n_tiles), b(kTPB);

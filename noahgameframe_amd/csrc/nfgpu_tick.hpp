@@ -334,6 +334,12 @@ __device__ void lb_scan_all(const Dev& d, unsigned long long* s_w) {
 // global ranks.
 // kWPE: waves per SIMD the register allocation aims at.  The LDS image of the frame-start values
 // is dynamic: n_w writable slots x kTPB.
+// Dev::xcd_map: workgroup b (dealt to XCD b mod 8) -> a tile of that XCD's contiguous range
+__device__ __forceinline__ int xcd_tile(int b, int n) {
+    const int x = b & 7, i = b >> 3, q = n >> 3, r = n & 7;
+    return x * q + min(x, r) + i;
+}
+
 template <int kWPE, int kU, class S = DynSchema>
 __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8))) void k_tick(Dev d) {
     constexpr int kW = kU < kMaxW ? kU : kMaxW;  // writable register slots
@@ -343,7 +349,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     __shared__ uint32_t s_pb[3];   // pl_slot run of the groups with dirty events [lo, hi), most recipients
     __shared__ uint32_t s_cm[NFK_MAX_CLASSES];  // Dev::u_cmask
     extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
-    const int tile = blockIdx.x;
+    const int tile = d.xcd_map ? xcd_tile((int)blockIdx.x, d.n_tiles) : (int)blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
     if (d.tile_work && !d.tile_work[tile]) {  // (block-uniform) a calls-only pass, no Set group here:
         if (d.has_recops && e < d.N) d.fired_mask[e] = 0;  // nothing fires, nothing is dirty
