@@ -74,6 +74,10 @@ def parse():
                    help="config[1], 1 GPU: also time frames with game-logic SetProperty / schedule calls")
     p.add_argument("--plugin-frame", choices=["auto", "off"], default="auto",
                    help="config[1], 1 GPU: also time the C++ plugin's frame (tests/cpp/plugin_bench)")
+    p.add_argument("--adapter-frame", choices=["auto", "off"], default="auto",
+                   help="config[1], 1 GPU: also time the drop-in path — the reference-side plugin "
+                        "(integration/NFGPUKernelPlugin.cpp) inside the reference's own kernel / AOI / schedule "
+                        "modules (tests/cpp/_ref/adapter_bench) — at config[1] and at config[0]")
     p.add_argument("--config", type=int, default=1, choices=[0, 1, 3, 4],
                    help="BASELINE config: 0 = Tutorial3 at 10k NPCs (the reference's CPU case), "
                         "1 = 1M entities/GPU (the metric's configuration; with --gpus > 1 "
@@ -326,6 +330,12 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = world_from_env(args.gpus)
+    # the drop-in path's config[1] leg builds its 1M host objects through the reference's CreateObject
+    # (minutes of single-threaded host work) while this process runs its GPU legs; it touches the GPU
+    # only when told to go, after them
+    adapter = None
+    if world == 1 and args.config == 1 and args.adapter_frame == "auto" and not args.self_migrate:
+        adapter = AdapterLeg(args)
     import torch
     import torch.distributed as dist
 
@@ -525,6 +535,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0 and world == 1 and args.config == 1 and args.other_configs == "auto" and not args.self_migrate:
         out["configs"] = other_config_legs(args)
+    if adapter is not None:
+        out["adapter_frame"] = {"config1": adapter.finish(), "config0": adapter_config0_run(args)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -564,6 +576,81 @@ def other_config_legs(args):
                          "traffic": rf["traffic"], "traffic_source": rf["traffic_source"]},
             "per_frame": d["per_frame"]}
     return legs
+
+
+ADAPTER_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "adapter_bench")
+
+
+class AdapterLeg:
+    """The drop-in path at config[1]: tests/cpp/_ref/adapter_bench — a NoahGameFrame server with the
+    reference-side plugin (NFGPUKernelAdapter, NFGPUSceneAOIAdapter, NFGPUScheduleAdapter) in
+    NFKernelPlugin's place among the reference's own modules — on the plugin_frame leg's world (1M
+    entities, a heartbeat functor on every schedule, a common property / record callback, the AOI
+    module's recipient-list callbacks).  Started first: it builds its host objects through the
+    reference's CreateObject while this process runs the GPU legs, then waits; finish() lets it
+    commit its world and time its frames on the idle GPU."""
+
+    def __init__(self, args):
+        self.proc, self.err = None, None
+        if not os.path.exists(ADAPTER_EXE):
+            self.err = "tests/cpp/_ref/adapter_bench not built (needs /root/reference at build time)"
+            return
+        from noahgameframe_amd import nfio, workload
+        self.tmp = tempfile.TemporaryDirectory()
+        wp = os.path.join(self.tmp.name, "w.nfio")
+        w = workload.bench_world(n_obj=args.entities, groups=args.groups, players_per_group=args.players_per_group,
+                                 n_ticks=args.warmup + args.steps, tick_ms=args.tick_ms, seed=2031, ext_frac=0.05,
+                                 host_ops=True)
+        nfio.write(wp, w)
+        self.t0 = time.perf_counter()
+        self.errf = open(os.path.join(self.tmp.name, "err.txt"), "w+")
+        self.proc = subprocess.Popen([ADAPTER_EXE, wp, str(args.warmup), str(args.steps), "0", "0", "1"],
+                                     stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=self.errf, text=True)
+
+    def finish(self, timeout=900):
+        if self.proc is None:
+            return {"error": self.err}
+        try:
+            ready = self.proc.stdout.readline()   # (blocks until its host objects are built)
+            self.proc.stdin.write("go\n")
+            self.proc.stdin.flush()
+            out, _ = self.proc.communicate(timeout=max(60.0, timeout - (time.perf_counter() - self.t0)))
+            self.errf.seek(0)
+            err = self.errf.read()
+        except Exception as e:  # (a timeout, or the process died before it was ready)
+            self.proc.kill()
+            self.proc.communicate()
+            return {"error": repr(e)[-300:]}
+        finally:
+            self.errf.close()
+            self.tmp.cleanup()
+        line = [x for x in out.splitlines() if x.startswith("{") and "adapter_frame_ms" in x]
+        if self.proc.returncode != 0 or not line:
+            return {"error": (err or out or ready)[-400:]}
+        return json.loads(line[-1])
+
+
+def adapter_config0_run(args):
+    """The drop-in path at config[0]: Tutorial3 (HelloWorld3Module.cpp) at 10k NPC objects through the
+    reference-side plugin — OnHeartBeat (5 s x 10, functor-only: an empty device program, its timers
+    scanned on the device, the functor on the host), a per-object callback on every object's World
+    property, and OnEvent's SetPropertyInt(self, "World", v) on 1 % of the objects per frame."""
+    if not os.path.exists(ADAPTER_EXE):
+        return {"error": "tests/cpp/_ref/adapter_bench not built"}
+    from noahgameframe_amd import nfio, workload
+    w = workload.tutorial3_world(n_ticks=args.warmup + args.steps, tick_ms=args.tick_ms)
+    with tempfile.TemporaryDirectory() as d:
+        wp = os.path.join(d, "w.nfio")
+        nfio.write(wp, w)
+        try:
+            r = subprocess.run([ADAPTER_EXE, wp, str(args.warmup), str(args.steps), "1"], capture_output=True,
+                               text=True, timeout=600)
+        except subprocess.TimeoutExpired:
+            return {"error": "timeout"}
+    line = [x for x in r.stdout.splitlines() if x.startswith("{") and "adapter_frame_ms" in x]
+    if r.returncode != 0 or not line:
+        return {"error": (r.stderr or r.stdout)[-400:]}
+    return json.loads(line[-1])
 
 
 def plugin_frame_run(args, workload):

@@ -442,6 +442,48 @@ public:
     bool AddPropertyEventCallBack(const PROPERTY_SINGLE_EVENT_FUNCTOR& cb);
     bool AddRecordEventCallBack(const RECORD_SINGLE_EVENT_FUNCTOR& cb);
 
+    // ---- per-Set chains (nfk_watch_props).  The reference fires a property's per-object callbacks
+    // once per accepted Set (NFCProperty::SetInt / SetFloat, PR:254-334); the frame's events are
+    // coalesced per (entity, property).  For the watched properties every Execute also reads the log
+    // of the Sets the frame's heartbeat programs made, ordered as NFCScheduleModule::Execute runs the
+    // functors: objects in NFGUID order, each object's schedules in name (kind id) order, each
+    // program's ops in order (SM:52-80).  LastChain() holds it from the frame hook on. ----
+    struct ChainEntry {
+        int32_t obj, kind, op, pid;  // object index, heartbeat kind, op index in its program, device property id
+        uint64_t old_bits, new_bits;
+    };
+    void WatchProperty(const std::string& name);  // int / float properties; before or after AfterInit
+    const std::vector<ChainEntry>& LastChain() const { return chain_; }
+    // called by Execute once the device frame's outputs are read back, before the heartbeat functors
+    // run: the frame's events (fh) and its chain are final (a reference-side adapter brings its host
+    // objects up to date here, so the functors and their callbacks see the frame's values)
+    void SetFrameHook(std::function<void(const nfk_frame_host&)> hook) { frame_hook_ = std::move(hook); }
+    // One call per event of every device pass, after the common callbacks: the object index, the
+    // event's recipient run (GetBroadCastObject, AOI:531-593) as NFGUIDs — empty for an event with
+    // none — and whether that run equals the last non-empty one passed, so a caller keeps what it
+    // built from it.  A reference-side adapter dispatches the reference's common and AOI callbacks
+    // from here in its own registration order.
+    struct SyncArgs {
+        int32_t obj;
+        const std::vector<NFGUID>* rcpt;
+        bool same;
+    };
+    using PROPERTY_SYNC_FUNCTOR = std::function<void(const NFGUID&, int /*device pid*/, const TData&, const TData&, const SyncArgs&)>;
+    using RECORD_SYNC_FUNCTOR = std::function<void(const NFGUID&, const RECORD_EVENT_DATA&, const TData&, const TData&, const SyncArgs&)>;
+    bool AddPropertySyncCallBack(const PROPERTY_SYNC_FUNCTOR& cb);
+    bool AddRecordSyncCallBack(const RECORD_SYNC_FUNCTOR& cb);
+    // object and schema accessors (object index = creation order in this module)
+    const NFGUID& ObjectGuid(int o) const { return guids_[(size_t)o]; }
+    int ObjectGroup(int o) const { return group_[(size_t)o]; }
+    int ObjectCount() const { return (int)guids_.size(); }
+    const std::string& PropertyName(int dev_pid) const { return props_[(size_t)def_of_pid_[(size_t)dev_pid]].name; }
+    TDATA_TYPE PropertyType(int dev_pid) const { return props_[(size_t)def_of_pid_[(size_t)dev_pid]].type; }
+    const std::string& RecordName(int rec) const { return records_[(size_t)rec].name; }
+    int RecordCount() const { return (int)records_.size(); }
+    int HeartBeatCount() const { return (int)heartbeats_.size(); }
+    // kind k's program with device operand ids (after AfterInit)
+    const std::vector<nfk_op>& HeartBeatOps(int k) const { return heartbeats_[(size_t)k].ops; }
+
     // ---- frame batch consumers: one call per device pass instead of one per event ----
     // The pass's outputs as arrays (nfk_read_frame's nfk_frame_host: the fired list, property and
     // record events, the recipient CSR, all in object-index terms; objects[i] is object i's
@@ -511,6 +553,13 @@ private:
     std::vector<PROPERTY_SINGLE_EVENT_FUNCTOR> aoi_prop_cb_;
     std::vector<RECORD_SINGLE_EVENT_FUNCTOR> aoi_rec_cb_;
     std::vector<FRAME_FUNCTOR> frame_cb_;
+    std::vector<PROPERTY_SYNC_FUNCTOR> sync_prop_cb_;
+    std::vector<RECORD_SYNC_FUNCTOR> sync_rec_cb_;
+    std::function<void(const nfk_frame_host&)> frame_hook_;
+    std::vector<std::string> watch_names_;  // WatchProperty before AfterInit
+    std::vector<int32_t> watch_pids_;
+    std::vector<ChainEntry> chain_;
+    void ReadChain();
     uint32_t frame_what_ = 0;  // union of the frame consumers' NFK_READ_* bits
     uint32_t ReadMask(bool per_event_fired) const;
     // the functor of each (object, kind) schedule: cb_slot_[object * n_kind + kind] indexes

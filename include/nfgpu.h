@@ -338,6 +338,20 @@ int nfk_exist_schedule(void* world, int64_t guid_head, int64_t guid_data, int32_
  * at most cap entries, *n = how many there are */
 int nfk_read_added(void* world, int32_t cap, int32_t* n, int64_t* guid_head, int64_t* guid_data, int32_t* kind);
 
+/* ---- per-Set chains: NFCProperty::SetInt / SetFloat fire a property's per-object callbacks
+ * (NFIKernelModule::AddPropertyCallBack, NFIKernelModule.h:40) once per accepted Set (PR:254-334),
+ * in the order NFCScheduleModule::Execute runs the heartbeat functors (SM:52-80).  The frame's
+ * events are coalesced per (entity, property); for the int / f64 properties named here each
+ * nfk_execute also logs every Set its heartbeat programs make that the change predicates accept:
+ * (object, kind, op index in the kind's program, property, old, new), so a host with per-object
+ * callbacks fires one per Set.  The last Set of an (entity, property) ends at the frame event's new
+ * value.  n = 0 watches nothing (no extra kernel runs). */
+int nfk_watch_props(void* world, int32_t n, const int32_t* pid);
+/* the last nfk_execute's log in device order (sort by (NFGUID, kind, op) for the reference's);
+ * at most cap entries copied, *n = how many there are (nfk_execute_calls fires nothing and keeps it) */
+int nfk_read_chain(void* world, int32_t cap, int32_t* n, int32_t* obj, int32_t* kind, int32_t* op, int32_t* pid,
+                   uint64_t* old_bits, uint64_t* new_bits);
+
 /* ---- one server frame: NFCScheduleModule::Execute (SM:49) + NFCKernelModule::Execute (KM:70)
  * + NFCSceneAOIModule::OnPropertyCommonEvent/GetBroadCastObject fan-out (AOI:227,260,531).
  * Asynchronous on the world's stream. */

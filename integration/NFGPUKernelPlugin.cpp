@@ -8,30 +8,42 @@
 //                         records of the class schema live on the device (nfgpu::NFGPUKernelModule);
 //                         strings, vectors, object lists, scenes and class events stay in the host
 //                         NFCKernelModule.  The schema is read from NFIClassModule in AfterInit.
-//                         The host objects stay a mirror of the device ones (below), so per-object
-//                         callbacks and direct NFIObject / NFIRecord access keep working.
+//   NFGPUSceneAOIAdapter  NFISceneAOIModule as a subclass of the reference's NFCSceneAOIModule: a device
+//                         property / record event reaches its OnPropertyEvent / OnRecordEvent
+//                         (AOI:703-727, the recipient-list callbacks) with the DEVICE's recipient list
+//                         (k_tick / k_records fan-out) — the host's GetBroadCastObject (AOI:531-593) is
+//                         never run for a device event; GroupID / SceneID events still run its
+//                         OnGroupEvent / OnSceneEvent (AOI:233-239); host-only properties (strings,
+//                         vectors) take the reference's own path.
 //   NFGPUScheduleAdapter  NFIScheduleModule (NFIScheduleModule.h:23-39): object schedules whose name
 //                         has a device program on the device; every other schedule (functor-only
 //                         heartbeats, module schedules) on the reference's own NFCScheduleModule.
+//   NFGPUKernelPlugin     the NFIPlugin that registers them (NFKernelPlugin.cpp:40-46 pattern).
 //
-// Host objects as a mirror of the device (NFIKernelModule.h:28-45 AddPropertyCallBack /
-// AddRecordCallBack register on the host NFCObject's NFCProperty / NFCRecord, NFCProperty.h:71):
+// The host NFCObjects are a MIRROR of the device objects, kept up to date lazily:
 //   * every write to a device property or int record cell goes to the HOST object first — through
-//     NFIKernelModule (SetPropertyInt / Float / Object, SetRecordInt, ClearRecord) or straight
-//     through the object (GetObject(self)->SetPropertyInt, FindRecord(self, r)->SetInt / AddRow /
-//     Remove) — so the reference's change predicates and per-object callbacks run at call time as in
-//     the reference; the host common event of that write is forwarded to the device (queued there)
-//     instead of reaching the common callbacks;
-//   * the common callbacks (the AOI module's client sync) receive the device's coalesced frame
-//     events (the dirty-sync list), exactly as before;
-//   * when Execute returns, every (object, property) and int cell that had a device event or a host
-//     write this window is read back from the device and written into the host object where it
-//     differs: the heartbeat programs' effects reach GetObject(self)->Get* and fire the per-object
-//     callbacks (old = the host value, new = the device value).
+//     NFIKernelModule or straight through the object (GetObject(self)->SetPropertyInt,
+//     FindRecord(self, r)->SetInt / AddRow / Remove) — so the reference's change predicates and
+//     per-object callbacks run at call time as in the reference; the host common event of that write
+//     is forwarded to the device queue instead of the common callbacks;
+//   * the common callbacks and the AOI module receive the device's coalesced frame events (the
+//     dirty-sync list) with the device's recipient lists;
+//   * objects with per-object callbacks (NFIKernelModule::AddPropertyCallBack / AddRecordCallBack,
+//     NFIKernelModule.h:28-45, or NFIObject's, seen through the object handle GetObject returns) are
+//     EAGER: after the device frame, before the heartbeat functors run, their callbacks fire once per
+//     accepted Set of the frame's heartbeat programs — the device's per-Set log (nfk_watch_props /
+//     k_chain) — in the order NFCScheduleModule::Execute makes the Sets: objects in NFGUID order, each
+//     object's schedules in name order, each program's ops (and a record op's rows) in order
+//     (SM:52-80); their other evented properties and cells take the frame's values;
+//   * every other object is marked STALE by its events (one byte per event) and brought up to date
+//     from the device the next time the host touches it: GetObject, FindRecord, any write through
+//     NFIKernelModule, SwitchScene.  A frame therefore costs the host nothing per event beyond the
+//     callbacks a server registered, instead of a read-back of every evented (object, property).
+//     SetEagerMirror(true) keeps every object eager (the round-4 behaviour) for a server that holds
+//     NFIObject pointers across frames without going back through GetObject.
 //   f64 record cells are the exception: NFCRecord::SetFloat stores a double into the int64 alternative
 //   of the cell (RC:243-297; tests/test_oracle.py::test_reference_record_setfloat_bug), so they are
 //   device-only (SetRecordFloat / GetRecordFloat through NFIKernelModule read and write the device).
-//   NFGPUKernelPlugin     the NFIPlugin that registers both (NFKernelPlugin.cpp:40-46 pattern).
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -40,12 +52,15 @@
 #include <memory>
 #include <set>
 #include <string>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "NFComm/NFKernelPlugin/NFCEventModule.h"
 #include "NFComm/NFKernelPlugin/NFCKernelModule.h"
 #include "NFComm/NFKernelPlugin/NFCScheduleModule.h"
 #include "NFComm/NFKernelPlugin/NFCSceneAOIModule.h"
+#include "NFComm/NFCore/NFCDataList.h"
 #include "NFComm/NFMessageDefine/NFProtocolDefine.hpp"
 #include "NFComm/NFPluginModule/NFIClassModule.h"
 #include "NFComm/NFPluginModule/NFIPlugin.h"
@@ -68,7 +83,28 @@ NFIDataList::TData to_ref(const nfgpu::TData& v) {
     else if (v.type == nfgpu::TDATA_OBJECT) r.SetObject(to_ref(v.o));
     return r;
 }
+double dbl(uint64_t u) {
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+}
+struct GuidHash {
+    size_t operator()(const NFGUID& g) const { return (size_t)(g.nData64 * 0x9E3779B97F4A7C15ull ^ (uint64_t)g.nHead64); }
+};
 }  // namespace
+
+// What a device event hands the AOI module (NFGPUSceneAOIAdapter): the event and the device's
+// recipient list for it.
+class NFGPUDeviceAOI {
+public:
+    virtual ~NFGPUDeviceAOI() {}
+    virtual void DevicePropertyEvent(const NFGUID& self, const std::string& name, const NFIDataList::TData& oldVar,
+                                     const NFIDataList::TData& newVar, const NFIDataList& to) = 0;
+    virtual void DeviceRecordEvent(const NFGUID& self, const RECORD_EVENT_DATA& ev, const NFIDataList::TData& oldVar,
+                                   const NFIDataList::TData& newVar, const NFIDataList& to) = 0;
+};
+
+class NFGPUObject;
 
 class NFGPUKernelAdapter : public NFCKernelModule {
 public:
@@ -123,7 +159,7 @@ public:
             MirrorRecords(o);
         }
         // host writes of device state -> the device (first in the host common lists: the modules
-        // register their common callbacks in their own AfterInit, after this one)
+        // register their common callbacks in their own Init / AfterInit)
         NFCKernelModule::RegisterCommonPropertyEvent(PROPERTY_EVENT_FUNCTOR_PTR(new PROPERTY_EVENT_FUNCTOR(
             [this](const NFGUID& self, const std::string& name, const NFIDataList::TData&, const NFIDataList::TData& v) {
                 return ForwardProperty(self, name, v);
@@ -132,36 +168,45 @@ public:
             [this](const NFGUID& self, const RECORD_EVENT_DATA& ev, const NFIDataList::TData&, const NFIDataList::TData&) {
                 return ForwardRecord(self, ev);
             })));
-        // the device's frame events -> the common callbacks, and their (object, property / cell) to
-        // the host mirror when Execute returns
-        gpu_.RegisterCommonPropertyEvent(
-            [this](const nfgpu::NFGUID& self, const std::string& name, const nfgpu::TData& a, const nfgpu::TData& b) {
-                const NFGUID s = to_ref(self);
-                for (auto& cb : prop_cb_) (*cb)(s, name, to_ref(a), to_ref(b));
-                sync_props_.emplace_back(s, name);
-                return 0;
-            });
-        gpu_.RegisterCommonRecordEvent(
-            [this](const nfgpu::NFGUID& self, const nfgpu::RECORD_EVENT_DATA& e, const nfgpu::TData& a, const nfgpu::TData& b) {
-                RECORD_EVENT_DATA ev;
-                ev.nOpType = (RECORD_EVENT_DATA::RecordOptype)e.nOpType;
-                ev.nRow = e.nRow;
-                ev.nCol = e.nCol;
-                ev.strRecordName = e.strRecordName;
-                const NFGUID s = to_ref(self);
-                for (auto& cb : rec_cb_) (*cb)(s, ev, to_ref(a), to_ref(b));
-                if (e.nOpType == nfgpu::RECORD_EVENT_DATA::Update && b.type == nfgpu::TDATA_INT)
-                    sync_cells_.push_back({s, e.strRecordName, e.nRow, e.nCol});
-                return 0;
-            });
-        return gpu_.AfterInit();
+        // the device's frame events -> the common callbacks and the AOI module, in registration order
+        gpu_.AddPropertySyncCallBack([this](const nfgpu::NFGUID& g, int pid, const nfgpu::TData& a, const nfgpu::TData& b,
+                                            const nfgpu::NFGPUKernelModule::SyncArgs& sa) { DeliverProperty(g, pid, a, b, sa); });
+        gpu_.AddRecordSyncCallBack([this](const nfgpu::NFGUID& g, const nfgpu::RECORD_EVENT_DATA& e, const nfgpu::TData& a,
+                                          const nfgpu::TData& b, const nfgpu::NFGPUKernelModule::SyncArgs& sa) {
+            DeliverRecord(g, e, a, b, sa);
+        });
+        // the host mirror after the device frame, before the heartbeat functors run
+        gpu_.SetFrameHook([this](const nfk_frame_host& f) { OnFrame(f); });
+        const bool ok = gpu_.AfterInit();
+        // the record op of each (record, column): its kind and op index, the order key of its
+        // per-object callbacks (at most one op per record column, nfgpu.h NFK_MAX_REC_OPS)
+        for (int k = 0; k < gpu_.HeartBeatCount(); k++) {
+            const std::vector<nfk_op>& ops = gpu_.HeartBeatOps(k);
+            for (int i = 0; i < (int)ops.size(); i++)
+                if (ops[i].code == NFK_OP_RIADD_CLAMP || ops[i].code == NFK_OP_RFAFFINE)
+                    rec_op_[ops[i].dst] = std::make_pair(k, i);
+        }
+        for (const std::string& nm : watch_pending_) gpu_.WatchProperty(nm);
+        watch_pending_.clear();
+        return ok;
     }
 
-    bool Execute() override {  // NFCKernelModule::Execute (KM:70) + NFCScheduleModule::Execute (SM:49) + AOI fan-out
-        NFCKernelModule::Execute();
-        const bool ok = gpu_.Execute();
-        SyncHostObjects();
-        return ok;
+    // NFCKernelModule::Execute (KM:70-99) + NFCScheduleModule::Execute (SM:49) + the AOI fan-out.  KM's
+    // walk of every object is kept only for the objects that can have components: NFCObject::Execute
+    // runs the object's components and nothing else (NFCObject.cpp:42-47, NFCComponentManager.cpp:73-85),
+    // and a component is added through the object's component manager (NFIObject::AddComponent), so the
+    // objects whose manager was handed out are walked, in NFGUID order as KM's map walk; the others'
+    // Execute is empty (a walk of 1M host objects costs ~0.7 s per frame).
+    bool Execute() override {
+        ProcessMemFree();
+        if (!mtDeleteSelfList.empty()) {  // KM:76-84
+            for (const NFGUID& g : mtDeleteSelfList) DestroyObject(g);
+            mtDeleteSelfList.clear();
+        }
+        if (NFISceneAOIModule* a = pPluginManager->FindModule<NFISceneAOIModule>()) a->Execute();  // KM:86
+        for (const NFGUID& g : has_components_)
+            if (NF_SHARE_PTR<NFIObject> o = GetElement(g)) o->Execute();
+        return gpu_.Execute();
     }
 
     bool CreateScene(const int nSceneID) override {  // KM:981
@@ -179,12 +224,62 @@ public:
     // the device world with those values (before AfterInit: with the layout; after it: at the start
     // of the next frame).  Rows that creation-time handlers add to a device record after AfterInit
     // are not carried over: the device record starts empty (use AddRow once the object exists).
+    // Returns the object's handle (NFGPUObject).
     NF_SHARE_PTR<NFIObject> CreateObject(const NFGUID& self, const int nSceneID, const int nGroupID,
                                          const std::string& strClassName, const std::string& strConfigIndex,
                                          const NFIDataList& arg) override {
         NF_SHARE_PTR<NFIObject> o = NFCKernelModule::CreateObject(self, nSceneID, nGroupID, strClassName, strConfigIndex, arg);
-        if (o && !dev_props_.empty()) MirrorObject(o);
-        return o;
+        if (!o) return o;
+        if (!dev_props_.empty()) MirrorObject(o);
+        CacheClassName(self, o);
+        return Handle(self, o);
+    }
+
+    // The reference's AOI module asks for a group's players with a ClassName test of every member
+    // (KM:1270-1294 reads each member's ClassName string through an NFGUID map) once per creation-time
+    // Set of an object entering a group (AOI:260 -> 531-593) and once per member in OnGroupEvent
+    // (AOI:357-440): O(group) string lookups per call.  The same answers, faster: the class name of each
+    // object kept beside it (CacheClassName), and a Player list taken from the group's player map — the
+    // objects CreateObject adds as players (KM:146) and every SwitchScene arrival (KM:945), whose
+    // ClassName is still tested — since no object of class Player is ever in the other map.
+    const std::string& GetPropertyString(const NFGUID& self, const std::string& name) override {  // KM:425
+        if (name == NFrame::IObject::ClassName()) {
+            auto it = class_of_.find(self);
+            if (it != class_of_.end()) return *it->second;
+        }
+        return NFCKernelModule::GetPropertyString(self, name);
+    }
+    bool SetPropertyString(const NFGUID& self, const std::string& name, const std::string& v) override {  // KM:349
+        const bool ok = NFCKernelModule::SetPropertyString(self, name, v);
+        if (name == NFrame::IObject::ClassName()) RefreshClassName(self);
+        return ok;
+    }
+    bool GetGroupObjectList(const int scene, const int group, const std::string& cls, const NFGUID& noSelf,
+                            NFIDataList& list) override {  // KM:1270
+        if (cls != NFrame::Player::ThisName()) return NFCKernelModule::GetGroupObjectList(scene, group, cls, noSelf, list);
+        NFCDataList& pl = gl_scratch_;
+        pl.Clear();
+        if (!NFCKernelModule::GetGroupObjectList(scene, group, pl, true)) return false;
+        for (int i = 0; i < pl.GetCount(); i++) {
+            const NFGUID id = pl.Object(i);
+            if (!id.IsNull() && id != noSelf && GetPropertyString(id, NFrame::IObject::ClassName()) == cls) list.AddObject(id);
+        }
+        return true;
+    }
+    bool GetGroupObjectList(const int scene, const int group, const std::string& cls, NFIDataList& list) override {  // KM:1245
+        return GetGroupObjectList(scene, group, cls, NFGUID(), list);
+    }
+    // the object's handle: its device state is brought up to date first
+    NF_SHARE_PTR<NFIObject> GetObject(const NFGUID& ident) override {
+        NF_SHARE_PTR<NFIObject> o = NFCKernelModule::GetObject(ident);
+        if (!o) return o;
+        SyncObject(ident);
+        return Handle(ident, o);
+    }
+    // a record handed out may get hooks and be read later: its object is kept up to date every frame
+    NF_SHARE_PTR<NFIRecord> FindRecord(const NFGUID& self, const std::string& rec) override {  // KM:479
+        if (DevRecord(self, rec)) MarkEager(self);
+        return NFCKernelModule::FindRecord(self, rec);
     }
 
     // the reference's DestroyObject reads SceneID / GroupID through GetPropertyInt (KM:283-284),
@@ -192,12 +287,43 @@ public:
     bool DestroyObject(const NFGUID& self) override {  // KM:273
         const bool ok = NFCKernelModule::DestroyObject(self);
         gpu_.DestroyObject(to_gpu(self));
+        handles_.erase(self);
+        pre_eager_.erase(self);
+        class_of_.erase(self);
+        has_components_.erase(self);
         return ok;
     }
 
-    // SetPropertyInt / Float / Object, SetRecordInt (by column and by tag), ClearRecord: the
-    // reference's own NFCKernelModule on the host object (KM:323-372, 492-544); ForwardProperty /
-    // ForwardRecord queue the accepted writes on the device.
+    // Writes through NFIKernelModule: the reference's own NFCKernelModule on the host object (KM:323-372,
+    // 492-544), its state brought up to date first; ForwardProperty / ForwardRecord queue the accepted
+    // writes on the device.
+    bool SetPropertyInt(const NFGUID& self, const std::string& name, const NFINT64 v) override {  // KM:323
+        SyncObject(self);
+        return NFCKernelModule::SetPropertyInt(self, name, v);
+    }
+    bool SetPropertyFloat(const NFGUID& self, const std::string& name, const double v) override {  // KM:336
+        SyncObject(self);
+        return NFCKernelModule::SetPropertyFloat(self, name, v);
+    }
+    bool SetPropertyObject(const NFGUID& self, const std::string& name, const NFGUID& v) override {  // KM:362
+        SyncObject(self);
+        return NFCKernelModule::SetPropertyObject(self, name, v);
+    }
+    bool SetRecordInt(const NFGUID& self, const std::string& rec, const int nRow, const int nCol, const NFINT64 v) override {
+        SyncObject(self);  // KM:505
+        return NFCKernelModule::SetRecordInt(self, rec, nRow, nCol, v);
+    }
+    bool SetRecordInt(const NFGUID& self, const std::string& rec, const int nRow, const std::string& tag,
+                      const NFINT64 v) override {  // KM:525
+        SyncObject(self);
+        return NFCKernelModule::SetRecordInt(self, rec, nRow, tag, v);
+    }
+    bool ClearRecord(const NFGUID& self, const std::string& rec) override {  // KM:492 (without marking the record handed out)
+        SyncObject(self);
+        NF_SHARE_PTR<NFIObject> o = GetElement(self);
+        NF_SHARE_PTR<NFIRecord> r = o ? o->GetRecordManager()->GetElement(rec) : nullptr;
+        return r ? r->Clear() : false;
+    }
     NFINT64 GetPropertyInt(const NFGUID& self, const std::string& name) override {  // KM:401, read-your-writes
         return DevProp(self, name) ? gpu_.GetPropertyInt(to_gpu(self), name) : NFCKernelModule::GetPropertyInt(self, name);
     }
@@ -245,10 +371,48 @@ public:
         // the host-side scene lists and the host object's SceneID / GroupID / X / Y / Z writes
         // (KM:930-942: its per-object callbacks fire here); the device queues the same writes with
         // the membership change itself, so they are not forwarded
+        SyncObject(self);
         ++quiet_;
         NFCKernelModule::SwitchScene(self, scene, group, fX, fY, fZ, fOrient, arg);
         --quiet_;
         return gpu_.SwitchScene(to_gpu(self), scene, group, fX, fY, fZ, fOrient);
+    }
+
+    // every object eager (the host mirror written every frame): for a server that keeps NFIObject
+    // pointers across frames without going back through GetObject
+    void SetEagerMirror(bool on) {
+        eager_all_ = on;
+        if (on)
+            for (auto& m : mstate_) m |= kEager;
+    }
+    // (measurement) device events that reached NFCSceneAOIModule's common handlers — and so its
+    // GetBroadCastObject — must stay 0; device events handed to the AOI module with the device's list
+    int64_t AOIHostDeviceCalls() const { return aoi_host_device_calls_; }
+    int64_t AOIDeviceCalls() const { return aoi_device_calls_; }
+    int64_t MirrorSyncs() const { return n_syncs_; }  // objects brought up to date lazily
+    int64_t ChainCallbacks() const { return n_chain_fired_; }
+
+    // NFGPUSceneAOIAdapter::Init wraps NFCSceneAOIModule::Init in these: the common callbacks the AOI
+    // module registers meanwhile (AOI.cpp:20-22) get the device's events through `aoi`
+    void BeginAOIRegistration(NFGPUDeviceAOI* aoi) {
+        aoi_ = aoi;
+        aoi_registering_ = true;
+    }
+    void EndAOIRegistration() { aoi_registering_ = false; }
+
+    // (NFGPUObject) the host object is about to be read or written through its handle
+    void Touch(const NFGUID& self) { SyncObject(self); }
+    // (NFGPUObject) its ClassName was written; its component manager was handed out
+    void ClassNameChanged(const NFGUID& self) { RefreshClassName(self); }
+    void HasComponents(const NFGUID& self) { has_components_.insert(self); }
+    // (NFGPUObject) a per-object callback registered on a device property / record, or the object's
+    // managers handed out: the object is eager from now on, a device property's Sets are logged
+    void Watched(const NFGUID& self, const std::string& prop) {
+        MarkEager(self);
+        if (prop.empty() || !dev_props_.count(prop) || watched_.count(prop)) return;
+        watched_.insert(prop);
+        if (gpu_.World()) gpu_.WatchProperty(prop);
+        else watch_pending_.push_back(prop);
     }
 
     nfgpu::NFGPUKernelModule gpu_;
@@ -256,61 +420,85 @@ public:
 protected:
     // Common property / record callbacks (NFIKernelModule.h:181-182): the device's coalesced events
     // for its properties and records (delivered by Execute), the host's for the rest (strings,
-    // vectors, host-only records).  The AOI module registers its OnPropertyCommonEvent /
-    // OnRecordCommonEvent (AOI:227, 260) here, so its client sync runs from the device event list.
+    // vectors, host-only records).  The AOI module's own (registered while BeginAOIRegistration is
+    // on) receive no device event: NFGPUSceneAOIAdapter gets those with the device's recipients.
     bool RegisterCommonPropertyEvent(const PROPERTY_EVENT_FUNCTOR_PTR& cb) override {
+        const bool aoi = aoi_registering_;
         PROPERTY_EVENT_FUNCTOR_PTR host(new PROPERTY_EVENT_FUNCTOR(
-            [this, cb](const NFGUID& self, const std::string& name, const NFIDataList::TData& a, const NFIDataList::TData& b) {
-                return DevProp(self, name) ? 0 : (*cb)(self, name, a, b);
+            [this, cb, aoi](const NFGUID& self, const std::string& name, const NFIDataList::TData& a, const NFIDataList::TData& b) {
+                if (DevProp(self, name)) return 0;
+                if (aoi) ++aoi_host_calls_;
+                return (*cb)(self, name, a, b);
             }));
         NFCKernelModule::RegisterCommonPropertyEvent(host);
-        prop_cb_.push_back(cb);
+        prop_cb_.push_back({cb, aoi});
         return true;
     }
     bool RegisterCommonRecordEvent(const RECORD_EVENT_FUNCTOR_PTR& cb) override {
+        const bool aoi = aoi_registering_;
         RECORD_EVENT_FUNCTOR_PTR host(new RECORD_EVENT_FUNCTOR(
-            [this, cb](const NFGUID& self, const RECORD_EVENT_DATA& ev, const NFIDataList::TData& a, const NFIDataList::TData& b) {
-                return DevRecord(self, ev.strRecordName) ? 0 : (*cb)(self, ev, a, b);
+            [this, cb, aoi](const NFGUID& self, const RECORD_EVENT_DATA& ev, const NFIDataList::TData& a, const NFIDataList::TData& b) {
+                if (DevRecord(self, ev.strRecordName)) return 0;
+                if (aoi) ++aoi_host_calls_;
+                return (*cb)(self, ev, a, b);
             }));
         NFCKernelModule::RegisterCommonRecordEvent(host);
-        rec_cb_.push_back(cb);
+        rec_cb_.push_back({cb, aoi});
         return true;
     }
 
 private:
-    struct Cell {
-        NFGUID self;
-        std::string rec;
-        int row, col;
+    template <class F>
+    struct Common {
+        F cb;
+        bool aoi;  // the AOI module's: device events go to NFGPUSceneAOIAdapter instead
     };
+    enum : uint8_t { kStale = 1, kEager = 2 };
+    // a Set whose per-object callbacks OnFrame fires, keyed (NFGUID of o, kind, op, row)
+    struct Fire {
+        int32_t o, kind, op, row;
+        int64_t i;  // LastChain() index (row < 0) or record event index
+    };
+
+    NF_SHARE_PTR<NFIObject> Handle(const NFGUID& self, const NF_SHARE_PTR<NFIObject>& o);
+    // the object's class name, one shared string per class (see GetPropertyString)
+    void CacheClassName(const NFGUID& self, const NF_SHARE_PTR<NFIObject>& o) {
+        const std::string& c = o->GetPropertyString(NFrame::IObject::ClassName());
+        auto it = class_names_.insert(c).first;
+        class_of_[self] = &*it;
+    }
+    void RefreshClassName(const NFGUID& self) {
+        NF_SHARE_PTR<NFIObject> o = GetElement(self);
+        if (o) CacheClassName(self, o);
+        else class_of_.erase(self);
+    }
 
     // an accepted host write of a device property (NFCProperty::SetInt / SetFloat / SetObject raised
     // the common event): queued on the device in call order
     int ForwardProperty(const NFGUID& self, const std::string& name, const NFIDataList::TData& v) {
-        if (quiet_ || !DevProp(self, name)) return 0;
+        if (quiet_ || OwnWrite(self, name, -1, -1) || !DevProp(self, name)) return 0;
         const nfgpu::NFGUID g = to_gpu(self);
         if (v.GetType() == TDATA_INT) gpu_.SetPropertyInt(g, name, v.GetInt());
         else if (v.GetType() == TDATA_FLOAT) gpu_.SetPropertyFloat(g, name, v.GetFloat());
         else if (v.GetType() == TDATA_OBJECT) gpu_.SetPropertyObject(g, name, to_gpu(v.GetObject()));
-        else return 0;
-        sync_props_.emplace_back(self, name);
         return 0;
     }
     // an accepted host write of a device record (NFCRecord's Update / Add / Cover / Del events,
     // RC:170-177, 225-231, 1092-1098): the same call queued on the device
     int ForwardRecord(const NFGUID& self, const RECORD_EVENT_DATA& ev) {
-        if (quiet_ || !DevRecord(self, ev.strRecordName)) return 0;
-        NF_SHARE_PTR<NFIRecord> r = NFCKernelModule::FindRecord(self, ev.strRecordName);
+        if (quiet_ || (ev.nOpType == RECORD_EVENT_DATA::Update && OwnWrite(self, ev.strRecordName, ev.nRow, ev.nCol)) ||
+            !DevRecord(self, ev.strRecordName))
+            return 0;
+        NF_SHARE_PTR<NFIObject> o = GetElement(self);
+        NF_SHARE_PTR<NFIRecord> r = o ? o->GetRecordManager()->GetElement(ev.strRecordName) : nullptr;
         if (!r) return 0;
         const nfgpu::NFGUID g = to_gpu(self);
         switch (ev.nOpType) {
             case RECORD_EVENT_DATA::Update:
                 // (an f64 cell written on the host holds the double in the int64 alternative and
                 // cannot be read back: f64 record cells are device-only)
-                if (r->GetColType(ev.nCol) == TDATA_INT) {
+                if (r->GetColType(ev.nCol) == TDATA_INT)
                     gpu_.SetRecordInt(g, ev.strRecordName, ev.nRow, ev.nCol, r->GetInt(ev.nRow, ev.nCol));
-                    sync_cells_.push_back({self, ev.strRecordName, ev.nRow, ev.nCol});
-                }
                 break;
             case RECORD_EVENT_DATA::Add:
             case RECORD_EVENT_DATA::Cover: {  // the row as AddRow left it (values already stored)
@@ -332,110 +520,282 @@ private:
         return 0;
     }
 
-    // When Execute returns: the device values of the window's written and evented properties and
-    // int cells, written into the host objects where they differ (one batched device read each);
-    // the host NFCProperty / NFCRecord then fires the per-object callbacks for the difference.
-    void SyncHostObjects() {
-        gpu_.Flush();  // (this reads the world through the C-ABI)
-        std::vector<std::pair<NFGUID, std::string>> props;
-        props.swap(sync_props_);
-        std::vector<Cell> cells;
-        cells.swap(sync_cells_);
-        std::sort(props.begin(), props.end());
-        props.erase(std::unique(props.begin(), props.end()), props.end());
-        std::vector<int64_t> gh, gd, oh;
-        std::vector<int32_t> pid;
-        std::vector<uint64_t> val;
-        std::vector<size_t> at;  // props index of each device read
-        for (size_t i = 0; i < props.size(); i++) {
-            if (!DevProp(props[i].first, props[i].second)) continue;  // (destroyed / left the shard)
-            at.push_back(i);
-            gh.push_back(props[i].first.nHead64);
-            gd.push_back(props[i].first.nData64);
-            pid.push_back(gpu_.PropertyId(props[i].second));
+    // the device's recipient run as the NFIDataList the AOI callbacks take (rebuilt only when the run
+    // differs from the last one: consecutive events of a scene group mostly share it)
+    const NFIDataList& Recipients(const nfgpu::NFGPUKernelModule::SyncArgs& sa) {
+        if (sa.rcpt->empty()) return none_;
+        if (!sa.same || !rl_valid_) {
+            rl_.Clear();
+            for (const nfgpu::NFGUID& g : *sa.rcpt) rl_.Add(to_ref(g));
+            rl_valid_ = true;
         }
-        if (!at.empty()) {
-            // int / f64 words, and the object columns' NFGUIDs (nfk_get_props refuses those)
-            std::vector<size_t> w, o;
-            for (size_t k = 0; k < at.size(); k++) (pid[k] < ObjectBase() ? w : o).push_back(k);
-            val.assign(at.size(), 0);
-            oh.assign(at.size(), 0);
-            auto gather = [&](const std::vector<size_t>& ks, bool obj) {
-                if (ks.empty()) return;
-                std::vector<int64_t> h(ks.size()), d(ks.size()), vh(ks.size()), vd(ks.size());
-                std::vector<int32_t> p(ks.size());
-                std::vector<uint64_t> v(ks.size());
-                for (size_t j = 0; j < ks.size(); j++) {
-                    h[j] = gh[ks[j]];
-                    d[j] = gd[ks[j]];
-                    p[j] = pid[ks[j]];
-                }
-                const int rc = obj ? nfk_get_objects(gpu_.World(), (int32_t)ks.size(), h.data(), d.data(), p.data(), vh.data(), vd.data())
-                                   : nfk_get_props(gpu_.World(), (int32_t)ks.size(), h.data(), d.data(), p.data(), v.data());
-                if (rc != NFK_OK) throw std::runtime_error(std::string("host mirror read: ") + nfk_last_error());
-                for (size_t j = 0; j < ks.size(); j++) {
-                    val[ks[j]] = obj ? (uint64_t)vd[j] : v[j];
-                    oh[ks[j]] = obj ? vh[j] : 0;
-                }
-            };
-            gather(w, false);
-            gather(o, true);
+        return rl_;
+    }
+    // one device property event: the common callbacks in registration order, the AOI module's slot
+    // with the device's recipient list
+    void DeliverProperty(const nfgpu::NFGUID& g, int pid, const nfgpu::TData& a, const nfgpu::TData& b,
+                         const nfgpu::NFGPUKernelModule::SyncArgs& sa) {
+        if (prop_cb_.empty()) return;
+        const NFGUID s = to_ref(g);
+        const std::string& name = gpu_.PropertyName(pid);
+        const NFIDataList::TData ra = to_ref(a), rb = to_ref(b);
+        for (auto& c : prop_cb_) {
+            if (!c.aoi) {
+                (*c.cb)(s, name, ra, rb);
+            } else if (aoi_) {
+                ++aoi_device_calls_;
+                aoi_->DevicePropertyEvent(s, name, ra, rb, Recipients(sa));
+            }
         }
-        ++quiet_;
-        for (size_t k = 0; k < at.size(); k++) {
-            const NFGUID& self = props[at[k]].first;
-            const std::string& name = props[at[k]].second;
+    }
+    void DeliverRecord(const nfgpu::NFGUID& g, const nfgpu::RECORD_EVENT_DATA& e, const nfgpu::TData& a,
+                       const nfgpu::TData& b, const nfgpu::NFGPUKernelModule::SyncArgs& sa) {
+        if (rec_cb_.empty()) return;
+        const NFGUID s = to_ref(g);
+        rev_.nOpType = (RECORD_EVENT_DATA::RecordOptype)e.nOpType;
+        rev_.nRow = e.nRow;
+        rev_.nCol = e.nCol;
+        if (rev_.strRecordName != e.strRecordName) rev_.strRecordName = e.strRecordName;
+        const NFIDataList::TData ra = to_ref(a), rb = to_ref(b);
+        for (auto& c : rec_cb_) {
+            if (!c.aoi) {
+                (*c.cb)(s, rev_, ra, rb);
+            } else if (aoi_ && gpu_.ObjectGroup(sa.obj) >= 0) {  // AOI:270-276: no sync for group < 0
+                ++aoi_device_calls_;
+                aoi_->DeviceRecordEvent(s, rev_, ra, rb, Recipients(sa));
+            }
+        }
+    }
+
+    uint8_t& State(int o) {
+        if ((size_t)o >= mstate_.size()) mstate_.resize((size_t)gpu_.ObjectCount() + 1024, eager_all_ ? kEager : 0);
+        return mstate_[(size_t)o];
+    }
+    void MarkEager(const NFGUID& self) {
+        const int o = gpu_.ObjectIndex(to_gpu(self));
+        if (o < 0) {
+            if (GetElement(self)) pre_eager_.insert(self);  // (being created: applied by MirrorObject)
+            return;
+        }
+        SyncObject(self);
+        State(o) |= kEager;
+    }
+
+    // After the device frame (the frame hook), before the heartbeat functors: eager objects take the
+    // frame's values with their per-object callbacks fired once per accepted Set of the frame's
+    // heartbeat programs in the reference's order; every other evented object is marked stale.
+    void OnFrame(const nfk_frame_host& f) {
+        std::vector<int64_t>& ep = fr_ep_;
+        std::vector<int64_t>& er = fr_er_;
+        ep.clear();
+        er.clear();
+        for (int64_t e = 0; e < f.n_ev; e++) {
+            uint8_t& m = State(f.ev_obj[e]);
+            if (m & kEager) ep.push_back(e);
+            else m |= kStale;
+        }
+        for (int64_t e = 0; e < f.n_re; e++) {
+            uint8_t& m = State(f.re_obj[e]);
+            if (m & kEager) er.push_back(e);
+            else m |= kStale;
+        }
+        if (ep.empty() && er.empty()) return;
+        // the Sets with callbacks, keyed (NFGUID, kind, op, row): the watched properties' per-Set log,
+        // and the record cells a record op changed (one op per record column: at most one change per
+        // cell and frame, so the frame's event is that Set)
+        std::vector<Fire>& fires = fr_fire_;
+        fires.clear();
+        const std::vector<nfgpu::NFGPUKernelModule::ChainEntry>& ch = gpu_.LastChain();
+        for (size_t i = 0; i < ch.size(); i++)
+            if (State(ch[i].obj) & kEager) fires.push_back({ch[i].obj, ch[i].kind, ch[i].op, -1, (int64_t)i});
+        for (int64_t e : er) {
+            const uint32_t rrc = f.re_rrc[e];
+            if ((rrc >> 24) & 3) continue;  // row events: the host record made them (AddRow / Remove / Clear)
+            auto it = rec_op_.find((uint16_t)((((rrc >> 16) & 0xFF) << 8) | (rrc & 0xFF)));
+            if (it == rec_op_.end()) continue;  // a SetRecord cell: the host record holds its value already
+            fires.push_back({f.re_obj[e], it->second.first, it->second.second, (int32_t)((rrc >> 8) & 0xFF), e});
+        }
+        std::stable_sort(fires.begin(), fires.end(), [this](const Fire& x, const Fire& y) {
+            if (x.o != y.o) {
+                const nfgpu::NFGUID &gx = gpu_.ObjectGuid(x.o), &gy = gpu_.ObjectGuid(y.o);
+                return gx < gy;
+            }
+            if (x.kind != y.kind) return x.kind < y.kind;
+            if (x.op != y.op) return x.op < y.op;
+            return x.row < y.row;
+        });
+        for (const Fire& fi : fires) {
+            const NFGUID self = to_ref(gpu_.ObjectGuid(fi.o));
             NF_SHARE_PTR<NFIObject> ob = GetElement(self);
+            if (!ob) continue;
+            if (fi.row < 0) {  // NFCProperty::SetInt / SetFloat of one Set (PR:254-334): its callbacks fire
+                const auto& c = ch[(size_t)fi.i];
+                const std::string& name = gpu_.PropertyName(c.pid);
+                NF_SHARE_PTR<NFIProperty> p = ob->GetPropertyManager()->GetElement(name);
+                if (!p) continue;
+                Mirror(self, name, -1, -1, [&] {
+                    if (p->GetType() == TDATA_INT) p->SetInt((NFINT64)c.new_bits);
+                    else if (p->GetType() == TDATA_FLOAT) p->SetFloat(dbl(c.new_bits));
+                });
+                n_chain_fired_++;
+            } else {  // NFCRecord::SetInt (RC:182)
+                const uint32_t rrc = f.re_rrc[fi.i];
+                const std::string& rn = gpu_.RecordName((int)((rrc >> 16) & 0xFF));
+                NF_SHARE_PTR<NFIRecord> r = ob->GetRecordManager()->GetElement(rn);
+                const int row = (int)((rrc >> 8) & 0xFF), col = (int)(rrc & 0xFF);
+                if (r && r->IsUsed(row) && r->GetColType(col) == TDATA_INT && r->GetInt(row, col) != (NFINT64)f.re_new[fi.i]) {
+                    Mirror(self, rn, row, col, [&] { r->SetInt(row, col, (NFINT64)f.re_new[fi.i]); });
+                    n_chain_fired_++;
+                }
+            }
+        }
+        // the eager objects' other evented properties: the frame's value (an unwatched property has no
+        // per-object callback that could tell the Sets apart)
+        for (int64_t e : ep) {
+            const NFGUID self = to_ref(gpu_.ObjectGuid(f.ev_obj[e]));
+            NF_SHARE_PTR<NFIObject> ob = GetElement(self);
+            const std::string& name = gpu_.PropertyName(f.ev_pid[e]);
             NF_SHARE_PTR<NFIProperty> p = ob ? ob->GetPropertyManager()->GetElement(name) : nullptr;
             if (!p) continue;
-            if (p->GetType() == TDATA_INT) {
-                if (p->GetInt() != (NFINT64)val[k]) p->SetInt((NFINT64)val[k]);
-            } else if (p->GetType() == TDATA_FLOAT) {
-                double v;
-                memcpy(&v, &val[k], 8);
-                const double h = p->GetFloat();
-                if (memcmp(&h, &v, 8) != 0 && !p->SetFloat(v)) {
-                    // (a coalesced change within NFCProperty::SetFloat's 1e-15, PR:314: stored as is)
-                    NFIDataList::TData t;
-                    t.SetFloat(v);
-                    p->SetValue(t);
+            Mirror(self, name, -1, -1, [&] {
+                if (p->GetType() == TDATA_OBJECT) {
+                    const NFGUID v(f.ev_new_h ? (int64_t)f.ev_new_h[e] : 0, (int64_t)f.ev_new[e]);
+                    if (p->GetObject() != v) p->SetObject(v);
+                } else {
+                    PutValue(p, f.ev_new[e]);
                 }
-            } else if (p->GetType() == TDATA_OBJECT) {
-                const NFGUID v(oh[k], (int64_t)val[k]);
-                if (p->GetObject() != v) p->SetObject(v);
+            });
+        }
+        // (record cells: a cell no record op writes changed only through the host record's own calls,
+        // which the host record holds already — the frame's coalesced event of such a cell can carry a
+        // SetRecord value an AddRow later overwrote, nfgpu.h nfk_set_records)
+    }
+    // One write of the mirror: the first host common hook it raises is NFCKernelModule's (registered on
+    // every property / record at creation, KM:166 / KM:186, before any per-object callback) and is the
+    // adapter's own, not forwarded; what the per-object callbacks write meanwhile is forwarded as usual.
+    struct MirrorMark {
+        bool on = false;
+        NFGUID self;
+        const std::string* name = nullptr;
+        int row = -1, col = -1;
+    };
+    template <class F>
+    void Mirror(const NFGUID& self, const std::string& name, int row, int col, F&& f) {
+        mw_.on = true;
+        mw_.self = self;
+        mw_.name = &name;
+        mw_.row = row;
+        mw_.col = col;
+        f();
+        mw_.on = false;
+    }
+    bool OwnWrite(const NFGUID& self, const std::string& name, int row, int col) {
+        if (!mw_.on || self != mw_.self || row != mw_.row || col != mw_.col || name != *mw_.name) return false;
+        mw_.on = false;
+        return true;
+    }
+    // an int / f64 host property set to a device value (bits)
+    static void PutValue(const NF_SHARE_PTR<NFIProperty>& p, uint64_t bits) {
+        if (p->GetType() == TDATA_INT) {
+            if (p->GetInt() != (NFINT64)bits) p->SetInt((NFINT64)bits);
+        } else if (p->GetType() == TDATA_FLOAT) {
+            const double v = dbl(bits), h = p->GetFloat();
+            if (memcmp(&h, &v, 8) != 0 && !p->SetFloat(v)) {
+                // (a coalesced change within NFCProperty::SetFloat's 1e-15, PR:314: stored as is)
+                NFIDataList::TData t;
+                t.SetFloat(v);
+                p->SetValue(t);
             }
         }
-        // int record cells
-        std::sort(cells.begin(), cells.end(), [](const Cell& a, const Cell& b) {
-            return std::tie(a.self, a.rec, a.row, a.col) < std::tie(b.self, b.rec, b.row, b.col);
-        });
-        cells.erase(std::unique(cells.begin(), cells.end(), [](const Cell& a, const Cell& b) {
-            return a.self == b.self && a.rec == b.rec && a.row == b.row && a.col == b.col;
-        }), cells.end());
-        std::vector<int64_t> ch, cd;
+    }
+
+    // A stale object's host mirror brought up to date from the device (its device properties and the
+    // used rows' int cells of its device records, batched device reads), each write quiet for the common
+    // hook.  Nothing of it has a per-object callback (that object would be eager).
+    void SyncObject(const NFGUID& self) {
+        if (!DevObject(self)) return;
+        const int o = gpu_.ObjectIndex(to_gpu(self));
+        if (o < 0 || (size_t)o >= mstate_.size() || !(mstate_[(size_t)o] & kStale)) return;
+        mstate_[(size_t)o] &= (uint8_t)~kStale;
+        NF_SHARE_PTR<NFIObject> ob = GetElement(self);
+        if (!ob) return;
+        n_syncs_++;
+        std::vector<NF_SHARE_PTR<NFIProperty>>& ps = sy_props_;
+        std::vector<int32_t>& pid = sy_pid_;
+        ps.clear();
+        pid.clear();
+        NF_SHARE_PTR<NFIPropertyManager> pm = ob->GetPropertyManager();
+        for (NF_SHARE_PTR<NFIProperty> p = pm->First(); p; p = pm->Next()) {
+            if (!dev_props_.count(p->GetKey())) continue;
+            ps.push_back(p);
+            pid.push_back(gpu_.PropertyId(p->GetKey()));
+        }
+        const int ob0 = gpu_.PropertyCount(nfgpu::TDATA_INT) + gpu_.PropertyCount(nfgpu::TDATA_FLOAT);
+        std::vector<int64_t> h, d, vh, vd;
+        std::vector<int32_t> qp;
+        std::vector<uint64_t> v;
+        for (int pass = 0; pass < 2; pass++) {  // int / f64 words, then the object columns' NFGUIDs
+            h.clear();
+            d.clear();
+            qp.clear();
+            for (size_t i = 0; i < ps.size(); i++)
+                if ((pid[i] >= ob0) == (pass == 1)) {
+                    h.push_back(self.nHead64);
+                    d.push_back(self.nData64);
+                    qp.push_back(pid[i]);
+                }
+            if (qp.empty()) continue;
+            v.assign(qp.size(), 0);
+            vh.assign(qp.size(), 0);
+            vd.assign(qp.size(), 0);
+            gpu_.Flush();
+            const int rc = pass ? nfk_get_objects(gpu_.World(), (int32_t)qp.size(), h.data(), d.data(), qp.data(), vh.data(), vd.data())
+                                : nfk_get_props(gpu_.World(), (int32_t)qp.size(), h.data(), d.data(), qp.data(), v.data());
+            if (rc != NFK_OK) throw std::runtime_error(std::string("host mirror read: ") + nfk_last_error());
+            for (size_t i = 0, j = 0; i < ps.size(); i++) {
+                if ((pid[i] >= ob0) != (pass == 1)) continue;
+                Mirror(self, ps[i]->GetKey(), -1, -1, [&] {
+                    if (pass) {
+                        const NFGUID g(vh[j], vd[j]);
+                        if (ps[i]->GetObject() != g) ps[i]->SetObject(g);
+                    } else {
+                        PutValue(ps[i], v[j]);
+                    }
+                });
+                j++;
+            }
+        }
+        // int cells of the used rows of its device records
+        NF_SHARE_PTR<NFIRecordManager> rm = ob->GetRecordManager();
+        std::vector<NF_SHARE_PTR<NFIRecord>> rs;
         std::vector<int32_t> cr, crow, ccol;
-        std::vector<const Cell*> live;
-        for (const Cell& c : cells) {
-            if (!DevRecord(c.self, c.rec)) continue;
-            live.push_back(&c);
-            ch.push_back(c.self.nHead64);
-            cd.push_back(c.self.nData64);
-            cr.push_back(gpu_.RecordId(c.rec));
-            crow.push_back(c.row);
-            ccol.push_back(c.col);
-        }
-        if (!live.empty()) {
-            std::vector<uint64_t> cv(live.size());
-            if (nfk_get_records(gpu_.World(), (int32_t)live.size(), ch.data(), cd.data(), cr.data(), crow.data(),
-                                ccol.data(), cv.data()) != NFK_OK)
-                throw std::runtime_error(std::string("host mirror read: ") + nfk_last_error());
-            for (size_t k = 0; k < live.size(); k++) {
-                NF_SHARE_PTR<NFIRecord> r = NFCKernelModule::FindRecord(live[k]->self, live[k]->rec);
-                if (r && r->IsUsed(live[k]->row) && r->GetInt(live[k]->row, live[k]->col) != (NFINT64)cv[k])
-                    r->SetInt(live[k]->row, live[k]->col, (NFINT64)cv[k]);
+        h.clear();
+        d.clear();
+        for (NF_SHARE_PTR<NFIRecord> r = rm->First(); r; r = rm->Next()) {
+            if (!dev_records_.count(r->GetName())) continue;
+            const int rid = gpu_.RecordId(r->GetName());
+            for (int row = 0; row < r->GetRows(); row++) {
+                if (!r->IsUsed(row)) continue;
+                for (int c = 0; c < r->GetCols(); c++) {
+                    if (r->GetColType(c) != TDATA_INT) continue;
+                    rs.push_back(r);
+                    h.push_back(self.nHead64);
+                    d.push_back(self.nData64);
+                    cr.push_back(rid);
+                    crow.push_back(row);
+                    ccol.push_back(c);
+                }
             }
         }
-        --quiet_;
+        if (!rs.empty()) {
+            v.assign(rs.size(), 0);
+            if (nfk_get_records(gpu_.World(), (int32_t)rs.size(), h.data(), d.data(), cr.data(), crow.data(), ccol.data(),
+                                v.data()) != NFK_OK)
+                throw std::runtime_error(std::string("host mirror read: ") + nfk_last_error());
+            for (size_t i = 0; i < rs.size(); i++)
+                if (rs[i]->GetInt(crow[i], ccol[i]) != (NFINT64)v[i])
+                    Mirror(self, rs[i]->GetName(), crow[i], ccol[i], [&] { rs[i]->SetInt(crow[i], ccol[i], (NFINT64)v[i]); });
+        }
     }
 
     // the host object's device properties as the device object's creation-time values
@@ -452,8 +812,15 @@ private:
             init[p->GetKey()] = v;
         }
         const std::string cls = o->GetPropertyString(NFrame::IObject::ClassName());
-        gpu_.CreateObject(to_gpu(o->Self()), (int)o->GetPropertyInt(NFrame::IObject::SceneID()),
+        const NFGUID self = o->Self();
+        gpu_.CreateObject(to_gpu(self), (int)o->GetPropertyInt(NFrame::IObject::SceneID()),
                           (int)o->GetPropertyInt(NFrame::IObject::GroupID()), cls, init);
+        const int idx = gpu_.ObjectIndex(to_gpu(self));
+        if (idx >= 0) {
+            uint8_t& m = State(idx);
+            m = eager_all_ || pre_eager_.count(self) ? kEager : 0;
+            pre_eager_.erase(self);
+        }
     }
     // (before AfterInit) the rows the host object's device records already hold: their state at frame 0
     void MirrorRecords(const NF_SHARE_PTR<NFIObject>& o) {
@@ -484,20 +851,14 @@ private:
     // one of the device's; an object being created (before MirrorObject) is the host's alone, so the
     // class-event handlers and the AOI module's creation-time reads and writes (KM:146-267, AOI:227-258)
     // see the host object, exactly as in the reference, and its final values enter the device.
-    bool DevProp(const NFGUID& self, const std::string& name) const {
-        return dev_props_.count(name) && gpu_.ObjectIndex(to_gpu(self)) >= 0;
-    }
-    bool DevRecord(const NFGUID& self, const std::string& rec) const {
-        return dev_records_.count(rec) && gpu_.ObjectIndex(to_gpu(self)) >= 0;
-    }
+    bool DevObject(const NFGUID& self) const { return gpu_.ObjectIndex(to_gpu(self)) >= 0; }
+    bool DevProp(const NFGUID& self, const std::string& name) const { return dev_props_.count(name) && DevObject(self); }
+    bool DevRecord(const NFGUID& self, const std::string& rec) const { return dev_records_.count(rec) && DevObject(self); }
     int ColOf(const std::string& rec, const std::string& tag) const {  // NFCRecord::GetCol (RC:1319)
         auto r = col_tags_.find(rec);
         if (r == col_tags_.end()) return -1;
         auto c = r->second.find(tag);
         return c == r->second.end() ? -1 : c->second;
-    }
-    int ObjectBase() const {  // the first object property id (int, then float, then object ids)
-        return gpu_.PropertyCount(nfgpu::TDATA_INT) + gpu_.PropertyCount(nfgpu::TDATA_FLOAT);
     }
 
     NFIClassModule* m_pClassModule = nullptr;
@@ -505,11 +866,180 @@ private:
     std::map<std::string, std::map<std::string, int>> col_tags_;
     std::set<int> scenes_;
     NFGUID obj_scratch_;
-    int quiet_ = 0;  // > 0: host writes are the adapter's own (mirror, SwitchScene), not forwarded
-    std::vector<PROPERTY_EVENT_FUNCTOR_PTR> prop_cb_;
-    std::vector<RECORD_EVENT_FUNCTOR_PTR> rec_cb_;
-    std::vector<std::pair<NFGUID, std::string>> sync_props_;  // this window's written / evented pairs
-    std::vector<Cell> sync_cells_;
+    int quiet_ = 0;  // > 0: host writes are the adapter's own (SwitchScene), not forwarded
+    MirrorMark mw_;
+    std::vector<Common<PROPERTY_EVENT_FUNCTOR_PTR>> prop_cb_;
+    std::vector<Common<RECORD_EVENT_FUNCTOR_PTR>> rec_cb_;
+    NFGPUDeviceAOI* aoi_ = nullptr;
+    bool aoi_registering_ = false;
+    int64_t aoi_host_calls_ = 0, aoi_host_device_calls_ = 0, aoi_device_calls_ = 0;
+    int64_t n_syncs_ = 0, n_chain_fired_ = 0;
+    NFCDataList rl_, none_;  // the recipient list last built, and the empty one
+    bool rl_valid_ = false;
+    RECORD_EVENT_DATA rev_;
+    // host mirror state per device object index (kStale / kEager), objects made eager before they
+    // reached the device, watched device properties
+    std::vector<uint8_t> mstate_;
+    std::unordered_set<NFGUID, GuidHash> pre_eager_;
+    bool eager_all_ = false;
+    std::set<std::string> watched_;
+    std::vector<std::string> watch_pending_;
+    std::map<uint16_t, std::pair<int, int>> rec_op_;  // (rec << 8 | col) -> (kind, op index)
+    std::unordered_map<NFGUID, NF_SHARE_PTR<NFIObject>, GuidHash> handles_;
+    std::set<std::string> class_names_;
+    std::unordered_map<NFGUID, const std::string*, GuidHash> class_of_;
+    NFCDataList gl_scratch_;
+    std::set<NFGUID> has_components_;  // objects whose component manager was handed out (Execute walks them)
+    // (scratch kept across frames)
+    std::vector<int64_t> fr_ep_, fr_er_;
+    std::vector<Fire> fr_fire_;
+    std::vector<NF_SHARE_PTR<NFIProperty>> sy_props_;
+    std::vector<int32_t> sy_pid_;
+};
+
+// The object handle NFGPUKernelAdapter hands out (GetObject, CreateObject): the host NFCObject behind
+// it, brought up to date from the device before any read or write; a per-object callback registered
+// through it (NFIObject::AddPropertyCallBack / AddRecordCallBack, NFIObject.h:155-157 — what
+// NFIKernelModule::AddPropertyCallBack calls, NFIKernelModule.h:40-45) makes the object eager and its
+// device property watched (per-Set callbacks, see the header).  Its managers handed out make it eager.
+class NFGPUObject : public NFIObject {
+public:
+    NFGPUObject(NFGPUKernelAdapter* k, const NFGUID& self, const NF_SHARE_PTR<NFIObject>& in)
+        : NFIObject(self), k_(k), self_(self), in_(in) {}
+    NFIObject* Inner() const { return in_.get(); }
+
+    bool Execute() override { return in_->Execute(); }
+    NFGUID Self() override { return self_; }
+    CLASS_OBJECT_EVENT GetState() override { return in_->GetState(); }
+    bool SetState(const CLASS_OBJECT_EVENT e) override { return in_->SetState(e); }
+    bool FindProperty(const std::string& n) override { return in_->FindProperty(n); }
+
+    bool SetPropertyInt(const std::string& n, const NFINT64 v) override { return T()->SetPropertyInt(n, v); }
+    bool SetPropertyFloat(const std::string& n, const double v) override { return T()->SetPropertyFloat(n, v); }
+    bool SetPropertyString(const std::string& n, const std::string& v) override {
+        const bool ok = T()->SetPropertyString(n, v);
+        if (n == NFrame::IObject::ClassName()) k_->ClassNameChanged(self_);
+        return ok;
+    }
+    bool SetPropertyObject(const std::string& n, const NFGUID& v) override { return T()->SetPropertyObject(n, v); }
+    bool SetPropertyVector2(const std::string& n, const NFVector2& v) override { return T()->SetPropertyVector2(n, v); }
+    bool SetPropertyVector3(const std::string& n, const NFVector3& v) override { return T()->SetPropertyVector3(n, v); }
+    NFINT64 GetPropertyInt(const std::string& n) override { return T()->GetPropertyInt(n); }
+    double GetPropertyFloat(const std::string& n) override { return T()->GetPropertyFloat(n); }
+    const std::string& GetPropertyString(const std::string& n) override { return in_->GetPropertyString(n); }
+    const NFGUID& GetPropertyObject(const std::string& n) override { return T()->GetPropertyObject(n); }
+    const NFVector2& GetPropertyVector2(const std::string& n) override { return in_->GetPropertyVector2(n); }
+    const NFVector3& GetPropertyVector3(const std::string& n) override { return in_->GetPropertyVector3(n); }
+
+    bool FindRecord(const std::string& r) override { return in_->FindRecord(r); }
+    bool SetRecordInt(const std::string& r, const int row, const int col, const NFINT64 v) override { return T()->SetRecordInt(r, row, col, v); }
+    bool SetRecordFloat(const std::string& r, const int row, const int col, const double v) override { return T()->SetRecordFloat(r, row, col, v); }
+    bool SetRecordString(const std::string& r, const int row, const int col, const std::string& v) override { return in_->SetRecordString(r, row, col, v); }
+    bool SetRecordObject(const std::string& r, const int row, const int col, const NFGUID& v) override { return in_->SetRecordObject(r, row, col, v); }
+    bool SetRecordVector2(const std::string& r, const int row, const int col, const NFVector2& v) override { return in_->SetRecordVector2(r, row, col, v); }
+    bool SetRecordVector3(const std::string& r, const int row, const int col, const NFVector3& v) override { return in_->SetRecordVector3(r, row, col, v); }
+    bool SetRecordInt(const std::string& r, const int row, const std::string& t, const NFINT64 v) override { return T()->SetRecordInt(r, row, t, v); }
+    bool SetRecordFloat(const std::string& r, const int row, const std::string& t, const double v) override { return T()->SetRecordFloat(r, row, t, v); }
+    bool SetRecordString(const std::string& r, const int row, const std::string& t, const std::string& v) override { return in_->SetRecordString(r, row, t, v); }
+    bool SetRecordObject(const std::string& r, const int row, const std::string& t, const NFGUID& v) override { return in_->SetRecordObject(r, row, t, v); }
+    bool SetRecordVector2(const std::string& r, const int row, const std::string& t, const NFVector2& v) override { return in_->SetRecordVector2(r, row, t, v); }
+    bool SetRecordVector3(const std::string& r, const int row, const std::string& t, const NFVector3& v) override { return in_->SetRecordVector3(r, row, t, v); }
+    NFINT64 GetRecordInt(const std::string& r, const int row, const int col) override { return T()->GetRecordInt(r, row, col); }
+    double GetRecordFloat(const std::string& r, const int row, const int col) override { return T()->GetRecordFloat(r, row, col); }
+    const std::string& GetRecordString(const std::string& r, const int row, const int col) override { return in_->GetRecordString(r, row, col); }
+    const NFGUID& GetRecordObject(const std::string& r, const int row, const int col) override { return in_->GetRecordObject(r, row, col); }
+    const NFVector2& GetRecordVector2(const std::string& r, const int row, const int col) override { return in_->GetRecordVector2(r, row, col); }
+    const NFVector3& GetRecordVector3(const std::string& r, const int row, const int col) override { return in_->GetRecordVector3(r, row, col); }
+    NFINT64 GetRecordInt(const std::string& r, const int row, const std::string& t) override { return T()->GetRecordInt(r, row, t); }
+    double GetRecordFloat(const std::string& r, const int row, const std::string& t) override { return T()->GetRecordFloat(r, row, t); }
+    const std::string& GetRecordString(const std::string& r, const int row, const std::string& t) override { return in_->GetRecordString(r, row, t); }
+    const NFGUID& GetRecordObject(const std::string& r, const int row, const std::string& t) override { return in_->GetRecordObject(r, row, t); }
+    const NFVector2& GetRecordVector2(const std::string& r, const int row, const std::string& t) override { return in_->GetRecordVector2(r, row, t); }
+    const NFVector3& GetRecordVector3(const std::string& r, const int row, const std::string& t) override { return in_->GetRecordVector3(r, row, t); }
+
+    // handed out: whatever is registered on or read from them later, the object stays current
+    NF_SHARE_PTR<NFIRecordManager> GetRecordManager() override {
+        k_->Watched(self_, "");
+        return in_->GetRecordManager();
+    }
+    NF_SHARE_PTR<NFIPropertyManager> GetPropertyManager() override {
+        k_->Watched(self_, "");
+        return in_->GetPropertyManager();
+    }
+    NF_SHARE_PTR<NFIComponentManager> GetComponentManager() override {  // (components run in KM's walk)
+        k_->HasComponents(self_);
+        return in_->GetComponentManager();
+    }
+    // (what NFCObject::AddRecordCallBack / AddPropertyCallBack do, NFCObject.cpp:49-73: NFIObject
+    // declares them protected)
+    bool AddRecordCallBack(const std::string& r, const RECORD_EVENT_FUNCTOR_PTR& cb) override {
+        k_->Watched(self_, "");
+        NF_SHARE_PTR<NFIRecord> rec = in_->GetRecordManager()->GetElement(r);
+        if (!rec) return false;
+        rec->AddRecordHook(cb);
+        return true;
+    }
+    bool AddPropertyCallBack(const std::string& p, const PROPERTY_EVENT_FUNCTOR_PTR& cb) override {
+        k_->Watched(self_, p);
+        NF_SHARE_PTR<NFIProperty> prop = in_->GetPropertyManager()->GetElement(p);
+        if (!prop) return false;
+        prop->RegisterCallback(cb);
+        return true;
+    }
+
+private:
+    NFIObject* T() {  // (the host object, current)
+        k_->Touch(self_);
+        return in_.get();
+    }
+    NFGPUKernelAdapter* k_;
+    NFGUID self_;
+    NF_SHARE_PTR<NFIObject> in_;
+};
+
+NF_SHARE_PTR<NFIObject> NFGPUKernelAdapter::Handle(const NFGUID& self, const NF_SHARE_PTR<NFIObject>& o) {
+    auto it = handles_.find(self);
+    if (it != handles_.end() && static_cast<NFGPUObject*>(it->second.get())->Inner() == o.get()) return it->second;
+    NF_SHARE_PTR<NFIObject> h(new NFGPUObject(this, self, o));
+    handles_[self] = h;
+    return h;
+}
+
+// NFISceneAOIModule (NFISceneAOIModule.h) as the reference's NFCSceneAOIModule, with device events
+// taken from the device frame: OnPropertyCommonEvent / OnRecordCommonEvent (AOI:227-288) without
+// GetBroadCastObject — the device computed the recipient list (k_tick / k_records fan-out of
+// GetBroadCastObject's rules, AOI:531-593) — straight to the protected OnPropertyEvent / OnRecordEvent
+// (AOI:703-727), which call the AddPropertyEventCallBack / AddRecordEventCallBack functors.
+class NFGPUSceneAOIAdapter : public NFCSceneAOIModule, public NFGPUDeviceAOI {
+public:
+    explicit NFGPUSceneAOIAdapter(NFIPluginManager* p) : NFCSceneAOIModule(p) {}
+    bool Init() override {
+        // the common callbacks NFCSceneAOIModule::Init registers (AOI.cpp:20-22) are marked as this
+        // module's: the kernel adapter hands device events to DevicePropertyEvent / DeviceRecordEvent
+        kernel_ = dynamic_cast<NFGPUKernelAdapter*>(pPluginManager->FindModule<NFIKernelModule>());
+        if (kernel_) kernel_->BeginAOIRegistration(this);
+        const bool ok = NFCSceneAOIModule::Init();
+        if (kernel_) kernel_->EndAOIRegistration();
+        return ok;
+    }
+    // AOI:227-256 for a device property: GroupID / SceneID run the enter / leave handlers; a device
+    // object has finished its creation (the COE_CREATE_FINISH test of AOI:240-247 holds); an empty
+    // list makes no call (AOI:250)
+    void DevicePropertyEvent(const NFGUID& self, const std::string& name, const NFIDataList::TData& oldVar,
+                             const NFIDataList::TData& newVar, const NFIDataList& to) override {
+        if (NFrame::Player::GroupID() == name) OnGroupEvent(self, name, oldVar, newVar);
+        if (NFrame::Player::SceneID() == name) OnSceneEvent(self, name, oldVar, newVar);
+        if (to.GetCount() <= 0) return;
+        OnPropertyEvent(self, name, oldVar, newVar, to);
+    }
+    // AOI:260-288 for a device record (the kernel adapter applied the GroupID < 0 test, AOI:270-276)
+    void DeviceRecordEvent(const NFGUID& self, const RECORD_EVENT_DATA& ev, const NFIDataList::TData& oldVar,
+                           const NFIDataList::TData& newVar, const NFIDataList& to) override {
+        OnRecordEvent(self, ev.strRecordName, ev, oldVar, newVar, to);
+    }
+
+private:
+    NFGPUKernelAdapter* kernel_ = nullptr;
 };
 
 class NFGPUScheduleAdapter : public NFIScheduleModule {
@@ -565,7 +1095,7 @@ public:
     const int GetPluginVersion() override { return 0; }
     const std::string GetPluginName() override { return GET_CLASS_NAME(NFGPUKernelPlugin); }
     void Install() override {
-        REGISTER_MODULE(pPluginManager, NFISceneAOIModule, NFCSceneAOIModule)  // enter / leave, client sync
+        REGISTER_MODULE(pPluginManager, NFISceneAOIModule, NFGPUSceneAOIAdapter)  // enter / leave, client sync
         REGISTER_MODULE(pPluginManager, NFIKernelModule, NFGPUKernelAdapter)
         REGISTER_MODULE(pPluginManager, NFIEventModule, NFCEventModule)
         REGISTER_MODULE(pPluginManager, NFIScheduleModule, NFGPUScheduleAdapter)
@@ -574,7 +1104,7 @@ public:
         UNREGISTER_MODULE(pPluginManager, NFIScheduleModule, NFGPUScheduleAdapter)
         UNREGISTER_MODULE(pPluginManager, NFIEventModule, NFCEventModule)
         UNREGISTER_MODULE(pPluginManager, NFIKernelModule, NFGPUKernelAdapter)
-        UNREGISTER_MODULE(pPluginManager, NFISceneAOIModule, NFCSceneAOIModule)
+        UNREGISTER_MODULE(pPluginManager, NFISceneAOIModule, NFGPUSceneAOIAdapter)
     }
 };
 

@@ -277,6 +277,13 @@ struct World {
     unsigned* err_pin = nullptr;
     hipEvent_t err_done = nullptr;
     int32_t max_np = 0;    // most players in one scene group (an upper bound between full re-layouts)
+    // per-Set chains of the watched properties (nfk_watch_props, k_chain): the watch mask, the log
+    // of the last nfk_execute (ChainEnt records, its count on the device) and whether that frame ran it
+    uint64_t chain_watch[2] = {0, 0};
+    ChainEnt* chain_d = nullptr;
+    uint32_t* chain_cnt_d = nullptr;
+    size_t chain_cap = 0;  // records
+    bool chain_ran = false;
 
     bool profiling = false;
     std::vector<PendingTiming> pend;
@@ -1704,6 +1711,8 @@ int nfk_destroy(void* world) {
     if (w->look_stream) (void)hipStreamDestroy(w->look_stream);
     if (w->gat) (void)hipFree(w->gat);
     if (w->hf_buf) (void)hipFree(w->hf_buf);
+    if (w->chain_d) (void)hipFree(w->chain_d);
+    if (w->chain_cnt_d) (void)hipFree(w->chain_cnt_d);
     for (auto& p : w->pend) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -2787,6 +2796,46 @@ int nfk_exist_schedule(void* world, int64_t gh, int64_t gd, int32_t kind, int32_
     return NFK_OK;
 }
 
+int nfk_watch_props(void* world, int32_t n, const int32_t* pid) {
+    World* w = (World*)world;
+    if (!w || n < 0 || (n && !pid)) return fail(NFK_ERR_ARG, "null argument");
+    uint64_t m[2] = {0, 0};
+    for (int32_t i = 0; i < n; i++) {
+        if (pid[i] < 0 || pid[i] >= w->n_if) return fail(NFK_ERR_ARG, "nfk_watch_props: not an int / f64 property");
+        m[pid[i] >> 6] |= 1ull << (pid[i] & 63);
+    }
+    w->chain_watch[0] = m[0];
+    w->chain_watch[1] = m[1];
+    return NFK_OK;
+}
+
+int nfk_read_chain(void* world, int32_t cap, int32_t* n, int32_t* obj, int32_t* kind, int32_t* op, int32_t* pid,
+                   uint64_t* old_bits, uint64_t* new_bits) {
+    World* w = (World*)world;
+    if (!w || !n || cap < 0) return fail(NFK_ERR_ARG, "null argument");
+    *n = 0;
+    if (!w->chain_ran) return NFK_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    uint32_t cnt = 0;
+    HIPCHK(hipMemcpy(&cnt, w->chain_cnt_d, sizeof(cnt), hipMemcpyDeviceToHost));
+    if (cnt > w->chain_cap) return fail(NFK_ERR_CAPACITY, "per-Set chain log overflow");
+    *n = (int32_t)cnt;
+    const uint32_t m = std::min<uint32_t>(cnt, (uint32_t)cap);
+    if (!m) return NFK_OK;
+    if (!obj || !kind || !op || !pid || !old_bits || !new_bits) return fail(NFK_ERR_ARG, "null argument");
+    std::vector<ChainEnt> h(m);
+    HIPCHK(hipMemcpy(h.data(), w->chain_d, (size_t)m * sizeof(ChainEnt), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < m; i++) {
+        obj[i] = w->obj_of_slot[h[i].slot];
+        kind[i] = h[i].kind;
+        op[i] = h[i].op;
+        pid[i] = h[i].pid;
+        old_bits[i] = h[i].old_bits;
+        new_bits[i] = h[i].new_bits;
+    }
+    return NFK_OK;
+}
+
 int nfk_read_added(void* world, int32_t cap, int32_t* n, int64_t* gh, int64_t* gd, int32_t* kind) {
     World* w = (World*)world;
     if (!w || !n || cap < 0 || (cap && (!gh || !gd || !kind))) return fail(NFK_ERR_ARG, "null argument");
@@ -3593,6 +3642,43 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
     }
     w->last_tcap = d.msg_tcap;
     w->last_rtcap = d.fuse_rec ? d.msg_rtcap : 0u;
+    // per-Set chains of the watched properties: the programs re-run read-only before k_tick
+    // (k_chain); a calls-only pass fires nothing and keeps the frame's log
+    if (!calls_only) w->chain_ran = false;
+    if (!calls_only && (w->chain_watch[0] | w->chain_watch[1]) && d.N) {
+        uint32_t kinds = 0;
+        int64_t wops = 0;  // (kind, op) pairs whose destination is watched: a bound of the log per slot
+        for (int k = 0; k < d.n_kind; k++)
+            for (int i = 0; i < w->tab.nops[k]; i++) {
+                const nfk_op& op = w->tab.ops[k][i];
+                const bool prop_op = op.code == NFK_OP_IADD_CLAMP || op.code == NFK_OP_FLERP ||
+                                     op.code == NFK_OP_FAFFINE || op.code == NFK_OP_ISET || op.code == NFK_OP_FSET;
+                if (prop_op && op.dst < 128 && ((w->chain_watch[op.dst >> 6] >> (op.dst & 63)) & 1)) {
+                    kinds |= 1u << k;
+                    wops++;
+                }
+            }
+        if (kinds) {
+            const size_t need = (size_t)d.N * (size_t)wops;
+            if (need > w->chain_cap) {
+                HIPCHK(hipStreamSynchronize(w->stream));
+                if (w->chain_d) HIPCHK(hipFree(w->chain_d));
+                w->chain_d = nullptr;
+                w->chain_cap = 0;
+                if (hipMalloc(&w->chain_d, need * sizeof(ChainEnt)) != hipSuccess)
+                    return drop_window(w, fail(NFK_ERR_CAPACITY, "hipMalloc (per-Set chain log)"));
+                w->chain_cap = need;
+            }
+            if (!w->chain_cnt_d) HIPCHK(hipMalloc(&w->chain_cnt_d, sizeof(uint32_t)));
+            TimeScope ts(w, KT_AUX);
+            HIPCHK(hipMemsetAsync(w->chain_cnt_d, 0, sizeof(uint32_t), w->stream));
+            hipLaunchKernelGGL(k_chain, dim3((unsigned)((d.N + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, d,
+                               w->chain_d, w->chain_cnt_d, (uint32_t)std::min<size_t>(w->chain_cap, 0xFFFFFFFFu), kinds,
+                               w->chain_watch[0], w->chain_watch[1]);
+            HIPCHK(hipGetLastError());
+            w->chain_ran = true;
+        }
+    }
     if (d.n_tiles) {
         TimeScope ts(w, KT_TICK);
         size_t lds = (size_t)std::max(d.n_w, 1) * kTPB * 8 + (size_t)std::max(d.n_kind, 1) * kTPB * 4;

@@ -463,7 +463,14 @@ struct Ent {
 // program at once (independent loads, one memory round trip); pass 2 runs the ops in order,
 // reading a property from the frame's written-property list when an earlier op (or kind, or
 // queued SetProperty) wrote it, else from the prefetched column value.
-__device__ __forceinline__ void run_program_chunk(Ent& en, const Tables* __restrict__ tab, int k, int i0, int n) {
+// Log: called with (kind, op, property, old, new) for every Set the predicates accept (k_chain's
+// per-Set log; k_tick_touch passes the empty one, which compiles away).
+struct NoChainLog {
+    __device__ __forceinline__ void operator()(int, int, uint32_t, uint64_t, uint64_t) const {}
+};
+template <class Log = NoChainLog>
+__device__ __forceinline__ void run_program_chunk(Ent& en, const Tables* __restrict__ tab, int k, int i0, int n,
+                                                  const Log& log = Log()) {
     uint64_t pre[4][5];  // dst, a, b, c, guard
 #pragma unroll
     for (int ii = 0; ii < 4; ii++) {
@@ -510,7 +517,10 @@ __device__ __forceinline__ void run_program_chunk(Ent& en, const Tables* __restr
             int64_t v = (int64_t)((uint64_t)cur + (uint64_t)a);
             v = v < lo ? lo : v;
             v = v > hi ? hi : v;
-            if (v != cur) en.tput(op.dst, (uint64_t)cur, (uint64_t)v);  // NFCProperty::SetInt (PR:273)
+            if (v != cur) {  // NFCProperty::SetInt (PR:273)
+                en.tput(op.dst, (uint64_t)cur, (uint64_t)v);
+                log(k, i, op.dst, (uint64_t)cur, (uint64_t)v);
+            }
         } else if (op.code == NFK_OP_FLERP || op.code == NFK_OP_FAFFINE) {
             uint64_t t;
             const double x = __longlong_as_double((long long)(en.tget(op.dst, t) ? t : pre[ii][0]));
@@ -524,8 +534,10 @@ __device__ __forceinline__ void run_program_chunk(Ent& en, const Tables* __restr
                 const double m = x * __longlong_as_double(op.a);
                 v = m + __longlong_as_double(op.b);
             }
-            if (!(fabs(v - x) <= 1e-15))  // NFCProperty::SetFloat (PR:314): IsZeroDouble(v - cur)
+            if (!(fabs(v - x) <= 1e-15)) {  // NFCProperty::SetFloat (PR:314): IsZeroDouble(v - cur)
                 en.tput(op.dst, (uint64_t)__double_as_longlong(x), (uint64_t)__double_as_longlong(v));
+                log(k, i, op.dst, (uint64_t)__double_as_longlong(x), (uint64_t)__double_as_longlong(v));
+            }
         } else if (op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) {
             uint64_t t;
             const uint64_t cur = en.tget(op.dst, t) ? t : pre[ii][0];
@@ -533,18 +545,22 @@ __device__ __forceinline__ void run_program_chunk(Ent& en, const Tables* __restr
             const bool set = op.code == NFK_OP_ISET
                                  ? r != cur  // NFCProperty::SetInt (PR:273)
                                  : !(fabs(__longlong_as_double((long long)r) - __longlong_as_double((long long)cur)) <= 1e-15);
-            if (set) en.tput(op.dst, cur, r);
+            if (set) {
+                en.tput(op.dst, cur, r);
+                log(k, i, op.dst, cur, r);
+            }
         }
         // record ops run in k_records
     }
 }
 
-__device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ tab, int k) {
+template <class Log = NoChainLog>
+__device__ __forceinline__ void run_program(Ent& en, const Tables* __restrict__ tab, int k, const Log& log = Log()) {
     const int n = tab->nops[k];
     // (ops in chunks of 4: an operand an earlier op wrote is read from the written list either way)
 #pragma unroll 1
     for (int i0 = 0; i0 < n; i0 += 4)
-        run_program_chunk(en, tab, k, i0, min(n, i0 + 4));
+        run_program_chunk(en, tab, k, i0, min(n, i0 + 4), log);
 }
 
 }  // namespace nfgpu
@@ -721,6 +737,48 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
         d.t_msg[tile] = (unsigned)tot;
         tally_add(d, kTallyTick, (unsigned long long)(s_bytes + 12));
     }
+}
+
+// ---------------------------------------------------------------------------------
+// Per-Set chains of watched properties (nfk_watch_props).  The frame's events are coalesced per
+// (entity, property); the reference fires a property's per-object callbacks once per accepted Set
+// (NFCProperty::SetInt / SetFloat, PR:254-334), in the order NFCScheduleModule::Execute runs the
+// functors (SM:52-80).  For the watched properties k_chain re-runs the frame's fire test and
+// heartbeat programs READ-ONLY, before k_tick, on the values k_sets left — k_tick_touch's own code
+// (sched_scan without its stores, run_program) — and logs every accepted Set of a watched property
+// as (slot, kind, op, property, old, new).  Off (not launched) while nothing is watched.
+struct ChainEnt {
+    uint32_t slot;
+    uint16_t pid;
+    uint8_t kind, op;
+    uint64_t old_bits, new_bits;
+};
+static_assert(sizeof(ChainEnt) == 24, "ChainEnt is read back as 24-byte records");
+__global__ __launch_bounds__(kTPB) void k_chain(Dev d, ChainEnt* __restrict__ out, uint32_t* __restrict__ count,
+                                                uint32_t cap, uint32_t kinds, uint64_t watch0, uint64_t watch1) {
+    __shared__ uint64_t s_old[NFK_MAX_TOUCH * kTPB];  // (Ent's frame-start list; unused here)
+    const int e = blockIdx.x * kTPB + (int)threadIdx.x;
+    if (e >= d.N) return;  // (no barrier follows)
+    unsigned bytes = 0;
+    uint64_t desc = kDeadDesc;
+    const uint32_t fired = sched_scan<DynSchema, false>(d, e, bytes, desc) & kinds;
+    if (desc_dead(desc) || !fired) return;
+    Ent en;
+    en.n = 0;
+    en.old = s_old + threadIdx.x;
+    en.ovf = false;
+    en.bytes = 0;
+    en.dv = &d;
+    en.cap = (size_t)d.cap;
+    en.n_int = d.n_int;
+    en.e = e;
+    auto log = [&](int k, int i, uint32_t p, uint64_t o, uint64_t n) {
+        if (!(((p < 64 ? watch0 >> p : watch1 >> (p - 64)) & 1ull))) return;
+        const uint32_t at = atomicAdd(count, 1u);
+        if (at < cap) out[at] = ChainEnt{(uint32_t)e, (uint16_t)p, (uint8_t)k, (uint8_t)i, o, n};
+    };
+    for (int k = 0; k < d.n_kind; k++)
+        if ((fired >> k) & 1) run_program(en, d.tab, k, log);
 }
 
 // ---------------------------------------------------------------------------------

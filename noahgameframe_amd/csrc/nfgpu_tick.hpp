@@ -195,7 +195,8 @@ constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: 
 // the first use of any of them: a load under a branch is followed by a wait at the join, and a
 // first use after the record stores would make the wave wait for the stores too (the vector
 // memory counter retires in order), i.e. one round trip per kind or per store batch.
-template <class S, bool kFirst>
+// kStore = false: the fire test only (k_chain re-runs it before k_tick; nothing is stored).
+template <class S, bool kFirst, bool kStore = true>
 __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigned& bytes, uint64_t& desc,
                                             bool& dead, bool& taken, uint32_t& fired, int32_t* s_rem,
                                             bool oob) {
@@ -245,21 +246,22 @@ __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigne
             }
             h[j].state = st | kStFired;
         }
-        if (!(d.ablate & kAblNoSchedStore)) st_nt<(S::kNt & kNtStateStore) != 0>(d.s_hot + (size_t)k * d.s_kstr + e, h[j]);
+        if (kStore && !(d.ablate & kAblNoSchedStore))
+            st_nt<(S::kNt & kNtStateStore) != 0>(d.s_hot + (size_t)k * d.s_kstr + e, h[j]);
         if (s_rem) s_rem[k * kTPB + threadIdx.x] = h[j].remain;  // for the fired list
         bytes += 16;
     }
 }
 // Loads desc = fan_desc[e] with the first chunk; returns the fired-kind mask.  oob: a slot past N
 // (e is then a valid slot re-read, treated as dead).
-template <class S = DynSchema>
+template <class S = DynSchema, bool kStore = true>
 __device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& bytes, uint64_t& desc,
                                                int32_t* s_rem = nullptr, bool oob = false) {
     uint32_t fired = 0;
     bool dead = true, taken = false;
-    sched_chunk<S, true>(d, e, 0, bytes, desc, dead, taken, fired, s_rem, oob);
+    sched_chunk<S, true, kStore>(d, e, 0, bytes, desc, dead, taken, fired, s_rem, oob);
     for (int k0 = kKindChunk; k0 < S::n_kind(d); k0 += kKindChunk)
-        sched_chunk<S, false>(d, e, k0, bytes, desc, dead, taken, fired, s_rem, oob);
+        sched_chunk<S, false, kStore>(d, e, k0, bytes, desc, dead, taken, fired, s_rem, oob);
     return fired;
 }
 

@@ -332,7 +332,42 @@ bool NFGPUKernelModule::AfterInit() {
         def_of_pid_[dev_pid_[p]] = p;
     }
     committed_ = true;
+    for (const std::string& nm : watch_names_) WatchProperty(nm);
+    watch_names_.clear();
     return true;
+}
+
+void NFGPUKernelModule::WatchProperty(const std::string& name) {
+    if (!committed_) {
+        watch_names_.push_back(name);
+        return;
+    }
+    auto it = prop_id_.find(name);
+    if (it == prop_id_.end() || props_[(size_t)it->second].type == TDATA_OBJECT) return;  // (programs write int / f64)
+    const int32_t pid = dev_pid_[(size_t)it->second];
+    if (std::find(watch_pids_.begin(), watch_pids_.end(), pid) != watch_pids_.end()) return;
+    watch_pids_.push_back(pid);
+    check(nfk_watch_props(world_, (int32_t)watch_pids_.size(), watch_pids_.data()), "nfk_watch_props");
+}
+
+// the frame's per-Set log in the order the reference's heartbeat walk makes the Sets: objects in
+// NFGUID order, then kind (name order), then op (SM:52-80)
+void NFGPUKernelModule::ReadChain() {
+    chain_.clear();
+    if (watch_pids_.empty()) return;
+    int32_t n = 0;
+    check(nfk_read_chain(world_, 0, &n, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr), "nfk_read_chain");
+    if (!n) return;
+    std::vector<int32_t> o((size_t)n), k((size_t)n), op((size_t)n), pid((size_t)n);
+    std::vector<uint64_t> a((size_t)n), b((size_t)n);
+    int32_t m = 0;
+    check(nfk_read_chain(world_, n, &m, o.data(), k.data(), op.data(), pid.data(), a.data(), b.data()), "nfk_read_chain");
+    chain_.resize((size_t)n);
+    for (int32_t i = 0; i < n; i++) chain_[(size_t)i] = {o[(size_t)i], k[(size_t)i], op[(size_t)i], pid[(size_t)i], a[(size_t)i], b[(size_t)i]};
+    std::sort(chain_.begin(), chain_.end(), [this](const ChainEntry& x, const ChainEntry& y) {
+        if (x.obj != y.obj) return guids_[(size_t)x.obj] < guids_[(size_t)y.obj];
+        return x.kind != y.kind ? x.kind < y.kind : x.op < y.op;
+    });
 }
 
 bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int nTargetGroupID, float fX, float fY,
@@ -740,6 +775,17 @@ bool NFGPUKernelModule::AddRecordEventCallBack(const RECORD_SINGLE_EVENT_FUNCTOR
     return true;
 }
 
+bool NFGPUKernelModule::AddPropertySyncCallBack(const PROPERTY_SYNC_FUNCTOR& cb) {
+    if (!cb) return false;
+    sync_prop_cb_.push_back(cb);
+    return true;
+}
+bool NFGPUKernelModule::AddRecordSyncCallBack(const RECORD_SYNC_FUNCTOR& cb) {
+    if (!cb) return false;
+    sync_rec_cb_.push_back(cb);
+    return true;
+}
+
 bool NFGPUKernelModule::AddFrameCallBack(const FRAME_FUNCTOR& cb, uint32_t what) {
     if (!cb) return false;
     frame_cb_.push_back(cb);
@@ -749,9 +795,10 @@ bool NFGPUKernelModule::AddFrameCallBack(const FRAME_FUNCTOR& cb, uint32_t what)
 
 // what one device pass reads back for the registered consumers (nfk_read_frame bits)
 uint32_t NFGPUKernelModule::ReadMask(bool per_event_fired) const {
+    const bool sync = !sync_prop_cb_.empty() || !sync_rec_cb_.empty();
     const bool cb_events = !common_prop_cb_.empty() || !aoi_prop_cb_.empty() || !common_rec_cb_.empty() ||
-                           !aoi_rec_cb_.empty();
-    const bool cb_fan = !aoi_prop_cb_.empty() || !aoi_rec_cb_.empty();
+                           !aoi_rec_cb_.empty() || sync || (per_event_fired && frame_hook_);
+    const bool cb_fan = !aoi_prop_cb_.empty() || !aoi_rec_cb_.empty() || sync;
     uint32_t what = 0;
     if (summary_.n_fired && ((per_event_fired && n_cb_) || (frame_what_ & NFK_READ_FIRED))) {
         what |= NFK_READ_FIRED;
@@ -890,7 +937,9 @@ bool NFGPUKernelModule::Execute() {
         ~GatherGuard() { m->WaitGather(); }
     } gather_guard{this};
     if (what) check(nfk_read_frame(world_, what, &fh), "nfk_read_frame");
+    ReadChain();
     stats_.events_read = ms_since(t1);
+    if (frame_hook_) frame_hook_(fh);  // (before the functors: they see the frame's values)
     t1 = std::chrono::steady_clock::now();
     // heartbeat functors with the reference's arguments, objects in NFGUID order (the fired list's)
     const int64_t nfi = n_cb_ ? fh.n_fi : 0;  // (a frame consumer may read the list without functors)
@@ -1081,7 +1130,8 @@ void NFGPUKernelModule::WaitGather() {
 // before every such write).  False for a frame too small to pay for it, or with no workers.
 bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
     WaitGather();
-    const bool ev = !(common_prop_cb_.empty() && aoi_prop_cb_.empty() && common_rec_cb_.empty() && aoi_rec_cb_.empty());
+    const bool ev = !(common_prop_cb_.empty() && aoi_prop_cb_.empty() && common_rec_cb_.empty() && aoi_rec_cb_.empty() &&
+                      sync_prop_cb_.empty() && sync_rec_cb_.empty());
     const int64_t nev = ev ? fh.n_ev : 0, nre = ev ? fh.n_re : 0;
     ev_self_.clear();
     re_self_.clear();
@@ -1101,7 +1151,7 @@ bool NFGPUKernelModule::GatherFrame(const nfk_frame_host& fh, int64_t nfi) {
     // (per property event: its recipient run equals the previous event's, so the delivery reuses the
     // NFGUID list it built; consecutive events of a scene group mostly share their recipients)
     static const bool same_on = !(getenv("NFGPU_PLUGIN_SAME") && getenv("NFGPU_PLUGIN_SAME")[0] == '0');
-    const bool runs = same_on && fh.msg_off && !aoi_prop_cb_.empty();
+    const bool runs = same_on && fh.msg_off && (!aoi_prop_cb_.empty() || !sync_prop_cb_.empty());
     ev_same_.resize(runs ? (size_t)nev : 0);
     constexpr int64_t kChunk = kGatherChunk, kPre = 16;
     const int64_t cf = (nfi + kChunk - 1) / kChunk, ce = (nev + kChunk - 1) / kChunk, cr = (nre + kChunk - 1) / kChunk;
@@ -1179,7 +1229,13 @@ static inline void TDataOf(TDATA_TYPE t, uint64_t vo, uint64_t vn, TData* a, TDa
 
 void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_self, const NFGUID* re_self,
                                       const uint8_t* ev_same) {
-    if (common_prop_cb_.empty() && aoi_prop_cb_.empty() && common_rec_cb_.empty() && aoi_rec_cb_.empty()) return;
+    if (common_prop_cb_.empty() && aoi_prop_cb_.empty() && common_rec_cb_.empty() && aoi_rec_cb_.empty() &&
+        sync_prop_cb_.empty() && sync_rec_cb_.empty())
+        return;
+    static const std::vector<NFGUID> kNone;
+    const bool sync_p = !sync_prop_cb_.empty(), sync_r = !sync_rec_cb_.empty();
+    const bool want_p = f.msg_off && (!aoi_prop_cb_.empty() || sync_p);
+    const bool want_r = f.msg_off && (!aoi_rec_cb_.empty() || sync_r);
     std::vector<NFGUID> rcpt;
     uint32_t rcpt_at = 0, rcpt_n = 0xFFFFFFFFu;  // the msg_rcpt run rcpt holds
     constexpr int64_t kPre = 16;  // events are in slot order; their objects' NFGUIDs are scattered
@@ -1194,12 +1250,14 @@ void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_
         }
         const NFGUID& self = ev_self ? ev_self[e] : guids_[f.ev_obj[e]];
         for (auto& cb : common_prop_cb_) cb(self, pd.name, a, b);
-        if (f.msg_off && !aoi_prop_cb_.empty() && f.msg_off[e + 1] > f.msg_off[e]) {  // AOI.cpp:250: no call for empty lists
+        bool same = false;
+        const bool run = want_p && f.msg_off[e + 1] > f.msg_off[e];
+        if (run) {  // AOI.cpp:250: no AOI call for an empty list
             // consecutive events of a scene group mostly share their recipients: rebuild the list
             // only when the run differs from the last one delivered (ev_same: compared by the workers)
             const uint32_t m0 = f.msg_off[e], m1 = f.msg_off[e + 1];
-            const bool same = ev_same ? ev_same[e] != 0
-                                      : m1 - m0 == rcpt_n && memcmp(f.msg_rcpt + m0, f.msg_rcpt + rcpt_at, (size_t)(m1 - m0) * 4) == 0;
+            same = ev_same ? ev_same[e] != 0
+                           : m1 - m0 == rcpt_n && memcmp(f.msg_rcpt + m0, f.msg_rcpt + rcpt_at, (size_t)(m1 - m0) * 4) == 0;
             if (!same) {
                 rcpt.resize(m1 - m0);
                 for (uint32_t m = m0; m < m1; m++) rcpt[m - m0] = guids_[f.msg_rcpt[m]];
@@ -1208,7 +1266,12 @@ void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_
             rcpt_n = m1 - m0;
             for (auto& cb : aoi_prop_cb_) cb(self, pd.name, a, b, rcpt);
         }
+        if (sync_p) {
+            const SyncArgs sa{f.ev_obj[e], run ? &rcpt : &kNone, run && same};
+            for (auto& cb : sync_prop_cb_) cb(self, f.ev_pid[e], a, b, sa);
+        }
     }
+    rcpt_n = 0xFFFFFFFFu;  // (the record runs: the first one is built)
     RECORD_EVENT_DATA ev;
     int ev_r = -1;  // the record ev.strRecordName holds (a name copy per event would allocate)
     for (int64_t e = 0; e < f.n_re; e++) {
@@ -1227,11 +1290,24 @@ void NFGPUKernelModule::DeliverEvents(const nfk_frame_host& f, const NFGUID* ev_
         TDataOf(op ? TDATA_UNKNOWN : records_[r].cols[col], f.re_old[e], f.re_new[e], &a, &b);
         const NFGUID& self = re_self ? re_self[e] : guids_[f.re_obj[e]];
         for (auto& cb : common_rec_cb_) cb(self, ev, a, b);
-        if (f.msg_off && !aoi_rec_cb_.empty()) {
-            rcpt_n = 0xFFFFFFFFu;
-            rcpt.clear();
-            for (uint32_t m = f.msg_off[f.n_ev + e]; m < f.msg_off[f.n_ev + e + 1]; m++) rcpt.push_back(guids_[f.msg_rcpt[m]]);
-            for (auto& cb : aoi_rec_cb_) cb(self, ev.strRecordName, ev, a, b, rcpt);
+        if (want_r) {  // (AOI.cpp:285-287 calls OnRecordEvent with an empty list too)
+            const uint32_t m0 = f.msg_off[f.n_ev + e], m1 = f.msg_off[f.n_ev + e + 1];
+            bool same = false;
+            if (m1 > m0) {
+                same = m1 - m0 == rcpt_n && memcmp(f.msg_rcpt + m0, f.msg_rcpt + rcpt_at, (size_t)(m1 - m0) * 4) == 0;
+                if (!same) {
+                    rcpt.resize(m1 - m0);
+                    for (uint32_t m = m0; m < m1; m++) rcpt[m - m0] = guids_[f.msg_rcpt[m]];
+                }
+                rcpt_at = m0;
+                rcpt_n = m1 - m0;
+            }
+            const std::vector<NFGUID>& rl = m1 > m0 ? rcpt : kNone;
+            for (auto& cb : aoi_rec_cb_) cb(self, ev.strRecordName, ev, a, b, rl);
+            if (sync_r) {
+                const SyncArgs sa{f.re_obj[e], &rl, m1 > m0 && same};
+                for (auto& cb : sync_rec_cb_) cb(self, ev, a, b, sa);
+            }
         }
     }
 }

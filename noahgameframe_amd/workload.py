@@ -85,7 +85,7 @@ def _prop_flags(n_oprops=0):
     return f
 
 
-def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False):
+def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False, lethal_poison=False):
     ops = np.zeros((len(KINDS), MAX_OPS), OP_DTYPE)
     n_ops = np.zeros(len(KINDS), np.int32)
 
@@ -119,6 +119,13 @@ def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False)
                        (OP_IADD_CLAMP, A_PROP, PID["SP"], 0, PID["Level"], 0, 1000)])  # (6 ops: > 4 per program)
         put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 1, PID["MAXHP"]),
                        (OP_ISET, GUARD, PID["SP"], guard(PID["Camp"], GUARD_LE0), 7, 0, 0)])
+    if lethal_poison:
+        # Poison may kill: HP clamps at 0, and the same functor revives a dead object at 3 HP — within
+        # one frame HP goes hp -> 0 -> 3, so NFCNPCRefreshModule::OnObjectHPEvent-style per-object
+        # callbacks (newVar <= 0 kills, NFCNPCRefreshModule.cpp:113-116) see the death only when they
+        # fire once per accepted Set
+        put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 0, PID["MAXHP"]),
+                       (OP_ISET, GUARD, PID["HP"], guard(PID["HP"], GUARD_LE0), 3, 0, 0)])
     if with_records:
         # skill table: col 1 = cooldown ms (int), col 2 = charge (f64) decays
         lst = [(OP_RIADD_CLAMP, 0, (0 << 8) | 1, 0, -100, 0, I64_MAX)]
@@ -143,7 +150,8 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
                t0=1_700_000_000_000, guid_heads=(7, 9), rec_float_op=True, rec_skill_op=False, sched_edges=False,
                switch_frac=0.0, switch_new_groups=False, rec_steady=False, ext_props=None, burst_frac=0.0,
                burst_props=20, rmw_frac=0.0, spawn_frac=0.0, destroy_frac=0.0, rec_set_frac=0.0,
-               rec_set_float=True, obj_props=False, obj_set_frac=0.05, rec_row_frac=0.0, set_ops=False):
+               rec_set_float=True, obj_props=False, obj_set_frac=0.05, rec_row_frac=0.0, set_ops=False,
+               lethal_poison=False):
     if spawn_frac > 0 or destroy_frac > 0:
         return _lifecycle_world(locals())
     rng = np.random.default_rng(seed)
@@ -168,6 +176,9 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
     maxhp = rng.integers(500, 5000, n_obj)
     init_i[PID["MAXHP"]] = maxhp
     init_i[PID["HP"]] = rng.integers(1, maxhp + 1)
+    if lethal_poison:  # a third of the objects near death
+        low = rng.random(n_obj) < 0.33
+        init_i[PID["HP"], low] = rng.integers(1, 40, int(low.sum()))
     init_i[PID["HPREGEN"]] = rng.integers(1, 50, n_obj)
     maxmp = rng.integers(100, 1000, n_obj)
     init_i[PID["MAXMP"]] = maxmp
@@ -201,7 +212,7 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
     still = rng.random(n_obj) < 0.02
     init_f[fi["X"], still] = init_f[fi["TargetX"], still]
 
-    ops, n_ops = programs(records, rec_float_op, rec_skill_op, set_ops)
+    ops, n_ops = programs(records, rec_float_op, rec_skill_op, set_ops, lethal_poison)
     n_kind = len(KINDS) if records else len(KINDS) - 1
 
     # ---- heartbeats registered before the first frame ----

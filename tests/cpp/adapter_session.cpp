@@ -13,8 +13,11 @@
 //   NFConfigPlugin              NFCClassModule, NFCElementModule (the class schema, read from XML that
 //                               this program writes for the workload's classes)
 // and two test doubles: the plugin manager (module registry, clock, in-memory config files) and a
-// log module.  The AOI module computes the recipient lists on the host (GetBroadCastObject,
-// AOI:531-593) from the device's coalesced events: they are compared with the oracle's.
+// log module.  The AOI module is the plugin's NFGPUSceneAOIAdapter: the recipient lists its
+// AddPropertyEventCallBack / AddRecordEventCallBack functors receive for device events are the
+// DEVICE's (k_tick / k_records fan-out), compared with the oracle's; the run also reports how many
+// device events reached NFCSceneAOIModule's own common handlers (and so GetBroadCastObject,
+// AOI:531-593) — 0.
 //
 // usage: adapter_session <workload.nfio> <out.nfio>
 #include <cstdio>
@@ -155,7 +158,7 @@ int main(int argc, char** argv) {
     NFCClassModule classes(&pm);
     NFCElementModule elements(&pm);
     NFGPUKernelAdapter kernel(&pm);
-    NFCSceneAOIModule aoi(&pm);
+    NFGPUSceneAOIAdapter aoi(&pm);
     NFCEventModule events(&pm);
     NFGPUScheduleAdapter sched(&pm);
     pm.AddModule(typeid(NFILogModule).name(), &log);
@@ -439,6 +442,10 @@ int main(int argc, char** argv) {
         snprintf(nm, sizeof nm, "final_rec%d_used", r);
         nfio_put1(&w, nm, NFIO_U64, used.data(), used.size(), 8);
     }
+    // device events handed to the AOI module with the device's lists, and device events that reached
+    // NFCSceneAOIModule::OnPropertyCommonEvent / OnRecordCommonEvent (GetBroadCastObject) on the host
+    const int64_t aoi_calls[2] = {kernel.AOIDeviceCalls(), kernel.AOIHostDeviceCalls()};
+    nfio_put1(&w, "aoi_calls", NFIO_I64, aoi_calls, 2, 8);
     nfio_wclose(&w);
     fflush(stdout);
     _exit(0);  // (static destructors: NFMemoryCounter's static map dies before the modules' objects)

@@ -6,7 +6,8 @@
 //               where they lie — the heartbeat effect programs run as functors through
 //               NFIKernelModule (as oracle/ref_session.cpp does);
 //   (default)   the reference-side GPU plugin (integration/NFGPUKernelPlugin.cpp: NFGPUKernelAdapter +
-//               NFGPUScheduleAdapter) in the same modules' place — the programs run on the device.
+//               NFGPUScheduleAdapter + NFGPUSceneAOIAdapter) in the same modules' place — the programs
+//               run on the device.
 //
 // The logic uses what the reference's game modules use beyond the frame path:
 //   * Tutorial3's own sequence (Tutorial/Tutorial3/HelloWorld3Module.cpp:40-110, restated): a class
@@ -18,13 +19,18 @@
 //     once per frame;
 //   * per-object callbacks (NFIKernelModule::AddPropertyCallBack / AddRecordCallBack,
 //     NFIKernelModule.h:28-45) on every workload object's HP, MP, X, TargetX, Gold, Level and rec0;
+//     the HP one also does what NFCNPCRefreshModule::OnObjectHPEvent does (NFCNPCRefreshModule.cpp:
+//     113-124, restated): at newVar <= 0 the object is killed and a functor-only heartbeat
+//     AddSchedule(self, "OnDeadDestroyHeart", 5.0f, 1) is added — so an HP that crosses 0 and recovers
+//     within one frame kills only when the callbacks fire per accepted Set;
 //   * the workload's window calls split between NFIKernelModule (SetProperty*, SetRecordInt,
 //     ClearRecord) and the objects themselves (GetObject(self)->SetProperty*,
 //     FindRecord(self, r)->SetInt / AddRow / Remove), read-modify-write Sets included; schedule
 //     calls; DestroyObject and CreateObject after start.
 //
 // Logged per frame t: per-object property and record callbacks with the phase they fired in (0 =
-// the window's calls, 1 = Execute), the heartbeat functors, Tutorial3's callback lines, and every
+// the window's calls, 1 = Execute), the heartbeat functors, Tutorial3's callback lines, the kills and
+// OnDeadDestroyHeart calls, and every
 // object's device properties and rec0 int cells read through the HOST objects
 // (GetObject(self)->GetProperty*, FindRecord(self, r)->GetInt) and through NFIKernelModule.
 //
@@ -90,11 +96,14 @@ struct Logic {
     std::vector<uint64_t> pc_old, pc_new, rc_old, rc_new;
     std::vector<int32_t> fi_obj, fi_kind, fi_rem;
     std::string t3;  // Tutorial3's callback lines
+    std::string kills, dead;  // OnObjectHPEvent's kills, OnDeadDestroyHeart's calls
     void clear() {
         for (auto* v : {&pc_phase, &pc_obj, &pc_pid, &rc_phase, &rc_obj, &fi_obj, &fi_kind, &fi_rem}) v->clear();
         rc_rrc.clear();
         for (auto* v : {&pc_old, &pc_new, &rc_old, &rc_new}) v->clear();
         t3.clear();
+        kills.clear();
+        dead.clear();
     }
     int ObjOf(const NFGUID& g) const {
         auto it = obj.find(g);
@@ -122,8 +131,22 @@ struct Logic {
         rc_new.push_back(op ? 0 : (uint64_t)b.GetInt());
         return 0;
     }
+    // NFCNPCRefreshModule::OnObjectHPEvent (NFCNPCRefreshModule.cpp:113-124, restated without the
+    // LastAttacker test: this schema has no object properties)
+    int OnObjectHPEvent(const NFGUID& self, const std::string&, const NFIDataList::TData& a, const NFIDataList::TData& b) {
+        if (b.GetInt() <= 0) {
+            kills += std::to_string(ObjOf(self)) + " " + std::to_string(a.GetInt()) + " " + std::to_string(b.GetInt()) + "\n";
+            sm->AddSchedule(self, "OnDeadDestroyHeart", this, &Logic::OnDeadDestroyHeart, 5.0f, 1);
+        }
+        return 0;
+    }
+    int OnDeadDestroyHeart(const NFGUID& self, const std::string&, const float, const int nCount) {  // :127
+        dead += std::to_string(ObjOf(self)) + " " + std::to_string(nCount) + "\n";
+        return 0;
+    }
     void Watch(const NFGUID& g) {
         for (const char* n : {"HP", "MP", "X", "TargetX", "Gold", "Level"}) km->AddPropertyCallBack(g, n, this, &Logic::OnObjProp);
+        km->AddPropertyCallBack(g, "HP", this, &Logic::OnObjectHPEvent);
         km->AddRecordCallBack(g, "rec0", this, &Logic::OnObjRecord);
     }
     // the heartbeat functor's log (both servers); the effect runs in Effect (reference) or on the device
@@ -227,11 +250,12 @@ int main(int argc, char** argv) {
 #ifdef LOGIC_REF
     NFCKernelModule kernel(&pm);
     NFCScheduleModule sched(&pm);
+    NFCSceneAOIModule aoi(&pm);
 #else
     NFGPUKernelAdapter kernel(&pm);
     NFGPUScheduleAdapter sched(&pm);
+    NFGPUSceneAOIAdapter aoi(&pm);
 #endif
-    NFCSceneAOIModule aoi(&pm);
     NFCEventModule events(&pm);
     pm.AddModule(typeid(NFILogModule).name(), &log);
     pm.AddModule(typeid(NFIClassModule).name(), &classes);
@@ -322,7 +346,18 @@ int main(int argc, char** argv) {
         const int k = L.kid.at(name);
         for (int i = 0; i < nops[k]; i++) {
             const nfk_op& op = ops[k * OPK + i];
-            if (op.code == NFK_OP_IADD_CLAMP) {
+            if (op.flags & NFK_GUARD) {  // the functor's `if (GetPropertyInt(self, g) ...)`
+                const int64_t g = km->GetPropertyInt(self, pname[op.guard & 0xFFFF]);
+                const int c = (op.guard >> 16) & 3;
+                if (!(c == NFK_GUARD_GT0 ? g > 0 : c == NFK_GUARD_LE0 ? g <= 0 : c == NFK_GUARD_NE0 ? g != 0 : g == 0))
+                    continue;
+            }
+            if (op.code == NFK_OP_ISET) {
+                km->SetPropertyInt(self, pname[op.dst], (op.flags & NFK_A_PROP) ? km->GetPropertyInt(self, pname[op.a]) : op.a);
+            } else if (op.code == NFK_OP_FSET) {
+                km->SetPropertyFloat(self, pname[op.dst], (op.flags & NFK_A_PROP) ? km->GetPropertyFloat(self, pname[op.a])
+                                                                                  : bitsd((uint64_t)op.a));
+            } else if (op.code == NFK_OP_IADD_CLAMP) {
                 const std::string& d = pname[op.dst];
                 const int64_t cur = km->GetPropertyInt(self, d);
                 const int64_t a = (op.flags & NFK_A_PROP) ? km->GetPropertyInt(self, pname[op.a]) : op.a;
@@ -496,9 +531,13 @@ int main(int argc, char** argv) {
         PUT("fi", "rem", NFIO_I32, L.fi_rem, 4);
         std::vector<uint8_t> t3(L.t3.begin(), L.t3.end());
         PUT("t3", "log", NFIO_U8, t3, 1);
+        std::vector<uint8_t> kl(L.kills.begin(), L.kills.end()), dl(L.dead.begin(), L.dead.end());
+        PUT("k", "kills", NFIO_U8, kl, 1);
+        PUT("k", "dead", NFIO_U8, dl, 1);
         // every object's properties through the host object and through NFIKernelModule, and its
         // rec0 used rows' int cells through the host record
         std::vector<uint64_t> vh((size_t)NP * N, 0), vk((size_t)NP * N, 0), rv((size_t)N * cols * rows, 0), ru(N, 0);
+        std::vector<uint64_t> rk((size_t)N * cols * rows, 0);  // (the same cells through NFIKernelModule::GetRecordInt)
         for (int64_t o = 0; o < N; o++) {
             if (!alive[o]) continue;
             const NFGUID g(gh[o], gd[o]);
@@ -511,13 +550,17 @@ int main(int argc, char** argv) {
             for (int row = 0; row < rows; row++) {
                 if (!R->IsUsed(row)) continue;
                 ru[o] |= 1ull << row;
-                for (int c = 0; c < cols; c++) rv[((size_t)o * cols + c) * rows + row] = (uint64_t)R->GetInt(row, c);
+                for (int c = 0; c < cols; c++) {
+                    rv[((size_t)o * cols + c) * rows + row] = (uint64_t)R->GetInt(row, c);
+                    rk[((size_t)o * cols + c) * rows + row] = (uint64_t)km->GetRecordInt(g, "rec0", row, c);
+                }
             }
         }
         PUT("v", "host", NFIO_U64, vh, 8);
         PUT("v", "kernel", NFIO_U64, vk, 8);
         PUT("r", "cells", NFIO_U64, rv, 8);
         PUT("r", "used", NFIO_U64, ru, 8);
+        PUT("r", "kcells", NFIO_U64, rk, 8);
     }
     nfio_wclose(&w);
     fflush(stdout);

@@ -389,6 +389,16 @@ int nfk_exist_schedule(void* w, int64_t h, int64_t d, int32_t kind, int32_t* e) 
     *e = o >= 0 && S(w)->sched[o].count(kind);
     return NFK_OK;
 }
+int nfk_watch_props(void*, int32_t n, const int32_t* pid) {
+    std::string t;
+    for (int32_t i = 0; i < n; i++) t += " " + std::to_string(pid[i]);
+    logf("watch%s", t.c_str());
+    return NFK_OK;
+}
+int nfk_read_chain(void*, int32_t, int32_t* n, int32_t*, int32_t*, int32_t*, int32_t*, uint64_t*, uint64_t*) {
+    *n = 0;  // (the stub runs no programs)
+    return NFK_OK;
+}
 int nfk_read_added(void*, int32_t, int32_t* n, int64_t*, int64_t*, int32_t*) {
     *n = 0;
     return NFK_OK;

@@ -92,7 +92,9 @@ def test_adapter_session_matches_oracle(gpu_available, tmp_path, seed):
     """CreateObject before and after AfterInit, Set/GetProperty Int/Float/Object (read-modify-write
     included), SetRecordInt/Float by column index and by column tag, AddRow / Remove / ClearRecord,
     DestroyObject, object heartbeats through NFIScheduleModule::AddSchedule functors — through the
-    reference's own kernel, AOI and class modules with the adapter in NFIKernelModule's place."""
+    reference's own kernel and class modules with the adapter in NFIKernelModule's place and
+    NFGPUSceneAOIAdapter (the reference's NFCSceneAOIModule fed the device's recipient lists) in
+    NFISceneAOIModule's."""
     if not os.path.exists(EXE):
         pytest.skip("adapter_session not built (needs /root/reference at build time)")
     w = _world(seed)
@@ -116,6 +118,11 @@ def test_adapter_session_matches_oracle(gpu_available, tmp_path, seed):
                  _normalise({k: ref[k] for k in keys if k in ref}, w, nt))
     assert sum(len(got[f"ev_t{t}_obj"]) for t in range(nt)) > 1000
     assert sum(len(got[f"mr_t{t}_obj"]) for t in range(nt)) > 1000
+    # the recipient lists came from the device: every device event went to NFGPUSceneAOIAdapter with the
+    # device's list, none to NFCSceneAOIModule's own handlers (no host GetBroadCastObject, AOI:531-593)
+    dev_calls, host_dev_calls = (int(x) for x in got["aoi_calls"])
+    assert host_dev_calls == 0
+    assert dev_calls == sum(len(got[f"ev_t{t}_obj"]) + len(got[f"re_t{t}_obj"]) for t in range(nt))
 
 
 STUB = os.path.join(ROOT, "tests", "cpp", "_stub")

@@ -10,10 +10,13 @@ properties with per-object callbacks, DoEvent).  Compared frame by frame:
 * the heartbeat functors, Tutorial3's callback lines, and every object's properties and rec0 cells read
   through the HOST objects and through NFIKernelModule: equal;
 * per-object callbacks of the window's calls (phase 0): the same sequence;
-* per-object callbacks fired by Execute (phase 1): per (object, property / cell) the reference's
-  chain (one callback per heartbeat functor Set) coalesced to (first old, last new) and dropped when
-  they are equal — the device applies a frame's programs and reports each (entity, property) once —
-  equal to the GPU plugin's, which fires once per (object, property / cell)."""
+* per-object callbacks fired by Execute (phase 1): the same sequence — one callback per accepted Set
+  of the heartbeat programs (the reference's functors' Sets; on the GPU plugin the device's per-Set
+  log, k_chain), objects in NFGUID order, each object's schedules in name order, each program's ops
+  and a record op's rows in order (SM:52-80);
+* with Poison able to kill (workload lethal_poison: HP -> 0 -> 3 within one program), the kills of an
+  NFCNPCRefreshModule::OnObjectHPEvent-style callback (newVar <= 0, NFCNPCRefreshModule.cpp:113-124)
+  and the OnDeadDestroyHeart heartbeats it adds: the same."""
 import os
 import subprocess
 
@@ -27,11 +30,11 @@ GPU_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "logic_session")
 REF_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "logic_session_ref")
 
 
-def _world(seed, n_obj=1200, n_ticks=12):
+def _world(seed, n_obj=1200, n_ticks=12, lethal=False):
     w = workload.make_world(n_obj=n_obj, n_scenes=2, groups_per_scene=3, players_per_group=4, n_ticks=n_ticks,
                             tick_ms=1000, seed=seed, ext_frac=0.05, host_ops=True, rmw_frac=0.02, spawn_frac=0.02,
                             destroy_frac=0.02, records=True, rec_rows=16, rec_float_op=False, rec_set_frac=0.03,
-                            rec_set_float=False, rec_row_frac=0.02)
+                            rec_set_float=False, rec_row_frac=0.02, lethal_poison=lethal)
     # an int-only record (the reference's NFCRecord::SetFloat cannot hold an f64 cell, test_oracle.py):
     # the charge column becomes an int column with the same bits; no program touches it
     w["rec_ctype"] = np.zeros_like(w["rec_ctype"])
@@ -53,16 +56,28 @@ def _chains(out, t, pfx, key):
 
 
 def _coalesce(seq):
-    """(obj, key) -> (first old, last new) over the phase's callbacks, dropping net-zero chains; record
-    row events (Add / Del / Cover) are kept as they come."""
-    first, last, rows = {}, {}, []
+    """(obj, key) -> (first old, last new) over the phase's callbacks (what one callback per
+    (object, property) and frame would report)"""
+    first, last = {}, {}
     for o, k, a, b in seq:
-        if k >> 24:
-            rows.append((o, k))
-            continue
         first.setdefault((o, k), a)
         last[(o, k)] = b
-    return {key: (first[key], last[key]) for key in first if first[key] != last[key]}, sorted(rows)
+    return {key: (first[key], last[key]) for key in first}
+
+
+def _cell_history(got, ref, t, flat, w):
+    """(diagnosis) the record callbacks of the object owning rec0 cell `flat` up to frame t, both sides"""
+    rows, cols = int(w["rec_rows"][0]), int(w["rec_cols"][0])
+    o, rem = divmod(int(flat), cols * rows)
+    c, row = divmod(rem, rows)
+    h = {}
+    for name, out in (("gpu", got), ("ref", ref)):
+        h[name] = [(u, int(ph), int(rrc) >> 24, (int(rrc) >> 8) & 255, int(rrc) & 255, int(a), int(b))
+                   for u in range(t + 1)
+                   for ph, ob, rrc, a, b in zip(out[f"rc_t{u}_phase"], out[f"rc_t{u}_obj"], out[f"rc_t{u}_rrc"],
+                                                out[f"rc_t{u}_old"], out[f"rc_t{u}_new"])
+                   if ob == o and (((int(rrc) >> 8) & 255) == row or int(rrc) >> 24)]
+    return {"obj": o, "row": row, "col": c, **h}
 
 
 def _t3(out, t):
@@ -90,32 +105,57 @@ def test_logic_session_reference_runs_tutorial3(tmp_path):
     assert any("OnEvent 1 10 1003 s3" in ln for ln in _t3(out, 3).splitlines())
 
 
+def test_logic_session_reference_kills_within_a_frame(tmp_path):
+    """CPU: with lethal Poison the reference's per-object HP callbacks see HP reach 0 and come back
+    within one frame (its functor's two Sets), so OnObjectHPEvent kills objects whose frame ends alive —
+    what a callback fired once per (object, property) and frame would miss."""
+    if not os.path.exists(REF_EXE):
+        pytest.skip("logic_session_ref not built (needs /root/reference at build time)")
+    w = _world(73, n_obj=600, lethal=True)
+    out = _run(REF_EXE, w, tmp_path, "ref")
+    hp = workload.PID["HP"]
+    hidden = kills = 0
+    for t in range(int(w["cfg"][7])):
+        kills += len(bytes(np.asarray(out[f"k_t{t}_kills"], np.uint8)).decode().splitlines())
+        chain = _chains(out, t, "pc", "pid")[1]
+        co = _coalesce([r for r in chain if r[1] == hp])
+        dead = {o for o, k, a, b in chain if k == hp and np.int64(np.uint64(b)) <= 0}
+        hidden += sum(1 for o in dead if np.int64(np.uint64(co[(o, hp)][1])) > 0)
+    assert kills > 20 and hidden > 20, (kills, hidden)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", [71, 72])
-def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, seed):
+@pytest.mark.parametrize("seed,lethal", [(71, False), (72, False), (73, True)])
+def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, seed, lethal):
     if not (os.path.exists(GPU_EXE) and os.path.exists(REF_EXE)):
         pytest.skip("logic_session not built (needs /root/reference at build time)")
-    w = _world(seed)
+    w = _world(seed, lethal=lethal)
     got, ref = _run(GPU_EXE, w, tmp_path, "gpu"), _run(REF_EXE, w, tmp_path, "ref")
     nt = int(w["cfg"][7])
     assert bytes(np.asarray(got["t3_setup"], np.uint8)) == bytes(np.asarray(ref["t3_setup"], np.uint8))
     n_obj_cb = n_rec_cb = 0
+    n_kills = 0
     for t in range(nt):
         assert _t3(got, t) == _t3(ref, t), t
+        for k in ("k_t{}_kills", "k_t{}_dead"):  # OnObjectHPEvent's kills, OnDeadDestroyHeart's calls
+            assert bytes(np.asarray(got[k.format(t)], np.uint8)) == bytes(np.asarray(ref[k.format(t)], np.uint8)), k.format(t)
+        n_kills += len(bytes(np.asarray(ref[f"k_t{t}_kills"], np.uint8)).decode().splitlines())
         fo = lambda o: sorted(zip(o[f"fi_t{t}_obj"], o[f"fi_t{t}_kind"], o[f"fi_t{t}_rem"]))
         assert fo(got) == fo(ref), t
-        for k in ("v_t{}_host", "v_t{}_kernel", "r_t{}_cells", "r_t{}_used"):
-            np.testing.assert_array_equal(got[k.format(t)], ref[k.format(t)], err_msg=k.format(t))
+        for k in ("v_t{}_host", "v_t{}_kernel", "r_t{}_kcells", "r_t{}_cells", "r_t{}_used"):
+            g_, r_ = np.asarray(got[k.format(t)]), np.asarray(ref[k.format(t)])
+            bad = np.nonzero(g_ != r_)[0]
+            assert len(bad) == 0, (k.format(t), [(int(i), int(g_[i]), int(r_[i])) for i in bad[:8]],
+                                   _cell_history(got, ref, t, bad[0], w) if k.startswith("r") else None)
         # the host objects agree with NFIKernelModule's reads (the device's, on the GPU plugin)
         np.testing.assert_array_equal(got[f"v_t{t}_host"], got[f"v_t{t}_kernel"])
         for pfx, key in (("pc", "pid"), ("rc", "rrc")):
             g, r = _chains(got, t, pfx, key), _chains(ref, t, pfx, key)
             assert g[0] == r[0], (t, pfx)   # the window's calls fire in call order, as in the reference
-            assert _coalesce(g[1]) == _coalesce(r[1]), (t, pfx)
-            # the GPU plugin fires each (object, property / cell) once per Execute
-            assert len({(o, k) for o, k, _, _ in g[1] if not k >> 24}) == sum(1 for _, k, _, _ in g[1] if not k >> 24)
+            assert g[1] == r[1], (t, pfx)   # Execute: one per accepted Set, in the heartbeat walk's order
             if pfx == "pc":
                 n_obj_cb += len(g[0]) + len(g[1])
             else:
                 n_rec_cb += len(g[0]) + len(g[1])
     assert n_obj_cb > 1000 and n_rec_cb > 100, (n_obj_cb, n_rec_cb)
+    assert n_kills > 20 or not lethal, n_kills
