@@ -416,14 +416,15 @@ public:
 
     // ---- scene shards (include/NFGPUSceneShard.hpp): one process per GPU, a scene range each ----
     // With a shard attached, SwitchScene into a scene another shard owns queues the entity's
-    // departure: from that call on the entity is no longer this module's (later calls on it return
-    // false, as after DestroyObject).  Execute ends by starting the all-gather of the departures'
-    // tickets (SceneShard::EndFrame, on an exchange frame; off the world's stream) and the next
-    // Execute begins by moving their rows (SceneShard::BeginFrame, collective: every rank's Execute
-    // makes it; no collective when no rank has a departure): the entity leaves at the start of the
-    // frame after the one its SwitchScene was queued before, with its state after that frame, and
-    // enters the owner's world with the SwitchScene property writes.  Arrivals' schedules call the
-    // functor registered for their name with SetKindFunctor (functors cannot cross processes).
+    // departure.  Execute ends by starting the all-gather of the departures' tickets
+    // (SceneShard::EndFrame, on an exchange frame; off the world's stream) and the next Execute begins
+    // by moving their rows (SceneShard::BeginFrame, collective: every rank's Execute makes it; no
+    // collective when no rank has a departure): the entity leaves at the start of the frame after the
+    // one its SwitchScene was queued before, with its state after that frame, and enters the owner's
+    // world with the SwitchScene property writes.  Until its row leaves it is this module's: its
+    // heartbeats fire here with their functors and calls on it apply here (they travel with the row);
+    // another SwitchScene or a DestroyObject of it returns false (Departing).  Arrivals' schedules call
+    // the functor registered for their name with SetKindFunctor (functors cannot cross processes).
     void AttachShard(SceneShard* shard) { shard_ = shard; }
     // the departures queued so far leave now and the arrivals enter (synchronous; collective: every
     // rank calls it the same number of times), so calls made after it in the window find the
@@ -433,9 +434,12 @@ public:
     }
     void SetKindFunctor(const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb, float fTime);
     int64_t MigratedOut() const { return shard_ ? shard_->migrated_out : 0; }
+    // a cross-shard SwitchScene of it is queued and its row has not left yet
+    bool Departing(const NFGUID& g) const { return departing_.count(g.nHead64, g.nData64) != 0; }
     int64_t MigratedIn() const { return shard_ ? shard_->migrated_in : 0; }
 
-    // ---- NFIRankRedisModule::GetRange(type, 0, k - 1, memberScoreVec) over a property ----
+    // ---- NFIRankRedisModule::GetRange(type, 0, k - 1, memberScoreVec) over a property: this world's
+    // entities, or with a shard attached every shard's (collective then: SceneShard::RankTop) ----
     bool GetRange(const std::string& prop, int k, std::vector<std::pair<std::string, double>>& memberScoreVec);
 
     // ---- NFISceneAOIModule recipient-list events ----
@@ -599,9 +603,9 @@ private:
     nfgpu_detail::NameIndex hb_ix_;  // schedule name -> kind (AfterInit)
     void QueueScheduleCall(int32_t op, const NFGUID& self, int32_t kind, float t, int32_t cnt, int64_t now);
     void DropPendingAdds(const NFGUID& g);
-    // objects that left for another shard and whose rows have not left the world yet: buffered
-    // calls on them are dropped at Flush, as calls on an object this module no longer has
-    nfgpu_detail::GuidMap departed_;
+    // objects with a queued cross-shard departure whose rows have not left the world yet (still this
+    // module's: see AttachShard)
+    nfgpu_detail::GuidMap departing_;
     int FlushSets();
     int FlushScheduleCalls();
     // the functor walk's and the deliveries' scattered host reads (functor slot, NFGUID, interval

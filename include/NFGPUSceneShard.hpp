@@ -148,6 +148,17 @@ public:
     int EndFrame();
     // synchronous exchange of the tickets queued so far (collective): gather, then rows
     int Migrate(std::vector<Ticket>* sent = nullptr, std::vector<Ticket>* received = nullptr);
+    // NFIRankRedisModule::GetRange(type, 0, k - 1) over every shard's entities
+    // (NFCRankRedisModule.cpp:109-118: a ZREVRANGE WITH SCORES of the whole key) with a property as the
+    // score: each rank's exact top k (nfk_rank_top on its world), all-gathered over the transport and
+    // merged in ZREVRANGE order — score descending, equal scores by member NFGUID::ToString()
+    // ("head-data", NFGUID.h:93) descending.  Collective (every rank calls it with the same pid and k,
+    // in the same order relative to its Execute; a ticket gather EndFrame started is waited for first).
+    struct RankRow {
+        int64_t guid_head, guid_data;
+        double score;
+    };
+    int RankTop(int pid, int k, std::vector<RankRow>* out);
     int64_t migrated_out = 0, migrated_in = 0;
     int64_t transport_calls = 0;  // collective calls this shard made (AllGather, AllToAllV)
     int64_t frames = 0;           // EndFrame calls

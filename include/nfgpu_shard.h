@@ -38,6 +38,11 @@ int nfs_received(void* shard, int64_t cap, int64_t* guid_head, int64_t* guid_dat
 int nfs_end_frame(void* shard);
 /* migrated out, migrated in, transport calls, frames */
 int nfs_stats(void* shard, int64_t* out4);
+/* collective: NFIRankRedisModule::GetRange(type, 0, k-1) over every shard's entities
+ * (NFCRankRedisModule.cpp:109-118) with property pid as the score — each rank's top k all-gathered
+ * and merged in ZREVRANGE order (SceneShard::RankTop); *n_out <= k rows */
+int nfs_rank_top(void* shard, int32_t pid, int32_t k, int32_t* n_out, int64_t* guid_head, int64_t* guid_data,
+                 double* score);
 
 #ifdef __cplusplus
 }

@@ -374,6 +374,7 @@ bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int 
                                     float fZ, float /*fOrient*/, const std::vector<TData>& /*arg*/) {
     Flush();  // (the buffered Set calls first: call order)
     if (!committed_ || ObjectIndex(self) < 0) return false;  // "There is no object" (KM:948)
+    if (departing_.count(self.nHead64, self.nData64)) return false;  // (on its way to another shard)
     if (shard_ && !shard_->Owns(nTargetSceneID)) {          // into another shard's scene
         const int o = ObjectIndex(self);
         // an entity spawned or switched in this window has no row to export until the frame applies
@@ -397,12 +398,14 @@ bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int 
     return true;
 }
 
+// The entity stays this module's until the exchange exports its row (MigrateNow, or the next Execute's
+// SceneShard::BeginFrame after the gather its Execute starts): its heartbeats fire with their functors
+// on this shard until then, and calls on it apply here and travel with its row (with the
+// asynchronous gather the entity ticks here one more device frame, whose functor calls were lost when
+// the functors were dropped at the SwitchScene)
 void NFGPUKernelModule::Depart(int o, const NFGUID& self, int scene, int group, float x, float y, float z) {
     shard_->QueueSwitch(self.nHead64, self.nData64, cls_[o], isplayer_[o], scene, group, x, y, z);
-    obj_of_.erase(self.nHead64, self.nData64);  // this module's no more (its index stays reserved)
-    departed_.insert(self.nHead64, self.nData64, o);
-    DropFunctors(o);
-    DropPendingAdds(self);
+    departing_.insert(self.nHead64, self.nData64, o);
 }
 
 void NFGPUKernelModule::DropDeferred(const NFGUID& self) {
@@ -437,7 +440,7 @@ void NFGPUKernelModule::WindowApplied() {
 bool NFGPUKernelModule::DestroyObject(const NFGUID& self) {
     Flush();  // (the buffered Set calls first: call order)
     const int o = ObjectIndex(self);
-    if (!committed_ || o < 0) return false;
+    if (!committed_ || o < 0 || departing_.count(self.nHead64, self.nData64)) return false;
     DropDeferred(self);
     check(nfk_destroy_objects(world_, 1, &self.nHead64, &self.nData64), "nfk_destroy_objects");
     pending_calls_++;
@@ -452,6 +455,13 @@ bool NFGPUKernelModule::GetRange(const std::string& prop, int k,
     Flush();  // (the buffered Set calls first: call order)
     memberScoreVec.clear();
     if (!committed_ || !prop_id_.count(prop) || k <= 0) return false;
+    if (shard_) {  // every shard's entities (collective: SceneShard::RankTop)
+        std::vector<SceneShard::RankRow> rows;
+        check(shard_->RankTop(PropertyId(prop), k, &rows), "SceneShard::RankTop");
+        for (const auto& q : rows)  // member = NFGUID::ToString() (NFGUID.h:93)
+            memberScoreVec.emplace_back(std::to_string(q.guid_head) + "-" + std::to_string(q.guid_data), q.score);
+        return true;
+    }
     std::vector<int64_t> gh(k), gd(k);
     std::vector<double> sc(k);
     int32_t n = 0;
@@ -501,21 +511,9 @@ void NFGPUKernelModule::Flush() {
 
 // the buffered Sets: one nfk_set_props (it rejects a batch naming an object the world does not
 // have, queueing none of it); then the calls on objects this module has, resolved here, by object
-// index.  Calls on objects that left for another shard are dropped first.
+// index.
 int NFGPUKernelModule::FlushSets() {
-    int32_t n = (int32_t)qs_h_.size();
-    if (departed_.size()) {
-        int32_t k = 0;
-        for (int32_t i = 0; i < n; i++) {
-            if (departed_.count(qs_h_[i], qs_d_[i])) continue;
-            qs_h_[k] = qs_h_[i];
-            qs_d_[k] = qs_d_[i];
-            qs_pid_[k] = qs_pid_[i];
-            qs_bits_[k] = qs_bits_[i];
-            k++;
-        }
-        n = k;
-    }
+    const int32_t n = (int32_t)qs_h_.size();
     if (!n) return NFK_OK;
     const int rc = nfk_set_props(world_, n, qs_h_.data(), qs_d_.data(), qs_pid_.data(), qs_bits_.data());
     if (rc != NFK_ERR_NOTFOUND) return rc;
@@ -534,22 +532,7 @@ int NFGPUKernelModule::FlushSets() {
 // the buffered schedule calls, as FlushSets (the reference's schedule module keeps no object
 // table: a call naming no object of this module changes nothing)
 int NFGPUKernelModule::FlushScheduleCalls() {
-    int32_t n = (int32_t)qh_op_.size();
-    if (departed_.size()) {
-        int32_t k = 0;
-        for (int32_t i = 0; i < n; i++) {
-            if (departed_.count(qh_h_[i], qh_d_[i])) continue;
-            qh_op_[k] = qh_op_[i];
-            qh_h_[k] = qh_h_[i];
-            qh_d_[k] = qh_d_[i];
-            qh_kind_[k] = qh_kind_[i];
-            qh_t_[k] = qh_t_[i];
-            qh_cnt_[k] = qh_cnt_[i];
-            qh_now_[k] = qh_now_[i];
-            k++;
-        }
-        n = k;
-    }
+    const int32_t n = (int32_t)qh_op_.size();
     if (!n) return NFK_OK;
     const int rc = nfk_schedule_calls(world_, n, qh_op_.data(), qh_h_.data(), qh_d_.data(), qh_kind_.data(),
                                       qh_t_.data(), qh_cnt_.data(), qh_now_.data());
@@ -896,7 +879,14 @@ void NFGPUKernelModule::MigrateShard(bool sync) {
     std::vector<Ticket> sent, recv;
     if (sync) check(shard_->Migrate(&sent, &recv), "SceneShard::Migrate");
     else check(shard_->BeginFrame(&sent, &recv), "SceneShard::BeginFrame");
-    for (const Ticket& k : sent) departed_.erase(k.guid_head, k.guid_data);  // (their rows have left the world)
+    for (const Ticket& k : sent) {  // their rows have left the world: no longer this module's objects
+        departing_.erase(k.guid_head, k.guid_data);
+        const int o = obj_of_.find(k.guid_head, k.guid_data);
+        if (o < 0) continue;
+        obj_of_.erase(k.guid_head, k.guid_data);  // (its object index stays reserved)
+        DropFunctors(o);
+        DropPendingAdds(NFGUID(k.guid_head, k.guid_data));
+    }
     for (const Ticket& k : recv) {
         const NFGUID g(k.guid_head, k.guid_data);
         const int o = (int)guids_.size();

@@ -188,6 +188,53 @@ int SceneShard::Migrate(std::vector<Ticket>* sent, std::vector<Ticket>* received
     return r;
 }
 
+// ZREVRANGE order of two leaderboard rows: score descending, then member NFGUID::ToString() descending
+static bool zrev_before(const SceneShard::RankRow& a, const SceneShard::RankRow& b) {
+    if (a.score != b.score) return a.score > b.score;
+    const std::string ma = std::to_string(a.guid_head) + "-" + std::to_string(a.guid_data);
+    const std::string mb = std::to_string(b.guid_head) + "-" + std::to_string(b.guid_data);
+    return ma > mb;
+}
+
+int SceneShard::RankTop(int pid, int k, std::vector<RankRow>* out) {
+    out->clear();
+    if (k < 0) k = 0;
+    std::vector<int64_t> gh((size_t)k + 1), gd((size_t)k + 1);
+    std::vector<double> sc((size_t)k + 1);
+    int32_t n = 0;
+    const int status = k ? nfk_rank_top(world_, pid, k, &n, gh.data(), gd.data(), sc.data()) : NFK_OK;
+    // (this rank's collectives in one order on every rank: the ticket gather in flight finishes first;
+    // BeginFrame still takes its plan)
+    if (pending_.valid()) pending_.wait();
+    // [count (-1: this rank failed), then head, data, score bits per row]
+    std::vector<int64_t> mine(1, status ? -1 : (int64_t)n), all;
+    for (int32_t i = 0; !status && i < n; i++) {
+        mine.push_back(gh[(size_t)i]);
+        mine.push_back(gd[(size_t)i]);
+        mine.push_back((int64_t)f64_bits(sc[(size_t)i]));
+    }
+    transport_calls++;
+    const int r = t_->AllGather(mine, all);
+    if (r) return r;
+    int bad = 0;
+    for (size_t at = 0; at < all.size();) {
+        const int64_t c = all[at++];
+        if (c < 0) {
+            bad = 1;
+            continue;
+        }
+        for (int64_t i = 0; i < c && at + 3 <= all.size(); i++, at += 3)
+            out->push_back({all[at], all[at + 1], bits_f64(all[at + 2])});
+    }
+    if (status || bad) {
+        out->clear();
+        return status ? status : NFK_ERR_STATE;  // (a peer's nfk_rank_top failed)
+    }
+    std::stable_sort(out->begin(), out->end(), zrev_before);
+    if ((int)out->size() > k) out->resize((size_t)k);
+    return NFK_OK;
+}
+
 // the rows of a global plan (every rank's tickets in (source rank, call) order), rank to rank
 int SceneShard::Rows(const std::vector<int64_t>& plan, std::vector<Ticket>* sent, std::vector<Ticket>* received) {
     const int ws = t_->Size(), me = t_->Rank();

@@ -226,4 +226,18 @@ int nfs_stats(void* shard, int64_t* out4) {
     out4[3] = c->s->frames;
     return NFK_OK;
 }
+
+int nfs_rank_top(void* shard, int32_t pid, int32_t k, int32_t* n_out, int64_t* gh, int64_t* gd, double* score) {
+    CShard* c = (CShard*)shard;
+    if (!c || !n_out || k < 0) return NFK_ERR_ARG;
+    std::vector<nfgpu::SceneShard::RankRow> rows;
+    const int r = c->s->RankTop(pid, k, &rows);
+    *n_out = (int32_t)rows.size();
+    for (size_t i = 0; i < rows.size(); i++) {
+        gh[i] = rows[i].guid_head;
+        gd[i] = rows[i].guid_data;
+        score[i] = rows[i].score;
+    }
+    return r;
+}
 }  // extern "C"

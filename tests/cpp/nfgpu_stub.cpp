@@ -5,6 +5,7 @@
 // write wins, no change predicates, no events, no heartbeats), and reports empty frame outputs.  The
 // test checks the adapter's wiring — the schema it derives from the class module, the objects and
 // values it hands over, where it routes each call — not frame semantics (the GPU tests do that).
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -442,8 +443,32 @@ int nfk_read_frame(void*, uint32_t, nfk_frame_host* out) {
     memset(out, 0, sizeof *out);
     return NFK_OK;
 }
-int nfk_rank_top(void*, int32_t, int32_t, int32_t* n, int64_t*, int64_t*, double*) {
-    *n = 0;
+// the live objects' top k by the property's value (ZREVRANGE order: score descending, then the
+// member string "head-data" descending), as the library's nfk_rank_top answers
+int nfk_rank_top(void* w, int32_t pid, int32_t k, int32_t* n, int64_t* gh, int64_t* gd, double* score) {
+    Stub* s = S(w);
+    struct R {
+        double v;
+        std::string m;
+        int64_t h, d;
+    };
+    std::vector<R> all;
+    for (const auto& kv : s->idx) {
+        const uint64_t b = s->words[(size_t)kv.second][(size_t)word_of(s, pid)];
+        double v;
+        if (pid < s->cfg.n_int) v = (double)(int64_t)b;
+        else memcpy(&v, &b, 8);
+        all.push_back({v, std::to_string(kv.first.first) + "-" + std::to_string(kv.first.second), kv.first.first,
+                       kv.first.second});
+    }
+    std::sort(all.begin(), all.end(), [](const R& a, const R& b) { return a.v != b.v ? a.v > b.v : a.m > b.m; });
+    *n = (int32_t)std::min<size_t>(all.size(), (size_t)std::max(k, 0));
+    for (int32_t i = 0; i < *n; i++) {
+        gh[i] = all[(size_t)i].h;
+        gd[i] = all[(size_t)i].d;
+        score[i] = all[(size_t)i].v;
+    }
+    logf("rank_top %d %d %d", pid, k, *n);
     return NFK_OK;
 }
 }

@@ -7,7 +7,11 @@
 // callbacks see is written per rank with global object indices, to be compared with the
 // single-world oracle split by owner (tests/test_shard_cpp.py).
 //
-// usage: plugin_shard_replay <workload.nfio> <out_dir> <ranks>
+// usage: plugin_shard_replay <workload.nfio> <out_dir> <ranks> [async]
+//   async 1: no MigrateNow — the departures move through Execute's own asynchronous exchange (tickets
+//   gathered at the end of an Execute, rows moved at the start of the next), so an entity ticks on its
+//   source shard for one more frame after its SwitchScene; calls on entities in transit are skipped
+//   (the test compares the heartbeat functors: schedules travel with the rows)
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -26,7 +30,8 @@ using namespace nfgpu;
 static std::string cstr(const uint8_t* p) { return std::string((const char*)p, strnlen((const char*)p, 32)); }
 
 int main(int argc, char** argv) {
-    if (argc != 4) return 2;
+    if (argc != 4 && argc != 5) return 2;
+    const bool async = argc == 5 && atoi(argv[4]) != 0;
     nfio_file wf;
     if (nfio_read(argv[1], &wf)) return 2;
     const std::string out_dir = argv[2];
@@ -240,16 +245,16 @@ int main(int argc, char** argv) {
                     cur_gr[o] = sw_group[wi];
                 }
                 const NFGUID g(gh[o], gd[o]);
-                if (km.ObjectIndex(g) < 0) continue;  // another rank's
+                if (km.ObjectIndex(g) < 0 || km.Departing(g)) continue;  // another rank's (or leaving)
                 if (owner(cur_sc[o]) == r) km.CreateScene(cur_sc[o]);
                 if (!km.SwitchScene(g, cur_sc[o], cur_gr[o], sw_x[wi], sw_y[wi], sw_z[wi])) {
                     rc[r] = 5;
                 }
             }
-            km.MigrateNow();
+            if (!async) km.MigrateNow();
             for (; hi < NH && h_tick[hi] == tk; hi++) {
                 const NFGUID g(gh[h_obj[hi]], gd[h_obj[hi]]);
-                if (km.ObjectIndex(g) < 0) continue;
+                if (km.ObjectIndex(g) < 0 || km.Departing(g)) continue;
                 now = h_time[hi];
                 if (h_op[hi] == 1) km.AddSchedule(g, kname[h_kind[hi]], hb, h_int[hi], h_cnt[hi]);
                 else if (h_op[hi] == 2) km.RemoveSchedule(g, kname[h_kind[hi]]);
@@ -257,7 +262,7 @@ int main(int argc, char** argv) {
             }
             for (; xi < NX && x_tick[xi] == tk; xi++) {
                 const NFGUID g(gh[x_obj[xi]], gd[x_obj[xi]]);
-                if (km.ObjectIndex(g) < 0) continue;
+                if (km.ObjectIndex(g) < 0 || km.Departing(g)) continue;
                 if (x_pid[xi] < NI) {
                     km.SetPropertyInt(g, pname[x_pid[xi]], (int64_t)x_bits[xi]);
                 } else {

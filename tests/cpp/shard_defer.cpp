@@ -75,10 +75,14 @@ int main(int argc, char** argv) {
                 CHECK(km.SwitchScene(F, 1, 4, 0.f, 0.f, 0.f), "SwitchScene(F) within the shard");
                 CHECK(km.SwitchScene(F, 2, 5, 0.f, 0.f, 0.f), "SwitchScene(F)");
                 CHECK(km.SwitchScene(G, 2, 6, 0.f, 0.f, 0.f), "SwitchScene(G)");
-                // G left at once; E and F stay this module's until the frame applied their change
-                CHECK(km.ObjectIndex(G) < 0 && km.ObjectIndex(E) >= 0 && km.ObjectIndex(F) >= 0, "after the calls");
+                // G's departure is queued (it stays this module's until its row is exported); E and F
+                // stay this module's until the frame applied their change
+                CHECK(km.Departing(G) && km.ObjectIndex(G) >= 0 && !km.Departing(E) && !km.Departing(F) &&
+                          km.ObjectIndex(E) >= 0 && km.ObjectIndex(F) >= 0, "after the calls");
+                CHECK(!km.SwitchScene(G, 1, 2, 0.f, 0.f, 0.f) && !km.DestroyObject(G), "G in transit");
             }
             km.MigrateNow();  // G moves now; E and F would be refused by the export
+            if (r == 0) CHECK(km.ObjectIndex(G) < 0 && !km.Departing(G), "G left");
             for (int f = 0; f < 3; f++) {
                 km.Execute();
                 now += 100;

@@ -153,3 +153,64 @@ def test_plugin_shard_replay_matches_oracle(gpu_available, tmp_path, ranks):
         np.testing.assert_array_equal(got["final_s_present"][:, own], ref["final_s_present"][:, own])
     assert np.all(owned == 1)        # every entity on exactly one shard
     assert moved > 40 * ranks // 2   # entities did cross shards
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_plugin_shard_async_exchange_keeps_functors(gpu_available, tmp_path, ranks):
+    """The plugin's own asynchronous exchange (no MigrateNow: tickets gathered at the end of an
+    Execute, rows moved at the start of the next): an entity whose cross-shard SwitchScene is queued
+    ticks on its source shard for one more device frame, and its heartbeat functors fire there with it
+    (they were dropped at the SwitchScene and those calls were lost on both shards).  The
+    schedules travel with the rows, so per frame the functor calls of all ranks together equal the
+    single-world oracle's fired list — none lost, none twice — while entities cross shards."""
+    import numpy as np
+    from noahgameframe_amd import nfio, workload
+    from tests.parity import run_oracle
+    exe = os.path.join(ROOT, "tests", "cpp", "_bin", "plugin_shard_replay")
+    _build()
+    w = workload.make_world(n_obj=4000, n_scenes=4, groups_per_scene=5, players_per_group=3, n_ticks=10,
+                            seed=91 + ranks, switch_frac=0.04, switch_new_groups=True, ext_frac=0.05, host_ops=False)
+    ref = run_oracle(w)
+    wp = str(tmp_path / "w.nfio")
+    nfio.write(wp, w)
+    r = subprocess.run([exe, wp, str(tmp_path), str(ranks), "1"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    outs = [nfio.read(str(tmp_path / f"rank{k}.nfio")) for k in range(ranks)]
+    moved = sum(int(o["migrated"][0]) for o in outs)
+    for t in range(int(w["cfg"][7])):
+        got = sorted((int(o_), int(k_), int(r_)) for out in outs
+                     for o_, k_, r_ in zip(out[f"fi_t{t}_obj"], out[f"fi_t{t}_kind"], out[f"fi_t{t}_rem"]))
+        exp = sorted((int(o_), int(k_), int(r_)) for o_, k_, r_ in
+                     zip(ref[f"fi_t{t}_obj"], ref[f"fi_t{t}_kind"], ref[f"fi_t{t}_rem"]))
+        assert got == exp, (t, sorted(set(exp) - set(got))[:8], sorted(set(got) - set(exp))[:8])
+    owned = sum(out["final_own"].astype(np.int64) for out in outs)
+    assert np.all(owned == 1)
+    assert moved > 40 * ranks // 2
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_shard_rank_top_host_stub(tmp_path, ranks):
+    """NFIRankRedisModule::GetRange across the C++ scene shards (SceneShard::RankTop, what
+    NFGPUKernelModule::GetRange uses with a shard attached; NFCRankRedisModule.cpp:109-118): every
+    rank's merged top k equals one world's nfk_rank_top over all the entities — an int and an f64
+    property with ties, members whose string order is not numeric, k below / at / above the entity
+    count — over the host stand-in transport and the stub C-ABI (tests/cpp/shard_rank.cpp)."""
+    _build()
+    exe = os.path.join(ROOT, "tests", "cpp", "_bin", "shard_rank")
+    env = dict(os.environ, NFGPU_STUB_LOG=str(tmp_path / "stub.log"),
+               LD_LIBRARY_PATH=STUB + ":" + os.environ.get("LD_LIBRARY_PATH", ""))
+    r = subprocess.run([exe, str(ranks)], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "ok" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_shard_rank_top_device(gpu_available, ranks):
+    """The same with the ranks' worlds on the GPU (libnfgpu.so: nfk_rank_top's device radix select)."""
+    _build()
+    exe = os.path.join(ROOT, "tests", "cpp", "_bin", "shard_rank")
+    r = subprocess.run([exe, str(ranks)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "ok" in r.stdout
