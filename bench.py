@@ -466,15 +466,28 @@ def main():
     dom = max((k for k in kern if kern[k]["alg_bytes_per_launch"]), key=lambda k: kern[k]["avg_us"])
     d = kern[dom]
     achieved = d["alg_bytes_per_launch"] / (d["avg_us"] * 1e-6) / 1e9
-    traffic, traffic_src = None, None
+    traffic, traffic_src, traffic_rw = None, None, None
     if os.path.exists(args.pmc_json) and not migrating:
         try:
             pm = json.load(open(args.pmc_json))
             ent = pm.get(f"config{args.config}", {}).get(dom) or (pm.get(dom) if args.config == 1 else None)
             traffic = (ent or {}).get("hbm_bytes_per_launch")
             traffic_src = ((pm.get(f"config{args.config}") or {}).get("source") or pm.get("source")) if traffic else None
+            if traffic:
+                traffic_rw = {"read": ent.get("read_bytes_per_launch"), "written": ent.get("write_bytes_per_launch")}
         except Exception:
             traffic = None
+    # k_tick's algorithmic bytes split into written and read (the tally counts both): in a frame without
+    # SetProperty calls every dirty event is its slot's 8-byte write-back + a 24-byte event record
+    # (slot, property, old, new), every fired heartbeat its 16-byte schedule record + a 12-byte fired
+    # record, every recipient a 4-byte word (fused tiles store no per-event message offsets), and with
+    # record programs every slot its 4-byte fired mask; the rest of the tally is reads
+    alg_rw = None
+    if dom == "k_tick" and args.config in (0, 1, 3):
+        wr = 32.0 * s["n_prop_events"] + 28.0 * s["n_fired"] + 4.0 * s["n_msgs"]
+        alg_rw = {"written": wr, "read": d["alg_bytes_per_launch"] - wr,
+                  "how": "written = 32 B per dirty event + 28 B per fired heartbeat + 4 B per recipient (k_tick's "
+                         "byte accounting, nfgpu_tick.hpp); read = the in-kernel tally minus that"}
     # the bandwidth a perfectly coalesced stream mix with this kernel's read:write ratio reaches on
     # an MI355X (tools/hbm_mix.hip), beside the 8 TB/s spec peak
     ceiling = None
@@ -520,13 +533,26 @@ def main():
         if migrating else None,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src, "mix_ceiling": ceiling},
+                     "traffic_source": traffic_src, "traffic_rw": traffic_rw, "alg_bytes_rw": alg_rw,
+                     "mix_ceiling": ceiling},
         "kernels": kern,
         "per_frame": {"prop_events": s["n_prop_events"], "rec_events": s["n_rec_events"], "fired": s["n_fired"],
                       "msgs": s["n_msgs"], "alg_bytes_all_kernels": total_alg,
                       "frame_GBps_alg": total_alg / (elapsed / args.steps) / 1e9},
         "cpu_baseline": None,
     }
+    # a launch-bound world: the per-kernel HIP events around every launch outlast the frame itself, so
+    # that kernel time (and a bandwidth from it) is no evidence
+    if d["avg_us"] * 1e-3 > out["ms_per_step"]:
+        out["roofline"]["frac"] = None
+        out["roofline"]["achieved"] = None
+        out["roofline"]["note"] = (f"launch-bound: {dom}'s HIP-event time ({d['avg_us']:.1f} us) exceeds the frame "
+                                   f"({out['ms_per_step'] * 1000:.1f} us); no bandwidth claimed")
+    # what the timed frame produces for the fan-out: the recipient runs per tile; each event's message
+    # offset is counted on the device when a consumer reads the frame (k_counted_moff), not in it
+    out["per_frame"]["message_offsets"] = ("produced at read time by k_counted_moff (nfk_outputs_get / nfk_read_*), "
+                                           "outside the timed frame; the headline loop's nfk_outputs_get builds "
+                                           "the dense ranks")
     if rank == 0 and world == 1 and args.config == 1 and args.host_calls == "auto":
         out["host_calls"] = host_calls_run(args, torch, kernel, workload)
     if rank == 0 and world == 1 and args.config == 1 and args.plugin_frame == "auto":
@@ -550,7 +576,8 @@ def other_config_legs(args):
     legs = {}
     for c in (0, 3, 4):
         cmd = [sys.executable, os.path.abspath(__file__), "--config", str(c), "--steps", str(args.steps),
-               "--warmup", str(args.warmup), "--cpu-baseline", "off", "--other-configs", "off"]
+               "--warmup", str(args.warmup), "--cpu-baseline", args.cpu_baseline, "--cpu-seconds", "8",
+               "--other-configs", "off"]
         env = dict(os.environ)
         for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
             env.pop(k, None)
@@ -572,9 +599,9 @@ def other_config_legs(args):
             "dominant_kernel": {"name": rf["kernel"], "avg_us": d["kernels"][rf["kernel"]]["avg_us"],
                                 "alg_bytes_per_launch": d["kernels"][rf["kernel"]]["alg_bytes_per_launch"]},
             "kernels": {k: round(v["avg_us"], 2) for k, v in d["kernels"].items()},
-            "roofline": {"achieved": rf["achieved"], "peak": rf["peak"], "unit": rf["unit"], "frac": rf["frac"],
-                         "traffic": rf["traffic"], "traffic_source": rf["traffic_source"]},
-            "per_frame": d["per_frame"]}
+            "roofline": {k_: rf.get(k_) for k_ in ("achieved", "peak", "unit", "frac", "traffic", "traffic_source",
+                                                   "traffic_rw", "alg_bytes_rw", "note")},
+            "per_frame": d["per_frame"], "cpu_baseline": d.get("cpu_baseline")}
     return legs
 
 

@@ -21,8 +21,9 @@ static_assert(kRTile >= 1 && kRTile <= 64, "a record tile is at most one wave of
 constexpr uint32_t kRrcHost = 0x03FFFFFFu;
 constexpr int kRrcSitShift = 26;
 
-// device error word bits (Ctrl::err)
-constexpr unsigned kErrMsgCap = 4, kErrTouch = 8, kErrFanBound = 16;
+// device error word bits (Ctrl::err); kErrRemain: a fired heartbeat's remain was read from an LDS slot
+// this launch never wrote (only with kAblCheckRem)
+constexpr unsigned kErrMsgCap = 4, kErrTouch = 8, kErrFanBound = 16, kErrRemain = 32;
 
 // Control block: frame totals written by k_scan_tiles, byte tallies accumulated across frames,
 // the error word is sticky until nfk_summary_get clears it.  msg_extent = end of the last tile's
@@ -87,6 +88,11 @@ constexpr unsigned kAblScanKernel = 1u << 28;  // dense ranks by k_scan_tiles in
 // serialise at ~7 ns each, profiles/r08s_last_arrival_ranks_ab.txt, so only small worlds gain)
 constexpr int kLbMaxTiles = 256;
 constexpr unsigned kAblNoFuse = 4096;  // fan-out in k_fanout instead of k_tick's tail (outputs stay exact)
+// a check, outputs exact: k_tick marks every kind's remain slot (s_rem) unwritten at its start and
+// raises kErrRemain when the fired list reads one that the schedule scan did not write (the r10w
+// hipRTC fired-list corruption read such slots: DESIGN.md §3)
+constexpr unsigned kAblCheckRem = 64;
+constexpr int32_t kRemUnset = (int32_t)0x80000001;
 
 // record op compiled from the kind programs, sorted by (rec, col)
 struct RecOp {

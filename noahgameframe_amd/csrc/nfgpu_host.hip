@@ -3926,6 +3926,7 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     clear_err_host(w);  // (the stream is idle: read_ctrl synchronised it)
     if (c.err & kErrTouch) return fail(NFK_ERR_TOUCH, "device touch list overflow");
     if (c.err & kErrFanBound) return fail(NFK_ERR_STATE, "a tile's fan-out exceeded its bound");
+    if (c.err & kErrRemain) return fail(NFK_ERR_STATE, "k_tick read a fired heartbeat's remain it never wrote");
     if (c.err & kErrMsgCap)
         return fail(NFK_ERR_CAPACITY, "device output capacity exceeded (err=" + std::to_string(c.err) + ")");
     return NFK_OK;

@@ -376,6 +376,8 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         s_pb[2] = 1;
     }
     int32_t* s_rem = (int32_t*)(s_o + (size_t)S::n_w(d) * kTPB);  // [n_kind][kTPB] remain after a fire
+    if (d.ablate & kAblCheckRem)  // (this thread's own column: read back only by this thread)
+        for (int k = 0; k < S::n_kind(d); k++) s_rem[k * kTPB + threadIdx.x] = kRemUnset;
     unsigned bytes = 0;
     uint32_t fired = 0, xh = 0, wm = 0;
     uint64_t desc = kDeadDesc;
@@ -606,9 +608,11 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             const int k = __builtin_ctz(fl);
             fl &= fl - 1;
             constexpr bool kNE = (S::kNt & kNtEventStore) != 0;
+            const int32_t rem = s_rem[k * kTPB + threadIdx.x];
+            if ((d.ablate & kAblCheckRem) && rem == kRemUnset) dev_error(d, kErrRemain);
             st_off_nt<kNE>(t_fis, pfi, (uint32_t)e);
             st_off_nt<kNE>(t_fik, pfi, (uint32_t)k);
-            st_off_nt<kNE>(t_fir, pfi, s_rem[k * kTPB + threadIdx.x]);
+            st_off_nt<kNE>(t_fir, pfi, rem);
             pfi++;
             bytes += 12;
         }

@@ -583,3 +583,16 @@ def test_record_reads_see_queued_sets(gpu_available):
         want = cur.get(k, int(cells[o[i], col[i], row[i]])) if (int(used[o[i]]) >> int(row[i])) & 1 else 0
         assert int(got[i]) == want, (i, k)
     m.close()
+
+
+@pytest.mark.parametrize("jit", ["1", "0"], ids=["hiprtc", "library"])
+def test_fired_remain_slots_written(gpu_available, monkeypatch, jit):
+    """The r10w hipRTC corruption put words of the LDS that no schedule scan had written
+    into the fired list's remain counts.  With kAblCheckRem (NFGPU_ABLATE=64) k_tick marks every kind's
+    remain slot unwritten at its start and raises a device error when the fired list reads one the
+    scan did not write: none here, on the hipRTC and the library kernels, and the outputs stay exact."""
+    monkeypatch.setenv("NFGPU_ABLATE", "64")
+    monkeypatch.setenv("NFGPU_JIT", jit)
+    for kw in (dict(records=True, rec_rows=16, sched_edges=True), dict(set_ops=True, host_ops=True, ext_frac=0.05)):
+        w = workload.make_world(n_obj=3000, n_scenes=2, groups_per_scene=6, players_per_group=3, n_ticks=8, seed=17, **kw)
+        compare_runs(run_gpu(w), run_oracle(w))
