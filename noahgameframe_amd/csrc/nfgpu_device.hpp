@@ -68,14 +68,10 @@ constexpr unsigned kAblNoRun = 512, kAblNoLoads = 1024, kAblNoEmit = 2048;  // t
 constexpr unsigned kAblNoWriteBack = 1u << 18, kAblNoSchedStore = 1u << 19;  // timing only (k_tick)
 constexpr unsigned kAblGroupColumns = 1u << 20, kAblSigGroups = 1u << 21;  // column layouts (outputs exact)
 constexpr unsigned kAblNoPad = 1u << 22;  // columns / schedule kinds at power-of-two strides (outputs exact)
-constexpr unsigned kAblRecVec = 1u << 23;  // k_records writes whole row-vectors back (outputs exact)
 constexpr unsigned kAblFanWin16 = 1u << 24, kAblFanWin32 = 1u << 25;  // k_tick fan-out LDS window up to 16 / 32 recipients (outputs exact)
 constexpr unsigned kAblFan1 = 1u << 26;      // k_tick fan-out: one recipient per lane (the round-1 form; outputs exact)
 constexpr unsigned kAblTinyTcap = 1u << 27;  // test hook: k_tick's fan-out bound set to 4 messages (kErrFanBound)
 constexpr unsigned kAblForceMsgCap = 1u << 29;  // test hook: the frame's ranks also raise kErrMsgCap
-// timing only (k_records): a private record event's recipient word and message offset not stored
-// (what an implicit-self message format would save)
-constexpr unsigned kAblRecNoMsg = 1u << 30;
 // four u32 at a dword-aligned address (gfx950 global memory allows it; one 16-byte store)
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Pad between consecutive property columns and schedule-kind arrays (bytes): with cap a power of
@@ -89,10 +85,24 @@ constexpr unsigned kAblScanKernel = 1u << 28;  // dense ranks by k_scan_tiles in
 constexpr int kLbMaxTiles = 256;
 constexpr unsigned kAblNoFuse = 4096;  // fan-out in k_fanout instead of k_tick's tail (outputs stay exact)
 // a check, outputs exact: k_tick marks every kind's remain slot (s_rem) unwritten at its start and
-// raises kErrRemain when the fired list reads one that the schedule scan did not write (the r10w
+// raises kErrRemain when the fired list reads one for a counted heartbeat that the schedule scan
+// did not write (a counted heartbeat's remain is >= 0 after a fire; a forever one's may be the
+// sentinel itself, so those are not checked) (the r10w
 // hipRTC fired-list corruption read such slots: DESIGN.md §3)
 constexpr unsigned kAblCheckRem = 64;
 constexpr int32_t kRemUnset = (int32_t)0x80000001;
+
+// Where row r of a record sits in its slot's [rows] vector of one column: the used rows first, in
+// row order, then the unused rows in row order (a stable partition by the used-row mask, so the
+// mask alone maps rows to places and back).  A wave reading the used rows of a column reads one
+// dense run of popcount(used) cells instead of the whole row-vector; an unused row keeps its
+// cells (RC:1086-1107: Remove does not clear them).  rowm: the record's row mask.
+__host__ __device__ inline uint32_t rec_pos(uint64_t used, uint64_t rowm, int r) {
+    const uint64_t below = (1ull << r) - 1;  // (r < 64)
+    return ((used >> r) & 1) ? (uint32_t)__builtin_popcountll(used & below)
+                             : (uint32_t)(__builtin_popcountll(used & rowm) + __builtin_popcountll(~used & rowm & below));
+}
+__host__ __device__ inline uint64_t rec_rowm(int rows) { return rows >= 64 ? ~0ull : ((1ull << rows) - 1); }
 
 // record op compiled from the kind programs, sorted by (rec, col)
 struct RecOp {
@@ -233,7 +243,7 @@ struct Dev {
     uint32_t* rss_pos;
     uint32_t* rss_pmsg;
     int32_t n_rss;
-    // records: cells [cap][cols][rows], used masks [cap]
+    // records: cells [cap][cols][rows] in packed row order (rec_pos), used masks [cap]
     uint64_t* rcells[NFK_MAX_RECORDS];
     uint64_t* rused[NFK_MAX_RECORDS];
     // membership (slots sorted by (scene, group, guid))

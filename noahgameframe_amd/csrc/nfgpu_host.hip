@@ -2174,8 +2174,14 @@ int nfk_commit(void* world) {
             for (int32_t s = 0; s < d.N; s++) {
                 int32_t o = w->obj_of_slot[s];
                 if (o < 0) continue;
-                memcpy(&cells[(size_t)s * per], &w->init_rcells[r][(size_t)o * per], per * 8);
                 used[s] = w->init_rused[r][o];
+                // each column's vector in packed row order (rec_pos)
+                const int rows = w->tab.rec_rows[r], cols = w->tab.rec_cols[r];
+                const uint64_t rowm = rec_rowm(rows);
+                const uint64_t* src = &w->init_rcells[r][(size_t)o * per];
+                uint64_t* dst = &cells[(size_t)s * per];
+                for (int c = 0; c < cols; c++)
+                    for (int q = 0; q < rows; q++) dst[(size_t)c * rows + rec_pos(used[s], rowm, q)] = src[(size_t)c * rows + q];
             }
         HIPCHK(hipMemcpy(d.rcells[r], cells.data(), cells.size() * 8, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(d.rused[r], used.data(), used.size() * 8, hipMemcpyHostToDevice));
@@ -2481,35 +2487,58 @@ int nfk_get_records(void* world, int32_t n, const int64_t* gh, const int64_t* gd
             col[i] < 0 || col[i] >= w->tab.rec_cols[r])
             return fail(NFK_ERR_ARG, "record cell out of range");
     }
-    // every query's used-row mask and cell, in one gather (a few single reads for small n)
-    std::vector<uint64_t> addr(2 * (size_t)n), got(2 * (size_t)n);
-    for (int32_t i = 0; i < n; i++) {
-        const int32_t o = obj[i], r = rec[i], rows = w->tab.rec_rows[r], cols = w->tab.rec_cols[r];
-        const uint64_t* cell;
-        const uint64_t* used;
-        if (w->src_row[o] >= 0) {  // entered in this window: its row of the import buffer
-            int64_t off = w->n_pw + 4 * w->cfg.n_kind;
-            for (int x = 0; x < r; x++) off += (int64_t)w->tab.rec_rows[x] * w->tab.rec_cols[x] + 1;
-            const uint64_t* base = w->ins_rows + (size_t)w->src_row[o] * w->row_words + off;
-            cell = base + (size_t)col[i] * rows + row[i];
-            used = base + (size_t)rows * cols;
-        } else if (w->slot_of_obj[o] >= 0) {
-            const size_t sl = (size_t)w->slot_of_obj[o];
-            cell = w->d.rcells[r] + (sl * cols + col[i]) * rows + row[i];
-            used = w->d.rused[r] + sl;
-        } else {
-            return fail(NFK_ERR_STATE, "object without a slot");
+    // every query's used-row mask (this window's cache, else one gather), then the cells of the
+    // rows the device holds as used in a second: a cell's place in its vector follows from the
+    // mask (rec_pos); a row the device holds unused reads 0 unless a queued AddRow writes it
+    std::vector<uint64_t> um(n), cv(n, 0);
+    {
+        std::vector<uint64_t> addr;
+        std::vector<int32_t> miss;
+        for (int32_t i = 0; i < n; i++) {
+            auto it = w->ucache.find(((uint64_t)obj[i] << 3) | (uint32_t)rec[i]);
+            if (it != w->ucache.end()) {
+                um[i] = it->second;
+                continue;
+            }
+            const uint64_t* u;
+            if (int r = used_addr(w, obj[i], rec[i], &u)) return r;
+            addr.push_back((uint64_t)(uintptr_t)u);
+            miss.push_back(i);
         }
-        addr[2 * (size_t)i] = (uint64_t)(uintptr_t)used;
-        addr[2 * (size_t)i + 1] = (uint64_t)(uintptr_t)cell;
+        std::vector<uint64_t> got(addr.size());
+        if (int r = read_abs(w, addr, got.data())) return r;
+        for (size_t q = 0; q < miss.size(); q++) {
+            um[miss[q]] = got[q];
+            w->ucache[((uint64_t)obj[miss[q]] << 3) | (uint32_t)rec[miss[q]]] = got[q];
+        }
     }
     {
-        int r = read_abs(w, addr, got.data());
-        if (r) return r;
+        std::vector<uint64_t> addr;
+        std::vector<int32_t> at;
+        for (int32_t i = 0; i < n; i++) {
+            const int32_t o = obj[i], r = rec[i], rows = w->tab.rec_rows[r], cols = w->tab.rec_cols[r];
+            if (!((um[i] >> row[i]) & 1)) continue;
+            const size_t place = (size_t)col[i] * rows + rec_pos(um[i], rec_rowm(rows), row[i]);
+            const uint64_t* cell;
+            if (w->src_row[o] >= 0) {  // entered in this window: its row of the import buffer
+                int64_t off = w->n_pw + 4 * w->cfg.n_kind;
+                for (int x = 0; x < r; x++) off += (int64_t)w->tab.rec_rows[x] * w->tab.rec_cols[x] + 1;
+                cell = w->ins_rows + (size_t)w->src_row[o] * w->row_words + off + place;
+            } else if (w->slot_of_obj[o] >= 0) {
+                cell = w->d.rcells[r] + (size_t)w->slot_of_obj[o] * cols * rows + place;
+            } else {
+                return fail(NFK_ERR_STATE, "object without a slot");
+            }
+            addr.push_back((uint64_t)(uintptr_t)cell);
+            at.push_back(i);
+        }
+        std::vector<uint64_t> got(addr.size());
+        if (int r = read_abs(w, addr, got.data())) return r;
+        for (size_t q = 0; q < at.size(); q++) cv[at[q]] = got[q];
     }
     for (int32_t i = 0; i < n; i++) {
         const int32_t o = obj[i], r = rec[i], rows = w->tab.rec_rows[r];
-        uint64_t u = got[2 * (size_t)i], c = got[2 * (size_t)i + 1];
+        uint64_t u = um[i], c = cv[i];
         // this window's queued calls on the record replayed in call order: SetRecord* through
         // RC:182 / RC:243 on the row's used state at that call, AddRow / Remove / ClearRecord on the
         // used-row mask (RC:111, RC:1086, RC:1109)
@@ -3719,19 +3748,22 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
         const dim3 g((unsigned)((d.n_rtiles + kWpb - 1) / kWpb)), b(kTPB);
         if (nrss)  // the SetRecord slots' events and messages, for k_records to reserve
             hipLaunchKernelGGL((k_rset_slots<false>), dim3((unsigned)((nrss + kWpb - 1) / kWpb)), b, 0, w->stream, d);
-        if (nrss) {  // (the SetRecord slots' instantiation: the fast path without them stays lean)
+        // (the SetRecord slots' instantiation, and the unfused one: the fast path stays lean)
+        auto launch = [&](auto sets, auto fuse) {
+            constexpr bool kS = decltype(sets)::value, kF = decltype(fuse)::value;
             if (d.n_rops <= 1)
-                hipLaunchKernelGGL((k_records<1, 4, true>), g, b, 0, w->stream, d);
+                hipLaunchKernelGGL((k_records<1, 4, kS, kF>), g, b, 0, w->stream, d);
             else if (d.n_rops <= 2)
-                hipLaunchKernelGGL((k_records<2, 4, true>), g, b, 0, w->stream, d);
+                hipLaunchKernelGGL((k_records<2, 4, kS, kF>), g, b, 0, w->stream, d);
             else
-                hipLaunchKernelGGL((k_records<NFK_MAX_REC_OPS, 2, true>), g, b, 0, w->stream, d);
-        } else if (d.n_rops <= 1)
-            hipLaunchKernelGGL((k_records<1, 4, false>), g, b, 0, w->stream, d);
-        else if (d.n_rops <= 2)
-            hipLaunchKernelGGL((k_records<2, 4, false>), g, b, 0, w->stream, d);
+                hipLaunchKernelGGL((k_records<NFK_MAX_REC_OPS, 2, kS, kF>), g, b, 0, w->stream, d);
+        };
+        using T = std::true_type;
+        using F = std::false_type;
+        if (nrss)
+            d.fuse_rec ? launch(T{}, T{}) : launch(T{}, F{});
         else
-            hipLaunchKernelGGL((k_records<NFK_MAX_REC_OPS, 2, false>), g, b, 0, w->stream, d);
+            d.fuse_rec ? launch(F{}, T{}) : launch(F{}, F{});
         if (nrss)  // ... and written into the room k_records left
             hipLaunchKernelGGL((k_rset_slots<true>), dim3((unsigned)((nrss + kWpb - 1) / kWpb)), b, 0, w->stream, d);
         HIPCHK(hipGetLastError());
@@ -4004,12 +4036,20 @@ int nfk_read_record(void* world, int32_t rec, uint64_t* cells) {
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     HIPCHK(hipStreamSynchronize(w->stream));
     const Dev& d = w->d;
-    size_t per = (size_t)w->tab.rec_rows[rec] * w->tab.rec_cols[rec];
-    std::vector<uint64_t> buf(per * d.N);
+    const int rows = w->tab.rec_rows[rec], cols = w->tab.rec_cols[rec];
+    const uint64_t rowm = rec_rowm(rows);
+    size_t per = (size_t)rows * cols;
+    std::vector<uint64_t> buf(per * d.N), used(d.N);
     HIPCHK(hipMemcpy(buf.data(), d.rcells[rec], buf.size() * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(used.data(), d.rused[rec], used.size() * 8, hipMemcpyDeviceToHost));
     memset(cells, 0, (size_t)w->n_obj * per * 8);
-    for (int32_t s = 0; s < d.N; s++)
-        if (w->obj_of_slot[s] >= 0) memcpy(cells + (size_t)w->obj_of_slot[s] * per, &buf[(size_t)s * per], per * 8);
+    for (int32_t s = 0; s < d.N; s++) {
+        if (w->obj_of_slot[s] < 0) continue;
+        uint64_t* dst = cells + (size_t)w->obj_of_slot[s] * per;  // row order (from packed, rec_pos)
+        const uint64_t* src = &buf[(size_t)s * per];
+        for (int c = 0; c < cols; c++)
+            for (int q = 0; q < rows; q++) dst[(size_t)c * rows + q] = src[(size_t)c * rows + rec_pos(used[s], rowm, q)];
+    }
     return NFK_OK;
 }
 

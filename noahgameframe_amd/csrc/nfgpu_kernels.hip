@@ -807,10 +807,11 @@ __global__ __launch_bounds__(kTPB) void k_rsets(Dev d) {
             cells = d.rcells[q];
             usedp = d.rused[q];
         }
-    uint64_t* cell = cells + ((size_t)e * cols + col) * rows + row;
+    const uint64_t used = usedp[e];
+    uint64_t* cell = cells + ((size_t)e * cols + col) * rows + rec_pos(used, rec_rowm(rows), row);
     const uint64_t c0 = *cell;
     uint64_t v = c0;
-    if ((usedp[e] >> row) & 1) {
+    if ((used >> row) & 1) {
         const bool f64 = d.tab->rec_ctype[r][col] != 0;
         bool logged = false;
         for (uint32_t k = d.rs_first[g]; k < d.rs_first[g + 1]; k++) {
@@ -841,6 +842,17 @@ __global__ __launch_bounds__(kTPB) void k_rsets(Dev d) {
 //       row is covered; the cells are written without Update events; one Add / Cover event;
 //   Remove(row) (RC:1086-1107): a used row's Del event, then the row is unused (cells kept);
 //   ClearRecord (KM:492 -> RC:1109): Remove from the last row to the first.
+// one slot's record vectors [cols][rows] moved from the places of mask `from` to those of `to`
+__device__ void rec_repack(uint64_t* cells, int rows, int cols, uint64_t rowm, uint64_t from, uint64_t to) {
+    if (from == to) return;
+    for (int c = 0; c < cols; c++) {
+        uint64_t* v = cells + (size_t)c * rows;
+        uint64_t t[64];
+        for (int r = 0; r < rows; r++) t[r] = v[rec_pos(from, rowm, r)];
+        for (int r = 0; r < rows; r++) v[rec_pos(to, rowm, r)] = t[r];
+    }
+}
+
 __global__ __launch_bounds__(kTPB) void k_rrows(Dev d) {
     const int l = blockIdx.x * kTPB + threadIdx.x;
     if (l >= d.n_rl) return;
@@ -856,8 +868,11 @@ __global__ __launch_bounds__(kTPB) void k_rrows(Dev d) {
             usedp = d.rused[q];
         }
     cells += (size_t)e * cols * rows;
-    const uint64_t rowm = rows >= 64 ? ~0ull : ((1ull << rows) - 1);
+    const uint64_t rowm = rec_rowm(rows);
     uint64_t used = usedp[e];
+    // the calls run on the cells in row order (rec_pos with an empty mask) and the vectors are
+    // packed again by the final mask (row operations are rare; one private vector per column)
+    rec_repack(cells, rows, cols, rowm, used, 0ull);
     uint32_t* ev = d.rl_ev + d.rl_ev0[l];
     unsigned nev = 0;
     for (uint32_t k = d.rl_c0[l]; k < d.rl_c0[l + 1]; k++) {
@@ -909,6 +924,7 @@ __global__ __launch_bounds__(kTPB) void k_rrows(Dev d) {
                 }
         }
     }
+    rec_repack(cells, rows, cols, rowm, 0ull, used);
     usedp[e] = used;
     d.rl_cnt[l] = nev;
 }
@@ -960,6 +976,7 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
         const unsigned per = event_msgs(desc, rfl);
         const uint64_t used = usedp[e];
         const bool act = lane < rows;
+        const uint32_t lp = act ? rec_pos(used, rec_rowm(rows), lane) : 0u;  // this lane's row's place
         // GetBroadCastObject (AOI:531-593) of one record event into its run at lmo
         auto fan = [&](uint32_t lmo) {
             uint32_t* out = d.msg_rcpt + mrb + lmo;
@@ -1019,7 +1036,7 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
             wb = false;
             if (!act || (!op && gi < 0)) return false;
             const bool has = gi >= 0 && d.rs_has[gi];
-            const uint64_t cur = cells[((size_t)e * cols + c) * rows + lane];
+            const uint64_t cur = cells[((size_t)e * cols + c) * rows + lp];
             nb = cur;
             if (op && ((used >> lane) & 1)) {
                 if (code == NFK_OP_RIADD_CLAMP) {
@@ -1062,7 +1079,7 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
                 bool wb;
                 const bool ev = eval(c, ob, nb, wb);
                 if (wb) {
-                    __builtin_nontemporal_store(nb, cells + ((size_t)e * cols + c) * rows + lane);
+                    __builtin_nontemporal_store(nb, cells + ((size_t)e * cols + c) * rows + lp);
                     bytes += 8;
                 }
                 if (!ev) continue;
@@ -1095,21 +1112,36 @@ __global__ __launch_bounds__(kTPB) void k_rset_slots(Dev d) {
 // order, kGroup at a time with every cell load of the group issued before any is consumed and
 // the next group's loads issued before this group's stores.  A record span's events are staged
 // in the wave's LDS rows and stored dense; changed cells are written back non-temporally.
-// Cells [cap][cols][rows] so a wave reads one (slot, col) row-vector contiguously.
+// Cells [cap][cols][rows] with the used rows packed first (rec_pos), so a wave reads one (slot,
+// col) run of popcount(used) cells contiguously and no line of unused rows.
+
+// x held in a vector register from here on (uniform values the compiler would otherwise keep in
+// scalar registers: k_records' per-op constants and used masks overflow the 102 SGPRs and were
+// spilled to VGPR lanes, one v_readlane per reload, a third of the kernel's VALU instructions)
+template <class T>
+__device__ __forceinline__ T in_vgpr(T x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+// lane l's value in every lane (l wave-uniform): v_readlane into a scalar register
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
+}
 
 // kOps: register slots for the record ops (>= n_rops), kGroup: slots whose cells are in flight
 // together; instantiated so that a frame's op count does not pay for NFK_MAX_REC_OPS registers.
 template <int kOps, int kGroup>
-struct RecGrp {  // one group of slots with record work: their cells and used-row masks
+struct RecGrp {  // one group of slots with record work: their fired kinds and cells
     int js[kGroup];
     uint32_t masks[kGroup];
     uint32_t rsg[kGroup];  // 1 + the slot's index among the SetRecord slots (0: none)
-    uint64_t used[kGroup][kOps];
     uint64_t cur[kGroup][kOps];
 };
 
 // kSets: the frame has SetRecord slots (k_rset_slots writes theirs; here their room is reserved)
-template <int kOps, int kGroup, bool kSets>
+template <int kOps, int kGroup, bool kSets, bool kFuse>
 __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
     __shared__ uint64_t s_eold[kTPB / 64][kOps * 64], s_enew[kTPB / 64][kOps * 64];  // a span's events,
@@ -1121,6 +1153,10 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     const int rt = blockIdx.x * (kTPB / 64) + w;
     if (rt >= d.n_rtiles) return;  // wave-uniform; no barrier follows
     const int nro = d.n_rops;
+    // popcount of a mask's bits below this lane: the lane's row's place among the used rows
+    const auto below = [&](uint64_t m) -> uint32_t {
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    };
     const int s0 = rt * kRTile;
     unsigned bytes = 0;    // per lane
     unsigned sbytes = 0;   // per wave (wave-uniform)
@@ -1139,6 +1175,28 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             bytes += 8;
         }
     }
+    // lane j: slot s0 + j's used-row mask of each op's record, loaded with the descriptors, so a
+    // group's cell addresses (the used rows' places, rec_pos) need no further round trip
+    uint64_t my_used[kOps];
+#pragma unroll
+    for (int j = 0; j < kOps; j++) {
+        my_used[j] = 0;
+        if (j < nro && !(kSets && my_rs) && ((my_mask >> d.rops[j].kind) & 1))
+            my_used[j] = d.rops[j].used[s0 + lane] & rec_rowm(d.rops[j].rows);
+    }
+    // per op: its column's vector of slot 0 (bytes), the slot stride (bytes) and the op's
+    // operands, in vector registers (in_vgpr)
+    uint64_t op_base[kOps], op_a[kOps], op_b[kOps], op_c[kOps];
+    uint32_t op_stride[kOps];
+#pragma unroll
+    for (int j = 0; j < kOps; j++) {
+        const bool on = j < nro;
+        op_base[j] = in_vgpr(on ? (uint64_t)(uintptr_t)(d.rops[j].cells + (size_t)d.rops[j].col * d.rops[j].rows) : 0ull);
+        op_stride[j] = in_vgpr(on ? (uint32_t)(d.rops[j].cols * d.rops[j].rows * 8) : 0u);
+        op_a[j] = in_vgpr(on ? (uint64_t)d.rops[j].a : 0ull);
+        op_b[j] = in_vgpr(on ? (uint64_t)d.rops[j].b : 0ull);
+        op_c[j] = in_vgpr(on ? (uint64_t)d.rops[j].c : 0ull);
+    }
     unsigned long long work = __ballot(my_mask != 0 || my_rs != 0);
     unsigned pos = 0, pmsg = 0;  // tile-local
     // this tile's output runs as wave-uniform base pointers, indexed by 32-bit tile-local offsets
@@ -1147,7 +1205,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     uint64_t* const t_old = d.re_old + re0;
     uint64_t* const t_new = d.re_new + re0;
     uint32_t* const t_moff = d.re_moff + re0;
-    const uint32_t mrb = d.fuse_rec ? d.msg_rb0 + (uint32_t)rt * d.msg_rtcap : 0u;  // fused: this tile's run
+    const uint32_t mrb = kFuse ? d.msg_rb0 + (uint32_t)rt * d.msg_rtcap : 0u;  // fused: this tile's run
     // Two groups in flight: the next group's cell loads are issued before the current group's
     // stores, so its wait covers the stores' acknowledgements (vmcnt counts loads and stores in
     // issue order) instead of a full HBM round trip after them.
@@ -1158,20 +1216,21 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
         for (int g = 0; g < kGroup; g++) {
             G.js[g] = work ? __builtin_ctzll(work) : -1;
             if (work) work &= work - 1;
-            G.masks[g] = G.js[g] >= 0 ? (uint32_t)__shfl((int)my_mask, G.js[g], 64) : 0u;
-            G.rsg[g] = (kSets && G.js[g] >= 0) ? (uint32_t)__shfl((int)my_rs, G.js[g], 64) : 0u;
+            // (js is wave-uniform: lane reads into scalar registers, no LDS permute)
+            G.masks[g] = G.js[g] >= 0 ? rl32(my_mask, G.js[g]) : 0u;
+            G.rsg[g] = (kSets && G.js[g] >= 0) ? rl32(my_rs, G.js[g]) : 0u;
         }
 #pragma unroll
         for (int g = 0; g < kGroup; g++)
 #pragma unroll
             for (int j = 0; j < kOps; j++) {
-                G.used[g][j] = 0;
                 G.cur[g][j] = 0;
                 if (j < nro && G.js[g] >= 0 && !(kSets && G.rsg[g]) && ((G.masks[g] >> d.rops[j].kind) & 1)) {
                     const int e = s0 + G.js[g];
-                    G.used[g][j] = d.rops[j].used[e];
-                    if (lane < d.rops[j].rows)
-                        G.cur[g][j] = (d.rops[j].cells + ((size_t)e * d.rops[j].cols + d.rops[j].col) * d.rops[j].rows)[lane];
+                    // only the used rows: one dense run at the vector's start (rec_pos), lane p
+                    // holding the p-th used row, so every load is lane-aligned
+                    if (lane < __builtin_popcountll(rl64(my_used[j], G.js[g])))
+                        G.cur[g][j] = ((const uint64_t*)(op_base[j] + (uint64_t)e * op_stride[j]))[lane];
                 }
             }
     };
@@ -1180,7 +1239,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
         for (int g = 0; g < kGroup; g++) {
             if (G.js[g] < 0) break;
             const int e = s0 + G.js[g];
-            const uint64_t desc = (uint64_t)__shfl((long long)my_desc, G.js[g], 64);
+            const uint64_t desc = rl64(my_desc, G.js[g]);
             const unsigned cls = (unsigned)(desc >> 60);
             if (kSets && G.rsg[g]) {  // (wave-uniform) a slot with SetRecord calls: k_rset_slots writes its
                              // events into the room reserved here
@@ -1202,22 +1261,22 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                 if (j >= nro || !((G.masks[g] >> d.rops[j].kind) & 1)) continue;
                 const RecOpX& ro = d.rops[j];
                 // algorithmic bytes, counted per wave: the used mask and the used rows' cells
-                const uint64_t rowm = ro.rows >= 64 ? ~0ull : ((1ull << ro.rows) - 1);
-                sbytes += 8u + 8u * (unsigned)__builtin_popcountll(G.used[g][j] & rowm);
-                if (lane >= ro.rows || !((G.used[g][j] >> lane) & 1)) continue;
+                const int nu = __builtin_popcountll(rl64(my_used[j], G.js[g]));
+                sbytes += 8u + 8u * (unsigned)nu;
+                if (lane >= nu) continue;  // lane p: the p-th used row
                 const uint64_t c = G.cur[g][j];
                 uint64_t nb;
                 bool changed;
                 if (ro.code == NFK_OP_RIADD_CLAMP) {
-                    int64_t v = (int64_t)(c + (uint64_t)ro.a);
-                    v = v < ro.b ? ro.b : v;
-                    v = v > ro.c ? ro.c : v;
+                    int64_t v = (int64_t)(c + op_a[j]);
+                    v = v < (int64_t)op_b[j] ? (int64_t)op_b[j] : v;
+                    v = v > (int64_t)op_c[j] ? (int64_t)op_c[j] : v;
                     nb = (uint64_t)v;
                     changed = v != (int64_t)c;  // TData::operator== (NFIDataList.h:98)
                 } else {
                     const double x = __longlong_as_double((long long)c);
-                    const double m = x * __longlong_as_double(ro.a);
-                    const double v = m + __longlong_as_double(ro.b);
+                    const double m = x * __longlong_as_double((long long)op_a[j]);
+                    const double v = m + __longlong_as_double((long long)op_b[j]);
                     const double df = v - x;
                     changed = !(df < 0.001 && df > -0.001);  // NFIDataList.h:106-113
                     nb = (uint64_t)__double_as_longlong(v);
@@ -1225,8 +1284,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                 if (changed) {
                     // (non-temporal: the cell is not read again this frame; measured -7 % of k_records,
                     // while non-temporal event stores cost +30 %: profiles/r01zzf_*)
-                    if (!(d.ablate & kAblRecVec))
-                        __builtin_nontemporal_store(nb, ro.cells + ((size_t)e * ro.cols + ro.col) * ro.rows + lane);
+                    __builtin_nontemporal_store(nb, (uint64_t*)(op_base[j] + (uint64_t)e * op_stride[j]) + lane);
                     wr[j] = true;
                     ch[j] = nb != c;  // coalesced diff: bits must differ
                     nv[j] = nb;
@@ -1235,23 +1293,22 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
 #pragma unroll
             for (int j = 0; j < kOps; j++)
                 if (j < nro) sbytes += 8u * (unsigned)__builtin_popcountll(__ballot(wr[j]));  // cells written
-            if (d.ablate & kAblRecVec) {
-                // whole row-vectors: every row of an operated column stored back (its new value or the
-                // value it had), so the column's lines are written in full
-#pragma unroll
-                for (int j = 0; j < kOps; j++) {
-                    if (j >= nro || !((G.masks[g] >> d.rops[j].kind) & 1)) continue;
-                    const RecOpX& ro = d.rops[j];
-                    if (lane < ro.rows)
-                        __builtin_nontemporal_store(ch[j] ? nv[j] : G.cur[g][j],
-                                                    ro.cells + ((size_t)e * ro.cols + ro.col) * ro.rows + lane);
-                }
-            }
             // per-slot event order (rec, row, col): records outer, lanes (rows), cols inner
 #pragma unroll
             for (int j0 = 0; j0 < kOps; j0++) {
                 if (j0 >= nro || d.rops[j0].gfirst != j0) continue;  // j0 opens a record's op span
                 const int j1 = d.rops[j0].glast;
+                // lane p's row (lane p holds the p-th used row): every lane sends its lane number to
+                // its row's place (rec_pos: a permutation of the lanes, rows past the record's
+                // rows in place), so lane p receives the row placed at p
+                uint64_t um = 0;
+#pragma unroll
+                for (int j = 0; j < kOps; j++)
+                    if (j >= j0 && j <= j1) um |= rl64(my_used[j], G.js[g]);  // (one record: one mask or 0)
+                const uint32_t place = ((um >> lane) & 1) ? below(um)
+                                       : lane < d.rops[j0].rows ? (uint32_t)__builtin_popcountll(um) + below(~um & rec_rowm(d.rops[j0].rows))
+                                                      : (uint32_t)lane;
+                const uint32_t row_at = (uint32_t)__builtin_amdgcn_ds_permute((int)(place * 4), lane);
                 // the span's events before this lane's (rows below it, every column) and in total:
                 // one ballot + lane-mask count per op instead of a wave scan
                 unsigned below = 0, n = 0;
@@ -1276,7 +1333,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     s_eold[w][q] = G.cur[g][j];
                     s_enew[w][q] = nv[j];
                     s_errc[w][q] = ((uint32_t)G.js[g] << kRrcSitShift) | ((uint32_t)d.rops[j].rec << 16) |
-                                   ((uint32_t)lane << 8) | (uint32_t)d.rops[j].col;
+                                   (row_at << 8) | (uint32_t)d.rops[j].col;
                     q++;
                 }
                 __builtin_amdgcn_wave_barrier();  // (one wave's LDS operations complete in order)
@@ -1285,14 +1342,13 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     if (qq >= n) break;
                     const unsigned at = pos + qq;
                     const uint32_t lmo = pmsg + per * qq;
-                    const bool skip_msg = (d.ablate & kAblRecNoMsg) && !(rfl & NFK_PUBLIC);  // (timing only)
                     t_rrc[at] = s_errc[w][qq];
                     t_old[at] = s_eold[w][qq];
                     t_new[at] = s_enew[w][qq];
                     // unfused: the tile-local offset k_fanout expands the event at; fused, the run is
                     // dense in event order and the readers count their way through it (k_counted_moff)
-                    if (!d.fuse_rec) t_moff[at] = lmo;
-                    if (d.fuse_rec && per && !skip_msg) {
+                    if (!kFuse) t_moff[at] = lmo;
+                    if (kFuse && per) {
                         // GetBroadCastObject (AOI:531-593) for the record event, into the tile's run
                         uint32_t* out = d.msg_rcpt + mrb + lmo;
                         if (!(rfl & NFK_PUBLIC)) {
@@ -1309,8 +1365,8 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                     }
                 }
                 // event records, their recipient words and (public) the player run read per event
-                sbytes += n * ((d.fuse_rec ? 20u : 24u) + ((d.fuse_rec && per) ? 4u * per : 0u) +
-                               ((d.fuse_rec && per && (rfl & NFK_PUBLIC)) ? 4u * (uint32_t)((desc >> 32) & 0x3FFF) : 0u));
+                sbytes += n * ((kFuse ? 20u : 24u) + ((kFuse && per) ? 4u * per : 0u) +
+                               ((kFuse && per && (rfl & NFK_PUBLIC)) ? 4u * (uint32_t)((desc >> 32) & 0x3FFF) : 0u));
                 __builtin_amdgcn_wave_barrier();
                 pos += n;
                 pmsg += per * n;

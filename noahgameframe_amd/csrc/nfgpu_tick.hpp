@@ -609,7 +609,12 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             fl &= fl - 1;
             constexpr bool kNE = (S::kNt & kNtEventStore) != 0;
             const int32_t rem = s_rem[k * kTPB + threadIdx.x];
-            if ((d.ablate & kAblCheckRem) && rem == kRemUnset) dev_error(d, kErrRemain);
+            // (a forever heartbeat's remain may be any int32, the sentinel too: sched_edges worlds
+            // wrap it through INT32_MIN; a counted one is >= 0 after a fire.  The forever bit is the
+            // same before and after the scan, so the record's state is read whatever the L1 holds)
+            if ((d.ablate & kAblCheckRem) && rem == kRemUnset &&
+                !(d.s_hot[(size_t)k * d.s_kstr + e].state & kStForever))
+                dev_error(d, kErrRemain);
             st_off_nt<kNE>(t_fis, pfi, (uint32_t)e);
             st_off_nt<kNE>(t_fik, pfi, (uint32_t)k);
             st_off_nt<kNE>(t_fir, pfi, rem);

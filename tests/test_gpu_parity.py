@@ -590,7 +590,8 @@ def test_fired_remain_slots_written(gpu_available, monkeypatch, jit):
     """The r10w hipRTC corruption put words of the LDS that no schedule scan had written
     into the fired list's remain counts.  With kAblCheckRem (NFGPU_ABLATE=64) k_tick marks every kind's
     remain slot unwritten at its start and raises a device error when the fired list reads one the
-    scan did not write: none here, on the hipRTC and the library kernels, and the outputs stay exact."""
+    scan did not write for a counted heartbeat (a forever one's remain wraps through the sentinel in
+    sched_edges worlds): none here, on the hipRTC and the library kernels, and the outputs stay exact."""
     monkeypatch.setenv("NFGPU_ABLATE", "64")
     monkeypatch.setenv("NFGPU_JIT", jit)
     for kw in (dict(records=True, rec_rows=16, sched_edges=True), dict(set_ops=True, host_ops=True, ext_frac=0.05)):
