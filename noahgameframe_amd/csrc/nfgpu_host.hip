@@ -3753,8 +3753,21 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
             constexpr bool kS = decltype(sets)::value, kF = decltype(fuse)::value;
             if (d.n_rops <= 1)
                 hipLaunchKernelGGL((k_records<1, 4, kS, kF>), g, b, 0, w->stream, d);
-            else if (d.n_rops <= 2)
-                hipLaunchKernelGGL((k_records<2, 4, kS, kF>), g, b, 0, w->stream, d);
+            else if (d.n_rops <= 2) {
+                // two known op codes (the fast path's common shape): compiled in
+                const unsigned c0 = d.rops[0].code == NFK_OP_RIADD_CLAMP ? 1u : 2u;
+                const unsigned c1 = d.rops[1].code == NFK_OP_RIADD_CLAMP ? 1u : 2u;
+                if (kS || !kF || d.n_rops != 2)
+                    hipLaunchKernelGGL((k_records<2, 4, kS, kF>), g, b, 0, w->stream, d);
+                else if (c0 == 1 && c1 == 1)
+                    hipLaunchKernelGGL((k_records<2, 4, kS, kF, 5u>), g, b, 0, w->stream, d);
+                else if (c0 == 1 && c1 == 2)
+                    hipLaunchKernelGGL((k_records<2, 4, kS, kF, 9u>), g, b, 0, w->stream, d);
+                else if (c0 == 2 && c1 == 1)
+                    hipLaunchKernelGGL((k_records<2, 4, kS, kF, 6u>), g, b, 0, w->stream, d);
+                else
+                    hipLaunchKernelGGL((k_records<2, 4, kS, kF, 10u>), g, b, 0, w->stream, d);
+            }
             else
                 hipLaunchKernelGGL((k_records<NFK_MAX_REC_OPS, 2, kS, kF>), g, b, 0, w->stream, d);
         };

@@ -1133,15 +1133,17 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
 // kOps: register slots for the record ops (>= n_rops), kGroup: slots whose cells are in flight
 // together; instantiated so that a frame's op count does not pay for NFK_MAX_REC_OPS registers.
 template <int kOps, int kGroup>
-struct RecGrp {  // one group of slots with record work: their fired kinds and cells
+struct RecGrp {  // one group of slots with record work: their ops and cells
     int js[kGroup];
-    uint32_t masks[kGroup];
+    uint32_t masks[kGroup];  // bit j: op j runs on the slot
     uint32_t rsg[kGroup];  // 1 + the slot's index among the SetRecord slots (0: none)
     uint64_t cur[kGroup][kOps];
 };
 
 // kSets: the frame has SetRecord slots (k_rset_slots writes theirs; here their room is reserved)
-template <int kOps, int kGroup, bool kSets, bool kFuse>
+// kCodes: per op j, bits 2j..2j+1 = 1 (RIADD_CLAMP) / 2 (RFAFFINE) when the launch knows it (the
+// common two-op shape: no per-op code branch or its masks), 0 = read from d.rops
+template <int kOps, int kGroup, bool kSets, bool kFuse, unsigned kCodes = 0>
 __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     __shared__ uint8_t s_rflags[NFK_MAX_CLASSES][NFK_MAX_RECORDS];
     __shared__ uint64_t s_eold[kTPB / 64][kOps * 64], s_enew[kTPB / 64][kOps * 64];  // a span's events,
@@ -1178,8 +1180,10 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
     // lane j: slot s0 + j's used-row mask of each op's record, loaded with the descriptors, so a
     // group's cell addresses (the used rows' places, rec_pos) need no further round trip
     uint64_t my_used[kOps];
+    uint32_t my_ops = 0;  // bit j: op j's kind fired on slot s0 + lane
 #pragma unroll
     for (int j = 0; j < kOps; j++) {
+        if (j < nro) my_ops |= ((my_mask >> d.rops[j].kind) & 1u) << j;
         my_used[j] = 0;
         if (j < nro && !(kSets && my_rs) && ((my_mask >> d.rops[j].kind) & 1))
             my_used[j] = d.rops[j].used[s0 + lane] & rec_rowm(d.rops[j].rows);
@@ -1217,7 +1221,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             G.js[g] = work ? __builtin_ctzll(work) : -1;
             if (work) work &= work - 1;
             // (js is wave-uniform: lane reads into scalar registers, no LDS permute)
-            G.masks[g] = G.js[g] >= 0 ? rl32(my_mask, G.js[g]) : 0u;
+            G.masks[g] = G.js[g] >= 0 ? rl32(my_ops, G.js[g]) : 0u;  // (bit j: op j runs on the slot)
             G.rsg[g] = (kSets && G.js[g] >= 0) ? rl32(my_rs, G.js[g]) : 0u;
         }
 #pragma unroll
@@ -1225,7 +1229,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
 #pragma unroll
             for (int j = 0; j < kOps; j++) {
                 G.cur[g][j] = 0;
-                if (j < nro && G.js[g] >= 0 && !(kSets && G.rsg[g]) && ((G.masks[g] >> d.rops[j].kind) & 1)) {
+                if (j < nro && G.js[g] >= 0 && !(kSets && G.rsg[g]) && ((G.masks[g] >> j) & 1)) {
                     const int e = s0 + G.js[g];
                     // only the used rows: one dense run at the vector's start (rec_pos), lane p
                     // holding the p-th used row, so every load is lane-aligned
@@ -1258,7 +1262,7 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
             for (int j = 0; j < kOps; j++) {
                 ch[j] = wr[j] = false;
                 nv[j] = 0;
-                if (j >= nro || !((G.masks[g] >> d.rops[j].kind) & 1)) continue;
+                if (j >= nro || !((G.masks[g] >> j) & 1)) continue;
                 const RecOpX& ro = d.rops[j];
                 // algorithmic bytes, counted per wave: the used mask and the used rows' cells
                 const int nu = __builtin_popcountll(rl64(my_used[j], G.js[g]));
@@ -1267,7 +1271,8 @@ __global__ __launch_bounds__(kTPB) void k_records(Dev d) {
                 const uint64_t c = G.cur[g][j];
                 uint64_t nb;
                 bool changed;
-                if (ro.code == NFK_OP_RIADD_CLAMP) {
+                const unsigned cc = (kCodes >> (2 * j)) & 3u;  // (j unrolled: a constant)
+                if (cc ? cc == 1u : ro.code == NFK_OP_RIADD_CLAMP) {
                     int64_t v = (int64_t)(c + op_a[j]);
                     v = v < (int64_t)op_b[j] ? (int64_t)op_b[j] : v;
                     v = v > (int64_t)op_c[j] ? (int64_t)op_c[j] : v;

@@ -349,7 +349,6 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     __shared__ unsigned s_bytes;
     __shared__ uint32_t s_lb_last;  // this tile ranks the frame's tiles (Dev::lb_rank)
     __shared__ uint32_t s_pb[3];   // pl_slot run of the groups with dirty events [lo, hi), most recipients
-    __shared__ uint32_t s_cm[NFK_MAX_CLASSES];  // Dev::u_cmask
     extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
     const int tile = d.xcd_map ? xcd_tile((int)blockIdx.x, d.n_tiles) : (int)blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
@@ -439,13 +438,6 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
         // the fired heartbeats' effect programs, in schedule-name order
         if (!(d.ablate & (kAblPrograms | kAblNoRun)) && fired) S::run(v, wm, d, fired);
     }
-    if (threadIdx.x < NFK_MAX_CLASSES) {  // (a select over kernel-argument scalars, no indexed copy)
-        uint32_t c = 0;
-#pragma unroll
-        for (int i = 0; i < NFK_MAX_CLASSES; i++) c = threadIdx.x == (unsigned)i ? S::cmask(d, i) : c;
-        s_cm[threadIdx.x] = c;
-    }
-    __syncthreads();  // s_pb / s_bytes / s_cm initialised
     // dirty diff against the frame-start values
     uint32_t dm = 0;
 #pragma unroll
@@ -464,7 +456,14 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     // fan-out message counts (event_msgs): a public property's event goes to every player of the
     // group but the entity itself, a private & !upload one to the entity only.  The message offset
     // of a slot's event = the counts of the dirty slots with lower property ids (Dev::u_lower).
-    const uint32_t cm = s_cm[desc >> 60];  // (class 15, a free slot: no slots)
+    // the entity's class's event masks (Dev::u_cmask; class 15, a free slot: no slots): a select
+    // over kernel-argument scalars, no indexed copy and no barrier
+    uint32_t cm = 0;
+    {
+        const unsigned cls = (unsigned)(desc >> 60);
+#pragma unroll
+        for (int i = 0; i < NFK_MAX_CLASSES; i++) cm = cls == (unsigned)i ? S::cmask(d, i) : cm;
+    }
     const uint32_t pubm = cm & 0xFFFFu, privm = cm >> 16;
     const uint32_t r1 = (uint32_t)((desc >> 46) & 0x3FFF);
     const uint32_t npub = (uint32_t)((desc >> 32) & 0x3FFF) - (r1 ? 1u : 0u);
@@ -511,6 +510,15 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     };
     const unsigned nf = __builtin_popcount(fired);
     const uint32_t dm_ = dm;
+    // tile-local compaction: one block scan of (fired:16 | events:16 | messages:32)
+    unsigned long long tot;
+    const unsigned long long excl =
+        block_excl_scan(((unsigned long long)nf << 48) | ((unsigned long long)nd << 32) | nmsg, s_w, tot);
+    const unsigned pev0 = (unsigned)((excl >> 32) & 0xFFFF);
+    unsigned pfi = (unsigned)(excl >> 48);
+    const unsigned pmsg0 = (unsigned)excl, tmsg = (unsigned)tot;
+    // (after the scan: its barrier orders thread 0's s_pb initialisation before these atomics, and
+    // the barrier before the fan-out orders them before its reads)
     if (fuse) {  // the pl_slot run of the groups whose members have messages (they are contiguous)
         const uint32_t np = (uint32_t)((desc >> 32) & 0x3FFF);
         uint32_t lo = nmsg ? (uint32_t)desc : 0xFFFFFFFFu, hi = nmsg ? (uint32_t)desc + np : 0u;
@@ -526,14 +534,6 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             atomicMax(&s_pb[2], nmax);
         }
     }
-
-    // tile-local compaction: one block scan of (fired:16 | events:16 | messages:32)
-    unsigned long long tot;
-    const unsigned long long excl =
-        block_excl_scan(((unsigned long long)nf << 48) | ((unsigned long long)nd << 32) | nmsg, s_w, tot);
-    const unsigned pev0 = (unsigned)((excl >> 32) & 0xFFFF);
-    unsigned pfi = (unsigned)(excl >> 48);
-    const unsigned pmsg0 = (unsigned)excl, tmsg = (unsigned)tot;
     // this tile's counts for the dense ranks; whether it is the last to publish them (thread 0)
     const bool lb_last = S::kLb && d.lb_rank && lb_arrive(d, tile, (unsigned)((tot >> 32) & 0xFFFF), (unsigned)(tot >> 48), tmsg);
     // this tile's output runs (wave-uniform bases, tile-local 32-bit offsets)
