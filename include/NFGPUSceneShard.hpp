@@ -76,6 +76,9 @@ public:
                           const std::vector<size_t>& rcount, void* stream) = 0;
     // the rows must be complete in memory before AllToAllV (host transports)
     virtual bool NeedsHostSync() const = 0;
+    // after an error, or when a peer never arrives: make a collective this rank is blocked in (or
+    // enters later) return an error instead of waiting; the transport is unusable afterwards
+    virtual void Abort() {}
 };
 
 // Ranks as threads of one process: every collective meets at a barrier in shared state.
@@ -90,6 +93,7 @@ public:
     int AllToAllV(const uint64_t* send, const std::vector<size_t>& scount, uint64_t* recv,
                   const std::vector<size_t>& rcount, void* stream) override;
     bool NeedsHostSync() const override { return true; }
+    void Abort() override;  // every rank's barrier returns an error from now on
 
 private:
     std::shared_ptr<Shared> s_;
@@ -114,6 +118,7 @@ public:
     int AllToAllV(const uint64_t* send, const std::vector<size_t>& scount, uint64_t* recv,
                   const std::vector<size_t>& rcount, void* stream) override;
     bool NeedsHostSync() const override { return false; }
+    void Abort() override;  // ncclCommAbort of both communicators
 
 private:
     void* comm_ = nullptr;       // rows
@@ -178,6 +183,7 @@ private:
     size_t scap_ = 0, rcap_ = 0;
     int every_ = 1;
     std::future<int> pending_;  // the ticket gather started by the last exchange EndFrame
+    bool failed_ = false;       // a transport call of this shard returned an error
     std::vector<int64_t> pending_plan_;
 };
 

@@ -213,6 +213,8 @@ struct World {
     std::vector<uint32_t> ov_prev;
     uint64_t* gat = nullptr;             // device scratch of gathered reads
     size_t gat_cap = 0;
+    uint32_t* moff_tmp = nullptr;        // device scratch of nfk_read_fanout's counted offsets
+    size_t moff_tmp_cap = 0;
     // host worker threads for large call batches (NFGPU_HOST_THREADS, default 1 = none)
     std::unique_ptr<HostPool> pool;
     size_t par_calls = 16384;  // batches from this size on use the pool (NFGPU_PAR_CALLS: tests)
@@ -1710,6 +1712,7 @@ int nfk_destroy(void* world) {
     if (w->look_pin) (void)hipHostFree(w->look_pin);
     if (w->look_stream) (void)hipStreamDestroy(w->look_stream);
     if (w->gat) (void)hipFree(w->gat);
+    if (w->moff_tmp) (void)hipFree(w->moff_tmp);
     if (w->hf_buf) (void)hipFree(w->hf_buf);
     if (w->chain_d) (void)hipFree(w->chain_d);
     if (w->chain_cnt_d) (void)hipFree(w->chain_cnt_d);
@@ -4217,8 +4220,10 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
     if (ncnt) {  // counted on the device (k_counted_moff) from the dense bases
         std::vector<uint32_t> dbv(ntt);
         for (int t = 0; t < ntt; t++) dbv[t] = (uint32_t)db[t];
-        uint32_t* tmp = nullptr;
-        HIPCHK(hipMalloc((void**)&tmp, ((size_t)ntt + (size_t)c.n_ev + (size_t)c.n_re) * 4));
+        // (a world-owned scratch, grown as needed: no allocation per call, nothing to free on errors)
+        r = dev_reserve(w, (void**)&w->moff_tmp, &w->moff_tmp_cap, ((size_t)ntt + (size_t)c.n_ev + (size_t)c.n_re) * 4);
+        if (r) return r;
+        uint32_t* const tmp = w->moff_tmp;
         HIPCHK(hipMemcpy(tmp, dbv.data(), (size_t)ntt * 4, hipMemcpyHostToDevice));
         uint32_t* out = tmp + ntt;  // [n_ev ++ n_re], as msg_off
         hipError_t ce = hipSuccess;
@@ -4237,7 +4242,6 @@ int nfk_read_fanout(void* world, uint32_t* msg_off, int32_t* msg_rcpt_obj) {
                 ce = hipMemcpyAsync(msg_off + c.n_ev, out + c.n_ev, (size_t)c.n_re * 4, hipMemcpyDeviceToHost, w->stream);
         }
         if (ce == hipSuccess) ce = hipStreamSynchronize(w->stream);
-        (void)hipFree(tmp);
         if (ce != hipSuccess) return fail(NFK_ERR_HIP, std::string("k_counted_moff: ") + hipGetErrorString(ce));
     }
     msg_off[c.n_ev + c.n_re] = (uint32_t)nm;

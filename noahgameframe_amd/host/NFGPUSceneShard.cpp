@@ -3,6 +3,8 @@
 #include "NFGPUSceneShard.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -21,12 +23,15 @@ struct HostTransport::Shared {
     std::condition_variable cv;
     int arrived = 0;
     int64_t generation = 0;
+    bool aborted = false;  // HostTransport::Abort: every barrier returns false
     std::vector<const std::vector<int64_t>*> gather_in;
     std::vector<const uint64_t*> send;
     std::vector<const std::vector<size_t>*> scount;
-    // a barrier every rank passes; fn runs on the last arrival, before anyone leaves
-    void barrier(const std::function<void()>& fn = nullptr) {
+    // a barrier every rank passes; fn runs on the last arrival, before anyone leaves; false once
+    // aborted (a rank that died or left never arrives)
+    bool barrier(const std::function<void()>& fn = nullptr) {
         std::unique_lock<std::mutex> lk(mu);
+        if (aborted) return false;
         const int64_t g = generation;
         if (++arrived == size) {
             if (fn) fn();
@@ -34,8 +39,9 @@ struct HostTransport::Shared {
             generation++;
             cv.notify_all();
         } else {
-            cv.wait(lk, [&] { return generation != g; });
+            cv.wait(lk, [&] { return generation != g || aborted; });
         }
+        return generation != g;
     }
 };
 
@@ -58,11 +64,17 @@ int HostTransport::AllGather(const std::vector<int64_t>& mine, std::vector<int64
         std::lock_guard<std::mutex> lk(s_->mu);
         s_->gather_in[rank_] = &mine;
     }
-    s_->barrier();  // every rank's input is published
+    if (!s_->barrier()) return NFK_ERR_STATE;  // every rank's input is published
     all.clear();
     for (int r = 0; r < s_->size; r++) all.insert(all.end(), s_->gather_in[r]->begin(), s_->gather_in[r]->end());
-    s_->barrier();  // every rank has read (the inputs may go)
+    if (!s_->barrier()) return NFK_ERR_STATE;  // every rank has read (the inputs may go)
     return NFK_OK;
+}
+
+void HostTransport::Abort() {
+    std::lock_guard<std::mutex> lk(s_->mu);
+    s_->aborted = true;
+    s_->cv.notify_all();
 }
 
 int HostTransport::AllToAllV(const uint64_t* send, const std::vector<size_t>& scount, uint64_t* recv,
@@ -72,7 +84,7 @@ int HostTransport::AllToAllV(const uint64_t* send, const std::vector<size_t>& sc
         s_->send[rank_] = send;
         s_->scount[rank_] = &scount;
     }
-    s_->barrier();
+    if (!s_->barrier()) return NFK_ERR_STATE;
     // pull my part of every source's buffer: source r packs its rows in destination order
     int rc = NFK_OK;
     size_t at = 0;
@@ -87,7 +99,7 @@ int HostTransport::AllToAllV(const uint64_t* send, const std::vector<size_t>& sc
         if (rcount[r]) mem_.copy(recv + at, s_->send[r] + off, rcount[r] * 8);
         at += rcount[r];
     }
-    s_->barrier();
+    if (!s_->barrier()) return NFK_ERR_STATE;
     return rc;
 }
 
@@ -102,7 +114,16 @@ SceneShard::SceneShard(void* world, ShardTransport* t, std::function<int(int)> o
 }
 
 SceneShard::~SceneShard() {
-    if (pending_.valid()) (void)pending_.get();  // (a gather still in flight: the peers need this rank in it)
+    // A gather still in flight: the peers need this rank in it, so it is waited for — but not
+    // forever.  After an error of this shard, or when it has not finished within
+    // NFGPU_SHARD_TEARDOWN_S seconds (default 30: a peer that died never arrives), the transport
+    // is aborted so that the collective returns and teardown completes.
+    if (pending_.valid()) {
+        const char* e = getenv("NFGPU_SHARD_TEARDOWN_S");
+        const double secs = failed_ ? 0.0 : (e ? atof(e) : 30.0);
+        if (pending_.wait_for(std::chrono::duration<double>(secs)) != std::future_status::ready) t_->Abort();
+        (void)pending_.get();
+    }
     if (sbuf_) mem_.release(sbuf_);
     if (rbuf_) mem_.release(rbuf_);
 }
@@ -167,10 +188,15 @@ int SceneShard::BeginFrame(std::vector<Ticket>* sent, std::vector<Ticket>* recei
     if (received) received->clear();
     if (!pending_.valid()) return NFK_OK;  // no gather since the last one: nothing to move
     const int r = pending_.get();
-    if (r) return r;
+    if (r) {
+        failed_ = true;
+        return r;
+    }
     std::vector<int64_t> plan;
     plan.swap(pending_plan_);
-    return Rows(plan, sent, received);
+    const int rr = Rows(plan, sent, received);
+    if (rr) failed_ = true;
+    return rr;
 }
 
 int SceneShard::Migrate(std::vector<Ticket>* sent, std::vector<Ticket>* received) {
@@ -181,8 +207,12 @@ int SceneShard::Migrate(std::vector<Ticket>* sent, std::vector<Ticket>* received
     std::vector<int64_t> plan;
     transport_calls++;
     r = t_->AllGather(TakeTickets(), plan);
-    if (r) return r;
+    if (r) {
+        failed_ = true;
+        return r;
+    }
     r = Rows(plan, sent, received);
+    if (r) failed_ = true;
     if (sent) sent->insert(sent->begin(), s0.begin(), s0.end());
     if (received) received->insert(received->begin(), r0.begin(), r0.end());
     return r;

@@ -60,6 +60,14 @@ RcclTransport::RcclTransport(const std::vector<uint8_t>& unique_id, int rank, in
     meta_stream_ = ms;
 }
 
+void RcclTransport::Abort() {
+    // (a collective blocked on a peer that never arrives returns; the communicators are gone)
+    if (meta_comm_) (void)ncclCommAbort((ncclComm_t)meta_comm_);
+    if (comm_) (void)ncclCommAbort((ncclComm_t)comm_);
+    meta_comm_ = nullptr;
+    comm_ = nullptr;
+}
+
 RcclTransport::~RcclTransport() {
     if (buf_) (void)hipFree(buf_);
     if (meta_comm_) (void)ncclCommDestroy((ncclComm_t)meta_comm_);

@@ -9,7 +9,9 @@
 // property writes GroupID = 0, SceneID, X, Y, Z, GroupID (KM:930-942).
 //
 // usage: shard_protocol [host|device]   (exit 0 = every check passed)
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -208,6 +210,24 @@ int main(int argc, char** argv) {
     CHECK(rc3[0] != NFK_OK && rc3[1] != NFK_OK, "a failed export: statuses %d %d", rc3[0], rc3[1]);
     nfk_destroy(w3[0]);
     nfk_destroy(w3[1]);
+
+    // ---- teardown while a peer never arrives: rank 1 never joins rank 0's ticket gather; the
+    // shard's destructor waits NFGPU_SHARD_TEARDOWN_S, then aborts the transport and returns ----
+    {
+        setenv("NFGPU_SHARD_TEARDOWN_S", "0.5", 1);
+        void* w4 = make_world(0);
+        auto shared4 = HostTransport::MakeShared(2);
+        const auto t0 = std::chrono::steady_clock::now();
+        {
+            HostTransport t(shared4, 0, mem);
+            SceneShard sh(w4, &t, [](int scene) { return scene == 1 ? 0 : 1; }, P_SCENE, P_GROUP, P_X, P_Y, P_Z, mem);
+            sh.QueueSwitch(7, 0, 0, 0, 2, 3, 0.f, 0.f, 0.f);
+            CHECK(sh.EndFrame() == NFK_OK, "EndFrame");
+        }  // (~SceneShard: the gather is still waiting for rank 1)
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        CHECK(s < 10.0, "teardown with an absent peer took %.1f s", s);
+        nfk_destroy(w4);
+    }
     if (!g_fail) printf("shard_protocol %s: ok\n", device ? "device" : "host");
     return g_fail;
 }
