@@ -66,6 +66,7 @@ constexpr unsigned kAblWaves6 = 16, kAblWaves8 = 32;  // k_tick register budgets
 constexpr unsigned kAblWaves5 = 8192;                  // (6 is the default)
 constexpr unsigned kAblNoRun = 512, kAblNoLoads = 1024, kAblNoEmit = 2048;  // timing only (k_tick)
 constexpr unsigned kAblNoWriteBack = 1u << 18, kAblNoSchedStore = 1u << 19;  // timing only (k_tick)
+constexpr unsigned kAblNoFiStore = 128, kAblNoEvStore = 256;  // timing only (k_tick): no fired-list / event-array stores
 constexpr unsigned kAblGroupColumns = 1u << 20, kAblSigGroups = 1u << 21;  // column layouts (outputs exact)
 constexpr unsigned kAblNoPad = 1u << 22;  // columns / schedule kinds at power-of-two strides (outputs exact)
 constexpr unsigned kAblFanWin16 = 1u << 24, kAblFanWin32 = 1u << 25;  // k_tick fan-out LDS window up to 16 / 32 recipients (outputs exact)
@@ -74,6 +75,7 @@ constexpr unsigned kAblTinyTcap = 1u << 27;  // test hook: k_tick's fan-out boun
 constexpr unsigned kAblForceMsgCap = 1u << 29;  // test hook: the frame's ranks also raise kErrMsgCap
 // four u32 at a dword-aligned address (gfx950 global memory allows it; one 16-byte store)
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 // Pad between consecutive property columns and schedule-kind arrays (bytes): with cap a power of
 // two, unpadded columns sit exactly 2^k bytes apart and one entity's values of every column fall
 // on the same HBM channel.
@@ -429,6 +431,15 @@ __device__ __forceinline__ void st_nt(T* p, T x) {
         __builtin_memcpy(&v, &x, 4);
         __builtin_nontemporal_store(v, (uint32_t*)p);
     }
+}
+// a vector of u32 (u32x2_a4 / u32x4_a4: dword-aligned) at a 32-bit byte offset from a wave-uniform base
+template <bool NT, typename V>
+__device__ __forceinline__ void st_vec(void* base, uint32_t byte_off, V x) {
+    V* p = (V*)((char*)base + byte_off);
+    if constexpr (NT)
+        __builtin_nontemporal_store(x, p);
+    else
+        *p = x;
 }
 template <bool NT, typename T>
 __device__ __forceinline__ void st_off_nt(T* base, uint32_t i, T x) {

@@ -142,25 +142,56 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
     return before + inc - v;
 }
 
+// Element i (stride str elements) of a wave-uniform array.  A policy with kOff32 (its world's arrays
+// are all under 4 GiB from their bases: nfgpu_jit.hpp) addresses it as the scalar base plus a 32-bit
+// byte offset, so a column access is one saddr load on an offset shared by every column of the same
+// stride, with no 64-bit address arithmetic or 64-bit address registers per lane.
+// (The base goes through readfirstlane, which the compiler cannot see through: otherwise it
+// re-associates base_k = s_hot + k * stride with the lane offset into one 64-bit lane address per
+// kind.  Every base here is wave-uniform, so the first lane's is the base.)
+template <class S, typename T>
+__device__ __forceinline__ T* elem(T* base, uint32_t i, uint32_t str = 1) {
+    if constexpr (S::kOff32) {
+        const uint64_t p = (uint64_t)base;
+        const uint64_t b = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)p) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p >> 32)) << 32);
+        typedef __attribute__((address_space(1))) char GChar;  // (global: the saddr forms)
+        return (T*)((GChar*)b + i * (uint32_t)(sizeof(T) * str));
+    } else
+        return base + (size_t)i * str;
+}
+
 // The schema k_tick runs: the heartbeat kinds, the programs' working set (U slots) and its event
 // order and fan-out classes.  DynSchema reads it at run time (Dev, kernel-argument scalars, and
 // Tables through the constant address space); a generated policy (nfgpu_host.hip, jit_source)
 // has the same members as constants and the programs as straight-line code on the registers.
 struct DynSchema {
     static constexpr bool kStatic = false;
+    static constexpr bool kOff32 = false;  // 64-bit element addresses (any world size)
     static constexpr uint32_t kSpecMask = 0;  // operands loaded before the fire test (none)
     // non-temporal hints (kNt* bits): none in the library's instantiations
     static constexpr uint32_t kNt = 0;
     // k_tick may rank a small world's tiles itself (Dev::lb_rank); a policy for a world of more than
     // kLbMaxTiles tiles compiles that code out (kLb = false) and the frame ranks by k_scan_tiles
     static constexpr bool kLb = true;
+    // a persistent k_tick (each workgroup runs several tiles; 1: the next one's schedule records
+    // loaded while the current one runs, 2: no prefetch): only a generated policy (nfgpu_jit.hpp)
+    static constexpr int kPf = 0;
     static constexpr int kNK = NFK_MAX_KINDS;  // (an upper bound only)
     __device__ static int n_kind(const Dev& d) { return d.n_kind; }
     __device__ static int n_w(const Dev& d) { return d.n_w; }
     __device__ static uint32_t u_lower(const Dev& d, int j) { return d.u_lower[j]; }
     __device__ static int u_pid(const Dev& d, int j) { return d.u_pid[j]; }
     __device__ static int u_order(const Dev& d, int i) { return d.u_order[i]; }
-    __device__ static uint32_t cmask(const Dev& d, int c) { return d.u_cmask[c]; }
+    __device__ static uint32_t u_str(const Dev& d, int j) { return (uint32_t)d.u_str[j]; }
+    // the event masks of the entity's class (Dev::u_cmask): a select over kernel-argument scalars,
+    // no indexed copy and no barrier
+    __device__ static uint32_t class_mask(const Dev& d, unsigned cls) {
+        uint32_t cm = 0;
+#pragma unroll
+        for (int i = 0; i < NFK_MAX_CLASSES; i++) cm = cls == (unsigned)i ? d.u_cmask[i] : cm;
+        return cm;
+    }
     // the U slots the fired kinds read or write
     __device__ static uint32_t need(const Dev& d, uint32_t fired) {
         uint32_t need = 0;
@@ -189,6 +220,31 @@ constexpr int kWavesU8 = 8, kWavesU12 = 7;
 constexpr int kWavesJit = 5;  // the hipRTC specialisation (nfgpu_jit.hpp; profiles/r11j_jit_waves_ab.txt)
 constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: at most 4 GiB reserved
 
+// A slot's schedule records of the first chunk of kinds, its descriptor and remove-list flag: what
+// sched_chunk loads itself, or what a persistent k_tick (S::kPf) loaded for its next tile while it
+// ran the current one (sched_load).
+struct SchedPre {
+    SchedHot h[kKindChunk];
+    uint64_t desc;
+    uint8_t ef;
+};
+template <class S>
+__device__ __forceinline__ void sched_load(const Dev& d, int e, int k0, SchedHot (&h)[kKindChunk]) {
+    // kinds past n_kind re-read the chunk's first record (a cache hit); a static schema loads
+    // exactly its kinds
+    const int nk = S::n_kind(d) - k0;
+#pragma unroll
+    for (int j = 0; j < kKindChunk; j++)
+        if (!S::kStatic || j < nk)
+            h[j] = ld_nt<(S::kNt & kNtSchedLoad) != 0>(elem<S>(d.s_hot + (size_t)(k0 + (j < nk ? j : 0)) * d.s_kstr, (uint32_t)e));
+}
+template <class S>
+__device__ __forceinline__ void sched_prefetch(const Dev& d, int e, SchedPre& p) {
+    sched_load<S>(d, e, 0, p.h);
+    p.desc = ld_nt<(S::kNt & kNtSchedLoad) != 0>(elem<S>(d.fan_desc, (uint32_t)e));
+    p.ef = *elem<S>(d.e_flags, (uint32_t)e);  // (always allocated)
+}
+
 // NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
 // order).  The hot records of a chunk of kinds are loaded together (independent 16 B loads).
 // Rescheduled / removed records are stored back.  Every load is issued without a branch and before
@@ -196,22 +252,27 @@ constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: 
 // first use after the record stores would make the wave wait for the stores too (the vector
 // memory counter retires in order), i.e. one round trip per kind or per store batch.
 // kStore = false: the fire test only (k_chain re-runs it before k_tick; nothing is stored).
+// pre: the first chunk's records, descriptor and flag, already loaded (a persistent k_tick's prefetch)
 template <class S, bool kFirst, bool kStore = true>
 __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigned& bytes, uint64_t& desc,
                                             bool& dead, bool& taken, uint32_t& fired, int32_t* s_rem,
-                                            bool oob) {
+                                            bool oob, const SchedPre* pre = nullptr) {
     SchedHot h[kKindChunk];
-    // kinds past n_kind re-read the chunk's first record (a cache hit); a static schema loads
-    // exactly its kinds
-    const SchedHot* base = d.s_hot + (size_t)k0 * d.s_kstr + e;
-    const int nk = S::n_kind(d) - k0;
+    uint8_t ef = 0;
+    if (kFirst && pre) {
 #pragma unroll
-    for (int j = 0; j < kKindChunk; j++)
-        if (!S::kStatic || j < nk) h[j] = ld_nt<(S::kNt & kNtSchedLoad) != 0>(base + (size_t)(j < nk ? j : 0) * d.s_kstr);
+        for (int j = 0; j < kKindChunk; j++) h[j] = pre->h[j];
+        desc = pre->desc;
+        ef = pre->ef;
+    } else {
+        sched_load<S>(d, e, k0, h);
+        if constexpr (kFirst) {
+            desc = ld_nt<(S::kNt & kNtSchedLoad) != 0>(elem<S>(d.fan_desc, (uint32_t)e));
+            ef = *elem<S>(d.e_flags, (uint32_t)e);  // (always allocated)
+            __builtin_amdgcn_sched_barrier(0);  // the scheduler would hoist the first use and its wait
+        }
+    }
     if constexpr (kFirst) {
-        desc = ld_nt<(S::kNt & kNtSchedLoad) != 0>(d.fan_desc + e);
-        const uint8_t ef = d.e_flags[e];  // (always allocated)
-        __builtin_amdgcn_sched_barrier(0);  // the scheduler would hoist the first use and its wait
         dead = oob || desc_dead(desc);  // a slack slot has no schedules; dead slots store nothing
         taken = d.has_pre && (ef & 1);  // std::map remove-list key already owned (SM:68)
         bytes += d.has_pre ? 1 : 0;
@@ -221,45 +282,50 @@ __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigne
         const int k = k0 + j;
         if (k >= S::n_kind(d)) break;
         bytes += 16;
-        if (dead || !(h[j].state & kStPresent) || !(d.now > h[j].next)) continue;
-        const bool forever = h[j].state & kStForever;
-        if (!(h[j].remain > 0 || forever)) continue;
-        h[j].remain -= 1;
-        fired |= 1u << k;
-        const uint32_t st = h[j].state;
-        if (h[j].remain <= 0 && !forever) {
-            if (!taken) {  // insert into the remove list succeeds for the first one only
-                h[j].state = 0;
-                taken = true;
-            }
-        } else {
-            const bool first = !(st & kStFired);
-            if ((st & kStStep) && (first || !forever || h[j].remain < 0)) {
-                // next = start + step * (all - remain) without the cold record (see kSt*)
-                if (!first) h[j].next += st_step(st);
-            } else {
-                const SchedCold c = d.s_cold[(size_t)k * d.s_kstr + e];
+        bool fire = false;
+        if (!dead && (h[j].state & kStPresent) && d.now > h[j].next) {
+            const bool forever = h[j].state & kStForever;
+            if (h[j].remain > 0 || forever) {
+                fire = true;
+                h[j].remain -= 1;
+                fired |= 1u << k;
+                const uint32_t st = h[j].state;
+                if (h[j].remain <= 0 && !forever) {
+                    if (!taken) {  // insert into the remove list succeeds for the first one only
+                        h[j].state = 0;
+                        taken = true;
+                    }
+                } else {
+                    const bool first = !(st & kStFired);
+                    if ((st & kStStep) && (first || !forever || h[j].remain < 0)) {
+                        // next = start + step * (all - remain) without the cold record (see kSt*)
+                        if (!first) h[j].next += st_step(st);
+                    } else {
+                        const SchedCold c = *elem<S>(d.s_cold + (size_t)k * d.s_kstr, (uint32_t)e);
+                        bytes += 16;
+                        const int64_t step = (int64_t)(c.interval * 1000.0f);
+                        const int32_t done = (int32_t)((uint32_t)c.all - (uint32_t)h[j].remain);
+                        h[j].next = c.start + step * (int64_t)done;
+                    }
+                    h[j].state = st | kStFired;
+                }
+                if (s_rem) s_rem[k * kTPB + threadIdx.x] = h[j].remain;  // for the fired list
                 bytes += 16;
-                const int64_t step = (int64_t)(c.interval * 1000.0f);
-                const int32_t done = (int32_t)((uint32_t)c.all - (uint32_t)h[j].remain);
-                h[j].next = c.start + step * (int64_t)done;
             }
-            h[j].state = st | kStFired;
         }
-        if (kStore && !(d.ablate & kAblNoSchedStore))
-            st_nt<(S::kNt & kNtStateStore) != 0>(d.s_hot + (size_t)k * d.s_kstr + e, h[j]);
-        if (s_rem) s_rem[k * kTPB + threadIdx.x] = h[j].remain;  // for the fired list
-        bytes += 16;
+        if (kStore && fire && !(d.ablate & kAblNoSchedStore))
+            st_nt<(S::kNt & kNtStateStore) != 0>(elem<S>(d.s_hot + (size_t)k * d.s_kstr, (uint32_t)e), h[j]);
     }
 }
 // Loads desc = fan_desc[e] with the first chunk; returns the fired-kind mask.  oob: a slot past N
 // (e is then a valid slot re-read, treated as dead).
 template <class S = DynSchema, bool kStore = true>
 __device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& bytes, uint64_t& desc,
-                                               int32_t* s_rem = nullptr, bool oob = false) {
+                                               int32_t* s_rem = nullptr, bool oob = false,
+                                               const SchedPre* pre = nullptr) {
     uint32_t fired = 0;
     bool dead = true, taken = false;
-    sched_chunk<S, true, kStore>(d, e, 0, bytes, desc, dead, taken, fired, s_rem, oob);
+    sched_chunk<S, true, kStore>(d, e, 0, bytes, desc, dead, taken, fired, s_rem, oob, pre);
     for (int k0 = kKindChunk; k0 < S::n_kind(d); k0 += kKindChunk)
         sched_chunk<S, false, kStore>(d, e, k0, bytes, desc, dead, taken, fired, s_rem, oob);
     return fired;
@@ -342,15 +408,15 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
     return x * q + min(x, r) + i;
 }
 
-template <int kWPE, int kU, class S = DynSchema>
-__global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8))) void k_tick(Dev d) {
+// One tile of k_tick.  pre: the tile's first schedule chunk, descriptors and flags already loaded
+// (a persistent k_tick, S::kPf), else null; pf(): issues the loads of the workgroup's next tile
+// (every thread calls it once, after this tile's operand loads, so waiting for those does not wait
+// for the prefetch: the vector memory counter retires in order).
+template <int kU, class S, class Pf>
+__device__ __forceinline__ void tick_tile(const Dev& d, const int tile, const SchedPre* pre, Pf&& pf,
+                                          unsigned long long* s_w, unsigned& s_bytes, uint32_t& s_lb_last,
+                                          uint32_t* s_pb, uint64_t* s_o) {
     constexpr int kW = kU < kMaxW ? kU : kMaxW;  // writable register slots
-    __shared__ unsigned long long s_w[kTPB / 64];
-    __shared__ unsigned s_bytes;
-    __shared__ uint32_t s_lb_last;  // this tile ranks the frame's tiles (Dev::lb_rank)
-    __shared__ uint32_t s_pb[3];   // pl_slot run of the groups with dirty events [lo, hi), most recipients
-    extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
-    const int tile = d.xcd_map ? xcd_tile((int)blockIdx.x, d.n_tiles) : (int)blockIdx.x;
     const int e = tile * kTile + (int)threadIdx.x;
     if (d.tile_work && !d.tile_work[tile]) {  // (block-uniform) a calls-only pass, no Set group here:
         if (d.has_recops && e < d.N) d.fired_mask[e] = 0;  // nothing fires, nothing is dirty
@@ -365,6 +431,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             __syncthreads();
             if (s_lb_last) lb_scan_all(d, s_w);
         }
+        pf();
         return;
     }
     const bool fuse = d.msg_tcap != 0;  // this tile's fan-out is written here, at tile * msg_tcap
@@ -394,9 +461,9 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             if (!(d.ablate & kAblNoLoads))
 #pragma unroll
                 for (int j = 0; j < kU; j++)
-                    if ((S::kSpecMask >> j) & 1) v[j] = d.u_col[j][(size_t)ec * d.u_str[j]];
+                    if ((S::kSpecMask >> j) & 1) v[j] = *elem<S>(d.u_col[j], (uint32_t)ec, S::u_str(d, j));
         }
-        fired = sched_scan<S>(d, ec, bytes, desc, s_rem, e >= d.N);  // NFCScheduleModule::Execute (SM:51-81)
+        fired = sched_scan<S>(d, ec, bytes, desc, s_rem, e >= d.N, pre);  // NFCScheduleModule::Execute (SM:51-81)
         desc = e < d.N ? desc : kDeadDesc;
         bytes = e < d.N ? bytes + 8 + 8u * (uint32_t)__builtin_popcount(S::kSpecMask) : 0u;
     }
@@ -404,7 +471,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     // queued Set groups of this slot (k_sets ran them): program destinations among them
     uint32_t xset = 0;
     if (live && d.n_x) {
-        xh = d.ext_head[e];
+        xh = *elem<S>(d.ext_head, (uint32_t)e);
         bytes += 4;
         if (xh)
             for (int g = (int)xh - 1; g < d.n_x && d.x_slot[g] == (uint32_t)e; g++) {
@@ -413,16 +480,20 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
                 bytes += 8;
             }
     }
+    uint32_t need = 0;
     if (live) {
-        uint32_t need = xset;
+        need = xset;
         if (!(d.ablate & kAblPrograms)) need |= S::need(d, fired);
         // one batch of independent loads: every value this entity's frame reads or writes
 #pragma unroll
         for (int j = 0; j < kU; j++)
             if (((need >> j) & 1) && !((S::kSpecMask >> j) & 1) && !(d.ablate & kAblNoLoads)) {
-                v[j] = ld_nt<(S::kNt & kNtColLoad) != 0>(d.u_col[j] + (size_t)e * d.u_str[j]);
+                v[j] = ld_nt<(S::kNt & kNtColLoad) != 0>(elem<S>(d.u_col[j], (uint32_t)e, S::u_str(d, j)));
                 bytes += 8;
             }
+    }
+    pf();  // the next tile's schedule records, in flight while this one runs
+    if (live) {
 #pragma unroll
         for (int j = 0; j < kW; j++)
             if (j < S::n_w(d) && ((need >> j) & 1)) s_o[j * kTPB + threadIdx.x] = v[j];
@@ -450,7 +521,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
 #pragma unroll
         for (int j = 0; j < kW; j++)
             if (j < S::n_w(d) && ((xset & ~dm) >> j) & 1) {
-                d.u_col[j][(size_t)e * d.u_str[j]] = v[j];
+                *elem<S>(d.u_col[j], (uint32_t)e, S::u_str(d, j)) = v[j];
                 bytes += 8;
             }
     // fan-out message counts (event_msgs): a public property's event goes to every player of the
@@ -458,12 +529,7 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     // of a slot's event = the counts of the dirty slots with lower property ids (Dev::u_lower).
     // the entity's class's event masks (Dev::u_cmask; class 15, a free slot: no slots): a select
     // over kernel-argument scalars, no indexed copy and no barrier
-    uint32_t cm = 0;
-    {
-        const unsigned cls = (unsigned)(desc >> 60);
-#pragma unroll
-        for (int i = 0; i < NFK_MAX_CLASSES; i++) cm = cls == (unsigned)i ? S::cmask(d, i) : cm;
-    }
+    const uint32_t cm = S::class_mask(d, (unsigned)(desc >> 60));
     const uint32_t pubm = cm & 0xFFFFu, privm = cm >> 16;
     const uint32_t r1 = (uint32_t)((desc >> 46) & 0x3FFF);
     const uint32_t npub = (uint32_t)((desc >> 32) & 0x3FFF) - (r1 ? 1u : 0u);
@@ -549,22 +615,53 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             uint64_t* const t_evo = d.ev_old + ev0;
             uint64_t* const t_evn = d.ev_new + ev0;
             if (!nsd) {
+                // A thread's events sit at consecutive ranks, so two consecutive ones are stored
+                // together (8-byte stores of the slot and pid words, 16-byte stores of the old and
+                // new values, at any dword): one store per array covers most of a wave's run instead
+                // of one per event slot with the lanes ~2.4 events apart
+                // (tools/event_store_probe.hip: 22.4 -> 18.8 us for config[1]'s 2.5M events)
+                constexpr bool kNE = (S::kNt & kNtEventStore) != 0;
+                bool pend = false;  // an event held back to be stored with the next one
+                uint32_t pa = 0, pp = 0;
+                uint64_t po = 0, pn = 0;
 #pragma unroll
                 for (int j = 0; j < kW; j++) {
                     if (j >= S::n_w(d) || !((dm >> j) & 1)) continue;
                     const uint32_t below = dm & S::u_lower(d, j);
                     const uint32_t at = pev0 + __builtin_popcount(below);
-                    const uint64_t nv = v[j];
-                    constexpr bool kNE = (S::kNt & kNtEventStore) != 0;
-                    if (!(d.ablate & kAblNoWriteBack)) st_nt<(S::kNt & kNtStateStore) != 0>(d.u_col[j] + (size_t)e * d.u_str[j], nv);
-                    st_off_nt<kNE>(t_evs, at, (uint32_t)e);
-                    st_off_nt<kNE>(t_evp, at, (uint32_t)S::u_pid(d, j));
-                    st_off_nt<kNE>(t_evo, at, s_o[j * kTPB + threadIdx.x]);
-                    st_off_nt<kNE>(t_evn, at, nv);
+                    const uint64_t nv = v[j], ov = s_o[j * kTPB + threadIdx.x];
+                    const uint32_t pid = (uint32_t)S::u_pid(d, j);
+                    if (!(d.ablate & kAblNoWriteBack)) st_nt<(S::kNt & kNtStateStore) != 0>(elem<S>(d.u_col[j], (uint32_t)e, S::u_str(d, j)), nv);
                     if (!fuse)  // tile-local; k_fanout adds the tile's message base
                         st_off(t_evm, at, pmsg0 + npub * __builtin_popcount(below & pubm) +
                                               __builtin_popcount(below & privm));
+                    if (d.ablate & kAblNoEvStore) {
+                    } else if (pend && at == pa + 1) {  // (the writable slots are in property-id order)
+                        st_vec<kNE>(t_evs, 4u * pa, u32x2_a4{(uint32_t)e, (uint32_t)e});
+                        st_vec<kNE>(t_evp, 4u * pa, u32x2_a4{pp, pid});
+                        st_vec<kNE>(t_evo, 8u * pa, u32x4_a4{(uint32_t)po, (uint32_t)(po >> 32), (uint32_t)ov, (uint32_t)(ov >> 32)});
+                        st_vec<kNE>(t_evn, 8u * pa, u32x4_a4{(uint32_t)pn, (uint32_t)(pn >> 32), (uint32_t)nv, (uint32_t)(nv >> 32)});
+                        pend = false;
+                    } else {
+                        if (pend) {
+                            st_off_nt<kNE>(t_evs, pa, (uint32_t)e);
+                            st_off_nt<kNE>(t_evp, pa, pp);
+                            st_off_nt<kNE>(t_evo, pa, po);
+                            st_off_nt<kNE>(t_evn, pa, pn);
+                        }
+                        pend = true;
+                        pa = at;
+                        pp = pid;
+                        po = ov;
+                        pn = nv;
+                    }
                     bytes += 8 + 24;
+                }
+                if (pend && !(d.ablate & kAblNoEvStore)) {
+                    st_off_nt<kNE>(t_evs, pa, (uint32_t)e);
+                    st_off_nt<kNE>(t_evp, pa, pp);
+                    st_off_nt<kNE>(t_evo, pa, po);
+                    st_off_nt<kNE>(t_evn, pa, pn);
                 }
             } else {
                 // (rare: an entity with standalone Set events) write back the slots, then every
@@ -573,14 +670,14 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
 #pragma unroll
                 for (int j = 0; j < kW; j++)
                     if (j < S::n_w(d) && ((dm >> j) & 1)) {
-                        d.u_col[j][(size_t)e * d.u_str[j]] = v[j];
+                        *elem<S>(d.u_col[j], (uint32_t)e, S::u_str(d, j)) = v[j];
                         bytes += 8;
                     }
                 walk([&](unsigned at, unsigned m, uint32_t pid, int j, int g, EvFan) {
                     uint64_t ov, nv;
                     if (j >= 0) {
                         ov = s_o[j * kTPB + threadIdx.x];
-                        nv = __hip_atomic_load(d.u_col[j] + (size_t)e * d.u_str[j], __ATOMIC_RELAXED,
+                        nv = __hip_atomic_load(elem<S>(d.u_col[j], (uint32_t)e, S::u_str(d, j)), __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WAVEFRONT);
                     } else {  // (k_sets wrote the column)
                         ov = d.x_old[g];
@@ -613,18 +710,20 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
             // wrap it through INT32_MIN; a counted one is >= 0 after a fire.  The forever bit is the
             // same before and after the scan, so the record's state is read whatever the L1 holds)
             if ((d.ablate & kAblCheckRem) && rem == kRemUnset &&
-                !(d.s_hot[(size_t)k * d.s_kstr + e].state & kStForever))
+                !(elem<S>(d.s_hot + (size_t)k * d.s_kstr, (uint32_t)e)->state & kStForever))
                 dev_error(d, kErrRemain);
-            st_off_nt<kNE>(t_fis, pfi, (uint32_t)e);
-            st_off_nt<kNE>(t_fik, pfi, (uint32_t)k);
-            st_off_nt<kNE>(t_fir, pfi, rem);
+            if (!(d.ablate & kAblNoFiStore)) {
+                st_off_nt<kNE>(t_fis, pfi, (uint32_t)e);
+                st_off_nt<kNE>(t_fik, pfi, (uint32_t)k);
+                st_off_nt<kNE>(t_fir, pfi, rem);
+            }
             pfi++;
             bytes += 12;
         }
-        if (xh) d.ext_head[e] = 0;
+        if (xh) *elem<S>(d.ext_head, (uint32_t)e) = 0;
     }
     if (d.has_recops && e < d.N) {  // slack slots too: a slot's previous occupant left a mask
-        d.fired_mask[e] = fired;
+        *elem<S>(d.fired_mask, (uint32_t)e) = fired;
         bytes += 4;
     }
     if (!fuse && !(d.ablate & kAblNoEmit)) bytes += 4 * nd;  // ev_moff
@@ -800,6 +899,54 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     }
     if constexpr (S::kLb)
         if (lb_scan) lb_scan_all(d, s_w);
+}
+
+template <int kWPE, int kU, class S = DynSchema>
+__global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8))) void k_tick(Dev d) {
+    __shared__ unsigned long long s_w[kTPB / 64];
+    __shared__ unsigned s_bytes;
+    __shared__ uint32_t s_lb_last;  // this tile ranks the frame's tiles (Dev::lb_rank)
+    __shared__ uint32_t s_pb[3];   // pl_slot run of the groups with dirty events [lo, hi), most recipients
+    extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
+    auto tile_of = [&](int b) { return d.xcd_map ? xcd_tile(b, d.n_tiles) : b; };
+    if constexpr (S::kPf == 0) {
+        tick_tile<kU, S>(d, tile_of((int)blockIdx.x), nullptr, [] {}, s_w, s_bytes, s_lb_last, s_pb, s_o);
+    } else {
+        // persistent: workgroup b runs the tiles of virtual workgroups b, b + G, b + 2G, ... (G a
+        // multiple of 8, so they stay on b's XCD and its range of tiles), each tile's schedule records
+        // loaded while the previous tile runs
+        static_assert(!S::kLb, "a persistent k_tick ranks by k_scan_tiles");
+        typedef const __attribute__((address_space(4))) Dev CDev;
+        // Each tile reads the kernel arguments through a pointer re-defined every iteration, so the
+        // compiler re-loads them per tile instead of keeping ~100 of them in registers across the
+        // loop (SGPR spills).  (The kernel's only argument sits at the start of its kernarg
+        // segment; &d would copy the struct to scratch.)
+        auto args = [] {
+            CDev* p = (CDev*)__builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(p));
+            return (const Dev*)p;
+        };
+        const int G = (int)gridDim.x, n_tiles = d.n_tiles;
+        SchedPre nx;
+        auto load = [&](const Dev& a, int b) {
+            const int t = a.xcd_map ? xcd_tile(b, n_tiles) : b;
+            const int e = t * kTile + (int)threadIdx.x;
+            sched_prefetch<S>(a, e < a.N ? e : a.N - 1, nx);
+        };
+        if (S::kPf == 1 && (int)blockIdx.x < n_tiles) load(*args(), (int)blockIdx.x);
+        for (int b = (int)blockIdx.x; b < n_tiles; b += G) {
+            const Dev& a = *args();
+            const int t = a.xcd_map ? xcd_tile(b, n_tiles) : b;
+            if constexpr (S::kPf == 1) {
+                const SchedPre cur = nx;
+                tick_tile<kU, S>(a, t, &cur, [&] {
+                    if (b + G < n_tiles) load(a, b + G);
+                }, s_w, s_bytes, s_lb_last, s_pb, s_o);
+            } else {
+                tick_tile<kU, S>(a, t, nullptr, [] {}, s_w, s_bytes, s_lb_last, s_pb, s_o);
+            }
+        }
+    }
 }
 
 }  // namespace nfgpu
