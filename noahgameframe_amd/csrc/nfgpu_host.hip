@@ -264,7 +264,6 @@ struct World {
     hipFunction_t jit_fn = nullptr;
     int jit_waves = 0, jit_u = 0;
     bool jit_lb = false;  // the specialisation keeps k_tick's in-kernel ranks (a world of <= kLbMaxTiles tiles)
-    int jit_grid = 0;     // > 0: a persistent specialisation (JitSchema::kPf) launched with this many workgroups
     std::string jit_msg = "not compiled";
 
     int32_t ticks = 0;
@@ -1055,10 +1054,7 @@ void build_jit(World* w) {
     // out of its specialisation (NFGPU_JIT_LB=1 keeps it, for A/B)
     bool lb = ((int64_t)w->d.cap + kTile - 1) / kTile <= kLbMaxTiles;
     if (const char* el = getenv("NFGPU_JIT_LB")) lb = el[0] == '1';
-    // persistent k_tick (NFGPU_JIT_PF=1: the next tile's schedule records prefetched; 2: not)
-    const char* ep = getenv("NFGPU_JIT_PF");
-    const int pf = (ep && !lb && w->d.n_kind <= kKindChunk) ? std::max(0, std::min(2, atoi(ep))) : 0;
-    const std::string src = jit_schema_source(w->tab, w->d, spec, nt, lb, pf);
+    const std::string src = jit_schema_source(w->tab, w->d, spec, nt, lb);
     int dev = 0;
     (void)hipGetDevice(&dev);
     const std::string key = std::to_string(dev) + "|" + std::to_string(waves) + "|" + std::to_string(u) + "|" + src;
@@ -1077,15 +1073,6 @@ void build_jit(World* w) {
     }
     w->jit_fn = it->second;
     w->jit_lb = lb;
-    w->jit_grid = 0;
-    if (pf) {  // every workgroup resident at once: the occupancy of the launch's LDS, on every CU
-        const size_t lds = (size_t)(163840 / waves - 2560) & ~(size_t)1023;
-        int per_cu = 0, cus = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, it->second, kTPB, lds) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            per_cu = cus = 0;
-        w->jit_grid = std::max(8, per_cu * cus / 8 * 8);
-    }
     w->jit_waves = waves;
     w->jit_u = u;
     w->jit_msg = jit_kernel_name(waves, u);
@@ -3746,8 +3733,8 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
         const dim3 g((unsigned)d.n_tiles), b(kTPB);
         if (jit) {
             void* args[] = {&d};
-            const unsigned grid = w->jit_grid > 0 ? (unsigned)std::min(w->jit_grid, d.n_tiles) : (unsigned)d.n_tiles;
-            HIPCHK(hipModuleLaunchKernel(w->jit_fn, grid, 1, 1, kTPB, 1, 1, (unsigned)lds, w->stream, args, nullptr));
+            HIPCHK(hipModuleLaunchKernel(w->jit_fn, (unsigned)d.n_tiles, 1, 1, kTPB, 1, 1, (unsigned)lds, w->stream,
+                                         args, nullptr));
         } else if (use_u && d.n_u <= 8 && !(d.ablate & kAblWaves6))
             hipLaunchKernelGGL((k_tick<kWavesU8, 8>), g, b, lds, w->stream, d);
         else if (use_u && d.n_u <= 12 && !(d.ablate & kAblWaves6))

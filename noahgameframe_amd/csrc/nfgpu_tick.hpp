@@ -174,9 +174,6 @@ struct DynSchema {
     // k_tick may rank a small world's tiles itself (Dev::lb_rank); a policy for a world of more than
     // kLbMaxTiles tiles compiles that code out (kLb = false) and the frame ranks by k_scan_tiles
     static constexpr bool kLb = true;
-    // a persistent k_tick (each workgroup runs several tiles; 1: the next one's schedule records
-    // loaded while the current one runs, 2: no prefetch): only a generated policy (nfgpu_jit.hpp)
-    static constexpr int kPf = 0;
     static constexpr int kNK = NFK_MAX_KINDS;  // (an upper bound only)
     __device__ static int n_kind(const Dev& d) { return d.n_kind; }
     __device__ static int n_w(const Dev& d) { return d.n_w; }
@@ -220,14 +217,6 @@ constexpr int kWavesU8 = 8, kWavesU12 = 7;
 constexpr int kWavesJit = 5;  // the hipRTC specialisation (nfgpu_jit.hpp; profiles/r11j_jit_waves_ab.txt)
 constexpr long long kMsgStrideLimit = 1ll << 30;  // fixed-stride message runs: at most 4 GiB reserved
 
-// A slot's schedule records of the first chunk of kinds, its descriptor and remove-list flag: what
-// sched_chunk loads itself, or what a persistent k_tick (S::kPf) loaded for its next tile while it
-// ran the current one (sched_load).
-struct SchedPre {
-    SchedHot h[kKindChunk];
-    uint64_t desc;
-    uint8_t ef;
-};
 template <class S>
 __device__ __forceinline__ void sched_load(const Dev& d, int e, int k0, SchedHot (&h)[kKindChunk]) {
     // kinds past n_kind re-read the chunk's first record (a cache hit); a static schema loads
@@ -238,13 +227,6 @@ __device__ __forceinline__ void sched_load(const Dev& d, int e, int k0, SchedHot
         if (!S::kStatic || j < nk)
             h[j] = ld_nt<(S::kNt & kNtSchedLoad) != 0>(elem<S>(d.s_hot + (size_t)(k0 + (j < nk ? j : 0)) * d.s_kstr, (uint32_t)e));
 }
-template <class S>
-__device__ __forceinline__ void sched_prefetch(const Dev& d, int e, SchedPre& p) {
-    sched_load<S>(d, e, 0, p.h);
-    p.desc = ld_nt<(S::kNt & kNtSchedLoad) != 0>(elem<S>(d.fan_desc, (uint32_t)e));
-    p.ef = *elem<S>(d.e_flags, (uint32_t)e);  // (always allocated)
-}
-
 // NFCScheduleModule::Execute (SM:51-81) for one object: its schedules in name order (kind id
 // order).  The hot records of a chunk of kinds are loaded together (independent 16 B loads).
 // Rescheduled / removed records are stored back.  Every load is issued without a branch and before
@@ -252,25 +234,17 @@ __device__ __forceinline__ void sched_prefetch(const Dev& d, int e, SchedPre& p)
 // first use after the record stores would make the wave wait for the stores too (the vector
 // memory counter retires in order), i.e. one round trip per kind or per store batch.
 // kStore = false: the fire test only (k_chain re-runs it before k_tick; nothing is stored).
-// pre: the first chunk's records, descriptor and flag, already loaded (a persistent k_tick's prefetch)
 template <class S, bool kFirst, bool kStore = true>
 __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigned& bytes, uint64_t& desc,
                                             bool& dead, bool& taken, uint32_t& fired, int32_t* s_rem,
-                                            bool oob, const SchedPre* pre = nullptr) {
+                                            bool oob) {
     SchedHot h[kKindChunk];
     uint8_t ef = 0;
-    if (kFirst && pre) {
-#pragma unroll
-        for (int j = 0; j < kKindChunk; j++) h[j] = pre->h[j];
-        desc = pre->desc;
-        ef = pre->ef;
-    } else {
-        sched_load<S>(d, e, k0, h);
-        if constexpr (kFirst) {
-            desc = ld_nt<(S::kNt & kNtSchedLoad) != 0>(elem<S>(d.fan_desc, (uint32_t)e));
-            ef = *elem<S>(d.e_flags, (uint32_t)e);  // (always allocated)
-            __builtin_amdgcn_sched_barrier(0);  // the scheduler would hoist the first use and its wait
-        }
+    sched_load<S>(d, e, k0, h);
+    if constexpr (kFirst) {
+        desc = ld_nt<(S::kNt & kNtSchedLoad) != 0>(elem<S>(d.fan_desc, (uint32_t)e));
+        ef = *elem<S>(d.e_flags, (uint32_t)e);  // (always allocated)
+        __builtin_amdgcn_sched_barrier(0);  // the scheduler would hoist the first use and its wait
     }
     if constexpr (kFirst) {
         dead = oob || desc_dead(desc);  // a slack slot has no schedules; dead slots store nothing
@@ -321,11 +295,10 @@ __device__ __forceinline__ void sched_chunk(const Dev& d, int e, int k0, unsigne
 // (e is then a valid slot re-read, treated as dead).
 template <class S = DynSchema, bool kStore = true>
 __device__ __forceinline__ uint32_t sched_scan(const Dev& d, int e, unsigned& bytes, uint64_t& desc,
-                                               int32_t* s_rem = nullptr, bool oob = false,
-                                               const SchedPre* pre = nullptr) {
+                                               int32_t* s_rem = nullptr, bool oob = false) {
     uint32_t fired = 0;
     bool dead = true, taken = false;
-    sched_chunk<S, true, kStore>(d, e, 0, bytes, desc, dead, taken, fired, s_rem, oob, pre);
+    sched_chunk<S, true, kStore>(d, e, 0, bytes, desc, dead, taken, fired, s_rem, oob);
     for (int k0 = kKindChunk; k0 < S::n_kind(d); k0 += kKindChunk)
         sched_chunk<S, false, kStore>(d, e, k0, bytes, desc, dead, taken, fired, s_rem, oob);
     return fired;
@@ -408,14 +381,10 @@ __device__ __forceinline__ int xcd_tile(int b, int n) {
     return x * q + min(x, r) + i;
 }
 
-// One tile of k_tick.  pre: the tile's first schedule chunk, descriptors and flags already loaded
-// (a persistent k_tick, S::kPf), else null; pf(): issues the loads of the workgroup's next tile
-// (every thread calls it once, after this tile's operand loads, so waiting for those does not wait
-// for the prefetch: the vector memory counter retires in order).
-template <int kU, class S, class Pf>
-__device__ __forceinline__ void tick_tile(const Dev& d, const int tile, const SchedPre* pre, Pf&& pf,
-                                          unsigned long long* s_w, unsigned& s_bytes, uint32_t& s_lb_last,
-                                          uint32_t* s_pb, uint64_t* s_o) {
+// One tile of k_tick (the workgroup's; its LDS passed in).
+template <int kU, class S>
+__device__ __forceinline__ void tick_tile(const Dev& d, const int tile, unsigned long long* s_w, unsigned& s_bytes,
+                                          uint32_t& s_lb_last, uint32_t* s_pb, uint64_t* s_o) {
     constexpr int kW = kU < kMaxW ? kU : kMaxW;  // writable register slots
     const int e = tile * kTile + (int)threadIdx.x;
     if (d.tile_work && !d.tile_work[tile]) {  // (block-uniform) a calls-only pass, no Set group here:
@@ -431,7 +400,6 @@ __device__ __forceinline__ void tick_tile(const Dev& d, const int tile, const Sc
             __syncthreads();
             if (s_lb_last) lb_scan_all(d, s_w);
         }
-        pf();
         return;
     }
     const bool fuse = d.msg_tcap != 0;  // this tile's fan-out is written here, at tile * msg_tcap
@@ -463,7 +431,7 @@ __device__ __forceinline__ void tick_tile(const Dev& d, const int tile, const Sc
                 for (int j = 0; j < kU; j++)
                     if ((S::kSpecMask >> j) & 1) v[j] = *elem<S>(d.u_col[j], (uint32_t)ec, S::u_str(d, j));
         }
-        fired = sched_scan<S>(d, ec, bytes, desc, s_rem, e >= d.N, pre);  // NFCScheduleModule::Execute (SM:51-81)
+        fired = sched_scan<S>(d, ec, bytes, desc, s_rem, e >= d.N);  // NFCScheduleModule::Execute (SM:51-81)
         desc = e < d.N ? desc : kDeadDesc;
         bytes = e < d.N ? bytes + 8 + 8u * (uint32_t)__builtin_popcount(S::kSpecMask) : 0u;
     }
@@ -492,7 +460,6 @@ __device__ __forceinline__ void tick_tile(const Dev& d, const int tile, const Sc
                 bytes += 8;
             }
     }
-    pf();  // the next tile's schedule records, in flight while this one runs
     if (live) {
 #pragma unroll
         for (int j = 0; j < kW; j++)
@@ -908,45 +875,8 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     __shared__ uint32_t s_lb_last;  // this tile ranks the frame's tiles (Dev::lb_rank)
     __shared__ uint32_t s_pb[3];   // pl_slot run of the groups with dirty events [lo, hi), most recipients
     extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
-    auto tile_of = [&](int b) { return d.xcd_map ? xcd_tile(b, d.n_tiles) : b; };
-    if constexpr (S::kPf == 0) {
-        tick_tile<kU, S>(d, tile_of((int)blockIdx.x), nullptr, [] {}, s_w, s_bytes, s_lb_last, s_pb, s_o);
-    } else {
-        // persistent: workgroup b runs the tiles of virtual workgroups b, b + G, b + 2G, ... (G a
-        // multiple of 8, so they stay on b's XCD and its range of tiles), each tile's schedule records
-        // loaded while the previous tile runs
-        static_assert(!S::kLb, "a persistent k_tick ranks by k_scan_tiles");
-        typedef const __attribute__((address_space(4))) Dev CDev;
-        // Each tile reads the kernel arguments through a pointer re-defined every iteration, so the
-        // compiler re-loads them per tile instead of keeping ~100 of them in registers across the
-        // loop (SGPR spills).  (The kernel's only argument sits at the start of its kernarg
-        // segment; &d would copy the struct to scratch.)
-        auto args = [] {
-            CDev* p = (CDev*)__builtin_amdgcn_kernarg_segment_ptr();
-            asm volatile("" : "+s"(p));
-            return (const Dev*)p;
-        };
-        const int G = (int)gridDim.x, n_tiles = d.n_tiles;
-        SchedPre nx;
-        auto load = [&](const Dev& a, int b) {
-            const int t = a.xcd_map ? xcd_tile(b, n_tiles) : b;
-            const int e = t * kTile + (int)threadIdx.x;
-            sched_prefetch<S>(a, e < a.N ? e : a.N - 1, nx);
-        };
-        if (S::kPf == 1 && (int)blockIdx.x < n_tiles) load(*args(), (int)blockIdx.x);
-        for (int b = (int)blockIdx.x; b < n_tiles; b += G) {
-            const Dev& a = *args();
-            const int t = a.xcd_map ? xcd_tile(b, n_tiles) : b;
-            if constexpr (S::kPf == 1) {
-                const SchedPre cur = nx;
-                tick_tile<kU, S>(a, t, &cur, [&] {
-                    if (b + G < n_tiles) load(a, b + G);
-                }, s_w, s_bytes, s_lb_last, s_pb, s_o);
-            } else {
-                tick_tile<kU, S>(a, t, nullptr, [] {}, s_w, s_bytes, s_lb_last, s_pb, s_o);
-            }
-        }
-    }
+    const int tile = d.xcd_map ? xcd_tile((int)blockIdx.x, d.n_tiles) : (int)blockIdx.x;
+    tick_tile<kU, S>(d, tile, s_w, s_bytes, s_lb_last, s_pb, s_o);
 }
 
 }  // namespace nfgpu
