@@ -330,7 +330,8 @@ public:
     // the same with operands by NAME, for a module that registers its programs before the schema
     // exists (before AfterInit, e.g. the reference-side adapter, whose schema comes from the class
     // module): a property operand (dst of a property op, a / lo / hi under NFK_A_PROP / NFK_LO_PROP /
-    // NFK_HI_PROP, FLERP's a, the guard's property under NFK_GUARD) is an index into props, a record
+    // NFK_HI_PROP, FLERP's a, the guard's property under NFK_GUARD and, with NFK_GUARD_PROP, the
+    // property it is compared to in guard >> 19) is an index into props, a record
     // op's dst is index << 8 | column with the index into records; resolved at AfterInit
     void AddHeartBeatProgram(const std::string& name, const std::vector<nfk_op>& ops,
                              const std::vector<std::string>& props, const std::vector<std::string>& records = {});

@@ -65,7 +65,9 @@ extern "C" {
  * Record ops: dst = (rec << 8) | col.
  * NFK_GUARD (property ops only): the op runs only when int property (guard & 0xFFFF), as the
  * program has left it so far, compares to 0 as NFK_GUARD_* in (guard >> 16) & 3 says — a functor's
- * `if (GetPropertyInt(self, g) > 0) SetProperty...(...)`. */
+ * `if (GetPropertyInt(self, g) > 0) SetProperty...(...)`.  With NFK_GUARD_PROP in guard it compares
+ * to int property (guard >> 19) instead of 0 (both as the program has left them):
+ * `if (GetPropertyInt(self, g) > GetPropertyInt(self, h)) ...`. */
 enum {
     NFK_OP_NOP = 0,
     NFK_OP_IADD_CLAMP = 1,
@@ -84,12 +86,13 @@ enum {
 #define NFK_GUARD_LE0 1 /* g <= 0 */
 #define NFK_GUARD_NE0 2 /* g != 0 */
 #define NFK_GUARD_EQ0 3 /* g == 0 */
+#define NFK_GUARD_PROP (1u << 18) /* compare g to int property guard >> 19 (< 8192) instead of 0 */
 
 typedef struct nfk_op {
     uint8_t code;
     uint8_t flags;
     uint16_t dst;
-    uint32_t guard; /* with NFK_GUARD: property id | NFK_GUARD_* << 16; else 0 */
+    uint32_t guard; /* with NFK_GUARD: property id | NFK_GUARD_* << 16 [| NFK_GUARD_PROP | h << 19]; else 0 */
     int64_t a, b, c;
 } nfk_op; /* 32 bytes */
 

@@ -137,11 +137,14 @@ struct OpX {
     uint32_t cfd;
     uint32_t slots;
     int64_t a, b, c;
-    uint32_t gd;  // NFK_GUARD: 0x80000000 | NFK_GUARD_* << 8 | the guard's U slot; else 0
+    // NFK_GUARD: 0x80000000 | NFK_GUARD_* << 8 | the guard's U slot, and with NFK_GUARD_PROP
+    // 0x40000000 | the compared property's U slot << 16; else 0
+    uint32_t gd;
 };
-// an NFK_GUARD op's condition on the guard property's current value
-__host__ __device__ __forceinline__ bool guard_ok(uint32_t cmp, int64_t g) {
-    return cmp == NFK_GUARD_GT0 ? g > 0 : cmp == NFK_GUARD_LE0 ? g <= 0 : cmp == NFK_GUARD_NE0 ? g != 0 : g == 0;
+// an NFK_GUARD op's condition on the guard property's current value g and what it is compared to
+// (h: another int property's current value under NFK_GUARD_PROP, else 0)
+__host__ __device__ __forceinline__ bool guard_ok(uint32_t cmp, int64_t g, int64_t h = 0) {
+    return cmp == NFK_GUARD_GT0 ? g > h : cmp == NFK_GUARD_LE0 ? g <= h : cmp == NFK_GUARD_NE0 ? g != h : g == h;
 }
 
 struct Tables {
@@ -155,6 +158,7 @@ struct Tables {
     uint32_t umask[NFK_MAX_KINDS];                 // kind k's U slots: writable bits | read-only indices << 16
     uint8_t opu[NFK_MAX_KINDS][NFK_MAX_OPS][4];    // U slot of dst, a, b, c (0x80 | r: read-only r; kNoU = immediate)
     uint8_t opg[NFK_MAX_KINDS][NFK_MAX_OPS];       // U slot of an NFK_GUARD op's guard property (kNoU: none)
+    uint8_t opg2[NFK_MAX_KINDS][NFK_MAX_OPS];      // U slot of the property it is compared to (NFK_GUARD_PROP; kNoU: 0)
     // property -> writable U slot (a program destination), kNoU otherwise.  A queued Set of a
     // property with a slot joins that slot's diff; any other queued Set is a "standalone" event.
     uint8_t w_slot[kMaxProps];

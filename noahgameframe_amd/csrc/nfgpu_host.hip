@@ -920,6 +920,8 @@ bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>&
                     R.push_back((int)op.a);
                 }
                 if ((op.flags & NFK_GUARD) && !is_w(op.guard & 0xFFFF)) R.push_back((int)(op.guard & 0xFFFF));
+                if ((op.flags & NFK_GUARD) && (op.guard & NFK_GUARD_PROP) && !is_w(op.guard >> 19))
+                    R.push_back((int)(op.guard >> 19));
             }
         std::sort(R.begin(), R.end());
         R.erase(std::unique(R.begin(), R.end()), R.end());
@@ -955,8 +957,9 @@ bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>&
                     if (op.flags & NFK_A_PROP) u[1] = slot(op.a);
                 }
                 tab.opg[k][i] = (op.flags & NFK_GUARD) ? slot(op.guard & 0xFFFF) : kNoU;
-                for (int q = 0; q < 5; q++) {  // writable bits | read-only bits << 16
-                    const uint8_t uq = q < 4 ? u[q] : tab.opg[k][i];
+                tab.opg2[k][i] = ((op.flags & NFK_GUARD) && (op.guard & NFK_GUARD_PROP)) ? slot(op.guard >> 19) : kNoU;
+                for (int q = 0; q < 6; q++) {  // writable bits | read-only bits << 16
+                    const uint8_t uq = q < 4 ? u[q] : q == 4 ? tab.opg[k][i] : tab.opg2[k][i];
                     if (uq != kNoU) tab.umask[k] |= (uq & 0x80) ? 1u << (16 + (uq & 0x7F)) : 1u << uq;
                 }
                 OpX& x = tab.opx[k][i];
@@ -966,6 +969,7 @@ bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>&
                 x.b = op.b;
                 x.c = op.c;
                 x.gd = (op.flags & NFK_GUARD) ? 0x80000000u | (((op.guard >> 16) & 3u) << 8) | tab.opg[k][i] : 0u;
+                if (tab.opg2[k][i] != kNoU) x.gd |= 0x40000000u | ((uint32_t)tab.opg2[k][i] << 16);
             }
         }
     }
@@ -1773,7 +1777,9 @@ int nfk_define_kind(void* world, int32_t kind, const nfk_op* ops, int32_t n_ops)
         auto isflt = [&](int64_t p) { return p >= ni && p < np; };
         if (op.flags & NFK_GUARD) {
             const bool rec = op.code == NFK_OP_RIADD_CLAMP || op.code == NFK_OP_RFAFFINE;
-            if (rec || op.code == NFK_OP_NOP || !isint(op.guard & 0xFFFF) || (op.guard >> 18))
+            // (NFK_GUARD_PROP: compared to the int property guard >> 19; otherwise no bits above 17)
+            const bool vs = (op.guard & NFK_GUARD_PROP) != 0;
+            if (rec || op.code == NFK_OP_NOP || !isint(op.guard & 0xFFFF) || (vs ? !isint(op.guard >> 19) : (op.guard >> 18) != 0))
                 return fail(NFK_ERR_ARG, "NFK_GUARD: a property op guarded by an int property");
         } else if (op.guard) {
             return fail(NFK_ERR_ARG, "nfk_op.guard without NFK_GUARD");
@@ -1941,6 +1947,7 @@ int nfk_commit(void* world) {
                     if (op.flags & NFK_A_PROP) add((int)op.a, 0);
                 }
                 if (op.flags & NFK_GUARD) add((int)(op.guard & 0xFFFF), 0);
+                if ((op.flags & NFK_GUARD) && (op.guard & NFK_GUARD_PROP)) add((int)(op.guard >> 19), 0);
             }
         std::map<std::vector<int>, int> gi;
         for (int p = 0; p < NP; p++) {
@@ -1982,6 +1989,7 @@ int nfk_commit(void* world) {
                     if (op.flags & NFK_A_PROP) ps.push_back((int)op.a);
                 }
                 if (op.flags & NFK_GUARD) ps.push_back((int)(op.guard & 0xFFFF));
+                if ((op.flags & NFK_GUARD) && (op.guard & NFK_GUARD_PROP)) ps.push_back((int)(op.guard >> 19));
             }
             for (size_t i = 1; i < ps.size(); i++) {
                 const int a = find(ps[0]), b = find(ps[i]);

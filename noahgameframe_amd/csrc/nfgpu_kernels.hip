@@ -471,7 +471,7 @@ struct NoChainLog {
 template <class Log = NoChainLog>
 __device__ __forceinline__ void run_program_chunk(Ent& en, const Tables* __restrict__ tab, int k, int i0, int n,
                                                   const Log& log = Log()) {
-    uint64_t pre[4][5];  // dst, a, b, c, guard
+    uint64_t pre[4][6];  // dst, a, b, c, guard, the property the guard compares to (NFK_GUARD_PROP)
 #pragma unroll
     for (int ii = 0; ii < 4; ii++) {
         const int i = i0 + ii;
@@ -488,6 +488,10 @@ __device__ __forceinline__ void run_program_chunk(Ent& en, const Tables* __restr
         if (op.flags & NFK_GUARD) {
             pre[ii][4] = *prop_ptr(*en.dv, op.guard & 0xFFFFu, en.e);
             en.bytes += 8;
+            if (op.guard & NFK_GUARD_PROP) {
+                pre[ii][5] = *prop_ptr(*en.dv, op.guard >> 19, en.e);
+                en.bytes += 8;
+            }
         }
         if (op.code == NFK_OP_FLERP || ((op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) && (op.flags & NFK_A_PROP))) {
             pre[ii][1] = *prop_ptr(*en.dv, (uint32_t)op.a, en.e);
@@ -506,7 +510,8 @@ __device__ __forceinline__ void run_program_chunk(Ent& en, const Tables* __restr
         if (op.flags & NFK_GUARD) {
             uint64_t t;
             const int64_t g = en.tget(op.guard & 0xFFFFu, t) ? (int64_t)t : (int64_t)pre[ii][4];
-            if (!guard_ok((op.guard >> 16) & 3u, g)) continue;
+            const int64_t h = !(op.guard & NFK_GUARD_PROP) ? 0 : en.tget(op.guard >> 19, t) ? (int64_t)t : (int64_t)pre[ii][5];
+            if (!guard_ok((op.guard >> 16) & 3u, g, h)) continue;
         }
         if (op.code == NFK_OP_IADD_CLAMP) {
             uint64_t t;

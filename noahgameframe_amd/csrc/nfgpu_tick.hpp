@@ -79,7 +79,9 @@ __device__ __forceinline__ void run_programs_u(uint64_t (&v)[kU], uint32_t& wm, 
             const uint32_t u0 = uslot(sl & 0xFF, n_w), u1 = uslot((sl >> 8) & 0xFF, n_w);
             const uint32_t u2 = uslot((sl >> 16) & 0xFF, n_w), u3 = uslot(sl >> 24, n_w);
             const uint32_t gd = tab->opx[k][i].gd;
-            if (gd && !guard_ok((gd >> 8) & 3u, (int64_t)uget(v, uslot(gd & 0xFF, n_w)))) continue;  // NFK_GUARD
+            if (gd && !guard_ok((gd >> 8) & 3u, (int64_t)uget(v, uslot(gd & 0xFF, n_w)),
+                                (gd & 0x40000000u) ? (int64_t)uget(v, uslot((gd >> 16) & 0xFF, n_w)) : 0))
+                continue;  // NFK_GUARD
             if (code == NFK_OP_IADD_CLAMP) {
                 const int64_t cur = (int64_t)uget(v, u0);
                 const int64_t a = (flags & NFK_A_PROP) ? (int64_t)uget(v, u1) : tab->opx[k][i].a;

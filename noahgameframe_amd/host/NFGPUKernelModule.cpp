@@ -92,7 +92,11 @@ static void resolve_program(std::vector<nfk_op>& ops, const std::vector<std::str
             if (i < 0 || i >= (int64_t)props.size()) throw std::runtime_error("heartbeat program: property operand out of range");
             return (int64_t)pid(props[(size_t)i]);
         };
-        if (op.flags & NFK_GUARD) op.guard = (op.guard & ~0xFFFFu) | (uint32_t)P(op.guard & 0xFFFF);
+        if (op.flags & NFK_GUARD) {
+            op.guard = (op.guard & ~0xFFFFu) | (uint32_t)P(op.guard & 0xFFFF);
+            if (op.guard & NFK_GUARD_PROP)  // (the compared property, guard >> 19)
+                op.guard = (op.guard & 0x7FFFFu) | ((uint32_t)P(op.guard >> 19) << 19);
+        }
         switch (op.code) {
             case NFK_OP_IADD_CLAMP:
                 op.dst = (uint16_t)P(op.dst);

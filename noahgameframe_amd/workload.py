@@ -41,11 +41,13 @@ KID = {n: i for i, n in enumerate(KINDS)}
 OP_IADD_CLAMP, OP_FLERP, OP_FAFFINE, OP_RIADD_CLAMP, OP_RFAFFINE, OP_ISET, OP_FSET = 1, 2, 3, 4, 5, 6, 7
 A_PROP, LO_PROP, HI_PROP, GUARD = 1, 2, 4, 8
 GUARD_GT0, GUARD_LE0, GUARD_NE0, GUARD_EQ0 = 0, 1, 2, 3
+GUARD_PROP = 1 << 18
 
 
-def guard(pid, cmp):
-    """nfk_op.guard of an NFK_GUARD op: the int property and its comparison with 0"""
-    return pid | (cmp << 16)
+def guard(pid, cmp, vs=None):
+    """nfk_op.guard of an NFK_GUARD op: the int property and its comparison with 0, or with the int
+    property `vs` (NFK_GUARD_PROP: a functor's `if (GetPropertyInt(self, g) > GetPropertyInt(self, h))`)"""
+    return pid | (cmp << 16) | (0 if vs is None else GUARD_PROP | (vs << 19))
 
 
 MAX_OPS = 8  # include/nfgpu.h NFK_MAX_OPS (workload files written before round 4 hold 4 per kind)
@@ -106,8 +108,11 @@ def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False,
         # another property's value): first Sets change the value, repeated ones raise no event; some
         # under a guard on an int property (a functor's `if (GetPropertyInt(self, g) ...)`), one of
         # them on a value the same program wrote just before
+        # (round 5: guards comparing two int properties, NFK_GUARD_PROP, in MPRegen, Patrol and Poison)
         put("MPRegen", [(OP_IADD_CLAMP, A_PROP | HI_PROP, PID["MP"], 0, PID["MPREGEN"], 0, PID["MAXMP"]),
-                        (OP_ISET, A_PROP | GUARD, PID["EXP"], guard(PID["Camp"], GUARD_NE0), PID["Level"], 0, 0)])
+                        (OP_ISET, A_PROP | GUARD, PID["EXP"], guard(PID["Camp"], GUARD_NE0), PID["Level"], 0, 0),
+                        (OP_IADD_CLAMP, HI_PROP | GUARD, PID["MP"], guard(PID["MP"], GUARD_GT0, vs=PID["SP"]), -3, 0,
+                         PID["MAXMP"])])
         put("Move", [(OP_FLERP, 0, PID["X"], 0, PID["TargetX"], f64bits(0.125), 0),
                      (OP_FLERP, 0, PID["Y"], 0, PID["TargetY"], f64bits(0.125), 0),
                      (OP_FSET, A_PROP | GUARD, PID["Z"], guard(PID["Camp"], GUARD_GT0), PID["TargetX"], 0, 0)])
@@ -116,9 +121,12 @@ def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False,
                        (OP_IADD_CLAMP, 0, PID["Camp"], 0, -1, 0, 3),
                        (OP_FSET, GUARD, PID["AtkDis"], guard(PID["Camp"], GUARD_EQ0), f64bits(2.5), 0, 0),
                        (OP_FAFFINE, GUARD, PID["AtkDis"], guard(PID["Camp"], GUARD_GT0), f64bits(1.5), f64bits(0.25), 0),
-                       (OP_IADD_CLAMP, A_PROP, PID["SP"], 0, PID["Level"], 0, 1000)])  # (6 ops: > 4 per program)
+                       (OP_IADD_CLAMP, A_PROP, PID["SP"], 0, PID["Level"], 0, 1000),  # (6 ops: > 4 per program)
+                       (OP_ISET, A_PROP | GUARD, PID["SP"], guard(PID["Level"], GUARD_LE0, vs=PID["Camp"]), PID["Level"], 0, 0)])
         put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 1, PID["MAXHP"]),
-                       (OP_ISET, GUARD, PID["SP"], guard(PID["Camp"], GUARD_LE0), 7, 0, 0)])
+                       (OP_ISET, GUARD, PID["SP"], guard(PID["Camp"], GUARD_LE0), 7, 0, 0),
+                       (OP_ISET, GUARD, PID["EXP"], guard(PID["HP"], GUARD_EQ0, vs=PID["MAXHP"]), 0, 0, 0),
+                       (OP_IADD_CLAMP, GUARD, PID["EXP"], guard(PID["SP"], GUARD_NE0, vs=PID["Level"]), 1, 0, 1 << 40)])
     if lethal_poison:
         # Poison may kill: HP clamps at 0, and the same functor revives a dead object at 3 HP — within
         # one frame HP goes hp -> 0 -> 3, so NFCNPCRefreshModule::OnObjectHPEvent-style per-object

@@ -198,8 +198,9 @@ static int OnHeartBeat(const NFGUID& self, const std::string& name, const float,
         const nfk_op& op = W.ops[kind][i];
         if (op.flags & NFK_GUARD) {
             const int64_t g = GetInt(self, (int)(op.guard & 0xFFFF));
+            const int64_t h = (op.guard & NFK_GUARD_PROP) ? GetInt(self, (int)(op.guard >> 19)) : 0;  // vs a property
             const int c = (op.guard >> 16) & 3;
-            if (!(c == NFK_GUARD_GT0 ? g > 0 : c == NFK_GUARD_LE0 ? g <= 0 : c == NFK_GUARD_NE0 ? g != 0 : g == 0)) continue;
+            if (!(c == NFK_GUARD_GT0 ? g > h : c == NFK_GUARD_LE0 ? g <= h : c == NFK_GUARD_NE0 ? g != h : g == h)) continue;
         }
         switch (op.code) {
         case NFK_OP_IADD_CLAMP: {

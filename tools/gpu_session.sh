@@ -82,6 +82,7 @@ for step in "$@"; do
       run pmc_summary 60 python tools/pmc_summary.py --calib "$OUT/calib_fetch" "$OUT/calib_write" \
         --bench "$OUT/pmc_fetch" "$OUT/pmc_write" --sq "$OUT/pmc_sq" ${ALG:+--alg "$ALG"} \
         --out "$OUT/pmc_traffic.json" ;;
+    abifloor) run abifloor 120 tools/_bin/ref_abi_floor ;;
     *) echo "unknown step $step" ;;
   esac
 done
