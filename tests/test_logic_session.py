@@ -30,11 +30,11 @@ GPU_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "logic_session")
 REF_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "logic_session_ref")
 
 
-def _world(seed, n_obj=1200, n_ticks=12, lethal=False):
+def _world(seed, n_obj=1200, n_ticks=12, lethal=False, set_ops=False):
     w = workload.make_world(n_obj=n_obj, n_scenes=2, groups_per_scene=3, players_per_group=4, n_ticks=n_ticks,
                             tick_ms=1000, seed=seed, ext_frac=0.05, host_ops=True, rmw_frac=0.02, spawn_frac=0.02,
                             destroy_frac=0.02, records=True, rec_rows=16, rec_float_op=False, rec_set_frac=0.03,
-                            rec_set_float=False, rec_row_frac=0.02, lethal_poison=lethal)
+                            rec_set_float=False, rec_row_frac=0.02, lethal_poison=lethal, set_ops=set_ops)
     # an int-only record (the reference's NFCRecord::SetFloat cannot hold an f64 cell, test_oracle.py):
     # the charge column becomes an int column with the same bits; no program touches it
     w["rec_ctype"] = np.zeros_like(w["rec_ctype"])
@@ -125,11 +125,13 @@ def test_logic_session_reference_kills_within_a_frame(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,lethal", [(71, False), (72, False), (73, True)])
-def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, seed, lethal):
+# seed 74: the set_ops programs (assignments, guards against 0 and against another int property)
+@pytest.mark.parametrize("seed,lethal,set_ops", [(71, False, False), (72, False, False), (73, True, False),
+                                                 (74, False, True)])
+def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, seed, lethal, set_ops):
     if not (os.path.exists(GPU_EXE) and os.path.exists(REF_EXE)):
         pytest.skip("logic_session not built (needs /root/reference at build time)")
-    w = _world(seed, lethal=lethal)
+    w = _world(seed, lethal=lethal, set_ops=set_ops)
     got, ref = _run(GPU_EXE, w, tmp_path, "gpu"), _run(REF_EXE, w, tmp_path, "ref")
     nt = int(w["cfg"][7])
     assert bytes(np.asarray(got["t3_setup"], np.uint8)) == bytes(np.asarray(ref["t3_setup"], np.uint8))
