@@ -71,6 +71,7 @@ constexpr unsigned kAblGroupColumns = 1u << 20, kAblSigGroups = 1u << 21;  // co
 constexpr unsigned kAblNoPad = 1u << 22;  // columns / schedule kinds at power-of-two strides (outputs exact)
 constexpr unsigned kAblFanWin16 = 1u << 24, kAblFanWin32 = 1u << 25;  // k_tick fan-out LDS window up to 16 / 32 recipients (outputs exact)
 constexpr unsigned kAblFan1 = 1u << 26;      // k_tick fan-out: one recipient per lane (the round-1 form; outputs exact)
+constexpr unsigned kAblFanNoWin = 1u << 30;  // k_tick fan-out: lane groups for every run length, no LDS window (outputs exact)
 constexpr unsigned kAblTinyTcap = 1u << 27;  // test hook: k_tick's fan-out bound set to 4 messages (kErrFanBound)
 constexpr unsigned kAblForceMsgCap = 1u << 29;  // test hook: the frame's ranks also raise kErrMsgCap
 // four u32 at a dword-aligned address (gfx950 global memory allows it; one 16-byte store)

@@ -720,7 +720,8 @@ __device__ __forceinline__ void tick_tile(const Dev& d, const int tile, unsigned
             const uint32_t nm = s_pb[2];
             const uint32_t L = nm <= 1 ? 1u : nm >= 64 ? 64u : 1u << (32 - __builtin_clz(nm - 1));
             const uint32_t sub = threadIdx.x & (L - 1);
-            const bool win = L < ((d.ablate & kAblFanWin32) ? 64u : (d.ablate & kAblFanWin16) ? 32u : 16u);
+            const bool win = !(d.ablate & kAblFanNoWin) &&
+                             L < ((d.ablate & kAblFanWin32) ? 64u : (d.ablate & kAblFanWin16) ? 32u : 16u);
             const bool staged = npl <= R / 4;
             const unsigned room = R - (staged ? npl : 0u);
             // events per chunk: all of them, or what leaves the window half of the room
