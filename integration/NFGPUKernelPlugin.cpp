@@ -453,7 +453,10 @@ private:
         F cb;
         bool aoi;  // the AOI module's: device events go to NFGPUSceneAOIAdapter instead
     };
-    enum : uint8_t { kStale = 1, kEager = 2 };
+    // kWritten: a host write of one of the object's device properties / records was forwarded since the
+    // last frame (OnFrame marks it stale: a heartbeat program may have put the value back where the
+    // frame started, which raises no event, while the host mirror holds the written value)
+    enum : uint8_t { kStale = 1, kEager = 2, kWritten = 4 };
     // a Set whose per-object callbacks OnFrame fires, keyed (NFGUID of o, kind, op, row)
     struct Fire {
         int32_t o, kind, op, row;
@@ -478,6 +481,7 @@ private:
     int ForwardProperty(const NFGUID& self, const std::string& name, const NFIDataList::TData& v) {
         if (quiet_ || OwnWrite(self, name, -1, -1) || !DevProp(self, name)) return 0;
         const nfgpu::NFGUID g = to_gpu(self);
+        Written(g);
         if (v.GetType() == TDATA_INT) gpu_.SetPropertyInt(g, name, v.GetInt());
         else if (v.GetType() == TDATA_FLOAT) gpu_.SetPropertyFloat(g, name, v.GetFloat());
         else if (v.GetType() == TDATA_OBJECT) gpu_.SetPropertyObject(g, name, to_gpu(v.GetObject()));
@@ -493,6 +497,7 @@ private:
         NF_SHARE_PTR<NFIRecord> r = o ? o->GetRecordManager()->GetElement(ev.strRecordName) : nullptr;
         if (!r) return 0;
         const nfgpu::NFGUID g = to_gpu(self);
+        Written(g);
         switch (ev.nOpType) {
             case RECORD_EVENT_DATA::Update:
                 // (an f64 cell written on the host holds the double in the int64 alternative and
@@ -571,6 +576,15 @@ private:
         if ((size_t)o >= mstate_.size()) mstate_.resize((size_t)gpu_.ObjectCount() + 1024, eager_all_ ? kEager : 0);
         return mstate_[(size_t)o];
     }
+    void Written(const nfgpu::NFGUID& g) {
+        const int o = gpu_.ObjectIndex(g);
+        if (o < 0) return;  // (being created: its creation values are the device's)
+        uint8_t& m = State(o);
+        if (!(m & kWritten)) {
+            m |= kWritten;
+            written_.push_back(o);
+        }
+    }
     void MarkEager(const NFGUID& self) {
         const int o = gpu_.ObjectIndex(to_gpu(self));
         if (o < 0) {
@@ -585,6 +599,12 @@ private:
     // frame's values with their per-object callbacks fired once per accepted Set of the frame's
     // heartbeat programs in the reference's order; every other evented object is marked stale.
     void OnFrame(const nfk_frame_host& f) {
+        // objects the host wrote this window: stale, whatever their events (a program may have put a
+        // written value back where the frame started, with no event).  An eager one's watched
+        // properties are brought up to date below with their callbacks, so its refresh on the next
+        // host access (SyncObject) finds them equal and fires nothing
+        for (int o : written_) State(o) = (uint8_t)((State(o) & ~kWritten) | kStale);
+        written_.clear();
         std::vector<int64_t>& ep = fr_ep_;
         std::vector<int64_t>& er = fr_er_;
         ep.clear();
@@ -892,6 +912,7 @@ private:
     std::set<NFGUID> has_components_;  // objects whose component manager was handed out (Execute walks them)
     // (scratch kept across frames)
     std::vector<int64_t> fr_ep_, fr_er_;
+    std::vector<int> written_;  // objects with kWritten (OnFrame)
     std::vector<Fire> fr_fire_;
     std::vector<NF_SHARE_PTR<NFIProperty>> sy_props_;
     std::vector<int32_t> sy_pid_;
