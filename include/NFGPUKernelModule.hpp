@@ -44,6 +44,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -338,6 +339,10 @@ public:
     int PropertyId(const std::string& name) const;
     // whether a schedule name has a device program (AddHeartBeatProgram, before or after AfterInit)
     bool HasHeartBeat(const std::string& name) const;
+    // whether a heartbeat program writes property pid / record rec's column col (after AfterInit)
+    bool ProgramWrites(int pid) const { return pid >= 0 && (size_t)pid < prog_props_.size() && prog_props_[(size_t)pid]; }
+    bool ProgramWritesRecord(int rec, int col) const { return prog_cells_.count((rec << 8) | col) != 0; }
+    bool ProgramWritesRecord(int rec) const { return prog_recs_.count(rec) != 0; }
     // properties of one type (device ids: int [0, n_int), float [n_int, n_int + n_flt), object after)
     int PropertyCount(TDATA_TYPE type) const;
     int RecordId(const std::string& name) const { return record_id_.at(name); }
@@ -541,6 +546,8 @@ private:
     std::vector<RecordDef> records_;
     std::unordered_map<std::string, int> record_id_;
     std::vector<HeartBeatDef> heartbeats_;
+    std::vector<bool> prog_props_;         // property ids a heartbeat program writes (AfterInit)
+    std::set<int> prog_cells_, prog_recs_;  // record rec << 8 | column, and records, a program writes
     std::unordered_map<std::string, int> hb_id_;
     std::map<int, bool> scenes_;
     // objects

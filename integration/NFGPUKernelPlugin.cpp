@@ -453,9 +453,10 @@ private:
         F cb;
         bool aoi;  // the AOI module's: device events go to NFGPUSceneAOIAdapter instead
     };
-    // kWritten: a host write of one of the object's device properties / records was forwarded since the
-    // last frame (OnFrame marks it stale: a heartbeat program may have put the value back where the
-    // frame started, which raises no event, while the host mirror holds the written value)
+    // kWritten: a host write of one of the object's device properties / record cells that a heartbeat
+    // program also writes was forwarded since the last frame (OnFrame marks it stale: the program may have
+    // put the value back where the frame started, which raises no event, while the host mirror holds the
+    // written value; a property no program writes has its event whenever the write changed it)
     enum : uint8_t { kStale = 1, kEager = 2, kWritten = 4 };
     // a Set whose per-object callbacks OnFrame fires, keyed (NFGUID of o, kind, op, row)
     struct Fire {
@@ -481,7 +482,7 @@ private:
     int ForwardProperty(const NFGUID& self, const std::string& name, const NFIDataList::TData& v) {
         if (quiet_ || OwnWrite(self, name, -1, -1) || !DevProp(self, name)) return 0;
         const nfgpu::NFGUID g = to_gpu(self);
-        Written(g);
+        if (gpu_.ProgramWrites(gpu_.PropertyId(name))) Written(g);  // (only a program can undo it unseen)
         if (v.GetType() == TDATA_INT) gpu_.SetPropertyInt(g, name, v.GetInt());
         else if (v.GetType() == TDATA_FLOAT) gpu_.SetPropertyFloat(g, name, v.GetFloat());
         else if (v.GetType() == TDATA_OBJECT) gpu_.SetPropertyObject(g, name, to_gpu(v.GetObject()));
@@ -497,7 +498,11 @@ private:
         NF_SHARE_PTR<NFIRecord> r = o ? o->GetRecordManager()->GetElement(ev.strRecordName) : nullptr;
         if (!r) return 0;
         const nfgpu::NFGUID g = to_gpu(self);
-        Written(g);
+        {
+            const int rid = gpu_.RecordId(ev.strRecordName);
+            if (ev.nOpType == RECORD_EVENT_DATA::Update ? gpu_.ProgramWritesRecord(rid, ev.nCol) : gpu_.ProgramWritesRecord(rid))
+                Written(g);
+        }
         switch (ev.nOpType) {
             case RECORD_EVENT_DATA::Update:
                 // (an f64 cell written on the host holds the double in the int64 alternative and

@@ -283,6 +283,15 @@ bool NFGPUKernelModule::AfterInit() {
                             [this](const std::string& n) { return record_id_.at(n); });
         check(nfk_define_kind(world_, k, heartbeats_[k].ops.data(), (int)heartbeats_[k].ops.size()),
               "nfk_define_kind");
+        for (const nfk_op& op : heartbeats_[k].ops) {  // (ProgramWrites)
+            if (op.code == NFK_OP_RIADD_CLAMP || op.code == NFK_OP_RFAFFINE) {
+                prog_cells_.insert(op.dst);
+                prog_recs_.insert(op.dst >> 8);
+            } else if (op.code != NFK_OP_NOP) {
+                if (prog_props_.size() <= op.dst) prog_props_.resize((size_t)op.dst + 1, false);
+                prog_props_[op.dst] = true;
+            }
+        }
     }
     const int n = (int)guids_.size();
     std::vector<int64_t> gh(n), gd(n);
