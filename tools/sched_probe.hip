@@ -49,7 +49,15 @@ struct P {
 // kLd: non-temporal schedule loads; kSt: 0 plain record stores, 1 non-temporal, 2 to a second
 // (shadow) copy of the records instead of in place, 3 only the dense kind's (Move) stores, 4 every
 // record of every kind stored (whole lines), fired or not
-template <int kMode, bool kLd = true, int kSt = 0>  // kMode 0 full, 1 nolist, 2 noscan, 3 loads
+// kLay: 0 records in [kind][slot] arrays (k_tick's layout), 1 one [slot][kind] block of every kind
+// (80 B per slot), 2 the dense kind (Move) in its own array and the four sparse kinds in one
+// [slot][4] block (64 B per slot)
+__host__ __device__ __forceinline__ size_t rec_at(int lay, int64_t kstr, int k, uint32_t e) {
+    if (lay == 1) return (size_t)e * kK + k;
+    if (lay == 2) return k == 2 ? (size_t)e : (size_t)kstr + (size_t)e * 4 + (k < 2 ? k : k - 1);
+    return (size_t)k * kstr + e;
+}
+template <int kMode, bool kLd = true, int kSt = 0, int kLay = 0>  // kMode 0 full, 1 nolist, 2 noscan, 3 loads
 __global__ __launch_bounds__(kTPB) void scan(P p) {
     __shared__ int32_t s_rem[kK * kTPB];
     __shared__ uint32_t s_w[4];
@@ -57,7 +65,7 @@ __global__ __launch_bounds__(kTPB) void scan(P p) {
     Rec h[kK];
 #pragma unroll
     for (int k = 0; k < kK; k++) {  // (non-temporal, as k_tick's schedule loads)
-        const u32x4* a = (const u32x4*)(p.hot + k * p.kstr + e);
+        const u32x4* a = (const u32x4*)(p.hot + rec_at(kLay, p.kstr, k, e));
         const u32x4 x = kLd ? __builtin_nontemporal_load(a) : *a;
         __builtin_memcpy(&h[k], &x, 16);
     }
@@ -71,7 +79,7 @@ __global__ __launch_bounds__(kTPB) void scan(P p) {
         h[k].next += (int64_t)((int32_t)h[k].state >> 4);
         if (kMode <= 2 && kSt >= 5) continue;  // (stored below, by lane groups)
         if (kMode <= 2 && kSt != 4 && !(kSt == 3 && k != 2)) {
-            Rec* d = (kSt == 2 ? p.shadow : p.hot) + k * p.kstr + e;
+            Rec* d = (kSt == 2 ? p.shadow : p.hot) + rec_at(kLay, p.kstr, k, e);
             u32x4 x;
             __builtin_memcpy(&x, &h[k], 16);
             if (kSt == 1)
@@ -158,11 +166,15 @@ int main() {
     // Move (kind 2) due every frame; kinds 0, 1, 3, 4 due for ~10 / 5 / 3 / 14 % of the slots
     const int pct[kK] = {10, 5, 100, 3, 14};
     uint32_t seed = 7;
+    std::vector<Rec> hot_lay[3];
+    for (int lay = 0; lay < 3; lay++) hot_lay[lay].assign(hot.size(), Rec{(int64_t)1 << 60, -1, 0u});
     for (int k = 0; k < kK; k++)
         for (int i = 0; i < N; i++) {
             seed = seed * 1664525u + 1013904223u;
             const bool due = (int)((seed >> 8) % 100) < pct[k];
-            hot[(size_t)k * kstr + i] = Rec{due ? 0 : (int64_t)1 << 60, -1, 1u | 2u | (0u << 4)};
+            const Rec r{due ? 0 : (int64_t)1 << 60, -1, 1u | 2u | (0u << 4)};
+            hot[(size_t)k * kstr + i] = r;
+            for (int lay = 0; lay < 3; lay++) hot_lay[lay][rec_at(lay, kstr, k, (uint32_t)i)] = r;
         }
     P p;
     CK(hipMalloc(&p.hot, hot.size() * sizeof(Rec)));
@@ -188,10 +200,13 @@ int main() {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    const char* names[15] = {"full", "nolist", "noscan", "loads", "stream", "nolist_plainld", "nolist_ntst",
+    const char* names[21] = {"full", "nolist", "noscan", "loads", "stream", "nolist_plainld", "nolist_ntst",
                              "nolist_shadow", "nolist_plainld_ntst", "nolist_dense_kind_only", "nolist_all_records",
-                             "nolist_all_records_plainld", "nolist_sector32", "nolist_sector64", "nolist_line128"};
-    for (int m = 0; m < 15; m++) {
+                             "nolist_all_records_plainld", "nolist_sector32", "nolist_sector64", "nolist_line128",
+                             "aos5_nolist", "aos5_loads", "aos5_full", "hyb_nolist", "hyb_loads", "hyb_full"};
+    for (int m = 0; m < 21; m++) {
+        const int lay = m >= 18 ? 2 : m >= 15 ? 1 : 0;  // the records in the case's layout
+        CK(hipMemcpy(p.hot, hot_lay[lay].data(), hot.size() * sizeof(Rec), hipMemcpyHostToDevice));
         std::vector<float> t;
         for (int it = 0; it < 22; it++) {
             CK(hipEventRecord(a));
@@ -210,6 +225,12 @@ int main() {
             if (m == 12) scan<1, true, 5><<<T, kTPB>>>(p);
             if (m == 13) scan<1, true, 6><<<T, kTPB>>>(p);
             if (m == 14) scan<1, true, 7><<<T, kTPB>>>(p);
+            if (m == 15) scan<1, true, 0, 1><<<T, kTPB>>>(p);
+            if (m == 16) scan<3, true, 0, 1><<<T, kTPB>>>(p);
+            if (m == 17) scan<0, true, 0, 1><<<T, kTPB>>>(p);
+            if (m == 18) scan<1, true, 0, 2><<<T, kTPB>>>(p);
+            if (m == 19) scan<3, true, 0, 2><<<T, kTPB>>>(p);
+            if (m == 20) scan<0, true, 0, 2><<<T, kTPB>>>(p);
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             float ms;
