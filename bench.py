@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 METRIC = "entity-ticks/sec (update+dirty-diff+fanout) at 1M entities/GPU, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HBM_CEILING_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "hbm_ceiling.json")
-KNAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles", "membership"]
+KNAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles", "membership", "k_chain"]
 CONFIG_NAMES = {
     0: "BASELINE config[0]: Tutorial3 (HelloWorld3Module.cpp) scaled to 10k NPC objects in scene 1 group 0: "
        "AddSchedule(self, \"OnHeartBeat\", 5.0, 10) per object (the tutorial's functor-only heartbeat: no "
@@ -625,13 +625,15 @@ class AdapterLeg:
         from noahgameframe_amd import nfio, workload
         self.tmp = tempfile.TemporaryDirectory()
         wp = os.path.join(self.tmp.name, "w.nfio")
+        # (twice the frames: the same frames again with NFCNPCRefreshModule's HP callback on every NPC,
+        # NFCNPCRefreshModule.cpp:104 — reported as adapter_frame.config1.npc_hp)
         w = workload.bench_world(n_obj=args.entities, groups=args.groups, players_per_group=args.players_per_group,
-                                 n_ticks=args.warmup + args.steps, tick_ms=args.tick_ms, seed=2031, ext_frac=0.05,
+                                 n_ticks=2 * (args.warmup + args.steps), tick_ms=args.tick_ms, seed=2031, ext_frac=0.05,
                                  host_ops=True)
         nfio.write(wp, w)
         self.t0 = time.perf_counter()
         self.errf = open(os.path.join(self.tmp.name, "err.txt"), "w+")
-        self.proc = subprocess.Popen([ADAPTER_EXE, wp, str(args.warmup), str(args.steps), "0", "0", "1"],
+        self.proc = subprocess.Popen([ADAPTER_EXE, wp, str(args.warmup), str(args.steps), "0", "0", "1", "1"],
                                      stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=self.errf, text=True)
 
     def finish(self, timeout=900):

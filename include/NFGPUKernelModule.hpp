@@ -464,6 +464,18 @@ public:
     };
     void WatchProperty(const std::string& name);  // int / float properties; before or after AfterInit
     const std::vector<ChainEntry>& LastChain() const { return chain_; }
+    // Walk-order reads.  NFCScheduleModule::Execute runs each object's functors in turn (SM:52-80), so a
+    // functor's GetPropertyInt(other, p) sees the Sets of the functors before it in the walk and none
+    // after.  Here the device programs (the functors' Sets) all run before the host functors, so by
+    // default such a read sees every object's programs of the frame.  On: every property
+    // a program writes is logged per Set (nfk_watch_props: k_chain runs every frame), and during the
+    // functor walk GetPropertyInt / GetPropertyFloat of a program-written property answer from the log
+    // as of the running functor's place — an object later in NFGUID order (or a later schedule name of
+    // the running object) before its programs' Sets — unless a functor of this walk set that property
+    // itself (its queued Set is read, as always).  Before or after AfterInit.
+    void SetWalkOrderReads(bool on);
+    bool WalkOrderReads() const { return walk_reads_; }
+    bool InFunctorWalk() const { return in_walk_; }
     // called by Execute once the device frame's outputs are read back, before the heartbeat functors
     // run: the frame's events (fh) and its chain are final (a reference-side adapter brings its host
     // objects up to date here, so the functors and their callbacks see the frame's values)
@@ -631,6 +643,16 @@ private:
     HVec<float> fg_t_;
     HVec<uint8_t> ev_same_;
     bool in_walk_ = false;  // (freed functor entries are not reused while the fired list is walked)
+    // walk-order reads (SetWalkOrderReads): the running functor's (object, kind), the log's range of
+    // each object (built on the walk's first such read), the (object, property) a functor of the walk set
+    bool walk_reads_ = false;
+    int32_t walk_o_ = -1, walk_k_ = -1;
+    bool walk_ix_built_ = false;
+    std::unordered_map<int32_t, std::pair<uint32_t, uint32_t>> walk_ix_;
+    std::unordered_map<uint64_t, uint8_t> walk_set_;
+    void WatchProgramProperties();
+    bool WalkRead(const NFGUID& self, int32_t pid, uint64_t* bits);
+    void WalkWrote(const NFGUID& self, int32_t pid);
     static constexpr int64_t kGatherChunk = 1 << 14;
     bool GatherFrame(const nfk_frame_host& fh, int64_t nfi);
     void WaitGather();

@@ -350,8 +350,9 @@ int nfk_read_added(void* world, int32_t cap, int32_t* n, int64_t* guid_head, int
  * callbacks fires one per Set.  The last Set of an (entity, property) ends at the frame event's new
  * value.  n = 0 watches nothing (no extra kernel runs). */
 int nfk_watch_props(void* world, int32_t n, const int32_t* pid);
-/* the last nfk_execute's log in device order (sort by (NFGUID, kind, op) for the reference's);
- * at most cap entries copied, *n = how many there are (nfk_execute_calls fires nothing and keeps it) */
+/* the last nfk_execute's log in the walk's order: objects in NFGUID order, then kind (name order),
+ * then op (SM:52-80) — sorted on the device; at most cap entries copied, *n = how many there are
+ * (nfk_execute_calls fires nothing and keeps it) */
 int nfk_read_chain(void* world, int32_t cap, int32_t* n, int32_t* obj, int32_t* kind, int32_t* op, int32_t* pid,
                    uint64_t* old_bits, uint64_t* new_bits);
 
@@ -442,9 +443,10 @@ int nfk_jit_preview(int32_t n_int, int32_t n_flt, int32_t n_class, int32_t n_kin
 int nfk_set_profiling(void* world, int32_t on);
 /* accumulated device time (ms), launch count and algorithmic bytes per kernel:
  * 0 k_tick, 1 k_records, 2 k_fanout, 3 aux (queued host calls), 4 k_scan_tiles,
- * 5 membership changes (k_seg_lists / k_pack / k_unpack / k_meta) */
-#define NFK_N_KERNEL_TIMERS 6
-int nfk_kernel_times(void* world, double* ms /* [6] */, int64_t* launches /* [6] */, int64_t* bytes /* [6] */);
+ * 5 membership changes (k_seg_lists / k_pack / k_unpack / k_meta), 6 k_chain (the per-Set log of
+ * the watched properties, nfk_watch_props) */
+#define NFK_N_KERNEL_TIMERS 7
+int nfk_kernel_times(void* world, double* ms /* [7] */, int64_t* launches /* [7] */, int64_t* bytes /* [7] */);
 /* membership changes applied so far: windows that rewrote only the changed scene-group segments
  * (n_seg) or rebuilt the segment table (n_full: a new scene group, or a segment out of slack), and
  * the host milliseconds nfk_execute spent planning them (the device part is timer 5 above) */

@@ -204,8 +204,16 @@ public:
             mtDeleteSelfList.clear();
         }
         if (NFISceneAOIModule* a = pPluginManager->FindModule<NFISceneAOIModule>()) a->Execute();  // KM:86
-        for (const NFGUID& g : has_components_)
-            if (NF_SHARE_PTR<NFIObject> o = GetElement(g)) o->Execute();
+        // (a copy: a component may destroy or create objects; its own object's DestroyObject is
+        // deferred to the next Execute through mtDeleteSelfList, KM:275-279 / KM:1434)
+        walk_.assign(has_components_.begin(), has_components_.end());
+        for (const NFGUID& g : walk_) {
+            NF_SHARE_PTR<NFIObject> o = GetElement(g);
+            if (!o) continue;
+            cur_exe_ = g;  // KM:92-94 (mnCurExeObject is private to NFCKernelModule)
+            o->Execute();
+            cur_exe_ = NFGUID();
+        }
         return gpu_.Execute();
     }
 
@@ -278,13 +286,17 @@ public:
     }
     // a record handed out may get hooks and be read later: its object is kept up to date every frame
     NF_SHARE_PTR<NFIRecord> FindRecord(const NFGUID& self, const std::string& rec) override {  // KM:479
-        if (DevRecord(self, rec)) MarkEager(self);
+        if (DevRecord(self, rec)) MarkEager(self, true);
         return NFCKernelModule::FindRecord(self, rec);
     }
 
     // the reference's DestroyObject reads SceneID / GroupID through GetPropertyInt (KM:283-284),
     // which this adapter answers from the device: it runs while the object is still there
     bool DestroyObject(const NFGUID& self) override {  // KM:273
+        if (self == cur_exe_ && !self.IsNull()) {  // KM:275-279: DestroySelf, applied by the next Execute
+            mtDeleteSelfList.push_back(self);
+            return true;
+        }
         const bool ok = NFCKernelModule::DestroyObject(self);
         gpu_.DestroyObject(to_gpu(self));
         handles_.erase(self);
@@ -383,7 +395,7 @@ public:
     void SetEagerMirror(bool on) {
         eager_all_ = on;
         if (on)
-            for (auto& m : mstate_) m |= kEager;
+            for (auto& m : mstate_) m |= kEager | kMirrorAll;
     }
     // (measurement) device events that reached NFCSceneAOIModule's common handlers — and so its
     // GetBroadCastObject — must stay 0; device events handed to the AOI module with the device's list
@@ -402,13 +414,18 @@ public:
 
     // (NFGPUObject) the host object is about to be read or written through its handle
     void Touch(const NFGUID& self) { SyncObject(self); }
+    // (NFGPUObject) a read of a device property inside the heartbeat functor walk with walk-order reads
+    // on (NFGPUKernelModule::SetWalkOrderReads) goes to the device log, not the host object
+    bool WalkRead(const NFGUID& self, const std::string& name) const {
+        return gpu_.WalkOrderReads() && gpu_.InFunctorWalk() && DevProp(self, name);
+    }
     // (NFGPUObject) its ClassName was written; its component manager was handed out
     void ClassNameChanged(const NFGUID& self) { RefreshClassName(self); }
     void HasComponents(const NFGUID& self) { has_components_.insert(self); }
     // (NFGPUObject) a per-object callback registered on a device property / record, or the object's
     // managers handed out: the object is eager from now on, a device property's Sets are logged
     void Watched(const NFGUID& self, const std::string& prop) {
-        MarkEager(self);
+        MarkEager(self, prop.empty());
         if (prop.empty() || !dev_props_.count(prop) || watched_.count(prop)) return;
         watched_.insert(prop);
         if (gpu_.World()) gpu_.WatchProperty(prop);
@@ -457,7 +474,12 @@ private:
     // program also writes was forwarded since the last frame (OnFrame marks it stale: the program may have
     // put the value back where the frame started, which raises no event, while the host mirror holds the
     // written value; a property no program writes has its event whenever the write changed it)
-    enum : uint8_t { kStale = 1, kEager = 2, kWritten = 4 };
+    // kEager: the object's per-object callbacks fire from the device's per-Set log (OnFrame); kMirrorAll:
+    // its host object is also written with every frame event (its managers or records were handed out,
+    // or SetEagerMirror) — an eager object without it is marked stale by its other events instead,
+    // like any other object (NFCNPCRefreshModule's HP callback on every NPC, NFCNPCRefreshModule.cpp:104,
+    // then costs the host the HP Sets' callbacks and a byte per other event)
+    enum : uint8_t { kStale = 1, kEager = 2, kWritten = 4, kMirrorAll = 8 };
     // a Set whose per-object callbacks OnFrame fires, keyed (NFGUID of o, kind, op, row)
     struct Fire {
         int32_t o, kind, op, row;
@@ -578,7 +600,8 @@ private:
     }
 
     uint8_t& State(int o) {
-        if ((size_t)o >= mstate_.size()) mstate_.resize((size_t)gpu_.ObjectCount() + 1024, eager_all_ ? kEager : 0);
+        if ((size_t)o >= mstate_.size())
+            mstate_.resize((size_t)gpu_.ObjectCount() + 1024, eager_all_ ? (uint8_t)(kEager | kMirrorAll) : (uint8_t)0);
         return mstate_[(size_t)o];
     }
     void Written(const nfgpu::NFGUID& g) {
@@ -590,14 +613,15 @@ private:
             written_.push_back(o);
         }
     }
-    void MarkEager(const NFGUID& self) {
+    void MarkEager(const NFGUID& self, bool all) {
+        const uint8_t bits = all ? (uint8_t)(kEager | kMirrorAll) : (uint8_t)kEager;
         const int o = gpu_.ObjectIndex(to_gpu(self));
         if (o < 0) {
-            if (GetElement(self)) pre_eager_.insert(self);  // (being created: applied by MirrorObject)
+            if (GetElement(self)) pre_eager_[self] |= bits;  // (being created: applied by MirrorObject)
             return;
         }
         SyncObject(self);
-        State(o) |= kEager;
+        State(o) |= bits;
     }
 
     // After the device frame (the frame hook), before the heartbeat functors: eager objects take the
@@ -630,9 +654,12 @@ private:
         // cell and frame, so the frame's event is that Set)
         std::vector<Fire>& fires = fr_fire_;
         fires.clear();
+        // (the log comes in the walk's order, nfk_read_chain; it may hold properties no callback
+        // here watches: the plugin's own walk-order reads)
         const std::vector<nfgpu::NFGPUKernelModule::ChainEntry>& ch = gpu_.LastChain();
         for (size_t i = 0; i < ch.size(); i++)
-            if (State(ch[i].obj) & kEager) fires.push_back({ch[i].obj, ch[i].kind, ch[i].op, -1, (int64_t)i});
+            if ((State(ch[i].obj) & kEager) && WatchedPid(ch[i].pid)) fires.push_back({ch[i].obj, ch[i].kind, ch[i].op, -1, (int64_t)i});
+        const size_t n_prop_fires = fires.size();
         for (int64_t e : er) {
             const uint32_t rrc = f.re_rrc[e];
             if ((rrc >> 24) & 3) continue;  // row events: the host record made them (AddRow / Remove / Clear)
@@ -640,7 +667,7 @@ private:
             if (it == rec_op_.end()) continue;  // a SetRecord cell: the host record holds its value already
             fires.push_back({f.re_obj[e], it->second.first, it->second.second, (int32_t)((rrc >> 8) & 0xFF), e});
         }
-        std::stable_sort(fires.begin(), fires.end(), [this](const Fire& x, const Fire& y) {
+        auto walk_less = [this](const Fire& x, const Fire& y) {
             if (x.o != y.o) {
                 const nfgpu::NFGUID &gx = gpu_.ObjectGuid(x.o), &gy = gpu_.ObjectGuid(y.o);
                 return gx < gy;
@@ -648,7 +675,11 @@ private:
             if (x.kind != y.kind) return x.kind < y.kind;
             if (x.op != y.op) return x.op < y.op;
             return x.row < y.row;
-        });
+        };
+        if (fires.size() > n_prop_fires) {  // the record ops' cells (device slot order) merged into the log's order
+            std::stable_sort(fires.begin() + (std::ptrdiff_t)n_prop_fires, fires.end(), walk_less);
+            std::inplace_merge(fires.begin(), fires.begin() + (std::ptrdiff_t)n_prop_fires, fires.end(), walk_less);
+        }
         for (const Fire& fi : fires) {
             const NFGUID self = to_ref(gpu_.ObjectGuid(fi.o));
             NF_SHARE_PTR<NFIObject> ob = GetElement(self);
@@ -675,8 +706,15 @@ private:
             }
         }
         // the eager objects' other evented properties: the frame's value (an unwatched property has no
-        // per-object callback that could tell the Sets apart)
+        // per-object callback that could tell the Sets apart) when the host object is read directly
+        // (kMirrorAll); otherwise the object is stale for them, as any other object (its watched
+        // properties are current: the log's callbacks above wrote them)
         for (int64_t e : ep) {
+            uint8_t& m = State(f.ev_obj[e]);
+            if (!(m & kMirrorAll)) {
+                if (!WatchedPid(f.ev_pid[e])) m |= kStale;
+                continue;
+            }
             const NFGUID self = to_ref(gpu_.ObjectGuid(f.ev_obj[e]));
             NF_SHARE_PTR<NFIObject> ob = GetElement(self);
             const std::string& name = gpu_.PropertyName(f.ev_pid[e]);
@@ -694,6 +732,17 @@ private:
         // (record cells: a cell no record op writes changed only through the host record's own calls,
         // which the host record holds already — the frame's coalesced event of such a cell can carry a
         // SetRecord value an AddRow later overwrote, nfgpu.h nfk_set_records)
+    }
+    // whether a device property id has a per-object callback somewhere (watched_, by device id)
+    bool WatchedPid(int pid) {
+        if (watched_pid_.size() != (size_t)gpu_.PropertyCount(nfgpu::TDATA_INT) + gpu_.PropertyCount(nfgpu::TDATA_FLOAT) +
+                                       gpu_.PropertyCount(nfgpu::TDATA_OBJECT) || watched_n_ != watched_.size()) {
+            watched_pid_.assign((size_t)gpu_.PropertyCount(nfgpu::TDATA_INT) + gpu_.PropertyCount(nfgpu::TDATA_FLOAT) +
+                                    gpu_.PropertyCount(nfgpu::TDATA_OBJECT), 0);
+            for (const std::string& nm : watched_) watched_pid_[(size_t)gpu_.PropertyId(nm)] = 1;
+            watched_n_ = watched_.size();
+        }
+        return pid >= 0 && (size_t)pid < watched_pid_.size() && watched_pid_[(size_t)pid];
     }
     // One write of the mirror: the first host common hook it raises is NFCKernelModule's (registered on
     // every property / record at creation, KM:166 / KM:186, before any per-object callback) and is the
@@ -843,8 +892,9 @@ private:
         const int idx = gpu_.ObjectIndex(to_gpu(self));
         if (idx >= 0) {
             uint8_t& m = State(idx);
-            m = eager_all_ || pre_eager_.count(self) ? kEager : 0;
-            pre_eager_.erase(self);
+            auto pe = pre_eager_.find(self);
+            m = eager_all_ ? (uint8_t)(kEager | kMirrorAll) : pe != pre_eager_.end() ? pe->second : (uint8_t)0;
+            if (pe != pre_eager_.end()) pre_eager_.erase(pe);
         }
     }
     // (before AfterInit) the rows the host object's device records already hold: their state at frame 0
@@ -905,9 +955,11 @@ private:
     // host mirror state per device object index (kStale / kEager), objects made eager before they
     // reached the device, watched device properties
     std::vector<uint8_t> mstate_;
-    std::unordered_set<NFGUID, GuidHash> pre_eager_;
+    std::unordered_map<NFGUID, uint8_t, GuidHash> pre_eager_;
     bool eager_all_ = false;
     std::set<std::string> watched_;
+    std::vector<uint8_t> watched_pid_;  // (WatchedPid's table, rebuilt when watched_ grows)
+    size_t watched_n_ = 0;
     std::vector<std::string> watch_pending_;
     std::map<uint16_t, std::pair<int, int>> rec_op_;  // (rec << 8 | col) -> (kind, op index)
     std::unordered_map<NFGUID, NF_SHARE_PTR<NFIObject>, GuidHash> handles_;
@@ -915,6 +967,8 @@ private:
     std::unordered_map<NFGUID, const std::string*, GuidHash> class_of_;
     NFCDataList gl_scratch_;
     std::set<NFGUID> has_components_;  // objects whose component manager was handed out (Execute walks them)
+    std::vector<NFGUID> walk_;          // Execute's copy of has_components_
+    NFGUID cur_exe_;                    // the object whose components Execute is running (KM's mnCurExeObject)
     // (scratch kept across frames)
     std::vector<int64_t> fr_ep_, fr_er_;
     std::vector<int> written_;  // objects with kWritten (OnFrame)
@@ -950,8 +1004,12 @@ public:
     bool SetPropertyObject(const std::string& n, const NFGUID& v) override { return T()->SetPropertyObject(n, v); }
     bool SetPropertyVector2(const std::string& n, const NFVector2& v) override { return T()->SetPropertyVector2(n, v); }
     bool SetPropertyVector3(const std::string& n, const NFVector3& v) override { return T()->SetPropertyVector3(n, v); }
-    NFINT64 GetPropertyInt(const std::string& n) override { return T()->GetPropertyInt(n); }
-    double GetPropertyFloat(const std::string& n) override { return T()->GetPropertyFloat(n); }
+    NFINT64 GetPropertyInt(const std::string& n) override {
+        return k_->WalkRead(self_, n) ? k_->GetPropertyInt(self_, n) : T()->GetPropertyInt(n);
+    }
+    double GetPropertyFloat(const std::string& n) override {
+        return k_->WalkRead(self_, n) ? k_->GetPropertyFloat(self_, n) : T()->GetPropertyFloat(n);
+    }
     const std::string& GetPropertyString(const std::string& n) override { return in_->GetPropertyString(n); }
     const NFGUID& GetPropertyObject(const std::string& n) override { return T()->GetPropertyObject(n); }
     const NFVector2& GetPropertyVector2(const std::string& n) override { return in_->GetPropertyVector2(n); }

@@ -55,7 +55,8 @@ int dalloc(T** p, size_t n) {
     return NFK_OK;
 }
 
-enum { KT_TICK = 0, KT_REC = 1, KT_FAN = 2, KT_AUX = 3, KT_SCAN = 4, KT_MEM = 5, KT_N = 6 };
+enum { KT_TICK = 0, KT_REC = 1, KT_FAN = 2, KT_AUX = 3, KT_SCAN = 4, KT_MEM = 5, KT_CHAIN = 6, KT_N = 7 };
+static_assert(KT_N == NFK_N_KERNEL_TIMERS, "nfk_kernel_times' arrays");
 
 struct PendingTiming {
     int kind;
@@ -281,11 +282,19 @@ struct World {
     int32_t max_np = 0;    // most players in one scene group (an upper bound between full re-layouts)
     // per-Set chains of the watched properties (nfk_watch_props, k_chain): the watch mask, the log
     // of the last nfk_execute (ChainEnt records, its count on the device) and whether that frame ran it
+    // (k_chain stages it per tile: chain_tcap records per tile, chain_cnt_d the tiles' counts; the
+    // read-back's device scratch and pinned copy are the chain's own, so nfk_read_frame's stay valid)
     uint64_t chain_watch[2] = {0, 0};
     ChainEnt* chain_d = nullptr;
     uint32_t* chain_cnt_d = nullptr;
     size_t chain_cap = 0;  // records
+    uint32_t chain_tcap = 0;
+    int32_t chain_tiles = 0;
     bool chain_ran = false;
+    void* chain_scr = nullptr;
+    size_t chain_scap = 0;
+    char* chain_pin = nullptr;
+    size_t chain_pcap = 0;
 
     bool profiling = false;
     std::vector<PendingTiming> pend;
@@ -1720,6 +1729,8 @@ int nfk_destroy(void* world) {
     if (w->hf_buf) (void)hipFree(w->hf_buf);
     if (w->chain_d) (void)hipFree(w->chain_d);
     if (w->chain_cnt_d) (void)hipFree(w->chain_cnt_d);
+    if (w->chain_scr) (void)hipFree(w->chain_scr);
+    if (w->chain_pin) (void)hipHostFree(w->chain_pin);
     for (auto& p : w->pend) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -2851,30 +2862,89 @@ int nfk_watch_props(void* world, int32_t n, const int32_t* pid) {
     return NFK_OK;
 }
 
+static int update_guid_ranks(World* w);
+
 int nfk_read_chain(void* world, int32_t cap, int32_t* n, int32_t* obj, int32_t* kind, int32_t* op, int32_t* pid,
                    uint64_t* old_bits, uint64_t* new_bits) {
     World* w = (World*)world;
     if (!w || !n || cap < 0) return fail(NFK_ERR_ARG, "null argument");
     *n = 0;
     if (!w->chain_ran) return NFK_OK;
-    HIPCHK(hipStreamSynchronize(w->stream));
+    // the tiles' counts -> dense bases (and the total), on the world's stream after the frame
+    const int32_t nt = w->chain_tiles;
+    const size_t s_db = 0, s_k1 = (((size_t)nt + 1) * 4 + 255) & ~(size_t)255;
+    if (s_k1 > w->chain_scap) {
+        HIPCHK(hipStreamSynchronize(w->stream));
+        if (w->chain_scr) HIPCHK(hipFree(w->chain_scr));
+        w->chain_scr = nullptr;
+        w->chain_scap = s_k1 + 4096;
+        HIPCHK(hipMalloc(&w->chain_scr, w->chain_scap));
+    }
+    uint32_t* db = (uint32_t*)((char*)w->chain_scr + s_db);
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, w->stream, w->chain_cnt_d, db, nt);
     uint32_t cnt = 0;
-    HIPCHK(hipMemcpy(&cnt, w->chain_cnt_d, sizeof(cnt), hipMemcpyDeviceToHost));
-    if (cnt > w->chain_cap) return fail(NFK_ERR_CAPACITY, "per-Set chain log overflow");
+    HIPCHK(hipMemcpyAsync(&cnt, db + nt, sizeof(cnt), hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
     *n = (int32_t)cnt;
     const uint32_t m = std::min<uint32_t>(cnt, (uint32_t)cap);
     if (!m) return NFK_OK;
     if (!obj || !kind || !op || !pid || !old_bits || !new_bits) return fail(NFK_ERR_ARG, "null argument");
-    std::vector<ChainEnt> h(m);
-    HIPCHK(hipMemcpy(h.data(), w->chain_d, (size_t)m * sizeof(ChainEnt), hipMemcpyDeviceToHost));
-    for (uint32_t i = 0; i < m; i++) {
-        obj[i] = w->obj_of_slot[h[i].slot];
-        kind[i] = h[i].kind;
-        op[i] = h[i].op;
-        pid[i] = h[i].pid;
-        old_bits[i] = h[i].old_bits;
-        new_bits[i] = h[i].new_bits;
+    // walk order: (NFGUID rank of the object, kind, op) keys sorted on the device, the entries
+    // gathered in that order as object-index columns, one copy back
+    int r = update_guid_ranks(w);
+    if (r) return r;
+    int key_bits = 8;
+    while ((1ll << (key_bits - 8)) < (long long)std::max(w->n_obj, 1)) key_bits++;
+    size_t sort_bytes = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                     (uint32_t*)nullptr, cnt, 0, key_bits, w->stream));
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t s_k2 = s_k1 + al((size_t)cnt * 8), s_i1 = s_k2 + al((size_t)cnt * 8), s_i2 = s_i1 + al((size_t)cnt * 4);
+    const size_t s_out = s_i2 + al((size_t)cnt * 4), s_tmp = s_out + al((size_t)cnt * 32);
+    const size_t need = s_tmp + sort_bytes + 256, pin = (size_t)cnt * 32;
+    if (need > w->chain_scap || pin > w->chain_pcap) {
+        // (db survives: the scan is redone into the new scratch)
+        HIPCHK(hipStreamSynchronize(w->stream));
+        if (need > w->chain_scap) {
+            HIPCHK(hipFree(w->chain_scr));
+            w->chain_scr = nullptr;
+            w->chain_scap = need + need / 4 + 4096;
+            HIPCHK(hipMalloc(&w->chain_scr, w->chain_scap));
+            db = (uint32_t*)((char*)w->chain_scr + s_db);
+            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, w->stream, w->chain_cnt_d, db, nt);
+        }
+        if (pin > w->chain_pcap) {
+            if (w->chain_pin) HIPCHK(hipHostFree(w->chain_pin));
+            w->chain_pin = nullptr;
+            w->chain_pcap = pin + pin / 4 + 4096;
+            HIPCHK(hipHostMalloc((void**)&w->chain_pin, w->chain_pcap, hipHostMallocDefault));
+        }
     }
+    char* S = (char*)w->chain_scr;
+    uint64_t* k1 = (uint64_t*)(S + s_k1);
+    uint64_t* k2 = (uint64_t*)(S + s_k2);
+    uint32_t* i1 = (uint32_t*)(S + s_i1);
+    uint32_t* i2 = (uint32_t*)(S + s_i2);
+    const unsigned gt = (unsigned)std::max(1, std::min(nt, 4096));
+    hipLaunchKernelGGL(k_chain_keys, dim3(gt), dim3(kTPB), 0, w->stream, (const ChainEnt*)w->chain_d, (const uint32_t*)db, nt,
+                       w->chain_tcap, (const int32_t*)w->slot_obj_d, (const int32_t*)w->rank_d, k1, i1);
+    size_t sb = sort_bytes;
+    HIPCHK(rocprim::radix_sort_pairs(S + s_tmp, sb, k1, k2, i1, i2, cnt, 0, key_bits, w->stream));
+    int32_t* oi = (int32_t*)(S + s_out);
+    uint64_t* ou = (uint64_t*)(S + s_out + (size_t)cnt * 16);
+    hipLaunchKernelGGL(k_chain_gather, dim3((cnt + kTPB - 1) / kTPB), dim3(kTPB), 0, w->stream, (const ChainEnt*)w->chain_d,
+                       (const uint32_t*)i2, (int)cnt, (const int32_t*)w->slot_obj_d, oi, ou);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(w->chain_pin, S + s_out, (size_t)cnt * 32, hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    const int32_t* hi = (const int32_t*)w->chain_pin;
+    const uint64_t* hu = (const uint64_t*)(w->chain_pin + (size_t)cnt * 16);
+    memcpy(obj, hi, (size_t)m * 4);
+    memcpy(kind, hi + cnt, (size_t)m * 4);
+    memcpy(op, hi + 2 * (size_t)cnt, (size_t)m * 4);
+    memcpy(pid, hi + 3 * (size_t)cnt, (size_t)m * 4);
+    memcpy(old_bits, hu, (size_t)m * 8);
+    memcpy(new_bits, hu + cnt, (size_t)m * 8);
     return NFK_OK;
 }
 
@@ -3701,24 +3771,35 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
                 }
             }
         if (kinds) {
-            const size_t need = (size_t)d.N * (size_t)wops;
-            if (need > w->chain_cap) {
+            // tile-staged: kTPB slots x the watched (kind, op) pairs per tile (each logs at most once)
+            const int32_t nt = (int32_t)((d.N + kTPB - 1) / kTPB);
+            const uint32_t tcap = (uint32_t)(kTPB * wops);
+            const size_t need = (size_t)nt * tcap;
+            if (need > w->chain_cap || nt > w->chain_tiles) {
                 HIPCHK(hipStreamSynchronize(w->stream));
-                if (w->chain_d) HIPCHK(hipFree(w->chain_d));
-                w->chain_d = nullptr;
-                w->chain_cap = 0;
-                if (hipMalloc(&w->chain_d, need * sizeof(ChainEnt)) != hipSuccess)
-                    return drop_window(w, fail(NFK_ERR_CAPACITY, "hipMalloc (per-Set chain log)"));
-                w->chain_cap = need;
+                if (need > w->chain_cap) {
+                    if (w->chain_d) HIPCHK(hipFree(w->chain_d));
+                    w->chain_d = nullptr;
+                    w->chain_cap = 0;
+                    if (hipMalloc(&w->chain_d, need * sizeof(ChainEnt)) != hipSuccess)
+                        return drop_window(w, fail(NFK_ERR_CAPACITY, "hipMalloc (per-Set chain log)"));
+                    w->chain_cap = need;
+                }
+                if (nt > w->chain_tiles) {
+                    if (w->chain_cnt_d) HIPCHK(hipFree(w->chain_cnt_d));
+                    w->chain_cnt_d = nullptr;
+                    w->chain_tiles = 0;
+                    HIPCHK(hipMalloc(&w->chain_cnt_d, ((size_t)nt + 1) * sizeof(uint32_t)));
+                    w->chain_tiles = nt;
+                }
             }
-            if (!w->chain_cnt_d) HIPCHK(hipMalloc(&w->chain_cnt_d, sizeof(uint32_t)));
-            TimeScope ts(w, KT_AUX);
-            HIPCHK(hipMemsetAsync(w->chain_cnt_d, 0, sizeof(uint32_t), w->stream));
-            hipLaunchKernelGGL(k_chain, dim3((unsigned)((d.N + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, d,
-                               w->chain_d, w->chain_cnt_d, (uint32_t)std::min<size_t>(w->chain_cap, 0xFFFFFFFFu), kinds,
-                               w->chain_watch[0], w->chain_watch[1]);
+            w->chain_tcap = tcap;
+            TimeScope ts(w, KT_CHAIN);
+            hipLaunchKernelGGL(k_chain, dim3((unsigned)nt), dim3(kTPB), 0, w->stream, d, w->chain_d, w->chain_cnt_d, tcap,
+                               kinds, w->chain_watch[0], w->chain_watch[1]);
             HIPCHK(hipGetLastError());
             w->chain_ran = true;
+            w->chain_tiles = nt;
         }
     }
     if (d.n_tiles) {

@@ -752,6 +752,11 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
 // heartbeat programs READ-ONLY, before k_tick, on the values k_sets left — k_tick_touch's own code
 // (sched_scan without its stores, run_program) — and logs every accepted Set of a watched property
 // as (slot, kind, op, property, old, new).  Off (not launched) while nothing is watched.
+// The log is tile-staged like the frame's other outputs: tile t's entries at t * tcap (tcap = the
+// tile's slots x the (kind, op) pairs whose destination is watched), in (slot, kind, op) order — a
+// thread's own in program order, the threads' placed by a block scan of their counts (the programs
+// run twice: count, then write) — and t_cnt[t] of them; no atomics, so the log is deterministic.
+// nfk_read_chain compacts it and sorts it into the walk's (NFGUID, kind, op) order on the device.
 struct ChainEnt {
     uint32_t slot;
     uint16_t pid;
@@ -759,31 +764,78 @@ struct ChainEnt {
     uint64_t old_bits, new_bits;
 };
 static_assert(sizeof(ChainEnt) == 24, "ChainEnt is read back as 24-byte records");
-__global__ __launch_bounds__(kTPB) void k_chain(Dev d, ChainEnt* __restrict__ out, uint32_t* __restrict__ count,
-                                                uint32_t cap, uint32_t kinds, uint64_t watch0, uint64_t watch1) {
+__global__ __launch_bounds__(kTPB) void k_chain(Dev d, ChainEnt* __restrict__ out, uint32_t* __restrict__ t_cnt,
+                                                uint32_t tcap, uint32_t kinds, uint64_t watch0, uint64_t watch1) {
     __shared__ uint64_t s_old[NFK_MAX_TOUCH * kTPB];  // (Ent's frame-start list; unused here)
+    __shared__ unsigned long long s_w[kTPB / 64];
     const int e = blockIdx.x * kTPB + (int)threadIdx.x;
-    if (e >= d.N) return;  // (no barrier follows)
-    unsigned bytes = 0;
-    uint64_t desc = kDeadDesc;
-    const uint32_t fired = sched_scan<DynSchema, false>(d, e, bytes, desc) & kinds;
-    if (desc_dead(desc) || !fired) return;
+    uint32_t fired = 0;
+    if (e < d.N) {
+        unsigned bytes = 0;
+        uint64_t desc = kDeadDesc;
+        fired = sched_scan<DynSchema, false>(d, e, bytes, desc) & kinds;
+        if (desc_dead(desc)) fired = 0;
+    }
     Ent en;
-    en.n = 0;
-    en.old = s_old + threadIdx.x;
-    en.ovf = false;
-    en.bytes = 0;
-    en.dv = &d;
-    en.cap = (size_t)d.cap;
-    en.n_int = d.n_int;
-    en.e = e;
-    auto log = [&](int k, int i, uint32_t p, uint64_t o, uint64_t n) {
-        if (!(((p < 64 ? watch0 >> p : watch1 >> (p - 64)) & 1ull))) return;
-        const uint32_t at = atomicAdd(count, 1u);
-        if (at < cap) out[at] = ChainEnt{(uint32_t)e, (uint16_t)p, (uint8_t)k, (uint8_t)i, o, n};
+    auto run = [&](auto&& log) {
+        en.n = 0;
+        en.old = s_old + threadIdx.x;
+        en.ovf = false;
+        en.bytes = 0;
+        en.dv = &d;
+        en.cap = (size_t)d.cap;
+        en.n_int = d.n_int;
+        en.e = e;
+        for (int k = 0; k < d.n_kind; k++)
+            if ((fired >> k) & 1) run_program(en, d.tab, k, log);
     };
-    for (int k = 0; k < d.n_kind; k++)
-        if ((fired >> k) & 1) run_program(en, d.tab, k, log);
+    auto watched = [&](uint32_t p) { return ((p < 64 ? watch0 >> p : watch1 >> (p - 64)) & 1ull) != 0; };
+    uint32_t cnt = 0;
+    bool ovf = false;
+    if (fired) {
+        run([&](int, int, uint32_t p, uint64_t, uint64_t) { cnt += watched(p) ? 1u : 0u; });
+        ovf = en.ovf;  // (a program touching more than NFK_MAX_TOUCH properties: k_tick raises it too)
+    }
+    unsigned long long tot;
+    uint32_t at = (uint32_t)block_excl_scan(cnt, s_w, tot);
+    if (cnt) {
+        ChainEnt* t_out = out + (size_t)blockIdx.x * tcap;
+        run([&](int k, int i, uint32_t p, uint64_t o, uint64_t n) {
+            if (watched(p) && at < tcap) t_out[at++] = ChainEnt{(uint32_t)e, (uint16_t)p, (uint8_t)k, (uint8_t)i, o, n};
+        });
+    }
+    if (threadIdx.x == 0) t_cnt[blockIdx.x] = (uint32_t)tot;
+    if (ovf) dev_error(d, kErrTouch);  // (the log of an overflowing entity is not the frame's)
+}
+// nfk_read_chain: the staged log -> sort keys (rank of the object's NFGUID, kind, op) and the staged
+// index of each entry, in dense order (db: the tiles' exclusive scan)
+__global__ __launch_bounds__(kTPB) void k_chain_keys(const ChainEnt* __restrict__ src, const uint32_t* __restrict__ db,
+                                                     int n_tiles, uint32_t tcap, const int32_t* __restrict__ slot_obj,
+                                                     const int32_t* __restrict__ rank, uint64_t* __restrict__ keys,
+                                                     uint32_t* __restrict__ idx) {
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const uint32_t b = db[t], n = db[t + 1] - b;
+        for (uint32_t i = threadIdx.x; i < n; i += kTPB) {
+            const size_t s = (size_t)t * tcap + i;
+            const ChainEnt c = src[s];
+            keys[b + i] = ((uint64_t)(uint32_t)rank[slot_obj[c.slot]] << 8) | ((uint64_t)c.kind << 3) | (uint64_t)c.op;
+            idx[b + i] = (uint32_t)s;
+        }
+    }
+}
+// the sorted log as object-index columns (obj, kind, op, pid as int32; old, new) for one copy back
+__global__ __launch_bounds__(kTPB) void k_chain_gather(const ChainEnt* __restrict__ src, const uint32_t* __restrict__ idx,
+                                                       int n, const int32_t* __restrict__ slot_obj,
+                                                       int32_t* __restrict__ i32, uint64_t* __restrict__ u64) {
+    const int j = blockIdx.x * kTPB + threadIdx.x;
+    if (j >= n) return;
+    const ChainEnt c = src[idx[j]];
+    i32[j] = slot_obj[c.slot];
+    i32[(size_t)n + j] = c.kind;
+    i32[2 * (size_t)n + j] = c.op;
+    i32[3 * (size_t)n + j] = c.pid;
+    u64[j] = c.old_bits;
+    u64[(size_t)n + j] = c.new_bits;
 }
 
 // ---------------------------------------------------------------------------------

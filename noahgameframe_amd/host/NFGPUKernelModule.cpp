@@ -347,7 +347,65 @@ bool NFGPUKernelModule::AfterInit() {
     committed_ = true;
     for (const std::string& nm : watch_names_) WatchProperty(nm);
     watch_names_.clear();
+    if (walk_reads_) WatchProgramProperties();
     return true;
+}
+
+void NFGPUKernelModule::SetWalkOrderReads(bool on) {
+    walk_reads_ = on;
+    if (on && committed_) WatchProgramProperties();
+}
+
+// every int / f64 property a heartbeat program writes joins the per-Set log
+void NFGPUKernelModule::WatchProgramProperties() {
+    bool added = false;
+    for (int32_t pid = 0; pid < (int32_t)prog_props_.size(); pid++) {
+        if (!prog_props_[(size_t)pid] || PropertyType(pid) == TDATA_OBJECT) continue;
+        if (std::find(watch_pids_.begin(), watch_pids_.end(), pid) != watch_pids_.end()) continue;
+        watch_pids_.push_back(pid);
+        added = true;
+    }
+    if (added) check(nfk_watch_props(world_, (int32_t)watch_pids_.size(), watch_pids_.data()), "nfk_watch_props");
+}
+
+// (walk-order reads) the value of (self, pid) as of the running functor's place in the walk, from the
+// frame's per-Set log: an object before it in NFGUID order has made all its Sets (the device's value),
+// one after it none (its first logged Set's old value), the running object those of its schedules up
+// to the running one (SM:52-80).  False: read the device (no logged Set, or a functor of this walk set
+// the property: its queued Set is what the reference's read returns).
+bool NFGPUKernelModule::WalkRead(const NFGUID& self, int32_t pid, uint64_t* bits) {
+    if (!walk_reads_ || !in_walk_ || walk_o_ < 0 || !ProgramWrites(pid)) return false;
+    const int32_t o = ObjectIndex(self);
+    if (o < 0 || walk_set_.count(((uint64_t)(uint32_t)o << 8) | (uint32_t)pid)) return false;
+    if (o != walk_o_ && guids_[(size_t)o] < guids_[(size_t)walk_o_]) return false;
+    if (!walk_ix_built_) {
+        walk_ix_.clear();
+        for (uint32_t i = 0; i < (uint32_t)chain_.size(); i++) {
+            auto it = walk_ix_.find(chain_[i].obj);
+            if (it == walk_ix_.end()) walk_ix_.emplace(chain_[i].obj, std::make_pair(i, i + 1));
+            else it->second.second = i + 1;  // (an object's entries are contiguous in the walk's order)
+        }
+        walk_ix_built_ = true;
+    }
+    auto it = walk_ix_.find(o);
+    if (it == walk_ix_.end()) return false;
+    const ChainEntry* first = nullptr;
+    const ChainEntry* last_before = nullptr;
+    for (uint32_t i = it->second.first; i < it->second.second; i++) {
+        const ChainEntry& c = chain_[i];
+        if (c.pid != pid) continue;
+        if (!first) first = &c;
+        if (o == walk_o_ && c.kind <= walk_k_) last_before = &c;
+    }
+    if (!first) return false;
+    *bits = last_before ? last_before->new_bits : first->old_bits;
+    return true;
+}
+
+void NFGPUKernelModule::WalkWrote(const NFGUID& self, int32_t pid) {
+    if (!walk_reads_ || !in_walk_) return;
+    const int32_t o = ObjectIndex(self);
+    if (o >= 0) walk_set_[((uint64_t)(uint32_t)o << 8) | (uint32_t)pid] = 1;
 }
 
 void NFGPUKernelModule::WatchProperty(const std::string& name) {
@@ -364,7 +422,7 @@ void NFGPUKernelModule::WatchProperty(const std::string& name) {
 }
 
 // the frame's per-Set log in the order the reference's heartbeat walk makes the Sets: objects in
-// NFGUID order, then kind (name order), then op (SM:52-80)
+// NFGUID order, then kind (name order), then op (SM:52-80), as nfk_read_chain hands it over
 void NFGPUKernelModule::ReadChain() {
     chain_.clear();
     if (watch_pids_.empty()) return;
@@ -375,12 +433,8 @@ void NFGPUKernelModule::ReadChain() {
     std::vector<uint64_t> a((size_t)n), b((size_t)n);
     int32_t m = 0;
     check(nfk_read_chain(world_, n, &m, o.data(), k.data(), op.data(), pid.data(), a.data(), b.data()), "nfk_read_chain");
-    chain_.resize((size_t)n);
+    chain_.resize((size_t)n);  // (in the walk's order already: nfk_read_chain sorts it on the device)
     for (int32_t i = 0; i < n; i++) chain_[(size_t)i] = {o[(size_t)i], k[(size_t)i], op[(size_t)i], pid[(size_t)i], a[(size_t)i], b[(size_t)i]};
-    std::sort(chain_.begin(), chain_.end(), [this](const ChainEntry& x, const ChainEntry& y) {
-        if (x.obj != y.obj) return guids_[(size_t)x.obj] < guids_[(size_t)y.obj];
-        return x.kind != y.kind ? x.kind < y.kind : x.op < y.op;
-    });
 }
 
 bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int nTargetGroupID, float fX, float fY,
@@ -494,6 +548,7 @@ int NFGPUKernelModule::ObjectIndex(const NFGUID& g) const { return obj_of_.find(
 bool NFGPUKernelModule::SetPropertyInt(const NFGUID& self, const std::string& name, int64_t v) {
     const int p = prop_ix_.find(name);
     if (!committed_ || p < 0 || props_[(size_t)p].type != TDATA_INT) return false;
+    if (walk_reads_ && in_walk_) WalkWrote(self, dev_pid_[(size_t)p]);
     qs_h_.push_back(self.nHead64);
     qs_d_.push_back(self.nData64);
     qs_pid_.push_back(dev_pid_[(size_t)p]);
@@ -701,6 +756,7 @@ double NFGPUKernelModule::GetRecordFloat(const NFGUID& self, const std::string& 
 bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& name, double v) {
     const int p = prop_ix_.find(name);
     if (!committed_ || p < 0 || props_[(size_t)p].type != TDATA_FLOAT) return false;
+    if (walk_reads_ && in_walk_) WalkWrote(self, dev_pid_[(size_t)p]);
     qs_h_.push_back(self.nHead64);
     qs_d_.push_back(self.nData64);
     qs_pid_.push_back(dev_pid_[(size_t)p]);
@@ -715,9 +771,10 @@ bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& 
 int64_t NFGPUKernelModule::GetPropertyInt(const NFGUID& self, const std::string& name) {
     const int p = prop_ix_.find(name);
     if (!committed_ || ObjectIndex(self) < 0 || p < 0 || props_[(size_t)p].type != TDATA_INT) return 0;
-    Flush();
     const int32_t pid = dev_pid_[(size_t)p];
     uint64_t b = 0;
+    if (walk_reads_ && WalkRead(self, pid, &b)) return (int64_t)b;
+    Flush();
     check(nfk_get_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b), "nfk_get_props");
     return (int64_t)b;
 }
@@ -725,9 +782,10 @@ int64_t NFGPUKernelModule::GetPropertyInt(const NFGUID& self, const std::string&
 double NFGPUKernelModule::GetPropertyFloat(const NFGUID& self, const std::string& name) {
     const int p = prop_ix_.find(name);
     if (!committed_ || ObjectIndex(self) < 0 || p < 0 || props_[(size_t)p].type != TDATA_FLOAT) return 0.0;
-    Flush();
     const int32_t pid = dev_pid_[(size_t)p];
     uint64_t b = 0;
+    if (walk_reads_ && WalkRead(self, pid, &b)) return dbl_of(b);
+    Flush();
     check(nfk_get_props(world_, 1, &self.nHead64, &self.nData64, &pid, &b), "nfk_get_props");
     return dbl_of(b);
 }
@@ -949,6 +1007,8 @@ bool NFGPUKernelModule::Execute() {
     const bool gathered = GatherFrame(fh, nfi);
     double gather_ms = ms_since(t1);
     in_walk_ = true;
+    walk_ix_built_ = false;
+    walk_set_.clear();
     if (gathered) {
         // the functor entries, NFGUIDs and intervals are dense arrays, gathered chunk by chunk
         // ahead of the walk: only the functor objects themselves are scattered (prefetched ahead)
@@ -965,7 +1025,11 @@ bool NFGPUKernelModule::Execute() {
                 if (i + kPre < i1 && fg_c_[(size_t)(i + kPre)] >= 0) __builtin_prefetch(&cb_pool_[(size_t)fg_c_[(size_t)(i + kPre)]]);
                 const int32_t c = fg_c_[(size_t)i];
                 // (empty: a functor earlier in this walk destroyed the object or moved it to another shard)
-                if (c >= 0 && cb_pool_[(size_t)c]) cb_pool_[(size_t)c](fg_g_[(size_t)i], heartbeats_[(size_t)fh.fi_kind[i]].name, fg_t_[(size_t)i], fh.fi_remain[i]);
+                if (c >= 0 && cb_pool_[(size_t)c]) {
+                    walk_o_ = fh.fi_obj[i];
+                    walk_k_ = fh.fi_kind[i];
+                    cb_pool_[(size_t)c](fg_g_[(size_t)i], heartbeats_[(size_t)fh.fi_kind[i]].name, fg_t_[(size_t)i], fh.fi_remain[i]);
+                }
             }
         }
     } else {
@@ -992,10 +1056,15 @@ bool NFGPUKernelModule::Execute() {
             const int o = fh.fi_obj[i], k = fh.fi_kind[i];
             const size_t at = (size_t)o * nk + (size_t)k;
             const int32_t c = at < cb_slot_.size() ? cb_slot_[at] : -1;
-            if (c >= 0) cb_pool_[c](guids_[o], heartbeats_[k].name, cb_time_[c], fh.fi_remain[i]);
+            if (c >= 0) {
+                walk_o_ = o;
+                walk_k_ = k;
+                cb_pool_[c](guids_[o], heartbeats_[k].name, cb_time_[c], fh.fi_remain[i]);
+            }
         }
     }
     in_walk_ = false;
+    walk_o_ = walk_k_ = -1;
     {
         const auto tw = std::chrono::steady_clock::now();
         WaitGather();  // the events' part, gathered while the walk ran

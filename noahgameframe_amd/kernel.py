@@ -56,8 +56,8 @@ class Outputs(ctypes.Structure):
                   "msg_rcpt", "slot_obj", "ev_old_h", "ev_new_h"]])
 
 
-N_KERNEL_TIMERS = 6
-KERNEL_TIMER_NAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles"]
+N_KERNEL_TIMERS = 7
+KERNEL_TIMER_NAMES = ["k_tick", "k_records", "k_fanout", "aux", "k_scan_tiles", "membership", "k_chain"]
 
 
 _lib = None

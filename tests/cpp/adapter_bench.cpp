@@ -18,7 +18,13 @@
 // host ms per frame (median of the timed frames), the plugin's phases, what the callbacks received and
 // how many device events reached NFCSceneAOIModule's own handlers (GetBroadCastObject) — 0.
 //
-// usage: adapter_bench <workload.nfio> <warmup> <frames> [mode] [calls] [wait]
+// With npc 1 the same frames then run again after every NPC has registered NFCNPCRefreshModule's callback
+// (NFCNPCRefreshModule.cpp:98-105: AddPropertyCallBack(self, "HP", OnObjectHPEvent) at creation; its
+// newVar <= 0 test counted): every NPC is eager and HP is logged per Set (k_chain), so each frame also
+// fires one callback per accepted HP Set of its heartbeat programs, in the walk's order; the JSON line
+// carries those frames as "npc_hp".
+//
+// usage: adapter_bench <workload.nfio> <warmup> <frames> [mode] [calls] [wait] [npc]
 //   mode 0: the config[1] logic above;  1: Tutorial3's (per-object World callbacks, OnEvent Sets)
 //   calls 1: the workload's SetProperty / schedule calls between frames (mode 1 always makes its Sets)
 //   wait 1: after the host objects are built (nothing has touched the GPU yet) print {"ready": ...} and
@@ -74,6 +80,12 @@ struct Counters {
         obj_cb++;
         return 0;
     }
+    int64_t kills = 0;
+    int OnObjectHPEvent(const NFGUID&, const std::string&, const NFIDataList::TData&, const NFIDataList::TData& b) {
+        obj_cb++;  // NFCNPCRefreshModule.cpp:113: newVar <= 0 kills
+        kills += b.GetInt() <= 0;
+        return 0;
+    }
 };
 
 int main(int argc, char** argv) {
@@ -84,6 +96,7 @@ int main(int argc, char** argv) {
     const int mode = argc > 4 ? atoi(argv[4]) : 0;
     const bool calls = mode == 1 || (argc > 5 && atoi(argv[5]) != 0);
     const bool wait = argc > 6 && atoi(argv[6]) != 0;
+    const bool npc = argc > 7 && atoi(argv[7]) != 0;
     auto A = [&](const char* n) {
         nfio_arr* a = nfio_get(&wf, n);
         if (!a) {
@@ -94,7 +107,7 @@ int main(int argc, char** argv) {
     };
     int64_t* cfg = (int64_t*)A("cfg")->data;
     const int64_t N = cfg[0], NI = cfg[1], NF = cfg[2], NC = cfg[3], NK = cfg[4], NR = cfg[5], NS = cfg[6], NT = cfg[7];
-    if (W + K > NT) {
+    if ((npc ? 2 : 1) * (W + K) > NT) {
         fprintf(stderr, "workload has %lld frames, %d requested\n", (long long)NT, W + K);
         return 2;
     }
@@ -221,71 +234,102 @@ int main(int argc, char** argv) {
     int32_t* h_cnt = (int32_t*)A("h_count")->data;
     int64_t* h_time = (int64_t*)A("h_time")->data;
 
-    std::vector<nfgpu::NFGPUKernelModule::FrameStats> st;
-    std::vector<double> call_ms, frame_ms;
-    int64_t xi = 0, hi = 0, ncalls = 0;
-    const int64_t syncs0 = kernel.MirrorSyncs();
-    Counters c0;
-    for (int t = 0; t < W + K; t++) {
-        if (t == W) c0 = C;
-        const auto t0 = std::chrono::steady_clock::now();
-        for (; hi < NH && h_tick[hi] == t; hi++) {
-            if (!calls) continue;
-            const NFGUID g(gh[h_obj[hi]], gd[h_obj[hi]]);
-            g_now = h_time[hi];
-            if (h_op[hi] == 1) sm->AddSchedule(g, kname[h_kind[hi]], hb, h_int[hi], h_cnt[hi]);
-            else if (h_op[hi] == 2) sm->RemoveSchedule(g, kname[h_kind[hi]]);
-            else sm->RemoveSchedule(g);
-            ncalls += t >= W;
+    int64_t xi = 0, hi = 0;
+    // frames [t0, t0 + W + K): the window's calls before each, every module's Execute; the timed K frames
+    // as one JSON object
+    auto run = [&](int t0) -> std::string {
+        std::vector<nfgpu::NFGPUKernelModule::FrameStats> st;
+        std::vector<double> call_ms, frame_ms;
+        int64_t ncalls = 0;
+        const int64_t syncs0 = kernel.MirrorSyncs(), chain0 = kernel.ChainCallbacks();
+        Counters c0;
+        for (int t = t0; t < t0 + W + K; t++) {
+            if (t == t0 + W) c0 = C;
+            const auto ts0 = std::chrono::steady_clock::now();
+            for (; hi < NH && h_tick[hi] == t; hi++) {
+                if (!calls) continue;
+                const NFGUID g(gh[h_obj[hi]], gd[h_obj[hi]]);
+                g_now = h_time[hi];
+                if (h_op[hi] == 1) sm->AddSchedule(g, kname[h_kind[hi]], hb, h_int[hi], h_cnt[hi]);
+                else if (h_op[hi] == 2) sm->RemoveSchedule(g, kname[h_kind[hi]]);
+                else sm->RemoveSchedule(g);
+                ncalls += t >= t0 + W;
+            }
+            for (; xi < NX && x_tick[xi] == t; xi++) {
+                if (!calls) continue;
+                const NFGUID g(gh[x_obj[xi]], gd[x_obj[xi]]);
+                if (x_pid[xi] < NI) km->SetPropertyInt(g, pname[x_pid[xi]], (int64_t)x_bits[xi]);
+                else km->SetPropertyFloat(g, pname[x_pid[xi]], bitsd(x_bits[xi]));
+                ncalls += t >= t0 + W;
+            }
+            const auto ts1 = std::chrono::steady_clock::now();
+            g_now = tick_time[t];
+            for (auto* m : all) m->Execute();
+            const auto ts2 = std::chrono::steady_clock::now();
+            if (t >= t0 + W) {
+                st.push_back(kernel.gpu_.LastFrameStats());
+                call_ms.push_back(std::chrono::duration<double, std::milli>(ts1 - ts0).count());
+                frame_ms.push_back(std::chrono::duration<double, std::milli>(ts2 - ts0).count());
+            }
         }
-        for (; xi < NX && x_tick[xi] == t; xi++) {
-            if (!calls) continue;
-            const NFGUID g(gh[x_obj[xi]], gd[x_obj[xi]]);
-            if (x_pid[xi] < NI) km->SetPropertyInt(g, pname[x_pid[xi]], (int64_t)x_bits[xi]);
-            else km->SetPropertyFloat(g, pname[x_pid[xi]], bitsd(x_bits[xi]));
-            ncalls += t >= W;
-        }
-        const auto t1 = std::chrono::steady_clock::now();
-        g_now = tick_time[t];
-        for (auto* m : all) m->Execute();
-        const auto t2 = std::chrono::steady_clock::now();
-        if (t >= W) {
-            st.push_back(kernel.gpu_.LastFrameStats());
-            call_ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
-            frame_ms.push_back(std::chrono::duration<double, std::milli>(t2 - t0).count());
-        }
+        auto med = [](std::vector<double> v) {
+            std::sort(v.begin(), v.end());
+            return v.empty() ? 0.0 : v[v.size() / 2];
+        };
+        auto medf = [&](double nfgpu::NFGPUKernelModule::FrameStats::*m) {
+            std::vector<double> v;
+            for (auto& s : st) v.push_back(s.*m);
+            return med(v);
+        };
+        const nfk_summary& s = kernel.gpu_.LastSummary();
+        const double kf = K ? (double)K : 1.0;
+        char buf[4096];
+        snprintf(buf, sizeof buf,
+                 "{\"adapter_frame_ms\": %.3f, \"entities\": %lld, \"entity_ticks_per_s\": %.4g, \"calls_per_frame\": %lld, "
+                 "\"phases_ms\": {\"calls\": %.3f, \"device\": %.3f, \"functors\": %.3f, \"events_read\": %.3f, "
+                 "\"deliver\": %.3f, \"functor_calls\": %.3f, \"plugin_execute\": %.3f, \"gather\": %.3f}, "
+                 "\"per_frame\": {\"fired\": %lld, \"prop_events\": %lld, \"rec_events\": %lld, \"messages\": %lld}, "
+                 "\"received_per_frame\": {\"heartbeats\": %.0f, \"common_prop\": %.0f, \"common_rec\": %.0f, \"aoi_prop\": %.0f, "
+                 "\"aoi_rec\": %.0f, \"recipients\": %.0f, \"per_object_callbacks\": %.0f, \"hp_kills\": %.0f}, "
+                 "\"aoi\": {\"device_list_calls\": %lld, \"host_getbroadcastobject_calls_for_device_events\": %lld}, "
+                 "\"mirror\": {\"lazy_syncs_per_frame\": %.1f, \"chain_callbacks_per_frame\": %.0f}, "
+                 "\"frames\": %d, \"warmup\": %d",
+                 med(frame_ms), (long long)N, (double)N / (med(frame_ms) * 1e-3), (long long)(K ? ncalls / K : 0),
+                 med(call_ms), medf(&nfgpu::NFGPUKernelModule::FrameStats::device),
+                 medf(&nfgpu::NFGPUKernelModule::FrameStats::functors), medf(&nfgpu::NFGPUKernelModule::FrameStats::events_read),
+                 medf(&nfgpu::NFGPUKernelModule::FrameStats::deliver), medf(&nfgpu::NFGPUKernelModule::FrameStats::calls),
+                 medf(&nfgpu::NFGPUKernelModule::FrameStats::total), medf(&nfgpu::NFGPUKernelModule::FrameStats::gather),
+                 (long long)s.n_fired, (long long)s.n_prop_events, (long long)s.n_rec_events, (long long)s.n_msgs,
+                 (C.hb - c0.hb) / kf, (C.prop - c0.prop) / kf, (C.rec - c0.rec) / kf, (C.aoi_prop - c0.aoi_prop) / kf,
+                 (C.aoi_rec - c0.aoi_rec) / kf, (C.rcpt - c0.rcpt) / kf, (C.obj_cb - c0.obj_cb) / kf, (C.kills - c0.kills) / kf,
+                 (long long)kernel.AOIDeviceCalls(), (long long)kernel.AOIHostDeviceCalls(),
+                 (kernel.MirrorSyncs() - syncs0) / kf, (kernel.ChainCallbacks() - chain0) / kf, K, W);
+        return buf;
+    };
+    std::string line = run(0);
+    std::string npc_line;
+    if (npc) {
+        // NFCNPCRefreshModule::OnObjectClassEvent at COE_CREATE_HASDATA (NFCNPCRefreshModule.cpp:104), for
+        // the NPCs this server already holds
+        const auto tc = std::chrono::steady_clock::now();
+        int64_t n_npc = 0;
+        for (int64_t o = 0; o < N; o++)
+            if (cl[o] == 0) {
+                km->AddPropertyCallBack(NFGUID(gh[o], gd[o]), "HP", &C, &Counters::OnObjectHPEvent);
+                n_npc++;
+            }
+        const double reg_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tc).count();
+        npc_line = run(W + K);
+        char tail[160];
+        snprintf(tail, sizeof tail, ", \"npcs_watched\": %lld, \"register_s\": %.2f}", (long long)n_npc, reg_s);
+        npc_line += tail;
     }
-    auto med = [](std::vector<double> v) {
-        std::sort(v.begin(), v.end());
-        return v.empty() ? 0.0 : v[v.size() / 2];
-    };
-    auto medf = [&](double nfgpu::NFGPUKernelModule::FrameStats::*m) {
-        std::vector<double> v;
-        for (auto& s : st) v.push_back(s.*m);
-        return med(v);
-    };
-    const nfk_summary& s = kernel.gpu_.LastSummary();
-    const double kf = K ? (double)K : 1.0;
-    printf("{\"adapter_frame_ms\": %.3f, \"entities\": %lld, \"entity_ticks_per_s\": %.4g, \"calls_per_frame\": %lld, "
-           "\"phases_ms\": {\"calls\": %.3f, \"device\": %.3f, \"functors\": %.3f, \"events_read\": %.3f, "
-           "\"deliver\": %.3f, \"functor_calls\": %.3f, \"plugin_execute\": %.3f, \"gather\": %.3f}, "
-           "\"per_frame\": {\"fired\": %lld, \"prop_events\": %lld, \"rec_events\": %lld, \"messages\": %lld}, "
-           "\"received_per_frame\": {\"heartbeats\": %.0f, \"common_prop\": %.0f, \"common_rec\": %.0f, \"aoi_prop\": %.0f, "
-           "\"aoi_rec\": %.0f, \"recipients\": %.0f, \"per_object_callbacks\": %.0f}, "
-           "\"aoi\": {\"device_list_calls\": %lld, \"host_getbroadcastobject_calls_for_device_events\": %lld}, "
-           "\"mirror\": {\"lazy_syncs_per_frame\": %.1f, \"chain_callbacks\": %lld}, "
-           "\"build_s\": %.1f, \"host_objects_s\": %.1f, \"frames\": %d, \"warmup\": %d, \"mode\": \"%s\"}\n",
-           med(frame_ms), (long long)N, (double)N / (med(frame_ms) * 1e-3), (long long)(K ? ncalls / K : 0),
-           med(call_ms), medf(&nfgpu::NFGPUKernelModule::FrameStats::device),
-           medf(&nfgpu::NFGPUKernelModule::FrameStats::functors), medf(&nfgpu::NFGPUKernelModule::FrameStats::events_read),
-           medf(&nfgpu::NFGPUKernelModule::FrameStats::deliver), medf(&nfgpu::NFGPUKernelModule::FrameStats::calls),
-           medf(&nfgpu::NFGPUKernelModule::FrameStats::total), medf(&nfgpu::NFGPUKernelModule::FrameStats::gather),
-           (long long)s.n_fired, (long long)s.n_prop_events, (long long)s.n_rec_events, (long long)s.n_msgs,
-           (C.hb - c0.hb) / kf, (C.prop - c0.prop) / kf, (C.rec - c0.rec) / kf, (C.aoi_prop - c0.aoi_prop) / kf,
-           (C.aoi_rec - c0.aoi_rec) / kf, (C.rcpt - c0.rcpt) / kf, (C.obj_cb - c0.obj_cb) / kf,
-           (long long)kernel.AOIDeviceCalls(), (long long)kernel.AOIHostDeviceCalls(),
-           (kernel.MirrorSyncs() - syncs0) / kf, (long long)kernel.ChainCallbacks(), build_s, host_build_s, K, W,
-           mode == 1 ? "tutorial3" : calls ? "config1-with-calls" : "config1");
+    char tail[200];
+    snprintf(tail, sizeof tail, ", \"build_s\": %.1f, \"host_objects_s\": %.1f, \"mode\": \"%s\"", build_s, host_build_s,
+             mode == 1 ? "tutorial3" : calls ? "config1-with-calls" : "config1");
+    line += tail;
+    if (npc) line += ", \"npc_hp\": " + npc_line;
+    printf("%s}\n", line.c_str());
     fflush(stdout);
     _exit(0);  // (static destructors: NFMemoryCounter's static map dies before the modules' objects)
 }

@@ -28,6 +28,20 @@
 //     FindRecord(self, r)->SetInt / AddRow / Remove), read-modify-write Sets included; schedule
 //     calls; DestroyObject and CreateObject after start.
 //
+// A workload's `logic_mode` bits (0 when absent) add:
+//   1  cross-object reads in the heartbeat functors: after its effect each functor reads another object's
+//      HP / X (NFIKernelModule::GetPropertyInt / Float) and MP through that object (GetObject(peer)->
+//      GetPropertyInt), and its own HP, which a later schedule name of the same object may write —
+//      NFCScheduleModule::Execute runs the functors object by object in NFGUID order (SM:52-80), so the
+//      reference's read sees the Sets of the functors before it in the walk and none after;
+//   2  (GPU plugin) NFGPUKernelModule::SetWalkOrderReads(true): those reads answered in walk order;
+//   4  components (NFIComponent, run by NFCObject::Execute in NFCKernelModule::Execute's walk, KM:88-95,
+//      NFCObject.cpp:42-47) that destroy their own object (deferred to the next Execute through
+//      mtDeleteSelfList, KM:275-279 / KM:1434) or another object (at once);
+//   8  NFCNPCRefreshModule's callbacks only (NFCNPCRefreshModule.cpp:98-105): every NPC gets
+//      AddPropertyCallBack(self, "HP", ...) at creation and nothing else is watched — every NPC's HP
+//      Sets fire callbacks, no record callbacks, no managers handed out.
+//
 // Logged per frame t: per-object property and record callbacks with the phase they fired in (0 =
 // the window's calls, 1 = Execute), the heartbeat functors, Tutorial3's callback lines, the kills and
 // OnDeadDestroyHeart calls, and every
@@ -39,7 +53,9 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -97,13 +113,19 @@ struct Logic {
     std::vector<int32_t> fi_obj, fi_kind, fi_rem;
     std::string t3;  // Tutorial3's callback lines
     std::string kills, dead;  // OnObjectHPEvent's kills, OnDeadDestroyHeart's calls
+    std::string comp;         // the components' DestroyObject calls and the objects gone after Execute
+    // (logic_mode 1) the functors' reads: reader, kind, peer, peer's HP / X / MP (through the object), own HP
+    std::vector<int32_t> xr_obj, xr_kind, xr_peer;
+    std::vector<uint64_t> xr_hp, xr_x, xr_mp, xr_self;
+    int64_t mode = 0;
     void clear() {
-        for (auto* v : {&pc_phase, &pc_obj, &pc_pid, &rc_phase, &rc_obj, &fi_obj, &fi_kind, &fi_rem}) v->clear();
+        for (auto* v : {&pc_phase, &pc_obj, &pc_pid, &rc_phase, &rc_obj, &fi_obj, &fi_kind, &fi_rem, &xr_obj, &xr_kind, &xr_peer}) v->clear();
         rc_rrc.clear();
-        for (auto* v : {&pc_old, &pc_new, &rc_old, &rc_new}) v->clear();
+        for (auto* v : {&pc_old, &pc_new, &rc_old, &rc_new, &xr_hp, &xr_x, &xr_mp, &xr_self}) v->clear();
         t3.clear();
         kills.clear();
         dead.clear();
+        comp.clear();
     }
     int ObjOf(const NFGUID& g) const {
         auto it = obj.find(g);
@@ -144,7 +166,14 @@ struct Logic {
         dead += std::to_string(ObjOf(self)) + " " + std::to_string(nCount) + "\n";
         return 0;
     }
-    void Watch(const NFGUID& g) {
+    void Watch(const NFGUID& g, bool npc) {
+        if (mode & 8) {  // NFCNPCRefreshModule.cpp:104: the NPCs' HP, nothing else
+            if (npc) {
+                km->AddPropertyCallBack(g, "HP", this, &Logic::OnObjProp);
+                km->AddPropertyCallBack(g, "HP", this, &Logic::OnObjectHPEvent);
+            }
+            return;
+        }
         for (const char* n : {"HP", "MP", "X", "TargetX", "Gold", "Level"}) km->AddPropertyCallBack(g, n, this, &Logic::OnObjProp);
         km->AddPropertyCallBack(g, "HP", this, &Logic::OnObjectHPEvent);
         km->AddRecordCallBack(g, "rec0", this, &Logic::OnObjRecord);
@@ -190,6 +219,17 @@ struct Logic {
         return 0;
     }
     NFGUID t3_self;
+    // (logic_mode 1) a functor's reads of another object and of itself, after its own effect
+    void CrossReads(const NFGUID& self, const std::string& name, const NFGUID& peer) {
+        xr_obj.push_back(ObjOf(self));
+        xr_kind.push_back(kid.at(name));
+        xr_peer.push_back(ObjOf(peer));
+        xr_hp.push_back((uint64_t)km->GetPropertyInt(peer, "HP"));
+        xr_x.push_back(dbits(km->GetPropertyFloat(peer, "X")));
+        NF_SHARE_PTR<NFIObject> po = km->GetObject(peer);
+        xr_mp.push_back(po ? (uint64_t)po->GetPropertyInt("MP") : 0);
+        xr_self.push_back((uint64_t)km->GetPropertyInt(self, "HP"));
+    }
     bool Tutorial3(int scene) {  // HelloWorld3Module::AfterInit (:68-100)
         km->AddClassCallBack(NFrame::Player::ThisName(), this, &Logic::OnClassEvent);
         NF_SHARE_PTR<NFIObject> o = km->CreateObject(NFGUID(0, 10), scene, 0, NFrame::Player::ThisName(), "", NFCDataList());
@@ -206,6 +246,24 @@ struct Logic {
     }
 };
 
+// (logic_mode 4) NFCComponentManager::Execute runs it in NFCKernelModule::Execute's object walk
+struct DestroyComponent : public NFIComponent {
+    DestroyComponent(Logic* l, const NFGUID& self, const NFGUID& victim, int at)
+        : NFIComponent(self, "DestroyComponent"), L(l), me(self), victim(victim), at(at) {}
+    bool Execute() override {
+        if (L->frame != at || done) return true;
+        done = true;
+        const bool ok = L->km->DestroyObject(victim);  // the reference defers its own object (KM:275)
+        L->comp += "destroy " + std::to_string(L->ObjOf(me)) + " " + std::to_string(L->ObjOf(victim)) + " " +
+                   std::to_string(ok ? 1 : 0) + "\n";
+        return true;
+    }
+    Logic* L;
+    NFGUID me, victim;
+    int at;
+    bool done = false;
+};
+
 int main(int argc, char** argv) {
     if (argc != 3) return 2;
     nfio_file wf;
@@ -220,6 +278,8 @@ int main(int argc, char** argv) {
     };
     int64_t* cfg = (int64_t*)A("cfg")->data;
     const int64_t N = cfg[0], NI = cfg[1], NF = cfg[2], NC = cfg[3], NK = cfg[4], NR = cfg[5], NS = cfg[6], NT = cfg[7];
+    nfio_arr* lma = nfio_get(&wf, "logic_mode");
+    const int64_t mode = lma ? ((int64_t*)lma->data)[0] : 0;
     nfio_arr* noa = nfio_get(&wf, "n_oprops");
     if ((noa && ((int64_t*)noa->data)[0]) || (nfio_get(&wf, "sw_tick") && A("sw_tick")->shape[0] > 0) || NR != 1) {
         fprintf(stderr, "logic_session: int/float properties, one record, no SwitchScene\n");
@@ -272,9 +332,13 @@ int main(int argc, char** argv) {
         kernel.gpu_.AddHeartBeatProgram(kname[k], std::vector<nfk_op>(ops + k * OPK, ops + k * OPK + nops[k]),
                                         pname, rname);
 #endif
+#ifndef LOGIC_REF
+    if (mode & 2) kernel.gpu_.SetWalkOrderReads(true);
+#endif
     for (auto* m : all) m->Awake();
     for (auto* m : all) m->Init();
     Logic L;
+    L.mode = mode;
     L.km = &kernel;
     L.sm = &sched;
     L.em = &events;
@@ -335,13 +399,49 @@ int main(int argc, char** argv) {
     if (born)
         for (int64_t o = 0; o < N; o++) alive[o] = born[o] < 0;
     for (int64_t o = 0; o < N; o++)
-        if (alive[o]) L.Watch(NFGUID(gh[o], gd[o]));
+        if (alive[o]) L.Watch(NFGUID(gh[o], gd[o]), cl[o] == 0);
+    nfio_arr* dta0 = nfio_get(&wf, "d_tick");
+    if (mode & 4) {  // components on objects that live from the start and that the workload never destroys
+        std::vector<uint8_t> keep(N, 1);
+        if (dta0)
+            for (int64_t i = 0; i < (int64_t)dta0->shape[0]; i++) keep[((int32_t*)A("d_obj")->data)[i]] = 0;
+        for (int64_t o = 0; o < N; o++)
+            if (!alive[o]) keep[o] = 0;
+        for (int64_t o = 0; o + 20 < N; o++) {
+            const NFGUID g(gh[o], gd[o]);
+            NFGUID victim;
+            int at = -1;
+            if (o % 61 == 3 && keep[o]) {
+                victim = g;  // itself
+                at = 1 + (int)((o / 61) % std::max<int64_t>(NT - 2, 1));
+            } else if (o % 61 == 10 && keep[o] && keep[o + 20]) {
+                victim = NFGUID(gh[o + 20], gd[o + 20]);
+                at = 2 + (int)((o / 61) % std::max<int64_t>(NT - 3, 1));
+            }
+            if (at < 0) continue;
+            NF_SHARE_PTR<NFIObject> ob = km->GetObject(g);
+            ob->GetComponentManager()->AddComponent("DestroyComponent", NF_SHARE_PTR<NFIComponent>(new DestroyComponent(&L, g, victim, at)));
+        }
+    }
 
     // the heartbeat functor: the effect program through NFIKernelModule on the reference; on the
     // device the program ran before the functor, which only logs
     std::function<int(const NFGUID&, const std::string&, const float, const int)> heartbeat =
         [&](const NFGUID& self, const std::string& name, const float, const int nCount) -> int {
         L.Fired(self, name, nCount);
+        struct XR {  // (logic_mode 1) the reads after the functor's effect, either way it is made
+            Logic& L;
+            const NFGUID& self;
+            const std::string& name;
+            int64_t N;
+            const int64_t *gh, *gd;
+            ~XR() {
+                if (!(L.mode & 1)) return;
+                const int o = L.ObjOf(self);
+                const int64_t q = (o * 7 + 3) % N;  // (random NFGUIDs: the peer is before or after it in the walk)
+                L.CrossReads(self, name, NFGUID(gh[q], gd[q]));
+            }
+        } xr{L, self, name, N, gh, gd};
 #ifdef LOGIC_REF
         const int k = L.kid.at(name);
         for (int i = 0; i < nops[k]; i++) {
@@ -443,6 +543,13 @@ int main(int argc, char** argv) {
     int32_t* d_tick = ND ? (int32_t*)dta->data : nullptr;
     int32_t* d_obj = ND ? (int32_t*)A("d_obj")->data : nullptr;
 
+    // (LOGIC_TIMING=1: seconds per phase on stderr)
+    const bool timing = getenv("LOGIC_TIMING") != nullptr;
+    double tm[4] = {0, 0, 0, 0};
+    auto clk = [] { return std::chrono::steady_clock::now(); };
+    auto since = [](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+    };
     nfio_writer w;
     if (nfio_wopen(&w, argv[2])) return 2;
     {
@@ -451,6 +558,7 @@ int main(int argc, char** argv) {
     }
     int64_t xi = 0, hi = 0, di = 0, ri = 0;
     for (int t = 0; t < NT; t++) {
+        auto tp = clk();
         L.clear();
         L.frame = t;
         L.phase = 0;
@@ -460,7 +568,7 @@ int main(int argc, char** argv) {
                 if (born[o] == t) {
                     if (!create(o)) return 8;
                     alive[o] = 1;
-                    L.Watch(NFGUID(gh[o], gd[o]));
+                    L.Watch(NFGUID(gh[o], gd[o]), cl[o] == 0);
                 }
         events.DoEvent(L.t3_self, NFEventDefine(1), NFCDataList() << (NFINT64)(1000 + t) << ("s" + std::to_string(t)));
         for (; hi < NH && h_tick[hi] == t; hi++) {
@@ -514,7 +622,17 @@ int main(int argc, char** argv) {
         }
         g_now = tick_time[t];
         L.phase = 1;
+        tm[0] += since(tp);
+        tp = clk();
         for (auto* m : all) m->Execute();
+        tm[1] += since(tp);
+        tp = clk();
+        if (mode & 4)  // the objects the components destroyed (their own: at the next Execute)
+            for (int64_t o = 0; o < N; o++)
+                if (alive[o] && !km->GetObject(NFGUID(gh[o], gd[o]))) {
+                    alive[o] = 0;
+                    L.comp += "gone " + std::to_string(o) + "\n";
+                }
         char nm[48];
 #define PUT(pfx, s, code, vec, es) snprintf(nm, sizeof nm, "%s_t%d_%s", pfx, t, s); nfio_put1(&w, nm, code, vec.data(), vec.size(), es);
         PUT("pc", "phase", NFIO_I32, L.pc_phase, 4);
@@ -535,6 +653,15 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> kl(L.kills.begin(), L.kills.end()), dl(L.dead.begin(), L.dead.end());
         PUT("k", "kills", NFIO_U8, kl, 1);
         PUT("k", "dead", NFIO_U8, dl, 1);
+        std::vector<uint8_t> cp(L.comp.begin(), L.comp.end());
+        PUT("k", "comp", NFIO_U8, cp, 1);
+        PUT("xr", "obj", NFIO_I32, L.xr_obj, 4);
+        PUT("xr", "kind", NFIO_I32, L.xr_kind, 4);
+        PUT("xr", "peer", NFIO_I32, L.xr_peer, 4);
+        PUT("xr", "hp", NFIO_U64, L.xr_hp, 8);
+        PUT("xr", "x", NFIO_U64, L.xr_x, 8);
+        PUT("xr", "mp", NFIO_U64, L.xr_mp, 8);
+        PUT("xr", "self", NFIO_U64, L.xr_self, 8);
         // every object's properties through the host object and through NFIKernelModule, and its
         // rec0 used rows' int cells through the host record
         std::vector<uint64_t> vh((size_t)NP * N, 0), vk((size_t)NP * N, 0), rv((size_t)N * cols * rows, 0), ru(N, 0);
@@ -562,7 +689,9 @@ int main(int argc, char** argv) {
         PUT("r", "cells", NFIO_U64, rv, 8);
         PUT("r", "used", NFIO_U64, ru, 8);
         PUT("r", "kcells", NFIO_U64, rk, 8);
+        tm[2] += since(tp);
     }
+    if (timing) fprintf(stderr, "logic_session: window calls %.2f s, Execute %.2f s, logging %.2f s\n", tm[0], tm[1], tm[2]);
     nfio_wclose(&w);
     fflush(stdout);
     _exit(0);  // (static destructors: NFMemoryCounter's static map dies before the modules' objects)

@@ -16,7 +16,12 @@ properties with per-object callbacks, DoEvent).  Compared frame by frame:
   and a record op's rows in order (SM:52-80);
 * with Poison able to kill (workload lethal_poison: HP -> 0 -> 3 within one program), the kills of an
   NFCNPCRefreshModule::OnObjectHPEvent-style callback (newVar <= 0, NFCNPCRefreshModule.cpp:113-124)
-  and the OnDeadDestroyHeart heartbeats it adds: the same."""
+  and the OnDeadDestroyHeart heartbeats it adds: the same;
+* (logic_mode, tests/cpp/logic_session.cpp) functors reading other objects' program-written properties
+  (the reference's walk order, SM:52-80: with NFGPUKernelModule::SetWalkOrderReads equal, without it the
+  documented divergence — the frame's values — asserted exactly); components that destroy their own
+  object (deferred to the next Execute, KM:275-279) or another one (at once); NFCNPCRefreshModule's own
+  callback pattern (an HP callback on every NPC, NFCNPCRefreshModule.cpp:104) at 20k objects."""
 import os
 import subprocess
 
@@ -30,14 +35,16 @@ GPU_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "logic_session")
 REF_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "logic_session_ref")
 
 
-def _world(seed, n_obj=1200, n_ticks=12, lethal=False, set_ops=False):
-    w = workload.make_world(n_obj=n_obj, n_scenes=2, groups_per_scene=3, players_per_group=4, n_ticks=n_ticks,
+def _world(seed, n_obj=1200, n_ticks=12, lethal=False, set_ops=False, logic_mode=0, groups_per_scene=3):
+    w = workload.make_world(n_obj=n_obj, n_scenes=2, groups_per_scene=groups_per_scene, players_per_group=4, n_ticks=n_ticks,
                             tick_ms=1000, seed=seed, ext_frac=0.05, host_ops=True, rmw_frac=0.02, spawn_frac=0.02,
                             destroy_frac=0.02, records=True, rec_rows=16, rec_float_op=False, rec_set_frac=0.03,
                             rec_set_float=False, rec_row_frac=0.02, lethal_poison=lethal, set_ops=set_ops)
     # an int-only record (the reference's NFCRecord::SetFloat cannot hold an f64 cell, test_oracle.py):
     # the charge column becomes an int column with the same bits; no program touches it
     w["rec_ctype"] = np.zeros_like(w["rec_ctype"])
+    if logic_mode:
+        w["logic_mode"] = np.array([logic_mode], np.int64)
     return w
 
 
@@ -124,16 +131,62 @@ def test_logic_session_reference_kills_within_a_frame(tmp_path):
     assert kills > 20 and hidden > 20, (kills, hidden)
 
 
+def _lines(out, key):
+    return bytes(np.asarray(out[key], np.uint8)).decode().splitlines()
+
+
+def test_logic_session_reference_components_destroy(tmp_path):
+    """CPU: components (NFIComponent, run in NFCKernelModule::Execute's object walk, KM:88-95) on the
+    reference's own modules: DestroyObject of the component's own object is deferred to the next Execute
+    (KM:275-279: DestroySelf puts it on mtDeleteSelfList, applied at KM:76-84), of another object applied at
+    once — the sequence the adapter must reproduce (its walk over a copy of the objects with components,
+    ADVICE r5)."""
+    if not os.path.exists(REF_EXE):
+        pytest.skip("logic_session_ref not built (needs /root/reference at build time)")
+    w = _world(75, n_obj=1200, logic_mode=4)
+    out = _run(REF_EXE, w, tmp_path, "ref")
+    nt = int(w["cfg"][7])
+    gone_at = {}
+    for t in range(nt):
+        for ln in _lines(out, f"k_t{t}_comp"):
+            if ln.startswith("gone "):
+                gone_at[int(ln.split()[1])] = t
+    n_self = n_other = 0
+    for t in range(nt):
+        for ln in _lines(out, f"k_t{t}_comp"):
+            if not ln.startswith("destroy "):
+                continue
+            me, victim, ok = (int(x) for x in ln.split()[1:])
+            assert ok == 1
+            if me == victim:  # deferred: gone after the NEXT Execute
+                n_self += 1
+                assert gone_at.get(victim) == (t + 1 if t + 1 < nt else None), ln
+            else:
+                n_other += 1
+                assert gone_at.get(victim) == t, ln
+    assert n_self >= 5 and n_other >= 5, (n_self, n_other)
+
+
 @pytest.mark.gpu
 # seed 74: the set_ops programs (assignments, guards against 0 and against another int property)
-@pytest.mark.parametrize("seed,lethal,set_ops", [(71, False, False), (72, False, False), (73, True, False),
-                                                 (74, False, True)])
-def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, seed, lethal, set_ops):
+# seed 75: logic_mode 1 | 2 | 4 — cross-object functor reads answered in walk order, components destroying
+# objects (their own deferred), with lethal Poison
+@pytest.mark.parametrize("seed,lethal,set_ops,mode", [(71, False, False, 0), (72, False, False, 0), (73, True, False, 0),
+                                                      (74, False, True, 0), (75, True, False, 7)])
+def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, seed, lethal, set_ops, mode):
     if not (os.path.exists(GPU_EXE) and os.path.exists(REF_EXE)):
         pytest.skip("logic_session not built (needs /root/reference at build time)")
-    w = _world(seed, lethal=lethal, set_ops=set_ops)
+    w = _world(seed, lethal=lethal, set_ops=set_ops, logic_mode=mode)
     got, ref = _run(GPU_EXE, w, tmp_path, "gpu"), _run(REF_EXE, w, tmp_path, "ref")
     nt = int(w["cfg"][7])
+    if mode:
+        n_xr = 0
+        for t in range(nt):
+            assert _lines(got, f"k_t{t}_comp") == _lines(ref, f"k_t{t}_comp"), t
+            for k in ("obj", "kind", "peer", "hp", "x", "mp", "self"):
+                np.testing.assert_array_equal(got[f"xr_t{t}_{k}"], ref[f"xr_t{t}_{k}"], err_msg=f"xr_t{t}_{k}")
+            n_xr += len(ref[f"xr_t{t}_obj"])
+        assert n_xr > 1000 and sum(len(_lines(ref, f"k_t{t}_comp")) for t in range(nt)) > 10
     assert bytes(np.asarray(got["t3_setup"], np.uint8)) == bytes(np.asarray(ref["t3_setup"], np.uint8))
     n_obj_cb = n_rec_cb = 0
     n_kills = 0
@@ -161,3 +214,96 @@ def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, see
                 n_rec_cb += len(g[0]) + len(g[1])
     assert n_obj_cb > 1000 and n_rec_cb > 100, (n_obj_cb, n_rec_cb)
     assert n_kills > 20 or not lethal, n_kills
+
+
+@pytest.mark.gpu
+def test_logic_session_cross_object_reads_divergence(gpu_available, tmp_path):
+    """Without walk-order reads (the plugin's default) a heartbeat functor's read of another object's
+    program-written property sees the frame's value — every object's device programs ran before the host
+    functors — where the reference's sees it as of its place in the walk (objects in NFGUID order,
+    SM:52-80).  Asserted exactly: every read equals that object's value after the frame (read back through
+    NFIKernelModule at the frame's end), and the reads differ from the reference's exactly where the peer
+    (or, for its own HP, a later schedule name of the reader) made a Set after the reader's place."""
+    if not (os.path.exists(GPU_EXE) and os.path.exists(REF_EXE)):
+        pytest.skip("logic_session not built (needs /root/reference at build time)")
+    w = _world(76, lethal=True, logic_mode=1)
+    got, ref = _run(GPU_EXE, w, tmp_path, "gpu"), _run(REF_EXE, w, tmp_path, "ref")
+    nt, n = int(w["cfg"][7]), len(w["guid_head"])
+    hp, x, mp = workload.PID["HP"], workload.PID["X"], workload.PID["MP"]
+    n_diff = n_later = 0
+    for t in range(nt):
+        vk = np.asarray(got[f"v_t{t}_kernel"]).reshape(-1, n)
+        peer = np.asarray(got[f"xr_t{t}_peer"])
+        obj = np.asarray(got[f"xr_t{t}_obj"])
+        np.testing.assert_array_equal(got[f"xr_t{t}_peer"], ref[f"xr_t{t}_peer"])
+        live = peer < n  # (the Tutorial3 object is never a peer)
+        alive = vk[workload.PID["MAXHP"], peer[live]] != 0
+        for k, p in (("hp", hp), ("x", x), ("mp", mp)):
+            g = np.asarray(got[f"xr_t{t}_{k}"])[live]
+            np.testing.assert_array_equal(g[alive], vk[p, peer[live][alive]], err_msg=f"xr_t{t}_{k}")
+        np.testing.assert_array_equal(np.asarray(got[f"xr_t{t}_self"]), vk[hp, obj], err_msg=f"xr_t{t}_self")
+        d = np.asarray(got[f"xr_t{t}_hp"]) != np.asarray(ref[f"xr_t{t}_hp"])
+        n_diff += int(d.sum())
+        # a peer BEFORE the reader in NFGUID order has made all its Sets in the reference too: equal
+        gk = lambda o: (np.asarray(w["guid_head"])[o], np.asarray(w["guid_data"])[o])
+        before = np.array([gk(p) < gk(o) for p, o in zip(peer, obj)], bool)
+        assert not (d & before).any(), t
+        n_later += int((~before).sum())
+    assert n_diff > 20 and n_later > 100, (n_diff, n_later)
+
+
+GOLDEN_NPC = os.path.join(ROOT, "tests", "golden", "logic_npc20k.json")
+
+
+def _npc20k_world():
+    """NFCNPCRefreshModule's callback pattern at 20k objects: an HP callback (and its kill logic) on every
+    NPC, nothing else watched, lethal Poison (tests/golden/gen_logic_golden.py)"""
+    return _world(77, n_obj=20000, lethal=True, logic_mode=8, groups_per_scene=64)
+
+
+def logic_digests(out, nt):
+    """per frame: sha256 of every logged array (the fired list as sorted triples), for a fixture of the
+    reference's run that is too slow to repeat on every GPU run (~4 min of the reference's modules)"""
+    import hashlib
+    d = {}
+    for t in range(nt):
+        for k in sorted(out):
+            if not k.startswith(("pc_t%d_" % t, "rc_t%d_" % t, "k_t%d_" % t, "v_t%d_" % t, "r_t%d_" % t, "t3_t%d_" % t)):
+                continue
+            d[k] = hashlib.sha256(np.ascontiguousarray(out[k]).tobytes()).hexdigest()
+        fi = np.array(sorted(zip(*(np.asarray(out[f"fi_t{t}_{c}"], np.int64) for c in ("obj", "kind", "rem")))),
+                      np.int64)
+        d[f"fi_t{t}"] = hashlib.sha256(fi.tobytes()).hexdigest()
+        d[f"n_pc_t{t}"] = int(len(out[f"pc_t{t}_obj"]))
+    return d
+
+
+def workload_digest(w):
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(w):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(w[k]).tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.gpu
+def test_logic_session_npc_hp_callbacks_20k(gpu_available, tmp_path):
+    """The reference's own per-NPC callback pattern (NFCNPCRefreshModule.cpp:98-105: AddPropertyCallBack(self,
+    HP) on every NPC at creation, its OnObjectHPEvent kill logic) at 20k objects through the GPU plugin, equal
+    frame by frame to the reference's modules (per-Set HP callbacks in the walk's order, kills, the fired
+    lists, every object's properties and record cells through the host objects and NFIKernelModule):
+    compared with digests of the reference's run (tests/golden/logic_npc20k.json, made by
+    tests/golden/gen_logic_golden.py from logic_session_ref)."""
+    if not os.path.exists(GPU_EXE):
+        pytest.skip("logic_session not built (needs /root/reference at build time)")
+    import json
+    gold = json.load(open(GOLDEN_NPC))
+    w = _npc20k_world()
+    assert workload_digest(w) == gold["workload"], "the generated workload differs from the fixture's"
+    got = _run(GPU_EXE, w, tmp_path, "gpu")
+    nt = int(w["cfg"][7])
+    dg = logic_digests(got, nt)
+    bad = [k for k in gold["digests"] if dg.get(k) != gold["digests"][k]]
+    assert not bad, bad[:10]
+    assert sum(gold["digests"][f"n_pc_t{t}"] for t in range(nt)) > 100000
