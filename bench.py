@@ -324,6 +324,7 @@ def world_from_env(gpus):
 
 
 def main():
+    t_start = time.perf_counter()
     args = parse()
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
@@ -553,23 +554,33 @@ def main():
     out["per_frame"]["message_offsets"] = ("produced at read time by k_counted_moff (nfk_outputs_get / nfk_read_*), "
                                            "outside the timed frame; the headline loop's nfk_outputs_get builds "
                                            "the dense ranks")
+    def progress(what):  # (a line on stderr per leg: the run is visibly alive between legs)
+        if rank == 0:
+            print(f"bench.py: {what} ({time.perf_counter() - t_start:.0f} s)", file=sys.stderr, flush=True)
+    progress("headline frames timed")
     if rank == 0 and world == 1 and args.config == 1 and args.host_calls == "auto":
         out["host_calls"] = host_calls_run(args, torch, kernel, workload)
+        progress("host_calls leg done")
     if rank == 0 and world == 1 and args.config == 1 and args.plugin_frame == "auto":
         out["plugin_frame"] = plugin_frame_run(args, workload)
+        progress("plugin_frame leg done")
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline(args)
+        progress("cpu_baseline leg done")
     if rank == 0 and world == 1 and args.config == 1 and args.other_configs == "auto" and not args.self_migrate:
-        out["configs"] = other_config_legs(args)
+        out["configs"] = other_config_legs(args, progress)
     if adapter is not None:
-        out["adapter_frame"] = {"config1": adapter.finish(), "config0": adapter_config0_run(args)}
+        out["adapter_frame"] = {"config1": adapter.finish(progress=progress)}
+        progress("adapter_frame config[1] leg done")
+        out["adapter_frame"]["config0"] = adapter_config0_run(args)
+        progress("adapter_frame config[0] leg done")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def other_config_legs(args):
+def other_config_legs(args, progress=lambda what: None):
     """BASELINE config[0], config[3] and config[4] as short legs of the default line: each runs
     `bench.py --config c` in its own process (same --steps / --warmup, no CPU baseline) and reports its
     throughput, frame time, dominant kernel and roofline fraction."""
@@ -586,6 +597,8 @@ def other_config_legs(args):
         except subprocess.TimeoutExpired:
             legs[f"config{c}"] = {"error": "timeout"}
             continue
+        finally:
+            progress(f"config[{c}] leg done")
         line = [x for x in r.stdout.splitlines() if x.startswith("{")]
         if r.returncode != 0 or not line:
             legs[f"config{c}"] = {"error": (r.stderr or r.stdout)[-400:]}
@@ -606,6 +619,7 @@ def other_config_legs(args):
 
 
 ADAPTER_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "adapter_bench")
+NPC_FRAMES = 8  # timed frames of the adapter leg's NPC phase (NFCNPCRefreshModule's HP callback on every NPC)
 
 
 class AdapterLeg:
@@ -628,22 +642,32 @@ class AdapterLeg:
         # (twice the frames: the same frames again with NFCNPCRefreshModule's HP callback on every NPC,
         # NFCNPCRefreshModule.cpp:104 — reported as adapter_frame.config1.npc_hp)
         w = workload.bench_world(n_obj=args.entities, groups=args.groups, players_per_group=args.players_per_group,
-                                 n_ticks=2 * (args.warmup + args.steps), tick_ms=args.tick_ms, seed=2031, ext_frac=0.05,
-                                 host_ops=True)
+                                 n_ticks=args.warmup + args.steps + 2 + NPC_FRAMES, tick_ms=args.tick_ms, seed=2031,
+                                 ext_frac=0.05, host_ops=True)
         nfio.write(wp, w)
         self.t0 = time.perf_counter()
         self.errf = open(os.path.join(self.tmp.name, "err.txt"), "w+")
-        self.proc = subprocess.Popen([ADAPTER_EXE, wp, str(args.warmup), str(args.steps), "0", "0", "1", "1"],
+        self.proc = subprocess.Popen([ADAPTER_EXE, wp, str(args.warmup), str(args.steps), "0", "0", "1", str(NPC_FRAMES)],
                                      stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=self.errf, text=True)
 
-    def finish(self, timeout=900):
+    def finish(self, timeout=900, progress=lambda what: None):
         if self.proc is None:
             return {"error": self.err}
         try:
             ready = self.proc.stdout.readline()   # (blocks until its host objects are built)
+            progress("adapter_frame config[1]: host objects built")
             self.proc.stdin.write("go\n")
             self.proc.stdin.flush()
-            out, _ = self.proc.communicate(timeout=max(60.0, timeout - (time.perf_counter() - self.t0)))
+            # (a line a minute while its frames run)
+            deadline = self.t0 + max(60.0, timeout)
+            while True:
+                try:
+                    out, _ = self.proc.communicate(timeout=max(1.0, min(60.0, deadline - time.perf_counter())))
+                    break
+                except subprocess.TimeoutExpired:
+                    if time.perf_counter() >= deadline:
+                        raise
+                    progress("adapter_frame config[1]: frames running")
             self.errf.seek(0)
             err = self.errf.read()
         except Exception as e:  # (a timeout, or the process died before it was ready)

@@ -49,6 +49,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "nfgpu.h"
@@ -428,8 +429,10 @@ public:
     // collective when no rank has a departure): the entity leaves at the start of the frame after the
     // one its SwitchScene was queued before, with its state after that frame, and enters the owner's
     // world with the SwitchScene property writes.  Until its row leaves it is this module's: its
-    // heartbeats fire here with their functors and calls on it apply here (they travel with the row);
-    // another SwitchScene or a DestroyObject of it returns false (Departing).  Arrivals' schedules call
+    // heartbeats fire here with their functors and calls on it apply here (they travel with the row: a
+    // window with calls while an entity is departing applies them in a device pass of its own, their
+    // events delivered, before the rows leave); another SwitchScene or a DestroyObject of it returns
+    // false (Departing).  Arrivals' schedules call
     // the functor registered for their name with SetKindFunctor (functors cannot cross processes).
     void AttachShard(SceneShard* shard) { shard_ = shard; }
     // the departures queued so far leave now and the arrivals enter (synchronous; collective: every
@@ -660,6 +663,13 @@ private:
     SceneShard* shard_ = nullptr;
     std::map<std::string, std::pair<OBJECT_SCHEDULE_FUNCTOR, float>> kind_cb_;  // arrivals' functors
     void MigrateShard(bool sync);
+    void CallsPass();
+    // (with a shard) the objects the calls since the last device pass named, and whether one of those
+    // calls named an entity in transit (NoteCall, Depart)
+    std::unordered_set<uint64_t> touched_;
+    bool transit_calls_ = false;
+    static uint64_t TouchKey(const NFGUID& g) { return (uint64_t)g.nData64 * 0x9E3779B97F4A7C15ull ^ (uint64_t)g.nHead64; }
+    void NoteCall(const NFGUID& self);
     // cross-shard SwitchScene of an entity whose membership changed in this window (spawned, or
     // switched within the shard): deferred until the frame has applied that change (an export of
     // it would be refused, and every rank would fail the exchange)

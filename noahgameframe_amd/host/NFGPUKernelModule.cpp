@@ -473,6 +473,14 @@ bool NFGPUKernelModule::SwitchScene(const NFGUID& self, int nTargetSceneID, int 
 void NFGPUKernelModule::Depart(int o, const NFGUID& self, int scene, int group, float x, float y, float z) {
     shard_->QueueSwitch(self.nHead64, self.nData64, cls_[o], isplayer_[o], scene, group, x, y, z);
     departing_.insert(self.nHead64, self.nData64, o);
+    if (touched_.count(TouchKey(self))) transit_calls_ = true;  // (calls on it earlier in this window)
+}
+
+// (with a shard) a call on self was queued: whether it is an entity in transit (its row may leave before
+// the next device pass applies the call: MigrateShard applies the window's calls first)
+void NFGPUKernelModule::NoteCall(const NFGUID& self) {
+    if (departing_.size() && departing_.count(self.nHead64, self.nData64)) transit_calls_ = true;
+    else touched_.insert(TouchKey(self));
 }
 
 void NFGPUKernelModule::DropDeferred(const NFGUID& self) {
@@ -553,6 +561,7 @@ bool NFGPUKernelModule::SetPropertyInt(const NFGUID& self, const std::string& na
     qs_d_.push_back(self.nData64);
     qs_pid_.push_back(dev_pid_[(size_t)p]);
     qs_bits_.push_back((uint64_t)v);
+    if (shard_) NoteCall(self);
     pending_calls_++;
     return true;
 }
@@ -637,6 +646,7 @@ bool NFGPUKernelModule::SetRecordInt(const NFGUID& self, const std::string& strR
     const uint8_t f = 0;
     const uint64_t b = (uint64_t)nValue;
     if (nfk_set_records(world_, 1, &self.nHead64, &self.nData64, &rec, &row, &col, &f, &b) != NFK_OK) return false;
+    if (shard_) NoteCall(self);
     pending_calls_++;
     return true;
 }
@@ -655,6 +665,7 @@ bool NFGPUKernelModule::SetRecordFloat(const NFGUID& self, const std::string& st
     uint64_t b;
     memcpy(&b, &dwValue, 8);
     if (nfk_set_records(world_, 1, &self.nHead64, &self.nData64, &rec, &row, &col, &f, &b) != NFK_OK) return false;
+    if (shard_) NoteCall(self);
     pending_calls_++;
     return true;
 }
@@ -698,6 +709,7 @@ int NFGPUKernelModule::AddRow(const NFGUID& self, const std::string& strRecordNa
     const int32_t rec = it->second, op = 1, row = nRow;
     if (nfk_record_rows(world_, 1, &self.nHead64, &self.nData64, &rec, &op, &row, values.empty() ? nullptr : v) != NFK_OK)
         return -1;
+    if (shard_) NoteCall(self);
     pending_calls_++;
     return nRow;
 }
@@ -711,6 +723,7 @@ bool NFGPUKernelModule::RemoveRow(const NFGUID& self, const std::string& strReco
     if (!((UsedRows(self, it->second) >> nRow) & 1)) return false;
     const int32_t rec = it->second, op = 2, row = nRow;
     if (nfk_record_rows(world_, 1, &self.nHead64, &self.nData64, &rec, &op, &row, nullptr) != NFK_OK) return false;
+    if (shard_) NoteCall(self);
     pending_calls_++;
     return true;
 }
@@ -722,6 +735,7 @@ bool NFGPUKernelModule::ClearRecord(const NFGUID& self, const std::string& strRe
     if (!committed_ || it == record_id_.end() || ObjectIndex(self) < 0) return false;
     const int32_t rec = it->second, op = 3, row = 0;
     if (nfk_record_rows(world_, 1, &self.nHead64, &self.nData64, &rec, &op, &row, nullptr) != NFK_OK) return false;
+    if (shard_) NoteCall(self);
     pending_calls_++;
     return true;
 }
@@ -761,6 +775,7 @@ bool NFGPUKernelModule::SetPropertyFloat(const NFGUID& self, const std::string& 
     qs_d_.push_back(self.nData64);
     qs_pid_.push_back(dev_pid_[(size_t)p]);
     qs_bits_.push_back(bits_of(v));
+    if (shard_) NoteCall(self);
     pending_calls_++;
     return true;
 }
@@ -796,6 +811,7 @@ bool NFGPUKernelModule::SetPropertyObject(const NFGUID& self, const std::string&
     if (!committed_ || it == prop_id_.end() || props_[it->second].type != TDATA_OBJECT || ObjectIndex(self) < 0) return false;
     const int32_t pid = dev_pid_[(size_t)it->second];
     if (nfk_set_objects(world_, 1, &self.nHead64, &self.nData64, &pid, &v.nHead64, &v.nData64) != NFK_OK) return false;
+    if (shard_) NoteCall(self);
     pending_calls_++;
     return true;
 }
@@ -902,6 +918,7 @@ void NFGPUKernelModule::QueueScheduleCall(int32_t op, const NFGUID& self, int32_
     qh_t_.push_back(t);
     qh_cnt_.push_back(cnt);
     qh_now_.push_back(now);
+    if (shard_) NoteCall(self);
     pending_calls_++;
 }
 
@@ -946,6 +963,11 @@ void NFGPUKernelModule::SetKindFunctor(const std::string& name, const OBJECT_SCH
 // rows of the gather the previous Execute started (SceneShard::BeginFrame)
 void NFGPUKernelModule::MigrateShard(bool sync) {
     WaitGather();  // (the gather's workers read guids_)
+    // calls made on a departing entity since the last device pass would stay queued in the world while
+    // its row leaves (k_pack copies the device row): the window's calls are applied first, in a pass of
+    // their own with their events delivered, as the functors' calls are; windows with no call
+    // on a departing entity pay nothing (NoteCall, Depart)
+    if (transit_calls_ && pending_calls_) CallsPass();
     Flush();  // (the buffered Set calls first: call order)
     std::vector<Ticket> sent, recv;
     if (sync) check(shard_->Migrate(&sent, &recv), "SceneShard::Migrate");
@@ -982,6 +1004,8 @@ bool NFGPUKernelModule::Execute() {
     Flush();
     check(nfk_execute(world_, clock_()), "nfk_execute");
     pending_calls_ = 0;
+    touched_.clear();
+    transit_calls_ = false;
     if (shard_) WindowApplied();
     check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
     stats_.device = ms_since(t0);
@@ -1083,21 +1107,7 @@ bool NFGPUKernelModule::Execute() {
     // what the functors called takes effect in this Execute (SM:65: their Sets land at once;
     // SM:83-119: their Add/RemoveSchedule calls are applied at the end of the walk)
     t1 = std::chrono::steady_clock::now();
-    if (same_frame_ && pending_calls_) {
-        Flush();
-        check(nfk_execute_calls(world_), "nfk_execute_calls");
-        pending_calls_ = 0;
-        check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
-        TakeAddedSchedules();
-        // the second pass fires no heartbeats: only its events
-        const uint32_t w2 = ReadMask(false) & ~(NFK_READ_FIRED | NFK_READ_FIRED_GUID_ORDER);
-        if (w2) {
-            nfk_frame_host f2{};
-            check(nfk_read_frame(world_, w2, &f2), "nfk_read_frame");
-            DeliverEvents(f2);
-            for (auto& fc : frame_cb_) fc(f2, guids_.data());
-        }
-    }
+    if (same_frame_ && pending_calls_) CallsPass();
     module_sched_.Execute(clock_);  // module schedules (SM:123-176)
     // the departures queued up to now (this window's and the functors'): their tickets are
     // gathered off the world's stream while the next window's game logic runs
@@ -1105,6 +1115,26 @@ bool NFGPUKernelModule::Execute() {
     stats_.calls = ms_since(t1);
     stats_.total = ms_since(t0);
     return true;
+}
+
+// The calls queued since the last device pass applied now (nfk_execute_calls: nothing fires), their
+// events delivered
+void NFGPUKernelModule::CallsPass() {
+    Flush();
+    check(nfk_execute_calls(world_), "nfk_execute_calls");
+    pending_calls_ = 0;
+    touched_.clear();
+    transit_calls_ = false;
+    check(nfk_summary_get(world_, &summary_), "nfk_summary_get");
+    TakeAddedSchedules();
+    // the pass fires no heartbeats: only its events
+    const uint32_t w2 = ReadMask(false) & ~(NFK_READ_FIRED | NFK_READ_FIRED_GUID_ORDER);
+    if (w2) {
+        nfk_frame_host f2{};
+        check(nfk_read_frame(world_, w2, &f2), "nfk_read_frame");
+        DeliverEvents(f2);
+        for (auto& fc : frame_cb_) fc(f2, guids_.data());
+    }
 }
 
 void NFGPUKernelModule::SetFunctor(int o, int k, const OBJECT_SCHEDULE_FUNCTOR& f, float t) {

@@ -24,7 +24,8 @@
 // fires one callback per accepted HP Set of its heartbeat programs, in the walk's order; the JSON line
 // carries those frames as "npc_hp".
 //
-// usage: adapter_bench <workload.nfio> <warmup> <frames> [mode] [calls] [wait] [npc]
+// usage: adapter_bench <workload.nfio> <warmup> <frames> [mode] [calls] [wait] [npc_frames]
+//   npc_frames > 0: the NPC phase above, 2 untimed frames and npc_frames timed ones
 //   mode 0: the config[1] logic above;  1: Tutorial3's (per-object World callbacks, OnEvent Sets)
 //   calls 1: the workload's SetProperty / schedule calls between frames (mode 1 always makes its Sets)
 //   wait 1: after the host objects are built (nothing has touched the GPU yet) print {"ready": ...} and
@@ -96,7 +97,8 @@ int main(int argc, char** argv) {
     const int mode = argc > 4 ? atoi(argv[4]) : 0;
     const bool calls = mode == 1 || (argc > 5 && atoi(argv[5]) != 0);
     const bool wait = argc > 6 && atoi(argv[6]) != 0;
-    const bool npc = argc > 7 && atoi(argv[7]) != 0;
+    const int K2 = argc > 7 ? atoi(argv[7]) : 0, W2 = K2 > 0 ? 2 : 0;
+    const bool npc = K2 > 0;
     auto A = [&](const char* n) {
         nfio_arr* a = nfio_get(&wf, n);
         if (!a) {
@@ -107,7 +109,7 @@ int main(int argc, char** argv) {
     };
     int64_t* cfg = (int64_t*)A("cfg")->data;
     const int64_t N = cfg[0], NI = cfg[1], NF = cfg[2], NC = cfg[3], NK = cfg[4], NR = cfg[5], NS = cfg[6], NT = cfg[7];
-    if ((npc ? 2 : 1) * (W + K) > NT) {
+    if (W + K + W2 + K2 > NT) {
         fprintf(stderr, "workload has %lld frames, %d requested\n", (long long)NT, W + K);
         return 2;
     }
@@ -237,7 +239,7 @@ int main(int argc, char** argv) {
     int64_t xi = 0, hi = 0;
     // frames [t0, t0 + W + K): the window's calls before each, every module's Execute; the timed K frames
     // as one JSON object
-    auto run = [&](int t0) -> std::string {
+    auto run = [&](int t0, int W, int K) -> std::string {
         std::vector<nfgpu::NFGPUKernelModule::FrameStats> st;
         std::vector<double> call_ms, frame_ms;
         int64_t ncalls = 0;
@@ -306,7 +308,8 @@ int main(int argc, char** argv) {
                  (kernel.MirrorSyncs() - syncs0) / kf, (kernel.ChainCallbacks() - chain0) / kf, K, W);
         return buf;
     };
-    std::string line = run(0);
+    std::string line = run(0, W, K);
+    fprintf(stderr, "adapter_bench: %d frames timed\n", K);
     std::string npc_line;
     if (npc) {
         // NFCNPCRefreshModule::OnObjectClassEvent at COE_CREATE_HASDATA (NFCNPCRefreshModule.cpp:104), for
@@ -319,7 +322,8 @@ int main(int argc, char** argv) {
                 n_npc++;
             }
         const double reg_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tc).count();
-        npc_line = run(W + K);
+        fprintf(stderr, "adapter_bench: HP callbacks on %lld NPCs registered in %.1f s\n", (long long)n_npc, reg_s);
+        npc_line = run(W + K, W2, K2);
         char tail[160];
         snprintf(tail, sizeof tail, ", \"npcs_watched\": %lld, \"register_s\": %.2f}", (long long)n_npc, reg_s);
         npc_line += tail;

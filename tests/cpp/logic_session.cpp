@@ -573,6 +573,9 @@ int main(int argc, char** argv) {
         events.DoEvent(L.t3_self, NFEventDefine(1), NFCDataList() << (NFINT64)(1000 + t) << ("s" + std::to_string(t)));
         for (; hi < NH && h_tick[hi] == t; hi++) {
             const NFGUID g(gh[h_obj[hi]], gd[h_obj[hi]]);
+            // (not on an object a component destroyed: NFCScheduleModule::AddSchedule has no object check,
+            // SM:257, and would keep a schedule firing for an object that is gone; the plugin drops it)
+            if (!alive[h_obj[hi]]) continue;
             g_now = h_time[hi];
             if (h_op[hi] == 1) sm->AddSchedule(g, kname[h_kind[hi]], hb, h_int[hi], h_cnt[hi]);
             else if (h_op[hi] == 2) sm->RemoveSchedule(g, kname[h_kind[hi]]);

@@ -12,6 +12,10 @@
 //   gathered at the end of an Execute, rows moved at the start of the next), so an entity ticks on its
 //   source shard for one more frame after its SwitchScene; calls on entities in transit are skipped
 //   (the test compares the heartbeat functors: schedules travel with the rows)
+//   async 2: as 1, and every window also writes ATK_VALUE (no program writes it) of every entity in
+//   transit on its source shard — after its SwitchScene, and after the Execute that started its ticket
+//   gather — and writes the last value written per object as "atk_expect" (-1: none): the owner's final
+//   ATK_VALUE must equal it (the writes travel with the row)
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -32,6 +36,7 @@ static std::string cstr(const uint8_t* p) { return std::string((const char*)p, s
 int main(int argc, char** argv) {
     if (argc != 4 && argc != 5) return 2;
     const bool async = argc == 5 && atoi(argv[4]) != 0;
+    const bool transit_writes = argc == 5 && atoi(argv[4]) == 2;
     nfio_file wf;
     if (nfio_read(argv[1], &wf)) return 2;
     const std::string out_dir = argv[2];
@@ -108,6 +113,7 @@ int main(int argc, char** argv) {
 
     auto shared = HostTransport::MakeShared(R);
     std::vector<int> rc(R, 0);
+    std::vector<int64_t> atk_expect(N, -1);  // (async 2; objects are written by one rank at a time)
     auto rank_main = [&](int r) {
         int64_t now = 0;
         HostTransport t(shared, r, DeviceRowMemory());
@@ -252,6 +258,14 @@ int main(int argc, char** argv) {
                 }
             }
             if (!async) km.MigrateNow();
+            if (transit_writes)  // the entities in transit on this rank, after their SwitchScene
+                for (int64_t o = 0; o < N; o++) {
+                    const NFGUID g(gh[o], gd[o]);
+                    if (!km.Departing(g)) continue;
+                    const int64_t v = 7000000 + o * 16 + tk;
+                    if (!km.SetPropertyInt(g, "ATK_VALUE", v)) rc[r] = 6;
+                    atk_expect[o] = v;
+                }
             for (; hi < NH && h_tick[hi] == tk; hi++) {
                 const NFGUID g(gh[h_obj[hi]], gd[h_obj[hi]]);
                 if (km.ObjectIndex(g) < 0 || km.Departing(g)) continue;
@@ -273,6 +287,14 @@ int main(int argc, char** argv) {
             }
             now = tick_time[tk];
             km.Execute();
+            if (transit_writes)  // ... and after the Execute that started their tickets' gather
+                for (int64_t o = 0; o < N; o++) {
+                    const NFGUID g(gh[o], gd[o]);
+                    if (!km.Departing(g)) continue;
+                    const int64_t v = 8000000 + o * 16 + tk;
+                    if (!km.SetPropertyInt(g, "ATK_VALUE", v)) rc[r] = 6;
+                    atk_expect[o] = v;
+                }
             moff.push_back((uint32_t)mr.size());
             char nm[40];
 #define PUT(pfx, s, code, vec, es) snprintf(nm, sizeof nm, "%s_t%d_%s", pfx, tk, s); nfio_put1(&w, nm, code, vec.data(), vec.size(), es);
@@ -320,5 +342,11 @@ int main(int argc, char** argv) {
     for (auto& x : th) x.join();
     for (int r = 0; r < R; r++)
         if (rc[r]) return rc[r];
+    if (transit_writes) {
+        nfio_writer w;
+        if (nfio_wopen(&w, (out_dir + "/atk_expect.nfio").c_str())) return 2;
+        nfio_put1(&w, "atk_expect", NFIO_I64, atk_expect.data(), atk_expect.size(), 8);
+        nfio_wclose(&w);
+    }
     return 0;
 }

@@ -189,6 +189,32 @@ def test_plugin_shard_async_exchange_keeps_functors(gpu_available, tmp_path, ran
     assert moved > 40 * ranks // 2
 
 
+@pytest.mark.gpu
+def test_plugin_shard_writes_in_transit_travel_with_the_row(gpu_available, tmp_path):
+    """Calls on an entity in transit (its cross-shard SwitchScene queued, its row not yet exported) made
+    after the Execute that started its ticket gather: they were queued in the source world while k_pack
+    copied the device row, and lost.  Now a window with calls while an entity departs applies
+    them in a device pass of their own before the rows leave: every entity's ATK_VALUE (no program writes
+    it) on its owner at the end equals the last value written while it was in transit."""
+    import numpy as np
+    from noahgameframe_amd import nfio, workload
+    exe = os.path.join(ROOT, "tests", "cpp", "_bin", "plugin_shard_replay")
+    _build()
+    w = workload.make_world(n_obj=4000, n_scenes=4, groups_per_scene=5, players_per_group=3, n_ticks=10,
+                            seed=97, switch_frac=0.04, switch_new_groups=True, ext_frac=0.05, host_ops=False)
+    wp = str(tmp_path / "w.nfio")
+    nfio.write(wp, w)
+    r = subprocess.run([exe, wp, str(tmp_path), "2", "2"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    outs = [nfio.read(str(tmp_path / f"rank{k}.nfio")) for k in range(2)]
+    exp = nfio.read(str(tmp_path / "atk_expect.nfio"))["atk_expect"]
+    atk = workload.PID["ATK_VALUE"]
+    final = sum(np.where(out["final_own"] == 1, out["final_i"][atk], 0) for out in outs)
+    written = exp >= 0
+    assert written.sum() > 40 and (exp >= 8000000).sum() > 20
+    np.testing.assert_array_equal(final[written], exp[written])
+
+
 @pytest.mark.parametrize("ranks", [2, 4])
 def test_shard_rank_top_host_stub(tmp_path, ranks):
     """NFIRankRedisModule::GetRange across the C++ scene shards (SceneShard::RankTop, what
