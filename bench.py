@@ -619,7 +619,6 @@ def other_config_legs(args, progress=lambda what: None):
 
 
 ADAPTER_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "adapter_bench")
-NPC_FRAMES = 8  # timed frames of the adapter leg's NPC phase (NFCNPCRefreshModule's HP callback on every NPC)
 
 
 class AdapterLeg:
@@ -627,60 +626,69 @@ class AdapterLeg:
     reference-side plugin (NFGPUKernelAdapter, NFGPUSceneAOIAdapter, NFGPUScheduleAdapter) in
     NFKernelPlugin's place among the reference's own modules — on the plugin_frame leg's world (1M
     entities, a heartbeat functor on every schedule, a common property / record callback, the AOI
-    module's recipient-list callbacks).  Started first: it builds its host objects through the
-    reference's CreateObject while this process runs the GPU legs, then waits; finish() lets it
-    commit its world and time its frames on the idle GPU."""
+    module's recipient-list callbacks); and a second server on the same world whose NPCs register
+    NFCNPCRefreshModule's HP callback at creation (NFCNPCRefreshModule.cpp:104: every NPC eager, HP logged
+    per Set by k_chain).  Started first: they build their host objects through the reference's
+    CreateObject while this process runs the GPU legs, then wait; finish() lets each in turn commit its
+    world and time its frames on the idle GPU."""
+    MODES = (0, 2)
 
     def __init__(self, args):
-        self.proc, self.err = None, None
+        self.procs, self.err = [], None
         if not os.path.exists(ADAPTER_EXE):
             self.err = "tests/cpp/_ref/adapter_bench not built (needs /root/reference at build time)"
             return
         from noahgameframe_amd import nfio, workload
         self.tmp = tempfile.TemporaryDirectory()
         wp = os.path.join(self.tmp.name, "w.nfio")
-        # (twice the frames: the same frames again with NFCNPCRefreshModule's HP callback on every NPC,
-        # NFCNPCRefreshModule.cpp:104 — reported as adapter_frame.config1.npc_hp)
         w = workload.bench_world(n_obj=args.entities, groups=args.groups, players_per_group=args.players_per_group,
-                                 n_ticks=args.warmup + args.steps + 2 + NPC_FRAMES, tick_ms=args.tick_ms, seed=2031,
-                                 ext_frac=0.05, host_ops=True)
+                                 n_ticks=args.warmup + args.steps, tick_ms=args.tick_ms, seed=2031, ext_frac=0.05,
+                                 host_ops=True)
         nfio.write(wp, w)
         self.t0 = time.perf_counter()
-        self.errf = open(os.path.join(self.tmp.name, "err.txt"), "w+")
-        self.proc = subprocess.Popen([ADAPTER_EXE, wp, str(args.warmup), str(args.steps), "0", "0", "1", str(NPC_FRAMES)],
-                                     stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=self.errf, text=True)
+        for m in self.MODES:
+            errf = open(os.path.join(self.tmp.name, f"err{m}.txt"), "w+")
+            p = subprocess.Popen([ADAPTER_EXE, wp, str(args.warmup), str(args.steps), str(m), "0", "1"],
+                                 stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=errf, text=True)
+            self.procs.append((m, p, errf))
 
-    def finish(self, timeout=900, progress=lambda what: None):
-        if self.proc is None:
-            return {"error": self.err}
+    def _finish_one(self, p, errf, deadline, progress, what):
         try:
-            ready = self.proc.stdout.readline()   # (blocks until its host objects are built)
-            progress("adapter_frame config[1]: host objects built")
-            self.proc.stdin.write("go\n")
-            self.proc.stdin.flush()
-            # (a line a minute while its frames run)
-            deadline = self.t0 + max(60.0, timeout)
-            while True:
+            ready = p.stdout.readline()   # (blocks until its host objects are built)
+            progress(f"{what}: host objects built")
+            p.stdin.write("go\n")
+            p.stdin.flush()
+            while True:  # (a line a minute while its frames run)
                 try:
-                    out, _ = self.proc.communicate(timeout=max(1.0, min(60.0, deadline - time.perf_counter())))
+                    out, _ = p.communicate(timeout=max(1.0, min(60.0, deadline - time.perf_counter())))
                     break
                 except subprocess.TimeoutExpired:
                     if time.perf_counter() >= deadline:
                         raise
-                    progress("adapter_frame config[1]: frames running")
-            self.errf.seek(0)
-            err = self.errf.read()
+                    progress(f"{what}: frames running")
+            errf.seek(0)
+            err = errf.read()
         except Exception as e:  # (a timeout, or the process died before it was ready)
-            self.proc.kill()
-            self.proc.communicate()
+            p.kill()
+            p.communicate()
             return {"error": repr(e)[-300:]}
         finally:
-            self.errf.close()
-            self.tmp.cleanup()
+            errf.close()
         line = [x for x in out.splitlines() if x.startswith("{") and "adapter_frame_ms" in x]
-        if self.proc.returncode != 0 or not line:
+        if p.returncode != 0 or not line:
             return {"error": (err or out or ready)[-400:]}
         return json.loads(line[-1])
+
+    def finish(self, timeout=1200, progress=lambda what: None):
+        if not self.procs:
+            return {"error": self.err}
+        deadline = self.t0 + timeout
+        res = {m: self._finish_one(p, errf, deadline, progress, f"adapter_frame config[1] mode {m}")
+               for m, p, errf in self.procs}
+        self.tmp.cleanup()
+        out = res[0]
+        out["npc_hp"] = res[2]
+        return out
 
 
 def adapter_config0_run(args):

@@ -413,6 +413,9 @@ public:
     // ---- NFIScheduleModule: object schedules (SM:218-285) ----
     bool AddSchedule(const NFGUID& self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb, float fTime,
                      int nCount);
+    // the same call made at time now_ms (NFGetTime() of the original call, for a caller that queued it)
+    bool AddSchedule(const NFGUID& self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb, float fTime,
+                     int nCount, int64_t now_ms);
     bool RemoveSchedule(const NFGUID& self, const std::string& name);
     bool RemoveSchedule(const NFGUID& self);
     bool ExistSchedule(const NFGUID& self, const std::string& name);

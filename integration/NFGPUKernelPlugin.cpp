@@ -132,7 +132,7 @@ public:
                 const nfgpu::TDATA_TYPE t = to_gpu(p->GetType());
                 if (t == nfgpu::TDATA_UNKNOWN) continue;  // strings / vectors stay on the host
                 gpu_.AddProperty(p->GetKey(), t);
-                dev_props_.insert(p->GetKey());
+                if (dev_props_.insert(p->GetKey()).second) dev_prop_ix_.insert(p->GetKey(), 1);
                 gpu_.SetPropertyFlags(cls, p->GetKey(), p->GetPublic(), p->GetPrivate(), p->GetUpload());
             }
             NF_SHARE_PTR<NFIRecordManager> rm = c->GetRecordManager();
@@ -148,6 +148,7 @@ public:
                 if (!dev_records_.count(r->GetName())) {
                     gpu_.AddRecord(r->GetName(), r->GetRows(), cols);
                     dev_records_.insert(r->GetName());
+                    dev_rec_ix_.insert(r->GetName(), 1);
                     for (int i = 0; i < r->GetCols(); i++) col_tags_[r->GetName()][r->GetColTag(i)] = i;
                 }
                 gpu_.SetRecordFlags(cls, r->GetName(), r->GetPublic(), r->GetPrivate(), r->GetUpload());
@@ -186,8 +187,12 @@ public:
                 if (ops[i].code == NFK_OP_RIADD_CLAMP || ops[i].code == NFK_OP_RFAFFINE)
                     rec_op_[ops[i].dst] = std::make_pair(k, i);
         }
-        for (const std::string& nm : watch_pending_) gpu_.WatchProperty(nm);
+        for (const std::string& nm : watch_pending_)
+            if (dev_props_.count(nm) && watched_.insert(nm).second) gpu_.WatchProperty(nm);
         watch_pending_.clear();
+        // the device schedule calls made while their objects were being created (class callbacks at
+        // COE_CREATE_HASDATA, e.g. HelloWorld3Module.cpp:47), now that the layout exists
+        FlushCreationSchedules();
         return ok;
     }
 
@@ -236,10 +241,16 @@ public:
     NF_SHARE_PTR<NFIObject> CreateObject(const NFGUID& self, const int nSceneID, const int nGroupID,
                                          const std::string& strClassName, const std::string& strConfigIndex,
                                          const NFIDataList& arg) override {
+        creating_.push_back(self);
         NF_SHARE_PTR<NFIObject> o = NFCKernelModule::CreateObject(self, nSceneID, nGroupID, strClassName, strConfigIndex, arg);
-        if (!o) return o;
+        creating_.pop_back();
+        if (!o) {
+            DropCreationSchedules(self);
+            return o;
+        }
         if (!dev_props_.empty()) MirrorObject(o);
         CacheClassName(self, o);
+        if (gpu_.World()) FlushCreationSchedules();
         return Handle(self, o);
     }
 
@@ -297,6 +308,8 @@ public:
             mtDeleteSelfList.push_back(self);
             return true;
         }
+        ForgetHostObject(self);
+        DropCreationSchedules(self);
         const bool ok = NFCKernelModule::DestroyObject(self);
         gpu_.DestroyObject(to_gpu(self));
         handles_.erase(self);
@@ -412,6 +425,23 @@ public:
     }
     void EndAOIRegistration() { aoi_registering_ = false; }
 
+    // (NFGPUScheduleAdapter) a device schedule call on an object that is not on the device yet — being
+    // created (its class callbacks run inside CreateObject, KM:146-267, before the adapter hands it to the
+    // device) or created before AfterInit: kept in call order with the clock of the call and made once the
+    // object is there (NFCScheduleModule applies AddSchedule at its next Execute anyway, SM:257, 95-117)
+    bool DeferSchedule(const NFGUID& self) const {
+        return !DevObject(self) && (!gpu_.World() || std::find(creating_.begin(), creating_.end(), self) != creating_.end());
+    }
+    struct DeferredSchedule {
+        int op;  // 1 AddSchedule, 2 RemoveSchedule(self, name), 3 RemoveSchedule(self)
+        NFGUID self;
+        std::string name;
+        nfgpu::OBJECT_SCHEDULE_FUNCTOR cb;
+        float t;
+        int count;
+        int64_t now;
+    };
+    void QueueCreationSchedule(DeferredSchedule d) { creation_sched_.push_back(std::move(d)); }
     // (NFGPUObject) the host object is about to be read or written through its handle
     void Touch(const NFGUID& self) { SyncObject(self); }
     // (NFGPUObject) a read of a device property inside the heartbeat functor walk with walk-order reads
@@ -426,10 +456,14 @@ public:
     // managers handed out: the object is eager from now on, a device property's Sets are logged
     void Watched(const NFGUID& self, const std::string& prop) {
         MarkEager(self, prop.empty());
-        if (prop.empty() || !dev_props_.count(prop) || watched_.count(prop)) return;
+        if (prop.empty() || watched_.count(prop)) return;
+        if (!gpu_.World()) {  // before AfterInit the device properties are not known yet (a callback
+            watch_pending_.push_back(prop);  // registered at creation, e.g. NFCNPCRefreshModule.cpp:104)
+            return;
+        }
+        if (!dev_props_.count(prop)) return;
         watched_.insert(prop);
-        if (gpu_.World()) gpu_.WatchProperty(prop);
-        else watch_pending_.push_back(prop);
+        gpu_.WatchProperty(prop);
     }
 
     nfgpu::NFGPUKernelModule gpu_;
@@ -682,12 +716,12 @@ private:
         }
         for (const Fire& fi : fires) {
             const NFGUID self = to_ref(gpu_.ObjectGuid(fi.o));
-            NF_SHARE_PTR<NFIObject> ob = GetElement(self);
+            NFIObject* ob = HostObject(fi.o);
             if (!ob) continue;
             if (fi.row < 0) {  // NFCProperty::SetInt / SetFloat of one Set (PR:254-334): its callbacks fire
                 const auto& c = ch[(size_t)fi.i];
                 const std::string& name = gpu_.PropertyName(c.pid);
-                NF_SHARE_PTR<NFIProperty> p = ob->GetPropertyManager()->GetElement(name);
+                NFIProperty* p = HostProperty(fi.o, c.pid, name);
                 if (!p) continue;
                 Mirror(self, name, -1, -1, [&] {
                     if (p->GetType() == TDATA_INT) p->SetInt((NFINT64)c.new_bits);
@@ -739,8 +773,14 @@ private:
                                        gpu_.PropertyCount(nfgpu::TDATA_OBJECT) || watched_n_ != watched_.size()) {
             watched_pid_.assign((size_t)gpu_.PropertyCount(nfgpu::TDATA_INT) + gpu_.PropertyCount(nfgpu::TDATA_FLOAT) +
                                     gpu_.PropertyCount(nfgpu::TDATA_OBJECT), 0);
-            for (const std::string& nm : watched_) watched_pid_[(size_t)gpu_.PropertyId(nm)] = 1;
+            watched_slot_.assign(watched_pid_.size(), -1);
+            watched_slots_ = 0;
+            for (const std::string& nm : watched_) {
+                watched_pid_[(size_t)gpu_.PropertyId(nm)] = 1;
+                watched_slot_[(size_t)gpu_.PropertyId(nm)] = (int)watched_slots_++;
+            }
             watched_n_ = watched_.size();
+            prop_cache_.clear();  // (slots renumbered)
         }
         return pid >= 0 && (size_t)pid < watched_pid_.size() && watched_pid_[(size_t)pid];
     }
@@ -927,8 +967,9 @@ private:
     // class-event handlers and the AOI module's creation-time reads and writes (KM:146-267, AOI:227-258)
     // see the host object, exactly as in the reference, and its final values enter the device.
     bool DevObject(const NFGUID& self) const { return gpu_.ObjectIndex(to_gpu(self)) >= 0; }
-    bool DevProp(const NFGUID& self, const std::string& name) const { return dev_props_.count(name) && DevObject(self); }
-    bool DevRecord(const NFGUID& self, const std::string& rec) const { return dev_records_.count(rec) && DevObject(self); }
+    // (asked by the common-callback wrappers on every host property / record event: one hash, not a tree walk)
+    bool DevProp(const NFGUID& self, const std::string& name) const { return dev_prop_ix_.find(name) >= 0 && DevObject(self); }
+    bool DevRecord(const NFGUID& self, const std::string& rec) const { return dev_rec_ix_.find(rec) >= 0 && DevObject(self); }
     int ColOf(const std::string& rec, const std::string& tag) const {  // NFCRecord::GetCol (RC:1319)
         auto r = col_tags_.find(rec);
         if (r == col_tags_.end()) return -1;
@@ -936,8 +977,64 @@ private:
         return c == r->second.end() ? -1 : c->second;
     }
 
+    void FlushCreationSchedules() {
+        if (creation_sched_.empty()) return;
+        std::vector<DeferredSchedule> q;
+        q.swap(creation_sched_);
+        for (DeferredSchedule& d : q) {
+            if (!DevObject(d.self)) {  // (still being created: an outer CreateObject's own objects)
+                creation_sched_.push_back(std::move(d));
+                continue;
+            }
+            const nfgpu::NFGUID g = to_gpu(d.self);
+            if (d.op == 1) gpu_.AddSchedule(g, d.name, d.cb, d.t, d.count, d.now);
+            else if (d.op == 2) gpu_.RemoveSchedule(g, d.name);
+            else gpu_.RemoveSchedule(g);
+        }
+    }
+    void DropCreationSchedules(const NFGUID& self) {
+        creation_sched_.erase(std::remove_if(creation_sched_.begin(), creation_sched_.end(),
+                                             [&](const DeferredSchedule& d) { return d.self == self; }),
+                              creation_sched_.end());
+    }
+    // the host object of a device object index (OnFrame's per-Set callbacks: no NFGUID map walk per Set),
+    // and the NFIProperty of a watched property (WatchedSlot) per object
+    NFIObject* HostObject(int o) {
+        if ((size_t)o < host_obj_.size() && host_obj_[(size_t)o]) return host_obj_[(size_t)o];
+        NF_SHARE_PTR<NFIObject> ob = GetElement(to_ref(gpu_.ObjectGuid(o)));
+        if (!ob) return nullptr;
+        if ((size_t)o >= host_obj_.size()) host_obj_.resize((size_t)gpu_.ObjectCount() + 1024, nullptr);
+        host_obj_[(size_t)o] = ob.get();  // (NFCKernelModule holds it until DestroyObject, which clears this)
+        return ob.get();
+    }
+    NFIProperty* HostProperty(int o, int pid, const std::string& name) {
+        const int w = WatchedSlot(pid);
+        const size_t at = (size_t)o * watched_slots_ + (size_t)w;
+        if (w >= 0 && at < prop_cache_.size() && prop_cache_[at]) return prop_cache_[at];
+        NFIObject* ob = HostObject(o);
+        NF_SHARE_PTR<NFIProperty> p = ob ? ob->GetPropertyManager()->GetElement(name) : nullptr;
+        if (!p) return nullptr;
+        if (w >= 0) {
+            if (at >= prop_cache_.size()) prop_cache_.resize(((size_t)gpu_.ObjectCount() + 1024) * watched_slots_, nullptr);
+            prop_cache_[at] = p.get();  // (the object's property manager holds it)
+        }
+        return p.get();
+    }
+    int WatchedSlot(int pid) {
+        WatchedPid(pid);  // (the table current)
+        return pid >= 0 && (size_t)pid < watched_slot_.size() ? watched_slot_[(size_t)pid] : -1;
+    }
+    void ForgetHostObject(const NFGUID& self) {
+        const int o = gpu_.ObjectIndex(to_gpu(self));
+        if (o < 0) return;
+        if ((size_t)o < host_obj_.size()) host_obj_[(size_t)o] = nullptr;
+        for (size_t w = 0; w < watched_slots_; w++)
+            if ((size_t)o * watched_slots_ + w < prop_cache_.size()) prop_cache_[(size_t)o * watched_slots_ + w] = nullptr;
+    }
+
     NFIClassModule* m_pClassModule = nullptr;
     std::set<std::string> dev_props_, dev_records_;
+    nfgpu_detail::NameIndex dev_prop_ix_, dev_rec_ix_;  // (the same names: DevProp / DevRecord)
     std::map<std::string, std::map<std::string, int>> col_tags_;
     std::set<int> scenes_;
     NFGUID obj_scratch_;
@@ -959,7 +1056,12 @@ private:
     bool eager_all_ = false;
     std::set<std::string> watched_;
     std::vector<uint8_t> watched_pid_;  // (WatchedPid's table, rebuilt when watched_ grows)
-    size_t watched_n_ = 0;
+    std::vector<int> watched_slot_;     // device pid -> index among the watched properties (-1: none)
+    size_t watched_n_ = 0, watched_slots_ = 0;
+    std::vector<NFIObject*> host_obj_;    // (HostObject)
+    std::vector<NFIProperty*> prop_cache_;  // (HostProperty: [object][watched slot])
+    std::vector<NFGUID> creating_;        // CreateObject calls in progress (nested: class callbacks may create)
+    std::vector<DeferredSchedule> creation_sched_;
     std::vector<std::string> watch_pending_;
     std::map<uint16_t, std::pair<int, int>> rec_op_;  // (rec << 8 | col) -> (kind, op index)
     std::unordered_map<NFGUID, NF_SHARE_PTR<NFIObject>, GuidHash> handles_;
@@ -1146,30 +1248,42 @@ public:
     bool AddSchedule(const NFGUID self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR_PTR& cb,
                      const float fTime, const int nCount) override {  // SM:257
         if (!gpu().HasHeartBeat(name)) return host_.AddSchedule(self, name, cb, fTime, nCount);
-        return gpu().AddSchedule(
-            to_gpu(self), name,
-            [cb](const nfgpu::NFGUID& g, const std::string& n, const float t, const int c) { return (*cb)(to_ref(g), n, t, c); },
-            fTime, nCount);
+        nfgpu::OBJECT_SCHEDULE_FUNCTOR f = [cb](const nfgpu::NFGUID& g, const std::string& n, const float t, const int c) {
+            return (*cb)(to_ref(g), n, t, c);
+        };
+        if (kernel()->DeferSchedule(self)) {  // (its object is being created: made once it is on the device)
+            kernel()->QueueCreationSchedule({1, self, name, f, fTime, nCount, NFGetTime()});
+            return true;
+        }
+        return gpu().AddSchedule(to_gpu(self), name, f, fTime, nCount);
     }
     bool RemoveSchedule(const NFGUID self) override {  // SM:240
+        if (kernel()->DeferSchedule(self)) kernel()->QueueCreationSchedule({3, self, "", nullptr, 0.f, 0, 0});
         const bool d = gpu().RemoveSchedule(to_gpu(self));
         const bool h = host_.RemoveSchedule(self);
         return d || h;
     }
     bool RemoveSchedule(const NFGUID self, const std::string& name) override {  // SM:245
-        return gpu().HasHeartBeat(name) ? gpu().RemoveSchedule(to_gpu(self), name) : host_.RemoveSchedule(self, name);
+        if (!gpu().HasHeartBeat(name)) return host_.RemoveSchedule(self, name);
+        if (kernel()->DeferSchedule(self)) {
+            kernel()->QueueCreationSchedule({2, self, name, nullptr, 0.f, 0, 0});
+            return true;
+        }
+        return gpu().RemoveSchedule(to_gpu(self), name);
     }
     bool ExistSchedule(const NFGUID self, const std::string& name) override {  // SM:276
-        return gpu().HasHeartBeat(name) ? gpu().ExistSchedule(to_gpu(self), name) : host_.ExistSchedule(self, name);
+        if (!gpu().HasHeartBeat(name)) return host_.ExistSchedule(self, name);
+        // (SM:276 sees an AddSchedule only after the Execute that applies it: one queued at creation is not there yet)
+        if (kernel()->DeferSchedule(self)) return false;
+        return gpu().ExistSchedule(to_gpu(self), name);
     }
     // the device frame (its object schedules) runs in NFGPUKernelAdapter::Execute; the host
     // schedules here
     bool Execute() override { return host_.Execute(); }
 
 private:
-    nfgpu::NFGPUKernelModule& gpu() {
-        return dynamic_cast<NFGPUKernelAdapter*>(pPluginManager->FindModule<NFIKernelModule>())->gpu_;
-    }
+    NFGPUKernelAdapter* kernel() { return dynamic_cast<NFGPUKernelAdapter*>(pPluginManager->FindModule<NFIKernelModule>()); }
+    nfgpu::NFGPUKernelModule& gpu() { return kernel()->gpu_; }
     NFCScheduleModule host_;
 };
 

@@ -886,9 +886,14 @@ uint32_t NFGPUKernelModule::ReadMask(bool per_event_fired) const {
 // on an object this module does not have is dropped at Flush)
 bool NFGPUKernelModule::AddSchedule(const NFGUID& self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb,
                                     float fTime, int nCount) {
+    return AddSchedule(self, name, cb, fTime, nCount, clock_());
+}
+
+bool NFGPUKernelModule::AddSchedule(const NFGUID& self, const std::string& name, const OBJECT_SCHEDULE_FUNCTOR& cb,
+                                    float fTime, int nCount, int64_t now_ms) {
     const int kind = hb_ix_.find(name);
     if (!committed_ || kind < 0) return false;
-    QueueScheduleCall(1, self, kind, fTime, nCount, clock_());
+    QueueScheduleCall(1, self, kind, fTime, nCount, now_ms);
     sched_add_.push_back({self.nHead64, self.nData64, kind, cb, fTime});  // the window's first call wins
     return true;
 }

@@ -18,14 +18,12 @@
 // host ms per frame (median of the timed frames), the plugin's phases, what the callbacks received and
 // how many device events reached NFCSceneAOIModule's own handlers (GetBroadCastObject) — 0.
 //
-// With npc 1 the same frames then run again after every NPC has registered NFCNPCRefreshModule's callback
-// (NFCNPCRefreshModule.cpp:98-105: AddPropertyCallBack(self, "HP", OnObjectHPEvent) at creation; its
-// newVar <= 0 test counted): every NPC is eager and HP is logged per Set (k_chain), so each frame also
-// fires one callback per accepted HP Set of its heartbeat programs, in the walk's order; the JSON line
-// carries those frames as "npc_hp".
+//   * mode 2 (config[1] with NFCNPCRefreshModule's callback, NFCNPCRefreshModule.cpp:98-105): every NPC
+//     registers AddPropertyCallBack(self, "HP", OnObjectHPEvent) at its creation (its newVar <= 0 test
+//     counted): every NPC is eager and HP is logged per Set (k_chain), so each frame also fires one callback
+//     per accepted HP Set of its heartbeat programs, in the walk's order.
 //
-// usage: adapter_bench <workload.nfio> <warmup> <frames> [mode] [calls] [wait] [npc_frames]
-//   npc_frames > 0: the NPC phase above, 2 untimed frames and npc_frames timed ones
+// usage: adapter_bench <workload.nfio> <warmup> <frames> [mode] [calls] [wait]
 //   mode 0: the config[1] logic above;  1: Tutorial3's (per-object World callbacks, OnEvent Sets)
 //   calls 1: the workload's SetProperty / schedule calls between frames (mode 1 always makes its Sets)
 //   wait 1: after the host objects are built (nothing has touched the GPU yet) print {"ready": ...} and
@@ -97,8 +95,7 @@ int main(int argc, char** argv) {
     const int mode = argc > 4 ? atoi(argv[4]) : 0;
     const bool calls = mode == 1 || (argc > 5 && atoi(argv[5]) != 0);
     const bool wait = argc > 6 && atoi(argv[6]) != 0;
-    const int K2 = argc > 7 ? atoi(argv[7]) : 0, W2 = K2 > 0 ? 2 : 0;
-    const bool npc = K2 > 0;
+
     auto A = [&](const char* n) {
         nfio_arr* a = nfio_get(&wf, n);
         if (!a) {
@@ -109,7 +106,7 @@ int main(int argc, char** argv) {
     };
     int64_t* cfg = (int64_t*)A("cfg")->data;
     const int64_t N = cfg[0], NI = cfg[1], NF = cfg[2], NC = cfg[3], NK = cfg[4], NR = cfg[5], NS = cfg[6], NT = cfg[7];
-    if (W + K + W2 + K2 > NT) {
+    if (W + K > NT) {
         fprintf(stderr, "workload has %lld frames, %d requested\n", (long long)NT, W + K);
         return 2;
     }
@@ -190,6 +187,8 @@ int main(int argc, char** argv) {
         NF_SHARE_PTR<NFIObject> ob = km->CreateObject(NFGUID(gh[o], gd[o]), sc[o], gr[o], cname[cl[o]], "", arg);
         if (!ob) return 3;
         if (mode == 1) ob->AddPropertyCallBack("World", &C, &Counters::OnWorld);  // HelloWorld3Module.cpp:95
+        if (mode == 2 && cl[o] == 0)  // NFCNPCRefreshModule.cpp:104, at the NPC's creation
+            km->AddPropertyCallBack(NFGUID(gh[o], gd[o]), "HP", &C, &Counters::OnObjectHPEvent);
     }
     const double host_build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count();
     if (wait) {
@@ -243,10 +242,14 @@ int main(int argc, char** argv) {
         std::vector<nfgpu::NFGPUKernelModule::FrameStats> st;
         std::vector<double> call_ms, frame_ms;
         int64_t ncalls = 0;
-        const int64_t syncs0 = kernel.MirrorSyncs(), chain0 = kernel.ChainCallbacks();
+        int64_t syncs0 = kernel.MirrorSyncs(), chain0 = kernel.ChainCallbacks();
         Counters c0;
         for (int t = t0; t < t0 + W + K; t++) {
-            if (t == t0 + W) c0 = C;
+            if (t == t0 + W) {  // (the timed frames' counts)
+                c0 = C;
+                syncs0 = kernel.MirrorSyncs();
+                chain0 = kernel.ChainCallbacks();
+            }
             const auto ts0 = std::chrono::steady_clock::now();
             for (; hi < NH && h_tick[hi] == t; hi++) {
                 if (!calls) continue;
@@ -309,30 +312,10 @@ int main(int argc, char** argv) {
         return buf;
     };
     std::string line = run(0, W, K);
-    fprintf(stderr, "adapter_bench: %d frames timed\n", K);
-    std::string npc_line;
-    if (npc) {
-        // NFCNPCRefreshModule::OnObjectClassEvent at COE_CREATE_HASDATA (NFCNPCRefreshModule.cpp:104), for
-        // the NPCs this server already holds
-        const auto tc = std::chrono::steady_clock::now();
-        int64_t n_npc = 0;
-        for (int64_t o = 0; o < N; o++)
-            if (cl[o] == 0) {
-                km->AddPropertyCallBack(NFGUID(gh[o], gd[o]), "HP", &C, &Counters::OnObjectHPEvent);
-                n_npc++;
-            }
-        const double reg_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tc).count();
-        fprintf(stderr, "adapter_bench: HP callbacks on %lld NPCs registered in %.1f s\n", (long long)n_npc, reg_s);
-        npc_line = run(W + K, W2, K2);
-        char tail[160];
-        snprintf(tail, sizeof tail, ", \"npcs_watched\": %lld, \"register_s\": %.2f}", (long long)n_npc, reg_s);
-        npc_line += tail;
-    }
     char tail[200];
     snprintf(tail, sizeof tail, ", \"build_s\": %.1f, \"host_objects_s\": %.1f, \"mode\": \"%s\"", build_s, host_build_s,
-             mode == 1 ? "tutorial3" : calls ? "config1-with-calls" : "config1");
+             mode == 1 ? "tutorial3" : mode == 2 ? "config1-npc-hp-callbacks" : calls ? "config1-with-calls" : "config1");
     line += tail;
-    if (npc) line += ", \"npc_hp\": " + npc_line;
     printf("%s}\n", line.c_str());
     fflush(stdout);
     _exit(0);  // (static destructors: NFMemoryCounter's static map dies before the modules' objects)
