@@ -533,6 +533,7 @@ public:
     struct FrameStats {
         double device, functors, events_read, deliver, calls, total;
         double gather;  // (of functors: the worker pool's gather of the frame's scattered reads)
+        double mirror;  // the frame hook (the drop-in adapter's mirror and per-Set callbacks)
     };
     const FrameStats& LastFrameStats() const { return stats_; }
     int ObjectIndex(const NFGUID& g) const;

@@ -30,6 +30,7 @@
 // A SwitchScene into another shard therefore takes effect at the start of the frame after the
 // next exchange frame.  Migrate() is the synchronous form (gather now, rows now).
 #pragma once
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <future>
@@ -123,6 +124,10 @@ public:
 private:
     void* comm_ = nullptr;       // rows
     void* meta_comm_ = nullptr;  // tickets
+    // set by Abort (possibly while the gather thread is inside a collective): the handles stay as they
+    // are — the collective paths check this flag first, and the destructor, which runs after the
+    // gather has been waited for, does not destroy communicators Abort has already released
+    std::atomic<bool> aborted_{false};
     void* stream_ = nullptr;     // rows, when AllToAllV is given no stream
     void* meta_stream_ = nullptr;
     int device_ = 0;

@@ -224,8 +224,13 @@ int nfk_destroy_objects(void* world, int32_t n, const int64_t* guid_head, const 
 int nfk_object_count(void* world, int32_t* n);
 /* An entity's state as a ROW of 64-bit words: properties (prop id order; an object property is two
  * words, data then head), per heartbeat kind its
- * schedule (next, remain|state, start, all|interval), per record its cells [cols][rows] and its
- * used-row mask.  Rows let a scene shard hand entities to another (SwitchScene across GPUs). */
+ * schedule (next, remain|state, start, all|interval), per record its cells [cols][places] and its
+ * used-row mask.  A column's cells are in the device's PACKED order, not row order: the used rows
+ * first in row order, then the unused rows in row order (a stable partition by the used mask, so the
+ * mask alone maps a row to its place and back: place = popcount(used & ((1 << row) - 1)) for a used
+ * row, popcount(used) + popcount(~used & ((1 << row) - 1)) for an unused one).  nfk_import_objects
+ * takes rows in the same form; a producer or consumer outside export / import must (un)pack by the
+ * row's mask.  Rows let a scene shard hand entities to another (SwitchScene across GPUs). */
 int nfk_row_words(void* world, int32_t* words);
 /* source side: write the entities' rows to rows_dev (device memory, [n][row_words]) on the world's
  * stream, and remove the entities from this world (they must not have other membership calls

@@ -45,6 +45,9 @@
 //   of the cell (RC:243-297; tests/test_oracle.py::test_reference_record_setfloat_bug), so they are
 //   device-only (SetRecordFloat / GetRecordFloat through NFIKernelModule read and write the device).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <tuple>
@@ -477,7 +480,7 @@ protected:
         const bool aoi = aoi_registering_;
         PROPERTY_EVENT_FUNCTOR_PTR host(new PROPERTY_EVENT_FUNCTOR(
             [this, cb, aoi](const NFGUID& self, const std::string& name, const NFIDataList::TData& a, const NFIDataList::TData& b) {
-                if (DevProp(self, name)) return 0;
+                if (MirrorTarget(self, name) || DevProp(self, name)) return 0;
                 if (aoi) ++aoi_host_calls_;
                 return (*cb)(self, name, a, b);
             }));
@@ -662,6 +665,7 @@ private:
     // frame's values with their per-object callbacks fired once per accepted Set of the frame's
     // heartbeat programs in the reference's order; every other evented object is marked stale.
     void OnFrame(const nfk_frame_host& f) {
+        prof_.Start();
         // objects the host wrote this window: stale, whatever their events (a program may have put a
         // written value back where the frame started, with no event).  An eager one's watched
         // properties are brought up to date below with their callbacks, so its refresh on the next
@@ -683,6 +687,7 @@ private:
             else m |= kStale;
         }
         if (ep.empty() && er.empty()) return;
+        prof_.Mark(0);
         // the Sets with callbacks, keyed (NFGUID, kind, op, row): the watched properties' per-Set log,
         // and the record cells a record op changed (one op per record column: at most one change per
         // cell and frame, so the frame's event is that Set)
@@ -714,7 +719,14 @@ private:
             std::stable_sort(fires.begin() + (std::ptrdiff_t)n_prop_fires, fires.end(), walk_less);
             std::inplace_merge(fires.begin(), fires.begin() + (std::ptrdiff_t)n_prop_fires, fires.end(), walk_less);
         }
-        for (const Fire& fi : fires) {
+        prof_.Mark(1);
+        // the fires' host objects are scattered over the host heap (NFGUID order is not allocation order):
+        // their table entries are prefetched kFar fires ahead, the property objects kNear ahead
+        constexpr size_t kFar = 24, kNear = 8;
+        for (size_t q = 0; q < fires.size(); q++) {
+            if (q + kFar < fires.size()) PrefetchFire(fires[q + kFar], false);
+            if (q + kNear < fires.size()) PrefetchFire(fires[q + kNear], true);
+            const Fire& fi = fires[q];
             const NFGUID self = to_ref(gpu_.ObjectGuid(fi.o));
             NFIObject* ob = HostObject(fi.o);
             if (!ob) continue;
@@ -739,6 +751,7 @@ private:
                 }
             }
         }
+        prof_.Mark(2);
         // the eager objects' other evented properties: the frame's value (an unwatched property has no
         // per-object callback that could tell the Sets apart) when the host object is read directly
         // (kMirrorAll); otherwise the object is stale for them, as any other object (its watched
@@ -763,9 +776,61 @@ private:
                 }
             });
         }
+        prof_.Mark(3);
+        prof_.Report(fires.size(), ep.size());
         // (record cells: a cell no record op writes changed only through the host record's own calls,
         // which the host record holds already — the frame's coalesced event of such a cell can carry a
         // SetRecord value an AddRow later overwrote, nfgpu.h nfk_set_records)
+    }
+    // (measurement, NFGPU_ADAPTER_PROF=1) OnFrame's parts per frame on stderr: state marks, the fire
+    // list, the per-Set callbacks, the eager objects' other events
+    struct FrameProf {
+        bool on = getenv("NFGPU_ADAPTER_PROF") != nullptr;
+        std::chrono::steady_clock::time_point t0;
+        double ms[4] = {0, 0, 0, 0};
+        void Start() {
+            if (on) t0 = std::chrono::steady_clock::now();
+        }
+        void Mark(int i) {
+            if (!on) return;
+            const auto t = std::chrono::steady_clock::now();
+            ms[i] = std::chrono::duration<double, std::milli>(t - t0).count();
+            t0 = t;
+        }
+        void Report(size_t nf, size_t nep) {
+            if (on) fprintf(stderr, "[onframe] marks %.3f fires %.3f callbacks %.3f others %.3f ms (%zu fires, %zu eager events)\n",
+                            ms[0], ms[1], ms[2], ms[3], nf, nep);
+        }
+    } prof_;
+    // (OnFrame) a fire's table entries (far), then the host property they point to (near)
+    void PrefetchFire(const Fire& fi, bool near) {
+        const size_t o = (size_t)fi.o;
+        if (!near) {
+            __builtin_prefetch(&gpu_.ObjectGuid(fi.o));
+            if (o < host_obj_.size()) __builtin_prefetch(&host_obj_[o]);
+            if (fi.row < 0 && watched_slots_) {
+                const int w = fi.kind >= 0 ? WatchedSlotFast(fr_pid_(fi)) : -1;
+                if (w >= 0 && o * watched_slots_ + (size_t)w < prop_cache_.size())
+                    __builtin_prefetch(&prop_cache_[o * watched_slots_ + (size_t)w]);
+            }
+            return;
+        }
+        if (fi.row < 0 && watched_slots_) {
+            const int w = WatchedSlotFast(fr_pid_(fi));
+            const size_t at = o * watched_slots_ + (size_t)w;
+            if (w >= 0 && at < prop_cache_.size() && prop_cache_[at]) {
+                const char* p = (const char*)prop_cache_[at];
+                __builtin_prefetch(p);
+                __builtin_prefetch(p + 64);
+                __builtin_prefetch(p + 128);
+            }
+        } else if (o < host_obj_.size() && host_obj_[o]) {
+            __builtin_prefetch(host_obj_[o]);
+        }
+    }
+    int fr_pid_(const Fire& fi) const { return gpu_.LastChain()[(size_t)fi.i].pid; }
+    int WatchedSlotFast(int pid) const {
+        return pid >= 0 && (size_t)pid < watched_slot_.size() ? watched_slot_[(size_t)pid] : -1;
     }
     // whether a device property id has a per-object callback somewhere (watched_, by device id)
     bool WatchedPid(int pid) {
@@ -800,9 +865,17 @@ private:
         mw_.name = &name;
         mw_.row = row;
         mw_.col = col;
+        mirroring_ = true;
         f();
+        mirroring_ = false;
         mw_.on = false;
     }
+    // the property the running mirror write sets (a device property of a device object: its host common
+    // callbacks receive nothing, as DevProp would say after an NFGUID lookup)
+    bool MirrorTarget(const NFGUID& self, const std::string& name) const {
+        return mirroring_ && mw_.row < 0 && self == mw_.self && name == *mw_.name;
+    }
+    bool mirroring_ = false;  // inside Mirror (mw_ keeps its target after OwnWrite cleared mw_.on)
     bool OwnWrite(const NFGUID& self, const std::string& name, int row, int col) {
         if (!mw_.on || self != mw_.self || row != mw_.row || col != mw_.col || name != *mw_.name) return false;
         mw_.on = false;

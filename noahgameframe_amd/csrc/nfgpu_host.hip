@@ -3770,6 +3770,46 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
                     wops++;
                 }
             }
+        // ... and every kind before one of those whose program writes a property a later re-run kind
+        // reads (an operand, a guard, or a destination's current value): the reference's functors run
+        // in name order on what the earlier ones left (SM:52-80), so the logged (old, new) of a watched
+        // Set depend on them.  Closed transitively, latest kind first.  (NFGPU_CHAIN_NO_CLOSURE=1: test
+        // hook, the watched kinds only — the round-5 form, which logged wrong (old, new) for such Sets)
+        static const bool no_closure = getenv("NFGPU_CHAIN_NO_CLOSURE") && getenv("NFGPU_CHAIN_NO_CLOSURE")[0] == '1';
+        if (kinds && !no_closure) {
+            auto bit = [](uint64_t (&m)[2], uint32_t p) {
+                if (p < 128) m[p >> 6] |= 1ull << (p & 63);
+            };
+            uint64_t rd[NFK_MAX_KINDS][2] = {}, wr[NFK_MAX_KINDS][2] = {};
+            for (int k = 0; k < d.n_kind; k++)
+                for (int i = 0; i < w->tab.nops[k]; i++) {
+                    const nfk_op& op = w->tab.ops[k][i];
+                    if (op.code != NFK_OP_IADD_CLAMP && op.code != NFK_OP_FLERP && op.code != NFK_OP_FAFFINE &&
+                        op.code != NFK_OP_ISET && op.code != NFK_OP_FSET)
+                        continue;
+                    bit(wr[k], op.dst);
+                    bit(rd[k], op.dst);
+                    if (op.flags & NFK_GUARD) {
+                        bit(rd[k], op.guard & 0xFFFFu);
+                        if (op.guard & NFK_GUARD_PROP) bit(rd[k], op.guard >> 19);
+                    }
+                    if (op.code == NFK_OP_FLERP || ((op.code == NFK_OP_ISET || op.code == NFK_OP_FSET) && (op.flags & NFK_A_PROP)))
+                        bit(rd[k], (uint32_t)op.a);
+                    if (op.code == NFK_OP_IADD_CLAMP) {
+                        if (op.flags & NFK_A_PROP) bit(rd[k], (uint32_t)op.a);
+                        if (op.flags & NFK_LO_PROP) bit(rd[k], (uint32_t)op.b);
+                        if (op.flags & NFK_HI_PROP) bit(rd[k], (uint32_t)op.c);
+                    }
+                }
+            uint64_t need[2] = {0, 0};  // what the re-run kinds after position k read
+            for (int k = d.n_kind - 1; k >= 0; k--) {
+                if (!((kinds >> k) & 1) && ((wr[k][0] & need[0]) | (wr[k][1] & need[1]))) kinds |= 1u << k;
+                if ((kinds >> k) & 1) {
+                    need[0] |= rd[k][0];
+                    need[1] |= rd[k][1];
+                }
+            }
+        }
         if (kinds) {
             // tile-staged: kTPB slots x the watched (kind, op) pairs per tile (each logs at most once)
             const int32_t nt = (int32_t)((d.N + kTPB - 1) / kTPB);

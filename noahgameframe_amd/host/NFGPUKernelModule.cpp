@@ -1029,7 +1029,9 @@ bool NFGPUKernelModule::Execute() {
     if (what) check(nfk_read_frame(world_, what, &fh), "nfk_read_frame");
     ReadChain();
     stats_.events_read = ms_since(t1);
+    t1 = std::chrono::steady_clock::now();
     if (frame_hook_) frame_hook_(fh);  // (before the functors: they see the frame's values)
+    stats_.mirror = ms_since(t1);
     t1 = std::chrono::steady_clock::now();
     // heartbeat functors with the reference's arguments, objects in NFGUID order (the fired list's)
     const int64_t nfi = n_cb_ ? fh.n_fi : 0;  // (a frame consumer may read the list without functors)

@@ -61,17 +61,19 @@ RcclTransport::RcclTransport(const std::vector<uint8_t>& unique_id, int rank, in
 }
 
 void RcclTransport::Abort() {
-    // (a collective blocked on a peer that never arrives returns; the communicators are gone)
+    // (a collective blocked on a peer that never arrives returns; the communicators are gone).  The
+    // handles are not reset here: the gather thread may be reading them; it sees aborted_ instead
+    if (aborted_.exchange(true)) return;
     if (meta_comm_) (void)ncclCommAbort((ncclComm_t)meta_comm_);
     if (comm_) (void)ncclCommAbort((ncclComm_t)comm_);
-    meta_comm_ = nullptr;
-    comm_ = nullptr;
 }
 
 RcclTransport::~RcclTransport() {
     if (buf_) (void)hipFree(buf_);
-    if (meta_comm_) (void)ncclCommDestroy((ncclComm_t)meta_comm_);
-    if (comm_) (void)ncclCommDestroy((ncclComm_t)comm_);
+    if (!aborted_.load()) {  // (aborted communicators were released by ncclCommAbort)
+        if (meta_comm_) (void)ncclCommDestroy((ncclComm_t)meta_comm_);
+        if (comm_) (void)ncclCommDestroy((ncclComm_t)comm_);
+    }
     if (meta_stream_) (void)hipStreamDestroy((hipStream_t)meta_stream_);
 }
 
@@ -79,7 +81,7 @@ RcclTransport::~RcclTransport() {
 // of device buffers on the tickets' communicator and stream; tickets are small).  May run on a
 // worker thread (SceneShard::EndFrame): the HIP device is per thread.
 int RcclTransport::AllGather(const std::vector<int64_t>& mine, std::vector<int64_t>& all) {
-    if (hipSetDevice(device_) != hipSuccess) return NFK_ERR_HIP;
+    if (aborted_.load() || hipSetDevice(device_) != hipSuccess) return NFK_ERR_HIP;
     hipStream_t s = (hipStream_t)meta_stream_;
     auto reserve = [&](size_t words) {
         if (words <= buf_cap_) return true;
@@ -99,7 +101,7 @@ int RcclTransport::AllGather(const std::vector<int64_t>& mine, std::vector<int64
     for (int64_t c : counts) mx = std::max(mx, c);
     all.clear();
     if (mx == 0) return NFK_OK;
-    if (!reserve((size_t)mx * (1 + size_))) return NFK_ERR_HIP;
+    if (aborted_.load() || !reserve((size_t)mx * (1 + size_))) return NFK_ERR_HIP;
     if ((n && hipMemcpyAsync(buf_, mine.data(), (size_t)n * 8, hipMemcpyHostToDevice, s) != hipSuccess) ||
         ncclAllGather(buf_, buf_ + mx, (size_t)mx, ncclInt64, (ncclComm_t)meta_comm_, s) != ncclSuccess)
         return NFK_ERR_HIP;
@@ -115,6 +117,7 @@ int RcclTransport::AllGather(const std::vector<int64_t>& mine, std::vector<int64
 // SceneShard passes), so the unpack that follows on it is ordered after the receive
 int RcclTransport::AllToAllV(const uint64_t* send, const std::vector<size_t>& scount, uint64_t* recv,
                              const std::vector<size_t>& rcount, void* stream) {
+    if (aborted_.load()) return NFK_ERR_HIP;
     hipStream_t s = (hipStream_t)(stream ? stream : stream_);
     size_t so = 0, ro = 0;
     if (ncclGroupStart() != ncclSuccess) return NFK_ERR_HIP;

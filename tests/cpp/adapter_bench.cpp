@@ -43,6 +43,9 @@
 #include "../../oracle/nfio.h"
 #include "../../oracle/ref_server.hpp"
 
+#ifdef ADAPTER_BENCH_PG
+extern "C" void _mcleanup(void);  // (glibc's gmon writer)
+#endif
 static std::string cstr(const uint8_t* p) { return std::string((const char*)p, strnlen((const char*)p, 32)); }
 static double bitsd(uint64_t u) {
     double d;
@@ -244,8 +247,10 @@ int main(int argc, char** argv) {
         int64_t ncalls = 0;
         int64_t syncs0 = kernel.MirrorSyncs(), chain0 = kernel.ChainCallbacks();
         Counters c0;
+        if (kernel.gpu_.World()) nfk_set_profiling(kernel.gpu_.World(), 1);  // (HIP events around each kernel)
         for (int t = t0; t < t0 + W + K; t++) {
             if (t == t0 + W) {  // (the timed frames' counts)
+                if (kernel.gpu_.World()) nfk_reset_kernel_times(kernel.gpu_.World());
                 c0 = C;
                 syncs0 = kernel.MirrorSyncs();
                 chain0 = kernel.ChainCallbacks();
@@ -286,29 +291,37 @@ int main(int argc, char** argv) {
             for (auto& s : st) v.push_back(s.*m);
             return med(v);
         };
+        // the device kernels' HIP-event time per frame (timer names: nfgpu.h nfk_kernel_times)
+        double kms[NFK_N_KERNEL_TIMERS] = {0};
+        int64_t kl[NFK_N_KERNEL_TIMERS] = {0}, kb[NFK_N_KERNEL_TIMERS] = {0};
+        if (kernel.gpu_.World()) nfk_kernel_times(kernel.gpu_.World(), kms, kl, kb);
         const nfk_summary& s = kernel.gpu_.LastSummary();
         const double kf = K ? (double)K : 1.0;
         char buf[4096];
         snprintf(buf, sizeof buf,
                  "{\"adapter_frame_ms\": %.3f, \"entities\": %lld, \"entity_ticks_per_s\": %.4g, \"calls_per_frame\": %lld, "
                  "\"phases_ms\": {\"calls\": %.3f, \"device\": %.3f, \"functors\": %.3f, \"events_read\": %.3f, "
-                 "\"deliver\": %.3f, \"functor_calls\": %.3f, \"plugin_execute\": %.3f, \"gather\": %.3f}, "
+                 "\"deliver\": %.3f, \"functor_calls\": %.3f, \"plugin_execute\": %.3f, \"gather\": %.3f, \"mirror\": %.3f}, "
                  "\"per_frame\": {\"fired\": %lld, \"prop_events\": %lld, \"rec_events\": %lld, \"messages\": %lld}, "
                  "\"received_per_frame\": {\"heartbeats\": %.0f, \"common_prop\": %.0f, \"common_rec\": %.0f, \"aoi_prop\": %.0f, "
                  "\"aoi_rec\": %.0f, \"recipients\": %.0f, \"per_object_callbacks\": %.0f, \"hp_kills\": %.0f}, "
                  "\"aoi\": {\"device_list_calls\": %lld, \"host_getbroadcastobject_calls_for_device_events\": %lld}, "
                  "\"mirror\": {\"lazy_syncs_per_frame\": %.1f, \"chain_callbacks_per_frame\": %.0f}, "
+                 "\"device_kernels_ms_per_frame\": {\"k_tick\": %.4f, \"k_records\": %.4f, \"k_fanout\": %.4f, \"aux\": %.4f, "
+                 "\"k_scan_tiles\": %.4f, \"membership\": %.4f, \"k_chain\": %.4f}, \"k_chain_launches\": %lld, "
                  "\"frames\": %d, \"warmup\": %d",
                  med(frame_ms), (long long)N, (double)N / (med(frame_ms) * 1e-3), (long long)(K ? ncalls / K : 0),
                  med(call_ms), medf(&nfgpu::NFGPUKernelModule::FrameStats::device),
                  medf(&nfgpu::NFGPUKernelModule::FrameStats::functors), medf(&nfgpu::NFGPUKernelModule::FrameStats::events_read),
                  medf(&nfgpu::NFGPUKernelModule::FrameStats::deliver), medf(&nfgpu::NFGPUKernelModule::FrameStats::calls),
                  medf(&nfgpu::NFGPUKernelModule::FrameStats::total), medf(&nfgpu::NFGPUKernelModule::FrameStats::gather),
+                 medf(&nfgpu::NFGPUKernelModule::FrameStats::mirror),
                  (long long)s.n_fired, (long long)s.n_prop_events, (long long)s.n_rec_events, (long long)s.n_msgs,
                  (C.hb - c0.hb) / kf, (C.prop - c0.prop) / kf, (C.rec - c0.rec) / kf, (C.aoi_prop - c0.aoi_prop) / kf,
                  (C.aoi_rec - c0.aoi_rec) / kf, (C.rcpt - c0.rcpt) / kf, (C.obj_cb - c0.obj_cb) / kf, (C.kills - c0.kills) / kf,
                  (long long)kernel.AOIDeviceCalls(), (long long)kernel.AOIHostDeviceCalls(),
-                 (kernel.MirrorSyncs() - syncs0) / kf, (kernel.ChainCallbacks() - chain0) / kf, K, W);
+                 (kernel.MirrorSyncs() - syncs0) / kf, (kernel.ChainCallbacks() - chain0) / kf, kms[0] / kf, kms[1] / kf,
+                 kms[2] / kf, kms[3] / kf, kms[4] / kf, kms[5] / kf, kms[6] / kf, (long long)kl[6], K, W);
         return buf;
     };
     std::string line = run(0, W, K);
@@ -318,5 +331,8 @@ int main(int argc, char** argv) {
     line += tail;
     printf("%s}\n", line.c_str());
     fflush(stdout);
+#ifdef ADAPTER_BENCH_PG
+    _mcleanup();  // (the -pg build: gmon.out, which exit() would write)
+#endif
     _exit(0);  // (static destructors: NFMemoryCounter's static map dies before the modules' objects)
 }

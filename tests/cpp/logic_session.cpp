@@ -40,7 +40,10 @@
 //      mtDeleteSelfList, KM:275-279 / KM:1434) or another object (at once);
 //   8  NFCNPCRefreshModule's callbacks only (NFCNPCRefreshModule.cpp:98-105): every NPC gets
 //      AddPropertyCallBack(self, "HP", ...) at creation and nothing else is watched — every NPC's HP
-//      Sets fire callbacks, no record callbacks, no managers handed out.
+//      Sets fire callbacks, no record callbacks, no managers handed out;
+//  16  only EXP watched (every object): with the set_ops programs, EXP's Sets in Poison depend on what the
+//      earlier schedule names Patrol (SP, Camp) and HPRegen (HP) left in the same walk, kinds that write
+//      no watched property themselves (the per-Set log must re-run them too).
 //
 // Logged per frame t: per-object property and record callbacks with the phase they fired in (0 =
 // the window's calls, 1 = Execute), the heartbeat functors, Tutorial3's callback lines, the kills and
@@ -167,6 +170,10 @@ struct Logic {
         return 0;
     }
     void Watch(const NFGUID& g, bool npc) {
+        if (mode & 16) {
+            km->AddPropertyCallBack(g, "EXP", this, &Logic::OnObjProp);
+            return;
+        }
         if (mode & 8) {  // NFCNPCRefreshModule.cpp:104: the NPCs' HP, nothing else
             if (npc) {
                 km->AddPropertyCallBack(g, "HP", this, &Logic::OnObjProp);

@@ -48,10 +48,10 @@ def _world(seed, n_obj=1200, n_ticks=12, lethal=False, set_ops=False, logic_mode
     return w
 
 
-def _run(exe, w, tmp_path, tag):
+def _run(exe, w, tmp_path, tag, env=None):
     wp, op = str(tmp_path / f"{tag}_w.nfio"), str(tmp_path / f"{tag}_o.nfio")
     nfio.write(wp, w)
-    subprocess.run([exe, wp, op], check=True, timeout=600)
+    subprocess.run([exe, wp, op], check=True, timeout=600, env=None if env is None else {**os.environ, **env})
     return nfio.read(op)
 
 
@@ -171,15 +171,17 @@ def test_logic_session_reference_components_destroy(tmp_path):
 # seed 74: the set_ops programs (assignments, guards against 0 and against another int property)
 # seed 75: logic_mode 1 | 2 | 4 — cross-object functor reads answered in walk order, components destroying
 # objects (their own deferred), with lethal Poison
+# seed 78: logic_mode 16 — only EXP watched with the set_ops programs: the per-Set log re-runs the earlier kinds
+# whose writes a watched Set reads (Patrol's SP / Camp, HPRegen's HP before Poison's EXP ops)
 @pytest.mark.parametrize("seed,lethal,set_ops,mode", [(71, False, False, 0), (72, False, False, 0), (73, True, False, 0),
-                                                      (74, False, True, 0), (75, True, False, 7)])
+                                                      (74, False, True, 0), (75, True, False, 7), (78, False, True, 16)])
 def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, seed, lethal, set_ops, mode):
     if not (os.path.exists(GPU_EXE) and os.path.exists(REF_EXE)):
         pytest.skip("logic_session not built (needs /root/reference at build time)")
     w = _world(seed, lethal=lethal, set_ops=set_ops, logic_mode=mode)
     got, ref = _run(GPU_EXE, w, tmp_path, "gpu"), _run(REF_EXE, w, tmp_path, "ref")
     nt = int(w["cfg"][7])
-    if mode:
+    if mode & 7:
         n_xr = 0
         for t in range(nt):
             assert _lines(got, f"k_t{t}_comp") == _lines(ref, f"k_t{t}_comp"), t
@@ -212,8 +214,11 @@ def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, see
                 n_obj_cb += len(g[0]) + len(g[1])
             else:
                 n_rec_cb += len(g[0]) + len(g[1])
-    assert n_obj_cb > 1000 and n_rec_cb > 100, (n_obj_cb, n_rec_cb)
+    assert n_obj_cb > (300 if mode & 16 else 1000) and (n_rec_cb > 100 or mode & 16), (n_obj_cb, n_rec_cb)
     assert n_kills > 20 or not lethal, n_kills
+    if mode & 16:  # the seed exercises the dependency: the log of the watched kinds alone differs
+        bad = _run(GPU_EXE, w, tmp_path, "gpu_noclosure", env={"NFGPU_CHAIN_NO_CLOSURE": "1"})
+        assert any(_chains(bad, t, "pc", "pid")[1] != _chains(ref, t, "pc", "pid")[1] for t in range(nt))
 
 
 @pytest.mark.gpu
