@@ -278,6 +278,9 @@ struct World {
     // checked before anything reads or replaces that frame's fan-out (check_fanout)
     bool fan_unchecked = false;
     unsigned* err_pin = nullptr;
+    // pinned landing area of the frame's control block and byte tallies (read_ctrl / read_ctrl_tallies:
+    // asynchronous copies behind the frame and one stream synchronisation, not two synchronous copies)
+    char* ctrl_pin = nullptr;
     hipEvent_t err_done = nullptr;
     int32_t max_np = 0;    // most players in one scene group (an upper bound between full re-layouts)
     // per-Set chains of the watched properties (nfk_watch_props, k_chain): the watch mask, the log
@@ -449,6 +452,9 @@ int lookup(World* w, int64_t h, int64_t d, int32_t* obj) {
 }
 
 // accumulated algorithmic-byte tallies of k_tick, k_records, k_fanout
+constexpr size_t kTallyBytes = (size_t)3 * kTallyN * 8 * 8;  // (the tallies' 64-byte spread slots)
+constexpr size_t kCtrlPinTally = (sizeof(Ctrl) + 255) & ~(size_t)255;
+constexpr size_t kCtrlPinBytes = kCtrlPinTally + kTallyBytes;
 int read_tallies(World* w, uint64_t out[3]) {
     std::vector<unsigned long long> t((size_t)3 * kTallyN * 8);
     HIPCHK(hipMemcpy(t.data(), w->d.tally, t.size() * 8, hipMemcpyDeviceToHost));
@@ -1678,6 +1684,7 @@ int nfk_create(const nfk_config* cfg, void** out) {
         hipEventCreateWithFlags(&w->mpin_done[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&w->err_done, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&w->err_pin, 64, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&w->ctrl_pin, kCtrlPinBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&w->err_host, 64, hipHostMallocMapped) != hipSuccess ||
         hipHostGetDevicePointer((void**)&w->err_host_d, w->err_host, 0) != hipSuccess) {
         delete w;
@@ -1739,6 +1746,7 @@ int nfk_destroy(void* world) {
     if (w->pin_done) (void)hipEventDestroy(w->pin_done);
     if (w->err_done) (void)hipEventDestroy(w->err_done);
     if (w->err_pin) (void)hipHostFree(w->err_pin);
+    if (w->ctrl_pin) (void)hipHostFree(w->ctrl_pin);
     if (w->err_host) (void)hipHostFree(w->err_host);
     for (int i = 0; i < 2; i++) {
         if (w->mpin_done[i]) (void)hipEventDestroy(w->mpin_done[i]);
@@ -4002,8 +4010,25 @@ static int ensure_ranks(World* w) {
 static int read_ctrl(World* w, Ctrl* c) {
     int r = ensure_ranks(w);
     if (r) return r;
+    HIPCHK(hipMemcpyAsync(w->ctrl_pin, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, w->stream));
     HIPCHK(hipStreamSynchronize(w->stream));
-    HIPCHK(hipMemcpy(c, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+    memcpy(c, w->ctrl_pin, sizeof(Ctrl));
+    return NFK_OK;
+}
+// the control block and the byte tallies (read_tallies) behind the frame, one synchronisation
+static int read_ctrl_tallies(World* w, Ctrl* c, uint64_t tb[3]) {
+    int r = ensure_ranks(w);
+    if (r) return r;
+    char* tp = w->ctrl_pin + kCtrlPinTally;
+    HIPCHK(hipMemcpyAsync(w->ctrl_pin, w->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipMemcpyAsync(tp, w->d.tally, kTallyBytes, hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    memcpy(c, w->ctrl_pin, sizeof(Ctrl));
+    const unsigned long long* t = (const unsigned long long*)tp;
+    for (int k = 0; k < 3; k++) {
+        tb[k] = 0;
+        for (int i = 0; i < kTallyN; i++) tb[k] += t[((size_t)k * kTallyN + i) * 8];
+    }
     return NFK_OK;
 }
 
@@ -4065,12 +4090,13 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     if (!w || !out) return fail(NFK_ERR_ARG, "null argument");
     if (!w->committed) return fail(NFK_ERR_STATE, "commit first");
     Ctrl c;
+    uint64_t tb[3];
     {
         int r = check_fanout(w);
         if (r) return r;
     }
     {
-        int r = read_ctrl(w, &c);
+        int r = read_ctrl_tallies(w, &c, tb);
         if (r) return r;
     }
     memset(out, 0, sizeof *out);
@@ -4084,9 +4110,6 @@ int nfk_summary_get(void* world, nfk_summary* out) {
     out->n_fired = (int64_t)c.n_fi;
     out->n_msgs = frame_msgs(w, c);
     {
-        uint64_t tb[3];
-        int r = read_tallies(w, tb);
-        if (r) return r;
         out->alg_bytes_tick = (int64_t)(tb[0] - w->last_bytes[0]);
         out->alg_bytes_rec = (int64_t)(tb[1] - w->last_bytes[1]);
         out->alg_bytes_fan = (int64_t)(tb[2] - w->last_bytes[2]);
