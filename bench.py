@@ -385,8 +385,10 @@ def main():
     # (--self-migrate: the migration path on one rank, its rows sent to itself — a host-cost
     # rehearsal of config[2] on one GPU; never the headline line)
     migrating = (world > 1 or args.self_migrate) and args.migrate > 0 and args.config == 1
-    # config[1] has no membership changes: no slack slots; config[2] keeps 32 per 256 for arrivals
-    slack = args.slack if args.slack is not None else (32 if migrating else -1)
+    # config[1] has no membership changes: no slack slots; config[2] keeps 8 per 256 for arrivals (its
+    # arrivals land in random groups, ~0.06 per group and exchange; a segment out of slack rebuilds the
+    # table with fresh slack.  32 per 256 cost k_tick 7 us of dead slots: profiles/r17e_selfmig_slack.txt)
+    slack = args.slack if args.slack is not None else (8 if migrating else -1)
     m = kernel.world_from_workload(w, stream=stream.cuda_stream, slack_per_256=slack)
     t0 = int(w["tick_time"][0])
     tick = 0

@@ -95,6 +95,9 @@ struct World {
         int32_t scene, group, base, cap;
         int32_t np = 0;             // players among objs (set by seg_meta)
         std::vector<int32_t> objs;  // live objects, NFGUID order
+        // their NFGUIDs, beside them: a joiner's place is binary-searched in this contiguous array
+        // instead of through guid[objs[i]] (one random host read per probe, ~8 per joiner)
+        std::vector<Guid> keys;
     };
     std::vector<Seg> segs;
     std::vector<uint64_t> seg_key;  // each segment's (scene, group) as seg_key_of gives it: ascending
@@ -263,6 +266,7 @@ struct World {
 
     // k_tick specialised to this world's schema (nfgpu_jit.hpp); null: the generic instantiations
     hipFunction_t jit_fn = nullptr;
+    hipFunction_t jit_chain_fn = nullptr;  // k_chain_u on the same policy
     int jit_waves = 0, jit_u = 0;
     bool jit_lb = false;  // the specialisation keeps k_tick's in-kernel ranks (a world of <= kLbMaxTiles tiles)
     std::string jit_msg = "not compiled";
@@ -548,6 +552,8 @@ int64_t plan_segments(World* w, int32_t slack, std::vector<World::Seg>& segs) {
         g.group = w->group[o];
         g.base = (int32_t)std::min<int64_t>(base, INT32_MAX);
         g.objs.assign(objs.begin() + i, objs.begin() + j);
+        g.keys.resize(g.objs.size());
+        for (size_t k = 0; k < g.objs.size(); k++) g.keys[k] = w->guid[g.objs[k]];
         g.cap = (int32_t)g.objs.size() + seg_slack(slack, (int32_t)g.objs.size());
         base += g.cap;
         segs.push_back(std::move(g));
@@ -1044,10 +1050,11 @@ constexpr uint32_t kJitNtDefault = kNtSchedLoad | kNtFanStore;
 // Specialised k_tick kernels built in this process, by (device, variant, policy source): a
 // schema compiles once however many worlds use it.
 std::mutex g_jit_mu;
-std::map<std::string, hipFunction_t> g_jit;
+std::map<std::string, std::pair<hipFunction_t, hipFunction_t>> g_jit;  // (k_tick, k_chain_u)
 
 void build_jit(World* w) {
     w->jit_fn = nullptr;
+    w->jit_chain_fn = nullptr;
     const char* env = getenv("NFGPU_JIT");
     if (env && env[0] == '0') {
         w->jit_msg = "disabled (NFGPU_JIT=0)";
@@ -1082,15 +1089,17 @@ void build_jit(World* w) {
     if (it == g_jit.end()) {
         JitBuild b = jit_compile(src, waves, u);
         hipModule_t mod = nullptr;
-        hipFunction_t fn = nullptr;
+        hipFunction_t fn = nullptr, cfn = nullptr;
         if (!b.ok || hipModuleLoadData(&mod, b.code.data()) != hipSuccess ||
-            hipModuleGetFunction(&fn, mod, b.lowered.c_str()) != hipSuccess) {
+            hipModuleGetFunction(&fn, mod, b.lowered.c_str()) != hipSuccess ||
+            hipModuleGetFunction(&cfn, mod, b.lowered_chain.c_str()) != hipSuccess) {
             w->jit_msg = "hipRTC build failed: " + b.log.substr(0, 2000);
             return;
         }
-        it = g_jit.emplace(key, fn).first;
+        it = g_jit.emplace(key, std::make_pair(fn, cfn)).first;
     }
-    w->jit_fn = it->second;
+    w->jit_fn = it->second.first;
+    w->jit_chain_fn = it->second.second;
     w->jit_lb = lb;
     w->jit_waves = waves;
     w->jit_u = u;
@@ -1216,6 +1225,7 @@ int plan_membership(World* w, MemPlan& p) {
             x.join.clear();
             x.ins.clear();
             x.seg.objs.clear();
+            x.seg.keys.clear();
             epos[g] = (int32_t)p.n_einfo++;
             aff.push_back(g);
         }
@@ -1249,7 +1259,9 @@ int plan_membership(World* w, MemPlan& p) {
         std::sort(x.rem.begin(), x.rem.end());
         std::sort(x.join.begin(), x.join.end(), cmp);
         std::vector<int32_t>& v = x.seg.objs;
+        std::vector<World::Guid>& kv = x.seg.keys;
         v.reserve(old.objs.size() - x.rem.size() + x.join.size());
+        kv.reserve(v.capacity());
         // (a joiner's place is searched in the old list, leavers included: they are still in
         // NFGUID order, and one that rejoins compares equal to itself and is skipped below)
         size_t r = 0, at = 0;
@@ -1260,12 +1272,16 @@ int plan_membership(World* w, MemPlan& p) {
                     continue;
                 }
                 v.push_back(old.objs[at]);
+                kv.push_back(old.keys[at]);
             }
         };
+        const auto key_less = [](const World::Guid& a, const World::Guid& b) { return a.h != b.h ? a.h < b.h : a.d < b.d; };
         for (int32_t o : x.join) {
-            copy_to((size_t)(std::lower_bound(old.objs.begin() + at, old.objs.end(), o, cmp) - old.objs.begin()));
+            const World::Guid go = w->guid[o];
+            copy_to((size_t)(std::lower_bound(old.keys.begin() + at, old.keys.end(), go, key_less) - old.keys.begin()));
             x.ins.push_back({(int32_t)v.size(), o});
             v.push_back(o);
+            kv.push_back(go);
         }
         copy_to(old.objs.size());
         if ((int32_t)v.size() > old.cap) full = true;
@@ -1344,6 +1360,8 @@ int plan_membership(World* w, MemPlan& p) {
             g.scene = fit->first.first;
             g.group = fit->first.second;
             g.objs = std::move(fit->second);
+            g.keys.resize(g.objs.size());
+            for (size_t k = 0; k < g.objs.size(); k++) g.keys[k] = w->guid[g.objs[k]];
             nsegs.push_back(std::move(g));
             nsrc.push_back(-1);
             nold.push_back(-1);
@@ -1358,7 +1376,10 @@ int plan_membership(World* w, MemPlan& p) {
             World::Seg g;
             g.scene = old.scene;
             g.group = old.group;
-            if (edited) g.objs = std::move(einfo[epos[gi]].seg.objs);
+            if (edited) {
+                g.objs = std::move(einfo[epos[gi]].seg.objs);
+                g.keys = std::move(einfo[epos[gi]].seg.keys);
+            }
             nsegs.push_back(std::move(g));
             nsrc.push_back(edited ? -1 : gi);
             nold.push_back(edited ? gi : -1);
@@ -1530,6 +1551,7 @@ int commit_membership(World* w, MemPlan& p) {
                 seg_base0[i] = w->segs[nsrc[i]].base;
                 seg_cap0[i] = w->segs[nsrc[i]].cap;
                 nsegs[i].objs = std::move(w->segs[nsrc[i]].objs);
+                nsegs[i].keys = std::move(w->segs[nsrc[i]].keys);
             }
         w->segs = std::move(nsegs);
         index_segs(w);
@@ -1547,6 +1569,7 @@ int commit_membership(World* w, MemPlan& p) {
         w->n_relayout_seg++;
         for (int32_t gi : aff) {  // (the old list's buffer goes back to the plan, for the next window)
             std::swap(w->segs[gi].objs, einfo[epos[gi]].seg.objs);
+            std::swap(w->segs[gi].keys, einfo[epos[gi]].seg.keys);
             w->segs[gi].np = einfo[epos[gi]].seg.np;
         }
     }
@@ -3843,8 +3866,25 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
             }
             w->chain_tcap = tcap;
             TimeScope ts(w, KT_CHAIN);
-            hipLaunchKernelGGL(k_chain, dim3((unsigned)nt), dim3(kTPB), 0, w->stream, d, w->chain_d, w->chain_cnt_d, tcap,
-                               kinds, w->chain_watch[0], w->chain_watch[1]);
+            // on the frame's register working set (the world's hipRTC policy, or the library's tables),
+            // else on k_tick_touch's written-property list (NFGPU_CHAIN_U=0 forces that one, for A/B)
+            static const bool chain_u = !getenv("NFGPU_CHAIN_U") || getenv("NFGPU_CHAIN_U")[0] != '0';
+            ChainEnt* cd = (ChainEnt*)w->chain_d;
+            uint32_t* cc = w->chain_cnt_d;
+            uint64_t w0 = w->chain_watch[0], w1 = w->chain_watch[1];
+            if (chain_u && use_u && w->jit_chain_fn) {
+                void* args[] = {&d, &cd, &cc, (void*)&tcap, &kinds, &w0, &w1};
+                HIPCHK(hipModuleLaunchKernel(w->jit_chain_fn, (unsigned)nt, 1, 1, kTPB, 1, 1, 0, w->stream, args, nullptr));
+            } else if (chain_u && use_u && d.n_u <= 8) {
+                hipLaunchKernelGGL((k_chain_u<8, DynSchema>), dim3((unsigned)nt), dim3(kTPB), 0, w->stream, d, cd, cc, tcap, kinds, w0, w1);
+            } else if (chain_u && use_u && d.n_u <= 12) {
+                hipLaunchKernelGGL((k_chain_u<12, DynSchema>), dim3((unsigned)nt), dim3(kTPB), 0, w->stream, d, cd, cc, tcap, kinds, w0, w1);
+            } else if (chain_u && use_u) {
+                hipLaunchKernelGGL((k_chain_u<16, DynSchema>), dim3((unsigned)nt), dim3(kTPB), 0, w->stream, d, cd, cc, tcap, kinds, w0, w1);
+            } else {
+                hipLaunchKernelGGL(k_chain, dim3((unsigned)nt), dim3(kTPB), 0, w->stream, d, w->chain_d, w->chain_cnt_d, tcap,
+                                   kinds, w->chain_watch[0], w->chain_watch[1]);
+            }
             HIPCHK(hipGetLastError());
             w->chain_ran = true;
             w->chain_tiles = nt;

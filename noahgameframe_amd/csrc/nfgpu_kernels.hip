@@ -757,13 +757,7 @@ __global__ __launch_bounds__(kTPB) void k_tick_touch(Dev d) {
 // thread's own in program order, the threads' placed by a block scan of their counts (the programs
 // run twice: count, then write) — and t_cnt[t] of them; no atomics, so the log is deterministic.
 // nfk_read_chain compacts it and sorts it into the walk's (NFGUID, kind, op) order on the device.
-struct ChainEnt {
-    uint32_t slot;
-    uint16_t pid;
-    uint8_t kind, op;
-    uint64_t old_bits, new_bits;
-};
-static_assert(sizeof(ChainEnt) == 24, "ChainEnt is read back as 24-byte records");
+// (ChainEnt: nfgpu_tick.hpp)
 __global__ __launch_bounds__(kTPB) void k_chain(Dev d, ChainEnt* __restrict__ out, uint32_t* __restrict__ t_cnt,
                                                 uint32_t tcap, uint32_t kinds, uint64_t watch0, uint64_t watch1) {
     __shared__ uint64_t s_old[NFK_MAX_TOUCH * kTPB];  // (Ent's frame-start list; unused here)

@@ -63,12 +63,17 @@ __device__ __forceinline__ void uput(uint64_t (&v)[kU], uint32_t j, uint64_t x) 
 #undef NFK_C
     }
 }
+// An accepted Set of a program op, as (kind, op index, U slot, old bits, new bits): k_chain_u's log
+// hook; k_tick passes this empty one, which compiles away.
+struct NoSetLog {
+    __device__ __forceinline__ void operator()(int, int, uint32_t, uint64_t, uint64_t) const {}
+};
 // The fired kinds' programs in schedule-name order on the register working set.  A Set that
 // fails the reference's change predicate leaves the value as it was; wm collects the slots a
 // Set changed at least once.
-template <int kU>
+template <int kU, class Log = NoSetLog>
 __device__ __forceinline__ void run_programs_u(uint64_t (&v)[kU], uint32_t& wm, const Tables* __restrict__ tab_,
-                                               uint32_t fired, int n_kind, uint32_t n_w) {
+                                               uint32_t fired, int n_kind, uint32_t n_w, const Log& log = Log()) {
     CTables* tab = ctab(tab_);
     for (int k = 0; k < n_kind; k++) {
         if (!((fired >> k) & 1)) continue;
@@ -92,6 +97,7 @@ __device__ __forceinline__ void run_programs_u(uint64_t (&v)[kU], uint32_t& wm, 
                 r = r > hi ? hi : r;
                 uput(v, u0, (uint64_t)r);  // NFCProperty::SetInt (PR:273): r == cur changes nothing
                 wm |= (r != cur) ? (1u << u0) : 0u;
+                if (r != cur) log(k, i, u0, (uint64_t)cur, (uint64_t)r);
             } else if (code == NFK_OP_FLERP || code == NFK_OP_FAFFINE) {
                 const uint64_t xb = uget(v, u0);
                 const double x = __longlong_as_double((long long)xb);
@@ -108,11 +114,13 @@ __device__ __forceinline__ void run_programs_u(uint64_t (&v)[kU], uint32_t& wm, 
                 const bool set = !(fabs(r - x) <= 1e-15);  // NFCProperty::SetFloat (PR:314): IsZeroDouble(v - cur)
                 uput(v, u0, set ? (uint64_t)__double_as_longlong(r) : xb);
                 wm |= set ? (1u << u0) : 0u;
+                if (set) log(k, i, u0, xb, (uint64_t)__double_as_longlong(r));
             } else if (code == NFK_OP_ISET) {
                 const uint64_t cur = uget(v, u0);
                 const uint64_t r = (flags & NFK_A_PROP) ? uget(v, u1) : (uint64_t)tab->opx[k][i].a;
                 uput(v, u0, r);  // NFCProperty::SetInt (PR:273): r == cur changes nothing
                 wm |= (r != cur) ? (1u << u0) : 0u;
+                if (r != cur) log(k, i, u0, cur, r);
             } else if (code == NFK_OP_FSET) {
                 const uint64_t xb = uget(v, u0);
                 const uint64_t rb = (flags & NFK_A_PROP) ? uget(v, u1) : (uint64_t)tab->opx[k][i].a;
@@ -120,6 +128,7 @@ __device__ __forceinline__ void run_programs_u(uint64_t (&v)[kU], uint32_t& wm, 
                 const bool set = !(fabs(r - x) <= 1e-15);  // NFCProperty::SetFloat (PR:314)
                 uput(v, u0, set ? rb : xb);
                 wm |= set ? (1u << u0) : 0u;
+                if (set) log(k, i, u0, xb, rb);
             }
             // record ops run in k_records
         }
@@ -201,9 +210,9 @@ struct DynSchema {
             }
         return need;
     }
-    template <int kU>
-    __device__ static void run(uint64_t (&v)[kU], uint32_t& wm, const Dev& d, uint32_t fired) {
-        run_programs_u(v, wm, d.tab, fired, d.n_kind, d.n_w);
+    template <int kU, class Log = NoSetLog>
+    __device__ static void run(uint64_t (&v)[kU], uint32_t& wm, const Dev& d, uint32_t fired, const Log& log = Log()) {
+        run_programs_u(v, wm, d.tab, fired, d.n_kind, d.n_w, log);
     }
 };
 
@@ -880,6 +889,69 @@ __global__ __launch_bounds__(kTPB) __attribute__((amdgpu_waves_per_eu(kWPE, 8)))
     extern __shared__ __align__(16) uint64_t s_o[];  // [n_w][kTPB] frame-start values of the writable slots
     const int tile = d.xcd_map ? xcd_tile((int)blockIdx.x, d.n_tiles) : (int)blockIdx.x;
     tick_tile<kU, S>(d, tile, s_w, s_bytes, s_lb_last, s_pb, s_o);
+}
+
+
+// ---------------------------------------------------------------------------------
+// The per-Set log of the watched properties (nfk_watch_props; see k_chain in nfgpu_kernels.hip) on
+// the frame's register working set, under the world's schema policy: the fire test without its
+// stores, the operand loads and the fired kinds' programs exactly as k_tick runs them (its hipRTC
+// specialisation's straight-line programs, or the library's tables), on the values k_sets left,
+// before k_tick.  The programs run twice on register copies — count the watched Sets, then write
+// them at their places from a block scan — so the log is tile-staged in (slot, kind, op) order with
+// no atomics: tile t's entries at t * tcap, t_cnt[t] of them.
+struct ChainEnt {
+    uint32_t slot;
+    uint16_t pid;
+    uint8_t kind, op;
+    uint64_t old_bits, new_bits;
+};
+static_assert(sizeof(ChainEnt) == 24, "ChainEnt is read back as 24-byte records");
+
+template <int kU, class S>
+__global__ __launch_bounds__(kTPB) void k_chain_u(Dev d, ChainEnt* __restrict__ out, uint32_t* __restrict__ t_cnt,
+                                                  uint32_t tcap, uint32_t kinds, uint64_t watch0, uint64_t watch1) {
+    __shared__ unsigned long long s_w[kTPB / 64];
+    const int e = blockIdx.x * kTPB + (int)threadIdx.x;
+    uint32_t fired = 0;
+    uint64_t v[kU];
+#pragma unroll
+    for (int j = 0; j < kU; j++) v[j] = 0;
+    if (e < d.N) {
+        unsigned bytes = 0;
+        uint64_t desc = kDeadDesc;
+        fired = sched_scan<S, false>(d, e, bytes, desc) & kinds;
+        if (desc_dead(desc)) fired = 0;
+    }
+    if (fired) {
+        const uint32_t need = S::need(d, fired);
+#pragma unroll
+        for (int j = 0; j < kU; j++)
+            if ((need >> j) & 1) v[j] = *elem<S>(d.u_col[j], (uint32_t)e, S::u_str(d, j));
+    }
+    const auto watched = [&](uint32_t u) {
+        const uint32_t p = (uint32_t)S::u_pid(d, (int)u);
+        return ((p < 64 ? watch0 >> p : watch1 >> (p - 64)) & 1ull) != 0;
+    };
+    uint32_t cnt = 0;
+    if (fired) {
+        uint64_t c[kU];
+#pragma unroll
+        for (int j = 0; j < kU; j++) c[j] = v[j];
+        uint32_t wm = 0;
+        S::run(c, wm, d, fired, [&](int, int, uint32_t u, uint64_t, uint64_t) { cnt += watched(u) ? 1u : 0u; });
+    }
+    unsigned long long tot;
+    uint32_t at = (uint32_t)block_excl_scan(cnt, s_w, tot);
+    if (cnt) {
+        ChainEnt* t_out = out + (size_t)blockIdx.x * tcap;
+        uint32_t wm = 0;
+        S::run(v, wm, d, fired, [&](int k, int i, uint32_t u, uint64_t o, uint64_t n) {
+            if (watched(u) && at < tcap)
+                t_out[at++] = ChainEnt{(uint32_t)e, (uint16_t)S::u_pid(d, (int)u), (uint8_t)k, (uint8_t)i, o, n};
+        });
+    }
+    if (threadIdx.x == 0) t_cnt[blockIdx.x] = (uint32_t)tot;
 }
 
 }  // namespace nfgpu

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <condition_variable>
 #include <cstring>
@@ -286,6 +287,11 @@ int SceneShard::Rows(const std::vector<int64_t>& plan, std::vector<Ticket>* sent
         k.dst = (int32_t)w[10];
         return k;
     };
+    // (NFGPU_TRACE_SHARD=1: this exchange's host phases on stderr)
+    static const bool trace = getenv("NFGPU_TRACE_SHARD") != nullptr;
+    using clk = std::chrono::steady_clock;
+    clk::time_point tp[6];
+    tp[0] = clk::now();
     std::vector<Ticket> snd, rcv;
     for (size_t i = 0; i < n; i++) {
         const Ticket k = tk(i);
@@ -327,6 +333,7 @@ int SceneShard::Rows(const std::vector<int64_t>& plan, std::vector<Ticket>* sent
         status = nfk_export_objects(world_, (int32_t)snd.size(), gh.data(), gd.data(), sbuf_);
     }
     if (!status && t_->NeedsHostSync()) status = nfk_sync(world_);
+    tp[1] = clk::now();
     // 2. every rank's status (collective): all ranks go on to the row exchange, or none does
     {
         std::vector<int64_t> mine(1, (int64_t)status), all;
@@ -336,10 +343,12 @@ int SceneShard::Rows(const std::vector<int64_t>& plan, std::vector<Ticket>* sent
         for (int64_t v : all)
             if (v) return status ? status : NFK_ERR_STATE;  // (a peer failed: its rows never come)
     }
+    tp[2] = clk::now();
     // 3. the rows, rank to rank (on the world's stream for RCCL)
     transport_calls++;
     int r = t_->AllToAllV(sbuf_, scount, rbuf_, rcount, stream_);
     if (r) return r;
+    tp[3] = tp[4] = clk::now();
     // 4. import, then the SwitchScene property writes (KM:930-942): GroupID = 0, SceneID, X, Y, Z,
     // GroupID, per entity in this order (the scene always changes here)
     if (!rcv.empty()) {
@@ -358,6 +367,7 @@ int SceneShard::Rows(const std::vector<int64_t>& plan, std::vector<Ticket>* sent
         r = nfk_import_objects(world_, (int32_t)m, gh.data(), gd.data(), sc.data(), gr.data(), cl.data(), pl.data(),
                                rbuf_);
         if (r) return r;
+        tp[4] = clk::now();
         std::vector<int64_t> wh, wd;
         std::vector<int32_t> wp;
         std::vector<uint64_t> wb;
@@ -381,6 +391,12 @@ int SceneShard::Rows(const std::vector<int64_t>& plan, std::vector<Ticket>* sent
             r = nfk_set_props(world_, (int32_t)wp.size(), wh.data(), wd.data(), wp.data(), wb.data());
             if (r) return r;
         }
+    }
+    if (trace) {
+        tp[5] = clk::now();
+        auto ms = [&](int a, int b) { return std::chrono::duration<double, std::milli>(tp[b] - tp[a]).count(); };
+        fprintf(stderr, "shard rows: %zu out %zu in: export %.3f ms, status gather %.3f ms, rows %.3f ms, import %.3f ms, "
+                "writes %.3f ms\n", snd.size(), rcv.size(), ms(0, 1), ms(1, 2), ms(2, 3), ms(3, 4), ms(4, 5));
     }
     migrated_out += (int64_t)snd.size();
     migrated_in += (int64_t)rcv.size();
