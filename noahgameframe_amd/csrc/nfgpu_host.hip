@@ -1174,6 +1174,7 @@ struct MemPlan {
     std::vector<int32_t> nsrc;      // full: nsegs[i] is untouched segment nsrc[i] (members kept), or -1
     int32_t mv_rows_dev = 0, mv_list_dev = 0, ed_rows = 0, ed_list = 0;
     std::chrono::steady_clock::time_point t_host, t_edit, t_lists;
+    std::chrono::steady_clock::time_point t_leave, t_join;  // (trace) the edit phase's parts
 };
 
 // Apply this window's membership changes (SwitchScene across groups, DestroyObject, exports,
@@ -1237,6 +1238,7 @@ int plan_membership(World* w, MemPlan& p) {
         const int32_t gi = seg_at(s);
         ed(gi).rem.push_back(s - w->segs[gi].base);  // members occupy [base, base + n) in NFGUID order
     }
+    p.t_leave = clk::now();
     for (int32_t o : w->touched) {
         if (!w->alive[o]) continue;
         const int32_t gi = find_seg(w, w->scene[o], w->group[o]);
@@ -1246,6 +1248,7 @@ int plan_membership(World* w, MemPlan& p) {
         }
         ed(gi).join.push_back(o);
     }
+    p.t_join = clk::now();
     // each new member list in one pass: the old list without its leavers (known by rank, no
     // NFGUID comparison), the joiners (sorted) spliced in at their binary-searched places
     for (int32_t g : aff) {
@@ -1265,14 +1268,17 @@ int plan_membership(World* w, MemPlan& p) {
         // (a joiner's place is searched in the old list, leavers included: they are still in
         // NFGUID order, and one that rejoins compares equal to itself and is skipped below)
         size_t r = 0, at = 0;
-        auto copy_to = [&](size_t p) {  // old ranks [at, p) without the leavers
-            for (; at < p; at++) {
+        auto copy_to = [&](size_t p) {  // old ranks [at, p) without the leavers, as runs (memcpy-speed copies)
+            while (at < p) {
                 if (r < x.rem.size() && x.rem[r] == (int32_t)at) {
                     r++;
+                    at++;
                     continue;
                 }
-                v.push_back(old.objs[at]);
-                kv.push_back(old.keys[at]);
+                const size_t e = (r < x.rem.size() && (size_t)x.rem[r] < p) ? (size_t)x.rem[r] : p;
+                v.insert(v.end(), old.objs.begin() + (std::ptrdiff_t)at, old.objs.begin() + (std::ptrdiff_t)e);
+                kv.insert(kv.end(), old.keys.begin() + (std::ptrdiff_t)at, old.keys.begin() + (std::ptrdiff_t)e);
+                at = e;
             }
         };
         const auto key_less = [](const World::Guid& a, const World::Guid& b) { return a.h != b.h ? a.h < b.h : a.d < b.d; };
@@ -1625,9 +1631,11 @@ int commit_membership(World* w, MemPlan& p) {
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     (full ? w->ms_relayout_full : w->ms_relayout_seg) += ms(p.t_host, p.t_lists) + ms(t_dev, t_end);
     if (getenv("NFGPU_TRACE_MEMBERSHIP"))
-        fprintf(stderr, "apply_membership %s: %zu touched, edit %.3f ms, lists %.3f ms (%zu edited segments, %zu moves; "
+        fprintf(stderr, "apply_membership %s: %zu touched, edit %.3f ms (leavers %.3f, joiners %.3f, member lists %.3f), "
+                "lists %.3f ms (%zu edited segments, %zu moves; "
                 "before the previous frame is waited for), upload+launch %.3f ms, host maps %.3f ms\n",
-                full ? "full" : "seg", n_touched, ms(p.t_host, p.t_edit), ms(p.t_edit, p.t_lists), edits.size(),
+                full ? "full" : "seg", n_touched, ms(p.t_host, p.t_edit), ms(p.t_host, p.t_leave), ms(p.t_leave, p.t_join),
+                ms(p.t_join, p.t_edit), ms(p.t_edit, p.t_lists), edits.size(),
                 moves.size(), ms(t_dev, t_launched), ms(t_launched, t_end));
     return NFK_OK;
 }
@@ -4543,15 +4551,16 @@ int nfk_read_frame(void* world, uint32_t what, nfk_frame_host* o) {
     const unsigned gt = (unsigned)std::max(1, std::min(d.n_tiles, 4096));
     const unsigned grt = (unsigned)std::max(1, std::min(d.n_rtiles, 4096));
     const int32_t* so = w->slot_obj_d;
+    // the fired list's destination: dense, or the sort's unsorted copies
+    int32_t* const fo = (int32_t*)(order ? S + s_f : D + o_fo);
+    int32_t* const fk = (int32_t*)(order ? S + s_f + ((nf * 4 + 255) & ~(size_t)255) : D + o_fk);
+    int32_t* const fr = (int32_t*)(order ? S + s_f + 2 * ((nf * 4 + 255) & ~(size_t)255) : D + o_fr);
+    // events and fired list of the property tiles in one launch (k_compact_frame)
+    if (ne || nf)
+        hipLaunchKernelGGL(k_compact_frame, dim3(gt), dim3(kTPB), 0, w->stream, d, so,
+                           ne ? (int32_t*)(D + o_eo) : nullptr, (uint32_t*)(D + o_ep), (uint64_t*)(D + o_eold),
+                           (uint64_t*)(D + o_enew), nf ? fo : nullptr, (uint32_t*)fk, fr);
     if (ne) {
-        hipLaunchKernelGGL(k_compact_obj, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_slot, (int32_t*)(D + o_eo),
-                           d.ev_base, d.n_tiles, d.ev_tcap, so);
-        hipLaunchKernelGGL(k_compact<uint32_t>, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_pid, (uint32_t*)(D + o_ep),
-                           d.ev_base, d.n_tiles, d.ev_tcap);
-        hipLaunchKernelGGL(k_compact<uint64_t>, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_old, (uint64_t*)(D + o_eold),
-                           d.ev_base, d.n_tiles, d.ev_tcap);
-        hipLaunchKernelGGL(k_compact<uint64_t>, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_new, (uint64_t*)(D + o_enew),
-                           d.ev_base, d.n_tiles, d.ev_tcap);
         if (heads) {
             hipLaunchKernelGGL(k_compact_h, dim3(gt), dim3(kTPB), 0, w->stream, d.ev_old_h, (uint64_t*)(D + o_eoh),
                                d.ev_pid, d.ev_base, d.n_tiles, d.ev_tcap, d.n_if);
@@ -4591,15 +4600,6 @@ int nfk_read_frame(void* world, uint32_t what, nfk_frame_host* o) {
         HIPCHK(hipMemsetAsync(D + o_mo, 0, 4, w->stream));
     }
     if (nf) {
-        int32_t* fo = (int32_t*)(order ? S + s_f : D + o_fo);
-        int32_t* fk = (int32_t*)(order ? S + s_f + ((nf * 4 + 255) & ~(size_t)255) : D + o_fk);
-        int32_t* fr = (int32_t*)(order ? S + s_f + 2 * ((nf * 4 + 255) & ~(size_t)255) : D + o_fr);
-        hipLaunchKernelGGL(k_compact_obj, dim3(gt), dim3(kTPB), 0, w->stream, d.fi_slot, fo, d.fi_base, d.n_tiles,
-                           d.fi_tcap, so);
-        hipLaunchKernelGGL(k_compact<uint32_t>, dim3(gt), dim3(kTPB), 0, w->stream, d.fi_kind, (uint32_t*)fk,
-                           d.fi_base, d.n_tiles, d.fi_tcap);
-        hipLaunchKernelGGL(k_compact<int32_t>, dim3(gt), dim3(kTPB), 0, w->stream, d.fi_remain, fr, d.fi_base,
-                           d.n_tiles, d.fi_tcap);
         if (order) {
             const unsigned g = (unsigned)((nf + kTPB - 1) / kTPB);
             uint64_t* k1 = (uint64_t*)(S + s_keys);

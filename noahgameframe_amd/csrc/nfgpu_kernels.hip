@@ -2046,6 +2046,36 @@ __global__ __launch_bounds__(kTPB) void k_compact_obj(const uint32_t* __restrict
         for (uint32_t i = threadIdx.x; i < n; i += kTPB) dst[b + i] = slot_obj[src[(size_t)t * tcap + i]];
     }
 }
+// the property tiles' events (object, property, old, new) and fired heartbeats (object, kind, remain)
+// in one launch: what four k_compact / k_compact_obj launches and three more do one array each
+// (a small world's read-back is launch-bound: config[0]).  A null destination skips its list.
+__global__ __launch_bounds__(kTPB) void k_compact_frame(Dev d, const int32_t* __restrict__ slot_obj,
+                                                        int32_t* __restrict__ eo, uint32_t* __restrict__ ep,
+                                                        uint64_t* __restrict__ eold, uint64_t* __restrict__ enew,
+                                                        int32_t* __restrict__ fo, uint32_t* __restrict__ fk,
+                                                        int32_t* __restrict__ fr) {
+    for (int t = blockIdx.x; t < d.n_tiles; t += gridDim.x) {
+        if (eo) {
+            const uint32_t b = d.ev_base[t], n = d.ev_base[t + 1] - b;
+            const size_t s0 = (size_t)t * d.ev_tcap;
+            for (uint32_t i = threadIdx.x; i < n; i += kTPB) {
+                eo[b + i] = slot_obj[d.ev_slot[s0 + i]];
+                ep[b + i] = d.ev_pid[s0 + i];
+                eold[b + i] = d.ev_old[s0 + i];
+                enew[b + i] = d.ev_new[s0 + i];
+            }
+        }
+        if (fo) {
+            const uint32_t b = d.fi_base[t], n = d.fi_base[t + 1] - b;
+            const size_t s0 = (size_t)t * d.fi_tcap;
+            for (uint32_t i = threadIdx.x; i < n; i += kTPB) {
+                fo[b + i] = slot_obj[d.fi_slot[s0 + i]];
+                fk[b + i] = d.fi_kind[s0 + i];
+                fr[b + i] = d.fi_remain[s0 + i];
+            }
+        }
+    }
+}
 // record events: the slot from the event word and its tile, the word in the host format
 __global__ __launch_bounds__(kTPB) void k_compact_rec(const uint32_t* __restrict__ src, int32_t* __restrict__ obj,
                                                       uint32_t* __restrict__ rrc, const uint32_t* __restrict__ base,
