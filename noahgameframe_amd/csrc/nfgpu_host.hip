@@ -1076,9 +1076,12 @@ void build_jit(World* w) {
     // non-temporal hints (kNt* bits of nfgpu_tick.hpp); NFGPU_JIT_NT overrides the default
     uint32_t nt = kJitNtDefault;
     if (const char* en = getenv("NFGPU_JIT_NT")) nt = (uint32_t)strtoul(en, nullptr, 0);
-    // a world whose capacity exceeds kLbMaxTiles tiles never ranks in k_tick: that code is compiled
-    // out of its specialisation (NFGPU_JIT_LB=1 keeps it, for A/B)
-    bool lb = ((int64_t)w->d.cap + kTile - 1) / kTile <= kLbMaxTiles;
+    // a world committed with more than kLbMaxTiles tiles does not rank in k_tick: that code is compiled
+    // out of its specialisation (NFGPU_JIT_LB=1 keeps it, for A/B).  By the slots in use, not the
+    // capacity: the drop-in reserves 1M slots whatever the world (Tutorial3's 10k objects rank in k_tick
+    // and skip k_scan_tiles); a world that grows past the bound later ranks by k_scan_tiles (Dev::lb_rank
+    // is decided per frame), one that shrinks below it keeps k_scan_tiles with this code compiled out
+    bool lb = ((int64_t)std::max(w->d.N, 1) + kTile - 1) / kTile <= kLbMaxTiles;
     if (const char* el = getenv("NFGPU_JIT_LB")) lb = el[0] == '1';
     const std::string src = jit_schema_source(w->tab, w->d, spec, nt, lb);
     int dev = 0;

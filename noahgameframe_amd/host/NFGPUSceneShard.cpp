@@ -188,7 +188,12 @@ int SceneShard::BeginFrame(std::vector<Ticket>* sent, std::vector<Ticket>* recei
     if (sent) sent->clear();
     if (received) received->clear();
     if (!pending_.valid()) return NFK_OK;  // no gather since the last one: nothing to move
+    static const bool trace = getenv("NFGPU_TRACE_SHARD") != nullptr;
+    const auto tw = std::chrono::steady_clock::now();
     const int r = pending_.get();
+    if (trace)
+        fprintf(stderr, "shard begin: ticket gather waited %.3f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count());
     if (r) {
         failed_ = true;
         return r;

@@ -222,6 +222,27 @@ def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, see
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"NFGPU_JIT": "0"}, {"NFGPU_CHAIN_U": "0"}], ids=["library_chain_u", "touch_chain"])
+def test_logic_session_per_set_log_kernels(gpu_available, tmp_path, env):
+    """The per-Set log on its other kernels: k_chain_u over the library's DynSchema tables (NFGPU_JIT=0)
+    and the written-property-list k_chain (NFGPU_CHAIN_U=0) — the lethal-Poison seed's per-object callbacks
+    (HP 5 -> 0 -> 3 inside one program, the kills) and the EXP-only seed's dependency closure, equal to the
+    compiled reference as on the default hipRTC k_chain_u."""
+    if not (os.path.exists(GPU_EXE) and os.path.exists(REF_EXE)):
+        pytest.skip("logic_session not built (needs /root/reference at build time)")
+    for seed, lethal, set_ops, mode in ((73, True, False, 0), (78, False, True, 16)):
+        w = _world(seed, lethal=lethal, set_ops=set_ops, logic_mode=mode)
+        got, ref = _run(GPU_EXE, w, tmp_path, f"gpu{seed}", env=env), _run(REF_EXE, w, tmp_path, f"ref{seed}")
+        n = 0
+        for t in range(int(w["cfg"][7])):
+            g, r = _chains(got, t, "pc", "pid"), _chains(ref, t, "pc", "pid")
+            assert g[1] == r[1], (seed, t)
+            assert bytes(np.asarray(got[f"k_t{t}_kills"], np.uint8)) == bytes(np.asarray(ref[f"k_t{t}_kills"], np.uint8))
+            n += len(g[1])
+        assert n > 300, (seed, n)
+
+
+@pytest.mark.gpu
 def test_logic_session_cross_object_reads_divergence(gpu_available, tmp_path):
     """Without walk-order reads (the plugin's default) a heartbeat functor's read of another object's
     program-written property sees the frame's value — every object's device programs ran before the host
