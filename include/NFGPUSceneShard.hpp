@@ -134,6 +134,12 @@ private:
     int rank_, size_;
     int64_t* buf_ = nullptr;  // device staging of the ticket all-gather
     size_t buf_cap_ = 0;
+    // words of every rank's list gathered in the all-gather's first round, with its count: one
+    // collective and one synchronisation when no rank has more (a second round gathers the rest).
+    // It grows with the largest list seen (every rank sees the same lists: it is the same on all)
+    size_t w_first_ = 16;
+    int64_t* host_ = nullptr;  // pinned landing area of the gathers
+    size_t host_cap_ = 0;
 };
 
 class SceneShard {

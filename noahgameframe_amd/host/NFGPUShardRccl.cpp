@@ -70,6 +70,7 @@ void RcclTransport::Abort() {
 
 RcclTransport::~RcclTransport() {
     if (buf_) (void)hipFree(buf_);
+    if (host_) (void)hipHostFree(host_);
     if (!aborted_.load()) {  // (aborted communicators were released by ncclCommAbort)
         if (meta_comm_) (void)ncclCommDestroy((ncclComm_t)meta_comm_);
         if (comm_) (void)ncclCommDestroy((ncclComm_t)comm_);
@@ -84,32 +85,64 @@ int RcclTransport::AllGather(const std::vector<int64_t>& mine, std::vector<int64
     if (aborted_.load() || hipSetDevice(device_) != hipSuccess) return NFK_ERR_HIP;
     hipStream_t s = (hipStream_t)meta_stream_;
     auto reserve = [&](size_t words) {
-        if (words <= buf_cap_) return true;
-        if (buf_) (void)hipFree(buf_);
-        buf_cap_ = words + words / 2 + 64;
-        return hipMalloc((void**)&buf_, buf_cap_ * 8) == hipSuccess;
+        if (words > buf_cap_) {
+            if (buf_) (void)hipFree(buf_);
+            buf_ = nullptr;
+            buf_cap_ = words + words / 2 + 64;
+            if (hipMalloc((void**)&buf_, buf_cap_ * 8) != hipSuccess) return false;
+        }
+        if (words > host_cap_) {
+            if (host_) (void)hipHostFree(host_);
+            host_ = nullptr;
+            host_cap_ = words + words / 2 + 64;
+            if (hipHostMalloc((void**)&host_, host_cap_ * 8, hipHostMallocDefault) != hipSuccess) return false;
+        }
+        return true;
     };
-    if (!reserve((size_t)2 * size_)) return NFK_ERR_HIP;
+    // round 1: [count, the first W words] from every rank (W the same on every rank)
+    const size_t W = w_first_, R = 1 + W;
     const int64_t n = (int64_t)mine.size();
-    if (hipMemcpyAsync(buf_, &n, 8, hipMemcpyHostToDevice, s) != hipSuccess) return NFK_ERR_HIP;
-    if (ncclAllGather(buf_, buf_ + size_, 1, ncclInt64, (ncclComm_t)meta_comm_, s) != ncclSuccess) return NFK_ERR_HIP;
-    std::vector<int64_t> counts(size_);
-    if (hipMemcpyAsync(counts.data(), buf_ + size_, 8 * (size_t)size_, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    const size_t n1 = std::min((size_t)n, W);
+    if (!reserve(R * (1 + (size_t)size_))) return NFK_ERR_HIP;
+    host_[0] = n;
+    if (n1) memcpy(host_ + 1, mine.data(), n1 * 8);
+    if (n1 < W) memset(host_ + 1 + n1, 0, (W - n1) * 8);
+    if (hipMemcpyAsync(buf_, host_, R * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        ncclAllGather(buf_, buf_ + R, R, ncclInt64, (ncclComm_t)meta_comm_, s) != ncclSuccess ||
+        hipMemcpyAsync(host_ + R, buf_ + R, R * (size_t)size_ * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return NFK_ERR_HIP;
+    std::vector<int64_t> counts((size_t)size_);
     int64_t mx = 0;
-    for (int64_t c : counts) mx = std::max(mx, c);
+    for (int r = 0; r < size_; r++) {
+        counts[(size_t)r] = host_[R + (size_t)r * R];
+        mx = std::max(mx, counts[(size_t)r]);
+    }
+    std::vector<int64_t> first(host_ + R, host_ + R + R * (size_t)size_);  // (host_ is reused below)
     all.clear();
-    if (mx == 0) return NFK_OK;
-    if (aborted_.load() || !reserve((size_t)mx * (1 + size_))) return NFK_ERR_HIP;
-    if ((n && hipMemcpyAsync(buf_, mine.data(), (size_t)n * 8, hipMemcpyHostToDevice, s) != hipSuccess) ||
-        ncclAllGather(buf_, buf_ + mx, (size_t)mx, ncclInt64, (ncclComm_t)meta_comm_, s) != ncclSuccess)
-        return NFK_ERR_HIP;
-    std::vector<int64_t> padded((size_t)mx * size_);
-    if (hipMemcpyAsync(padded.data(), buf_ + mx, padded.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return NFK_ERR_HIP;
-    for (int r = 0; r < size_; r++) all.insert(all.end(), padded.begin() + (size_t)r * mx, padded.begin() + (size_t)r * mx + counts[r]);
+    if ((size_t)mx <= W) {
+        for (int r = 0; r < size_; r++)
+            all.insert(all.end(), first.begin() + (size_t)r * R + 1, first.begin() + (size_t)r * R + 1 + (size_t)counts[(size_t)r]);
+    } else {
+        // round 2: the words past W, padded to the largest remainder
+        const size_t T = (size_t)mx - W;
+        if (aborted_.load() || !reserve(T * (1 + (size_t)size_))) return NFK_ERR_HIP;
+        const size_t n2 = (size_t)n > W ? (size_t)n - W : 0;
+        if (n2) memcpy(host_, mine.data() + W, n2 * 8);
+        if (n2 < T) memset(host_ + n2, 0, (T - n2) * 8);
+        if (hipMemcpyAsync(buf_, host_, T * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+            ncclAllGather(buf_, buf_ + T, T, ncclInt64, (ncclComm_t)meta_comm_, s) != ncclSuccess ||
+            hipMemcpyAsync(host_ + T, buf_ + T, T * (size_t)size_ * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return NFK_ERR_HIP;
+        for (int r = 0; r < size_; r++) {
+            const size_t c = (size_t)counts[(size_t)r];
+            all.insert(all.end(), first.begin() + (size_t)r * R + 1, first.begin() + (size_t)r * R + 1 + std::min(c, W));
+            if (c > W) all.insert(all.end(), host_ + T + (size_t)r * T, host_ + T + (size_t)r * T + (c - W));
+        }
+    }
+    // the next first round holds this gather's largest list (up to 64k words, 512 KB per rank)
+    while (w_first_ < (size_t)mx && w_first_ < ((size_t)1 << 16)) w_first_ *= 2;
     return NFK_OK;
 }
 

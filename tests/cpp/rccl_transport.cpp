@@ -1,6 +1,6 @@
 // rccl_transport.cpp — the scene shards' RCCL transport (include/NFGPUSceneShard.hpp RcclTransport,
 // noahgameframe_amd/host/NFGPUShardRccl.cpp) run on the GPU at world size 1: the ticket all-gather
-// (count, then the padded rows) and the rows' grouped ncclSend / ncclRecv to the rank itself, on the
+// (the count and the first words in one round, the rest in a second when a list is longer) and the rows' grouped ncclSend / ncclRecv to the rank itself, on the
 // world's stream, device to device.  More ranks need more GPUs (the driver's 8-GPU run); this
 // checks the calls, buffers and stream handling one GPU can.
 // usage: rccl_transport        prints one JSON line; exit 0 when every check holds
@@ -24,7 +24,14 @@ int main() {
     fails += t.AllGather({}, all) != NFK_OK || !all.empty();
     std::vector<int64_t> mine(3 * kTicketWords);
     for (size_t i = 0; i < mine.size(); i++) mine[i] = (int64_t)(i * 7919 + 13) - 1000;
+    fails += t.AllGather(mine, all) != NFK_OK || all != mine;  // (33 words: past the first round's 16)
+    // the first round grows with the largest list: these fit it, then a longer one takes two rounds again
     fails += t.AllGather(mine, all) != NFK_OK || all != mine;
+    fails += t.AllGather({5}, all) != NFK_OK || all != std::vector<int64_t>{5};
+    std::vector<int64_t> big(300 * kTicketWords);
+    for (size_t i = 0; i < big.size(); i++) big[i] = (int64_t)(i * 104729 + 7);
+    fails += t.AllGather(big, all) != NFK_OK || all != big;
+    fails += t.AllGather(big, all) != NFK_OK || all != big;
     // rows: 4096 words to the rank itself through RCCL, on the stream
     const size_t n = 4096;
     std::vector<uint64_t> h(n), back(n, 0);
