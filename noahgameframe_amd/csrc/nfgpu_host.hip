@@ -4579,7 +4579,10 @@ int nfk_read_frame(void* world, uint32_t what, nfk_frame_host* o) {
         hipLaunchKernelGGL(k_compact<uint64_t>, dim3(grt), dim3(kTPB), 0, w->stream, d.re_new, (uint64_t*)(D + o_rnew),
                            d.re_base, d.n_rtiles, d.re_tcap);
     }
-    if (fan && ntt) {
+    if (fan && ntt && nm == 0) {
+        // (a frame without messages, e.g. Tutorial3's private World Sets: every offset is 0)
+        HIPCHK(hipMemsetAsync(D + o_mo, 0, (ne + nr + 1) * 4, w->stream));
+    } else if (fan && ntt) {
         uint32_t* db = (uint32_t*)(S + s_db);
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, w->stream, d.t_msg, db, ntt);
         // (tiles k_tick / k_records fanned out themselves store no offsets: counted here)
@@ -4603,7 +4606,11 @@ int nfk_read_frame(void* world, uint32_t what, nfk_frame_host* o) {
         HIPCHK(hipMemsetAsync(D + o_mo, 0, 4, w->stream));
     }
     if (nf) {
-        if (order) {
+        if (order && nf <= (size_t)kSmallSort) {
+            hipLaunchKernelGGL(k_fired_small, dim3(1), dim3(kSmallSort), 0, w->stream, (const int32_t*)fo,
+                               (const int32_t*)fk, (const int32_t*)fr, w->rank_d, (int32_t*)(D + o_fo),
+                               (int32_t*)(D + o_fk), (int32_t*)(D + o_fr), (int)nf);
+        } else if (order) {
             const unsigned g = (unsigned)((nf + kTPB - 1) / kTPB);
             uint64_t* k1 = (uint64_t*)(S + s_keys);
             uint64_t* k2 = (uint64_t*)(S + s_k2);

@@ -2206,6 +2206,30 @@ __global__ __launch_bounds__(kTPB) void k_fired_keys(const int32_t* __restrict__
     keys[i] = ((uint64_t)(uint32_t)rank[fobj[i]] << 5) | (uint64_t)fkind[i];
     idx[i] = (uint32_t)i;
 }
+// a small frame's fired list (n <= kSmallSort) into the walk's order in one launch: the keys are unique
+// ((object, kind) fires once a frame), so each entry's place is the count of smaller keys (what the
+// radix sort of k_fired_keys' keys and k_permute3 give, without their launches: config[0])
+constexpr int kSmallSort = 1024;
+__global__ __launch_bounds__(kSmallSort) void k_fired_small(const int32_t* __restrict__ fobj,
+                                                            const int32_t* __restrict__ fkind,
+                                                            const int32_t* __restrict__ frem,
+                                                            const int32_t* __restrict__ rank, int32_t* __restrict__ ao,
+                                                            int32_t* __restrict__ bo, int32_t* __restrict__ co, int n) {
+    __shared__ uint64_t sk[kSmallSort];
+    const int i = threadIdx.x;
+    uint64_t k = 0;
+    if (i < n) {
+        k = ((uint64_t)(uint32_t)rank[fobj[i]] << 5) | (uint64_t)fkind[i];
+        sk[i] = k;
+    }
+    __syncthreads();
+    if (i >= n) return;
+    int at = 0;
+    for (int j = 0; j < n; j++) at += sk[j] < k ? 1 : 0;
+    ao[at] = fobj[i];
+    bo[at] = fkind[i];
+    co[at] = frem[i];
+}
 __global__ __launch_bounds__(kTPB) void k_permute3(const uint32_t* __restrict__ idx, const int32_t* __restrict__ a,
                                                    const int32_t* __restrict__ b, const int32_t* __restrict__ c,
                                                    int32_t* __restrict__ ao, int32_t* __restrict__ bo,
