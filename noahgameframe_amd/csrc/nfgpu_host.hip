@@ -2971,7 +2971,11 @@ int nfk_read_chain(void* world, int32_t cap, int32_t* n, int32_t* obj, int32_t* 
     hipLaunchKernelGGL(k_chain_keys, dim3(gt), dim3(kTPB), 0, w->stream, (const ChainEnt*)w->chain_d, (const uint32_t*)db, nt,
                        w->chain_tcap, (const int32_t*)w->slot_obj_d, (const int32_t*)w->rank_d, k1, i1);
     size_t sb = sort_bytes;
-    HIPCHK(rocprim::radix_sort_pairs(S + s_tmp, sb, k1, k2, i1, i2, cnt, 0, key_bits, w->stream));
+    if (cnt <= (uint32_t)kSmallPairs)
+        hipLaunchKernelGGL(k_sort_small_pairs, dim3(1), dim3(1024), 0, w->stream, (const uint64_t*)k1, k2,
+                           (const uint32_t*)i1, i2, (int)cnt);
+    else
+        HIPCHK(rocprim::radix_sort_pairs(S + s_tmp, sb, k1, k2, i1, i2, cnt, 0, key_bits, w->stream));
     int32_t* oi = (int32_t*)(S + s_out);
     uint64_t* ou = (uint64_t*)(S + s_out + (size_t)cnt * 16);
     hipLaunchKernelGGL(k_chain_gather, dim3((cnt + kTPB - 1) / kTPB), dim3(kTPB), 0, w->stream, (const ChainEnt*)w->chain_d,
@@ -3676,7 +3680,11 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
             hipLaunchKernelGGL(k_xkeys, dim3(gx), dim3(256), 0, w->stream, xc, (int32_t)ng,
                                (const int32_t*)w->obj_slot_d, k1, i1, (uint32_t*)d.x_slot);
             size_t sb = xf_sort;
-            HIPCHK(rocprim::radix_sort_pairs(XF + xo_tmp, sb, k1, k2, i1, i2, ng, 0, xkey_bits, w->stream));
+            if (ng <= (size_t)kSmallPairs)  // (a window's few calls: one launch instead of the radix passes)
+                hipLaunchKernelGGL(k_sort_small_pairs, dim3(1), dim3(1024), 0, w->stream, (const uint64_t*)k1, k2,
+                                   (const uint32_t*)i1, i2, (int)ng);
+            else
+                HIPCHK(rocprim::radix_sort_pairs(XF + xo_tmp, sb, k1, k2, i1, i2, ng, 0, xkey_bits, w->stream));
             hipLaunchKernelGGL(k_scan_heads, dim3(1), dim3(1024), 0, w->stream, (const uint64_t*)k2, (int)ng, gi);
             hipLaunchKernelGGL(k_xgroups, dim3(gx), dim3(256), 0, w->stream, (const uint64_t*)k2, (const uint32_t*)i2,
                                (const uint32_t*)gi, xc, objs ? (const uint64_t*)(S + off_xh) : nullptr, (int32_t)ng,
@@ -3709,7 +3717,11 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
             hipLaunchKernelGGL(k_hkeys, dim3(gh_), dim3(256), 0, w->stream, hc, (int32_t)nhq,
                                (const int32_t*)w->obj_slot_d, k1, i1);
             size_t sb = hf_sort;
-            HIPCHK(rocprim::radix_sort_pairs(HF + ho_tmp, sb, k1, k2, i1, i2, nhq, 0, hkey_bits, w->stream));
+            if (nhq <= (size_t)kSmallPairs)
+                hipLaunchKernelGGL(k_sort_small_pairs, dim3(1), dim3(1024), 0, w->stream, (const uint64_t*)k1, k2,
+                                   (const uint32_t*)i1, i2, (int)nhq);
+            else
+                HIPCHK(rocprim::radix_sort_pairs(HF + ho_tmp, sb, k1, k2, i1, i2, nhq, 0, hkey_bits, w->stream));
             hipLaunchKernelGGL(k_hfold<false>, dim3((unsigned)((nhq + 1 + 255) / 256)), dim3(256), 0, w->stream,
                                (const uint64_t*)k2, (const uint32_t*)i2,
                                hc, (int32_t)nhq, cp, cq, (const uint32_t*)nullptr, (const uint32_t*)nullptr, ps, po, hpost);

@@ -2206,6 +2206,25 @@ __global__ __launch_bounds__(kTPB) void k_fired_keys(const int32_t* __restrict__
     keys[i] = ((uint64_t)(uint32_t)rank[fobj[i]] << 5) | (uint64_t)fkind[i];
     idx[i] = (uint32_t)i;
 }
+// A stable sort of n <= 2 * kSmallSort (key, value) pairs in one launch: each pair's place is the count
+// of pairs with a smaller key, or an equal key and a smaller index — the order rocPRIM's stable radix
+// sort of the same keys gives, without its passes' launches (a window's few hundred SetProperty or
+// schedule calls, a small per-Set log: config[0], the migration frames' SwitchScene writes)
+constexpr int kSmallPairs = 2048;
+__global__ __launch_bounds__(1024) void k_sort_small_pairs(const uint64_t* __restrict__ k1, uint64_t* __restrict__ k2,
+                                                           const uint32_t* __restrict__ v1, uint32_t* __restrict__ v2,
+                                                           int n) {
+    __shared__ uint64_t sk[kSmallPairs];
+    for (int i = threadIdx.x; i < n; i += 1024) sk[i] = k1[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const uint64_t k = sk[i];
+        int at = 0;
+        for (int j = 0; j < n; j++) at += (sk[j] < k || (sk[j] == k && j < i)) ? 1 : 0;
+        k2[at] = k;
+        v2[at] = v1[i];
+    }
+}
 // a small frame's fired list (n <= kSmallSort) into the walk's order in one launch: the keys are unique
 // ((object, kind) fires once a frame), so each entry's place is the count of smaller keys (what the
 // radix sort of k_fired_keys' keys and k_permute3 give, without their launches: config[0])
