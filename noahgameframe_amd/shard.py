@@ -290,19 +290,35 @@ class CppSceneShard:
 
     def begin_frame(self):
         """Collective: the rows of the last gather; returns the arrivals as a ticket array."""
+        cols = self.begin_frame_cols()
+        n = len(cols[0])
+        out = np.zeros((n, 11), np.int64)
+        if n:
+            gh, gd, cl, pl, sc, gr = cols
+            out[:, T_GH], out[:, T_GD], out[:, T_CLS], out[:, T_PL], out[:, T_SCENE], out[:, T_GROUP] = gh, gd, cl, pl, sc, gr
+            out[:, T_DST] = self.rank
+        return out
+
+    def begin_frame_cols(self):
+        """begin_frame's arrivals as columns (guid head, guid data, class, is_player, scene, group), without
+        the ticket array (a frame loop that only keeps a few of them)"""
         ns, nr = self.ct.c_int64(), self.ct.c_int64()
         r = self.lib.nfs_begin_frame(self.h, self.ct.byref(ns), self.ct.byref(nr))
         if r:
             raise RuntimeError(f"SceneShard::BeginFrame failed ({r})")
         n = nr.value
-        out = np.zeros((n, 11), np.int64)
+        gh, gd = np.empty(n, np.int64), np.empty(n, np.int64)
+        cl, pl, sc, gr = (np.empty(n, np.int32) for _ in range(4))
         if n:
-            gh, gd = np.zeros(n, np.int64), np.zeros(n, np.int64)
-            cl, pl, sc, gr = (np.zeros(n, np.int32) for _ in range(4))
             self.lib.nfs_received(self.h, n, *[a.ctypes.data for a in (gh, gd, cl, pl, sc, gr)])
-            out[:, T_GH], out[:, T_GD], out[:, T_CLS], out[:, T_PL], out[:, T_SCENE], out[:, T_GROUP] = gh, gd, cl, pl, sc, gr
-            out[:, T_DST] = self.rank
-        return out
+        return gh, gd, cl, pl, sc, gr
+
+    def queue_cols(self, gh, gd, cls, pl, scene, group, x, y, z):
+        """Departures as contiguous columns (int64 guid halves, int32 class / is_player / scene / group,
+        float32 position): queue without building a ticket array."""
+        n = len(gh)
+        if n and self.lib.nfs_queue_switch(self.h, n, *[c.ctypes.data for c in (gh, gd, cls, pl, scene, group, x, y, z)]):
+            raise RuntimeError("nfs_queue_switch failed")
 
     def end_frame(self):
         if self.lib.nfs_end_frame(self.h):

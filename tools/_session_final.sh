@@ -1,9 +1,7 @@
 set -u
-T=${1:-r17z}
+T=${1:-r17o}
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1
-echo "smoke rc=$?"; tail -2 gpurun_out/$T/smoke.log
 timeout -k 10 1000 python bench.py --steps 50 --warmup 5 > gpurun_out/$T/bench.log 2> gpurun_out/$T/bench.err
 rc=$?
 echo "bench rc=$rc"; tail -3 gpurun_out/$T/bench.err
@@ -13,3 +11,4 @@ for c in 1 3 4; do
   timeout -k 10 -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/$T/stats$c -o run -- $B > gpurun_out/$T/stats$c.log 2>&1
   echo "stats$c rc=$?"
 done
+SLACKS=8 bash tools/_session_mig.sh $T
