@@ -325,16 +325,18 @@ public:
     // Writes through NFIKernelModule: the reference's own NFCKernelModule on the host object (KM:323-372,
     // 492-544), its state brought up to date first; ForwardProperty / ForwardRecord queue the accepted
     // writes on the device.
+    // (a device object's host NFCObject from the adapter's index-keyed cache: KM:325-328's GetElement(self)
+    // without its walk of the object tree; any other object takes the reference's own path)
     bool SetPropertyInt(const NFGUID& self, const std::string& name, const NFINT64 v) override {  // KM:323
-        SyncObject(self);
+        if (NFIObject* ob = SyncedHostObject(self)) return ob->SetPropertyInt(name, v);
         return NFCKernelModule::SetPropertyInt(self, name, v);
     }
     bool SetPropertyFloat(const NFGUID& self, const std::string& name, const double v) override {  // KM:336
-        SyncObject(self);
+        if (NFIObject* ob = SyncedHostObject(self)) return ob->SetPropertyFloat(name, v);
         return NFCKernelModule::SetPropertyFloat(self, name, v);
     }
     bool SetPropertyObject(const NFGUID& self, const std::string& name, const NFGUID& v) override {  // KM:362
-        SyncObject(self);
+        if (NFIObject* ob = SyncedHostObject(self)) return ob->SetPropertyObject(name, v);
         return NFCKernelModule::SetPropertyObject(self, name, v);
     }
     bool SetRecordInt(const NFGUID& self, const std::string& rec, const int nRow, const int nCol, const NFINT64 v) override {
@@ -756,10 +758,16 @@ private:
         // per-object callback that could tell the Sets apart) when the host object is read directly
         // (kMirrorAll); otherwise the object is stale for them, as any other object (its watched
         // properties are current: the log's callbacks above wrote them)
+        WatchedPid(0);  // (the watched-property table current: read directly in the loop below)
+        const uint8_t* const wpid = watched_pid_.data();
+        const size_t n_wpid = watched_pid_.size();
         for (int64_t e : ep) {
-            uint8_t& m = State(f.ev_obj[e]);
+            // (mstate_ is sized for every evented object by the marks above; indexed afresh each time:
+            // a mirror write's callbacks below may create objects and grow it)
+            uint8_t& m = mstate_[(size_t)f.ev_obj[e]];
             if (!(m & kMirrorAll)) {
-                if (!WatchedPid(f.ev_pid[e])) m |= kStale;
+                const int32_t pid = f.ev_pid[e];
+                if (!(pid >= 0 && (size_t)pid < n_wpid && wpid[pid])) m |= kStale;
                 continue;
             }
             const NFGUID self = to_ref(gpu_.ObjectGuid(f.ev_obj[e]));
@@ -1079,6 +1087,16 @@ private:
         if ((size_t)o >= host_obj_.size()) host_obj_.resize((size_t)gpu_.ObjectCount() + 1024, nullptr);
         host_obj_[(size_t)o] = ob.get();  // (NFCKernelModule holds it until DestroyObject, which clears this)
         return ob.get();
+    }
+    // a device object's host object, brought up to date first (SyncObject); null for any other object
+    NFIObject* SyncedHostObject(const NFGUID& self) {
+        const int o = gpu_.ObjectIndex(to_gpu(self));
+        if (o < 0) {
+            SyncObject(self);
+            return nullptr;
+        }
+        if ((size_t)o < mstate_.size() && (mstate_[(size_t)o] & kStale)) SyncObject(self);
+        return HostObject(o);
     }
     NFIProperty* HostProperty(int o, int pid, const std::string& name) {
         const int w = WatchedSlot(pid);

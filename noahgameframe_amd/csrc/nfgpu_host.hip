@@ -2972,8 +2972,8 @@ int nfk_read_chain(void* world, int32_t cap, int32_t* n, int32_t* obj, int32_t* 
                        w->chain_tcap, (const int32_t*)w->slot_obj_d, (const int32_t*)w->rank_d, k1, i1);
     size_t sb = sort_bytes;
     if (cnt <= (uint32_t)kSmallPairs)
-        hipLaunchKernelGGL(k_sort_small_pairs, dim3(1), dim3(1024), 0, w->stream, (const uint64_t*)k1, k2,
-                           (const uint32_t*)i1, i2, (int)cnt);
+        hipLaunchKernelGGL(k_sort_small_pairs, dim3((cnt + kTPB - 1) / kTPB), dim3(kTPB), 0, w->stream, (const uint64_t*)k1,
+                           k2, (const uint32_t*)i1, i2, (int)cnt);
     else
         HIPCHK(rocprim::radix_sort_pairs(S + s_tmp, sb, k1, k2, i1, i2, cnt, 0, key_bits, w->stream));
     int32_t* oi = (int32_t*)(S + s_out);
@@ -3681,8 +3681,8 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
                                (const int32_t*)w->obj_slot_d, k1, i1, (uint32_t*)d.x_slot);
             size_t sb = xf_sort;
             if (ng <= (size_t)kSmallPairs)  // (a window's few calls: one launch instead of the radix passes)
-                hipLaunchKernelGGL(k_sort_small_pairs, dim3(1), dim3(1024), 0, w->stream, (const uint64_t*)k1, k2,
-                                   (const uint32_t*)i1, i2, (int)ng);
+                hipLaunchKernelGGL(k_sort_small_pairs, dim3((unsigned)((ng + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream,
+                                   (const uint64_t*)k1, k2, (const uint32_t*)i1, i2, (int)ng);
             else
                 HIPCHK(rocprim::radix_sort_pairs(XF + xo_tmp, sb, k1, k2, i1, i2, ng, 0, xkey_bits, w->stream));
             hipLaunchKernelGGL(k_scan_heads, dim3(1), dim3(1024), 0, w->stream, (const uint64_t*)k2, (int)ng, gi);
@@ -3718,8 +3718,8 @@ static int execute_frame(World* w, int64_t now_ms, bool calls_only) {
                                (const int32_t*)w->obj_slot_d, k1, i1);
             size_t sb = hf_sort;
             if (nhq <= (size_t)kSmallPairs)
-                hipLaunchKernelGGL(k_sort_small_pairs, dim3(1), dim3(1024), 0, w->stream, (const uint64_t*)k1, k2,
-                                   (const uint32_t*)i1, i2, (int)nhq);
+                hipLaunchKernelGGL(k_sort_small_pairs, dim3((unsigned)((nhq + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream,
+                                   (const uint64_t*)k1, k2, (const uint32_t*)i1, i2, (int)nhq);
             else
                 HIPCHK(rocprim::radix_sort_pairs(HF + ho_tmp, sb, k1, k2, i1, i2, nhq, 0, hkey_bits, w->stream));
             hipLaunchKernelGGL(k_hfold<false>, dim3((unsigned)((nhq + 1 + 255) / 256)), dim3(256), 0, w->stream,
@@ -4619,7 +4619,7 @@ int nfk_read_frame(void* world, uint32_t what, nfk_frame_host* o) {
     }
     if (nf) {
         if (order && nf <= (size_t)kSmallSort) {
-            hipLaunchKernelGGL(k_fired_small, dim3(1), dim3(kSmallSort), 0, w->stream, (const int32_t*)fo,
+            hipLaunchKernelGGL(k_fired_small, dim3((unsigned)((nf + kTPB - 1) / kTPB)), dim3(kTPB), 0, w->stream, (const int32_t*)fo,
                                (const int32_t*)fk, (const int32_t*)fr, w->rank_d, (int32_t*)(D + o_fo),
                                (int32_t*)(D + o_fk), (int32_t*)(D + o_fr), (int)nf);
         } else if (order) {

@@ -2210,39 +2210,38 @@ __global__ __launch_bounds__(kTPB) void k_fired_keys(const int32_t* __restrict__
 // of pairs with a smaller key, or an equal key and a smaller index — the order rocPRIM's stable radix
 // sort of the same keys gives, without its passes' launches (a window's few hundred SetProperty or
 // schedule calls, a small per-Set log: config[0], the migration frames' SwitchScene writes)
+// One workgroup per 256 pairs (each loads every key into LDS), so the n^2 compares spread over n / 256
+// CUs (one workgroup of 1024 threads took 110 us for the 1536 SwitchScene writes of a migration frame).
 constexpr int kSmallPairs = 2048;
-__global__ __launch_bounds__(1024) void k_sort_small_pairs(const uint64_t* __restrict__ k1, uint64_t* __restrict__ k2,
+__global__ __launch_bounds__(kTPB) void k_sort_small_pairs(const uint64_t* __restrict__ k1, uint64_t* __restrict__ k2,
                                                            const uint32_t* __restrict__ v1, uint32_t* __restrict__ v2,
                                                            int n) {
     __shared__ uint64_t sk[kSmallPairs];
-    for (int i = threadIdx.x; i < n; i += 1024) sk[i] = k1[i];
+    for (int i = threadIdx.x; i < n; i += kTPB) sk[i] = k1[i];
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += 1024) {
-        const uint64_t k = sk[i];
-        int at = 0;
-        for (int j = 0; j < n; j++) at += (sk[j] < k || (sk[j] == k && j < i)) ? 1 : 0;
-        k2[at] = k;
-        v2[at] = v1[i];
-    }
+    const int i = blockIdx.x * kTPB + (int)threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = sk[i];
+    int at = 0;
+    for (int j = 0; j < n; j++) at += (sk[j] < k || (sk[j] == k && j < i)) ? 1 : 0;
+    k2[at] = k;
+    v2[at] = v1[i];
 }
 // a small frame's fired list (n <= kSmallSort) into the walk's order in one launch: the keys are unique
 // ((object, kind) fires once a frame), so each entry's place is the count of smaller keys (what the
 // radix sort of k_fired_keys' keys and k_permute3 give, without their launches: config[0])
 constexpr int kSmallSort = 1024;
-__global__ __launch_bounds__(kSmallSort) void k_fired_small(const int32_t* __restrict__ fobj,
-                                                            const int32_t* __restrict__ fkind,
-                                                            const int32_t* __restrict__ frem,
-                                                            const int32_t* __restrict__ rank, int32_t* __restrict__ ao,
-                                                            int32_t* __restrict__ bo, int32_t* __restrict__ co, int n) {
-    __shared__ uint64_t sk[kSmallSort];
-    const int i = threadIdx.x;
-    uint64_t k = 0;
-    if (i < n) {
-        k = ((uint64_t)(uint32_t)rank[fobj[i]] << 5) | (uint64_t)fkind[i];
-        sk[i] = k;
-    }
+__global__ __launch_bounds__(kTPB) void k_fired_small(const int32_t* __restrict__ fobj,
+                                                      const int32_t* __restrict__ fkind,
+                                                      const int32_t* __restrict__ frem,
+                                                      const int32_t* __restrict__ rank, int32_t* __restrict__ ao,
+                                                      int32_t* __restrict__ bo, int32_t* __restrict__ co, int n) {
+    __shared__ uint64_t sk[kSmallSort];  // (every key, in each of the n / 256 workgroups)
+    for (int j = threadIdx.x; j < n; j += kTPB) sk[j] = ((uint64_t)(uint32_t)rank[fobj[j]] << 5) | (uint64_t)fkind[j];
     __syncthreads();
+    const int i = blockIdx.x * kTPB + (int)threadIdx.x;
     if (i >= n) return;
+    const uint64_t k = sk[i];
     int at = 0;
     for (int j = 0; j < n; j++) at += sk[j] < k ? 1 : 0;
     ao[at] = fobj[i];
