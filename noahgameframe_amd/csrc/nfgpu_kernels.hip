@@ -2211,12 +2211,14 @@ __global__ __launch_bounds__(kTPB) void k_fired_keys(const int32_t* __restrict__
 // sort of the same keys gives, without its passes' launches (a window's few hundred SetProperty or
 // schedule calls, a small per-Set log: config[0], the migration frames' SwitchScene writes)
 // One workgroup per 256 pairs (each loads every key into LDS), so the n^2 compares spread over n / 256
-// CUs (one workgroup of 1024 threads took 110 us for the 1536 SwitchScene writes of a migration frame).
-constexpr int kSmallPairs = 2048;
+// CUs.  Used up to kSmallPairs pairs: at 1536 (a migration frame's SwitchScene writes) the compares cost
+// more than rocPRIM's passes (aux 34.5 -> 60.8 us; one workgroup of 1024 threads: 110 us,
+// profiles/r17o_selfmig_trace.txt, r17p_selfmig_trace.txt); at a hundred (config[0]) one launch wins.
+constexpr int kSmallPairs = 512;
 __global__ __launch_bounds__(kTPB) void k_sort_small_pairs(const uint64_t* __restrict__ k1, uint64_t* __restrict__ k2,
                                                            const uint32_t* __restrict__ v1, uint32_t* __restrict__ v2,
                                                            int n) {
-    __shared__ uint64_t sk[kSmallPairs];
+    __shared__ uint64_t sk[kSmallPairs];  // (n <= kSmallPairs)
     for (int i = threadIdx.x; i < n; i += kTPB) sk[i] = k1[i];
     __syncthreads();
     const int i = blockIdx.x * kTPB + (int)threadIdx.x;
