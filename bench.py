@@ -423,9 +423,15 @@ def main():
         nonlocal tick
         if mig:
             timed("migrate", mig.before_frame)
+        # the C++ shard: this window's departures are queued (the game logic's SwitchScene calls) and their
+        # ticket gather started before the frame runs, so it proceeds while this frame is launched
+        # (a server's game logic between frames hides it the same way); the Python shard keeps its order
+        early = mig is not None and mig.impl == "cpp"
+        if early:
+            timed("tickets", mig.after_frame)
         timed("execute", lambda: m.Execute(t0 + tick * args.tick_ms))
         m.outputs_raw()   # the consumer's read of the frame's outputs (dense ranks: k_scan_tiles)
-        if mig:
+        if mig and not early:
             timed("tickets", mig.after_frame)   # tickets, exchanged while this and the next frame run
         tick += 1
 
