@@ -31,10 +31,13 @@
 // next exchange frame.  Migrate() is the synchronous form (gather now, rows now).
 #pragma once
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <functional>
 #include <future>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 namespace nfgpu {
@@ -196,6 +199,15 @@ private:
     std::future<int> pending_;  // the ticket gather started by the last exchange EndFrame
     bool failed_ = false;       // a transport call of this shard returned an error
     std::vector<int64_t> pending_plan_;
+    // the gathers run on one persistent worker thread (started by the first exchange): a thread per
+    // gather (std::async) cost its creation, and the HIP device's set-up on it, on every exchange frame
+    void GatherLoop();
+    std::thread worker_;
+    std::mutex wmu_;
+    std::condition_variable wcv_;
+    bool wstop_ = false, wjob_ = false;
+    std::vector<int64_t> wmine_;
+    std::promise<int> wprom_;
 };
 
 }  // namespace nfgpu

@@ -817,14 +817,14 @@ private:
             __builtin_prefetch(&gpu_.ObjectGuid(fi.o));
             if (o < host_obj_.size()) __builtin_prefetch(&host_obj_[o]);
             if (fi.row < 0 && watched_slots_) {
-                const int w = fi.kind >= 0 ? WatchedSlotFast(fr_pid_(fi)) : -1;
+                const int w = WatchedSlotFast(FirePid(fi));
                 if (w >= 0 && o * watched_slots_ + (size_t)w < prop_cache_.size())
                     __builtin_prefetch(&prop_cache_[o * watched_slots_ + (size_t)w]);
             }
             return;
         }
         if (fi.row < 0 && watched_slots_) {
-            const int w = WatchedSlotFast(fr_pid_(fi));
+            const int w = WatchedSlotFast(FirePid(fi));
             const size_t at = o * watched_slots_ + (size_t)w;
             if (w >= 0 && at < prop_cache_.size() && prop_cache_[at]) {
                 const char* p = (const char*)prop_cache_[at];
@@ -836,7 +836,8 @@ private:
             __builtin_prefetch(host_obj_[o]);
         }
     }
-    int fr_pid_(const Fire& fi) const { return gpu_.LastChain()[(size_t)fi.i].pid; }
+    // the property of a per-Set fire (row < 0: fi.i indexes the frame's per-Set log)
+    int FirePid(const Fire& fi) const { return gpu_.LastChain()[(size_t)fi.i].pid; }
     int WatchedSlotFast(int pid) const {
         return pid >= 0 && (size_t)pid < watched_slot_.size() ? watched_slot_[(size_t)pid] : -1;
     }

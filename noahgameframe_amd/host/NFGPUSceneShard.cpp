@@ -125,6 +125,14 @@ SceneShard::~SceneShard() {
         if (pending_.wait_for(std::chrono::duration<double>(secs)) != std::future_status::ready) t_->Abort();
         (void)pending_.get();
     }
+    if (worker_.joinable()) {  // (idle now: its last gather has been taken)
+        {
+            std::lock_guard<std::mutex> lk(wmu_);
+            wstop_ = true;
+        }
+        wcv_.notify_one();
+        worker_.join();
+    }
     if (sbuf_) mem_.release(sbuf_);
     if (rbuf_) mem_.release(rbuf_);
 }
@@ -178,10 +186,38 @@ int SceneShard::EndFrame() {
     std::vector<int64_t> mine = TakeTickets();
     transport_calls++;
     pending_plan_.clear();
-    // on a worker thread: the game logic of the next window runs meanwhile
-    pending_ = std::async(std::launch::async,
-                          [this, mine = std::move(mine)]() { return t_->AllGather(mine, pending_plan_); });
+    // on the worker thread: the game logic of the next window runs meanwhile
+    std::promise<int> pr;
+    pending_ = pr.get_future();
+    {
+        std::lock_guard<std::mutex> lk(wmu_);
+        if (!worker_.joinable()) worker_ = std::thread(&SceneShard::GatherLoop, this);
+        wmine_ = std::move(mine);
+        wprom_ = std::move(pr);
+        wjob_ = true;
+    }
+    wcv_.notify_one();
     return NFK_OK;
+}
+
+void SceneShard::GatherLoop() {
+    std::unique_lock<std::mutex> lk(wmu_);
+    for (;;) {
+        wcv_.wait(lk, [this] { return wstop_ || wjob_; });
+        if (!wjob_) return;  // (stopped, nothing queued)
+        wjob_ = false;
+        std::vector<int64_t> mine = std::move(wmine_);
+        std::promise<int> pr = std::move(wprom_);
+        lk.unlock();
+        int r;
+        try {
+            r = t_->AllGather(mine, pending_plan_);
+        } catch (...) {
+            r = NFK_ERR_HIP;
+        }
+        pr.set_value(r);
+        lk.lock();
+    }
 }
 
 int SceneShard::BeginFrame(std::vector<Ticket>* sent, std::vector<Ticket>* received) {
