@@ -67,7 +67,9 @@ extern "C" {
  * program has left it so far, compares to 0 as NFK_GUARD_* in (guard >> 16) & 3 says — a functor's
  * `if (GetPropertyInt(self, g) > 0) SetProperty...(...)`.  With NFK_GUARD_PROP in guard it compares
  * to int property (guard >> 19) instead of 0 (both as the program has left them):
- * `if (GetPropertyInt(self, g) > GetPropertyInt(self, h)) ...`. */
+ * `if (GetPropertyInt(self, g) > GetPropertyInt(self, h)) ...`.  Without it, bits 19..31 hold a
+ * signed constant K in [-4096, 4095] (NFK_GUARD_K; 0 by default) that g is compared to instead:
+ * `if (GetPropertyInt(self, g) > 10) ...` (>= K and < K are > K-1 and <= K-1). */
 enum {
     NFK_OP_NOP = 0,
     NFK_OP_IADD_CLAMP = 1,
@@ -87,12 +89,16 @@ enum {
 #define NFK_GUARD_NE0 2 /* g != 0 */
 #define NFK_GUARD_EQ0 3 /* g == 0 */
 #define NFK_GUARD_PROP (1u << 18) /* compare g to int property guard >> 19 (< 8192) instead of 0 */
+#define NFK_GUARD_K(k) (((uint32_t)(k) & 0x1FFFu) << 19) /* compare g to the constant k (no NFK_GUARD_PROP) */
+#define NFK_GUARD_KVAL(guard) ((int32_t)(guard) >> 19)   /* the constant of a guard word without NFK_GUARD_PROP */
+#define NFK_GUARD_KMIN (-4096)
+#define NFK_GUARD_KMAX 4095
 
 typedef struct nfk_op {
     uint8_t code;
     uint8_t flags;
     uint16_t dst;
-    uint32_t guard; /* with NFK_GUARD: property id | NFK_GUARD_* << 16 [| NFK_GUARD_PROP | h << 19]; else 0 */
+    uint32_t guard; /* with NFK_GUARD: property id | NFK_GUARD_* << 16 [| NFK_GUARD_PROP | h << 19 or | NFK_GUARD_K(k)]; else 0 */
     int64_t a, b, c;
 } nfk_op; /* 32 bytes */
 

@@ -139,11 +139,12 @@ struct OpX {
     uint32_t slots;
     int64_t a, b, c;
     // NFK_GUARD: 0x80000000 | NFK_GUARD_* << 8 | the guard's U slot, and with NFK_GUARD_PROP
-    // 0x40000000 | the compared property's U slot << 16; else 0
+    // 0x40000000 | the compared property's U slot << 16, else the guard's constant (13 bits, signed)
+    // << 16; else 0
     uint32_t gd;
 };
 // an NFK_GUARD op's condition on the guard property's current value g and what it is compared to
-// (h: another int property's current value under NFK_GUARD_PROP, else 0)
+// (h: another int property's current value under NFK_GUARD_PROP, else the constant NFK_GUARD_K)
 __host__ __device__ __forceinline__ bool guard_ok(uint32_t cmp, int64_t g, int64_t h = 0) {
     return cmp == NFK_GUARD_GT0 ? g > h : cmp == NFK_GUARD_LE0 ? g <= h : cmp == NFK_GUARD_NE0 ? g != h : g == h;
 }

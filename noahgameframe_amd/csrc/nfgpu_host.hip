@@ -991,6 +991,7 @@ bool build_u_tables(Tables& tab, int NK, std::vector<int>& wp, std::vector<int>&
                 x.c = op.c;
                 x.gd = (op.flags & NFK_GUARD) ? 0x80000000u | (((op.guard >> 16) & 3u) << 8) | tab.opg[k][i] : 0u;
                 if (tab.opg2[k][i] != kNoU) x.gd |= 0x40000000u | ((uint32_t)tab.opg2[k][i] << 16);
+                else if (op.flags & NFK_GUARD) x.gd |= ((op.guard >> 19) & 0x1FFFu) << 16;  // NFK_GUARD_K
             }
         }
     }
@@ -1830,9 +1831,10 @@ int nfk_define_kind(void* world, int32_t kind, const nfk_op* ops, int32_t n_ops)
         auto isflt = [&](int64_t p) { return p >= ni && p < np; };
         if (op.flags & NFK_GUARD) {
             const bool rec = op.code == NFK_OP_RIADD_CLAMP || op.code == NFK_OP_RFAFFINE;
-            // (NFK_GUARD_PROP: compared to the int property guard >> 19; otherwise no bits above 17)
+            // (NFK_GUARD_PROP: compared to the int property guard >> 19; otherwise to the constant
+            // NFK_GUARD_KVAL(guard) in bits 19..31, any value)
             const bool vs = (op.guard & NFK_GUARD_PROP) != 0;
-            if (rec || op.code == NFK_OP_NOP || !isint(op.guard & 0xFFFF) || (vs ? !isint(op.guard >> 19) : (op.guard >> 18) != 0))
+            if (rec || op.code == NFK_OP_NOP || !isint(op.guard & 0xFFFF) || (vs && !isint(op.guard >> 19)))
                 return fail(NFK_ERR_ARG, "NFK_GUARD: a property op guarded by an int property");
         } else if (op.guard) {
             return fail(NFK_ERR_ARG, "nfk_op.guard without NFK_GUARD");

@@ -510,7 +510,7 @@ __device__ __forceinline__ void run_program_chunk(Ent& en, const Tables* __restr
         if (op.flags & NFK_GUARD) {
             uint64_t t;
             const int64_t g = en.tget(op.guard & 0xFFFFu, t) ? (int64_t)t : (int64_t)pre[ii][4];
-            const int64_t h = !(op.guard & NFK_GUARD_PROP) ? 0 : en.tget(op.guard >> 19, t) ? (int64_t)t : (int64_t)pre[ii][5];
+            const int64_t h = !(op.guard & NFK_GUARD_PROP) ? (int64_t)NFK_GUARD_KVAL(op.guard) : en.tget(op.guard >> 19, t) ? (int64_t)t : (int64_t)pre[ii][5];
             if (!guard_ok((op.guard >> 16) & 3u, g, h)) continue;
         }
         if (op.code == NFK_OP_IADD_CLAMP) {

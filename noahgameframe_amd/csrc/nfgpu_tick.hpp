@@ -85,7 +85,8 @@ __device__ __forceinline__ void run_programs_u(uint64_t (&v)[kU], uint32_t& wm, 
             const uint32_t u2 = uslot((sl >> 16) & 0xFF, n_w), u3 = uslot(sl >> 24, n_w);
             const uint32_t gd = tab->opx[k][i].gd;
             if (gd && !guard_ok((gd >> 8) & 3u, (int64_t)uget(v, uslot(gd & 0xFF, n_w)),
-                                (gd & 0x40000000u) ? (int64_t)uget(v, uslot((gd >> 16) & 0xFF, n_w)) : 0))
+                                (gd & 0x40000000u) ? (int64_t)uget(v, uslot((gd >> 16) & 0xFF, n_w))
+                                                   : (int64_t)((int32_t)(gd << 3) >> 19)))  // the constant, bits 16..28
                 continue;  // NFK_GUARD
             if (code == NFK_OP_IADD_CLAMP) {
                 const int64_t cur = (int64_t)uget(v, u0);

@@ -42,12 +42,15 @@ OP_IADD_CLAMP, OP_FLERP, OP_FAFFINE, OP_RIADD_CLAMP, OP_RFAFFINE, OP_ISET, OP_FS
 A_PROP, LO_PROP, HI_PROP, GUARD = 1, 2, 4, 8
 GUARD_GT0, GUARD_LE0, GUARD_NE0, GUARD_EQ0 = 0, 1, 2, 3
 GUARD_PROP = 1 << 18
+GUARD_KMIN, GUARD_KMAX = -4096, 4095
 
 
-def guard(pid, cmp, vs=None):
-    """nfk_op.guard of an NFK_GUARD op: the int property and its comparison with 0, or with the int
-    property `vs` (NFK_GUARD_PROP: a functor's `if (GetPropertyInt(self, g) > GetPropertyInt(self, h))`)"""
-    return pid | (cmp << 16) | (0 if vs is None else GUARD_PROP | (vs << 19))
+def guard(pid, cmp, vs=None, k=0):
+    """nfk_op.guard of an NFK_GUARD op: the int property and its comparison with the constant k (0 by
+    default; NFK_GUARD_K, a functor's `if (GetPropertyInt(self, g) > 30)`), or with the int property
+    `vs` (NFK_GUARD_PROP: a functor's `if (GetPropertyInt(self, g) > GetPropertyInt(self, h))`)"""
+    assert GUARD_KMIN <= k <= GUARD_KMAX and (vs is None or k == 0)
+    return pid | (cmp << 16) | ((k & 0x1FFF) << 19 if vs is None else GUARD_PROP | (vs << 19))
 
 
 MAX_OPS = 8  # include/nfgpu.h NFK_MAX_OPS (workload files written before round 4 hold 4 per kind)
@@ -87,7 +90,8 @@ def _prop_flags(n_oprops=0):
     return f
 
 
-def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False, lethal_poison=False):
+def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False, lethal_poison=False,
+             const_guards=False):
     ops = np.zeros((len(KINDS), MAX_OPS), OP_DTYPE)
     n_ops = np.zeros(len(KINDS), np.int32)
 
@@ -134,6 +138,21 @@ def programs(with_records, rec_float_op=True, rec_skill_op=False, set_ops=False,
         # fire once per accepted Set
         put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 0, PID["MAXHP"]),
                        (OP_ISET, GUARD, PID["HP"], guard(PID["HP"], GUARD_LE0), 3, 0, 0)])
+    if const_guards:
+        # guards against constants other than 0 (round 6, NFK_GUARD_K): a functor's
+        # `if (GetPropertyInt(self, "Level") > 30)`; ATK_VALUE falls by 900 a Poison fire, so the guards
+        # on it meet negative constants and both ends of the range (<= -4096 lifts it by 9000 to > 4095)
+        put("HPRegen", [(OP_IADD_CLAMP, A_PROP | HI_PROP, PID["HP"], 0, PID["HPREGEN"], 0, PID["MAXHP"]),
+                        (OP_IADD_CLAMP, GUARD, PID["SP"], guard(PID["Level"], GUARD_GT0, k=30), 1, 0, 1000),
+                        (OP_ISET, GUARD, PID["SP"], guard(PID["HP"], GUARD_LE0, k=1500), 5, 0, 0)])
+        put("Poison", [(OP_IADD_CLAMP, HI_PROP, PID["HP"], 0, -13, 1, PID["MAXHP"]),
+                       (OP_IADD_CLAMP, 0, PID["ATK_VALUE"], 0, -900, -5000, 5000),
+                       (OP_ISET, GUARD, PID["DEF_VALUE"], guard(PID["ATK_VALUE"], GUARD_LE0, k=-100), 1, 0, 0),
+                       (OP_IADD_CLAMP, GUARD, PID["ATK_VALUE"], guard(PID["ATK_VALUE"], GUARD_LE0, k=GUARD_KMIN),
+                        9000, -5000, 5000),
+                       (OP_ISET, GUARD, PID["DEF_VALUE"], guard(PID["ATK_VALUE"], GUARD_GT0, k=GUARD_KMAX), 777, 0, 0),
+                       (OP_ISET, GUARD, PID["Level"], guard(PID["Camp"], GUARD_EQ0, k=2), 61, 0, 0),
+                       (OP_IADD_CLAMP, GUARD, PID["SP"], guard(PID["Level"], GUARD_NE0, k=61), -1, 0, 1000)])
     if with_records:
         # skill table: col 1 = cooldown ms (int), col 2 = charge (f64) decays
         lst = [(OP_RIADD_CLAMP, 0, (0 << 8) | 1, 0, -100, 0, I64_MAX)]
@@ -159,7 +178,7 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
                switch_frac=0.0, switch_new_groups=False, rec_steady=False, ext_props=None, burst_frac=0.0,
                burst_props=20, rmw_frac=0.0, spawn_frac=0.0, destroy_frac=0.0, rec_set_frac=0.0,
                rec_set_float=True, obj_props=False, obj_set_frac=0.05, rec_row_frac=0.0, set_ops=False,
-               lethal_poison=False):
+               lethal_poison=False, const_guards=False):
     if spawn_frac > 0 or destroy_frac > 0:
         return _lifecycle_world(locals())
     rng = np.random.default_rng(seed)
@@ -220,7 +239,7 @@ def make_world(n_obj=4096, n_scenes=1, groups_per_scene=16, players_per_group=4,
     still = rng.random(n_obj) < 0.02
     init_f[fi["X"], still] = init_f[fi["TargetX"], still]
 
-    ops, n_ops = programs(records, rec_float_op, rec_skill_op, set_ops, lethal_poison)
+    ops, n_ops = programs(records, rec_float_op, rec_skill_op, set_ops, lethal_poison, const_guards)
     n_kind = len(KINDS) if records else len(KINDS) - 1
 
     # ---- heartbeats registered before the first frame ----

@@ -226,8 +226,8 @@ static void run_program(int32_t obj, int kind) {
         const nfk_op* op = &ops[kind][i];
         if (op->flags & NFK_GUARD) { /* the functor's `if (GetPropertyInt(self, g) ...)` */
             int64_t g = iget(obj, op->guard & 0xFFFF);
-            /* ... compared to 0, or to GetPropertyInt(self, h) under NFK_GUARD_PROP */
-            int64_t h = (op->guard & NFK_GUARD_PROP) ? iget(obj, (int32_t)(op->guard >> 19)) : 0;
+            /* ... compared to a constant (0 by default), or to GetPropertyInt(self, h) under NFK_GUARD_PROP */
+            int64_t h = (op->guard & NFK_GUARD_PROP) ? iget(obj, (int32_t)(op->guard >> 19)) : NFK_GUARD_KVAL(op->guard);
             int c = (op->guard >> 16) & 3;
             if (!(c == NFK_GUARD_GT0 ? g > h : c == NFK_GUARD_LE0 ? g <= h : c == NFK_GUARD_NE0 ? g != h : g == h)) continue;
         }

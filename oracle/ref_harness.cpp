@@ -198,7 +198,8 @@ static int OnHeartBeat(const NFGUID& self, const std::string& name, const float,
         const nfk_op& op = W.ops[kind][i];
         if (op.flags & NFK_GUARD) {
             const int64_t g = GetInt(self, (int)(op.guard & 0xFFFF));
-            const int64_t h = (op.guard & NFK_GUARD_PROP) ? GetInt(self, (int)(op.guard >> 19)) : 0;  // vs a property
+            const int64_t h = (op.guard & NFK_GUARD_PROP) ? GetInt(self, (int)(op.guard >> 19))  // vs a property
+                                                             : NFK_GUARD_KVAL(op.guard);   // or a constant
             const int c = (op.guard >> 16) & 3;
             if (!(c == NFK_GUARD_GT0 ? g > h : c == NFK_GUARD_LE0 ? g <= h : c == NFK_GUARD_NE0 ? g != h : g == h)) continue;
         }

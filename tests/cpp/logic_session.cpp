@@ -455,7 +455,7 @@ int main(int argc, char** argv) {
             const nfk_op& op = ops[k * OPK + i];
             if (op.flags & NFK_GUARD) {  // the functor's `if (GetPropertyInt(self, g) ...)`
                 const int64_t g = km->GetPropertyInt(self, pname[op.guard & 0xFFFF]);
-                const int64_t h = (op.guard & NFK_GUARD_PROP) ? km->GetPropertyInt(self, pname[op.guard >> 19]) : 0;
+                const int64_t h = (op.guard & NFK_GUARD_PROP) ? km->GetPropertyInt(self, pname[op.guard >> 19]) : NFK_GUARD_KVAL(op.guard);
                 const int c = (op.guard >> 16) & 3;
                 if (!(c == NFK_GUARD_GT0 ? g > h : c == NFK_GUARD_LE0 ? g <= h : c == NFK_GUARD_NE0 ? g != h : g == h))
                     continue;

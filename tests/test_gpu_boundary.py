@@ -129,10 +129,10 @@ def test_failed_frame_drops_the_whole_window(gpu_available, monkeypatch):
 
 def test_program_op_validation(gpu_available):
     """nfk_define_kind refuses what a program cannot mean: NFK_GUARD on a record op or on a float
-    property, a guard compared to a float property (NFK_GUARD_PROP) or with stray bits above its
-    comparison, a guard word without NFK_GUARD, assignment ops onto the other type, more than
-    NFK_MAX_OPS ops; and takes 8 ops with guards (against 0 and against another int property) and
-    assignments (include/nfgpu.h)."""
+    property, a guard compared to a float property (NFK_GUARD_PROP), a guard on a NOP, a guard word
+    without NFK_GUARD, assignment ops onto the other type, more than NFK_MAX_OPS ops; and takes 8 ops
+    with guards (against 0, against another int property, against both ends of NFK_GUARD_K's range)
+    and assignments (include/nfgpu.h)."""
     W = workload
     m = kernel.NFKernelModule(64, n_rec=1)
     try:
@@ -149,7 +149,7 @@ def test_program_op_validation(gpu_available):
             ops((W.OP_ISET, W.GUARD, P["SP"], W.guard(P["X"], W.GUARD_GT0), 7, 0, 0)),
             ops((W.OP_ISET, 0, P["SP"], W.guard(P["Camp"], W.GUARD_GT0), 7, 0, 0)),
             ops((W.OP_ISET, W.GUARD, P["SP"], W.guard(P["Camp"], W.GUARD_GT0, vs=P["X"]), 7, 0, 0)),
-            ops((W.OP_ISET, W.GUARD, P["SP"], W.guard(P["Camp"], W.GUARD_GT0) | (P["MP"] << 19), 7, 0, 0)),
+            ops((0, W.GUARD, P["SP"], W.guard(P["Camp"], W.GUARD_GT0, k=3), 0, 0, 0)),
             ops((W.OP_ISET, 0, P["X"], 0, 7, 0, 0)),
             ops((W.OP_FSET, W.A_PROP, P["X"], 0, P["HP"], 0, 0)),
             ops(*[(W.OP_ISET, 0, P["SP"], 0, 7, 0, 0)] * 9),
@@ -159,7 +159,9 @@ def test_program_op_validation(gpu_available):
                 m.define_kind(0, a)
         good = ops(*([(W.OP_ISET, W.GUARD, P["SP"], W.guard(P["Camp"], W.GUARD_EQ0), 7, 0, 0),
                       (W.OP_FSET, W.A_PROP | W.GUARD, P["Z"], W.guard(P["HP"], W.GUARD_LE0, vs=P["MAXHP"]), P["X"], 0,
-                       0)] * 4))
+                       0),
+                      (W.OP_IADD_CLAMP, W.GUARD, P["SP"], W.guard(P["Camp"], W.GUARD_GT0, k=W.GUARD_KMIN), 1, 0, 9),
+                      (W.OP_ISET, W.GUARD, P["SP"], W.guard(P["MP"], W.GUARD_NE0, k=W.GUARD_KMAX), 7, 0, 0)] * 2))
         m.define_kind(0, good)
     finally:
         m.close()

@@ -97,6 +97,10 @@ CASES = {
     "set_ops": dict(n_obj=4000, n_scenes=2, groups_per_scene=6, players_per_group=4, set_ops=True, ext_frac=0.1,
                     ext_props="all", rmw_frac=0.02, switch_frac=0.02, spawn_frac=0.02, destroy_frac=0.02,
                     host_ops=True, records=True, rec_rows=32),
+    # guards against constants other than 0 (NFK_GUARD_K: negative ones and both ends of the range),
+    # with SetProperty calls on the guarded properties (oracle pinned: test_oracle.py seeds 17, 34)
+    "const_guards": dict(n_obj=4000, n_scenes=2, groups_per_scene=6, players_per_group=4, const_guards=True,
+                         tick_ms=500, ext_frac=0.1, ext_props="all", rmw_frac=0.02, host_ops=True),
     "wide_sets_records": dict(n_obj=3000, n_scenes=2, groups_per_scene=5, players_per_group=6, records=True,
                               rec_rows=32, ext_frac=0.1, ext_props="all", burst_frac=0.02, burst_props=24,
                               switch_frac=0.01),

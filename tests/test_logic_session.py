@@ -35,11 +35,13 @@ GPU_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "logic_session")
 REF_EXE = os.path.join(ROOT, "tests", "cpp", "_ref", "logic_session_ref")
 
 
-def _world(seed, n_obj=1200, n_ticks=12, lethal=False, set_ops=False, logic_mode=0, groups_per_scene=3):
+def _world(seed, n_obj=1200, n_ticks=12, lethal=False, set_ops=False, logic_mode=0, groups_per_scene=3,
+           const_guards=False):
     w = workload.make_world(n_obj=n_obj, n_scenes=2, groups_per_scene=groups_per_scene, players_per_group=4, n_ticks=n_ticks,
                             tick_ms=1000, seed=seed, ext_frac=0.05, host_ops=True, rmw_frac=0.02, spawn_frac=0.02,
                             destroy_frac=0.02, records=True, rec_rows=16, rec_float_op=False, rec_set_frac=0.03,
-                            rec_set_float=False, rec_row_frac=0.02, lethal_poison=lethal, set_ops=set_ops)
+                            rec_set_float=False, rec_row_frac=0.02, lethal_poison=lethal, set_ops=set_ops,
+                            const_guards=const_guards)
     # an int-only record (the reference's NFCRecord::SetFloat cannot hold an f64 cell, test_oracle.py):
     # the charge column becomes an int column with the same bits; no program touches it
     w["rec_ctype"] = np.zeros_like(w["rec_ctype"])
@@ -171,14 +173,16 @@ def test_logic_session_reference_components_destroy(tmp_path):
 # seed 74: the set_ops programs (assignments, guards against 0 and against another int property)
 # seed 75: logic_mode 1 | 2 | 4 — cross-object functor reads answered in walk order, components destroying
 # objects (their own deferred), with lethal Poison
+# seed 79: guards against constants other than 0 (NFK_GUARD_K; mode 32 = the const_guards programs)
 # seed 78: logic_mode 16 — only EXP watched with the set_ops programs: the per-Set log re-runs the earlier kinds
 # whose writes a watched Set reads (Patrol's SP / Camp, HPRegen's HP before Poison's EXP ops)
 @pytest.mark.parametrize("seed,lethal,set_ops,mode", [(71, False, False, 0), (72, False, False, 0), (73, True, False, 0),
-                                                      (74, False, True, 0), (75, True, False, 7), (78, False, True, 16)])
+                                                      (74, False, True, 0), (75, True, False, 7), (78, False, True, 16),
+                                                      (79, False, False, 32)])
 def test_logic_session_gpu_plugin_matches_reference(gpu_available, tmp_path, seed, lethal, set_ops, mode):
     if not (os.path.exists(GPU_EXE) and os.path.exists(REF_EXE)):
         pytest.skip("logic_session not built (needs /root/reference at build time)")
-    w = _world(seed, lethal=lethal, set_ops=set_ops, logic_mode=mode)
+    w = _world(seed, lethal=lethal, set_ops=set_ops, logic_mode=mode & ~32, const_guards=bool(mode & 32))
     got, ref = _run(GPU_EXE, w, tmp_path, "gpu"), _run(REF_EXE, w, tmp_path, "ref")
     nt = int(w["cfg"][7])
     if mode & 7:
@@ -230,8 +234,8 @@ def test_logic_session_per_set_log_kernels(gpu_available, tmp_path, env):
     compiled reference as on the default hipRTC k_chain_u."""
     if not (os.path.exists(GPU_EXE) and os.path.exists(REF_EXE)):
         pytest.skip("logic_session not built (needs /root/reference at build time)")
-    for seed, lethal, set_ops, mode in ((73, True, False, 0), (78, False, True, 16)):
-        w = _world(seed, lethal=lethal, set_ops=set_ops, logic_mode=mode)
+    for seed, lethal, set_ops, mode in ((73, True, False, 0), (78, False, True, 16), (79, False, False, 32)):
+        w = _world(seed, lethal=lethal, set_ops=set_ops, logic_mode=mode & ~32, const_guards=bool(mode & 32))
         got, ref = _run(GPU_EXE, w, tmp_path, f"gpu{seed}", env=env), _run(REF_EXE, w, tmp_path, f"ref{seed}")
         n = 0
         for t in range(int(w["cfg"][7])):

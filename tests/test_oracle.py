@@ -78,6 +78,10 @@ def test_golden_fixtures_are_nontrivial():
     (16, dict(n_obj=300, n_scenes=1, groups_per_scene=2, players_per_group=5, records=True, rec_rows=64,
               rec_float_op=False, rec_skill_op=True, rec_set_frac=0.2, rec_set_float=False, rec_row_frac=0.2,
               spawn_frac=0.03, destroy_frac=0.03)),
+    # guards against constants other than 0 (NFK_GUARD_K): ATK_VALUE driven through negative values to
+    # both ends of the constant's range, with SetProperty calls on the guarded properties
+    (17, dict(n_obj=600, n_scenes=2, groups_per_scene=3, players_per_group=3, const_guards=True, tick_ms=500,
+              ext_frac=0.1, ext_props="all", host_ops=True)),
 ])
 def test_oracle_matches_reference(seed, kw):
     w = workload.make_world(n_ticks=9, seed=seed, **kw)
@@ -94,6 +98,8 @@ SESSION = os.path.join(ROOT, "oracle", "_ref", "nf_ref_session")
               rmw_frac=0.03, sched_edges=True, host_ops=True)),
     (33, dict(n_obj=800, n_scenes=2, groups_per_scene=2, players_per_group=3, records=True, rec_rows=16,
               rec_float_op=False, ext_frac=0.05)),
+    (34, dict(n_obj=1000, n_scenes=2, groups_per_scene=3, players_per_group=4, const_guards=True, tick_ms=500,
+              ext_frac=0.05, ext_props="all", rmw_frac=0.02, host_ops=True)),
 ])
 def test_oracle_matches_reference_server_modules(tmp_path, seed, kw):
     """The oracle's final state against the reference's own server modules (oracle/ref_session.cpp:
