@@ -59,6 +59,11 @@ FIXTURES = {
     "setops": dict(n_obj=500, n_scenes=2, groups_per_scene=4, players_per_group=3, n_ticks=10, seed=1212,
                    ext_frac=0.05, ext_props="all", host_ops=True, set_ops=True, records=True, rec_rows=16,
                    rec_float_op=False),
+    # guards against constants other than 0 (NFK_GUARD_K: a functor's `if (GetPropertyInt(self, g) > 30)`,
+    # negative constants, both ends of the range) with SetProperty calls on the guarded properties
+    "constguards": dict(n_obj=500, n_scenes=2, groups_per_scene=4, players_per_group=3, n_ticks=12, seed=1313,
+                        tick_ms=500, ext_frac=0.05, ext_props="all", host_ops=True, rmw_frac=0.02,
+                        const_guards=True),
     "rowops": dict(n_obj=400, n_scenes=2, groups_per_scene=4, players_per_group=4, n_ticks=8, seed=1111,
                    records=True, rec_rows=24, rec_float_op=False, rec_set_frac=0.08, rec_set_float=False,
                    rec_row_frac=0.08, ext_frac=0.03, spawn_frac=0.02, destroy_frac=0.02),
@@ -74,7 +79,7 @@ TUTORIAL3 = {"tutorial3": dict(n_obj=2000, n_ticks=80, seed=606, world_effect=Tr
 # compiled from the reference): <name>.session.nfio holds what those modules raised in every frame
 # (property / record events in call order, fired heartbeats, GetBroadCastObject lists at the frame's
 # end) and their final state; tests/test_oracle.py derives each frame's dirty-sync list from it
-SESSION_FIXTURES = ["switch", "lifecycle", "rowops", "objects", "setops"]
+SESSION_FIXTURES = ["switch", "lifecycle", "rowops", "objects", "setops", "constguards"]
 
 
 def session(name, w, wp):

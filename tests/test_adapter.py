@@ -87,7 +87,7 @@ def _run_session(w, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,set_ops", [(61, False), (62, False), (63, True)])
+@pytest.mark.parametrize("seed,set_ops", [(61, False), (62, False), (63, True), (64, "const_guards")])
 def test_adapter_session_matches_oracle(gpu_available, tmp_path, seed, set_ops):
     """CreateObject before and after AfterInit, Set/GetProperty Int/Float/Object (read-modify-write
     included), SetRecordInt/Float by column index and by column tag, AddRow / Remove / ClearRecord,
@@ -97,7 +97,9 @@ def test_adapter_session_matches_oracle(gpu_available, tmp_path, seed, set_ops):
     NFISceneAOIModule's."""
     if not os.path.exists(EXE):
         pytest.skip("adapter_session not built (needs /root/reference at build time)")
-    w = _world(seed, set_ops=set_ops)  # (seed 63: assignments and guards, against 0 and another property)
+    # (seed 63: assignments and guards, against 0 and another property; seed 64: guards against other
+    # constants, NFK_GUARD_K)
+    w = _world(seed, set_ops=set_ops is True, const_guards=set_ops == "const_guards", tick_ms=500 if set_ops == "const_guards" else 100)
     nt = int(w["cfg"][7])
     assert len(w["sw_tick"]) == 0 and (w["born"] >= 0).sum() > 0 and len(w["d_tick"]) > 0
     assert w["x_mode"].sum() > 0 and (w["r_op"] > 0).sum() > 0 and (w["x_pid"] >= workload.N_INT + workload.N_FLT).any()

@@ -27,7 +27,8 @@ def set_path(monkeypatch, path):
 
 @PATHS
 @pytest.mark.parametrize("name", ["props", "records", "allplayers", "switch", "wide_sets", "tutorial3", "rmw",
-                                  "lifecycle", "recsets", "objects", "rowops", "setops"])
+                                  "lifecycle", "recsets", "objects", "rowops", "setops",
+                                  "constguards"])
 def test_gpu_matches_reference_golden(gpu_available, monkeypatch, name, path):
     set_path(monkeypatch, path)
     w = nfio.read(os.path.join(GOLDEN, f"{name}.workload.nfio"))
