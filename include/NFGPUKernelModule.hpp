@@ -334,7 +334,8 @@ public:
     // module): a property operand (dst of a property op, a / lo / hi under NFK_A_PROP / NFK_LO_PROP /
     // NFK_HI_PROP, FLERP's a, the guard's property under NFK_GUARD and, with NFK_GUARD_PROP, the
     // property it is compared to in guard >> 19) is an index into props, a record
-    // op's dst is index << 8 | column with the index into records; resolved at AfterInit
+    // op's dst is index << 8 | column with the index into records; resolved at AfterInit (a
+    // guard's constant, NFK_GUARD_K, is kept as it is)
     void AddHeartBeatProgram(const std::string& name, const std::vector<nfk_op>& ops,
                              const std::vector<std::string>& props, const std::vector<std::string>& records = {});
     int PropertyId(const std::string& name) const;
