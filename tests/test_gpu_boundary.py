@@ -165,3 +165,58 @@ def test_program_op_validation(gpu_available):
         m.define_kind(0, good)
     finally:
         m.close()
+
+
+def test_large_call_batches_reject_bad_calls(gpu_available):
+    """Batches past the device-lookup threshold (SetProperty batches queued on the device,
+    set_props_dev; schedule calls looked up on the device, find_many_dev) check every call before
+    queueing any: a bad property id or a bad schedule op or kind anywhere in a 5000-call batch fails
+    the whole batch with that call's error, and the world then runs exactly like a twin that never had
+    the batch; the same batch without the bad call is taken."""
+    w = workload.make_world(n_obj=6000, n_scenes=1, groups_per_scene=4, players_per_group=2, n_ticks=3, seed=5,
+                            ext_frac=0.0, host_ops=False)
+    m = kernel.world_from_workload(w)
+    twin = kernel.world_from_workload(w)
+    for x in (m, twin):
+        x.Execute(int(w["tick_time"][0]))
+    gh, gd = w["guid_head"], w["guid_data"]
+    n = 5000
+    rng = np.random.default_rng(8)
+    o = rng.integers(0, len(gh), n)
+    P = workload.PID
+    pid = rng.choice([P["HP"], P["Gold"], P["X"], P["EXP"], P["Camp"]], n).astype(np.int32)
+    bits = rng.integers(0, 1000, n).astype(np.uint64)
+    n_if = workload.N_INT + workload.N_FLT
+    for bad in (-1, n_if, 127):
+        p2 = pid.copy()
+        p2[-7] = bad
+        with pytest.raises(kernel.NFKError) as e:
+            m.set_props(gh[o], gd[o], p2, bits)
+        assert "bad property id" in str(e.value), str(e.value)
+    op = rng.integers(1, 4, n).astype(np.int32)
+    kind = rng.integers(-1, len(workload.KINDS) - 1, n).astype(np.int32)
+    kind[op == 1] = np.maximum(kind[op == 1], 0)
+    iv = np.full(n, 1.0, np.float32)
+    cnt = np.full(n, 5, np.int32)
+    now = np.full(n, int(w["tick_time"][0]), np.int64)
+    for field, val, msg in (("op", 4, "op must be"), ("op", 0, "op must be"), ("kind", 99, "kind")):
+        a, k = op.copy(), kind.copy()
+        (a if field == "op" else k)[-3] = val
+        if field == "kind":
+            a[-3] = 1
+        with pytest.raises(kernel.NFKError) as e:
+            m.schedule_calls(a, gh[o], gd[o], k, iv, cnt, now)
+        assert msg in str(e.value), str(e.value)
+    for x in (m, twin):  # the good batches, on both
+        x.set_props(gh[o], gd[o], pid, bits)
+        x.schedule_calls(op, gh[o], gd[o], kind, iv, cnt, now)
+    for x in (m, twin):
+        x.Execute(int(w["tick_time"][1]))
+        x.Execute(int(w["tick_time"][2]))
+    for p in range(n_if):
+        np.testing.assert_array_equal(m.read_prop(p), twin.read_prop(p))
+    for a, b in zip(m.read_schedules(), twin.read_schedules()):
+        np.testing.assert_array_equal(a, b)
+    assert (m.read_prop(P["Gold"])[o[pid == P["Gold"]]] < 1000).all()
+    m.close()
+    twin.close()
