@@ -2752,14 +2752,13 @@ static int queue_schedule_calls(World* w, int32_t n, const int32_t* op, const in
                 return fail(NFK_ERR_ARG, "undefined heartbeat kind");
             if (op[i] == 2 && (kind[i] < -1 || kind[i] >= w->cfg.n_kind)) return fail(NFK_ERR_ARG, "bad kind");
         }
-    const size_t base = w->hops.size();
-    w->hops.resize(base + (size_t)n);
-    World::HOp* h = w->hops.data() + base;
+    if (w->hops.capacity() < w->hops.size() + (size_t)n)  // (geometric: single calls append one by one)
+        w->hops.reserve(std::max(w->hops.size() + (size_t)n, 2 * w->hops.capacity()));
     for (int32_t i = 0; i < n; i++) {
         const int32_t o = op[i];
         const bool add = o == 1;
-        h[i] = {o, (uint32_t)obj[i], o == 3 ? 0u : (kind[i] < 0 ? kNoKind : (uint32_t)kind[i]), add ? interval[i] : 0.f,
-                add ? count[i] : 0, add ? now_ms[i] : 0};
+        w->hops.push_back({o, (uint32_t)obj[i], o == 3 ? 0u : (kind[i] < 0 ? kNoKind : (uint32_t)kind[i]),
+                           add ? interval[i] : 0.f, add ? count[i] : 0, add ? now_ms[i] : 0});
     }
     return NFK_OK;
 }
