@@ -2731,18 +2731,26 @@ int nfk_remove_all_schedules(void* world, int64_t gh, int64_t gd) {
 static int queue_schedule_calls(World* w, int32_t n, const int32_t* op, const int32_t* obj, const int32_t* kind,
                                 const float* interval, const int32_t* count, const int64_t* now_ms, const int64_t* gh,
                                 const int64_t* gd) {
-    // checked without a branch per call first (the ops of a batch come in no predictable order);
-    // a batch with a bad call is walked again for the first one's error
+    // appended and checked in one pass without a branch per check (the ops of a batch come in no
+    // predictable order); a batch with a bad call is taken back out and walked again for the first
+    // one's error
     const int32_t nk = w->cfg.n_kind;
+    const size_t base = w->hops.size();
+    if (w->hops.capacity() < base + (size_t)n)  // (geometric: single calls append one by one)
+        w->hops.reserve(std::max(base + (size_t)n, 2 * w->hops.capacity()));
     uint32_t bad = 0;
     for (int32_t i = 0; i < n; i++) {
         const int32_t o = op[i], k = kind[i];
+        const bool add = o == 1;
         const bool kin = (uint32_t)k < (uint32_t)nk;
         const bool def = w->kind_defined[kin ? k : 0] && kin;
-        bad |= (uint32_t)(obj[i] < 0) | (uint32_t)((uint32_t)(o - 1) > 2u) | (uint32_t)(o == 1 && !def) |
+        bad |= (uint32_t)(obj[i] < 0) | (uint32_t)((uint32_t)(o - 1) > 2u) | (uint32_t)(add && !def) |
                (uint32_t)(o == 2 && (k < -1 || k >= nk));
+        w->hops.push_back({o, (uint32_t)obj[i], o == 3 ? 0u : (k < 0 ? kNoKind : (uint32_t)k), add ? interval[i] : 0.f,
+                           add ? count[i] : 0, add ? now_ms[i] : 0});
     }
-    if (bad)
+    if (bad) {
+        w->hops.resize(base);
         for (int32_t i = 0; i < n; i++) {
             if (obj[i] < 0)
                 return fail(NFK_ERR_NOTFOUND, gh ? "no object " + std::to_string(gh[i]) + "-" + std::to_string(gd[i])
@@ -2752,13 +2760,7 @@ static int queue_schedule_calls(World* w, int32_t n, const int32_t* op, const in
                 return fail(NFK_ERR_ARG, "undefined heartbeat kind");
             if (op[i] == 2 && (kind[i] < -1 || kind[i] >= w->cfg.n_kind)) return fail(NFK_ERR_ARG, "bad kind");
         }
-    if (w->hops.capacity() < w->hops.size() + (size_t)n)  // (geometric: single calls append one by one)
-        w->hops.reserve(std::max(w->hops.size() + (size_t)n, 2 * w->hops.capacity()));
-    for (int32_t i = 0; i < n; i++) {
-        const int32_t o = op[i];
-        const bool add = o == 1;
-        w->hops.push_back({o, (uint32_t)obj[i], o == 3 ? 0u : (kind[i] < 0 ? kNoKind : (uint32_t)kind[i]),
-                           add ? interval[i] : 0.f, add ? count[i] : 0, add ? now_ms[i] : 0});
+        return fail(NFK_ERR_ARG, "bad schedule call");
     }
     return NFK_OK;
 }
