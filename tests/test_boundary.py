@@ -127,17 +127,22 @@ def test_module_schedules_match_reference(tmp_path, seed):
     assert got == ref
 
 
-@pytest.mark.parametrize("which", ["config1", "tutorial3", "records"])
+@pytest.mark.parametrize("which", ["config1", "tutorial3", "records", "set_ops", "const_guards"])
 def test_jit_preview_compiles_for_gfx950(which):
     """nfk_jit_preview (nfgpu.h): the schema policy nfk_commit generates for a world is valid
     hipRTC input — k_tick<.., JitSchema> builds for gfx950 with no GPU present.  (GPU parity runs
     with the specialisation on by default; NFGPU_JIT=0 selects the library's DynSchema kernels.)"""
     w = {"config1": lambda: workload.make_world(n_obj=512, n_ticks=1),
          "tutorial3": lambda: workload.tutorial3_world(n_obj=512, n_ticks=1),
-         "records": lambda: workload.make_world(n_obj=512, n_ticks=1, records=True)}[which]()
+         "records": lambda: workload.make_world(n_obj=512, n_ticks=1, records=True),
+         "set_ops": lambda: workload.make_world(n_obj=512, n_ticks=1, set_ops=True, records=True),
+         "const_guards": lambda: workload.make_world(n_obj=512, n_ticks=1, const_guards=True)}[which]()
     src, ok, _ = kernel.jit_preview(w, compile=False)
     assert ok and "struct JitSchema" in src
     assert f"kNK = {int(w['cfg'][4])};" in src
+    if which == "const_guards":  # guards against constants are literals of the generated programs
+        for k in (30, 1500, -100, workload.GUARD_KMIN, workload.GUARD_KMAX, 2, 61):
+            assert f"(int64_t)({k})" in src, k
     _, ok, msg = kernel.jit_preview(w, compile=True)
     assert ok, msg
     assert msg.startswith("_ZN5nfgpu6k_tick") and "JitSchema" in msg
